@@ -1,0 +1,237 @@
+/*
+ * wtfgpu.h — C ABI of the MI355X (gfx950) execution backend for wtf.
+ *
+ * This is the thin `extern "C"` launch layer that the C++ `GpuBackend_t`
+ * (wtf_amd/host/gpu_backend.*) drives, and that a maintainer of upstream wtf
+ * would bind from `src/wtf/gpu_backend.cc`. No torch,
+ * no fmt, no C++ types cross this boundary: plain pointers, sizes and int
+ * status codes (0 = ok, < 0 = error), never exceptions.
+ *
+ * Each entry point replaces one piece of the reference bochscpu backend
+ * (paths relative to the reference tree, m4drat/wtf @ 2025-02-17):
+ *
+ *   wtfgpu_load_pool          <- BochscpuBackend_t::Initialize + StaticGpaMissingHandler
+ *                                (src/wtf/bochscpu_backend.cc:269-335, :36-138): the
+ *                                kdmp physical pages become a read-only HBM page pool,
+ *                                missing GPAs read as zeros (:124-131).
+ *   wtfgpu_set_initial_state  <- BochscpuBackend_t::LoadState (bochscpu_backend.cc:1026-1122)
+ *   wtfgpu_restore            <- BochscpuBackend_t::Restore (bochscpu_backend.cc:730-797):
+ *                                dirty-list reset of per-lane copy-on-write overlays.
+ *   wtfgpu_set_limit          <- BochscpuBackend_t::SetLimit (bochscpu_backend.cc:347-350)
+ *   wtfgpu_set_breakpoints    <- BochscpuBackend_t::SetBreakpoint (bochscpu_backend.cc:337-345)
+ *   wtfgpu_run                <- BochscpuBackend_t::Run / bochscpu_cpu_run
+ *                                (bochscpu_backend.cc:352-410) + the before/after execution,
+ *                                lin_access, interrupt, hlt hooks (:445-697).
+ *   wtfgpu_read_regs/write_regs <- Get/SetReg (bochscpu_backend.cc:1124-1190)
+ *   wtfgpu_lane_translate     <- VirtTranslate (bochscpu_backend.cc:891-896)
+ *   wtfgpu_lane_read_phys/write_phys <- PhysTranslate + memcpy / DirtyGpa
+ *                                (bochscpu_backend.cc:887-900, backend.cc:16-127)
+ *   wtfgpu_read_dirty         <- DirtyGpas_ (bochscpu_backend.h, RunStats_.DirtyGpas)
+ *   wtfgpu_read_coverage      <- AggregatedCodeCoverage_/LastNewCoverage_
+ *                                (bochscpu_backend.cc:501-504, :1001-1016)
+ *   wtfgpu_commit_coverage    <- AggregatedCodeCoverage_.emplace (bochscpu_backend.cc:501)
+ *   wtfgpu_coverage_device_map <- the per-GPU coverage bitmap merged with RCCL MAX (new).
+ */
+#ifndef WTFGPU_H
+#define WTFGPU_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WTFGPU_ABI_VERSION 1
+#define WTFGPU_PAGE_SIZE 4096u
+
+/* Status codes. */
+#define WTFGPU_OK 0
+#define WTFGPU_ERR_INVALID (-1)
+#define WTFGPU_ERR_NODEV (-2)
+#define WTFGPU_ERR_OOM (-3)
+#define WTFGPU_ERR_HIP (-4)
+#define WTFGPU_ERR_STATE (-5)
+#define WTFGPU_ERR_TRANSLATE (-6)
+
+/* Per-lane status / exit reasons. A lane with status RUNNING is runnable. */
+enum wtfgpu_status {
+  WTFGPU_RUNNING = 0,
+  WTFGPU_EXIT_BREAKPOINT = 1, /* before executing the instruction at rip; host services it */
+  WTFGPU_EXIT_TIMEOUT = 2,    /* retired count > limit (bochscpu_backend.cc:458-469) */
+  WTFGPU_EXIT_INT3 = 3,       /* int3 -> Crash_t() (bochscpu_backend.cc:595-619) */
+  WTFGPU_EXIT_HLT = 4,        /* hlt -> Crash_t() (bochscpu_backend.cc:690-697) */
+  WTFGPU_EXIT_FAULT = 5,      /* architectural exception raised; vector/error/addr in exit */
+  WTFGPU_EXIT_UNIMPLEMENTED = 6, /* opcode outside the engine's ISA subset */
+  WTFGPU_EXIT_CR3 = 7,        /* cr3 write != initial cr3 (bochscpu_backend.cc:628-657) */
+  WTFGPU_EXIT_OVERLAY_FULL = 8, /* lane ran out of copy-on-write pages */
+  WTFGPU_EXIT_STOPPED = 9,    /* host called Stop(); result kept on the host */
+  WTFGPU_EXIT_IDLE = 10       /* lane holds no testcase */
+};
+
+/* x86 exception vectors reported in wtfgpu_exit_t.vector. */
+#define WTFGPU_VEC_DE 0
+#define WTFGPU_VEC_UD 6
+#define WTFGPU_VEC_GP 13
+#define WTFGPU_VEC_PF 14
+
+/* General purpose register indices (x86 encoding order). */
+enum wtfgpu_gpr {
+  WTFGPU_RAX = 0, WTFGPU_RCX, WTFGPU_RDX, WTFGPU_RBX, WTFGPU_RSP, WTFGPU_RBP,
+  WTFGPU_RSI, WTFGPU_RDI, WTFGPU_R8, WTFGPU_R9, WTFGPU_R10, WTFGPU_R11,
+  WTFGPU_R12, WTFGPU_R13, WTFGPU_R14, WTFGPU_R15
+};
+
+/* Segment register indices in wtfgpu_regs_t.seg. */
+enum wtfgpu_segidx { WTFGPU_ES = 0, WTFGPU_CS, WTFGPU_SS, WTFGPU_DS, WTFGPU_FS, WTFGPU_GS,
+                  WTFGPU_TR, WTFGPU_LDTR };
+
+typedef struct wtfgpu_seg {
+  uint64_t base;
+  uint32_t limit;
+  uint16_t selector;
+  uint16_t attr;
+  uint8_t present;
+  uint8_t pad[7];
+} wtfgpu_seg_t;
+
+/*
+ * Architectural state of one lane (= one testcase). Mirrors CpuState_t
+ * (src/wtf/globals.h:1020-1082) for the fields the engine models.
+ */
+typedef struct wtfgpu_regs {
+  uint64_t gpr[16];
+  uint64_t rip;
+  uint64_t rflags;
+  uint64_t cr0, cr2, cr3, cr4, cr8;
+  uint64_t efer;
+  uint64_t xcr0;
+  uint64_t kernel_gs_base;
+  uint64_t star, lstar, cstar, sfmask;
+  uint64_t tsc, tsc_aux, apic_base, pat;
+  uint64_t sysenter_cs, sysenter_eip, sysenter_esp;
+  wtfgpu_seg_t seg[8]; /* es cs ss ds fs gs tr ldtr; fs/gs .base are the 64-bit bases */
+  uint64_t gdtr_base, idtr_base;
+  uint32_t gdtr_limit, idtr_limit;
+  uint32_t mxcsr, mxcsr_mask;
+  uint16_t fpcw, fpsw, fptw, fpop;
+  uint32_t pad0;
+  uint64_t fpst[8];
+  uint64_t xmm[16][2];
+} wtfgpu_regs_t;
+
+/* Why a lane stopped. */
+typedef struct wtfgpu_exit {
+  uint32_t status;   /* enum wtfgpu_status */
+  uint32_t vector;   /* FAULT: exception vector */
+  uint32_t error;    /* FAULT: error code (#PF bits as in backend.h PfError_t) */
+  uint32_t opcode;   /* UNIMPLEMENTED: first opcode bytes, little endian */
+  uint64_t addr;     /* FAULT #PF: faulting linear address (cr2) */
+  uint64_t rip;      /* rip at exit */
+  uint64_t icount;   /* instructions retired by this testcase so far */
+} wtfgpu_exit_t;
+
+typedef struct wtfgpu_run_stats {
+  uint64_t kernel_launches;
+  uint64_t group_steps;    /* wave-level decode+execute iterations */
+  uint64_t lane_retired;   /* instructions retired by all lanes */
+  double kernel_ms;        /* device time measured with HIP events */
+} wtfgpu_run_stats_t;
+
+typedef struct wtfgpu_ctx wtfgpu_ctx;
+
+/* Device / context. */
+int wtfgpu_abi_version(void);
+int wtfgpu_device_count(void);
+int wtfgpu_create(int device, wtfgpu_ctx **out);
+int wtfgpu_destroy(wtfgpu_ctx *ctx);
+/* The HIP stream the context launches on (hipStream_t, as void*). */
+void *wtfgpu_stream(wtfgpu_ctx *ctx);
+
+/* Snapshot physical memory: npages pages of 4096 bytes, page i backs gpfns[i]. */
+int wtfgpu_load_pool(wtfgpu_ctx *ctx, const uint64_t *gpfns, const uint8_t *pages,
+                     uint64_t npages);
+
+/* Allocate lane storage. overlay_pages: copy-on-write pages per lane;
+ * cov_entries: per-wave new-coverage log capacity (power of two). */
+int wtfgpu_alloc_lanes(wtfgpu_ctx *ctx, uint32_t nlanes, uint32_t overlay_pages,
+                       uint32_t cov_entries);
+uint32_t wtfgpu_lane_count(wtfgpu_ctx *ctx);
+
+int wtfgpu_set_initial_state(wtfgpu_ctx *ctx, const wtfgpu_regs_t *regs);
+int wtfgpu_set_limit(wtfgpu_ctx *ctx, uint64_t limit);
+int wtfgpu_set_breakpoints(wtfgpu_ctx *ctx, const uint64_t *gvas, uint32_t n);
+
+/* Coverage index space: code pages (gva >> 12) that get a 4096-byte slot in
+ * the per-GPU coverage map. Pages outside it are still logged per lane. */
+int wtfgpu_set_code_pages(wtfgpu_ctx *ctx, const uint64_t *vpns, uint32_t n);
+
+/* Reset lanes [first, first+count) to the initial state: registers, dirty
+ * overlays dropped, retired count 0, coverage logs cleared, status RUNNING. */
+int wtfgpu_restore(wtfgpu_ctx *ctx, uint32_t first, uint32_t count);
+
+/* Bulk register I/O for lanes [first, first+count). */
+int wtfgpu_read_regs(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, wtfgpu_regs_t *out);
+int wtfgpu_write_regs(wtfgpu_ctx *ctx, uint32_t first, uint32_t count,
+                      const wtfgpu_regs_t *in);
+/* Only the 16 GPRs + rip + rflags (18 u64 per lane, that order). */
+int wtfgpu_read_gprs(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, uint64_t *out18);
+int wtfgpu_write_gprs(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, const uint64_t *in18);
+
+int wtfgpu_read_exits(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, wtfgpu_exit_t *out);
+/* Set lanes back to RUNNING. skip_bp != 0: the breakpoint at the current rip
+ * is not re-triggered (the handler returned without moving rip). */
+int wtfgpu_resume(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, const uint8_t *skip_bp);
+/* Mark lanes stopped (host-side Stop()). */
+int wtfgpu_stop(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, uint32_t status);
+
+/* Run every RUNNING lane in [first, first+count) until it exits or
+ * max_steps wave-steps elapse. Blocking. */
+int wtfgpu_run(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, uint64_t max_steps,
+               wtfgpu_run_stats_t *stats);
+
+/* Per-lane memory. gva translation uses the lane's cr3 and its overlays. */
+int wtfgpu_lane_translate(wtfgpu_ctx *ctx, uint32_t lane, uint64_t gva, uint64_t *gpa);
+int wtfgpu_lane_read_phys(wtfgpu_ctx *ctx, uint32_t lane, uint64_t gpa, void *buf, uint64_t len);
+/* Writes are copy-on-write into the lane overlay and dirty the page. */
+int wtfgpu_lane_write_phys(wtfgpu_ctx *ctx, uint32_t lane, uint64_t gpa, const void *buf,
+                           uint64_t len);
+int wtfgpu_lane_read_virt(wtfgpu_ctx *ctx, uint32_t lane, uint64_t gva, void *buf, uint64_t len);
+int wtfgpu_lane_write_virt(wtfgpu_ctx *ctx, uint32_t lane, uint64_t gva, const void *buf,
+                           uint64_t len);
+
+/* Batched guest-memory writes, one record per (lane, gva, len); data packed
+ * back to back in `data` at `data_off`. Copy-on-write + dirty per lane. */
+typedef struct wtfgpu_write {
+  uint32_t lane;
+  uint32_t len;
+  uint64_t gva;
+  uint64_t data_off;
+} wtfgpu_write_t;
+int wtfgpu_apply_writes(wtfgpu_ctx *ctx, const wtfgpu_write_t *writes, uint32_t n,
+                        const uint8_t *data, uint64_t data_len, int32_t *status_out);
+
+/* Dirty GPAs (page aligned) of one lane; *n gets the count (may exceed cap). */
+int wtfgpu_read_dirty(wtfgpu_ctx *ctx, uint32_t lane, uint64_t *gpas, uint32_t cap, uint32_t *n);
+
+/* New-coverage logs: RIPs executed by lanes [first, first+count) that were
+ * absent from the coverage map when executed. Writes up to cap (lane, rip)
+ * pairs; *n gets the total. *overflow != 0 if a log overflowed. */
+int wtfgpu_read_coverage(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, uint32_t *lanes,
+                         uint64_t *rips, uint64_t cap, uint64_t *n, uint32_t *overflow);
+/* Add RIPs to the coverage map (aggregate coverage). */
+int wtfgpu_commit_coverage(wtfgpu_ctx *ctx, const uint64_t *rips, uint64_t n);
+int wtfgpu_reset_coverage(wtfgpu_ctx *ctx);
+/* Device pointer + size of the uint8 coverage map (for an RCCL MAX all-reduce). */
+int wtfgpu_coverage_device_map(wtfgpu_ctx *ctx, void **dev_ptr, uint64_t *bytes);
+/* Host copy of the coverage map's set bytes as RIPs. */
+int wtfgpu_coverage_rips(wtfgpu_ctx *ctx, uint64_t *rips, uint64_t cap, uint64_t *n);
+
+/* Per-lane algorithmic byte counters (ilen + data bytes read/written),
+ * for the roofline numerator. */
+int wtfgpu_read_bytes(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, uint64_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WTFGPU_H */

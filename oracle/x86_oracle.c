@@ -1,0 +1,1718 @@
+/*
+ * x86_oracle.c — scalar CPU restatement of the wtf execution hot path.
+ * TEST INFRASTRUCTURE ONLY (see x86_oracle.h). Plain C99, one lane, no tricks:
+ * decode with a classic byte switch, execute, account hooks.
+ *
+ * Semantic conventions for behaviour the SDM leaves undefined (SURVEY.md
+ * H1 / Appendix C). The GPU engine implements the same choices; DESIGN.md §5
+ * lists them:
+ *   U1 logic ops (and/or/xor/test): CF=OF=AF=0.
+ *   U2 shl/shr/sar, count!=0: AF=0; OF = (shl) msb(res)^CF, (shr) msb(orig),
+ *      (sar) 0 for every count; CF=0 when count > operand bits.
+ *   U3 rol/ror: OF = msb(res)^lsb(res) (rol), msb(res)^msb-1(res) (ror), any count.
+ *      rcl/rcr: OF = msb(res)^CF (rcl), msb(res)^msb-1(res) (rcr), any count.
+ *   U4 mul/imul: SF/ZF/PF from the low half of the product, AF=0.
+ *   U5 div/idiv: flags unchanged.
+ *   U6 bsf/bsr: only ZF written; zero source leaves the destination unchanged.
+ *      tzcnt/lzcnt: only CF and ZF written. bt/bts/btr/btc: only CF written.
+ *   U7 shld/shrd: AF=0, OF = msb(res)^msb(orig); count > operand bits (16-bit
+ *      forms) shifts through the 32-bit concatenation modulo 32.
+ *   U8 no accessed/dirty bit updates during page walks; no TLB (every access walks).
+ *   U9 a rep string instruction is one retired instruction whatever the count.
+ *   U10 a breakpoint handler that stops the lane or moves rip cancels the
+ *      hooked instruction (not executed, not counted).
+ *   U11 exceptions are not delivered through the IDT: the lane exits FAULT
+ *      with vector / error code / cr2 and the faulting instruction not retired.
+ *   U12 int3 and hlt exit before retiring.
+ *   U13 16-bit bswap writes 0.
+ */
+#include "x86_oracle.h"
+#include <stdlib.h>
+#include <string.h>
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+typedef uint16_t u16;
+typedef uint8_t u8;
+typedef int64_t i64;
+
+/* ---------------- small open-addressing hash map u64 -> pointer ---------------- */
+typedef struct {
+  u64 *keys;
+  void **vals;
+  u8 *used;
+  u64 cap, n;
+} hmap;
+
+static u64 hmix(u64 x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return x;
+}
+
+static void hm_init(hmap *h, u64 cap) {
+  h->cap = cap;
+  h->n = 0;
+  h->keys = (u64 *)calloc(cap, sizeof(u64));
+  h->vals = (void **)calloc(cap, sizeof(void *));
+  h->used = (u8 *)calloc(cap, 1);
+}
+static void hm_free(hmap *h) {
+  free(h->keys);
+  free(h->vals);
+  free(h->used);
+  memset(h, 0, sizeof(*h));
+}
+static void **hm_slot(hmap *h, u64 k, int insert);
+static void hm_grow(hmap *h) {
+  hmap n;
+  hm_init(&n, h->cap * 2);
+  for (u64 i = 0; i < h->cap; i++)
+    if (h->used[i]) *hm_slot(&n, h->keys[i], 1) = h->vals[i];
+  hm_free(h);
+  *h = n;
+}
+static void **hm_slot(hmap *h, u64 k, int insert) {
+  if (insert && (h->n + 1) * 2 > h->cap) hm_grow(h);
+  u64 i = hmix(k) & (h->cap - 1);
+  for (;;) {
+    if (!h->used[i]) {
+      if (!insert) return NULL;
+      h->used[i] = 1;
+      h->keys[i] = k;
+      h->vals[i] = NULL;
+      h->n++;
+      return &h->vals[i];
+    }
+    if (h->keys[i] == k) return &h->vals[i];
+    i = (i + 1) & (h->cap - 1);
+  }
+}
+static void *hm_get(hmap *h, u64 k) {
+  void **s = hm_slot(h, k, 0);
+  return s ? *s : NULL;
+}
+static int hm_has(hmap *h, u64 k) { return hm_slot(h, k, 0) != NULL; }
+
+/* growable u64 vector */
+typedef struct {
+  u64 *v;
+  u64 n, cap;
+} vec;
+static void vec_push(vec *a, u64 x) {
+  if (a->n == a->cap) {
+    a->cap = a->cap ? a->cap * 2 : 64;
+    a->v = (u64 *)realloc(a->v, a->cap * sizeof(u64));
+  }
+  a->v[a->n++] = x;
+}
+
+/* ---------------- machine ---------------- */
+struct orc_machine {
+  hmap snap;    /* gpfn -> const page (owned copy) */
+  hmap overlay; /* gpfn -> private page */
+  vec dirty;    /* gpfns in first-write order */
+  hmap bps;     /* gva -> (void*)1 */
+  hmap cov;     /* rip -> (void*)1 */
+  vec covlist;
+  wtfgpu_regs_t r;
+  u64 initial_cr3;
+  u64 limit;
+  u64 icount;
+  u64 bytes;
+  /* per-instruction scratch */
+  wtfgpu_exit_t *ex;
+  int faulted;
+};
+
+static const u8 kZeroPage[4096];
+
+#define RF_CF 0x1ULL
+#define RF_PF 0x4ULL
+#define RF_AF 0x10ULL
+#define RF_ZF 0x40ULL
+#define RF_SF 0x80ULL
+#define RF_TF 0x100ULL
+#define RF_IF 0x200ULL
+#define RF_DF 0x400ULL
+#define RF_OF 0x800ULL
+#define RF_STATUS (RF_CF | RF_PF | RF_AF | RF_ZF | RF_SF | RF_OF)
+
+orc_machine *orc_create(void) {
+  orc_machine *m = (orc_machine *)calloc(1, sizeof(*m));
+  hm_init(&m->snap, 1024);
+  hm_init(&m->overlay, 64);
+  hm_init(&m->bps, 64);
+  hm_init(&m->cov, 1024);
+  return m;
+}
+
+void orc_destroy(orc_machine *m) {
+  if (!m) return;
+  for (u64 i = 0; i < m->snap.cap; i++)
+    if (m->snap.used[i]) free(m->snap.vals[i]);
+  for (u64 i = 0; i < m->overlay.cap; i++)
+    if (m->overlay.used[i]) free(m->overlay.vals[i]);
+  hm_free(&m->snap);
+  hm_free(&m->overlay);
+  hm_free(&m->bps);
+  hm_free(&m->cov);
+  free(m->dirty.v);
+  free(m->covlist.v);
+  free(m);
+}
+
+int orc_add_page(orc_machine *m, u64 gpfn, const u8 *page) {
+  void **s = hm_slot(&m->snap, gpfn, 1);
+  if (!*s) *s = malloc(4096);
+  memcpy(*s, page, 4096);
+  return 0;
+}
+
+void orc_set_regs(orc_machine *m, const wtfgpu_regs_t *r) { m->r = *r; }
+void orc_get_regs(orc_machine *m, wtfgpu_regs_t *r) { *r = m->r; }
+void orc_set_limit(orc_machine *m, u64 limit) { m->limit = limit; }
+
+int orc_set_breakpoints(orc_machine *m, const u64 *gvas, u32 n) {
+  hm_free(&m->bps);
+  hm_init(&m->bps, 64);
+  for (u32 i = 0; i < n; i++) *hm_slot(&m->bps, gvas[i], 1) = (void *)1;
+  return 0;
+}
+
+void orc_restore(orc_machine *m, const wtfgpu_regs_t *r) {
+  for (u64 i = 0; i < m->overlay.cap; i++)
+    if (m->overlay.used[i]) free(m->overlay.vals[i]);
+  hm_free(&m->overlay);
+  hm_init(&m->overlay, 64);
+  m->dirty.n = 0;
+  hm_free(&m->cov);
+  hm_init(&m->cov, 1024);
+  m->covlist.n = 0;
+  m->r = *r;
+  m->initial_cr3 = r->cr3;
+  m->icount = 0;
+  m->bytes = 0;
+}
+
+uint64_t orc_icount(orc_machine *m) { return m->icount; }
+uint64_t orc_bytes(orc_machine *m) { return m->bytes; }
+
+uint64_t orc_coverage(orc_machine *m, u64 *out, u64 cap) {
+  for (u64 i = 0; i < m->covlist.n && i < cap; i++) out[i] = m->covlist.v[i];
+  return m->covlist.n;
+}
+uint64_t orc_dirty(orc_machine *m, u64 *out, u64 cap) {
+  for (u64 i = 0; i < m->dirty.n && i < cap; i++) out[i] = m->dirty.v[i] << 12;
+  return m->dirty.n;
+}
+
+/* ---------------- physical memory ---------------- */
+static const u8 *phys_ro(orc_machine *m, u64 gpfn) {
+  const u8 *p = (const u8 *)hm_get(&m->overlay, gpfn);
+  if (p) return p;
+  p = (const u8 *)hm_get(&m->snap, gpfn);
+  return p ? p : kZeroPage;
+}
+/* Copy-on-write: the page joins the lane's dirty set (bochscpu_backend.cc:887-889). */
+static u8 *phys_rw(orc_machine *m, u64 gpfn) {
+  void **s = hm_slot(&m->overlay, gpfn, 1);
+  if (!*s) {
+    u8 *p = (u8 *)malloc(4096);
+    const u8 *src = (const u8 *)hm_get(&m->snap, gpfn);
+    memcpy(p, src ? src : kZeroPage, 4096);
+    *s = p;
+    vec_push(&m->dirty, gpfn);
+  }
+  return (u8 *)*s;
+}
+static u64 phys_read64(orc_machine *m, u64 pa) {
+  u64 v;
+  memcpy(&v, phys_ro(m, pa >> 12) + (pa & 0xfff), 8);
+  return v;
+}
+
+int orc_read_phys(orc_machine *m, u64 gpa, void *buf, u64 len) {
+  u8 *o = (u8 *)buf;
+  while (len) {
+    u64 off = gpa & 0xfff, n = 4096 - off;
+    if (n > len) n = len;
+    memcpy(o, phys_ro(m, gpa >> 12) + off, n);
+    o += n;
+    gpa += n;
+    len -= n;
+  }
+  return 0;
+}
+int orc_write_phys(orc_machine *m, u64 gpa, const void *buf, u64 len) {
+  const u8 *i = (const u8 *)buf;
+  while (len) {
+    u64 off = gpa & 0xfff, n = 4096 - off;
+    if (n > len) n = len;
+    memcpy(phys_rw(m, gpa >> 12) + off, i, n);
+    i += n;
+    gpa += n;
+    len -= n;
+  }
+  return 0;
+}
+
+/* ---------------- page walk ---------------- */
+enum { ACC_R = 0, ACC_W = 1, ACC_X = 2 };
+#define PTE_P 0x1ULL
+#define PTE_W 0x2ULL
+#define PTE_U 0x4ULL
+#define PTE_PS 0x80ULL
+#define PTE_NX (1ULL << 63)
+#define PTE_ADDR 0x000ffffffffff000ULL
+
+static int cpl(orc_machine *m) { return m->r.seg[WTFGPU_CS].selector & 3; }
+
+static int is_canonical(u64 va) {
+  i64 s = (i64)(va << 16) >> 16;
+  return (u64)s == va;
+}
+
+/* 4-level walk; check: perform permission checks. Returns 0 ok, else sets fault. */
+static int walk(orc_machine *m, u64 va, int acc, int check, u64 *pa) {
+  const int user = cpl(m) == 3;
+  const int nxe = (m->r.efer >> 11) & 1;
+  const int wp = (m->r.cr0 >> 16) & 1;
+  u64 table = m->r.cr3 & PTE_ADDR;
+  int allow_w = 1, allow_u = 1, nx = 0;
+  u64 e = 0;
+  int level;
+  u64 page_mask = 0xfff;
+  if (check && !is_canonical(va)) {
+    m->faulted = 1;
+    m->ex->status = WTFGPU_EXIT_FAULT;
+    m->ex->vector = WTFGPU_VEC_GP;
+    m->ex->error = 0;
+    m->ex->addr = va;
+    return -1;
+  }
+  for (level = 3; level >= 0; level--) {
+    const u64 idx = (va >> (12 + 9 * level)) & 0x1ff;
+    e = phys_read64(m, table + idx * 8);
+    if (!(e & PTE_P)) goto pf_notpresent;
+    allow_w &= (e & PTE_W) != 0;
+    allow_u &= (e & PTE_U) != 0;
+    if (nxe && (e & PTE_NX)) nx = 1;
+    if (level > 0 && level < 3 && (e & PTE_PS)) {
+      page_mask = level == 2 ? 0x3fffffffULL : 0x1fffffULL;
+      break;
+    }
+    table = e & PTE_ADDR;
+  }
+  if (check) {
+    int bad = 0;
+    if (user && !allow_u) bad = 1;
+    if (acc == ACC_W && !allow_w && (user || wp)) bad = 1;
+    if (acc == ACC_X && nx) bad = 1;
+    if (bad) {
+      m->faulted = 1;
+      m->ex->status = WTFGPU_EXIT_FAULT;
+      m->ex->vector = WTFGPU_VEC_PF;
+      m->ex->error = 1 | (acc == ACC_W ? 2 : 0) | (user ? 4 : 0) | (acc == ACC_X && nxe ? 16 : 0);
+      m->ex->addr = va;
+      return -1;
+    }
+  }
+  *pa = ((e & PTE_ADDR) & ~page_mask) | (va & page_mask);
+  return 0;
+pf_notpresent:
+  if (check) {
+    m->faulted = 1;
+    m->ex->status = WTFGPU_EXIT_FAULT;
+    m->ex->vector = WTFGPU_VEC_PF;
+    m->ex->error = (acc == ACC_W ? 2 : 0) | (user ? 4 : 0) | (acc == ACC_X && nxe ? 16 : 0);
+    m->ex->addr = va;
+  }
+  return -1;
+}
+
+int orc_translate(orc_machine *m, u64 gva, u64 *gpa) {
+  wtfgpu_exit_t dummy;
+  wtfgpu_exit_t *save = m->ex;
+  m->ex = &dummy;
+  int rc = walk(m, gva, ACC_R, 0, gpa);
+  m->ex = save;
+  return rc;
+}
+int orc_read_virt(orc_machine *m, u64 gva, void *buf, u64 len) {
+  u8 *o = (u8 *)buf;
+  while (len) {
+    u64 off = gva & 0xfff, n = 4096 - off, pa;
+    if (n > len) n = len;
+    if (orc_translate(m, gva, &pa)) return -1;
+    orc_read_phys(m, pa, o, n);
+    o += n;
+    gva += n;
+    len -= n;
+  }
+  return 0;
+}
+int orc_write_virt(orc_machine *m, u64 gva, const void *buf, u64 len) {
+  const u8 *i = (const u8 *)buf;
+  while (len) {
+    u64 off = gva & 0xfff, n = 4096 - off, pa;
+    if (n > len) n = len;
+    if (orc_translate(m, gva, &pa)) return -1;
+    orc_write_phys(m, pa, i, n);
+    i += n;
+    gva += n;
+    len -= n;
+  }
+  return 0;
+}
+
+/* ---------------- guest virtual access with permission checks ---------------- */
+/* Translate [va, va+len) (len <= 16) for acc; fills up to two physical spans. */
+static int vprobe(orc_machine *m, u64 va, u32 len, int acc, u64 pa[2], u32 n[2]) {
+  u64 off = va & 0xfff;
+  if (walk(m, va, acc, 1, &pa[0])) return -1;
+  if (off + len <= 4096) {
+    n[0] = len;
+    n[1] = 0;
+    return 0;
+  }
+  n[0] = (u32)(4096 - off);
+  n[1] = len - n[0];
+  if (walk(m, va + n[0], acc, 1, &pa[1])) return -1;
+  return 0;
+}
+static int vread(orc_machine *m, u64 va, u32 len, void *out) {
+  u64 pa[2];
+  u32 n[2];
+  if (vprobe(m, va, len, ACC_R, pa, n)) return -1;
+  orc_read_phys(m, pa[0], out, n[0]);
+  if (n[1]) orc_read_phys(m, pa[1], (u8 *)out + n[0], n[1]);
+  m->bytes += len;
+  return 0;
+}
+static int vwrite(orc_machine *m, u64 va, u32 len, const void *in) {
+  u64 pa[2];
+  u32 n[2];
+  if (vprobe(m, va, len, ACC_W, pa, n)) return -1;
+  orc_write_phys(m, pa[0], in, n[0]);
+  if (n[1]) orc_write_phys(m, pa[1], (const u8 *)in + n[0], n[1]);
+  m->bytes += len;
+  return 0;
+}
+/* Read for a read-modify-write: write permission required, pages dirtied at
+ * read time like bochs' read_RMW (reported as BOCHSCPU_HOOK_MEM_RW). */
+static int vread_rmw(orc_machine *m, u64 va, u32 len, void *out) {
+  u64 pa[2];
+  u32 n[2];
+  if (vprobe(m, va, len, ACC_W, pa, n)) return -1;
+  memcpy(out, phys_rw(m, pa[0] >> 12) + (pa[0] & 0xfff), n[0]);
+  if (n[1]) memcpy((u8 *)out + n[0], phys_rw(m, pa[1] >> 12) + (pa[1] & 0xfff), n[1]);
+  m->bytes += len;
+  return 0;
+}
+
+/* ---------------- decode ---------------- */
+typedef struct {
+  u64 start;
+  u32 len;
+  u32 pfx66, pfx67, rep, lock, seg; /* seg: 0 none, 4 fs, 5 gs */
+  u32 rex, rexw, rexr, rexx, rexb;
+  u32 opmap; /* 0 one-byte, 1 = 0F, 2 = 0F38, 3 = 0F3A */
+  u32 op;
+  u32 has_modrm, mod, reg, rm; /* reg, rm include REX extension */
+  u32 is_mem;
+  u64 ea; /* effective address (linear, seg base included) */
+  u8 bytes[16];
+  u32 pos;
+  int fetch_fail;
+} insn;
+
+static u8 fetch8(orc_machine *m, insn *d) {
+  if (d->pos >= 15) {
+    d->fetch_fail = 2; /* too long -> #GP */
+    return 0;
+  }
+  u64 va = d->start + d->pos;
+  u64 pa;
+  if (walk(m, va, ACC_X, 1, &pa)) {
+    d->fetch_fail = 1;
+    return 0;
+  }
+  u8 b = phys_ro(m, pa >> 12)[pa & 0xfff];
+  d->bytes[d->pos++] = b;
+  return b;
+}
+static u64 fetchn(orc_machine *m, insn *d, int n) {
+  u64 v = 0;
+  for (int i = 0; i < n; i++) v |= (u64)fetch8(m, d) << (8 * i);
+  return v;
+}
+static u64 sxn(u64 v, int bytes) {
+  int s = 64 - 8 * bytes;
+  return (u64)(((i64)(v << s)) >> s);
+}
+
+static u64 seg_base(orc_machine *m, u32 seg) {
+  if (seg == 4) return m->r.seg[WTFGPU_FS].base;
+  if (seg == 5) return m->r.seg[WTFGPU_GS].base;
+  return 0;
+}
+
+/* Decode modrm (+sib, disp). ea computed relative to rip of next insn later
+ * (rip-relative needs final length) -> store components. */
+typedef struct {
+  int riprel;
+  u64 disp;
+  int base, index, scale;
+} memref;
+
+static void decode_modrm(orc_machine *m, insn *d, memref *mr) {
+  u8 b = fetch8(m, d);
+  d->has_modrm = 1;
+  d->mod = b >> 6;
+  d->reg = ((b >> 3) & 7) | (d->rexr << 3);
+  u32 rm = b & 7;
+  memset(mr, 0, sizeof(*mr));
+  mr->base = -1;
+  mr->index = -1;
+  if (d->mod == 3) {
+    d->rm = rm | (d->rexb << 3);
+    d->is_mem = 0;
+    return;
+  }
+  d->is_mem = 1;
+  if (rm == 4) {
+    u8 sib = fetch8(m, d);
+    u32 ss = sib >> 6, idx = ((sib >> 3) & 7) | (d->rexx << 3), base = sib & 7;
+    if (idx != 4) {
+      mr->index = (int)idx;
+      mr->scale = 1 << ss;
+    }
+    if (base == 5 && d->mod == 0) {
+      mr->disp = sxn(fetchn(m, d, 4), 4);
+    } else {
+      mr->base = (int)(base | (d->rexb << 3));
+    }
+  } else if (rm == 5 && d->mod == 0) {
+    mr->riprel = 1;
+    mr->disp = sxn(fetchn(m, d, 4), 4);
+  } else {
+    mr->base = (int)(rm | (d->rexb << 3));
+  }
+  if (d->mod == 1) mr->disp = sxn(fetchn(m, d, 1), 1);
+  if (d->mod == 2) mr->disp = sxn(fetchn(m, d, 4), 4);
+}
+
+static void finish_ea(orc_machine *m, insn *d, memref *mr) {
+  if (!d->is_mem) return;
+  u64 ea;
+  if (mr->riprel) {
+    ea = d->start + d->len + mr->disp;
+  } else {
+    ea = mr->disp;
+    if (mr->base >= 0) ea += m->r.gpr[mr->base];
+    if (mr->index >= 0) ea += m->r.gpr[mr->index] * (u64)mr->scale;
+  }
+  if (d->pfx67) ea &= 0xffffffffULL;
+  d->ea = ea + seg_base(m, d->seg);
+}
+
+/* ---------------- registers ---------------- */
+static u64 szmask(int sz) { return sz == 8 ? ~0ULL : ((1ULL << (8 * sz)) - 1); }
+
+static u64 getreg(orc_machine *m, insn *d, u32 r, int sz) {
+  if (sz == 1) {
+    if (!d->rex && r >= 4 && r < 8) return (m->r.gpr[r - 4] >> 8) & 0xff;
+    return m->r.gpr[r] & 0xff;
+  }
+  return m->r.gpr[r] & szmask(sz);
+}
+static void setreg(orc_machine *m, insn *d, u32 r, int sz, u64 v) {
+  if (sz == 1) {
+    if (!d->rex && r >= 4 && r < 8) {
+      m->r.gpr[r - 4] = (m->r.gpr[r - 4] & ~0xff00ULL) | ((v & 0xff) << 8);
+    } else {
+      m->r.gpr[r] = (m->r.gpr[r] & ~0xffULL) | (v & 0xff);
+    }
+  } else if (sz == 2) {
+    m->r.gpr[r] = (m->r.gpr[r] & ~0xffffULL) | (v & 0xffff);
+  } else if (sz == 4) {
+    m->r.gpr[r] = v & 0xffffffffULL;
+  } else {
+    m->r.gpr[r] = v;
+  }
+}
+
+/* rm operand access */
+static int rd_rm(orc_machine *m, insn *d, int sz, u64 *v) {
+  if (!d->is_mem) {
+    *v = getreg(m, d, d->rm, sz);
+    return 0;
+  }
+  *v = 0;
+  return vread(m, d->ea, (u32)sz, v);
+}
+static int rd_rm_rmw(orc_machine *m, insn *d, int sz, u64 *v) {
+  if (!d->is_mem) {
+    *v = getreg(m, d, d->rm, sz);
+    return 0;
+  }
+  *v = 0;
+  return vread_rmw(m, d->ea, (u32)sz, v);
+}
+static int wr_rm(orc_machine *m, insn *d, int sz, u64 v) {
+  if (!d->is_mem) {
+    setreg(m, d, d->rm, sz, v);
+    return 0;
+  }
+  return vwrite(m, d->ea, (u32)sz, &v);
+}
+
+/* ---------------- flags ---------------- */
+static int parity8(u64 v) { return !__builtin_parity((unsigned)(v & 0xff)); }
+static u64 msb(u64 v, int sz) { return (v >> (8 * sz - 1)) & 1; }
+
+static void set_flags(orc_machine *m, u64 mask, u64 vals) {
+  m->r.rflags = (m->r.rflags & ~mask) | (vals & mask);
+}
+static u64 szp(u64 res, int sz) {
+  res &= szmask(sz);
+  return (res == 0 ? RF_ZF : 0) | (msb(res, sz) ? RF_SF : 0) | (parity8(res) ? RF_PF : 0);
+}
+static int CF(orc_machine *m) { return (m->r.rflags & RF_CF) != 0; }
+
+/* ALU binary op: 0 add,1 or,2 adc,3 sbb,4 and,5 sub,6 xor,7 cmp. Returns result. */
+static u64 alu2(orc_machine *m, int op, u64 a, u64 b, int sz) {
+  const u64 mk = szmask(sz);
+  a &= mk;
+  b &= mk;
+  u64 res = 0, f = 0;
+  u64 c = 0;
+  switch (op) {
+  case 0:
+  case 2: {
+    c = (op == 2) ? (u64)CF(m) : 0;
+    res = (a + b + c) & mk;
+    int carry;
+    if (sz == 8)
+      carry = (res < a) || (c && res == a);
+    else
+      carry = ((a + b + c) >> (8 * sz)) & 1;
+    f = szp(res, sz) | (carry ? RF_CF : 0) | (((a ^ b ^ res) & 0x10) ? RF_AF : 0) |
+        (msb((a ^ res) & (b ^ res), sz) ? RF_OF : 0);
+    break;
+  }
+  case 3:
+  case 5:
+  case 7: {
+    c = (op == 3) ? (u64)CF(m) : 0;
+    res = (a - b - c) & mk;
+    int borrow = (a < b) || (c && a == b);
+    f = szp(res, sz) | (borrow ? RF_CF : 0) | (((a ^ b ^ res) & 0x10) ? RF_AF : 0) |
+        (msb((a ^ b) & (a ^ res), sz) ? RF_OF : 0);
+    break;
+  }
+  case 1:
+    res = a | b;
+    f = szp(res, sz);
+    break;
+  case 4:
+    res = a & b;
+    f = szp(res, sz);
+    break;
+  case 6:
+    res = a ^ b;
+    f = szp(res, sz);
+    break;
+  }
+  set_flags(m, RF_STATUS, f);
+  return res;
+}
+
+static int cond(orc_machine *m, u32 cc) {
+  const u64 f = m->r.rflags;
+  const int cf = (f & RF_CF) != 0, zf = (f & RF_ZF) != 0, sf = (f & RF_SF) != 0,
+            of = (f & RF_OF) != 0, pf = (f & RF_PF) != 0;
+  int r;
+  switch (cc >> 1) {
+  case 0: r = of; break;
+  case 1: r = cf; break;
+  case 2: r = zf; break;
+  case 3: r = cf || zf; break;
+  case 4: r = sf; break;
+  case 5: r = pf; break;
+  case 6: r = sf != of; break;
+  default: r = zf || (sf != of); break;
+  }
+  return (cc & 1) ? !r : r;
+}
+
+/* shifts/rotates: op = modrm.reg (0 rol,1 ror,2 rcl,3 rcr,4 shl,5 shr,6 sal=shl,7 sar) */
+static u64 shift_op(orc_machine *m, int op, u64 v, u32 count, int sz) {
+  const int bits = 8 * sz;
+  const u64 mk = szmask(sz);
+  u32 cnt = count & (sz == 8 ? 0x3f : 0x1f);
+  v &= mk;
+  if (cnt == 0) return v;
+  u64 res = v;
+  u64 f = m->r.rflags;
+  int cf;
+  switch (op) {
+  case 0: { /* rol */
+    u32 c = cnt % bits;
+    res = c ? ((v << c) | (v >> (bits - c))) & mk : v;
+    cf = res & 1;
+    f = (f & ~(RF_CF | RF_OF)) | (cf ? RF_CF : 0) | ((msb(res, sz) ^ cf) ? RF_OF : 0);
+    break;
+  }
+  case 1: { /* ror */
+    u32 c = cnt % bits;
+    res = c ? ((v >> c) | (v << (bits - c))) & mk : v;
+    cf = (int)msb(res, sz);
+    f = (f & ~(RF_CF | RF_OF)) | (cf ? RF_CF : 0) |
+        ((msb(res, sz) ^ ((res >> (bits - 2)) & 1)) ? RF_OF : 0);
+    break;
+  }
+  case 2: { /* rcl */
+    u32 c = (sz == 1) ? cnt % 9 : (sz == 2) ? cnt % 17 : cnt;
+    int carry = CF(m);
+    for (u32 i = 0; i < c; i++) {
+      int out = (int)msb(res, sz);
+      res = ((res << 1) | (u64)carry) & mk;
+      carry = out;
+    }
+    f = (f & ~(RF_CF | RF_OF)) | (carry ? RF_CF : 0) | ((msb(res, sz) ^ (u64)carry) ? RF_OF : 0);
+    break;
+  }
+  case 3: { /* rcr */
+    u32 c = (sz == 1) ? cnt % 9 : (sz == 2) ? cnt % 17 : cnt;
+    int carry = CF(m);
+    for (u32 i = 0; i < c; i++) {
+      int out = (int)(res & 1);
+      res = (res >> 1) | ((u64)carry << (bits - 1));
+      carry = out;
+    }
+    f = (f & ~(RF_CF | RF_OF)) | (carry ? RF_CF : 0) |
+        ((msb(res, sz) ^ ((res >> (bits - 2)) & 1)) ? RF_OF : 0);
+    break;
+  }
+  case 4:
+  case 6: { /* shl */
+    res = cnt >= 64 ? 0 : (v << cnt) & mk;
+    cf = cnt <= (u32)bits ? (int)((v >> (bits - cnt)) & 1) : 0;
+    f = (f & ~RF_STATUS) | szp(res, sz) | (cf ? RF_CF : 0) | ((msb(res, sz) ^ (u64)cf) ? RF_OF : 0);
+    break;
+  }
+  case 5: { /* shr */
+    res = cnt >= 64 ? 0 : v >> cnt;
+    cf = cnt <= (u32)bits ? (int)((v >> (cnt - 1)) & 1) : 0;
+    f = (f & ~RF_STATUS) | szp(res, sz) | (cf ? RF_CF : 0) | (msb(v, sz) ? RF_OF : 0);
+    break;
+  }
+  case 7: { /* sar */
+    i64 sv = (i64)sxn(v, sz);
+    u32 c = cnt >= (u32)bits ? (u32)bits - 1 : cnt;
+    res = (u64)(sv >> c) & mk;
+    cf = (int)(((u64)(sv >> (cnt >= (u32)bits ? (u32)bits - 1 : cnt - 1))) & 1);
+    f = (f & ~RF_STATUS) | szp(res, sz) | (cf ? RF_CF : 0);
+    break;
+  }
+  }
+  m->r.rflags = f;
+  return res;
+}
+
+/* ---------------- stack ---------------- */
+static int push64(orc_machine *m, u64 v, int sz) {
+  u64 rsp = m->r.gpr[WTFGPU_RSP] - (u64)sz;
+  if (vwrite(m, rsp, (u32)sz, &v)) return -1;
+  m->r.gpr[WTFGPU_RSP] = rsp;
+  return 0;
+}
+static int pop64(orc_machine *m, u64 *v, int sz) {
+  u64 t = 0;
+  if (vread(m, m->r.gpr[WTFGPU_RSP], (u32)sz, &t)) return -1;
+  m->r.gpr[WTFGPU_RSP] += (u64)sz;
+  *v = t;
+  return 0;
+}
+
+static void fault(orc_machine *m, u32 vec, u32 err) {
+  m->faulted = 1;
+  m->ex->status = WTFGPU_EXIT_FAULT;
+  m->ex->vector = vec;
+  m->ex->error = err;
+  m->ex->addr = 0;
+}
+
+/* ---------------- string instructions ---------------- */
+static int string_op(orc_machine *m, insn *d, u32 op, int sz) {
+  /* op: a4 movs, a6 cmps, aa stos, ac lods, ae scas (sz from low bit) */
+  const u64 amask = d->pfx67 ? 0xffffffffULL : ~0ULL;
+  const int df = (m->r.rflags & RF_DF) != 0;
+  const u64 step = df ? (u64)-(i64)sz : (u64)sz;
+  const u64 srcbase = seg_base(m, d->seg);
+  for (;;) {
+    if (d->rep) {
+      if ((m->r.gpr[WTFGPU_RCX] & amask) == 0) break;
+    }
+    u64 rsi = m->r.gpr[WTFGPU_RSI] & amask, rdi = m->r.gpr[WTFGPU_RDI] & amask;
+    u64 a = 0, b = 0;
+    int stop_rep = 0;
+    switch (op) {
+    case 0xa4:
+      if (vread(m, srcbase + rsi, (u32)sz, &a)) return -1;
+      if (vwrite(m, rdi, (u32)sz, &a)) return -1;
+      break;
+    case 0xa6:
+      if (vread(m, srcbase + rsi, (u32)sz, &a)) return -1;
+      if (vread(m, rdi, (u32)sz, &b)) return -1;
+      alu2(m, 7, a, b, sz);
+      break;
+    case 0xaa:
+      a = m->r.gpr[WTFGPU_RAX];
+      if (vwrite(m, rdi, (u32)sz, &a)) return -1;
+      break;
+    case 0xac:
+      if (vread(m, srcbase + rsi, (u32)sz, &a)) return -1;
+      setreg(m, d, WTFGPU_RAX, sz, a);
+      break;
+    case 0xae:
+      if (vread(m, rdi, (u32)sz, &b)) return -1;
+      alu2(m, 7, m->r.gpr[WTFGPU_RAX], b, sz);
+      break;
+    }
+    if (op == 0xa4 || op == 0xa6 || op == 0xac) {
+      u64 n = (rsi + step) & amask;
+      m->r.gpr[WTFGPU_RSI] = n;
+    }
+    if (op != 0xac) {
+      u64 n = (rdi + step) & amask;
+      m->r.gpr[WTFGPU_RDI] = n;
+    }
+    if (!d->rep) break;
+    {
+      u64 c = (m->r.gpr[WTFGPU_RCX] - 1) & amask;
+      m->r.gpr[WTFGPU_RCX] = c;
+    }
+    if (op == 0xa6 || op == 0xae) {
+      const int zf = (m->r.rflags & RF_ZF) != 0;
+      if (d->rep == 0xf3 && !zf) stop_rep = 1;
+      if (d->rep == 0xf2 && zf) stop_rep = 1;
+    }
+    if (stop_rep) break;
+  }
+  return 0;
+}
+
+/* ---------------- mul / div ---------------- */
+static int muldiv(orc_machine *m, insn *d, int sub, int sz, u64 src) {
+  const u64 mk = szmask(sz);
+  const int bits = 8 * sz;
+  u64 a = m->r.gpr[WTFGPU_RAX] & mk;
+  if (sz == 1) a = m->r.gpr[WTFGPU_RAX] & 0xff;
+  switch (sub) {
+  case 4: { /* mul */
+    unsigned __int128 p = (unsigned __int128)a * (src & mk);
+    u64 lo = (u64)p & mk, hi = (u64)(p >> bits) & mk;
+    if (sz == 8) hi = (u64)(p >> 64);
+    if (sz == 1) {
+      setreg(m, d, WTFGPU_RAX, 2, (u64)p & 0xffff);
+    } else {
+      setreg(m, d, WTFGPU_RAX, sz, lo);
+      setreg(m, d, WTFGPU_RDX, sz, hi);
+    }
+    u64 f = szp(lo, sz) | (hi ? (RF_CF | RF_OF) : 0);
+    set_flags(m, RF_STATUS, f);
+    return 0;
+  }
+  case 5: { /* imul */
+    __int128 p = (__int128)(i64)sxn(a, sz) * (__int128)(i64)sxn(src & mk, sz);
+    u64 lo = (u64)p & mk;
+    u64 hi = (u64)(p >> bits) & mk;
+    if (sz == 8) hi = (u64)(p >> 64);
+    int ovf = (__int128)(i64)sxn(lo, sz) != p;
+    if (sz == 1) {
+      setreg(m, d, WTFGPU_RAX, 2, (u64)p & 0xffff);
+    } else {
+      setreg(m, d, WTFGPU_RAX, sz, lo);
+      setreg(m, d, WTFGPU_RDX, sz, hi);
+    }
+    set_flags(m, RF_STATUS, szp(lo, sz) | (ovf ? (RF_CF | RF_OF) : 0));
+    return 0;
+  }
+  case 6: { /* div */
+    u64 dv = src & mk;
+    if (dv == 0) {
+      fault(m, WTFGPU_VEC_DE, 0);
+      return -1;
+    }
+    unsigned __int128 n;
+    if (sz == 1)
+      n = m->r.gpr[WTFGPU_RAX] & 0xffff;
+    else
+      n = ((unsigned __int128)(m->r.gpr[WTFGPU_RDX] & mk) << bits) | a;
+    unsigned __int128 q = n / dv, r = n % dv;
+    if (q > mk) {
+      fault(m, WTFGPU_VEC_DE, 0);
+      return -1;
+    }
+    if (sz == 1) {
+      setreg(m, d, WTFGPU_RAX, 2, ((u64)r << 8) | (u64)q);
+    } else {
+      setreg(m, d, WTFGPU_RAX, sz, (u64)q);
+      setreg(m, d, WTFGPU_RDX, sz, (u64)r);
+    }
+    return 0;
+  }
+  case 7: { /* idiv */
+    i64 dv = (i64)sxn(src & mk, sz);
+    if (dv == 0) {
+      fault(m, WTFGPU_VEC_DE, 0);
+      return -1;
+    }
+    __int128 n;
+    if (sz == 1)
+      n = (__int128)(int16_t)(m->r.gpr[WTFGPU_RAX] & 0xffff);
+    else if (sz == 8)
+      n = (__int128)(((unsigned __int128)m->r.gpr[WTFGPU_RDX] << 64) | a);
+    else
+      n = (__int128)(i64)sxn(((m->r.gpr[WTFGPU_RDX] & mk) << bits) | a, 2 * sz);
+    /* overflow: quotient out of range (also INT_MIN / -1) */
+    __int128 q, r;
+    if (dv == -1) {
+      if (n < -(((__int128)1 << (bits - 1)) - 1)) { /* -n would leave the range */
+        fault(m, WTFGPU_VEC_DE, 0);
+        return -1;
+      }
+      q = -n;
+      r = 0;
+    } else {
+      q = n / dv;
+      r = n % dv;
+    }
+    __int128 lo = -((__int128)1 << (bits - 1)), hi = ((__int128)1 << (bits - 1)) - 1;
+    if (q < lo || q > hi) {
+      fault(m, WTFGPU_VEC_DE, 0);
+      return -1;
+    }
+    if (sz == 1) {
+      setreg(m, d, WTFGPU_RAX, 2, (((u64)r & 0xff) << 8) | ((u64)q & 0xff));
+    } else {
+      setreg(m, d, WTFGPU_RAX, sz, (u64)q);
+      setreg(m, d, WTFGPU_RDX, sz, (u64)r);
+    }
+    return 0;
+  }
+  }
+  return 0;
+}
+
+/* ---------------- execute one instruction ---------------- */
+enum { X_OK = 0, X_FAULT = 1, X_UNIMPL = 2, X_INT3 = 3, X_HLT = 4, X_CR3 = 5, X_FAULT_KEEP = 6 };
+
+#define CHK(x)                                                                                   \
+  do {                                                                                           \
+    if (x) return X_FAULT;                                                                       \
+  } while (0)
+
+static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
+  (void)mr;
+  const u32 op = d->op;
+  const int osz = d->rexw ? 8 : (d->pfx66 ? 2 : 4);
+  u64 nrip = d->start + d->len;
+  u64 a = 0, b = 0, res = 0;
+  *next_rip = nrip;
+
+  if (d->opmap == 0) {
+    /* ALU ops 00-3f */
+    if (op < 0x40 && (op & 7) < 6) {
+      const int aluop = (int)(op >> 3);
+      const int form = op & 7;
+      const int sz = (form & 1) ? osz : 1;
+      if (form <= 1) { /* Ex, Gx */
+        if (aluop == 7) {
+          CHK(rd_rm(m, d, sz, &a));
+          alu2(m, 7, a, getreg(m, d, d->reg, sz), sz);
+        } else {
+          CHK(rd_rm_rmw(m, d, sz, &a));
+          res = alu2(m, aluop, a, getreg(m, d, d->reg, sz), sz);
+          CHK(wr_rm(m, d, sz, res));
+        }
+      } else if (form <= 3) { /* Gx, Ex */
+        CHK(rd_rm(m, d, sz, &b));
+        res = alu2(m, aluop, getreg(m, d, d->reg, sz), b, sz);
+        if (aluop != 7) setreg(m, d, d->reg, sz, res);
+      } else { /* AL/eAX, imm */
+        b = form == 4 ? d->bytes[d->len - 1] : sxn(0, 1);
+        if (form == 5) {
+          int isz = osz == 2 ? 2 : 4;
+          b = 0;
+          memcpy(&b, d->bytes + d->len - isz, (size_t)isz);
+          b = sxn(b, isz);
+        }
+        res = alu2(m, aluop, getreg(m, d, 0, sz), b, sz);
+        if (aluop != 7) setreg(m, d, 0, sz, res);
+      }
+      return X_OK;
+    }
+    switch (op) {
+    case 0x50: case 0x51: case 0x52: case 0x53: case 0x54: case 0x55: case 0x56: case 0x57: {
+      const int sz = d->pfx66 ? 2 : 8;
+      const u32 r = (op & 7) | (d->rexb << 3);
+      CHK(push64(m, m->r.gpr[r] & szmask(sz), sz));
+      return X_OK;
+    }
+    case 0x58: case 0x59: case 0x5a: case 0x5b: case 0x5c: case 0x5d: case 0x5e: case 0x5f: {
+      const int sz = d->pfx66 ? 2 : 8;
+      const u32 r = (op & 7) | (d->rexb << 3);
+      CHK(pop64(m, &a, sz));
+      setreg(m, d, r, sz, a);
+      return X_OK;
+    }
+    case 0x63: /* movsxd */
+      CHK(rd_rm(m, d, 4, &a));
+      setreg(m, d, d->reg, osz, osz == 8 ? sxn(a, 4) : a);
+      return X_OK;
+    case 0x68:
+    case 0x6a: {
+      const int sz = d->pfx66 ? 2 : 8;
+      int isz = op == 0x6a ? 1 : (d->pfx66 ? 2 : 4);
+      memcpy(&a, d->bytes + d->len - isz, (size_t)isz);
+      a = sxn(a, isz) & szmask(sz);
+      CHK(push64(m, a, sz));
+      return X_OK;
+    }
+    case 0x69:
+    case 0x6b: {
+      int isz = op == 0x6b ? 1 : (osz == 2 ? 2 : 4);
+      b = 0;
+      memcpy(&b, d->bytes + d->len - isz, (size_t)isz);
+      b = sxn(b, isz);
+      CHK(rd_rm(m, d, osz, &a));
+      {
+      __int128 p = (__int128)(i64)sxn(a & szmask(osz), osz) * (__int128)(i64)sxn(b & szmask(osz), osz);
+      u64 lo = (u64)p & szmask(osz);
+      int ovf = (__int128)(i64)sxn(lo, osz) != p;
+      setreg(m, d, d->reg, osz, lo);
+      set_flags(m, RF_STATUS, szp(lo, osz) | (ovf ? (RF_CF | RF_OF) : 0));
+      return X_OK;
+    }
+    }
+    case 0x70: case 0x71: case 0x72: case 0x73: case 0x74: case 0x75: case 0x76: case 0x77:
+    case 0x78: case 0x79: case 0x7a: case 0x7b: case 0x7c: case 0x7d: case 0x7e: case 0x7f:
+      if (cond(m, op & 0xf)) *next_rip = nrip + sxn(d->bytes[d->len - 1], 1);
+      return X_OK;
+    case 0x80:
+    case 0x81:
+    case 0x83: {
+      const int sz = op == 0x80 ? 1 : osz;
+      int isz = op == 0x81 ? (osz == 2 ? 2 : 4) : 1;
+      b = 0;
+      memcpy(&b, d->bytes + d->len - isz, (size_t)isz);
+      b = sxn(b, isz);
+      const int aluop = (int)(d->reg & 7);
+      if (aluop == 7) {
+        CHK(rd_rm(m, d, sz, &a));
+        alu2(m, 7, a, b, sz);
+      } else {
+        CHK(rd_rm_rmw(m, d, sz, &a));
+        res = alu2(m, aluop, a, b, sz);
+        CHK(wr_rm(m, d, sz, res));
+      }
+      return X_OK;
+    }
+    case 0x84:
+    case 0x85: {
+      const int sz = op == 0x84 ? 1 : osz;
+      CHK(rd_rm(m, d, sz, &a));
+      alu2(m, 4, a, getreg(m, d, d->reg, sz), sz);
+      return X_OK;
+    }
+    case 0x86:
+    case 0x87: {
+      const int sz = op == 0x86 ? 1 : osz;
+      CHK(rd_rm_rmw(m, d, sz, &a));
+      b = getreg(m, d, d->reg, sz);
+      CHK(wr_rm(m, d, sz, b));
+      setreg(m, d, d->reg, sz, a);
+      return X_OK;
+    }
+    case 0x88:
+    case 0x89: {
+      const int sz = op == 0x88 ? 1 : osz;
+      CHK(wr_rm(m, d, sz, getreg(m, d, d->reg, sz)));
+      return X_OK;
+    }
+    case 0x8a:
+    case 0x8b: {
+      const int sz = op == 0x8a ? 1 : osz;
+      CHK(rd_rm(m, d, sz, &a));
+      setreg(m, d, d->reg, sz, a);
+      return X_OK;
+    }
+    case 0x8d:
+      if (!d->is_mem) {
+        fault(m, WTFGPU_VEC_UD, 0);
+        return X_FAULT;
+      }
+      /* lea: effective address without segment base */
+      setreg(m, d, d->reg, osz, d->ea - seg_base(m, d->seg));
+      return X_OK;
+    case 0x8f: {
+      if ((d->reg & 7) != 0) return X_UNIMPL;
+      const int sz = d->pfx66 ? 2 : 8;
+      /* pop r/m: the address is computed with rsp already incremented */
+      u64 rsp0 = m->r.gpr[WTFGPU_RSP];
+      CHK(vread(m, rsp0, (u32)sz, &a) ? 1 : 0);
+      m->r.gpr[WTFGPU_RSP] = rsp0 + (u64)sz;
+      if (d->is_mem) finish_ea(m, d, mr);
+      if (wr_rm(m, d, sz, a)) {
+        m->r.gpr[WTFGPU_RSP] = rsp0;
+        return X_FAULT;
+      }
+      return X_OK;
+    }
+    case 0x90:
+      if (d->rexb) { /* xchg r8, rax */
+        a = getreg(m, d, 8, osz);
+        setreg(m, d, 8, osz, getreg(m, d, 0, osz));
+        setreg(m, d, 0, osz, a);
+      }
+      return X_OK; /* nop / pause */
+    case 0x91: case 0x92: case 0x93: case 0x94: case 0x95: case 0x96: case 0x97: {
+      const u32 r = (op & 7) | (d->rexb << 3);
+      a = getreg(m, d, r, osz);
+      setreg(m, d, r, osz, getreg(m, d, 0, osz));
+      setreg(m, d, 0, osz, a);
+      return X_OK;
+    }
+    case 0x98: /* cbw/cwde/cdqe */
+      if (osz == 2) setreg(m, d, 0, 2, sxn(m->r.gpr[0], 1));
+      else if (osz == 4) setreg(m, d, 0, 4, sxn(m->r.gpr[0], 2));
+      else m->r.gpr[0] = sxn(m->r.gpr[0], 4);
+      return X_OK;
+    case 0x99: /* cwd/cdq/cqo */
+      setreg(m, d, WTFGPU_RDX, osz, msb(m->r.gpr[0], osz) ? ~0ULL : 0);
+      return X_OK;
+    case 0x9c: { /* pushf */
+      const int sz = d->pfx66 ? 2 : 8;
+      CHK(push64(m, m->r.rflags & 0xfcffffULL & szmask(sz), sz));
+      return X_OK;
+    }
+    case 0x9d: { /* popf */
+      const int sz = d->pfx66 ? 2 : 8;
+      CHK(pop64(m, &a, sz));
+      u64 mask = RF_STATUS | RF_TF | RF_DF | 0x4000ULL /*NT*/ | 0x40000ULL /*AC*/ | 0x200000ULL /*ID*/;
+      if (cpl(m) == 0) mask |= RF_IF | 0x3000ULL;
+      if (sz == 2) mask &= 0xffff;
+      m->r.rflags = ((m->r.rflags & ~mask) | (a & mask) | 2) & ~0x10000ULL;
+      return X_OK;
+    }
+    case 0x9e: /* sahf */
+      set_flags(m, RF_SF | RF_ZF | RF_AF | RF_PF | RF_CF, (m->r.gpr[0] >> 8) & 0xff);
+      return X_OK;
+    case 0x9f: /* lahf */
+      m->r.gpr[0] = (m->r.gpr[0] & ~0xff00ULL) | (((m->r.rflags & 0xd5) | 2) << 8);
+      return X_OK;
+    case 0xa0: case 0xa1: case 0xa2: case 0xa3: { /* mov moffs */
+      const int sz = (op & 1) ? osz : 1;
+      const int asz = d->pfx67 ? 4 : 8;
+      u64 addr = 0;
+      memcpy(&addr, d->bytes + d->len - asz, (size_t)asz);
+      addr += seg_base(m, d->seg);
+      if (op <= 0xa1) {
+        a = 0;
+        CHK(vread(m, addr, (u32)sz, &a));
+        setreg(m, d, 0, sz, a);
+      } else {
+        a = getreg(m, d, 0, sz);
+        CHK(vwrite(m, addr, (u32)sz, &a));
+      }
+      return X_OK;
+    }
+    case 0xa4: case 0xa5: case 0xa6: case 0xa7: case 0xaa: case 0xab: case 0xac: case 0xad:
+    case 0xae: case 0xaf: {
+      const int sz = (op & 1) ? osz : 1;
+      /* a fault inside rep keeps the completed iterations (rcx/rsi/rdi), rip stays */
+      if (string_op(m, d, op & ~1u, sz)) return X_FAULT_KEEP;
+      return X_OK;
+    }
+    case 0xa8:
+    case 0xa9: {
+      const int sz = op == 0xa8 ? 1 : osz;
+      int isz = op == 0xa8 ? 1 : (osz == 2 ? 2 : 4);
+      b = 0;
+      memcpy(&b, d->bytes + d->len - isz, (size_t)isz);
+      alu2(m, 4, getreg(m, d, 0, sz), sxn(b, isz), sz);
+      return X_OK;
+    }
+    case 0xb0: case 0xb1: case 0xb2: case 0xb3: case 0xb4: case 0xb5: case 0xb6: case 0xb7:
+      setreg(m, d, (op & 7) | (d->rexb << 3), 1, d->bytes[d->len - 1]);
+      return X_OK;
+    case 0xb8: case 0xb9: case 0xba: case 0xbb: case 0xbc: case 0xbd: case 0xbe: case 0xbf: {
+      int isz = osz;
+      a = 0;
+      memcpy(&a, d->bytes + d->len - isz, (size_t)isz);
+      setreg(m, d, (op & 7) | (d->rexb << 3), osz, a);
+      return X_OK;
+    }
+    case 0xc0: case 0xc1: case 0xd0: case 0xd1: case 0xd2: case 0xd3: {
+      const int sz = (op & 1) ? osz : 1;
+      u32 cnt = (op <= 0xc1) ? d->bytes[d->len - 1] : (op <= 0xd1 ? 1 : (u32)(m->r.gpr[1] & 0xff));
+      CHK(rd_rm_rmw(m, d, sz, &a));
+      u64 saved = m->r.rflags;
+      res = shift_op(m, (int)(d->reg & 7), a, cnt, sz);
+      if (wr_rm(m, d, sz, res)) {
+        m->r.rflags = saved;
+        return X_FAULT;
+      }
+      return X_OK;
+    }
+    case 0xc2:
+    case 0xc3: {
+      CHK(vread(m, m->r.gpr[WTFGPU_RSP], 8, &a));
+      u64 extra = 0;
+      if (op == 0xc2) extra = (u64)d->bytes[d->len - 2] | ((u64)d->bytes[d->len - 1] << 8);
+      m->r.gpr[WTFGPU_RSP] += 8 + extra;
+      *next_rip = a;
+      return X_OK;
+    }
+    case 0xc6:
+    case 0xc7: {
+      if ((d->reg & 7) != 0) return X_UNIMPL;
+      const int sz = op == 0xc6 ? 1 : osz;
+      int isz = op == 0xc6 ? 1 : (osz == 2 ? 2 : 4);
+      b = 0;
+      memcpy(&b, d->bytes + d->len - isz, (size_t)isz);
+      CHK(wr_rm(m, d, sz, sxn(b, isz)));
+      return X_OK;
+    }
+    case 0xc9: { /* leave */
+      u64 rbp = m->r.gpr[WTFGPU_RBP];
+      CHK(vread(m, rbp, 8, &a));
+      m->r.gpr[WTFGPU_RSP] = rbp + 8;
+      m->r.gpr[WTFGPU_RBP] = a;
+      return X_OK;
+    }
+    case 0xcc:
+      return X_INT3;
+    case 0xd7: { /* xlat */
+      u64 addr = (m->r.gpr[WTFGPU_RBX] + (m->r.gpr[0] & 0xff));
+      if (d->pfx67) addr &= 0xffffffffULL;
+      a = 0;
+      CHK(vread(m, addr + seg_base(m, d->seg), 1, &a));
+      setreg(m, d, 0, 1, a);
+      return X_OK;
+    }
+    case 0xe8: {
+      u64 rel = 0;
+      memcpy(&rel, d->bytes + d->len - 4, 4);
+      CHK(push64(m, nrip, 8));
+      *next_rip = nrip + sxn(rel, 4);
+      return X_OK;
+    }
+    case 0xe9: {
+      u64 rel = 0;
+      memcpy(&rel, d->bytes + d->len - 4, 4);
+      *next_rip = nrip + sxn(rel, 4);
+      return X_OK;
+    }
+    case 0xeb:
+      *next_rip = nrip + sxn(d->bytes[d->len - 1], 1);
+      return X_OK;
+    case 0xf4:
+      return X_HLT;
+    case 0xf5:
+      m->r.rflags ^= RF_CF;
+      return X_OK;
+    case 0xf6:
+    case 0xf7: {
+      const int sz = op == 0xf6 ? 1 : osz;
+      const int sub = (int)(d->reg & 7);
+      if (sub <= 1) { /* test */
+        int isz = op == 0xf6 ? 1 : (osz == 2 ? 2 : 4);
+        b = 0;
+        memcpy(&b, d->bytes + d->len - isz, (size_t)isz);
+        CHK(rd_rm(m, d, sz, &a));
+        alu2(m, 4, a, sxn(b, isz), sz);
+      } else if (sub == 2) { /* not */
+        CHK(rd_rm_rmw(m, d, sz, &a));
+        CHK(wr_rm(m, d, sz, ~a));
+      } else if (sub == 3) { /* neg */
+        CHK(rd_rm_rmw(m, d, sz, &a));
+        u64 saved = m->r.rflags;
+        res = alu2(m, 5, 0, a, sz);
+        if (wr_rm(m, d, sz, res)) {
+          m->r.rflags = saved;
+          return X_FAULT;
+        }
+      } else {
+        CHK(rd_rm(m, d, sz, &a));
+        if (muldiv(m, d, sub, sz, a)) return X_FAULT;
+      }
+      return X_OK;
+    }
+    case 0xf8: m->r.rflags &= ~RF_CF; return X_OK;
+    case 0xf9: m->r.rflags |= RF_CF; return X_OK;
+    case 0xfc: m->r.rflags &= ~RF_DF; return X_OK;
+    case 0xfd: m->r.rflags |= RF_DF; return X_OK;
+    case 0xfe:
+    case 0xff: {
+      const int sz = op == 0xfe ? 1 : osz;
+      const int sub = (int)(d->reg & 7);
+      if (sub <= 1) { /* inc/dec */
+        CHK(rd_rm_rmw(m, d, sz, &a));
+        u64 cf = m->r.rflags & RF_CF;
+        u64 saved = m->r.rflags;
+        res = alu2(m, sub ? 5 : 0, a, 1, sz);
+        m->r.rflags = (m->r.rflags & ~RF_CF) | cf;
+        if (wr_rm(m, d, sz, res)) {
+          m->r.rflags = saved;
+          return X_FAULT;
+        }
+        return X_OK;
+      }
+      if (op == 0xfe) return X_UNIMPL;
+      if (sub == 2 || sub == 4) { /* call / jmp near indirect (64-bit) */
+        CHK(rd_rm(m, d, 8, &a));
+        if (sub == 2) CHK(push64(m, nrip, 8));
+        *next_rip = a;
+        return X_OK;
+      }
+      if (sub == 6) { /* push r/m */
+        const int psz = d->pfx66 ? 2 : 8;
+        CHK(rd_rm(m, d, psz, &a));
+        CHK(push64(m, a, psz));
+        return X_OK;
+      }
+      return X_UNIMPL;
+    }
+    default:
+      return X_UNIMPL;
+    }
+  }
+
+  if (d->opmap == 1) {
+    switch (op) {
+    case 0x0b:
+      fault(m, WTFGPU_VEC_UD, 0);
+      return X_FAULT;
+    case 0x0d: /* prefetchw */
+    case 0x18: case 0x19: case 0x1a: case 0x1b: case 0x1c: case 0x1d: case 0x1e: case 0x1f:
+      return X_OK; /* hint nops, endbr64 */
+    case 0x40: case 0x41: case 0x42: case 0x43: case 0x44: case 0x45: case 0x46: case 0x47:
+    case 0x48: case 0x49: case 0x4a: case 0x4b: case 0x4c: case 0x4d: case 0x4e: case 0x4f:
+      CHK(rd_rm(m, d, osz, &a)); /* source always read */
+      if (cond(m, op & 0xf))
+        setreg(m, d, d->reg, osz, a);
+      else if (osz == 4)
+        setreg(m, d, d->reg, 4, m->r.gpr[d->reg]); /* zero upper half */
+      return X_OK;
+    case 0x80: case 0x81: case 0x82: case 0x83: case 0x84: case 0x85: case 0x86: case 0x87:
+    case 0x88: case 0x89: case 0x8a: case 0x8b: case 0x8c: case 0x8d: case 0x8e: case 0x8f: {
+      u64 rel = 0;
+      memcpy(&rel, d->bytes + d->len - 4, 4);
+      if (cond(m, op & 0xf)) *next_rip = nrip + sxn(rel, 4);
+      return X_OK;
+    }
+    case 0x90: case 0x91: case 0x92: case 0x93: case 0x94: case 0x95: case 0x96: case 0x97:
+    case 0x98: case 0x99: case 0x9a: case 0x9b: case 0x9c: case 0x9d: case 0x9e: case 0x9f:
+      CHK(wr_rm(m, d, 1, (u64)cond(m, op & 0xf)));
+      return X_OK;
+    case 0xa3: case 0xab: case 0xb3: case 0xbb: case 0xba: {
+      /* bt/bts/btr/btc */
+      int sub = op == 0xa3 ? 4 : op == 0xab ? 5 : op == 0xb3 ? 6 : op == 0xbb ? 7 : (int)(d->reg & 7);
+      if (sub < 4) return X_UNIMPL;
+      const int bits = 8 * osz;
+      u64 bitoff;
+      u64 addr = d->ea;
+      if (op == 0xba) {
+        bitoff = d->bytes[d->len - 1] & (u64)(bits - 1);
+      } else {
+        u64 r = getreg(m, d, d->reg, osz);
+        if (d->is_mem) {
+          i64 s = (i64)sxn(r, osz);
+          i64 word = s >> (osz == 8 ? 6 : osz == 4 ? 5 : 4);
+          addr = d->ea + (u64)(word * osz);
+          bitoff = (u64)s & (u64)(bits - 1);
+        } else {
+          bitoff = r & (u64)(bits - 1);
+        }
+      }
+      if (d->is_mem) {
+        if (sub == 4)
+          CHK(vread(m, addr, (u32)osz, &a) ? 1 : 0);
+        else
+          CHK(vread_rmw(m, addr, (u32)osz, &a) ? 1 : 0);
+      } else {
+        a = getreg(m, d, d->rm, osz);
+      }
+      int bit = (int)((a >> bitoff) & 1);
+      if (sub == 5) res = a | (1ULL << bitoff);
+      else if (sub == 6) res = a & ~(1ULL << bitoff);
+      else if (sub == 7) res = a ^ (1ULL << bitoff);
+      if (sub != 4) {
+        if (d->is_mem) {
+          CHK(vwrite(m, addr, (u32)osz, &res));
+        } else {
+          setreg(m, d, d->rm, osz, res);
+        }
+      }
+      set_flags(m, RF_CF, bit ? RF_CF : 0);
+      return X_OK;
+    }
+    case 0xa4: case 0xa5: case 0xac: case 0xad: { /* shld / shrd */
+      const int bits = 8 * osz;
+      u32 cnt = (op & 1) ? (u32)(m->r.gpr[1] & 0xff) : d->bytes[d->len - 1];
+      cnt &= (osz == 8) ? 0x3f : 0x1f;
+      CHK(rd_rm_rmw(m, d, osz, &a));
+      if (cnt == 0) return X_OK;
+      b = getreg(m, d, d->reg, osz);
+      const u64 mk = szmask(osz);
+      int cf;
+      if (osz == 2) {
+        /* 32-bit concatenation, count modulo 32 (U7) */
+        if (op <= 0xa5) { /* shift the 48-bit pattern a:b:a */
+          u64 pat = ((a & 0xffff) << 32) | ((b & 0xffff) << 16) | (a & 0xffff);
+          res = ((pat << cnt) >> 32) & 0xffff;
+          cf = (int)(((pat << (cnt - 1)) >> 47) & 1);
+        } else {
+          u64 pat = ((a & 0xffff)) | ((b & 0xffff) << 16) | ((a & 0xffff) << 32);
+          res = (pat >> cnt) & 0xffff;
+          cf = (int)((pat >> (cnt - 1)) & 1);
+        }
+      } else if (op <= 0xa5) {
+        res = ((a << cnt) | (b >> (bits - cnt))) & mk;
+        cf = (int)((a >> (bits - cnt)) & 1);
+      } else {
+        res = ((a >> cnt) | (b << (bits - cnt))) & mk;
+        cf = (int)((a >> (cnt - 1)) & 1);
+      }
+      u64 saved = m->r.rflags;
+      set_flags(m, RF_STATUS, szp(res, osz) | (cf ? RF_CF : 0) | ((msb(res, osz) ^ msb(a, osz)) ? RF_OF : 0));
+      if (wr_rm(m, d, osz, res)) {
+        m->r.rflags = saved;
+        return X_FAULT;
+      }
+      return X_OK;
+    }
+    case 0xaf:
+      CHK(rd_rm(m, d, osz, &a));
+      b = getreg(m, d, d->reg, osz);
+      {
+        __int128 p = (__int128)(i64)sxn(a & szmask(osz), osz) * (__int128)(i64)sxn(b & szmask(osz), osz);
+        u64 lo = (u64)p & szmask(osz);
+        int ovf = (__int128)(i64)sxn(lo, osz) != p;
+        setreg(m, d, d->reg, osz, lo);
+        set_flags(m, RF_STATUS, szp(lo, osz) | (ovf ? (RF_CF | RF_OF) : 0));
+      }
+      return X_OK;
+    case 0xb0:
+    case 0xb1: { /* cmpxchg: destination always written (SDM) */
+      const int sz = op == 0xb0 ? 1 : osz;
+      CHK(rd_rm_rmw(m, d, sz, &a));
+      u64 acc = getreg(m, d, 0, sz);
+      u64 saved = m->r.rflags;
+      alu2(m, 7, acc, a, sz);
+      if ((acc & szmask(sz)) == (a & szmask(sz))) {
+        if (wr_rm(m, d, sz, getreg(m, d, d->reg, sz))) {
+          m->r.rflags = saved;
+          return X_FAULT;
+        }
+      } else {
+        /* memory destinations are written back with the old value (locked cycle);
+         * a register destination is left untouched (its upper half survives) */
+        if (d->is_mem && wr_rm(m, d, sz, a)) {
+          m->r.rflags = saved;
+          return X_FAULT;
+        }
+        setreg(m, d, 0, sz, a);
+      }
+      return X_OK;
+    }
+    case 0xb6: case 0xb7: case 0xbe: case 0xbf: {
+      const int ssz = (op & 1) ? 2 : 1;
+      CHK(rd_rm(m, d, ssz, &a));
+      if (op >= 0xbe) a = sxn(a, ssz);
+      setreg(m, d, d->reg, osz, a & szmask(osz));
+      return X_OK;
+    }
+    case 0xb8: /* popcnt (f3) */
+      if (d->rep != 0xf3) return X_UNIMPL;
+      CHK(rd_rm(m, d, osz, &a));
+      res = (u64)__builtin_popcountll(a & szmask(osz));
+      setreg(m, d, d->reg, osz, res);
+      set_flags(m, RF_STATUS, a & szmask(osz) ? 0 : RF_ZF);
+      return X_OK;
+    case 0xbc:
+    case 0xbd: {
+      const int bits = 8 * osz;
+      CHK(rd_rm(m, d, osz, &a));
+      a &= szmask(osz);
+      if (d->rep == 0xf3) { /* tzcnt / lzcnt */
+        if (op == 0xbc) res = a ? (u64)__builtin_ctzll(a) : (u64)bits;
+        else res = a ? (u64)(__builtin_clzll(a) - (64 - bits)) : (u64)bits;
+        setreg(m, d, d->reg, osz, res);
+        set_flags(m, RF_CF | RF_ZF, (a == 0 ? RF_CF : 0) | (res == 0 ? RF_ZF : 0));
+        return X_OK;
+      }
+      if (a == 0) {
+        set_flags(m, RF_ZF, RF_ZF);
+        return X_OK;
+      }
+      res = op == 0xbc ? (u64)__builtin_ctzll(a) : (u64)(63 - __builtin_clzll(a));
+      setreg(m, d, d->reg, osz, res);
+      set_flags(m, RF_ZF, 0);
+      return X_OK;
+    }
+    case 0xc0:
+    case 0xc1: { /* xadd */
+      const int sz = op == 0xc0 ? 1 : osz;
+      CHK(rd_rm_rmw(m, d, sz, &a));
+      b = getreg(m, d, d->reg, sz);
+      u64 saved = m->r.rflags;
+      res = alu2(m, 0, a, b, sz);
+      if (wr_rm(m, d, sz, res)) {
+        m->r.rflags = saved;
+        return X_FAULT;
+      }
+      setreg(m, d, d->reg, sz, a);
+      return X_OK;
+    }
+    case 0xc8: case 0xc9: case 0xca: case 0xcb: case 0xcc: case 0xcd: case 0xce: case 0xcf: {
+      const u32 r = (op & 7) | (d->rexb << 3);
+      if (osz == 8) m->r.gpr[r] = __builtin_bswap64(m->r.gpr[r]);
+      else if (osz == 4) setreg(m, d, r, 4, __builtin_bswap32((u32)m->r.gpr[r]));
+      else setreg(m, d, r, 2, 0);
+      return X_OK;
+    }
+    default:
+      return X_UNIMPL;
+    }
+  }
+  return X_UNIMPL;
+}
+
+/* Decode at rip. Returns 0 ok, -1 fetch fault (exit filled), 1 unimplemented encoding. */
+static int decode(orc_machine *m, insn *d, memref *mr) {
+  memset(d, 0, sizeof(*d));
+  memset(mr, 0, sizeof(*mr));
+  d->start = m->r.rip;
+  u8 b;
+  /* legacy prefixes and REX; a REX not immediately before the opcode is ignored */
+  for (;;) {
+    b = fetch8(m, d);
+    if (d->fetch_fail) return -1;
+    if ((b & 0xf0) == 0x40) {
+      d->rex = b;
+      continue;
+    }
+    if (b == 0x66) d->pfx66 = 1;
+    else if (b == 0x67) d->pfx67 = 1;
+    else if (b == 0xf2 || b == 0xf3) d->rep = b;
+    else if (b == 0xf0) d->lock = 1;
+    else if (b == 0x64) d->seg = 4;
+    else if (b == 0x65) d->seg = 5;
+    else if (b == 0x26 || b == 0x2e || b == 0x36 || b == 0x3e) { /* null segments in 64-bit */ }
+    else break;
+    d->rex = 0;
+  }
+  if (d->rex) {
+    d->rexw = (d->rex >> 3) & 1;
+    d->rexr = (d->rex >> 2) & 1;
+    d->rexx = (d->rex >> 1) & 1;
+    d->rexb = d->rex & 1;
+  }
+  if (b == 0x0f) {
+    d->opmap = 1;
+    b = fetch8(m, d);
+    if (d->fetch_fail) return -1;
+    if (b == 0x38 || b == 0x3a) {
+      d->opmap = b == 0x38 ? 2 : 3;
+      d->op = fetch8(m, d);
+      d->len = d->pos;
+      return d->fetch_fail ? -1 : 1;
+    }
+  }
+  d->op = b;
+  const int osz = d->rexw ? 8 : (d->pfx66 ? 2 : 4);
+  const int izsz = osz == 2 ? 2 : 4;
+  int has_modrm = 0, imm = 0;
+  if (d->opmap == 0) {
+    switch (b) {
+    case 0x00: case 0x01: case 0x02: case 0x03: case 0x08: case 0x09: case 0x0a: case 0x0b:
+    case 0x10: case 0x11: case 0x12: case 0x13: case 0x18: case 0x19: case 0x1a: case 0x1b:
+    case 0x20: case 0x21: case 0x22: case 0x23: case 0x28: case 0x29: case 0x2a: case 0x2b:
+    case 0x30: case 0x31: case 0x32: case 0x33: case 0x38: case 0x39: case 0x3a: case 0x3b:
+    case 0x63: case 0x84: case 0x85: case 0x86: case 0x87: case 0x88: case 0x89: case 0x8a:
+    case 0x8b: case 0x8d: case 0x8f: case 0xd0: case 0xd1: case 0xd2: case 0xd3: case 0xfe:
+    case 0xff:
+      has_modrm = 1;
+      break;
+    case 0x04: case 0x0c: case 0x14: case 0x1c: case 0x24: case 0x2c: case 0x34: case 0x3c:
+    case 0x6a: case 0xa8: case 0xb0: case 0xb1: case 0xb2: case 0xb3: case 0xb4: case 0xb5:
+    case 0xb6: case 0xb7: case 0xeb:
+    case 0x70: case 0x71: case 0x72: case 0x73: case 0x74: case 0x75: case 0x76: case 0x77:
+    case 0x78: case 0x79: case 0x7a: case 0x7b: case 0x7c: case 0x7d: case 0x7e: case 0x7f:
+      imm = 1;
+      break;
+    case 0x05: case 0x0d: case 0x15: case 0x1d: case 0x25: case 0x2d: case 0x35: case 0x3d:
+    case 0xa9:
+      imm = izsz;
+      break;
+    case 0x68:
+      imm = d->pfx66 ? 2 : 4;
+      break;
+    case 0xe8: case 0xe9:
+      imm = 4;
+      break;
+    case 0xc2:
+      imm = 2;
+      break;
+    case 0xb8: case 0xb9: case 0xba: case 0xbb: case 0xbc: case 0xbd: case 0xbe: case 0xbf:
+      imm = osz;
+      break;
+    case 0xa0: case 0xa1: case 0xa2: case 0xa3:
+      imm = d->pfx67 ? 4 : 8;
+      break;
+    case 0x69:
+      has_modrm = 1;
+      imm = izsz;
+      break;
+    case 0x6b: case 0x80: case 0x83: case 0xc0: case 0xc1: case 0xc6:
+      has_modrm = 1;
+      imm = 1;
+      break;
+    case 0x81: case 0xc7:
+      has_modrm = 1;
+      imm = izsz;
+      break;
+    case 0xf6: case 0xf7:
+      has_modrm = 1;
+      break;
+    default:
+      break;
+    }
+  } else {
+    if ((b >= 0x40 && b <= 0x4f) || (b >= 0x90 && b <= 0x9f) || b == 0xa3 || b == 0xab ||
+        b == 0xb3 || b == 0xbb || b == 0xaf || b == 0xb0 || b == 0xb1 || b == 0xb6 ||
+        b == 0xb7 || b == 0xbe || b == 0xbf || b == 0xbc || b == 0xbd || b == 0xb8 ||
+        b == 0xc0 || b == 0xc1 || b == 0xa5 || b == 0xad || b == 0x0d ||
+        (b >= 0x18 && b <= 0x1f))
+      has_modrm = 1;
+    if (b == 0xa4 || b == 0xac || b == 0xba) {
+      has_modrm = 1;
+      imm = 1;
+    }
+    if (b >= 0x80 && b <= 0x8f) imm = 4;
+  }
+  if (has_modrm) {
+    decode_modrm(m, d, mr);
+    if (d->fetch_fail) return -1;
+  }
+  if (d->opmap == 0 && (b == 0xf6 || b == 0xf7) && ((d->reg & 7) <= 1)) imm = b == 0xf6 ? 1 : izsz;
+  for (int i = 0; i < imm; i++) {
+    fetch8(m, d);
+    if (d->fetch_fail) return -1;
+  }
+  d->len = d->pos;
+  finish_ea(m, d, mr);
+  return 0;
+}
+
+static void fill_exit(orc_machine *m, wtfgpu_exit_t *ex, u32 status) {
+  ex->status = status;
+  ex->rip = m->r.rip;
+  ex->icount = m->icount;
+}
+
+/* One instruction: fetch, decode, coverage, breakpoint, execute, retire. */
+static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
+  insn d;
+  memref mr;
+  memset(ex, 0, sizeof(*ex));
+  m->ex = ex;
+  m->faulted = 0;
+  int rc = decode(m, &d, &mr);
+  if (rc < 0) {
+    if (d.fetch_fail == 2) {
+      ex->status = WTFGPU_EXIT_FAULT;
+      ex->vector = WTFGPU_VEC_GP;
+      ex->error = 0;
+      ex->addr = 0;
+    }
+    fill_exit(m, ex, WTFGPU_EXIT_FAULT);
+    return ex->status;
+  }
+  /* coverage (bochscpu_backend.cc:501-504) then breakpoint lookup (:545-547) */
+  if (!hm_has(&m->cov, m->r.rip)) {
+    *hm_slot(&m->cov, m->r.rip, 1) = (void *)1;
+    vec_push(&m->covlist, m->r.rip);
+  }
+  if (check_bp && hm_has(&m->bps, m->r.rip)) {
+    fill_exit(m, ex, WTFGPU_EXIT_BREAKPOINT);
+    return ex->status;
+  }
+  if (rc == 1) {
+    memcpy(&ex->opcode, d.bytes, 4);
+    fill_exit(m, ex, WTFGPU_EXIT_UNIMPLEMENTED);
+    return ex->status;
+  }
+  wtfgpu_regs_t saved = m->r;
+  u64 saved_bytes = m->bytes;
+  u64 next = 0;
+  int x = exec_insn(m, &d, &mr, &next);
+  if (x == X_OK) {
+    m->r.rip = next;
+    m->bytes += d.len;
+    m->icount++;
+    if (m->limit > 0 && m->icount > m->limit) {
+      fill_exit(m, ex, WTFGPU_EXIT_TIMEOUT);
+      return ex->status;
+    }
+    ex->status = WTFGPU_RUNNING;
+    return WTFGPU_RUNNING;
+  }
+  /* not retired: registers rolled back (memory writes precede register updates),
+   * except rep string progress which is architecturally committed */
+  if (x == X_FAULT_KEEP) {
+    m->r.rip = saved.rip;
+    x = X_FAULT;
+  } else {
+    m->r = saved;
+    m->bytes = saved_bytes;
+  }
+  switch (x) {
+  case X_FAULT: {
+    wtfgpu_exit_t keep = *ex;
+    fill_exit(m, ex, WTFGPU_EXIT_FAULT);
+    ex->vector = keep.vector;
+    ex->error = keep.error;
+    ex->addr = keep.addr;
+    break;
+  }
+  case X_UNIMPL:
+    memcpy(&ex->opcode, d.bytes, 4);
+    fill_exit(m, ex, WTFGPU_EXIT_UNIMPLEMENTED);
+    break;
+  case X_INT3: fill_exit(m, ex, WTFGPU_EXIT_INT3); break;
+  case X_HLT: fill_exit(m, ex, WTFGPU_EXIT_HLT); break;
+  default: fill_exit(m, ex, WTFGPU_EXIT_UNIMPLEMENTED); break;
+  }
+  return ex->status;
+}
+
+int orc_run(orc_machine *m, int skip_bp, wtfgpu_exit_t *ex) {
+  int first = 1;
+  for (;;) {
+    int st = one(m, !(first && skip_bp), ex);
+    first = 0;
+    if (st != WTFGPU_RUNNING) return st;
+  }
+}
+
+int orc_step(orc_machine *m, wtfgpu_exit_t *ex) { return one(m, 0, ex); }
