@@ -1370,7 +1370,9 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
       u32 cnt = (op & 1) ? (u32)(m->r.gpr[1] & 0xff) : d->bytes[d->len - 1];
       cnt &= (osz == 8) ? 0x3f : 0x1f;
       CHK(rd_rm_rmw(m, d, osz, &a));
-      if (cnt == 0) return X_OK;
+      /* count 0: flags untouched, but the destination is still written (a
+       * 32-bit register is zero-extended, as measured on hardware) */
+      if (cnt == 0) return wr_rm(m, d, osz, a) ? X_FAULT : X_OK;
       b = getreg(m, d, d->reg, osz);
       const u64 mk = szmask(osz);
       int cf;
@@ -1474,13 +1476,10 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
       const int sz = op == 0xc0 ? 1 : osz;
       CHK(rd_rm_rmw(m, d, sz, &a));
       b = getreg(m, d, d->reg, sz);
-      u64 saved = m->r.rflags;
       res = alu2(m, 0, a, b, sz);
-      if (wr_rm(m, d, sz, res)) {
-        m->r.rflags = saved;
-        return X_FAULT;
-      }
+      /* SDM: TEMP := SRC + DEST; SRC := DEST; DEST := TEMP (xadd r,r keeps the sum) */
       setreg(m, d, d->reg, sz, a);
+      if (wr_rm(m, d, sz, res)) return X_FAULT; /* registers are rolled back by the caller */
       return X_OK;
     }
     case 0xc8: case 0xc9: case 0xca: case 0xcb: case 0xcc: case 0xcd: case 0xce: case 0xcf: {

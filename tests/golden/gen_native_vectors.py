@@ -268,6 +268,21 @@ def gen_forms(rng):
         # cbw/cwd
         forms.append(Enc(pfx(size) + ([0x48] if size == 8 else []) + [0x98], f"cbw.{size}"))
         forms.append(Enc(pfx(size) + ([0x48] if size == 8 else []) + [0x99], f"cwd.{size}"))
+    # count-0 forms: the destination is still written (32-bit registers zero-extend)
+    for size in (2, 4, 8):
+        for opc in (0xA4, 0xAC):
+            forms.append(Enc(rr([0x0F, opc], size, RBX, 13, rng) + [0], f"shxd0.{opc:x}.{size}", fmask=STATUS))
+            forms.append(Enc(rr([0x0F, opc], size, RBX, 13, rng) + [32], f"shxd32.{opc:x}.{size}",
+                             fmask=STATUS if size != 8 else STATUS & ~AF & ~OF))
+        for sub in range(8):
+            forms.append(Enc(rr([0xC1], size, sub, 14, rng) + [0], f"shift0.{sub}.{size}", fmask=STATUS))
+    # same-register forms (xadd r,r: SRC := DEST then DEST := TEMP)
+    for r in (RAX, RBX, 9, 13):
+        for size in (1, 2, 4, 8):
+            b = size == 1
+            forms.append(Enc(rr([0x0F, 0xC0 if b else 0xC1], size, r, r, rng, b), f"xadd.same{size}.{r}"))
+            forms.append(Enc(rr([0x0F, 0xB0 if b else 0xB1], size, r, r, rng, b), f"cmpxchg.same{size}.{r}", cls="cmpxchg"))
+            forms.append(Enc(rr([0x86 if b else 0x87], size, r, r, rng, b), f"xchg.same{size}.{r}"))
     # bswap
     for r in range(16):
         if r == RSP:

@@ -1,0 +1,118 @@
+"""Random x86-64 programs for GPU-vs-oracle differential tests.
+
+A program is a chain of blocks; each block re-establishes the pointer
+registers its instruction form needs (mov r64, imm64 into a data window) and
+then runs one random form drawn from the native-vector generator's encodings
+(tests/golden/gen_native_vectors.py). Some blocks are guarded by a forward
+conditional jump, some jump backwards through a counted loop. Programs end in
+int3. Faults (#DE, #PF on a read-only page, ...) end a lane early; both
+engines must agree on that too.
+"""
+from __future__ import annotations
+
+import random
+
+from tests.golden.gen_native_vectors import RCX, RDI, RSI, RSP, gen_forms
+from wtf_amd.abi import regs_from_state
+from wtf_amd.tools.snapshot import AddressSpace, user_state
+
+CODE_VA = 0x100000000
+SLOT = 0x2000
+WIN_VA = 0x200000000     # two RW pages
+RO_VA = 0x200002000      # one read-only page right after (writes fault)
+STACK_VA = 0x300000000   # two pages
+STACK_TOP = STACK_VA + 0x2000 - 0x100
+
+
+def mov_imm64(r, v):
+    return bytes([0x48 | (r >> 3), 0xB8 + (r & 7)]) + (v & 0xFFFFFFFFFFFFFFFF).to_bytes(8, "little")
+
+
+def make_program(rng: random.Random, forms, n_blocks=24) -> bytes:
+    code = bytearray()
+    for _ in range(n_blocks):
+        f = rng.choice(forms)
+        if f.cls == "div" and rng.random() < 0.7:
+            continue
+        setup = bytearray()
+        base = WIN_VA + rng.choice([0x100, 0x800, 0xF00, 0xFF8 - 0x80])
+        for r, off in f.ptrs.items():
+            setup += mov_imm64(r, base + off)
+        for r, (lo, hi) in f.smalls.items():
+            setup += mov_imm64(r, rng.randint(lo, hi))
+        if f.cls == "string":
+            setup += mov_imm64(RSI, WIN_VA + rng.randrange(0x40, 0x1F00))
+            setup += mov_imm64(RDI, rng.choice([WIN_VA + rng.randrange(0x40, 0x1F00), RO_VA - 4]))
+            setup += mov_imm64(RCX, rng.randrange(0, 12))
+        if f.cls in ("stack", "popf"):
+            setup += mov_imm64(RSP, STACK_TOP - rng.randrange(0, 32) * 8)
+        block = bytes(setup) + f.code
+        r = rng.random()
+        if r < 0.15 and len(block) < 120:
+            code += bytes([0x70 + rng.randrange(16), len(block)])  # jcc over the block
+        elif r < 0.2 and len(block) < 100:
+            # a short counted loop around the block: mov ecx, k ; block ; dec ecx ; jnz
+            k = rng.randrange(1, 4)
+            code += bytes([0xB9]) + k.to_bytes(4, "little")
+            body = block + bytes([0xFF, 0xC9])
+            code += body + bytes([0x75, (-(len(body) + 2)) & 0xFF])
+            continue
+        code += block
+        if len(code) > SLOT - 64:
+            break
+    code += b"\xcc"
+    return bytes(code[:SLOT])
+
+
+def build(n_programs: int, seed: int):
+    """Returns (AddressSpace, base state, list of (code_va, regs dict))."""
+    rng = random.Random(seed)
+    forms = gen_forms(random.Random(seed ^ 0xABCDEF))
+    sp = AddressSpace()
+    progs = []
+    for i in range(n_programs):
+        code = make_program(rng, forms)
+        va = CODE_VA + i * SLOT
+        sp.map_range(va, code + b"\xcc" * (SLOT - len(code)), write=False)
+        progs.append(va)
+    win = bytes(rng.getrandbits(8) for _ in range(0x2000))
+    sp.map_range(WIN_VA, win, nx=True)
+    sp.map(RO_VA, bytes(rng.getrandbits(8) for _ in range(0x1000)), write=False, nx=True)
+    sp.map_range(STACK_VA, bytes(0x2000), nx=True)
+    st = user_state(CODE_VA, STACK_TOP, sp.cr3)
+    lanes = []
+    for i, va in enumerate(progs):
+        regs = [rng.getrandbits(64) for _ in range(16)]
+        regs[RSP] = STACK_TOP
+        flags = 0x202 | (rng.getrandbits(12) & 0x8D5)
+        lanes.append((va, regs, flags))
+    return sp, st, lanes
+
+
+def oracle_run(sp: AddressSpace, st: dict, lanes, limit=20000, breakpoints=()):
+    """Runs every lane on the CPU oracle; returns per-lane result dicts."""
+    from tests.oracle_lib import Oracle
+
+    pfns, blob = sp.phys()
+    o = Oracle(pfns=pfns, blob=blob)
+    base = regs_from_state(st)
+    o.set_limit(limit)
+    o.set_breakpoints(list(breakpoints))
+    out = []
+    for va, regs, flags in lanes:
+        r = regs_from_state(st)
+        for k in range(16):
+            r.gpr[k] = regs[k]
+        r.rip = va
+        r.rflags = flags
+        o.restore(base)
+        o.set_regs(r)
+        ex = o.run()
+        rr = o.regs()
+        out.append({
+            "status": ex.status, "vector": ex.vector, "error": ex.error, "addr": ex.addr, "rip": rr.rip,
+            "icount": ex.icount, "gpr": list(rr.gpr), "rflags": rr.rflags, "cov": set(o.coverage()),
+            "dirty": set(o.dirty()), "bytes": o.nbytes(),
+            "win": o.read_virt(WIN_VA, 0x2000), "stack": o.read_virt(STACK_VA, 0x2000),
+        })
+    return out

@@ -1,0 +1,1379 @@
+// engine.hip — kernels + host implementation of the C ABI in include/wtfgpu.h.
+//
+// Hot kernel: k_run, the RIP-grouped lane-per-testcase x86-64 interpreter
+// (engine_device.h explains the scheme). Everything else here is plumbing:
+// lane restore (the dirty-list reset that replaces bochscpu's per-page memcpy,
+// bochscpu_backend.cc:730-797), batched guest-memory writes for host-side
+// handlers, coverage log compaction and the aggregate coverage map.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "engine_ops.h"
+
+using namespace wtfgpu_dev;
+
+// ====================================================================== device
+namespace {
+
+__device__ __forceinline__ u64 wave_min(u64 v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const u64 o = __shfl_xor(v, off, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+__device__ __forceinline__ u64 wave_sum(u64 v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ u64 readlane64(u64 v, int l) {
+  const u32 lo = __builtin_amdgcn_readlane((u32)v, l);
+  const u32 hi = __builtin_amdgcn_readlane((u32)(v >> 32), l);
+  return ((u64)hi << 32) | lo;
+}
+
+__device__ __forceinline__ bool hash_find(const u64 *keys, u32 mask, u64 key, u32 &slot) {
+  u32 h = (u32)mix64(key) & mask;
+  for (u32 i = 0; i <= mask; i++) {
+    const u64 k = rfl64(keys[h]);
+    if (k == key) {
+      slot = h;
+      return true;
+    }
+    if (k == EMPTY_KEY) return false;
+    h = (h + 1) & mask;
+  }
+  return false;
+}
+
+__device__ __forceinline__ void load_lane(const Dev &P, u32 lane, Lane &L) {
+  const u64 N = P.nlanes;
+#pragma unroll
+  for (int i = 0; i < 16; i++) R(L, i) = P.gpr[i * N + lane];
+  L.rip = P.rip[lane];
+  L.rflags = P.rflags[lane];
+  L.icount = P.icount[lane];
+  L.nbytes = P.nbytes[lane];
+  L.status = P.status[lane];
+  const LaneSys s = P.sys[lane];
+  L.cr0 = s.cr0;
+  L.cr3 = s.cr3;
+  L.efer = s.efer;
+  L.cpl = s.cpl;
+  L.ovn = P.ov_count[lane];
+  L.bloom = 0;
+  for (u32 k = 0; k < L.ovn; k++) L.bloom |= bloom_bit(P.ov_gpfn[(u64)k * N + lane]);
+  L.lane = lane;
+  tlb_flush(L);
+  L.tnext = 0;
+  L.exvec = L.exerr = L.exop = 0;
+  L.exaddr = 0;
+  L.miss = L.miss_acc = L.flush = L.pend = 0;
+  L.miss_va = 0;
+}
+
+__device__ __forceinline__ void store_lane(const Dev &P, const Lane &L) {
+  const u64 N = P.nlanes;
+  const u32 lane = L.lane;
+#pragma unroll
+  for (int i = 0; i < 16; i++) P.gpr[i * N + lane] = R(L, i);
+  P.rip[lane] = L.rip;
+  P.rflags[lane] = L.rflags;
+  P.icount[lane] = L.icount;
+  P.nbytes[lane] = L.nbytes;
+  P.status[lane] = L.status;
+  P.ov_count[lane] = L.ovn;
+}
+
+// Coverage (bochscpu_backend.cc:501-504): every executed rip absent from the
+// aggregate map is logged once per wave with the mask of lanes that ran it.
+__device__ __forceinline__ void cover(const Dev &P, u64 rip, u64 gmask, u32 wv, u32 lid, u64 &cvpn, int &cslot,
+                                      u32 ep) {
+  const u64 vpn = rip >> 12;
+  if (vpn != cvpn) {
+    cvpn = vpn;
+    u32 s;
+    cslot = (P.code_keys && hash_find(P.code_keys, P.code_mask, vpn, s)) ? (int)rfl32(P.code_slot[s]) : -1;
+  }
+  if (cslot >= 0) {
+    const u32 byte = rfl32(P.cov_map[(u64)cslot * WTFGPU_PAGE_SIZE + (rip & 0xfff)]);
+    if (byte) return;
+  }
+  const u32 H = P.H;
+  const u64 base = (u64)wv * H;
+  u32 h = (u32)mix64(rip) & (H - 1);
+  for (u32 probe = 0; probe < H; probe++) {
+    const u64 idx = base + h;
+    const u32 e = rfl32(P.cov_ep[idx]);
+    if (e != ep) {
+      if (lid == 0) {
+        P.cov_rip[idx] = rip;
+        P.cov_mask[idx] = gmask;
+        P.cov_ep[idx] = ep;
+      }
+      return;
+    }
+    if (rfl64(P.cov_rip[idx]) == rip) {
+      const u64 m = rfl64(P.cov_mask[idx]);
+      if ((m | gmask) != m && lid == 0) P.cov_mask[idx] = m | gmask;
+      return;
+    }
+    h = (h + 1) & (H - 1);
+  }
+  if (lid == 0) P.cov_overflow[wv] = 1;
+}
+
+// Uniform fetch of up to 16 bytes at page pointer p (within one page).
+__device__ __forceinline__ void fetch_bytes(u64 pageptr, u32 off, u32 n, u64 &lo, u64 &hi) {
+  // n <= 16 and off + n <= 4096
+  const u64 a = (pageptr + off) & ~7ull;
+  const u32 sh = (u32)((pageptr + off) & 7);
+  const u64 pend = pageptr + WTFGPU_PAGE_SIZE;
+  const u64 w0 = rfl64(*(const u64 *)a);
+  const u64 w1 = (a + 8 < pend) ? rfl64(*(const u64 *)(a + 8)) : 0;
+  const u64 w2 = (a + 16 < pend) ? rfl64(*(const u64 *)(a + 16)) : 0;
+  if (sh == 0) {
+    lo = w0;
+    hi = w1;
+  } else {
+    lo = (w0 >> (8 * sh)) | (w1 << (64 - 8 * sh));
+    hi = (w1 >> (8 * sh)) | (w2 << (64 - 8 * sh));
+  }
+  if (n < 16) {
+    if (n <= 8) {
+      hi = 0;
+      lo = n == 8 ? lo : (lo & ((1ull << (8 * n)) - 1));
+    } else {
+      hi &= (1ull << (8 * (n - 8))) - 1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- main kernel
+__global__ __launch_bounds__(256) void k_run(Dev P, u32 first, u32 count, u64 max_steps) {
+  const u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 lane = first + tid;
+  const bool valid = tid < count && lane < P.nlanes;
+  const u32 lid = threadIdx.x & 63;
+  const u32 wv = lane >> 6;  // first is 64-aligned: hardware wave == log wave
+  __shared__ u64 sG[16 * GPR_STRIDE];
+  Lane L;
+  L.g = &sG[threadIdx.x];
+  if (valid) {
+    load_lane(P, lane, L);
+  } else {
+    L.status = WTFGPU_EXIT_IDLE;
+    L.lane = 0;
+    L.rip = 0;
+    L.icount = 0;
+  }
+  const u64 icount0 = L.icount;
+  bool skip = valid && (P.lflags[lane] & 1);
+  const u32 ep = (P.cov_rip && wv < (P.nlanes + 63) / 64) ? rfl32(P.cov_wave_ep[rfl32(wv)]) : 0;
+  u64 cvpn = EMPTY_KEY;
+  int cslot = -1;
+  u64 steps = 0;
+
+  while (steps < max_steps) {
+    const bool active = valid && L.status == WTFGPU_RUNNING;
+    const u64 grip = rfl64(wave_min(active ? L.rip : EMPTY_KEY));
+    if (grip == EMPTY_KEY) break;
+    steps++;
+    bool cand = active && L.rip == grip;
+    u64 cptr = 0;
+    if (cand) {
+      u64 td;
+      if (!tlb_get(L, grip >> 12, td) || !perm_ok(L, td, ACC_X)) {
+        if (service_miss(P, L, grip & ~0xfffull, ACC_X)) tlb_get(L, grip >> 12, td);
+        else td = 0;
+        if (td && !perm_ok(L, td, ACC_X)) td = 0;
+        if (!td && L.status == WTFGPU_EXIT_FAULT) L.exaddr = grip;
+      }
+      if (td) cptr = td & ~0xfffull;
+      else cand = false;
+    }
+    u64 cm = __ballot(cand);
+    if (cm == 0) continue;
+    int leader = __ffsll((long long)cm) - 1;
+    const u64 lptr = readlane64(cptr, leader);
+    bool ing = cand && cptr == lptr;
+
+    // ---- fetch + decode, once per group (uniform)
+    const u32 off = (u32)(grip & 0xfff);
+    IBytes ib;
+    ib.avail = 4096 - off < 16 ? 4096 - off : 16;
+    fetch_bytes(lptr, off, ib.avail, ib.lo, ib.hi);
+    UOp d;
+    int dr = decode(ib, d);
+    if (dr == 1) {
+      // the instruction continues on the next page: translate it per lane
+      u64 nptr = 0;
+      if (ing) {
+        const u64 va2 = (grip & ~0xfffull) + 4096;
+        u64 td;
+        if (!tlb_get(L, va2 >> 12, td) || !perm_ok(L, td, ACC_X)) {
+          if (service_miss(P, L, va2, ACC_X)) tlb_get(L, va2 >> 12, td);
+          else td = 0;
+        }
+        if (td) nptr = td & ~0xfffull;
+        else ing = false;
+      }
+      cm = __ballot(ing);
+      if (cm == 0) continue;
+      leader = __ffsll((long long)cm) - 1;
+      const u64 lnptr = readlane64(nptr, leader);
+      ing = ing && nptr == lnptr;
+      const u32 n0 = ib.avail;
+      u64 lo2, hi2;
+      fetch_bytes(lnptr, 0, 16 - n0, lo2, hi2);
+      // splice: bytes [0,n0) from page 1, [n0,16) from page 2
+      if (n0 >= 8) {
+        ib.hi = (n0 == 8 ? 0 : ib.hi) | (n0 == 8 ? lo2 : (lo2 << (8 * (n0 - 8))));
+      } else {
+        ib.lo = ib.lo | (lo2 << (8 * n0));
+        ib.hi = (lo2 >> (64 - 8 * n0)) | (hi2 << (8 * n0));
+      }
+      ib.avail = 16;
+      dr = decode(ib, d);
+    }
+    const u64 gmask = __ballot(ing);
+    if (dr == 2) {
+      if (ing) set_fault(L, WTFGPU_VEC_GP, 0, 0);
+      continue;
+    }
+    if (gmask == 0) continue;
+
+    // ---- coverage, then breakpoint (bochscpu_backend.cc:501-547)
+    if (P.cov_rip) cover(P, grip, gmask, wv, lid, cvpn, cslot, ep);
+    bool isbp = false;
+    if (P.bp_keys) {
+      u32 s;
+      isbp = hash_find(P.bp_keys, P.bp_mask, grip, s);
+    }
+    if (ing) {
+      if (isbp && !skip) {
+        L.status = WTFGPU_EXIT_BREAKPOINT;
+        ing = false;
+      }
+      skip = false;
+    }
+    if (!d.supported) {
+      if (ing) {
+        L.status = WTFGPU_EXIT_UNIMPLEMENTED;
+        L.exop = d.len >= 4 ? d.opbytes : (d.opbytes & ((1u << (8 * d.len)) - 1));
+      }
+      continue;
+    }
+    if (ing) {
+      u64 next = 0;
+      int x;
+      // restartable execution: a TLB miss / first write abandons the attempt,
+      // service_miss fills the TLB (or copies the page), the attempt reruns
+      for (int attempt = 0;; attempt++) {
+        L.miss = 0;
+        L.pend = 0;
+        x = exec(P, L, d, grip + d.len, next);
+        if (!L.miss || L.status != WTFGPU_RUNNING) break;
+        if (attempt >= 16 || !service_miss(P, L, L.miss_va, (int)L.miss_acc)) {
+          if (attempt >= 16) set_fault(L, WTFGPU_VEC_GP, 0xffff, L.miss_va);
+          break;
+        }
+      }
+      if (L.flush) {
+        tlb_flush(L);
+        L.flush = 0;
+      }
+      if (x == X_OK && L.status == WTFGPU_RUNNING) {
+        L.rip = next;
+        L.icount++;
+        L.nbytes += d.len + L.pend;
+        if (P.limit && L.icount > P.limit) L.status = WTFGPU_EXIT_TIMEOUT;
+      } else if (L.status != WTFGPU_RUNNING) {
+        // faulted / overlay full inside exec or service_miss; rip unchanged
+      } else if (x == X_UNIMPL) {
+        L.status = WTFGPU_EXIT_UNIMPLEMENTED;
+        L.exop = d.len >= 4 ? d.opbytes : (d.opbytes & ((1u << (8 * d.len)) - 1));
+      } else if (x == X_INT3) {
+        L.status = WTFGPU_EXIT_INT3;
+      } else if (x == X_HLT) {
+        L.status = WTFGPU_EXIT_HLT;
+      }
+      // X_FAULT / 6: status already FAULT or OVERLAY_FULL; rip unchanged
+    }
+  }
+
+  if (valid) {
+    store_lane(P, L);
+    if (L.status == WTFGPU_EXIT_FAULT || L.status == WTFGPU_EXIT_UNIMPLEMENTED) {
+      ExitInfo e;
+      e.vector = L.exvec;
+      e.error = L.exerr;
+      e.opcode = L.exop;
+      e.pad = 0;
+      e.addr = L.exaddr;
+      P.exinfo[lane] = e;
+    }
+    P.lflags[lane] = skip ? 1u : 0u;
+  }
+  const u64 retired = wave_sum(valid ? L.icount - icount0 : 0);
+  const u64 running = wave_sum((valid && L.status == WTFGPU_RUNNING) ? 1 : 0);
+  if (lid == 0) {
+    atomicAdd((unsigned long long *)&P.stat[0], (unsigned long long)steps);
+    atomicAdd((unsigned long long *)&P.stat[1], (unsigned long long)retired);
+    if (running) atomicAdd((unsigned long long *)&P.stat[2], (unsigned long long)running);
+  }
+}
+
+// ---------------------------------------------------------------- restore
+struct InitState {
+  u64 g[16];
+  u64 rip, rflags, fsb, gsb;
+  LaneSys sys;
+};
+
+__global__ void k_restore(Dev P, const InitState *S, u32 first, u32 count) {
+  const u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 lane = first + tid;
+  if (tid >= count || lane >= P.nlanes) return;
+  const u64 N = P.nlanes;
+  const InitState s = *S;
+#pragma unroll
+  for (int i = 0; i < 16; i++) P.gpr[i * N + lane] = s.g[i];
+  P.rip[lane] = s.rip;
+  P.rflags[lane] = s.rflags;
+  P.fs_base[lane] = s.fsb;
+  P.gs_base[lane] = s.gsb;
+  P.icount[lane] = 0;
+  P.nbytes[lane] = 0;
+  P.status[lane] = WTFGPU_RUNNING;
+  P.lflags[lane] = 0;
+  P.sys[lane] = s.sys;
+  P.ov_count[lane] = 0;  // the dirty-list reset: overlays dropped, nothing copied
+  if (P.cov_rip) {
+    const u32 wv = lane >> 6;
+    const u32 w0 = wv * 64, w1 = w0 + 64;
+    const bool whole = w0 >= first && w1 <= first + count;
+    if ((lane & 63) == 0 && whole) {
+      P.cov_wave_ep[wv] += 1;  // invalidates every log entry of the wave
+      P.cov_overflow[wv] = 0;
+    } else if (!whole) {
+      // partial wave: drop this lane's bit from the wave's entries
+      for (u32 h = 0; h < P.H; h++) {
+        const u64 idx = (u64)wv * P.H + h;
+        if (P.cov_ep[idx] == P.cov_wave_ep[wv])
+          atomicAnd((unsigned long long *)&P.cov_mask[idx], ~(1ull << (lane & 63)));
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- host-driven lane memory
+// One thread per lane with pending writes (records sorted by lane). op: 0 write virt.
+struct WriteRec {
+  u32 lane, len;
+  u64 gva, data_off;
+};
+
+__device__ __forceinline__ void lane_min_load(const Dev &P, u32 lane, Lane &L) {
+  const LaneSys s = P.sys[lane];
+  L.cr0 = s.cr0;
+  L.cr3 = s.cr3;
+  L.efer = s.efer;
+  L.cpl = 0;  // host accesses are not subject to user checks (VirtTranslate has none)
+  L.ovn = P.ov_count[lane];
+  L.bloom = 0;
+  for (u32 k = 0; k < L.ovn; k++) L.bloom |= bloom_bit(P.ov_gpfn[(u64)k * P.nlanes + lane]);
+  L.lane = lane;
+  L.status = WTFGPU_RUNNING;
+  L.nbytes = 0;
+  tlb_flush(L);
+  L.tnext = 0;
+  L.miss = L.miss_acc = L.flush = L.pend = 0;
+}
+
+// Host-side translation (bochscpu_mem_virt_translate semantics: present bits
+// only, no permission checks).
+__device__ __forceinline__ bool host_walk(const Dev &P, Lane &L, u64 va, u64 &gpa) {
+  u64 table = L.cr3 & 0x000ffffffffff000ull;
+  bool priv;
+  u64 e = 0, pmask = 0xfff;
+  for (int level = 3; level >= 0; level--) {
+    const u8 *pg = phys_page(P, L.lane, L.ovn, L.bloom, table >> 12, priv);
+    e = *(const u64 *)(pg + ((va >> (12 + 9 * level)) & 0x1ff) * 8);
+    if (!(e & 1)) return false;
+    if ((level == 1 || level == 2) && (e & 0x80)) {
+      pmask = level == 2 ? 0x3fffffffull : 0x1fffffull;
+      break;
+    }
+    table = e & 0x000ffffffffff000ull;
+  }
+  gpa = ((e & 0x000ffffffffff000ull) & ~pmask) | (va & pmask);
+  return true;
+}
+
+// Write len bytes at gpa into the lane's overlay (copy-on-write + dirty).
+__device__ __forceinline__ bool lane_phys_write(const Dev &P, Lane &L, u64 gpa, const u8 *src, u64 len) {
+  while (len) {
+    const u64 off = gpa & 0xfff;
+    u64 n = 4096 - off;
+    if (n > len) n = len;
+    bool priv;
+    const u8 *pg = phys_page(P, L.lane, L.ovn, L.bloom, gpa >> 12, priv);
+    u8 *dst = (u8 *)pg;
+    if (!priv) {
+      if (L.ovn >= P.K) return false;
+      dst = cow_copy(P, L.lane, L.ovn, gpa >> 12, pg);
+      L.ovn++;
+      L.bloom |= bloom_bit(gpa >> 12);
+    }
+    for (u64 i = 0; i < n; i++) dst[off + i] = src[i];
+    src += n;
+    gpa += n;
+    len -= n;
+  }
+  return true;
+}
+
+__global__ void k_apply_writes(Dev P, const WriteRec *recs, const u32 *starts, u32 nlanes_w, const u8 *data,
+                               i32 *status_out) {
+  const u32 t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nlanes_w) return;
+  const u32 r0 = starts[t], r1 = starts[t + 1];
+  const u32 lane = recs[r0].lane;
+  Lane L;
+  lane_min_load(P, lane, L);
+  for (u32 r = r0; r < r1; r++) {
+    const WriteRec w = recs[r];
+    u64 va = w.gva, left = w.len;
+    const u8 *src = data + w.data_off;
+    i32 st = 0;
+    while (left) {
+      const u64 off = va & 0xfff;
+      u64 n = 4096 - off;
+      if (n > left) n = left;
+      u64 gpa;
+      if (!host_walk(P, L, va, gpa)) {
+        st = WTFGPU_ERR_TRANSLATE;
+        break;
+      }
+      if (!lane_phys_write(P, L, gpa, src, n)) {
+        st = WTFGPU_ERR_OOM;
+        break;
+      }
+      va += n;
+      src += n;
+      left -= n;
+    }
+    status_out[r] = st;
+  }
+  P.ov_count[lane] = L.ovn;
+}
+
+// Single-lane memory services for the host proxy.
+// op 0: translate (out u64 gpa), 1: read phys, 2: write phys, 3: read virt, 4: write virt
+__global__ void k_lane_mem(Dev P, u32 lane, u32 op, u64 addr, u64 len, u8 *buf, i64 *result) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Lane L;
+  lane_min_load(P, lane, L);
+  i64 rc = 0;
+  if (op == 0) {
+    u64 gpa;
+    rc = host_walk(P, L, addr, gpa) ? (i64)gpa : -1;
+  } else if (op == 1 || op == 3) {
+    u64 a = addr;
+    for (u64 i = 0; i < len;) {
+      u64 gpa = a;
+      if (op == 3 && !host_walk(P, L, a, gpa)) {
+        rc = -1;
+        break;
+      }
+      u64 n = 4096 - (a & 0xfff);
+      if (n > len - i) n = len - i;
+      bool priv;
+      const u8 *pg = phys_page(P, L.lane, L.ovn, L.bloom, gpa >> 12, priv);
+      for (u64 k = 0; k < n; k++) buf[i + k] = pg[(gpa & 0xfff) + k];
+      i += n;
+      a += n;
+    }
+  } else {
+    u64 a = addr;
+    for (u64 i = 0; i < len;) {
+      u64 gpa = a;
+      if (op == 4 && !host_walk(P, L, a, gpa)) {
+        rc = -1;
+        break;
+      }
+      u64 n = 4096 - (a & 0xfff);
+      if (n > len - i) n = len - i;
+      if (!lane_phys_write(P, L, gpa, buf + i, n)) {
+        rc = -2;
+        break;
+      }
+      i += n;
+      a += n;
+    }
+    P.ov_count[lane] = L.ovn;
+  }
+  *result = rc;
+}
+
+// ---------------------------------------------------------------- coverage services
+__global__ void k_cov_collect(Dev P, u32 first, u32 count, u32 *out_lane, u64 *out_rip, u64 cap,
+                              unsigned long long *n_out) {
+  const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 w0 = first / 64, w1 = (first + count + 63) / 64;
+  const u64 total = (u64)(w1 - w0) * P.H;
+  if (t >= total) return;
+  const u32 wv = w0 + (u32)(t / P.H);
+  const u64 idx = (u64)wv * P.H + (t % P.H);
+  if (P.cov_ep[idx] != P.cov_wave_ep[wv]) return;
+  u64 m = P.cov_mask[idx];
+  const u64 rip = P.cov_rip[idx];
+  while (m) {
+    const int b = __ffsll((long long)m) - 1;
+    m &= m - 1;
+    const u32 lane = wv * 64 + b;
+    if (lane < first || lane >= first + count) continue;
+    const unsigned long long pos = atomicAdd(n_out, 1ull);
+    if (pos < cap) {
+      out_lane[pos] = lane;
+      out_rip[pos] = rip;
+    }
+  }
+}
+
+__global__ void k_cov_commit(Dev P, const u64 *rips, u64 n) {
+  const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n || !P.code_keys) return;
+  const u64 rip = rips[t];
+  u32 h = (u32)mix64(rip >> 12) & P.code_mask;
+  for (u32 i = 0; i <= P.code_mask; i++) {
+    const u64 k = P.code_keys[h];
+    if (k == rip >> 12) {
+      P.cov_map[(u64)P.code_slot[h] * WTFGPU_PAGE_SIZE + (rip & 0xfff)] = 1;
+      return;
+    }
+    if (k == EMPTY_KEY) return;
+    h = (h + 1) & P.code_mask;
+  }
+}
+
+}  // namespace
+
+// ====================================================================== host
+#define HIPCHK(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) {                                                              \
+      fprintf(stderr, "wtfgpu: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, \
+              __LINE__);                                                                 \
+      return WTFGPU_ERR_HIP;                                                             \
+    }                                                                                    \
+  } while (0)
+
+struct wtfgpu_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  Dev P{};
+  // pool
+  u8 *d_pool = nullptr;
+  u32 *d_pfnmap = nullptr;
+  u32 *d_ptbits = nullptr;
+  u64 npool = 0;
+  // lanes
+  u64 *d_gpr = nullptr, *d_rip = nullptr, *d_rflags = nullptr, *d_fsb = nullptr, *d_gsb = nullptr,
+      *d_icount = nullptr, *d_nbytes = nullptr;
+  u32 *d_status = nullptr, *d_lflags = nullptr, *d_ovcount = nullptr, *d_ovgpfn = nullptr;
+  ExitInfo *d_exinfo = nullptr;
+  LaneSys *d_sys = nullptr;
+  u8 *d_ovdata = nullptr;
+  wtfgpu_regs_t *d_full = nullptr;  // full per-lane architectural state (cold fields)
+  // breakpoints
+  u64 *d_bp = nullptr;
+  // coverage
+  u64 *d_codekeys = nullptr;
+  u32 *d_codeslot = nullptr;
+  u8 *d_covmap = nullptr;
+  u64 ncovslots = 0;
+  u64 *d_covrip = nullptr, *d_covmask = nullptr;
+  u32 *d_covep = nullptr, *d_covwep = nullptr, *d_covovf = nullptr;
+  std::vector<u64> code_vpns;
+  // host copy of the pool (page-table marking, host-side reads)
+  std::vector<u8> h_pool;
+  std::vector<u32> h_map;
+  // misc
+  u64 *d_stat = nullptr;
+  InitState *d_init = nullptr;
+  wtfgpu_regs_t initial{};
+  bool have_initial = false;
+  u8 *d_scratch = nullptr;
+  u64 scratch_bytes = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+namespace {
+
+template <typename T>
+int dalloc(T **p, u64 count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc((void **)p, count * sizeof(T));
+  if (e != hipSuccess) {
+    fprintf(stderr, "wtfgpu: hipMalloc(%llu bytes) failed: %s\n", (unsigned long long)(count * sizeof(T)),
+            hipGetErrorString(e));
+    return WTFGPU_ERR_OOM;
+  }
+  return WTFGPU_OK;
+}
+template <typename T>
+void dfree(T *&p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+int ensure_scratch(wtfgpu_ctx *c, u64 bytes) {
+  if (c->scratch_bytes >= bytes) return WTFGPU_OK;
+  dfree(c->d_scratch);
+  c->scratch_bytes = 0;
+  if (dalloc(&c->d_scratch, bytes)) return WTFGPU_ERR_OOM;
+  c->scratch_bytes = bytes;
+  return WTFGPU_OK;
+}
+
+u64 hmix(u64 x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+u32 table_size(u64 n) {
+  u32 s = 16;
+  while (s < 2 * n + 2) s <<= 1;
+  return s;
+}
+
+InitState make_init(const wtfgpu_regs_t &r) {
+  InitState s{};
+  for (int i = 0; i < 16; i++) s.g[i] = r.gpr[i];
+  s.rip = r.rip;
+  s.rflags = r.rflags;
+  s.fsb = r.seg[WTFGPU_FS].base;
+  s.gsb = r.seg[WTFGPU_GS].base;
+  s.sys.cr0 = r.cr0;
+  s.sys.cr3 = r.cr3;
+  s.sys.cr4 = r.cr4;
+  s.sys.efer = r.efer;
+  s.sys.cpl = r.seg[WTFGPU_CS].selector & 3;
+  return s;
+}
+
+bool lanes_ok(wtfgpu_ctx *c, u32 first, u32 count) {
+  return c && c->d_gpr && (u64)first + count <= c->P.nlanes;
+}
+
+template <typename T>
+int d2h(wtfgpu_ctx *c, T *dst, const T *src, u64 n) {
+  HIPCHK(hipMemcpyAsync(dst, src, n * sizeof(T), hipMemcpyDeviceToHost, c->stream));
+  return WTFGPU_OK;
+}
+template <typename T>
+int h2d(wtfgpu_ctx *c, T *dst, const T *src, u64 n) {
+  HIPCHK(hipMemcpyAsync(dst, src, n * sizeof(T), hipMemcpyHostToDevice, c->stream));
+  return WTFGPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wtfgpu_abi_version(void) { return WTFGPU_ABI_VERSION; }
+
+int wtfgpu_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int wtfgpu_create(int device, wtfgpu_ctx **out) {
+  if (!out) return WTFGPU_ERR_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return WTFGPU_ERR_NODEV;
+  HIPCHK(hipSetDevice(device));
+  wtfgpu_ctx *c = new (std::nothrow) wtfgpu_ctx();
+  if (!c) return WTFGPU_ERR_OOM;
+  c->device = device;
+  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreate(&c->ev0));
+  HIPCHK(hipEventCreate(&c->ev1));
+  if (dalloc(&c->d_stat, 4) || dalloc(&c->d_init, 1)) return WTFGPU_ERR_OOM;
+  *out = c;
+  return WTFGPU_OK;
+}
+
+void *wtfgpu_stream(wtfgpu_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+static void free_lanes(wtfgpu_ctx *c) {
+  dfree(c->d_gpr);
+  dfree(c->d_rip);
+  dfree(c->d_rflags);
+  dfree(c->d_fsb);
+  dfree(c->d_gsb);
+  dfree(c->d_icount);
+  dfree(c->d_nbytes);
+  dfree(c->d_status);
+  dfree(c->d_lflags);
+  dfree(c->d_ovcount);
+  dfree(c->d_ovgpfn);
+  dfree(c->d_exinfo);
+  dfree(c->d_sys);
+  dfree(c->d_ovdata);
+  dfree(c->d_full);
+  dfree(c->d_covrip);
+  dfree(c->d_covmask);
+  dfree(c->d_covep);
+  dfree(c->d_covwep);
+  dfree(c->d_covovf);
+}
+
+int wtfgpu_destroy(wtfgpu_ctx *c) {
+  if (!c) return WTFGPU_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  free_lanes(c);
+  dfree(c->d_pool);
+  dfree(c->d_pfnmap);
+  dfree(c->d_ptbits);
+  dfree(c->d_bp);
+  dfree(c->d_codekeys);
+  dfree(c->d_codeslot);
+  dfree(c->d_covmap);
+  dfree(c->d_stat);
+  dfree(c->d_init);
+  dfree(c->d_scratch);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return WTFGPU_OK;
+}
+
+static int mark_pt_pages(wtfgpu_ctx *c);
+
+// Snapshot page pool. Also marks page-table pages reachable from the
+// initial cr3 (set later by wtfgpu_set_initial_state).
+int wtfgpu_load_pool(wtfgpu_ctx *c, const uint64_t *gpfns, const uint8_t *pages, uint64_t npages) {
+  if (!c || (npages && (!gpfns || !pages))) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  dfree(c->d_pool);
+  dfree(c->d_pfnmap);
+  dfree(c->d_ptbits);
+  u64 maxpfn = 0;
+  for (u64 i = 0; i < npages; i++) maxpfn = std::max<u64>(maxpfn, gpfns[i]);
+  const u64 maplen = npages ? maxpfn + 1 : 1;
+  std::vector<u32> map(maplen, 0);
+  for (u64 i = 0; i < npages; i++)
+    if (map[gpfns[i]] == 0) map[gpfns[i]] = (u32)(i + 1);  // first occurrence wins (try_emplace)
+  if (dalloc(&c->d_pool, (npages + 1) * WTFGPU_PAGE_SIZE)) return WTFGPU_ERR_OOM;
+  if (dalloc(&c->d_pfnmap, maplen)) return WTFGPU_ERR_OOM;
+  if (dalloc(&c->d_ptbits, (maplen + 31) / 32)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemsetAsync(c->d_pool, 0, WTFGPU_PAGE_SIZE, c->stream));
+  if (npages)
+    HIPCHK(hipMemcpyAsync(c->d_pool + WTFGPU_PAGE_SIZE, pages, npages * WTFGPU_PAGE_SIZE, hipMemcpyHostToDevice,
+                          c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_pfnmap, map.data(), maplen * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_ptbits, 0, (maplen + 31) / 32 * 4, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+
+  c->npool = npages;
+  c->h_pool.assign(pages, pages + npages * WTFGPU_PAGE_SIZE);
+  c->h_map = std::move(map);
+  c->P.pool = c->d_pool;
+  c->P.pfn_map = c->d_pfnmap;
+  c->P.pfn_map_len = maplen;
+  c->P.ptbits = c->d_ptbits;
+  if (c->have_initial) return mark_pt_pages(c);
+  return WTFGPU_OK;
+}
+
+int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, uint32_t cov_entries) {
+  if (!c || nlanes == 0 || overlay_pages == 0) return WTFGPU_ERR_INVALID;
+  if (cov_entries & (cov_entries - 1)) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  free_lanes(c);
+  const u64 N = nlanes;
+  const u64 nw = (N + 63) / 64;
+  int rc = 0;
+  rc |= dalloc(&c->d_gpr, 16 * N);
+  rc |= dalloc(&c->d_rip, N);
+  rc |= dalloc(&c->d_rflags, N);
+  rc |= dalloc(&c->d_fsb, N);
+  rc |= dalloc(&c->d_gsb, N);
+  rc |= dalloc(&c->d_icount, N);
+  rc |= dalloc(&c->d_nbytes, N);
+  rc |= dalloc(&c->d_status, N);
+  rc |= dalloc(&c->d_lflags, N);
+  rc |= dalloc(&c->d_ovcount, N);
+  rc |= dalloc(&c->d_ovgpfn, (u64)overlay_pages * N);
+  rc |= dalloc(&c->d_exinfo, N);
+  rc |= dalloc(&c->d_sys, N);
+  rc |= dalloc(&c->d_ovdata, N * overlay_pages * WTFGPU_PAGE_SIZE);
+  rc |= dalloc(&c->d_full, N);
+  if (cov_entries) {
+    rc |= dalloc(&c->d_covrip, nw * cov_entries);
+    rc |= dalloc(&c->d_covmask, nw * cov_entries);
+    rc |= dalloc(&c->d_covep, nw * cov_entries);
+    rc |= dalloc(&c->d_covwep, nw);
+    rc |= dalloc(&c->d_covovf, nw);
+  }
+  if (rc) return WTFGPU_ERR_OOM;
+  std::vector<u32> idle(N, WTFGPU_EXIT_IDLE);
+  HIPCHK(hipMemcpyAsync(c->d_status, idle.data(), N * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_ovcount, 0, N * 4, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_lflags, 0, N * 4, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_icount, 0, N * 8, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_nbytes, 0, N * 8, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_exinfo, 0, N * sizeof(ExitInfo), c->stream));
+  if (cov_entries) {
+    HIPCHK(hipMemsetAsync(c->d_covep, 0, nw * cov_entries * 4, c->stream));
+    std::vector<u32> one(nw, 1);
+    HIPCHK(hipMemcpyAsync(c->d_covwep, one.data(), nw * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_covovf, 0, nw * 4, c->stream));
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  Dev &P = c->P;
+  P.nlanes = nlanes;
+  P.K = overlay_pages;
+  P.gpr = c->d_gpr;
+  P.rip = c->d_rip;
+  P.rflags = c->d_rflags;
+  P.fs_base = c->d_fsb;
+  P.gs_base = c->d_gsb;
+  P.icount = c->d_icount;
+  P.nbytes = c->d_nbytes;
+  P.status = c->d_status;
+  P.lflags = c->d_lflags;
+  P.exinfo = c->d_exinfo;
+  P.sys = c->d_sys;
+  P.ov_count = c->d_ovcount;
+  P.ov_gpfn = c->d_ovgpfn;
+  P.ov_data = c->d_ovdata;
+  P.cov_rip = c->d_covrip;
+  P.cov_mask = c->d_covmask;
+  P.cov_ep = c->d_covep;
+  P.cov_wave_ep = c->d_covwep;
+  P.cov_overflow = c->d_covovf;
+  P.H = cov_entries;
+  P.stat = c->d_stat;
+  return WTFGPU_OK;
+}
+
+uint32_t wtfgpu_lane_count(wtfgpu_ctx *c) { return c ? c->P.nlanes : 0; }
+
+// Walks the initial page tables on the host copy of the pool to mark
+// page-table pages (a guest write to one invalidates the lane TLB).
+static int mark_pt_pages(wtfgpu_ctx *c) {
+  if (!c->d_ptbits) return WTFGPU_OK;
+  const u64 maplen = c->h_map.size();
+  if (maplen == 0) return WTFGPU_OK;
+  std::vector<u32> bits((maplen + 31) / 32, 0);
+  auto page = [&](u64 gpfn) -> const u8 * {
+    const u32 idx = gpfn < maplen ? c->h_map[gpfn] : 0;
+    return idx ? c->h_pool.data() + (u64)(idx - 1) * WTFGPU_PAGE_SIZE : nullptr;
+  };
+  auto mark = [&](u64 gpfn) {
+    if (gpfn < maplen) bits[gpfn >> 5] |= 1u << (gpfn & 31);
+  };
+  std::vector<std::pair<u64, int>> work;
+  work.push_back({c->initial.cr3 >> 12 & 0xffffffffffull, 3});
+  while (!work.empty()) {
+    auto [pfn, level] = work.back();
+    work.pop_back();
+    if (pfn < maplen && (bits[pfn >> 5] >> (pfn & 31)) & 1) continue;
+    mark(pfn);
+    const u8 *pg = page(pfn);
+    if (!pg || level == 0) continue;
+    for (int i = 0; i < 512; i++) {
+      u64 e;
+      memcpy(&e, pg + 8 * i, 8);
+      if (!(e & 1)) continue;
+      if ((level == 1 || level == 2) && (e & 0x80)) continue;  // large leaf
+      work.push_back({(e & 0x000ffffffffff000ull) >> 12, level - 1});
+    }
+  }
+  HIPCHK(hipMemcpyAsync(c->d_ptbits, bits.data(), bits.size() * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_set_initial_state(wtfgpu_ctx *c, const wtfgpu_regs_t *regs) {
+  if (!c || !regs) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  c->initial = *regs;
+  c->have_initial = true;
+  const InitState s = make_init(*regs);
+  HIPCHK(hipMemcpyAsync(c->d_init, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return mark_pt_pages(c);
+}
+
+int wtfgpu_set_limit(wtfgpu_ctx *c, uint64_t limit) {
+  if (!c) return WTFGPU_ERR_INVALID;
+  c->P.limit = limit;
+  return WTFGPU_OK;
+}
+
+int wtfgpu_set_breakpoints(wtfgpu_ctx *c, const uint64_t *gvas, uint32_t n) {
+  if (!c || (n && !gvas)) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  dfree(c->d_bp);
+  c->P.bp_keys = nullptr;
+  c->P.bp_mask = 0;
+  if (n == 0) return WTFGPU_OK;
+  const u32 sz = table_size(n);
+  std::vector<u64> t(sz, EMPTY_KEY);
+  for (u32 i = 0; i < n; i++) {
+    u32 h = (u32)hmix(gvas[i]) & (sz - 1);
+    while (t[h] != EMPTY_KEY && t[h] != gvas[i]) h = (h + 1) & (sz - 1);
+    t[h] = gvas[i];
+  }
+  if (dalloc(&c->d_bp, sz)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemcpyAsync(c->d_bp, t.data(), sz * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->P.bp_keys = c->d_bp;
+  c->P.bp_mask = sz - 1;
+  return WTFGPU_OK;
+}
+
+int wtfgpu_set_code_pages(wtfgpu_ctx *c, const uint64_t *vpns, uint32_t n) {
+  if (!c || (n && !vpns)) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  dfree(c->d_codekeys);
+  dfree(c->d_codeslot);
+  dfree(c->d_covmap);
+  c->P.code_keys = nullptr;
+  c->P.code_slot = nullptr;
+  c->P.cov_map = nullptr;
+  c->P.code_mask = 0;
+  c->code_vpns.assign(vpns, vpns + n);
+  c->ncovslots = n;
+  if (n == 0) return WTFGPU_OK;
+  const u32 sz = table_size(n);
+  std::vector<u64> keys(sz, EMPTY_KEY);
+  std::vector<u32> slots(sz, 0);
+  for (u32 i = 0; i < n; i++) {
+    u32 h = (u32)hmix(vpns[i]) & (sz - 1);
+    while (keys[h] != EMPTY_KEY && keys[h] != vpns[i]) h = (h + 1) & (sz - 1);
+    keys[h] = vpns[i];
+    slots[h] = i;
+  }
+  if (dalloc(&c->d_codekeys, sz) || dalloc(&c->d_codeslot, sz) || dalloc(&c->d_covmap, (u64)n * WTFGPU_PAGE_SIZE))
+    return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemcpyAsync(c->d_codekeys, keys.data(), sz * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_codeslot, slots.data(), sz * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_covmap, 0, (u64)n * WTFGPU_PAGE_SIZE, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->P.code_keys = c->d_codekeys;
+  c->P.code_slot = c->d_codeslot;
+  c->P.code_mask = sz - 1;
+  c->P.cov_map = c->d_covmap;
+  return WTFGPU_OK;
+}
+
+int wtfgpu_restore(wtfgpu_ctx *c, uint32_t first, uint32_t count) {
+  if (!lanes_ok(c, first, count) || !c->have_initial) return WTFGPU_ERR_STATE;
+  if (count == 0) return WTFGPU_OK;
+  HIPCHK(hipSetDevice(c->device));
+  k_restore<<<(count + 255) / 256, 256, 0, c->stream>>>(c->P, c->d_init, first, count);
+  HIPCHK(hipGetLastError());
+  // cold architectural state
+  std::vector<wtfgpu_regs_t> full(count, c->initial);
+  HIPCHK(hipMemcpyAsync(c->d_full + first, full.data(), (u64)count * sizeof(wtfgpu_regs_t), hipMemcpyHostToDevice,
+                        c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+// ---- register I/O
+
+int wtfgpu_read_gprs(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t *out18) {
+  if (!lanes_ok(c, first, count) || !out18) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  const u64 N = c->P.nlanes;
+  std::vector<u64> tmp((u64)18 * count);
+  int rc = 0;
+  for (int i = 0; i < 16; i++) rc |= d2h(c, tmp.data() + (u64)i * count, c->d_gpr + i * N + first, count);
+  rc |= d2h(c, tmp.data() + (u64)16 * count, c->d_rip + first, count);
+  rc |= d2h(c, tmp.data() + (u64)17 * count, c->d_rflags + first, count);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (u64 l = 0; l < count; l++)
+    for (int i = 0; i < 18; i++) out18[l * 18 + i] = tmp[(u64)i * count + l];
+  return WTFGPU_OK;
+}
+
+int wtfgpu_write_gprs(wtfgpu_ctx *c, uint32_t first, uint32_t count, const uint64_t *in18) {
+  if (!lanes_ok(c, first, count) || !in18) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  const u64 N = c->P.nlanes;
+  std::vector<u64> tmp((u64)18 * count);
+  for (u64 l = 0; l < count; l++)
+    for (int i = 0; i < 18; i++) tmp[(u64)i * count + l] = in18[l * 18 + i];
+  int rc = 0;
+  for (int i = 0; i < 16; i++) rc |= h2d(c, c->d_gpr + i * N + first, tmp.data() + (u64)i * count, count);
+  rc |= h2d(c, c->d_rip + first, tmp.data() + (u64)16 * count, count);
+  rc |= h2d(c, c->d_rflags + first, tmp.data() + (u64)17 * count, count);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_read_regs(wtfgpu_ctx *c, uint32_t first, uint32_t count, wtfgpu_regs_t *out) {
+  if (!lanes_ok(c, first, count) || !out) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  std::vector<u64> g((u64)18 * count);
+  int rc = wtfgpu_read_gprs(c, first, count, g.data());
+  if (rc) return rc;
+  std::vector<u64> fsb(count), gsb(count);
+  std::vector<LaneSys> sys(count);
+  rc |= d2h(c, out, c->d_full + first, count);
+  rc |= d2h(c, fsb.data(), c->d_fsb + first, count);
+  rc |= d2h(c, gsb.data(), c->d_gsb + first, count);
+  rc |= d2h(c, sys.data(), c->d_sys + first, count);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (u64 l = 0; l < count; l++) {
+    wtfgpu_regs_t &r = out[l];
+    for (int i = 0; i < 16; i++) r.gpr[i] = g[l * 18 + i];
+    r.rip = g[l * 18 + 16];
+    r.rflags = g[l * 18 + 17];
+    r.seg[WTFGPU_FS].base = fsb[l];
+    r.seg[WTFGPU_GS].base = gsb[l];
+    r.cr0 = sys[l].cr0;
+    r.cr3 = sys[l].cr3;
+    r.cr4 = sys[l].cr4;
+    r.efer = sys[l].efer;
+  }
+  return WTFGPU_OK;
+}
+
+int wtfgpu_write_regs(wtfgpu_ctx *c, uint32_t first, uint32_t count, const wtfgpu_regs_t *in) {
+  if (!lanes_ok(c, first, count) || !in) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  std::vector<u64> g((u64)18 * count), fsb(count), gsb(count);
+  std::vector<LaneSys> sys(count);
+  for (u64 l = 0; l < count; l++) {
+    const wtfgpu_regs_t &r = in[l];
+    for (int i = 0; i < 16; i++) g[l * 18 + i] = r.gpr[i];
+    g[l * 18 + 16] = r.rip;
+    g[l * 18 + 17] = r.rflags;
+    fsb[l] = r.seg[WTFGPU_FS].base;
+    gsb[l] = r.seg[WTFGPU_GS].base;
+    sys[l] = make_init(r).sys;
+  }
+  int rc = wtfgpu_write_gprs(c, first, count, g.data());
+  if (rc) return rc;
+  rc |= h2d(c, c->d_full + first, in, count);
+  rc |= h2d(c, c->d_fsb + first, fsb.data(), count);
+  rc |= h2d(c, c->d_gsb + first, gsb.data(), count);
+  rc |= h2d(c, c->d_sys + first, sys.data(), count);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_read_exits(wtfgpu_ctx *c, uint32_t first, uint32_t count, wtfgpu_exit_t *out) {
+  if (!lanes_ok(c, first, count) || !out) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  std::vector<u32> st(count);
+  std::vector<ExitInfo> ex(count);
+  std::vector<u64> rip(count), ic(count);
+  int rc = 0;
+  rc |= d2h(c, st.data(), c->d_status + first, count);
+  rc |= d2h(c, ex.data(), c->d_exinfo + first, count);
+  rc |= d2h(c, rip.data(), c->d_rip + first, count);
+  rc |= d2h(c, ic.data(), c->d_icount + first, count);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (u64 l = 0; l < count; l++) {
+    wtfgpu_exit_t &e = out[l];
+    memset(&e, 0, sizeof(e));
+    e.status = st[l];
+    if (st[l] == WTFGPU_EXIT_FAULT) {
+      e.vector = ex[l].vector;
+      e.error = ex[l].error;
+      e.addr = ex[l].addr;
+    }
+    if (st[l] == WTFGPU_EXIT_UNIMPLEMENTED) e.opcode = ex[l].opcode;
+    e.rip = rip[l];
+    e.icount = ic[l];
+  }
+  return WTFGPU_OK;
+}
+
+static int set_status_list(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, uint32_t status, const uint8_t *skip) {
+  if (!c || !c->d_status || (n && !lanes)) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  // small lists: per-lane copies; large: read-modify-write of the whole array
+  std::vector<u32> st(c->P.nlanes), fl(c->P.nlanes);
+  HIPCHK(hipMemcpyAsync(st.data(), c->d_status, st.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(fl.data(), c->d_lflags, fl.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (u32 i = 0; i < n; i++) {
+    if (lanes[i] >= c->P.nlanes) return WTFGPU_ERR_INVALID;
+    st[lanes[i]] = status;
+    if (skip) fl[lanes[i]] = skip[i] ? 1u : 0u;
+  }
+  HIPCHK(hipMemcpyAsync(c->d_status, st.data(), st.size() * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_lflags, fl.data(), fl.size() * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_resume(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, const uint8_t *skip_bp) {
+  std::vector<u8> zeros;
+  if (!skip_bp) {
+    zeros.assign(n, 0);
+    skip_bp = zeros.data();
+  }
+  return set_status_list(c, lanes, n, WTFGPU_RUNNING, skip_bp);
+}
+
+int wtfgpu_stop(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, uint32_t status) {
+  return set_status_list(c, lanes, n, status, nullptr);
+}
+
+int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps, wtfgpu_run_stats_t *stats) {
+  if (!lanes_ok(c, first, count) || (first & 63)) return WTFGPU_ERR_INVALID;
+  if (!c->P.pool) return WTFGPU_ERR_STATE;
+  HIPCHK(hipSetDevice(c->device));
+  wtfgpu_run_stats_t st{};
+  const u64 chunk = 1ull << 20;  // wave-steps per launch: keeps every launch short
+  u64 done = 0;
+  float ms_total = 0;
+  for (;;) {
+    const u64 steps = std::min<u64>(chunk, max_steps - done);
+    HIPCHK(hipMemsetAsync(c->d_stat, 0, 4 * 8, c->stream));
+    HIPCHK(hipEventRecord(c->ev0, c->stream));
+    k_run<<<(count + 255) / 256, 256, 0, c->stream>>>(c->P, first, count, steps);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev1, c->stream));
+    u64 s[4];
+    HIPCHK(hipMemcpyAsync(s, c->d_stat, sizeof(s), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    ms_total += ms;
+    st.kernel_launches++;
+    st.group_steps += s[0];
+    st.lane_retired += s[1];
+    done += steps;
+    if (s[2] == 0 || done >= max_steps) break;
+  }
+  st.kernel_ms = ms_total;
+  if (stats) *stats = st;
+  return WTFGPU_OK;
+}
+
+// ---- lane memory services
+static int lane_mem(wtfgpu_ctx *c, uint32_t lane, u32 op, u64 addr, void *buf, u64 len, i64 *result) {
+  if (!c || lane >= c->P.nlanes) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  if (ensure_scratch(c, len + 64)) return WTFGPU_ERR_OOM;
+  i64 *d_res = (i64 *)c->d_scratch;
+  u8 *d_buf = c->d_scratch + 64;
+  if ((op == 2 || op == 4) && len) HIPCHK(hipMemcpyAsync(d_buf, buf, len, hipMemcpyHostToDevice, c->stream));
+  k_lane_mem<<<1, 64, 0, c->stream>>>(c->P, lane, op, addr, len, d_buf, d_res);
+  HIPCHK(hipGetLastError());
+  if ((op == 1 || op == 3) && len) HIPCHK(hipMemcpyAsync(buf, d_buf, len, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(result, d_res, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_lane_translate(wtfgpu_ctx *c, uint32_t lane, uint64_t gva, uint64_t *gpa) {
+  i64 r = 0;
+  int rc = lane_mem(c, lane, 0, gva, nullptr, 0, &r);
+  if (rc) return rc;
+  if (r < 0) return WTFGPU_ERR_TRANSLATE;
+  if (gpa) *gpa = (u64)r;
+  return WTFGPU_OK;
+}
+int wtfgpu_lane_read_phys(wtfgpu_ctx *c, uint32_t lane, uint64_t gpa, void *buf, uint64_t len) {
+  i64 r = 0;
+  int rc = lane_mem(c, lane, 1, gpa, buf, len, &r);
+  return rc ? rc : (r < 0 ? WTFGPU_ERR_TRANSLATE : WTFGPU_OK);
+}
+int wtfgpu_lane_write_phys(wtfgpu_ctx *c, uint32_t lane, uint64_t gpa, const void *buf, uint64_t len) {
+  i64 r = 0;
+  int rc = lane_mem(c, lane, 2, gpa, (void *)buf, len, &r);
+  return rc ? rc : (r == -2 ? WTFGPU_ERR_OOM : (r < 0 ? WTFGPU_ERR_TRANSLATE : WTFGPU_OK));
+}
+int wtfgpu_lane_read_virt(wtfgpu_ctx *c, uint32_t lane, uint64_t gva, void *buf, uint64_t len) {
+  i64 r = 0;
+  int rc = lane_mem(c, lane, 3, gva, buf, len, &r);
+  return rc ? rc : (r < 0 ? WTFGPU_ERR_TRANSLATE : WTFGPU_OK);
+}
+int wtfgpu_lane_write_virt(wtfgpu_ctx *c, uint32_t lane, uint64_t gva, const void *buf, uint64_t len) {
+  i64 r = 0;
+  int rc = lane_mem(c, lane, 4, gva, (void *)buf, len, &r);
+  return rc ? rc : (r == -2 ? WTFGPU_ERR_OOM : (r < 0 ? WTFGPU_ERR_TRANSLATE : WTFGPU_OK));
+}
+
+int wtfgpu_apply_writes(wtfgpu_ctx *c, const wtfgpu_write_t *writes, uint32_t n, const uint8_t *data,
+                        uint64_t data_len, int32_t *status_out) {
+  if (!c || (n && (!writes || !data))) return WTFGPU_ERR_INVALID;
+  if (n == 0) return WTFGPU_OK;
+  HIPCHK(hipSetDevice(c->device));
+  std::vector<u32> order(n);
+  for (u32 i = 0; i < n; i++) {
+    order[i] = i;
+    if (writes[i].lane >= c->P.nlanes || writes[i].data_off + writes[i].len > data_len) return WTFGPU_ERR_INVALID;
+  }
+  std::stable_sort(order.begin(), order.end(), [&](u32 a, u32 b) { return writes[a].lane < writes[b].lane; });
+  std::vector<WriteRec> recs(n);
+  std::vector<u32> starts;
+  for (u32 i = 0; i < n; i++) {
+    const wtfgpu_write_t &w = writes[order[i]];
+    recs[i] = WriteRec{w.lane, w.len, w.gva, w.data_off};
+    if (i == 0 || w.lane != recs[i - 1].lane) starts.push_back(i);
+  }
+  const u32 nl = (u32)starts.size();
+  starts.push_back(n);
+  const u64 b_recs = (u64)n * sizeof(WriteRec), b_starts = starts.size() * 4ull, b_st = (u64)n * 4;
+  const u64 o_starts = (b_recs + 255) & ~255ull, o_st = (o_starts + b_starts + 255) & ~255ull,
+            o_data = (o_st + b_st + 255) & ~255ull;
+  if (ensure_scratch(c, o_data + data_len)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemcpyAsync(c->d_scratch, recs.data(), b_recs, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_scratch + o_starts, starts.data(), b_starts, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_scratch + o_data, data, data_len, hipMemcpyHostToDevice, c->stream));
+  k_apply_writes<<<(nl + 63) / 64, 64, 0, c->stream>>>(c->P, (const WriteRec *)c->d_scratch,
+                                                       (const u32 *)(c->d_scratch + o_starts), nl,
+                                                       c->d_scratch + o_data, (i32 *)(c->d_scratch + o_st));
+  HIPCHK(hipGetLastError());
+  std::vector<i32> st(n);
+  HIPCHK(hipMemcpyAsync(st.data(), c->d_scratch + o_st, b_st, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  int rc = WTFGPU_OK;
+  for (u32 i = 0; i < n; i++) {
+    if (status_out) status_out[order[i]] = st[i];
+    if (st[i]) rc = st[i];
+  }
+  return rc;
+}
+
+int wtfgpu_read_dirty(wtfgpu_ctx *c, uint32_t lane, uint64_t *gpas, uint32_t cap, uint32_t *n) {
+  if (!c || lane >= c->P.nlanes || !n) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  u32 cnt = 0;
+  HIPCHK(hipMemcpy(&cnt, c->d_ovcount + lane, 4, hipMemcpyDeviceToHost));
+  *n = cnt;
+  for (u32 k = 0; k < cnt && k < cap; k++) {
+    u32 g = 0;
+    HIPCHK(hipMemcpy(&g, c->d_ovgpfn + (u64)k * c->P.nlanes + lane, 4, hipMemcpyDeviceToHost));
+    gpas[k] = (u64)g << 12;
+  }
+  return WTFGPU_OK;
+}
+
+int wtfgpu_read_coverage(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint32_t *lanes, uint64_t *rips,
+                         uint64_t cap, uint64_t *n, uint32_t *overflow) {
+  if (!lanes_ok(c, first, count) || !n) return WTFGPU_ERR_INVALID;
+  *n = 0;
+  if (overflow) *overflow = 0;
+  if (!c->d_covrip || count == 0) return WTFGPU_OK;
+  HIPCHK(hipSetDevice(c->device));
+  const u32 w0 = first / 64, w1 = (first + count + 63) / 64;
+  const u64 total = (u64)(w1 - w0) * c->P.H;
+  const u64 room = std::max<u64>(cap, 1);
+  const u64 o_rip = (room * 4 + 255) & ~255ull, o_n = (o_rip + room * 8 + 255) & ~255ull;
+  if (ensure_scratch(c, o_n + 64)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemsetAsync(c->d_scratch + o_n, 0, 8, c->stream));
+  k_cov_collect<<<(u32)((total + 255) / 256), 256, 0, c->stream>>>(
+      c->P, first, count, (u32 *)c->d_scratch, (u64 *)(c->d_scratch + o_rip), cap,
+      (unsigned long long *)(c->d_scratch + o_n));
+  HIPCHK(hipGetLastError());
+  u64 got = 0;
+  HIPCHK(hipMemcpyAsync(&got, c->d_scratch + o_n, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const u64 m = std::min(got, cap);
+  if (m) {
+    HIPCHK(hipMemcpyAsync(lanes, c->d_scratch, m * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(rips, c->d_scratch + o_rip, m * 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  if (overflow) {
+    std::vector<u32> ov(w1 - w0);
+    HIPCHK(hipMemcpyAsync(ov.data(), c->d_covovf + w0, (u64)(w1 - w0) * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (u32 v : ov) *overflow |= v;
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  *n = got;
+  return WTFGPU_OK;
+}
+
+int wtfgpu_commit_coverage(wtfgpu_ctx *c, const uint64_t *rips, uint64_t n) {
+  if (!c || (n && !rips)) return WTFGPU_ERR_INVALID;
+  if (n == 0 || !c->d_covmap) return WTFGPU_OK;
+  HIPCHK(hipSetDevice(c->device));
+  if (ensure_scratch(c, n * 8)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemcpyAsync(c->d_scratch, rips, n * 8, hipMemcpyHostToDevice, c->stream));
+  k_cov_commit<<<(u32)((n + 255) / 256), 256, 0, c->stream>>>(c->P, (const u64 *)c->d_scratch, n);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_reset_coverage(wtfgpu_ctx *c) {
+  if (!c) return WTFGPU_ERR_INVALID;
+  if (!c->d_covmap) return WTFGPU_OK;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemsetAsync(c->d_covmap, 0, c->ncovslots * WTFGPU_PAGE_SIZE, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_coverage_device_map(wtfgpu_ctx *c, void **dev_ptr, uint64_t *bytes) {
+  if (!c || !dev_ptr || !bytes) return WTFGPU_ERR_INVALID;
+  *dev_ptr = c->d_covmap;
+  *bytes = c->ncovslots * WTFGPU_PAGE_SIZE;
+  return WTFGPU_OK;
+}
+
+int wtfgpu_coverage_rips(wtfgpu_ctx *c, uint64_t *rips, uint64_t cap, uint64_t *n) {
+  if (!c || !n) return WTFGPU_ERR_INVALID;
+  *n = 0;
+  if (!c->d_covmap) return WTFGPU_OK;
+  HIPCHK(hipSetDevice(c->device));
+  std::vector<u8> m(c->ncovslots * WTFGPU_PAGE_SIZE);
+  HIPCHK(hipMemcpy(m.data(), c->d_covmap, m.size(), hipMemcpyDeviceToHost));
+  u64 k = 0;
+  for (u64 s = 0; s < c->ncovslots; s++)
+    for (u64 o = 0; o < WTFGPU_PAGE_SIZE; o++)
+      if (m[s * WTFGPU_PAGE_SIZE + o]) {
+        if (k < cap && rips) rips[k] = (c->code_vpns[s] << 12) | o;
+        k++;
+      }
+  *n = k;
+  return WTFGPU_OK;
+}
+
+int wtfgpu_read_bytes(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t *out) {
+  if (!lanes_ok(c, first, count) || !out) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemcpy(out, c->d_nbytes + first, (u64)count * 8, hipMemcpyDeviceToHost));
+  return WTFGPU_OK;
+}
+
+}  // extern "C"

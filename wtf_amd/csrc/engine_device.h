@@ -1,0 +1,116 @@
+// engine_device.h — CDNA4 device side of the wtf gpu execution backend.
+//
+// One lane = one testcase. The kernel runs each wavefront as a RIP-grouped
+// SIMT interpreter:
+//   1. min-RIP over the wave's running lanes (wave reduction) picks the group;
+//   2. the group's instruction is fetched + decoded ONCE, as wave-uniform
+//      (scalar) work, from the lane page pool;
+//   3. coverage / breakpoint checks are uniform (one lookup per group);
+//   4. the semantics execute per lane on the group's exec mask, GPRs held in
+//      VGPRs (16 x u64, indexed with s_set_gpr_idx by the uniform register
+//      number), memory through a per-lane 4-entry TLB in VGPRs, page walks over
+//      the lane's copy-on-write view of guest physical memory.
+//
+// The semantics mirror the hooks of the reference bochscpu backend
+// (src/wtf/bochscpu_backend.cc:445-728) and the conventions U1-U13 written in
+// DESIGN.md §5. This header is included by engine.hip only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/wtfgpu.h"
+
+namespace wtfgpu_dev {
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+typedef uint16_t u16;
+typedef uint8_t u8;
+typedef int64_t i64;
+typedef int32_t i32;
+
+constexpr u64 F_CF = 0x1, F_PF = 0x4, F_AF = 0x10, F_ZF = 0x40, F_SF = 0x80, F_TF = 0x100,
+              F_IF = 0x200, F_DF = 0x400, F_OF = 0x800;
+constexpr u64 F_STATUS = F_CF | F_PF | F_AF | F_ZF | F_SF | F_OF;
+constexpr u64 EMPTY_KEY = ~0ull;
+
+// TLB entry data: page pointer | permission bits in the low 12 bits.
+constexpr u64 T_W = 1, T_U = 2, T_NX = 4, T_PRIV = 8, T_PT = 16;
+constexpr int TLB_N = 4;
+
+struct LaneSys {   // rarely touched per-lane system state
+  u64 cr0, cr3, cr4, efer;
+  u32 cpl;
+  u32 pad;
+};
+
+struct ExitInfo {
+  u32 vector, error, opcode, pad;
+  u64 addr;
+};
+
+// Everything the kernels need, passed by value.
+struct Dev {
+  // snapshot page pool (index 0 = zero page)
+  const u8 *pool;
+  const u32 *pfn_map;    // gpfn -> pool page index
+  u64 pfn_map_len;
+  const u32 *ptbits;     // bitmap over gpfn: page-table pages of the snapshot
+  // lanes, SoA
+  u32 nlanes;
+  u32 K;                 // copy-on-write pages per lane
+  u64 *gpr;              // [16][nlanes]
+  u64 *rip, *rflags, *fs_base, *gs_base, *icount, *nbytes;
+  u32 *status, *lflags;  // lflags bit0: skip breakpoint once
+  ExitInfo *exinfo;
+  LaneSys *sys;
+  u32 *ov_count;         // [nlanes]
+  u32 *ov_gpfn;          // [K][nlanes]
+  u8 *ov_data;           // [nlanes][K][4096]
+  // breakpoints (open addressing, EMPTY_KEY)
+  const u64 *bp_keys;
+  u32 bp_mask;           // table size - 1; 0 with bp_keys==nullptr = none
+  // coverage
+  const u64 *code_keys;  // vpn hash table
+  const u32 *code_slot;
+  u32 code_mask;
+  u8 *cov_map;           // [slots][4096]
+  u64 *cov_rip;          // per wave [nwaves][H]
+  u64 *cov_mask;
+  u32 *cov_ep;           // entry epoch
+  u32 *cov_wave_ep;      // current epoch per wave
+  u32 *cov_overflow;     // per wave
+  u32 H;                 // entries per wave (power of two)
+  u64 limit;
+  u64 *stat;             // [0] group steps, [1] retired, [2] lanes still running
+};
+
+// ---------------------------------------------------------------- helpers
+__device__ __forceinline__ u64 rfl64(u64 v) {
+  u32 lo = __builtin_amdgcn_readfirstlane((u32)v);
+  u32 hi = __builtin_amdgcn_readfirstlane((u32)(v >> 32));
+  return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ u32 rfl32(u32 v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ u64 mix64(u64 x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+__device__ __forceinline__ u64 szmask(u32 sz) { return sz == 8 ? ~0ull : ((1ull << (8 * sz)) - 1); }
+__device__ __forceinline__ u64 sext(u64 v, u32 bytes) {
+  const u32 s = 64 - 8 * bytes;
+  return bytes >= 8 ? v : (u64)(((i64)(v << s)) >> s);
+}
+__device__ __forceinline__ u64 msb(u64 v, u32 sz) { return (v >> (8 * sz - 1)) & 1; }
+__device__ __forceinline__ u64 szp(u64 res, u32 sz) {
+  res &= szmask(sz);
+  const u64 pf = (__builtin_popcount((u32)(res & 0xff)) & 1) ? 0 : F_PF;
+  return (res == 0 ? F_ZF : 0) | (msb(res, sz) ? F_SF : 0) | pf;
+}
+
+}  // namespace wtfgpu_dev

@@ -1,0 +1,281 @@
+// engine_exec.h — per-lane state, guest memory, decode and execute for the
+// RIP-grouped interpreter (see engine_device.h). Included by engine.hip only.
+#pragma once
+#include "engine_device.h"
+
+namespace wtfgpu_dev {
+
+// ------------------------------------------------------------------ lane state
+constexpr u32 GPR_STRIDE = 256;  // threads per block: LDS register file is [16][256] u64
+
+struct Lane {
+  u64 *g;                    // this lane's GPR column in the block's LDS register file
+  u64 rip, rflags, icount, nbytes;
+  u64 tv[TLB_N], td[TLB_N];  // TLB: vpn tags, page pointer | T_* bits
+  u64 bloom;                 // overlay membership filter
+  u64 cr0, cr3, efer;
+  u64 exaddr;
+  u64 miss_va;               // pending translation (TLB miss or copy-on-write)
+  u32 tnext, ovn, cpl, status, lane, exvec, exerr, exop;
+  u32 miss, miss_acc, flush, pend;  // pend: bytes accessed by the attempt in flight
+};
+
+// GPR r of the lane (LDS; a uniform r + lane*8 is bank-conflict free)
+__device__ __forceinline__ u64 &R(const Lane &L, u32 r) { return L.g[r * GPR_STRIDE]; }
+
+// ------------------------------------------------------------------ TLB
+__device__ __forceinline__ bool tlb_get(const Lane &L, u64 vpn, u64 &td) {
+  bool hit = false;
+  u64 r = 0;
+#pragma unroll
+  for (int i = 0; i < TLB_N; i++) {
+    if (L.tv[i] == vpn) {
+      hit = true;
+      r = L.td[i];
+    }
+  }
+  td = r;
+  return hit;
+}
+__device__ __forceinline__ void tlb_put(Lane &L, u64 vpn, u64 td) {
+#pragma unroll
+  for (int i = 0; i < TLB_N; i++) {
+    if (L.tnext == (u32)i) {
+      L.tv[i] = vpn;
+      L.td[i] = td;
+    }
+  }
+  L.tnext = (L.tnext + 1) & (TLB_N - 1);
+}
+__device__ __forceinline__ void tlb_flush(Lane &L) {
+#pragma unroll
+  for (int i = 0; i < TLB_N; i++) L.tv[i] = EMPTY_KEY;
+}
+
+// ------------------------------------------------------------------ physical memory
+__device__ __forceinline__ u64 bloom_bit(u64 gpfn) { return 1ull << ((gpfn * 0x9E3779B97F4A7C15ull) >> 58); }
+
+// Lane view of a guest physical page: private overlay copy if the lane wrote
+// it, else the snapshot pool page, else the zero page (bochscpu_backend.cc:124-131).
+__device__ __forceinline__ const u8 *phys_page(const Dev &P, u32 lane, u32 ovn, u64 bloom, u64 gpfn, bool &priv) {
+  priv = false;
+  if (bloom & bloom_bit(gpfn)) {
+    for (u32 k = 0; k < ovn; k++) {
+      if (P.ov_gpfn[(u64)k * P.nlanes + lane] == (u32)gpfn) {
+        priv = true;
+        return P.ov_data + ((u64)lane * P.K + k) * WTFGPU_PAGE_SIZE;
+      }
+    }
+  }
+  const u32 idx = gpfn < P.pfn_map_len ? P.pfn_map[gpfn] : 0u;
+  return P.pool + (u64)idx * WTFGPU_PAGE_SIZE;
+}
+
+__device__ __forceinline__ bool is_ptpage(const Dev &P, u64 gpfn) {
+  if (gpfn >= P.pfn_map_len) return false;
+  return (P.ptbits[gpfn >> 5] >> (gpfn & 31)) & 1;
+}
+
+// Little-endian load of sz bytes that do not cross a page: aligned u64 pair + funnel.
+__device__ __forceinline__ u64 load_le(const u8 *p, u32 sz) {
+  const uintptr_t a = (uintptr_t)p & ~(uintptr_t)7;
+  const u32 off = (u32)((uintptr_t)p & 7);
+  const u64 lo = *(const u64 *)a;
+  u64 v = lo >> (8 * off);
+  if (off + sz > 8) {
+    const u64 hi = *(const u64 *)(a + 8);
+    v |= hi << (64 - 8 * off);
+  }
+  return v & szmask(sz);
+}
+__device__ __forceinline__ void store_le(u8 *p, u32 sz, u64 v) {
+  const uintptr_t a = (uintptr_t)p;
+  if ((a & (sz - 1)) == 0) {
+    if (sz == 8) *(u64 *)p = v;
+    else if (sz == 4) *(u32 *)p = (u32)v;
+    else if (sz == 2) *(u16 *)p = (u16)v;
+    else *p = (u8)v;
+    return;
+  }
+  for (u32 i = 0; i < sz; i++) p[i] = (u8)(v >> (8 * i));
+}
+
+enum { ACC_R = 0, ACC_W = 1, ACC_X = 2, ACC_WPROBE = 3 };  // WPROBE: write permission check only
+
+__device__ __forceinline__ void set_fault(Lane &L, u32 vec, u32 err, u64 addr) {
+  L.status = WTFGPU_EXIT_FAULT;
+  L.exvec = vec;
+  L.exerr = err;
+  L.exaddr = addr;
+}
+
+__device__ __forceinline__ bool canonical(u64 va) { return (u64)(((i64)(va << 16)) >> 16) == va; }
+
+__device__ __forceinline__ u32 pf_error(const Lane &L, int acc, bool present) {
+  const bool nxe = (L.efer >> 11) & 1;
+  return (present ? 1u : 0u) | (acc == ACC_W || acc == ACC_WPROBE ? 2u : 0u) | (L.cpl == 3 ? 4u : 0u) |
+         (acc == ACC_X && nxe ? 16u : 0u);
+}
+
+// Permission check of a translation (SDM 4.6): U/S, R/W (+CR0.WP), NX.
+__device__ __forceinline__ bool perm_ok(const Lane &L, u64 td, int acc) {
+  const bool user = L.cpl == 3;
+  const bool wp = (L.cr0 >> 16) & 1;
+  const bool w = acc == ACC_W || acc == ACC_WPROBE;
+  return !((user && !(td & T_U)) || (w && !(td & T_W) && (user || wp)) || (acc == ACC_X && (td & T_NX)));
+}
+
+// 4-level walk through the lane's physical view (kdmp-parser.h:269-345 shape,
+// SDM permission bits accumulated). No A/D updates (U8). Faults set on L.
+__device__ __forceinline__ bool walk(const Dev &P, Lane &L, u64 va, int acc, u64 &td, u64 &gpfn) {
+  const bool nxe = (L.efer >> 11) & 1;
+  if (!canonical(va)) {
+    set_fault(L, WTFGPU_VEC_GP, 0, va);
+    return false;
+  }
+  u64 table = L.cr3 & 0x000ffffffffff000ull;
+  bool aw = true, au = true, nx = false;
+  u64 e = 0, pmask = 0xfff;
+  bool priv;
+  for (int level = 3; level >= 0; level--) {
+    const u64 idx = (va >> (12 + 9 * level)) & 0x1ff;
+    const u8 *pg = phys_page(P, L.lane, L.ovn, L.bloom, table >> 12, priv);
+    e = *(const u64 *)(pg + idx * 8);
+    if (!(e & 1)) {
+      set_fault(L, WTFGPU_VEC_PF, pf_error(L, acc, false), va);
+      return false;
+    }
+    aw &= (e & 2) != 0;
+    au &= (e & 4) != 0;
+    if (nxe && (e >> 63)) nx = true;
+    if ((level == 2 || level == 1) && (e & 0x80)) {
+      pmask = level == 2 ? 0x3fffffffull : 0x1fffffull;
+      break;
+    }
+    table = e & 0x000ffffffffff000ull;
+  }
+  const u64 gpa = ((e & 0x000ffffffffff000ull) & ~pmask) | (va & pmask);
+  gpfn = gpa >> 12;
+  const u8 *pg = phys_page(P, L.lane, L.ovn, L.bloom, gpfn, priv);
+  td = (u64)(uintptr_t)pg | (aw ? T_W : 0) | (au ? T_U : 0) | (nx ? T_NX : 0) | (priv ? T_PRIV : 0) |
+       (is_ptpage(P, gpfn) ? T_PT : 0);
+  return true;
+}
+
+// Copy-on-write into overlay slot `slot` of `lane`: the page joins the dirty
+// list (bochscpu_backend.cc:887-889 DirtyGpa; dropped again by restore :751-772).
+__device__ __forceinline__ u8 *cow_copy(const Dev &P, u32 lane, u32 slot, u64 gpfn, const u8 *src) {
+  u8 *dst = P.ov_data + ((u64)lane * P.K + slot) * WTFGPU_PAGE_SIZE;
+  const uint4 *s4 = (const uint4 *)src;
+  uint4 *d4 = (uint4 *)dst;
+  for (int i = 0; i < 256; i += 4) {
+    const uint4 a = s4[i], b = s4[i + 1], c = s4[i + 2], d = s4[i + 3];
+    d4[i] = a;
+    d4[i + 1] = b;
+    d4[i + 2] = c;
+    d4[i + 3] = d;
+  }
+  P.ov_gpfn[(u64)slot * P.nlanes + lane] = (u32)gpfn;
+  return dst;
+}
+
+// Slow path of a translation (one call site in the kernel): walk, permission
+// check, copy-on-write, TLB fill. false = the lane faulted / ran out of overlay.
+__device__ __forceinline__ bool service_miss(const Dev &P, Lane &L, u64 va, int acc) {
+  u64 td, gpfn;
+  if (!walk(P, L, va, acc, td, gpfn)) return false;
+  if (!perm_ok(L, td, acc)) {
+    set_fault(L, WTFGPU_VEC_PF, pf_error(L, acc, true), va);
+    return false;
+  }
+  if (acc == ACC_W && !(td & T_PRIV)) {
+    if (L.ovn >= P.K) {
+      L.status = WTFGPU_EXIT_OVERLAY_FULL;
+      return false;
+    }
+    u8 *np = cow_copy(P, L.lane, L.ovn, gpfn, (const u8 *)(uintptr_t)(td & ~0xfffull));
+    L.ovn++;
+    L.bloom |= bloom_bit(gpfn);
+    tlb_flush(L);  // other vpns may alias the old page
+    td = (u64)(uintptr_t)np | (td & 0xfff) | T_PRIV;
+  }
+  tlb_put(L, va >> 12, td);
+  return true;
+}
+
+// Fast path: TLB hit + permission check. A miss (or a write to a shared page)
+// records the address in L.miss and returns nullptr: the instruction is
+// abandoned and re-executed after service_miss. Real faults set L.status.
+__device__ __forceinline__ u8 *xlate(Lane &L, u64 va, int acc, u64 *tdo = nullptr) {
+  u64 td;
+  if (!tlb_get(L, va >> 12, td)) {
+    L.miss = 1;
+    L.miss_va = va;
+    L.miss_acc = (u32)acc;
+    return nullptr;
+  }
+  if (!perm_ok(L, td, acc)) {
+    set_fault(L, WTFGPU_VEC_PF, pf_error(L, acc, true), va);
+    return nullptr;
+  }
+  if (acc == ACC_W && !(td & T_PRIV)) {  // first write: copy-on-write in service_miss
+    L.miss = 1;
+    L.miss_va = va;
+    L.miss_acc = (u32)acc;
+    return nullptr;
+  }
+  if (tdo) *tdo = td;
+  return (u8 *)(uintptr_t)(td & ~0xfffull) + (va & 0xfff);
+}
+
+// Guest virtual reads / writes of 1..8 bytes (page crossing handled).
+__device__ __forceinline__ bool vread(Lane &L, u64 va, u32 sz, u64 &out, int acc = ACC_R) {
+  const u32 off = (u32)(va & 0xfff);
+  if (off + sz <= 4096) {
+    const u8 *p = xlate(L, va, acc);
+    if (!p) return false;
+    out = load_le(p, sz);
+  } else {
+    const u32 n0 = 4096 - off;
+    if (acc == ACC_W) {  // both pages must pass the write check before either is copied
+      if (!xlate(L, va, ACC_WPROBE) || !xlate(L, va + n0, ACC_WPROBE)) return false;
+    }
+    const u8 *p0 = xlate(L, va, acc);
+    if (!p0) return false;
+    const u8 *p1 = xlate(L, va + n0, acc);
+    if (!p1) return false;
+    u64 v = 0;
+    for (u32 i = 0; i < sz; i++) v |= (u64)(i < n0 ? p0[i] : p1[i - n0]) << (8 * i);
+    out = v;
+  }
+  L.pend += sz;
+  return true;
+}
+
+__device__ __forceinline__ bool vwrite(Lane &L, u64 va, u32 sz, u64 v) {
+  const u32 off = (u32)(va & 0xfff);
+  u64 td0 = 0, td1 = 0;
+  if (off + sz <= 4096) {
+    u8 *p = xlate(L, va, ACC_W, &td0);
+    if (!p) return false;
+    store_le(p, sz, v);
+  } else {
+    const u32 n0 = 4096 - off;
+    if (!xlate(L, va, ACC_WPROBE) || !xlate(L, va + n0, ACC_WPROBE)) return false;
+    u8 *p0 = xlate(L, va, ACC_W, &td0);
+    if (!p0) return false;
+    u8 *p1 = xlate(L, va + n0, ACC_W, &td1);
+    if (!p1) return false;
+    for (u32 i = 0; i < sz; i++) {
+      if (i < n0) p0[i] = (u8)(v >> (8 * i));
+      else p1[i - n0] = (u8)(v >> (8 * i));
+    }
+  }
+  // a write into a page-table page invalidates cached translations (applied
+  // when the instruction retires, so a restart cannot livelock)
+  if ((td0 | td1) & T_PT) L.flush = 1;
+  L.pend += sz;
+  return true;
+}
+
+}  // namespace wtfgpu_dev

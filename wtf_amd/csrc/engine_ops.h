@@ -1,0 +1,1027 @@
+// engine_ops.h — decode into a wave-uniform micro-op and execute it per lane.
+//
+// Every supported instruction is decoded (once per RIP group, scalar work)
+// into a UOp: an operation, an A operand (destination / first source), a B
+// operand (second source) and their sizes. exec() is then one fixed pipeline:
+//   1. register / immediate operands;
+//   2. the single memory read (B, or A for read-modify-write);
+//   3. a pure compute switch on the operation;
+//   4. the single memory write (A);
+//   5. commit: registers, flags, rsp, rip.
+// Steps 2 and 4 are the only guest-memory call sites, so the kernel stays
+// small, and nothing is committed before every access has succeeded: a TLB
+// miss / first write abandons the attempt and the kernel re-runs it after
+// service_miss (engine_exec.h); a fault leaves no trace (U11). Rep string
+// instructions run their own loop and commit per iteration (x86 semantics).
+#pragma once
+#include "engine_exec.h"
+
+namespace wtfgpu_dev {
+
+enum { X_OK = 0, X_FAULT = 1, X_UNIMPL = 2, X_INT3 = 3, X_HLT = 4, X_KEEP = 6 };
+
+// operations
+enum : u32 {
+  O_ALU = 0,  // sub: 0 add,1 or,2 adc,3 sbb,4 and,5 sub,6 xor,7 cmp
+  O_TEST, O_MOV, O_MOVZX, O_MOVSX, O_XCHG, O_XADD, O_CMPXCHG, O_INCDEC, O_NOT, O_NEG,
+  O_SHIFT, O_SHXD, O_MULDIV, O_IMUL, O_BT, O_BSF, O_BSR, O_TZCNT, O_LZCNT, O_POPCNT,
+  O_CMOV, O_SETCC, O_BSWAP, O_CBW, O_CWD, O_LAHF, O_SAHF, O_FLAGOP, O_NOP, O_JCC, O_JMP,
+  O_CALL, O_RET, O_PUSH, O_POP, O_PUSHF, O_POPF, O_LEAVE, O_STRING, O_INT3, O_HLT, O_UD,
+  O_LEA, O_UNIMPL
+};
+// operand locations
+enum : u32 {
+  L_NONE = 0, L_GREG, L_RM, L_RAX, L_OPREG, L_IMM, L_ONE, L_CL, L_PUSH, L_POP, L_MOFFS,
+  L_RBPMEM, L_XLAT
+};
+// size kinds
+enum : u32 { Z_B = 0, Z_V, Z_STK, Z_Q, Z_W, Z_D };
+
+struct UOp {
+  u32 len, op, sub, asrc, bsrc, asz, bsz;
+  u32 aread, awrite, bwrite;
+  u32 reg, rm, opreg, is_mem, riprel, p67, rex, rep, seg;
+  i32 base, index;
+  u32 scale;
+  u64 disp, imm;
+  u32 supported, opbytes;
+};
+
+// ---------------------------------------------------------------- registers
+__device__ __forceinline__ u64 getr(const Lane &L, u32 rex, u32 r, u32 sz) {
+  if (sz == 1) {
+    if (!rex && r >= 4 && r < 8) return (R(L, r - 4) >> 8) & 0xff;
+    return R(L, r) & 0xff;
+  }
+  return R(L, r) & szmask(sz);
+}
+__device__ __forceinline__ void setr(Lane &L, u32 rex, u32 r, u32 sz, u64 v) {
+  if (sz == 1) {
+    if (!rex && r >= 4 && r < 8) {
+      R(L, r - 4) = (R(L, r - 4) & ~0xff00ull) | ((v & 0xff) << 8);
+    } else {
+      R(L, r) = (R(L, r) & ~0xffull) | (v & 0xff);
+    }
+  } else if (sz == 2) {
+    R(L, r) = (R(L, r) & ~0xffffull) | (v & 0xffff);
+  } else if (sz == 4) {
+    R(L, r) = v & 0xffffffffull;
+  } else {
+    R(L, r) = v;
+  }
+}
+
+// fs / gs bases are cold: read from lane memory when an override appears
+__device__ __forceinline__ u64 segbase(const Dev &P, const Lane &L, u32 seg) {
+  return seg == 4 ? P.fs_base[L.lane] : (seg == 5 ? P.gs_base[L.lane] : 0);
+}
+
+// ---------------------------------------------------------------- decode tables
+// entry: op(6) | asrc(4)<<6 | bsrc(4)<<10 | asz(3)<<14 | bsz(3)<<17 | aread<<20 |
+//        awrite<<21 | bwrite<<22 | modrm<<23 | immk(3)<<24 | group(4)<<27
+#define E(op, a, b, az, bz, ar, aw, bw, m, ik, grp)                                                        \
+  ((u32)(op) | ((u32)(a) << 6) | ((u32)(b) << 10) | ((u32)(az) << 14) | ((u32)(bz) << 17) |             \
+   ((u32)(ar) << 20) | ((u32)(aw) << 21) | ((u32)(bw) << 22) | ((u32)(m) << 23) | ((u32)(ik) << 24) | \
+   ((u32)(grp) << 27))
+#define UN E(O_UNIMPL, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
+enum : u32 { K_NONE = 0, K_B, K_W, K_Z, K_V, K_MOFFS, K_D };
+enum : u32 { G_NONE = 0, G_1, G_2, G_3, G_4, G_5, G_8F, G_C6, G_BA, G_ALU };
+
+#define ALU4                                                                             \
+  E(O_ALU, L_RM, L_GREG, Z_B, Z_B, 1, 1, 0, 1, K_NONE, G_ALU),                            \
+      E(O_ALU, L_RM, L_GREG, Z_V, Z_V, 1, 1, 0, 1, K_NONE, G_ALU),                        \
+      E(O_ALU, L_GREG, L_RM, Z_B, Z_B, 1, 1, 0, 1, K_NONE, G_ALU),                        \
+      E(O_ALU, L_GREG, L_RM, Z_V, Z_V, 1, 1, 0, 1, K_NONE, G_ALU),                        \
+      E(O_ALU, L_RAX, L_IMM, Z_B, Z_B, 1, 1, 0, 0, K_B, G_ALU),                           \
+      E(O_ALU, L_RAX, L_IMM, Z_V, Z_V, 1, 1, 0, 0, K_Z, G_ALU), UN, UN
+#define JCC E(O_JCC, 0, L_IMM, 0, Z_Q, 0, 0, 0, 0, K_B, 0)
+#define PUSHR E(O_PUSH, L_PUSH, L_OPREG, Z_STK, Z_STK, 0, 1, 0, 0, K_NONE, 0)
+#define POPR E(O_POP, L_OPREG, L_POP, Z_STK, Z_STK, 0, 1, 0, 0, K_NONE, 0)
+#define XCHGR E(O_XCHG, L_RAX, L_OPREG, Z_V, Z_V, 1, 1, 1, 0, K_NONE, 0)
+#define MOVR8 E(O_MOV, L_OPREG, L_IMM, Z_B, Z_B, 0, 1, 0, 0, K_B, 0)
+#define MOVRV E(O_MOV, L_OPREG, L_IMM, Z_V, Z_V, 0, 1, 0, 0, K_V, 0)
+#define STR(sz) E(O_STRING, 0, 0, sz, sz, 0, 0, 0, 0, K_NONE, 0)
+#define FLG E(O_FLAGOP, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0)
+
+__constant__ u32 kMap1[256] = {
+    /*00*/ ALU4, ALU4, ALU4, ALU4, ALU4, ALU4, ALU4, ALU4,
+    /*40*/ UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN,
+    /*50*/ PUSHR, PUSHR, PUSHR, PUSHR, PUSHR, PUSHR, PUSHR, PUSHR, POPR, POPR, POPR, POPR, POPR, POPR, POPR, POPR,
+    /*60*/ UN, UN, UN, E(O_MOVSX, L_GREG, L_RM, Z_V, Z_D, 0, 1, 0, 1, K_NONE, 0), UN, UN, UN, UN,
+    /*68*/ E(O_PUSH, L_PUSH, L_IMM, Z_STK, Z_STK, 0, 1, 0, 0, K_Z, 0),
+    E(O_IMUL, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_Z, 0),
+    E(O_PUSH, L_PUSH, L_IMM, Z_STK, Z_STK, 0, 1, 0, 0, K_B, 0),
+    E(O_IMUL, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_B, 0), UN, UN, UN, UN,
+    /*70*/ JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC,
+    /*80*/ E(O_ALU, L_RM, L_IMM, Z_B, Z_B, 1, 1, 0, 1, K_B, G_1), E(O_ALU, L_RM, L_IMM, Z_V, Z_V, 1, 1, 0, 1, K_Z, G_1),
+    UN, E(O_ALU, L_RM, L_IMM, Z_V, Z_V, 1, 1, 0, 1, K_B, G_1),
+    E(O_TEST, L_RM, L_GREG, Z_B, Z_B, 1, 0, 0, 1, K_NONE, 0), E(O_TEST, L_RM, L_GREG, Z_V, Z_V, 1, 0, 0, 1, K_NONE, 0),
+    E(O_XCHG, L_RM, L_GREG, Z_B, Z_B, 1, 1, 1, 1, K_NONE, 0), E(O_XCHG, L_RM, L_GREG, Z_V, Z_V, 1, 1, 1, 1, K_NONE, 0),
+    /*88*/ E(O_MOV, L_RM, L_GREG, Z_B, Z_B, 0, 1, 0, 1, K_NONE, 0), E(O_MOV, L_RM, L_GREG, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0),
+    E(O_MOV, L_GREG, L_RM, Z_B, Z_B, 0, 1, 0, 1, K_NONE, 0), E(O_MOV, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0),
+    UN, E(O_LEA, L_GREG, 0, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0), UN,
+    E(O_POP, L_RM, L_POP, Z_STK, Z_STK, 0, 1, 0, 1, K_NONE, G_8F),
+    /*90*/ XCHGR, XCHGR, XCHGR, XCHGR, XCHGR, XCHGR, XCHGR, XCHGR,
+    /*98*/ E(O_CBW, 0, 0, Z_V, Z_V, 0, 0, 0, 0, K_NONE, 0), E(O_CWD, 0, 0, Z_V, Z_V, 0, 0, 0, 0, K_NONE, 0), UN, UN,
+    E(O_PUSHF, L_PUSH, 0, Z_STK, Z_STK, 0, 1, 0, 0, K_NONE, 0), E(O_POPF, 0, L_POP, Z_STK, Z_STK, 0, 0, 0, 0, K_NONE, 0),
+    E(O_SAHF, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), E(O_LAHF, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0),
+    /*a0*/ E(O_MOV, L_RAX, L_MOFFS, Z_B, Z_B, 0, 1, 0, 0, K_MOFFS, 0), E(O_MOV, L_RAX, L_MOFFS, Z_V, Z_V, 0, 1, 0, 0, K_MOFFS, 0),
+    E(O_MOV, L_MOFFS, L_RAX, Z_B, Z_B, 0, 1, 0, 0, K_MOFFS, 0), E(O_MOV, L_MOFFS, L_RAX, Z_V, Z_V, 0, 1, 0, 0, K_MOFFS, 0),
+    STR(Z_B), STR(Z_V), STR(Z_B), STR(Z_V),
+    /*a8*/ E(O_TEST, L_RAX, L_IMM, Z_B, Z_B, 1, 0, 0, 0, K_B, 0), E(O_TEST, L_RAX, L_IMM, Z_V, Z_V, 1, 0, 0, 0, K_Z, 0),
+    STR(Z_B), STR(Z_V), STR(Z_B), STR(Z_V), STR(Z_B), STR(Z_V),
+    /*b0*/ MOVR8, MOVR8, MOVR8, MOVR8, MOVR8, MOVR8, MOVR8, MOVR8, MOVRV, MOVRV, MOVRV, MOVRV, MOVRV, MOVRV, MOVRV, MOVRV,
+    /*c0*/ E(O_SHIFT, L_RM, L_IMM, Z_B, Z_B, 1, 1, 0, 1, K_B, G_2), E(O_SHIFT, L_RM, L_IMM, Z_V, Z_B, 1, 1, 0, 1, K_B, G_2),
+    E(O_RET, 0, L_POP, Z_Q, Z_Q, 0, 0, 0, 0, K_W, 0), E(O_RET, 0, L_POP, Z_Q, Z_Q, 0, 0, 0, 0, K_NONE, 0), UN, UN,
+    E(O_MOV, L_RM, L_IMM, Z_B, Z_B, 0, 1, 0, 1, K_B, G_C6), E(O_MOV, L_RM, L_IMM, Z_V, Z_V, 0, 1, 0, 1, K_Z, G_C6),
+    /*c8*/ UN, E(O_LEAVE, 0, L_RBPMEM, Z_Q, Z_Q, 0, 0, 0, 0, K_NONE, 0), UN, UN,
+    E(O_INT3, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, UN, UN,
+    /*d0*/ E(O_SHIFT, L_RM, L_ONE, Z_B, Z_B, 1, 1, 0, 1, K_NONE, G_2), E(O_SHIFT, L_RM, L_ONE, Z_V, Z_B, 1, 1, 0, 1, K_NONE, G_2),
+    E(O_SHIFT, L_RM, L_CL, Z_B, Z_B, 1, 1, 0, 1, K_NONE, G_2), E(O_SHIFT, L_RM, L_CL, Z_V, Z_B, 1, 1, 0, 1, K_NONE, G_2),
+    UN, UN, UN, E(O_MOV, L_RAX, L_XLAT, Z_B, Z_B, 0, 1, 0, 0, K_NONE, 0),
+    /*d8*/ UN, UN, UN, UN, UN, UN, UN, UN,
+    /*e0*/ UN, UN, UN, UN, UN, UN, UN, UN,
+    /*e8*/ E(O_CALL, L_PUSH, L_IMM, Z_Q, Z_Q, 0, 1, 0, 0, K_D, 0), E(O_JMP, 0, L_IMM, Z_Q, Z_Q, 0, 0, 0, 0, K_D, 0), UN,
+    E(O_JMP, 0, L_IMM, Z_Q, Z_Q, 0, 0, 0, 0, K_B, 0), UN, UN, UN, UN,
+    /*f0*/ UN, UN, UN, UN, E(O_HLT, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), FLG,
+    E(O_TEST, L_RM, L_IMM, Z_B, Z_B, 1, 0, 0, 1, K_NONE, G_3), E(O_TEST, L_RM, L_IMM, Z_V, Z_V, 1, 0, 0, 1, K_NONE, G_3),
+    /*f8*/ FLG, FLG, UN, UN, FLG, FLG,
+    E(O_INCDEC, L_RM, 0, Z_B, Z_B, 1, 1, 0, 1, K_NONE, G_4), E(O_INCDEC, L_RM, 0, Z_V, Z_V, 1, 1, 0, 1, K_NONE, G_5),
+};
+
+#define NOPM E(O_NOP, 0, 0, 0, 0, 0, 0, 0, 1, K_NONE, 0)
+#define CMOV E(O_CMOV, L_GREG, L_RM, Z_V, Z_V, 1, 1, 0, 1, K_NONE, 0)
+#define JCC32 E(O_JCC, 0, L_IMM, 0, Z_Q, 0, 0, 0, 0, K_D, 0)
+#define SETCC E(O_SETCC, L_RM, 0, Z_B, Z_B, 0, 1, 0, 1, K_NONE, 0)
+#define BSWAP E(O_BSWAP, L_OPREG, 0, Z_V, Z_V, 1, 1, 0, 0, K_NONE, 0)
+#define BTRW E(O_BT, L_RM, L_GREG, Z_V, Z_V, 1, 1, 0, 1, K_NONE, 0)
+#define SHXD(ik) E(O_SHXD, L_RM, L_GREG, Z_V, Z_V, 1, 1, 0, 1, ik, 0)
+#define UN16 UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN
+__constant__ u32 kMap2[256] = {
+    /*00*/ UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, E(O_UD, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, NOPM, UN, UN,
+    /*10*/ UN, UN, UN, UN, UN, UN, UN, UN, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM,
+    /*20*/ UN16,
+    /*30*/ UN16,
+    /*40*/ CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV,
+    /*50*/ UN16,
+    /*60*/ UN16,
+    /*70*/ UN16,
+    /*80*/ JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32,
+    /*90*/ SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC,
+    /*a0*/ UN, UN, UN, E(O_BT, L_RM, L_GREG, Z_V, Z_V, 1, 0, 0, 1, K_NONE, 0), SHXD(K_B), SHXD(K_NONE), UN, UN,
+    /*a8*/ UN, UN, UN, BTRW, SHXD(K_B), SHXD(K_NONE), UN, E(O_IMUL, L_GREG, L_RM, Z_V, Z_V, 1, 1, 0, 1, K_NONE, 0),
+    /*b0*/ E(O_CMPXCHG, L_RM, L_GREG, Z_B, Z_B, 1, 1, 0, 1, K_NONE, 0),
+    E(O_CMPXCHG, L_RM, L_GREG, Z_V, Z_V, 1, 1, 0, 1, K_NONE, 0), UN, BTRW, UN, UN,
+    E(O_MOVZX, L_GREG, L_RM, Z_V, Z_B, 0, 1, 0, 1, K_NONE, 0), E(O_MOVZX, L_GREG, L_RM, Z_V, Z_W, 0, 1, 0, 1, K_NONE, 0),
+    /*b8*/ E(O_POPCNT, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0), UN,
+    E(O_BT, L_RM, L_IMM, Z_V, Z_B, 1, 1, 0, 1, K_B, G_BA), BTRW,
+    E(O_BSF, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0), E(O_BSR, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0),
+    E(O_MOVSX, L_GREG, L_RM, Z_V, Z_B, 0, 1, 0, 1, K_NONE, 0), E(O_MOVSX, L_GREG, L_RM, Z_V, Z_W, 0, 1, 0, 1, K_NONE, 0),
+    /*c0*/ E(O_XADD, L_RM, L_GREG, Z_B, Z_B, 1, 1, 1, 1, K_NONE, 0), E(O_XADD, L_RM, L_GREG, Z_V, Z_V, 1, 1, 1, 1, K_NONE, 0),
+    UN, UN, UN, UN, UN, UN, BSWAP, BSWAP, BSWAP, BSWAP, BSWAP, BSWAP, BSWAP, BSWAP,
+    /*d0*/ UN16,
+    /*e0*/ UN16,
+    /*f0*/ UN16,
+};
+#undef E
+#undef UN
+#undef ALU4
+#undef JCC
+#undef PUSHR
+#undef POPR
+#undef XCHGR
+#undef MOVR8
+#undef MOVRV
+#undef STR
+#undef FLG
+#undef NOPM
+#undef CMOV
+#undef JCC32
+#undef SETCC
+#undef BSWAP
+#undef BTRW
+#undef SHXD
+#undef UN16
+
+// Instruction bytes as two uniform u64 (SGPR pairs).
+struct IBytes {
+  u64 lo, hi;
+  u32 avail;
+};
+__device__ __forceinline__ u32 ib_at(const IBytes &b, u32 i) {
+  return (u32)((i < 8 ? (b.lo >> (8 * i)) : (b.hi >> (8 * (i - 8)))) & 0xff);
+}
+__device__ __forceinline__ u64 ib_get(const IBytes &b, u32 pos, u32 n) {
+  u64 v = 0;
+  for (u32 i = 0; i < n; i++) v |= (u64)ib_at(b, pos + i) << (8 * i);
+  return v;
+}
+
+__device__ __forceinline__ u32 zsize(u32 z, u32 osz, u32 p66) {
+  switch (z) {
+    case Z_B: return 1;
+    case Z_V: return osz;
+    case Z_STK: return p66 ? 2 : 8;
+    case Z_Q: return 8;
+    case Z_W: return 2;
+    default: return 4;
+  }
+}
+
+// Decode (uniform). 0 ok, 1 needs bytes beyond avail, 2 longer than 15 (#GP).
+__device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
+  u32 pos = 0, p66 = 0, rex = 0, c;
+  u.p67 = u.rep = u.seg = 0;
+  for (;;) {
+    if (pos >= 15) return 2;
+    if (pos >= b.avail) return 1;
+    c = ib_at(b, pos++);
+    if ((c & 0xf0) == 0x40) {  // REX; ignored unless it is the last prefix
+      rex = c;
+      continue;
+    }
+    if (c == 0x66) p66 = 1;
+    else if (c == 0x67) u.p67 = 1;
+    else if (c == 0xf2 || c == 0xf3) u.rep = c;
+    else if (c == 0x64) u.seg = 4;
+    else if (c == 0x65) u.seg = 5;
+    else if (c != 0xf0 && c != 0x26 && c != 0x2e && c != 0x36 && c != 0x3e) break;
+    rex = 0;
+  }
+  u.rex = rex;
+  const u32 rexw = (rex >> 3) & 1, rexr = (rex >> 2) & 1, rexx = (rex >> 1) & 1, rexb = rex & 1;
+  u32 e, map2 = 0;
+  if (c == 0x0f) {
+    if (pos >= 15) return 2;
+    if (pos >= b.avail) return 1;
+    c = ib_at(b, pos++);
+    if (c == 0x38 || c == 0x3a) {  // three-byte maps: outside the ISA subset
+      if (pos >= 15) return 2;
+      if (pos >= b.avail) return 1;
+      pos++;
+      u.len = pos;
+      u.op = O_UNIMPL;
+      u.supported = 0;
+      u.opbytes = pos >= 4 ? (u32)b.lo : ((u32)b.lo & ((1u << (8 * pos)) - 1));
+      return 0;
+    }
+    map2 = 1;
+    e = kMap2[c];
+    if (c == 0xb8 && u.rep != 0xf3) e = O_UNIMPL;  // popcnt needs f3
+  } else {
+    e = kMap1[c];
+    if (c == 0x90 && !rexb) e = O_NOP;  // 90 is nop (no zero-extension), f3 90 pause
+  }
+  const u32 osz = rexw ? 8 : (p66 ? 2 : 4);
+  u.op = e & 63;
+  u.asrc = (e >> 6) & 15;
+  u.bsrc = (e >> 10) & 15;
+  u.asz = zsize((e >> 14) & 7, osz, p66);
+  u.bsz = zsize((e >> 17) & 7, osz, p66);
+  u.aread = (e >> 20) & 1;
+  u.awrite = (e >> 21) & 1;
+  u.bwrite = (e >> 22) & 1;
+  const u32 hasm = (e >> 23) & 1;
+  u32 ik = (e >> 24) & 7;
+  const u32 grp = (e >> 27) & 15;
+  u.sub = c & 0xf;  // cc for jcc/cmov/setcc, string opcode low bits
+  if (grp == G_ALU) u.sub = (c >> 3) & 7;
+  u.opreg = (c & 7) | (rexb << 3);
+  u.is_mem = u.riprel = 0;
+  u.reg = u.rm = 0;
+  u.base = u.index = -1;
+  u.scale = 0;
+  u.disp = 0;
+  if (hasm) {
+    if (pos >= 15) return 2;
+    if (pos >= b.avail) return 1;
+    const u32 m = ib_at(b, pos++);
+    const u32 mod = m >> 6, rm = m & 7;
+    u.reg = ((m >> 3) & 7) | (rexr << 3);
+    if (mod == 3) {
+      u.rm = rm | (rexb << 3);
+    } else {
+      u.is_mem = 1;
+      if (rm == 4) {
+        if (pos >= 15) return 2;
+        if (pos >= b.avail) return 1;
+        const u32 sib = ib_at(b, pos++);
+        const u32 idx = ((sib >> 3) & 7) | (rexx << 3), base = sib & 7;
+        if (idx != 4) {
+          u.index = (i32)idx;
+          u.scale = sib >> 6;
+        }
+        if (base == 5 && mod == 0) {
+          if (pos + 4 > 15) return 2;
+          if (pos + 4 > b.avail) return 1;
+          u.disp = sext(ib_get(b, pos, 4), 4);
+          pos += 4;
+        } else {
+          u.base = (i32)(base | (rexb << 3));
+        }
+      } else if (rm == 5 && mod == 0) {
+        if (pos + 4 > 15) return 2;
+        if (pos + 4 > b.avail) return 1;
+        u.riprel = 1;
+        u.disp = sext(ib_get(b, pos, 4), 4);
+        pos += 4;
+      } else {
+        u.base = (i32)(rm | (rexb << 3));
+      }
+      if (mod == 1) {
+        if (pos + 1 > 15) return 2;
+        if (pos + 1 > b.avail) return 1;
+        u.disp = sext(ib_get(b, pos, 1), 1);
+        pos += 1;
+      } else if (mod == 2) {
+        if (pos + 4 > 15) return 2;
+        if (pos + 4 > b.avail) return 1;
+        u.disp = sext(ib_get(b, pos, 4), 4);
+        pos += 4;
+      }
+    }
+    // modrm.reg selected forms
+    const u32 r3 = u.reg & 7;
+    switch (grp) {
+      case G_1:
+      case G_2:
+        u.sub = r3;
+        break;
+      case G_3:
+        if (r3 <= 1) {
+          ik = c == 0xf6 ? K_B : K_Z;
+        } else if (r3 == 2 || r3 == 3) {
+          u.op = r3 == 2 ? O_NOT : O_NEG;
+          u.awrite = 1;
+          u.bsrc = L_NONE;
+        } else {
+          u.op = O_MULDIV;
+          u.sub = r3;
+          u.bsrc = L_RM;
+          u.bsz = u.asz;
+          u.asrc = L_NONE;
+          u.aread = 0;
+          u.awrite = 0;
+        }
+        break;
+      case G_4:
+        if (r3 > 1) u.op = O_UNIMPL;
+        u.sub = r3;
+        break;
+      case G_5:
+        u.sub = r3;
+        if (r3 == 2 || r3 == 4) {  // call / jmp near indirect: 64-bit target
+          u.op = r3 == 2 ? O_CALL : O_JMP;
+          u.asrc = r3 == 2 ? L_PUSH : L_NONE;
+          u.asz = 8;
+          u.aread = 0;
+          u.awrite = r3 == 2;
+          u.bsrc = L_RM;
+          u.bsz = 8;
+        } else if (r3 == 6) {
+          u.op = O_PUSH;
+          u.asrc = L_PUSH;
+          u.asz = u.bsz = p66 ? 2 : 8;
+          u.aread = 0;
+          u.awrite = 1;
+          u.bsrc = L_RM;
+        } else if (r3 > 1) {
+          u.op = O_UNIMPL;
+        }
+        break;
+      case G_8F:
+      case G_C6:
+        if (r3 != 0) u.op = O_UNIMPL;
+        break;
+      case G_BA:
+        if (r3 < 4) u.op = O_UNIMPL;
+        u.sub = r3;
+        if (r3 == 4) u.awrite = 0;
+        break;
+      default:
+        break;
+    }
+  }
+  if (u.op == O_ALU && u.sub == 7) u.awrite = 0;  // cmp reads its destination, never writes it
+  if (map2) {
+    if (u.op == O_BT && grp != G_BA) u.sub = c == 0xa3 ? 4 : c == 0xab ? 5 : c == 0xb3 ? 6 : 7;
+    if (u.op == O_SHXD) u.sub = (c >= 0xac ? 1u : 0u) | ((c & 1) ? 2u : 0u);  // bit0 shrd, bit1 count in cl
+    if (u.op == O_BSF && u.rep == 0xf3) u.op = O_TZCNT;
+    if (u.op == O_BSR && u.rep == 0xf3) u.op = O_LZCNT;
+  } else if (u.op == O_FLAGOP) {
+    u.sub = c;
+  }
+  u32 n = 0;
+  switch (ik) {
+    case K_B: n = 1; break;
+    case K_W: n = 2; break;
+    case K_Z: n = osz == 2 ? 2 : 4; break;
+    case K_V: n = osz; break;
+    case K_MOFFS: n = u.p67 ? 4 : 8; break;
+    case K_D: n = 4; break;
+    default: n = 0;
+  }
+  if (pos + n > 15) return 2;
+  if (pos + n > b.avail) return 1;
+  const u64 raw = ib_get(b, pos, n);
+  // the immediates x86 sign-extends: Ib/Iz of alu/test/push/imul, branch displacements, c7 Iz
+  const bool sx = n && (u.op == O_ALU || u.op == O_TEST || u.op == O_PUSH || u.op == O_IMUL || u.op == O_JCC ||
+                        u.op == O_JMP || u.op == O_CALL || (u.op == O_MOV && c == 0xc7 && !map2));
+  u.imm = sx ? sext(raw, n) : raw;
+  pos += n;
+  u.len = pos;
+  u.opbytes = pos >= 4 ? (u32)b.lo : ((u32)b.lo & ((1u << (8 * pos)) - 1));
+  u.supported = u.op != O_UNIMPL;
+  return 0;
+}
+
+// ---------------------------------------------------------------- arithmetic
+// 0 add,1 or,2 adc,3 sbb,4 and,5 sub,6 xor,7 cmp; returns result, status flags in f
+__device__ __forceinline__ u64 alu2(u32 op, u64 a, u64 b, u32 sz, u64 rfl, u64 &f) {
+  const u64 mk = szmask(sz);
+  a &= mk;
+  b &= mk;
+  u64 res;
+  if (op == 0 || op == 2) {
+    const u64 c = op == 2 ? (rfl & F_CF) : 0;
+    res = (a + b + c) & mk;
+    bool carry;
+    if (sz == 8) carry = (res < a) || (c && res == a);
+    else carry = ((a + b + c) >> (8 * sz)) & 1;
+    f = szp(res, sz) | (carry ? F_CF : 0) | (((a ^ b ^ res) & 0x10) ? F_AF : 0) |
+        (msb((a ^ res) & (b ^ res), sz) ? F_OF : 0);
+  } else if (op == 3 || op == 5 || op == 7) {
+    const u64 c = op == 3 ? (rfl & F_CF) : 0;
+    res = (a - b - c) & mk;
+    const bool borrow = (a < b) || (c && a == b);
+    f = szp(res, sz) | (borrow ? F_CF : 0) | (((a ^ b ^ res) & 0x10) ? F_AF : 0) |
+        (msb((a ^ b) & (a ^ res), sz) ? F_OF : 0);
+  } else {
+    res = op == 1 ? (a | b) : (op == 4 ? (a & b) : (a ^ b));
+    f = szp(res, sz);
+  }
+  return res;
+}
+__device__ __forceinline__ u64 with_status(u64 rfl, u64 f) { return (rfl & ~F_STATUS) | f; }
+
+__device__ __forceinline__ bool cond(u64 fl, u32 cc) {
+  const bool cf = fl & F_CF, zf = fl & F_ZF, sf = fl & F_SF, of = fl & F_OF, pf = fl & F_PF;
+  bool r;
+  switch (cc >> 1) {
+    case 0: r = of; break;
+    case 1: r = cf; break;
+    case 2: r = zf; break;
+    case 3: r = cf || zf; break;
+    case 4: r = sf; break;
+    case 5: r = pf; break;
+    case 6: r = sf != of; break;
+    default: r = zf || (sf != of); break;
+  }
+  return (cc & 1) ? !r : r;
+}
+
+// shifts / rotates (U2, U3)
+__device__ __forceinline__ u64 shift_op(u32 op, u64 v, u32 count, u32 sz, u64 &fl) {
+  const u32 bits = 8 * sz;
+  const u64 mk = szmask(sz);
+  const u32 cnt = count & (sz == 8 ? 0x3f : 0x1f);
+  v &= mk;
+  if (cnt == 0) return v;
+  u64 res = v, f = fl, cf;
+  switch (op) {
+    case 0: {
+      const u32 c = cnt % bits;
+      res = c ? ((v << c) | (v >> (bits - c))) & mk : v;
+      cf = res & 1;
+      f = (f & ~(F_CF | F_OF)) | (cf ? F_CF : 0) | ((msb(res, sz) ^ cf) ? F_OF : 0);
+      break;
+    }
+    case 1: {
+      const u32 c = cnt % bits;
+      res = c ? ((v >> c) | (v << (bits - c))) & mk : v;
+      cf = msb(res, sz);
+      f = (f & ~(F_CF | F_OF)) | (cf ? F_CF : 0) | ((msb(res, sz) ^ ((res >> (bits - 2)) & 1)) ? F_OF : 0);
+      break;
+    }
+    case 2: {
+      const u32 c = sz == 1 ? cnt % 9 : (sz == 2 ? cnt % 17 : cnt);
+      u64 carry = fl & F_CF;
+      if (c) {
+        const u64 hi_part = c == 1 ? 0 : (v >> (bits - c + 1));
+        res = (((v << c) & mk) | (carry << (c - 1)) | hi_part) & mk;
+        carry = (v >> (bits - c)) & 1;
+      }
+      f = (f & ~(F_CF | F_OF)) | (carry ? F_CF : 0) | ((msb(res, sz) ^ carry) ? F_OF : 0);
+      break;
+    }
+    case 3: {
+      const u32 c = sz == 1 ? cnt % 9 : (sz == 2 ? cnt % 17 : cnt);
+      u64 carry = fl & F_CF;
+      if (c) {
+        const u64 hi_part = c == 1 ? 0 : ((v << (bits - c + 1)) & mk);
+        res = ((v >> c) | (carry << (bits - c)) | hi_part) & mk;
+        carry = (v >> (c - 1)) & 1;
+      }
+      f = (f & ~(F_CF | F_OF)) | (carry ? F_CF : 0) | ((msb(res, sz) ^ ((res >> (bits - 2)) & 1)) ? F_OF : 0);
+      break;
+    }
+    case 4:
+    case 6:
+      res = (v << cnt) & mk;
+      cf = cnt <= bits ? ((v >> (bits - cnt)) & 1) : 0;
+      f = (f & ~F_STATUS) | szp(res, sz) | (cf ? F_CF : 0) | ((msb(res, sz) ^ cf) ? F_OF : 0);
+      break;
+    case 5:
+      res = v >> cnt;
+      cf = cnt <= bits ? ((v >> (cnt - 1)) & 1) : 0;
+      f = (f & ~F_STATUS) | szp(res, sz) | (cf ? F_CF : 0) | (msb(v, sz) ? F_OF : 0);
+      break;
+    default: {
+      const i64 sv = (i64)sext(v, sz);
+      res = (u64)(sv >> (cnt >= bits ? bits - 1 : cnt)) & mk;
+      cf = ((u64)(sv >> (cnt >= bits ? bits - 1 : cnt - 1))) & 1;
+      f = (f & ~F_STATUS) | szp(res, sz) | (cf ? F_CF : 0);
+      break;
+    }
+  }
+  fl = f;
+  return res;
+}
+
+// shld / shrd (U7): sub bit0 = shrd
+__device__ __forceinline__ u64 shxd(u32 sub, u64 a, u64 b, u32 cnt, u32 sz, u64 &fl) {
+  const u32 bits = 8 * sz;
+  const u32 c = cnt & (sz == 8 ? 0x3f : 0x1f);
+  if (c == 0) return a;
+  const u64 mk = szmask(sz);
+  u64 res, cf;
+  if (sz == 2) {
+    if (!(sub & 1)) {
+      const u64 pat = ((a & 0xffff) << 32) | ((b & 0xffff) << 16) | (a & 0xffff);
+      res = ((pat << c) >> 32) & 0xffff;
+      cf = ((pat << (c - 1)) >> 47) & 1;
+    } else {
+      const u64 pat = (a & 0xffff) | ((b & 0xffff) << 16) | ((a & 0xffff) << 32);
+      res = (pat >> c) & 0xffff;
+      cf = (pat >> (c - 1)) & 1;
+    }
+  } else if (!(sub & 1)) {
+    res = ((a << c) | (b >> (bits - c))) & mk;
+    cf = (a >> (bits - c)) & 1;
+  } else {
+    res = ((a >> c) | (b << (bits - c))) & mk;
+    cf = (a >> (c - 1)) & 1;
+  }
+  fl = with_status(fl, szp(res, sz) | (cf ? F_CF : 0) | ((msb(res, sz) ^ msb(a, sz)) ? F_OF : 0));
+  return res;
+}
+
+// unsigned 128/64 division; requires hi < dv
+__device__ __forceinline__ void divu128(u64 hi, u64 lo, u64 dv, u64 &q, u64 &r) {
+  if (hi == 0) {
+    q = lo / dv;
+    r = lo % dv;
+    return;
+  }
+  u64 qq = 0, rem = hi;
+  for (int i = 63; i >= 0; i--) {
+    const u64 top = rem >> 63;
+    rem = (rem << 1) | ((lo >> i) & 1);
+    if (top || rem >= dv) {
+      rem -= dv;
+      qq |= 1ull << i;
+    }
+  }
+  q = qq;
+  r = rem;
+}
+
+// signed multiply of sz-byte operands: low result + overflow (CF=OF)
+__device__ __forceinline__ u64 imul_lo(u64 a, u64 b, u32 sz, bool &ovf) {
+  const i64 sa = (i64)sext(a & szmask(sz), sz), sb = (i64)sext(b & szmask(sz), sz);
+  if (sz == 8) {
+    const u64 lo = (u64)sa * (u64)sb;
+    ovf = (u64)__mul64hi(sa, sb) != (u64)((i64)lo >> 63);
+    return lo;
+  }
+  const i64 p = sa * sb;
+  const u64 lo = (u64)p & szmask(sz);
+  ovf = (i64)sext(lo, sz) != p;
+  return lo;
+}
+
+// mul / imul / div / idiv (f6/f7 /4../7) into ra (rax or ax) and rd (rdx).
+__device__ __forceinline__ bool muldiv(const Lane &L, u32 sub, u32 sz, u64 src, u64 &ra, u64 &rd, u64 &fl) {
+  const u64 mk = szmask(sz);
+  const u32 bits = 8 * sz;
+  src &= mk;
+  const u64 a = sz == 1 ? (R(L, 0) & 0xff) : (R(L, 0) & mk);
+  if (sub == 4 || sub == 5) {
+    u64 lo, hi;
+    bool ovf;
+    if (sub == 4) {
+      if (sz == 8) {
+        lo = a * src;
+        hi = __umul64hi(a, src);
+      } else {
+        const u64 p = a * src;
+        lo = p & mk;
+        hi = (p >> bits) & mk;
+      }
+      ovf = hi != 0;
+    } else {
+      const i64 sa = (i64)sext(a, sz), sb = (i64)sext(src, sz);
+      if (sz == 8) {
+        lo = (u64)sa * (u64)sb;
+        hi = (u64)__mul64hi(sa, sb);
+        ovf = hi != (u64)((i64)lo >> 63);
+      } else {
+        const i64 p = sa * sb;
+        lo = (u64)p & mk;
+        hi = ((u64)p >> bits) & mk;
+        ovf = (i64)sext(lo, sz) != p;
+      }
+    }
+    if (sz == 1) ra = (hi << 8) | lo;
+    else {
+      ra = lo;
+      rd = hi;
+    }
+    fl = with_status(fl, szp(lo, sz) | (ovf ? (F_CF | F_OF) : 0));
+    return true;
+  }
+  if (src == 0) return false;
+  if (sub == 6) {
+    u64 q, r;
+    if (sz == 1) {
+      const u64 n = R(L, 0) & 0xffff;
+      q = n / src;
+      r = n % src;
+      if (q > 0xff) return false;
+      ra = (r << 8) | q;
+      return true;
+    }
+    const u64 hi = R(L, 2) & mk;
+    if (sz == 8) {
+      if (hi >= src) return false;
+      divu128(hi, a, src, q, r);
+    } else {
+      const u64 n = (hi << bits) | a;
+      q = n / src;
+      r = n % src;
+      if (q > mk) return false;
+    }
+    ra = q;
+    rd = r;
+    return true;
+  }
+  const i64 dv = (i64)sext(src, sz);
+  if (sz != 8) {
+    const i64 n = sz == 1 ? (i64)(int16_t)(R(L, 0) & 0xffff) : (i64)sext(((R(L, 2) & mk) << bits) | a, 2 * sz);
+    if (dv == -1 && n == INT64_MIN) return false;
+    const i64 q = n / dv, r = n % dv;
+    if (q < -((i64)1 << (bits - 1)) || q > ((i64)1 << (bits - 1)) - 1) return false;
+    if (sz == 1) ra = (((u64)r & 0xff) << 8) | ((u64)q & 0xff);
+    else {
+      ra = (u64)q;
+      rd = (u64)r;
+    }
+    return true;
+  }
+  const u64 nhi = R(L, 2), nlo = R(L, 0);
+  const bool nneg = (i64)nhi < 0, dneg = dv < 0;
+  u64 ahi = nhi, alo = nlo;
+  if (nneg) {
+    alo = ~nlo + 1;
+    ahi = ~nhi + (alo == 0 ? 1 : 0);
+  }
+  const u64 adv = dneg ? (u64)(-(dv + 1)) + 1 : (u64)dv;
+  if (ahi >= adv) return false;
+  u64 q, r;
+  divu128(ahi, alo, adv, q, r);
+  const bool qneg = nneg != dneg;
+  if ((!qneg && q > 0x7fffffffffffffffull) || (qneg && q > 0x8000000000000000ull)) return false;
+  ra = qneg ? (u64)(-(i64)(q - 1) - 1) : q;
+  rd = nneg ? (u64)(-(i64)r) : r;
+  return true;
+}
+
+// ---------------------------------------------------------------- string ops
+__device__ __forceinline__ int string_op(const Dev &P, Lane &L, const UOp &u) {
+  const u32 op = 0xa0 | (u.sub & 0xe);
+  const u32 sz = u.asz;
+  const u64 amask = u.p67 ? 0xffffffffull : ~0ull;
+  const u64 step = (L.rflags & F_DF) ? (u64)(-(i64)sz) : (u64)sz;
+  const u64 sb = segbase(P, L, u.seg);
+  const bool src = op == 0xa4 || op == 0xa6 || op == 0xac;
+  const bool dstw = op == 0xa4 || op == 0xaa;
+  const bool dstr = op == 0xa6 || op == 0xae;
+  for (;;) {
+    if (u.rep && (R(L, 1) & amask) == 0) break;
+    const u64 rsi = R(L, 6) & amask, rdi = R(L, 7) & amask;
+    u64 a = R(L, 0), b = 0;
+    if (src && !vread(L, sb + rsi, sz, a)) return X_KEEP;
+    if (dstr && !vread(L, rdi, sz, b)) return X_KEEP;
+    if (dstw && !vwrite(L, rdi, sz, a)) return X_KEEP;
+    if (dstr) {
+      u64 f;
+      alu2(7, op == 0xa6 ? a : R(L, 0), b, sz, L.rflags, f);
+      L.rflags = with_status(L.rflags, f);
+    }
+    if (op == 0xac) setr(L, u.rex, 0, sz, a);
+    if (src) R(L, 6) = (rsi + step) & amask;
+    if (op != 0xac) R(L, 7) = (rdi + step) & amask;
+    L.nbytes += L.pend;  // the iteration is architecturally complete
+    L.pend = 0;
+    if (!u.rep) break;
+    R(L, 1) = (R(L, 1) - 1) & amask;
+    if (dstr) {
+      const bool zf = L.rflags & F_ZF;
+      if (u.rep == 0xf3 && !zf) break;
+      if (u.rep == 0xf2 && zf) break;
+    }
+  }
+  return X_OK;
+}
+
+// ---------------------------------------------------------------- execute
+__device__ __forceinline__ bool loc_is_mem(const UOp &u, u32 loc) {
+  return (loc == L_RM && u.is_mem) || loc >= L_PUSH;
+}
+__device__ __forceinline__ u64 loc_reg_read(const Lane &L, const UOp &u, u32 loc, u32 sz) {
+  switch (loc) {
+    case L_GREG: return getr(L, u.rex, u.reg, sz);
+    case L_RM: return getr(L, u.rex, u.rm, sz);
+    case L_RAX: return getr(L, u.rex, 0, sz);
+    case L_OPREG: return getr(L, u.rex, u.opreg, sz);
+    case L_IMM: return u.imm;
+    case L_ONE: return 1;
+    case L_CL: return R(L, 1) & 0xff;
+    default: return 0;
+  }
+}
+__device__ __forceinline__ u32 loc_reg(const UOp &u, u32 loc) {
+  return loc == L_GREG ? u.reg : loc == L_RM ? u.rm : loc == L_OPREG ? u.opreg : 0;
+}
+
+// One attempt at the instruction; nrip = address of the next instruction.
+__device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next) {
+  next = nrip;
+  const u32 op = u.op;
+  if (op == O_STRING) return string_op(P, L, u);
+  if (op == O_LEA && !u.is_mem) {
+    set_fault(L, WTFGPU_VEC_UD, 0, 0);
+    return X_FAULT;
+  }
+  // ---- addresses
+  const u64 sb = u.seg ? segbase(P, L, u.seg) : 0;
+  u64 ea = 0;
+  if (u.is_mem) {
+    if (u.riprel) {
+      ea = nrip + u.disp;
+    } else {
+      ea = u.disp;
+      if (u.base >= 0) ea += R(L, u.base);
+      if (u.index >= 0) ea += R(L, u.index) << u.scale;
+    }
+    if (u.p67) ea &= 0xffffffffull;
+  }
+  const u64 rsp = R(L, 4);
+  // ---- register / immediate operands
+  u64 a = (u.aread && !loc_is_mem(u, u.asrc)) ? loc_reg_read(L, u, u.asrc, u.asz) : 0;
+  u64 b = loc_is_mem(u, u.bsrc) ? 0 : loc_reg_read(L, u, u.bsrc, u.bsz);
+  if (op == O_BT && u.is_mem && u.bsrc == L_GREG) {
+    // bit string addressing: the signed register offset selects the word
+    const i64 s = (i64)sext(b, u.bsz);
+    ea += (u64)((s >> (u.asz == 8 ? 6 : u.asz == 4 ? 5 : 4)) * (i64)u.asz);
+  }
+  // ---- the memory read
+  const bool bmem = loc_is_mem(u, u.bsrc);
+  const bool amem = loc_is_mem(u, u.asrc);
+  if (bmem || (u.aread && amem)) {
+    const u32 rloc = bmem ? u.bsrc : u.asrc;
+    u64 addr;
+    switch (rloc) {
+      case L_RM: addr = ea + sb; break;
+      case L_POP: addr = rsp; break;
+      case L_MOFFS: addr = u.imm + sb; break;
+      case L_RBPMEM: addr = R(L, 5); break;
+      default: {  // xlat
+        u64 x = R(L, 3) + (R(L, 0) & 0xff);
+        if (u.p67) x &= 0xffffffffull;
+        addr = x + sb;
+        break;
+      }
+    }
+    const bool rmw = !bmem && u.awrite;
+    u64 v = 0;
+    if (!vread(L, addr, bmem ? u.bsz : u.asz, v, rmw ? ACC_W : ACC_R)) return X_FAULT;
+    if (bmem) b = v;
+    else a = v;
+  }
+  // ---- compute (pure: lane state untouched)
+  const u32 asz = u.asz;
+  u64 res = 0, resb = 0, fl = L.rflags, f, ra = 0, rd = 0;
+  bool wa = u.awrite, wrax = false, wrdx = false;
+  u32 raxsz = asz;
+  i64 drsp = 0;
+  switch (op) {
+    case O_ALU:
+      res = alu2(u.sub, a, b, asz, fl, f);
+      fl = with_status(fl, f);
+      wa = u.sub != 7;
+      break;
+    case O_TEST:
+      alu2(4, a, b, asz, fl, f);
+      fl = with_status(fl, f);
+      break;
+    case O_MOV: res = b; break;
+    case O_LEA: res = ea; break;
+    case O_MOVZX: res = b & szmask(u.bsz); break;
+    case O_MOVSX: res = sext(b & szmask(u.bsz), u.bsz); break;
+    case O_XCHG:
+      res = b;
+      resb = a;
+      break;
+    case O_XADD:
+      res = alu2(0, a, b, asz, fl, f);
+      fl = with_status(fl, f);
+      resb = a;
+      break;
+    case O_CMPXCHG: {
+      const u64 acc = getr(L, u.rex, 0, asz);
+      alu2(7, acc, a, asz, fl, f);
+      fl = with_status(fl, f);
+      if ((acc & szmask(asz)) == (a & szmask(asz))) {
+        res = b;
+      } else {
+        res = a;
+        wa = u.is_mem;  // memory is written back; a register destination is untouched
+        ra = a;
+        wrax = true;
+      }
+      break;
+    }
+    case O_INCDEC:
+      res = alu2(u.sub ? 5 : 0, a, 1, asz, fl, f);
+      fl = (fl & ~(F_STATUS & ~F_CF)) | (f & ~F_CF);
+      break;
+    case O_NOT: res = ~a; break;
+    case O_NEG:
+      res = alu2(5, 0, a, asz, fl, f);
+      fl = with_status(fl, f);
+      break;
+    case O_SHIFT: res = shift_op(u.sub, a, (u32)b, asz, fl); break;
+    case O_SHXD: res = shxd(u.sub, a, b, (u.sub & 2) ? (u32)(R(L, 1) & 0xff) : (u32)u.imm, asz, fl); break;
+    case O_MULDIV:
+      if (!muldiv(L, u.sub, u.bsz, b, ra, rd, fl)) {
+        set_fault(L, WTFGPU_VEC_DE, 0, 0);
+        return X_FAULT;
+      }
+      wrax = true;
+      wrdx = u.bsz != 1;
+      raxsz = u.bsz == 1 ? 2 : u.bsz;
+      break;
+    case O_IMUL: {
+      bool ovf;
+      // 0f af: dest * r/m ; 69 / 6b: r/m * imm
+      res = u.aread ? imul_lo(a, b, asz, ovf) : imul_lo(b, u.imm, asz, ovf);
+      fl = with_status(fl, szp(res, asz) | (ovf ? (F_CF | F_OF) : 0));
+      break;
+    }
+    case O_BT: {
+      const u64 bitoff = b & (8 * asz - 1);
+      res = u.sub == 5 ? (a | (1ull << bitoff)) : u.sub == 6 ? (a & ~(1ull << bitoff)) : (a ^ (1ull << bitoff));
+      wa = u.sub != 4;
+      fl = (fl & ~F_CF) | ((a >> bitoff) & 1);
+      break;
+    }
+    case O_BSF:
+    case O_BSR: {
+      const u64 v = b & szmask(u.bsz);
+      if (v == 0) {
+        fl |= F_ZF;
+        wa = false;  // destination unchanged (U6)
+      } else {
+        res = op == O_BSF ? (u64)__builtin_ctzll(v) : (u64)(63 - __builtin_clzll(v));
+        fl &= ~F_ZF;
+      }
+      break;
+    }
+    case O_TZCNT:
+    case O_LZCNT: {
+      const u32 bits = 8 * u.bsz;
+      const u64 v = b & szmask(u.bsz);
+      if (op == O_TZCNT) res = v ? (u64)__builtin_ctzll(v) : bits;
+      else res = v ? (u64)(__builtin_clzll(v) - (64 - bits)) : bits;
+      fl = (fl & ~(F_CF | F_ZF)) | (v == 0 ? F_CF : 0) | (res == 0 ? F_ZF : 0);
+      break;
+    }
+    case O_POPCNT: {
+      const u64 v = b & szmask(u.bsz);
+      res = (u64)__popcll(v);
+      fl = with_status(fl, v ? 0 : F_ZF);
+      break;
+    }
+    case O_CMOV: {
+      // the source is always read; a false condition still zero-extends a 32-bit destination
+      const bool t = cond(fl, u.sub);
+      res = t ? b : a;
+      wa = t || asz == 4;
+      break;
+    }
+    case O_SETCC: res = cond(fl, u.sub) ? 1 : 0; break;
+    case O_BSWAP: res = asz == 8 ? __builtin_bswap64(a) : asz == 4 ? (u64)__builtin_bswap32((u32)a) : 0; break;
+    case O_CBW:
+      ra = asz == 2 ? sext(R(L, 0), 1) : asz == 4 ? sext(R(L, 0), 2) : sext(R(L, 0), 4);
+      wrax = true;
+      break;
+    case O_CWD:
+      rd = msb(R(L, 0), asz) ? ~0ull : 0;
+      wrdx = true;
+      break;
+    case O_LAHF:
+      ra = (R(L, 0) & ~0xff00ull) | (((fl & 0xd5) | 2) << 8);
+      wrax = true;
+      raxsz = 8;
+      break;
+    case O_SAHF:
+      fl = (fl & ~(F_SF | F_ZF | F_AF | F_PF | F_CF)) | ((R(L, 0) >> 8) & (F_SF | F_ZF | F_AF | F_PF | F_CF));
+      break;
+    case O_FLAGOP:
+      if (u.sub == 0xf5) fl ^= F_CF;
+      else if (u.sub == 0xf8) fl &= ~F_CF;
+      else if (u.sub == 0xf9) fl |= F_CF;
+      else if (u.sub == 0xfc) fl &= ~F_DF;
+      else fl |= F_DF;
+      break;
+    case O_NOP: break;
+    case O_JCC:
+      if (cond(fl, u.sub)) next = nrip + b;
+      break;
+    case O_JMP: next = u.bsrc == L_IMM ? nrip + b : b; break;
+    case O_CALL:
+      res = nrip;
+      next = u.bsrc == L_IMM ? nrip + b : b;
+      drsp = -8;
+      break;
+    case O_RET:
+      next = b;
+      drsp = 8 + (i64)u.imm;
+      break;
+    case O_PUSH:
+      res = b;
+      drsp = -(i64)asz;
+      break;
+    case O_PUSHF:
+      res = fl & 0xfcffffull & szmask(asz);
+      drsp = -(i64)asz;
+      break;
+    case O_POP:
+      res = b;
+      drsp = (i64)u.bsz;
+      break;
+    case O_POPF: {
+      u64 mask = F_STATUS | F_TF | F_DF | 0x4000ull | 0x40000ull | 0x200000ull;
+      if (L.cpl == 0) mask |= F_IF | 0x3000ull;
+      if (u.bsz == 2) mask &= 0xffff;
+      fl = ((fl & ~mask) | (b & mask) | 2) & ~0x10000ull;
+      drsp = (i64)u.bsz;
+      break;
+    }
+    case O_LEAVE: break;
+    case O_INT3: return X_INT3;
+    case O_HLT: return X_HLT;
+    case O_UD:
+      set_fault(L, WTFGPU_VEC_UD, 0, 0);
+      return X_FAULT;
+    default: return X_UNIMPL;
+  }
+  // ---- the memory write
+  if (wa && amem) {
+    u64 addr;
+    if (u.asrc == L_RM) {
+      // pop r/m computes its address with rsp already incremented
+      addr = (op == O_POP && u.base == 4 ? ea + u.bsz : ea) + sb;
+    } else if (u.asrc == L_PUSH) {
+      addr = rsp - asz;
+    } else {
+      addr = u.imm + sb;
+    }
+    if (!vwrite(L, addr, asz, res)) return X_FAULT;
+  }
+  // ---- commit
+  if (op == O_LEAVE) {
+    R(L, 4) = R(L, 5) + 8;
+    R(L, 5) = b;
+  }
+  if (drsp) R(L, 4) = rsp + (u64)drsp;
+  if (u.bwrite && !bmem) setr(L, u.rex, loc_reg(u, u.bsrc), u.bsz, resb);  // xchg / xadd source
+  if (wa && !amem) setr(L, u.rex, loc_reg(u, u.asrc), asz, res);  // xadd r,r: DEST := TEMP last (SDM)
+  if (wrax) setr(L, u.rex, 0, raxsz, ra);
+  if (wrdx) setr(L, u.rex, 2, asz, rd);
+  L.rflags = fl;
+  return X_OK;
+}
+
+}  // namespace wtfgpu_dev

@@ -1,0 +1,182 @@
+"""Python handle on the HIP engine (libwtfgpu.so) through its C ABI.
+
+Used by tests and bench.py to drive lanes directly; the C++ GpuBackend_t
+(wtf_amd/host) is the drop-in for wtf's Backend_t. Every call goes to the HIP
+library; a missing library or device raises instead of falling back.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def _chk(rc, what):
+    if rc != 0:
+        raise EngineError(f"{what} failed: {rc}")
+
+
+class Engine:
+    def __init__(self, device: int = 0):
+        self.L = abi.load_hip_library()
+        ctx = C.c_void_p()
+        _chk(self.L.wtfgpu_create(device, C.byref(ctx)), "wtfgpu_create")
+        self.ctx = ctx
+        self.nlanes = 0
+
+    def close(self):
+        if self.ctx:
+            self.L.wtfgpu_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- setup
+    def load_pool(self, pfns, blob: bytes):
+        arr = (C.c_uint64 * max(1, len(pfns)))(*pfns)
+        _chk(self.L.wtfgpu_load_pool(self.ctx, arr, blob, len(pfns)), "load_pool")
+
+    def alloc_lanes(self, n, overlay_pages=16, cov_entries=1024):
+        _chk(self.L.wtfgpu_alloc_lanes(self.ctx, n, overlay_pages, cov_entries), "alloc_lanes")
+        self.nlanes = n
+
+    def set_initial_state(self, regs: abi.Regs):
+        _chk(self.L.wtfgpu_set_initial_state(self.ctx, C.byref(regs)), "set_initial_state")
+
+    def set_limit(self, n):
+        _chk(self.L.wtfgpu_set_limit(self.ctx, n), "set_limit")
+
+    def set_breakpoints(self, gvas):
+        arr = (C.c_uint64 * max(1, len(gvas)))(*gvas)
+        _chk(self.L.wtfgpu_set_breakpoints(self.ctx, arr, len(gvas)), "set_breakpoints")
+
+    def set_code_pages(self, vpns):
+        arr = (C.c_uint64 * max(1, len(vpns)))(*vpns)
+        _chk(self.L.wtfgpu_set_code_pages(self.ctx, arr, len(vpns)), "set_code_pages")
+
+    def restore(self, first=0, count=None):
+        count = self.nlanes - first if count is None else count
+        _chk(self.L.wtfgpu_restore(self.ctx, first, count), "restore")
+
+    # ---- registers
+    def read_gprs(self, first=0, count=None) -> np.ndarray:
+        count = self.nlanes - first if count is None else count
+        out = np.zeros((count, 18), dtype=np.uint64)
+        _chk(self.L.wtfgpu_read_gprs(self.ctx, first, count, out.ctypes.data_as(C.POINTER(C.c_uint64))),
+             "read_gprs")
+        return out
+
+    def write_gprs(self, g: np.ndarray, first=0):
+        g = np.ascontiguousarray(g, dtype=np.uint64)
+        _chk(self.L.wtfgpu_write_gprs(self.ctx, first, g.shape[0], g.ctypes.data_as(C.POINTER(C.c_uint64))),
+             "write_gprs")
+
+    def read_regs(self, first=0, count=1):
+        arr = (abi.Regs * count)()
+        _chk(self.L.wtfgpu_read_regs(self.ctx, first, count, arr), "read_regs")
+        return list(arr)
+
+    def write_regs(self, regs, first=0):
+        arr = (abi.Regs * len(regs))(*regs)
+        _chk(self.L.wtfgpu_write_regs(self.ctx, first, len(regs), arr), "write_regs")
+
+    # ---- run
+    def run(self, first=0, count=None, max_steps=1 << 40) -> abi.RunStats:
+        count = self.nlanes - first if count is None else count
+        st = abi.RunStats()
+        _chk(self.L.wtfgpu_run(self.ctx, first, count, max_steps, C.byref(st)), "run")
+        return st
+
+    def exits(self, first=0, count=None):
+        count = self.nlanes - first if count is None else count
+        arr = (abi.Exit * count)()
+        _chk(self.L.wtfgpu_read_exits(self.ctx, first, count, arr), "read_exits")
+        return list(arr)
+
+    def resume(self, lanes, skip):
+        n = len(lanes)
+        la = (C.c_uint32 * max(1, n))(*lanes)
+        sk = (C.c_uint8 * max(1, n))(*[1 if s else 0 for s in skip])
+        _chk(self.L.wtfgpu_resume(self.ctx, la, n, sk), "resume")
+
+    def stop(self, lanes, status=abi.EXIT_STOPPED):
+        n = len(lanes)
+        la = (C.c_uint32 * max(1, n))(*lanes)
+        _chk(self.L.wtfgpu_stop(self.ctx, la, n, status), "stop")
+
+    # ---- memory
+    def apply_writes(self, writes):
+        """writes: list of (lane, gva, bytes)."""
+        if not writes:
+            return
+        recs = (abi.Write * len(writes))()
+        blob = bytearray()
+        for i, (lane, gva, data) in enumerate(writes):
+            recs[i].lane, recs[i].len, recs[i].gva, recs[i].data_off = lane, len(data), gva, len(blob)
+            blob += data
+        st = (C.c_int32 * len(writes))()
+        _chk(self.L.wtfgpu_apply_writes(self.ctx, recs, len(writes), bytes(blob), len(blob), st), "apply_writes")
+
+    def read_virt(self, lane, gva, n) -> bytes:
+        b = C.create_string_buffer(n)
+        _chk(self.L.wtfgpu_lane_read_virt(self.ctx, lane, gva, b, n), "read_virt")
+        return b.raw
+
+    def write_virt(self, lane, gva, data: bytes):
+        _chk(self.L.wtfgpu_lane_write_virt(self.ctx, lane, gva, data, len(data)), "write_virt")
+
+    def read_phys(self, lane, gpa, n) -> bytes:
+        b = C.create_string_buffer(n)
+        _chk(self.L.wtfgpu_lane_read_phys(self.ctx, lane, gpa, b, n), "read_phys")
+        return b.raw
+
+    def translate(self, lane, gva):
+        out = C.c_uint64()
+        rc = self.L.wtfgpu_lane_translate(self.ctx, lane, gva, C.byref(out))
+        return None if rc else out.value
+
+    def dirty(self, lane) -> list[int]:
+        n = C.c_uint32()
+        cap = 4096
+        arr = (C.c_uint64 * cap)()
+        _chk(self.L.wtfgpu_read_dirty(self.ctx, lane, arr, cap, C.byref(n)), "read_dirty")
+        return list(arr[: min(n.value, cap)])
+
+    def coverage(self, first=0, count=None, cap=1 << 22):
+        """{lane: set(rips)} of rips absent from the coverage map when executed."""
+        count = self.nlanes - first if count is None else count
+        lanes = np.zeros(cap, dtype=np.uint32)
+        rips = np.zeros(cap, dtype=np.uint64)
+        n = C.c_uint64()
+        ovf = C.c_uint32()
+        _chk(self.L.wtfgpu_read_coverage(self.ctx, first, count, lanes.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                         rips.ctypes.data_as(C.POINTER(C.c_uint64)), cap, C.byref(n),
+                                         C.byref(ovf)), "read_coverage")
+        if n.value > cap:
+            raise EngineError("coverage buffer too small")
+        out: dict[int, set] = {}
+        for ln, rp in zip(lanes[: n.value].tolist(), rips[: n.value].tolist()):
+            out.setdefault(ln, set()).add(rp)
+        return out, bool(ovf.value)
+
+    def commit_coverage(self, rips):
+        arr = np.ascontiguousarray(np.array(sorted(rips), dtype=np.uint64))
+        _chk(self.L.wtfgpu_commit_coverage(self.ctx, arr.ctypes.data_as(C.POINTER(C.c_uint64)), len(arr)),
+             "commit_coverage")
+
+    def nbytes(self, first=0, count=None) -> np.ndarray:
+        count = self.nlanes - first if count is None else count
+        out = np.zeros(count, dtype=np.uint64)
+        _chk(self.L.wtfgpu_read_bytes(self.ctx, first, count, out.ctypes.data_as(C.POINTER(C.c_uint64))),
+             "read_bytes")
+        return out
