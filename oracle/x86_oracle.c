@@ -762,26 +762,27 @@ static int string_op(orc_machine *m, insn *d, u32 op, int sz) {
     u64 rsi = m->r.gpr[WTFGPU_RSI] & amask, rdi = m->r.gpr[WTFGPU_RDI] & amask;
     u64 a = 0, b = 0;
     int stop_rep = 0;
+    const u64 bytes0 = m->bytes; /* a faulting iteration accounts no bytes */
     switch (op) {
     case 0xa4:
-      if (vread(m, srcbase + rsi, (u32)sz, &a)) return -1;
-      if (vwrite(m, rdi, (u32)sz, &a)) return -1;
+      if (vread(m, srcbase + rsi, (u32)sz, &a)) { m->bytes = bytes0; return -1; }
+      if (vwrite(m, rdi, (u32)sz, &a)) { m->bytes = bytes0; return -1; }
       break;
     case 0xa6:
-      if (vread(m, srcbase + rsi, (u32)sz, &a)) return -1;
-      if (vread(m, rdi, (u32)sz, &b)) return -1;
+      if (vread(m, srcbase + rsi, (u32)sz, &a)) { m->bytes = bytes0; return -1; }
+      if (vread(m, rdi, (u32)sz, &b)) { m->bytes = bytes0; return -1; }
       alu2(m, 7, a, b, sz);
       break;
     case 0xaa:
       a = m->r.gpr[WTFGPU_RAX];
-      if (vwrite(m, rdi, (u32)sz, &a)) return -1;
+      if (vwrite(m, rdi, (u32)sz, &a)) { m->bytes = bytes0; return -1; }
       break;
     case 0xac:
-      if (vread(m, srcbase + rsi, (u32)sz, &a)) return -1;
+      if (vread(m, srcbase + rsi, (u32)sz, &a)) { m->bytes = bytes0; return -1; }
       setreg(m, d, WTFGPU_RAX, sz, a);
       break;
     case 0xae:
-      if (vread(m, rdi, (u32)sz, &b)) return -1;
+      if (vread(m, rdi, (u32)sz, &b)) { m->bytes = bytes0; return -1; }
       alu2(m, 7, m->r.gpr[WTFGPU_RAX], b, sz);
       break;
     }

@@ -1,0 +1,139 @@
+// sim_lane.cc — TEST INFRASTRUCTURE ONLY: one lane of the GPU interpreter's
+// per-step logic (engine.hip k_run: code translation, fetch, decode, exec with
+// miss/retry, retire) compiled for the host, for divergence debugging.
+#include <cstdlib>
+#include <vector>
+#include "../../wtf_amd/csrc/engine_ops.h"
+using namespace wtfgpu_dev;
+
+extern "C" {
+struct SimResult {
+  uint64_t gpr[16], rip, rflags, icount, nbytes;
+  uint32_t status, vector, error, ovn;
+  uint64_t addr;
+  uint64_t dirty[64];
+};
+
+int sim_run(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, const wtfgpu_regs_t *r0,
+            uint64_t limit, SimResult *out) {
+  uint64_t maxpfn = 0;
+  for (uint64_t i = 0; i < npages; i++) maxpfn = gpfns[i] > maxpfn ? gpfns[i] : maxpfn;
+  // page pointers carry flags in their low 12 bits: storage must be 4 KiB aligned
+  uint8_t *pool = (uint8_t *)aligned_alloc(4096, (npages + 1) * 4096);
+  memset(pool, 0, 4096);
+  memcpy(pool + 4096, pages, npages * 4096);
+  std::vector<uint32_t> map(maxpfn + 1, 0);
+  for (uint64_t i = 0; i < npages; i++) if (!map[gpfns[i]]) map[gpfns[i]] = (uint32_t)(i + 1);
+  std::vector<uint32_t> ptbits((maxpfn + 32) / 32, 0);
+  const uint32_t K = 64;
+  uint8_t *ov = (uint8_t *)aligned_alloc(4096, K * 4096);
+  std::vector<uint32_t> ovg(K), ovc(1);
+  std::vector<uint64_t> fsb(1, r0->seg[WTFGPU_FS].base), gsb(1, r0->seg[WTFGPU_GS].base);
+  Dev P{};
+  P.pool = pool;
+  P.pfn_map = map.data();
+  P.pfn_map_len = map.size();
+  P.ptbits = ptbits.data();
+  P.nlanes = 1;
+  P.K = K;
+  P.ov_count = ovc.data();
+  P.ov_gpfn = ovg.data();
+  P.ov_data = ov;
+  P.fs_base = fsb.data();
+  P.gs_base = gsb.data();
+  P.limit = limit;
+  uint64_t G[16 * GPR_STRIDE];
+  Lane L{};
+  L.g = G;
+  for (int i = 0; i < 16; i++) R(L, i) = r0->gpr[i];
+  L.rip = r0->rip;
+  L.rflags = r0->rflags;
+  L.cr0 = r0->cr0;
+  L.cr3 = r0->cr3;
+  L.efer = r0->efer;
+  L.cpl = r0->seg[WTFGPU_CS].selector & 3;
+  L.status = WTFGPU_RUNNING;
+  tlb_flush(L);
+  for (uint64_t steps = 0; steps < 100000000 && L.status == WTFGPU_RUNNING; steps++) {
+    const uint64_t grip = L.rip;
+    uint64_t td;
+    if (!tlb_get(L, grip >> 12, td) || !perm_ok(L, td, ACC_X)) {
+      if (service_miss(P, L, grip & ~0xfffull, ACC_X)) tlb_get(L, grip >> 12, td);
+      else td = 0;
+      if (!td && L.status == WTFGPU_EXIT_FAULT) L.exaddr = grip;
+    }
+    if (!td) break;
+    const uint8_t *page = (const uint8_t *)(uintptr_t)(td & ~0xfffull);
+    const uint32_t off = grip & 0xfff;
+    IBytes ib;
+    ib.avail = 4096 - off < 16 ? 4096 - off : 16;
+    uint8_t bytes[16] = {0};
+    memcpy(bytes, page + off, ib.avail);
+    UOp d;
+    memcpy(&ib.lo, bytes, 8);
+    memcpy(&ib.hi, bytes + 8, 8);
+    int dr = decode(ib, d);
+    if (dr == 1) {
+      const uint64_t va2 = (grip & ~0xfffull) + 4096;
+      if (!tlb_get(L, va2 >> 12, td) || !perm_ok(L, td, ACC_X)) {
+        if (service_miss(P, L, va2, ACC_X)) tlb_get(L, va2 >> 12, td);
+        else td = 0;
+      }
+      if (!td) break;
+      memcpy(bytes + ib.avail, (const uint8_t *)(uintptr_t)(td & ~0xfffull), 16 - ib.avail);
+      memcpy(&ib.lo, bytes, 8);
+      memcpy(&ib.hi, bytes + 8, 8);
+      ib.avail = 16;
+      dr = decode(ib, d);
+    }
+    if (dr == 2) {
+      set_fault(L, WTFGPU_VEC_GP, 0, 0);
+      break;
+    }
+    if (!d.supported) {
+      L.status = WTFGPU_EXIT_UNIMPLEMENTED;
+      break;
+    }
+    uint64_t next = 0;
+    int x;
+    for (int attempt = 0;; attempt++) {
+      L.miss = 0;
+      L.pend = 0;
+      x = exec(P, L, d, grip + d.len, next);
+      if (!L.miss || L.status != WTFGPU_RUNNING) break;
+      if (attempt >= 16 || !service_miss(P, L, L.miss_va, (int)L.miss_acc)) break;
+    }
+    if (L.flush) {
+      tlb_flush(L);
+      L.flush = 0;
+    }
+    if (x == X_OK && L.status == WTFGPU_RUNNING) {
+      L.rip = next;
+      L.icount++;
+      L.nbytes += d.len + L.pend;
+      if (P.limit && L.icount > P.limit) L.status = WTFGPU_EXIT_TIMEOUT;
+    } else if (L.status != WTFGPU_RUNNING) {
+    } else if (x == X_UNIMPL) {
+      L.status = WTFGPU_EXIT_UNIMPLEMENTED;
+    } else if (x == X_INT3) {
+      L.status = WTFGPU_EXIT_INT3;
+    } else if (x == X_HLT) {
+      L.status = WTFGPU_EXIT_HLT;
+    }
+  }
+  for (int i = 0; i < 16; i++) out->gpr[i] = R(L, i);
+  out->rip = L.rip;
+  out->rflags = L.rflags;
+  out->icount = L.icount;
+  out->nbytes = L.nbytes;
+  out->status = L.status;
+  out->vector = L.exvec;
+  out->error = L.exerr;
+  out->addr = L.exaddr;
+  out->ovn = L.ovn;
+  for (uint32_t k = 0; k < L.ovn && k < 64; k++) out->dirty[k] = (uint64_t)ovg[k] << 12;
+  free(pool);
+  free(ov);
+  return 0;
+}
+}

@@ -786,6 +786,11 @@ int wtfgpu_load_pool(wtfgpu_ctx *c, const uint64_t *gpfns, const uint8_t *pages,
   for (u64 i = 0; i < npages; i++)
     if (map[gpfns[i]] == 0) map[gpfns[i]] = (u32)(i + 1);  // first occurrence wins (try_emplace)
   if (dalloc(&c->d_pool, (npages + 1) * WTFGPU_PAGE_SIZE)) return WTFGPU_ERR_OOM;
+  // TLB entries pack permission bits into the low 12 bits of page pointers
+  if ((uintptr_t)c->d_pool & 0xfff) {
+    fprintf(stderr, "wtfgpu: page pool not 4 KiB aligned\n");
+    return WTFGPU_ERR_OOM;
+  }
   if (dalloc(&c->d_pfnmap, maplen)) return WTFGPU_ERR_OOM;
   if (dalloc(&c->d_ptbits, (maplen + 31) / 32)) return WTFGPU_ERR_OOM;
   HIPCHK(hipMemsetAsync(c->d_pool, 0, WTFGPU_PAGE_SIZE, c->stream));
@@ -829,6 +834,10 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
   rc |= dalloc(&c->d_exinfo, N);
   rc |= dalloc(&c->d_sys, N);
   rc |= dalloc(&c->d_ovdata, N * overlay_pages * WTFGPU_PAGE_SIZE);
+  if (!rc && ((uintptr_t)c->d_ovdata & 0xfff)) {
+    fprintf(stderr, "wtfgpu: overlay pages not 4 KiB aligned\n");
+    return WTFGPU_ERR_OOM;
+  }
   rc |= dalloc(&c->d_full, N);
   if (cov_entries) {
     rc |= dalloc(&c->d_covrip, nw * cov_entries);

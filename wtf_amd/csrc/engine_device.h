@@ -15,7 +15,11 @@
 // (src/wtf/bochscpu_backend.cc:445-728) and the conventions U1-U13 written in
 // DESIGN.md §5. This header is included by engine.hip only.
 #pragma once
+#ifndef WTFGPU_HOST_SIM
 #include <hip/hip_runtime.h>
+#else
+#include "../../tests/native/host_sim_shim.h"  // test-only CPU build of the device code
+#endif
 #include <stdint.h>
 #include "../../include/wtfgpu.h"
 
