@@ -339,12 +339,14 @@ struct InitState {
   LaneSys sys;
 };
 
-__global__ void k_restore(Dev P, const InitState *S, u32 first, u32 count) {
+__global__ void k_restore(Dev P, const InitState *S, const wtfgpu_regs_t *full0, wtfgpu_regs_t *full, u32 first,
+                          u32 count) {
   const u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
   const u32 lane = first + tid;
   if (tid >= count || lane >= P.nlanes) return;
   const u64 N = P.nlanes;
   const InitState s = *S;
+  full[lane] = *full0;  // cold architectural state (read/write_regs only)
 #pragma unroll
   for (int i = 0; i < 16; i++) P.gpr[i * N + lane] = s.g[i];
   P.rip[lane] = s.rip;
@@ -612,6 +614,7 @@ struct wtfgpu_ctx {
   // misc
   u64 *d_stat = nullptr;
   InitState *d_init = nullptr;
+  wtfgpu_regs_t *d_init_full = nullptr;  // initial architectural state, copied per lane by k_restore
   wtfgpu_regs_t initial{};
   bool have_initial = false;
   u8 *d_scratch = nullptr;
@@ -717,7 +720,7 @@ int wtfgpu_create(int device, wtfgpu_ctx **out) {
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIPCHK(hipEventCreate(&c->ev0));
   HIPCHK(hipEventCreate(&c->ev1));
-  if (dalloc(&c->d_stat, 4) || dalloc(&c->d_init, 1)) return WTFGPU_ERR_OOM;
+  if (dalloc(&c->d_stat, 4) || dalloc(&c->d_init, 1) || dalloc(&c->d_init_full, 1)) return WTFGPU_ERR_OOM;
   *out = c;
   return WTFGPU_OK;
 }
@@ -761,6 +764,7 @@ int wtfgpu_destroy(wtfgpu_ctx *c) {
   dfree(c->d_covmap);
   dfree(c->d_stat);
   dfree(c->d_init);
+  dfree(c->d_init_full);
   dfree(c->d_scratch);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -933,6 +937,7 @@ int wtfgpu_set_initial_state(wtfgpu_ctx *c, const wtfgpu_regs_t *regs) {
   c->have_initial = true;
   const InitState s = make_init(*regs);
   HIPCHK(hipMemcpyAsync(c->d_init, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_init_full, regs, sizeof(*regs), hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return mark_pt_pages(c);
 }
@@ -1004,12 +1009,8 @@ int wtfgpu_restore(wtfgpu_ctx *c, uint32_t first, uint32_t count) {
   if (!lanes_ok(c, first, count) || !c->have_initial) return WTFGPU_ERR_STATE;
   if (count == 0) return WTFGPU_OK;
   HIPCHK(hipSetDevice(c->device));
-  k_restore<<<(count + 255) / 256, 256, 0, c->stream>>>(c->P, c->d_init, first, count);
+  k_restore<<<(count + 255) / 256, 256, 0, c->stream>>>(c->P, c->d_init, c->d_init_full, c->d_full, first, count);
   HIPCHK(hipGetLastError());
-  // cold architectural state
-  std::vector<wtfgpu_regs_t> full(count, c->initial);
-  HIPCHK(hipMemcpyAsync(c->d_full + first, full.data(), (u64)count * sizeof(wtfgpu_regs_t), hipMemcpyHostToDevice,
-                        c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return WTFGPU_OK;
 }

@@ -103,6 +103,18 @@ class Engine:
         _chk(self.L.wtfgpu_read_exits(self.ctx, first, count, arr), "read_exits")
         return list(arr)
 
+    EXIT_DTYPE = np.dtype([("status", "<u4"), ("vector", "<u4"), ("error", "<u4"), ("opcode", "<u4"),
+                           ("addr", "<u8"), ("rip", "<u8"), ("icount", "<u8")])
+
+    def exits_np(self, first=0, count=None) -> np.ndarray:
+        """read_exits as a numpy structured array (one record per lane)."""
+        count = self.nlanes - first if count is None else count
+        out = np.zeros(count, dtype=self.EXIT_DTYPE)
+        assert out.itemsize == C.sizeof(abi.Exit)
+        _chk(self.L.wtfgpu_read_exits(self.ctx, first, count, out.ctypes.data_as(C.POINTER(abi.Exit))),
+             "read_exits")
+        return out
+
     def resume(self, lanes, skip):
         n = len(lanes)
         la = (C.c_uint32 * max(1, n))(*lanes)
