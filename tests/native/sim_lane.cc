@@ -42,10 +42,11 @@ int sim_run(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, const 
   P.fs_base = fsb.data();
   P.gs_base = gsb.data();
   P.limit = limit;
-  uint64_t G[16 * GPR_STRIDE];
+  uint32_t glo[16], ghi[16];
   Lane L{};
-  L.g = G;
-  for (int i = 0; i < 16; i++) R(L, i) = r0->gpr[i];
+  L.glo = glo;
+  L.ghi = ghi;
+  for (int i = 0; i < 16; i++) RS(L, i, r0->gpr[i]);
   L.rip = r0->rip;
   L.rflags = r0->rflags;
   L.cr0 = r0->cr0;

@@ -102,5 +102,8 @@ def test_gpu_matches_native_vectors():
             win[k] = v
         if eng.read_virt(i, buf_va, 256) != bytes(win):
             memfails.append((c["name"], c["code"]))
+    if fails:
+        import collections
+        print("failing classes:", collections.Counter(f[0] for f in fails).most_common())
     assert not fails, f"{len(fails)}/{len(cases)} register mismatches, first: {fails[:6]}"
     assert not memfails, f"{len(memfails)} memory mismatches, first: {memfails[:6]}"

@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "csrc", "libwtfgpu.so")
+LIB_PATH = os.environ.get("WTFGPU_LIB") or os.path.join(HERE, "csrc", "libwtfgpu.so")
 HOST_LIB_PATH = os.path.join(HERE, "host", "libwtf_host.so")
 
 RUNNING, EXIT_BREAKPOINT, EXIT_TIMEOUT, EXIT_INT3, EXIT_HLT, EXIT_FAULT, EXIT_UNIMPLEMENTED, \

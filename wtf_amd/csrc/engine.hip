@@ -14,7 +14,7 @@
 #include <new>
 #include <vector>
 
-#include "engine_ops.h"
+#include "engine_fast.h"
 
 using namespace wtfgpu_dev;
 
@@ -57,7 +57,7 @@ __device__ __forceinline__ bool hash_find(const u64 *keys, u32 mask, u64 key, u3
 __device__ __forceinline__ void load_lane(const Dev &P, u32 lane, Lane &L) {
   const u64 N = P.nlanes;
 #pragma unroll
-  for (int i = 0; i < 16; i++) R(L, i) = P.gpr[i * N + lane];
+  for (int i = 0; i < 16; i++) RS(L, i, P.gpr[i * N + lane]);
   L.rip = P.rip[lane];
   L.rflags = P.rflags[lane];
   L.icount = P.icount[lane];
@@ -95,17 +95,14 @@ __device__ __forceinline__ void store_lane(const Dev &P, const Lane &L) {
 
 // Coverage (bochscpu_backend.cc:501-504): every executed rip absent from the
 // aggregate map is logged once per wave with the mask of lanes that ran it.
-__device__ __forceinline__ void cover(const Dev &P, u64 rip, u64 gmask, u32 wv, u32 lid, u64 &cvpn, int &cslot,
-                                      u32 ep) {
-  const u64 vpn = rip >> 12;
-  if (vpn != cvpn) {
-    cvpn = vpn;
+// Uniform; only reached for rips the uop cache does not already know are covered.
+__device__ __noinline__ void cover(const Dev &P, u64 rip, u64 gmask, u32 wv, u32 lid, u32 ep) {
+  if (P.code_keys) {
     u32 s;
-    cslot = (P.code_keys && hash_find(P.code_keys, P.code_mask, vpn, s)) ? (int)rfl32(P.code_slot[s]) : -1;
-  }
-  if (cslot >= 0) {
-    const u32 byte = rfl32(P.cov_map[(u64)cslot * WTFGPU_PAGE_SIZE + (rip & 0xfff)]);
-    if (byte) return;
+    if (hash_find(P.code_keys, P.code_mask, rip >> 12, s)) {
+      const u32 cs = rfl32(P.code_slot[s]);
+      if (rfl32(P.cov_map[(u64)cs * WTFGPU_PAGE_SIZE + (rip & 0xfff)])) return;
+    }
   }
   const u32 H = P.H;
   const u64 base = (u64)wv * H;
@@ -157,6 +154,239 @@ __device__ __forceinline__ void fetch_bytes(u64 pageptr, u32 off, u32 n, u64 &lo
   }
 }
 
+// ---------------------------------------------------------------- decoded-uop cache
+// Per wave, in LDS, for the lifetime of one k_run launch. Key = page pointer |
+// offset of the instruction's first byte; only pages of the read-only snapshot
+// pool are cached (a lane's overlay copy can be rewritten by the guest). An
+// entry holds the decoded UOp (generic path), its FOp digest (fast path), the
+// breakpoint lookup (the set is fixed during a launch), whether the rip is
+// already in the aggregate coverage map, and the lanes this wave has already
+// logged for it in this launch.
+constexpr u32 UC_N = 64;  // entries per wave (power of two)
+constexpr u32 UC_BP = 1, UC_COVERED = 2, UC_CROSS = 4, UC_BADLEN = 8, UC_UNSUP = 16;
+struct UCEntry {
+  u64 key;
+  u64 logged;
+  u32 flags, pad;
+  FOp f;
+  UOp u;
+};
+static_assert(sizeof(UOp) % 4 == 0 && sizeof(FOp) % 4 == 0, "copied as dwords");
+
+__device__ __forceinline__ u32 uc_slot(u64 key) { return (u32)((key ^ (key >> 12) * 0x9E3779B1u) & (UC_N - 1)); }
+
+template <typename T>
+__device__ __forceinline__ void lds_uniform_read(const T *src, T &dst) {
+  const u32 *s = (const u32 *)src;
+  u32 *d = (u32 *)&dst;
+#pragma unroll
+  for (u32 i = 0; i < sizeof(T) / 4; i++) d[i] = rfl32(s[i]);
+}
+
+__device__ __forceinline__ bool bp_lookup(const Dev &P, u64 rip) {
+  u32 s;
+  return P.bp_keys && hash_find(P.bp_keys, P.bp_mask, rip, s);
+}
+
+// Fill one entry (uniform): fetch + decode from the pool page, digest, lookups.
+__device__ __noinline__ void uc_fill(const Dev &P, UCEntry *e, u64 key, u64 lptr, u32 off, u64 rip, u32 lid) {
+  IBytes ib;
+  ib.avail = 4096 - off < 16 ? 4096 - off : 16;
+  fetch_bytes(lptr, off, ib.avail, ib.lo, ib.hi);
+  UOp d;
+  const int dr = decode(ib, d);
+  u32 flags = dr == 1 ? UC_CROSS : dr == 2 ? UC_BADLEN : 0;
+  FOp f;
+  if (dr == 0) {
+    digest(d, f);
+    if (!d.supported) flags |= UC_UNSUP;
+    if (bp_lookup(P, rip)) flags |= UC_BP;
+    if (P.code_keys) {
+      u32 s;
+      if (hash_find(P.code_keys, P.code_mask, rip >> 12, s)) {
+        const u32 cs = rfl32(P.code_slot[s]);
+        if (rfl32(P.cov_map[(u64)cs * WTFGPU_PAGE_SIZE + off])) flags |= UC_COVERED;
+      }
+    }
+  } else {
+    f = FOp{};
+  }
+  if (lid == 0) {
+    e->logged = 0;
+    e->flags = flags;
+    e->f = f;
+    e->u = d;
+    e->key = key;
+  }
+}
+
+// Instruction-page translation for lanes whose code-page cache missed.
+__device__ __noinline__ void code_xlate(const Dev &P, Lane &L, u64 rip) {
+  u64 td;
+  const u64 vpn = rip >> 12;
+  if (!tlb_get(L, vpn, td) || !perm_ok(L, td, ACC_X)) {
+    if (service_miss(P, L, rip & ~0xfffull, ACC_X)) tlb_get(L, vpn, td);
+    else td = 0;
+    if (td && !perm_ok(L, td, ACC_X)) td = 0;
+    if (!td && L.status == WTFGPU_EXIT_FAULT) L.exaddr = rip;
+  }
+  if (td) {
+    L.cvpn = vpn;
+    L.cptr = td & ~0xfffull;
+  }
+}
+
+__device__ __noinline__ bool miss_service(const Dev &P, Lane &L, int attempt) {
+  if (attempt >= 16 || !service_miss(P, L, L.miss_va, (int)L.miss_acc)) {
+    if (attempt >= 16) set_fault(L, WTFGPU_VEC_GP, 0xffff, L.miss_va);
+    return false;
+  }
+  return true;
+}
+
+__device__ __noinline__ int exec_generic(const Dev &P, Lane &L, const UOp *ul, u64 &next) {
+  UOp d;
+  lds_uniform_read(ul, d);
+  return exec(P, L, d, L.rip + d.len, next);
+}
+
+// Retire / exit bookkeeping after the last attempt at an instruction.
+__device__ __forceinline__ void retire(const Dev &P, Lane &L, int x, u32 len, u64 next, u32 opbytes) {
+  if (L.flush) {
+    tlb_flush(L);
+    L.flush = 0;
+  }
+  if (x == X_OK && L.status == WTFGPU_RUNNING) {
+    L.rip = next;
+    L.icount++;
+    L.nbytes += len + L.pend;
+    if (P.limit && L.icount > P.limit) L.status = WTFGPU_EXIT_TIMEOUT;
+  } else if (L.status != WTFGPU_RUNNING) {
+    // faulted / overlay full inside exec or service_miss; rip unchanged
+  } else if (x == X_UNIMPL) {
+    L.status = WTFGPU_EXIT_UNIMPLEMENTED;
+    L.exop = len >= 4 ? opbytes : (opbytes & ((1u << (8 * len)) - 1));
+  } else if (x == X_INT3) {
+    L.status = WTFGPU_EXIT_INT3;
+  } else if (x == X_HLT) {
+    L.status = WTFGPU_EXIT_HLT;
+  }
+}
+
+// A step the uop cache cannot serve: code on a lane overlay page, or an
+// instruction that crosses into the next page (translated per lane).
+__device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr, bool ing, bool &skip, u32 wv,
+                                       u32 lid, u32 ep) {
+  const u32 off = (u32)(grip & 0xfff);
+  IBytes ib;
+  ib.avail = 4096 - off < 16 ? 4096 - off : 16;
+  fetch_bytes(lptr, off, ib.avail, ib.lo, ib.hi);
+  UOp d;
+  int dr = decode(ib, d);
+  if (dr == 1) {
+    u64 nptr = 0;
+    if (ing) {
+      const u64 va2 = (grip & ~0xfffull) + 4096;
+      u64 td;
+      if (!tlb_get(L, va2 >> 12, td) || !perm_ok(L, td, ACC_X)) {
+        if (service_miss(P, L, va2, ACC_X)) tlb_get(L, va2 >> 12, td);
+        else td = 0;
+      }
+      if (td) nptr = td & ~0xfffull;
+      else ing = false;
+    }
+    const u64 cm = __ballot(ing);
+    if (cm == 0) return;
+    const int leader = __ffsll((long long)cm) - 1;
+    const u64 lnptr = readlane64(nptr, leader);
+    ing = ing && nptr == lnptr;
+    const u32 n0 = ib.avail;
+    u64 lo2, hi2;
+    fetch_bytes(lnptr, 0, 16 - n0, lo2, hi2);
+    // splice: bytes [0,n0) from page 1, [n0,16) from page 2
+    if (n0 >= 8) {
+      ib.hi = (n0 == 8 ? 0 : ib.hi) | (n0 == 8 ? lo2 : (lo2 << (8 * (n0 - 8))));
+    } else {
+      ib.lo = ib.lo | (lo2 << (8 * n0));
+      ib.hi = (lo2 >> (64 - 8 * n0)) | (hi2 << (8 * n0));
+    }
+    ib.avail = 16;
+    dr = decode(ib, d);
+  }
+  if (dr == 2) {
+    if (ing) set_fault(L, WTFGPU_VEC_GP, 0, 0);
+    return;
+  }
+  const u64 gmask = __ballot(ing);
+  if (gmask == 0) return;
+  if (P.cov_rip) cover(P, grip, gmask, wv, lid, ep);
+  const bool isbp = bp_lookup(P, grip);
+  if (ing) {
+    if (isbp && !skip) {
+      L.status = WTFGPU_EXIT_BREAKPOINT;
+      ing = false;
+    }
+    skip = false;
+  }
+  if (!d.supported) {
+    if (ing) {
+      L.status = WTFGPU_EXIT_UNIMPLEMENTED;
+      L.exop = d.len >= 4 ? d.opbytes : (d.opbytes & ((1u << (8 * d.len)) - 1));
+    }
+    return;
+  }
+  if (ing) {
+    u64 next = 0;
+    int x;
+    for (int attempt = 0;; attempt++) {
+      L.miss = 0;
+      L.pend = 0;
+      x = exec(P, L, d, grip + d.len, next);
+      if (!L.miss || L.status != WTFGPU_RUNNING) break;
+      if (!miss_service(P, L, attempt)) break;
+    }
+    retire(P, L, x, d.len, next, d.opbytes);
+  }
+}
+
+// Runs `call` on a copy T of lane L whose registers live in arrays of their
+// own, so the kernel's register arrays never escape into a called function
+// (they stay in VGPRs); the copy goes through scratch, which only rare paths pay.
+#define WITH_LANE_COPY(call)                      \
+  do {                                            \
+    u32 tlo_[16], thi_[16];                       \
+    _Pragma("unroll") for (int i_ = 0; i_ < 16; i_++) { \
+      tlo_[i_] = glo[i_];                         \
+      thi_[i_] = ghi[i_];                         \
+    }                                             \
+    Lane T = L;                                   \
+    T.glo = tlo_;                                 \
+    T.ghi = thi_;                                 \
+    call;                                         \
+    L = T;                                        \
+    L.glo = glo;                                  \
+    L.ghi = ghi;                                  \
+    _Pragma("unroll") for (int i_ = 0; i_ < 16; i_++) { \
+      glo[i_] = tlo_[i_];                         \
+      ghi[i_] = thi_[i_];                         \
+    }                                             \
+  } while (0)
+
+// Diagnostic build only (-DWTFGPU_STAMPS, `make stamps`): per-phase s_memtime
+// cycle totals of the step loop, summed into stat[4..11] (never in the product).
+#ifdef WTFGPU_STAMPS
+#define STAMP(k)                                   \
+  do {                                             \
+    const u64 t_ = __builtin_amdgcn_s_memtime();   \
+    stamp_[k] += t_ - tprev_;                      \
+    tprev_ = t_;                                   \
+  } while (0)
+#else
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#endif
+
 // ---------------------------------------------------------------- main kernel
 __global__ __launch_bounds__(256) void k_run(Dev P, u32 first, u32 count, u64 max_steps) {
   const u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -164,9 +394,13 @@ __global__ __launch_bounds__(256) void k_run(Dev P, u32 first, u32 count, u64 ma
   const bool valid = tid < count && lane < P.nlanes;
   const u32 lid = threadIdx.x & 63;
   const u32 wv = lane >> 6;  // first is 64-aligned: hardware wave == log wave
-  __shared__ u64 sG[16 * GPR_STRIDE];
+  __shared__ UCEntry sUC[4][UC_N];
+  UCEntry *uc = sUC[threadIdx.x >> 6];
+  for (u32 i = lid; i < UC_N; i += 64) uc[i].key = EMPTY_KEY;
+  u32 glo[16], ghi[16];
   Lane L;
-  L.g = &sG[threadIdx.x];
+  L.glo = glo;
+  L.ghi = ghi;
   if (valid) {
     load_lane(P, lane, L);
   } else {
@@ -174,152 +408,156 @@ __global__ __launch_bounds__(256) void k_run(Dev P, u32 first, u32 count, u64 ma
     L.lane = 0;
     L.rip = 0;
     L.icount = 0;
+    L.cvpn = EMPTY_KEY;
   }
   const u64 icount0 = L.icount;
   bool skip = valid && (P.lflags[lane] & 1);
   const u32 ep = (P.cov_rip && wv < (P.nlanes + 63) / 64) ? rfl32(P.cov_wave_ep[rfl32(wv)]) : 0;
-  u64 cvpn = EMPTY_KEY;
-  int cslot = -1;
+  const u64 pool_lo = (u64)(uintptr_t)P.pool, pool_hi = pool_lo + (P.npool + 1) * WTFGPU_PAGE_SIZE;
   u64 steps = 0;
+#ifdef WTFGPU_STAMPS
+  u64 stamp_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  u64 tprev_ = __builtin_amdgcn_s_memtime();
+#endif
 
-  while (steps < max_steps) {
-    const bool active = valid && L.status == WTFGPU_RUNNING;
-    const u64 grip = rfl64(wave_min(active ? L.rip : EMPTY_KEY));
-    if (grip == EMPTY_KEY) break;
-    steps++;
-    bool cand = active && L.rip == grip;
-    u64 cptr = 0;
-    if (cand) {
-      u64 td;
-      if (!tlb_get(L, grip >> 12, td) || !perm_ok(L, td, ACC_X)) {
-        if (service_miss(P, L, grip & ~0xfffull, ACC_X)) tlb_get(L, grip >> 12, td);
-        else td = 0;
-        if (td && !perm_ok(L, td, ACC_X)) td = 0;
-        if (!td && L.status == WTFGPU_EXIT_FAULT) L.exaddr = grip;
-      }
-      if (td) cptr = td & ~0xfffull;
-      else cand = false;
-    }
-    u64 cm = __ballot(cand);
-    if (cm == 0) continue;
-    int leader = __ffsll((long long)cm) - 1;
-    const u64 lptr = readlane64(cptr, leader);
-    bool ing = cand && cptr == lptr;
-
-    // ---- fetch + decode, once per group (uniform)
-    const u32 off = (u32)(grip & 0xfff);
-    IBytes ib;
-    ib.avail = 4096 - off < 16 ? 4096 - off : 16;
-    fetch_bytes(lptr, off, ib.avail, ib.lo, ib.hi);
-    UOp d;
-    int dr = decode(ib, d);
-    if (dr == 1) {
-      // the instruction continues on the next page: translate it per lane
-      u64 nptr = 0;
+  for (;;) {
+    // ================= fast loop: the common step, no calls. Leaves with
+    // `have` set and `grip` = the group it could not serve.
+    u64 grip = 0;
+    bool have = false;
+    for (;;) {
+      if (steps >= max_steps) break;
+      const bool active = valid && L.status == WTFGPU_RUNNING;
+      const u64 am = __ballot(active);
+      if (am == 0) break;
+      // group = lanes at the min rip; when the wave is converged (the common
+      // case) the first active lane's rip is that min and the reduction is skipped
+      grip = readlane64(L.rip, __ffsll((long long)am) - 1);
+      if (__ballot(active && L.rip == grip) != am) grip = rfl64(wave_min(active ? L.rip : EMPTY_KEY));
+      have = true;
+      const bool cand = active && L.rip == grip;
+      if (__ballot(cand && (grip >> 12) != L.cvpn)) break;
+      const int leader = __ffsll((long long)__ballot(cand)) - 1;
+      const u64 lptr = readlane64(L.cptr, leader);
+      if (lptr < pool_lo || lptr >= pool_hi) break;
+      const bool ing = cand && L.cptr == lptr;
+      const u64 key = lptr | (grip & 0xfff);
+      UCEntry *e = &uc[uc_slot(key)];
+      if (rfl64(e->key) != key) break;
+      const u32 flags = rfl32(e->flags);
+      if (flags & (UC_BP | UC_CROSS | UC_BADLEN | UC_UNSUP)) break;
+      if (P.cov_rip && !(flags & UC_COVERED) && (__ballot(ing) & ~rfl64(e->logged))) break;
+      FOp f;
+      lds_uniform_read(&e->f, f);
+      if (f.kind == FK_GENERIC) break;
+      steps++;
+      have = false;
       if (ing) {
-        const u64 va2 = (grip & ~0xfffull) + 4096;
-        u64 td;
-        if (!tlb_get(L, va2 >> 12, td) || !perm_ok(L, td, ACC_X)) {
-          if (service_miss(P, L, va2, ACC_X)) tlb_get(L, va2 >> 12, td);
-          else td = 0;
-        }
-        if (td) nptr = td & ~0xfffull;
-        else ing = false;
+        skip = false;
+        L.miss = 0;
+        L.pend = 0;
+        u64 next;
+        const int x = fast_exec(L, f, grip + f.len, next);
+        if (!L.miss) retire(P, L, x, f.len, next, 0);
       }
-      cm = __ballot(ing);
-      if (cm == 0) continue;
-      leader = __ffsll((long long)cm) - 1;
-      const u64 lnptr = readlane64(nptr, leader);
-      ing = ing && nptr == lnptr;
-      const u32 n0 = ib.avail;
-      u64 lo2, hi2;
-      fetch_bytes(lnptr, 0, 16 - n0, lo2, hi2);
-      // splice: bytes [0,n0) from page 1, [n0,16) from page 2
-      if (n0 >= 8) {
-        ib.hi = (n0 == 8 ? 0 : ib.hi) | (n0 == 8 ? lo2 : (lo2 << (8 * (n0 - 8))));
-      } else {
-        ib.lo = ib.lo | (lo2 << (8 * n0));
-        ib.hi = (lo2 >> (64 - 8 * n0)) | (hi2 << (8 * n0));
+      // lanes that missed keep their rip: the slow step services them
+      if (__ballot(ing && L.miss)) {
+        have = true;
+        break;
       }
-      ib.avail = 16;
-      dr = decode(ib, d);
     }
-    const u64 gmask = __ballot(ing);
-    if (dr == 2) {
-      if (ing) set_fault(L, WTFGPU_VEC_GP, 0, 0);
+    STAMP(0);
+    if (!have) break;
+
+    // ================= slow step for group `grip`: translation misses, cache
+    // fills, page-crossing / overlay code, coverage logging, breakpoints,
+    // generic instructions, TLB misses and copy-on-write
+    steps++;
+    const bool active = valid && L.status == WTFGPU_RUNNING;
+    bool cand = active && L.rip == grip;
+    if (cand && (grip >> 12) != L.cvpn) WITH_LANE_COPY(code_xlate(P, T, grip));
+    cand = cand && (grip >> 12) == L.cvpn;
+    const u64 cm = __ballot(cand);
+    if (cm == 0) continue;
+    const int leader = __ffsll((long long)cm) - 1;
+    const u64 lptr = readlane64(L.cptr, leader);
+    bool ing = cand && L.cptr == lptr;
+
+    const u32 off = (u32)(grip & 0xfff);
+    const u64 key = lptr | off;
+    UCEntry *e = &uc[uc_slot(key)];
+    const bool cacheable = lptr >= pool_lo && lptr < pool_hi;
+    if (cacheable && rfl64(e->key) != key) uc_fill(P, e, key, lptr, off, grip, lid);
+    const u32 flags = cacheable ? rfl32(e->flags) : UC_CROSS;
+    if (flags & (UC_CROSS | UC_BADLEN)) {
+      if (flags & UC_BADLEN) {
+        if (ing) set_fault(L, WTFGPU_VEC_GP, 0, 0);
+      } else {
+        WITH_LANE_COPY(slow_step(P, T, grip, lptr, ing, skip, wv, lid, ep));
+      }
+      STAMP(1);
       continue;
     }
-    if (gmask == 0) continue;
+    FOp f;
+    lds_uniform_read(&e->f, f);
+    const u64 gmask = __ballot(ing);
 
     // ---- coverage, then breakpoint (bochscpu_backend.cc:501-547)
-    if (P.cov_rip) cover(P, grip, gmask, wv, lid, cvpn, cslot, ep);
-    bool isbp = false;
-    if (P.bp_keys) {
-      u32 s;
-      isbp = hash_find(P.bp_keys, P.bp_mask, grip, s);
+    if (P.cov_rip && !(flags & UC_COVERED)) {
+      const u64 logged = rfl64(e->logged);
+      if (gmask & ~logged) {
+        cover(P, grip, gmask, wv, lid, ep);
+        if (lid == 0) e->logged = logged | gmask;
+      }
     }
     if (ing) {
-      if (isbp && !skip) {
+      if ((flags & UC_BP) && !skip) {
         L.status = WTFGPU_EXIT_BREAKPOINT;
         ing = false;
       }
       skip = false;
     }
-    if (!d.supported) {
-      if (ing) {
-        L.status = WTFGPU_EXIT_UNIMPLEMENTED;
-        L.exop = d.len >= 4 ? d.opbytes : (d.opbytes & ((1u << (8 * d.len)) - 1));
-      }
-      continue;
+    if (ing && (flags & UC_UNSUP)) {
+      const u32 ob = e->u.opbytes, n = f.len;
+      L.status = WTFGPU_EXIT_UNIMPLEMENTED;
+      L.exop = n >= 4 ? ob : (ob & ((1u << (8 * n)) - 1));
+      ing = false;
     }
     if (ing) {
+      // restartable attempts: a TLB miss / first write abandons the attempt,
+      // miss_service fills the TLB or copies the page, the attempt reruns
       u64 next = 0;
       int x;
-      // restartable execution: a TLB miss / first write abandons the attempt,
-      // service_miss fills the TLB (or copies the page), the attempt reruns
       for (int attempt = 0;; attempt++) {
         L.miss = 0;
         L.pend = 0;
-        x = exec(P, L, d, grip + d.len, next);
-        if (!L.miss || L.status != WTFGPU_RUNNING) break;
-        if (attempt >= 16 || !service_miss(P, L, L.miss_va, (int)L.miss_acc)) {
-          if (attempt >= 16) set_fault(L, WTFGPU_VEC_GP, 0xffff, L.miss_va);
-          break;
+        if (f.kind != FK_GENERIC) {
+          x = fast_exec(L, f, grip + f.len, next);
+        } else {
+          WITH_LANE_COPY(x = exec_generic(P, T, &e->u, next));
         }
+        if (!L.miss || L.status != WTFGPU_RUNNING) break;
+        bool ok;
+        WITH_LANE_COPY(ok = miss_service(P, T, attempt));
+        if (!ok) break;
       }
-      if (L.flush) {
-        tlb_flush(L);
-        L.flush = 0;
-      }
-      if (x == X_OK && L.status == WTFGPU_RUNNING) {
-        L.rip = next;
-        L.icount++;
-        L.nbytes += d.len + L.pend;
-        if (P.limit && L.icount > P.limit) L.status = WTFGPU_EXIT_TIMEOUT;
-      } else if (L.status != WTFGPU_RUNNING) {
-        // faulted / overlay full inside exec or service_miss; rip unchanged
-      } else if (x == X_UNIMPL) {
-        L.status = WTFGPU_EXIT_UNIMPLEMENTED;
-        L.exop = d.len >= 4 ? d.opbytes : (d.opbytes & ((1u << (8 * d.len)) - 1));
-      } else if (x == X_INT3) {
-        L.status = WTFGPU_EXIT_INT3;
-      } else if (x == X_HLT) {
-        L.status = WTFGPU_EXIT_HLT;
-      }
-      // X_FAULT / 6: status already FAULT or OVERLAY_FULL; rip unchanged
+      u32 opbytes = 0;
+      if (x == X_UNIMPL) opbytes = e->u.opbytes;
+      retire(P, L, x, f.len, next, opbytes);
     }
+    STAMP(1);
   }
 
   if (valid) {
     store_lane(P, L);
     if (L.status == WTFGPU_EXIT_FAULT || L.status == WTFGPU_EXIT_UNIMPLEMENTED) {
-      ExitInfo e;
-      e.vector = L.exvec;
-      e.error = L.exerr;
-      e.opcode = L.exop;
-      e.pad = 0;
-      e.addr = L.exaddr;
-      P.exinfo[lane] = e;
+      ExitInfo ei;
+      ei.vector = L.exvec;
+      ei.error = L.exerr;
+      ei.opcode = L.exop;
+      ei.pad = 0;
+      ei.addr = L.exaddr;
+      P.exinfo[lane] = ei;
     }
     P.lflags[lane] = skip ? 1u : 0u;
   }
@@ -329,6 +567,9 @@ __global__ __launch_bounds__(256) void k_run(Dev P, u32 first, u32 count, u64 ma
     atomicAdd((unsigned long long *)&P.stat[0], (unsigned long long)steps);
     atomicAdd((unsigned long long *)&P.stat[1], (unsigned long long)retired);
     if (running) atomicAdd((unsigned long long *)&P.stat[2], (unsigned long long)running);
+#ifdef WTFGPU_STAMPS
+    for (int k = 0; k < 8; k++) atomicAdd((unsigned long long *)&P.stat[4 + k], (unsigned long long)stamp_[k]);
+#endif
   }
 }
 
@@ -720,7 +961,7 @@ int wtfgpu_create(int device, wtfgpu_ctx **out) {
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIPCHK(hipEventCreate(&c->ev0));
   HIPCHK(hipEventCreate(&c->ev1));
-  if (dalloc(&c->d_stat, 4) || dalloc(&c->d_init, 1) || dalloc(&c->d_init_full, 1)) return WTFGPU_ERR_OOM;
+  if (dalloc(&c->d_stat, 16) || dalloc(&c->d_init, 1) || dalloc(&c->d_init_full, 1)) return WTFGPU_ERR_OOM;
   *out = c;
   return WTFGPU_OK;
 }
@@ -811,6 +1052,7 @@ int wtfgpu_load_pool(wtfgpu_ctx *c, const uint64_t *gpfns, const uint8_t *pages,
   c->P.pool = c->d_pool;
   c->P.pfn_map = c->d_pfnmap;
   c->P.pfn_map_len = maplen;
+  c->P.npool = npages;
   c->P.ptbits = c->d_ptbits;
   if (c->have_initial) return mark_pt_pages(c);
   return WTFGPU_OK;
@@ -1174,12 +1416,12 @@ int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps
   float ms_total = 0;
   for (;;) {
     const u64 steps = std::min<u64>(chunk, max_steps - done);
-    HIPCHK(hipMemsetAsync(c->d_stat, 0, 4 * 8, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_stat, 0, 16 * 8, c->stream));
     HIPCHK(hipEventRecord(c->ev0, c->stream));
     k_run<<<(count + 255) / 256, 256, 0, c->stream>>>(c->P, first, count, steps);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev1, c->stream));
-    u64 s[4];
+    u64 s[16];
     HIPCHK(hipMemcpyAsync(s, c->d_stat, sizeof(s), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     float ms = 0;
@@ -1188,6 +1430,10 @@ int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps
     st.kernel_launches++;
     st.group_steps += s[0];
     st.lane_retired += s[1];
+#ifdef WTFGPU_STAMPS
+    fprintf(stderr, "wtfgpu stamps (cycles per wave-step): fast loop %.0f, slow steps %.0f\n", (double)s[4] / s[0],
+            (double)s[5] / s[0]);
+#endif
     done += steps;
     if (s[2] == 0 || done >= max_steps) break;
   }

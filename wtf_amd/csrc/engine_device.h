@@ -58,6 +58,7 @@ struct Dev {
   const u8 *pool;
   const u32 *pfn_map;    // gpfn -> pool page index
   u64 pfn_map_len;
+  u64 npool;             // pages in the pool after the zero page
   const u32 *ptbits;     // bitmap over gpfn: page-table pages of the snapshot
   // lanes, SoA
   u32 nlanes;

@@ -6,13 +6,13 @@
 namespace wtfgpu_dev {
 
 // ------------------------------------------------------------------ lane state
-constexpr u32 GPR_STRIDE = 256;  // threads per block: LDS register file is [16][256] u64
 
 struct Lane {
-  u64 *g;                    // this lane's GPR column in the block's LDS register file
+  u32 *glo, *ghi;            // guest GPRs: two 16 x u32 arrays local to the kernel (VGPRs)
   u64 rip, rflags, icount, nbytes;
   u64 tv[TLB_N], td[TLB_N];  // TLB: vpn tags, page pointer | T_* bits
   u64 bloom;                 // overlay membership filter
+  u64 cvpn, cptr;            // code-page cache: vpn of the last instruction page, its page pointer
   u64 cr0, cr3, efer;
   u64 exaddr;
   u64 miss_va;               // pending translation (TLB miss or copy-on-write)
@@ -20,8 +20,14 @@ struct Lane {
   u32 miss, miss_acc, flush, pend;  // pend: bytes accessed by the attempt in flight
 };
 
-// GPR r of the lane (LDS; a uniform r + lane*8 is bank-conflict free)
-__device__ __forceinline__ u64 &R(const Lane &L, u32 r) { return L.g[r * GPR_STRIDE]; }
+// GPR r of the lane. r is wave-uniform and the halves live in two u32 arrays
+// that the compiler keeps in VGPRs, indexed with s_set_gpr_idx (32-bit moves
+// only: no memory, no per-register select chains).
+__device__ __forceinline__ u64 R(const Lane &L, u32 r) { return ((u64)L.ghi[r & 15] << 32) | L.glo[r & 15]; }
+__device__ __forceinline__ void RS(Lane &L, u32 r, u64 v) {
+  L.glo[r & 15] = (u32)v;
+  L.ghi[r & 15] = (u32)(v >> 32);
+}
 
 // ------------------------------------------------------------------ TLB
 __device__ __forceinline__ bool tlb_get(const Lane &L, u64 vpn, u64 &td) {
@@ -50,6 +56,7 @@ __device__ __forceinline__ void tlb_put(Lane &L, u64 vpn, u64 td) {
 __device__ __forceinline__ void tlb_flush(Lane &L) {
 #pragma unroll
   for (int i = 0; i < TLB_N; i++) L.tv[i] = EMPTY_KEY;
+  L.cvpn = EMPTY_KEY;
 }
 
 // ------------------------------------------------------------------ physical memory

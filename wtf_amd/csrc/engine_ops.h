@@ -58,16 +58,16 @@ __device__ __forceinline__ u64 getr(const Lane &L, u32 rex, u32 r, u32 sz) {
 __device__ __forceinline__ void setr(Lane &L, u32 rex, u32 r, u32 sz, u64 v) {
   if (sz == 1) {
     if (!rex && r >= 4 && r < 8) {
-      R(L, r - 4) = (R(L, r - 4) & ~0xff00ull) | ((v & 0xff) << 8);
+      RS(L, r - 4, (R(L, r - 4) & ~0xff00ull) | ((v & 0xff) << 8));
     } else {
-      R(L, r) = (R(L, r) & ~0xffull) | (v & 0xff);
+      RS(L, r, (R(L, r) & ~0xffull) | (v & 0xff));
     }
   } else if (sz == 2) {
-    R(L, r) = (R(L, r) & ~0xffffull) | (v & 0xffff);
+    RS(L, r, (R(L, r) & ~0xffffull) | (v & 0xffff));
   } else if (sz == 4) {
-    R(L, r) = v & 0xffffffffull;
+    RS(L, r, v & 0xffffffffull);
   } else {
-    R(L, r) = v;
+    RS(L, r, v);
   }
 }
 
@@ -729,12 +729,12 @@ __device__ __forceinline__ int string_op(const Dev &P, Lane &L, const UOp &u) {
       L.rflags = with_status(L.rflags, f);
     }
     if (op == 0xac) setr(L, u.rex, 0, sz, a);
-    if (src) R(L, 6) = (rsi + step) & amask;
-    if (op != 0xac) R(L, 7) = (rdi + step) & amask;
+    if (src) RS(L, 6, (rsi + step) & amask);
+    if (op != 0xac) RS(L, 7, (rdi + step) & amask);
     L.nbytes += L.pend;  // the iteration is architecturally complete
     L.pend = 0;
     if (!u.rep) break;
-    R(L, 1) = (R(L, 1) - 1) & amask;
+    RS(L, 1, (R(L, 1) - 1) & amask);
     if (dstr) {
       const bool zf = L.rflags & F_ZF;
       if (u.rep == 0xf3 && !zf) break;
@@ -1012,10 +1012,10 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
   }
   // ---- commit
   if (op == O_LEAVE) {
-    R(L, 4) = R(L, 5) + 8;
-    R(L, 5) = b;
+    RS(L, 4, R(L, 5) + 8);
+    RS(L, 5, b);
   }
-  if (drsp) R(L, 4) = rsp + (u64)drsp;
+  if (drsp) RS(L, 4, rsp + (u64)drsp);
   if (u.bwrite && !bmem) setr(L, u.rex, loc_reg(u, u.bsrc), u.bsz, resb);  // xchg / xadd source
   if (wa && !amem) setr(L, u.rex, loc_reg(u, u.asrc), asz, res);  // xadd r,r: DEST := TEMP last (SDM)
   if (wrax) setr(L, u.rex, 0, raxsz, ra);
