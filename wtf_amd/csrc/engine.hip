@@ -388,12 +388,15 @@ __device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr
 #endif
 
 // ---------------------------------------------------------------- main kernel
+// One hardware wave runs P.lpw lanes (64, or 32 / 16 to put more waves on
+// each SIMD when the batch is small: the step loop is latency-bound).
 __global__ __launch_bounds__(256) void k_run(Dev P, u32 first, u32 count, u64 max_steps) {
-  const u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
-  const u32 lane = first + tid;
-  const bool valid = tid < count && lane < P.nlanes;
   const u32 lid = threadIdx.x & 63;
-  const u32 wv = lane >> 6;  // first is 64-aligned: hardware wave == log wave
+  const u32 hw = rfl32(blockIdx.x * 4 + (threadIdx.x >> 6));  // hardware wave in the launch (uniform)
+  const u32 tid = hw * P.lpw + lid;
+  const u32 lane = first + tid;
+  const bool valid = lid < P.lpw && tid < count && lane < P.nlanes;
+  const u32 wv = first / P.lpw + hw;  // first is lpw-aligned: hardware wave == log wave (uniform)
   __shared__ UCEntry sUC[4][UC_N];
   UCEntry *uc = sUC[threadIdx.x >> 6];
   for (u32 i = lid; i < UC_N; i += 64) uc[i].key = EMPTY_KEY;
@@ -412,7 +415,7 @@ __global__ __launch_bounds__(256) void k_run(Dev P, u32 first, u32 count, u64 ma
   }
   const u64 icount0 = L.icount;
   bool skip = valid && (P.lflags[lane] & 1);
-  const u32 ep = (P.cov_rip && wv < (P.nlanes + 63) / 64) ? rfl32(P.cov_wave_ep[rfl32(wv)]) : 0;
+  const u32 ep = (P.cov_rip && wv < (P.nlanes + P.lpw - 1) / P.lpw) ? rfl32(P.cov_wave_ep[rfl32(wv)]) : 0;
   const u64 pool_lo = (u64)(uintptr_t)P.pool, pool_hi = pool_lo + (P.npool + 1) * WTFGPU_PAGE_SIZE;
   u64 steps = 0;
 #ifdef WTFGPU_STAMPS
@@ -449,16 +452,22 @@ __global__ __launch_bounds__(256) void k_run(Dev P, u32 first, u32 count, u64 ma
       if (P.cov_rip && !(flags & UC_COVERED) && (__ballot(ing) & ~rfl64(e->logged))) break;
       FOp f;
       lds_uniform_read(&e->f, f);
-      if (f.kind == FK_GENERIC) break;
+      if (fo_op(f) == FO_GENERIC) break;
       steps++;
       have = false;
       if (ing) {
         skip = false;
         L.miss = 0;
         L.pend = 0;
+        const u32 len = fo_len(f);
         u64 next;
-        const int x = fast_exec(L, f, grip + f.len, next);
-        if (!L.miss) retire(P, L, x, f.len, next, 0);
+        fast_exec(L, f, grip + len, next);
+        if (!L.miss) {
+          L.rip = next;
+          L.icount++;
+          L.nbytes += len + L.pend;
+          if (P.limit && L.icount > P.limit) L.status = WTFGPU_EXIT_TIMEOUT;
+        }
       }
       // lanes that missed keep their rip: the slow step services them
       if (__ballot(ing && L.miss)) {
@@ -498,8 +507,7 @@ __global__ __launch_bounds__(256) void k_run(Dev P, u32 first, u32 count, u64 ma
       STAMP(1);
       continue;
     }
-    FOp f;
-    lds_uniform_read(&e->f, f);
+    const u32 len = rfl32(e->u.len);
     const u64 gmask = __ballot(ing);
 
     // ---- coverage, then breakpoint (bochscpu_backend.cc:501-547)
@@ -518,7 +526,7 @@ __global__ __launch_bounds__(256) void k_run(Dev P, u32 first, u32 count, u64 ma
       skip = false;
     }
     if (ing && (flags & UC_UNSUP)) {
-      const u32 ob = e->u.opbytes, n = f.len;
+      const u32 ob = e->u.opbytes, n = len;
       L.status = WTFGPU_EXIT_UNIMPLEMENTED;
       L.exop = n >= 4 ? ob : (ob & ((1u << (8 * n)) - 1));
       ing = false;
@@ -531,11 +539,7 @@ __global__ __launch_bounds__(256) void k_run(Dev P, u32 first, u32 count, u64 ma
       for (int attempt = 0;; attempt++) {
         L.miss = 0;
         L.pend = 0;
-        if (f.kind != FK_GENERIC) {
-          x = fast_exec(L, f, grip + f.len, next);
-        } else {
-          WITH_LANE_COPY(x = exec_generic(P, T, &e->u, next));
-        }
+        WITH_LANE_COPY(x = exec_generic(P, T, &e->u, next));
         if (!L.miss || L.status != WTFGPU_RUNNING) break;
         bool ok;
         WITH_LANE_COPY(ok = miss_service(P, T, attempt));
@@ -543,7 +547,7 @@ __global__ __launch_bounds__(256) void k_run(Dev P, u32 first, u32 count, u64 ma
       }
       u32 opbytes = 0;
       if (x == X_UNIMPL) opbytes = e->u.opbytes;
-      retire(P, L, x, f.len, next, opbytes);
+      retire(P, L, x, len, next, opbytes);
     }
     STAMP(1);
   }
@@ -601,10 +605,10 @@ __global__ void k_restore(Dev P, const InitState *S, const wtfgpu_regs_t *full0,
   P.sys[lane] = s.sys;
   P.ov_count[lane] = 0;  // the dirty-list reset: overlays dropped, nothing copied
   if (P.cov_rip) {
-    const u32 wv = lane >> 6;
-    const u32 w0 = wv * 64, w1 = w0 + 64;
+    const u32 wv = lane / P.lpw, bit = lane % P.lpw;
+    const u32 w0 = wv * P.lpw, w1 = w0 + P.lpw;
     const bool whole = w0 >= first && w1 <= first + count;
-    if ((lane & 63) == 0 && whole) {
+    if (bit == 0 && whole) {
       P.cov_wave_ep[wv] += 1;  // invalidates every log entry of the wave
       P.cov_overflow[wv] = 0;
     } else if (!whole) {
@@ -612,7 +616,7 @@ __global__ void k_restore(Dev P, const InitState *S, const wtfgpu_regs_t *full0,
       for (u32 h = 0; h < P.H; h++) {
         const u64 idx = (u64)wv * P.H + h;
         if (P.cov_ep[idx] == P.cov_wave_ep[wv])
-          atomicAnd((unsigned long long *)&P.cov_mask[idx], ~(1ull << (lane & 63)));
+          atomicAnd((unsigned long long *)&P.cov_mask[idx], ~(1ull << bit));
       }
     }
   }
@@ -772,7 +776,7 @@ __global__ void k_lane_mem(Dev P, u32 lane, u32 op, u64 addr, u64 len, u8 *buf, 
 __global__ void k_cov_collect(Dev P, u32 first, u32 count, u32 *out_lane, u64 *out_rip, u64 cap,
                               unsigned long long *n_out) {
   const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  const u32 w0 = first / 64, w1 = (first + count + 63) / 64;
+  const u32 w0 = first / P.lpw, w1 = (first + count + P.lpw - 1) / P.lpw;
   const u64 total = (u64)(w1 - w0) * P.H;
   if (t >= total) return;
   const u32 wv = w0 + (u32)(t / P.H);
@@ -783,7 +787,7 @@ __global__ void k_cov_collect(Dev P, u32 first, u32 count, u32 *out_lane, u64 *o
   while (m) {
     const int b = __ffsll((long long)m) - 1;
     m &= m - 1;
-    const u32 lane = wv * 64 + b;
+    const u32 lane = wv * P.lpw + b;
     if (lane < first || lane >= first + count) continue;
     const unsigned long long pos = atomicAdd(n_out, 1ull);
     if (pos < cap) {
@@ -1064,7 +1068,14 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
   HIPCHK(hipSetDevice(c->device));
   free_lanes(c);
   const u64 N = nlanes;
-  const u64 nw = (N + 63) / 64;
+  // lanes per wave: full waves once there are >= 2 per SIMD (256 CUs x 4),
+  // otherwise fewer lanes per wave and more waves (overridable: WTFGPU_LPW)
+  u32 lpw = N >= 2ull * 1024 * 64 ? 64 : (N >= 2ull * 1024 * 32 ? 32 : 16);
+  if (const char *e = getenv("WTFGPU_LPW")) {
+    const u32 v = (u32)atoi(e);
+    if (v == 64 || v == 32 || v == 16) lpw = v;
+  }
+  const u64 nw = (N + lpw - 1) / lpw;
   int rc = 0;
   rc |= dalloc(&c->d_gpr, 16 * N);
   rc |= dalloc(&c->d_rip, N);
@@ -1110,6 +1121,7 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
   Dev &P = c->P;
   P.nlanes = nlanes;
   P.K = overlay_pages;
+  P.lpw = lpw;
   P.gpr = c->d_gpr;
   P.rip = c->d_rip;
   P.rflags = c->d_rflags;
@@ -1407,7 +1419,7 @@ int wtfgpu_stop(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, uint32_t statu
 }
 
 int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps, wtfgpu_run_stats_t *stats) {
-  if (!lanes_ok(c, first, count) || (first & 63)) return WTFGPU_ERR_INVALID;
+  if (!lanes_ok(c, first, count) || (first % c->P.lpw)) return WTFGPU_ERR_INVALID;
   if (!c->P.pool) return WTFGPU_ERR_STATE;
   HIPCHK(hipSetDevice(c->device));
   wtfgpu_run_stats_t st{};
@@ -1418,7 +1430,8 @@ int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps
     const u64 steps = std::min<u64>(chunk, max_steps - done);
     HIPCHK(hipMemsetAsync(c->d_stat, 0, 16 * 8, c->stream));
     HIPCHK(hipEventRecord(c->ev0, c->stream));
-    k_run<<<(count + 255) / 256, 256, 0, c->stream>>>(c->P, first, count, steps);
+    const u32 hwaves = (count + c->P.lpw - 1) / c->P.lpw;
+    k_run<<<(hwaves + 3) / 4, 256, 0, c->stream>>>(c->P, first, count, steps);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev1, c->stream));
     u64 s[16];
@@ -1550,7 +1563,7 @@ int wtfgpu_read_coverage(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint32_t
   if (overflow) *overflow = 0;
   if (!c->d_covrip || count == 0) return WTFGPU_OK;
   HIPCHK(hipSetDevice(c->device));
-  const u32 w0 = first / 64, w1 = (first + count + 63) / 64;
+  const u32 w0 = first / c->P.lpw, w1 = (first + count + c->P.lpw - 1) / c->P.lpw;
   const u64 total = (u64)(w1 - w0) * c->P.H;
   const u64 room = std::max<u64>(cap, 1);
   const u64 o_rip = (room * 4 + 255) & ~255ull, o_n = (o_rip + room * 8 + 255) & ~255ull;

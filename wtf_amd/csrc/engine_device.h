@@ -63,6 +63,7 @@ struct Dev {
   // lanes, SoA
   u32 nlanes;
   u32 K;                 // copy-on-write pages per lane
+  u32 lpw;               // lanes per hardware wave (64, 32 or 16): coverage-log wave = lane / lpw
   u64 *gpr;              // [16][nlanes]
   u64 *rip, *rflags, *fs_base, *gs_base, *icount, *nbytes;
   u32 *status, *lflags;  // lflags bit0: skip breakpoint once

@@ -3,56 +3,78 @@
 // decode() (engine_ops.h) produces a general UOp that the generic exec()
 // pipeline interprets field by field. That generality is paid on every step
 // (operand-location switches, sizes, prefixes), so at uop-cache fill time the
-// UOp is also digested into an FOp: one `kind` per common operand form, with
-// registers, sizes and the effective-address recipe resolved. fast_exec()
-// then runs a short body per kind. Anything outside those forms (segment or
-// address-size overrides, high-byte registers, string ops, mul/div, system
-// instructions, ...) keeps kind FK_GENERIC and goes through exec() unchanged,
-// so the fast path only ever re-states semantics exec() already has (the same
-// helpers: alu2, shift_op, cond, vread/vwrite).
+// UOp is also digested into an FOp: a compute op plus a set of pipeline flags
+// (which operands are registers / immediates / memory, where the address comes
+// from, what is written back), with registers, sizes and the effective-address
+// recipe resolved and packed into 8 dwords. fast_exec() is then one short
+// pipeline with a single memory-read and a single memory-write site, so the
+// call-free fast loop of k_run stays small.
+//
+// Anything outside the common forms (segment or address-size overrides,
+// high-byte registers, string ops, mul/div, system instructions, ...) keeps op
+// FO_GENERIC and runs through exec() in the slow step; so does any fast
+// attempt that meets something the fast path does not handle (TLB miss, first
+// write to a page, write to a page-table page, page-crossing access,
+// permission fault): it sets L.miss, commits nothing, and the slow step re-runs
+// the instruction with exec(). The fast path only re-states semantics exec()
+// already has, with the same helpers (alu2, shift_op, cond, szmask, sext).
 #pragma once
 #include "engine_ops.h"
 
 namespace wtfgpu_dev {
 
+// compute ops
 enum : u32 {
-  FK_GENERIC = 0,
-  FK_NOP,
-  FK_MOV_RR,    // ra <- rb
-  FK_MOV_RI,    // ra <- imm
-  FK_LOAD,      // ra <- [ea]
-  FK_STORE,     // [ea] <- rb
-  FK_STORE_I,   // [ea] <- imm
-  FK_ALU_RR,    // ra <- ra op rb (sub = alu op; 7 = cmp writes nothing)
-  FK_ALU_RI,    // ra <- ra op imm
-  FK_ALU_RM,    // ra <- ra op [ea]
-  FK_ALU_MR,    // [ea] <- [ea] op rb
-  FK_ALU_MI,    // [ea] <- [ea] op imm
-  FK_TEST_RR,   // flags of ra & rb
-  FK_TEST_RI,   // flags of ra & imm
-  FK_LEA,       // ra <- ea
-  FK_INCDEC_R,  // ra <- ra +/- 1 (sub 0 inc, 1 dec), CF kept
-  FK_JCC,       // rip <- nrip + imm if cond(sub)
-  FK_JMP,       // rip <- nrip + imm
-  FK_CALL,      // push nrip; rip <- nrip + imm
-  FK_RET,       // rip <- pop; rsp += imm
-  FK_PUSH_R,    // push rb
-  FK_POP_R,     // ra <- pop
-  FK_MOVX_RR,   // ra <- zext/sext(rb, szb) (sub 1 = sign)
-  FK_MOVX_RM,   // ra <- zext/sext([ea], szb)
-  FK_SHIFT_RI,  // ra <- shift(sub, ra, imm)
-  FK_CMOV_RR,   // ra <- cond(sub) ? rb : ra
-  FK_SETCC_R,   // ra.b <- cond(sub)
+  FO_GENERIC = 0,
+  FO_NOP,
+  FO_MOV,     // res = b
+  FO_ALU,     // res = alu2(sub, a, b); sub 7 (cmp) writes nothing
+  FO_LEA,     // res = ea
+  FO_INCDEC,  // res = a +/- 1, CF kept
+  FO_JCC,     // next = nrip + imm if cond(sub)
+  FO_JMP,     // next = nrip + imm
+  FO_CALL,    // res = nrip (pushed), next = nrip + imm
+  FO_RET,     // next = b (popped)
+  FO_MOVX,    // res = zext/sext(b, szb), sub 1 = sign
+  FO_SHIFT,   // res = shift_op(sub, a, imm)
+  FO_CMOV,    // res = cond(sub) ? b : a
+  FO_SETCC,   // res = cond(sub)
+};
+// pipeline flags
+enum : u32 {
+  FF_AREG = 1,      // a = R(ra)
+  FF_BREG = 2,      // b = R(rb) (else b = imm)
+  FF_EA = 4,        // address = effective address
+  FF_PUSH = 8,      // address = rsp - 8, rsp -= 8 at commit
+  FF_POP = 16,      // address = rsp, rsp += 8 + imm at commit (imm only for ret)
+  FF_MR_A = 32,     // memory read into a (read-modify-write when FF_MW)
+  FF_MR_B = 64,     // memory read into b
+  FF_MW = 128,      // memory write of res at the address
+  FF_WRA = 256,     // register write of res into ra
+  FF_FLAGS = 512,   // rflags updated by the op
 };
 
 constexpr u32 NOREG = 16;
 
 struct FOp {
-  u32 kind, len, sz, szb;
-  u32 ra, rb, sub, base;
-  u32 index, scale, riprel, pad;
+  u32 w0;  // op | sub << 8 | sz << 12 | szb << 16 | len << 20 | scale << 26 | riprel << 28
+  u32 fl;  // FF_*
+  u32 w2;  // ra | rb << 8 | base << 16 | index << 24
+  u32 pad;
   u64 disp, imm;
 };
+
+__device__ __forceinline__ u32 fo_op(const FOp &f) { return f.w0 & 0xff; }
+__device__ __forceinline__ u32 fo_sub(const FOp &f) { return (f.w0 >> 8) & 0xf; }
+__device__ __forceinline__ u32 fo_sz(const FOp &f) { return (f.w0 >> 12) & 0xf; }
+__device__ __forceinline__ u32 fo_szb(const FOp &f) { return (f.w0 >> 16) & 0xf; }
+__device__ __forceinline__ u32 fo_len(const FOp &f) { return (f.w0 >> 20) & 0x3f; }
+__device__ __forceinline__ u32 fo_scale(const FOp &f) { return (f.w0 >> 26) & 3; }
+__device__ __forceinline__ u32 fo_riprel(const FOp &f) { return (f.w0 >> 28) & 1; }
+__device__ __forceinline__ u32 fo_ra(const FOp &f) { return f.w2 & 0xff; }
+__device__ __forceinline__ u32 fo_rb(const FOp &f) { return (f.w2 >> 8) & 0xff; }
+__device__ __forceinline__ u32 fo_base(const FOp &f) { return (f.w2 >> 16) & 0xff; }
+__device__ __forceinline__ u32 fo_index(const FOp &f) { return (f.w2 >> 24) & 0xff; }
 
 // ---------------------------------------------------------------- digest (fill time, uniform)
 __device__ __forceinline__ u32 loc_regno(const UOp &u, u32 loc) {
@@ -66,93 +88,88 @@ __device__ __forceinline__ u32 loc_regno(const UOp &u, u32 loc) {
 }
 
 __device__ __forceinline__ void digest(const UOp &u, FOp &f) {
-  f.kind = FK_GENERIC;
-  f.len = u.len;
-  f.sz = u.asz;
-  f.szb = u.bsz;
-  f.sub = u.sub;
-  f.base = u.base >= 0 ? (u32)u.base : NOREG;
-  f.index = u.index >= 0 ? (u32)u.index : NOREG;
-  f.scale = u.scale;
-  f.riprel = u.riprel;
-  f.pad = 0;
-  f.disp = u.disp;
-  f.imm = u.imm;
-  f.ra = loc_regno(u, u.asrc);
-  f.rb = loc_regno(u, u.bsrc);
-  if (!u.supported || u.seg || u.p67 || u.rep) return;
-  // high-byte registers (ah/ch/dh/bh) stay on the generic path
-  const bool hb = !u.rex && ((u.asz == 1 && ((u.asrc == L_GREG && u.reg >= 4 && u.reg < 8) ||
-                                             (u.asrc == L_RM && !u.is_mem && u.rm >= 4 && u.rm < 8) ||
-                                             (u.asrc == L_OPREG && u.opreg >= 4 && u.opreg < 8))) ||
-                             (u.bsz == 1 && ((u.bsrc == L_GREG && u.reg >= 4 && u.reg < 8) ||
-                                             (u.bsrc == L_RM && !u.is_mem && u.rm >= 4 && u.rm < 8))));
-  if (hb) return;
+  u32 op = FO_GENERIC, fl = 0, sub = u.sub;
+  const u32 ra = loc_regno(u, u.asrc), rb = loc_regno(u, u.bsrc);
   const bool amem = u.asrc == L_RM && u.is_mem;
   const bool bmem = u.bsrc == L_RM && u.is_mem;
-  const bool areg = f.ra != NOREG;
-  const bool breg = f.rb != NOREG;
-  const bool bimm = u.bsrc == L_IMM;
-  switch (u.op) {
-    case O_NOP: f.kind = FK_NOP; break;
-    case O_MOV:
-      if (areg && breg) f.kind = FK_MOV_RR;
-      else if (areg && bimm) f.kind = FK_MOV_RI;
-      else if (areg && bmem) f.kind = FK_LOAD;
-      else if (amem && breg) f.kind = FK_STORE;
-      else if (amem && bimm) f.kind = FK_STORE_I;
-      break;
-    case O_ALU:
-      if (areg && breg) f.kind = FK_ALU_RR;
-      else if (areg && bimm) f.kind = FK_ALU_RI;
-      else if (areg && bmem) f.kind = FK_ALU_RM;
-      else if (amem && breg) f.kind = FK_ALU_MR;
-      else if (amem && bimm) f.kind = FK_ALU_MI;
-      break;
-    case O_TEST:
-      if (areg && breg) f.kind = FK_TEST_RR;
-      else if (areg && bimm) f.kind = FK_TEST_RI;
-      break;
-    case O_LEA:
-      if (areg && u.is_mem) f.kind = FK_LEA;
-      break;
-    case O_INCDEC:
-      if (areg) f.kind = FK_INCDEC_R;
-      break;
-    case O_JCC: f.kind = FK_JCC; break;
-    case O_JMP:
-      if (bimm) f.kind = FK_JMP;
-      break;
-    case O_CALL:
-      if (bimm) f.kind = FK_CALL;
-      break;
-    case O_RET: f.kind = FK_RET; break;
-    case O_PUSH:
-      if (breg && u.asz == 8) f.kind = FK_PUSH_R;
-      break;
-    case O_POP:
-      if (areg && u.asrc == L_OPREG && u.bsz == 8) f.kind = FK_POP_R;
-      break;
-    case O_MOVZX:
-    case O_MOVSX:
-      f.sub = u.op == O_MOVSX ? 1 : 0;
-      if (areg && breg) f.kind = FK_MOVX_RR;
-      else if (areg && bmem) f.kind = FK_MOVX_RM;
-      break;
-    case O_SHIFT:
-      if (areg && (bimm || u.bsrc == L_ONE)) {
-        f.kind = FK_SHIFT_RI;
-        if (u.bsrc == L_ONE) f.imm = 1;
+  const bool areg = ra != NOREG, breg = rb != NOREG, bimm = u.bsrc == L_IMM;
+  // high-byte registers (ah/ch/dh/bh) stay on the generic path
+  const bool hb = !u.rex && ((u.asz == 1 && areg && ra >= 4 && ra < 8) || (u.bsz == 1 && breg && rb >= 4 && rb < 8));
+  u64 imm = u.imm;
+  if (u.supported && !u.seg && !u.p67 && !u.rep && !hb) {
+    switch (u.op) {
+      case O_NOP: op = FO_NOP; break;
+      case O_MOV:
+        if (areg && breg) op = FO_MOV, fl = FF_BREG | FF_WRA;
+        else if (areg && bimm) op = FO_MOV, fl = FF_WRA;
+        else if (areg && bmem) op = FO_MOV, fl = FF_EA | FF_MR_B | FF_WRA;
+        else if (amem && breg) op = FO_MOV, fl = FF_BREG | FF_EA | FF_MW;
+        else if (amem && bimm) op = FO_MOV, fl = FF_EA | FF_MW;
+        break;
+      case O_ALU: {
+        const u32 w = u.sub != 7;  // cmp reads its destination, never writes it
+        if (areg && breg) op = FO_ALU, fl = FF_AREG | FF_BREG | (w ? FF_WRA : 0);
+        else if (areg && bimm) op = FO_ALU, fl = FF_AREG | (w ? FF_WRA : 0);
+        else if (areg && bmem) op = FO_ALU, fl = FF_AREG | FF_EA | FF_MR_B | (w ? FF_WRA : 0);
+        else if (amem && breg) op = FO_ALU, fl = FF_BREG | FF_EA | FF_MR_A | (w ? FF_MW : 0);
+        else if (amem && bimm) op = FO_ALU, fl = FF_EA | FF_MR_A | (w ? FF_MW : 0);
+        if (op) fl |= FF_FLAGS;
+        break;
       }
-      break;
-    case O_CMOV:
-      if (areg && breg) f.kind = FK_CMOV_RR;
-      break;
-    case O_SETCC:
-      if (areg) f.kind = FK_SETCC_R;
-      break;
-    default: break;
+      case O_TEST:
+        sub = 4;
+        if (areg && breg) op = FO_ALU, fl = FF_AREG | FF_BREG | FF_FLAGS;
+        else if (areg && bimm) op = FO_ALU, fl = FF_AREG | FF_FLAGS;
+        break;
+      case O_LEA:
+        if (areg && u.is_mem) op = FO_LEA, fl = FF_EA | FF_WRA;
+        break;
+      case O_INCDEC:
+        if (areg) op = FO_INCDEC, fl = FF_AREG | FF_WRA | FF_FLAGS;
+        break;
+      case O_JCC: op = FO_JCC; break;
+      case O_JMP:
+        if (bimm) op = FO_JMP;
+        break;
+      case O_CALL:
+        if (bimm) op = FO_CALL, fl = FF_PUSH | FF_MW;
+        break;
+      case O_RET: op = FO_RET, fl = FF_POP | FF_MR_B; break;
+      case O_PUSH:
+        if (breg && u.asz == 8) op = FO_MOV, fl = FF_BREG | FF_PUSH | FF_MW;
+        break;
+      case O_POP:
+        if (areg && u.asrc == L_OPREG && u.bsz == 8) op = FO_MOV, fl = FF_POP | FF_MR_B | FF_WRA, imm = 0;
+        break;
+      case O_MOVZX:
+      case O_MOVSX:
+        sub = u.op == O_MOVSX ? 1 : 0;
+        if (areg && breg) op = FO_MOVX, fl = FF_BREG | FF_WRA;
+        else if (areg && bmem) op = FO_MOVX, fl = FF_EA | FF_MR_B | FF_WRA;
+        break;
+      case O_SHIFT:
+        if (areg && (bimm || u.bsrc == L_ONE)) {
+          op = FO_SHIFT, fl = FF_AREG | FF_WRA | FF_FLAGS;
+          if (u.bsrc == L_ONE) imm = 1;
+        }
+        break;
+      case O_CMOV:
+        if (areg && breg) op = FO_CMOV, fl = FF_AREG | FF_BREG | FF_WRA;
+        break;
+      case O_SETCC:
+        if (areg) op = FO_SETCC, fl = FF_WRA;
+        break;
+      default: break;
+    }
   }
+  const u32 base = u.base >= 0 ? (u32)u.base : NOREG, index = u.index >= 0 ? (u32)u.index : NOREG;
+  f.w0 = op | (sub & 0xf) << 8 | (u.asz & 0xf) << 12 | (u.bsz & 0xf) << 16 | (u.len & 0x3f) << 20 |
+         (u.scale & 3) << 26 | (u.riprel & 1) << 28;
+  f.fl = fl;
+  f.w2 = (ra & 0xff) | (rb & 0xff) << 8 | (base & 0xff) << 16 | (index & 0xff) << 24;
+  f.pad = 0;
+  f.disp = u.disp;
+  f.imm = imm;
 }
 
 // ---------------------------------------------------------------- execute (per lane)
@@ -164,129 +181,99 @@ __device__ __forceinline__ void wr(Lane &L, u32 r, u32 sz, u64 v) {
   else RS(L, r, (R(L, r) & ~0xffull) | (v & 0xff));
 }
 
-__device__ __forceinline__ u64 fea(const Lane &L, const FOp &f, u64 nrip) {
-  u64 ea = f.disp + (f.riprel ? nrip : 0);
-  if (f.base != NOREG) ea += R(L, f.base);
-  if (f.index != NOREG) ea += R(L, f.index) << f.scale;
-  return ea;
+// Fast translation: TLB hit with the permission already granted, and for a
+// write a private (copy-on-write done) page that is not a page-table page.
+// Everything else -> L.miss, the slow step takes over.
+__device__ __forceinline__ u8 *fxlate(Lane &L, u64 va, u32 sz, int acc) {
+  u64 td;
+  const bool w = acc == ACC_W;
+  if ((va & 0xfff) + sz > 4096 || !tlb_get(L, va >> 12, td) || !perm_ok(L, td, acc) ||
+      (w && ((td & (T_PRIV | T_PT)) != T_PRIV))) {
+    L.miss = 1;
+    return nullptr;
+  }
+  return (u8 *)(uintptr_t)(td & ~0xfffull) + (va & 0xfff);
 }
 
-// One attempt; same contract as exec(): X_OK with `next`, or X_FAULT with
-// L.miss set (retry after service_miss) / L.status set (architectural fault).
-// Nothing is committed before every memory access has succeeded.
 __device__ __forceinline__ int fast_exec(Lane &L, const FOp &f, u64 nrip, u64 &next) {
   next = nrip;
-  const u32 sz = f.sz;
-  const u64 mk = szmask(sz);
-  u64 fl = L.rflags, fo;
-  switch (f.kind) {
-    case FK_NOP: return X_OK;
-    case FK_MOV_RR: wr(L, f.ra, sz, R(L, f.rb)); return X_OK;
-    case FK_MOV_RI: wr(L, f.ra, sz, f.imm); return X_OK;
-    case FK_LOAD: {
-      u64 v;
-      if (!vread(L, fea(L, f, nrip), sz, v)) return X_FAULT;
-      wr(L, f.ra, sz, v);
-      return X_OK;
-    }
-    case FK_STORE: return vwrite(L, fea(L, f, nrip), sz, R(L, f.rb) & mk) ? X_OK : X_FAULT;
-    case FK_STORE_I: return vwrite(L, fea(L, f, nrip), sz, f.imm & mk) ? X_OK : X_FAULT;
-    case FK_ALU_RR:
-    case FK_ALU_RI:
-    case FK_ALU_RM: {
-      u64 b;
-      if (f.kind == FK_ALU_RM) {
-        if (!vread(L, fea(L, f, nrip), sz, b)) return X_FAULT;
-      } else {
-        b = f.kind == FK_ALU_RR ? R(L, f.rb) : f.imm;
-      }
-      const u64 res = alu2(f.sub, R(L, f.ra), b, sz, fl, fo);
-      if (f.sub != 7) wr(L, f.ra, sz, res);
-      L.rflags = with_status(fl, fo);
-      return X_OK;
-    }
-    case FK_ALU_MR:
-    case FK_ALU_MI: {
-      const u64 ea = fea(L, f, nrip);
-      u64 a;
-      if (!vread(L, ea, sz, a, f.sub == 7 ? ACC_R : ACC_W)) return X_FAULT;
-      const u64 res = alu2(f.sub, a, f.kind == FK_ALU_MR ? R(L, f.rb) : f.imm, sz, fl, fo);
-      if (f.sub != 7 && !vwrite(L, ea, sz, res)) return X_FAULT;
-      L.rflags = with_status(fl, fo);
-      return X_OK;
-    }
-    case FK_TEST_RR:
-    case FK_TEST_RI:
-      alu2(4, R(L, f.ra), f.kind == FK_TEST_RR ? R(L, f.rb) : f.imm, sz, fl, fo);
-      L.rflags = with_status(fl, fo);
-      return X_OK;
-    case FK_LEA: wr(L, f.ra, sz, fea(L, f, nrip)); return X_OK;
-    case FK_INCDEC_R: {
-      const u64 res = alu2(f.sub ? 5 : 0, R(L, f.ra), 1, sz, fl, fo);
-      wr(L, f.ra, sz, res);
-      L.rflags = (fl & ~(F_STATUS & ~F_CF)) | (fo & ~F_CF);
-      return X_OK;
-    }
-    case FK_JCC:
-      if (cond(fl, f.sub)) next = nrip + f.imm;
-      return X_OK;
-    case FK_JMP: next = nrip + f.imm; return X_OK;
-    case FK_CALL: {
-      const u64 rsp = R(L, 4);
-      if (!vwrite(L, rsp - 8, 8, nrip)) return X_FAULT;
-      RS(L, 4, rsp - 8);
-      next = nrip + f.imm;
-      return X_OK;
-    }
-    case FK_RET: {
-      const u64 rsp = R(L, 4);
-      u64 t;
-      if (!vread(L, rsp, 8, t)) return X_FAULT;
-      RS(L, 4, rsp + 8 + f.imm);
-      next = t;
-      return X_OK;
-    }
-    case FK_PUSH_R: {
-      const u64 rsp = R(L, 4);
-      if (!vwrite(L, rsp - 8, 8, R(L, f.rb))) return X_FAULT;
-      RS(L, 4, rsp - 8);
-      return X_OK;
-    }
-    case FK_POP_R: {
-      const u64 rsp = R(L, 4);
-      u64 t;
-      if (!vread(L, rsp, 8, t)) return X_FAULT;
-      RS(L, 4, rsp + 8);  // rsp first: pop rsp loads the popped value (exec() commit order)
-      RS(L, f.ra, t);
-      return X_OK;
-    }
-    case FK_MOVX_RR:
-    case FK_MOVX_RM: {
-      u64 b;
-      if (f.kind == FK_MOVX_RM) {
-        if (!vread(L, fea(L, f, nrip), f.szb, b)) return X_FAULT;
-      } else {
-        b = R(L, f.rb);
-      }
-      b &= szmask(f.szb);
-      wr(L, f.ra, sz, f.sub ? sext(b, f.szb) : b);
-      return X_OK;
-    }
-    case FK_SHIFT_RI: {
-      const u64 res = shift_op(f.sub, R(L, f.ra), (u32)f.imm, sz, fl);
-      wr(L, f.ra, sz, res);
-      L.rflags = fl;
-      return X_OK;
-    }
-    case FK_CMOV_RR: {
-      const bool t = cond(fl, f.sub);
-      if (t) wr(L, f.ra, sz, R(L, f.rb));
-      else if (sz == 4) wr(L, f.ra, 4, R(L, f.ra));
-      return X_OK;
-    }
-    case FK_SETCC_R: wr(L, f.ra, 1, cond(fl, f.sub) ? 1 : 0); return X_OK;
-    default: return X_UNIMPL;
+  const u32 F = f.fl, op = fo_op(f), sub = fo_sub(f), sz = fo_sz(f);
+  const u64 rsp = R(L, 4);
+  u64 a = (F & FF_AREG) ? R(L, fo_ra(f)) : 0;
+  u64 b = (F & FF_BREG) ? R(L, fo_rb(f)) : f.imm;
+  u64 addr = 0;
+  if (F & FF_EA) {
+    addr = f.disp + (fo_riprel(f) ? nrip : 0);
+    if (fo_base(f) != NOREG) addr += R(L, fo_base(f));
+    if (fo_index(f) != NOREG) addr += R(L, fo_index(f)) << fo_scale(f);
+  } else if (F & FF_PUSH) {
+    addr = rsp - 8;
+  } else {
+    addr = rsp;
   }
+  // ---- the memory read
+  u8 *mp = nullptr;
+  if (F & (FF_MR_A | FF_MR_B)) {
+    const u32 rsz = (F & (FF_PUSH | FF_POP)) ? 8 : (op == FO_MOVX ? fo_szb(f) : sz);
+    mp = fxlate(L, addr, rsz, (F & FF_MW) ? ACC_W : ACC_R);
+    if (!mp) return X_FAULT;
+    const u64 v = load_le(mp, rsz);
+    L.pend += rsz;
+    if (F & FF_MR_A) a = v;
+    else b = v;
+  }
+  // ---- compute (pure)
+  u64 res = 0, fl = L.rflags, fo;
+  switch (op) {
+    case FO_MOV: res = b; break;
+    case FO_ALU:
+      res = alu2(sub, a, b, sz, fl, fo);
+      fl = with_status(fl, fo);
+      break;
+    case FO_LEA: res = addr; break;
+    case FO_INCDEC:
+      res = alu2(sub ? 5 : 0, a, 1, sz, fl, fo);
+      fl = (fl & ~(F_STATUS & ~F_CF)) | (fo & ~F_CF);
+      break;
+    case FO_JCC:
+      if (cond(fl, sub)) next = nrip + f.imm;
+      break;
+    case FO_JMP: next = nrip + f.imm; break;
+    case FO_CALL:
+      res = nrip;
+      next = nrip + f.imm;
+      break;
+    case FO_RET: next = b; break;
+    case FO_MOVX: {
+      const u32 szb = fo_szb(f);
+      b &= szmask(szb);
+      res = sub ? sext(b, szb) : b;
+      break;
+    }
+    case FO_SHIFT: res = shift_op(sub, a, (u32)f.imm, sz, fl); break;
+    case FO_CMOV:
+      // a false condition still zero-extends a 32-bit destination
+      res = cond(fl, sub) ? b : a;
+      break;
+    case FO_SETCC: res = cond(fl, sub) ? 1 : 0; break;
+    default: break;
+  }
+  // ---- the memory write
+  if (F & FF_MW) {
+    const u32 wsz = (F & FF_PUSH) ? 8 : sz;
+    if (!mp) {
+      mp = fxlate(L, addr, wsz, ACC_W);
+      if (!mp) return X_FAULT;
+    }
+    store_le(mp, wsz, res & szmask(wsz));
+    L.pend += wsz;
+  }
+  // ---- commit
+  if (F & FF_PUSH) RS(L, 4, rsp - 8);
+  if (F & FF_POP) RS(L, 4, rsp + 8 + (op == FO_RET ? f.imm : 0));
+  if (F & FF_WRA) wr(L, fo_ra(f), sz, res);
+  if (F & FF_FLAGS) L.rflags = fl;
+  return X_OK;
 }
 
 }  // namespace wtfgpu_dev
