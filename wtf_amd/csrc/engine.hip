@@ -1068,9 +1068,10 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
   HIPCHK(hipSetDevice(c->device));
   free_lanes(c);
   const u64 N = nlanes;
-  // lanes per wave: full waves once there are >= 2 per SIMD (256 CUs x 4),
-  // otherwise fewer lanes per wave and more waves (overridable: WTFGPU_LPW)
-  u32 lpw = N >= 2ull * 1024 * 64 ? 64 : (N >= 2ull * 1024 * 32 ? 32 : 16);
+  // lanes per wave: 64. Measured on MI355X (SYN, 64K lanes): 32 and 16 lanes
+  // per wave take 2x / 4x the time: the step loop's cost is per wave-step,
+  // more resident waves do not overlap it (WTFGPU_LPW overrides, for tests)
+  u32 lpw = 64;
   if (const char *e = getenv("WTFGPU_LPW")) {
     const u32 v = (u32)atoi(e);
     if (v == 64 || v == 32 || v == 16) lpw = v;
