@@ -177,7 +177,7 @@ def main():
         rs = eng.run()
         ex = eng.exits_np()
         ok = int(np.count_nonzero(ex["status"] == EXIT_BREAKPOINT))
-        cov, _ovf = eng.coverage(cap=1 << 23)
+        cov, _ovf = eng.coverage()
         new = set()
         for s in cov.values():
             new |= s

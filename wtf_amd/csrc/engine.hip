@@ -164,11 +164,22 @@ __device__ __forceinline__ void fetch_bytes(u64 pageptr, u32 off, u32 n, u64 &lo
 // logged for it in this launch.
 constexpr u32 UC_N = 64;  // entries per wave (power of two)
 constexpr u32 UC_BP = 1, UC_COVERED = 2, UC_CROSS = 4, UC_BADLEN = 8, UC_UNSUP = 16;
-struct UCEntry {
+struct UCHead {
   u64 key;
   u64 logged;
   u32 flags, pad;
   FOp f;
+};
+struct UCEntry {
+  union {
+    UCHead h;
+    struct {
+      u64 key;
+      u64 logged;
+      u32 flags, pad;
+      FOp f;
+    };
+  };
   UOp u;
 };
 static_assert(sizeof(UOp) % 4 == 0 && sizeof(FOp) % 4 == 0, "copied as dwords");
@@ -390,7 +401,7 @@ __device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr
 // ---------------------------------------------------------------- main kernel
 // One hardware wave runs P.lpw lanes (64, or 32 / 16 to put more waves on
 // each SIMD when the batch is small: the step loop is latency-bound).
-__global__ __launch_bounds__(256) void k_run(Dev P, u32 first, u32 count, u64 max_steps) {
+__global__ __launch_bounds__(256, 2) void k_run(Dev P, u32 first, u32 count, u64 max_steps) {
   const u32 lid = threadIdx.x & 63;
   const u32 hw = rfl32(blockIdx.x * 4 + (threadIdx.x >> 6));  // hardware wave in the launch (uniform)
   const u32 tid = hw * P.lpw + lid;
@@ -446,12 +457,14 @@ __global__ __launch_bounds__(256) void k_run(Dev P, u32 first, u32 count, u64 ma
       const bool ing = cand && L.cptr == lptr;
       const u64 key = lptr | (grip & 0xfff);
       UCEntry *e = &uc[uc_slot(key)];
-      if (rfl64(e->key) != key) break;
-      const u32 flags = rfl32(e->flags);
+      // one LDS round trip: key, logged mask, flags and the FOp are contiguous
+      UCHead h;
+      lds_uniform_read(&e->h, h);
+      if (h.key != key) break;
+      const u32 flags = h.flags;
       if (flags & (UC_BP | UC_CROSS | UC_BADLEN | UC_UNSUP)) break;
-      if (P.cov_rip && !(flags & UC_COVERED) && (__ballot(ing) & ~rfl64(e->logged))) break;
-      FOp f;
-      lds_uniform_read(&e->f, f);
+      if (P.cov_rip && !(flags & UC_COVERED) && (__ballot(ing) & ~h.logged)) break;
+      const FOp &f = h.f;
       if (fo_op(f) == FO_GENERIC) break;
       steps++;
       have = false;

@@ -164,21 +164,25 @@ class Engine:
         _chk(self.L.wtfgpu_read_dirty(self.ctx, lane, arr, cap, C.byref(n)), "read_dirty")
         return list(arr[: min(n.value, cap)])
 
-    def coverage(self, first=0, count=None, cap=1 << 22):
-        """{lane: set(rips)} of rips absent from the coverage map when executed."""
+    def coverage(self, first=0, count=None, cap=None):
+        """{lane: set(rips)} of rips absent from the coverage map when executed
+        (a first call sizes the buffers: after warm-up the log is usually empty)."""
         count = self.nlanes - first if count is None else count
-        lanes = np.zeros(cap, dtype=np.uint32)
-        rips = np.zeros(cap, dtype=np.uint64)
         n = C.c_uint64()
         ovf = C.c_uint32()
-        _chk(self.L.wtfgpu_read_coverage(self.ctx, first, count, lanes.ctypes.data_as(C.POINTER(C.c_uint32)),
-                                         rips.ctypes.data_as(C.POINTER(C.c_uint64)), cap, C.byref(n),
-                                         C.byref(ovf)), "read_coverage")
-        if n.value > cap:
-            raise EngineError("coverage buffer too small")
+        dummy_l, dummy_r = (C.c_uint32 * 1)(), (C.c_uint64 * 1)()
+        _chk(self.L.wtfgpu_read_coverage(self.ctx, first, count, dummy_l, dummy_r, 0, C.byref(n), C.byref(ovf)),
+             "read_coverage")
         out: dict[int, set] = {}
-        for ln, rp in zip(lanes[: n.value].tolist(), rips[: n.value].tolist()):
-            out.setdefault(ln, set()).add(rp)
+        total = n.value
+        if total:
+            lanes = np.zeros(total, dtype=np.uint32)
+            rips = np.zeros(total, dtype=np.uint64)
+            _chk(self.L.wtfgpu_read_coverage(self.ctx, first, count, lanes.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                             rips.ctypes.data_as(C.POINTER(C.c_uint64)), total, C.byref(n),
+                                             C.byref(ovf)), "read_coverage")
+            for ln, rp in zip(lanes.tolist(), rips.tolist()):
+                out.setdefault(ln, set()).add(rp)
         return out, bool(ovf.value)
 
     def commit_coverage(self, rips):
