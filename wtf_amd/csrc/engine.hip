@@ -401,7 +401,23 @@ __device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr
 // ---------------------------------------------------------------- main kernel
 // One hardware wave runs P.lpw lanes (64, or 32 / 16 to put more waves on
 // each SIMD when the batch is small: the step loop is latency-bound).
-__global__ __launch_bounds__(256, 2) void k_run(Dev P, u32 first, u32 count, u64 max_steps) {
+// Build knobs (measured variants): WTFGPU_KRUN_WAVES = the
+// minimum waves per SIMD the register allocation must allow; WTFGPU_P_BYREF =
+// P read from device memory instead of the by-value kernel argument (which is
+// copied to scratch because the rare-path functions take it by reference).
+#ifndef WTFGPU_KRUN_WAVES
+#define WTFGPU_KRUN_WAVES 2
+#endif
+#ifndef WTFGPU_P_BYREF
+#define WTFGPU_P_BYREF 0
+#endif
+#if WTFGPU_P_BYREF
+__global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(const Dev *__restrict__ Pp, u32 first, u32 count,
+                                                                u64 max_steps) {
+  const Dev &P = *Pp;
+#else
+__global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first, u32 count, u64 max_steps) {
+#endif
   const u32 lid = threadIdx.x & 63;
   const u32 hw = rfl32(blockIdx.x * 4 + (threadIdx.x >> 6));  // hardware wave in the launch (uniform)
   const u32 tid = hw * P.lpw + lid;
@@ -873,6 +889,7 @@ struct wtfgpu_ctx {
   u64 *d_stat = nullptr;
   InitState *d_init = nullptr;
   wtfgpu_regs_t *d_init_full = nullptr;  // initial architectural state, copied per lane by k_restore
+  Dev *d_dev = nullptr;                  // device copy of P for k_run
   wtfgpu_regs_t initial{};
   bool have_initial = false;
   u8 *d_scratch = nullptr;
@@ -978,7 +995,8 @@ int wtfgpu_create(int device, wtfgpu_ctx **out) {
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIPCHK(hipEventCreate(&c->ev0));
   HIPCHK(hipEventCreate(&c->ev1));
-  if (dalloc(&c->d_stat, 16) || dalloc(&c->d_init, 1) || dalloc(&c->d_init_full, 1)) return WTFGPU_ERR_OOM;
+  if (dalloc(&c->d_stat, 16) || dalloc(&c->d_init, 1) || dalloc(&c->d_init_full, 1) || dalloc(&c->d_dev, 1))
+    return WTFGPU_ERR_OOM;
   *out = c;
   return WTFGPU_OK;
 }
@@ -1023,6 +1041,7 @@ int wtfgpu_destroy(wtfgpu_ctx *c) {
   dfree(c->d_stat);
   dfree(c->d_init);
   dfree(c->d_init_full);
+  dfree(c->d_dev);
   dfree(c->d_scratch);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -1445,7 +1464,12 @@ int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps
     HIPCHK(hipMemsetAsync(c->d_stat, 0, 16 * 8, c->stream));
     HIPCHK(hipEventRecord(c->ev0, c->stream));
     const u32 hwaves = (count + c->P.lpw - 1) / c->P.lpw;
+    HIPCHK(hipMemcpyAsync(c->d_dev, &c->P, sizeof(Dev), hipMemcpyHostToDevice, c->stream));
+#if WTFGPU_P_BYREF
+    k_run<<<(hwaves + 3) / 4, 256, 0, c->stream>>>(c->d_dev, first, count, steps);
+#else
     k_run<<<(hwaves + 3) / 4, 256, 0, c->stream>>>(c->P, first, count, steps);
+#endif
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev1, c->stream));
     u64 s[16];
