@@ -211,6 +211,22 @@ typedef struct wtfgpu_write {
 int wtfgpu_apply_writes(wtfgpu_ctx *ctx, const wtfgpu_write_t *writes, uint32_t n,
                         const uint8_t *data, uint64_t data_len, int32_t *status_out);
 
+/* Same, with gva read as a guest physical address (PhysWrite, backend.cc:16-28). */
+int wtfgpu_apply_phys_writes(wtfgpu_ctx *ctx, const wtfgpu_write_t *writes, uint32_t n, const uint8_t *data,
+                             uint64_t data_len, int32_t *status_out);
+
+/* Bulk services for breakpoint handling of many lanes per round trip
+ * (the batched form of Get/SetReg and of the dirty-page and PhysTranslate views,
+ * bochscpu_backend.cc:1124-1190, :887-900):
+ * gprs + rip + rflags (18 u64 per lane) of a lane list, read / written;
+ * dirty lists: out[i * (overlay_pages + 1)] = count, then the gpfns;
+ * pages: the lane's current view of each (lane, gpa) page, 4096 bytes each. */
+int wtfgpu_read_gprs_list(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, uint64_t *out18);
+int wtfgpu_write_gprs_list(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, const uint64_t *in18);
+int wtfgpu_read_dirty_list(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, uint32_t *out);
+uint32_t wtfgpu_overlay_pages(wtfgpu_ctx *ctx);
+int wtfgpu_gather_pages(wtfgpu_ctx *ctx, const uint32_t *lanes, const uint64_t *gpas, uint32_t n, uint8_t *out);
+
 /* Dirty GPAs (page aligned) of one lane; *n gets the count (may exceed cap). */
 int wtfgpu_read_dirty(wtfgpu_ctx *ctx, uint32_t lane, uint64_t *gpas, uint32_t cap, uint32_t *n);
 

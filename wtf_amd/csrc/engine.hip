@@ -719,7 +719,7 @@ __device__ __forceinline__ bool lane_phys_write(const Dev &P, Lane &L, u64 gpa, 
 }
 
 __global__ void k_apply_writes(Dev P, const WriteRec *recs, const u32 *starts, u32 nlanes_w, const u8 *data,
-                               i32 *status_out) {
+                               i32 *status_out, u32 phys) {
   const u32 t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nlanes_w) return;
   const u32 r0 = starts[t], r1 = starts[t + 1];
@@ -735,8 +735,8 @@ __global__ void k_apply_writes(Dev P, const WriteRec *recs, const u32 *starts, u
       const u64 off = va & 0xfff;
       u64 n = 4096 - off;
       if (n > left) n = left;
-      u64 gpa;
-      if (!host_walk(P, L, va, gpa)) {
+      u64 gpa = va;
+      if (!phys && !host_walk(P, L, va, gpa)) {
         st = WTFGPU_ERR_TRANSLATE;
         break;
       }
@@ -799,6 +799,48 @@ __global__ void k_lane_mem(Dev P, u32 lane, u32 op, u64 addr, u64 len, u8 *buf, 
     P.ov_count[lane] = L.ovn;
   }
   *result = rc;
+}
+
+// ---------------------------------------------------------------- bulk lane services
+// GPRs + rip + rflags (18 u64, that order) of a lane list, gathered / scattered.
+__global__ void k_gather_gprs(Dev P, const u32 *lanes, u32 n, u64 *out) {
+  const u32 t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const u64 N = P.nlanes, l = lanes[t];
+  for (int i = 0; i < 16; i++) out[(u64)t * 18 + i] = P.gpr[i * N + l];
+  out[(u64)t * 18 + 16] = P.rip[l];
+  out[(u64)t * 18 + 17] = P.rflags[l];
+}
+__global__ void k_scatter_gprs(Dev P, const u32 *lanes, u32 n, const u64 *in) {
+  const u32 t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const u64 N = P.nlanes, l = lanes[t];
+  for (int i = 0; i < 16; i++) P.gpr[i * N + l] = in[(u64)t * 18 + i];
+  P.rip[l] = in[(u64)t * 18 + 16];
+  P.rflags[l] = in[(u64)t * 18 + 17];
+}
+// Dirty lists of a lane list: out[t * (K + 1)] = count, then the gpfns.
+__global__ void k_gather_dirty(Dev P, const u32 *lanes, u32 n, u32 *out) {
+  const u32 t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const u32 l = lanes[t], cnt = P.ov_count[l];
+  u32 *o = out + (u64)t * (P.K + 1);
+  o[0] = cnt;
+  for (u32 k = 0; k < cnt && k < P.K; k++) o[1 + k] = P.ov_gpfn[(u64)k * P.nlanes + l];
+}
+// Lane views of physical pages (overlay copy, else snapshot, else zeros): one
+// 256-thread block per (lane, gpa) request, 16 bytes per thread.
+__global__ void k_gather_pages(Dev P, const u32 *lanes, const u64 *gpas, u32 n, u8 *out) {
+  const u32 r = blockIdx.x;
+  if (r >= n) return;
+  const u32 l = lanes[r];
+  const u64 gpfn = gpas[r] >> 12;
+  const u32 ovn = P.ov_count[l];
+  u64 bloom = 0;
+  for (u32 k = 0; k < ovn; k++) bloom |= bloom_bit(P.ov_gpfn[(u64)k * P.nlanes + l]);
+  bool priv;
+  const uint4 *src = (const uint4 *)phys_page(P, l, ovn, bloom, gpfn, priv);
+  ((uint4 *)(out + (u64)r * WTFGPU_PAGE_SIZE))[threadIdx.x] = src[threadIdx.x];
 }
 
 // ---------------------------------------------------------------- coverage services
@@ -1538,8 +1580,8 @@ int wtfgpu_lane_write_virt(wtfgpu_ctx *c, uint32_t lane, uint64_t gva, const voi
   return rc ? rc : (r == -2 ? WTFGPU_ERR_OOM : (r < 0 ? WTFGPU_ERR_TRANSLATE : WTFGPU_OK));
 }
 
-int wtfgpu_apply_writes(wtfgpu_ctx *c, const wtfgpu_write_t *writes, uint32_t n, const uint8_t *data,
-                        uint64_t data_len, int32_t *status_out) {
+static int apply_writes(wtfgpu_ctx *c, const wtfgpu_write_t *writes, uint32_t n, const uint8_t *data,
+                        uint64_t data_len, int32_t *status_out, u32 phys) {
   if (!c || (n && (!writes || !data))) return WTFGPU_ERR_INVALID;
   if (n == 0) return WTFGPU_OK;
   HIPCHK(hipSetDevice(c->device));
@@ -1567,7 +1609,7 @@ int wtfgpu_apply_writes(wtfgpu_ctx *c, const wtfgpu_write_t *writes, uint32_t n,
   HIPCHK(hipMemcpyAsync(c->d_scratch + o_data, data, data_len, hipMemcpyHostToDevice, c->stream));
   k_apply_writes<<<(nl + 63) / 64, 64, 0, c->stream>>>(c->P, (const WriteRec *)c->d_scratch,
                                                        (const u32 *)(c->d_scratch + o_starts), nl,
-                                                       c->d_scratch + o_data, (i32 *)(c->d_scratch + o_st));
+                                                       c->d_scratch + o_data, (i32 *)(c->d_scratch + o_st), phys);
   HIPCHK(hipGetLastError());
   std::vector<i32> st(n);
   HIPCHK(hipMemcpyAsync(st.data(), c->d_scratch + o_st, b_st, hipMemcpyDeviceToHost, c->stream));
@@ -1578,6 +1620,87 @@ int wtfgpu_apply_writes(wtfgpu_ctx *c, const wtfgpu_write_t *writes, uint32_t n,
     if (st[i]) rc = st[i];
   }
   return rc;
+}
+
+int wtfgpu_apply_writes(wtfgpu_ctx *c, const wtfgpu_write_t *writes, uint32_t n, const uint8_t *data,
+                        uint64_t data_len, int32_t *status_out) {
+  return apply_writes(c, writes, n, data, data_len, status_out, 0);
+}
+int wtfgpu_apply_phys_writes(wtfgpu_ctx *c, const wtfgpu_write_t *writes, uint32_t n, const uint8_t *data,
+                             uint64_t data_len, int32_t *status_out) {
+  return apply_writes(c, writes, n, data, data_len, status_out, 1);
+}
+
+static int check_lane_list(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n) {
+  if (!c || !c->d_gpr || (n && !lanes)) return WTFGPU_ERR_INVALID;
+  for (uint32_t i = 0; i < n; i++)
+    if (lanes[i] >= c->P.nlanes) return WTFGPU_ERR_INVALID;
+  return WTFGPU_OK;
+}
+
+int wtfgpu_read_gprs_list(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, uint64_t *out18) {
+  if (int rc = check_lane_list(c, lanes, n)) return rc;
+  if (n == 0) return WTFGPU_OK;
+  HIPCHK(hipSetDevice(c->device));
+  const u64 o_out = ((u64)n * 4 + 255) & ~255ull;
+  if (ensure_scratch(c, o_out + (u64)n * 18 * 8)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemcpyAsync(c->d_scratch, lanes, (u64)n * 4, hipMemcpyHostToDevice, c->stream));
+  k_gather_gprs<<<(n + 255) / 256, 256, 0, c->stream>>>(c->P, (const u32 *)c->d_scratch, n,
+                                                         (u64 *)(c->d_scratch + o_out));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out18, c->d_scratch + o_out, (u64)n * 18 * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_write_gprs_list(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, const uint64_t *in18) {
+  if (int rc = check_lane_list(c, lanes, n)) return rc;
+  if (n == 0) return WTFGPU_OK;
+  HIPCHK(hipSetDevice(c->device));
+  const u64 o_in = ((u64)n * 4 + 255) & ~255ull;
+  if (ensure_scratch(c, o_in + (u64)n * 18 * 8)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemcpyAsync(c->d_scratch, lanes, (u64)n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_scratch + o_in, in18, (u64)n * 18 * 8, hipMemcpyHostToDevice, c->stream));
+  k_scatter_gprs<<<(n + 255) / 256, 256, 0, c->stream>>>(c->P, (const u32 *)c->d_scratch, n,
+                                                          (const u64 *)(c->d_scratch + o_in));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_read_dirty_list(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, uint32_t *out) {
+  if (int rc = check_lane_list(c, lanes, n)) return rc;
+  if (n == 0) return WTFGPU_OK;
+  HIPCHK(hipSetDevice(c->device));
+  const u64 stride = (u64)c->P.K + 1;
+  const u64 o_out = ((u64)n * 4 + 255) & ~255ull;
+  if (ensure_scratch(c, o_out + (u64)n * stride * 4)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemcpyAsync(c->d_scratch, lanes, (u64)n * 4, hipMemcpyHostToDevice, c->stream));
+  k_gather_dirty<<<(n + 255) / 256, 256, 0, c->stream>>>(c->P, (const u32 *)c->d_scratch, n,
+                                                          (u32 *)(c->d_scratch + o_out));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, c->d_scratch + o_out, (u64)n * stride * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+uint32_t wtfgpu_overlay_pages(wtfgpu_ctx *c) { return c ? c->P.K : 0; }
+
+int wtfgpu_gather_pages(wtfgpu_ctx *c, const uint32_t *lanes, const uint64_t *gpas, uint32_t n, uint8_t *out) {
+  if (int rc = check_lane_list(c, lanes, n)) return rc;
+  if (n == 0) return WTFGPU_OK;
+  if (!gpas || !out || !c->P.pool) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  const u64 o_gpa = ((u64)n * 4 + 255) & ~255ull, o_out = (o_gpa + (u64)n * 8 + 4095) & ~4095ull;
+  if (ensure_scratch(c, o_out + (u64)n * WTFGPU_PAGE_SIZE)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemcpyAsync(c->d_scratch, lanes, (u64)n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_scratch + o_gpa, gpas, (u64)n * 8, hipMemcpyHostToDevice, c->stream));
+  k_gather_pages<<<n, 256, 0, c->stream>>>(c->P, (const u32 *)c->d_scratch, (const u64 *)(c->d_scratch + o_gpa), n,
+                                           c->d_scratch + o_out);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, c->d_scratch + o_out, (u64)n * WTFGPU_PAGE_SIZE, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
 }
 
 int wtfgpu_read_dirty(wtfgpu_ctx *c, uint32_t lane, uint64_t *gpas, uint32_t cap, uint32_t *n) {

@@ -1,0 +1,340 @@
+// wtf_api.h — the wtf host interface the gpu backend and fuzzer modules are
+// written against, restated for building this repository on its own.
+//
+// The names, member signatures and semantics follow the reference so that a
+// module source written for wtf compiles unchanged against this header and a
+// maintainer can drop `gpu_backend.{h,cc}` into upstream wtf next to
+// `bochscpu_backend`:
+//   Gva_t / Gpa_t               src/wtf/gxa.h:10-53
+//   TestcaseResult_t            src/wtf/backend.h:12-31
+//   Registers_t, MemoryValidate_t, BreakpointHandler_t   backend.h:110-154
+//   Backend_t                   backend.h:161-602, helpers backend.cc:16-332
+//   CpuState_t, Options_t       src/wtf/globals.h:1020-1385 (fields this path uses)
+//   Target_t / Targets_t        src/wtf/targets.h:14-48, targets.cc:11-38
+//   Debugger_t (Linux)          src/wtf/debugger.h:346-388 (symbol-store.json)
+// Coverage sets use std::unordered_set where the reference uses tsl::robin_set
+// (same interface for the members modules call).
+#pragma once
+#include <cstdint>
+#include <cstring>
+#include <filesystem>
+#include <functional>
+#include <memory>
+#include <optional>
+#include <random>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <unordered_set>
+#include <variant>
+#include <vector>
+
+namespace fs = std::filesystem;
+
+namespace Page {
+constexpr uint64_t Size = 0x1000;
+}
+
+// ------------------------------------------------------------------ addresses
+template <typename Tag>
+class Address_t {
+  uint64_t v_ = 0;
+
+ public:
+  Address_t() = default;
+  explicit Address_t(const uint64_t V) : v_(V) {}
+  uint64_t U64() const { return v_; }
+  Address_t Offset() const { return Address_t(v_ & 0xfff); }
+  Address_t Align() const { return Address_t(v_ & ~0xfffull); }
+  explicit operator bool() const { return v_ != 0; }
+  bool operator==(const Address_t &O) const { return v_ == O.v_; }
+  bool operator!=(const Address_t &O) const { return v_ != O.v_; }
+  bool operator<(const Address_t &O) const { return v_ < O.v_; }
+  Address_t operator+(const Address_t &O) const { return Address_t(v_ + O.v_); }
+  Address_t operator-(const Address_t &O) const { return Address_t(v_ - O.v_); }
+  Address_t operator*(const Address_t &O) const { return Address_t(v_ * O.v_); }
+  Address_t &operator+=(const Address_t &O) {
+    v_ += O.v_;
+    return *this;
+  }
+  uint64_t *operator&() { return &v_; }
+};
+using Gva_t = Address_t<struct GvaTag_t>;
+using Gpa_t = Address_t<struct GpaTag_t>;
+
+template <typename Tag>
+struct std::hash<Address_t<Tag>> {
+  size_t operator()(const Address_t<Tag> &A) const noexcept { return std::hash<uint64_t>()(A.U64()); }
+};
+
+// ------------------------------------------------------------------ results
+struct Ok_t {
+  constexpr std::string_view Name() const { return "ok"; }
+};
+struct Timedout_t {
+  constexpr std::string_view Name() const { return "timedout"; }
+};
+struct Cr3Change_t {
+  constexpr std::string_view Name() const { return "cr3"; }
+};
+struct Crash_t {
+  std::string CrashName;
+  Crash_t() = default;
+  explicit Crash_t(const std::string &Name) : CrashName(Name) {}
+  std::string_view Name() const { return "crash"; }
+};
+using TestcaseResult_t = std::variant<Ok_t, Timedout_t, Cr3Change_t, Crash_t>;
+
+enum PfError_t {
+  ErrorPresent = 1 << 0,
+  ErrorWrite = 1 << 1,
+  ErrorUser = 1 << 2,
+  ErrorReservedWrite = 1 << 3,
+  ErrorInstructionFetch = 1 << 4
+};
+
+enum class MemoryValidate_t : uint32_t {
+  ValidateRead = 1,
+  ValidateWrite = 2,
+  ValidateExecute = 4,
+  ValidateReadWrite = 3,
+  ValidateReadExecute = 5
+};
+inline bool operator&(const MemoryValidate_t &A, const MemoryValidate_t &B) {
+  return (uint32_t(A) & uint32_t(B)) != 0;
+}
+
+// Order as in the reference (backend.h:133-154).
+enum class Registers_t : uint32_t {
+  Rax, Rbx, Rcx, Rdx, Rsi, Rdi, Rip, Rsp, Rbp,
+  R8, R9, R10, R11, R12, R13, R14, R15, Rflags, Cr2, Cr3
+};
+
+enum class TraceType_t { NoTrace, Rip, UniqueRip, Tenet };
+enum class BackendType_t { Bochscpu, Whv, Kvm, Gpu };
+
+// ------------------------------------------------------------------ cpu state
+struct Seg_t {
+  bool Present = false;
+  uint16_t Selector = 0;
+  uint64_t Base = 0;
+  uint32_t Limit = 0;
+  uint16_t Attr = 0;
+  // bits 8-11 of Attr mirror Limit bits 16-19 (utils.cc:234-243)
+  uint16_t Reserved() const { return (Attr >> 8) & 0xf; }
+  bool operator==(const Seg_t &) const = default;
+};
+struct GlobalSeg_t {
+  uint64_t Base = 0;
+  uint16_t Limit = 0;
+  bool operator==(const GlobalSeg_t &) const = default;
+};
+struct FlagsReg_t {  // Cr0_t / Cr4_t / Efer_t expose .Flags (globals.h)
+  uint64_t Flags = 0;
+  bool operator==(const FlagsReg_t &) const = default;
+};
+struct Zmm_t {
+  uint64_t Q[8] = {};
+  bool operator==(const Zmm_t &) const = default;
+};
+
+struct CpuState_t {
+  uint64_t Seed = 0;
+  uint64_t Rax = 0, Rcx = 0, Rdx = 0, Rbx = 0, Rsp = 0, Rbp = 0, Rsi = 0, Rdi = 0;
+  uint64_t R8 = 0, R9 = 0, R10 = 0, R11 = 0, R12 = 0, R13 = 0, R14 = 0, R15 = 0;
+  uint64_t Rip = 0, Rflags = 0;
+  Seg_t Es, Cs, Ss, Ds, Fs, Gs, Ldtr, Tr;
+  GlobalSeg_t Gdtr, Idtr;
+  FlagsReg_t Cr0;
+  uint64_t Cr2 = 0, Cr3 = 0;
+  FlagsReg_t Cr4;
+  uint64_t Cr8 = 0;
+  uint64_t Dr0 = 0, Dr1 = 0, Dr2 = 0, Dr3 = 0;
+  uint32_t Dr6 = 0, Dr7 = 0;
+  uint32_t Xcr0 = 0;
+  Zmm_t Zmm[32];
+  uint16_t Fpcw = 0, Fpsw = 0, Fptw = 0, Fpop = 0;
+  uint64_t Fpst[8] = {};
+  uint32_t Mxcsr = 0, MxcsrMask = 0;
+  uint64_t Tsc = 0;
+  FlagsReg_t Efer;
+  uint64_t KernelGsBase = 0, ApicBase = 0, Pat = 0;
+  uint64_t SysenterCs = 0, SysenterEip = 0, SysenterEsp = 0;
+  uint64_t Star = 0, Lstar = 0, Cstar = 0, Sfmask = 0, TscAux = 0;
+  bool operator==(const CpuState_t &) const = default;
+};
+
+struct RunOptions_t {
+  fs::path BaseTracePath;
+  TraceType_t TraceType = TraceType_t::NoTrace;
+  fs::path InputPath;
+  uint64_t Runs = 0;
+};
+struct FuzzOptions_t {
+  fs::path TargetPath;
+  uint32_t Seed = 0;
+  std::string Address;
+};
+
+struct Options_t {
+  bool Verbose = false;
+  BackendType_t Backend = BackendType_t::Gpu;
+  std::string TargetName;
+  fs::path StatePath, DumpPath, CpuStatePath, SymbolFilePath, GuestFilesPath, CoveragePath;
+  uint64_t Limit = 0;
+  CpuState_t CpuState;
+  bool Edges = false;
+  RunOptions_t Run;
+  FuzzOptions_t Fuzz;
+  // gpu backend knobs (new): device, lanes per batch, copy-on-write pages per lane
+  int GpuDevice = 0;
+  uint32_t GpuLanes = 1;
+  uint32_t GpuOverlayPages = 32;
+};
+
+// ------------------------------------------------------------------ backend
+class Backend_t;
+using BreakpointHandler_t = void (*)(Backend_t *);
+
+class Backend_t {
+ public:
+  virtual ~Backend_t() = default;
+
+  // pure virtuals (backend.h:171-263, 583-589)
+  virtual bool Initialize(const Options_t &Opts, const CpuState_t &CpuState) = 0;
+  virtual std::optional<TestcaseResult_t> Run(const uint8_t *Buffer, const uint64_t BufferSize) = 0;
+  virtual bool Restore(const CpuState_t &CpuState) = 0;
+  virtual void Stop(const TestcaseResult_t &Res) = 0;
+  virtual void SetLimit(const uint64_t Limit) = 0;
+  virtual uint64_t GetReg(const Registers_t Reg) = 0;
+  virtual uint64_t SetReg(const Registers_t Reg, const uint64_t Value) = 0;
+  virtual uint64_t Rdrand() = 0;
+  virtual void PrintRunStats() = 0;
+  virtual bool SetTraceFile(const fs::path &TestcaseTracePath, const TraceType_t TraceType);
+  virtual bool SetBreakpoint(const Gva_t Gva, const BreakpointHandler_t Handler) = 0;
+  virtual bool DirtyGpa(const Gpa_t Gpa) = 0;
+  virtual bool VirtTranslate(const Gva_t Gva, Gpa_t &Gpa, const MemoryValidate_t Validate) const = 0;
+  virtual uint8_t *PhysTranslate(const Gpa_t Gpa) const = 0;
+  virtual bool PageFaultsMemoryIfNeeded(const Gva_t Gva, const uint64_t Size) = 0;
+  virtual const std::unordered_set<Gva_t> &LastNewCoverage() const = 0;
+  virtual bool RevokeLastNewCoverage() = 0;
+
+  // helpers implemented on top of the virtuals (backend.cc)
+  bool SaveCrash(const Gva_t ExceptionAddress, const uint32_t ExceptionCode);
+  bool SetBreakpoint(const char *Symbol, const BreakpointHandler_t Handler);
+  bool SetCrashBreakpoint(const char *Symbol);
+  bool SetCrashBreakpoint(const Gva_t Gva);
+  bool PhysWrite(const Gpa_t Gpa, const uint8_t *Buffer, const uint64_t BufferSize, const bool Dirty = false);
+  bool VirtRead(const Gva_t Gva, uint8_t *Buffer, const uint64_t BufferSize) const;
+  template <typename Ty>
+  bool VirtReadStruct(const Gva_t Gva, const Ty *Buffer) const {
+    return VirtRead(Gva, (uint8_t *)Buffer, sizeof(Ty));
+  }
+  uint32_t VirtRead4(const Gva_t Gva) const;
+  uint64_t VirtRead8(const Gva_t Gva) const;
+  Gva_t VirtReadGva(const Gva_t Gva) const;
+  Gpa_t VirtReadGpa(const Gva_t Gva) const;
+  std::string VirtReadString(const Gva_t Gva, const uint64_t MaxLength = 256) const;
+  std::u16string VirtReadWideString(const Gva_t Gva, const uint64_t MaxLength = 256) const;
+  bool VirtWrite(const Gva_t Gva, const uint8_t *Buffer, const uint64_t BufferSize, const bool Dirty = false);
+  template <typename Ty>
+  bool VirtWriteStruct(const Gva_t Gva, const Ty *Buffer) {
+    return VirtWrite(Gva, (uint8_t *)Buffer, sizeof(Ty));
+  }
+  bool VirtWriteDirty(const Gva_t Gva, const uint8_t *Buffer, const uint64_t BufferSize);
+  template <typename Ty>
+  bool VirtWriteStructDirty(const Gva_t Gva, const Ty *Buffer) {
+    return VirtWriteDirty(Gva, (uint8_t *)Buffer, sizeof(Ty));
+  }
+  bool SimulateReturnFromFunction(const uint64_t Return);
+  bool SimulateReturnFrom32bitFunction(const uint32_t Return, const uint32_t StdcallArgsCount = 0);
+  uint64_t GetArg(const uint64_t Idx);
+  Gva_t GetArgGva(const uint64_t Idx);
+  Gva_t GetArgAddress(const uint64_t Idx);
+  std::pair<uint64_t, Gva_t> GetArgAndAddress(const uint64_t Idx);
+  std::pair<Gva_t, Gva_t> GetArgAndAddressGva(const uint64_t Idx);
+
+#define WTF_REG_ACCESSORS(Name)                                   \
+  uint64_t Name() { return GetReg(Registers_t::Name); }           \
+  void Name(const uint64_t V) { SetReg(Registers_t::Name, V); }   \
+  void Name(const Gva_t V) { SetReg(Registers_t::Name, V.U64()); }
+  WTF_REG_ACCESSORS(Rsp)
+  WTF_REG_ACCESSORS(Rbp)
+  WTF_REG_ACCESSORS(Rip)
+  WTF_REG_ACCESSORS(Rax)
+  WTF_REG_ACCESSORS(Rbx)
+  WTF_REG_ACCESSORS(Rcx)
+  WTF_REG_ACCESSORS(Rdx)
+  WTF_REG_ACCESSORS(Rsi)
+  WTF_REG_ACCESSORS(Rdi)
+  WTF_REG_ACCESSORS(R8)
+  WTF_REG_ACCESSORS(R9)
+  WTF_REG_ACCESSORS(R10)
+  WTF_REG_ACCESSORS(R11)
+  WTF_REG_ACCESSORS(R12)
+  WTF_REG_ACCESSORS(R13)
+  WTF_REG_ACCESSORS(R14)
+  WTF_REG_ACCESSORS(R15)
+#undef WTF_REG_ACCESSORS
+  void PrintRegisters();
+};
+
+extern Backend_t *g_Backend;
+
+// ------------------------------------------------------------------ targets
+class Mutator_t;
+struct Corpus_t;
+
+struct Target_t {
+  using Init_t = bool (*)(const Options_t &, const CpuState_t &);
+  using InsertTestcase_t = bool (*)(const uint8_t *, const size_t);
+  using Restore_t = bool (*)();
+  using CreateMutator_t = std::unique_ptr<Mutator_t> (*)(std::mt19937_64 &, const size_t);
+
+  explicit Target_t(const std::string &Name, const Init_t Init, const InsertTestcase_t InsertTestcase,
+                    const Restore_t Restore = []() { return true; }, const CreateMutator_t CreateMutator = nullptr);
+
+  std::string Name;
+  Init_t Init = nullptr;
+  InsertTestcase_t InsertTestcase = nullptr;
+  Restore_t Restore = nullptr;
+  CreateMutator_t CreateMutator = nullptr;
+};
+
+struct Targets_t {
+  std::vector<Target_t> Targets;
+  Target_t *Get(const std::string &Name);
+  void DisplayRegisteredTargets();
+  void Registers(const Target_t &Target);
+  static Targets_t &Instance();
+};
+
+// ------------------------------------------------------------------ symbols
+class Debugger_t {
+  std::unordered_map<std::string, uint64_t> Symbols_;
+
+ public:
+  bool Init(const fs::path &DumpPath, const fs::path &SymbolFilePath);
+  bool AddSymbol(const std::string &Name, const uint64_t Address);
+  uint64_t GetModuleBase(const char *Name) const { return GetSymbol(Name); }
+  // Like the reference, a missing symbol ends the process (debugger.h:368-376).
+  uint64_t GetSymbol(const char *Name) const;
+};
+extern Debugger_t g_Dbg;
+
+// ------------------------------------------------------------------ utils
+std::string_view ExceptionCodeToStr(const uint32_t ExceptionCode);
+bool LoadCpuStateFromJSON(CpuState_t &CpuState, const fs::path &CpuStatePath);
+bool SanitizeCpuState(CpuState_t &CpuState);
+
+// NT status codes used by crash naming (nt.h:256-258 plus the standard ones).
+constexpr uint32_t EXCEPTION_ACCESS_VIOLATION = 0xC0000005;
+constexpr uint32_t EXCEPTION_INT_DIVIDE_BY_ZERO = 0xC0000094;
+constexpr uint32_t EXCEPTION_ILLEGAL_INSTRUCTION = 0xC000001D;
+constexpr uint32_t EXCEPTION_PRIV_INSTRUCTION = 0xC0000096;
+constexpr uint32_t EXCEPTION_BREAKPOINT = 0x80000003;
+constexpr uint32_t STATUS_STACK_BUFFER_OVERRUN = 0xC0000409;
+constexpr uint32_t STATUS_HEAP_CORRUPTION = 0xC0000374;
+constexpr uint32_t EXCEPTION_ACCESS_VIOLATION_READ = 0xCFFFFFFF;
+constexpr uint32_t EXCEPTION_ACCESS_VIOLATION_WRITE = 0xCFFFFFFE;
+constexpr uint32_t EXCEPTION_ACCESS_VIOLATION_EXECUTE = 0xCFFFFFFD;
