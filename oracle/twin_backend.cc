@@ -1,0 +1,289 @@
+// twin_backend.cc — TEST INFRASTRUCTURE ONLY: the CPU twin of the gpu backend.
+//
+// A Backend_t over the scalar oracle (x86_oracle.c), running testcases one
+// after the other exactly as wtf's client loop drives bochscpu
+// (RunTestcaseAndRestore, client.cc:88-180; BochscpuBackend_t::Run /
+// Restore, bochscpu_backend.cc:352-410, 730-797). It runs the same fuzzer
+// modules and the same batched runner as `wtfgpu`, so per-testcase results,
+// retired counts, final registers and coverage sets can be compared lane by
+// lane (tests/test_gpu_tlv.py), and it is the CPU baseline of the TLV bench
+// (one process per host core, bench.py). The product never links this file.
+#include <cstdio>
+#include <cstring>
+#include <unordered_map>
+
+#include "../include/wtfgpu.h"
+#include "../wtf_amd/host/runner.h"
+#include "../wtf_amd/host/wtf_api.h"
+#include "x86_oracle.h"
+#include "../wtf_amd/host/kdmp.h"
+#include "../wtf_amd/host/blake3_lite.h"
+
+using namespace wtfgpu_host;
+
+
+namespace {
+int gpr_index(Registers_t r) {
+  switch (r) {
+    case Registers_t::Rax: return WTFGPU_RAX;
+    case Registers_t::Rbx: return WTFGPU_RBX;
+    case Registers_t::Rcx: return WTFGPU_RCX;
+    case Registers_t::Rdx: return WTFGPU_RDX;
+    case Registers_t::Rsi: return WTFGPU_RSI;
+    case Registers_t::Rdi: return WTFGPU_RDI;
+    case Registers_t::Rsp: return WTFGPU_RSP;
+    case Registers_t::Rbp: return WTFGPU_RBP;
+    case Registers_t::R8: return WTFGPU_R8;
+    case Registers_t::R9: return WTFGPU_R9;
+    case Registers_t::R10: return WTFGPU_R10;
+    case Registers_t::R11: return WTFGPU_R11;
+    case Registers_t::R12: return WTFGPU_R12;
+    case Registers_t::R13: return WTFGPU_R13;
+    case Registers_t::R14: return WTFGPU_R14;
+    case Registers_t::R15: return WTFGPU_R15;
+    default: return -1;
+  }
+}
+}  // namespace
+
+class TwinBackend_t final : public Backend_t, public Executor_t {
+  orc_machine *m_ = nullptr;
+  KernelDump dump_;
+  CpuState_t initial_{};
+  wtfgpu_regs_t regs0_{};
+  std::unordered_map<uint64_t, BreakpointHandler_t> bps_;
+  std::optional<TestcaseResult_t> result_;
+  uint64_t seed_ = 0;
+  struct Staged {
+    std::vector<uint8_t> data, orig;
+  };
+  mutable std::unordered_map<uint64_t, Staged> staged_;
+  std::unordered_set<uint64_t> aggregate_;
+  std::unordered_set<Gva_t> last_new_;
+  uint64_t retired_total_ = 0;
+
+  wtfgpu_regs_t regs() const {
+    wtfgpu_regs_t r;
+    orc_get_regs(m_, &r);
+    return r;
+  }
+  void flush() {
+    for (auto &[gpfn, s] : staged_)
+      if (s.data != s.orig) orc_write_phys(m_, gpfn << 12, s.data.data(), 4096);
+    staged_.clear();
+  }
+
+ public:
+  ~TwinBackend_t() override {
+    if (m_) orc_destroy(m_);
+  }
+  bool Initialize(const Options_t &Opts, const CpuState_t &CpuState) override {
+    if (!dump_.Parse(Opts.DumpPath.string())) return false;
+    m_ = orc_create();
+    for (auto &[gpfn, page] : dump_.Pages()) orc_add_page(m_, gpfn, page);
+    if (Opts.Limit) orc_set_limit(m_, Opts.Limit);
+    return Restore(CpuState);
+  }
+  // bochscpu_backend.cc:352-410 (+ the handler dispatch of :476-548)
+  std::optional<TestcaseResult_t> Run(const uint8_t *, const uint64_t) override {
+    flush();
+    int skip = 0;
+    for (;;) {
+      wtfgpu_exit_t e{};
+      orc_run(m_, skip, &e);
+      skip = 0;
+      if (e.status == WTFGPU_EXIT_BREAKPOINT) {
+        const uint64_t rip0 = regs().rip;
+        auto it = bps_.find(rip0);
+        if (it != bps_.end()) it->second(this);
+        flush();
+        if (result_) break;
+        skip = regs().rip == rip0;  // U10: a moved rip cancels the hooked instruction
+        continue;
+      }
+      const uint32_t cpl = initial_.Cs.Selector & 3;
+      switch (e.status) {
+        case WTFGPU_EXIT_TIMEOUT: result_ = Timedout_t(); break;
+        case WTFGPU_EXIT_INT3:
+        case WTFGPU_EXIT_HLT: result_ = Crash_t(); break;
+        case WTFGPU_EXIT_CR3: result_ = Cr3Change_t(); break;
+        case WTFGPU_EXIT_FAULT: result_ = FaultToResult(e.vector, e.error, e.rip, cpl); break;
+        default: result_ = Crash_t("engine-" + std::to_string(e.status)); break;
+      }
+      break;
+    }
+    // coverage of this testcase against the aggregate (bochscpu_backend.cc:501-504)
+    std::vector<uint64_t> cov(orc_coverage(m_, nullptr, 0));
+    orc_coverage(m_, cov.data(), cov.size());
+    last_new_.clear();
+    if (full_) aggregate_.clear();
+    for (uint64_t r : cov)
+      if (aggregate_.insert(r).second) last_new_.insert(Gva_t(r));
+    retired_total_ += orc_icount(m_);
+    return result_;
+  }
+  bool Restore(const CpuState_t &CpuState) override {
+    initial_ = CpuState;
+    regs0_ = RegsFromCpuState(CpuState);
+    orc_restore(m_, &regs0_);
+    staged_.clear();
+    result_.reset();
+    seed_ = CpuState.Seed;
+    return true;
+  }
+  void Stop(const TestcaseResult_t &Res) override { result_ = Res; }
+  void SetLimit(const uint64_t Limit) override { orc_set_limit(m_, Limit); }
+  uint64_t GetReg(const Registers_t Reg) override {
+    const wtfgpu_regs_t r = regs();
+    const int i = gpr_index(Reg);
+    if (i >= 0) return r.gpr[i];
+    if (Reg == Registers_t::Rip) return r.rip;
+    if (Reg == Registers_t::Rflags) return r.rflags;
+    if (Reg == Registers_t::Cr3) return r.cr3;
+    if (Reg == Registers_t::Cr2) return r.cr2;
+    return 0;
+  }
+  uint64_t SetReg(const Registers_t Reg, const uint64_t Value) override {
+    wtfgpu_regs_t r = regs();
+    const int i = gpr_index(Reg);
+    if (i >= 0) r.gpr[i] = Value;
+    else if (Reg == Registers_t::Rip) r.rip = Value;
+    else if (Reg == Registers_t::Rflags) r.rflags = Value;
+    else return Value;
+    orc_set_regs(m_, &r);
+    return Value;
+  }
+  uint64_t Rdrand() override;
+  void PrintRunStats() override {}
+  bool SetBreakpoint(const Gva_t Gva, const BreakpointHandler_t Handler) override {
+    if (bps_.count(Gva.U64())) return false;
+    bps_[Gva.U64()] = Handler;
+    std::vector<uint64_t> v;
+    for (auto &kv : bps_) v.push_back(kv.first);
+    return orc_set_breakpoints(m_, v.data(), (uint32_t)v.size()) == 0;
+  }
+  using Backend_t::SetBreakpoint;
+  bool DirtyGpa(const Gpa_t) override { return true; }
+  bool VirtTranslate(const Gva_t Gva, Gpa_t &Gpa, const MemoryValidate_t) const override {
+    // the staged pages may hold page-table edits not yet flushed: walk them
+    uint64_t table = regs().cr3 & 0x000ffffffffff000ull;
+    const uint64_t va = Gva.U64();
+    for (int level = 3; level >= 0; level--) {
+      uint64_t e;
+      memcpy(&e, PhysTranslate(Gpa_t(table + ((va >> (12 + 9 * level)) & 0x1ff) * 8)), 8);
+      if (!(e & 1)) return false;
+      const uint64_t frame = e & 0x000ffffffffff000ull;
+      if (level == 2 && (e & 0x80)) {
+        Gpa = Gpa_t((frame & ~0x3fffffffull) | (va & 0x3fffffffull));
+        return true;
+      }
+      if (level == 1 && (e & 0x80)) {
+        Gpa = Gpa_t((frame & ~0x1fffffull) | (va & 0x1fffffull));
+        return true;
+      }
+      table = frame;
+    }
+    Gpa = Gpa_t(table | (va & 0xfff));
+    return true;
+  }
+  uint8_t *PhysTranslate(const Gpa_t Gpa) const override {
+    const uint64_t gpfn = Gpa.U64() >> 12;
+    auto it = staged_.find(gpfn);
+    if (it == staged_.end()) {
+      Staged s;
+      s.data.resize(4096);
+      orc_read_phys(m_, gpfn << 12, s.data.data(), 4096);
+      s.orig = s.data;
+      it = staged_.emplace(gpfn, std::move(s)).first;
+    }
+    return it->second.data.data() + (Gpa.U64() & 0xfff);
+  }
+  bool PageFaultsMemoryIfNeeded(const Gva_t, const uint64_t) override { return false; }
+  const std::unordered_set<Gva_t> &LastNewCoverage() const override { return last_new_; }
+  bool RevokeLastNewCoverage() override {
+    for (const Gva_t &g : last_new_) aggregate_.erase(g.U64());
+    last_new_.clear();
+    return true;
+  }
+
+  // ---- Executor_t: RunTestcaseAndRestore per testcase (client.cc:88-180)
+  Backend_t *AsBackend() override { return this; }
+  uint32_t Lanes() const override { return 1u << 30; }
+  void ResetCoverage() override {
+    aggregate_.clear();
+    last_new_.clear();
+  }
+  bool full_ = false;
+  void SetFullCoverage(bool On) override { full_ = On; }
+  size_t CoverageSize() const override { return aggregate_.size(); }
+  bool RunBatch(const Target_t &Target, const std::vector<std::pair<const uint8_t *, size_t>> &Tc,
+                std::vector<LaneResult> &Out, ModuleSlots *) override {
+    Out.assign(Tc.size(), LaneResult{});
+    g_Backend = this;
+    for (size_t i = 0; i < Tc.size(); i++) {
+      LaneResult &L = Out[i];
+      Restore(initial_);
+      if (!Target.InsertTestcase(Tc[i].first, Tc[i].second)) result_ = Crash_t("insert-testcase-failed");
+      std::optional<TestcaseResult_t> R;
+      if (result_) {
+        R = result_;
+        last_new_.clear();
+      } else {
+        R = Run(Tc[i].first, Tc[i].second);
+      }
+      L.result = *R;
+      if (std::holds_alternative<Timedout_t>(*R)) {
+        L.new_coverage.assign(0, 0);
+        for (const Gva_t &g : last_new_) L.new_coverage.push_back(g.U64());
+        RevokeLastNewCoverage();
+      } else {
+        for (const Gva_t &g : last_new_) L.new_coverage.push_back(g.U64());
+      }
+      const wtfgpu_regs_t r = regs();
+      memcpy(L.gprs, r.gpr, 16 * 8);
+      L.gprs[16] = r.rip;
+      L.gprs[17] = r.rflags;
+      L.rip = r.rip;
+      L.icount = orc_icount(m_);
+      Target.Restore();
+    }
+    Restore(initial_);
+    return true;
+  }
+  std::string StatsJson() const override {
+    return "{\"kind\":\"twin\",\"retired\":" + std::to_string(retired_total_) + "}";
+  }
+};
+
+uint64_t TwinBackend_t::Rdrand() { return wtf_rdrand(seed_); }
+
+
+int main(int argc, char **argv) {
+  setvbuf(stdout, nullptr, _IOLBF, 0);
+  RunnerOptions O;
+  if (!ParseRunnerArgs(argc, argv, O)) return 2;
+  Options_t Opts;
+  CpuState_t State;
+  if (!LoadTarget(O, Opts, State)) return 1;
+  auto *B = new TwinBackend_t();
+  g_Backend = B;
+  if (!B->Initialize(Opts, State)) return 1;
+  // the runner sizes batches by Lanes(); the twin takes the requested lane count
+  struct Sized final : Executor_t {
+    TwinBackend_t *b;
+    uint32_t n;
+    Backend_t *AsBackend() override { return b; }
+    uint32_t Lanes() const override { return n; }
+    bool RunBatch(const Target_t &T, const std::vector<std::pair<const uint8_t *, size_t>> &Tc,
+                  std::vector<LaneResult> &Out, ModuleSlots *S) override {
+      return b->RunBatch(T, Tc, Out, S);
+    }
+    void ResetCoverage() override { b->ResetCoverage(); }
+    void SetFullCoverage(bool On) override { b->SetFullCoverage(On); }
+    size_t CoverageSize() const override { return b->CoverageSize(); }
+    std::string StatsJson() const override { return b->StatsJson(); }
+  } E;
+  E.b = B;
+  E.n = O.lanes ? O.lanes : 1;
+  return RunnerMain(O, E, Opts, State);
+}

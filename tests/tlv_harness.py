@@ -1,0 +1,39 @@
+"""Drives `wtfgpu` (the product node, wtf_amd/host) and `oracle/wtf_twin`
+(its CPU twin) over the synthetic tlv_server snapshot."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WTFGPU = os.path.join(ROOT, "wtf_amd", "host", "wtfgpu")
+TWIN = os.path.join(ROOT, "oracle", "wtf_twin")
+
+
+def build_target(d: str) -> str:
+    from wtf_amd.tools.tlv import build, seed_inputs
+    build(os.path.join(d, "state"), os.path.join(d, "work"))
+    seed_inputs(os.path.join(d, "inputs"))
+    return d
+
+
+def run(exe: str, target: str, inputs: str, results: str, lanes: int, limit: int = 100000,
+        full_coverage: bool = True, timeout: int = 300, extra=()) -> list[dict]:
+    cmd = [exe, "run", "--name", "tlv_server", "--target", target, "--input", inputs, "--results", results,
+           "--lanes", str(lanes), "--limit", str(limit), *extra]
+    if full_coverage:
+        cmd.append("--full-coverage")
+    subprocess.run(cmd, check=True, timeout=timeout)
+    with open(results) as f:
+        return [json.loads(line) for line in f]
+
+
+def fuzz(exe: str, target: str, runs: int, lanes: int, seed: int = 1337, limit: int = 100000,
+         seconds: float = 0, timeout: int = 600) -> dict:
+    cmd = [exe, "fuzz", "--name", "tlv_server", "--target", target, "--runs", str(runs), "--lanes", str(lanes),
+           "--seed", str(seed), "--limit", str(limit)]
+    if seconds:
+        cmd += ["--seconds", str(seconds)]
+    out = subprocess.run(cmd, check=True, timeout=timeout, capture_output=True, text=True).stdout
+    return json.loads([line for line in out.splitlines() if line.startswith("{")][-1])

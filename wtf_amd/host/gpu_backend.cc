@@ -41,37 +41,7 @@ int gpr_index(Registers_t r) {
   }
 }
 
-void seg(wtfgpu_seg_t &d, const Seg_t &s) {
-  d.base = s.Base;
-  d.limit = s.Limit;
-  d.selector = s.Selector;
-  d.attr = s.Attr;
-  d.present = s.Present;
-}
 }  // namespace
-
-wtfgpu_regs_t RegsFromCpuState(const CpuState_t &S) {
-  wtfgpu_regs_t r{};
-  const uint64_t g[16] = {S.Rax, S.Rcx, S.Rdx, S.Rbx, S.Rsp, S.Rbp, S.Rsi, S.Rdi,
-                          S.R8, S.R9, S.R10, S.R11, S.R12, S.R13, S.R14, S.R15};
-  memcpy(r.gpr, g, sizeof(g));
-  r.rip = S.Rip;
-  r.rflags = S.Rflags;
-  r.cr0 = S.Cr0.Flags, r.cr2 = S.Cr2, r.cr3 = S.Cr3, r.cr4 = S.Cr4.Flags, r.cr8 = S.Cr8;
-  r.efer = S.Efer.Flags, r.xcr0 = S.Xcr0, r.kernel_gs_base = S.KernelGsBase;
-  r.star = S.Star, r.lstar = S.Lstar, r.cstar = S.Cstar, r.sfmask = S.Sfmask;
-  r.tsc = S.Tsc, r.tsc_aux = S.TscAux, r.apic_base = S.ApicBase, r.pat = S.Pat;
-  r.sysenter_cs = S.SysenterCs, r.sysenter_eip = S.SysenterEip, r.sysenter_esp = S.SysenterEsp;
-  seg(r.seg[WTFGPU_ES], S.Es), seg(r.seg[WTFGPU_CS], S.Cs), seg(r.seg[WTFGPU_SS], S.Ss);
-  seg(r.seg[WTFGPU_DS], S.Ds), seg(r.seg[WTFGPU_FS], S.Fs), seg(r.seg[WTFGPU_GS], S.Gs);
-  seg(r.seg[WTFGPU_TR], S.Tr), seg(r.seg[WTFGPU_LDTR], S.Ldtr);
-  r.gdtr_base = S.Gdtr.Base, r.gdtr_limit = S.Gdtr.Limit, r.idtr_base = S.Idtr.Base, r.idtr_limit = S.Idtr.Limit;
-  r.mxcsr = S.Mxcsr, r.mxcsr_mask = S.MxcsrMask;
-  r.fpcw = S.Fpcw, r.fpsw = S.Fpsw, r.fptw = S.Fptw, r.fpop = S.Fpop;
-  memcpy(r.fpst, S.Fpst, sizeof(r.fpst));
-  for (int i = 0; i < 16; i++) r.xmm[i][0] = S.Zmm[i].Q[0], r.xmm[i][1] = S.Zmm[i].Q[1];
-  return r;
-}
 
 GpuBackend_t::GpuBackend_t() = default;
 GpuBackend_t::~GpuBackend_t() {
@@ -104,7 +74,8 @@ bool GpuBackend_t::Initialize(const Options_t &Opts, const CpuState_t &CpuState)
   views_.clear();
   views_.resize(nlanes_);
   if (Opts.Limit) SetLimit(Opts.Limit);
-  return Restore(CpuState);
+  if (!Restore(CpuState)) return false;
+  return set_code_pages();
 }
 
 // bochscpu_backend.cc:730-797 (+ LoadState :1026-1122): registers from the
@@ -294,30 +265,6 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
   return rc;
 }
 
-// A lane's FAULT exit is what the guest would turn into an exception; the
-// build's convention names it the way the user-mode crash
-// detection would (crash_detection_umode.cc:53-129 + backend.cc:204-212).
-TestcaseResult_t GpuBackend_t::fault_to_result(const wtfgpu_exit_t &e, uint32_t cpl) {
-  uint32_t code = EXCEPTION_ACCESS_VIOLATION_READ;
-  switch (e.vector) {
-    case WTFGPU_VEC_DE: code = EXCEPTION_INT_DIVIDE_BY_ZERO; break;
-    case WTFGPU_VEC_UD: code = EXCEPTION_ILLEGAL_INSTRUCTION; break;
-    case WTFGPU_VEC_PF:
-      code = (e.error & ErrorInstructionFetch) ? EXCEPTION_ACCESS_VIOLATION_EXECUTE
-             : (e.error & ErrorWrite)          ? EXCEPTION_ACCESS_VIOLATION_WRITE
-                                               : EXCEPTION_ACCESS_VIOLATION_READ;
-      break;
-    default: break;
-  }
-  char name[160];
-  if (cpl == 3)
-    snprintf(name, sizeof(name), "crash-%s-%#llx", std::string(ExceptionCodeToStr(code)).c_str(),
-             (unsigned long long)e.rip);
-  else
-    snprintf(name, sizeof(name), "crash-kernel-vector%u-%#llx", e.vector, (unsigned long long)e.rip);
-  return Crash_t(name);
-}
-
 // The run loop over `lanes` (ascending): launch, classify exits, service
 // breakpoint hits on the host, resume; until every lane has a result.
 bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<LaneResult> *out, ModuleSlots *slots,
@@ -355,7 +302,7 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
         case WTFGPU_EXIT_INT3:                                         // :595-619
         case WTFGPU_EXIT_HLT: v.result = Crash_t(); break;             // :690-697
         case WTFGPU_EXIT_CR3: v.result = Cr3Change_t(); break;         // :628-657
-        case WTFGPU_EXIT_FAULT: v.result = fault_to_result(e, cpl); break;
+        case WTFGPU_EXIT_FAULT: v.result = FaultToResult(e.vector, e.error, e.rip, cpl); break;
         case WTFGPU_EXIT_STOPPED: break;
         default:  // unimplemented opcode / overlay full: the engine cannot finish it
           if (out) (*out)[l].error = true;
@@ -468,6 +415,11 @@ void GpuBackend_t::finish_coverage(uint32_t n, std::vector<LaneResult> *out, std
   last_new_coverage_.clear();
   for (uint32_t l = 0; l < n; l++) {
     std::sort(per[l].begin(), per[l].end());
+    per[l].erase(std::unique(per[l].begin(), per[l].end()), per[l].end());
+    if (full_coverage_) {
+      if (out) (*out)[l].new_coverage = per[l];
+      continue;
+    }
     const bool revoke = timedout && std::find(timedout->begin(), timedout->end(), l) != timedout->end();
     for (uint64_t rip : per[l]) {
       if (aggregate_.count(rip)) continue;
@@ -477,6 +429,10 @@ void GpuBackend_t::finish_coverage(uint32_t n, std::vector<LaneResult> *out, std
       fresh.push_back(rip);
       if (n == 1) last_new_coverage_.insert(Gva_t(rip));
     }
+  }
+  if (full_coverage_) {  // parity mode: every lane ran against an empty map
+    wtfgpu_reset_coverage(ctx_);
+    return;
   }
   if (!fresh.empty()) wtfgpu_commit_coverage(ctx_, fresh.data(), fresh.size());
 }
@@ -503,6 +459,7 @@ bool GpuBackend_t::RunBatch(const Target_t &Target, const std::vector<std::pair<
   const uint32_t n = (uint32_t)Testcases.size();
   if (n == 0 || n > nlanes_) return false;
   Out.assign(n, LaneResult{});
+  if (Slots) Slots->ResetAll();
   if (wtfgpu_restore(ctx_, 0, n)) return false;
   for (uint32_t l = 0; l < n; l++) reset_view(l);
   // InsertTestcase per lane (client.cc:102), module state per lane
@@ -536,7 +493,73 @@ bool GpuBackend_t::RunBatch(const Target_t &Target, const std::vector<std::pair<
   g_Backend = saved;
   cur_ = 0;
   stats_.total_ms += ms_since(t0);
+  stats_.batches++;
+  stats_.testcases += n;
   return true;
+}
+
+void GpuBackend_t::ResetCoverage() {
+  aggregate_.clear();
+  last_new_coverage_.clear();
+  wtfgpu_reset_coverage(ctx_);
+}
+
+std::string GpuBackend_t::StatsJson() const {
+  char b[512];
+  snprintf(b, sizeof(b),
+           "{\"kind\":\"gpu\",\"rounds\":%llu,\"breakpoint_hits\":%llu,\"kernel_launches\":%llu,"
+           "\"kernel_ms\":%.3f,\"service_ms\":%.3f,\"total_ms\":%.3f,\"page_fetches\":%llu,"
+           "\"prefetched_pages\":%llu}",
+           (unsigned long long)stats_.rounds, (unsigned long long)stats_.breakpoint_hits,
+           (unsigned long long)stats_.kernel_launches, stats_.kernel_ms, stats_.service_ms, stats_.total_ms,
+           (unsigned long long)stats_.page_fetches, (unsigned long long)stats_.prefetched_pages);
+  return b;
+}
+
+// Coverage index space: every executable leaf page reachable
+// from the snapshot cr3 gets a slot in the device coverage map; identical on
+// every GPU, so the maps can be merged with a MAX all-reduce.
+bool GpuBackend_t::set_code_pages() {
+  std::vector<uint64_t> vpns;
+  const uint64_t kMaxPages = 1u << 16;
+  const uint64_t mask = 0x000ffffffffff000ull;
+  auto entry = [&](uint64_t table, uint64_t idx, uint64_t &e) {
+    const uint8_t *pg = dump_.GetPhysicalPage(table & mask);
+    if (!pg) return false;
+    memcpy(&e, pg + idx * 8, 8);
+    return (e & 1) != 0;
+  };
+  const uint64_t cr3 = initial_.Cr3 & mask;
+  for (uint64_t i4 = 0; i4 < 512 && vpns.size() < kMaxPages; i4++) {
+    uint64_t e4;
+    if (!entry(cr3, i4, e4)) continue;
+    for (uint64_t i3 = 0; i3 < 512 && vpns.size() < kMaxPages; i3++) {
+      uint64_t e3;
+      if (!entry(e4, i3, e3)) continue;
+      const bool nx3 = ((e4 | e3) >> 63) & 1;
+      if (e3 & 0x80) continue;  // 1 GiB leaves are data mappings in practice
+      for (uint64_t i2 = 0; i2 < 512 && vpns.size() < kMaxPages; i2++) {
+        uint64_t e2;
+        if (!entry(e3, i2, e2)) continue;
+        const bool nx2 = nx3 || ((e2 >> 63) & 1);
+        uint64_t va = (i4 << 39) | (i3 << 30) | (i2 << 21);
+        if (va & (1ull << 47)) va |= 0xffff000000000000ull;
+        if (e2 & 0x80) {
+          if (!nx2)
+            for (uint64_t k = 0; k < 512; k++) vpns.push_back((va >> 12) + k);
+          continue;
+        }
+        for (uint64_t i1 = 0; i1 < 512 && vpns.size() < kMaxPages; i1++) {
+          uint64_t e1;
+          if (!entry(e2, i1, e1)) continue;
+          if (nx2 || ((e1 >> 63) & 1)) continue;
+          vpns.push_back((va >> 12) + i1);
+        }
+      }
+    }
+  }
+  if (vpns.empty()) return true;
+  return wtfgpu_set_code_pages(ctx_, vpns.data(), (uint32_t)vpns.size()) == WTFGPU_OK;
 }
 
 }  // namespace wtfgpu_host

@@ -21,27 +21,18 @@
 #include "../../include/wtfgpu.h"
 #include "kdmp.h"
 #include "module_slots.h"
+#include "runner.h"
 #include "wtf_api.h"
 
 namespace wtfgpu_host {
 
-struct LaneResult {
-  TestcaseResult_t result;
-  bool error = false;       // the engine could not finish the testcase (unimplemented opcode, overlay full)
-  uint32_t exit_status = 0; // last engine exit status (wtfgpu_status)
-  uint64_t icount = 0;      // retired instructions
-  uint64_t rip = 0;
-  uint64_t gprs[18] = {};   // final gprs + rip + rflags
-  std::vector<uint64_t> new_coverage;  // LastNewCoverage, lane order attribution
-};
-
 struct BatchStats {
   uint64_t rounds = 0, breakpoint_hits = 0, kernel_launches = 0, retired = 0;
-  uint64_t page_fetches = 0, prefetched_pages = 0;
+  uint64_t page_fetches = 0, prefetched_pages = 0, batches = 0, testcases = 0;
   double kernel_ms = 0, service_ms = 0, total_ms = 0;
 };
 
-class GpuBackend_t final : public Backend_t {
+class GpuBackend_t final : public Backend_t, public Executor_t {
  public:
   GpuBackend_t();
   ~GpuBackend_t() override;
@@ -73,9 +64,14 @@ class GpuBackend_t final : public Backend_t {
   // then restores every lane. `slots` (optional) gives each lane its own module
   // state. Coverage is attributed in lane order against the aggregate set.
   bool RunBatch(const Target_t &Target, const std::vector<std::pair<const uint8_t *, size_t>> &Testcases,
-                std::vector<LaneResult> &Out, ModuleSlots *Slots);
+                std::vector<LaneResult> &Out, ModuleSlots *Slots) override;
+  Backend_t *AsBackend() override { return this; }
+  void ResetCoverage() override;
+  void SetFullCoverage(bool On) override { full_coverage_ = On; }
+  size_t CoverageSize() const override { return aggregate_.size(); }
+  std::string StatsJson() const override;
   const BatchStats &Stats() const { return stats_; }
-  uint32_t Lanes() const { return nlanes_; }
+  uint32_t Lanes() const override { return nlanes_; }
   wtfgpu_ctx *Engine() const { return ctx_; }
   const std::unordered_set<uint64_t> &AggregateCoverage() const { return aggregate_; }
 
@@ -100,7 +96,7 @@ class GpuBackend_t final : public Backend_t {
   bool run_lanes(const std::vector<uint32_t> &lanes, std::vector<LaneResult> *out, ModuleSlots *slots,
                  bool per_lane_state);
   void finish_coverage(uint32_t n, std::vector<LaneResult> *out, std::vector<uint32_t> *timedout);
-  static TestcaseResult_t fault_to_result(const wtfgpu_exit_t &e, uint32_t cpl);
+  bool set_code_pages();
 
   wtfgpu_ctx *ctx_ = nullptr;
   KernelDump dump_;
@@ -114,9 +110,8 @@ class GpuBackend_t final : public Backend_t {
   std::unordered_set<uint64_t> aggregate_;
   std::unordered_set<Gva_t> last_new_coverage_;
   mutable BatchStats stats_;
+  bool full_coverage_ = false;
 };
 
-// The ring-3 CpuState_t -> wtfgpu_regs_t mapping (LoadState, bochscpu_backend.cc:1026-1122).
-wtfgpu_regs_t RegsFromCpuState(const CpuState_t &S);
 
 }  // namespace wtfgpu_host

@@ -1,94 +1,71 @@
 // module_slots.cc — see module_slots.h.
 #include "module_slots.h"
 
-#include <dlfcn.h>
-#include <link.h>
-
 #include <cstdio>
-#include <cstring>
+#include <cstdlib>
 
 namespace wtfgpu_host {
 
-namespace {
-struct FindCtx {
-  const char *path;
-  std::vector<std::pair<uintptr_t, size_t>> rw;
-  std::pair<uintptr_t, size_t> relro{0, 0};
-  bool found = false;
-};
-
-int find_module(struct dl_phdr_info *info, size_t, void *data) {
-  FindCtx *c = (FindCtx *)data;
-  if (!info->dlpi_name || !strstr(info->dlpi_name, c->path)) return 0;
-  c->found = true;
-  for (int i = 0; i < info->dlpi_phnum; i++) {
-    const ElfW(Phdr) &ph = info->dlpi_phdr[i];
-    const uintptr_t a = info->dlpi_addr + ph.p_vaddr;
-    if (ph.p_type == PT_LOAD && (ph.p_flags & PF_W)) c->rw.push_back({a, ph.p_memsz});
-    if (ph.p_type == PT_GNU_RELRO) c->relro = {a, ph.p_memsz};
-  }
-  return 1;
-}
-}  // namespace
-
-bool ModuleSlots::Load(const std::string &so_path) {
-  handle_ = dlopen(so_path.c_str(), RTLD_NOW | RTLD_LOCAL);
-  if (!handle_) {
-    fprintf(stderr, "ModuleSlots: dlopen(%s): %s\n", so_path.c_str(), dlerror());
-    return false;
-  }
-  const char *base = strrchr(so_path.c_str(), '/');
-  FindCtx c;
-  c.path = base ? base + 1 : so_path.c_str();
-  dl_iterate_phdr(find_module, &c);
-  if (!c.found) return false;
-  for (auto [a, n] : c.rw) {
-    // drop the RELRO prefix (GOT / vtables made read-only after relocation)
-    uintptr_t lo = a, hi = a + n;
-    const uintptr_t rlo = c.relro.first, rhi = c.relro.first + c.relro.second;
-    if (c.relro.second && rlo <= lo && rhi > lo) lo = rhi < hi ? rhi : hi;
-    if (hi > lo) segs_.push_back({(uint8_t *)lo, hi - lo});
-  }
-  return true;
+std::vector<LaneStateOps> &LaneStateRegistry() {
+  static std::vector<LaneStateOps> R;
+  return R;
 }
 
-size_t ModuleSlots::StateBytes() const {
-  size_t n = 0;
-  for (auto &s : segs_) n += s.size;
-  return n;
+ModuleSlots::~ModuleSlots() { release(); }
+
+void ModuleSlots::release() {
+  const auto &R = LaneStateRegistry();
+  for (auto &objs : lanes_)
+    for (size_t i = 0; i < objs.size(); i++)
+      if (objs[i]) R[i].destroy(objs[i]);
+  for (size_t i = 0; i < initial_.size(); i++) R[i].destroy(initial_[i]);
+  lanes_.clear();
+  initial_.clear();
+  dirty_.clear();
 }
 
 void ModuleSlots::Capture(uint32_t lanes) {
-  initial_.resize(StateBytes());
-  size_t off = 0;
-  for (auto &s : segs_) {
-    memcpy(initial_.data() + off, s.addr, s.size);
-    off += s.size;
-  }
-  slots_.assign(lanes, {});
-  touched_.assign(lanes, 0);
+  release();
+  const auto &R = LaneStateRegistry();
+  for (const auto &ops : R) initial_.push_back(ops.clone(ops.object));
+  lanes_.assign(lanes, std::vector<void *>(R.size(), nullptr));
+  dirty_.assign(lanes, 0);
   in_ = -1;
 }
 
-void ModuleSlots::SwapIn(uint32_t lane) {
-  const std::vector<uint8_t> &src = touched_[lane] ? slots_[lane] : initial_;
-  size_t off = 0;
-  for (auto &s : segs_) {
-    memcpy(s.addr, src.data() + off, s.size);
-    off += s.size;
+void ModuleSlots::ResetAll() {
+  const auto &R = LaneStateRegistry();
+  for (size_t l = 0; l < lanes_.size(); l++) {
+    if (!dirty_[l]) continue;
+    for (size_t i = 0; i < R.size(); i++)
+      if (lanes_[l][i]) R[i].assign(lanes_[l][i], initial_[i]);
+    dirty_[l] = 0;
   }
-  in_ = (int32_t)lane;
+}
+
+void ModuleSlots::SwapIn(uint32_t lane) {
+  if (in_ >= 0) {
+    fprintf(stderr, "ModuleSlots: lane %lld still swapped in\n", (long long)in_);
+    std::abort();
+  }
+  const auto &R = LaneStateRegistry();
+  auto &objs = lanes_.at(lane);
+  for (size_t i = 0; i < R.size(); i++) {
+    if (!objs[i]) objs[i] = R[i].clone(initial_[i]);
+    R[i].swap(R[i].object, objs[i]);
+  }
+  dirty_[lane] = 1;
+  in_ = lane;
 }
 
 void ModuleSlots::SwapOut(uint32_t lane) {
-  std::vector<uint8_t> &dst = slots_[lane];
-  dst.resize(initial_.size());
-  size_t off = 0;
-  for (auto &s : segs_) {
-    memcpy(dst.data() + off, s.addr, s.size);
-    off += s.size;
+  if (in_ != (int64_t)lane) {
+    fprintf(stderr, "ModuleSlots: swap-out of lane %u, lane %lld is in\n", lane, (long long)in_);
+    std::abort();
   }
-  touched_[lane] = 1;
+  const auto &R = LaneStateRegistry();
+  auto &objs = lanes_[lane];
+  for (size_t i = 0; i < R.size(); i++) R[i].swap(R[i].object, objs[i]);
   in_ = -1;
 }
 

@@ -1,45 +1,88 @@
-// module_slots.h — per-lane state for unchanged fuzzer modules.
+// module_slots.h — per-lane state for fuzzer modules.
 //
 // wtf modules keep testcase state in globals (fuzzer_tlv_server.cc:42-65 holds
 // the packet deque the ProcessPacket breakpoint consumes) and assume one
 // testcase runs at a time. A batch runs N testcases at once, so each lane needs
-// its own copy of that state. A module is built as its own shared object; its
-// writable data (the RW PT_LOAD segments minus the RELRO part: .data, .bss) is
-// the module state. ModuleSlots keeps one copy of those bytes per lane and swaps
-// the lane's copy in around every call into the module for that lane (Insert,
-// breakpoint handlers, Restore). Heap objects the state points to belong to that
-// lane's copy (the module allocates and frees them through its own globals), so
-// they need no copying.
+// its own copy of that state while its handlers run.
+//
+// A module names its per-testcase global once, next to its definition:
+//
+//     struct { std::deque<Packet_t> Packets; CpuState_t Context; } GlobalState;
+//     WTF_LANE_STATE(GlobalState);
+//
+// That one line is the only addition a module needs for batching; everything
+// else (Init, InsertTestcase, Restore, the handlers) is unchanged. Upstream wtf
+// defines the macro as nothing.
+//
+// ModuleSlots keeps one typed copy of every registered object per lane. The
+// lane's copy is swapped into the global (std::swap: container pointers are
+// exchanged, no element copies) around every call into the module for that
+// lane, and swapped back out afterwards. A lane's first swap-in starts from a
+// deep copy of the state as Init left it. Raw byte copies of the module's data
+// segment are NOT used: containers built during Init (a deque's first node)
+// would then be shared between lanes and clobbered by the first insert.
 #pragma once
 #include <cstddef>
 #include <cstdint>
-#include <string>
+#include <memory>
+#include <utility>
 #include <vector>
 
 namespace wtfgpu_host {
 
+// Type-erased operations over one registered global.
+struct LaneStateOps {
+  void *object;
+  void *(*clone)(const void *);          // new T(copy)
+  void (*assign)(void *, const void *);  // dst = src
+  void (*swap)(void *, void *);
+  void (*destroy)(void *);
+};
+
+// Registry of WTF_LANE_STATE objects (filled by static initialisers).
+std::vector<LaneStateOps> &LaneStateRegistry();
+
+template <typename T>
+struct LaneStateRegistrar {
+  explicit LaneStateRegistrar(T &Object) {
+    LaneStateRegistry().push_back(LaneStateOps{
+        &Object, [](const void *S) -> void * { return new T(*(const T *)S); },
+        [](void *D, const void *S) { *(T *)D = *(const T *)S; },
+        [](void *A, void *B) {
+          using std::swap;
+          swap(*(T *)A, *(T *)B);
+        },
+        [](void *P) { delete (T *)P; }});
+  }
+};
+
 class ModuleSlots {
  public:
-  // Loads the module (dlopen). Its static Target_t registers itself.
-  bool Load(const std::string &so_path);
+  ModuleSlots() = default;
+  ~ModuleSlots();
+  ModuleSlots(const ModuleSlots &) = delete;
+  ModuleSlots &operator=(const ModuleSlots &) = delete;
+
   // The current module state becomes every lane's initial state (call after Init).
   void Capture(uint32_t lanes);
+  // Every lane's copy back to the captured state (start of a batch).
+  void ResetAll();
   void SwapIn(uint32_t lane);
   void SwapOut(uint32_t lane);
-  size_t StateBytes() const;
-  void *Handle() const { return handle_; }
+  size_t Objects() const { return initial_.size(); }
 
  private:
-  struct Segment {
-    uint8_t *addr;
-    size_t size;
-  };
-  void *handle_ = nullptr;
-  std::vector<Segment> segs_;
-  std::vector<uint8_t> initial_;
-  std::vector<std::vector<uint8_t>> slots_;  // lazily materialised from initial_
-  std::vector<uint8_t> touched_;
-  int32_t in_ = -1;
+  void release();
+  std::vector<void *> initial_;             // per registered object
+  std::vector<std::vector<void *>> lanes_;  // [lane][object], nullptr = not materialised
+  std::vector<uint8_t> dirty_;              // lane copy differs from initial
+  int64_t in_ = -1;
 };
 
 }  // namespace wtfgpu_host
+
+#define WTF_LANE_STATE_CAT2(a, b) a##b
+#define WTF_LANE_STATE_CAT(a, b) WTF_LANE_STATE_CAT2(a, b)
+#define WTF_LANE_STATE(Object)                                                                      \
+  static ::wtfgpu_host::LaneStateRegistrar<decltype(Object)> WTF_LANE_STATE_CAT(LaneStateReg_, __LINE__)( \
+      Object)

@@ -1,0 +1,209 @@
+// fuzzer_tlv_server.cc — the tlv_server fuzzer module (src/wtf/fuzzer_tlv_server.cc),
+// written against this repository's wtf interface. Behaviour follows the
+// reference module:
+//  * a testcase is a JSON list of packets {Command, Id, BodySize, Body}
+//    (:27-40); InsertTestcase queues them (:67-75);
+//  * ProcessPacket breakpoint (:83-166): no packet left -> Stop(Ok); else the
+//    next packet is written so that it ends at the end of the packet page
+//    (rcx + 0x1000 - size, the guard page catches over-reads), rdx = size;
+//    a packet of 0x1000 bytes or more ends the testcase;
+//  * return-address breakpoint (:171-179): registers back to the snapshot's
+//    so the receive loop calls ProcessPacket again;
+//  * printf breakpoint (:184-189): skipped (return 0);
+//  * user-mode crash detection (:191-194);
+//  * the custom mutator (:204-365): Generate 1..10 packets one time in five,
+//    otherwise insert / copy-field / delete on a corpus testcase.
+// The only addition for batched execution is WTF_LANE_STATE(GlobalState)
+// (module_slots.h): the packet queue is per testcase, so per lane.
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "../json_lite.h"
+#include "../wtf_api.h"
+#include "crash_detection_umode.h"
+
+namespace TlvServer {
+
+struct Packet_t {
+  uint32_t Command = 0;
+  uint16_t Id = 0;
+  uint16_t BodySize = 0;
+  std::vector<uint8_t> Body;
+};
+
+// JSON testcase -> packets (nlohmann get<>: integers are cast to the field type)
+bool Deserialize(const uint8_t *Buffer, const size_t BufferSize, std::vector<Packet_t> &Out) {
+  Out.clear();
+  try {
+    const jsonl::Value Root = jsonl::parse(Buffer, BufferSize);
+    for (const jsonl::Value &P : Root.at("Packets").arr) {
+      Packet_t Pk;
+      Pk.Command = (uint32_t)P.at("Command").u64();
+      Pk.Id = (uint16_t)P.at("Id").u64();
+      Pk.BodySize = (uint16_t)P.at("BodySize").u64();
+      for (const jsonl::Value &B : P.at("Body").arr) Pk.Body.push_back((uint8_t)B.u64());
+      Out.push_back(std::move(Pk));
+    }
+  } catch (const std::exception &) {
+    return false;
+  }
+  return true;
+}
+
+// packets -> JSON as nlohmann's dump() writes it (sorted keys, no spaces)
+std::string Serialize(const std::vector<Packet_t> &Packets) {
+  std::string S = "{\"Packets\":[";
+  for (size_t i = 0; i < Packets.size(); i++) {
+    const Packet_t &P = Packets[i];
+    if (i) S += ',';
+    S += "{\"Body\":[";
+    for (size_t j = 0; j < P.Body.size(); j++) {
+      if (j) S += ',';
+      S += std::to_string(P.Body[j]);
+    }
+    S += "],\"BodySize\":" + std::to_string(P.BodySize) + ",\"Command\":" + std::to_string(P.Command) +
+         ",\"Id\":" + std::to_string(P.Id) + "}";
+  }
+  return S + "]}";
+}
+
+struct {
+  std::deque<Packet_t> Packets;
+  CpuState_t Context;
+
+  void RestoreGprs(Backend_t *B) {
+    const CpuState_t &C = Context;
+    B->Rsp(C.Rsp), B->Rip(C.Rip), B->Rax(C.Rax), B->Rbx(C.Rbx), B->Rcx(C.Rcx), B->Rdx(C.Rdx);
+    B->Rsi(C.Rsi), B->Rdi(C.Rdi), B->R8(C.R8), B->R9(C.R9), B->R10(C.R10), B->R11(C.R11);
+    B->R12(C.R12), B->R13(C.R13), B->R14(C.R14), B->R15(C.R15);
+  }
+} GlobalState;
+WTF_LANE_STATE(GlobalState);
+
+bool InsertTestcase(const uint8_t *Buffer, const size_t BufferSize) {
+  GlobalState.Packets.clear();
+  std::vector<Packet_t> Packets;
+  if (!Deserialize(Buffer, BufferSize, Packets)) return false;
+  for (Packet_t &P : Packets) GlobalState.Packets.emplace_back(std::move(P));
+  return true;
+}
+
+void OnProcessPacket(Backend_t *Backend) {
+  if (GlobalState.Packets.empty()) return g_Backend->Stop(Ok_t());
+  const Packet_t &P = GlobalState.Packets.front();
+  const size_t PacketSize = sizeof(P.Command) + sizeof(P.Id) + sizeof(P.BodySize) + P.Body.size();
+  if (PacketSize >= 0x1000) {
+    GlobalState.Packets.pop_front();
+    Backend->Stop(Ok_t());
+    printf("This testcase is too big to fit, bailing\n");
+    return;
+  }
+  Backend->Rdx(PacketSize);
+  uint64_t Address = Backend->Rcx() + (0x1000 - PacketSize);  // ends at the guard page
+  Backend->Rcx(Address);
+  if (!Backend->VirtWriteStructDirty(Gva_t(Address), &P.Command)) std::abort();
+  Address += sizeof(P.Command);
+  if (!Backend->VirtWriteStructDirty(Gva_t(Address), &P.Id)) std::abort();
+  Address += sizeof(P.Id);
+  if (!Backend->VirtWriteStructDirty(Gva_t(Address), &P.BodySize)) std::abort();
+  Address += sizeof(P.BodySize);
+  if (!Backend->VirtWriteDirty(Gva_t(Address), P.Body.data(), P.Body.size())) std::abort();
+  GlobalState.Packets.pop_front();
+}
+
+bool Init(const Options_t &, const CpuState_t &State) {
+  GlobalState.Context = State;
+  const Gva_t ReturnAddress = Gva_t(g_Backend->VirtRead8(Gva_t(g_Backend->Rsp())));
+  if (!g_Backend->SetBreakpoint("tlv_server!ProcessPacket", OnProcessPacket)) return false;
+  if (!g_Backend->SetBreakpoint(ReturnAddress, [](Backend_t *) { GlobalState.RestoreGprs(g_Backend); })) {
+    printf("Failed to SetBreakpoint on the return address.\n");
+    return false;
+  }
+  if (!g_Backend->SetBreakpoint("tlv_server!printf", [](Backend_t *Backend) {
+        const std::string Format = Backend->VirtReadString(Backend->GetArgGva(0));
+        (void)Format;
+        Backend->SimulateReturnFromFunction(0);
+      })) {
+    printf("Failed to SetBreakpoint on printf\n");
+    return false;
+  }
+  if (!SetupUsermodeCrashDetectionHooks()) {
+    printf("Failed to SetupUsermodeCrashDetectionHooks\n");
+    return false;
+  }
+  return true;
+}
+
+bool Restore() { return true; }
+
+class CustomMutator_t : public Mutator_t {
+  std::mt19937_64 &Rng_;
+
+  uint32_t GetUint32(const uint32_t A, const uint32_t B) { return std::uniform_int_distribution<uint32_t>(A, B)(Rng_); }
+
+  std::string Generate() {
+    std::vector<Packet_t> Packets;
+    const uint32_t N = GetUint32(1, 10);
+    for (uint32_t Idx = 0; Idx < N; Idx++) {
+      Packet_t P;
+      P.Id = (uint16_t)Idx;
+      P.Command = GetUint32(0, 10);
+      P.Body.resize(GetUint32(0, 100));
+      P.BodySize = (uint16_t)P.Body.size();
+      if (GetUint32(1, 3) == 1) P.BodySize ^= (uint16_t)(1u << GetUint32(0, 15));
+      Packets.push_back(std::move(P));
+    }
+    return Serialize(Packets);
+  }
+
+  std::string Mutate(const uint8_t *Data, const size_t DataLen) {
+    std::vector<Packet_t> Packets;
+    Deserialize(Data, DataLen, Packets);
+    switch (GetUint32(0, 2)) {
+      case 0:  // insert a copy of a packet somewhere (at most 11 packets)
+        if (Packets.size() <= 10 && !Packets.empty()) {
+          const uint32_t From = GetUint32(0, (uint32_t)Packets.size() - 1);
+          const uint32_t To = GetUint32(0, (uint32_t)Packets.size());
+          const Packet_t Copy = Packets[From];
+          Packets.insert(Packets.begin() + To, Copy);
+        }
+        break;
+      case 1: {  // copy one field between packets
+        if (Packets.empty()) break;
+        const uint32_t Src = GetUint32(0, (uint32_t)Packets.size() - 1);
+        const uint32_t Dst = GetUint32(0, (uint32_t)Packets.size() - 1);
+        switch (GetUint32(0, 3)) {
+          case 0: Packets[Dst].Id = Packets[Src].Id; break;
+          case 1: Packets[Dst].Command = Packets[Src].Command; break;
+          case 2: Packets[Dst].BodySize = Packets[Src].BodySize; break;
+          case 3: Packets[Dst].Body = Packets[Src].Body; break;
+        }
+        break;
+      }
+      case 2:  // delete a packet
+        if (!Packets.empty()) Packets.erase(Packets.begin() + GetUint32(0, (uint32_t)Packets.size() - 1));
+        break;
+    }
+    return Serialize(Packets);
+  }
+
+ public:
+  CustomMutator_t(std::mt19937_64 &Rng, const size_t) : Rng_(Rng) {}
+  static std::unique_ptr<Mutator_t> Create(std::mt19937_64 &Rng, const size_t MaxSize) {
+    return std::make_unique<CustomMutator_t>(Rng, MaxSize);
+  }
+  std::string GetNewTestcase(const Corpus_t &Corpus) override {
+    if (GetUint32(1, 5) == 5) return Generate();
+    const Testcase_t *T = Corpus.PickTestcase();
+    if (!T) {
+      printf("The corpus is empty, exiting\n");
+      std::abort();
+    }
+    return Mutate(T->Buffer_.get(), T->BufferSize_);
+  }
+};
+
+Target_t TlvServer("tlv_server", Init, InsertTestcase, Restore, CustomMutator_t::Create);
+
+}  // namespace TlvServer

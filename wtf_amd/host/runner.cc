@@ -1,0 +1,303 @@
+// runner.cc — see runner.h.
+#include "runner.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+
+#include "../../include/wtfgpu.h"
+
+namespace wtfgpu_host {
+
+namespace {
+using Clock = std::chrono::steady_clock;
+double secs_since(Clock::time_point t0) { return std::chrono::duration<double>(Clock::now() - t0).count(); }
+
+std::string crash_name(const TestcaseResult_t &R) {
+  if (const Crash_t *C = std::get_if<Crash_t>(&R)) return C->CrashName;
+  return "";
+}
+
+std::string json_escape(const std::string &S) {
+  std::string O;
+  for (char c : S) {
+    if (c == '"' || c == '\\') O += '\\';
+    O += c;
+  }
+  return O;
+}
+
+std::vector<fs::path> list_inputs(const fs::path &P) {
+  std::vector<fs::path> V;
+  if (fs::is_directory(P)) {
+    for (const auto &E : fs::directory_iterator(P))
+      if (E.is_regular_file()) V.push_back(E.path());
+    std::sort(V.begin(), V.end());
+  } else if (fs::exists(P)) {
+    V.push_back(P);
+  }
+  return V;
+}
+  void seg(wtfgpu_seg_t &d, const Seg_t &s) {
+  d.base = s.Base;
+  d.limit = s.Limit;
+  d.selector = s.Selector;
+  d.attr = s.Attr;
+  d.present = s.Present;
+}
+}  // namespace
+
+// The ring-3 CpuState_t -> wtfgpu_regs_t mapping (LoadState, bochscpu_backend.cc:1026-1122).
+wtfgpu_regs_t RegsFromCpuState(const CpuState_t &S) {
+  wtfgpu_regs_t r{};
+  const uint64_t g[16] = {S.Rax, S.Rcx, S.Rdx, S.Rbx, S.Rsp, S.Rbp, S.Rsi, S.Rdi,
+                          S.R8, S.R9, S.R10, S.R11, S.R12, S.R13, S.R14, S.R15};
+  memcpy(r.gpr, g, sizeof(g));
+  r.rip = S.Rip;
+  r.rflags = S.Rflags;
+  r.cr0 = S.Cr0.Flags, r.cr2 = S.Cr2, r.cr3 = S.Cr3, r.cr4 = S.Cr4.Flags, r.cr8 = S.Cr8;
+  r.efer = S.Efer.Flags, r.xcr0 = S.Xcr0, r.kernel_gs_base = S.KernelGsBase;
+  r.star = S.Star, r.lstar = S.Lstar, r.cstar = S.Cstar, r.sfmask = S.Sfmask;
+  r.tsc = S.Tsc, r.tsc_aux = S.TscAux, r.apic_base = S.ApicBase, r.pat = S.Pat;
+  r.sysenter_cs = S.SysenterCs, r.sysenter_eip = S.SysenterEip, r.sysenter_esp = S.SysenterEsp;
+  seg(r.seg[WTFGPU_ES], S.Es), seg(r.seg[WTFGPU_CS], S.Cs), seg(r.seg[WTFGPU_SS], S.Ss);
+  seg(r.seg[WTFGPU_DS], S.Ds), seg(r.seg[WTFGPU_FS], S.Fs), seg(r.seg[WTFGPU_GS], S.Gs);
+  seg(r.seg[WTFGPU_TR], S.Tr), seg(r.seg[WTFGPU_LDTR], S.Ldtr);
+  r.gdtr_base = S.Gdtr.Base, r.gdtr_limit = S.Gdtr.Limit, r.idtr_base = S.Idtr.Base, r.idtr_limit = S.Idtr.Limit;
+  r.mxcsr = S.Mxcsr, r.mxcsr_mask = S.MxcsrMask;
+  r.fpcw = S.Fpcw, r.fpsw = S.Fpsw, r.fptw = S.Fptw, r.fpop = S.Fpop;
+  memcpy(r.fpst, S.Fpst, sizeof(r.fpst));
+  for (int i = 0; i < 16; i++) r.xmm[i][0] = S.Zmm[i].Q[0], r.xmm[i][1] = S.Zmm[i].Q[1];
+  return r;
+}
+
+TestcaseResult_t FaultToResult(uint32_t vector, uint32_t error, uint64_t rip, uint32_t cpl) {
+  uint32_t code = EXCEPTION_ACCESS_VIOLATION_READ;
+  switch (vector) {
+    case WTFGPU_VEC_DE: code = EXCEPTION_INT_DIVIDE_BY_ZERO; break;
+    case WTFGPU_VEC_UD: code = EXCEPTION_ILLEGAL_INSTRUCTION; break;
+    case WTFGPU_VEC_GP: code = EXCEPTION_ACCESS_VIOLATION_READ; break;
+    case WTFGPU_VEC_PF:
+      code = (error & ErrorInstructionFetch) ? EXCEPTION_ACCESS_VIOLATION_EXECUTE
+             : (error & ErrorWrite)          ? EXCEPTION_ACCESS_VIOLATION_WRITE
+                                             : EXCEPTION_ACCESS_VIOLATION_READ;
+      break;
+    default: break;
+  }
+  char name[160];
+  if (cpl == 3)
+    snprintf(name, sizeof(name), "crash-%s-%#llx", std::string(ExceptionCodeToStr(code)).c_str(),
+             (unsigned long long)rip);
+  else
+    snprintf(name, sizeof(name), "crash-kernel-vector%u-%#llx", vector, (unsigned long long)rip);
+  return Crash_t(name);
+}
+
+bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
+  for (int i = 1; i < argc; i++) {
+    const std::string a = argv[i];
+    auto next = [&](const char *what) -> const char * {
+      if (i + 1 >= argc) {
+        fprintf(stderr, "%s needs a value\n", what);
+        exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "run" || a == "fuzz") O.mode = a;
+    else if (a == "--name") O.name = next("--name");
+    else if (a == "--target") O.target = next("--target");
+    else if (a == "--input") O.input = next("--input");
+    else if (a == "--results") O.results = next("--results");
+    else if (a == "--limit") O.limit = strtoull(next("--limit"), nullptr, 0);
+    else if (a == "--lanes") O.lanes = (uint32_t)strtoul(next("--lanes"), nullptr, 0);
+    else if (a == "--overlay-pages") O.overlay_pages = (uint32_t)strtoul(next("--overlay-pages"), nullptr, 0);
+    else if (a == "--runs") O.runs = strtoull(next("--runs"), nullptr, 0);
+    else if (a == "--seconds") O.seconds = atof(next("--seconds"));
+    else if (a == "--seed") O.seed = strtoull(next("--seed"), nullptr, 0);
+    else if (a == "--max_len") O.max_len = strtoull(next("--max_len"), nullptr, 0);
+    else if (a == "--device") O.device = atoi(next("--device"));
+    else if (a == "--full-coverage") O.full_coverage = true;
+    else if (a == "--quiet") O.quiet = true;
+    else {
+      fprintf(stderr, "unknown argument %s\n", a.c_str());
+      return false;
+    }
+  }
+  if (O.name.empty() || O.target.empty()) {
+    fprintf(stderr, "usage: [run|fuzz] --name <target> --target <dir> [--input p] [--results f] [--limit n]\n"
+                    "       [--lanes n] [--overlay-pages k] [--runs n] [--seconds s] [--seed s] [--full-coverage]\n");
+    return false;
+  }
+  return true;
+}
+
+// wtf.cc:300-420 (state loading + sanitisation + symbol store), backend-independent
+bool LoadTarget(const RunnerOptions &O, Options_t &Opts, CpuState_t &State) {
+  const fs::path T(O.target);
+  Opts.TargetName = O.name;
+  Opts.StatePath = T / "state";
+  Opts.DumpPath = Opts.StatePath / "mem.dmp";
+  Opts.CpuStatePath = Opts.StatePath / "regs.json";
+  Opts.SymbolFilePath = Opts.StatePath / "symbol-store.json";
+  Opts.Limit = O.limit;
+  Opts.GpuDevice = O.device;
+  Opts.GpuLanes = O.lanes;
+  Opts.GpuOverlayPages = O.overlay_pages;
+  Opts.Fuzz.Seed = (uint32_t)O.seed;
+  if (!LoadCpuStateFromJSON(State, Opts.CpuStatePath)) {
+    printf("Failed to load the CPU state from %s\n", Opts.CpuStatePath.string().c_str());
+    return false;
+  }
+  if (!SanitizeCpuState(State)) return false;
+  Opts.CpuState = State;
+  if (!g_Dbg.Init(Opts.DumpPath, Opts.SymbolFilePath)) return false;
+  return true;
+}
+
+int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, const CpuState_t &State) {
+  Target_t *Target = Targets_t::Instance().Get(O.name);
+  if (!Target) {
+    printf("Target %s not found\n", O.name.c_str());
+    Targets_t::Instance().DisplayRegisteredTargets();
+    return 1;
+  }
+  g_Backend = Exec.AsBackend();
+  if (!Target->Init(Opts, State)) {
+    printf("Failed to initialize the target\n");
+    return 1;
+  }
+  const uint32_t N = Exec.Lanes();
+  ModuleSlots Slots;
+  Slots.Capture(N);
+  Exec.SetFullCoverage(O.full_coverage);
+
+  if (O.mode == "run") {
+    const auto Inputs = list_inputs(O.input.empty() ? fs::path(O.target) / "inputs" : fs::path(O.input));
+    FILE *Out = O.results.empty() ? stdout : fopen(O.results.c_str(), "w");
+    if (!Out) return 1;
+    const auto t0 = Clock::now();
+    uint64_t Retired = 0;
+    for (size_t b = 0; b < Inputs.size(); b += N) {
+      const size_t n = std::min<size_t>(N, Inputs.size() - b);
+      std::vector<std::vector<uint8_t>> Bufs(n);
+      std::vector<std::pair<const uint8_t *, size_t>> Tc(n);
+      for (size_t i = 0; i < n; i++) {
+        Bufs[i] = ReadFile(Inputs[b + i]);
+        Tc[i] = {Bufs[i].data(), Bufs[i].size()};
+      }
+      if (O.full_coverage) Exec.ResetCoverage();
+      std::vector<LaneResult> R;
+      if (!Exec.RunBatch(*Target, Tc, R, &Slots)) {
+        printf("RunBatch failed\n");
+        return 1;
+      }
+      for (size_t i = 0; i < n; i++) {
+        const LaneResult &L = R[i];
+        Retired += L.icount;
+        std::vector<uint64_t> Cov = L.new_coverage;
+        std::sort(Cov.begin(), Cov.end());
+        fprintf(Out, "{\"input\":\"%s\",\"result\":\"%s\",\"crash\":\"%s\",\"error\":%d,\"exit\":%u,\"icount\":%llu,",
+                json_escape(Inputs[b + i].filename().string()).c_str(), TestcaseResultName(L.result).c_str(),
+                json_escape(crash_name(L.result)).c_str(), (int)L.error, L.exit_status,
+                (unsigned long long)L.icount);
+        fprintf(Out, "\"gprs\":[");
+        for (int g = 0; g < 18; g++) fprintf(Out, "%s%llu", g ? "," : "", (unsigned long long)L.gprs[g]);
+        fprintf(Out, "],\"coverage\":[");
+        for (size_t c = 0; c < Cov.size(); c++) fprintf(Out, "%s%llu", c ? "," : "", (unsigned long long)Cov[c]);
+        fprintf(Out, "]}\n");
+      }
+    }
+    if (Out != stdout) fclose(Out);
+    if (!O.quiet)
+      fprintf(stderr, "run: %zu testcases, %llu instructions, %.3f s\n", Inputs.size(), (unsigned long long)Retired,
+              secs_since(t0));
+    return 0;
+  }
+
+  // ---- fuzz: in-process master + batched node
+  std::mt19937_64 Rng(O.seed);
+  const fs::path T(O.target);
+  fs::create_directories(T / "outputs");
+  fs::create_directories(T / "crashes");
+  Corpus_t Corpus(T / "outputs", Rng);
+  std::unique_ptr<Mutator_t> Mutator;
+  if (Target->CreateMutator) Mutator = Target->CreateMutator(Rng, O.max_len);
+  if (!Mutator) {
+    printf("Target %s has no mutator\n", O.name.c_str());
+    return 1;
+  }
+  // the master sends the corpus first (server.h:756-790), then mutations
+  std::vector<std::string> Pending;
+  for (const auto &P : list_inputs(T / "inputs")) {
+    const auto B = ReadFile(P);
+    Pending.emplace_back(B.begin(), B.end());
+  }
+  uint64_t Execs = 0, Retired = 0, Crashes = 0, Timeouts = 0, Cr3s = 0, Errors = 0, Batches = 0;
+  std::unordered_set<std::string> CrashNames;
+  double RunSeconds = 0;
+  const auto t0 = Clock::now();
+  while ((O.runs == 0 || Execs < O.runs) && (O.seconds <= 0 || secs_since(t0) < O.seconds)) {
+    uint64_t n = N;
+    if (O.runs) n = std::min<uint64_t>(n, O.runs - Execs);
+    std::vector<std::string> Batch;
+    Batch.reserve(n);
+    while (Batch.size() < n && !Pending.empty()) {
+      Batch.push_back(std::move(Pending.back()));
+      Pending.pop_back();
+    }
+    while (Batch.size() < n) {
+      if (Corpus.Size() == 0 && Batch.empty()) break;
+      std::string S = Corpus.Size() ? Mutator->GetNewTestcase(Corpus) : Batch[Rng() % Batch.size()];
+      if (S.size() > O.max_len) S.resize(O.max_len);
+      Batch.push_back(std::move(S));
+    }
+    if (Batch.empty()) {
+      printf("Nothing to run: empty corpus and no inputs\n");
+      return 1;
+    }
+    std::vector<std::pair<const uint8_t *, size_t>> Tc(Batch.size());
+    for (size_t i = 0; i < Batch.size(); i++) Tc[i] = {(const uint8_t *)Batch[i].data(), Batch[i].size()};
+    std::vector<LaneResult> R;
+    const auto tb = Clock::now();
+    if (!Exec.RunBatch(*Target, Tc, R, &Slots)) {
+      printf("RunBatch failed\n");
+      return 1;
+    }
+    RunSeconds += secs_since(tb);
+    Batches++;
+    // master bookkeeping in lane order (server.h:816-886)
+    for (size_t i = 0; i < Batch.size(); i++) {
+      const LaneResult &L = R[i];
+      Execs++;
+      Retired += L.icount;
+      Errors += L.error;
+      if (std::holds_alternative<Timedout_t>(L.result)) Timeouts++;
+      if (std::holds_alternative<Cr3Change_t>(L.result)) Cr3s++;
+      if (const Crash_t *C = std::get_if<Crash_t>(&L.result)) {
+        Crashes++;
+        if (!C->CrashName.empty() && CrashNames.insert(C->CrashName).second)
+          SaveFile(T / "crashes" / C->CrashName, (const uint8_t *)Batch[i].data(), Batch[i].size());
+      }
+      if (!L.new_coverage.empty() && !std::holds_alternative<Crash_t>(L.result)) {
+        Testcase_t Tcase((const uint8_t *)Batch[i].data(), Batch[i].size());
+        Mutator->OnNewCoverage(Tcase);
+        Corpus.SaveTestcase(L.result, std::move(Tcase));
+      }
+    }
+  }
+  const double Wall = secs_since(t0);
+  printf("{\"mode\":\"fuzz\",\"target\":\"%s\",\"lanes\":%u,\"batches\":%llu,\"execs\":%llu,\"retired\":%llu,"
+         "\"wall_s\":%.6f,\"run_s\":%.6f,\"execs_per_s\":%.3f,\"instr_per_s\":%.3f,\"coverage\":%zu,"
+         "\"corpus\":%zu,\"crashes\":%llu,\"unique_crashes\":%zu,\"timeouts\":%llu,\"cr3\":%llu,\"errors\":%llu,"
+         "\"backend\":%s}\n",
+         O.name.c_str(), N, (unsigned long long)Batches, (unsigned long long)Execs, (unsigned long long)Retired, Wall,
+         RunSeconds, Execs / RunSeconds, Retired / RunSeconds, Exec.CoverageSize(), Corpus.Size(),
+         (unsigned long long)Crashes, CrashNames.size(), (unsigned long long)Timeouts, (unsigned long long)Cr3s,
+         (unsigned long long)Errors, Exec.StatsJson().c_str());
+  return 0;
+}
+
+}  // namespace wtfgpu_host

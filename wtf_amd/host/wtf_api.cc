@@ -7,6 +7,7 @@
 #include <fstream>
 #include <sstream>
 
+#include "blake3_lite.h"
 #include "json_lite.h"
 
 Backend_t *g_Backend = nullptr;
@@ -295,5 +296,53 @@ bool SanitizeCpuState(CpuState_t &S) {
     }
   }
   if (S.MxcsrMask == 0) S.MxcsrMask = 0xffbf;
+  return true;
+}
+
+// ------------------------------------------------------------------ corpus / files
+std::string TestcaseResultName(const TestcaseResult_t &Res) {
+  return std::string(std::visit([](const auto &R) { return std::string_view(R.Name()); }, Res));
+}
+
+// utils.cc:279-300: 16-byte BLAKE3 digest as hex, low nibble first per byte
+// (the reference's order, so saved file names match)
+std::string Blake3HexDigest(const uint8_t *Data, const size_t DataSize) {
+  uint8_t H[16];
+  wtfgpu_host::blake3_hash(Data, DataSize, H, sizeof(H));
+  static const char *Hex = "0123456789abcdef";
+  std::string S;
+  for (uint8_t B : H) {
+    S.push_back(Hex[B & 15]);
+    S.push_back(Hex[B >> 4]);
+  }
+  return S;
+}
+
+bool SaveFile(const fs::path &Path, const uint8_t *Buffer, const size_t BufferSize) {
+  std::ofstream F(Path, std::ios::binary);
+  if (!F) return false;
+  F.write((const char *)Buffer, BufferSize);
+  return bool(F);
+}
+
+std::vector<uint8_t> ReadFile(const fs::path &Path) {
+  std::ifstream F(Path, std::ios::binary);
+  return std::vector<uint8_t>((std::istreambuf_iterator<char>(F)), std::istreambuf_iterator<char>());
+}
+
+// corpus.h:56-86
+bool Corpus_t::SaveTestcase(const TestcaseResult_t &Result, Testcase_t Testcase) {
+  const std::string Hash = Blake3HexDigest(Testcase.Buffer_.get(), Testcase.BufferSize_);
+  std::string Name = Hash;
+  if (!std::holds_alternative<Ok_t>(Result)) Name = TestcaseResultName(Result) + "-" + Hash;
+  if (!OutputsPath_.empty()) {
+    const fs::path Out = OutputsPath_ / Name;
+    if (!fs::exists(Out) && !SaveFile(Out, Testcase.Buffer_.get(), Testcase.BufferSize_)) {
+      printf("Could not create the destination file.\n");
+      return false;
+    }
+  }
+  Bytes_ += Testcase.BufferSize_;
+  Testcases_.emplace_back(std::move(Testcase));
   return true;
 }

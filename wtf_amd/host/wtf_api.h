@@ -29,6 +29,8 @@
 #include <variant>
 #include <vector>
 
+#include "module_slots.h"
+
 namespace fs = std::filesystem;
 
 namespace Page {
@@ -281,9 +283,48 @@ class Backend_t {
 
 extern Backend_t *g_Backend;
 
+// ------------------------------------------------------------------ corpus / mutators
+// corpus.h:17-38 (Testcase_t), :40-103 (Corpus_t); mutator.h:10-20 (Mutator_t).
+struct Testcase_t {
+  std::unique_ptr<uint8_t[]> Buffer_;
+  size_t BufferSize_ = 0;
+  Testcase_t(const uint8_t *Buffer, const size_t BufferSize)
+      : Buffer_(new uint8_t[BufferSize ? BufferSize : 1]), BufferSize_(BufferSize) {
+    if (BufferSize) memcpy(Buffer_.get(), Buffer, BufferSize);
+  }
+  Testcase_t(Testcase_t &&) = default;
+  Testcase_t &operator=(Testcase_t &&) = default;
+};
+
+class Corpus_t {
+  std::vector<Testcase_t> Testcases_;
+  fs::path OutputsPath_;
+  uint64_t Bytes_ = 0;
+  std::mt19937_64 &Rng_;
+
+ public:
+  Corpus_t(const fs::path &OutputsPath, std::mt19937_64 &Rng) : OutputsPath_(OutputsPath), Rng_(Rng) {}
+  Corpus_t(const Corpus_t &) = delete;
+  Corpus_t &operator=(const Corpus_t &) = delete;
+  size_t Size() const { return Testcases_.size(); }
+  // Saved as <result>-<blake3 hex> ("ok" results unprefixed) under OutputsPath (corpus.h:56-86).
+  bool SaveTestcase(const TestcaseResult_t &Result, Testcase_t Testcase);
+  const Testcase_t *PickTestcase() const {
+    if (Testcases_.empty()) return nullptr;
+    return &Testcases_[std::uniform_int_distribution<size_t>(0, Testcases_.size() - 1)(Rng_)];
+  }
+  uint64_t Bytes() const { return Bytes_; }
+};
+
+class Mutator_t {
+ public:
+  Mutator_t() = default;
+  virtual ~Mutator_t() = default;
+  virtual std::string GetNewTestcase(const Corpus_t &Corpus) = 0;
+  virtual void OnNewCoverage(const Testcase_t &) {}
+};
+
 // ------------------------------------------------------------------ targets
-class Mutator_t;
-struct Corpus_t;
 
 struct Target_t {
   using Init_t = bool (*)(const Options_t &, const CpuState_t &);
@@ -324,6 +365,10 @@ extern Debugger_t g_Dbg;
 
 // ------------------------------------------------------------------ utils
 std::string_view ExceptionCodeToStr(const uint32_t ExceptionCode);
+std::string TestcaseResultName(const TestcaseResult_t &Res);
+std::string Blake3HexDigest(const uint8_t *Data, const size_t DataSize);
+bool SaveFile(const fs::path &Path, const uint8_t *Buffer, const size_t BufferSize);
+std::vector<uint8_t> ReadFile(const fs::path &Path);
 bool LoadCpuStateFromJSON(CpuState_t &CpuState, const fs::path &CpuStatePath);
 bool SanitizeCpuState(CpuState_t &CpuState);
 
