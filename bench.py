@@ -65,6 +65,7 @@ def cpu_baseline(seconds: float, threads: int, limit: int):
 
     from tests.oracle_lib import Oracle
     from wtf_amd.abi import EXIT_BREAKPOINT, regs_from_state
+    from wtf_amd import shard
     from wtf_amd.tools import syn
 
     sp, st, _ = syn.build()
@@ -161,7 +162,7 @@ def main():
         eng.L.wtfgpu_coverage_device_map(eng.ctx, C.byref(p), C.byref(nb))
         cov_t = torch.as_tensor(_DevBuf(p.value, nb.value), device=f"cuda:{local}")
 
-    rng_seed = syn.SEED + 7919 * rank
+    rng_seed = shard.rank_seed(syn.SEED, rank)
     pool = syn.inputs(n * 4, seed=rng_seed)  # input pool; each step takes a rotating window
 
     stats = {"execs": 0, "retired": 0, "kernel_ms": 0.0, "launches": 0, "bytes_alg": 0, "dirty": 0,
@@ -185,7 +186,7 @@ def main():
             eng.commit_coverage(new)
         if cov_t is not None:
             torch.cuda.synchronize()
-            dist.all_reduce(cov_t, op=dist.ReduceOp.MAX)
+            shard.merge_coverage_map(cov_t, dist)
             torch.cuda.synchronize()
         if record:
             nb = eng.nbytes()
@@ -212,16 +213,8 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
 
-    totals = np.array([dt, stats["execs"], stats["retired"]], dtype=np.float64)
-    if dist is not None:
-        t = torch.tensor(totals, device=f"cuda:{local}")
-        tmax = t.clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        dt = float(tmax[0].item())
-        execs, retired = float(t[1].item()), float(t[2].item())
-    else:
-        execs, retired = float(totals[1]), float(totals[2])
+    dt, execs, retired = shard.job_totals(dt, float(stats["execs"]), float(stats["retired"]), dist,
+                                          device=f"cuda:{local}")
 
     if stats["bad"]:
         raise SystemExit(f"{stats['bad']} testcases did not reach the exit breakpoint")
