@@ -24,6 +24,13 @@ The JSON line carries:
   cpu_baseline  the C oracle ("port": the build's scalar restatement, since
                 bochscpu is unbuildable) timed on host cores over a
                 bounded sample of the same SYN workload, one lane per thread.
+  tlv           (N=1, rank 0) BASELINE.json configs[2]: the synthetic
+                tlv_server snapshot fuzzed by the `wtfgpu` node (C++
+                GpuBackend_t, tlv module, breakpoints serviced on host
+                threads), next to the oracle twin `wtf_twin fuzz` run as one
+                process per host core (the reference's one-client-per-core
+                layout). Both rates are execs / wall time,
+                mutation included.
 """
 from __future__ import annotations
 
@@ -53,7 +60,63 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (wall)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-tlv", action="store_true", help="skip the tlv_server leg")
+    ap.add_argument("--tlv-batches", type=int, default=6)
+    ap.add_argument("--tlv-cpu-seconds", type=float, default=10.0)
     return ap.parse_args()
+
+
+# ----------------------------------------------------------------- tlv_server leg
+def tlv_leg(lanes: int, batches: int, cpu_seconds: float, cores: int, limit: int, run_cpu: bool):
+    """configs[2]: wtfgpu fuzz on the synthetic tlv_server snapshot (one GPU),
+    and the oracle twin on `cores` host processes over the same wall window."""
+    import shutil
+    import subprocess
+    import tempfile
+
+    from wtf_amd.tools.tlv import build, seed_inputs
+
+    wtfgpu = os.path.join(ROOT, "wtf_amd", "host", "wtfgpu")
+    twin = os.path.join(ROOT, "oracle", "wtf_twin")
+    tmp = tempfile.mkdtemp(prefix="wtf_tlv_")
+    try:
+        base = os.path.join(tmp, "t0")
+        build(os.path.join(base, "state"), os.path.join(base, "work"))
+        seed_inputs(os.path.join(base, "inputs"))
+        out = subprocess.run([wtfgpu, "fuzz", "--name", "tlv_server", "--target", base, "--lanes", str(lanes),
+                              "--runs", str(lanes * batches), "--seed", "1337", "--limit", str(limit)],
+                             check=True, capture_output=True, text=True, timeout=600).stdout
+        g = json.loads([x for x in out.splitlines() if x.startswith("{")][-1])
+        res = {"workload": "synthetic tlv_server snapshot (BASELINE.json configs[2]), tlv mutator, seed 1337",
+               "lanes": lanes, "execs": g["execs"], "wall_s": g["wall_s"],
+               "value": g["execs"] / g["wall_s"], "unit": "execs/s",
+               "instr_per_s": g["retired"] / g["wall_s"], "instr_per_exec": g["retired"] / max(1, g["execs"]),
+               "unique_crashes": g["unique_crashes"], "coverage": g["coverage"], "errors": g["errors"],
+               "backend": g["backend"]}
+        if run_cpu:
+            procs = []
+            for i in range(cores):
+                d = os.path.join(tmp, f"c{i}")
+                shutil.copytree(base, d, ignore=shutil.ignore_patterns("outputs", "crashes", "work"))
+                procs.append(subprocess.Popen([twin, "fuzz", "--name", "tlv_server", "--target", d, "--lanes", "1024",
+                                               "--seconds", str(cpu_seconds), "--seed", str(1337 + i),
+                                               "--limit", str(limit)], stdout=subprocess.PIPE, text=True))
+            execs = instr = 0.0
+            wall = 0.0
+            for p in procs:
+                o, _ = p.communicate(timeout=cpu_seconds * 4 + 120)
+                t = json.loads([x for x in o.splitlines() if x.startswith("{")][-1])
+                execs += t["execs"]
+                instr += t["retired"]
+                wall = max(wall, t["wall_s"])
+            res["cpu_baseline"] = {"value": execs / wall, "unit": "execs/s", "instr_per_s": instr / wall,
+                                   "cores": cores, "kind": "port",
+                                   "sample": f"{int(execs)} tlv testcases over {wall:.1f}s, {cores} wtf_twin fuzz "
+                                             f"processes (oracle behind Backend_t, one per core)"}
+            res["vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+        return res
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 # ----------------------------------------------------------------- CPU baseline
@@ -65,7 +128,6 @@ def cpu_baseline(seconds: float, threads: int, limit: int):
 
     from tests.oracle_lib import Oracle
     from wtf_amd.abi import EXIT_BREAKPOINT, regs_from_state
-    from wtf_amd import shard
     from wtf_amd.tools import syn
 
     sp, st, _ = syn.build()
@@ -147,6 +209,7 @@ def main():
 
     from tests.syn_harness import make_engine
     from wtf_amd.abi import EXIT_BREAKPOINT
+    from wtf_amd import shard
     from wtf_amd.tools import syn
 
     n = a.lanes
@@ -260,8 +323,14 @@ def main():
             "gpu_retired_fraction": 1.0,
             "cpu_baseline": cpu,
         }
+        if world == 1 and not a.no_tlv:
+            eng.close()
+            eng = None
+            out["tlv"] = tlv_leg(a.lanes, a.tlv_batches, a.tlv_cpu_seconds,
+                                 a.cpu_threads or min(16, os.cpu_count() or 1), a.limit, not a.no_cpu)
         print(json.dumps(out), flush=True)
-    eng.close()
+    if eng is not None:
+        eng.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -227,6 +227,10 @@ int wtfgpu_read_dirty_list(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, u
 uint32_t wtfgpu_overlay_pages(wtfgpu_ctx *ctx);
 int wtfgpu_gather_pages(wtfgpu_ctx *ctx, const uint32_t *lanes, const uint64_t *gpas, uint32_t n, uint8_t *out);
 
+/* Page-locked host memory (for gather/scatter staging buffers). */
+int wtfgpu_host_alloc(wtfgpu_ctx *ctx, uint64_t bytes, void **out);
+int wtfgpu_host_free(wtfgpu_ctx *ctx, void *p);
+
 /* Dirty GPAs (page aligned) of one lane; *n gets the count (may exceed cap). */
 int wtfgpu_read_dirty(wtfgpu_ctx *ctx, uint32_t lane, uint64_t *gpas, uint32_t cap, uint32_t *n);
 

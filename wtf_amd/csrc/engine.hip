@@ -1703,6 +1703,21 @@ int wtfgpu_gather_pages(wtfgpu_ctx *c, const uint32_t *lanes, const uint64_t *gp
   return WTFGPU_OK;
 }
 
+// Page-locked host memory for staging buffers: device<->host copies into it
+// are plain DMA (no bounce through a driver staging buffer).
+int wtfgpu_host_alloc(wtfgpu_ctx *c, uint64_t bytes, void **out) {
+  if (!c || !out || !bytes) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) return WTFGPU_ERR_OOM;
+  return WTFGPU_OK;
+}
+
+int wtfgpu_host_free(wtfgpu_ctx *c, void *p) {
+  if (!c) return WTFGPU_ERR_INVALID;
+  if (p) HIPCHK(hipHostFree(p));
+  return WTFGPU_OK;
+}
+
 int wtfgpu_read_dirty(wtfgpu_ctx *c, uint32_t lane, uint64_t *gpas, uint32_t cap, uint32_t *n) {
   if (!c || lane >= c->P.nlanes || !n) return WTFGPU_ERR_INVALID;
   HIPCHK(hipSetDevice(c->device));

@@ -6,9 +6,16 @@
 #include <cstdio>
 #include <cstring>
 
+#include <omp.h>
+
 #include "blake3_lite.h"
 
 namespace wtfgpu_host {
+
+thread_local uint32_t GpuBackend_t::cur_ = 0;
+thread_local uint64_t GpuBackend_t::servicing_bp_ = ~0ull;
+thread_local uint64_t GpuBackend_t::servicing_sp_ = ~0ull;
+thread_local bool GpuBackend_t::scouting_ = false;
 
 namespace {
 using Clock = std::chrono::steady_clock;
@@ -73,6 +80,7 @@ bool GpuBackend_t::Initialize(const Options_t &Opts, const CpuState_t &CpuState)
   if (wtfgpu_alloc_lanes(ctx_, nlanes_, overlay_pages_, 1024)) return false;
   views_.clear();
   views_.resize(nlanes_);
+  arenas_.resize(omp_get_max_threads() + 1);
   if (Opts.Limit) SetLimit(Opts.Limit);
   if (!Restore(CpuState)) return false;
   return set_code_pages();
@@ -100,7 +108,7 @@ void GpuBackend_t::reset_view(uint32_t lane) {
   v.seed = initial_.Seed;  // Rdrand seed (bochscpu_backend.cc:1030)
   v.dirty_known = true;    // a restored lane has an empty overlay
   v.dirty.clear();
-  v.pages.clear();
+  drop_staged(v);
 }
 
 void GpuBackend_t::Stop(const TestcaseResult_t &Res) { cur().result = Res; }
@@ -154,35 +162,126 @@ bool GpuBackend_t::SetBreakpoint(const Gva_t Gva, const BreakpointHandler_t Hand
 // Writes go to lane overlays, which the device dirties by itself.
 bool GpuBackend_t::DirtyGpa(const Gpa_t) { return true; }
 
+namespace {
+constexpr size_t kArenaBlock = 16u << 20;  // 4096 staging slots per block
+const uint8_t kZeroPage[Page::Size] = {};
+}  // namespace
+
+size_t GpuBackend_t::alloc_slots(size_t n, uint8_t **orig, uint8_t **data) const {
+  Arena &A = arenas_[omp_in_parallel() ? omp_get_thread_num() : 0];
+  while (A.cur < A.blocks.size() && A.blocks[A.cur].cap - A.blocks[A.cur].used < n) A.cur++;
+  if (A.cur == A.blocks.size()) {
+    Block b;
+    b.cap = std::max<size_t>(n, kArenaBlock / Page::Size);
+    void *p = nullptr;
+    int rc;
+    {
+      std::lock_guard<std::mutex> g(engine_mu_);
+      rc = wtfgpu_host_alloc(ctx_, b.cap * Page::Size, &p);
+    }
+    if (rc != WTFGPU_OK) {
+      printf("wtfgpu_host_alloc failed\n");
+      std::abort();
+    }
+    b.orig = (uint8_t *)p;
+    b.data.reset(new uint8_t[b.cap * Page::Size]);
+    A.blocks.push_back(std::move(b));
+  }
+  Block &b = A.blocks[A.cur];
+  *orig = b.orig + b.used * Page::Size;
+  *data = b.data.get() + b.used * Page::Size;
+  const size_t first = b.used;
+  b.used += n;
+  return first;
+}
+
+bool GpuBackend_t::parallel_service(const ModuleSlots *slots) const {
+  return slots && slots->ThreadSafe() && omp_get_max_threads() > 1;
+}
+
+uint8_t *GpuBackend_t::stage(uint32_t lane, uint64_t gpfn, const uint8_t *orig, uint8_t *data) const {
+  live_staged_++;
+  views_[lane].pages.push_back(Staged{gpfn, data, orig});
+  return data;
+}
+
+uint8_t *GpuBackend_t::stage_copy(uint32_t lane, uint64_t gpfn, const uint8_t *orig) const {
+  uint8_t *o, *d;
+  alloc_slots(1, &o, &d);
+  memcpy(d, orig, Page::Size);
+  return stage(lane, gpfn, orig, d);
+}
+
+void GpuBackend_t::drop_staged(LaneView &v) const {
+  live_staged_ -= v.pages.size();
+  v.pages.clear();
+  if (live_staged_ == 0 && !omp_in_parallel()) {  // every staged page consumed: recycle the arenas
+    for (Arena &A : arenas_) {
+      for (Block &b : A.blocks) b.used = 0;
+      A.cur = 0;
+    }
+  }
+}
+
+GpuBackend_t::Staged *GpuBackend_t::find_staged(uint32_t lane, uint64_t gpfn) const {
+  for (Staged &p : views_[lane].pages)
+    if (p.gpfn == gpfn) return &p;
+  return nullptr;
+}
+
+bool GpuBackend_t::in_overlay(const LaneView &v, uint64_t gpfn) const {
+  return std::find(v.dirty.begin(), v.dirty.end(), (uint32_t)gpfn) != v.dirty.end();
+}
+
 // The lane's view of a physical page, on the host: staged copy, else a fetch of
 // the lane's overlay page, else the dump page (or zeros).
 uint8_t *GpuBackend_t::lane_page(uint32_t lane, uint64_t gpfn) const {
+  if (Staged *p = find_staged(lane, gpfn)) return p->data;
   LaneView &v = views_[lane];
-  auto it = v.pages.find(gpfn);
-  if (it != v.pages.end()) return it->second.data.get();
   if (!v.dirty_known) {
     std::vector<uint32_t> buf(overlay_pages_ + 1);
+    std::lock_guard<std::mutex> g(engine_mu_);
     wtfgpu_read_dirty_list(ctx_, &lane, 1, buf.data());
     v.dirty.assign(buf.begin() + 1, buf.begin() + 1 + std::min<uint32_t>(buf[0], overlay_pages_));
     v.dirty_known = true;
   }
-  HostPage hp;
-  hp.data.reset(new uint8_t[Page::Size]);
-  const bool in_overlay = std::find(v.dirty.begin(), v.dirty.end(), (uint32_t)gpfn) != v.dirty.end();
-  if (in_overlay) {
+  if (in_overlay(v, gpfn)) {
+    const auto t0 = Clock::now();
+    uint8_t *o, *d;
+    alloc_slots(1, &o, &d);
     const uint64_t gpa = gpfn << 12;
-    wtfgpu_gather_pages(ctx_, &lane, &gpa, 1, hp.data.get());
+    std::lock_guard<std::mutex> g(engine_mu_);
+    wtfgpu_gather_pages(ctx_, &lane, &gpa, 1, o);
+    memcpy(d, o, Page::Size);
     stats_.page_fetches++;
-  } else if (const uint8_t *p = dump_.GetPhysicalPage(gpfn << 12)) {
-    memcpy(hp.data.get(), p, Page::Size);
-  } else {
-    memset(hp.data.get(), 0, Page::Size);
+    stats_.fetch_ms += ms_since(t0);
+    fetch_by_bp_[servicing_bp_]++;
+    learn(gpfn);
+    return stage(lane, gpfn, o, d);
   }
-  hp.orig.reset(new uint8_t[Page::Size]);
-  memcpy(hp.orig.get(), hp.data.get(), Page::Size);
-  uint8_t *r = hp.data.get();
-  v.pages.emplace(gpfn, std::move(hp));
-  return r;
+  if (scouting_) learn(gpfn);  // serial: no other thread reads or writes the tables
+  const uint8_t *p = dump_.GetPhysicalPage(gpfn << 12);
+  return stage_copy(lane, gpfn, p ? p : kZeroPage);
+}
+
+// Learned prefetch: the breakpoint being serviced touched frame `gpfn`
+// (caller holds engine_mu_ or runs serially).
+void GpuBackend_t::learn(uint64_t gpfn) const {
+  if (servicing_bp_ == ~0ull) return;
+  if (gpfn == servicing_sp_) {
+    bp_stack_.insert(servicing_bp_);
+    return;
+  }
+  auto &l = bp_pages_[servicing_bp_];
+  if (l.size() < 8 && std::find(l.begin(), l.end(), gpfn) == l.end()) l.push_back(gpfn);
+}
+
+const uint8_t *GpuBackend_t::lane_page_ro(uint32_t lane, uint64_t gpfn) const {
+  if (Staged *p = find_staged(lane, gpfn)) return p->data;
+  const LaneView &v = views_[lane];
+  if (!v.dirty_known || in_overlay(v, gpfn)) return lane_page(lane, gpfn);
+  const uint8_t *p = dump_.GetPhysicalPage(gpfn << 12);
+  return p ? p : kZeroPage;
 }
 
 // bochscpu_mem_virt_translate semantics (present bits only), on the lane view
@@ -190,7 +289,7 @@ bool GpuBackend_t::VirtTranslate(const Gva_t Gva, Gpa_t &Gpa, const MemoryValida
   uint64_t table = initial_.Cr3 & 0x000ffffffffff000ull;
   const uint64_t va = Gva.U64();
   for (int level = 3; level >= 0; level--) {
-    const uint8_t *pg = lane_page(cur_, table >> 12);
+    const uint8_t *pg = lane_page_ro(cur_, table >> 12);
     uint64_t e;
     memcpy(&e, pg + ((va >> (12 + 9 * level)) & 0x1ff) * 8, 8);
     if (!(e & 1)) return false;
@@ -229,12 +328,18 @@ bool GpuBackend_t::RevokeLastNewCoverage() {
   return true;
 }
 
-// Staged registers and memory of `lanes` -> device.
+// Staged registers and memory of `lanes` -> device. Pages are diffed against
+// their original content in parallel; each changed byte range becomes one
+// write record (copy-on-write + dirty on the device).
 int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
   std::vector<uint32_t> rl;
   std::vector<uint64_t> regs;
-  std::vector<wtfgpu_write_t> writes;
-  std::vector<uint8_t> data;
+  struct Cand {
+    uint32_t lane;
+    const Staged *p;
+    uint32_t lo, hi;
+  };
+  std::vector<Cand> cand;
   for (uint32_t l : lanes) {
     LaneView &v = views_[l];
     if (v.regs_dirty) {
@@ -242,22 +347,35 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
       regs.insert(regs.end(), v.gpr, v.gpr + 18);
       v.regs_dirty = false;
     }
-    for (auto &[gpfn, hp] : v.pages) {
-      size_t lo = 0, hi = Page::Size;
-      while (lo < hi && hp.data[lo] == hp.orig[lo]) lo++;
-      while (hi > lo && hp.data[hi - 1] == hp.orig[hi - 1]) hi--;
-      if (lo == hi) continue;
-      wtfgpu_write_t w{};
-      w.lane = l;
-      w.len = (uint32_t)(hi - lo);
-      w.gva = (gpfn << 12) | lo;
-      w.data_off = data.size();
-      data.insert(data.end(), hp.data.get() + lo, hp.data.get() + hi);
-      writes.push_back(w);
-      v.dirty_known = false;  // the device overlay changed
-    }
-    v.pages.clear();
+    for (const Staged &p : v.pages) cand.push_back(Cand{l, &p, 0, 0});
   }
+#pragma omp parallel for schedule(dynamic, 64)
+  for (size_t i = 0; i < cand.size(); i++) {
+    const uint8_t *d = cand[i].p->data, *o = cand[i].p->orig;
+    if (!memcmp(d, o, Page::Size)) continue;
+    size_t lo = 0, hi = Page::Size;
+    while (lo + 8 <= hi && !memcmp(d + lo, o + lo, 8)) lo += 8;
+    while (lo < hi && d[lo] == o[lo]) lo++;
+    while (hi >= lo + 8 && !memcmp(d + hi - 8, o + hi - 8, 8)) hi -= 8;
+    while (hi > lo && d[hi - 1] == o[hi - 1]) hi--;
+    cand[i].lo = (uint32_t)lo;
+    cand[i].hi = (uint32_t)hi;
+  }
+  std::vector<wtfgpu_write_t> writes;
+  std::vector<uint8_t> data;
+  for (const Cand &c : cand) {
+    if (c.lo == c.hi) continue;
+    wtfgpu_write_t w{};
+    w.lane = c.lane;
+    w.len = c.hi - c.lo;
+    w.gva = (c.p->gpfn << 12) | c.lo;
+    w.data_off = data.size();
+    data.insert(data.end(), c.p->data + c.lo, c.p->data + c.hi);
+    writes.push_back(w);
+    views_[c.lane].dirty_known = false;  // the device overlay changed
+  }
+  stats_.staged_pages += cand.size();
+  for (uint32_t l : lanes) drop_staged(views_[l]);
   int rc = WTFGPU_OK;
   if (!rl.empty()) rc = wtfgpu_write_gprs_list(ctx_, rl.data(), (uint32_t)rl.size(), regs.data());
   if (!rc && !writes.empty())
@@ -318,65 +436,122 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
     const uint32_t stride = overlay_pages_ + 1;
     std::vector<uint32_t> dl(hits.size() * stride);
     if (wtfgpu_read_dirty_list(ctx_, hits.data(), (uint32_t)hits.size(), dl.data())) return false;
-    // prefetch the stack page of every hit lane whose overlay holds it (handlers
-    // read their return address / arguments there)
-    std::vector<uint32_t> pf_lanes;
-    std::vector<uint64_t> pf_gpas;
+    const auto t1 = Clock::now();
+    stats_.bulk_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    // prefetch, in one bulk gather, the overlay frames the handlers will touch,
+    // learned from the on-demand fetches of earlier hits of the same
+    // breakpoint: its stack page (return address / arguments, bp_stack_) and
+    // fixed frames (e.g. the tlv packet buffer, bp_pages_)
+    std::vector<uint64_t> sp_gpfn(hits.size(), ~0ull);
     for (size_t i = 0; i < hits.size(); i++) {
       LaneView &v = views_[hits[i]];
       memcpy(v.gpr, &regs[i * 18], 18 * 8);
       v.regs_dirty = false;
-      v.pages.clear();
+      drop_staged(v);
       const uint32_t cnt = std::min(dl[i * stride], overlay_pages_);
       v.dirty.assign(dl.begin() + i * stride + 1, dl.begin() + i * stride + 1 + cnt);
       v.dirty_known = true;
       cur_ = hits[i];
       Gpa_t sp;
-      if (VirtTranslate(Gva_t(v.gpr[WTFGPU_RSP]), sp, MemoryValidate_t::ValidateRead) &&
-          std::find(v.dirty.begin(), v.dirty.end(), (uint32_t)(sp.U64() >> 12)) != v.dirty.end()) {
-        pf_lanes.push_back(hits[i]);
-        pf_gpas.push_back(sp.U64() & ~0xfffull);
-      }
+      if (VirtTranslate(Gva_t(v.gpr[WTFGPU_RSP]), sp, MemoryValidate_t::ValidateRead)) sp_gpfn[i] = sp.U64() >> 12;
     }
-    if (!pf_lanes.empty()) {
-      std::vector<uint8_t> buf(pf_lanes.size() * Page::Size);
-      if (wtfgpu_gather_pages(ctx_, pf_lanes.data(), pf_gpas.data(), (uint32_t)pf_lanes.size(), buf.data()))
-        return false;
-      for (size_t i = 0; i < pf_lanes.size(); i++) {
-        HostPage hp;
-        hp.data.reset(new uint8_t[Page::Size]);
-        hp.orig.reset(new uint8_t[Page::Size]);
-        memcpy(hp.data.get(), buf.data() + i * Page::Size, Page::Size);
-        memcpy(hp.orig.get(), hp.data.get(), Page::Size);
-        views_[pf_lanes[i]].pages[pf_gpas[i] >> 12] = std::move(hp);
-      }
-      stats_.prefetched_pages += pf_lanes.size();
-    }
-    std::vector<uint32_t> resume, stop;
-    std::vector<uint8_t> skip;
-    Backend_t *saved = g_Backend;
-    g_Backend = this;
-    for (uint32_t l : hits) {
+    // the handlers: lane by lane, or on all host threads when the module keeps
+    // its per-testcase state thread_local (each thread services its own lanes
+    // with g_Backend = this and its own swapped-in module state). The order of
+    // lanes does not matter: every lane has its own view and module state.
+    std::vector<uint8_t> action(hits.size());  // 0 stop, 1 resume, 2 resume + skip the breakpoint
+    auto service = [&](size_t h) {
+      const uint32_t l = hits[h];
       LaneView &v = views_[l];
       cur_ = l;
       const uint64_t rip0 = v.gpr[16];
+      servicing_sp_ = sp_gpfn[h];
       auto it = breakpoints_.find(rip0);
       if (per_lane_state && slots) slots->SwapIn(l);
+      servicing_bp_ = rip0;
       if (it != breakpoints_.end()) it->second(this);  // BeforeExecutionHook (bochscpu_backend.cc:545-547)
+      servicing_bp_ = ~0ull;
       if (per_lane_state && slots) slots->SwapOut(l);
-      stats_.breakpoint_hits++;
-      if (v.result) {
-        stop.push_back(l);
-        done[l - first] = 1;
-      } else {
-        resume.push_back(l);
-        skip.push_back(v.gpr[16] == rip0 ? 1 : 0);  // U10: a moved rip cancels the hooked instruction
+      action[h] = v.result ? 0 : (v.gpr[16] == rip0 ? 2 : 1);  // U10: a moved rip cancels the hooked instruction
+    };
+    Backend_t *saved = g_Backend;
+    g_Backend = this;
+    // scouts: the first hit of a breakpoint never serviced before runs alone
+    // first, so its on-demand page fetches teach the prefetcher (below) what
+    // the other lanes' handlers will touch
+    std::vector<uint8_t> scouted(hits.size(), 0);
+    for (size_t i = 0; i < hits.size(); i++) {
+      if (!bp_seen_.insert(views_[hits[i]].gpr[16]).second) continue;
+      scouting_ = true;
+      service(i);
+      scouting_ = false;
+      scouted[i] = 1;
+    }
+    // prefetch, in one bulk gather, the overlay frames the handlers will touch,
+    // learned from the on-demand fetches of earlier hits of the same
+    // breakpoint: its stack page (return address / arguments, bp_stack_) and
+    // fixed frames (e.g. the tlv packet buffer, bp_pages_)
+    std::vector<uint32_t> pf_lanes;
+    std::vector<uint64_t> pf_gpas;
+    for (size_t i = 0; i < hits.size(); i++) {
+      if (scouted[i]) continue;
+      const LaneView &v = views_[hits[i]];
+      auto want = [&](uint64_t gpfn) {
+        if (!in_overlay(v, gpfn)) return;
+        for (size_t k = pf_gpas.size(); k-- > 0 && pf_lanes[k] == hits[i];)
+          if (pf_gpas[k] == gpfn << 12) return;
+        pf_lanes.push_back(hits[i]);
+        pf_gpas.push_back(gpfn << 12);
+      };
+      if (sp_gpfn[i] != ~0ull && bp_stack_.count(v.gpr[16])) want(sp_gpfn[i]);
+      auto lp = bp_pages_.find(v.gpr[16]);
+      if (lp != bp_pages_.end())
+        for (uint64_t g : lp->second) want(g);
+    }
+    if (!pf_lanes.empty()) {
+      const size_t np = pf_lanes.size();
+      uint8_t *o, *d;
+      alloc_slots(np, &o, &d);
+      if (wtfgpu_gather_pages(ctx_, pf_lanes.data(), pf_gpas.data(), (uint32_t)np, o)) return false;
+#pragma omp parallel for schedule(static)
+      for (size_t i = 0; i < np; i++) memcpy(d + i * Page::Size, o + i * Page::Size, Page::Size);
+      for (size_t i = 0; i < np; i++)
+        stage(pf_lanes[i], pf_gpas[i] >> 12, o + i * Page::Size, d + i * Page::Size);
+      stats_.prefetched_pages += np;
+    }
+    const auto t2 = Clock::now();
+    stats_.prefetch_ms += std::chrono::duration<double, std::milli>(t2 - t1).count();
+    if (per_lane_state && parallel_service(slots)) {
+#pragma omp parallel
+      {
+        g_Backend = this;
+#pragma omp for schedule(dynamic, 64)
+        for (size_t h = 0; h < hits.size(); h++)
+          if (!scouted[h]) service(h);
       }
+    } else {
+      for (size_t h = 0; h < hits.size(); h++)
+        if (!scouted[h]) service(h);
     }
     g_Backend = saved;
+    stats_.breakpoint_hits += hits.size();
+    std::vector<uint32_t> resume, stop;
+    std::vector<uint8_t> skip;
+    for (size_t h = 0; h < hits.size(); h++) {
+      if (action[h] == 0) {
+        stop.push_back(hits[h]);
+        done[hits[h] - first] = 1;
+      } else {
+        resume.push_back(hits[h]);
+        skip.push_back(action[h] == 2);
+      }
+    }
+    const auto t3 = Clock::now();
+    stats_.handler_ms += std::chrono::duration<double, std::milli>(t3 - t2).count();
     if (flush_lanes(hits)) return false;
     if (!stop.empty() && wtfgpu_stop(ctx_, stop.data(), (uint32_t)stop.size(), WTFGPU_EXIT_STOPPED)) return false;
     if (!resume.empty() && wtfgpu_resume(ctx_, resume.data(), (uint32_t)resume.size(), skip.data())) return false;
+    stats_.flush_ms += ms_since(t3);
     stats_.service_ms += ms_since(t0);
     pending = resume;
   }
@@ -464,34 +639,63 @@ bool GpuBackend_t::RunBatch(const Target_t &Target, const std::vector<std::pair<
   for (uint32_t l = 0; l < n; l++) reset_view(l);
   // InsertTestcase per lane (client.cc:102), module state per lane
   Backend_t *saved = g_Backend;
-  g_Backend = this;
   std::vector<uint32_t> lanes(n);
-  for (uint32_t l = 0; l < n; l++) {
-    lanes[l] = l;
+  std::vector<uint8_t> insert_ok(n, 1);
+  auto insert = [&](uint32_t l) {
     cur_ = l;
     if (Slots) Slots->SwapIn(l);
-    const bool ok = Target.InsertTestcase(Testcases[l].first, Testcases[l].second);
+    insert_ok[l] = Target.InsertTestcase(Testcases[l].first, Testcases[l].second);
     if (Slots) Slots->SwapOut(l);
-    if (!ok) views_[l].result = Crash_t("insert-testcase-failed");
+  };
+  const bool par = parallel_service(Slots);
+  if (par) {
+#pragma omp parallel
+    {
+      g_Backend = this;
+#pragma omp for schedule(dynamic, 256)
+      for (uint32_t l = 0; l < n; l++) insert(l);
+    }
+  } else {
+    g_Backend = this;
+    for (uint32_t l = 0; l < n; l++) insert(l);
   }
   g_Backend = saved;
+  for (uint32_t l = 0; l < n; l++) {
+    lanes[l] = l;
+    if (!insert_ok[l]) views_[l].result = Crash_t("insert-testcase-failed");
+  }
   if (flush_lanes(lanes)) return false;
+  stats_.insert_ms += ms_since(t0);
   if (!run_lanes(lanes, &Out, Slots, Slots != nullptr)) return false;
+  const auto tc = Clock::now();
   std::vector<uint32_t> timedout;
   for (uint32_t l = 0; l < n; l++)
     if (std::holds_alternative<Timedout_t>(Out[l].result)) timedout.push_back(l);
   finish_coverage(n, &Out, &timedout);
+  const auto tr = Clock::now();
+  stats_.coverage_ms += std::chrono::duration<double, std::milli>(tr - tc).count();
   // Target.Restore per lane (client.cc:145), then the device restore happens
   // at the start of the next batch (dirty-list reset)
-  g_Backend = this;
-  for (uint32_t l = 0; l < n; l++) {
+  auto restore = [&](uint32_t l) {
     cur_ = l;
     if (Slots) Slots->SwapIn(l);
     Target.Restore();
     if (Slots) Slots->SwapOut(l);
+  };
+  if (par) {
+#pragma omp parallel
+    {
+      g_Backend = this;
+#pragma omp for schedule(dynamic, 256)
+      for (uint32_t l = 0; l < n; l++) restore(l);
+    }
+  } else {
+    g_Backend = this;
+    for (uint32_t l = 0; l < n; l++) restore(l);
   }
   g_Backend = saved;
   cur_ = 0;
+  stats_.target_restore_ms += ms_since(tr);
   stats_.total_ms += ms_since(t0);
   stats_.batches++;
   stats_.testcases += n;
@@ -505,15 +709,29 @@ void GpuBackend_t::ResetCoverage() {
 }
 
 std::string GpuBackend_t::StatsJson() const {
-  char b[512];
+  char b[1024];
   snprintf(b, sizeof(b),
            "{\"kind\":\"gpu\",\"rounds\":%llu,\"breakpoint_hits\":%llu,\"kernel_launches\":%llu,"
            "\"kernel_ms\":%.3f,\"service_ms\":%.3f,\"total_ms\":%.3f,\"page_fetches\":%llu,"
-           "\"prefetched_pages\":%llu}",
+           "\"prefetched_pages\":%llu,\"staged_pages\":%llu,\"bulk_ms\":%.3f,\"prefetch_ms\":%.3f,"
+           "\"handler_ms\":%.3f,\"fetch_ms\":%.3f,\"flush_ms\":%.3f,\"insert_ms\":%.3f,\"coverage_ms\":%.3f,"
+           "\"target_restore_ms\":%.3f}",
            (unsigned long long)stats_.rounds, (unsigned long long)stats_.breakpoint_hits,
            (unsigned long long)stats_.kernel_launches, stats_.kernel_ms, stats_.service_ms, stats_.total_ms,
-           (unsigned long long)stats_.page_fetches, (unsigned long long)stats_.prefetched_pages);
-  return b;
+           (unsigned long long)stats_.page_fetches, (unsigned long long)stats_.prefetched_pages,
+           (unsigned long long)stats_.staged_pages, stats_.bulk_ms, stats_.prefetch_ms, stats_.handler_ms,
+           stats_.fetch_ms, stats_.flush_ms, stats_.insert_ms, stats_.coverage_ms, stats_.target_restore_ms);
+  std::string r(b);
+  r.pop_back();
+  r += ",\"fetch_by_bp\":{";
+  bool first = true;
+  for (const auto &[bp, n] : fetch_by_bp_) {
+    char e[64];
+    snprintf(e, sizeof(e), "%s\"%#llx\":%llu", first ? "" : ",", (unsigned long long)bp, (unsigned long long)n);
+    r += e;
+    first = false;
+  }
+  return r + "}}";
 }
 
 // Coverage index space: every executable leaf page reachable

@@ -13,7 +13,9 @@
 //    the lane (registers gathered in bulk, pages fetched on demand or
 //    prefetched for the stack, writes staged and applied in bulk).
 #pragma once
+#include <atomic>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -28,8 +30,13 @@ namespace wtfgpu_host {
 
 struct BatchStats {
   uint64_t rounds = 0, breakpoint_hits = 0, kernel_launches = 0, retired = 0;
-  uint64_t page_fetches = 0, prefetched_pages = 0, batches = 0, testcases = 0;
+  uint64_t page_fetches = 0, prefetched_pages = 0, batches = 0, testcases = 0, staged_pages = 0;
   double kernel_ms = 0, service_ms = 0, total_ms = 0;
+  // service_ms split: bulk reads (regs, dirty lists), stack/learned prefetch,
+  // module handlers (incl. on-demand page fetches), flush (writes + resume/stop)
+  double bulk_ms = 0, prefetch_ms = 0, handler_ms = 0, fetch_ms = 0, flush_ms = 0;
+  // RunBatch outside the run loop: restore + InsertTestcase + flush, coverage attribution, Target.Restore
+  double insert_ms = 0, coverage_ms = 0, target_restore_ms = 0;
 };
 
 class GpuBackend_t final : public Backend_t, public Executor_t {
@@ -76,8 +83,13 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   const std::unordered_set<uint64_t> &AggregateCoverage() const { return aggregate_; }
 
  private:
-  struct HostPage {
-    std::unique_ptr<uint8_t[]> data, orig;
+  // A page of a lane's view staged on the host: `data` is what handlers see and
+  // may write through PhysTranslate, `orig` its content when staged (flush
+  // diffs the two). Both live in the staging arena.
+  struct Staged {
+    uint64_t gpfn;
+    uint8_t *data;
+    const uint8_t *orig;
   };
   struct LaneView {
     uint64_t gpr[18] = {};  // wtfgpu order: 16 gprs, rip, rflags
@@ -86,12 +98,24 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
     uint64_t seed = 0;
     bool dirty_known = false;
     std::vector<uint32_t> dirty;  // gpfns the lane's overlay holds
-    std::unordered_map<uint64_t, HostPage> pages;  // gpfn -> host copy (mutable through PhysTranslate)
+    std::vector<Staged> pages;    // staged pages (few per lane: linear search)
   };
 
   LaneView &cur() const { return views_[cur_]; }
   void reset_view(uint32_t lane);
   uint8_t *lane_page(uint32_t lane, uint64_t gpfn) const;
+  // read-only view for page walks: the dump page when the lane's overlay does
+  // not hold the frame (no staging copy)
+  const uint8_t *lane_page_ro(uint32_t lane, uint64_t gpfn) const;
+  Staged *find_staged(uint32_t lane, uint64_t gpfn) const;
+  // n consecutive staging slots (one block): pinned orig pages + data pages
+  size_t alloc_slots(size_t n, uint8_t **orig, uint8_t **data) const;
+  // stage a page whose original content is `orig` (kept alive by the caller:
+  // a dump page, the zero page or a pinned staging slot)
+  uint8_t *stage(uint32_t lane, uint64_t gpfn, const uint8_t *orig, uint8_t *data) const;
+  uint8_t *stage_copy(uint32_t lane, uint64_t gpfn, const uint8_t *orig) const;
+  void drop_staged(LaneView &v) const;
+  bool in_overlay(const LaneView &v, uint64_t gpfn) const;
   int flush_lanes(const std::vector<uint32_t> &lanes);
   bool run_lanes(const std::vector<uint32_t> &lanes, std::vector<LaneResult> *out, ModuleSlots *slots,
                  bool per_lane_state);
@@ -105,11 +129,40 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   uint32_t nlanes_ = 0, overlay_pages_ = 0;
   uint64_t limit_ = 0;
   mutable std::vector<LaneView> views_;
-  uint32_t cur_ = 0;
+  // the lane the calling thread services (handlers of different lanes run on
+  // several threads when the module state is thread_local, module_slots.h)
+  static thread_local uint32_t cur_;
   std::unordered_map<uint64_t, BreakpointHandler_t> breakpoints_;
   std::unordered_set<uint64_t> aggregate_;
   std::unordered_set<Gva_t> last_new_coverage_;
   mutable BatchStats stats_;
+  // staging arena: blocks of slots, each slot a pinned 4 KiB page (device
+  // gathers land there directly) + a 4 KiB data page handed to handlers;
+  // recycled once no lane holds a staged page
+  struct Block {
+    uint8_t *orig = nullptr;
+    std::unique_ptr<uint8_t[]> data;
+    size_t cap = 0, used = 0;
+  };
+  struct Arena {  // one per host thread
+    std::vector<Block> blocks;
+    size_t cur = 0;
+  };
+  mutable std::vector<Arena> arenas_;
+  mutable std::atomic<size_t> live_staged_{0};
+  // serialises engine calls made from handler threads (shared scratch buffers)
+  // and the learned-prefetch tables
+  mutable std::mutex engine_mu_;
+  bool parallel_service(const ModuleSlots *slots) const;
+  // learned prefetch: overlay frames a breakpoint's handler fetched on demand
+  // (e.g. the tlv packet buffer); fetched in bulk for that breakpoint's next hits
+  mutable std::unordered_map<uint64_t, std::vector<uint64_t>> bp_pages_;
+  mutable std::unordered_map<uint64_t, uint64_t> fetch_by_bp_;  // on-demand fetches per breakpoint (stats)
+  mutable std::unordered_set<uint64_t> bp_stack_;
+  std::unordered_set<uint64_t> bp_seen_;  // breakpoints serviced at least once (scouting)  // breakpoints whose handler reads the stack page
+  static thread_local uint64_t servicing_bp_, servicing_sp_;
+  static thread_local bool scouting_;
+  void learn(uint64_t gpfn) const;
   bool full_coverage_ = false;
 };
 

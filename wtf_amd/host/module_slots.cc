@@ -11,7 +11,17 @@ std::vector<LaneStateOps> &LaneStateRegistry() {
   return R;
 }
 
+namespace {
+thread_local int64_t t_in = -1;  // lane swapped in on this thread
+}
+
 ModuleSlots::~ModuleSlots() { release(); }
+
+bool ModuleSlots::ThreadSafe() const {
+  for (const auto &ops : LaneStateRegistry())
+    if (!ops.tls) return false;
+  return !LaneStateRegistry().empty();
+}
 
 void ModuleSlots::release() {
   const auto &R = LaneStateRegistry();
@@ -27,10 +37,10 @@ void ModuleSlots::release() {
 void ModuleSlots::Capture(uint32_t lanes) {
   release();
   const auto &R = LaneStateRegistry();
-  for (const auto &ops : R) initial_.push_back(ops.clone(ops.object));
+  for (const auto &ops : R) initial_.push_back(ops.clone(ops.object()));
   lanes_.assign(lanes, std::vector<void *>(R.size(), nullptr));
   dirty_.assign(lanes, 0);
-  in_ = -1;
+  t_in = -1;
 }
 
 void ModuleSlots::ResetAll() {
@@ -44,29 +54,29 @@ void ModuleSlots::ResetAll() {
 }
 
 void ModuleSlots::SwapIn(uint32_t lane) {
-  if (in_ >= 0) {
-    fprintf(stderr, "ModuleSlots: lane %lld still swapped in\n", (long long)in_);
+  if (t_in >= 0) {
+    fprintf(stderr, "ModuleSlots: lane %lld still swapped in\n", (long long)t_in);
     std::abort();
   }
   const auto &R = LaneStateRegistry();
   auto &objs = lanes_.at(lane);
   for (size_t i = 0; i < R.size(); i++) {
     if (!objs[i]) objs[i] = R[i].clone(initial_[i]);
-    R[i].swap(R[i].object, objs[i]);
+    R[i].swap(R[i].object(), objs[i]);
   }
   dirty_[lane] = 1;
-  in_ = lane;
+  t_in = lane;
 }
 
 void ModuleSlots::SwapOut(uint32_t lane) {
-  if (in_ != (int64_t)lane) {
-    fprintf(stderr, "ModuleSlots: swap-out of lane %u, lane %lld is in\n", lane, (long long)in_);
+  if (t_in != (int64_t)lane) {
+    fprintf(stderr, "ModuleSlots: swap-out of lane %u, lane %lld is in\n", lane, (long long)t_in);
     std::abort();
   }
   const auto &R = LaneStateRegistry();
   auto &objs = lanes_[lane];
-  for (size_t i = 0; i < R.size(); i++) R[i].swap(R[i].object, objs[i]);
-  in_ = -1;
+  for (size_t i = 0; i < R.size(); i++) R[i].swap(R[i].object(), objs[i]);
+  t_in = -1;
 }
 
 }  // namespace wtfgpu_host

@@ -14,6 +14,12 @@
 // else (Init, InsertTestcase, Restore, the handlers) is unchanged. Upstream wtf
 // defines the macro as nothing.
 //
+// A module whose per-testcase global is `thread_local` names it with
+// WTF_LANE_STATE_TLS instead: the gpu backend then services breakpoint hits of
+// different lanes on several host threads at once (each thread swaps the lane
+// it services into its own instance of the global). g_Backend is thread_local
+// in this build for the same reason; module code is unchanged by it.
+//
 // ModuleSlots keeps one typed copy of every registered object per lane. The
 // lane's copy is swapped into the global (std::swap: container pointers are
 // exchanged, no element copies) around every call into the module for that
@@ -25,6 +31,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <memory>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -32,7 +39,8 @@ namespace wtfgpu_host {
 
 // Type-erased operations over one registered global.
 struct LaneStateOps {
-  void *object;
+  void *(*object)();                     // the calling thread's instance
+  bool tls;                              // declared thread_local
   void *(*clone)(const void *);          // new T(copy)
   void (*assign)(void *, const void *);  // dst = src
   void (*swap)(void *, void *);
@@ -44,9 +52,9 @@ std::vector<LaneStateOps> &LaneStateRegistry();
 
 template <typename T>
 struct LaneStateRegistrar {
-  explicit LaneStateRegistrar(T &Object) {
+  LaneStateRegistrar(void *(*Object)(), bool Tls) {
     LaneStateRegistry().push_back(LaneStateOps{
-        &Object, [](const void *S) -> void * { return new T(*(const T *)S); },
+        Object, Tls, [](const void *S) -> void * { return new T(*(const T *)S); },
         [](void *D, const void *S) { *(T *)D = *(const T *)S; },
         [](void *A, void *B) {
           using std::swap;
@@ -70,19 +78,22 @@ class ModuleSlots {
   void SwapIn(uint32_t lane);
   void SwapOut(uint32_t lane);
   size_t Objects() const { return initial_.size(); }
+  // every registered object is thread_local: lanes may be serviced in parallel
+  bool ThreadSafe() const;
 
  private:
   void release();
   std::vector<void *> initial_;             // per registered object
   std::vector<std::vector<void *>> lanes_;  // [lane][object], nullptr = not materialised
   std::vector<uint8_t> dirty_;              // lane copy differs from initial
-  int64_t in_ = -1;
 };
 
 }  // namespace wtfgpu_host
 
 #define WTF_LANE_STATE_CAT2(a, b) a##b
 #define WTF_LANE_STATE_CAT(a, b) WTF_LANE_STATE_CAT2(a, b)
-#define WTF_LANE_STATE(Object)                                                                      \
-  static ::wtfgpu_host::LaneStateRegistrar<decltype(Object)> WTF_LANE_STATE_CAT(LaneStateReg_, __LINE__)( \
-      Object)
+#define WTF_LANE_STATE_REG(Object, Tls)                                                          \
+  static ::wtfgpu_host::LaneStateRegistrar<std::remove_reference_t<decltype(Object)>> WTF_LANE_STATE_CAT( \
+      LaneStateReg_, __LINE__)([]() -> void * { return &Object; }, Tls)
+#define WTF_LANE_STATE(Object) WTF_LANE_STATE_REG(Object, false)
+#define WTF_LANE_STATE_TLS(Object) WTF_LANE_STATE_REG(Object, true)

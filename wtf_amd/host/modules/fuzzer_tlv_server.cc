@@ -13,8 +13,10 @@
 //  * user-mode crash detection (:191-194);
 //  * the custom mutator (:204-365): Generate 1..10 packets one time in five,
 //    otherwise insert / copy-field / delete on a corpus testcase.
-// The only addition for batched execution is WTF_LANE_STATE(GlobalState)
-// (module_slots.h): the packet queue is per testcase, so per lane.
+// The only changes for batched execution are on GlobalState: it is declared
+// thread_local and named with WTF_LANE_STATE_TLS (module_slots.h). The packet
+// queue is per testcase, so per lane, and lanes are serviced on several host
+// threads at once.
 #include <deque>
 #include <string>
 #include <vector>
@@ -68,7 +70,7 @@ std::string Serialize(const std::vector<Packet_t> &Packets) {
   return S + "]}";
 }
 
-struct {
+thread_local struct {
   std::deque<Packet_t> Packets;
   CpuState_t Context;
 
@@ -79,7 +81,7 @@ struct {
     B->R12(C.R12), B->R13(C.R13), B->R14(C.R14), B->R15(C.R15);
   }
 } GlobalState;
-WTF_LANE_STATE(GlobalState);
+WTF_LANE_STATE_TLS(GlobalState);
 
 bool InsertTestcase(const uint8_t *Buffer, const size_t BufferSize) {
   GlobalState.Packets.clear();

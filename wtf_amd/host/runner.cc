@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <future>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
@@ -239,9 +240,12 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
   std::unordered_set<std::string> CrashNames;
   double RunSeconds = 0;
   const auto t0 = Clock::now();
-  while ((O.runs == 0 || Execs < O.runs) && (O.seconds <= 0 || secs_since(t0) < O.seconds)) {
+  // The next batch is mutated on a host thread while the executor runs the
+  // current one (a node's master and client overlap the same way); it is
+  // built from the corpus as it stood before the current batch's results.
+  auto make_batch = [&](uint64_t done) {
     uint64_t n = N;
-    if (O.runs) n = std::min<uint64_t>(n, O.runs - Execs);
+    if (O.runs) n = std::min<uint64_t>(n, O.runs - done);
     std::vector<std::string> Batch;
     Batch.reserve(n);
     while (Batch.size() < n && !Pending.empty()) {
@@ -254,20 +258,32 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
       if (S.size() > O.max_len) S.resize(O.max_len);
       Batch.push_back(std::move(S));
     }
-    if (Batch.empty()) {
-      printf("Nothing to run: empty corpus and no inputs\n");
-      return 1;
-    }
+    return Batch;
+  };
+  auto more = [&](uint64_t done) {
+    return (O.runs == 0 || done < O.runs) && (O.seconds <= 0 || secs_since(t0) < O.seconds);
+  };
+  std::vector<std::string> Batch = make_batch(0);
+  if (Batch.empty()) {
+    printf("Nothing to run: empty corpus and no inputs\n");
+    return 1;
+  }
+  while (!Batch.empty()) {
     std::vector<std::pair<const uint8_t *, size_t>> Tc(Batch.size());
     for (size_t i = 0; i < Batch.size(); i++) Tc[i] = {(const uint8_t *)Batch[i].data(), Batch[i].size()};
     std::vector<LaneResult> R;
     const auto tb = Clock::now();
+    const uint64_t after = Execs + Batch.size();
+    std::future<std::vector<std::string>> Next;
+    if (more(after) && Corpus.Size()) Next = std::async(std::launch::async, make_batch, after);
     if (!Exec.RunBatch(*Target, Tc, R, &Slots)) {
       printf("RunBatch failed\n");
       return 1;
     }
     RunSeconds += secs_since(tb);
     Batches++;
+    std::vector<std::string> NextBatch;
+    if (Next.valid()) NextBatch = Next.get();  // before the corpus / mutator change below
     // master bookkeeping in lane order (server.h:816-886)
     for (size_t i = 0; i < Batch.size(); i++) {
       const LaneResult &L = R[i];
@@ -287,6 +303,10 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
         Corpus.SaveTestcase(L.result, std::move(Tcase));
       }
     }
+    if (!NextBatch.empty() || !more(Execs))
+      Batch = std::move(NextBatch);
+    else
+      Batch = make_batch(Execs);
   }
   const double Wall = secs_since(t0);
   printf("{\"mode\":\"fuzz\",\"target\":\"%s\",\"lanes\":%u,\"batches\":%llu,\"execs\":%llu,\"retired\":%llu,"

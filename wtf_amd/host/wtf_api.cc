@@ -10,7 +10,7 @@
 #include "blake3_lite.h"
 #include "json_lite.h"
 
-Backend_t *g_Backend = nullptr;
+thread_local Backend_t *g_Backend = nullptr;
 Debugger_t g_Dbg;
 
 // backend.cc:11-14

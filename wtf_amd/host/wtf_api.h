@@ -281,7 +281,9 @@ class Backend_t {
   void PrintRegisters();
 };
 
-extern Backend_t *g_Backend;
+// thread_local: the gpu backend services lanes on several host threads
+// (module_slots.h); module code reads it exactly as upstream's global.
+extern thread_local Backend_t *g_Backend;
 
 // ------------------------------------------------------------------ corpus / mutators
 // corpus.h:17-38 (Testcase_t), :40-103 (Corpus_t); mutator.h:10-20 (Mutator_t).
