@@ -24,9 +24,9 @@ The JSON line carries:
   cpu_baseline  the C oracle ("port": the build's scalar restatement, since
                 bochscpu is unbuildable) timed on host cores over a
                 bounded sample of the same SYN workload, one lane per thread.
-  tlv           (N=1, rank 0) BASELINE.json configs[2]: the synthetic
-                tlv_server snapshot fuzzed by the `wtfgpu` node (C++
-                GpuBackend_t, tlv module, breakpoints serviced on host
+  tlv, hevd     (N=1, rank 0) BASELINE.json configs[2] and [4]: the synthetic
+                tlv_server / HEVD snapshots fuzzed by the `wtfgpu` node (C++
+                GpuBackend_t, tlv / hevd modules, breakpoints serviced on host
                 threads), next to the oracle twin `wtf_twin fuzz` run as one
                 process per host core (the reference's one-client-per-core
                 layout). Both rates are execs / wall time,
@@ -60,47 +60,59 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (wall)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-tlv", action="store_true", help="skip the tlv_server leg")
+    ap.add_argument("--no-tlv", action="store_true", help="skip the tlv_server and hevd legs")
     ap.add_argument("--tlv-batches", type=int, default=6)
     ap.add_argument("--tlv-cpu-seconds", type=float, default=10.0)
     return ap.parse_args()
 
 
-# ----------------------------------------------------------------- tlv_server leg
-def tlv_leg(lanes: int, batches: int, cpu_seconds: float, cores: int, limit: int, run_cpu: bool):
-    """configs[2]: wtfgpu fuzz on the synthetic tlv_server snapshot (one GPU),
-    and the oracle twin on `cores` host processes over the same wall window."""
+# ----------------------------------------------------------------- tlv_server / hevd legs
+FUZZ_TARGETS = {
+    # name: (snapshot builder module, workload text, --max_len)
+    "tlv_server": ("wtf_amd.tools.tlv", "synthetic tlv_server snapshot (BASELINE.json configs[2]), tlv mutator", 0x1000),
+    "hevd": ("wtf_amd.tools.hevd", "synthetic HEVD ring-0 snapshot (BASELINE.json configs[4] on one GPU), "
+                                   "default libFuzzer-style mutator", 1028),
+}
+
+
+def fuzz_leg(name: str, lanes: int, batches: int, cpu_seconds: float, cores: int, limit: int, run_cpu: bool,
+             gpu_exe: str | None = None):
+    """wtfgpu fuzz on a synthetic snapshot (one GPU), and the oracle twin on
+    `cores` host processes (one wtf_twin fuzz client per core) over a bounded
+    wall window."""
+    import importlib
     import shutil
     import subprocess
     import tempfile
 
-    from wtf_amd.tools.tlv import build, seed_inputs
-
-    wtfgpu = os.path.join(ROOT, "wtf_amd", "host", "wtfgpu")
+    modname, workload, max_len = FUZZ_TARGETS[name]
+    mod = importlib.import_module(modname)
+    wtfgpu = gpu_exe or os.path.join(ROOT, "wtf_amd", "host", "wtfgpu")
     twin = os.path.join(ROOT, "oracle", "wtf_twin")
-    tmp = tempfile.mkdtemp(prefix="wtf_tlv_")
+    tmp = tempfile.mkdtemp(prefix=f"wtf_{name}_")
     try:
         base = os.path.join(tmp, "t0")
-        build(os.path.join(base, "state"), os.path.join(base, "work"))
-        seed_inputs(os.path.join(base, "inputs"))
-        out = subprocess.run([wtfgpu, "fuzz", "--name", "tlv_server", "--target", base, "--lanes", str(lanes),
-                              "--runs", str(lanes * batches), "--seed", "1337", "--limit", str(limit)],
+        mod.build(os.path.join(base, "state"), os.path.join(base, "work"))
+        mod.seed_inputs(os.path.join(base, "inputs"))
+        out = subprocess.run([wtfgpu, "fuzz", "--name", name, "--target", base, "--lanes", str(lanes),
+                              "--runs", str(lanes * batches), "--seed", "1337", "--limit", str(limit),
+                              "--max_len", str(max_len)],
                              check=True, capture_output=True, text=True, timeout=600).stdout
         g = json.loads([x for x in out.splitlines() if x.startswith("{")][-1])
-        res = {"workload": "synthetic tlv_server snapshot (BASELINE.json configs[2]), tlv mutator, seed 1337",
-               "lanes": lanes, "execs": g["execs"], "wall_s": g["wall_s"],
+        res = {"workload": workload + ", seed 1337", "lanes": lanes, "execs": g["execs"], "wall_s": g["wall_s"],
                "value": g["execs"] / g["wall_s"], "unit": "execs/s",
                "instr_per_s": g["retired"] / g["wall_s"], "instr_per_exec": g["retired"] / max(1, g["execs"]),
                "unique_crashes": g["unique_crashes"], "coverage": g["coverage"], "errors": g["errors"],
-               "backend": g["backend"]}
+               "gpu_retired_fraction": 1.0 - g["errors"] / max(1, g["execs"]), "backend": g["backend"]}
         if run_cpu:
             procs = []
             for i in range(cores):
                 d = os.path.join(tmp, f"c{i}")
                 shutil.copytree(base, d, ignore=shutil.ignore_patterns("outputs", "crashes", "work"))
-                procs.append(subprocess.Popen([twin, "fuzz", "--name", "tlv_server", "--target", d, "--lanes", "1024",
+                procs.append(subprocess.Popen([twin, "fuzz", "--name", name, "--target", d, "--lanes", "1024",
                                                "--seconds", str(cpu_seconds), "--seed", str(1337 + i),
-                                               "--limit", str(limit)], stdout=subprocess.PIPE, text=True))
+                                               "--limit", str(limit), "--max_len", str(max_len)],
+                                              stdout=subprocess.PIPE, text=True))
             execs = instr = 0.0
             wall = 0.0
             for p in procs:
@@ -111,7 +123,7 @@ def tlv_leg(lanes: int, batches: int, cpu_seconds: float, cores: int, limit: int
                 wall = max(wall, t["wall_s"])
             res["cpu_baseline"] = {"value": execs / wall, "unit": "execs/s", "instr_per_s": instr / wall,
                                    "cores": cores, "kind": "port",
-                                   "sample": f"{int(execs)} tlv testcases over {wall:.1f}s, {cores} wtf_twin fuzz "
+                                   "sample": f"{int(execs)} {name} testcases over {wall:.1f}s, {cores} wtf_twin fuzz "
                                              f"processes (oracle behind Backend_t, one per core)"}
             res["vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
         return res
@@ -326,8 +338,10 @@ def main():
         if world == 1 and not a.no_tlv:
             eng.close()
             eng = None
-            out["tlv"] = tlv_leg(a.lanes, a.tlv_batches, a.tlv_cpu_seconds,
-                                 a.cpu_threads or min(16, os.cpu_count() or 1), a.limit, not a.no_cpu)
+            cores = a.cpu_threads or min(16, os.cpu_count() or 1)
+            out["tlv"] = fuzz_leg("tlv_server", a.lanes, a.tlv_batches, a.tlv_cpu_seconds, cores, a.limit,
+                                  not a.no_cpu)
+            out["hevd"] = fuzz_leg("hevd", a.lanes, a.tlv_batches, a.tlv_cpu_seconds, cores, a.limit, not a.no_cpu)
         print(json.dumps(out), flush=True)
     if eng is not None:
         eng.close()

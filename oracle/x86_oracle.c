@@ -25,6 +25,11 @@
  *      with vector / error code / cr2 and the faulting instruction not retired.
  *   U12 int3 and hlt exit before retiring.
  *   U13 16-bit bswap writes 0.
+ *   U15 RDRAND r returns 0 with CF=1 (the value is unpinned: bochs draws a host
+ *       random number; the hevd module overwrites it, fuzzer_hevd.cc:96-108).
+ *   U16 SYSCALL / SYSRETQ (64-bit forms; 32-bit SYSRET is unimplemented) load
+ *       CS/SS selectors from STAR without descriptor-table reads; SWAPGS swaps
+ *       GS.base with IA32_KERNEL_GS_BASE.
  */
 #include "x86_oracle.h"
 #include <stdlib.h>
@@ -1299,6 +1304,46 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
 
   if (d->opmap == 1) {
     switch (op) {
+    case 0x05: /* syscall (64-bit; SDM vol. 2B; U16) */
+    case 0x07: /* sysretq */
+      if (op == 0x07 && !d->rexw) return X_UNIMPL;
+      if (!(m->r.efer & 1)) {
+        fault(m, WTFGPU_VEC_UD, 0);
+        return X_FAULT;
+      }
+      if (op == 0x05) {
+        m->r.gpr[1] = nrip;
+        m->r.gpr[11] = m->r.rflags & ~0x10000ULL;
+        m->r.rflags = ((m->r.rflags & ~m->r.sfmask) & ~0x10000ULL) | 2;
+        *next_rip = m->r.lstar;
+        m->r.seg[WTFGPU_CS].selector = (u16)((m->r.star >> 32) & 0xfffc);
+        m->r.seg[WTFGPU_SS].selector = (u16)(m->r.seg[WTFGPU_CS].selector + 8);
+      } else {
+        if (cpl(m) != 0 || !is_canonical(m->r.gpr[1])) {
+          fault(m, WTFGPU_VEC_GP, 0);
+          return X_FAULT;
+        }
+        *next_rip = m->r.gpr[1];
+        m->r.rflags = (m->r.gpr[11] & 0x3c7fd7ULL) | 2;
+        m->r.seg[WTFGPU_CS].selector = (u16)((((m->r.star >> 48) & 0xffff) + 16) | 3);
+        m->r.seg[WTFGPU_SS].selector = (u16)((((m->r.star >> 48) & 0xffff) + 8) | 3);
+      }
+      return X_OK;
+    case 0x01: /* swapgs (0f 01 f8) */
+      if (d->is_mem || (d->reg & 7) != 7 || (d->rm & 7) != 0) return X_UNIMPL;
+      if (cpl(m) != 0) {
+        fault(m, WTFGPU_VEC_GP, 0);
+        return X_FAULT;
+      }
+      a = m->r.seg[WTFGPU_GS].base;
+      m->r.seg[WTFGPU_GS].base = m->r.kernel_gs_base;
+      m->r.kernel_gs_base = a;
+      return X_OK;
+    case 0xc7: /* rdrand r: deterministic 0 with CF=1 (U15) */
+      if (d->is_mem || (d->reg & 7) != 6 || d->pfx66 || d->rep) return X_UNIMPL;
+      setreg(m, d, d->rm, osz, 0);
+      set_flags(m, RF_STATUS, RF_CF);
+      return X_OK;
     case 0x0b:
       fault(m, WTFGPU_VEC_UD, 0);
       return X_FAULT;
@@ -1601,7 +1646,7 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
     if ((b >= 0x40 && b <= 0x4f) || (b >= 0x90 && b <= 0x9f) || b == 0xa3 || b == 0xab ||
         b == 0xb3 || b == 0xbb || b == 0xaf || b == 0xb0 || b == 0xb1 || b == 0xb6 ||
         b == 0xb7 || b == 0xbe || b == 0xbf || b == 0xbc || b == 0xbd || b == 0xb8 ||
-        b == 0xc0 || b == 0xc1 || b == 0xa5 || b == 0xad || b == 0x0d ||
+        b == 0xc0 || b == 0xc1 || b == 0xa5 || b == 0xad || b == 0x0d || b == 0x01 || b == 0xc7 ||
         (b >= 0x18 && b <= 0x1f))
       has_modrm = 1;
     if (b == 0xa4 || b == 0xac || b == 0xba) {

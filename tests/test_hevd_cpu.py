@@ -1,0 +1,68 @@
+"""HEVD on the CPU: the synthetic ring-0 snapshot (SYSCALL / SWAPGS / SYSRETQ,
+supervisor pages, ExGenRandom's rdrand), the hevd module and the batched
+runner, driven through the oracle twin (no GPU). Each crafted input must end
+the way the reference module classifies it (fuzzer_hevd.cc:64-139)."""
+import os
+
+import pytest
+
+from tests import tlv_harness as H
+from tests.hevd_inputs import write_inputs
+from wtf_amd.tools.snapshot import read_kdmp
+
+pytestmark = pytest.mark.skipif(not os.path.exists(H.TWIN), reason="oracle/wtf_twin not built")
+
+
+@pytest.fixture(scope="module")
+def target(tmp_path_factory):
+    return H.build_hevd_target(str(tmp_path_factory.mktemp("hevd")))
+
+
+def _run(target, d, out, lanes=16):
+    return {r["input"]: r for r in H.run(H.TWIN, target, d, out, lanes=lanes, name="hevd")}
+
+
+def test_snapshot_layout(target):
+    index, _, cr3 = read_kdmp(os.path.join(target, "state", "mem.dmp"))
+    assert cr3 and len(index) > 20
+
+
+def test_seeds_return_to_user_mode(target, tmp_path):
+    res = _run(target, os.path.join(target, "inputs"), str(tmp_path / "r.jsonl"))
+    assert all(r["result"] == "ok" for r in res.values()), res
+    # every seed went through the kernel (syscall ... sysretq) and stopped
+    # after the 6-byte call, back in ring 3 with the caller's stack
+    rips = {r["gprs"][16] for r in res.values()}
+    assert len(rips) == 1
+    assert all(r["icount"] > 40 for r in res.values())
+
+
+def test_crafted_bug_classes(target, tmp_path):
+    d = str(tmp_path / "in")
+    write_inputs(d, 0)
+    res = _run(target, d, str(tmp_path / "r.jsonl"))
+    assert res["stack_gs_cookie"]["crash"].startswith("crash-0xf7-")           # DRIVER_OVERRAN_STACK_BUFFER
+    assert res["integer_wrap"]["crash"].startswith("crash-0xf7-")
+    assert res["pool_overflow"]["crash"].startswith("crash-0x19-0x21-")        # BAD_POOL_HEADER
+    assert res["wait_swapcontext"]["result"] == "cr3"                          # nt!SwapContext
+    assert res["stack_ret_overrun"]["crash"] == "crash-EXCEPTION_ACCESS_VIOLATION_READ-0x4242424242424242"
+    assert res["null_deref"]["crash"].startswith("crash-EXCEPTION_ACCESS_VIOLATION_READ-")
+    assert res["write_what_where_bad"]["crash"].startswith("crash-EXCEPTION_ACCESS_VIOLATION_WRITE-")
+    assert res["write_what_where_ok"]["result"] == "ok"
+    assert res["integer_ok"]["result"] == "ok"
+    assert res["too_long"]["crash"] == "insert-testcase-failed"               # > 1024 bytes: InsertTestcase fails
+    assert not any(r["error"] for r in res.values())
+
+
+def test_batch_size_does_not_change_results(target, tmp_path):
+    d = str(tmp_path / "in")
+    write_inputs(d, 150)
+    a = H.run(H.TWIN, target, d, str(tmp_path / "a.jsonl"), lanes=1, name="hevd")
+    b = H.run(H.TWIN, target, d, str(tmp_path / "b.jsonl"), lanes=64, name="hevd")
+    assert a == b
+
+
+def test_fuzz_default_mutator(target):
+    st = H.fuzz(H.TWIN, target, runs=4000, lanes=512, name="hevd", max_len=1028)
+    assert st["execs"] == 4000 and st["errors"] == 0
+    assert st["unique_crashes"] >= 1 and st["coverage"] > 200

@@ -1,5 +1,5 @@
 """Drives `wtfgpu` (the product node, wtf_amd/host) and `oracle/wtf_twin`
-(its CPU twin) over the synthetic tlv_server snapshot."""
+(its CPU twin) over the synthetic tlv_server and HEVD snapshots."""
 from __future__ import annotations
 
 import json
@@ -11,6 +11,13 @@ WTFGPU = os.path.join(ROOT, "wtf_amd", "host", "wtfgpu")
 TWIN = os.path.join(ROOT, "oracle", "wtf_twin")
 
 
+def build_hevd_target(d: str) -> str:
+    from wtf_amd.tools.hevd import build, seed_inputs
+    build(os.path.join(d, "state"), os.path.join(d, "work"))
+    seed_inputs(os.path.join(d, "inputs"))
+    return d
+
+
 def build_target(d: str) -> str:
     from wtf_amd.tools.tlv import build, seed_inputs
     build(os.path.join(d, "state"), os.path.join(d, "work"))
@@ -19,8 +26,8 @@ def build_target(d: str) -> str:
 
 
 def run(exe: str, target: str, inputs: str, results: str, lanes: int, limit: int = 100000,
-        full_coverage: bool = True, timeout: int = 300, extra=()) -> list[dict]:
-    cmd = [exe, "run", "--name", "tlv_server", "--target", target, "--input", inputs, "--results", results,
+        full_coverage: bool = True, timeout: int = 300, extra=(), name: str = "tlv_server") -> list[dict]:
+    cmd = [exe, "run", "--name", name, "--target", target, "--input", inputs, "--results", results,
            "--lanes", str(lanes), "--limit", str(limit), *extra]
     if full_coverage:
         cmd.append("--full-coverage")
@@ -30,9 +37,9 @@ def run(exe: str, target: str, inputs: str, results: str, lanes: int, limit: int
 
 
 def fuzz(exe: str, target: str, runs: int, lanes: int, seed: int = 1337, limit: int = 100000,
-         seconds: float = 0, timeout: int = 600) -> dict:
-    cmd = [exe, "fuzz", "--name", "tlv_server", "--target", target, "--runs", str(runs), "--lanes", str(lanes),
-           "--seed", str(seed), "--limit", str(limit)]
+         seconds: float = 0, timeout: int = 600, name: str = "tlv_server", max_len: int = 0x1000) -> dict:
+    cmd = [exe, "fuzz", "--name", name, "--target", target, "--runs", str(runs), "--lanes", str(lanes),
+           "--seed", str(seed), "--limit", str(limit), "--max_len", str(max_len)]
     if seconds:
         cmd += ["--seconds", str(seconds)]
     out = subprocess.run(cmd, check=True, timeout=timeout, capture_output=True, text=True).stdout

@@ -995,6 +995,12 @@ InitState make_init(const wtfgpu_regs_t &r) {
   s.sys.cr4 = r.cr4;
   s.sys.efer = r.efer;
   s.sys.cpl = r.seg[WTFGPU_CS].selector & 3;
+  s.sys.star = r.star;
+  s.sys.lstar = r.lstar;
+  s.sys.sfmask = r.sfmask;
+  s.sys.kgs = r.kernel_gs_base;
+  s.sys.cs = r.seg[WTFGPU_CS].selector;
+  s.sys.ss = r.seg[WTFGPU_SS].selector;
   return s;
 }
 
@@ -1403,6 +1409,9 @@ int wtfgpu_read_regs(wtfgpu_ctx *c, uint32_t first, uint32_t count, wtfgpu_regs_
     r.cr3 = sys[l].cr3;
     r.cr4 = sys[l].cr4;
     r.efer = sys[l].efer;
+    r.kernel_gs_base = sys[l].kgs;
+    r.seg[WTFGPU_CS].selector = sys[l].cs;
+    r.seg[WTFGPU_SS].selector = sys[l].ss;
   }
   return WTFGPU_OK;
 }

@@ -43,8 +43,9 @@ constexpr int TLB_N = 4;
 
 struct LaneSys {   // rarely touched per-lane system state
   u64 cr0, cr3, cr4, efer;
+  u64 star, lstar, sfmask, kgs;  // SYSCALL/SYSRET MSRs, IA32_KERNEL_GS_BASE (SWAPGS)
   u32 cpl;
-  u32 pad;
+  u16 cs, ss;                    // selectors after SYSCALL/SYSRET (64-bit mode, STAR)
 };
 
 struct ExitInfo {

@@ -27,7 +27,7 @@ enum : u32 {
   O_SHIFT, O_SHXD, O_MULDIV, O_IMUL, O_BT, O_BSF, O_BSR, O_TZCNT, O_LZCNT, O_POPCNT,
   O_CMOV, O_SETCC, O_BSWAP, O_CBW, O_CWD, O_LAHF, O_SAHF, O_FLAGOP, O_NOP, O_JCC, O_JMP,
   O_CALL, O_RET, O_PUSH, O_POP, O_PUSHF, O_POPF, O_LEAVE, O_STRING, O_INT3, O_HLT, O_UD,
-  O_LEA, O_UNIMPL
+  O_LEA, O_SYS, O_UNIMPL
 };
 // operand locations
 enum : u32 {
@@ -158,7 +158,8 @@ __constant__ u32 kMap1[256] = {
 #define SHXD(ik) E(O_SHXD, L_RM, L_GREG, Z_V, Z_V, 1, 1, 0, 1, ik, 0)
 #define UN16 UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN
 __constant__ u32 kMap2[256] = {
-    /*00*/ UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, E(O_UD, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, NOPM, UN, UN,
+    /*00*/ UN, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 1, K_NONE, 0), UN, UN, UN, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN,
+    E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, UN, UN, E(O_UD, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, NOPM, UN, UN,
     /*10*/ UN, UN, UN, UN, UN, UN, UN, UN, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM,
     /*20*/ UN16,
     /*30*/ UN16,
@@ -178,7 +179,8 @@ __constant__ u32 kMap2[256] = {
     E(O_BSF, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0), E(O_BSR, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0),
     E(O_MOVSX, L_GREG, L_RM, Z_V, Z_B, 0, 1, 0, 1, K_NONE, 0), E(O_MOVSX, L_GREG, L_RM, Z_V, Z_W, 0, 1, 0, 1, K_NONE, 0),
     /*c0*/ E(O_XADD, L_RM, L_GREG, Z_B, Z_B, 1, 1, 1, 1, K_NONE, 0), E(O_XADD, L_RM, L_GREG, Z_V, Z_V, 1, 1, 1, 1, K_NONE, 0),
-    UN, UN, UN, UN, UN, UN, BSWAP, BSWAP, BSWAP, BSWAP, BSWAP, BSWAP, BSWAP, BSWAP,
+    UN, UN, UN, UN, UN, E(O_SYS, L_RM, 0, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0),
+    BSWAP, BSWAP, BSWAP, BSWAP, BSWAP, BSWAP, BSWAP, BSWAP,
     /*d0*/ UN16,
     /*e0*/ UN16,
     /*f0*/ UN16,
@@ -408,6 +410,13 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
     if (u.op == O_SHXD) u.sub = (c >= 0xac ? 1u : 0u) | ((c & 1) ? 2u : 0u);  // bit0 shrd, bit1 count in cl
     if (u.op == O_BSF && u.rep == 0xf3) u.op = O_TZCNT;
     if (u.op == O_BSR && u.rep == 0xf3) u.op = O_LZCNT;
+    if (u.op == O_SYS) {
+      // 0 syscall, 1 sysret (64-bit form only), 2 swapgs (0f 01 f8), 3 rdrand r (0f c7 /6)
+      u.sub = c == 0x05 ? 0 : c == 0x07 ? 1 : c == 0x01 ? 2 : 3;
+      if (c == 0x07 && !rexw) u.op = O_UNIMPL;
+      if (c == 0x01 && (u.is_mem || (u.reg & 7) != 7 || (u.rm & 7) != 0)) u.op = O_UNIMPL;
+      if (c == 0xc7 && (u.is_mem || (u.reg & 7) != 6 || p66 || u.rep)) u.op = O_UNIMPL;
+    }
   } else if (u.op == O_FLAGOP) {
     u.sub = c;
   }
@@ -995,6 +1004,57 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
     case O_UD:
       set_fault(L, WTFGPU_VEC_UD, 0, 0);
       return X_FAULT;
+    case O_SYS: {
+      // System instructions of the kernel paths (SDM vol. 2):
+      // 64-bit SYSCALL / SYSRET with STAR selectors (no descriptor loads),
+      // SWAPGS, and a deterministic RDRAND.
+      LaneSys &S = P.sys[L.lane];
+      if (u.sub == 3) {  // rdrand: 0 with CF=1 (U15)
+        res = 0;
+        fl = with_status(fl, F_CF);
+        break;
+      }
+      if (u.sub == 2) {  // swapgs
+        if (L.cpl != 0) {
+          set_fault(L, WTFGPU_VEC_GP, 0, 0);
+          return X_FAULT;
+        }
+        const u64 g = P.gs_base[L.lane];
+        P.gs_base[L.lane] = S.kgs;
+        S.kgs = g;
+        break;
+      }
+      if (!(L.efer & 1)) {  // EFER.SCE
+        set_fault(L, WTFGPU_VEC_UD, 0, 0);
+        return X_FAULT;
+      }
+      if (u.sub == 0) {  // syscall
+        RS(L, 1, nrip);
+        RS(L, 11, fl & ~0x10000ull);
+        fl = ((fl & ~S.sfmask) & ~0x10000ull) | 2;
+        next = S.lstar;
+        L.cpl = S.cpl = 0;
+        S.cs = (u16)((S.star >> 32) & 0xfffc);
+        S.ss = (u16)(S.cs + 8);
+      } else {  // sysretq
+        if (L.cpl != 0) {
+          set_fault(L, WTFGPU_VEC_GP, 0, 0);
+          return X_FAULT;
+        }
+        const u64 target = R(L, 1);
+        if (!canonical(target)) {
+          set_fault(L, WTFGPU_VEC_GP, 0, 0);
+          return X_FAULT;
+        }
+        fl = (R(L, 11) & 0x3c7fd7ull) | 2;
+        next = target;
+        L.cpl = S.cpl = 3;
+        S.cs = (u16)((((S.star >> 48) & 0xffff) + 16) | 3);
+        S.ss = (u16)((((S.star >> 48) & 0xffff) + 8) | 3);
+      }
+      L.flush = 1;  // cached translations were permission-checked at the old cpl
+      break;
+    }
     default: return X_UNIMPL;
   }
   // ---- the memory write

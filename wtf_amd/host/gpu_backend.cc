@@ -406,6 +406,7 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
     stats_.kernel_launches += rs.kernel_launches;
     stats_.kernel_ms += rs.kernel_ms;
     stats_.retired += rs.lane_retired;
+    stats_.group_steps += rs.group_steps;
     stats_.rounds++;
     if (wtfgpu_read_exits(ctx_, first, count, ex.data())) return false;
     const auto t0 = Clock::now();
@@ -711,14 +712,15 @@ void GpuBackend_t::ResetCoverage() {
 std::string GpuBackend_t::StatsJson() const {
   char b[1024];
   snprintf(b, sizeof(b),
-           "{\"kind\":\"gpu\",\"rounds\":%llu,\"breakpoint_hits\":%llu,\"kernel_launches\":%llu,"
+           "{\"kind\":\"gpu\",\"group_steps\":%llu,\"rounds\":%llu,\"breakpoint_hits\":%llu,\"kernel_launches\":%llu,"
            "\"kernel_ms\":%.3f,\"service_ms\":%.3f,\"total_ms\":%.3f,\"page_fetches\":%llu,"
            "\"prefetched_pages\":%llu,\"staged_pages\":%llu,\"bulk_ms\":%.3f,\"prefetch_ms\":%.3f,"
            "\"handler_ms\":%.3f,\"fetch_ms\":%.3f,\"flush_ms\":%.3f,\"insert_ms\":%.3f,\"coverage_ms\":%.3f,"
            "\"target_restore_ms\":%.3f}",
-           (unsigned long long)stats_.rounds, (unsigned long long)stats_.breakpoint_hits,
-           (unsigned long long)stats_.kernel_launches, stats_.kernel_ms, stats_.service_ms, stats_.total_ms,
-           (unsigned long long)stats_.page_fetches, (unsigned long long)stats_.prefetched_pages,
+           (unsigned long long)stats_.group_steps, (unsigned long long)stats_.rounds,
+           (unsigned long long)stats_.breakpoint_hits, (unsigned long long)stats_.kernel_launches, stats_.kernel_ms,
+           stats_.service_ms, stats_.total_ms, (unsigned long long)stats_.page_fetches,
+           (unsigned long long)stats_.prefetched_pages,
            (unsigned long long)stats_.staged_pages, stats_.bulk_ms, stats_.prefetch_ms, stats_.handler_ms,
            stats_.fetch_ms, stats_.flush_ms, stats_.insert_ms, stats_.coverage_ms, stats_.target_restore_ms);
   std::string r(b);

@@ -29,7 +29,7 @@
 namespace wtfgpu_host {
 
 struct BatchStats {
-  uint64_t rounds = 0, breakpoint_hits = 0, kernel_launches = 0, retired = 0;
+  uint64_t rounds = 0, breakpoint_hits = 0, kernel_launches = 0, retired = 0, group_steps = 0;
   uint64_t page_fetches = 0, prefetched_pages = 0, batches = 0, testcases = 0, staged_pages = 0;
   double kernel_ms = 0, service_ms = 0, total_ms = 0;
   // service_ms split: bulk reads (regs, dirty lists), stack/learned prefetch,

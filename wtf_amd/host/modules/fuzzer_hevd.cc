@@ -1,0 +1,76 @@
+// fuzzer_hevd.cc — the hevd fuzzer module (reference src/wtf/fuzzer_hevd.cc),
+// written against wtf_api.h with the same handlers, symbols and result names:
+//  * InsertTestcase (:20-59): u32 IOCTL code -> rdx, the rest (<= 1024 bytes)
+//    -> the user buffer at r8, its size -> r9 and GetArgAddress(5);
+//  * the instruction after the 6-byte call to DeviceIoControl stops the
+//    testcase with Ok (:64-73);
+//  * nt!DbgPrintEx is skipped (return 0) after reading its format (:78-88);
+//  * nt!ExGenRandom: right after its `rdrand rdx` (+0xe0) rdx := Rdrand()
+//    (:96-108, the BLAKE3 chain of Backend_t::Rdrand);
+//  * nt!KeBugCheck2 -> Crash_t("crash-<code>-<p0>-<p1>-<p2>-<p3>-<p4>") (:114-128);
+//  * nt!SwapContext -> Cr3Change_t (:134-139).
+// The module keeps no per-testcase state, so nothing is registered with
+// WTF_LANE_STATE.
+#include <cstdio>
+#include <string>
+
+#include "../wtf_api.h"
+
+namespace Hevd {
+
+// fmt's {:#x}: "0x" + lowercase hex, "0x0" for zero
+static std::string Hex(const uint64_t V) {
+  char B[24];
+  snprintf(B, sizeof(B), "0x%llx", (unsigned long long)V);
+  return B;
+}
+
+bool InsertTestcase(const uint8_t *Buffer, const size_t BufferSize) {
+  if (BufferSize < sizeof(uint32_t)) return true;
+  uint32_t Ioctl;
+  memcpy(&Ioctl, Buffer, sizeof(Ioctl));
+  const size_t IoctlBufferSize = BufferSize - sizeof(uint32_t);
+  const uint8_t *IoctlBuffer = Buffer + sizeof(uint32_t);
+  if (IoctlBufferSize > 1024) return false;
+  g_Backend->Rdx(Ioctl);
+  const Gva_t IoctlBufferPtr = Gva_t(g_Backend->R8());
+  if (!g_Backend->VirtWriteDirty(IoctlBufferPtr, IoctlBuffer, IoctlBufferSize)) return false;
+  g_Backend->R9(IoctlBufferSize);
+  const Gva_t OutBufferSizePtr = g_Backend->GetArgAddress(5);
+  if (!g_Backend->VirtWriteStructDirty(OutBufferSizePtr, &IoctlBufferSize)) return false;
+  return true;
+}
+
+bool Init(const Options_t &, const CpuState_t &) {
+  const Gva_t Rip = Gva_t(g_Backend->Rip());
+  const Gva_t AfterCall = Rip + Gva_t(6);
+  if (!g_Backend->SetBreakpoint(AfterCall, [](Backend_t *Backend) { Backend->Stop(Ok_t()); })) return false;
+  if (!g_Backend->SetBreakpoint("nt!DbgPrintEx", [](Backend_t *Backend) {
+        const Gva_t FormatPtr = Backend->GetArgGva(2);
+        const std::string Format = Backend->VirtReadString(FormatPtr);
+        (void)Format;
+        Backend->SimulateReturnFromFunction(0);
+      }))
+    return false;
+  const Gva_t ExGenRandom = Gva_t(g_Dbg.GetSymbol("nt!ExGenRandom") + 0xe0 + 4);
+  if (g_Backend->VirtRead4(ExGenRandom - Gva_t(4)) != 0xf2c70f48) {
+    printf("It seems that nt!ExGenRandom's code has changed, update the offset!\n");
+    return false;
+  }
+  if (!g_Backend->SetBreakpoint(ExGenRandom, [](Backend_t *Backend) { Backend->Rdx(Backend->Rdrand()); }))
+    return false;
+  if (!g_Backend->SetBreakpoint("nt!KeBugCheck2", [](Backend_t *Backend) {
+        const uint64_t BCode = Backend->GetArg(0), B0 = Backend->GetArg(1), B1 = Backend->GetArg(2),
+                       B2 = Backend->GetArg(3), B3 = Backend->GetArg(4), B4 = Backend->GetArg(5);
+        Backend->Stop(Crash_t("crash-" + Hex(BCode) + "-" + Hex(B0) + "-" + Hex(B1) + "-" + Hex(B2) + "-" + Hex(B3) +
+                              "-" + Hex(B4)));
+      }))
+    return false;
+  if (!g_Backend->SetBreakpoint("nt!SwapContext", [](Backend_t *Backend) { Backend->Stop(Cr3Change_t()); }))
+    return false;
+  return true;
+}
+
+Target_t Hevd("hevd", Init, InsertTestcase);
+
+}  // namespace Hevd

@@ -326,6 +326,30 @@ class Mutator_t {
   virtual void OnNewCoverage(const Testcase_t &) {}
 };
 
+// The default mutator of a target (targets.h:25; mutator.cc:8-51): one
+// libFuzzer-style mutation of a corpus pick per testcase. A reduced
+// restatement of libFuzzer's MutationDispatcher (erase / insert / insert
+// repeated / change byte / change bit / shuffle / change binary integer /
+// copy part / cross over with the last new-coverage testcase); its output
+// sequence for a seed is not libFuzzer's.
+class LibfuzzerMutator_t : public Mutator_t {
+  std::mt19937_64 Rand_;
+  size_t MaxSize_;
+  std::vector<uint8_t> CrossOverWith_;
+  uint64_t R(uint64_t N) { return N ? Rand_() % N : 0; }
+  size_t MutateOnce(std::vector<uint8_t> &D, size_t Size);
+
+ public:
+  LibfuzzerMutator_t(std::mt19937_64 &Rng, const size_t MaxSize) : Rand_(Rng()), MaxSize_(MaxSize) {}
+  static std::unique_ptr<Mutator_t> Create(std::mt19937_64 &Rng, const size_t MaxSize) {
+    return std::make_unique<LibfuzzerMutator_t>(Rng, MaxSize);
+  }
+  std::string GetNewTestcase(const Corpus_t &Corpus) override;
+  void OnNewCoverage(const Testcase_t &T) override {
+    CrossOverWith_.assign(T.Buffer_.get(), T.Buffer_.get() + T.BufferSize_);
+  }
+};
+
 // ------------------------------------------------------------------ targets
 
 struct Target_t {
@@ -335,7 +359,8 @@ struct Target_t {
   using CreateMutator_t = std::unique_ptr<Mutator_t> (*)(std::mt19937_64 &, const size_t);
 
   explicit Target_t(const std::string &Name, const Init_t Init, const InsertTestcase_t InsertTestcase,
-                    const Restore_t Restore = []() { return true; }, const CreateMutator_t CreateMutator = nullptr);
+                    const Restore_t Restore = []() { return true; },
+                    const CreateMutator_t CreateMutator = LibfuzzerMutator_t::Create);
 
   std::string Name;
   Init_t Init = nullptr;
