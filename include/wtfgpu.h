@@ -125,7 +125,7 @@ typedef struct wtfgpu_exit {
   uint32_t status;   /* enum wtfgpu_status */
   uint32_t vector;   /* FAULT: exception vector */
   uint32_t error;    /* FAULT: error code (#PF bits as in backend.h PfError_t) */
-  uint32_t opcode;   /* UNIMPLEMENTED: first opcode bytes, little endian */
+  uint32_t opcode;   /* UNIMPLEMENTED: first opcode bytes, little endian; FAULT: CPL at the fault */
   uint64_t addr;     /* FAULT #PF: faulting linear address (cr2) */
   uint64_t rip;      /* rip at exit */
   uint64_t icount;   /* instructions retired by this testcase so far */
@@ -226,6 +226,12 @@ int wtfgpu_write_gprs_list(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, c
 int wtfgpu_read_dirty_list(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, uint32_t *out);
 uint32_t wtfgpu_overlay_pages(wtfgpu_ctx *ctx);
 int wtfgpu_gather_pages(wtfgpu_ctx *ctx, const uint32_t *lanes, const uint64_t *gpas, uint32_t n, uint8_t *out);
+
+/* `len` bytes (<= 256) at each (lane, gpa) of the lanes' current views; each
+ * range stays within one page. Sub-page prefetch of what handlers read (the
+ * return address / stack arguments), instead of whole pages. */
+int wtfgpu_gather_bytes(wtfgpu_ctx *ctx, const uint32_t *lanes, const uint64_t *gpas, uint32_t n, uint32_t len,
+                        uint8_t *out);
 
 /* Page-locked host memory (for gather/scatter staging buffers). */
 int wtfgpu_host_alloc(wtfgpu_ctx *ctx, uint64_t bytes, void **out);

@@ -101,13 +101,12 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
         skip = regs().rip == rip0;  // U10: a moved rip cancels the hooked instruction
         continue;
       }
-      const uint32_t cpl = initial_.Cs.Selector & 3;
       switch (e.status) {
         case WTFGPU_EXIT_TIMEOUT: result_ = Timedout_t(); break;
         case WTFGPU_EXIT_INT3:
         case WTFGPU_EXIT_HLT: result_ = Crash_t(); break;
         case WTFGPU_EXIT_CR3: result_ = Cr3Change_t(); break;
-        case WTFGPU_EXIT_FAULT: result_ = FaultToResult(e.vector, e.error, e.rip, cpl); break;
+        case WTFGPU_EXIT_FAULT: result_ = FaultToResult(e.vector, e.error, e.rip, e.addr, e.opcode); break;
         default: result_ = Crash_t("engine-" + std::to_string(e.status)); break;
       }
       break;

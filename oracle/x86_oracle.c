@@ -1671,6 +1671,7 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
 
 static void fill_exit(orc_machine *m, wtfgpu_exit_t *ex, u32 status) {
   ex->status = status;
+  if (status == WTFGPU_EXIT_FAULT) ex->opcode = (u32)cpl(m); /* the privilege level it was raised at */
   ex->rip = m->r.rip;
   ex->icount = m->icount;
 }

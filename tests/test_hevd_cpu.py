@@ -45,9 +45,10 @@ def test_crafted_bug_classes(target, tmp_path):
     assert res["integer_wrap"]["crash"].startswith("crash-0xf7-")
     assert res["pool_overflow"]["crash"].startswith("crash-0x19-0x21-")        # BAD_POOL_HEADER
     assert res["wait_swapcontext"]["result"] == "cr3"                          # nt!SwapContext
-    assert res["stack_ret_overrun"]["crash"] == "crash-EXCEPTION_ACCESS_VIOLATION_READ-0x4242424242424242"
-    assert res["null_deref"]["crash"].startswith("crash-EXCEPTION_ACCESS_VIOLATION_READ-")
-    assert res["write_what_where_bad"]["crash"].startswith("crash-EXCEPTION_ACCESS_VIOLATION_WRITE-")
+    # ring-0 faults are named as the bugcheck the kernel raises
+    assert res["stack_ret_overrun"]["crash"] == "crash-0x1e-0xc0000005-0x4242424242424242-0x0-0x0-0x0"
+    assert res["null_deref"]["crash"].startswith("crash-0x50-0x8-0x0-0xfffff800")      # read of NULL->Callback
+    assert res["write_what_where_bad"]["crash"].startswith("crash-0x50-0xffff800000000000-0x2-")
     assert res["write_what_where_ok"]["result"] == "ok"
     assert res["integer_ok"]["result"] == "ok"
     assert res["too_long"]["crash"] == "insert-testcase-failed"               # > 1024 bytes: InsertTestcase fails

@@ -588,7 +588,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       ei.vector = L.exvec;
       ei.error = L.exerr;
       ei.opcode = L.exop;
-      ei.pad = 0;
+      ei.cpl = L.cpl;
       ei.addr = L.exaddr;
       P.exinfo[lane] = ei;
     }
@@ -753,6 +753,15 @@ __global__ void k_apply_writes(Dev P, const WriteRec *recs, const u32 *starts, u
   P.ov_count[lane] = L.ovn;
 }
 
+// Lane status (+ skip-breakpoint-once flag) for a lane list (resume / stop).
+__global__ void k_set_status(Dev P, const u32 *lanes, u32 n, u32 status, const u8 *skip) {
+  const u32 t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const u32 lane = lanes[t];
+  P.status[lane] = status;
+  if (skip) P.lflags[lane] = skip[t] ? 1u : 0u;
+}
+
 // Single-lane memory services for the host proxy.
 // op 0: translate (out u64 gpa), 1: read phys, 2: write phys, 3: read virt, 4: write virt
 __global__ void k_lane_mem(Dev P, u32 lane, u32 op, u64 addr, u64 len, u8 *buf, i64 *result) {
@@ -830,6 +839,21 @@ __global__ void k_gather_dirty(Dev P, const u32 *lanes, u32 n, u32 *out) {
 }
 // Lane views of physical pages (overlay copy, else snapshot, else zeros): one
 // 256-thread block per (lane, gpa) request, 16 bytes per thread.
+// `len` bytes (<= 256, within one page) at (lane, gpa) from each lane's view:
+// one 64-thread block per record, 4 bytes per thread.
+__global__ void k_gather_bytes(Dev P, const u32 *lanes, const u64 *gpas, u32 n, u32 len, u8 *out) {
+  const u32 r = blockIdx.x;
+  if (r >= n) return;
+  const u32 l = lanes[r];
+  const u64 gpa = gpas[r];
+  const u32 ovn = P.ov_count[l];
+  u64 bloom = 0;
+  for (u32 k = 0; k < ovn; k++) bloom |= bloom_bit(P.ov_gpfn[(u64)k * P.nlanes + l]);
+  bool priv;
+  const u8 *src = phys_page(P, l, ovn, bloom, gpa >> 12, priv) + (gpa & 0xfff);
+  for (u32 i = threadIdx.x; i < len; i += blockDim.x) out[(u64)r * len + i] = src[i];
+}
+
 __global__ void k_gather_pages(Dev P, const u32 *lanes, const u64 *gpas, u32 n, u8 *out) {
   const u32 r = blockIdx.x;
   if (r >= n) return;
@@ -1462,6 +1486,7 @@ int wtfgpu_read_exits(wtfgpu_ctx *c, uint32_t first, uint32_t count, wtfgpu_exit
       e.vector = ex[l].vector;
       e.error = ex[l].error;
       e.addr = ex[l].addr;
+      e.opcode = ex[l].cpl;
     }
     if (st[l] == WTFGPU_EXIT_UNIMPLEMENTED) e.opcode = ex[l].opcode;
     e.rip = rip[l];
@@ -1472,19 +1497,18 @@ int wtfgpu_read_exits(wtfgpu_ctx *c, uint32_t first, uint32_t count, wtfgpu_exit
 
 static int set_status_list(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, uint32_t status, const uint8_t *skip) {
   if (!c || !c->d_status || (n && !lanes)) return WTFGPU_ERR_INVALID;
-  HIPCHK(hipSetDevice(c->device));
-  // small lists: per-lane copies; large: read-modify-write of the whole array
-  std::vector<u32> st(c->P.nlanes), fl(c->P.nlanes);
-  HIPCHK(hipMemcpyAsync(st.data(), c->d_status, st.size() * 4, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(fl.data(), c->d_lflags, fl.size() * 4, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  for (u32 i = 0; i < n; i++) {
+  if (n == 0) return WTFGPU_OK;
+  for (u32 i = 0; i < n; i++)
     if (lanes[i] >= c->P.nlanes) return WTFGPU_ERR_INVALID;
-    st[lanes[i]] = status;
-    if (skip) fl[lanes[i]] = skip[i] ? 1u : 0u;
-  }
-  HIPCHK(hipMemcpyAsync(c->d_status, st.data(), st.size() * 4, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipMemcpyAsync(c->d_lflags, fl.data(), fl.size() * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipSetDevice(c->device));
+  // lane list (+ skip flags) -> scratch, one scatter kernel: no whole-array round trips
+  const u64 o_skip = ((u64)n * 4 + 255) & ~255ull;
+  if (ensure_scratch(c, o_skip + n)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemcpyAsync(c->d_scratch, lanes, (u64)n * 4, hipMemcpyHostToDevice, c->stream));
+  if (skip) HIPCHK(hipMemcpyAsync(c->d_scratch + o_skip, skip, n, hipMemcpyHostToDevice, c->stream));
+  k_set_status<<<(n + 255) / 256, 256, 0, c->stream>>>(c->P, (const u32 *)c->d_scratch, n, status,
+                                                      skip ? c->d_scratch + o_skip : nullptr);
+  HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   return WTFGPU_OK;
 }
@@ -1708,6 +1732,26 @@ int wtfgpu_gather_pages(wtfgpu_ctx *c, const uint32_t *lanes, const uint64_t *gp
                                            c->d_scratch + o_out);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(out, c->d_scratch + o_out, (u64)n * WTFGPU_PAGE_SIZE, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_gather_bytes(wtfgpu_ctx *c, const uint32_t *lanes, const uint64_t *gpas, uint32_t n, uint32_t len,
+                        uint8_t *out) {
+  if (int rc = check_lane_list(c, lanes, n)) return rc;
+  if (n == 0) return WTFGPU_OK;
+  if (!gpas || !out || !c->P.pool || len == 0 || len > 256) return WTFGPU_ERR_INVALID;
+  for (u32 i = 0; i < n; i++)
+    if ((gpas[i] & 0xfff) + len > WTFGPU_PAGE_SIZE) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  const u64 o_gpa = ((u64)n * 4 + 255) & ~255ull, o_out = (o_gpa + (u64)n * 8 + 255) & ~255ull;
+  if (ensure_scratch(c, o_out + (u64)n * len)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemcpyAsync(c->d_scratch, lanes, (u64)n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_scratch + o_gpa, gpas, (u64)n * 8, hipMemcpyHostToDevice, c->stream));
+  k_gather_bytes<<<n, 64, 0, c->stream>>>(c->P, (const u32 *)c->d_scratch, (const u64 *)(c->d_scratch + o_gpa), n,
+                                          len, c->d_scratch + o_out);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, c->d_scratch + o_out, (u64)n * len, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return WTFGPU_OK;
 }

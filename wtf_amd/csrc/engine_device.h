@@ -49,7 +49,7 @@ struct LaneSys {   // rarely touched per-lane system state
 };
 
 struct ExitInfo {
-  u32 vector, error, opcode, pad;
+  u32 vector, error, opcode, cpl;  // cpl: privilege level the fault was raised at
   u64 addr;
 };
 

@@ -108,6 +108,9 @@ void GpuBackend_t::reset_view(uint32_t lane) {
   v.seed = initial_.Seed;  // Rdrand seed (bochscpu_backend.cc:1030)
   v.dirty_known = true;    // a restored lane has an empty overlay
   v.dirty.clear();
+  v.wlog.clear();
+  v.wdata.clear();
+  v.win_len = 0;
   drop_staged(v);
 }
 
@@ -201,8 +204,66 @@ bool GpuBackend_t::parallel_service(const ModuleSlots *slots) const {
 
 uint8_t *GpuBackend_t::stage(uint32_t lane, uint64_t gpfn, const uint8_t *orig, uint8_t *data) const {
   live_staged_++;
-  views_[lane].pages.push_back(Staged{gpfn, data, orig});
+  LaneView &v = views_[lane];
+  v.pages.push_back(Staged{gpfn, data, orig});
+  for (LaneView::Logged &w : v.wlog)  // logged writes to this page move into it
+    if (w.len && (w.gpa >> 12) == gpfn) {
+      memcpy(data + (w.gpa & 0xfff), v.wdata.data() + w.off, w.len);
+      w.len = 0;
+    }
   return data;
+}
+
+// A handler's write to a page that is not staged is logged (gpa, bytes)
+// instead of fetching the page: handlers mostly write buffers they never read
+// back (the tlv packet, the hevd IOCTL buffer). Flush turns the log into
+// device write records. Size stays within one page (Backend_t::VirtWrite).
+bool GpuBackend_t::PhysWriteDirect(const Gpa_t Gpa, const uint8_t *Buffer, const uint64_t Size) {
+  const uint32_t lane = cur_;
+  if (Staged *p = find_staged(lane, Gpa.U64() >> 12)) {
+    memcpy(p->data + (Gpa.U64() & 0xfff), Buffer, Size);
+    return true;
+  }
+  LaneView &v = views_[lane];
+  if (v.win_len && Gpa.U64() < v.win_gpa + v.win_len && Gpa.U64() + Size > v.win_gpa) {  // keep the window current
+    const uint64_t lo = std::max(Gpa.U64(), v.win_gpa), hi = std::min(Gpa.U64() + Size, v.win_gpa + v.win_len);
+    memcpy(v.win + (lo - v.win_gpa), Buffer + (lo - Gpa.U64()), hi - lo);
+  }
+  if (!v.wlog.empty()) {  // coalesce with the previous write when it ends where this one starts
+    LaneView::Logged &last = v.wlog.back();
+    if (last.len && last.off + last.len == v.wdata.size() && last.gpa + last.len == Gpa.U64() &&
+        ((last.gpa ^ Gpa.U64()) >> 12) == 0) {
+      last.len += (uint32_t)Size;
+      v.wdata.insert(v.wdata.end(), Buffer, Buffer + Size);
+      return true;
+    }
+  }
+  v.wlog.push_back(LaneView::Logged{Gpa.U64(), (uint32_t)Size, (uint32_t)v.wdata.size()});
+  v.wdata.insert(v.wdata.end(), Buffer, Buffer + Size);
+  return true;
+}
+
+// Reads of clean snapshot pages come straight from the dump (no staging copy);
+// staged pages from their copy; overlay pages and pages with logged writes
+// take the PhysTranslate path (fetch / prefetch, then staged).
+bool GpuBackend_t::PhysReadDirect(const Gpa_t Gpa, uint8_t *Buffer, const uint64_t Size) const {
+  const uint32_t lane = cur_;
+  const uint64_t gpfn = Gpa.U64() >> 12;
+  if (Staged *p = find_staged(lane, gpfn)) {
+    memcpy(Buffer, p->data + (Gpa.U64() & 0xfff), Size);
+    return true;
+  }
+  const LaneView &v = views_[lane];
+  if (v.win_len && Gpa.U64() >= v.win_gpa && Gpa.U64() + Size <= v.win_gpa + v.win_len) {
+    memcpy(Buffer, v.win + (Gpa.U64() - v.win_gpa), Size);
+    return true;
+  }
+  if (!v.dirty_known || in_overlay(v, gpfn)) return false;
+  for (const LaneView::Logged &w : v.wlog)
+    if (w.len && (w.gpa >> 12) == gpfn) return false;
+  const uint8_t *p = dump_.GetPhysicalPage(gpfn << 12);
+  memcpy(Buffer, (p ? p : kZeroPage) + (Gpa.U64() & 0xfff), Size);
+  return true;
 }
 
 uint8_t *GpuBackend_t::stage_copy(uint32_t lane, uint64_t gpfn, const uint8_t *orig) const {
@@ -363,6 +424,17 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
   }
   std::vector<wtfgpu_write_t> writes;
   std::vector<uint8_t> data;
+  for (uint32_t l : lanes) {
+    LaneView &v = views_[l];
+    for (const LaneView::Logged &w : v.wlog) {
+      if (!w.len) continue;
+      writes.push_back(wtfgpu_write_t{l, w.len, w.gpa, data.size()});
+      data.insert(data.end(), v.wdata.begin() + w.off, v.wdata.begin() + w.off + w.len);
+      v.dirty_known = false;
+    }
+    v.wlog.clear();
+    v.wdata.clear();
+  }
   for (const Cand &c : cand) {
     if (c.lo == c.hi) continue;
     wtfgpu_write_t w{};
@@ -389,7 +461,6 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
                              bool per_lane_state) {
   if (lanes.empty()) return true;
   const uint32_t first = lanes.front() & ~63u, count = lanes.back() + 1 - first;
-  const uint32_t cpl = initial_.Cs.Selector & 3;
   std::vector<wtfgpu_exit_t> ex(count);
   std::vector<uint8_t> done(count, 0);
   std::vector<uint32_t> pending = lanes;
@@ -421,7 +492,7 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
         case WTFGPU_EXIT_INT3:                                         // :595-619
         case WTFGPU_EXIT_HLT: v.result = Crash_t(); break;             // :690-697
         case WTFGPU_EXIT_CR3: v.result = Cr3Change_t(); break;         // :628-657
-        case WTFGPU_EXIT_FAULT: v.result = FaultToResult(e.vector, e.error, e.rip, cpl); break;
+        case WTFGPU_EXIT_FAULT: v.result = FaultToResult(e.vector, e.error, e.rip, e.addr, e.opcode); break;
         case WTFGPU_EXIT_STOPPED: break;
         default:  // unimplemented opcode / overlay full: the engine cannot finish it
           if (out) (*out)[l].error = true;
@@ -443,18 +514,27 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
     // learned from the on-demand fetches of earlier hits of the same
     // breakpoint: its stack page (return address / arguments, bp_stack_) and
     // fixed frames (e.g. the tlv packet buffer, bp_pages_)
-    std::vector<uint64_t> sp_gpfn(hits.size(), ~0ull);
+    std::vector<uint64_t> sp_gpfn(hits.size(), ~0ull), sp_gpa(hits.size(), ~0ull);
     for (size_t i = 0; i < hits.size(); i++) {
       LaneView &v = views_[hits[i]];
       memcpy(v.gpr, &regs[i * 18], 18 * 8);
       v.regs_dirty = false;
+      v.win_len = 0;
       drop_staged(v);
       const uint32_t cnt = std::min(dl[i * stride], overlay_pages_);
       v.dirty.assign(dl.begin() + i * stride + 1, dl.begin() + i * stride + 1 + cnt);
       v.dirty_known = true;
-      cur_ = hits[i];
-      Gpa_t sp;
-      if (VirtTranslate(Gva_t(v.gpr[WTFGPU_RSP]), sp, MemoryValidate_t::ValidateRead)) sp_gpfn[i] = sp.U64() >> 12;
+      // the stack page is needed to learn (a breakpoint's first hit) or to
+      // prefetch for breakpoints whose handler reads the stack
+      const uint64_t rip = v.gpr[16];
+      if (!bp_seen_.count(rip) || bp_stack_.count(rip)) {
+        cur_ = hits[i];
+        Gpa_t sp;
+        if (VirtTranslate(Gva_t(v.gpr[WTFGPU_RSP]), sp, MemoryValidate_t::ValidateRead)) {
+          sp_gpa[i] = sp.U64();
+          sp_gpfn[i] = sp.U64() >> 12;
+        }
+      }
     }
     // the handlers: lane by lane, or on all host threads when the module keeps
     // its per-testcase state thread_local (each thread services its own lanes
@@ -492,8 +572,11 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
     // learned from the on-demand fetches of earlier hits of the same
     // breakpoint: its stack page (return address / arguments, bp_stack_) and
     // fixed frames (e.g. the tlv packet buffer, bp_pages_)
-    std::vector<uint32_t> pf_lanes;
-    std::vector<uint64_t> pf_gpas;
+    // The stack is fetched as a kWin-byte window at [rsp] (return address and
+    // stack arguments) when that window stays inside the page; handler reads
+    // outside it fall back to the page path.
+    std::vector<uint32_t> pf_lanes, win_lanes;
+    std::vector<uint64_t> pf_gpas, win_gpas;
     for (size_t i = 0; i < hits.size(); i++) {
       if (scouted[i]) continue;
       const LaneView &v = views_[hits[i]];
@@ -504,10 +587,30 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
         pf_lanes.push_back(hits[i]);
         pf_gpas.push_back(gpfn << 12);
       };
-      if (sp_gpfn[i] != ~0ull && bp_stack_.count(v.gpr[16])) want(sp_gpfn[i]);
+      if (sp_gpfn[i] != ~0ull && bp_stack_.count(v.gpr[16]) && in_overlay(v, sp_gpfn[i])) {
+        if ((sp_gpa[i] & 0xfff) + LaneView::kWin <= Page::Size) {
+          win_lanes.push_back(hits[i]);
+          win_gpas.push_back(sp_gpa[i]);
+        } else {
+          want(sp_gpfn[i]);
+        }
+      }
       auto lp = bp_pages_.find(v.gpr[16]);
       if (lp != bp_pages_.end())
         for (uint64_t g : lp->second) want(g);
+    }
+    if (!win_lanes.empty()) {
+      const size_t nw = win_lanes.size();
+      std::vector<uint8_t> buf(nw * LaneView::kWin);
+      if (wtfgpu_gather_bytes(ctx_, win_lanes.data(), win_gpas.data(), (uint32_t)nw, LaneView::kWin, buf.data()))
+        return false;
+      for (size_t i = 0; i < nw; i++) {
+        LaneView &v = views_[win_lanes[i]];
+        v.win_gpa = win_gpas[i];
+        v.win_len = LaneView::kWin;
+        memcpy(v.win, buf.data() + i * LaneView::kWin, LaneView::kWin);
+      }
+      stats_.stack_windows += nw;
     }
     if (!pf_lanes.empty()) {
       const size_t np = pf_lanes.size();
@@ -714,13 +817,13 @@ std::string GpuBackend_t::StatsJson() const {
   snprintf(b, sizeof(b),
            "{\"kind\":\"gpu\",\"group_steps\":%llu,\"rounds\":%llu,\"breakpoint_hits\":%llu,\"kernel_launches\":%llu,"
            "\"kernel_ms\":%.3f,\"service_ms\":%.3f,\"total_ms\":%.3f,\"page_fetches\":%llu,"
-           "\"prefetched_pages\":%llu,\"staged_pages\":%llu,\"bulk_ms\":%.3f,\"prefetch_ms\":%.3f,"
+           "\"prefetched_pages\":%llu,\"stack_windows\":%llu,\"staged_pages\":%llu,\"bulk_ms\":%.3f,\"prefetch_ms\":%.3f,"
            "\"handler_ms\":%.3f,\"fetch_ms\":%.3f,\"flush_ms\":%.3f,\"insert_ms\":%.3f,\"coverage_ms\":%.3f,"
            "\"target_restore_ms\":%.3f}",
            (unsigned long long)stats_.group_steps, (unsigned long long)stats_.rounds,
            (unsigned long long)stats_.breakpoint_hits, (unsigned long long)stats_.kernel_launches, stats_.kernel_ms,
            stats_.service_ms, stats_.total_ms, (unsigned long long)stats_.page_fetches,
-           (unsigned long long)stats_.prefetched_pages,
+           (unsigned long long)stats_.prefetched_pages, (unsigned long long)stats_.stack_windows,
            (unsigned long long)stats_.staged_pages, stats_.bulk_ms, stats_.prefetch_ms, stats_.handler_ms,
            stats_.fetch_ms, stats_.flush_ms, stats_.insert_ms, stats_.coverage_ms, stats_.target_restore_ms);
   std::string r(b);

@@ -30,7 +30,7 @@ namespace wtfgpu_host {
 
 struct BatchStats {
   uint64_t rounds = 0, breakpoint_hits = 0, kernel_launches = 0, retired = 0, group_steps = 0;
-  uint64_t page_fetches = 0, prefetched_pages = 0, batches = 0, testcases = 0, staged_pages = 0;
+  uint64_t page_fetches = 0, prefetched_pages = 0, batches = 0, testcases = 0, staged_pages = 0, stack_windows = 0;
   double kernel_ms = 0, service_ms = 0, total_ms = 0;
   // service_ms split: bulk reads (regs, dirty lists), stack/learned prefetch,
   // module handlers (incl. on-demand page fetches), flush (writes + resume/stop)
@@ -62,6 +62,8 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   bool VirtTranslate(const Gva_t Gva, Gpa_t &Gpa, const MemoryValidate_t Validate) const override;
   uint8_t *PhysTranslate(const Gpa_t Gpa) const override;
   bool PageFaultsMemoryIfNeeded(const Gva_t Gva, const uint64_t Size) override;
+  bool PhysWriteDirect(const Gpa_t Gpa, const uint8_t *Buffer, const uint64_t Size) override;
+  bool PhysReadDirect(const Gpa_t Gpa, uint8_t *Buffer, const uint64_t Size) const override;
   const std::unordered_set<Gva_t> &LastNewCoverage() const override;
   bool RevokeLastNewCoverage() override;
   using Backend_t::SetBreakpoint;
@@ -99,6 +101,20 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
     bool dirty_known = false;
     std::vector<uint32_t> dirty;  // gpfns the lane's overlay holds
     std::vector<Staged> pages;    // staged pages (few per lane: linear search)
+    // writes to pages that are not staged, logged instead of fetching the
+    // page (PhysWriteDirect); merged into a page if it gets staged later
+    struct Logged {
+      uint64_t gpa;
+      uint32_t len, off;
+    };
+    std::vector<Logged> wlog;
+    std::vector<uint8_t> wdata;
+    // stack window: kWin bytes at [rsp] gathered for handlers that read their
+    // return address / stack arguments (sub-page prefetch, valid one round)
+    static constexpr uint32_t kWin = 128;
+    uint64_t win_gpa = 0;
+    uint32_t win_len = 0;
+    uint8_t win[kWin];
   };
 
   LaneView &cur() const { return views_[cur_]; }

@@ -75,7 +75,7 @@ wtfgpu_regs_t RegsFromCpuState(const CpuState_t &S) {
   return r;
 }
 
-TestcaseResult_t FaultToResult(uint32_t vector, uint32_t error, uint64_t rip, uint32_t cpl) {
+TestcaseResult_t FaultToResult(uint32_t vector, uint32_t error, uint64_t rip, uint64_t addr, uint32_t cpl) {
   uint32_t code = EXCEPTION_ACCESS_VIOLATION_READ;
   switch (vector) {
     case WTFGPU_VEC_DE: code = EXCEPTION_INT_DIVIDE_BY_ZERO; break;
@@ -92,8 +92,13 @@ TestcaseResult_t FaultToResult(uint32_t vector, uint32_t error, uint64_t rip, ui
   if (cpl == 3)
     snprintf(name, sizeof(name), "crash-%s-%#llx", std::string(ExceptionCodeToStr(code)).c_str(),
              (unsigned long long)rip);
-  else
-    snprintf(name, sizeof(name), "crash-kernel-vector%u-%#llx", vector, (unsigned long long)rip);
+  else if (vector == WTFGPU_VEC_PF)  // KiPageFault -> KeBugCheckEx(PAGE_FAULT_IN_NONPAGED_AREA, cr2, access, rip, 0)
+    snprintf(name, sizeof(name), "crash-0x50-0x%llx-0x%x-0x%llx-0x0-0x0", (unsigned long long)addr,
+             (error & ErrorInstructionFetch) ? 0x10u : (error & ErrorWrite) ? 2u : 0u, (unsigned long long)rip);
+  else  // KMODE_EXCEPTION_NOT_HANDLED(NTSTATUS, rip, 0, 0)
+    snprintf(name, sizeof(name), "crash-0x1e-0x%x-0x%llx-0x0-0x0-0x0",
+             vector == WTFGPU_VEC_DE ? 0xc0000094u : vector == WTFGPU_VEC_UD ? 0xc000001du : 0xc0000005u,
+             (unsigned long long)rip);
   return Crash_t(name);
 }
 

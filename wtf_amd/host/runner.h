@@ -68,9 +68,10 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
 // Options_t + CpuState_t from <target>/state (regs.json, symbol store) and the runner options.
 bool LoadTarget(const RunnerOptions &O, Options_t &Opts, CpuState_t &State);
 
-// A lane's FAULT exit as the user-mode crash detection would name it
+// A lane's FAULT exit named as the guest would report it: ring 3 as the user-mode
+// crash detection does, ring 0 as the bugcheck the kernel raises
 // (crash_detection_umode.cc:53-129 + backend.cc:204-212).
-TestcaseResult_t FaultToResult(uint32_t vector, uint32_t error, uint64_t rip, uint32_t cpl);
+TestcaseResult_t FaultToResult(uint32_t vector, uint32_t error, uint64_t rip, uint64_t addr, uint32_t cpl);
 
 // The CpuState_t -> wtfgpu_regs_t mapping (LoadState, bochscpu_backend.cc:1026-1122).
 wtfgpu_regs_t RegsFromCpuState(const CpuState_t &S);

@@ -21,6 +21,7 @@ bool Backend_t::SetTraceFile(const fs::path &, const TraceType_t) {
 
 // backend.cc:16-28
 bool Backend_t::PhysWrite(const Gpa_t Gpa, const uint8_t *Buffer, const uint64_t BufferSize, const bool Dirty) {
+  if (PhysWriteDirect(Gpa, Buffer, BufferSize)) return true;  // the backend dirties what it writes
   uint8_t *Dst = PhysTranslate(Gpa);
   if (!Dst) return false;
   memcpy(Dst, Buffer, BufferSize);
@@ -40,9 +41,11 @@ bool Backend_t::VirtRead(const Gva_t Gva, uint8_t *Buffer, const uint64_t Buffer
       return false;
     }
     const uint64_t Chunk = std::min<uint64_t>(Left, Page::Size - (Cur & 0xfff));
-    const uint8_t *Hva = PhysTranslate(Gpa);
-    if (!Hva) return false;
-    memcpy(Buffer, Hva, Chunk);
+    if (!PhysReadDirect(Gpa, Buffer, Chunk)) {
+      const uint8_t *Hva = PhysTranslate(Gpa);
+      if (!Hva) return false;
+      memcpy(Buffer, Hva, Chunk);
+    }
     Buffer += Chunk;
     Cur += Chunk;
     Left -= Chunk;

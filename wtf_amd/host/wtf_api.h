@@ -220,6 +220,12 @@ class Backend_t {
   virtual bool PageFaultsMemoryIfNeeded(const Gva_t Gva, const uint64_t Size) = 0;
   virtual const std::unordered_set<Gva_t> &LastNewCoverage() const = 0;
   virtual bool RevokeLastNewCoverage() = 0;
+  // Optional fast paths under PhysWrite / VirtRead (not in the reference, whose
+  // helpers always go through PhysTranslate, backend.cc:16-56): a backend that
+  // does not hold guest memory in host pages serves a physical read or write
+  // without materialising the page. false = not handled, use PhysTranslate.
+  virtual bool PhysWriteDirect(const Gpa_t, const uint8_t *, const uint64_t) { return false; }
+  virtual bool PhysReadDirect(const Gpa_t, uint8_t *, const uint64_t) const { return false; }
 
   // helpers implemented on top of the virtuals (backend.cc)
   bool SaveCrash(const Gva_t ExceptionAddress, const uint32_t ExceptionCode);
