@@ -526,6 +526,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     UCEntry *e = &uc[uc_slot(key)];
     const bool cacheable = lptr >= pool_lo && lptr < pool_hi;
     if (cacheable && rfl64(e->key) != key) uc_fill(P, e, key, lptr, off, grip, lid);
+    STAMP(2);
     const u32 flags = cacheable ? rfl32(e->flags) : UC_CROSS;
     if (flags & (UC_CROSS | UC_BADLEN)) {
       if (flags & UC_BADLEN) {
@@ -533,7 +534,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       } else {
         WITH_LANE_COPY(slow_step(P, T, grip, lptr, ing, skip, wv, lid, ep));
       }
-      STAMP(1);
+      STAMP(5);
       continue;
     }
     const u32 len = rfl32(e->u.len);
@@ -547,6 +548,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
         if (lid == 0) e->logged = logged | gmask;
       }
     }
+    STAMP(3);
     if (ing) {
       if ((flags & UC_BP) && !skip) {
         L.status = WTFGPU_EXIT_BREAKPOINT;
@@ -1557,8 +1559,11 @@ int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps
     st.group_steps += s[0];
     st.lane_retired += s[1];
 #ifdef WTFGPU_STAMPS
-    fprintf(stderr, "wtfgpu stamps (cycles per wave-step): fast loop %.0f, slow steps %.0f\n", (double)s[4] / s[0],
-            (double)s[5] / s[0]);
+    fprintf(stderr,
+            "wtfgpu stamps (cycles per wave-step, %llu steps): fast loop %.0f, slow: xlate+fill %.0f, coverage %.0f, "
+            "exec %.0f, cross-page %.0f\n",
+            (unsigned long long)s[0], (double)s[4] / s[0], (double)s[6] / s[0], (double)s[7] / s[0],
+            (double)s[5] / s[0], (double)s[9] / s[0]);
 #endif
     done += steps;
     if (s[2] == 0 || done >= max_steps) break;

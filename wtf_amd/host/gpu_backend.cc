@@ -346,26 +346,60 @@ const uint8_t *GpuBackend_t::lane_page_ro(uint32_t lane, uint64_t gpfn) const {
 }
 
 // bochscpu_mem_virt_translate semantics (present bits only), on the lane view
+// Walk memo (per host thread, direct mapped): a walk that read only snapshot
+// page-table pages (none staged or in the lane's overlay) holds for every lane
+// whose view does not hold those table frames either, so it is reused after a
+// per-lane check of at most four frames instead of a four-level walk.
+namespace {
+struct WalkMemo {
+  uint64_t vpn = ~0ull, base = 0, mask = 0;
+  uint64_t tables[4] = {};
+  uint32_t ntables = 0;
+};
+thread_local WalkMemo t_walk_memo[64];
+}  // namespace
+
 bool GpuBackend_t::VirtTranslate(const Gva_t Gva, Gpa_t &Gpa, const MemoryValidate_t) const {
+  const uint64_t va = Gva.U64(), vpn = va >> 12;
+  const LaneView &v = views_[cur_];
+  WalkMemo &m = t_walk_memo[vpn & 63];
+  if (m.vpn == vpn && v.dirty_known) {
+    bool clean = true;
+    for (uint32_t k = 0; k < m.ntables && clean; k++)
+      clean = !in_overlay(v, m.tables[k]) && !find_staged(cur_, m.tables[k]);
+    if (clean) {
+      Gpa = Gpa_t(m.base | (va & m.mask));
+      return true;
+    }
+  }
   uint64_t table = initial_.Cr3 & 0x000ffffffffff000ull;
-  const uint64_t va = Gva.U64();
+  WalkMemo w;
+  bool from_dump = v.dirty_known;
   for (int level = 3; level >= 0; level--) {
-    const uint8_t *pg = lane_page_ro(cur_, table >> 12);
+    const uint64_t tf = table >> 12;
+    w.tables[w.ntables++] = tf;
+    from_dump = from_dump && !in_overlay(v, tf) && !find_staged(cur_, tf);
+    const uint8_t *pg = lane_page_ro(cur_, tf);
     uint64_t e;
     memcpy(&e, pg + ((va >> (12 + 9 * level)) & 0x1ff) * 8, 8);
     if (!(e & 1)) return false;
     const uint64_t frame = e & 0x000ffffffffff000ull;
-    if (level == 2 && (e & 0x80)) {
-      Gpa = Gpa_t((frame & ~0x3fffffffull) | (va & 0x3fffffffull));
-      return true;
+    if ((level == 2 || level == 1) && (e & 0x80)) {
+      w.mask = level == 2 ? 0x3fffffffull : 0x1fffffull;
+      w.base = frame & ~w.mask;
+      break;
     }
-    if (level == 1 && (e & 0x80)) {
-      Gpa = Gpa_t((frame & ~0x1fffffull) | (va & 0x1fffffull));
-      return true;
+    if (level == 0) {
+      w.mask = 0xfff;
+      w.base = frame;
     }
     table = frame;
   }
-  Gpa = Gpa_t(table | (va & 0xfff));
+  Gpa = Gpa_t(w.base | (va & w.mask));
+  if (from_dump) {
+    w.vpn = vpn;
+    m = w;
+  }
   return true;
 }
 
