@@ -549,6 +549,8 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
     // breakpoint: its stack page (return address / arguments, bp_stack_) and
     // fixed frames (e.g. the tlv packet buffer, bp_pages_)
     std::vector<uint64_t> sp_gpfn(hits.size(), ~0ull), sp_gpa(hits.size(), ~0ull);
+    // lane views of the hits (independent per lane: all host threads)
+#pragma omp parallel for schedule(static)
     for (size_t i = 0; i < hits.size(); i++) {
       LaneView &v = views_[hits[i]];
       memcpy(v.gpr, &regs[i * 18], 18 * 8);
@@ -611,6 +613,14 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
     // outside it fall back to the page path.
     std::vector<uint32_t> pf_lanes, win_lanes;
     std::vector<uint64_t> pf_gpas, win_gpas;
+    std::vector<uint8_t> use_win(hits.size(), 0);
+#pragma omp parallel for schedule(static)
+    for (size_t i = 0; i < hits.size(); i++) {
+      if (scouted[i] || sp_gpfn[i] == ~0ull) continue;
+      const LaneView &v = views_[hits[i]];
+      if (bp_stack_.count(v.gpr[16]) && in_overlay(v, sp_gpfn[i]))
+        use_win[i] = (sp_gpa[i] & 0xfff) + LaneView::kWin <= Page::Size ? 1 : 2;  // 2: whole page
+    }
     for (size_t i = 0; i < hits.size(); i++) {
       if (scouted[i]) continue;
       const LaneView &v = views_[hits[i]];
@@ -621,23 +631,24 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
         pf_lanes.push_back(hits[i]);
         pf_gpas.push_back(gpfn << 12);
       };
-      if (sp_gpfn[i] != ~0ull && bp_stack_.count(v.gpr[16]) && in_overlay(v, sp_gpfn[i])) {
-        if ((sp_gpa[i] & 0xfff) + LaneView::kWin <= Page::Size) {
-          win_lanes.push_back(hits[i]);
-          win_gpas.push_back(sp_gpa[i]);
-        } else {
-          want(sp_gpfn[i]);
-        }
+      if (use_win[i] == 1) {
+        win_lanes.push_back(hits[i]);
+        win_gpas.push_back(sp_gpa[i]);
+      } else if (use_win[i] == 2) {
+        want(sp_gpfn[i]);
       }
-      auto lp = bp_pages_.find(v.gpr[16]);
-      if (lp != bp_pages_.end())
-        for (uint64_t g : lp->second) want(g);
+      if (!bp_pages_.empty()) {
+        auto lp = bp_pages_.find(v.gpr[16]);
+        if (lp != bp_pages_.end())
+          for (uint64_t g : lp->second) want(g);
+      }
     }
     if (!win_lanes.empty()) {
       const size_t nw = win_lanes.size();
       std::vector<uint8_t> buf(nw * LaneView::kWin);
       if (wtfgpu_gather_bytes(ctx_, win_lanes.data(), win_gpas.data(), (uint32_t)nw, LaneView::kWin, buf.data()))
         return false;
+#pragma omp parallel for schedule(static)
       for (size_t i = 0; i < nw; i++) {
         LaneView &v = views_[win_lanes[i]];
         v.win_gpa = win_gpas[i];
