@@ -163,7 +163,7 @@ __device__ __forceinline__ void fetch_bytes(u64 pageptr, u32 off, u32 n, u64 &lo
 // already in the aggregate coverage map, and the lanes this wave has already
 // logged for it in this launch.
 #ifndef WTFGPU_UC_N
-#define WTFGPU_UC_N 128
+#define WTFGPU_UC_N 64  // 128 (with a packed UOp) measured: no tlv gain, SYN k_run +3 %
 #endif
 constexpr u32 UC_N = WTFGPU_UC_N;  // entries per wave (power of two)
 constexpr u32 UC_BP = 1, UC_COVERED = 2, UC_CROSS = 4, UC_BADLEN = 8, UC_UNSUP = 16;

@@ -37,19 +37,15 @@ enum : u32 {
 // size kinds
 enum : u32 { Z_B = 0, Z_V, Z_STK, Z_Q, Z_W, Z_D };
 
-// Packed to 48 bytes (byte fields) so 128 decoded entries per wave fit the
-// LDS budget of two 256-thread blocks per CU (engine.hip UC_N).
 struct UOp {
+  u32 len, op, sub, asrc, bsrc, asz, bsz;
+  u32 aread, awrite, bwrite;
+  u32 reg, rm, opreg, is_mem, riprel, p67, rex, rep, seg;
+  i32 base, index;
+  u32 scale;
   u64 disp, imm;
-  u32 opbytes;
-  u8 len, op, sub, asrc, bsrc, asz, bsz;
-  u8 aread, awrite, bwrite;
-  u8 reg, rm, opreg, is_mem, riprel, p67, rex, rep, seg;
-  u8 scale, supported;
-  int8_t base, index;
-  u8 pad_[5];
+  u32 supported, opbytes;
 };
-static_assert(sizeof(UOp) == 48, "UOp layout");
 
 // ---------------------------------------------------------------- registers
 __device__ __forceinline__ u64 getr(const Lane &L, u32 rex, u32 r, u32 sz) {
