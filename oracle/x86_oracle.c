@@ -128,6 +128,8 @@ struct orc_machine {
   u64 limit;
   u64 icount;
   u64 bytes;
+  u64 deliv_icount; /* retired count at the last IDT delivery (valid if deliv_valid) */
+  int deliv_valid;
   /* per-instruction scratch */
   wtfgpu_exit_t *ex;
   int faulted;
@@ -201,6 +203,7 @@ void orc_restore(orc_machine *m, const wtfgpu_regs_t *r) {
   m->initial_cr3 = r->cr3;
   m->icount = 0;
   m->bytes = 0;
+  m->deliv_valid = 0;
 }
 
 uint64_t orc_icount(orc_machine *m) { return m->icount; }
@@ -1339,6 +1342,26 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
       m->r.seg[WTFGPU_GS].base = m->r.kernel_gs_base;
       m->r.kernel_gs_base = a;
       return X_OK;
+    case 0x20: { /* mov r64, crN (ring 0) */
+      if (d->is_mem) return X_UNIMPL;
+      if (cpl(m) != 0) {
+        fault(m, WTFGPU_VEC_GP, 0);
+        return X_FAULT;
+      }
+      const u32 n = d->reg & 15;
+      u64 v;
+      if (n == 0) v = m->r.cr0;
+      else if (n == 2) v = m->r.cr2;
+      else if (n == 3) v = m->r.cr3;
+      else if (n == 4) v = m->r.cr4;
+      else if (n == 8) v = 0;
+      else {
+        fault(m, WTFGPU_VEC_UD, 0);
+        return X_FAULT;
+      }
+      setreg(m, d, d->rm, 8, v);
+      return X_OK;
+    }
     case 0xc7: /* rdrand r: deterministic 0 with CF=1 (U15) */
       if (d->is_mem || (d->reg & 7) != 6 || d->pfx66 || d->rep) return X_UNIMPL;
       setreg(m, d, d->rm, osz, 0);
@@ -1646,7 +1669,7 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
     if ((b >= 0x40 && b <= 0x4f) || (b >= 0x90 && b <= 0x9f) || b == 0xa3 || b == 0xab ||
         b == 0xb3 || b == 0xbb || b == 0xaf || b == 0xb0 || b == 0xb1 || b == 0xb6 ||
         b == 0xb7 || b == 0xbe || b == 0xbf || b == 0xbc || b == 0xbd || b == 0xb8 ||
-        b == 0xc0 || b == 0xc1 || b == 0xa5 || b == 0xad || b == 0x0d || b == 0x01 || b == 0xc7 ||
+        b == 0xc0 || b == 0xc1 || b == 0xa5 || b == 0xad || b == 0x0d || b == 0x01 || b == 0xc7 || b == 0x20 ||
         (b >= 0x18 && b <= 0x1f))
       has_modrm = 1;
     if (b == 0xa4 || b == 0xac || b == 0xba) {
@@ -1677,6 +1700,74 @@ static void fill_exit(orc_machine *m, wtfgpu_exit_t *ex, u32 status) {
 }
 
 /* One instruction: fetch, decode, coverage, breakpoint, execute, retire. */
+/* ---------------- exception delivery (U18) ----------------
+ * A fault is delivered through the guest IDT when the snapshot has a present
+ * 64-bit interrupt / trap gate for it (SDM vol. 3 6.12-6.14); otherwise, or
+ * for a fault before any instruction retired since the last delivery (a
+ * double fault), the machine stops with the fault. Implicit supervisor
+ * accesses: no permission checks. Frame words are written lowest first. */
+static int has_error_code(u32 v) { return v == 8 || (v >= 10 && v <= 14) || v == 17 || v == 21 || v == 29 || v == 30; }
+static int sup_read(orc_machine *m, u64 va, void *out, u32 n) {
+  u64 pa;
+  if (walk(m, va, ACC_R, 0, &pa)) return -1;
+  if ((pa & 0xfff) + n > 4096) return -1;
+  memcpy(out, phys_ro(m, pa >> 12) + (pa & 0xfff), n);
+  return 0;
+}
+static int sup_write8(orc_machine *m, u64 va, u64 v) {
+  u64 pa;
+  if (walk(m, va, ACC_W, 0, &pa)) return -1;
+  if ((pa & 0xfff) + 8 > 4096) return -1;
+  memcpy(phys_rw(m, pa >> 12) + (pa & 0xfff), &v, 8);
+  return 0;
+}
+static int deliver(orc_machine *m, u32 vec, u32 err, u64 cr2) {
+  wtfgpu_exit_t keep = *m->ex;
+  const int fk = m->faulted;
+  int ok = 0;
+  do {
+    if (m->deliv_valid && m->deliv_icount == m->icount) break;
+    if (!m->r.idtr_base || vec > 31 || (u64)vec * 16 + 15 > m->r.idtr_limit) break;
+    u64 g[2];
+    if (sup_read(m, m->r.idtr_base + (u64)vec * 16, g, 16)) break;
+    const u32 attr = (u32)(g[0] >> 40) & 0xff, type = attr & 0xf, ist = (u32)(g[0] >> 32) & 7;
+    if (!(attr & 0x80) || (type != 0xe && type != 0xf)) break;
+    const u64 target = (g[0] & 0xffff) | ((g[0] >> 32) & 0xffff0000ULL) | (g[1] << 32);
+    const u16 sel = (u16)((g[0] >> 16) & 0xffff);
+    const u32 ncpl = sel & 3, ocpl = (u32)cpl(m);
+    if (!is_canonical(target) || ncpl > ocpl) break;
+    u64 rsp = m->r.gpr[WTFGPU_RSP];
+    if (ist || ncpl < ocpl) {
+      const u64 off = ist ? 0x24 + (u64)(ist - 1) * 8 : 4 + (u64)ncpl * 8;
+      if (sup_read(m, m->r.seg[WTFGPU_TR].base + off, &rsp, 8)) break;
+    }
+    rsp &= ~0xfULL;
+    u64 frame[6];
+    u32 n = 0;
+    if (has_error_code(vec)) frame[n++] = err;
+    frame[n++] = m->r.rip;
+    frame[n++] = m->r.seg[WTFGPU_CS].selector;
+    frame[n++] = m->r.rflags;
+    frame[n++] = m->r.gpr[WTFGPU_RSP];
+    frame[n++] = m->r.seg[WTFGPU_SS].selector;
+    int wr = 1;
+    for (u32 i = 0; i < n && wr; i++) wr = sup_write8(m, rsp - 8 * n + 8 * i, frame[i]) == 0;
+    if (!wr) break;
+    if (ncpl < ocpl) m->r.seg[WTFGPU_SS].selector = (u16)ncpl;
+    m->r.seg[WTFGPU_CS].selector = sel;
+    if (vec == WTFGPU_VEC_PF) m->r.cr2 = cr2;
+    m->deliv_valid = 1;
+    m->deliv_icount = m->icount;
+    m->r.gpr[WTFGPU_RSP] = rsp - 8 * n;
+    m->r.rflags &= ~(0x100ULL | 0x4000ULL | 0x10000ULL | 0x20000ULL | (type == 0xe ? 0x200ULL : 0));
+    m->r.rip = target;
+    ok = 1;
+  } while (0);
+  *m->ex = keep;
+  m->faulted = fk;
+  return ok;
+}
+
 static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
   insn d;
   memref mr;
@@ -1692,6 +1783,7 @@ static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
       ex->addr = 0;
     }
     fill_exit(m, ex, WTFGPU_EXIT_FAULT);
+    if (deliver(m, ex->vector, ex->error, ex->addr)) return ex->status = WTFGPU_RUNNING;
     return ex->status;
   }
   /* coverage (bochscpu_backend.cc:501-504) then breakpoint lookup (:545-547) */
@@ -1739,6 +1831,7 @@ static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
     ex->vector = keep.vector;
     ex->error = keep.error;
     ex->addr = keep.addr;
+    if (deliver(m, ex->vector, ex->error, ex->addr)) return ex->status = WTFGPU_RUNNING;
     break;
   }
   case X_UNIMPL:

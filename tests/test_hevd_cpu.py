@@ -55,6 +55,19 @@ def test_crafted_bug_classes(target, tmp_path):
     assert not any(r["error"] for r in res.values())
 
 
+def test_kernel_faults_delivered_through_idt(target, tmp_path):
+    """Ring-0 faults go through the guest IDT (U18): the #PF / #GP handlers run
+    (their rips are covered) and the bugcheck comes from nt!KeBugCheck2."""
+    import json
+    d = str(tmp_path / "in")
+    write_inputs(d, 0)
+    res = _run(target, d, str(tmp_path / "r.jsonl"))
+    sym = {k: int(v, 16) for k, v in json.load(open(os.path.join(target, "state", "symbol-store.json"))).items()}
+    assert sym["nt!KiPageFault"] in res["null_deref"]["coverage"]
+    assert sym["nt!KiGeneralProtectionFault"] in res["stack_ret_overrun"]["coverage"]
+    assert sym["nt!KeBugCheck2"] in res["null_deref"]["coverage"]
+
+
 def test_batch_size_does_not_change_results(target, tmp_path):
     d = str(tmp_path / "in")
     write_inputs(d, 150)

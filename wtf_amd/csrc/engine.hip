@@ -77,6 +77,7 @@ __device__ __forceinline__ void load_lane(const Dev &P, u32 lane, Lane &L) {
   L.exvec = L.exerr = L.exop = 0;
   L.exaddr = 0;
   L.miss = L.miss_acc = L.flush = L.pend = 0;
+  L.nodeliver = 0;
   L.miss_va = 0;
 }
 
@@ -203,6 +204,119 @@ __device__ __forceinline__ bool bp_lookup(const Dev &P, u64 rip) {
 }
 
 // Fill one entry (uniform): fetch + decode from the pool page, digest, lookups.
+// Write len bytes at gpa into the lane's overlay (copy-on-write + dirty).
+__device__ __forceinline__ bool lane_phys_write(const Dev &P, Lane &L, u64 gpa, const u8 *src, u64 len) {
+  while (len) {
+    const u64 off = gpa & 0xfff;
+    u64 n = 4096 - off;
+    if (n > len) n = len;
+    bool priv;
+    const u8 *pg = phys_page(P, L.lane, L.ovn, L.bloom, gpa >> 12, priv);
+    u8 *dst = (u8 *)pg;
+    if (!priv) {
+      if (L.ovn >= P.K) return false;
+      dst = cow_copy(P, L.lane, L.ovn, gpa >> 12, pg);
+      L.ovn++;
+      L.bloom |= bloom_bit(gpa >> 12);
+    }
+    for (u64 i = 0; i < n; i++) dst[off + i] = src[i];
+    src += n;
+    gpa += n;
+    len -= n;
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------- exception delivery
+// A fault is delivered through the guest IDT when the snapshot has a present
+// 64-bit interrupt / trap gate for it (SDM vol. 3 6.12-6.14): stack switch to
+// TSS.RSP0 / IST on a privilege change, SS:RSP, RFLAGS, CS:RIP and the error
+// code pushed, IF cleared for interrupt gates, cr2 set for #PF. Otherwise (no
+// IDT: the ring-3 snapshots; a nested fault while delivering) the lane exits
+// with the fault as before.
+__device__ __forceinline__ bool has_error_code(u32 vec) {
+  return vec == 8 || (vec >= 10 && vec <= 14) || vec == 17 || vec == 21 || vec == 29 || vec == 30;
+}
+__device__ __forceinline__ bool sup_xlate(const Dev &P, Lane &L, u64 va, int acc, u64 &gpa) {
+  u64 td, gpfn;
+  if (!walk(P, L, va, acc, td, gpfn)) return false;
+  gpa = (gpfn << 12) | (va & 0xfff);
+  return true;
+}
+__device__ __noinline__ bool deliver_fault(const Dev &P, Lane &L) {
+  LaneSys &S = P.sys[L.lane];
+  const u32 vec = L.exvec, err = L.exerr;
+  const u64 cr2 = L.exaddr, frip = L.rip;
+  const u32 st0 = L.status, cpl0 = L.cpl;
+  bool ok = false;
+  do {
+    // a fault before any instruction retired since the last delivery (the
+    // handler itself faults at once) ends as an exit: the double / triple fault
+    // a CPU would raise (U18)
+    if (S.deliv_icount == L.icount) break;
+    if (!S.idtr || vec > 31 || (u64)vec * 16 + 15 > S.idtr_limit) break;
+    u64 ga;
+    if (!sup_xlate(P, L, S.idtr + vec * 16, ACC_R, ga) || (ga & 0xfff) > 4096 - 16) break;
+    bool priv;
+    const u8 *g = phys_page(P, L.lane, L.ovn, L.bloom, ga >> 12, priv) + (ga & 0xfff);
+    const u64 lo = *(const u64 *)g, hi = *(const u64 *)(g + 8);
+    const u32 attr = (u32)(lo >> 40) & 0xff, type = attr & 0xf, ist = (u32)(lo >> 32) & 7;
+    if (!(attr & 0x80) || (type != 0xe && type != 0xf)) break;
+    const u64 target = (lo & 0xffff) | ((lo >> 32) & 0xffff0000ull) | (hi << 32);
+    const u16 sel = (u16)((lo >> 16) & 0xffff);
+    const u32 ncpl = sel & 3;
+    if (!canonical(target) || ncpl > L.cpl) break;
+    u64 rsp = R(L, 4);
+    if (ist || ncpl < L.cpl) {  // TSS64: RSP0 at +4, IST1 at +0x24
+      const u64 off = ist ? 0x24 + (u64)(ist - 1) * 8 : 4 + (u64)ncpl * 8;
+      u64 ta;
+      if (!sup_xlate(P, L, S.tss + off, ACC_R, ta) || (ta & 0xfff) > 4096 - 8) break;
+      const u8 *t = phys_page(P, L.lane, L.ovn, L.bloom, ta >> 12, priv) + (ta & 0xfff);
+      u64 v = 0;
+      for (int i = 0; i < 8; i++) v |= (u64)t[i] << (8 * i);
+      rsp = v;
+    }
+    rsp &= ~0xfull;
+    const bool ec = has_error_code(vec);
+    u64 frame[6];
+    u32 n = 0;
+    if (ec) frame[n++] = err;
+    frame[n++] = frip;
+    frame[n++] = S.cs;
+    frame[n++] = L.rflags;
+    frame[n++] = R(L, 4);
+    frame[n++] = S.ss;
+    L.cpl = 0;  // implicit supervisor accesses
+    bool wr = true;
+    for (u32 i = 0; i < n && wr; i++) {  // frame[0] lands at the lowest address
+      u64 pa;
+      wr = sup_xlate(P, L, rsp - 8 * n + 8 * i, ACC_W, pa) && (pa & 0xfff) <= 4096 - 8 &&
+           lane_phys_write(P, L, pa, (const u8 *)&frame[i], 8);
+    }
+    if (!wr) break;
+    if (ncpl < cpl0) S.ss = (u16)ncpl;  // SS := NULL selector at the new privilege level
+    S.cs = sel;
+    if (vec == WTFGPU_VEC_PF) S.cr2 = cr2;
+    L.cpl = S.cpl = ncpl;
+    S.deliv_icount = L.icount;
+    RS(L, 4, rsp - 8 * n);
+    L.rflags &= ~(0x100ull | 0x4000ull | 0x10000ull | 0x20000ull | (type == 0xe ? 0x200ull : 0));
+    L.rip = target;
+    L.status = WTFGPU_RUNNING;
+    L.flush = 1;
+    ok = true;
+  } while (0);
+  if (!ok) {  // keep the original fault
+    L.cpl = cpl0;
+    L.status = st0;
+    L.exvec = vec;
+    L.exerr = err;
+    L.exaddr = cr2;
+    L.nodeliver = 1;
+  }
+  return ok;
+}
+
 __device__ __noinline__ void uc_fill(const Dev &P, UCEntry *e, u64 key, u64 lptr, u32 off, u64 rip, u32 lid) {
   IBytes ib;
   ib.avail = 4096 - off < 16 ? 4096 - off : 16;
@@ -508,6 +622,16 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       }
     }
     STAMP(0);
+    // faults raised by the last slow step: deliver through the guest IDT when
+    // it has a gate (the lane resumes at the handler), else the lane exits
+    if (__ballot(valid && L.status == WTFGPU_EXIT_FAULT && !L.nodeliver)) {
+      if (valid && L.status == WTFGPU_EXIT_FAULT && !L.nodeliver) {
+        bool dv;
+        WITH_LANE_COPY(dv = deliver_fault(P, T));
+        (void)dv;
+      }
+      continue;
+    }
     if (!have) break;
 
     // ================= slow step for group `grip`: translation misses, cache
@@ -678,6 +802,7 @@ __device__ __forceinline__ void lane_min_load(const Dev &P, u32 lane, Lane &L) {
   tlb_flush(L);
   L.tnext = 0;
   L.miss = L.miss_acc = L.flush = L.pend = 0;
+  L.nodeliver = 0;
 }
 
 // Host-side translation (bochscpu_mem_virt_translate semantics: present bits
@@ -697,29 +822,6 @@ __device__ __forceinline__ bool host_walk(const Dev &P, Lane &L, u64 va, u64 &gp
     table = e & 0x000ffffffffff000ull;
   }
   gpa = ((e & 0x000ffffffffff000ull) & ~pmask) | (va & pmask);
-  return true;
-}
-
-// Write len bytes at gpa into the lane's overlay (copy-on-write + dirty).
-__device__ __forceinline__ bool lane_phys_write(const Dev &P, Lane &L, u64 gpa, const u8 *src, u64 len) {
-  while (len) {
-    const u64 off = gpa & 0xfff;
-    u64 n = 4096 - off;
-    if (n > len) n = len;
-    bool priv;
-    const u8 *pg = phys_page(P, L.lane, L.ovn, L.bloom, gpa >> 12, priv);
-    u8 *dst = (u8 *)pg;
-    if (!priv) {
-      if (L.ovn >= P.K) return false;
-      dst = cow_copy(P, L.lane, L.ovn, gpa >> 12, pg);
-      L.ovn++;
-      L.bloom |= bloom_bit(gpa >> 12);
-    }
-    for (u64 i = 0; i < n; i++) dst[off + i] = src[i];
-    src += n;
-    gpa += n;
-    len -= n;
-  }
   return true;
 }
 
@@ -1029,6 +1131,11 @@ InitState make_init(const wtfgpu_regs_t &r) {
   s.sys.sfmask = r.sfmask;
   s.sys.kgs = r.kernel_gs_base;
   s.sys.cs = r.seg[WTFGPU_CS].selector;
+  s.sys.idtr = r.idtr_base;
+  s.sys.idtr_limit = r.idtr_limit;
+  s.sys.tss = r.seg[WTFGPU_TR].base;
+  s.sys.cr2 = r.cr2;
+  s.sys.deliv_icount = ~0ull;
   s.sys.ss = r.seg[WTFGPU_SS].selector;
   return s;
 }
@@ -1439,6 +1546,7 @@ int wtfgpu_read_regs(wtfgpu_ctx *c, uint32_t first, uint32_t count, wtfgpu_regs_
     r.cr4 = sys[l].cr4;
     r.efer = sys[l].efer;
     r.kernel_gs_base = sys[l].kgs;
+    r.cr2 = sys[l].cr2;
     r.seg[WTFGPU_CS].selector = sys[l].cs;
     r.seg[WTFGPU_SS].selector = sys[l].ss;
   }

@@ -44,6 +44,9 @@ constexpr int TLB_N = 4;
 struct LaneSys {   // rarely touched per-lane system state
   u64 cr0, cr3, cr4, efer;
   u64 star, lstar, sfmask, kgs;  // SYSCALL/SYSRET MSRs, IA32_KERNEL_GS_BASE (SWAPGS)
+  u64 idtr, tss, cr2;            // IDT base, TSS base (TR), cr2 (exception delivery)
+  u64 deliv_icount;              // retired count at the last delivery (~0: none)
+  u32 idtr_limit, pad;
   u32 cpl;
   u16 cs, ss;                    // selectors after SYSCALL/SYSRET (64-bit mode, STAR)
 };

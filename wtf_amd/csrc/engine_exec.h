@@ -18,6 +18,7 @@ struct Lane {
   u64 miss_va;               // pending translation (TLB miss or copy-on-write)
   u32 tnext, ovn, cpl, status, lane, exvec, exerr, exop;
   u32 miss, miss_acc, flush, pend;  // pend: bytes accessed by the attempt in flight
+  u32 nodeliver;                    // this fault could not be delivered through the guest IDT
 };
 
 // GPR r of the lane. r is wave-uniform and the halves live in two u32 arrays

@@ -161,7 +161,7 @@ __constant__ u32 kMap2[256] = {
     /*00*/ UN, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 1, K_NONE, 0), UN, UN, UN, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN,
     E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, UN, UN, E(O_UD, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, NOPM, UN, UN,
     /*10*/ UN, UN, UN, UN, UN, UN, UN, UN, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM,
-    /*20*/ UN16,
+    /*20*/ E(O_SYS, L_RM, 0, Z_Q, Z_Q, 0, 1, 0, 1, K_NONE, 0), UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN,
     /*30*/ UN16,
     /*40*/ CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV,
     /*50*/ UN16,
@@ -411,8 +411,10 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
     if (u.op == O_BSF && u.rep == 0xf3) u.op = O_TZCNT;
     if (u.op == O_BSR && u.rep == 0xf3) u.op = O_LZCNT;
     if (u.op == O_SYS) {
-      // 0 syscall, 1 sysret (64-bit form only), 2 swapgs (0f 01 f8), 3 rdrand r (0f c7 /6)
-      u.sub = c == 0x05 ? 0 : c == 0x07 ? 1 : c == 0x01 ? 2 : 3;
+      // 0 syscall, 1 sysret (64-bit form only), 2 swapgs (0f 01 f8), 3 rdrand r (0f c7 /6),
+      // 4 mov r64, crN (0f 20 /r)
+      u.sub = c == 0x05 ? 0 : c == 0x07 ? 1 : c == 0x01 ? 2 : c == 0x20 ? 4 : 3;
+      if (c == 0x20 && u.is_mem) u.op = O_UNIMPL;
       if (c == 0x07 && !rexw) u.op = O_UNIMPL;
       if (c == 0x01 && (u.is_mem || (u.reg & 7) != 7 || (u.rm & 7) != 0)) u.op = O_UNIMPL;
       if (c == 0xc7 && (u.is_mem || (u.reg & 7) != 6 || p66 || u.rep)) u.op = O_UNIMPL;
@@ -1009,6 +1011,23 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
       // 64-bit SYSCALL / SYSRET with STAR selectors (no descriptor loads),
       // SWAPGS, and a deterministic RDRAND.
       LaneSys &S = P.sys[L.lane];
+      if (u.sub == 4) {  // mov r64, crN (ring 0)
+        if (L.cpl != 0) {
+          set_fault(L, WTFGPU_VEC_GP, 0, 0);
+          return X_FAULT;
+        }
+        const u32 n = u.reg & 15;
+        if (n == 0) res = S.cr0;
+        else if (n == 2) res = S.cr2;
+        else if (n == 3) res = S.cr3;
+        else if (n == 4) res = S.cr4;
+        else if (n == 8) res = 0;
+        else {
+          set_fault(L, WTFGPU_VEC_UD, 0, 0);
+          return X_FAULT;
+        }
+        break;
+      }
       if (u.sub == 3) {  // rdrand: 0 with CF=1 (U15)
         res = 0;
         fl = with_status(fl, F_CF);

@@ -272,3 +272,32 @@ __asm__(".globl KiSystemCall64\n"
         "  mov %gs:0x10, %rsp\n"
         "  swapgs\n"
         "  sysretq\n");
+
+/* ---- exception entry (the IDT built by hevd.py points here). A kernel-mode
+ * fault bugchecks the way Windows reports it: #PF as
+ * PAGE_FAULT_IN_NONPAGED_AREA(cr2, access, rip, 0), the others as
+ * KMODE_EXCEPTION_NOT_HANDLED(NTSTATUS, rip, 0, 0). A user-mode fault ends the
+ * thread: the scheduler switches away (nt!SwapContext). */
+struct TrapFrame {
+  u64 Error, Rip, Cs, Rflags, Rsp, Ss;
+};
+__attribute__((noipa, used)) void KiTrapHandler(u64 Vector, struct TrapFrame *F, u64 Cr2) {
+  if (F->Cs & 3) ((void (*)(void))SwapContext)();
+  if (Vector == 14)
+    KeBugCheckEx(0x50, Cr2, (F->Error & 0x10) ? 0x10 : (F->Error & 2) ? 2 : 0, F->Rip, 0);
+  KeBugCheckEx(0x1E, Vector == 0 ? 0xC0000094u : Vector == 6 ? 0xC000001Du : 0xC0000005u, F->Rip, 0, 0);
+}
+/* stubs: faults without an error code push a zero so every frame is a TrapFrame */
+__asm__(".globl KiDivideErrorFault\n.globl KiInvalidOpcodeFault\n.globl KiGeneralProtectionFault\n"
+        ".globl KiPageFault\n"
+        ".p2align 4\nKiDivideErrorFault:\n  push $0\n  mov $0, %ecx\n  jmp KiTrapCommon\n"
+        ".p2align 4\nKiInvalidOpcodeFault:\n  push $0\n  mov $6, %ecx\n  jmp KiTrapCommon\n"
+        ".p2align 4\nKiGeneralProtectionFault:\n  mov $13, %ecx\n  jmp KiTrapCommon\n"
+        ".p2align 4\nKiPageFault:\n  mov $14, %ecx\n  jmp KiTrapCommon\n"
+        "KiTrapCommon:\n"
+        "  mov %rsp, %rdx\n"
+        "  mov %cr2, %r8\n"
+        "  and $-16, %rsp\n"
+        "  sub $0x20, %rsp\n"
+        "  call KiTrapHandler\n"
+        "  hlt\n");

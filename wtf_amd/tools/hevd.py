@@ -26,6 +26,8 @@ Layout (guest virtual):
   0x10000000                  user buffer, 2 pages (rw-)
   STACK_TOP-0x4000..STACK_TOP user stack (rw-)
   0xFFFFF80000100000          kernel image (supervisor)
+  0xFFFFF80000002000          TSS (RSP0 = kernel stack), 0xFFFFF80000004000 IDT
+                              (#DE/#UD/#GP/#PF gates -> KiTrapHandler)
   0xFFFFF80000200000          KPCR page (supervisor rw-)
   0xFFFFF80000300000..+0x8000 kernel stack (supervisor rw-)
 """
@@ -49,7 +51,21 @@ STACK_TOP = 0x7FF000000000
 KPCR = 0xFFFFF80000200000
 KSTACK = 0xFFFFF80000300000
 KSTACK_PAGES = 8
+IDT = 0xFFFFF80000004000  # idtr (user_state), limit 0xfff
+TSS = 0xFFFFF80000002000  # tr.base (user_state)
 HANDLE = 0x3C
+TRAPS = {0: "KiDivideErrorFault", 6: "KiInvalidOpcodeFault", 13: "KiGeneralProtectionFault", 14: "KiPageFault"}
+
+
+def idt_page(ksyms: dict) -> bytes:
+    """64-bit interrupt gates (present, DPL 0, type 0xE, selector 0x10) for the
+    fault vectors the kernel image handles; the other vectors stay not-present."""
+    idt = bytearray(PAGE)
+    for vec, name in TRAPS.items():
+        off = ksyms[name]
+        lo = (off & 0xFFFF) | (0x10 << 16) | (0x8E << 40) | (((off >> 16) & 0xFFFF) << 48)
+        struct.pack_into("<QQ", idt, vec * 16, lo, off >> 32)
+    return bytes(idt)
 
 
 def compile_images(work_dir: str) -> tuple[str, str]:
@@ -84,6 +100,10 @@ def build(state_dir: str, work_dir: str | None = None) -> dict:
         sp.map(USER_BUF + i * PAGE, b"", nx=True)
     for va in range(STACK_TOP - 0x4000, STACK_TOP, PAGE):
         sp.map(va, b"", nx=True)
+    sp.map(IDT, idt_page(ksyms), user=False, write=False, nx=True)
+    tss = bytearray(PAGE)
+    struct.pack_into("<Q", tss, 4, KSTACK + KSTACK_PAGES * PAGE - 0x40)  # RSP0
+    sp.map(TSS, bytes(tss), user=False, nx=True)
     kpcr = bytearray(PAGE)
     struct.pack_into("<Q", kpcr, 0x1A8, KSTACK + KSTACK_PAGES * PAGE - 0x40)
     sp.map(KPCR, bytes(kpcr), user=False, nx=True)
@@ -102,6 +122,8 @@ def build(state_dir: str, work_dir: str | None = None) -> dict:
         "nt!ExGenRandom": ksyms["ExGenRandom"],
         "nt!KeBugCheck2": ksyms["KeBugCheck2"],
         "nt!SwapContext": ksyms["SwapContext"],
+        "nt!KiPageFault": ksyms["KiPageFault"],
+        "nt!KiGeneralProtectionFault": ksyms["KiGeneralProtectionFault"],
         "nt!KiSystemCall64": ksyms["KiSystemCall64"],
         "HEVD!IrpDeviceIoCtlHandler": ksyms["NtDeviceIoControlFile"],
         "kernelbase!DeviceIoControl": usyms["DeviceIoControl"],
