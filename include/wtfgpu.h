@@ -233,6 +233,13 @@ int wtfgpu_gather_pages(wtfgpu_ctx *ctx, const uint32_t *lanes, const uint64_t *
 int wtfgpu_gather_bytes(wtfgpu_ctx *ctx, const uint32_t *lanes, const uint64_t *gpas, uint32_t n, uint32_t len,
                         uint8_t *out);
 
+/* Inject an exception into each lane (PageFaultsMemoryIfNeeded,
+ * bochscpu_backend.cc:917-999): delivered through the guest IDT now (cr2 :=
+ * addrs[i] for #PF); the lane resumes at the handler. delivered[i] = 0 when the
+ * snapshot has no usable gate (the lane is left as it was). */
+int wtfgpu_inject_fault(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, uint32_t vector, uint32_t error,
+                        const uint64_t *addrs, int32_t *delivered);
+
 /* Page-locked host memory (for gather/scatter staging buffers). */
 int wtfgpu_host_alloc(wtfgpu_ctx *ctx, uint64_t bytes, void **out);
 int wtfgpu_host_free(wtfgpu_ctx *ctx, void *p);

@@ -61,6 +61,7 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
   std::unordered_set<uint64_t> aggregate_;
   std::unordered_set<Gva_t> last_new_;
   uint64_t retired_total_ = 0;
+  uint64_t inject_ = ~0ull;  // page to #PF after the current handler
 
   wtfgpu_regs_t regs() const {
     wtfgpu_regs_t r;
@@ -95,10 +96,18 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
       if (e.status == WTFGPU_EXIT_BREAKPOINT) {
         const uint64_t rip0 = regs().rip;
         auto it = bps_.find(rip0);
+        inject_ = ~0ull;
         if (it != bps_.end()) it->second(this);
         flush();
         if (result_) break;
         skip = regs().rip == rip0;  // U10: a moved rip cancels the hooked instruction
+        if (inject_ != ~0ull) {  // PageFaultsMemoryIfNeeded: #PF(Write|User) before the instruction
+          if (!orc_inject_fault(m_, WTFGPU_VEC_PF, ErrorWrite | ErrorUser, inject_)) {
+            result_ = Crash_t();  // no IDT to take it: the triple fault bochs would stop on
+            break;
+          }
+          skip = 0;
+        }
         continue;
       }
       switch (e.status) {
@@ -197,7 +206,18 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
     }
     return it->second.data.data() + (Gpa.U64() & 0xfff);
   }
-  bool PageFaultsMemoryIfNeeded(const Gva_t, const uint64_t) override { return false; }
+  // bochscpu_backend.cc:902-999: the first page of the range that does not
+  // translate gets a #PF injected once the handler returns
+  bool PageFaultsMemoryIfNeeded(const Gva_t Gva, const uint64_t Size) override {
+    for (uint64_t a = Gva.U64() & ~0xfffull; a < Gva.U64() + Size; a += 0x1000) {
+      Gpa_t G;
+      if (!VirtTranslate(Gva_t(a), G, MemoryValidate_t::ValidateRead)) {
+        inject_ = a;
+        return true;
+      }
+    }
+    return false;
+  }
   const std::unordered_set<Gva_t> &LastNewCoverage() const override { return last_new_; }
   bool RevokeLastNewCoverage() override {
     for (const Gva_t &g : last_new_) aggregate_.erase(g.U64());

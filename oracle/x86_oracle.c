@@ -1845,6 +1845,15 @@ static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
   return ex->status;
 }
 
+/* Host-injected exception (PageFaultsMemoryIfNeeded, bochscpu_backend.cc:917-999):
+ * delivered through the guest IDT before the next instruction. 1 = delivered. */
+int orc_inject_fault(orc_machine *m, uint32_t vector, uint32_t error, uint64_t addr) {
+  wtfgpu_exit_t ex;
+  memset(&ex, 0, sizeof(ex));
+  m->ex = &ex;
+  return deliver(m, vector, error, addr);
+}
+
 int orc_run(orc_machine *m, int skip_bp, wtfgpu_exit_t *ex) {
   int first = 1;
   for (;;) {

@@ -42,6 +42,7 @@ int orc_set_breakpoints(orc_machine *m, const uint64_t *gvas, uint32_t n);
 /* Restore: drop overlays, reload registers, zero counters and coverage. */
 void orc_restore(orc_machine *m, const wtfgpu_regs_t *r);
 /* Run until an exit. skip_bp: do not trigger the breakpoint at the current rip once. */
+int orc_inject_fault(orc_machine *m, uint32_t vector, uint32_t error, uint64_t addr);
 int orc_run(orc_machine *m, int skip_bp, wtfgpu_exit_t *exit);
 /* Execute exactly one instruction (no breakpoint check); returns status. */
 int orc_step(orc_machine *m, wtfgpu_exit_t *exit);

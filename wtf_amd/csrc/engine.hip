@@ -303,7 +303,10 @@ __device__ __noinline__ bool deliver_fault(const Dev &P, Lane &L) {
     L.rflags &= ~(0x100ull | 0x4000ull | 0x10000ull | 0x20000ull | (type == 0xe ? 0x200ull : 0));
     L.rip = target;
     L.status = WTFGPU_RUNNING;
-    L.flush = 1;
+    // the frame pushes may have copied the stack page and the cpl changed:
+    // drop cached translations now (the handler may run in the fast loop)
+    tlb_flush(L);
+    L.flush = 0;
     ok = true;
   } while (0);
   if (!ok) {  // keep the original fault
@@ -858,6 +861,29 @@ __global__ void k_apply_writes(Dev P, const WriteRec *recs, const u32 *starts, u
     status_out[r] = st;
   }
   P.ov_count[lane] = L.ovn;
+}
+
+// Host-injected exception per lane (PageFaultsMemoryIfNeeded): delivered
+// through the guest IDT now; the lane resumes at the handler.
+__global__ void k_inject_fault(Dev P, const u32 *lanes, const u64 *addrs, u32 n, u32 vector, u32 error, i32 *ok) {
+  const u32 t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const u32 lane = lanes[t];
+  u32 glo[16], ghi[16];
+  Lane L;
+  L.glo = glo;
+  L.ghi = ghi;
+  load_lane(P, lane, L);
+  L.status = WTFGPU_EXIT_FAULT;
+  L.exvec = vector;
+  L.exerr = error;
+  L.exaddr = addrs[t];
+  const bool d = deliver_fault(P, L);
+  ok[t] = d ? 1 : 0;
+  if (d) {
+    store_lane(P, L);
+    P.lflags[lane] = 0;
+  }
 }
 
 // Lane status (+ skip-breakpoint-once flag) for a lane list (resume / stop).
@@ -1848,6 +1874,25 @@ int wtfgpu_gather_pages(wtfgpu_ctx *c, const uint32_t *lanes, const uint64_t *gp
                                            c->d_scratch + o_out);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(out, c->d_scratch + o_out, (u64)n * WTFGPU_PAGE_SIZE, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_inject_fault(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, uint32_t vector, uint32_t error,
+                        const uint64_t *addrs, int32_t *delivered) {
+  if (int rc = check_lane_list(c, lanes, n)) return rc;
+  if (n == 0) return WTFGPU_OK;
+  if (!addrs || !delivered || vector > 31) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  const u64 o_a = ((u64)n * 4 + 255) & ~255ull, o_ok = (o_a + (u64)n * 8 + 255) & ~255ull;
+  if (ensure_scratch(c, o_ok + (u64)n * 4)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemcpyAsync(c->d_scratch, lanes, (u64)n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_scratch + o_a, addrs, (u64)n * 8, hipMemcpyHostToDevice, c->stream));
+  k_inject_fault<<<(n + 63) / 64, 64, 0, c->stream>>>(c->P, (const u32 *)c->d_scratch,
+                                                     (const u64 *)(c->d_scratch + o_a), n, vector, error,
+                                                     (i32 *)(c->d_scratch + o_ok));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(delivered, c->d_scratch + o_ok, (u64)n * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return WTFGPU_OK;
 }

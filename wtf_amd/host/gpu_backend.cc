@@ -409,8 +409,17 @@ uint8_t *GpuBackend_t::PhysTranslate(const Gpa_t Gpa) const {
   return lane_page(cur_, Gpa.U64() >> 12) + (Gpa.U64() & 0xfff);
 }
 
-bool GpuBackend_t::PageFaultsMemoryIfNeeded(const Gva_t, const uint64_t) {
-  // needs #PF injection through the guest IDT: not in this engine yet
+// bochscpu_backend.cc:902-999: the first page of the range that does not
+// translate gets a #PF(Write|User) injected when the handler returns; the guest
+// pages it in and re-executes the hooked instruction (its breakpoint fires again).
+bool GpuBackend_t::PageFaultsMemoryIfNeeded(const Gva_t Gva, const uint64_t Size) {
+  for (uint64_t a = Gva.U64() & ~0xfffull; a < Gva.U64() + Size; a += Page::Size) {
+    Gpa_t G;
+    if (!VirtTranslate(Gva_t(a), G, MemoryValidate_t::ValidateRead)) {
+      cur().inject = a;
+      return true;
+    }
+  }
   return false;
 }
 
@@ -586,6 +595,7 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
       auto it = breakpoints_.find(rip0);
       if (per_lane_state && slots) slots->SwapIn(l);
       servicing_bp_ = rip0;
+      v.inject = ~0ull;
       if (it != breakpoints_.end()) it->second(this);  // BeforeExecutionHook (bochscpu_backend.cc:545-547)
       servicing_bp_ = ~0ull;
       if (per_lane_state && slots) slots->SwapOut(l);
@@ -684,6 +694,34 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
     }
     g_Backend = saved;
     stats_.breakpoint_hits += hits.size();
+    const auto t3 = Clock::now();
+    stats_.handler_ms += std::chrono::duration<double, std::milli>(t3 - t2).count();
+    if (flush_lanes(hits)) return false;
+    {  // PageFaultsMemoryIfNeeded requests: #PF through the guest IDT, resume at the handler
+      std::vector<uint32_t> il;
+      std::vector<uint64_t> ia;
+      std::vector<size_t> ih;
+      for (size_t h = 0; h < hits.size(); h++)
+        if (action[h] != 0 && views_[hits[h]].inject != ~0ull) {
+          il.push_back(hits[h]);
+          ia.push_back(views_[hits[h]].inject);
+          ih.push_back(h);
+        }
+      if (!il.empty()) {
+        std::vector<int32_t> ok(il.size());
+        if (wtfgpu_inject_fault(ctx_, il.data(), (uint32_t)il.size(), WTFGPU_VEC_PF, ErrorWrite | ErrorUser, ia.data(),
+                                ok.data()))
+          return false;
+        for (size_t k = 0; k < il.size(); k++) {
+          if (ok[k]) {
+            action[ih[k]] = 1;  // resume at the handler, no breakpoint skip
+          } else {
+            views_[il[k]].result = Crash_t();  // no IDT to take it: the triple fault bochs stops on
+            action[ih[k]] = 0;
+          }
+        }
+      }
+    }
     std::vector<uint32_t> resume, stop;
     std::vector<uint8_t> skip;
     for (size_t h = 0; h < hits.size(); h++) {
@@ -695,9 +733,6 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
         skip.push_back(action[h] == 2);
       }
     }
-    const auto t3 = Clock::now();
-    stats_.handler_ms += std::chrono::duration<double, std::milli>(t3 - t2).count();
-    if (flush_lanes(hits)) return false;
     if (!stop.empty() && wtfgpu_stop(ctx_, stop.data(), (uint32_t)stop.size(), WTFGPU_EXIT_STOPPED)) return false;
     if (!resume.empty() && wtfgpu_resume(ctx_, resume.data(), (uint32_t)resume.size(), skip.data())) return false;
     stats_.flush_ms += ms_since(t3);

@@ -98,6 +98,7 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
     bool regs_dirty = false;
     std::optional<TestcaseResult_t> result;
     uint64_t seed = 0;
+    uint64_t inject = ~0ull;  // PageFaultsMemoryIfNeeded: page to #PF after the handler
     bool dirty_known = false;
     std::vector<uint32_t> dirty;  // gpfns the lane's overlay holds
     std::vector<Staged> pages;    // staged pages (few per lane: linear search)
