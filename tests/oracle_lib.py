@@ -38,6 +38,7 @@ def lib() -> C.CDLL:
         "orc_write_phys": ([P, U64, P, U64], C.c_int),
         "orc_read_virt": ([P, U64, P, U64], C.c_int),
         "orc_write_virt": ([P, U64, P, U64], C.c_int),
+        "orc_inject_fault": ([P, U32, U32, U64], C.c_int),
     }
     for n, (a, r) in sig.items():
         f = getattr(L, n)
@@ -125,6 +126,9 @@ class Oracle:
         b = C.create_string_buffer(n)
         self.L.orc_read_phys(self.m, gpa, b, n)
         return b.raw
+
+    def inject_fault(self, vector, error, addr) -> bool:
+        return bool(self.L.orc_inject_fault(self.m, vector, error, addr))
 
     def translate(self, gva):
         out = C.c_uint64()

@@ -111,6 +111,7 @@ def load_hip_library(path: str = LIB_PATH) -> C.CDLL:
         "wtfgpu_write_gprs": ([P, U32, U32, C.POINTER(U64)], C.c_int),
         "wtfgpu_read_exits": ([P, U32, U32, C.POINTER(Exit)], C.c_int),
         "wtfgpu_resume": ([P, C.POINTER(U32), U32, C.POINTER(C.c_uint8)], C.c_int),
+        "wtfgpu_inject_fault": ([P, C.POINTER(U32), U32, U32, U32, C.POINTER(U64), C.POINTER(C.c_int32)], C.c_int),
         "wtfgpu_stop": ([P, C.POINTER(U32), U32, U32], C.c_int),
         "wtfgpu_run": ([P, U32, U32, U64, C.POINTER(RunStats)], C.c_int),
         "wtfgpu_lane_translate": ([P, U32, U64, C.POINTER(U64)], C.c_int),

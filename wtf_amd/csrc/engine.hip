@@ -227,6 +227,21 @@ __device__ __forceinline__ bool lane_phys_write(const Dev &P, Lane &L, u64 gpa, 
   return true;
 }
 
+// One aligned 64-bit word at gpa (copy-on-write + dirty).
+__device__ __forceinline__ bool lane_phys_write64(const Dev &P, Lane &L, u64 gpa, u64 v) {
+  bool priv;
+  const u8 *pg = phys_page(P, L.lane, L.ovn, L.bloom, gpa >> 12, priv);
+  u8 *dst = (u8 *)pg;
+  if (!priv) {
+    if (L.ovn >= P.K) return false;
+    dst = cow_copy(P, L.lane, L.ovn, gpa >> 12, pg);
+    L.ovn++;
+    L.bloom |= bloom_bit(gpa >> 12);
+  }
+  *(u64 *)(dst + (gpa & 0xfff)) = v;
+  return true;
+}
+
 // ---------------------------------------------------------------- exception delivery
 // A fault is delivered through the guest IDT when the snapshot has a present
 // 64-bit interrupt / trap gate for it (SDM vol. 3 6.12-6.14): stack switch to
@@ -278,20 +293,16 @@ __device__ __noinline__ bool deliver_fault(const Dev &P, Lane &L) {
     }
     rsp &= ~0xfull;
     const bool ec = has_error_code(vec);
-    u64 frame[6];
-    u32 n = 0;
-    if (ec) frame[n++] = err;
-    frame[n++] = frip;
-    frame[n++] = S.cs;
-    frame[n++] = L.rflags;
-    frame[n++] = R(L, 4);
-    frame[n++] = S.ss;
+    const u32 n = ec ? 6 : 5;
+    const u64 ors = R(L, 4), orfl = L.rflags, ocs = S.cs, oss = S.ss;
     L.cpl = 0;  // implicit supervisor accesses
     bool wr = true;
-    for (u32 i = 0; i < n && wr; i++) {  // frame[0] lands at the lowest address
+    // frame words, lowest address first: [error], rip, cs, rflags, rsp, ss
+    for (u32 i = 0; i < n && wr; i++) {
+      const u32 k = ec ? i : i + 1;
+      const u64 w = k == 0 ? (u64)err : k == 1 ? frip : k == 2 ? ocs : k == 3 ? orfl : k == 4 ? ors : oss;
       u64 pa;
-      wr = sup_xlate(P, L, rsp - 8 * n + 8 * i, ACC_W, pa) && (pa & 0xfff) <= 4096 - 8 &&
-           lane_phys_write(P, L, pa, (const u8 *)&frame[i], 8);
+      wr = sup_xlate(P, L, rsp - 8 * n + 8 * i, ACC_W, pa) && (pa & 7) == 0 && lane_phys_write64(P, L, pa, w);
     }
     if (!wr) break;
     if (ncpl < cpl0) S.ss = (u16)ncpl;  // SS := NULL selector at the new privilege level

@@ -121,6 +121,14 @@ class Engine:
         sk = (C.c_uint8 * max(1, n))(*[1 if s else 0 for s in skip])
         _chk(self.L.wtfgpu_resume(self.ctx, la, n, sk), "resume")
 
+    def inject_fault(self, lanes, vector, error, addrs) -> list[bool]:
+        n = len(lanes)
+        la = (C.c_uint32 * max(1, n))(*lanes)
+        aa = (C.c_uint64 * max(1, n))(*addrs)
+        ok = (C.c_int32 * max(1, n))()
+        _chk(self.L.wtfgpu_inject_fault(self.ctx, la, n, vector, error, aa, ok), "inject_fault")
+        return [bool(ok[i]) for i in range(n)]
+
     def stop(self, lanes, status=abi.EXIT_STOPPED):
         n = len(lanes)
         la = (C.c_uint32 * max(1, n))(*lanes)

@@ -87,7 +87,13 @@ def _map_image(sp: AddressSpace, segs, user: bool) -> None:
 def build(state_dir: str, work_dir: str | None = None) -> dict:
     """Compiles both images and writes mem.dmp / regs.json / symbol-store.json
     into state_dir. Returns {name: address} of the guest symbols."""
-    work_dir = work_dir or state_dir
+    sp, st, symbols, syms = build_space(work_dir or state_dir)
+    write_snapshot(state_dir, sp, st, symbols)
+    return syms
+
+
+def build_space(work_dir: str):
+    """(address space, CPU state, symbol store, guest symbols) of the snapshot."""
     user_elf, kernel_elf = compile_images(work_dir)
     usegs, usyms = _elf(user_elf)
     ksegs, ksyms = _elf(kernel_elf)
@@ -128,8 +134,8 @@ def build(state_dir: str, work_dir: str | None = None) -> dict:
         "HEVD!IrpDeviceIoCtlHandler": ksyms["NtDeviceIoControlFile"],
         "kernelbase!DeviceIoControl": usyms["DeviceIoControl"],
     }
-    write_snapshot(state_dir, sp, st, symbols)
-    return {**{f"user:{k}": v for k, v in usyms.items()}, **{f"kernel:{k}": v for k, v in ksyms.items()}}
+    syms = {**{f"user:{k}": v for k, v in usyms.items()}, **{f"kernel:{k}": v for k, v in ksyms.items()}}
+    return sp, st, symbols, syms
 
 
 def testcase(ioctl: int, body: bytes) -> bytes:
