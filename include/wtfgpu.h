@@ -162,6 +162,29 @@ int wtfgpu_set_initial_state(wtfgpu_ctx *ctx, const wtfgpu_regs_t *regs);
 int wtfgpu_set_limit(wtfgpu_ctx *ctx, uint64_t limit);
 int wtfgpu_set_breakpoints(wtfgpu_ctx *ctx, const uint64_t *gvas, uint32_t n);
 
+/* Device-side breakpoint actions (new; no bochscpu counterpart). A breakpoint
+ * whose handler only moves registers — a Backend_t handler that is
+ * SimulateReturnFromFunction(value) (backend.cc:129-146), or one that loads a
+ * fixed GPR set + rip (fuzzer_tlv_server.cc:171-179) — can be declared as
+ * data; the lane then applies it inside wtfgpu_run and keeps running instead
+ * of exiting to the host. The hooked instruction is cancelled as for a host
+ * handler that moves rip (U10); a lane whose action fails (the return address
+ * does not translate) exits with WTFGPU_EXIT_BREAKPOINT and the host handler
+ * runs. Actions apply only at gvas also passed to wtfgpu_set_breakpoints. */
+enum wtfgpu_bp_action_kind {
+  WTFGPU_BPACT_HOST = 0,           /* exit to the host (default) */
+  WTFGPU_BPACT_RETURN = 1,         /* rax = value; rip = [rsp]; rsp += 8 */
+  WTFGPU_BPACT_SET_GPRS = 2,       /* gprs[0..15] (WTFGPU_RAX order), rip = gprs[16] */
+};
+typedef struct wtfgpu_bp_action {
+  uint64_t gva;
+  uint32_t kind;
+  uint32_t pad;
+  uint64_t value;
+  uint64_t gprs[17];
+} wtfgpu_bp_action_t;
+int wtfgpu_set_breakpoint_actions(wtfgpu_ctx *ctx, const wtfgpu_bp_action_t *acts, uint32_t n);
+
 /* Coverage index space: code pages (gva >> 12) that get a 4096-byte slot in
  * the per-GPU coverage map. Pages outside it are still logged per lane. */
 int wtfgpu_set_code_pages(wtfgpu_ctx *ctx, const uint64_t *vpns, uint32_t n);

@@ -53,6 +53,15 @@ class RunStats(C.Structure):
                 ("lane_retired", C.c_uint64), ("kernel_ms", C.c_double)]
 
 
+class BpAction(C.Structure):
+    """wtfgpu_bp_action_t: a breakpoint handler's device-side register effect."""
+    _fields_ = [("gva", C.c_uint64), ("kind", C.c_uint32), ("pad", C.c_uint32),
+                ("value", C.c_uint64), ("gprs", C.c_uint64 * 17)]
+
+
+BPACT_HOST, BPACT_RETURN, BPACT_SET_GPRS = 0, 1, 2
+
+
 class Write(C.Structure):
     _fields_ = [("lane", C.c_uint32), ("len", C.c_uint32), ("gva", C.c_uint64),
                 ("data_off", C.c_uint64)]
@@ -103,6 +112,7 @@ def load_hip_library(path: str = LIB_PATH) -> C.CDLL:
         "wtfgpu_set_initial_state": ([P, C.POINTER(Regs)], C.c_int),
         "wtfgpu_set_limit": ([P, U64], C.c_int),
         "wtfgpu_set_breakpoints": ([P, C.POINTER(U64), U32], C.c_int),
+        "wtfgpu_set_breakpoint_actions": ([P, C.POINTER(BpAction), U32], C.c_int),
         "wtfgpu_set_code_pages": ([P, C.POINTER(U64), U32], C.c_int),
         "wtfgpu_restore": ([P, U32, U32], C.c_int),
         "wtfgpu_read_regs": ([P, U32, U32, C.POINTER(Regs)], C.c_int),

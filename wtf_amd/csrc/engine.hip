@@ -415,6 +415,41 @@ __device__ __forceinline__ void retire(const Dev &P, Lane &L, int x, u32 len, u6
   }
 }
 
+// Device-side breakpoint action (wtfgpu_set_breakpoint_actions) at `grip`.
+// true = applied, the lane keeps running at its new rip; false = none
+// declared or it could not be applied: the lane exits to the host handler,
+// registers untouched. RETURN reads [rsp] as the host's
+// SimulateReturnFromFunction does (backend.cc:129-146); a read that would fault
+// is left to the host path, whose translation decides the outcome.
+__device__ __noinline__ bool bp_apply(const Dev &P, Lane &L, u64 grip) {
+  u32 s;
+  if (!P.act_keys || !hash_find(P.act_keys, P.act_mask, grip, s)) return false;
+  const wtfgpu_bp_action_t &a = P.act[s];
+  if (a.kind == WTFGPU_BPACT_SET_GPRS) {
+    for (u32 i = 0; i < 16; i++) RS(L, i, a.gprs[i]);
+    L.rip = a.gprs[16];
+    return true;
+  }
+  if (a.kind != WTFGPU_BPACT_RETURN) return false;
+  const u64 rsp = R(L, WTFGPU_RSP);
+  u64 ra = 0;
+  for (int attempt = 0;; attempt++) {
+    L.miss = 0;
+    if (vread(L, rsp, 8, ra)) break;
+    if (L.status != WTFGPU_RUNNING || !L.miss || !miss_service(P, L, attempt)) {
+      L.status = WTFGPU_RUNNING;  // undo a fault: the host handler decides
+      L.miss = 0;
+      L.pend = 0;
+      return false;
+    }
+  }
+  L.pend = 0;
+  RS(L, WTFGPU_RAX, a.value);
+  RS(L, WTFGPU_RSP, rsp + 8);
+  L.rip = ra;
+  return true;
+}
+
 // A step the uop cache cannot serve: code on a lane overlay page, or an
 // instruction that crosses into the next page (translated per lane).
 __device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr, bool ing, bool &skip, u32 wv,
@@ -465,10 +500,15 @@ __device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr
   const bool isbp = bp_lookup(P, grip);
   if (ing) {
     if (isbp && !skip) {
-      L.status = WTFGPU_EXIT_BREAKPOINT;
+      // breakpoint hit (bochscpu_backend.cc:545-547): device action or host exit;
+      // an action that left rip unchanged runs the instruction next step (skip)
+      const bool applied = bp_apply(P, L, grip);
+      if (!applied) L.status = WTFGPU_EXIT_BREAKPOINT;
+      skip = applied && L.rip == grip;
       ing = false;
+    } else {
+      skip = false;
     }
-    skip = false;
   }
   if (!d.supported) {
     if (ing) {
@@ -692,10 +732,15 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     STAMP(3);
     if (ing) {
       if ((flags & UC_BP) && !skip) {
-        L.status = WTFGPU_EXIT_BREAKPOINT;
+        // breakpoint hit: device action (the lane keeps running) or host exit
+        bool applied = false;
+        if (P.act_keys) WITH_LANE_COPY(applied = bp_apply(P, T, grip));
+        if (!applied) L.status = WTFGPU_EXIT_BREAKPOINT;
+        skip = applied && L.rip == grip;
         ing = false;
+      } else {
+        skip = false;
       }
-      skip = false;
     }
     if (ing && (flags & UC_UNSUP)) {
       const u32 ob = e->u.opbytes, n = len;
@@ -1084,6 +1129,8 @@ struct wtfgpu_ctx {
   wtfgpu_regs_t *d_full = nullptr;  // full per-lane architectural state (cold fields)
   // breakpoints
   u64 *d_bp = nullptr;
+  u64 *d_actkeys = nullptr;
+  wtfgpu_bp_action_t *d_act = nullptr;
   // coverage
   u64 *d_codekeys = nullptr;
   u32 *d_codeslot = nullptr;
@@ -1256,6 +1303,8 @@ int wtfgpu_destroy(wtfgpu_ctx *c) {
   dfree(c->d_pfnmap);
   dfree(c->d_ptbits);
   dfree(c->d_bp);
+  dfree(c->d_actkeys);
+  dfree(c->d_act);
   dfree(c->d_codekeys);
   dfree(c->d_codeslot);
   dfree(c->d_covmap);
@@ -1475,6 +1524,38 @@ int wtfgpu_set_breakpoints(wtfgpu_ctx *c, const uint64_t *gvas, uint32_t n) {
   HIPCHK(hipStreamSynchronize(c->stream));
   c->P.bp_keys = c->d_bp;
   c->P.bp_mask = sz - 1;
+  return WTFGPU_OK;
+}
+
+int wtfgpu_set_breakpoint_actions(wtfgpu_ctx *c, const wtfgpu_bp_action_t *acts, uint32_t n) {
+  if (!c || (n && !acts)) return WTFGPU_ERR_INVALID;
+  for (u32 i = 0; i < n; i++)
+    if (acts[i].kind > WTFGPU_BPACT_SET_GPRS || acts[i].gva == EMPTY_KEY) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  dfree(c->d_actkeys);
+  dfree(c->d_act);
+  c->P.act_keys = nullptr;
+  c->P.act = nullptr;
+  c->P.act_mask = 0;
+  if (n == 0) return WTFGPU_OK;
+  const u32 sz = table_size(n);
+  std::vector<u64> t(sz, EMPTY_KEY);
+  std::vector<wtfgpu_bp_action_t> a(sz);
+  memset(a.data(), 0, sz * sizeof(wtfgpu_bp_action_t));
+  for (u32 i = 0; i < n; i++) {
+    u32 h = (u32)hmix(acts[i].gva) & (sz - 1);
+    while (t[h] != EMPTY_KEY && t[h] != acts[i].gva) h = (h + 1) & (sz - 1);
+    t[h] = acts[i].gva;
+    a[h] = acts[i];
+  }
+  if (dalloc(&c->d_actkeys, sz) || dalloc(&c->d_act, sz)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemcpyAsync(c->d_actkeys, t.data(), sz * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_act, a.data(), sz * sizeof(wtfgpu_bp_action_t), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->P.act_keys = c->d_actkeys;
+  c->P.act = c->d_act;
+  c->P.act_mask = sz - 1;
   return WTFGPU_OK;
 }
 

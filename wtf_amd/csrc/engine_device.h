@@ -79,6 +79,10 @@ struct Dev {
   // breakpoints (open addressing, EMPTY_KEY)
   const u64 *bp_keys;
   u32 bp_mask;           // table size - 1; 0 with bp_keys==nullptr = none
+  // device-side breakpoint actions (own hash table, looked up on a hit only)
+  const u64 *act_keys;
+  const wtfgpu_bp_action_t *act;
+  u32 act_mask;
   // coverage
   const u64 *code_keys;  // vpn hash table
   const u32 *code_slot;

@@ -162,6 +162,25 @@ bool GpuBackend_t::SetBreakpoint(const Gva_t Gva, const BreakpointHandler_t Hand
   return wtfgpu_set_breakpoints(ctx_, v.data(), (uint32_t)v.size()) == WTFGPU_OK;
 }
 
+bool GpuBackend_t::SetBreakpoint(const Gva_t Gva, const BreakpointHandler_t Handler,
+                                 const BreakpointAction_t &Action) {
+  if (!SetBreakpoint(Gva, Handler)) return false;
+  const char *Env = getenv("WTFGPU_DEVICE_BP_ACTIONS");
+  if (Action.Kind == BreakpointAction_t::Kind_t::Host || (Env && Env[0] == '0')) return true;
+  wtfgpu_bp_action_t A;
+  memset(&A, 0, sizeof(A));
+  A.gva = Gva.U64();
+  if (Action.Kind == BreakpointAction_t::Kind_t::SimulateReturn) {
+    A.kind = WTFGPU_BPACT_RETURN;
+    A.value = Action.Return;
+  } else {
+    A.kind = WTFGPU_BPACT_SET_GPRS;
+    memcpy(A.gprs, Action.Gprs, sizeof(A.gprs));
+  }
+  bp_actions_.push_back(A);
+  return wtfgpu_set_breakpoint_actions(ctx_, bp_actions_.data(), (uint32_t)bp_actions_.size()) == WTFGPU_OK;
+}
+
 // Writes go to lane overlays, which the device dirties by itself.
 bool GpuBackend_t::DirtyGpa(const Gpa_t) { return true; }
 

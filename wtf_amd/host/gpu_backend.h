@@ -58,6 +58,9 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   uint64_t Rdrand() override;
   void PrintRunStats() override;
   bool SetBreakpoint(const Gva_t Gva, const BreakpointHandler_t Handler) override;
+  // also declares the handler's device-side action (wtfgpu_set_breakpoint_actions);
+  // WTFGPU_DEVICE_BP_ACTIONS=0 in the environment keeps every hit on the host
+  bool SetBreakpoint(const Gva_t Gva, const BreakpointHandler_t Handler, const BreakpointAction_t &Action) override;
   bool DirtyGpa(const Gpa_t Gpa) override;
   bool VirtTranslate(const Gva_t Gva, Gpa_t &Gpa, const MemoryValidate_t Validate) const override;
   uint8_t *PhysTranslate(const Gpa_t Gpa) const override;
@@ -150,6 +153,7 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   // several threads when the module state is thread_local, module_slots.h)
   static thread_local uint32_t cur_;
   std::unordered_map<uint64_t, BreakpointHandler_t> breakpoints_;
+  std::vector<wtfgpu_bp_action_t> bp_actions_;  // device-side equivalents of some handlers
   std::unordered_set<uint64_t> aggregate_;
   std::unordered_set<Gva_t> last_new_coverage_;
   mutable BatchStats stats_;

@@ -50,7 +50,8 @@ bool Init(const Options_t &, const CpuState_t &) {
         const std::string Format = Backend->VirtReadString(FormatPtr);
         (void)Format;
         Backend->SimulateReturnFromFunction(0);
-      }))
+      },
+      BreakpointAction_t::SimulateReturn(0)))  // device-side on the gpu backend
     return false;
   const Gva_t ExGenRandom = Gva_t(g_Dbg.GetSymbol("nt!ExGenRandom") + 0xe0 + 4);
   if (g_Backend->VirtRead4(ExGenRandom - Gva_t(4)) != 0xf2c70f48) {

@@ -10,6 +10,8 @@
 //  * return-address breakpoint (:171-179): registers back to the snapshot's
 //    so the receive loop calls ProcessPacket again;
 //  * printf breakpoint (:184-189): skipped (return 0);
+//  * the return-address and printf handlers are also declared as data
+//    (BreakpointAction_t): the gpu backend applies them on the device;
 //  * user-mode crash detection (:191-194);
 //  * the custom mutator (:204-365): Generate 1..10 packets one time in five,
 //    otherwise insert / copy-field / delete on a corpus testcase.
@@ -118,7 +120,11 @@ bool Init(const Options_t &, const CpuState_t &State) {
   GlobalState.Context = State;
   const Gva_t ReturnAddress = Gva_t(g_Backend->VirtRead8(Gva_t(g_Backend->Rsp())));
   if (!g_Backend->SetBreakpoint("tlv_server!ProcessPacket", OnProcessPacket)) return false;
-  if (!g_Backend->SetBreakpoint(ReturnAddress, [](Backend_t *) { GlobalState.RestoreGprs(g_Backend); })) {
+  // both handlers below only move registers: their BreakpointAction_t lets the
+  // gpu backend apply them on the device (no host round trip per packet)
+  if (!g_Backend->SetBreakpoint(
+          ReturnAddress, [](Backend_t *) { GlobalState.RestoreGprs(g_Backend); },
+          BreakpointAction_t::SetGprs(State))) {
     printf("Failed to SetBreakpoint on the return address.\n");
     return false;
   }
@@ -126,7 +132,8 @@ bool Init(const Options_t &, const CpuState_t &State) {
         const std::string Format = Backend->VirtReadString(Backend->GetArgGva(0));
         (void)Format;
         Backend->SimulateReturnFromFunction(0);
-      })) {
+      },
+      BreakpointAction_t::SimulateReturn(0))) {
     printf("Failed to SetBreakpoint on printf\n");
     return false;
   }

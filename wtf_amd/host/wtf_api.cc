@@ -167,6 +167,23 @@ bool Backend_t::SetBreakpoint(const char *Symbol, const BreakpointHandler_t Hand
   }
   return SetBreakpoint(Gva, Handler);
 }
+bool Backend_t::SetBreakpoint(const char *Symbol, const BreakpointHandler_t Handler,
+                              const BreakpointAction_t &Action) {
+  const Gva_t Gva = Gva_t(g_Dbg.GetSymbol(Symbol));
+  if (Gva == Gva_t(0)) {
+    printf("Could not set a breakpoint at %s.\n", Symbol);
+    return false;
+  }
+  return SetBreakpoint(Gva, Handler, Action);
+}
+BreakpointAction_t BreakpointAction_t::SetGprs(const CpuState_t &C) {
+  BreakpointAction_t A;
+  A.Kind = Kind_t::SetGprs;
+  const uint64_t G[17] = {C.Rax, C.Rcx, C.Rdx, C.Rbx, C.Rsp, C.Rbp, C.Rsi, C.Rdi, C.R8,
+                          C.R9,  C.R10, C.R11, C.R12, C.R13, C.R14, C.R15, C.Rip};
+  for (int i = 0; i < 17; i++) A.Gprs[i] = G[i];
+  return A;
+}
 bool Backend_t::SetCrashBreakpoint(const Gva_t Gva) {
   return SetBreakpoint(Gva, [](Backend_t *B) { B->Stop(Crash_t()); });
 }

@@ -198,6 +198,28 @@ struct Options_t {
 class Backend_t;
 using BreakpointHandler_t = void (*)(Backend_t *);
 
+// What a breakpoint handler does, stated as data (this repository's
+// extension; the reference only has the handler). A backend that can apply it
+// without leaving the execution engine (the gpu backend does it on the device,
+// wtfgpu_set_breakpoint_actions) may do so instead of calling the handler; any
+// other backend calls the handler. The module guarantees the two are the same
+// register effect; the GPU-vs-twin parity tests check it testcase by testcase.
+struct BreakpointAction_t {
+  enum class Kind_t { Host, SimulateReturn, SetGprs };
+  Kind_t Kind = Kind_t::Host;
+  uint64_t Return = 0;  // SimulateReturn: SimulateReturnFromFunction(Return)
+  uint64_t Gprs[17] = {};  // SetGprs: rax, rcx, rdx, rbx, rsp, rbp, rsi, rdi, r8..r15, rip
+
+  static BreakpointAction_t SimulateReturn(const uint64_t Value) {
+    BreakpointAction_t A;
+    A.Kind = Kind_t::SimulateReturn;
+    A.Return = Value;
+    return A;
+  }
+  // the 16 GPRs and rip of a CpuState_t (registers only; rflags untouched)
+  static BreakpointAction_t SetGprs(const struct CpuState_t &State);
+};
+
 class Backend_t {
  public:
   virtual ~Backend_t() = default;
@@ -230,6 +252,12 @@ class Backend_t {
   // helpers implemented on top of the virtuals (backend.cc)
   bool SaveCrash(const Gva_t ExceptionAddress, const uint32_t ExceptionCode);
   bool SetBreakpoint(const char *Symbol, const BreakpointHandler_t Handler);
+  // Handler + its data-form equivalent (BreakpointAction_t). Default: the
+  // action is ignored and the handler is the breakpoint.
+  virtual bool SetBreakpoint(const Gva_t Gva, const BreakpointHandler_t Handler, const BreakpointAction_t &) {
+    return SetBreakpoint(Gva, Handler);
+  }
+  bool SetBreakpoint(const char *Symbol, const BreakpointHandler_t Handler, const BreakpointAction_t &Action);
   bool SetCrashBreakpoint(const char *Symbol);
   bool SetCrashBreakpoint(const Gva_t Gva);
   bool PhysWrite(const Gpa_t Gpa, const uint8_t *Buffer, const uint64_t BufferSize, const bool Dirty = false);
