@@ -45,6 +45,17 @@ def test_tlv_full_coverage_parity(target, tmp_path):
     assert not any(r["error"] for r in g)
 
 
+def test_tlv_parity_host_handlers_only(target, tmp_path):
+    """The return-address and printf breakpoints carry device-side actions
+    (BreakpointAction_t); with them switched off every hit goes through the
+    host handler. Both paths must match the twin, and each other."""
+    inp = os.path.join(target, "parity")
+    h = H.run(H.WTFGPU, target, inp, str(tmp_path / "h.jsonl"), lanes=512,
+              env={"WTFGPU_DEVICE_BP_ACTIONS": "0"})
+    t = H.run(H.TWIN, target, inp, str(tmp_path / "t.jsonl"), lanes=512)
+    assert not _diff(h, t)
+
+
 def test_tlv_lane_order_coverage_attribution(target, tmp_path):
     """Without --full-coverage each lane reports only coverage no earlier lane
     (or batch) found: the order-dependent LastNewCoverage of the serial client."""

@@ -26,12 +26,13 @@ def build_target(d: str) -> str:
 
 
 def run(exe: str, target: str, inputs: str, results: str, lanes: int, limit: int = 100000,
-        full_coverage: bool = True, timeout: int = 300, extra=(), name: str = "tlv_server") -> list[dict]:
+        full_coverage: bool = True, timeout: int = 300, extra=(), name: str = "tlv_server",
+        env: dict | None = None) -> list[dict]:
     cmd = [exe, "run", "--name", name, "--target", target, "--input", inputs, "--results", results,
            "--lanes", str(lanes), "--limit", str(limit), *extra]
     if full_coverage:
         cmd.append("--full-coverage")
-    subprocess.run(cmd, check=True, timeout=timeout)
+    subprocess.run(cmd, check=True, timeout=timeout, env=None if env is None else {**os.environ, **env})
     with open(results) as f:
         return [json.loads(line) for line in f]
 
