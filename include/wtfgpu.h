@@ -66,7 +66,9 @@ enum wtfgpu_status {
   WTFGPU_EXIT_CR3 = 7,        /* cr3 write != initial cr3 (bochscpu_backend.cc:628-657) */
   WTFGPU_EXIT_OVERLAY_FULL = 8, /* lane ran out of copy-on-write pages */
   WTFGPU_EXIT_STOPPED = 9,    /* host called Stop(); result kept on the host */
-  WTFGPU_EXIT_IDLE = 10       /* lane holds no testcase */
+  WTFGPU_EXIT_IDLE = 10,      /* lane holds no testcase */
+  WTFGPU_EXIT_STOP_OK = 11,   /* a device FEED action found the lane's feed drained: Stop(Ok_t()) */
+  WTFGPU_EXIT_FEED_FAULT = 12 /* a device FEED action could not write its chunk (engine error) */
 };
 
 /* x86 exception vectors reported in wtfgpu_exit_t.vector. */
@@ -175,6 +177,13 @@ enum wtfgpu_bp_action_kind {
   WTFGPU_BPACT_HOST = 0,           /* exit to the host (default) */
   WTFGPU_BPACT_RETURN = 1,         /* rax = value; rip = [rsp]; rsp += 8 */
   WTFGPU_BPACT_SET_GPRS = 2,       /* gprs[0..15] (WTFGPU_RAX order), rip = gprs[16] */
+  /* Pop the lane's next feed chunk (wtfgpu_set_feed): none left, or a chunk of
+   * `value` bytes or more -> the lane stops with WTFGPU_EXIT_STOP_OK; else the
+   * chunk is written (dirty) so that it ends at gpr[b] + value, then gpr[b] =
+   * its address and gpr[n] = its size, b = gprs[0], n = gprs[1]; rip is kept
+   * and the hooked instruction runs (fuzzer_tlv_server.cc:83-166). A lane
+   * without a feed exits to the host handler. */
+  WTFGPU_BPACT_FEED = 3,
 };
 typedef struct wtfgpu_bp_action {
   uint64_t gva;
@@ -184,6 +193,14 @@ typedef struct wtfgpu_bp_action {
   uint64_t gprs[17];
 } wtfgpu_bp_action_t;
 int wtfgpu_set_breakpoint_actions(wtfgpu_ctx *ctx, const wtfgpu_bp_action_t *acts, uint32_t n);
+/* Per-lane input feed of lanes [first, first+count): lane first+i owns
+ * bytes[offsets[i] .. offsets[i+1]) (count+1 non-decreasing offsets), a
+ * sequence of chunks each stored as a little-endian u32 size and that many
+ * bytes. has_feed[i] == 0 means "no feed" for that lane: its FEED hits go to
+ * the host (has_feed NULL = every lane has one). The bytes replace any earlier
+ * feed of the context; wtfgpu_restore leaves the feed in place. */
+int wtfgpu_set_feed(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, const uint64_t *offsets,
+                    const uint8_t *has_feed, const uint8_t *bytes, uint64_t nbytes);
 
 /* Coverage index space: code pages (gva >> 12) that get a 4096-byte slot in
  * the per-GPU coverage map. Pages outside it are still logged per lane. */

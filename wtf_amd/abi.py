@@ -15,7 +15,7 @@ HOST_LIB_PATH = os.path.join(HERE, "host", "libwtf_host.so")
 RUNNING, EXIT_BREAKPOINT, EXIT_TIMEOUT, EXIT_INT3, EXIT_HLT, EXIT_FAULT, EXIT_UNIMPLEMENTED, \
     EXIT_CR3, EXIT_OVERLAY_FULL, EXIT_STOPPED, EXIT_IDLE = range(11)
 STATUS_NAMES = ["running", "breakpoint", "timeout", "int3", "hlt", "fault", "unimplemented",
-                "cr3", "overlay_full", "stopped", "idle"]
+                "cr3", "overlay_full", "stopped", "idle", "stop_ok", "feed_fault"]
 
 
 class Seg(C.Structure):
@@ -59,7 +59,7 @@ class BpAction(C.Structure):
                 ("value", C.c_uint64), ("gprs", C.c_uint64 * 17)]
 
 
-BPACT_HOST, BPACT_RETURN, BPACT_SET_GPRS = 0, 1, 2
+BPACT_HOST, BPACT_RETURN, BPACT_SET_GPRS, BPACT_FEED = 0, 1, 2, 3
 
 
 class Write(C.Structure):
@@ -113,6 +113,7 @@ def load_hip_library(path: str = LIB_PATH) -> C.CDLL:
         "wtfgpu_set_limit": ([P, U64], C.c_int),
         "wtfgpu_set_breakpoints": ([P, C.POINTER(U64), U32], C.c_int),
         "wtfgpu_set_breakpoint_actions": ([P, C.POINTER(BpAction), U32], C.c_int),
+        "wtfgpu_set_feed": ([P, U32, U32, C.POINTER(U64), C.c_char_p, C.c_char_p, U64], C.c_int),
         "wtfgpu_set_code_pages": ([P, C.POINTER(U64), U32], C.c_int),
         "wtfgpu_restore": ([P, U32, U32], C.c_int),
         "wtfgpu_read_regs": ([P, U32, U32, C.POINTER(Regs)], C.c_int),

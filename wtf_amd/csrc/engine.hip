@@ -415,6 +415,54 @@ __device__ __forceinline__ void retire(const Dev &P, Lane &L, int x, u32 len, u6
   }
 }
 
+// FEED action: the next chunk of the lane's feed goes to gpr[b] + window -
+// size, as fuzzer_tlv_server.cc:83-166 writes the next packet. Writes go
+// through the copy-on-write path (the pages are dirtied as VirtWriteDirty
+// does); 8-byte stores, then single bytes.
+__device__ __noinline__ bool feed_apply(const Dev &P, Lane &L, const wtfgpu_bp_action_t &a) {
+  if (!P.feed_pos) return false;
+  const u64 pos = P.feed_pos[L.lane];
+  if (pos == ~0ull) return false;  // no feed: the host handler serves the lane
+  const u64 end = P.feed_end[L.lane];
+  if (pos + 4 > end) {
+    L.status = WTFGPU_EXIT_STOP_OK;
+    return true;
+  }
+  const u8 *src = P.feed_data + pos;
+  const u32 n = (u32)src[0] | ((u32)src[1] << 8) | ((u32)src[2] << 16) | ((u32)src[3] << 24);
+  P.feed_pos[L.lane] = pos + 4 + n;
+  if (n >= a.value || pos + 4 + n > end) {
+    L.status = WTFGPU_EXIT_STOP_OK;
+    return true;
+  }
+  const u32 rb = (u32)a.gprs[0] & 15, rn = (u32)a.gprs[1] & 15;
+  const u64 dst = R(L, rb) + a.value - n;
+  for (u32 o = 0; o < n;) {
+    const u32 sz = n - o >= 8 ? 8 : 1;
+    u64 v = 0;
+    for (u32 i = 0; i < sz; i++) v |= (u64)src[4 + o + i] << (8 * i);
+    for (int attempt = 0;; attempt++) {
+      L.miss = 0;
+      if (vwrite(L, dst + o, sz, v)) break;
+      if (L.status != WTFGPU_RUNNING || !L.miss || !miss_service(P, L, attempt)) {
+        if (L.status == WTFGPU_RUNNING || L.status == WTFGPU_EXIT_FAULT) L.status = WTFGPU_EXIT_FEED_FAULT;
+        L.miss = 0;
+        L.pend = 0;
+        return true;
+      }
+    }
+    o += sz;
+  }
+  L.pend = 0;
+  if (L.flush) {
+    tlb_flush(L);
+    L.flush = 0;
+  }
+  RS(L, rn, n);
+  RS(L, rb, dst);
+  return true;
+}
+
 // Device-side breakpoint action (wtfgpu_set_breakpoint_actions) at `grip`.
 // true = applied, the lane keeps running at its new rip; false = none
 // declared or it could not be applied: the lane exits to the host handler,
@@ -430,6 +478,7 @@ __device__ __noinline__ bool bp_apply(const Dev &P, Lane &L, u64 grip) {
     L.rip = a.gprs[16];
     return true;
   }
+  if (a.kind == WTFGPU_BPACT_FEED) return feed_apply(P, L, a);
   if (a.kind != WTFGPU_BPACT_RETURN) return false;
   const u64 rsp = R(L, WTFGPU_RSP);
   u64 ra = 0;
@@ -1131,6 +1180,9 @@ struct wtfgpu_ctx {
   u64 *d_bp = nullptr;
   u64 *d_actkeys = nullptr;
   wtfgpu_bp_action_t *d_act = nullptr;
+  u64 *d_feedpos = nullptr, *d_feedend = nullptr;
+  u8 *d_feeddata = nullptr;
+  u64 feed_cap = 0;
   // coverage
   u64 *d_codekeys = nullptr;
   u32 *d_codeslot = nullptr;
@@ -1272,6 +1324,11 @@ int wtfgpu_create(int device, wtfgpu_ctx **out) {
 void *wtfgpu_stream(wtfgpu_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
 static void free_lanes(wtfgpu_ctx *c) {
+  dfree(c->d_feedpos);  // sized by the lane count
+  dfree(c->d_feedend);
+  c->d_feedpos = c->d_feedend = nullptr;
+  c->P.feed_pos = nullptr;
+  c->P.feed_end = nullptr;
   dfree(c->d_gpr);
   dfree(c->d_rip);
   dfree(c->d_rflags);
@@ -1305,6 +1362,9 @@ int wtfgpu_destroy(wtfgpu_ctx *c) {
   dfree(c->d_bp);
   dfree(c->d_actkeys);
   dfree(c->d_act);
+  dfree(c->d_feedpos);
+  dfree(c->d_feedend);
+  dfree(c->d_feeddata);
   dfree(c->d_codekeys);
   dfree(c->d_codeslot);
   dfree(c->d_covmap);
@@ -1530,7 +1590,7 @@ int wtfgpu_set_breakpoints(wtfgpu_ctx *c, const uint64_t *gvas, uint32_t n) {
 int wtfgpu_set_breakpoint_actions(wtfgpu_ctx *c, const wtfgpu_bp_action_t *acts, uint32_t n) {
   if (!c || (n && !acts)) return WTFGPU_ERR_INVALID;
   for (u32 i = 0; i < n; i++)
-    if (acts[i].kind > WTFGPU_BPACT_SET_GPRS || acts[i].gva == EMPTY_KEY) return WTFGPU_ERR_INVALID;
+    if (acts[i].kind > WTFGPU_BPACT_FEED || acts[i].gva == EMPTY_KEY) return WTFGPU_ERR_INVALID;
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   dfree(c->d_actkeys);
@@ -1556,6 +1616,43 @@ int wtfgpu_set_breakpoint_actions(wtfgpu_ctx *c, const wtfgpu_bp_action_t *acts,
   c->P.act_keys = c->d_actkeys;
   c->P.act = c->d_act;
   c->P.act_mask = sz - 1;
+  return WTFGPU_OK;
+}
+
+int wtfgpu_set_feed(wtfgpu_ctx *c, uint32_t first, uint32_t count, const uint64_t *offsets, const uint8_t *has_feed,
+                    const uint8_t *bytes, uint64_t nbytes) {
+  if (!lanes_ok(c, first, count) || !offsets || (nbytes && !bytes)) return WTFGPU_ERR_INVALID;
+  for (u32 i = 0; i < count; i++)
+    if (offsets[i + 1] < offsets[i] || offsets[i + 1] > nbytes) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const u64 N = c->P.nlanes;
+  if (!c->d_feedpos) {
+    if (dalloc(&c->d_feedpos, N) || dalloc(&c->d_feedend, N)) return WTFGPU_ERR_OOM;
+    std::vector<u64> none(N, ~0ull);
+    HIPCHK(hipMemcpy(c->d_feedpos, none.data(), N * 8, hipMemcpyHostToDevice));
+  }
+  // the data of one call is the whole feed (earlier feeds are replaced)
+  if (nbytes > c->feed_cap) {
+    dfree(c->d_feeddata);
+    c->d_feeddata = nullptr;
+    c->feed_cap = 0;
+    if (dalloc(&c->d_feeddata, nbytes)) return WTFGPU_ERR_OOM;
+    c->feed_cap = nbytes;
+  }
+  std::vector<u64> pos(count), end(count);
+  for (u32 i = 0; i < count; i++) {
+    const bool has = !has_feed || has_feed[i];
+    pos[i] = has ? offsets[i] : ~0ull;
+    end[i] = offsets[i + 1];
+  }
+  if (nbytes) HIPCHK(hipMemcpyAsync(c->d_feeddata, bytes, nbytes, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_feedpos + first, pos.data(), count * 8ull, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_feedend + first, end.data(), count * 8ull, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->P.feed_pos = c->d_feedpos;
+  c->P.feed_end = c->d_feedend;
+  c->P.feed_data = c->d_feeddata;
   return WTFGPU_OK;
 }
 

@@ -83,6 +83,10 @@ struct Dev {
   const u64 *act_keys;
   const wtfgpu_bp_action_t *act;
   u32 act_mask;
+  // per-lane input feed for WTFGPU_BPACT_FEED: cursor / end into feed_data
+  u64 *feed_pos;         // [nlanes], ~0 = no feed
+  const u64 *feed_end;   // [nlanes]
+  const u8 *feed_data;
   // coverage
   const u64 *code_keys;  // vpn hash table
   const u32 *code_slot;

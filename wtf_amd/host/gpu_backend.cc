@@ -106,6 +106,8 @@ void GpuBackend_t::reset_view(uint32_t lane) {
   v.regs_dirty = false;
   v.result.reset();
   v.seed = initial_.Seed;  // Rdrand seed (bochscpu_backend.cc:1030)
+  v.has_feed = false;
+  v.feed.clear();
   v.dirty_known = true;    // a restored lane has an empty overlay
   v.dirty.clear();
   v.wlog.clear();
@@ -173,12 +175,45 @@ bool GpuBackend_t::SetBreakpoint(const Gva_t Gva, const BreakpointHandler_t Hand
   if (Action.Kind == BreakpointAction_t::Kind_t::SimulateReturn) {
     A.kind = WTFGPU_BPACT_RETURN;
     A.value = Action.Return;
+  } else if (Action.Kind == BreakpointAction_t::Kind_t::Feed) {
+    A.kind = WTFGPU_BPACT_FEED;
+    A.value = Action.Return;
+    A.gprs[0] = (uint64_t)gpr_index((Registers_t)Action.Gprs[0]);
+    A.gprs[1] = (uint64_t)gpr_index((Registers_t)Action.Gprs[1]);
+    feed_action_ = true;
   } else {
     A.kind = WTFGPU_BPACT_SET_GPRS;
     memcpy(A.gprs, Action.Gprs, sizeof(A.gprs));
   }
   bp_actions_.push_back(A);
   return wtfgpu_set_breakpoint_actions(ctx_, bp_actions_.data(), (uint32_t)bp_actions_.size()) == WTFGPU_OK;
+}
+
+bool GpuBackend_t::SetFeed(const uint8_t *Data, const uint64_t Size) {
+  if (!feed_action_) return false;
+  LaneView &v = cur();
+  v.has_feed = true;
+  v.feed.assign(Data, Data + Size);
+  return true;
+}
+
+// One wtfgpu_set_feed call for lanes [0, n); lanes without SetFeed keep the
+// host handler.
+int GpuBackend_t::upload_feed(uint32_t n) {
+  if (!feed_action_ || n == 0) return WTFGPU_OK;
+  std::vector<uint64_t> off(n + 1);
+  std::vector<uint8_t> has(n);
+  uint64_t total = 0;
+  for (uint32_t l = 0; l < n; l++) total += views_[l].feed.size();
+  std::vector<uint8_t> bytes;
+  bytes.reserve(total);
+  for (uint32_t l = 0; l < n; l++) {
+    off[l] = bytes.size();
+    has[l] = views_[l].has_feed;
+    bytes.insert(bytes.end(), views_[l].feed.begin(), views_[l].feed.end());
+  }
+  off[n] = bytes.size();
+  return wtfgpu_set_feed(ctx_, 0, n, off.data(), has.data(), bytes.data(), bytes.size());
 }
 
 // Writes go to lane overlays, which the device dirties by itself.
@@ -556,6 +591,7 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
         case WTFGPU_EXIT_CR3: v.result = Cr3Change_t(); break;         // :628-657
         case WTFGPU_EXIT_FAULT: v.result = FaultToResult(e.vector, e.error, e.rip, e.addr, e.opcode); break;
         case WTFGPU_EXIT_STOPPED: break;
+        case WTFGPU_EXIT_STOP_OK: v.result = Ok_t(); break;           // device Feed action: Stop(Ok_t())
         default:  // unimplemented opcode / overlay full: the engine cannot finish it
           if (out) (*out)[l].error = true;
           if (!v.result) v.result = Crash_t("engine-" + std::to_string(e.status));
@@ -820,7 +856,7 @@ void GpuBackend_t::finish_coverage(uint32_t n, std::vector<LaneResult> *out, std
 std::optional<TestcaseResult_t> GpuBackend_t::Run(const uint8_t *, const uint64_t) {
   const auto t0 = Clock::now();
   cur_ = 0;
-  if (flush_lanes({0})) return std::nullopt;
+  if (flush_lanes({0}) || upload_feed(1)) return std::nullopt;
   std::vector<LaneResult> out(1);
   if (!run_lanes({0}, &out, nullptr, false)) return std::nullopt;
   std::vector<uint32_t> to;
@@ -867,7 +903,7 @@ bool GpuBackend_t::RunBatch(const Target_t &Target, const std::vector<std::pair<
     lanes[l] = l;
     if (!insert_ok[l]) views_[l].result = Crash_t("insert-testcase-failed");
   }
-  if (flush_lanes(lanes)) return false;
+  if (flush_lanes(lanes) || upload_feed(n)) return false;
   stats_.insert_ms += ms_since(t0);
   if (!run_lanes(lanes, &Out, Slots, Slots != nullptr)) return false;
   const auto tc = Clock::now();

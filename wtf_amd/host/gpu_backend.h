@@ -67,6 +67,7 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   bool PageFaultsMemoryIfNeeded(const Gva_t Gva, const uint64_t Size) override;
   bool PhysWriteDirect(const Gpa_t Gpa, const uint8_t *Buffer, const uint64_t Size) override;
   bool PhysReadDirect(const Gpa_t Gpa, uint8_t *Buffer, const uint64_t Size) const override;
+  bool SetFeed(const uint8_t *Data, const uint64_t Size) override;
   const std::unordered_set<Gva_t> &LastNewCoverage() const override;
   bool RevokeLastNewCoverage() override;
   using Backend_t::SetBreakpoint;
@@ -102,6 +103,8 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
     std::optional<TestcaseResult_t> result;
     uint64_t seed = 0;
     uint64_t inject = ~0ull;  // PageFaultsMemoryIfNeeded: page to #PF after the handler
+    bool has_feed = false;    // SetFeed: chunks for the device Feed action
+    std::vector<uint8_t> feed;
     bool dirty_known = false;
     std::vector<uint32_t> dirty;  // gpfns the lane's overlay holds
     std::vector<Staged> pages;    // staged pages (few per lane: linear search)
@@ -154,6 +157,8 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   static thread_local uint32_t cur_;
   std::unordered_map<uint64_t, BreakpointHandler_t> breakpoints_;
   std::vector<wtfgpu_bp_action_t> bp_actions_;  // device-side equivalents of some handlers
+  bool feed_action_ = false;                     // a Feed action is on the device
+  int upload_feed(uint32_t n);                   // lanes [0, n)
   std::unordered_set<uint64_t> aggregate_;
   std::unordered_set<Gva_t> last_new_coverage_;
   mutable BatchStats stats_;

@@ -10,8 +10,9 @@
 //  * return-address breakpoint (:171-179): registers back to the snapshot's
 //    so the receive loop calls ProcessPacket again;
 //  * printf breakpoint (:184-189): skipped (return 0);
-//  * the return-address and printf handlers are also declared as data
-//    (BreakpointAction_t): the gpu backend applies them on the device;
+//  * the three handlers are also declared as data (BreakpointAction_t; the
+//    packets as Feed chunks at insert): the gpu backend applies them on the
+//    device, other backends run the handlers;
 //  * user-mode crash detection (:191-194);
 //  * the custom mutator (:204-365): Generate 1..10 packets one time in five,
 //    otherwise insert / copy-field / delete on a corpus testcase.
@@ -89,6 +90,22 @@ bool InsertTestcase(const uint8_t *Buffer, const size_t BufferSize) {
   GlobalState.Packets.clear();
   std::vector<Packet_t> Packets;
   if (!Deserialize(Buffer, BufferSize, Packets)) return false;
+  // the same packets as Feed chunks (Command, Id, BodySize, Body: the bytes
+  // OnProcessPacket writes); a backend that takes them serves ProcessPacket
+  // itself, the deque then stays unused
+  std::vector<uint8_t> Feed;
+  for (const Packet_t &P : Packets) {
+    const uint32_t Size = uint32_t(sizeof(P.Command) + sizeof(P.Id) + sizeof(P.BodySize) + P.Body.size());
+    const size_t At = Feed.size();
+    Feed.resize(At + 4 + Size);
+    uint8_t *Q = Feed.data() + At;
+    memcpy(Q, &Size, 4);
+    memcpy(Q + 4, &P.Command, 4);
+    memcpy(Q + 8, &P.Id, 2);
+    memcpy(Q + 10, &P.BodySize, 2);
+    if (!P.Body.empty()) memcpy(Q + 12, P.Body.data(), P.Body.size());
+  }
+  g_Backend->SetFeed(Feed.data(), Feed.size());
   for (Packet_t &P : Packets) GlobalState.Packets.emplace_back(std::move(P));
   return true;
 }
@@ -119,7 +136,9 @@ void OnProcessPacket(Backend_t *Backend) {
 bool Init(const Options_t &, const CpuState_t &State) {
   GlobalState.Context = State;
   const Gva_t ReturnAddress = Gva_t(g_Backend->VirtRead8(Gva_t(g_Backend->Rsp())));
-  if (!g_Backend->SetBreakpoint("tlv_server!ProcessPacket", OnProcessPacket)) return false;
+  if (!g_Backend->SetBreakpoint("tlv_server!ProcessPacket", OnProcessPacket,
+                                BreakpointAction_t::Feed(Registers_t::Rcx, Registers_t::Rdx, 0x1000)))
+    return false;
   // both handlers below only move registers: their BreakpointAction_t lets the
   // gpu backend apply them on the device (no host round trip per packet)
   if (!g_Backend->SetBreakpoint(

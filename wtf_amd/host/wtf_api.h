@@ -205,7 +205,7 @@ using BreakpointHandler_t = void (*)(Backend_t *);
 // other backend calls the handler. The module guarantees the two are the same
 // register effect; the GPU-vs-twin parity tests check it testcase by testcase.
 struct BreakpointAction_t {
-  enum class Kind_t { Host, SimulateReturn, SetGprs };
+  enum class Kind_t { Host, SimulateReturn, SetGprs, Feed };
   Kind_t Kind = Kind_t::Host;
   uint64_t Return = 0;  // SimulateReturn: SimulateReturnFromFunction(Return)
   uint64_t Gprs[17] = {};  // SetGprs: rax, rcx, rdx, rbx, rsp, rbp, rsi, rdi, r8..r15, rip
@@ -218,6 +218,19 @@ struct BreakpointAction_t {
   }
   // the 16 GPRs and rip of a CpuState_t (registers only; rflags untouched)
   static BreakpointAction_t SetGprs(const struct CpuState_t &State);
+  // pop the testcase's next input chunk (Backend_t::SetFeed): none left, or
+  // Size >= Window -> Stop(Ok_t()); else write it so that it ends at
+  // Base + Window (dirty), Base = its address, Len = its size; the hooked
+  // instruction then runs (Gprs[0] / Gprs[1] hold the two Registers_t)
+  static BreakpointAction_t Feed(const Registers_t Base, const Registers_t Len,
+                                 const uint64_t Window) {
+    BreakpointAction_t A;
+    A.Kind = Kind_t::Feed;
+    A.Return = Window;
+    A.Gprs[0] = (uint64_t)Base;
+    A.Gprs[1] = (uint64_t)Len;
+    return A;
+  }
 };
 
 class Backend_t {
@@ -248,6 +261,10 @@ class Backend_t {
   // without materialising the page. false = not handled, use PhysTranslate.
   virtual bool PhysWriteDirect(const Gpa_t, const uint8_t *, const uint64_t) { return false; }
   virtual bool PhysReadDirect(const Gpa_t, uint8_t *, const uint64_t) const { return false; }
+  // The current testcase's input chunks for a Feed breakpoint action, as
+  // (u32 little-endian size, bytes) records. true = the backend serves that
+  // breakpoint from them; false (default) = its handler runs.
+  virtual bool SetFeed(const uint8_t *, const uint64_t) { return false; }
 
   // helpers implemented on top of the virtuals (backend.cc)
   bool SaveCrash(const Gva_t ExceptionAddress, const uint32_t ExceptionCode);
