@@ -41,6 +41,17 @@ def test_hevd_full_coverage_parity(target, tmp_path):
     assert not any(r["error"] for r in g)
 
 
+def test_hevd_parity_host_handlers_only(target, tmp_path):
+    """nt!DbgPrintEx carries a device-side SimulateReturn action; with device
+    actions off every hit is a host handler. Both must match the twin."""
+    inp = os.path.join(target, "parity")
+    h = H.run(H.WTFGPU, target, inp, str(tmp_path / "h.jsonl"), lanes=512, name="hevd",
+              env={"WTFGPU_DEVICE_BP_ACTIONS": "0"})
+    t = H.run(H.TWIN, target, inp, str(tmp_path / "t.jsonl"), lanes=512, name="hevd")
+    bad = [(x["input"], k) for x, y in zip(h, t) for k in FIELDS if x[k] != y[k]]
+    assert len(h) == len(t) and not bad, bad[:10]
+
+
 def test_hevd_fuzz_smoke(target):
     st = H.fuzz(H.WTFGPU, target, runs=8192, lanes=4096, name="hevd", max_len=1028)
     assert st["execs"] == 8192 and st["errors"] == 0

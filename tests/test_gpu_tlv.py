@@ -46,9 +46,10 @@ def test_tlv_full_coverage_parity(target, tmp_path):
 
 
 def test_tlv_parity_host_handlers_only(target, tmp_path):
-    """The return-address and printf breakpoints carry device-side actions
-    (BreakpointAction_t); with them switched off every hit goes through the
-    host handler. Both paths must match the twin, and each other."""
+    """ProcessPacket (Feed), the return address (SetGprs) and printf
+    (SimulateReturn) carry device-side actions (BreakpointAction_t); with them
+    switched off every hit goes through the host handler. Both paths must
+    match the twin."""
     inp = os.path.join(target, "parity")
     h = H.run(H.WTFGPU, target, inp, str(tmp_path / "h.jsonl"), lanes=512,
               env={"WTFGPU_DEVICE_BP_ACTIONS": "0"})
