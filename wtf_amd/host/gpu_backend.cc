@@ -873,7 +873,8 @@ bool GpuBackend_t::RunBatch(const Target_t &Target, const std::vector<std::pair<
   const uint32_t n = (uint32_t)Testcases.size();
   if (n == 0 || n > nlanes_) return false;
   Out.assign(n, LaneResult{});
-  if (Slots) Slots->ResetAll();
+  // module state: each lane is reset right before its InsertTestcase, inside
+  // the (parallel) insert loop (ModuleSlots::ResetLane)
   if (wtfgpu_restore(ctx_, 0, n)) return false;
   for (uint32_t l = 0; l < n; l++) reset_view(l);
   // InsertTestcase per lane (client.cc:102), module state per lane
@@ -882,7 +883,10 @@ bool GpuBackend_t::RunBatch(const Target_t &Target, const std::vector<std::pair<
   std::vector<uint8_t> insert_ok(n, 1);
   auto insert = [&](uint32_t l) {
     cur_ = l;
-    if (Slots) Slots->SwapIn(l);
+    if (Slots) {
+      Slots->ResetLane(l);
+      Slots->SwapIn(l);
+    }
     insert_ok[l] = Target.InsertTestcase(Testcases[l].first, Testcases[l].second);
     if (Slots) Slots->SwapOut(l);
   };

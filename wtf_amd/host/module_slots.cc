@@ -44,13 +44,15 @@ void ModuleSlots::Capture(uint32_t lanes) {
 }
 
 void ModuleSlots::ResetAll() {
+  for (size_t l = 0; l < lanes_.size(); l++) ResetLane((uint32_t)l);
+}
+
+void ModuleSlots::ResetLane(uint32_t l) {
+  if (l >= lanes_.size() || !dirty_[l]) return;
   const auto &R = LaneStateRegistry();
-  for (size_t l = 0; l < lanes_.size(); l++) {
-    if (!dirty_[l]) continue;
-    for (size_t i = 0; i < R.size(); i++)
-      if (lanes_[l][i]) R[i].assign(lanes_[l][i], initial_[i]);
-    dirty_[l] = 0;
-  }
+  for (size_t i = 0; i < R.size(); i++)
+    if (lanes_[l][i]) R[i].assign(lanes_[l][i], initial_[i]);
+  dirty_[l] = 0;
 }
 
 void ModuleSlots::SwapIn(uint32_t lane) {

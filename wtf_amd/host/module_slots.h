@@ -75,6 +75,9 @@ class ModuleSlots {
   void Capture(uint32_t lanes);
   // Every lane's copy back to the captured state (start of a batch).
   void ResetAll();
+  // ResetAll for one lane (lanes are independent: callers may reset
+  // different lanes on different threads)
+  void ResetLane(uint32_t lane);
   void SwapIn(uint32_t lane);
   void SwapOut(uint32_t lane);
   size_t Objects() const { return initial_.size(); }
