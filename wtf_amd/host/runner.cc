@@ -2,18 +2,32 @@
 #include "runner.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <future>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <thread>
 
 #include "../../include/wtfgpu.h"
 
 namespace wtfgpu_host {
 
 namespace {
+
+// parallel mutation of a fuzz batch (make_batch): batches of at least
+// kParMutateMin new testcases, kMutateChunk testcases per generator
+constexpr size_t kParMutateMin = 8192, kMutateChunk = 2048;
+
+// host threads for batch mutation: OMP_NUM_THREADS when set, else up to 16
+unsigned host_threads() {
+  if (const char *E = getenv("OMP_NUM_THREADS"))
+    if (atoi(E) > 0) return (unsigned)atoi(E);
+  const unsigned H = std::thread::hardware_concurrency();
+  return H == 0 ? 1 : std::min(H, 16u);
+}
 using Clock = std::chrono::steady_clock;
 double secs_since(Clock::time_point t0) { return std::chrono::duration<double>(Clock::now() - t0).count(); }
 
@@ -256,6 +270,34 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
     while (Batch.size() < n && !Pending.empty()) {
       Batch.push_back(std::move(Pending.back()));
       Pending.pop_back();
+    }
+    // large batches: mutate in fixed chunks on the host threads; chunk c has
+    // its own generator, seeded from Rng in chunk order, its own mutator and
+    // a read-only view of the corpus (deterministic for a seed whatever the
+    // thread count; the corpus does not change while the batch is built)
+    const size_t Need = n - Batch.size();
+    if (Corpus.Size() && Need >= kParMutateMin) {
+      const size_t Chunks = (Need + kMutateChunk - 1) / kMutateChunk;
+      std::vector<uint64_t> Seeds(Chunks);
+      for (uint64_t &S : Seeds) S = Rng();
+      std::vector<std::string> Out(Need);
+      std::atomic<size_t> NextChunk{0};
+      auto Work = [&]() {
+        for (size_t c; (c = NextChunk.fetch_add(1)) < Chunks;) {
+          std::mt19937_64 R(Seeds[c]);
+          Corpus_t View(Corpus, R);
+          std::unique_ptr<Mutator_t> M = Target->CreateMutator(R, O.max_len);
+          for (size_t i = c * kMutateChunk; i < std::min(Need, (c + 1) * kMutateChunk); i++) {
+            Out[i] = M->GetNewTestcase(View);
+            if (Out[i].size() > O.max_len) Out[i].resize(O.max_len);
+          }
+        }
+      };
+      std::vector<std::thread> Pool;
+      for (unsigned t = 1; t < host_threads(); t++) Pool.emplace_back(Work);
+      Work();
+      for (std::thread &Th : Pool) Th.join();
+      for (std::string &S : Out) Batch.push_back(std::move(S));
     }
     while (Batch.size() < n) {
       if (Corpus.Size() == 0 && Batch.empty()) break;

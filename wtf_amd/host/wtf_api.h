@@ -354,17 +354,23 @@ class Corpus_t {
   fs::path OutputsPath_;
   uint64_t Bytes_ = 0;
   std::mt19937_64 &Rng_;
+  const std::vector<Testcase_t> *View_ = nullptr;  // read-only view of another corpus
 
  public:
   Corpus_t(const fs::path &OutputsPath, std::mt19937_64 &Rng) : OutputsPath_(OutputsPath), Rng_(Rng) {}
+  // a read-only view of Base's testcases that picks with its own generator
+  // (parallel mutation; Base must not change while the view is used)
+  Corpus_t(const Corpus_t &Base, std::mt19937_64 &Rng)
+      : OutputsPath_(Base.OutputsPath_), Rng_(Rng), View_(Base.View_ ? Base.View_ : &Base.Testcases_) {}
   Corpus_t(const Corpus_t &) = delete;
   Corpus_t &operator=(const Corpus_t &) = delete;
-  size_t Size() const { return Testcases_.size(); }
+  size_t Size() const { return View_ ? View_->size() : Testcases_.size(); }
   // Saved as <result>-<blake3 hex> ("ok" results unprefixed) under OutputsPath (corpus.h:56-86).
   bool SaveTestcase(const TestcaseResult_t &Result, Testcase_t Testcase);
   const Testcase_t *PickTestcase() const {
-    if (Testcases_.empty()) return nullptr;
-    return &Testcases_[std::uniform_int_distribution<size_t>(0, Testcases_.size() - 1)(Rng_)];
+    const std::vector<Testcase_t> &T = View_ ? *View_ : Testcases_;
+    if (T.empty()) return nullptr;
+    return &T[std::uniform_int_distribution<size_t>(0, T.size() - 1)(Rng_)];
   }
   uint64_t Bytes() const { return Bytes_; }
 };
