@@ -22,7 +22,8 @@
  *   wtfgpu_run                <- BochscpuBackend_t::Run / bochscpu_cpu_run
  *                                (bochscpu_backend.cc:352-410) + the before/after execution,
  *                                lin_access, interrupt, hlt hooks (:445-697).
- *   wtfgpu_read_regs/write_regs <- Get/SetReg (bochscpu_backend.cc:1124-1190)
+ *   wtfgpu_read_regs/write_regs, wtfgpu_lane_get_cr/set_cr
+ *                             <- Get/SetReg (bochscpu_backend.cc:1124-1190)
  *   wtfgpu_lane_translate     <- VirtTranslate (bochscpu_backend.cc:891-896)
  *   wtfgpu_lane_read_phys/write_phys <- PhysTranslate + memcpy / DirtyGpa
  *                                (bochscpu_backend.cc:887-900, backend.cc:16-127)
@@ -279,6 +280,13 @@ int wtfgpu_gather_bytes(wtfgpu_ctx *ctx, const uint32_t *lanes, const uint64_t *
  * snapshot has no usable gate (the lane is left as it was). */
 int wtfgpu_inject_fault(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, uint32_t vector, uint32_t error,
                         const uint64_t *addrs, int32_t *delivered);
+
+/* A lane's cr2 / cr3 (cr = 2 or 3): GetReg / SetReg(Registers_t::Cr2 / Cr3)
+ * (bochscpu_backend.cc:1124-1190). cr2 is the lane's, as last written by an
+ * exception delivered through the guest IDT; a cr3 written here is the lane's
+ * page-table root from its next run on. */
+int wtfgpu_lane_get_cr(wtfgpu_ctx *ctx, uint32_t lane, uint32_t cr, uint64_t *value);
+int wtfgpu_lane_set_cr(wtfgpu_ctx *ctx, uint32_t lane, uint32_t cr, uint64_t value);
 
 /* Page-locked host memory (for gather/scatter staging buffers). */
 int wtfgpu_host_alloc(wtfgpu_ctx *ctx, uint64_t bytes, void **out);

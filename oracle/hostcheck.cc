@@ -1,0 +1,159 @@
+// Host-logic checker driver (TEST INFRASTRUCTURE ONLY, never linked into the
+// product). One source, built twice by oracle/Makefile:
+//   * oracle/_ref/ref_hostcheck: against the reference's own host sources where
+//     they lie under /root/reference/src (utils.cc, mutator.cc, FuzzerMutate.cpp,
+//     fuzzer_tlv_server.cc, ...; target `ref`);
+//   * oracle/hostcheck: against this repository's restatements (libwtfhost.a,
+//     -DWTF_AMD_HOST).
+// tests/test_host_parity.py compares the two outputs, and both against the
+// fixtures tests/golden/gen_host_fixtures.py recorded from the reference build.
+// Subcommands:
+//
+//   cpustate <regs.json>
+//       LoadCpuStateFromJSON + SanitizeCpuState (src/wtf/utils.cc:57-258):
+//       "OK <0|1>" then one "<field> <hex>" line per CpuState_t field.
+//   mutate <libfuzzer|tlv_server> <seed> <maxlen> <count> <newcov_every> <file>...
+//       std::mt19937_64 Rng(seed) (server.h:339), Corpus_t over the files in
+//       order (corpus.h:56-87, no outputs dir), Mutator = the target's
+//       CreateMutator (fuzzer_tlv_server.cc:204-365) or LibfuzzerMutator_t
+//       (mutator.cc:8-54, targets.h:25); `count` GetNewTestcase calls, each
+//       printed as "T <hex>"; every `newcov_every`-th output (1-based, 0 =
+//       never) is fed back through OnNewCoverage (server.h:816-853), which
+//       arms libFuzzer's CrossOver.
+//   blake3 <hexbytes>
+//       Blake3HexDigest (utils.cc) of the bytes.
+// This repository's build only (the reference exposes neither as a function
+// it can link without bochscpu):
+//   xof <hexbytes> <outlen>   BLAKE3 extended output (pinned by the official
+//                             test vectors, src/libs/BLAKE3/test_vectors)
+//   rdrand <seed> <n>         n values of the Rdrand chain from seed
+//                             (BochscpuBackend_t::Rdrand, bochscpu_backend.cc:874-885)
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iterator>
+#include <memory>
+#include <random>
+#include <string>
+#include <vector>
+
+#ifdef WTF_AMD_HOST
+#include "../wtf_amd/host/blake3_lite.h"
+#include "../wtf_amd/host/wtf_api.h"
+#else
+#include "backend.h"
+#include "corpus.h"
+#include "mutator.h"
+#include "targets.h"
+#include "utils.h"
+#endif
+
+static std::vector<uint8_t> read_all(const char *path) {
+  std::ifstream f(path, std::ios::binary);
+  return std::vector<uint8_t>(std::istreambuf_iterator<char>(f), {});
+}
+
+static void hexline(const char *tag, const std::string &s) {
+  printf("%s ", tag);
+  for (unsigned char c : s) printf("%02x", c);
+  printf("\n");
+}
+
+static int cmd_cpustate(const char *path) {
+  CpuState_t S{};
+  if (!LoadCpuStateFromJSON(S, path)) {
+    printf("LOAD_FAIL\n");
+    return 1;
+  }
+  const bool ok = SanitizeCpuState(S);
+  printf("OK %d\n", ok ? 1 : 0);
+#define P(name, v) printf(name " %llx\n", (unsigned long long)(v))
+  P("rax", S.Rax); P("rbx", S.Rbx); P("rcx", S.Rcx); P("rdx", S.Rdx);
+  P("rsi", S.Rsi); P("rdi", S.Rdi); P("rip", S.Rip); P("rsp", S.Rsp);
+  P("rbp", S.Rbp); P("r8", S.R8); P("r9", S.R9); P("r10", S.R10);
+  P("r11", S.R11); P("r12", S.R12); P("r13", S.R13); P("r14", S.R14);
+  P("r15", S.R15); P("rflags", S.Rflags); P("tsc", S.Tsc);
+  P("apic_base", S.ApicBase); P("sysenter_cs", S.SysenterCs);
+  P("sysenter_esp", S.SysenterEsp); P("sysenter_eip", S.SysenterEip);
+  P("pat", S.Pat); P("efer", S.Efer.Flags); P("star", S.Star);
+  P("lstar", S.Lstar); P("cstar", S.Cstar); P("sfmask", S.Sfmask);
+  P("kernel_gs_base", S.KernelGsBase); P("tsc_aux", S.TscAux);
+  P("fpcw", S.Fpcw); P("fpsw", S.Fpsw); P("fptw", S.Fptw); P("fpop", S.Fpop);
+  P("cr0", S.Cr0.Flags); P("cr2", S.Cr2); P("cr3", S.Cr3); P("cr4", S.Cr4.Flags);
+  P("cr8", S.Cr8); P("xcr0", S.Xcr0); P("dr0", S.Dr0); P("dr1", S.Dr1);
+  P("dr2", S.Dr2); P("dr3", S.Dr3); P("dr6", S.Dr6); P("dr7", S.Dr7);
+  P("mxcsr", S.Mxcsr); P("mxcsr_mask", S.MxcsrMask);
+  P("gdtr.base", S.Gdtr.Base); P("gdtr.limit", S.Gdtr.Limit);
+  P("idtr.base", S.Idtr.Base); P("idtr.limit", S.Idtr.Limit);
+  const Seg_t *segs[] = {&S.Es, &S.Cs, &S.Ss, &S.Ds, &S.Fs, &S.Gs, &S.Tr, &S.Ldtr};
+  const char *names[] = {"es", "cs", "ss", "ds", "fs", "gs", "tr", "ldtr"};
+  for (int i = 0; i < 8; i++)
+    printf("%s %x %x %llx %x %x\n", names[i], (unsigned)segs[i]->Present, (unsigned)segs[i]->Selector,
+           (unsigned long long)segs[i]->Base, (unsigned)segs[i]->Limit, (unsigned)segs[i]->Attr);
+  for (int i = 0; i < 8; i++) printf("fpst%d %llx\n", i, (unsigned long long)S.Fpst[i]);
+#undef P
+  return 0;
+}
+
+static int cmd_mutate(int argc, char **argv) {
+  if (argc < 7) return 2;
+  const std::string name = argv[2];
+  std::mt19937_64 Rng(strtoull(argv[3], nullptr, 0));
+  const size_t maxlen = strtoull(argv[4], nullptr, 0);
+  const size_t count = strtoull(argv[5], nullptr, 0);
+  const size_t every = strtoull(argv[6], nullptr, 0);
+  Corpus_t Corpus("", Rng);
+  for (int i = 7; i < argc; i++) {
+    const auto b = read_all(argv[i]);
+    Corpus.SaveTestcase(Ok_t(), Testcase_t(b.data(), b.size()));
+  }
+  std::unique_ptr<Mutator_t> M;
+  if (name == "libfuzzer") {
+    M = LibfuzzerMutator_t::Create(Rng, maxlen);
+  } else {
+    Target_t *T = Targets_t::Instance().Get(name);
+    if (!T) return 3;
+    M = T->CreateMutator(Rng, maxlen);
+  }
+  for (size_t i = 1; i <= count; i++) {
+    std::string s = M->GetNewTestcase(Corpus);
+    hexline("T", s);
+    if (every && i % every == 0) M->OnNewCoverage(Testcase_t((const uint8_t *)s.data(), s.size()));
+  }
+  return 0;
+}
+
+static std::vector<uint8_t> unhex(const char *p) {
+  std::vector<uint8_t> b;
+  for (; p[0] && p[1]; p += 2) b.push_back((uint8_t)strtoul(std::string(p, 2).c_str(), nullptr, 16));
+  return b;
+}
+
+int main(int argc, char **argv) {
+  if (argc < 2) return 2;
+  const std::string cmd = argv[1];
+#ifdef WTF_AMD_HOST
+  if (cmd == "xof" && argc == 4) {
+    const auto b = unhex(argv[2]);
+    std::vector<uint8_t> o(strtoull(argv[3], nullptr, 0));
+    wtfgpu_host::blake3_hash(b.data(), b.size(), o.data(), o.size());
+    for (uint8_t c : o) printf("%02x", c);
+    printf("\n");
+    return 0;
+  }
+  if (cmd == "rdrand" && argc == 4) {
+    uint64_t seed = strtoull(argv[2], nullptr, 0);
+    for (uint64_t i = 0, n = strtoull(argv[3], nullptr, 0); i < n; i++)
+      printf("%016llx\n", (unsigned long long)wtfgpu_host::wtf_rdrand(seed));
+    return 0;
+  }
+#endif
+  if (cmd == "cpustate" && argc == 3) return cmd_cpustate(argv[2]);
+  if (cmd == "mutate") return cmd_mutate(argc, argv);
+  if (cmd == "blake3" && argc == 3) {
+    const auto b = unhex(argv[2]);
+    printf("%s\n", Blake3HexDigest(b.data(), b.size()).c_str());
+    return 0;
+  }
+  return 2;
+}

@@ -116,7 +116,10 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
         case WTFGPU_EXIT_HLT: result_ = Crash_t(); break;
         case WTFGPU_EXIT_CR3: result_ = Cr3Change_t(); break;
         case WTFGPU_EXIT_FAULT: result_ = FaultToResult(e.vector, e.error, e.rip, e.addr, e.opcode); break;
-        default: result_ = Crash_t("engine-" + std::to_string(e.status)); break;
+        default:  // outside the engine subset: an engine error, not a target crash
+          result_ = Crash_t();
+          engine_error_ = true;
+          break;
       }
       break;
     }
@@ -233,6 +236,7 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
     last_new_.clear();
   }
   bool full_ = false;
+  bool engine_error_ = false;
   void SetFullCoverage(bool On) override { full_ = On; }
   size_t CoverageSize() const override { return aggregate_.size(); }
   bool RunBatch(const Target_t &Target, const std::vector<std::pair<const uint8_t *, size_t>> &Tc,
@@ -251,6 +255,8 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
         R = Run(Tc[i].first, Tc[i].second);
       }
       L.result = *R;
+      L.error = engine_error_;
+      engine_error_ = false;
       if (std::holds_alternative<Timedout_t>(*R)) {
         L.new_coverage.assign(0, 0);
         for (const Gva_t &g : last_new_) L.new_coverage.push_back(g.U64());

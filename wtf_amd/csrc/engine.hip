@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -2102,6 +2103,30 @@ int wtfgpu_gather_bytes(wtfgpu_ctx *c, const uint32_t *lanes, const uint64_t *gp
                                           len, c->d_scratch + o_out);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(out, c->d_scratch + o_out, (u64)n * len, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+static int lane_cr_ptr(wtfgpu_ctx *c, uint32_t lane, uint32_t cr, u8 **p) {
+  if (!c || !c->d_sys || lane >= c->P.nlanes || (cr != 2 && cr != 3)) return WTFGPU_ERR_INVALID;
+  *p = (u8 *)(c->d_sys + lane) + (cr == 2 ? offsetof(LaneSys, cr2) : offsetof(LaneSys, cr3));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_lane_get_cr(wtfgpu_ctx *c, uint32_t lane, uint32_t cr, uint64_t *value) {
+  u8 *p = nullptr;
+  if (!value || lane_cr_ptr(c, lane, cr, &p)) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemcpyAsync(value, p, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_lane_set_cr(wtfgpu_ctx *c, uint32_t lane, uint32_t cr, uint64_t value) {
+  u8 *p = nullptr;
+  if (lane_cr_ptr(c, lane, cr, &p)) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemcpyAsync(p, &value, 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return WTFGPU_OK;
 }

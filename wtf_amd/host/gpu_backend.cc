@@ -104,6 +104,10 @@ void GpuBackend_t::reset_view(uint32_t lane) {
   v.gpr[16] = initial_regs_.rip;
   v.gpr[17] = initial_regs_.rflags;
   v.regs_dirty = false;
+  v.cr[0] = initial_regs_.cr2;
+  v.cr[1] = initial_regs_.cr3;
+  v.cr_known = 3;
+  v.cr_dirty = 0;
   v.result.reset();
   v.seed = initial_.Seed;  // Rdrand seed (bochscpu_backend.cc:1030)
   v.has_feed = false;
@@ -126,8 +130,16 @@ void GpuBackend_t::SetLimit(const uint64_t Limit) {
 uint64_t GpuBackend_t::GetReg(const Registers_t Reg) {
   const int i = gpr_index(Reg);
   if (i >= 0) return cur().gpr[i];
-  if (Reg == Registers_t::Cr3) return initial_.Cr3;  // ring-3 lanes cannot change cr3
-  if (Reg == Registers_t::Cr2) return initial_.Cr2;
+  if (Reg == Registers_t::Cr2 || Reg == Registers_t::Cr3) {  // the lane's own (bochscpu_cpu_cr2/cr3)
+    const int k = Reg == Registers_t::Cr2 ? 0 : 1;
+    LaneView &v = cur();
+    if (!(v.cr_known & (1 << k))) {
+      std::lock_guard<std::mutex> g(engine_mu_);
+      if (wtfgpu_lane_get_cr(ctx_, cur_, k ? 3 : 2, &v.cr[k]) != WTFGPU_OK) std::abort();
+      v.cr_known |= uint8_t(1 << k);
+    }
+    return v.cr[k];
+  }
   return 0;
 }
 
@@ -136,6 +148,11 @@ uint64_t GpuBackend_t::SetReg(const Registers_t Reg, const uint64_t Value) {
   if (i >= 0) {
     cur().gpr[i] = Value;
     cur().regs_dirty = true;
+  } else if (Reg == Registers_t::Cr2 || Reg == Registers_t::Cr3) {
+    const int k = Reg == Registers_t::Cr2 ? 0 : 1;
+    cur().cr[k] = Value;
+    cur().cr_known |= uint8_t(1 << k);
+    cur().cr_dirty |= uint8_t(1 << k);
   }
   return Value;
 }
@@ -417,7 +434,7 @@ bool GpuBackend_t::VirtTranslate(const Gva_t Gva, Gpa_t &Gpa, const MemoryValida
   const uint64_t va = Gva.U64(), vpn = va >> 12;
   const LaneView &v = views_[cur_];
   WalkMemo &m = t_walk_memo[vpn & 63];
-  if (m.vpn == vpn && v.dirty_known) {
+  if (m.vpn == vpn && v.dirty_known && (!(v.cr_known & 2) || v.cr[1] == initial_.Cr3)) {
     bool clean = true;
     for (uint32_t k = 0; k < m.ntables && clean; k++)
       clean = !in_overlay(v, m.tables[k]) && !find_staged(cur_, m.tables[k]);
@@ -429,6 +446,10 @@ bool GpuBackend_t::VirtTranslate(const Gva_t Gva, Gpa_t &Gpa, const MemoryValida
   uint64_t table = initial_.Cr3 & 0x000ffffffffff000ull;
   WalkMemo w;
   bool from_dump = v.dirty_known;
+  if ((v.cr_known & 2) && v.cr[1] != initial_.Cr3) {  // a handler moved the lane's cr3
+    table = v.cr[1] & 0x000ffffffffff000ull;
+    from_dump = false;  // not memoised: the memo holds walks from the snapshot's cr3
+  }
   for (int level = 3; level >= 0; level--) {
     const uint64_t tf = table >> 12;
     w.tables[w.ntables++] = tf;
@@ -506,6 +527,12 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
       v.regs_dirty = false;
     }
     for (const Staged &p : v.pages) cand.push_back(Cand{l, &p, 0, 0});
+    for (int k = 0; k < 2; k++)
+      if (v.cr_dirty & (1 << k)) {
+        std::lock_guard<std::mutex> g(engine_mu_);
+        if (wtfgpu_lane_set_cr(ctx_, l, k ? 3 : 2, v.cr[k]) != WTFGPU_OK) return WTFGPU_ERR_INVALID;
+      }
+    v.cr_dirty = 0;
   }
 #pragma omp parallel for schedule(dynamic, 64)
   for (size_t i = 0; i < cand.size(); i++) {
@@ -592,9 +619,13 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
         case WTFGPU_EXIT_FAULT: v.result = FaultToResult(e.vector, e.error, e.rip, e.addr, e.opcode); break;
         case WTFGPU_EXIT_STOPPED: break;
         case WTFGPU_EXIT_STOP_OK: v.result = Ok_t(); break;           // device Feed action: Stop(Ok_t())
-        default:  // unimplemented opcode / overlay full: the engine cannot finish it
+        default:
+          // unimplemented opcode / overlay full / a device Feed write that
+          // failed: the engine cannot finish the testcase. Not a target bug:
+          // flagged as an engine error, with an unnamed Crash_t (which no
+          // master saves, server.h:861-877) as its result
           if (out) (*out)[l].error = true;
-          if (!v.result) v.result = Crash_t("engine-" + std::to_string(e.status));
+          if (!v.result) v.result = Crash_t();
           break;
       }
       done[l - first] = 1;
@@ -619,6 +650,7 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
       LaneView &v = views_[hits[i]];
       memcpy(v.gpr, &regs[i * 18], 18 * 8);
       v.regs_dirty = false;
+      v.cr_known = 0;  // an exception delivery or a cr write may have changed them
       v.win_len = 0;
       drop_staged(v);
       const uint32_t cnt = std::min(dl[i * stride], overlay_pages_);

@@ -100,6 +100,10 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   struct LaneView {
     uint64_t gpr[18] = {};  // wtfgpu order: 16 gprs, rip, rflags
     bool regs_dirty = false;
+    // cr2 / cr3 (GetReg / SetReg): bit 0 = cr2, bit 1 = cr3; fetched from the
+    // device on first use after a run, written back at flush when dirty
+    uint64_t cr[2] = {};
+    uint8_t cr_known = 0, cr_dirty = 0;
     std::optional<TestcaseResult_t> result;
     uint64_t seed = 0;
     uint64_t inject = ~0ull;  // PageFaultsMemoryIfNeeded: page to #PF after the handler

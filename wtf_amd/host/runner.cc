@@ -141,6 +141,7 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
     else if (a == "--device") O.device = atoi(next("--device"));
     else if (a == "--full-coverage") O.full_coverage = true;
     else if (a == "--quiet") O.quiet = true;
+    else if (a == "--serial-mutation") O.serial_mutation = true;
     else {
       fprintf(stderr, "unknown argument %s\n", a.c_str());
       return false;
@@ -148,7 +149,8 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
   }
   if (O.name.empty() || O.target.empty()) {
     fprintf(stderr, "usage: [run|fuzz] --name <target> --target <dir> [--input p] [--results f] [--limit n]\n"
-                    "       [--lanes n] [--overlay-pages k] [--runs n] [--seconds s] [--seed s] [--full-coverage]\n");
+                    "       [--lanes n] [--overlay-pages k] [--runs n] [--seconds s] [--seed s] [--full-coverage]\n"
+                    "       [--serial-mutation]\n");
     return false;
   }
   return true;
@@ -251,6 +253,8 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
   }
   // the master sends the corpus first (server.h:756-790), then mutations
   std::vector<std::string> Pending;
+  std::string LastNewCov;  // the testcase last passed to Mutator->OnNewCoverage
+  bool HaveNewCov = false;
   for (const auto &P : list_inputs(T / "inputs")) {
     const auto B = ReadFile(P);
     Pending.emplace_back(B.begin(), B.end());
@@ -276,7 +280,7 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
     // a read-only view of the corpus (deterministic for a seed whatever the
     // thread count; the corpus does not change while the batch is built)
     const size_t Need = n - Batch.size();
-    if (Corpus.Size() && Need >= kParMutateMin) {
+    if (Corpus.Size() && Need >= kParMutateMin && !O.serial_mutation) {
       const size_t Chunks = (Need + kMutateChunk - 1) / kMutateChunk;
       std::vector<uint64_t> Seeds(Chunks);
       for (uint64_t &S : Seeds) S = Rng();
@@ -287,6 +291,9 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
           std::mt19937_64 R(Seeds[c]);
           Corpus_t View(Corpus, R);
           std::unique_ptr<Mutator_t> M = Target->CreateMutator(R, O.max_len);
+          // the master mutator's cross-over partner (the last new-coverage
+          // testcase) is every chunk mutator's too
+          if (HaveNewCov) M->OnNewCoverage(Testcase_t((const uint8_t *)LastNewCov.data(), LastNewCov.size()));
           for (size_t i = c * kMutateChunk; i < std::min(Need, (c + 1) * kMutateChunk); i++) {
             Out[i] = M->GetNewTestcase(View);
             if (Out[i].size() > O.max_len) Out[i].resize(O.max_len);
@@ -336,7 +343,10 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
       const LaneResult &L = R[i];
       Execs++;
       Retired += L.icount;
-      Errors += L.error;
+      if (L.error) {  // the engine could not finish it: neither a crash nor coverage
+        Errors++;
+        continue;
+      }
       if (std::holds_alternative<Timedout_t>(L.result)) Timeouts++;
       if (std::holds_alternative<Cr3Change_t>(L.result)) Cr3s++;
       if (const Crash_t *C = std::get_if<Crash_t>(&L.result)) {
@@ -344,9 +354,15 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
         if (!C->CrashName.empty() && CrashNames.insert(C->CrashName).second)
           SaveFile(T / "crashes" / C->CrashName, (const uint8_t *)Batch[i].data(), Batch[i].size());
       }
-      if (!L.new_coverage.empty() && !std::holds_alternative<Crash_t>(L.result)) {
+      // a timed-out testcase reports no coverage (the client revokes it,
+      // client.cc:122-133); any other result with new coverage, crashes
+      // included, joins the corpus after arming the mutator's cross-over
+      // (server.h:816-853)
+      if (!L.new_coverage.empty() && !std::holds_alternative<Timedout_t>(L.result)) {
         Testcase_t Tcase((const uint8_t *)Batch[i].data(), Batch[i].size());
         Mutator->OnNewCoverage(Tcase);
+        LastNewCov = Batch[i];
+        HaveNewCov = true;
         Corpus.SaveTestcase(L.result, std::move(Tcase));
       }
     }

@@ -59,6 +59,7 @@ struct RunnerOptions {
   int device = 0;
   bool full_coverage = false;
   bool quiet = false;
+  bool serial_mutation = false;  // one mutator, in order: the reference master's stream exactly
 };
 
 bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O);

@@ -287,6 +287,9 @@ bool LoadCpuStateFromJSON(CpuState_t &S, const fs::path &Path) {
     D.Base = V.at("base").u64();
     D.Limit = (uint32_t)V.at("limit").u64();
     D.Attr = (uint16_t)V.at("attr").u64();
+    // the reference's Present is bit 7 of the Attr union (globals.h:33-51), so
+    // the attr write overrides the JSON "present" flag (utils.cc:116-129)
+    D.Present = (D.Attr >> 7) & 1;
   };
   Seg("es", S.Es), Seg("cs", S.Cs), Seg("ss", S.Ss), Seg("ds", S.Ds), Seg("fs", S.Fs), Seg("gs", S.Gs);
   Seg("tr", S.Tr), Seg("ldtr", S.Ldtr);

@@ -383,27 +383,41 @@ class Mutator_t {
   virtual void OnNewCoverage(const Testcase_t &) {}
 };
 
-// The default mutator of a target (targets.h:25; mutator.cc:8-51): one
-// libFuzzer-style mutation of a corpus pick per testcase. A reduced
-// restatement of libFuzzer's MutationDispatcher (erase / insert / insert
-// repeated / change byte / change bit / shuffle / change binary integer /
-// copy part / cross over with the last new-coverage testcase); its output
-// sequence for a seed is not libFuzzer's.
+// The default mutator of a target (targets.h:25; mutator.cc:8-54): one
+// mutation of a corpus pick per testcase by libFuzzer's MutationDispatcher
+// (src/libs/libfuzzer/FuzzerMutate.cpp, vendored by the reference), restated
+// in mutator_lite.cc with the same generator (std::minstd_rand seeded with the
+// low 32 bits of one draw of the master's mt19937_64), the same 12 mutators in
+// the same order, the same draw order and the same persistent scratch state;
+// its output stream for a seed is the reference's, bit for bit
+// (tests/test_host_parity.py against the reference build).
 class LibfuzzerMutator_t : public Mutator_t {
-  std::mt19937_64 Rand_;
+  std::minstd_rand Rand_;                 // fuzzer::Random (FuzzerMutate.h:212-228)
   size_t MaxSize_;
-  std::vector<uint8_t> CrossOverWith_;
-  uint64_t R(uint64_t N) { return N ? Rand_() % N : 0; }
-  size_t MutateOnce(std::vector<uint8_t> &D, size_t Size);
+  std::vector<uint8_t> Scratch_;          // ScratchBuffer_ (mutator.cc:17-18)
+  std::vector<uint8_t> InPlace_;          // MutationDispatcher::MutateInPlaceHere
+  std::vector<uint8_t> CrossOverWith_;    // last new-coverage testcase
+  bool HasCrossOver_ = false;
+  size_t R(size_t N) { return N ? size_t(Rand_()) % N : 0; }
+  bool RB() { return size_t(Rand_()) % 2; }
+  uint8_t RandCh();
+  size_t Apply(size_t Which, uint8_t *Data, size_t Size);
+  size_t CopyPartOf(const uint8_t *From, size_t FromSize, uint8_t *To, size_t ToSize);
+  size_t InsertPartOf(const uint8_t *From, size_t FromSize, uint8_t *To, size_t ToSize, size_t MaxToSize);
+  size_t CrossOver(const uint8_t *A, size_t SizeA, const uint8_t *B, size_t SizeB, uint8_t *Out, size_t MaxOut);
+  template <typename T>
+  size_t ChangeBinaryInteger(uint8_t *Data, size_t Size);
 
  public:
-  LibfuzzerMutator_t(std::mt19937_64 &Rng, const size_t MaxSize) : Rand_(Rng()), MaxSize_(MaxSize) {}
+  LibfuzzerMutator_t(std::mt19937_64 &Rng, const size_t MaxSize)
+      : Rand_((unsigned int)Rng()), MaxSize_(MaxSize), Scratch_(MaxSize) {}
   static std::unique_ptr<Mutator_t> Create(std::mt19937_64 &Rng, const size_t MaxSize) {
     return std::make_unique<LibfuzzerMutator_t>(Rng, MaxSize);
   }
   std::string GetNewTestcase(const Corpus_t &Corpus) override;
   void OnNewCoverage(const Testcase_t &T) override {
     CrossOverWith_.assign(T.Buffer_.get(), T.Buffer_.get() + T.BufferSize_);
+    HasCrossOver_ = true;
   }
 };
 
