@@ -28,6 +28,9 @@
 //                             test vectors, src/libs/BLAKE3/test_vectors)
 //   rdrand <seed> <n>         n values of the Rdrand chain from seed
 //                             (BochscpuBackend_t::Rdrand, bochscpu_backend.cc:874-885)
+//   kdmp <dump> [gva...]      wtf_amd/host/kdmp.cc in oracle/ref_kdmp_dump.cc's
+//                             output format (TYPE / CR3 / RIP / PAGE / VT lines),
+//                             for comparison with oracle/_ref/kdmp_ref
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -39,6 +42,7 @@
 
 #ifdef WTF_AMD_HOST
 #include "../wtf_amd/host/blake3_lite.h"
+#include "../wtf_amd/host/kdmp.h"
 #include "../wtf_amd/host/wtf_api.h"
 #else
 #include "backend.h"
@@ -139,6 +143,29 @@ int main(int argc, char **argv) {
     wtfgpu_host::blake3_hash(b.data(), b.size(), o.data(), o.size());
     for (uint8_t c : o) printf("%02x", c);
     printf("\n");
+    return 0;
+  }
+  if (cmd == "kdmp" && argc >= 3) {
+    wtfgpu_host::KernelDump D;
+    if (!D.Parse(argv[2])) {
+      printf("PARSE_FAIL\n");
+      return 1;
+    }
+    auto fnv = [](const uint8_t *p) {
+      uint64_t h = 1469598103934665603ULL;
+      for (size_t i = 0; i < 4096; i++) h = (h ^ p[i]) * 1099511628211ULL;
+      return h;
+    };
+    printf("TYPE %u\nCR3 %llx\nRIP %llx\n", D.DumpType(), (unsigned long long)D.DirectoryTableBase(),
+           (unsigned long long)D.ContextRip());
+    for (const auto &[gpfn, page] : D.Pages())
+      printf("PAGE %llx %llx\n", (unsigned long long)(gpfn << 12), (unsigned long long)fnv(page));
+    for (int i = 3; i < argc; i++) {
+      const uint64_t gva = strtoull(argv[i], nullptr, 0);
+      const auto gpa = D.VirtTranslate(gva);
+      if (gpa) printf("VT %llx %llx\n", (unsigned long long)gva, (unsigned long long)*gpa);
+      else printf("VT %llx -1\n", (unsigned long long)gva);
+    }
     return 0;
   }
   if (cmd == "rdrand" && argc == 4) {

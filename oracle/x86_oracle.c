@@ -21,8 +21,13 @@
  *   U9 a rep string instruction is one retired instruction whatever the count.
  *   U10 a breakpoint handler that stops the lane or moves rip cancels the
  *      hooked instruction (not executed, not counted).
- *   U11 exceptions are not delivered through the IDT: the lane exits FAULT
- *      with vector / error code / cr2 and the faulting instruction not retired.
+ *   U11 an exception is delivered through the guest IDT when the snapshot has
+ *      a present 64-bit interrupt / trap gate for its vector (TSS RSP0 / IST
+ *      stack switch, frame push, cr2 for #PF, IF cleared by interrupt gates);
+ *      otherwise the lane exits FAULT with vector / error code / cr2 and the
+ *      faulting instruction not retired. A fault raised before any instruction
+ *      retired since the previous delivery exits too (the double / triple
+ *      fault a CPU would raise, U18).
  *   U12 int3 and hlt exit before retiring.
  *   U13 16-bit bswap writes 0.
  *   U15 RDRAND r returns 0 with CF=1 (the value is unpinned: bochs draws a host
