@@ -1,0 +1,5 @@
+// compat/globals.h — the reference header of the same name (src/wtf/globals.h), for
+// building an upstream module source unchanged against this backend: the
+// declarations it needs are in wtf_api.h (see compat/README.md).
+#pragma once
+#include "../wtf_api.h"

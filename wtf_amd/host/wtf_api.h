@@ -22,6 +22,7 @@
 #include <memory>
 #include <optional>
 #include <random>
+#include <span>
 #include <string>
 #include <string_view>
 #include <unordered_map>
@@ -462,6 +463,11 @@ class Debugger_t {
 extern Debugger_t g_Dbg;
 
 // ------------------------------------------------------------------ utils
+// utils.h:19, 226-227
+using span_u8 = std::span<uint8_t>;
+const uint64_t _1KB = 1024;
+const uint64_t _1MB = _1KB * _1KB;
+
 std::string_view ExceptionCodeToStr(const uint32_t ExceptionCode);
 std::string TestcaseResultName(const TestcaseResult_t &Res);
 std::string Blake3HexDigest(const uint8_t *Data, const size_t DataSize);
