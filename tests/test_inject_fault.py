@@ -68,8 +68,14 @@ def test_gpu_inject_matches_oracle(snap):
             r = o.regs()
             assert list(g[lane][:16]) == list(r.gpr) and g[lane][16] == r.rip and g[lane][17] == r.rflags
             assert eng.read_regs(lane, 1)[0].cr2 == addr
+            assert eng.get_cr(lane, 2) == addr          # GetReg(Cr2): the lane's own
+            assert eng.get_cr(lane, 3) == st["cr3"]
             assert eng.read_virt(lane, r.gpr[4], 48) == o.read_virt(r.gpr[4], 48)
         untouched = eng.read_gprs()[1]
         assert untouched[16] == st["rip"]
+        assert eng.get_cr(1, 2) == st["cr2"]
+        eng.set_cr(1, 2, 0x1234000)                    # SetReg(Cr2)
+        assert eng.get_cr(1, 2) == 0x1234000 and eng.read_regs(1, 1)[0].cr2 == 0x1234000
+        assert eng.get_cr(2, 2) == st["cr2"]
     finally:
         eng.close()

@@ -204,3 +204,21 @@ class Engine:
         _chk(self.L.wtfgpu_read_bytes(self.ctx, first, count, out.ctypes.data_as(C.POINTER(C.c_uint64))),
              "read_bytes")
         return out
+
+    def gather_pages(self, lanes, gpas) -> np.ndarray:
+        """[n, 4096] u8: each lane's current view of each guest-physical page."""
+        lanes = np.ascontiguousarray(lanes, dtype=np.uint32)
+        gpas = np.ascontiguousarray(gpas, dtype=np.uint64)
+        out = np.zeros((len(lanes), 4096), dtype=np.uint8)
+        _chk(self.L.wtfgpu_gather_pages(self.ctx, lanes.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                        gpas.ctypes.data_as(C.POINTER(C.c_uint64)), len(lanes),
+                                        out.ctypes.data_as(C.c_void_p)), "gather_pages")
+        return out
+
+    def get_cr(self, lane, cr) -> int:
+        out = C.c_uint64()
+        _chk(self.L.wtfgpu_lane_get_cr(self.ctx, lane, cr, C.byref(out)), "lane_get_cr")
+        return out.value
+
+    def set_cr(self, lane, cr, value):
+        _chk(self.L.wtfgpu_lane_set_cr(self.ctx, lane, cr, value), "lane_set_cr")

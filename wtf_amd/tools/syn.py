@@ -80,3 +80,33 @@ def insert(gprs: np.ndarray, inp: np.ndarray) -> None:
 def expected_instructions(inp: np.ndarray) -> np.ndarray:
     trip = 1 + ((inp[:, 0].astype(np.int64) | (inp[:, 1].astype(np.int64) << 8)) % 4096)
     return trip * INSNS_PER_ITER + 1
+
+
+def model(inp: np.ndarray, table: bytes):
+    """The SYN loop restated over whole batches in numpy (a test checker):
+    final rax, rbx, rcx, rdx, r8, r9, r10 of every testcase, and the scratch
+    page each one leaves (uint64[n, 512]). Same insert as `insert`."""
+    n = len(inp)
+    g = np.zeros((n, 18), dtype=np.uint64)
+    insert(g, inp)
+    tab = np.frombuffer(table, dtype=np.uint64)
+    rax, rbx, r9, rcx = g[:, 0].copy(), g[:, 3].copy(), g[:, 9].copy(), g[:, 1].copy()
+    rdx = np.zeros(n, np.uint64)
+    r8 = np.zeros(n, np.uint64)
+    r10 = np.zeros(n, np.uint64)
+    scratch = np.zeros((n, 512), dtype=np.uint64)
+    idx = np.arange(n)
+    live = np.ones(n, dtype=bool)
+    with np.errstate(over="ignore"):
+        while live.any():
+            k = idx[live]
+            rdx[k] = rax[k] & np.uint64(0x1F8)
+            r8[k] = tab[(rdx[k] >> np.uint64(3)).astype(np.int64)]
+            rax[k] = rax[k] + r8[k]
+            rbx[k] = rbx[k] ^ rax[k]
+            r9[k] = r9[k] - rbx[k]
+            r10[k] = (rax[k] + rbx[k] * np.uint64(2) + np.uint64(0x10)) & np.uint64(0xFF8)
+            scratch[k, (r10[k] >> np.uint64(3)).astype(np.int64)] = r9[k]
+            rcx[k] = rcx[k] - np.uint64(1)
+            live[k] = rcx[k] != 0
+    return {"rax": rax, "rbx": rbx, "rcx": rcx, "rdx": rdx, "r8": r8, "r9": r9, "r10": r10}, scratch
