@@ -1,43 +1,47 @@
-"""bench.py — execs/s + emulated instr/s of the MI355X `gpu` execution backend.
+"""bench.py — execs/s + emulated instr/s of the MI355X `gpu` execution backend
+(BASELINE.json metric: "execs/sec + emulated instr/s per node (tlv_server,
+HEVD) at 1/2/4/8 GPUs").
 
-Workload (BASELINE.json configs[1], SURVEY.md §8(d) "SYN"): the synthetic
-ring-3 ALU/branch/load-store loop snapshot (wtf_amd/tools/syn.py), 65,536 lanes
-(= testcases) per GPU, `--limit 100000`, 64-byte uniform-random inputs.
+Headline (`value`): fuzzer_tlv_server on the gpu backend (BASELINE.json
+configs[2] at N=1, configs[3] at N>1): the synthetic tlv_server snapshot
+(wtf_amd/tools/tlv.py; the real one cannot be fetched), the tlv
+module and its custom mutator, seed 1337, 65,536 lanes per GPU, --limit 100000.
+One step = one fuzz batch of the node (include/wtfnode.h, libwtfnode.so, the
+same C++ as `wtfgpu fuzz`): mutate (overlapped with the previous batch) ->
+InsertTestcase x N -> k_run with breakpoints serviced -> lane-order coverage
+attribution -> Target.Restore, and for N > 1 the RCCL MAX merge of the
+per-GPU coverage maps (the only collective; every GPU is otherwise an
+independent shard with seed + rank). One process per GPU; `value` = testcases
+all ranks executed / max-over-ranks wall time of the K timed steps.
 
-One step = one batch through the hot path of wtf's client loop
-(`RunTestcaseAndRestore`, reference src/wtf/client.cc:88-180):
-    Backend.Restore (dirty-list reset, bochscpu_backend.cc:730-797)
-    -> Target.InsertTestcase (64-byte input -> registers)
-    -> Backend.Run (HIP kernel k_run until every lane hits the exit breakpoint)
-    -> per-lane results + new-coverage log -> aggregate coverage commit
-    -> (N > 1) RCCL MAX all-reduce of the per-GPU coverage map.
-
-Multi-GPU: one process per GPU, each an independent shard of the testcase
-stream (seed + rank); the only collective is the coverage-map merge. `value` =
-testcases all ranks executed / max-over-ranks wall time ("weak" scaling).
-
-The JSON line carries:
-  roofline      k_run's algorithmic bytes per launch (Σ ilen + data bytes read +
-                written, counted per lane by the kernel itself)
-                / its average launch duration (HIP events on the engine stream);
-                `traffic` from the committed rocprofv3 PMC summary when present.
-  cpu_baseline  the C oracle ("port": the build's scalar restatement, since
-                bochscpu is unbuildable) timed on host cores over a
-                bounded sample of the same SYN workload, one lane per thread.
-  tlv, hevd     (N=1, rank 0) BASELINE.json configs[2] and [4]: the synthetic
-                tlv_server / HEVD snapshots fuzzed by the `wtfgpu` node (C++
-                GpuBackend_t, tlv / hevd modules, breakpoints serviced on host
-                threads), next to the oracle twin `wtf_twin fuzz` run as one
-                process per host core (the reference's one-client-per-core
-                layout). Both rates are execs / wall time,
-                mutation included.
+Also on the line (N=1, rank 0):
+  roofline      k_run (the dominant kernel) on the headline workload:
+                algorithmic bytes per launch (instruction bytes + data bytes
+                read + written, counted per lane by the kernel) /
+                average launch duration (HIP events on the engine's stream);
+                `traffic` and VALU utilisation from the committed rocprofv3 PMC
+                summary of the same workload (profiles/pmc_tlv_k_run.json).
+  cpu_baseline  the oracle twin (`oracle/wtf_twin`: the C restatement behind
+                Backend_t, "port" — bochscpu is unbuildable) as one
+                `wtf_twin fuzz` process per host core, same module, mutator
+                and seed scheme, over a bounded wall window.
+  hevd          BASELINE.json configs[4] on one GPU: the synthetic ring-0 HEVD
+                snapshot, the hevd module, libFuzzer's mutator (bit-exact
+                restatement), --limit 10000000, --max_len 1028, >= 10 s of
+                node wall time, with its own roofline and twin baseline.
+  syn           BASELINE.json configs[1]: the ring-3 ALU/branch/load-store
+                interpreter microbench, 65,536 lanes, with its roofline and the
+                C oracle's rate on the host cores.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -47,93 +51,109 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "execs/sec + emulated instr/s per node (tlv_server, HEVD) at 1/2/4/8 GPUs"
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_k_run.json")
+PROFILES = os.path.join(ROOT, "profiles")
+WTFGPU = os.path.join(ROOT, "wtf_amd", "host", "wtfgpu")
+TWIN = os.path.join(ROOT, "oracle", "wtf_twin")
+
+TARGETS = {
+    # name: (snapshot builder module, workload text, --max_len)
+    "tlv_server": ("wtf_amd.tools.tlv", "fuzzer_tlv_server on the synthetic tlv_server snapshot "
+                                        "(BASELINE.json configs[2]/[3]), tlv CustomMutator_t, seed 1337", 0x1000),
+    "hevd": ("wtf_amd.tools.hevd", "fuzzer_hevd on the synthetic ring-0 HEVD snapshot (BASELINE.json configs[4] "
+                                   "on one GPU), libFuzzer MutationDispatcher, seed 1337", 1028),
+}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--lanes", type=int, default=65536)
     ap.add_argument("--limit", type=int, default=100000)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (wall)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--hevd-limit", type=int, default=10_000_000, help="BASELINE.md: HEVD runs --limit 10000000")
+    ap.add_argument("--leg-seconds", type=float, default=10.0, help="GPU wall window of the hevd leg")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall window of each CPU baseline")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host CPU share (see cpu_cores)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-tlv", action="store_true", help="skip the tlv_server and hevd legs")
-    ap.add_argument("--tlv-batches", type=int, default=6)
-    ap.add_argument("--tlv-cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-legs", action="store_true", help="headline only (skip hevd / syn)")
     return ap.parse_args()
 
 
-# ----------------------------------------------------------------- tlv_server / hevd legs
-FUZZ_TARGETS = {
-    # name: (snapshot builder module, workload text, --max_len)
-    "tlv_server": ("wtf_amd.tools.tlv", "synthetic tlv_server snapshot (BASELINE.json configs[2]), tlv mutator", 0x1000),
-    "hevd": ("wtf_amd.tools.hevd", "synthetic HEVD ring-0 snapshot (BASELINE.json configs[4] on one GPU), "
-                                   "default libFuzzer-style mutator", 1028),
-}
+def cpu_cores() -> tuple[int, dict]:
+    """Host threads the CPU baselines use: the CPU share the job may use
+    (OMP_NUM_THREADS when the environment sets it, as the GPU box does, else
+    the affinity mask), recorded with the machine's counts."""
+    aff = len(os.sched_getaffinity(0))
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    use = min(aff, env) if env > 0 else aff
+    return use, {"os_cpu_count": os.cpu_count(), "affinity": aff, "omp_num_threads": env or None, "used": use}
 
 
-def fuzz_leg(name: str, lanes: int, batches: int, cpu_seconds: float, cores: int, limit: int, run_cpu: bool,
-             gpu_exe: str | None = None):
-    """wtfgpu fuzz on a synthetic snapshot (one GPU), and the oracle twin on
-    `cores` host processes (one wtf_twin fuzz client per core) over a bounded
-    wall window."""
+def build_target(name: str, d: str) -> str:
     import importlib
-    import shutil
-    import subprocess
-    import tempfile
 
-    modname, workload, max_len = FUZZ_TARGETS[name]
-    mod = importlib.import_module(modname)
-    wtfgpu = gpu_exe or os.path.join(ROOT, "wtf_amd", "host", "wtfgpu")
-    twin = os.path.join(ROOT, "oracle", "wtf_twin")
-    tmp = tempfile.mkdtemp(prefix=f"wtf_{name}_")
+    mod = importlib.import_module(TARGETS[name][0])
+    mod.build(os.path.join(d, "state"), os.path.join(d, "work"))
+    mod.seed_inputs(os.path.join(d, "inputs"))
+    return d
+
+
+def load_pmc(name: str, lanes: int, limit: int) -> dict | None:
+    """The committed rocprofv3 PMC summary of k_run on this workload (made by
+    scripts/pmc_summary.py from the profiles/ CSVs), if its config matches."""
+    p = os.path.join(PROFILES, f"pmc_{name}_k_run.json")
     try:
-        base = os.path.join(tmp, "t0")
-        mod.build(os.path.join(base, "state"), os.path.join(base, "work"))
-        mod.seed_inputs(os.path.join(base, "inputs"))
-        out = subprocess.run([wtfgpu, "fuzz", "--name", name, "--target", base, "--lanes", str(lanes),
-                              "--runs", str(lanes * batches), "--seed", "1337", "--limit", str(limit),
-                              "--max_len", str(max_len)],
-                             check=True, capture_output=True, text=True, timeout=600).stdout
-        g = json.loads([x for x in out.splitlines() if x.startswith("{")][-1])
-        res = {"workload": workload + ", seed 1337", "lanes": lanes, "execs": g["execs"], "wall_s": g["wall_s"],
-               "value": g["execs"] / g["wall_s"], "unit": "execs/s",
-               "instr_per_s": g["retired"] / g["wall_s"], "instr_per_exec": g["retired"] / max(1, g["execs"]),
-               "unique_crashes": g["unique_crashes"], "coverage": g["coverage"], "errors": g["errors"],
-               "gpu_retired_fraction": 1.0 - g["errors"] / max(1, g["execs"]), "backend": g["backend"]}
-        if run_cpu:
-            procs = []
-            for i in range(cores):
-                d = os.path.join(tmp, f"c{i}")
-                shutil.copytree(base, d, ignore=shutil.ignore_patterns("outputs", "crashes", "work"))
-                procs.append(subprocess.Popen([twin, "fuzz", "--name", name, "--target", d, "--lanes", "1024",
-                                               "--seconds", str(cpu_seconds), "--seed", str(1337 + i),
-                                               "--limit", str(limit), "--max_len", str(max_len)],
-                                              stdout=subprocess.PIPE, text=True))
-            execs = instr = 0.0
-            wall = 0.0
-            for p in procs:
-                o, _ = p.communicate(timeout=cpu_seconds * 4 + 120)
-                t = json.loads([x for x in o.splitlines() if x.startswith("{")][-1])
-                execs += t["execs"]
-                instr += t["retired"]
-                wall = max(wall, t["wall_s"])
-            res["cpu_baseline"] = {"value": execs / wall, "unit": "execs/s", "instr_per_s": instr / wall,
-                                   "cores": cores, "kind": "port",
-                                   "sample": f"{int(execs)} {name} testcases over {wall:.1f}s, {cores} wtf_twin fuzz "
-                                             f"processes (oracle behind Backend_t, one per core)"}
-            res["vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
-        return res
+        pmc = json.load(open(p))
+    except (OSError, ValueError):
+        return None
+    if pmc.get("lanes") != lanes or pmc.get("limit") != limit:
+        return None
+    return pmc
+
+
+def roofline(alg_bytes: float, launches: float, kernel_ms: float, pmc: dict | None) -> dict:
+    avg_s = kernel_ms / 1e3 / max(1.0, launches)
+    per_launch = alg_bytes / max(1.0, launches)
+    achieved = per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+            "kernel": "k_run", "alg_bytes_per_launch": per_launch, "avg_launch_ms": avg_s * 1e3,
+            "valu_util": pmc.get("valu_util") if pmc else None,
+            "wait_frac": pmc.get("wait_frac") if pmc else None}
+
+
+# ----------------------------------------------------------------- CPU baselines
+def twin_baseline(name: str, base: str, seconds: float, cores: int, limit: int) -> dict:
+    """One `wtf_twin fuzz` client per host core (the reference's one node per
+    core), seeds 1337 + i, for `seconds` of wall time."""
+    max_len = TARGETS[name][2]
+    tmp = tempfile.mkdtemp(prefix=f"twin_{name}_")
+    try:
+        procs = []
+        for i in range(cores):
+            d = os.path.join(tmp, f"c{i}")
+            shutil.copytree(base, d, ignore=shutil.ignore_patterns("outputs", "crashes", "work"))
+            procs.append(subprocess.Popen([TWIN, "fuzz", "--name", name, "--target", d, "--lanes", "1024",
+                                           "--seconds", str(seconds), "--seed", str(1337 + i), "--limit", str(limit),
+                                           "--max_len", str(max_len)], stdout=subprocess.PIPE, text=True,
+                                          env={**os.environ, "OMP_NUM_THREADS": "1"}))
+        execs = instr = wall = 0.0
+        for p in procs:
+            o, _ = p.communicate(timeout=seconds * 4 + 300)
+            t = json.loads([x for x in o.splitlines() if x.startswith("{")][-1])
+            execs += t["execs"]
+            instr += t["retired"]
+            wall = max(wall, t["wall_s"])
+        return {"value": execs / wall, "unit": "execs/s", "instr_per_s": instr / wall, "cores": cores, "kind": "port",
+                "sample": f"{int(execs)} {name} testcases over {wall:.1f}s: {cores} wtf_twin fuzz processes, one per "
+                          f"host core (the C oracle behind Backend_t; bochscpu is unbuildable, SURVEY F2)"}
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-# ----------------------------------------------------------------- CPU baseline
-def cpu_baseline(seconds: float, threads: int, limit: int):
-    """The C oracle (tests/oracle_lib, TEST INFRASTRUCTURE) on the same SYN
+def syn_cpu_baseline(seconds: float, threads: int, limit: int) -> dict:
+    """The C oracle (tests/oracle_lib, TEST INFRASTRUCTURE) on the SYN
     workload: each thread owns one oracle machine and runs testcases
     restore -> insert -> run back to back until the time budget is spent."""
     import threading
@@ -181,19 +201,90 @@ def cpu_baseline(seconds: float, threads: int, limit: int):
     execs = sum(c[0] for c in counts)
     instr = sum(c[1] for c in counts)
     assert not bad, f"oracle exits {set(bad)}"
-    return {"value": execs / dt, "unit": "execs/s", "instr_per_s": instr / dt, "cores": threads,
-            "kind": "port",
+    return {"value": execs / dt, "unit": "execs/s", "instr_per_s": instr / dt, "cores": threads, "kind": "port",
             "sample": f"{execs} SYN testcases ({instr} instructions) over {dt:.1f}s, {threads} threads, "
                       f"one C-oracle machine per thread (bochscpu unbuildable: SURVEY F2)"}
 
 
-# ----------------------------------------------------------------- coverage merge
-class _DevBuf:
-    """__cuda_array_interface__ view of an engine device buffer (for RCCL)."""
+# ----------------------------------------------------------------- GPU legs
+def node_fields(s0: dict, s1: dict) -> dict:
+    """Kernel-efficiency evidence of a node over [s0, s1]."""
+    d = {k: s1[k] - s0[k] for k in s1}
+    return {
+        "lanes_per_wave_step": d["retired"] / max(1, d["group_steps"]),
+        "gpu_retired_fraction": (d["retired"] - d["error_retired"]) / max(1, d["retired"]),
+        "kernel_ms": d["kernel_ms"], "kernel_launches": d["kernel_launches"], "group_steps": d["group_steps"],
+        "breakpoint_hits": d["breakpoint_hits"], "rounds": d["rounds"], "insert_ms": d["insert_ms"],
+        "coverage_ms": d["coverage_ms"], "service_ms": d["service_ms"], "node_ms": d["total_ms"],
+        "merge_ms": d["merge_ms"], "errors": d["errors"], "alg_bytes": d["alg_bytes"],
+    }
 
-    def __init__(self, ptr, nbytes):
-        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
-                                         "version": 2, "strides": None}
+
+def hevd_leg(base: str, lanes: int, limit: int, seconds: float) -> dict:
+    """`wtfgpu fuzz` (the product node binary) on HEVD for `seconds` of wall time."""
+    out = subprocess.run([WTFGPU, "fuzz", "--name", "hevd", "--target", base, "--lanes", str(lanes),
+                          "--seconds", str(seconds), "--seed", "1337", "--limit", str(limit), "--max_len", "1028"],
+                         check=True, capture_output=True, text=True, timeout=seconds * 6 + 300).stdout
+    g = json.loads([x for x in out.splitlines() if x.startswith("{")][-1])
+    b = g["backend"]
+    pmc = load_pmc("hevd", lanes, limit)
+    return {"workload": TARGETS["hevd"][1], "lanes": lanes, "limit": limit, "execs": g["execs"],
+            "wall_s": g["wall_s"], "value": g["execs"] / g["wall_s"], "unit": "execs/s",
+            "instr_per_s": g["retired"] / g["wall_s"], "instr_per_exec": g["retired"] / max(1, g["execs"]),
+            "unique_crashes": g["unique_crashes"], "coverage": g["coverage"], "errors": g["errors"],
+            "gpu_retired_fraction": (g["retired"] - g["error_retired"]) / max(1, g["retired"]),
+            "lanes_per_wave_step": g["retired"] / max(1, b["group_steps"]),
+            "roofline": roofline(b["alg_bytes"], b["kernel_launches"], b["kernel_ms"], pmc), "backend": b}
+
+
+def syn_leg(lanes: int, limit: int, steps: int, device: int) -> dict:
+    from tests.syn_harness import make_engine
+    from wtf_amd.abi import EXIT_BREAKPOINT
+    from wtf_amd.tools import syn
+
+    eng, sp, st = make_engine(lanes, limit=limit, device=device)
+    eng.restore()
+    base = eng.read_gprs(0, 1)[0].copy()
+    pool = syn.inputs(lanes * 4, seed=syn.SEED)
+    acc = {"execs": 0, "retired": 0, "kernel_ms": 0.0, "launches": 0, "bytes": 0, "steps": 0, "bad": 0}
+
+    def step(i, record):
+        off = (i * 7919) % (3 * lanes)
+        inp = pool[off:off + lanes]
+        eng.restore()
+        g = np.tile(base, (lanes, 1))
+        syn.insert(g, inp)
+        eng.write_gprs(g)
+        rs = eng.run()
+        ex = eng.exits_np()
+        cov, _ = eng.coverage()
+        new = set().union(*cov.values()) if cov else set()
+        if new:
+            eng.commit_coverage(new)
+        if record:
+            acc["execs"] += lanes
+            acc["retired"] += rs.lane_retired
+            acc["kernel_ms"] += rs.kernel_ms
+            acc["launches"] += rs.kernel_launches
+            acc["steps"] += rs.group_steps
+            acc["bytes"] += int(eng.nbytes().sum())
+            acc["bad"] += int(np.count_nonzero(ex["status"] != EXIT_BREAKPOINT))
+
+    step(0, False)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(1 + i, True)
+    dt = time.perf_counter() - t0
+    eng.close()
+    if acc["bad"]:
+        raise SystemExit(f"SYN: {acc['bad']} testcases did not reach the exit breakpoint")
+    return {"workload": "SYN: synthetic ring-3 ALU/branch/load-store loop snapshot (BASELINE.json configs[1]), "
+                        "uniform random 64-byte inputs",
+            "lanes": lanes, "limit": limit, "steps": steps, "value": acc["execs"] / dt, "unit": "execs/s",
+            "instr_per_s": acc["retired"] / dt, "instr_per_exec": acc["retired"] / max(1, acc["execs"]),
+            "ms_per_step": dt * 1e3 / steps, "lanes_per_wave_step": acc["retired"] / max(1, acc["steps"]),
+            "gpu_retired_fraction": 1.0,
+            "roofline": roofline(acc["bytes"], acc["launches"], acc["kernel_ms"], load_pmc("syn", lanes, limit))}
 
 
 def main():
@@ -201,112 +292,66 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        a.gpus = world
+    a.gpus = world
+    tmp = tempfile.mkdtemp(prefix=f"wtfbench_r{rank}_")
+    try:
+        run(a, rank, world, local, tmp)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
-    # CPU baseline first (rank 0, N=1), before anything touches the GPU
-    cpu = None
+
+def run(a, rank, world, local, tmp):
+    # snapshots + CPU baselines first (rank 0, N = 1), before anything touches the GPU
+    tlv_dir = build_target("tlv_server", os.path.join(tmp, "tlv"))
+    legs = rank == 0 and world == 1 and not a.no_legs
+    hevd_dir = build_target("hevd", os.path.join(tmp, "hevd")) if legs else None
+    cores, core_info = cpu_cores()
+    if a.cpu_threads:
+        cores = a.cpu_threads
+    cpu = {}
     if rank == 0 and world == 1 and not a.no_cpu:
-        threads = a.cpu_threads or min(16, os.cpu_count() or 1)
-        cpu = cpu_baseline(a.cpu_seconds, threads, a.limit)
+        cpu["tlv_server"] = twin_baseline("tlv_server", tlv_dir, a.cpu_seconds, cores, a.limit)
+        if legs:
+            cpu["hevd"] = twin_baseline("hevd", hevd_dir, a.cpu_seconds, cores, a.hevd_limit)
+            cpu["syn"] = syn_cpu_baseline(a.cpu_seconds, cores, a.limit)
 
     import torch
 
+    from wtf_amd import node as wn
+    from wtf_amd import shard
+
+    torch.cuda.set_device(local)
     dist = None
+    rccl_id = None
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world)  # control plane only
+        rccl_id = shard.share_bytes(wn.rccl_unique_id() if rank == 0 else None, dist)
 
-    from tests.syn_harness import make_engine
-    from wtf_amd.abi import EXIT_BREAKPOINT
-    from wtf_amd import shard
-    from wtf_amd.tools import syn
-
-    n = a.lanes
-    eng, sp, st = make_engine(n, limit=a.limit, device=local)
-    eng.restore()
-    base = eng.read_gprs(0, 1)[0].copy()
-
-    cov_t = None
-    if dist is not None:
-        import ctypes as C
-
-        p, nb = C.c_void_p(), C.c_uint64()
-        eng.L.wtfgpu_coverage_device_map(eng.ctx, C.byref(p), C.byref(nb))
-        cov_t = torch.as_tensor(_DevBuf(p.value, nb.value), device=f"cuda:{local}")
-
-    rng_seed = shard.rank_seed(syn.SEED, rank)
-    pool = syn.inputs(n * 4, seed=rng_seed)  # input pool; each step takes a rotating window
-
-    stats = {"execs": 0, "retired": 0, "kernel_ms": 0.0, "launches": 0, "bytes_alg": 0, "dirty": 0,
-             "input_bytes": 0, "newcov": 0, "bad": 0}
-
-    def step(i, record):
-        off = (i * 7919) % (3 * n)
-        inp = pool[off:off + n]
-        eng.restore()
-        g = np.tile(base, (n, 1))
-        syn.insert(g, inp)
-        eng.write_gprs(g)
-        rs = eng.run()
-        ex = eng.exits_np()
-        ok = int(np.count_nonzero(ex["status"] == EXIT_BREAKPOINT))
-        cov, _ovf = eng.coverage()
-        new = set()
-        for s in cov.values():
-            new |= s
-        if new:
-            eng.commit_coverage(new)
-        if cov_t is not None:
-            torch.cuda.synchronize()
-            shard.merge_coverage_map(cov_t, dist)
-            torch.cuda.synchronize()
-        if record:
-            nb = eng.nbytes()
-            stats["execs"] += n
-            stats["retired"] += rs.lane_retired
-            stats["kernel_ms"] += rs.kernel_ms
-            stats["launches"] += rs.kernel_launches
-            stats["bytes_alg"] += int(nb.sum())
-            stats["dirty"] += n  # SYN: every testcase dirties exactly its scratch page
-            stats["input_bytes"] += n * syn.INPUT_SIZE
-            stats["newcov"] += len(new)
-            stats["bad"] += n - ok
-
-    for i in range(a.warmup):
-        step(i, False)
+    node = wn.Node("tlv_server", tlv_dir, a.lanes, a.limit, seed=1337, max_len=TARGETS["tlv_server"][2],
+                   device=local, rank=rank, world=world, rccl_id=rccl_id)
+    for _ in range(a.warmup):
+        node.step()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
+    s0 = node.stats()
     t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(a.warmup + i, True)
+    for _ in range(a.steps):
+        node.step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
-
-    dt, execs, retired = shard.job_totals(dt, float(stats["execs"]), float(stats["retired"]), dist,
-                                          device=f"cuda:{local}")
-
-    if stats["bad"]:
-        raise SystemExit(f"{stats['bad']} testcases did not reach the exit breakpoint")
+    s1 = node.stats()
+    execs, retired = s1["execs"] - s0["execs"], s1["retired"] - s0["retired"]
+    dt, execs, retired = shard.job_totals(dt, float(execs), float(retired), dist)
+    fields = node_fields(s0, s1)
+    summary = node.summary()
+    node.close()
 
     if rank == 0:
-        avg_launch_s = stats["kernel_ms"] / 1e3 / max(1, stats["launches"])
-        bytes_per_launch = stats["bytes_alg"] / max(1, stats["launches"])
-        achieved = bytes_per_launch / avg_launch_s / 1e9
-        traffic = None
-        if os.path.exists(PMC_SUMMARY):
-            try:
-                pmc = json.load(open(PMC_SUMMARY))
-                if pmc.get("lanes") == n and pmc.get("limit") == a.limit:
-                    traffic = pmc.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        b_exec = stats["bytes_alg"] + stats["input_bytes"] + 2 * 4096 * stats["dirty"]
         out = {
             "metric": METRIC,
             "value": execs / dt,
@@ -320,31 +365,34 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
-            "data": "synthetic (SYN ring-3 snapshot built in-process; uniform random 64-byte inputs)",
-            "config": {"workload": "SYN: synthetic ring-3 ALU/branch/load-store loop snapshot "
-                                   "(BASELINE.json configs[1])",
-                       "lanes_per_gpu": n, "limit": a.limit, "input_bytes": syn.INPUT_SIZE,
-                       "parallelism": f"shard{world} (independent testcases) + RCCL MAX coverage merge"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_run", "alg_bytes_per_launch": bytes_per_launch,
-                         "avg_launch_ms": avg_launch_s * 1e3},
-            "gpu_kernel_ms_per_step": stats["kernel_ms"] / a.steps,
-            "instr_per_exec": stats["retired"] / max(1, stats["execs"]),
-            "b_exec_gbs_wall": b_exec / (dt if world == 1 else dt) / 1e9,
-            "gpu_retired_fraction": 1.0,
-            "cpu_baseline": cpu,
+            "data": "synthetic (tlv_server look-alike snapshot built in-process; the tlv module's CustomMutator_t "
+                    "over its seed corpus)",
+            "config": {"workload": TARGETS["tlv_server"][1], "lanes_per_gpu": a.lanes, "limit": a.limit,
+                       "max_len": TARGETS["tlv_server"][2],
+                       "parallelism": f"shard{world}: one node per GPU (seed + rank), RCCL MAX coverage-map "
+                                      f"merge per batch"},
+            "instr_per_exec": retired / max(1.0, execs),
+            "roofline": roofline(fields["alg_bytes"], fields["kernel_launches"], fields["kernel_ms"],
+                                 load_pmc("tlv", a.lanes, a.limit)),
+            **{k: fields[k] for k in ("lanes_per_wave_step", "gpu_retired_fraction")},
+            "node": {k: v for k, v in fields.items() if k not in ("lanes_per_wave_step", "gpu_retired_fraction")},
+            "coverage": summary["coverage"], "unique_crashes": summary["unique_crashes"],
+            "cpu_baseline": cpu.get("tlv_server"),
+            "host_cpus": core_info,
         }
-        if world == 1 and not a.no_tlv:
-            eng.close()
-            eng = None
-            cores = a.cpu_threads or min(16, os.cpu_count() or 1)
-            out["tlv"] = fuzz_leg("tlv_server", a.lanes, a.tlv_batches, a.tlv_cpu_seconds, cores, a.limit,
-                                  not a.no_cpu)
-            out["hevd"] = fuzz_leg("hevd", a.lanes, a.tlv_batches, a.tlv_cpu_seconds, cores, a.limit, not a.no_cpu)
+        if out["cpu_baseline"]:
+            out["vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+        if legs:
+            h = hevd_leg(hevd_dir, a.lanes, a.hevd_limit, a.leg_seconds)
+            if "hevd" in cpu:
+                h["cpu_baseline"] = cpu["hevd"]
+                h["vs_cpu"] = h["value"] / cpu["hevd"]["value"]
+            out["hevd"] = h
+            s = syn_leg(a.lanes, a.limit, 10, local)
+            if "syn" in cpu:
+                s["cpu_baseline"] = cpu["syn"]
+            out["syn"] = s
         print(json.dumps(out), flush=True)
-    if eng is not None:
-        eng.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -31,7 +31,8 @@
  *   wtfgpu_read_coverage      <- AggregatedCodeCoverage_/LastNewCoverage_
  *                                (bochscpu_backend.cc:501-504, :1001-1016)
  *   wtfgpu_commit_coverage    <- AggregatedCodeCoverage_.emplace (bochscpu_backend.cc:501)
- *   wtfgpu_coverage_device_map <- the per-GPU coverage bitmap merged with RCCL MAX (new).
+ *   wtfgpu_coverage_device_map, wtfgpu_coverage_absorb
+ *                             <- the per-GPU coverage bitmap merged with RCCL MAX (new).
  */
 #ifndef WTFGPU_H
 #define WTFGPU_H
@@ -305,6 +306,11 @@ int wtfgpu_commit_coverage(wtfgpu_ctx *ctx, const uint64_t *rips, uint64_t n);
 int wtfgpu_reset_coverage(wtfgpu_ctx *ctx);
 /* Device pointer + size of the uint8 coverage map (for an RCCL MAX all-reduce). */
 int wtfgpu_coverage_device_map(wtfgpu_ctx *ctx, void **dev_ptr, uint64_t *bytes);
+/* After a MAX all-reduce of the map (other shards' coverage merged in): the
+ * RIPs set in the map since the last absorb, excluding this context's own
+ * wtfgpu_commit_coverage calls, sorted; *n gets the count. cap = 0 only
+ * counts; a call with cap >= that count also marks them seen. */
+int wtfgpu_coverage_absorb(wtfgpu_ctx *ctx, uint64_t *rips, uint64_t cap, uint64_t *n);
 /* Host copy of the coverage map's set bytes as RIPs. */
 int wtfgpu_coverage_rips(wtfgpu_ctx *ctx, uint64_t *rips, uint64_t cap, uint64_t *n);
 

@@ -18,6 +18,9 @@
 #include "x86_oracle.h"
 #include "../wtf_amd/host/kdmp.h"
 #include "../wtf_amd/host/blake3_lite.h"
+#include "../wtf_amd/host/net_exchange.h"
+
+#include <memory>
 
 using namespace wtfgpu_host;
 
@@ -62,6 +65,17 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
   std::unordered_set<Gva_t> last_new_;
   uint64_t retired_total_ = 0;
   uint64_t inject_ = ~0ull;  // page to #PF after the current handler
+  // coverage map over the executable-page slots (ExecutablePages, as the gpu
+  // backend builds it) and its shadow, for the shard merge
+  std::unordered_map<uint64_t, uint32_t> slot_;
+  std::vector<uint64_t> slot_vpn_;
+  std::vector<uint8_t> map_, shadow_;
+  void map_set(uint64_t rip) {
+    auto it = slot_.find(rip >> 12);
+    if (it == slot_.end()) return;
+    const uint64_t at = (uint64_t)it->second * 4096 + (rip & 0xfff);
+    map_[at] = shadow_[at] = 1;
+  }
 
   wtfgpu_regs_t regs() const {
     wtfgpu_regs_t r;
@@ -80,6 +94,10 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
   }
   bool Initialize(const Options_t &Opts, const CpuState_t &CpuState) override {
     if (!dump_.Parse(Opts.DumpPath.string())) return false;
+    slot_vpn_ = ExecutablePages(dump_, CpuState.Cr3);
+    for (uint32_t i = 0; i < slot_vpn_.size(); i++) slot_.emplace(slot_vpn_[i], i);
+    map_.assign(slot_vpn_.size() * 4096, 0);
+    shadow_.assign(map_.size(), 0);
     m_ = orc_create();
     for (auto &[gpfn, page] : dump_.Pages()) orc_add_page(m_, gpfn, page);
     if (Opts.Limit) orc_set_limit(m_, Opts.Limit);
@@ -130,6 +148,8 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
     if (full_) aggregate_.clear();
     for (uint64_t r : cov)
       if (aggregate_.insert(r).second) last_new_.insert(Gva_t(r));
+    if (!full_)
+      for (const Gva_t &g : last_new_) map_set(g.U64());
     retired_total_ += orc_icount(m_);
     return result_;
   }
@@ -223,7 +243,11 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
   }
   const std::unordered_set<Gva_t> &LastNewCoverage() const override { return last_new_; }
   bool RevokeLastNewCoverage() override {
-    for (const Gva_t &g : last_new_) aggregate_.erase(g.U64());
+    for (const Gva_t &g : last_new_) {
+      aggregate_.erase(g.U64());
+      auto it = slot_.find(g.U64() >> 12);
+      if (it != slot_.end()) map_[(uint64_t)it->second * 4096 + (g.U64() & 0xfff)] = shadow_[(uint64_t)it->second * 4096 + (g.U64() & 0xfff)] = 0;
+    }
     last_new_.clear();
     return true;
   }
@@ -234,6 +258,23 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
   void ResetCoverage() override {
     aggregate_.clear();
     last_new_.clear();
+    std::fill(map_.begin(), map_.end(), 0);
+    std::fill(shadow_.begin(), shadow_.end(), 0);
+  }
+  bool CoverageMap(uint8_t **Map, uint64_t *Bytes, bool *Device) override {
+    *Map = map_.data();
+    *Bytes = map_.size();
+    *Device = false;
+    return true;
+  }
+  size_t AbsorbCoverageMap() override {
+    size_t added = 0;
+    for (size_t i = 0; i < map_.size(); i++)
+      if (map_[i] && !shadow_[i]) {
+        shadow_[i] = 1;
+        added += aggregate_.insert((slot_vpn_[i / 4096] << 12) | (i % 4096)).second;
+      }
+    return added;
   }
   bool full_ = false;
   bool engine_error_ = false;
@@ -307,8 +348,21 @@ int main(int argc, char **argv) {
     void SetFullCoverage(bool On) override { b->SetFullCoverage(On); }
     size_t CoverageSize() const override { return b->CoverageSize(); }
     std::string StatsJson() const override { return b->StatsJson(); }
+    bool CoverageMap(uint8_t **M, uint64_t *N, bool *D) override { return b->CoverageMap(M, N, D); }
+    size_t AbsorbCoverageMap() override { return b->AbsorbCoverageMap(); }
   } E;
   E.b = B;
   E.n = O.lanes ? O.lanes : 1;
-  return RunnerMain(O, E, Opts, State);
+  // CPU shards merge their host coverage maps over TCP (net_exchange.cc)
+  std::unique_ptr<TcpExchange_t> X;
+  if (O.world > 1) {
+    const size_t colon = O.exchange.rfind(':');
+    X = std::make_unique<TcpExchange_t>(O.rank, O.world);
+    if (colon == std::string::npos ||
+        !X->Connect(O.exchange.substr(0, colon), (uint16_t)atoi(O.exchange.c_str() + colon + 1))) {
+      printf("coverage exchange %s failed\n", O.exchange.c_str());
+      return 1;
+    }
+  }
+  return RunnerMain(O, E, Opts, State, X.get());
 }

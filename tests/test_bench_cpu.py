@@ -1,6 +1,5 @@
-"""bench.py's fuzz legs on the CPU: the plumbing (snapshot build, node run,
-per-core twin clients, JSON fields) with the oracle twin standing in for the
-gpu node."""
+"""bench.py's plumbing on the CPU: snapshot builds, the one-process-per-core
+twin baselines, and the JSON field arithmetic (roofline, node fields)."""
 import os
 
 import pytest
@@ -12,10 +11,25 @@ TWIN = os.path.join(bench.ROOT, "oracle", "wtf_twin")
 
 @pytest.mark.skipif(not os.path.exists(TWIN), reason="oracle/wtf_twin not built")
 @pytest.mark.parametrize("name", ["tlv_server", "hevd"])
-def test_fuzz_leg_fields(name):
-    r = bench.fuzz_leg(name, lanes=256, batches=2, cpu_seconds=1.0, cores=2, limit=100000, run_cpu=True,
-                       gpu_exe=TWIN)
-    assert r["execs"] == 512 and r["value"] > 0 and r["errors"] == 0
-    cb = r["cpu_baseline"]
-    assert cb["cores"] == 2 and cb["kind"] == "port" and cb["value"] > 0
-    assert r["vs_cpu"] == pytest.approx(r["value"] / cb["value"])
+def test_twin_baseline_fields(name, tmp_path):
+    d = bench.build_target(name, str(tmp_path / name))
+    cb = bench.twin_baseline(name, d, seconds=1.0, cores=2, limit=100000)
+    assert cb["cores"] == 2 and cb["kind"] == "port" and cb["value"] > 0 and cb["instr_per_s"] > 0
+
+
+def test_roofline_and_node_fields():
+    r = bench.roofline(alg_bytes=8e9, launches=4, kernel_ms=100.0, pmc=None)
+    assert r["achieved"] == pytest.approx(2e9 / 0.025 / 1e9)
+    assert r["frac"] == pytest.approx(r["achieved"] / 8000.0) and r["traffic"] is None
+    keys = ("execs retired batches crashes unique_crashes timeouts cr3 errors coverage corpus merged_rips "
+            "kernel_launches group_steps alg_bytes breakpoint_hits rounds error_retired run_s kernel_ms "
+            "merge_ms insert_ms coverage_ms service_ms total_ms").split()
+    s0 = {k: 0 for k in keys}
+    s1 = dict(s0, retired=6400, group_steps=200, error_retired=64, kernel_launches=2, kernel_ms=5.0)
+    f = bench.node_fields(s0, s1)
+    assert f["lanes_per_wave_step"] == 32 and f["gpu_retired_fraction"] == pytest.approx(0.99)
+
+
+def test_cpu_cores_reports_share():
+    used, info = bench.cpu_cores()
+    assert used >= 1 and info["used"] == used and info["os_cpu_count"] >= 1

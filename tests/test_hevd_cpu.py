@@ -80,3 +80,22 @@ def test_fuzz_default_mutator(target):
     st = H.fuzz(H.TWIN, target, runs=4000, lanes=512, name="hevd", max_len=1028)
     assert st["execs"] == 4000 and st["errors"] == 0
     assert st["unique_crashes"] >= 1 and st["coverage"] > 200
+
+
+def test_parallel_mutation_is_deterministic(target, tmp_path):
+    """Batches of >= 8192 new testcases are mutated in fixed chunks on the host
+    threads (runner.cc MakeBatch): the corpus and crash set of a seed must not
+    depend on the thread count."""
+    import shutil
+    import subprocess
+
+    out = []
+    for threads in ("1", "4"):
+        d = str(tmp_path / f"t{threads}")
+        shutil.copytree(target, d, ignore=shutil.ignore_patterns("outputs", "crashes", "work"))
+        subprocess.run([H.TWIN, "fuzz", "--name", "hevd", "--target", d, "--runs", "24576", "--lanes", "8192",
+                        "--seed", "7", "--limit", "100000", "--max_len", "1028"], check=True, capture_output=True,
+                       timeout=600, env={**os.environ, "OMP_NUM_THREADS": threads})
+        out.append((sorted(os.listdir(os.path.join(d, "outputs"))), sorted(os.listdir(os.path.join(d, "crashes")))))
+    assert out[0] == out[1]
+    assert len(out[0][0]) > 10

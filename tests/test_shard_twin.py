@@ -1,0 +1,73 @@
+"""Multi-shard fuzzing on the CPU (the GPU node does the same with
+RCCL, rccl_exchange.cc): two `wtf_twin fuzz` ranks, each an independent shard
+(seed + rank, its own corpus), merge their coverage maps after every batch
+through the node's CoverageExchange_t (TCP on the CPU, net_exchange.cc).
+
+  * both ranks end with the same aggregate coverage: the union;
+  * each rank absorbed rips the other one found (merged_rips > 0) and kept
+    only its own testcases in its corpus;
+  * the union is at least what either shard alone covers.
+"""
+import json
+import os
+import shutil
+import socket
+import subprocess
+
+import pytest
+
+from tests import tlv_harness as H
+
+pytestmark = pytest.mark.skipif(not os.path.exists(H.TWIN), reason="oracle/wtf_twin not built")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _fuzz_cmd(d, rank, world, port, runs=3072, lanes=512):
+    return [H.TWIN, "fuzz", "--name", "tlv_server", "--target", d, "--runs", str(runs), "--lanes", str(lanes),
+            "--seed", "1337", "--limit", "100000", "--rank", str(rank), "--world", str(world),
+            "--exchange", f"127.0.0.1:{port}"]
+
+
+def _last_json(out):
+    return json.loads([x for x in out.splitlines() if x.startswith("{")][-1])
+
+
+@pytest.fixture(scope="module")
+def base(tmp_path_factory):
+    return H.build_target(str(tmp_path_factory.mktemp("tlv_shards")))
+
+
+def test_two_twin_shards_merge_coverage(base, tmp_path):
+    # the shards start from different seed inputs, so each finds code the
+    # other has not run yet
+    seeds = sorted(os.listdir(os.path.join(base, "inputs")))
+    dirs = []
+    for r in range(2):
+        d = str(tmp_path / f"r{r}")
+        shutil.copytree(base, d, ignore=shutil.ignore_patterns("outputs", "crashes", "work"))
+        for i, name in enumerate(seeds):
+            if i % 2 != r:
+                os.remove(os.path.join(d, "inputs", name))
+        dirs.append(d)
+    port = _free_port()
+    procs = [subprocess.Popen(_fuzz_cmd(dirs[r], r, 2, port), stdout=subprocess.PIPE, text=True) for r in range(2)]
+    res = [_last_json(p.communicate(timeout=300)[0]) for p in procs]
+    assert all(p.returncode == 0 for p in procs)
+    assert [r["rank"] for r in res] == [0, 1] and all(r["world"] == 2 for r in res)
+    assert res[0]["coverage"] == res[1]["coverage"]
+    assert all(r["merged_rips"] > 0 for r in res)
+    # corpora stay per shard: rank 1's seed differs, so its corpus differs
+    c0, c1 = (set(os.listdir(os.path.join(d, "outputs"))) for d in dirs)
+    assert c0 != c1
+    # one shard alone (same seed as rank 0) covers no more than the union
+    solo = str(tmp_path / "solo")
+    shutil.copytree(base, solo, ignore=shutil.ignore_patterns("outputs", "crashes", "work"))
+    one = subprocess.run(_fuzz_cmd(solo, 0, 1, port), capture_output=True, text=True, timeout=300, check=True)
+    assert _last_json(one.stdout)["coverage"] <= res[0]["coverage"]

@@ -142,6 +142,7 @@ def load_hip_library(path: str = LIB_PATH) -> C.CDLL:
         "wtfgpu_gather_pages": ([P, C.POINTER(U32), C.POINTER(U64), U32, P], C.c_int),
         "wtfgpu_lane_get_cr": ([P, U32, U32, C.POINTER(U64)], C.c_int),
         "wtfgpu_lane_set_cr": ([P, U32, U32, U64], C.c_int),
+        "wtfgpu_coverage_absorb": ([P, C.POINTER(U64), U64, C.POINTER(U64)], C.c_int),
     }
     for name, (args, ret) in sig.items():
         fn = getattr(lib, name)

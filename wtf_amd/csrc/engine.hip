@@ -1131,6 +1131,25 @@ __global__ void k_cov_collect(Dev P, u32 first, u32 count, u32 *out_lane, u64 *o
   }
 }
 
+// Bytes set in the coverage map but not in its shadow (what a MAX all-reduce
+// brought in from other shards since the last look), as byte indices; with
+// `write`, the shadow catches up with the map. Sixteen bytes per thread.
+__global__ void k_cov_absorb(const u8 *map, u8 *shadow, u64 n16, u64 *out_idx, u64 cap,
+                             unsigned long long *count, int write) {
+  const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n16) return;
+  const uint4 m = ((const uint4 *)map)[t], s = ((const uint4 *)shadow)[t];
+  if (m.x == s.x && m.y == s.y && m.z == s.z && m.w == s.w) return;
+  const u32 mw[4] = {m.x, m.y, m.z, m.w}, sw[4] = {s.x, s.y, s.z, s.w};
+  for (int w = 0; w < 4; w++)
+    for (int b = 0; b < 4; b++)
+      if (((mw[w] >> (8 * b)) & 0xff) && !((sw[w] >> (8 * b)) & 0xff)) {
+        const unsigned long long pos = atomicAdd(count, 1ull);
+        if (write && pos < cap) out_idx[pos] = t * 16 + w * 4 + b;
+      }
+  if (write) ((uint4 *)shadow)[t] = m;
+}
+
 __global__ void k_cov_commit(Dev P, const u64 *rips, u64 n) {
   const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n || !P.code_keys) return;
@@ -1139,7 +1158,9 @@ __global__ void k_cov_commit(Dev P, const u64 *rips, u64 n) {
   for (u32 i = 0; i <= P.code_mask; i++) {
     const u64 k = P.code_keys[h];
     if (k == rip >> 12) {
-      P.cov_map[(u64)P.code_slot[h] * WTFGPU_PAGE_SIZE + (rip & 0xfff)] = 1;
+      const u64 at = (u64)P.code_slot[h] * WTFGPU_PAGE_SIZE + (rip & 0xfff);
+      P.cov_map[at] = 1;
+      P.cov_shadow[at] = 1;  // this shard's own find: not reported by absorb
       return;
     }
     if (k == EMPTY_KEY) return;
@@ -1188,6 +1209,7 @@ struct wtfgpu_ctx {
   u64 *d_codekeys = nullptr;
   u32 *d_codeslot = nullptr;
   u8 *d_covmap = nullptr;
+  u8 *d_covshadow = nullptr;  // the map as of the last absorb / own commit
   u64 ncovslots = 0;
   u64 *d_covrip = nullptr, *d_covmask = nullptr;
   u32 *d_covep = nullptr, *d_covwep = nullptr, *d_covovf = nullptr;
@@ -1369,6 +1391,7 @@ int wtfgpu_destroy(wtfgpu_ctx *c) {
   dfree(c->d_codekeys);
   dfree(c->d_codeslot);
   dfree(c->d_covmap);
+  dfree(c->d_covshadow);
   dfree(c->d_stat);
   dfree(c->d_init);
   dfree(c->d_init_full);
@@ -1663,9 +1686,11 @@ int wtfgpu_set_code_pages(wtfgpu_ctx *c, const uint64_t *vpns, uint32_t n) {
   dfree(c->d_codekeys);
   dfree(c->d_codeslot);
   dfree(c->d_covmap);
+  dfree(c->d_covshadow);
   c->P.code_keys = nullptr;
   c->P.code_slot = nullptr;
   c->P.cov_map = nullptr;
+  c->P.cov_shadow = nullptr;
   c->P.code_mask = 0;
   c->code_vpns.assign(vpns, vpns + n);
   c->ncovslots = n;
@@ -1679,12 +1704,15 @@ int wtfgpu_set_code_pages(wtfgpu_ctx *c, const uint64_t *vpns, uint32_t n) {
     keys[h] = vpns[i];
     slots[h] = i;
   }
-  if (dalloc(&c->d_codekeys, sz) || dalloc(&c->d_codeslot, sz) || dalloc(&c->d_covmap, (u64)n * WTFGPU_PAGE_SIZE))
+  if (dalloc(&c->d_codekeys, sz) || dalloc(&c->d_codeslot, sz) || dalloc(&c->d_covmap, (u64)n * WTFGPU_PAGE_SIZE) ||
+      dalloc(&c->d_covshadow, (u64)n * WTFGPU_PAGE_SIZE))
     return WTFGPU_ERR_OOM;
   HIPCHK(hipMemcpyAsync(c->d_codekeys, keys.data(), sz * 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->d_codeslot, slots.data(), sz * 4, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemsetAsync(c->d_covmap, 0, (u64)n * WTFGPU_PAGE_SIZE, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_covshadow, 0, (u64)n * WTFGPU_PAGE_SIZE, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  c->P.cov_shadow = c->d_covshadow;
   c->P.code_keys = c->d_codekeys;
   c->P.code_slot = c->d_codeslot;
   c->P.code_mask = sz - 1;
@@ -2213,7 +2241,36 @@ int wtfgpu_reset_coverage(wtfgpu_ctx *c) {
   if (!c->d_covmap) return WTFGPU_OK;
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipMemsetAsync(c->d_covmap, 0, c->ncovslots * WTFGPU_PAGE_SIZE, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_covshadow, 0, c->ncovslots * WTFGPU_PAGE_SIZE, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_coverage_absorb(wtfgpu_ctx *c, uint64_t *rips, uint64_t cap, uint64_t *n) {
+  if (!c || !n || (cap && !rips)) return WTFGPU_ERR_INVALID;
+  *n = 0;
+  if (!c->d_covmap || !c->ncovslots) return WTFGPU_OK;
+  HIPCHK(hipSetDevice(c->device));
+  const u64 bytes = c->ncovslots * WTFGPU_PAGE_SIZE, n16 = bytes / 16;
+  if (ensure_scratch(c, 256 + cap * 8)) return WTFGPU_ERR_OOM;
+  unsigned long long *d_count = (unsigned long long *)c->d_scratch;
+  u64 *d_idx = (u64 *)(c->d_scratch + 256);
+  HIPCHK(hipMemsetAsync(d_count, 0, 8, c->stream));
+  k_cov_absorb<<<(u32)((n16 + 255) / 256), 256, 0, c->stream>>>(c->d_covmap, c->d_covshadow, n16, d_idx, cap, d_count,
+                                                                 cap ? 1 : 0);
+  HIPCHK(hipGetLastError());
+  u64 total = 0;
+  HIPCHK(hipMemcpyAsync(&total, d_count, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const u64 m = std::min(total, cap);
+  if (m) {
+    std::vector<u64> idx(m);
+    HIPCHK(hipMemcpyAsync(idx.data(), d_idx, m * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    std::sort(idx.begin(), idx.end());
+    for (u64 i = 0; i < m; i++) rips[i] = (c->code_vpns[idx[i] / WTFGPU_PAGE_SIZE] << 12) | (idx[i] % WTFGPU_PAGE_SIZE);
+  }
+  *n = total;
   return WTFGPU_OK;
 }
 

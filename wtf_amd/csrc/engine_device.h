@@ -92,6 +92,7 @@ struct Dev {
   const u32 *code_slot;
   u32 code_mask;
   u8 *cov_map;           // [slots][4096]
+  u8 *cov_shadow;        // [slots][4096]: the map as of the last absorb
   u64 *cov_rip;          // per wave [nwaves][H]
   u64 *cov_mask;
   u32 *cov_ep;           // entry epoch

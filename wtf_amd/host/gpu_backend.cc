@@ -942,6 +942,11 @@ bool GpuBackend_t::RunBatch(const Target_t &Target, const std::vector<std::pair<
   if (flush_lanes(lanes) || upload_feed(n)) return false;
   stats_.insert_ms += ms_since(t0);
   if (!run_lanes(lanes, &Out, Slots, Slots != nullptr)) return false;
+  {
+    std::vector<uint64_t> nb(n);
+    if (wtfgpu_read_bytes(ctx_, 0, n, nb.data()) == WTFGPU_OK)
+      for (uint64_t b : nb) stats_.alg_bytes += b;
+  }
   const auto tc = Clock::now();
   std::vector<uint32_t> timedout;
   for (uint32_t l = 0; l < n; l++)
@@ -990,13 +995,14 @@ std::string GpuBackend_t::StatsJson() const {
            "\"kernel_ms\":%.3f,\"service_ms\":%.3f,\"total_ms\":%.3f,\"page_fetches\":%llu,"
            "\"prefetched_pages\":%llu,\"stack_windows\":%llu,\"staged_pages\":%llu,\"bulk_ms\":%.3f,\"prefetch_ms\":%.3f,"
            "\"handler_ms\":%.3f,\"fetch_ms\":%.3f,\"flush_ms\":%.3f,\"insert_ms\":%.3f,\"coverage_ms\":%.3f,"
-           "\"target_restore_ms\":%.3f}",
+           "\"target_restore_ms\":%.3f,\"alg_bytes\":%llu}",
            (unsigned long long)stats_.group_steps, (unsigned long long)stats_.rounds,
            (unsigned long long)stats_.breakpoint_hits, (unsigned long long)stats_.kernel_launches, stats_.kernel_ms,
            stats_.service_ms, stats_.total_ms, (unsigned long long)stats_.page_fetches,
            (unsigned long long)stats_.prefetched_pages, (unsigned long long)stats_.stack_windows,
            (unsigned long long)stats_.staged_pages, stats_.bulk_ms, stats_.prefetch_ms, stats_.handler_ms,
-           stats_.fetch_ms, stats_.flush_ms, stats_.insert_ms, stats_.coverage_ms, stats_.target_restore_ms);
+           stats_.fetch_ms, stats_.flush_ms, stats_.insert_ms, stats_.coverage_ms, stats_.target_restore_ms,
+           (unsigned long long)stats_.alg_bytes);
   std::string r(b);
   r.pop_back();
   r += ",\"fetch_by_bp\":{";
@@ -1014,46 +1020,29 @@ std::string GpuBackend_t::StatsJson() const {
 // from the snapshot cr3 gets a slot in the device coverage map; identical on
 // every GPU, so the maps can be merged with a MAX all-reduce.
 bool GpuBackend_t::set_code_pages() {
-  std::vector<uint64_t> vpns;
-  const uint64_t kMaxPages = 1u << 16;
-  const uint64_t mask = 0x000ffffffffff000ull;
-  auto entry = [&](uint64_t table, uint64_t idx, uint64_t &e) {
-    const uint8_t *pg = dump_.GetPhysicalPage(table & mask);
-    if (!pg) return false;
-    memcpy(&e, pg + idx * 8, 8);
-    return (e & 1) != 0;
-  };
-  const uint64_t cr3 = initial_.Cr3 & mask;
-  for (uint64_t i4 = 0; i4 < 512 && vpns.size() < kMaxPages; i4++) {
-    uint64_t e4;
-    if (!entry(cr3, i4, e4)) continue;
-    for (uint64_t i3 = 0; i3 < 512 && vpns.size() < kMaxPages; i3++) {
-      uint64_t e3;
-      if (!entry(e4, i3, e3)) continue;
-      const bool nx3 = ((e4 | e3) >> 63) & 1;
-      if (e3 & 0x80) continue;  // 1 GiB leaves are data mappings in practice
-      for (uint64_t i2 = 0; i2 < 512 && vpns.size() < kMaxPages; i2++) {
-        uint64_t e2;
-        if (!entry(e3, i2, e2)) continue;
-        const bool nx2 = nx3 || ((e2 >> 63) & 1);
-        uint64_t va = (i4 << 39) | (i3 << 30) | (i2 << 21);
-        if (va & (1ull << 47)) va |= 0xffff000000000000ull;
-        if (e2 & 0x80) {
-          if (!nx2)
-            for (uint64_t k = 0; k < 512; k++) vpns.push_back((va >> 12) + k);
-          continue;
-        }
-        for (uint64_t i1 = 0; i1 < 512 && vpns.size() < kMaxPages; i1++) {
-          uint64_t e1;
-          if (!entry(e2, i1, e1)) continue;
-          if (nx2 || ((e1 >> 63) & 1)) continue;
-          vpns.push_back((va >> 12) + i1);
-        }
-      }
-    }
-  }
+  const std::vector<uint64_t> vpns = ExecutablePages(dump_, initial_.Cr3);
   if (vpns.empty()) return true;
   return wtfgpu_set_code_pages(ctx_, vpns.data(), (uint32_t)vpns.size()) == WTFGPU_OK;
+}
+
+bool GpuBackend_t::CoverageMap(uint8_t **Map, uint64_t *Bytes, bool *Device) {
+  void *p = nullptr;
+  if (wtfgpu_coverage_device_map(ctx_, &p, Bytes) != WTFGPU_OK) return false;
+  *Map = (uint8_t *)p;
+  *Device = true;
+  return true;
+}
+
+// Rips other shards set in the merged map (the engine reports what changed
+// since its last look; its own commits are not reported) join the aggregate.
+size_t GpuBackend_t::AbsorbCoverageMap() {
+  uint64_t n = 0;
+  if (wtfgpu_coverage_absorb(ctx_, nullptr, 0, &n) != WTFGPU_OK || n == 0) return 0;
+  std::vector<uint64_t> rips(n);
+  if (wtfgpu_coverage_absorb(ctx_, rips.data(), n, &n) != WTFGPU_OK) return 0;
+  size_t added = 0;
+  for (uint64_t i = 0; i < n && i < rips.size(); i++) added += aggregate_.insert(rips[i]).second;
+  return added;
 }
 
 }  // namespace wtfgpu_host

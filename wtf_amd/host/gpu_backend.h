@@ -37,6 +37,9 @@ struct BatchStats {
   double bulk_ms = 0, prefetch_ms = 0, handler_ms = 0, fetch_ms = 0, flush_ms = 0;
   // RunBatch outside the run loop: restore + InsertTestcase + flush, coverage attribution, Target.Restore
   double insert_ms = 0, coverage_ms = 0, target_restore_ms = 0;
+  // algorithmic bytes the lanes moved (instruction bytes + data
+  // bytes read + written, counted per lane by k_run)
+  uint64_t alg_bytes = 0;
 };
 
 class GpuBackend_t final : public Backend_t, public Executor_t {
@@ -83,6 +86,8 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   void SetFullCoverage(bool On) override { full_coverage_ = On; }
   size_t CoverageSize() const override { return aggregate_.size(); }
   std::string StatsJson() const override;
+  bool CoverageMap(uint8_t **Map, uint64_t *Bytes, bool *Device) override;
+  size_t AbsorbCoverageMap() override;
   const BatchStats &Stats() const { return stats_; }
   uint32_t Lanes() const override { return nlanes_; }
   wtfgpu_ctx *Engine() const { return ctx_; }

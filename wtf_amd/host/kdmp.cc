@@ -110,4 +110,45 @@ std::vector<std::pair<uint64_t, const uint8_t *>> KernelDump::Pages() const {
   return v;
 }
 
+std::vector<uint64_t> ExecutablePages(const KernelDump &Dump, uint64_t cr3, size_t max_pages) {
+  std::vector<uint64_t> vpns;
+  const uint64_t mask = 0x000ffffffffff000ull;
+  auto entry = [&](uint64_t table, uint64_t idx, uint64_t &e) {
+    const uint8_t *pg = Dump.GetPhysicalPage(table & mask);
+    if (!pg) return false;
+    memcpy(&e, pg + idx * 8, 8);
+    return (e & 1) != 0;
+  };
+  cr3 &= mask;
+  for (uint64_t i4 = 0; i4 < 512 && vpns.size() < max_pages; i4++) {
+    uint64_t e4;
+    if (!entry(cr3, i4, e4)) continue;
+    for (uint64_t i3 = 0; i3 < 512 && vpns.size() < max_pages; i3++) {
+      uint64_t e3;
+      if (!entry(e4, i3, e3)) continue;
+      const bool nx3 = ((e4 | e3) >> 63) & 1;
+      if (e3 & 0x80) continue;
+      for (uint64_t i2 = 0; i2 < 512 && vpns.size() < max_pages; i2++) {
+        uint64_t e2;
+        if (!entry(e3, i2, e2)) continue;
+        const bool nx2 = nx3 || ((e2 >> 63) & 1);
+        uint64_t va = (i4 << 39) | (i3 << 30) | (i2 << 21);
+        if (va & (1ull << 47)) va |= 0xffff000000000000ull;
+        if (e2 & 0x80) {
+          if (!nx2)
+            for (uint64_t k = 0; k < 512; k++) vpns.push_back((va >> 12) + k);
+          continue;
+        }
+        for (uint64_t i1 = 0; i1 < 512 && vpns.size() < max_pages; i1++) {
+          uint64_t e1;
+          if (!entry(e2, i1, e1)) continue;
+          if (nx2 || ((e1 >> 63) & 1)) continue;
+          vpns.push_back((va >> 12) + i1);
+        }
+      }
+    }
+  }
+  return vpns;
+}
+
 }  // namespace wtfgpu_host

@@ -36,4 +36,11 @@ class KernelDump {
   std::unordered_map<uint64_t, const uint8_t *> pages_;  // gpfn -> page
 };
 
+// The coverage index space: every executable 4 KiB page (leaf
+// not NX at any level) reachable from `cr3` in the dump, in page-table walk
+// order, up to `max_pages`. 1 GiB leaves are skipped (data mappings in
+// practice). Identical for every shard built from the same snapshot, so
+// per-shard coverage maps over these slots merge with a MAX all-reduce.
+std::vector<uint64_t> ExecutablePages(const KernelDump &Dump, uint64_t cr3, size_t max_pages = 1u << 16);
+
 }  // namespace wtfgpu_host

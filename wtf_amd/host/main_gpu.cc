@@ -1,10 +1,14 @@
 // main_gpu.cc — `wtfgpu`: the batched wtf node on one MI355X.
 //   wtfgpu run  --name tlv_server --target targets/tlv --lanes 4096 [--input dir] [--full-coverage]
 //   wtfgpu fuzz --name tlv_server --target targets/tlv --lanes 65536 --runs N --seed 1337
-// The same runner drives the oracle twin (oracle/twin_main.cc) for parity.
+//   wtfgpu fuzz ... --device r --rank r --world n --nccl-id-file /tmp/id   (one process per GPU:
+//       shard r mutates with seed + r; coverage maps merged with RCCL MAX after every batch)
+// The same runner drives the oracle twin (oracle/twin_backend.cc) for parity.
 #include <cstdio>
+#include <memory>
 
 #include "gpu_backend.h"
+#include "rccl_exchange.h"
 #include "runner.h"
 
 int main(int argc, char **argv) {
@@ -20,5 +24,15 @@ int main(int argc, char **argv) {
     printf("Failed to initialize the gpu backend\n");
     return 1;
   }
-  return wtfgpu_host::RunnerMain(O, *B, Opts, State);
+  std::unique_ptr<wtfgpu_host::RcclExchange_t> X;
+  if (O.world > 1) {
+    uint8_t Id[wtfgpu_host::kRcclIdBytes];
+    if (O.nccl_id_file.empty() || !wtfgpu_host::RcclIdViaFile(O.nccl_id_file, O.rank, Id)) {
+      printf("--world > 1 needs --nccl-id-file (rank 0 writes the RCCL id there)\n");
+      return 1;
+    }
+    X = std::make_unique<wtfgpu_host::RcclExchange_t>(O.rank, O.world);
+    if (!X->Init(Id, wtfgpu_stream(B->Engine()))) return 1;
+  }
+  return wtfgpu_host::RunnerMain(O, *B, Opts, State, X.get());
 }

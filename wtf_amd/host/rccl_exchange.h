@@ -1,0 +1,34 @@
+// rccl_exchange.h — CoverageExchange_t over RCCL (see rccl_exchange.cc).
+#pragma once
+#include <cstdint>
+#include <cstring>
+#include <string>
+
+#include "runner.h"
+
+namespace wtfgpu_host {
+
+constexpr size_t kRcclIdBytes = 128;  // sizeof(ncclUniqueId)
+
+// a fresh communicator id (rank 0)
+bool RcclUniqueId(uint8_t Out[kRcclIdBytes]);
+// rank 0 makes the id and writes it to Path; the others wait for the file
+bool RcclIdViaFile(const std::string &Path, int Rank, uint8_t Id[kRcclIdBytes], double TimeoutS = 120);
+
+class RcclExchange_t final : public CoverageExchange_t {
+ public:
+  RcclExchange_t(int Rank, int World);
+  ~RcclExchange_t() override;
+  // Stream: the engine's HIP stream (wtfgpu_stream); collective on every rank
+  bool Init(const uint8_t Id[kRcclIdBytes], void *Stream);
+  int Rank() const override { return rank_; }
+  int World() const override { return world_; }
+  bool AllReduceMax(uint8_t *Map, uint64_t Bytes, bool Device) override;
+
+ private:
+  struct Impl;
+  int rank_, world_;
+  Impl *impl_;
+};
+
+}  // namespace wtfgpu_host

@@ -142,15 +142,23 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
     else if (a == "--full-coverage") O.full_coverage = true;
     else if (a == "--quiet") O.quiet = true;
     else if (a == "--serial-mutation") O.serial_mutation = true;
+    else if (a == "--rank") O.rank = atoi(next("--rank"));
+    else if (a == "--world") O.world = atoi(next("--world"));
+    else if (a == "--exchange") O.exchange = next("--exchange");
+    else if (a == "--nccl-id-file") O.nccl_id_file = next("--nccl-id-file");
     else {
       fprintf(stderr, "unknown argument %s\n", a.c_str());
       return false;
     }
   }
+  if (O.world < 1 || O.rank < 0 || O.rank >= O.world) {
+    fprintf(stderr, "--rank must be in [0, --world)\n");
+    return false;
+  }
   if (O.name.empty() || O.target.empty()) {
     fprintf(stderr, "usage: [run|fuzz] --name <target> --target <dir> [--input p] [--results f] [--limit n]\n"
                     "       [--lanes n] [--overlay-pages k] [--runs n] [--seconds s] [--seed s] [--full-coverage]\n"
-                    "       [--serial-mutation]\n");
+                    "       [--serial-mutation] [--rank r --world n [--exchange host:port | --nccl-id-file f]]\n");
     return false;
   }
   return true;
@@ -179,7 +187,8 @@ bool LoadTarget(const RunnerOptions &O, Options_t &Opts, CpuState_t &State) {
   return true;
 }
 
-int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, const CpuState_t &State) {
+int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, const CpuState_t &State,
+               CoverageExchange_t *X) {
   Target_t *Target = Targets_t::Instance().Get(O.name);
   if (!Target) {
     printf("Target %s not found\n", O.name.c_str());
@@ -240,147 +249,190 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
   }
 
   // ---- fuzz: in-process master + batched node
-  std::mt19937_64 Rng(O.seed);
-  const fs::path T(O.target);
-  fs::create_directories(T / "outputs");
-  fs::create_directories(T / "crashes");
-  Corpus_t Corpus(T / "outputs", Rng);
-  std::unique_ptr<Mutator_t> Mutator;
-  if (Target->CreateMutator) Mutator = Target->CreateMutator(Rng, O.max_len);
-  if (!Mutator) {
-    printf("Target %s has no mutator\n", O.name.c_str());
-    return 1;
-  }
-  // the master sends the corpus first (server.h:756-790), then mutations
-  std::vector<std::string> Pending;
-  std::string LastNewCov;  // the testcase last passed to Mutator->OnNewCoverage
-  bool HaveNewCov = false;
-  for (const auto &P : list_inputs(T / "inputs")) {
-    const auto B = ReadFile(P);
-    Pending.emplace_back(B.begin(), B.end());
-  }
-  uint64_t Execs = 0, Retired = 0, Crashes = 0, Timeouts = 0, Cr3s = 0, Errors = 0, Batches = 0;
-  std::unordered_set<std::string> CrashNames;
-  double RunSeconds = 0;
-  const auto t0 = Clock::now();
-  // The next batch is mutated on a host thread while the executor runs the
-  // current one (a node's master and client overlap the same way); it is
-  // built from the corpus as it stood before the current batch's results.
-  auto make_batch = [&](uint64_t done) {
-    uint64_t n = N;
-    if (O.runs) n = std::min<uint64_t>(n, O.runs - done);
-    std::vector<std::string> Batch;
-    Batch.reserve(n);
-    while (Batch.size() < n && !Pending.empty()) {
-      Batch.push_back(std::move(Pending.back()));
-      Pending.pop_back();
-    }
-    // large batches: mutate in fixed chunks on the host threads; chunk c has
-    // its own generator, seeded from Rng in chunk order, its own mutator and
-    // a read-only view of the corpus (deterministic for a seed whatever the
-    // thread count; the corpus does not change while the batch is built)
-    const size_t Need = n - Batch.size();
-    if (Corpus.Size() && Need >= kParMutateMin && !O.serial_mutation) {
-      const size_t Chunks = (Need + kMutateChunk - 1) / kMutateChunk;
-      std::vector<uint64_t> Seeds(Chunks);
-      for (uint64_t &S : Seeds) S = Rng();
-      std::vector<std::string> Out(Need);
-      std::atomic<size_t> NextChunk{0};
-      auto Work = [&]() {
-        for (size_t c; (c = NextChunk.fetch_add(1)) < Chunks;) {
-          std::mt19937_64 R(Seeds[c]);
-          Corpus_t View(Corpus, R);
-          std::unique_ptr<Mutator_t> M = Target->CreateMutator(R, O.max_len);
-          // the master mutator's cross-over partner (the last new-coverage
-          // testcase) is every chunk mutator's too
-          if (HaveNewCov) M->OnNewCoverage(Testcase_t((const uint8_t *)LastNewCov.data(), LastNewCov.size()));
-          for (size_t i = c * kMutateChunk; i < std::min(Need, (c + 1) * kMutateChunk); i++) {
-            Out[i] = M->GetNewTestcase(View);
-            if (Out[i].size() > O.max_len) Out[i].resize(O.max_len);
-          }
-        }
-      };
-      std::vector<std::thread> Pool;
-      for (unsigned t = 1; t < host_threads(); t++) Pool.emplace_back(Work);
-      Work();
-      for (std::thread &Th : Pool) Th.join();
-      for (std::string &S : Out) Batch.push_back(std::move(S));
-    }
-    while (Batch.size() < n) {
-      if (Corpus.Size() == 0 && Batch.empty()) break;
-      std::string S = Corpus.Size() ? Mutator->GetNewTestcase(Corpus) : Batch[Rng() % Batch.size()];
-      if (S.size() > O.max_len) S.resize(O.max_len);
-      Batch.push_back(std::move(S));
-    }
-    return Batch;
-  };
-  auto more = [&](uint64_t done) {
-    return (O.runs == 0 || done < O.runs) && (O.seconds <= 0 || secs_since(t0) < O.seconds);
-  };
-  std::vector<std::string> Batch = make_batch(0);
-  if (Batch.empty()) {
+  FuzzSession F(O, Exec, *Target, Slots, X);
+  if (!F.Start()) {
     printf("Nothing to run: empty corpus and no inputs\n");
     return 1;
   }
-  while (!Batch.empty()) {
-    std::vector<std::pair<const uint8_t *, size_t>> Tc(Batch.size());
-    for (size_t i = 0; i < Batch.size(); i++) Tc[i] = {(const uint8_t *)Batch[i].data(), Batch[i].size()};
-    std::vector<LaneResult> R;
-    const auto tb = Clock::now();
-    const uint64_t after = Execs + Batch.size();
-    std::future<std::vector<std::string>> Next;
-    if (more(after) && Corpus.Size()) Next = std::async(std::launch::async, make_batch, after);
-    if (!Exec.RunBatch(*Target, Tc, R, &Slots)) {
+  while (!F.Done())
+    if (!F.Step()) {
       printf("RunBatch failed\n");
       return 1;
     }
-    RunSeconds += secs_since(tb);
-    Batches++;
-    std::vector<std::string> NextBatch;
-    if (Next.valid()) NextBatch = Next.get();  // before the corpus / mutator change below
-    // master bookkeeping in lane order (server.h:816-886)
-    for (size_t i = 0; i < Batch.size(); i++) {
-      const LaneResult &L = R[i];
-      Execs++;
-      Retired += L.icount;
-      if (L.error) {  // the engine could not finish it: neither a crash nor coverage
-        Errors++;
-        continue;
-      }
-      if (std::holds_alternative<Timedout_t>(L.result)) Timeouts++;
-      if (std::holds_alternative<Cr3Change_t>(L.result)) Cr3s++;
-      if (const Crash_t *C = std::get_if<Crash_t>(&L.result)) {
-        Crashes++;
-        if (!C->CrashName.empty() && CrashNames.insert(C->CrashName).second)
-          SaveFile(T / "crashes" / C->CrashName, (const uint8_t *)Batch[i].data(), Batch[i].size());
-      }
-      // a timed-out testcase reports no coverage (the client revokes it,
-      // client.cc:122-133); any other result with new coverage, crashes
-      // included, joins the corpus after arming the mutator's cross-over
-      // (server.h:816-853)
-      if (!L.new_coverage.empty() && !std::holds_alternative<Timedout_t>(L.result)) {
-        Testcase_t Tcase((const uint8_t *)Batch[i].data(), Batch[i].size());
-        Mutator->OnNewCoverage(Tcase);
-        LastNewCov = Batch[i];
-        HaveNewCov = true;
-        Corpus.SaveTestcase(L.result, std::move(Tcase));
-      }
-    }
-    if (!NextBatch.empty() || !more(Execs))
-      Batch = std::move(NextBatch);
-    else
-      Batch = make_batch(Execs);
-  }
-  const double Wall = secs_since(t0);
-  printf("{\"mode\":\"fuzz\",\"target\":\"%s\",\"lanes\":%u,\"batches\":%llu,\"execs\":%llu,\"retired\":%llu,"
-         "\"wall_s\":%.6f,\"run_s\":%.6f,\"execs_per_s\":%.3f,\"instr_per_s\":%.3f,\"coverage\":%zu,"
-         "\"corpus\":%zu,\"crashes\":%llu,\"unique_crashes\":%zu,\"timeouts\":%llu,\"cr3\":%llu,\"errors\":%llu,"
-         "\"backend\":%s}\n",
-         O.name.c_str(), N, (unsigned long long)Batches, (unsigned long long)Execs, (unsigned long long)Retired, Wall,
-         RunSeconds, Execs / RunSeconds, Retired / RunSeconds, Exec.CoverageSize(), Corpus.Size(),
-         (unsigned long long)Crashes, CrashNames.size(), (unsigned long long)Timeouts, (unsigned long long)Cr3s,
-         (unsigned long long)Errors, Exec.StatsJson().c_str());
+  printf("%s\n", F.SummaryJson().c_str());
   return 0;
+}
+
+// ------------------------------------------------------------------ FuzzSession
+FuzzSession::FuzzSession(const RunnerOptions &O, Executor_t &Exec, Target_t &Target, ModuleSlots &Slots,
+                         CoverageExchange_t *X)
+    : O_(O), Exec_(Exec), Target_(Target), Slots_(Slots), X_(X),
+      Rng_(O.seed + (X ? (uint64_t)X->Rank() : 0)), T_(O.target), Corpus_(T_ / "outputs", Rng_) {}
+
+FuzzSession::~FuzzSession() {
+  if (Next_.valid()) Next_.wait();
+}
+
+bool FuzzSession::Start() {
+  fs::create_directories(T_ / "outputs");
+  fs::create_directories(T_ / "crashes");
+  if (Target_.CreateMutator) Mutator_ = Target_.CreateMutator(Rng_, O_.max_len);
+  if (!Mutator_) {
+    printf("Target %s has no mutator\n", O_.name.c_str());
+    return false;
+  }
+  // the master sends the corpus first (server.h:756-790), then mutations
+  for (const auto &P : list_inputs(T_ / "inputs")) {
+    const auto B = ReadFile(P);
+    Pending_.emplace_back(B.begin(), B.end());
+  }
+  t0_ = Clock::now();
+  Batch_ = MakeBatch(0);
+  return !Batch_.empty();
+}
+
+bool FuzzSession::More(uint64_t done) const {
+  return (O_.runs == 0 || done < O_.runs) && (O_.seconds <= 0 || secs_since(t0_) < O_.seconds);
+}
+
+double FuzzSession::WallSeconds() const { return secs_since(t0_); }
+
+// The next batch: the corpus inputs first, then mutations of corpus picks.
+std::vector<std::string> FuzzSession::MakeBatch(uint64_t done) {
+  uint64_t n = Exec_.Lanes();
+  if (O_.runs) n = std::min<uint64_t>(n, O_.runs - done);
+  std::vector<std::string> Batch;
+  Batch.reserve(n);
+  while (Batch.size() < n && !Pending_.empty()) {
+    Batch.push_back(std::move(Pending_.back()));
+    Pending_.pop_back();
+  }
+  // large batches: mutate in fixed chunks on the host threads; chunk c has
+  // its own generator, seeded from Rng in chunk order, its own mutator and
+  // a read-only view of the corpus (deterministic for a seed whatever the
+  // thread count; the corpus does not change while the batch is built)
+  const size_t Need = n - Batch.size();
+  if (Corpus_.Size() && Need >= kParMutateMin && !O_.serial_mutation) {
+    const size_t Chunks = (Need + kMutateChunk - 1) / kMutateChunk;
+    std::vector<uint64_t> Seeds(Chunks);
+    for (uint64_t &S : Seeds) S = Rng_();
+    std::vector<std::string> Out(Need);
+    std::atomic<size_t> NextChunk{0};
+    auto Work = [&]() {
+      for (size_t c; (c = NextChunk.fetch_add(1)) < Chunks;) {
+        std::mt19937_64 R(Seeds[c]);
+        Corpus_t View(Corpus_, R);
+        std::unique_ptr<Mutator_t> M = Target_.CreateMutator(R, O_.max_len);
+        // the master mutator's cross-over partner (the last new-coverage
+        // testcase) is every chunk mutator's too
+        if (HaveNewCov_) M->OnNewCoverage(Testcase_t((const uint8_t *)LastNewCov_.data(), LastNewCov_.size()));
+        for (size_t i = c * kMutateChunk; i < std::min(Need, (c + 1) * kMutateChunk); i++) {
+          Out[i] = M->GetNewTestcase(View);
+          if (Out[i].size() > O_.max_len) Out[i].resize(O_.max_len);
+        }
+      }
+    };
+    std::vector<std::thread> Pool;
+    for (unsigned t = 1; t < host_threads(); t++) Pool.emplace_back(Work);
+    Work();
+    for (std::thread &Th : Pool) Th.join();
+    for (std::string &S : Out) Batch.push_back(std::move(S));
+  }
+  while (Batch.size() < n) {
+    if (Corpus_.Size() == 0 && Batch.empty()) break;
+    std::string S = Corpus_.Size() ? Mutator_->GetNewTestcase(Corpus_) : Batch[Rng_() % Batch.size()];
+    if (S.size() > O_.max_len) S.resize(O_.max_len);
+    Batch.push_back(std::move(S));
+  }
+  return Batch;
+}
+
+// One batch: the executor runs it while the next batch is mutated on a host
+// thread (a node's master and client overlap the same way; the next batch is
+// built from the corpus as it stood before this batch's results); then the
+// master's bookkeeping in lane order (server.h:816-886) and, across shards,
+// the coverage-map merge.
+bool FuzzSession::Step() {
+  if (Batch_.empty()) return true;
+  std::vector<std::pair<const uint8_t *, size_t>> Tc(Batch_.size());
+  for (size_t i = 0; i < Batch_.size(); i++) Tc[i] = {(const uint8_t *)Batch_[i].data(), Batch_[i].size()};
+  std::vector<LaneResult> R;
+  const auto tb = Clock::now();
+  const uint64_t after = S_.execs + Batch_.size();
+  if (More(after) && Corpus_.Size()) Next_ = std::async(std::launch::async, &FuzzSession::MakeBatch, this, after);
+  if (!Exec_.RunBatch(Target_, Tc, R, &Slots_)) return false;
+  S_.run_s += secs_since(tb);
+  S_.batches++;
+  std::vector<std::string> NextBatch;
+  if (Next_.valid()) NextBatch = Next_.get();  // before the corpus / mutator change below
+  for (size_t i = 0; i < Batch_.size(); i++) {
+    const LaneResult &L = R[i];
+    S_.execs++;
+    S_.retired += L.icount;
+    if (L.error) {  // the engine could not finish it: neither a crash nor coverage
+      S_.errors++;
+      S_.error_retired += L.icount;
+      continue;
+    }
+    if (std::holds_alternative<Timedout_t>(L.result)) S_.timeouts++;
+    if (std::holds_alternative<Cr3Change_t>(L.result)) S_.cr3++;
+    if (const Crash_t *C = std::get_if<Crash_t>(&L.result)) {
+      S_.crashes++;
+      if (!C->CrashName.empty() && CrashNames_.insert(C->CrashName).second)
+        SaveFile(T_ / "crashes" / C->CrashName, (const uint8_t *)Batch_[i].data(), Batch_[i].size());
+    }
+    // a timed-out testcase reports no coverage (the client revokes it,
+    // client.cc:122-133); any other result with new coverage, crashes
+    // included, joins the corpus after arming the mutator's cross-over
+    // (server.h:816-853)
+    if (!L.new_coverage.empty() && !std::holds_alternative<Timedout_t>(L.result)) {
+      Testcase_t Tcase((const uint8_t *)Batch_[i].data(), Batch_[i].size());
+      Mutator_->OnNewCoverage(Tcase);
+      LastNewCov_ = Batch_[i];
+      HaveNewCov_ = true;
+      Corpus_.SaveTestcase(L.result, std::move(Tcase));
+    }
+  }
+  if (X_ && X_->World() > 1 && !MergeCoverage()) return false;
+  if (!NextBatch.empty() || !More(S_.execs))
+    Batch_ = std::move(NextBatch);
+  else
+    Batch_ = MakeBatch(S_.execs);
+  return true;
+}
+
+// every shard's coverage map, MAX-reduced over the shards; the
+// rips other shards found join this shard's aggregate (so its lanes stop
+// reporting them as new). Testcases stay with the shard that found them.
+bool FuzzSession::MergeCoverage() {
+  const auto t = Clock::now();
+  uint8_t *Map = nullptr;
+  uint64_t Bytes = 0;
+  bool Device = false;
+  if (!Exec_.CoverageMap(&Map, &Bytes, &Device)) return false;
+  if (Bytes && !X_->AllReduceMax(Map, Bytes, Device)) return false;
+  S_.merged_rips += Exec_.AbsorbCoverageMap();
+  S_.merge_ms += secs_since(t) * 1e3;
+  return true;
+}
+
+std::string FuzzSession::SummaryJson() const {
+  const double Wall = WallSeconds();
+  char b[1024];
+  snprintf(b, sizeof(b),
+           "{\"mode\":\"fuzz\",\"target\":\"%s\",\"lanes\":%u,\"rank\":%d,\"world\":%d,\"batches\":%llu,"
+           "\"execs\":%llu,\"retired\":%llu,\"wall_s\":%.6f,\"run_s\":%.6f,\"execs_per_s\":%.3f,"
+           "\"instr_per_s\":%.3f,\"coverage\":%zu,\"corpus\":%zu,\"crashes\":%llu,\"unique_crashes\":%zu,"
+           "\"timeouts\":%llu,\"cr3\":%llu,\"errors\":%llu,\"error_retired\":%llu,\"merged_rips\":%llu,"
+           "\"merge_ms\":%.3f,"
+           "\"backend\":",
+           O_.name.c_str(), Exec_.Lanes(), X_ ? X_->Rank() : 0, X_ ? X_->World() : 1,
+           (unsigned long long)S_.batches, (unsigned long long)S_.execs, (unsigned long long)S_.retired, Wall,
+           S_.run_s, S_.run_s > 0 ? S_.execs / S_.run_s : 0.0, S_.run_s > 0 ? S_.retired / S_.run_s : 0.0,
+           Exec_.CoverageSize(), Corpus_.Size(), (unsigned long long)S_.crashes, CrashNames_.size(),
+           (unsigned long long)S_.timeouts, (unsigned long long)S_.cr3, (unsigned long long)S_.errors,
+           (unsigned long long)S_.error_retired, (unsigned long long)S_.merged_rips, S_.merge_ms);
+  return std::string(b) + Exec_.StatsJson() + "}";
 }
 
 }  // namespace wtfgpu_host

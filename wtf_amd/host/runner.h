@@ -4,8 +4,12 @@
 // mutate, run, keep testcases that found new coverage, save crashes), both
 // batched N testcases per executor call.
 #pragma once
+#include <chrono>
 #include <cstdint>
+#include <future>
+#include <random>
 #include <string>
+#include <unordered_set>
 #include <utility>
 #include <vector>
 
@@ -41,6 +45,29 @@ class Executor_t {
   virtual void SetFullCoverage(bool On) = 0;
   virtual size_t CoverageSize() const = 0;
   virtual std::string StatsJson() const { return "{}"; }
+  // The coverage map over the executable-page slot table (one byte per code
+  // byte of every executable page reachable from the snapshot cr3; identical
+  // on every shard): host or device memory.
+  virtual bool CoverageMap(uint8_t **Map, uint64_t *Bytes, bool *Device) {
+    *Map = nullptr;
+    *Bytes = 0;
+    *Device = false;
+    return true;
+  }
+  // Rips set in the map (after a merge) that the aggregate lacks join it;
+  // returns how many.
+  virtual size_t AbsorbCoverageMap() { return 0; }
+};
+
+// The collective between shards (one node per GPU): an in-place MAX
+// all-reduce of every shard's coverage map. RCCL over xGMI on the GPU node
+// (main_gpu.cc, node_capi.cc); TCP on the CPU (net_exchange.cc) for the twin.
+class CoverageExchange_t {
+ public:
+  virtual ~CoverageExchange_t() = default;
+  virtual int Rank() const = 0;
+  virtual int World() const = 0;
+  virtual bool AllReduceMax(uint8_t *Map, uint64_t Bytes, bool Device) = 0;
 };
 
 struct RunnerOptions {
@@ -60,12 +87,63 @@ struct RunnerOptions {
   bool full_coverage = false;
   bool quiet = false;
   bool serial_mutation = false;  // one mutator, in order: the reference master's stream exactly
+  int rank = 0, world = 1;         // fuzz: shard rank of world (one node per GPU)
+  std::string exchange = "127.0.0.1:31337";  // TCP coverage exchange (CPU shards): rank 0 listens here
+  std::string nccl_id_file;        // GPU shards: RCCL unique id file (rank 0 writes it)
+};
+
+struct FuzzStats {
+  uint64_t execs = 0, retired = 0, crashes = 0, timeouts = 0, cr3 = 0, errors = 0, batches = 0, merged_rips = 0;
+  uint64_t error_retired = 0;  // instructions retired by testcases the engine could not finish
+  double run_s = 0, merge_ms = 0;
+};
+
+// The fuzz loop of one node / shard, one batch per Step(): an in-process
+// master (corpus, mutator, crash saving: server.h:629-886) feeding the
+// executor N testcases at a time (client.cc:187-258, batched). With a
+// CoverageExchange_t of world > 1, shard r mutates with seed + r and merges
+// coverage maps after every batch.
+class FuzzSession {
+ public:
+  FuzzSession(const RunnerOptions &O, Executor_t &Exec, Target_t &Target, ModuleSlots &Slots,
+              CoverageExchange_t *X);
+  ~FuzzSession();
+  bool Start();      // corpus inputs + the first batch; false = nothing to run
+  bool Step();       // one batch; false = the executor failed
+  bool Done() const { return Batch_.empty(); }
+  const FuzzStats &Stats() const { return S_; }
+  size_t CorpusSize() const { return Corpus_.Size(); }
+  double WallSeconds() const;
+  std::string SummaryJson() const;
+
+ private:
+  std::vector<std::string> MakeBatch(uint64_t done);
+  bool More(uint64_t done) const;
+  bool MergeCoverage();
+
+  const RunnerOptions O_;
+  Executor_t &Exec_;
+  Target_t &Target_;
+  ModuleSlots &Slots_;
+  CoverageExchange_t *X_;
+  std::mt19937_64 Rng_;
+  fs::path T_;
+  Corpus_t Corpus_;
+  std::unique_ptr<Mutator_t> Mutator_;
+  std::vector<std::string> Pending_, Batch_;
+  std::string LastNewCov_;  // the testcase last passed to Mutator_->OnNewCoverage
+  bool HaveNewCov_ = false;
+  std::future<std::vector<std::string>> Next_;
+  std::unordered_set<std::string> CrashNames_;
+  FuzzStats S_;
+  std::chrono::steady_clock::time_point t0_;
 };
 
 bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O);
 // Loads the snapshot, initialises the executor and the module, runs the mode.
 // make_executor is called after the options are parsed; returns the exit code.
-int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, const CpuState_t &State);
+int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, const CpuState_t &State,
+               CoverageExchange_t *X = nullptr);
 // Options_t + CpuState_t from <target>/state (regs.json, symbol store) and the runner options.
 bool LoadTarget(const RunnerOptions &O, Options_t &Opts, CpuState_t &State);
 
