@@ -909,6 +909,8 @@ bool GpuBackend_t::RunBatch(const Target_t &Target, const std::vector<std::pair<
   // the (parallel) insert loop (ModuleSlots::ResetLane)
   if (wtfgpu_restore(ctx_, 0, n)) return false;
   for (uint32_t l = 0; l < n; l++) reset_view(l);
+  const auto tm = Clock::now();
+  stats_.restore_ms += std::chrono::duration<double, std::milli>(tm - t0).count();
   // InsertTestcase per lane (client.cc:102), module state per lane
   Backend_t *saved = g_Backend;
   std::vector<uint32_t> lanes(n);
@@ -939,7 +941,10 @@ bool GpuBackend_t::RunBatch(const Target_t &Target, const std::vector<std::pair<
     lanes[l] = l;
     if (!insert_ok[l]) views_[l].result = Crash_t("insert-testcase-failed");
   }
+  const auto tu = Clock::now();
+  stats_.module_ms += std::chrono::duration<double, std::milli>(tu - tm).count();
   if (flush_lanes(lanes) || upload_feed(n)) return false;
+  stats_.upload_ms += ms_since(tu);
   stats_.insert_ms += ms_since(t0);
   if (!run_lanes(lanes, &Out, Slots, Slots != nullptr)) return false;
   {
@@ -989,20 +994,21 @@ void GpuBackend_t::ResetCoverage() {
 }
 
 std::string GpuBackend_t::StatsJson() const {
-  char b[1024];
+  char b[2048];
   snprintf(b, sizeof(b),
            "{\"kind\":\"gpu\",\"group_steps\":%llu,\"rounds\":%llu,\"breakpoint_hits\":%llu,\"kernel_launches\":%llu,"
            "\"kernel_ms\":%.3f,\"service_ms\":%.3f,\"total_ms\":%.3f,\"page_fetches\":%llu,"
            "\"prefetched_pages\":%llu,\"stack_windows\":%llu,\"staged_pages\":%llu,\"bulk_ms\":%.3f,\"prefetch_ms\":%.3f,"
            "\"handler_ms\":%.3f,\"fetch_ms\":%.3f,\"flush_ms\":%.3f,\"insert_ms\":%.3f,\"coverage_ms\":%.3f,"
-           "\"target_restore_ms\":%.3f,\"alg_bytes\":%llu}",
+           "\"target_restore_ms\":%.3f,\"alg_bytes\":%llu,\"restore_ms\":%.3f,\"module_ms\":%.3f,"
+           "\"upload_ms\":%.3f}",
            (unsigned long long)stats_.group_steps, (unsigned long long)stats_.rounds,
            (unsigned long long)stats_.breakpoint_hits, (unsigned long long)stats_.kernel_launches, stats_.kernel_ms,
            stats_.service_ms, stats_.total_ms, (unsigned long long)stats_.page_fetches,
            (unsigned long long)stats_.prefetched_pages, (unsigned long long)stats_.stack_windows,
            (unsigned long long)stats_.staged_pages, stats_.bulk_ms, stats_.prefetch_ms, stats_.handler_ms,
            stats_.fetch_ms, stats_.flush_ms, stats_.insert_ms, stats_.coverage_ms, stats_.target_restore_ms,
-           (unsigned long long)stats_.alg_bytes);
+           (unsigned long long)stats_.alg_bytes, stats_.restore_ms, stats_.module_ms, stats_.upload_ms);
   std::string r(b);
   r.pop_back();
   r += ",\"fetch_by_bp\":{";

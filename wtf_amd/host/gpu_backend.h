@@ -40,6 +40,9 @@ struct BatchStats {
   // algorithmic bytes the lanes moved (instruction bytes + data
   // bytes read + written, counted per lane by k_run)
   uint64_t alg_bytes = 0;
+  // insert_ms split: device restore + host views, module InsertTestcase calls,
+  // register / memory / feed uploads
+  double restore_ms = 0, module_ms = 0, upload_ms = 0;
 };
 
 class GpuBackend_t final : public Backend_t, public Executor_t {

@@ -23,9 +23,10 @@ struct Value {
   std::vector<Value> arr;
   std::vector<std::pair<std::string, Value>> obj;
 
+  // a key given twice: the last one counts (nlohmann's parser overwrites)
   const Value *find(const std::string &k) const {
-    for (auto &kv : obj)
-      if (kv.first == k) return &kv.second;
+    for (auto it = obj.rbegin(); it != obj.rend(); ++it)
+      if (it->first == k) return &it->second;
     return nullptr;
   }
   const Value &at(const std::string &k) const {

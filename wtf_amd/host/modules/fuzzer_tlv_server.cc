@@ -37,8 +37,75 @@ struct Packet_t {
   std::vector<uint8_t> Body;
 };
 
+// Fast path of Deserialize for the canonical form the mutator writes (the
+// nlohmann dump() of Packets_t: no whitespace, unsigned integers, each packet
+// key once): parsed in place, no document tree. Anything else -> false, and
+// the general parser below decides. Both give the same packets.
+namespace {
+struct Cursor {
+  const char *p, *e;
+  bool lit(const char *s) {
+    const size_t n = strlen(s);
+    if ((size_t)(e - p) < n || memcmp(p, s, n)) return false;
+    p += n;
+    return true;
+  }
+  bool num(uint64_t &v) {
+    const char *s = p;
+    v = 0;
+    while (p < e && *p >= '0' && *p <= '9' && p - s < 19) v = v * 10 + uint64_t(*p++ - '0');
+    return p > s && (p == e || *p < '0' || *p > '9');
+  }
+};
+}  // namespace
+
+bool FastDeserialize(const uint8_t *Buffer, const size_t BufferSize, std::vector<Packet_t> &Out) {
+  Cursor C{(const char *)Buffer, (const char *)Buffer + BufferSize};
+  if (!C.lit("{\"Packets\":[")) return false;
+  if (C.lit("]}")) return C.p == C.e;
+  for (;;) {
+    Packet_t P;
+    unsigned seen = 0;
+    if (!C.lit("{")) return false;
+    for (;;) {
+      uint64_t v;
+      if (C.lit("\"Body\":[")) {
+        if (seen & 1) return false;
+        seen |= 1;
+        if (!C.lit("]")) {
+          for (;;) {
+            if (!C.num(v)) return false;
+            P.Body.push_back((uint8_t)v);
+            if (C.lit("]")) break;
+            if (!C.lit(",")) return false;
+          }
+        }
+      } else if (C.lit("\"BodySize\":")) {
+        if ((seen & 2) || !C.num(v)) return false;
+        seen |= 2, P.BodySize = (uint16_t)v;
+      } else if (C.lit("\"Command\":")) {
+        if ((seen & 4) || !C.num(v)) return false;
+        seen |= 4, P.Command = (uint32_t)v;
+      } else if (C.lit("\"Id\":")) {
+        if ((seen & 8) || !C.num(v)) return false;
+        seen |= 8, P.Id = (uint16_t)v;
+      } else {
+        return false;
+      }
+      if (C.lit("}")) break;
+      if (!C.lit(",")) return false;
+    }
+    if (seen != 15) return false;
+    Out.push_back(std::move(P));
+    if (C.lit("]}")) return C.p == C.e;
+    if (!C.lit(",")) return false;
+  }
+}
+
 // JSON testcase -> packets (nlohmann get<>: integers are cast to the field type)
 bool Deserialize(const uint8_t *Buffer, const size_t BufferSize, std::vector<Packet_t> &Out) {
+  Out.clear();
+  if (FastDeserialize(Buffer, BufferSize, Out)) return true;
   Out.clear();
   try {
     const jsonl::Value Root = jsonl::parse(Buffer, BufferSize);
