@@ -377,6 +377,7 @@ def run(a, rank, world, local, tmp):
             **{k: fields[k] for k in ("lanes_per_wave_step", "gpu_retired_fraction")},
             "node": {k: v for k, v in fields.items() if k not in ("lanes_per_wave_step", "gpu_retired_fraction")},
             "coverage": summary["coverage"], "unique_crashes": summary["unique_crashes"],
+            "node_summary": summary,
             "cpu_baseline": cpu.get("tlv_server"),
             "host_cpus": core_info,
         }

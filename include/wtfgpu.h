@@ -212,6 +212,22 @@ int wtfgpu_set_code_pages(wtfgpu_ctx *ctx, const uint64_t *vpns, uint32_t n);
  * overlays dropped, retired count 0, coverage logs cleared, status RUNNING. */
 int wtfgpu_restore(wtfgpu_ctx *ctx, uint32_t first, uint32_t count);
 
+/* Streaming (continuous batching: lanes are slots refilled as their
+ * testcases finish; the same reset as wtfgpu_restore for a lane list). The
+ * lanes' coverage-log bits must have been collected with
+ * wtfgpu_collect_coverage_lanes first. */
+int wtfgpu_restore_lanes(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n);
+/* Feeds of a lane list, each in a fixed per-lane region (running lanes keep
+ * theirs): lane lanes[i] gets bytes[offsets[i] .. offsets[i+1]); has_feed[i]
+ * == 0, or a feed larger than the region, sends that lane's FEED hits to the
+ * host handler. */
+int wtfgpu_set_feed_lanes(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, const uint64_t *offsets,
+                          const uint8_t *has_feed, const uint8_t *bytes, uint64_t nbytes);
+/* New-coverage logs of a lane list (as wtfgpu_read_coverage); cap = 0 only
+ * counts, a call with cap >= the count also drops those lanes from the logs. */
+int wtfgpu_collect_coverage_lanes(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, uint32_t *out_lanes,
+                                  uint64_t *out_rips, uint64_t cap, uint64_t *total, uint32_t *overflow);
+
 /* Bulk register I/O for lanes [first, first+count). */
 int wtfgpu_read_regs(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, wtfgpu_regs_t *out);
 int wtfgpu_write_regs(wtfgpu_ctx *ctx, uint32_t first, uint32_t count,

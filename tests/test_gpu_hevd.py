@@ -52,6 +52,18 @@ def test_hevd_parity_host_handlers_only(target, tmp_path):
     assert len(h) == len(t) and not bad, bad[:10]
 
 
+@pytest.mark.parametrize("slice_steps", [128, 4096])
+def test_hevd_streaming_parity(target, tmp_path, slice_steps):
+    """Continuous batching with host-serviced breakpoints (ExGenRandom,
+    KeBugCheck2, SwapContext) and ring-0 paths: every input as the twin."""
+    inp = os.path.join(target, "parity")
+    g = H.run(H.WTFGPU, target, inp, str(tmp_path / "g.jsonl"), lanes=256, name="hevd",
+              extra=("--stream-run", "--slice-steps", str(slice_steps)))
+    t = H.run(H.TWIN, target, inp, str(tmp_path / "t.jsonl"), lanes=512, name="hevd")
+    bad = [(x["input"], k) for x, y in zip(g, t) for k in FIELDS if x[k] != y[k]]
+    assert len(g) == len(t) and not bad, bad[:10]
+
+
 def test_hevd_fuzz_smoke(target):
     st = H.fuzz(H.WTFGPU, target, runs=8192, lanes=4096, name="hevd", max_len=1028)
     assert st["execs"] == 8192 and st["errors"] == 0

@@ -66,7 +66,22 @@ def test_tlv_lane_order_coverage_attribution(target, tmp_path):
     assert not _diff(g, t)
 
 
-def test_tlv_fuzz_smoke(target):
-    st = H.fuzz(H.WTFGPU, target, runs=8192, lanes=4096)
+@pytest.mark.parametrize("slice_steps", [64, 2048])
+def test_tlv_streaming_parity(target, tmp_path, slice_steps):
+    """Continuous batching (lanes refilled as their testcases finish: per-lane
+    restore, feed regions, per-lane coverage collection) replays every input
+    exactly as the twin does; short slices force many refills and lanes that
+    straddle slices."""
+    inp = os.path.join(target, "parity")
+    g = H.run(H.WTFGPU, target, inp, str(tmp_path / "g.jsonl"), lanes=256,
+              extra=("--stream-run", "--slice-steps", str(slice_steps)))
+    t = H.run(H.TWIN, target, inp, str(tmp_path / "t.jsonl"), lanes=512)
+    assert len(g) == len(t)
+    assert not _diff(g, t)
+
+
+@pytest.mark.parametrize("slice_steps", [0, 4096])
+def test_tlv_fuzz_smoke(target, slice_steps):
+    st = H.fuzz(H.WTFGPU, target, runs=8192, lanes=4096, extra=("--slice-steps", str(slice_steps)))
     assert st["execs"] == 8192 and st["errors"] == 0
-    assert st["unique_crashes"] >= 2
+    assert st["unique_crashes"] >= 2 and st["coverage"] >= 150

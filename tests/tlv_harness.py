@@ -38,9 +38,10 @@ def run(exe: str, target: str, inputs: str, results: str, lanes: int, limit: int
 
 
 def fuzz(exe: str, target: str, runs: int, lanes: int, seed: int = 1337, limit: int = 100000,
-         seconds: float = 0, timeout: int = 600, name: str = "tlv_server", max_len: int = 0x1000) -> dict:
+         seconds: float = 0, timeout: int = 600, name: str = "tlv_server", max_len: int = 0x1000,
+         extra=()) -> dict:
     cmd = [exe, "fuzz", "--name", name, "--target", target, "--runs", str(runs), "--lanes", str(lanes),
-           "--seed", str(seed), "--limit", str(limit), "--max_len", str(max_len)]
+           "--seed", str(seed), "--limit", str(limit), "--max_len", str(max_len), *extra]
     if seconds:
         cmd += ["--seconds", str(seconds)]
     out = subprocess.run(cmd, check=True, timeout=timeout, capture_output=True, text=True).stdout

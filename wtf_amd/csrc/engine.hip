@@ -851,6 +851,36 @@ struct InitState {
   LaneSys sys;
 };
 
+// Registers, system state and overlay of one lane back to the snapshot (the
+// dirty-list reset: overlays dropped, nothing copied).
+__device__ __forceinline__ void restore_lane(const Dev &P, const InitState &s, const wtfgpu_regs_t *full0,
+                                             wtfgpu_regs_t *full, u32 lane) {
+  const u64 N = P.nlanes;
+  full[lane] = *full0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) P.gpr[i * N + lane] = s.g[i];
+  P.rip[lane] = s.rip;
+  P.rflags[lane] = s.rflags;
+  P.fs_base[lane] = s.fsb;
+  P.gs_base[lane] = s.gsb;
+  P.icount[lane] = 0;
+  P.nbytes[lane] = 0;
+  P.status[lane] = WTFGPU_RUNNING;
+  P.lflags[lane] = 0;
+  P.sys[lane] = s.sys;
+  P.ov_count[lane] = 0;
+}
+
+// Streaming form: a lane list. Coverage-log bits of these lanes were cleared
+// when their previous testcase was collected (k_cov_collect_lanes).
+__global__ void k_restore_list(Dev P, const InitState *S, const wtfgpu_regs_t *full0, wtfgpu_regs_t *full,
+                               const u32 *lanes, u32 n) {
+  const u32 t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const InitState s = *S;
+  restore_lane(P, s, full0, full, lanes[t]);
+}
+
 __global__ void k_restore(Dev P, const InitState *S, const wtfgpu_regs_t *full0, wtfgpu_regs_t *full, u32 first,
                           u32 count) {
   const u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1150,6 +1180,49 @@ __global__ void k_cov_absorb(const u8 *map, u8 *shadow, u64 n16, u64 *out_idx, u
   if (write) ((uint4 *)shadow)[t] = m;
 }
 
+// Streaming collection: the log entries of the requested lanes of each listed
+// wave (waves[i], lane mask masks[i]); with `clear`, those lanes' bits leave
+// the entries, and an entry left with no lane is freed (a later insert of
+// its rip may then make a second entry: harmless, both are collected).
+__global__ void k_cov_collect_lanes(Dev P, const u32 *waves, const u64 *masks, u32 nw, u32 *out_lane, u64 *out_rip,
+                                    u64 cap, unsigned long long *n_out, int clear) {
+  const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (u64)nw * P.H) return;
+  const u32 i = (u32)(t / P.H), wv = waves[i];
+  const u64 idx = (u64)wv * P.H + (t % P.H);
+  if (P.cov_ep[idx] != P.cov_wave_ep[wv]) return;
+  const u64 em = P.cov_mask[idx], hit = em & masks[i];
+  if (!hit) return;
+  const u64 rip = P.cov_rip[idx];
+  for (u64 m = hit; m; m &= m - 1) {
+    const int b = __ffsll((long long)m) - 1;
+    const unsigned long long pos = atomicAdd(n_out, 1ull);
+    if (pos < cap) {
+      out_lane[pos] = wv * P.lpw + b;
+      out_rip[pos] = rip;
+    }
+  }
+  if (clear) {
+    P.cov_mask[idx] = em & ~masks[i];
+    if ((em & ~masks[i]) == 0) P.cov_ep[idx] = 0;
+  }
+}
+
+// Per-lane feed regions (streaming): `n` lanes, lane lanes[i] gets
+// len[i] bytes from src + off[i] at its region.
+__global__ void k_feed_scatter(u8 *feed, u64 stride, const u32 *lanes, const u64 *off, const u64 *len, u32 n,
+                               const u8 *src, u64 *feed_pos, u64 *feed_end, const u64 *pos, const u64 *end) {
+  const u32 i = blockIdx.x;
+  if (i >= n) return;
+  if (threadIdx.x == 0) {
+    feed_pos[lanes[i]] = pos[i];
+    feed_end[lanes[i]] = end[i];
+  }
+  u8 *dst = feed + (u64)lanes[i] * stride;
+  const u8 *s = src + off[i];
+  for (u64 k = threadIdx.x; k < len[i]; k += blockDim.x) dst[k] = s[k];
+}
+
 __global__ void k_cov_commit(Dev P, const u64 *rips, u64 n) {
   const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n || !P.code_keys) return;
@@ -1205,6 +1278,7 @@ struct wtfgpu_ctx {
   u64 *d_feedpos = nullptr, *d_feedend = nullptr;
   u8 *d_feeddata = nullptr;
   u64 feed_cap = 0;
+  u64 feed_stride = 0;  // streaming: bytes of feed region per lane (0 = one packed feed)
   // coverage
   u64 *d_codekeys = nullptr;
   u32 *d_codeslot = nullptr;
@@ -1657,6 +1731,7 @@ int wtfgpu_set_feed(wtfgpu_ctx *c, uint32_t first, uint32_t count, const uint64_
     HIPCHK(hipMemcpy(c->d_feedpos, none.data(), N * 8, hipMemcpyHostToDevice));
   }
   // the data of one call is the whole feed (earlier feeds are replaced)
+  c->feed_stride = 0;  // packed layout (per-lane regions: wtfgpu_set_feed_lanes)
   if (nbytes > c->feed_cap) {
     dfree(c->d_feeddata);
     c->d_feeddata = nullptr;
@@ -1727,6 +1802,81 @@ int wtfgpu_restore(wtfgpu_ctx *c, uint32_t first, uint32_t count) {
   k_restore<<<(count + 255) / 256, 256, 0, c->stream>>>(c->P, c->d_init, c->d_init_full, c->d_full, first, count);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_restore_lanes(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n) {
+  if (!c || !c->d_gpr || !c->have_initial || (n && !lanes)) return WTFGPU_ERR_INVALID;
+  if (n == 0) return WTFGPU_OK;
+  for (u32 i = 0; i < n; i++)
+    if (lanes[i] >= c->P.nlanes) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  if (ensure_scratch(c, (u64)n * 4)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemcpyAsync(c->d_scratch, lanes, (u64)n * 4, hipMemcpyHostToDevice, c->stream));
+  k_restore_list<<<(n + 255) / 256, 256, 0, c->stream>>>(c->P, c->d_init, c->d_init_full, c->d_full,
+                                                         (const u32 *)c->d_scratch, n);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_set_feed_lanes(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, const uint64_t *offsets,
+                          const uint8_t *has_feed, const uint8_t *bytes, uint64_t nbytes) {
+  if (!c || !c->d_gpr || (n && (!lanes || !offsets)) || (nbytes && !bytes)) return WTFGPU_ERR_INVALID;
+  for (u32 i = 0; i < n; i++)
+    if (lanes[i] >= c->P.nlanes || offsets[i + 1] < offsets[i] || offsets[i + 1] > nbytes) return WTFGPU_ERR_INVALID;
+  if (n == 0) return WTFGPU_OK;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const u64 N = c->P.nlanes;
+  if (!c->d_feedpos) {
+    if (dalloc(&c->d_feedpos, N) || dalloc(&c->d_feedend, N)) return WTFGPU_ERR_OOM;
+    std::vector<u64> none(N, ~0ull);
+    HIPCHK(hipMemcpy(c->d_feedpos, none.data(), N * 8, hipMemcpyHostToDevice));
+  }
+  if (c->feed_stride == 0) {  // switch to per-lane regions (a packed feed's lanes are finished by now)
+    const u64 stride = 16384;
+    dfree(c->d_feeddata);
+    c->d_feeddata = nullptr;
+    c->feed_cap = 0;
+    if (dalloc(&c->d_feeddata, N * stride)) return WTFGPU_ERR_OOM;
+    c->feed_cap = N * stride;
+    c->feed_stride = stride;
+  }
+  const u64 S = c->feed_stride;
+  std::vector<u64> pos(n), end(n), off(n), len(n);
+  for (u32 i = 0; i < n; i++) {
+    const u64 L = offsets[i + 1] - offsets[i];
+    const bool has = (!has_feed || has_feed[i]) && L <= S;  // a feed too big for its region: host handler
+    off[i] = offsets[i];
+    len[i] = has ? L : 0;
+    pos[i] = has ? (u64)lanes[i] * S : ~0ull;
+    end[i] = has ? (u64)lanes[i] * S + L : 0;
+  }
+  // one staging upload of the lane metadata (lanes | off | len | pos | end),
+  // one of the bytes (straight from the caller's buffer: pinned memory DMAs),
+  // then one scatter
+  const u64 a8 = ((u64)n * 8 + 255) & ~255ull;
+  const u64 o_off = ((u64)n * 4 + 255) & ~255ull, o_len = o_off + a8, o_pos = o_len + a8, o_end = o_pos + a8,
+            o_data = o_end + a8;
+  if (ensure_scratch(c, o_data + nbytes)) return WTFGPU_ERR_OOM;
+  std::vector<u8> stage(o_data);
+  memcpy(stage.data(), lanes, (u64)n * 4);
+  memcpy(stage.data() + o_off, off.data(), (u64)n * 8);
+  memcpy(stage.data() + o_len, len.data(), (u64)n * 8);
+  memcpy(stage.data() + o_pos, pos.data(), (u64)n * 8);
+  memcpy(stage.data() + o_end, end.data(), (u64)n * 8);
+  HIPCHK(hipMemcpyAsync(c->d_scratch, stage.data(), stage.size(), hipMemcpyHostToDevice, c->stream));
+  if (nbytes) HIPCHK(hipMemcpyAsync(c->d_scratch + o_data, bytes, nbytes, hipMemcpyHostToDevice, c->stream));
+  k_feed_scatter<<<n, 256, 0, c->stream>>>(c->d_feeddata, S, (const u32 *)c->d_scratch,
+                                           (const u64 *)(c->d_scratch + o_off), (const u64 *)(c->d_scratch + o_len), n,
+                                           c->d_scratch + o_data, c->d_feedpos, c->d_feedend,
+                                           (const u64 *)(c->d_scratch + o_pos), (const u64 *)(c->d_scratch + o_end));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->P.feed_pos = c->d_feedpos;
+  c->P.feed_end = c->d_feedend;
+  c->P.feed_data = c->d_feeddata;
   return WTFGPU_OK;
 }
 
@@ -2221,6 +2371,62 @@ int wtfgpu_read_coverage(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint32_t
   }
   HIPCHK(hipStreamSynchronize(c->stream));
   *n = got;
+  return WTFGPU_OK;
+}
+
+int wtfgpu_collect_coverage_lanes(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, uint32_t *out_lanes,
+                                  uint64_t *out_rips, uint64_t cap, uint64_t *total, uint32_t *overflow) {
+  if (!c || !total || (n && !lanes) || (cap && (!out_lanes || !out_rips))) return WTFGPU_ERR_INVALID;
+  *total = 0;
+  if (overflow) *overflow = 0;
+  if (!c->d_covrip || n == 0) return WTFGPU_OK;
+  HIPCHK(hipSetDevice(c->device));
+  // per-wave request masks
+  std::vector<u32> waves;
+  std::vector<u64> masks;
+  {
+    std::vector<u32> sorted(lanes, lanes + n);
+    std::sort(sorted.begin(), sorted.end());
+    for (u32 l : sorted) {
+      if (l >= c->P.nlanes) return WTFGPU_ERR_INVALID;
+      const u32 w = l / c->P.lpw;
+      if (waves.empty() || waves.back() != w) {
+        waves.push_back(w);
+        masks.push_back(0);
+      }
+      masks.back() |= 1ull << (l % c->P.lpw);
+    }
+  }
+  const u32 nw = (u32)waves.size();
+  const u64 room = std::max<u64>(cap, 1);
+  const u64 o_m = ((u64)nw * 4 + 255) & ~255ull, o_n = (o_m + (u64)nw * 8 + 255) & ~255ull, o_l = o_n + 256,
+            o_r = (o_l + room * 4 + 255) & ~255ull;
+  if (ensure_scratch(c, o_r + room * 8)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemcpyAsync(c->d_scratch, waves.data(), (u64)nw * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_scratch + o_m, masks.data(), (u64)nw * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_scratch + o_n, 0, 8, c->stream));
+  const u64 threads = (u64)nw * c->P.H;
+  k_cov_collect_lanes<<<(u32)((threads + 255) / 256), 256, 0, c->stream>>>(
+      c->P, (const u32 *)c->d_scratch, (const u64 *)(c->d_scratch + o_m), nw, (u32 *)(c->d_scratch + o_l),
+      (u64 *)(c->d_scratch + o_r), cap, (unsigned long long *)(c->d_scratch + o_n), cap ? 1 : 0);
+  HIPCHK(hipGetLastError());
+  u64 got = 0;
+  HIPCHK(hipMemcpyAsync(&got, c->d_scratch + o_n, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const u64 m = std::min(got, cap);
+  if (m) {
+    HIPCHK(hipMemcpyAsync(out_lanes, c->d_scratch + o_l, m * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(out_rips, c->d_scratch + o_r, m * 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  if (overflow) {
+    const u32 nall = (c->P.nlanes + c->P.lpw - 1) / c->P.lpw;
+    std::vector<u32> ov(nall);
+    HIPCHK(hipMemcpyAsync(ov.data(), c->d_covovf, (u64)nall * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (u32 w : waves) *overflow |= ov[w];
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  *total = got;
   return WTFGPU_OK;
 }
 

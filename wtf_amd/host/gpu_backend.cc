@@ -18,6 +18,7 @@ thread_local uint64_t GpuBackend_t::servicing_sp_ = ~0ull;
 thread_local bool GpuBackend_t::scouting_ = false;
 
 namespace {
+constexpr uint64_t kFeedRegion = 16384;  // engine.hip wtfgpu_set_feed_lanes per-lane region
 using Clock = std::chrono::steady_clock;
 double ms_since(Clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
@@ -52,6 +53,7 @@ int gpr_index(Registers_t r) {
 
 GpuBackend_t::GpuBackend_t() = default;
 GpuBackend_t::~GpuBackend_t() {
+  if (feed_pin_) wtfgpu_host_free(ctx_, feed_pin_);
   if (ctx_) wtfgpu_destroy(ctx_);
 }
 
@@ -207,7 +209,10 @@ bool GpuBackend_t::SetBreakpoint(const Gva_t Gva, const BreakpointHandler_t Hand
 }
 
 bool GpuBackend_t::SetFeed(const uint8_t *Data, const uint64_t Size) {
-  if (!feed_action_) return false;
+  // the device serves the Feed action unless actions are off or the feed
+  // does not fit a lane's feed region (wtfgpu_set_feed_lanes): then the
+  // module's host handler must have its own copy
+  if (!feed_action_ || Size > kFeedRegion) return false;
   LaneView &v = cur();
   v.has_feed = true;
   v.feed.assign(Data, Data + Size);
@@ -345,6 +350,7 @@ uint8_t *GpuBackend_t::stage_copy(uint32_t lane, uint64_t gpfn, const uint8_t *o
 }
 
 void GpuBackend_t::drop_staged(LaneView &v) const {
+  if (v.pages.empty()) return;
   live_staged_ -= v.pages.size();
   v.pages.clear();
   if (live_staged_ == 0 && !omp_in_parallel()) {  // every staged page consumed: recycle the arenas
@@ -582,8 +588,9 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
 // The run loop over `lanes` (ascending): launch, classify exits, service
 // breakpoint hits on the host, resume; until every lane has a result.
 bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<LaneResult> *out, ModuleSlots *slots,
-                             bool per_lane_state) {
+                             bool per_lane_state, uint64_t slice, std::vector<uint32_t> *finished) {
   if (lanes.empty()) return true;
+  const bool sliced = finished != nullptr;  // one slice of `slice` wave-steps, then return
   const uint32_t first = lanes.front() & ~63u, count = lanes.back() + 1 - first;
   std::vector<wtfgpu_exit_t> ex(count);
   std::vector<uint8_t> done(count, 0);
@@ -597,14 +604,13 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
 
   for (;;) {
     wtfgpu_run_stats_t rs{};
-    if (wtfgpu_run(ctx_, first, count, ~0ull, &rs)) return false;
+    if (wtfgpu_run(ctx_, first, count, sliced ? slice : ~0ull, &rs)) return false;
     stats_.kernel_launches += rs.kernel_launches;
     stats_.kernel_ms += rs.kernel_ms;
     stats_.retired += rs.lane_retired;
     stats_.group_steps += rs.group_steps;
     stats_.rounds++;
     if (wtfgpu_read_exits(ctx_, first, count, ex.data())) return false;
-    const auto t0 = Clock::now();
     std::vector<uint32_t> hits;
     for (uint32_t l : pending) {
       if (done[l - first]) continue;
@@ -612,6 +618,7 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
       LaneView &v = views_[l];
       switch (e.status) {
         case WTFGPU_EXIT_BREAKPOINT: hits.push_back(l); continue;
+        case WTFGPU_RUNNING: continue;  // sliced: still running when the slice ended
         case WTFGPU_EXIT_TIMEOUT: v.result = Timedout_t(); break;    // bochscpu_backend.cc:458-469
         case WTFGPU_EXIT_INT3:                                         // :595-619
         case WTFGPU_EXIT_HLT: v.result = Crash_t(); break;             // :690-697
@@ -631,6 +638,44 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
       done[l - first] = 1;
     }
     if (hits.empty()) break;
+    if (!service_hits(hits, first, done, slots, per_lane_state)) return false;
+    if (sliced) break;  // the serviced lanes resume in the next slice
+    pending.clear();
+    for (uint32_t l : hits)
+      if (!done[l - first]) pending.push_back(l);
+  }
+  if (finished)
+    for (uint32_t l : lanes)
+      if (done[l - first]) finished->push_back(l);
+  // final state of every finished lane
+  if (out) {
+    std::vector<uint32_t> fin;
+    for (uint32_t l : lanes)
+      if (done[l - first]) fin.push_back(l);
+    std::vector<uint64_t> regs(fin.size() * 18);
+    if (!fin.empty() && wtfgpu_read_gprs_list(ctx_, fin.data(), (uint32_t)fin.size(), regs.data())) return false;
+    if (wtfgpu_read_exits(ctx_, first, count, ex.data())) return false;
+    for (size_t i = 0; i < fin.size(); i++) {
+      LaneResult &r = (*out)[fin[i]];
+      const LaneView &v = views_[fin[i]];
+      r.result = v.result ? *v.result : TestcaseResult_t(Ok_t());
+      memcpy(r.gprs, &regs[i * 18], 18 * 8);
+      r.rip = r.gprs[16];
+      r.icount = ex[fin[i] - first].icount;
+      r.exit_status = ex[fin[i] - first].status;
+    }
+  }
+  return true;
+}
+
+// Services one round's breakpoint hits on the host (BeforeExecutionHook,
+// bochscpu_backend.cc:476-548): bulk reads, prefetch, handlers (on all host
+// threads when the module's state is thread_local), flush, then each lane is
+// resumed or stopped (done[l - first] = 1).
+bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t first, std::vector<uint8_t> &done,
+                                ModuleSlots *slots, bool per_lane_state) {
+  const auto t0 = Clock::now();
+  {
     // ---- service the round's breakpoint hits
     std::vector<uint64_t> regs(hits.size() * 18);
     if (wtfgpu_read_gprs_list(ctx_, hits.data(), (uint32_t)hits.size(), regs.data())) return false;
@@ -824,22 +869,6 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
     if (!resume.empty() && wtfgpu_resume(ctx_, resume.data(), (uint32_t)resume.size(), skip.data())) return false;
     stats_.flush_ms += ms_since(t3);
     stats_.service_ms += ms_since(t0);
-    pending = resume;
-  }
-  // final state of every lane
-  if (out) {
-    std::vector<uint64_t> regs(lanes.size() * 18);
-    if (wtfgpu_read_gprs_list(ctx_, lanes.data(), (uint32_t)lanes.size(), regs.data())) return false;
-    if (wtfgpu_read_exits(ctx_, first, count, ex.data())) return false;
-    for (size_t i = 0; i < lanes.size(); i++) {
-      LaneResult &r = (*out)[lanes[i]];
-      const LaneView &v = views_[lanes[i]];
-      r.result = v.result ? *v.result : TestcaseResult_t(Ok_t());
-      memcpy(r.gprs, &regs[i * 18], 18 * 8);
-      r.rip = r.gprs[16];
-      r.icount = ex[lanes[i] - first].icount;
-      r.exit_status = ex[lanes[i] - first].status;
-    }
   }
   return true;
 }
@@ -912,35 +941,12 @@ bool GpuBackend_t::RunBatch(const Target_t &Target, const std::vector<std::pair<
   const auto tm = Clock::now();
   stats_.restore_ms += std::chrono::duration<double, std::milli>(tm - t0).count();
   // InsertTestcase per lane (client.cc:102), module state per lane
-  Backend_t *saved = g_Backend;
   std::vector<uint32_t> lanes(n);
-  std::vector<uint8_t> insert_ok(n, 1);
-  auto insert = [&](uint32_t l) {
-    cur_ = l;
-    if (Slots) {
-      Slots->ResetLane(l);
-      Slots->SwapIn(l);
-    }
-    insert_ok[l] = Target.InsertTestcase(Testcases[l].first, Testcases[l].second);
-    if (Slots) Slots->SwapOut(l);
-  };
-  const bool par = parallel_service(Slots);
-  if (par) {
-#pragma omp parallel
-    {
-      g_Backend = this;
-#pragma omp for schedule(dynamic, 256)
-      for (uint32_t l = 0; l < n; l++) insert(l);
-    }
-  } else {
-    g_Backend = this;
-    for (uint32_t l = 0; l < n; l++) insert(l);
-  }
-  g_Backend = saved;
-  for (uint32_t l = 0; l < n; l++) {
-    lanes[l] = l;
+  for (uint32_t l = 0; l < n; l++) lanes[l] = l;
+  std::vector<uint8_t> insert_ok;
+  insert_lanes(Target, lanes, Testcases, Slots, insert_ok);
+  for (uint32_t l = 0; l < n; l++)
     if (!insert_ok[l]) views_[l].result = Crash_t("insert-testcase-failed");
-  }
   const auto tu = Clock::now();
   stats_.module_ms += std::chrono::duration<double, std::milli>(tu - tm).count();
   if (flush_lanes(lanes) || upload_feed(n)) return false;
@@ -961,29 +967,231 @@ bool GpuBackend_t::RunBatch(const Target_t &Target, const std::vector<std::pair<
   stats_.coverage_ms += std::chrono::duration<double, std::milli>(tr - tc).count();
   // Target.Restore per lane (client.cc:145), then the device restore happens
   // at the start of the next batch (dirty-list reset)
+  target_restore(Target, lanes, Slots);
+  stats_.target_restore_ms += ms_since(tr);
+  stats_.total_ms += ms_since(t0);
+  stats_.batches++;
+  stats_.testcases += n;
+  return true;
+}
+
+void GpuBackend_t::insert_lanes(const Target_t &Target, const std::vector<uint32_t> &lanes,
+                                const std::vector<std::pair<const uint8_t *, size_t>> &tcs, ModuleSlots *Slots,
+                                std::vector<uint8_t> &ok) {
+  Backend_t *saved = g_Backend;
+  ok.assign(lanes.size(), 1);
+  auto insert = [&](size_t i) {
+    const uint32_t l = lanes[i];
+    cur_ = l;
+    if (Slots) {
+      Slots->ResetLane(l);
+      Slots->SwapIn(l);
+    }
+    ok[i] = Target.InsertTestcase(tcs[i].first, tcs[i].second);
+    if (Slots) Slots->SwapOut(l);
+  };
+  if (parallel_service(Slots)) {
+#pragma omp parallel
+    {
+      g_Backend = this;
+#pragma omp for schedule(dynamic, 256)
+      for (size_t i = 0; i < lanes.size(); i++) insert(i);
+    }
+  } else {
+    g_Backend = this;
+    for (size_t i = 0; i < lanes.size(); i++) insert(i);
+  }
+  g_Backend = saved;
+}
+
+// Target.Restore per lane (client.cc:145)
+void GpuBackend_t::target_restore(const Target_t &Target, const std::vector<uint32_t> &lanes, ModuleSlots *Slots) {
+  Backend_t *saved = g_Backend;
   auto restore = [&](uint32_t l) {
     cur_ = l;
     if (Slots) Slots->SwapIn(l);
     Target.Restore();
     if (Slots) Slots->SwapOut(l);
   };
-  if (par) {
+  if (parallel_service(Slots)) {
 #pragma omp parallel
     {
       g_Backend = this;
 #pragma omp for schedule(dynamic, 256)
-      for (uint32_t l = 0; l < n; l++) restore(l);
+      for (size_t i = 0; i < lanes.size(); i++) restore(lanes[i]);
     }
   } else {
     g_Backend = this;
-    for (uint32_t l = 0; l < n; l++) restore(l);
+    for (uint32_t l : lanes) restore(l);
   }
   g_Backend = saved;
   cur_ = 0;
+}
+
+// Streaming form of finish_coverage: the finished lanes' new rips, attributed
+// in the given order against the aggregate (bochscpu_backend.cc:501-504);
+// timed-out lanes' are revoked (client.cc:122-125); the fresh ones join the
+// device map. Their log bits are dropped (the lanes get new testcases next).
+void GpuBackend_t::collect_coverage(const std::vector<uint32_t> &lanes, std::vector<LaneResult> &res) {
+  const auto t0 = Clock::now();
+  uint64_t total = 0;
+  uint32_t ovf = 0;
+  wtfgpu_collect_coverage_lanes(ctx_, lanes.data(), (uint32_t)lanes.size(), nullptr, nullptr, 0, &total, &ovf);
+  std::vector<uint32_t> cl(total);
+  std::vector<uint64_t> cr(total);
+  if (total)
+    wtfgpu_collect_coverage_lanes(ctx_, lanes.data(), (uint32_t)lanes.size(), cl.data(), cr.data(), total, &total,
+                                  &ovf);
+  else  // nothing logged: still drop the lanes from the logs
+    wtfgpu_collect_coverage_lanes(ctx_, lanes.data(), (uint32_t)lanes.size(), cl.data(), cr.data(), 1, &total, &ovf);
+  const auto t1 = Clock::now();
+  stats_.covlog_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+  stats_.cov_entries += total;
+  if (getenv("WTFGPU_DEBUG_COV") && total) {
+    size_t known = 0;
+    for (uint64_t i = 0; i < total && i < cr.size(); i++) known += aggregate_.count(cr[i]);
+    fprintf(stderr, "collect: %zu lanes, %llu entries (%zu already in the aggregate of %zu); first rip %#llx\n",
+            lanes.size(), (unsigned long long)total, known, aggregate_.size(), (unsigned long long)(cr.empty() ? 0 : cr[0]));
+  }
+  std::unordered_map<uint32_t, std::vector<uint64_t>> per;
+  for (uint64_t i = 0; i < total && i < cl.size(); i++) per[cl[i]].push_back(cr[i]);
+  std::vector<uint64_t> fresh;
+  last_new_coverage_.clear();
+  for (uint32_t l : lanes) {
+    auto it = per.find(l);
+    if (it == per.end()) continue;
+    std::vector<uint64_t> &v = it->second;
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    if (full_coverage_) {  // parity mode: the lane's whole rip set, nothing committed
+      res[l].new_coverage = v;
+      continue;
+    }
+    const bool revoke = std::holds_alternative<Timedout_t>(res[l].result);
+    for (uint64_t rip : v) {
+      if (aggregate_.count(rip)) continue;
+      res[l].new_coverage.push_back(rip);
+      if (revoke) continue;
+      aggregate_.insert(rip);
+      fresh.push_back(rip);
+    }
+  }
+  if (!fresh.empty()) wtfgpu_commit_coverage(ctx_, fresh.data(), fresh.size());
+  stats_.attrib_ms += ms_since(t1);
+}
+
+uint32_t GpuBackend_t::FreeLanes() const {
+  if (busy_.empty()) return nlanes_;
+  uint32_t n = 0;
+  for (uint8_t b : busy_) n += !b;
+  return n;
+}
+
+// One streaming step: new testcases into free lanes (device reset of those
+// lanes + InsertTestcase + uploads), one slice over every occupied lane with
+// breakpoints serviced, then the finished lanes are harvested (results,
+// coverage attribution in lane order, Target.Restore) and freed.
+bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTestcase_t> &In, uint64_t Slice,
+                              std::vector<StreamResult_t> &Out, ModuleSlots *Slots) {
+  const auto t0 = Clock::now();
+  if (busy_.empty()) {
+    busy_.assign(nlanes_, 0);
+    tag_.assign(nlanes_, 0);
+    lres_.assign(nlanes_, LaneResult{});
+    // every lane idle until it gets a testcase
+    std::vector<uint32_t> all(nlanes_);
+    for (uint32_t l = 0; l < nlanes_; l++) all[l] = l;
+    if (wtfgpu_stop(ctx_, all.data(), nlanes_, WTFGPU_EXIT_IDLE)) return false;
+  }
+  // ---- refill
+  std::vector<uint32_t> fresh;
+  std::vector<std::pair<const uint8_t *, size_t>> tcs;
+  for (uint32_t l = 0; l < nlanes_ && fresh.size() < In.size(); l++)
+    if (!busy_[l]) {
+      fresh.push_back(l);
+      tcs.push_back({In[fresh.size() - 1].data, In[fresh.size() - 1].size});
+    }
+  if (!fresh.empty()) {
+    if (wtfgpu_restore_lanes(ctx_, fresh.data(), (uint32_t)fresh.size())) return false;
+#pragma omp parallel for schedule(static)
+    for (size_t i = 0; i < fresh.size(); i++) {
+      const uint32_t l = fresh[i];
+      reset_view(l);
+      busy_[l] = 1;
+      tag_[l] = In[i].tag;
+      lres_[l] = LaneResult{};
+    }
+    const auto tm = Clock::now();
+    stats_.restore_ms += std::chrono::duration<double, std::milli>(tm - t0).count();
+    std::vector<uint8_t> ok;
+    insert_lanes(Target, fresh, tcs, Slots, ok);
+    for (size_t i = 0; i < fresh.size(); i++)
+      if (!ok[i]) views_[fresh[i]].result = Crash_t("insert-testcase-failed");
+    const auto tu = Clock::now();
+    stats_.module_ms += std::chrono::duration<double, std::milli>(tu - tm).count();
+    if (flush_lanes(fresh)) return false;
+    if (feed_action_) {
+      const size_t n = fresh.size();
+      std::vector<uint64_t> off(n + 1, 0);
+      std::vector<uint8_t> has(n);
+      for (size_t i = 0; i < n; i++) {
+        const LaneView &v = views_[fresh[i]];
+        off[i + 1] = off[i] + v.feed.size();
+        has[i] = v.has_feed;
+      }
+      // packed into a pinned buffer on all host threads: one DMA to the device
+      if (off[n] > feed_pin_cap_) {
+        if (feed_pin_) wtfgpu_host_free(ctx_, feed_pin_);
+        feed_pin_ = nullptr;
+        feed_pin_cap_ = std::max<uint64_t>(off[n] * 2, 1 << 20);
+        void *p = nullptr;
+        if (wtfgpu_host_alloc(ctx_, feed_pin_cap_, &p)) return false;
+        feed_pin_ = (uint8_t *)p;
+      }
+#pragma omp parallel for schedule(static, 256)
+      for (size_t i = 0; i < n; i++) {
+        const LaneView &v = views_[fresh[i]];
+        if (!v.feed.empty()) memcpy(feed_pin_ + off[i], v.feed.data(), v.feed.size());
+      }
+      if (wtfgpu_set_feed_lanes(ctx_, fresh.data(), (uint32_t)n, off.data(), has.data(), feed_pin_, off[n]))
+        return false;
+    }
+    stats_.upload_ms += ms_since(tu);
+    stats_.testcases += fresh.size();
+  }
+  stats_.insert_ms += ms_since(t0);
+  // ---- one slice over the occupied lanes
+  std::vector<uint32_t> occupied, finished;
+  for (uint32_t l = 0; l < nlanes_; l++)
+    if (busy_[l]) occupied.push_back(l);
+  if (occupied.empty()) return true;
+  if (!run_lanes(occupied, &lres_, Slots, Slots != nullptr, Slice, &finished)) return false;
+  if (finished.empty()) {
+    stats_.total_ms += ms_since(t0);
+    return true;
+  }
+  // ---- harvest
+  const auto tc = Clock::now();
+  {
+    uint32_t lo = finished.front() & ~63u, hi = finished.back() + 1;
+    std::vector<uint64_t> nb(hi - lo);
+    if (wtfgpu_read_bytes(ctx_, lo, hi - lo, nb.data()) == WTFGPU_OK)
+      for (uint32_t l : finished) stats_.alg_bytes += nb[l - lo];
+  }
+  stats_.bytes_ms += ms_since(tc);
+  collect_coverage(finished, lres_);
+  const auto tr = Clock::now();
+  stats_.coverage_ms += std::chrono::duration<double, std::milli>(tr - tc).count();
+  target_restore(Target, finished, Slots);
   stats_.target_restore_ms += ms_since(tr);
+  for (uint32_t l : finished) {
+    Out.push_back(StreamResult_t{tag_[l], std::move(lres_[l])});
+    lres_[l] = LaneResult{};
+    busy_[l] = 0;
+    // not runnable until refilled (a finished lane keeps its exit status)
+  }
   stats_.total_ms += ms_since(t0);
   stats_.batches++;
-  stats_.testcases += n;
   return true;
 }
 
@@ -1001,14 +1209,15 @@ std::string GpuBackend_t::StatsJson() const {
            "\"prefetched_pages\":%llu,\"stack_windows\":%llu,\"staged_pages\":%llu,\"bulk_ms\":%.3f,\"prefetch_ms\":%.3f,"
            "\"handler_ms\":%.3f,\"fetch_ms\":%.3f,\"flush_ms\":%.3f,\"insert_ms\":%.3f,\"coverage_ms\":%.3f,"
            "\"target_restore_ms\":%.3f,\"alg_bytes\":%llu,\"restore_ms\":%.3f,\"module_ms\":%.3f,"
-           "\"upload_ms\":%.3f}",
+           "\"upload_ms\":%.3f,\"bytes_ms\":%.3f,\"covlog_ms\":%.3f,\"attrib_ms\":%.3f,\"cov_entries\":%llu}",
            (unsigned long long)stats_.group_steps, (unsigned long long)stats_.rounds,
            (unsigned long long)stats_.breakpoint_hits, (unsigned long long)stats_.kernel_launches, stats_.kernel_ms,
            stats_.service_ms, stats_.total_ms, (unsigned long long)stats_.page_fetches,
            (unsigned long long)stats_.prefetched_pages, (unsigned long long)stats_.stack_windows,
            (unsigned long long)stats_.staged_pages, stats_.bulk_ms, stats_.prefetch_ms, stats_.handler_ms,
            stats_.fetch_ms, stats_.flush_ms, stats_.insert_ms, stats_.coverage_ms, stats_.target_restore_ms,
-           (unsigned long long)stats_.alg_bytes, stats_.restore_ms, stats_.module_ms, stats_.upload_ms);
+           (unsigned long long)stats_.alg_bytes, stats_.restore_ms, stats_.module_ms, stats_.upload_ms,
+           stats_.bytes_ms, stats_.covlog_ms, stats_.attrib_ms, (unsigned long long)stats_.cov_entries);
   std::string r(b);
   r.pop_back();
   r += ",\"fetch_by_bp\":{";

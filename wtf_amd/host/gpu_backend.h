@@ -43,6 +43,9 @@ struct BatchStats {
   // insert_ms split: device restore + host views, module InsertTestcase calls,
   // register / memory / feed uploads
   double restore_ms = 0, module_ms = 0, upload_ms = 0;
+  // streaming harvest split: per-lane byte counters, coverage logs, attribution
+  double bytes_ms = 0, covlog_ms = 0, attrib_ms = 0;
+  uint64_t cov_entries = 0;  // (lane, rip) new-coverage log entries collected
 };
 
 class GpuBackend_t final : public Backend_t, public Executor_t {
@@ -85,6 +88,11 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   bool RunBatch(const Target_t &Target, const std::vector<std::pair<const uint8_t *, size_t>> &Testcases,
                 std::vector<LaneResult> &Out, ModuleSlots *Slots) override;
   Backend_t *AsBackend() override { return this; }
+  // streaming (continuous batching): see Executor_t
+  bool CanStream() const override { return true; }
+  uint32_t FreeLanes() const override;
+  bool StreamStep(const Target_t &Target, const std::vector<StreamTestcase_t> &In, uint64_t Slice,
+                  std::vector<StreamResult_t> &Out, ModuleSlots *Slots) override;
   void ResetCoverage() override;
   void SetFullCoverage(bool On) override { full_coverage_ = On; }
   size_t CoverageSize() const override { return aggregate_.size(); }
@@ -152,8 +160,26 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   void drop_staged(LaneView &v) const;
   bool in_overlay(const LaneView &v, uint64_t gpfn) const;
   int flush_lanes(const std::vector<uint32_t> &lanes);
+  // until every lane has a result; or, with `finished`, one slice of `slice`
+  // wave-steps (finished lanes appended to it, the others keep running)
   bool run_lanes(const std::vector<uint32_t> &lanes, std::vector<LaneResult> *out, ModuleSlots *slots,
-                 bool per_lane_state);
+                 bool per_lane_state, uint64_t slice = ~0ull, std::vector<uint32_t> *finished = nullptr);
+  bool service_hits(const std::vector<uint32_t> &hits, uint32_t first, std::vector<uint8_t> &done, ModuleSlots *slots,
+                    bool per_lane_state);
+  // InsertTestcase for `lanes` (restored views), module state per lane, on all
+  // host threads when the module allows it
+  void insert_lanes(const Target_t &Target, const std::vector<uint32_t> &lanes,
+                    const std::vector<std::pair<const uint8_t *, size_t>> &tcs, ModuleSlots *Slots,
+                    std::vector<uint8_t> &ok);
+  void target_restore(const Target_t &Target, const std::vector<uint32_t> &lanes, ModuleSlots *Slots);
+  // coverage of finished lanes, attributed in the order given (LastNewCoverage)
+  void collect_coverage(const std::vector<uint32_t> &lanes, std::vector<LaneResult> &res);
+  // streaming state: slot occupancy, the caller's tag per lane, results
+  std::vector<uint8_t> busy_;
+  std::vector<uint64_t> tag_;
+  std::vector<LaneResult> lres_;
+  uint8_t *feed_pin_ = nullptr;  // pinned staging of streamed feeds
+  uint64_t feed_pin_cap_ = 0;
   void finish_coverage(uint32_t n, std::vector<LaneResult> *out, std::vector<uint32_t> *timedout);
   bool set_code_pages();
 

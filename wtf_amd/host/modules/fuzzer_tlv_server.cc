@@ -17,9 +17,11 @@
 //  * the custom mutator (:204-365): Generate 1..10 packets one time in five,
 //    otherwise insert / copy-field / delete on a corpus testcase.
 // The only changes for batched execution are on GlobalState: it is declared
-// thread_local and named with WTF_LANE_STATE_TLS (module_slots.h). The packet
-// queue is per testcase, so per lane, and lanes are serviced on several host
-// threads at once.
+// thread_local and named with WTF_LANE_STATE_TLS (module_slots.h), and it holds
+// only the per-testcase packet queue (the snapshot registers moved out: they
+// are read-only after Init). The packet queue is per testcase, so per lane,
+// and lanes are serviced on several host threads at once. A backend that
+// takes the packets as a Feed (SetFeed true) leaves the queue empty.
 #include <deque>
 #include <string>
 #include <vector>
@@ -140,16 +142,19 @@ std::string Serialize(const std::vector<Packet_t> &Packets) {
   return S + "]}";
 }
 
+// The snapshot's registers (Init): read-only once set, so kept out of the
+// per-testcase state (the reference keeps both in one GlobalState,
+// fuzzer_tlv_server.cc:42-65).
+CpuState_t Context;
+void RestoreGprs(Backend_t *B) {
+  const CpuState_t &C = Context;
+  B->Rsp(C.Rsp), B->Rip(C.Rip), B->Rax(C.Rax), B->Rbx(C.Rbx), B->Rcx(C.Rcx), B->Rdx(C.Rdx);
+  B->Rsi(C.Rsi), B->Rdi(C.Rdi), B->R8(C.R8), B->R9(C.R9), B->R10(C.R10), B->R11(C.R11);
+  B->R12(C.R12), B->R13(C.R13), B->R14(C.R14), B->R15(C.R15);
+}
+
 thread_local struct {
   std::deque<Packet_t> Packets;
-  CpuState_t Context;
-
-  void RestoreGprs(Backend_t *B) {
-    const CpuState_t &C = Context;
-    B->Rsp(C.Rsp), B->Rip(C.Rip), B->Rax(C.Rax), B->Rbx(C.Rbx), B->Rcx(C.Rcx), B->Rdx(C.Rdx);
-    B->Rsi(C.Rsi), B->Rdi(C.Rdi), B->R8(C.R8), B->R9(C.R9), B->R10(C.R10), B->R11(C.R11);
-    B->R12(C.R12), B->R13(C.R13), B->R14(C.R14), B->R15(C.R15);
-  }
 } GlobalState;
 WTF_LANE_STATE_TLS(GlobalState);
 
@@ -172,7 +177,9 @@ bool InsertTestcase(const uint8_t *Buffer, const size_t BufferSize) {
     memcpy(Q + 10, &P.BodySize, 2);
     if (!P.Body.empty()) memcpy(Q + 12, P.Body.data(), P.Body.size());
   }
-  g_Backend->SetFeed(Feed.data(), Feed.size());
+  // a backend that serves ProcessPacket from the feed never runs the handler
+  // for this testcase: the queue stays empty
+  if (g_Backend->SetFeed(Feed.data(), Feed.size())) return true;
   for (Packet_t &P : Packets) GlobalState.Packets.emplace_back(std::move(P));
   return true;
 }
@@ -201,7 +208,7 @@ void OnProcessPacket(Backend_t *Backend) {
 }
 
 bool Init(const Options_t &, const CpuState_t &State) {
-  GlobalState.Context = State;
+  Context = State;
   const Gva_t ReturnAddress = Gva_t(g_Backend->VirtRead8(Gva_t(g_Backend->Rsp())));
   if (!g_Backend->SetBreakpoint("tlv_server!ProcessPacket", OnProcessPacket,
                                 BreakpointAction_t::Feed(Registers_t::Rcx, Registers_t::Rdx, 0x1000)))
@@ -209,7 +216,7 @@ bool Init(const Options_t &, const CpuState_t &State) {
   // both handlers below only move registers: their BreakpointAction_t lets the
   // gpu backend apply them on the device (no host round trip per packet)
   if (!g_Backend->SetBreakpoint(
-          ReturnAddress, [](Backend_t *) { GlobalState.RestoreGprs(g_Backend); },
+          ReturnAddress, [](Backend_t *) { RestoreGprs(g_Backend); },
           BreakpointAction_t::SetGprs(State))) {
     printf("Failed to SetBreakpoint on the return address.\n");
     return false;

@@ -120,4 +120,11 @@ bool TcpExchange_t::AllReduceMax(uint8_t *Map, uint64_t Bytes, bool Device) {
   return true;
 }
 
+bool TcpExchange_t::AllDone(bool Mine, bool *All) {
+  uint8_t notdone = Mine ? 0 : 1;
+  if (!AllReduceMax(&notdone, 1, false)) return false;
+  *All = notdone == 0;
+  return true;
+}
+
 }  // namespace wtfgpu_host

@@ -17,6 +17,7 @@ class TcpExchange_t final : public CoverageExchange_t {
   int Rank() const override { return rank_; }
   int World() const override { return world_; }
   bool AllReduceMax(uint8_t *Map, uint64_t Bytes, bool Device) override;
+  bool AllDone(bool Mine, bool *All) override;
 
  private:
   int rank_, world_;

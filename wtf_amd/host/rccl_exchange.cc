@@ -20,6 +20,7 @@ namespace wtfgpu_host {
 struct RcclExchange_t::Impl {
   ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;
+  uint8_t *flag = nullptr;  // device byte for AllDone
 };
 
 bool RcclUniqueId(uint8_t Out[kRcclIdBytes]) {
@@ -55,6 +56,7 @@ RcclExchange_t::RcclExchange_t(int Rank, int World) : rank_(Rank), world_(World)
 
 RcclExchange_t::~RcclExchange_t() {
   if (impl_->comm) ncclCommDestroy(impl_->comm);
+  if (impl_->flag) (void)hipFree(impl_->flag);
   delete impl_;
 }
 
@@ -76,6 +78,22 @@ bool RcclExchange_t::AllReduceMax(uint8_t *Map, uint64_t Bytes, bool Device) {
   if (!Device || !impl_->comm) return false;
   if (ncclAllReduce(Map, Map, Bytes, ncclUint8, ncclMax, impl_->comm, impl_->stream) != ncclSuccess) return false;
   return hipStreamSynchronize(impl_->stream) == hipSuccess;
+}
+
+bool RcclExchange_t::AllDone(bool Mine, bool *All) {
+  if (world_ <= 1) {
+    *All = Mine;
+    return true;
+  }
+  if (!impl_->flag && hipMalloc((void **)&impl_->flag, 1) != hipSuccess) return false;
+  uint8_t notdone = Mine ? 0 : 1;
+  if (hipMemcpyAsync(impl_->flag, &notdone, 1, hipMemcpyHostToDevice, impl_->stream) != hipSuccess) return false;
+  if (!AllReduceMax(impl_->flag, 1, true)) return false;
+  if (hipMemcpyAsync(&notdone, impl_->flag, 1, hipMemcpyDeviceToHost, impl_->stream) != hipSuccess ||
+      hipStreamSynchronize(impl_->stream) != hipSuccess)
+    return false;
+  *All = notdone == 0;
+  return true;
 }
 
 }  // namespace wtfgpu_host

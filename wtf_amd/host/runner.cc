@@ -142,6 +142,8 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
     else if (a == "--full-coverage") O.full_coverage = true;
     else if (a == "--quiet") O.quiet = true;
     else if (a == "--serial-mutation") O.serial_mutation = true;
+    else if (a == "--slice-steps") O.slice = strtoull(next("--slice-steps"), nullptr, 0);
+    else if (a == "--stream-run") O.stream_run = true;
     else if (a == "--rank") O.rank = atoi(next("--rank"));
     else if (a == "--world") O.world = atoi(next("--world"));
     else if (a == "--exchange") O.exchange = next("--exchange");
@@ -158,7 +160,7 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
   if (O.name.empty() || O.target.empty()) {
     fprintf(stderr, "usage: [run|fuzz] --name <target> --target <dir> [--input p] [--results f] [--limit n]\n"
                     "       [--lanes n] [--overlay-pages k] [--runs n] [--seconds s] [--seed s] [--full-coverage]\n"
-                    "       [--serial-mutation] [--rank r --world n [--exchange host:port | --nccl-id-file f]]\n");
+                    "       [--serial-mutation] [--slice-steps s] [--rank r --world n [--exchange host:port | --nccl-id-file f]]\n");
     return false;
   }
   return true;
@@ -211,7 +213,48 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
     if (!Out) return 1;
     const auto t0 = Clock::now();
     uint64_t Retired = 0;
-    for (size_t b = 0; b < Inputs.size(); b += N) {
+    auto print = [&](const fs::path &In, const LaneResult &L) {
+      std::vector<uint64_t> Cov = L.new_coverage;
+      std::sort(Cov.begin(), Cov.end());
+      fprintf(Out, "{\"input\":\"%s\",\"result\":\"%s\",\"crash\":\"%s\",\"error\":%d,\"exit\":%u,\"icount\":%llu,",
+              json_escape(In.filename().string()).c_str(), TestcaseResultName(L.result).c_str(),
+              json_escape(crash_name(L.result)).c_str(), (int)L.error, L.exit_status, (unsigned long long)L.icount);
+      fprintf(Out, "\"gprs\":[");
+      for (int g = 0; g < 18; g++) fprintf(Out, "%s%llu", g ? "," : "", (unsigned long long)L.gprs[g]);
+      fprintf(Out, "],\"coverage\":[");
+      for (size_t c = 0; c < Cov.size(); c++) fprintf(Out, "%s%llu", c ? "," : "", (unsigned long long)Cov[c]);
+      fprintf(Out, "]}\n");
+    };
+    if (O.stream_run && Exec.CanStream()) {
+      // streaming replay: lanes refilled as testcases finish, results printed
+      // in input order (parity with the batched replay, tests/test_gpu_tlv.py)
+      std::vector<std::vector<uint8_t>> Bufs(Inputs.size());
+      std::vector<LaneResult> Res(Inputs.size());
+      std::vector<uint8_t> Got(Inputs.size(), 0);
+      size_t next = 0, got = 0;
+      while (got < Inputs.size()) {
+        std::vector<StreamTestcase_t> In;
+        for (uint32_t f = Exec.FreeLanes(); f && next < Inputs.size(); f--, next++) {
+          Bufs[next] = ReadFile(Inputs[next]);
+          In.push_back(StreamTestcase_t{Bufs[next].data(), Bufs[next].size(), next});
+        }
+        std::vector<StreamResult_t> R;
+        if (!Exec.StreamStep(*Target, In, O.slice ? O.slice : 4096, R, &Slots)) {
+          printf("StreamStep failed\n");
+          return 1;
+        }
+        for (StreamResult_t &F : R) {
+          Res[F.tag] = std::move(F.r);
+          Got[F.tag] = 1;
+          got++;
+        }
+      }
+      for (size_t i = 0; i < Inputs.size(); i++) {
+        Retired += Res[i].icount;
+        print(Inputs[i], Res[i]);
+      }
+    }
+    for (size_t b = O.stream_run && Exec.CanStream() ? Inputs.size() : 0; b < Inputs.size(); b += N) {
       const size_t n = std::min<size_t>(N, Inputs.size() - b);
       std::vector<std::vector<uint8_t>> Bufs(n);
       std::vector<std::pair<const uint8_t *, size_t>> Tc(n);
@@ -226,19 +269,8 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
         return 1;
       }
       for (size_t i = 0; i < n; i++) {
-        const LaneResult &L = R[i];
-        Retired += L.icount;
-        std::vector<uint64_t> Cov = L.new_coverage;
-        std::sort(Cov.begin(), Cov.end());
-        fprintf(Out, "{\"input\":\"%s\",\"result\":\"%s\",\"crash\":\"%s\",\"error\":%d,\"exit\":%u,\"icount\":%llu,",
-                json_escape(Inputs[b + i].filename().string()).c_str(), TestcaseResultName(L.result).c_str(),
-                json_escape(crash_name(L.result)).c_str(), (int)L.error, L.exit_status,
-                (unsigned long long)L.icount);
-        fprintf(Out, "\"gprs\":[");
-        for (int g = 0; g < 18; g++) fprintf(Out, "%s%llu", g ? "," : "", (unsigned long long)L.gprs[g]);
-        fprintf(Out, "],\"coverage\":[");
-        for (size_t c = 0; c < Cov.size(); c++) fprintf(Out, "%s%llu", c ? "," : "", (unsigned long long)Cov[c]);
-        fprintf(Out, "]}\n");
+        Retired += R[i].icount;
+        print(Inputs[b + i], R[i]);
       }
     }
     if (Out != stdout) fclose(Out);
@@ -254,11 +286,15 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
     printf("Nothing to run: empty corpus and no inputs\n");
     return 1;
   }
-  while (!F.Done())
+  for (;;) {
+    bool done = F.Done();
+    if (X && X->World() > 1 && !X->AllDone(done, &done)) return 1;  // every shard stops together
+    if (done) break;
     if (!F.Step()) {
       printf("RunBatch failed\n");
       return 1;
     }
+  }
   printf("%s\n", F.SummaryJson().c_str());
   return 0;
 }
@@ -287,8 +323,27 @@ bool FuzzSession::Start() {
     Pending_.emplace_back(B.begin(), B.end());
   }
   t0_ = Clock::now();
-  Batch_ = MakeBatch(0);
+  stream_ = O_.slice && Exec_.CanStream();
+  if (stream_) {
+    for (std::string &S : MakeBatch(Budget(Exec_.Lanes()))) Ready_.push_back(std::move(S));
+    return !Ready_.empty();
+  }
+  Batch_ = MakeBatch(Budget(Exec_.Lanes()));
   return !Batch_.empty();
+}
+
+// at most n more testcases within the --runs budget
+uint64_t FuzzSession::Budget(uint64_t n) const {
+  if (!O_.runs) return n;
+  const uint64_t made = S_.execs + (stream_ ? InFlight_ + Ready_.size() : 0);
+  return made >= O_.runs ? 0 : std::min<uint64_t>(n, O_.runs - made);
+}
+
+bool FuzzSession::Done() const {
+  if (!stream_) return Batch_.empty();
+  if (O_.seconds > 0 && secs_since(t0_) >= O_.seconds) return true;  // in-flight testcases are dropped
+  return Ready_.empty() && InFlight_ == 0 && !Next_.valid() &&
+         (Budget(1) == 0 || !More(S_.execs) || Corpus_.Size() == 0);
 }
 
 bool FuzzSession::More(uint64_t done) const {
@@ -297,10 +352,8 @@ bool FuzzSession::More(uint64_t done) const {
 
 double FuzzSession::WallSeconds() const { return secs_since(t0_); }
 
-// The next batch: the corpus inputs first, then mutations of corpus picks.
-std::vector<std::string> FuzzSession::MakeBatch(uint64_t done) {
-  uint64_t n = Exec_.Lanes();
-  if (O_.runs) n = std::min<uint64_t>(n, O_.runs - done);
+// The next n testcases: the corpus inputs first, then mutations of corpus picks.
+std::vector<std::string> FuzzSession::MakeBatch(uint64_t n) {
   std::vector<std::string> Batch;
   Batch.reserve(n);
   while (Batch.size() < n && !Pending_.empty()) {
@@ -353,52 +406,113 @@ std::vector<std::string> FuzzSession::MakeBatch(uint64_t done) {
 // master's bookkeeping in lane order (server.h:816-886) and, across shards,
 // the coverage-map merge.
 bool FuzzSession::Step() {
+  // a shard that is done keeps joining the other shards' merges
+  if (X_ && X_->World() > 1 && Done()) return MergeCoverage();
+  if (stream_) return StreamStep();
   if (Batch_.empty()) return true;
   std::vector<std::pair<const uint8_t *, size_t>> Tc(Batch_.size());
   for (size_t i = 0; i < Batch_.size(); i++) Tc[i] = {(const uint8_t *)Batch_[i].data(), Batch_[i].size()};
   std::vector<LaneResult> R;
   const auto tb = Clock::now();
   const uint64_t after = S_.execs + Batch_.size();
-  if (More(after) && Corpus_.Size()) Next_ = std::async(std::launch::async, &FuzzSession::MakeBatch, this, after);
+  if (More(after) && Corpus_.Size()) {
+    const uint64_t n = O_.runs ? std::min<uint64_t>(Exec_.Lanes(), O_.runs - after) : Exec_.Lanes();
+    Next_ = std::async(std::launch::async, &FuzzSession::MakeBatch, this, n);
+  }
   if (!Exec_.RunBatch(Target_, Tc, R, &Slots_)) return false;
   S_.run_s += secs_since(tb);
   S_.batches++;
   std::vector<std::string> NextBatch;
   if (Next_.valid()) NextBatch = Next_.get();  // before the corpus / mutator change below
-  for (size_t i = 0; i < Batch_.size(); i++) {
-    const LaneResult &L = R[i];
-    S_.execs++;
+  for (size_t i = 0; i < Batch_.size(); i++) Account(Batch_[i], R[i]);
+  if (X_ && X_->World() > 1 && !MergeCoverage()) return false;
+  if (!NextBatch.empty() || !More(S_.execs))
+    Batch_ = std::move(NextBatch);
+  else
+    Batch_ = MakeBatch(Budget(Exec_.Lanes()));
+  return true;
+}
+
+// Streaming step (continuous batching): the free lanes get testcases from the
+// ready queue, every occupied lane runs one slice, the finished testcases are
+// accounted. The producer mutates the next testcases meanwhile, from the
+// corpus as it stood before this step's results.
+bool FuzzSession::StreamStep() {
+  if (Done()) return true;
+  std::vector<StreamTestcase_t> In;
+  const bool open = More(S_.execs);
+  if (open) {
+    const uint32_t free = Exec_.FreeLanes();
+    if (Ready_.size() < free && !Next_.valid() && Corpus_.Size())  // nothing in the pipe: make them now
+      for (std::string &S : MakeBatch(Budget(free - Ready_.size()))) Ready_.push_back(std::move(S));
+    const size_t take = std::min<size_t>(free, Ready_.size());
+    In.reserve(take);
+    for (size_t i = 0; i < take; i++) {
+      if (FreeSlot_.empty()) {
+        FreeSlot_.push_back(Slot_.size());
+        Slot_.emplace_back();
+      }
+      const uint64_t tag = FreeSlot_.back();
+      FreeSlot_.pop_back();
+      std::string &slot = Slot_[tag];
+      slot.swap(Ready_.front());
+      Ready_.pop_front();
+      InFlight_++;
+      In.push_back(StreamTestcase_t{(const uint8_t *)slot.data(), slot.size(), tag});
+    }
+    const uint64_t want = Budget(Exec_.Lanes() > Ready_.size() ? Exec_.Lanes() - Ready_.size() : 0);
+    if (want && Corpus_.Size() && !Next_.valid())
+      Next_ = std::async(std::launch::async, &FuzzSession::MakeBatch, this, want);
+  }
+  std::vector<StreamResult_t> Out;
+  const auto tb = Clock::now();
+  const bool ok = Exec_.StreamStep(Target_, In, O_.slice, Out, &Slots_);
+  S_.run_s += secs_since(tb);
+  const auto tw = Clock::now();
+  if (Next_.valid())  // before the corpus / mutator change below
+    for (std::string &S : Next_.get()) Ready_.push_back(std::move(S));
+  const auto ta = Clock::now();
+  S_.produce_wait_ms += std::chrono::duration<double, std::milli>(ta - tw).count();
+  if (!ok) return false;
+  S_.batches++;
+  for (StreamResult_t &F : Out) {
+    if (F.tag >= Slot_.size()) return false;
+    Account(Slot_[F.tag], F.r);
+    FreeSlot_.push_back(F.tag);  // the string keeps its buffer for the next testcase
+    InFlight_--;
+  }
+  S_.account_ms += secs_since(ta) * 1e3;
+  if (X_ && X_->World() > 1 && !MergeCoverage()) return false;
+  return true;
+}
+
+// The master's bookkeeping of one result (server.h:816-886).
+void FuzzSession::Account(const std::string &Tc, const LaneResult &L) {
+  S_.execs++;
     S_.retired += L.icount;
     if (L.error) {  // the engine could not finish it: neither a crash nor coverage
       S_.errors++;
       S_.error_retired += L.icount;
-      continue;
+      return;
     }
     if (std::holds_alternative<Timedout_t>(L.result)) S_.timeouts++;
     if (std::holds_alternative<Cr3Change_t>(L.result)) S_.cr3++;
     if (const Crash_t *C = std::get_if<Crash_t>(&L.result)) {
       S_.crashes++;
       if (!C->CrashName.empty() && CrashNames_.insert(C->CrashName).second)
-        SaveFile(T_ / "crashes" / C->CrashName, (const uint8_t *)Batch_[i].data(), Batch_[i].size());
+        SaveFile(T_ / "crashes" / C->CrashName, (const uint8_t *)Tc.data(), Tc.size());
     }
     // a timed-out testcase reports no coverage (the client revokes it,
     // client.cc:122-133); any other result with new coverage, crashes
     // included, joins the corpus after arming the mutator's cross-over
     // (server.h:816-853)
     if (!L.new_coverage.empty() && !std::holds_alternative<Timedout_t>(L.result)) {
-      Testcase_t Tcase((const uint8_t *)Batch_[i].data(), Batch_[i].size());
+      Testcase_t Tcase((const uint8_t *)Tc.data(), Tc.size());
       Mutator_->OnNewCoverage(Tcase);
-      LastNewCov_ = Batch_[i];
+      LastNewCov_ = Tc;
       HaveNewCov_ = true;
       Corpus_.SaveTestcase(L.result, std::move(Tcase));
     }
-  }
-  if (X_ && X_->World() > 1 && !MergeCoverage()) return false;
-  if (!NextBatch.empty() || !More(S_.execs))
-    Batch_ = std::move(NextBatch);
-  else
-    Batch_ = MakeBatch(S_.execs);
-  return true;
 }
 
 // every shard's coverage map, MAX-reduced over the shards; the
@@ -418,20 +532,21 @@ bool FuzzSession::MergeCoverage() {
 
 std::string FuzzSession::SummaryJson() const {
   const double Wall = WallSeconds();
-  char b[1024];
+  char b[2048];
   snprintf(b, sizeof(b),
            "{\"mode\":\"fuzz\",\"target\":\"%s\",\"lanes\":%u,\"rank\":%d,\"world\":%d,\"batches\":%llu,"
            "\"execs\":%llu,\"retired\":%llu,\"wall_s\":%.6f,\"run_s\":%.6f,\"execs_per_s\":%.3f,"
            "\"instr_per_s\":%.3f,\"coverage\":%zu,\"corpus\":%zu,\"crashes\":%llu,\"unique_crashes\":%zu,"
            "\"timeouts\":%llu,\"cr3\":%llu,\"errors\":%llu,\"error_retired\":%llu,\"merged_rips\":%llu,"
-           "\"merge_ms\":%.3f,"
+           "\"merge_ms\":%.3f,\"produce_wait_ms\":%.3f,\"account_ms\":%.3f,"
            "\"backend\":",
            O_.name.c_str(), Exec_.Lanes(), X_ ? X_->Rank() : 0, X_ ? X_->World() : 1,
            (unsigned long long)S_.batches, (unsigned long long)S_.execs, (unsigned long long)S_.retired, Wall,
            S_.run_s, S_.run_s > 0 ? S_.execs / S_.run_s : 0.0, S_.run_s > 0 ? S_.retired / S_.run_s : 0.0,
            Exec_.CoverageSize(), Corpus_.Size(), (unsigned long long)S_.crashes, CrashNames_.size(),
            (unsigned long long)S_.timeouts, (unsigned long long)S_.cr3, (unsigned long long)S_.errors,
-           (unsigned long long)S_.error_retired, (unsigned long long)S_.merged_rips, S_.merge_ms);
+           (unsigned long long)S_.error_retired, (unsigned long long)S_.merged_rips, S_.merge_ms, S_.produce_wait_ms,
+           S_.account_ms);
   return std::string(b) + Exec_.StatsJson() + "}";
 }
 

@@ -6,6 +6,8 @@
 #pragma once
 #include <chrono>
 #include <cstdint>
+#include <deque>
+#include <unordered_map>
 #include <future>
 #include <random>
 #include <string>
@@ -28,10 +30,31 @@ struct LaneResult {
   std::vector<uint64_t> new_coverage;  // LastNewCoverage, attributed in lane order
 };
 
+struct StreamTestcase_t {
+  const uint8_t *data;
+  size_t size;
+  uint64_t tag;  // the caller's name for it, returned with its result
+};
+struct StreamResult_t {
+  uint64_t tag;
+  LaneResult r;
+};
+
 // A backend that runs many testcases per call (GpuBackend_t; the oracle twin
 // runs them one after the other).
 class Executor_t {
  public:
+  // ---- streaming (continuous batching): lanes are slots. StreamStep puts
+  // testcases into free lanes (at most FreeLanes()), runs every occupied lane
+  // for one slice of `Slice` wave-steps and returns the testcases that
+  // finished, in lane order. A testcase's data is only read during the call.
+  virtual bool CanStream() const { return false; }
+  virtual uint32_t FreeLanes() const { return 0; }
+  virtual bool StreamStep(const Target_t &, const std::vector<StreamTestcase_t> &, uint64_t,
+                          std::vector<StreamResult_t> &, ModuleSlots *) {
+    return false;
+  }
+
   virtual ~Executor_t() = default;
   virtual Backend_t *AsBackend() = 0;
   virtual uint32_t Lanes() const = 0;
@@ -68,6 +91,8 @@ class CoverageExchange_t {
   virtual int Rank() const = 0;
   virtual int World() const = 0;
   virtual bool AllReduceMax(uint8_t *Map, uint64_t Bytes, bool Device) = 0;
+  // *All = every shard's Mine is true
+  virtual bool AllDone(bool Mine, bool *All) = 0;
 };
 
 struct RunnerOptions {
@@ -87,6 +112,11 @@ struct RunnerOptions {
   bool full_coverage = false;
   bool quiet = false;
   bool serial_mutation = false;  // one mutator, in order: the reference master's stream exactly
+  // fuzz: continuous batching on executors that stream (the gpu node): every
+  // occupied lane runs `slice` wave-steps per step, finished lanes are
+  // refilled at once; 0 = whole batches (every lane runs to its end)
+  uint64_t slice = 4096;
+  bool stream_run = false;  // run: replay the inputs through the streaming path
   int rank = 0, world = 1;         // fuzz: shard rank of world (one node per GPU)
   std::string exchange = "127.0.0.1:31337";  // TCP coverage exchange (CPU shards): rank 0 listens here
   std::string nccl_id_file;        // GPU shards: RCCL unique id file (rank 0 writes it)
@@ -96,6 +126,7 @@ struct FuzzStats {
   uint64_t execs = 0, retired = 0, crashes = 0, timeouts = 0, cr3 = 0, errors = 0, batches = 0, merged_rips = 0;
   uint64_t error_retired = 0;  // instructions retired by testcases the engine could not finish
   double run_s = 0, merge_ms = 0;
+  double produce_wait_ms = 0, account_ms = 0;  // streaming: waiting on the mutator, master bookkeeping
 };
 
 // The fuzz loop of one node / shard, one batch per Step(): an in-process
@@ -110,16 +141,19 @@ class FuzzSession {
   ~FuzzSession();
   bool Start();      // corpus inputs + the first batch; false = nothing to run
   bool Step();       // one batch; false = the executor failed
-  bool Done() const { return Batch_.empty(); }
+  bool Done() const;
   const FuzzStats &Stats() const { return S_; }
   size_t CorpusSize() const { return Corpus_.Size(); }
   double WallSeconds() const;
   std::string SummaryJson() const;
 
  private:
-  std::vector<std::string> MakeBatch(uint64_t done);
+  std::vector<std::string> MakeBatch(uint64_t n);
+  uint64_t Budget(uint64_t n) const;
   bool More(uint64_t done) const;
   bool MergeCoverage();
+  bool StreamStep();
+  void Account(const std::string &Tc, const LaneResult &L);
 
   const RunnerOptions O_;
   Executor_t &Exec_;
@@ -137,6 +171,12 @@ class FuzzSession {
   std::unordered_set<std::string> CrashNames_;
   FuzzStats S_;
   std::chrono::steady_clock::time_point t0_;
+  // streaming (RunnerOptions::slice != 0 on an executor that streams)
+  bool stream_ = false;
+  std::deque<std::string> Ready_;                      // mutated, not yet in a lane
+  std::vector<std::string> Slot_;  // tag -> testcase in a lane (tags are slot indices)
+  std::vector<uint64_t> FreeSlot_;
+  size_t InFlight_ = 0;
 };
 
 bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O);
