@@ -157,7 +157,7 @@ int wtfgpu_load_pool(wtfgpu_ctx *ctx, const uint64_t *gpfns, const uint8_t *page
                      uint64_t npages);
 
 /* Allocate lane storage. overlay_pages: copy-on-write pages per lane;
- * cov_entries: per-wave new-coverage log capacity (power of two). */
+ * cov_entries: per-lane new-coverage set capacity (power of two; 3/4 usable). */
 int wtfgpu_alloc_lanes(wtfgpu_ctx *ctx, uint32_t nlanes, uint32_t overlay_pages,
                        uint32_t cov_entries);
 uint32_t wtfgpu_lane_count(wtfgpu_ctx *ctx);
@@ -223,8 +223,9 @@ int wtfgpu_restore_lanes(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n);
  * host handler. */
 int wtfgpu_set_feed_lanes(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, const uint64_t *offsets,
                           const uint8_t *has_feed, const uint8_t *bytes, uint64_t nbytes);
-/* New-coverage logs of a lane list (as wtfgpu_read_coverage); cap = 0 only
- * counts, a call with cap >= the count also drops those lanes from the logs. */
+/* New-coverage sets of a lane list (as wtfgpu_read_coverage); a call whose
+ * cap covers the count also empties those lanes' sets (cap = 0 with an empty
+ * result included). */
 int wtfgpu_collect_coverage_lanes(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, uint32_t *out_lanes,
                                   uint64_t *out_rips, uint64_t cap, uint64_t *total, uint32_t *overflow);
 
@@ -312,9 +313,9 @@ int wtfgpu_host_free(wtfgpu_ctx *ctx, void *p);
 /* Dirty GPAs (page aligned) of one lane; *n gets the count (may exceed cap). */
 int wtfgpu_read_dirty(wtfgpu_ctx *ctx, uint32_t lane, uint64_t *gpas, uint32_t cap, uint32_t *n);
 
-/* New-coverage logs: RIPs executed by lanes [first, first+count) that were
+/* New-coverage sets: RIPs executed by lanes [first, first+count) that were
  * absent from the coverage map when executed. Writes up to cap (lane, rip)
- * pairs; *n gets the total. *overflow != 0 if a log overflowed. */
+ * pairs; *n gets the total. *overflow != 0 if a lane's set filled up. */
 int wtfgpu_read_coverage(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, uint32_t *lanes,
                          uint64_t *rips, uint64_t cap, uint64_t *n, uint32_t *overflow);
 /* Add RIPs to the coverage map (aggregate coverage). */

@@ -35,6 +35,20 @@
  *   U16 SYSCALL / SYSRETQ (64-bit forms; 32-bit SYSRET is unimplemented) load
  *       CS/SS selectors from STAR without descriptor-table reads; SWAPGS swaps
  *       GS.base with IA32_KERNEL_GS_BASE.
+ *   U19 IRETQ (64-bit operand size) pops rip, cs, rflags, rsp, ss and loads the
+ *       selectors without descriptor-table reads; the new CPL is cs.RPL (a
+ *       return to an inner ring, or a null cs, is #GP); rflags bits change as
+ *       the SDM's IRET lists for the current CPL / IOPL.
+ *   U20 MOV crN, r64 at CPL 0: cr0 / cr2 / cr4 / cr8 are written; a cr3 other
+ *       than the testcase's initial cr3 retires the instruction and ends the
+ *       testcase with Cr3Change_t (bochscpu_backend.cc:628-657; the limit
+ *       check of the retire hook runs after it and wins).
+ *   U21 RDTSC / RDTSCP return the snapshot's Tsc + the instructions retired
+ *       so far (bochs' tick counter advances one per instruction); RDMSR /
+ *       WRMSR at CPL 0 reach the MSRs CpuState_t carries (TSC, APIC_BASE,
+ *       SYSENTER_*, PAT, EFER, STAR, LSTAR, CSTAR, SFMASK, FS/GS/KERNEL_GS
+ *       base, TSC_AUX); any other MSR, a non-canonical base / entry point or
+ *       upper bits in SFMASK / TSC_AUX is #GP(0); EFER.LMA is read-only.
  */
 #include "x86_oracle.h"
 #include <stdlib.h>
@@ -1214,6 +1228,32 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
     }
     case 0xcc:
       return X_INT3;
+    case 0xcf: { /* iretq (64-bit operand size only; U19) */
+      if (!d->rexw) return X_UNIMPL;
+      u64 f[5]; /* rip, cs, rflags, rsp, ss: every read before any change */
+      for (int i = 0; i < 5; i++) CHK(vread(m, m->r.gpr[WTFGPU_RSP] + 8 * (u64)i, 8, &f[i]));
+      const u32 ocpl = (u32)cpl(m), ncpl = (u32)f[1] & 3;
+      if ((f[1] & 0xfffc) == 0 || ncpl < ocpl) {
+        fault(m, WTFGPU_VEC_GP, (u32)f[1] & 0xfffc);
+        return X_FAULT;
+      }
+      if (!is_canonical(f[0])) {
+        fault(m, WTFGPU_VEC_GP, 0);
+        return X_FAULT;
+      }
+      /* SDM IRET: status, TF, DF, NT, RF, AC, ID always; IF if CPL <= IOPL;
+       * IOPL, VIF, VIP at CPL 0 only; VM never in 64-bit mode */
+      u64 mask = 0x254dd5ULL;
+      const u32 iopl = (u32)(m->r.rflags >> 12) & 3;
+      if (ocpl == 0) mask |= 0x200ULL | 0x3000ULL | 0x80000ULL | 0x100000ULL;
+      else if (ocpl <= iopl) mask |= 0x200ULL;
+      m->r.rflags = (m->r.rflags & ~mask) | (f[2] & mask) | 2;
+      m->r.seg[WTFGPU_CS].selector = (u16)f[1];
+      m->r.seg[WTFGPU_SS].selector = (u16)f[4];
+      m->r.gpr[WTFGPU_RSP] = f[3];
+      *next_rip = f[0];
+      return X_OK;
+    }
     case 0xd7: { /* xlat */
       u64 addr = (m->r.gpr[WTFGPU_RBX] + (m->r.gpr[0] & 0xff));
       if (d->pfx67) addr &= 0xffffffffULL;
@@ -1337,8 +1377,19 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
         m->r.seg[WTFGPU_SS].selector = (u16)((((m->r.star >> 48) & 0xffff) + 8) | 3);
       }
       return X_OK;
-    case 0x01: /* swapgs (0f 01 f8) */
-      if (d->is_mem || (d->reg & 7) != 7 || (d->rm & 7) != 0) return X_UNIMPL;
+    case 0x01: /* swapgs (0f 01 f8), rdtscp (0f 01 f9) */
+      if (d->is_mem || (d->reg & 7) != 7 || (d->rm & 7) > 1) return X_UNIMPL;
+      if ((d->rm & 7) == 1) {
+        if ((m->r.cr4 & 4) && cpl(m) != 0) {
+          fault(m, WTFGPU_VEC_GP, 0);
+          return X_FAULT;
+        }
+        a = m->r.tsc + m->icount;
+        m->r.gpr[0] = a & 0xffffffffULL;
+        m->r.gpr[2] = a >> 32;
+        m->r.gpr[1] = m->r.tsc_aux & 0xffffffffULL;
+        return X_OK;
+      }
       if (cpl(m) != 0) {
         fault(m, WTFGPU_VEC_GP, 0);
         return X_FAULT;
@@ -1365,6 +1416,86 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
         return X_FAULT;
       }
       setreg(m, d, d->rm, 8, v);
+      return X_OK;
+    }
+    case 0x22: { /* mov crN, r64 (ring 0); a cr3 other than the testcase's
+                  * initial one ends it with Cr3Change_t after retiring
+                  * (bochscpu_backend.cc:628-657; U20) */
+      if (cpl(m) != 0) {
+        fault(m, WTFGPU_VEC_GP, 0);
+        return X_FAULT;
+      }
+      const u32 n = d->reg & 15;
+      const u64 v = m->r.gpr[d->rm & 15];
+      if (n == 0) m->r.cr0 = v;
+      else if (n == 2) m->r.cr2 = v;
+      else if (n == 3) {
+        m->r.cr3 = v;
+        if (v != m->initial_cr3) return X_CR3;
+      } else if (n == 4) m->r.cr4 = v;
+      else if (n == 8) m->r.cr8 = v & 15;
+      else {
+        fault(m, WTFGPU_VEC_UD, 0);
+        return X_FAULT;
+      }
+      return X_OK;
+    }
+    case 0x31: /* rdtsc: TSC = the snapshot's Tsc + instructions retired (U21) */
+      if ((m->r.cr4 & 4) && cpl(m) != 0) {
+        fault(m, WTFGPU_VEC_GP, 0);
+        return X_FAULT;
+      }
+      a = m->r.tsc + m->icount;
+      m->r.gpr[0] = a & 0xffffffffULL;
+      m->r.gpr[2] = a >> 32;
+      return X_OK;
+    case 0x30: /* wrmsr */
+    case 0x32: { /* rdmsr (the MSRs of CpuState_t; others #GP, U21) */
+      if (cpl(m) != 0) {
+        fault(m, WTFGPU_VEC_GP, 0);
+        return X_FAULT;
+      }
+      const u32 idx = (u32)m->r.gpr[1];
+      u64 *slot = NULL;
+      u64 tsc = m->r.tsc + m->icount, aux = m->r.tsc_aux, sfm = m->r.sfmask;
+      int canon = 0, lo32 = 0;
+      switch (idx) {
+      case 0x10: slot = &tsc; break;
+      case 0x1b: slot = &m->r.apic_base; break;
+      case 0x174: slot = &m->r.sysenter_cs; break;
+      case 0x175: slot = &m->r.sysenter_esp; canon = 1; break;
+      case 0x176: slot = &m->r.sysenter_eip; canon = 1; break;
+      case 0x277: slot = &m->r.pat; break;
+      case 0xc0000080: slot = &m->r.efer; break;
+      case 0xc0000081: slot = &m->r.star; break;
+      case 0xc0000082: slot = &m->r.lstar; canon = 1; break;
+      case 0xc0000083: slot = &m->r.cstar; canon = 1; break;
+      case 0xc0000084: slot = &sfm; lo32 = 1; break;
+      case 0xc0000100: slot = &m->r.seg[WTFGPU_FS].base; canon = 1; break;
+      case 0xc0000101: slot = &m->r.seg[WTFGPU_GS].base; canon = 1; break;
+      case 0xc0000102: slot = &m->r.kernel_gs_base; canon = 1; break;
+      case 0xc0000103: slot = &aux; lo32 = 1; break;
+      default: break;
+      }
+      if (!slot) {
+        fault(m, WTFGPU_VEC_GP, 0);
+        return X_FAULT;
+      }
+      if (op == 0x32) {
+        m->r.gpr[0] = *slot & 0xffffffffULL;
+        m->r.gpr[2] = *slot >> 32;
+        return X_OK;
+      }
+      const u64 v = (m->r.gpr[0] & 0xffffffffULL) | (m->r.gpr[2] << 32);
+      if ((canon && !is_canonical(v)) || (lo32 && (v >> 32))) {
+        fault(m, WTFGPU_VEC_GP, 0);
+        return X_FAULT;
+      }
+      if (idx == 0xc0000080) *slot = (v & ~0x400ULL) | (m->r.efer & 0x400ULL); /* LMA is read-only */
+      else *slot = v;
+      if (idx == 0x10) m->r.tsc = v - m->icount;
+      if (idx == 0xc0000084) m->r.sfmask = v;
+      if (idx == 0xc0000103) m->r.tsc_aux = v;
       return X_OK;
     }
     case 0xc7: /* rdrand r: deterministic 0 with CF=1 (U15) */
@@ -1675,6 +1806,7 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
         b == 0xb3 || b == 0xbb || b == 0xaf || b == 0xb0 || b == 0xb1 || b == 0xb6 ||
         b == 0xb7 || b == 0xbe || b == 0xbf || b == 0xbc || b == 0xbd || b == 0xb8 ||
         b == 0xc0 || b == 0xc1 || b == 0xa5 || b == 0xad || b == 0x0d || b == 0x01 || b == 0xc7 || b == 0x20 ||
+        b == 0x22 ||
         (b >= 0x18 && b <= 0x1f))
       has_modrm = 1;
     if (b == 0xa4 || b == 0xac || b == 0xba) {
@@ -1809,12 +1941,17 @@ static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
   u64 saved_bytes = m->bytes;
   u64 next = 0;
   int x = exec_insn(m, &d, &mr, &next);
-  if (x == X_OK) {
+  if (x == X_OK || x == X_CR3) {
     m->r.rip = next;
     m->bytes += d.len;
     m->icount++;
+    /* the limit check of the retire hook runs after the cr3 hook and wins */
     if (m->limit > 0 && m->icount > m->limit) {
       fill_exit(m, ex, WTFGPU_EXIT_TIMEOUT);
+      return ex->status;
+    }
+    if (x == X_CR3) {
+      fill_exit(m, ex, WTFGPU_EXIT_CR3);
       return ex->status;
     }
     ex->status = WTFGPU_RUNNING;

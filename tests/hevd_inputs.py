@@ -15,10 +15,12 @@ IOCTLS = [0x222003, 0x222007, 0x22200B, 0x22200F, 0x222013, 0x222017, 0x22201B, 
 
 def crafted() -> dict[str, bytes]:
     return {
-        "stack_ret_overrun": testcase(0x222003, b"A" * 512 + b"B" * 64),    # return address -> 0x4242.. (#GP)
+        "stack_ret_overrun": testcase(0x222003, b"A" * 512 + b"B" * 80),    # return address -> 0x4242.. (#GP)
         "stack_gs_cookie": testcase(0x222007, b"A" * 520),                  # cookie -> KeBugCheck2(0xF7)
         "write_what_where_bad": testcase(0x22200B, struct.pack("<QQ", USER_BUF, 0xFFFF800000000000)),
         "write_what_where_ok": testcase(0x22200B, struct.pack("<QQ", USER_BUF + 0x10, USER_BUF + 0x20)),
+        # a user address that faults inside __try: the trap resumes the handler through IRETQ
+        "write_what_where_user_fault": testcase(0x22200B, struct.pack("<QQ", 0x20000000, USER_BUF + 0x20)),
         "pool_overflow": testcase(0x22200F, b"P" * 0x210),                  # next header -> KeBugCheck2(0x19)
         "null_deref": testcase(0x222013, struct.pack("<I", 0xBAD0B0B0)),     # callback through NULL (#PF)
         "integer_wrap": testcase(0x222017, struct.pack("<I", 0xFFFFFFFC) + b"I" * 600 + struct.pack("<I", 0xBAD0B0B0)),

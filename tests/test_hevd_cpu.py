@@ -42,6 +42,10 @@ def test_crafted_bug_classes(target, tmp_path):
     write_inputs(d, 0)
     res = _run(target, d, str(tmp_path / "r.jsonl"))
     assert res["stack_gs_cookie"]["crash"].startswith("crash-0xf7-")           # DRIVER_OVERRAN_STACK_BUFFER
+    # a user-address fault inside __try: KiPageFault resumes the handler through
+    # IRETQ, which returns STATUS_ACCESS_VIOLATION to user mode
+    assert res["write_what_where_user_fault"]["result"] == "ok"
+    assert res["write_what_where_user_fault"]["gprs"][0] == 0xC0000005
     assert res["integer_wrap"]["crash"].startswith("crash-0xf7-")
     assert res["pool_overflow"]["crash"].startswith("crash-0x19-0x21-")        # BAD_POOL_HEADER
     assert res["wait_swapcontext"]["result"] == "cr3"                          # nt!SwapContext

@@ -6,6 +6,7 @@
 // bochscpu_backend.cc:730-797), batched guest-memory writes for host-side
 // handlers, coverage log compaction and the aggregate coverage map.
 #include <hip/hip_runtime.h>
+#include <hipcub/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <cstddef>
@@ -73,6 +74,8 @@ __device__ __forceinline__ void load_lane(const Dev &P, u32 lane, Lane &L) {
   L.bloom = 0;
   for (u32 k = 0; k < L.ovn; k++) L.bloom |= bloom_bit(P.ov_gpfn[(u64)k * N + lane]);
   L.lane = lane;
+  L.cgen = P.lane_gen ? P.lane_gen[lane] : 0;
+  L.ccnt = P.cov_cnt ? P.cov_cnt[lane] : 0;
   tlb_flush(L);
   L.tnext = 0;
   L.exvec = L.exerr = L.exop = 0;
@@ -93,41 +96,40 @@ __device__ __forceinline__ void store_lane(const Dev &P, const Lane &L) {
   P.nbytes[lane] = L.nbytes;
   P.status[lane] = L.status;
   P.ov_count[lane] = L.ovn;
+  if (P.cov_cnt) P.cov_cnt[lane] = L.ccnt;
 }
 
-// Coverage (bochscpu_backend.cc:501-504): every executed rip absent from the
-// aggregate map is logged once per wave with the mask of lanes that ran it.
-// Uniform; only reached for rips the uop cache does not already know are covered.
-__device__ __noinline__ void cover(const Dev &P, u64 rip, u64 gmask, u32 wv, u32 lid, u32 ep) {
+// Coverage (bochscpu_backend.cc:501-504): a rip absent from the aggregate map
+// joins the set of every lane that ran it (`mine`). The map check is uniform;
+// the set insert is per lane (its own open-addressing table, no contention
+// whatever wave runs the lane). Returns the lane's new entry count.
+__device__ __noinline__ u32 cover(const Dev &P, u64 rip, bool mine, u32 lane, u32 gen, u32 cnt) {
   if (P.code_keys) {
     u32 s;
     if (hash_find(P.code_keys, P.code_mask, rip >> 12, s)) {
       const u32 cs = rfl32(P.code_slot[s]);
-      if (rfl32(P.cov_map[(u64)cs * WTFGPU_PAGE_SIZE + (rip & 0xfff)])) return;
+      if (rfl32(P.cov_map[(u64)cs * WTFGPU_PAGE_SIZE + (rip & 0xfff)])) return cnt;
     }
   }
+  if (!mine) return cnt;
   const u32 H = P.H;
-  const u64 base = (u64)wv * H;
+  const u64 base = (u64)lane * H;
   u32 h = (u32)mix64(rip) & (H - 1);
   for (u32 probe = 0; probe < H; probe++) {
     const u64 idx = base + h;
-    const u32 e = rfl32(P.cov_ep[idx]);
-    if (e != ep) {
-      if (lid == 0) {
-        P.cov_rip[idx] = rip;
-        P.cov_mask[idx] = gmask;
-        P.cov_ep[idx] = ep;
+    if (P.cov_gen[idx] != gen) {
+      if (cnt >= H - H / 4) {  // keep probes short: a full set drops the rip
+        P.cov_overflow[lane] = 1;
+        return cnt;
       }
-      return;
+      P.cov_rip[idx] = rip;
+      P.cov_gen[idx] = gen;
+      return cnt + 1;
     }
-    if (rfl64(P.cov_rip[idx]) == rip) {
-      const u64 m = rfl64(P.cov_mask[idx]);
-      if ((m | gmask) != m && lid == 0) P.cov_mask[idx] = m | gmask;
-      return;
-    }
+    if (P.cov_rip[idx] == rip) return cnt;
     h = (h + 1) & (H - 1);
   }
-  if (lid == 0) P.cov_overflow[wv] = 1;
+  return cnt;
 }
 
 // Uniform fetch of up to 16 bytes at page pointer p (within one page).
@@ -399,11 +401,12 @@ __device__ __forceinline__ void retire(const Dev &P, Lane &L, int x, u32 len, u6
     tlb_flush(L);
     L.flush = 0;
   }
-  if (x == X_OK && L.status == WTFGPU_RUNNING) {
+  if ((x == X_OK || x == X_CR3) && L.status == WTFGPU_RUNNING) {
     L.rip = next;
     L.icount++;
     L.nbytes += len + L.pend;
     if (P.limit && L.icount > P.limit) L.status = WTFGPU_EXIT_TIMEOUT;
+    else if (x == X_CR3) L.status = WTFGPU_EXIT_CR3;  // bochscpu_backend.cc:628-657 (U20)
   } else if (L.status != WTFGPU_RUNNING) {
     // faulted / overlay full inside exec or service_miss; rip unchanged
   } else if (x == X_UNIMPL) {
@@ -502,8 +505,7 @@ __device__ __noinline__ bool bp_apply(const Dev &P, Lane &L, u64 grip) {
 
 // A step the uop cache cannot serve: code on a lane overlay page, or an
 // instruction that crosses into the next page (translated per lane).
-__device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr, bool ing, bool &skip, u32 wv,
-                                       u32 lid, u32 ep) {
+__device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr, bool ing, bool &skip) {
   const u32 off = (u32)(grip & 0xfff);
   IBytes ib;
   ib.avail = 4096 - off < 16 ? 4096 - off : 16;
@@ -546,7 +548,7 @@ __device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr
   }
   const u64 gmask = __ballot(ing);
   if (gmask == 0) return;
-  if (P.cov_rip) cover(P, grip, gmask, wv, lid, ep);
+  if (P.cov_rip) L.ccnt = cover(P, grip, ing, L.lane, L.cgen, L.ccnt);
   const bool isbp = bp_lookup(P, grip);
   if (ing) {
     if (isbp && !skip) {
@@ -642,9 +644,13 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
   const u32 lid = threadIdx.x & 63;
   const u32 hw = rfl32(blockIdx.x * 4 + (threadIdx.x >> 6));  // hardware wave in the launch (uniform)
   const u32 tid = hw * P.lpw + lid;
-  const u32 lane = first + tid;
-  const bool valid = lid < P.lpw && tid < count && lane < P.nlanes;
-  const u32 wv = first / P.lpw + hw;  // first is lpw-aligned: hardware wave == log wave (uniform)
+  const bool inrange = lid < P.lpw && tid < count && first + tid < P.nlanes;
+  // the lane this position runs: identity, or the regrouping order (lanes at
+  // the same rip side by side, k_regroup_keys + radix sort)
+  const u32 lane = inrange ? (P.perm ? P.perm[first + tid] : first + tid) : 0;
+  // a lane that is not running has its final exit already (or waits for the
+  // host): it is neither loaded nor stored
+  const bool valid = inrange && P.status[lane] == WTFGPU_RUNNING;
   __shared__ UCEntry sUC[4][UC_N];
   UCEntry *uc = sUC[threadIdx.x >> 6];
   for (u32 i = lid; i < UC_N; i += 64) uc[i].key = EMPTY_KEY;
@@ -663,7 +669,6 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
   }
   const u64 icount0 = L.icount;
   bool skip = valid && (P.lflags[lane] & 1);
-  const u32 ep = (P.cov_rip && wv < (P.nlanes + P.lpw - 1) / P.lpw) ? rfl32(P.cov_wave_ep[rfl32(wv)]) : 0;
   const u64 pool_lo = (u64)(uintptr_t)P.pool, pool_hi = pool_lo + (P.npool + 1) * WTFGPU_PAGE_SIZE;
   u64 steps = 0;
 #ifdef WTFGPU_STAMPS
@@ -763,7 +768,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       if (flags & UC_BADLEN) {
         if (ing) set_fault(L, WTFGPU_VEC_GP, 0, 0);
       } else {
-        WITH_LANE_COPY(slow_step(P, T, grip, lptr, ing, skip, wv, lid, ep));
+        WITH_LANE_COPY(slow_step(P, T, grip, lptr, ing, skip));
       }
       STAMP(5);
       continue;
@@ -775,7 +780,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     if (P.cov_rip && !(flags & UC_COVERED)) {
       const u64 logged = rfl64(e->logged);
       if (gmask & ~logged) {
-        cover(P, grip, gmask, wv, lid, ep);
+        L.ccnt = cover(P, grip, ing && !((logged >> lid) & 1), L.lane, L.cgen, L.ccnt);
         if (lid == 0) e->logged = logged | gmask;
       }
     }
@@ -869,10 +874,14 @@ __device__ __forceinline__ void restore_lane(const Dev &P, const InitState &s, c
   P.lflags[lane] = 0;
   P.sys[lane] = s.sys;
   P.ov_count[lane] = 0;
+  if (P.cov_rip) {
+    P.lane_gen[lane] += 1;
+    P.cov_cnt[lane] = 0;
+    P.cov_overflow[lane] = 0;
+  }
 }
 
-// Streaming form: a lane list. Coverage-log bits of these lanes were cleared
-// when their previous testcase was collected (k_cov_collect_lanes).
+// Streaming form: a lane list.
 __global__ void k_restore_list(Dev P, const InitState *S, const wtfgpu_regs_t *full0, wtfgpu_regs_t *full,
                                const u32 *lanes, u32 n) {
   const u32 t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -901,21 +910,10 @@ __global__ void k_restore(Dev P, const InitState *S, const wtfgpu_regs_t *full0,
   P.lflags[lane] = 0;
   P.sys[lane] = s.sys;
   P.ov_count[lane] = 0;  // the dirty-list reset: overlays dropped, nothing copied
-  if (P.cov_rip) {
-    const u32 wv = lane / P.lpw, bit = lane % P.lpw;
-    const u32 w0 = wv * P.lpw, w1 = w0 + P.lpw;
-    const bool whole = w0 >= first && w1 <= first + count;
-    if (bit == 0 && whole) {
-      P.cov_wave_ep[wv] += 1;  // invalidates every log entry of the wave
-      P.cov_overflow[wv] = 0;
-    } else if (!whole) {
-      // partial wave: drop this lane's bit from the wave's entries
-      for (u32 h = 0; h < P.H; h++) {
-        const u64 idx = (u64)wv * P.H + h;
-        if (P.cov_ep[idx] == P.cov_wave_ep[wv])
-          atomicAnd((unsigned long long *)&P.cov_mask[idx], ~(1ull << bit));
-      }
-    }
+  if (P.cov_rip) {       // the lane's coverage set empties
+    P.lane_gen[lane] += 1;
+    P.cov_cnt[lane] = 0;
+    P.cov_overflow[lane] = 0;
   }
 }
 
@@ -1137,28 +1135,46 @@ __global__ void k_gather_pages(Dev P, const u32 *lanes, const u64 *gpas, u32 n, 
 }
 
 // ---------------------------------------------------------------- coverage services
-__global__ void k_cov_collect(Dev P, u32 first, u32 count, u32 *out_lane, u64 *out_rip, u64 cap,
-                              unsigned long long *n_out) {
-  const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  const u32 w0 = first / P.lpw, w1 = (first + count + P.lpw - 1) / P.lpw;
-  const u64 total = (u64)(w1 - w0) * P.H;
-  if (t >= total) return;
-  const u32 wv = w0 + (u32)(t / P.H);
-  const u64 idx = (u64)wv * P.H + (t % P.H);
-  if (P.cov_ep[idx] != P.cov_wave_ep[wv]) return;
-  u64 m = P.cov_mask[idx];
-  const u64 rip = P.cov_rip[idx];
-  while (m) {
-    const int b = __ffsll((long long)m) - 1;
-    m &= m - 1;
-    const u32 lane = wv * P.lpw + b;
-    if (lane < first || lane >= first + count) continue;
+// The coverage sets of a lane list (lanes == nullptr: lanes first + i), one
+// block per lane, compacted into (lane, rip) pairs.
+__global__ void k_cov_collect(Dev P, const u32 *lanes, u32 first, u32 n, u32 *out_lane, u64 *out_rip, u64 cap,
+                              unsigned long long *n_out, u32 *ovf) {
+  const u32 i = blockIdx.x;
+  if (i >= n) return;
+  const u32 lane = lanes ? lanes[i] : first + i;
+  const u32 g = P.lane_gen[lane];
+  const u64 base = (u64)lane * P.H;
+  for (u32 k = threadIdx.x; k < P.H; k += blockDim.x) {
+    if (P.cov_gen[base + k] != g) continue;
     const unsigned long long pos = atomicAdd(n_out, 1ull);
     if (pos < cap) {
       out_lane[pos] = lane;
-      out_rip[pos] = rip;
+      out_rip[pos] = P.cov_rip[base + k];
     }
   }
+  if (threadIdx.x == 0 && P.cov_overflow[lane]) atomicOr(ovf, 1u);
+}
+
+// Regrouping keys: running lanes by rip (lanes at one rip become neighbours,
+// so one wave step serves them all), every other lane after them (their
+// waves find nothing to run and leave at once).
+__global__ void k_regroup_keys(Dev P, u32 first, u32 count, u32 *keys, u32 *lanes) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const u32 lane = first + i;
+  const u32 r = (u32)P.rip[lane] & 0xffffffu;  // 24 key bits: three radix passes
+  keys[i] = P.status[lane] == WTFGPU_RUNNING ? (r == 0xffffffu ? r - 1 : r) : 0xffffffu;
+  lanes[i] = lane;
+}
+
+// Empty the coverage sets of a lane list (generation bump: O(1) per lane).
+__global__ void k_cov_clear(Dev P, const u32 *lanes, u32 n) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const u32 lane = lanes[i];
+  P.lane_gen[lane] += 1;
+  P.cov_cnt[lane] = 0;
+  P.cov_overflow[lane] = 0;
 }
 
 // Bytes set in the coverage map but not in its shadow (what a MAX all-reduce
@@ -1178,34 +1194,6 @@ __global__ void k_cov_absorb(const u8 *map, u8 *shadow, u64 n16, u64 *out_idx, u
         if (write && pos < cap) out_idx[pos] = t * 16 + w * 4 + b;
       }
   if (write) ((uint4 *)shadow)[t] = m;
-}
-
-// Streaming collection: the log entries of the requested lanes of each listed
-// wave (waves[i], lane mask masks[i]); with `clear`, those lanes' bits leave
-// the entries, and an entry left with no lane is freed (a later insert of
-// its rip may then make a second entry: harmless, both are collected).
-__global__ void k_cov_collect_lanes(Dev P, const u32 *waves, const u64 *masks, u32 nw, u32 *out_lane, u64 *out_rip,
-                                    u64 cap, unsigned long long *n_out, int clear) {
-  const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (u64)nw * P.H) return;
-  const u32 i = (u32)(t / P.H), wv = waves[i];
-  const u64 idx = (u64)wv * P.H + (t % P.H);
-  if (P.cov_ep[idx] != P.cov_wave_ep[wv]) return;
-  const u64 em = P.cov_mask[idx], hit = em & masks[i];
-  if (!hit) return;
-  const u64 rip = P.cov_rip[idx];
-  for (u64 m = hit; m; m &= m - 1) {
-    const int b = __ffsll((long long)m) - 1;
-    const unsigned long long pos = atomicAdd(n_out, 1ull);
-    if (pos < cap) {
-      out_lane[pos] = wv * P.lpw + b;
-      out_rip[pos] = rip;
-    }
-  }
-  if (clear) {
-    P.cov_mask[idx] = em & ~masks[i];
-    if ((em & ~masks[i]) == 0) P.cov_ep[idx] = 0;
-  }
 }
 
 // Per-lane feed regions (streaming): `n` lanes, lane lanes[i] gets
@@ -1285,8 +1273,8 @@ struct wtfgpu_ctx {
   u8 *d_covmap = nullptr;
   u8 *d_covshadow = nullptr;  // the map as of the last absorb / own commit
   u64 ncovslots = 0;
-  u64 *d_covrip = nullptr, *d_covmask = nullptr;
-  u32 *d_covep = nullptr, *d_covwep = nullptr, *d_covovf = nullptr;
+  u64 *d_covrip = nullptr;
+  u32 *d_covgen = nullptr, *d_lanegen = nullptr, *d_covcnt = nullptr, *d_covovf = nullptr;
   std::vector<u64> code_vpns;
   // host copy of the pool (page-table marking, host-side reads)
   std::vector<u8> h_pool;
@@ -1299,8 +1287,13 @@ struct wtfgpu_ctx {
   wtfgpu_regs_t initial{};
   bool have_initial = false;
   u8 *d_scratch = nullptr;
+  // cross-wave regrouping (wtfgpu_run): sort keys, the lane order, radix-sort scratch
+  u32 *d_rkeys = nullptr, *d_rkeys2 = nullptr, *d_rlanes = nullptr, *d_perm = nullptr;
+  void *d_rtemp = nullptr;
+  size_t rtemp_bytes = 0;
   u64 scratch_bytes = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  u64 regroup_steps = 0;
 };
 
 namespace {
@@ -1409,6 +1402,7 @@ int wtfgpu_create(int device, wtfgpu_ctx **out) {
   wtfgpu_ctx *c = new (std::nothrow) wtfgpu_ctx();
   if (!c) return WTFGPU_ERR_OOM;
   c->device = device;
+  if (const char *e = getenv("WTFGPU_REGROUP_STEPS")) c->regroup_steps = strtoull(e, nullptr, 0);
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIPCHK(hipEventCreate(&c->ev0));
   HIPCHK(hipEventCreate(&c->ev1));
@@ -1441,10 +1435,17 @@ static void free_lanes(wtfgpu_ctx *c) {
   dfree(c->d_sys);
   dfree(c->d_ovdata);
   dfree(c->d_full);
+  dfree(c->d_rkeys);
+  dfree(c->d_rkeys2);
+  dfree(c->d_rlanes);
+  dfree(c->d_perm);
+  if (c->d_rtemp) (void)hipFree(c->d_rtemp);
+  c->d_rtemp = nullptr;
+  c->rtemp_bytes = 0;
   dfree(c->d_covrip);
-  dfree(c->d_covmask);
-  dfree(c->d_covep);
-  dfree(c->d_covwep);
+  dfree(c->d_covgen);
+  dfree(c->d_lanegen);
+  dfree(c->d_covcnt);
   dfree(c->d_covovf);
 }
 
@@ -1536,7 +1537,6 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
     const u32 v = (u32)atoi(e);
     if (v == 64 || v == 32 || v == 16) lpw = v;
   }
-  const u64 nw = (N + lpw - 1) / lpw;
   int rc = 0;
   rc |= dalloc(&c->d_gpr, 16 * N);
   rc |= dalloc(&c->d_rip, N);
@@ -1558,11 +1558,11 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
   }
   rc |= dalloc(&c->d_full, N);
   if (cov_entries) {
-    rc |= dalloc(&c->d_covrip, nw * cov_entries);
-    rc |= dalloc(&c->d_covmask, nw * cov_entries);
-    rc |= dalloc(&c->d_covep, nw * cov_entries);
-    rc |= dalloc(&c->d_covwep, nw);
-    rc |= dalloc(&c->d_covovf, nw);
+    rc |= dalloc(&c->d_covrip, N * cov_entries);
+    rc |= dalloc(&c->d_covgen, N * cov_entries);
+    rc |= dalloc(&c->d_lanegen, N);
+    rc |= dalloc(&c->d_covcnt, N);
+    rc |= dalloc(&c->d_covovf, N);
   }
   if (rc) return WTFGPU_ERR_OOM;
   std::vector<u32> idle(N, WTFGPU_EXIT_IDLE);
@@ -1573,10 +1573,11 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
   HIPCHK(hipMemsetAsync(c->d_nbytes, 0, N * 8, c->stream));
   HIPCHK(hipMemsetAsync(c->d_exinfo, 0, N * sizeof(ExitInfo), c->stream));
   if (cov_entries) {
-    HIPCHK(hipMemsetAsync(c->d_covep, 0, nw * cov_entries * 4, c->stream));
-    std::vector<u32> one(nw, 1);
-    HIPCHK(hipMemcpyAsync(c->d_covwep, one.data(), nw * 4, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemsetAsync(c->d_covovf, 0, nw * 4, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_covgen, 0, N * cov_entries * 4, c->stream));
+    std::vector<u32> one(N, 1);  // generation 1: every entry (0) is empty
+    HIPCHK(hipMemcpyAsync(c->d_lanegen, one.data(), N * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_covcnt, 0, N * 4, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_covovf, 0, N * 4, c->stream));
   }
   HIPCHK(hipStreamSynchronize(c->stream));
   Dev &P = c->P;
@@ -1597,10 +1598,11 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
   P.ov_count = c->d_ovcount;
   P.ov_gpfn = c->d_ovgpfn;
   P.ov_data = c->d_ovdata;
+  P.full = c->d_full;
   P.cov_rip = c->d_covrip;
-  P.cov_mask = c->d_covmask;
-  P.cov_ep = c->d_covep;
-  P.cov_wave_ep = c->d_covwep;
+  P.cov_gen = c->d_covgen;
+  P.lane_gen = c->d_lanegen;
+  P.cov_cnt = c->d_covcnt;
   P.cov_overflow = c->d_covovf;
   P.H = cov_entries;
   P.stat = c->d_stat;
@@ -1650,6 +1652,7 @@ int wtfgpu_set_initial_state(wtfgpu_ctx *c, const wtfgpu_regs_t *regs) {
   HIPCHK(hipSetDevice(c->device));
   c->initial = *regs;
   c->have_initial = true;
+  c->P.cr3_0 = regs->cr3;
   const InitState s = make_init(*regs);
   HIPCHK(hipMemcpyAsync(c->d_init, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->d_init_full, regs, sizeof(*regs), hipMemcpyHostToDevice, c->stream));
@@ -1940,6 +1943,9 @@ int wtfgpu_read_regs(wtfgpu_ctx *c, uint32_t first, uint32_t count, wtfgpu_regs_
     r.cr4 = sys[l].cr4;
     r.efer = sys[l].efer;
     r.kernel_gs_base = sys[l].kgs;
+    r.star = sys[l].star;
+    r.lstar = sys[l].lstar;
+    r.sfmask = sys[l].sfmask;
     r.cr2 = sys[l].cr2;
     r.seg[WTFGPU_CS].selector = sys[l].cs;
     r.seg[WTFGPU_SS].selector = sys[l].ss;
@@ -2038,21 +2044,59 @@ int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps
   if (!c->P.pool) return WTFGPU_ERR_STATE;
   HIPCHK(hipSetDevice(c->device));
   wtfgpu_run_stats_t st{};
-  const u64 chunk = 1ull << 20;  // wave-steps per launch: keeps every launch short
+  u64 chunk = 1ull << 20;  // wave-steps per launch: keeps every launch short
+  // Cross-wave regrouping: launches of `regroup` wave-steps, between them the
+  // lanes are sorted by rip so that lanes that diverged from their wave
+  // neighbours meet lanes at the same rip in another wave (WTFGPU_REGROUP_STEPS
+  // sets it, 0 = fixed lane order).
+  u64 regroup = c->regroup_steps;
+  if (count < 2 * c->P.lpw) regroup = 0;
+  if (regroup) {
+    chunk = regroup;
+    if (!c->d_perm) {
+      const u64 N = c->P.nlanes;
+      if (dalloc(&c->d_rkeys, N) || dalloc(&c->d_rkeys2, N) || dalloc(&c->d_rlanes, N) || dalloc(&c->d_perm, N))
+        return WTFGPU_ERR_OOM;
+      size_t bytes = 0;
+      HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, c->d_rkeys, c->d_rkeys2, c->d_rlanes, c->d_perm,
+                                                (int)N, 0, 24, c->stream));
+      HIPCHK(hipMalloc(&c->d_rtemp, bytes));
+      c->rtemp_bytes = bytes;
+    }
+  }
+  Dev Q = c->P;
+  Q.perm = regroup ? c->d_perm : nullptr;
+#if WTFGPU_P_BYREF
+  HIPCHK(hipMemcpyAsync(c->d_dev, &Q, sizeof(Dev), hipMemcpyHostToDevice, c->stream));
+#endif
+  // launches per host synchronisation: regrouped chunks are short, so a
+  // group of them is queued at once (one stats read-back per group)
+  const u32 group = regroup ? (u32)std::max<u64>(1, 1024 / regroup) : 1;
+  const u32 hwaves = (count + c->P.lpw - 1) / c->P.lpw;
   u64 done = 0;
   float ms_total = 0;
   for (;;) {
-    const u64 steps = std::min<u64>(chunk, max_steps - done);
     HIPCHK(hipMemsetAsync(c->d_stat, 0, 16 * 8, c->stream));
     HIPCHK(hipEventRecord(c->ev0, c->stream));
-    const u32 hwaves = (count + c->P.lpw - 1) / c->P.lpw;
-    HIPCHK(hipMemcpyAsync(c->d_dev, &c->P, sizeof(Dev), hipMemcpyHostToDevice, c->stream));
+    u32 k = 0;
+    for (; k < group && done < max_steps; k++) {
+      const u64 steps = std::min<u64>(chunk, max_steps - done);
+      if (regroup) {
+        k_regroup_keys<<<(count + 255) / 256, 256, 0, c->stream>>>(c->P, first, count, c->d_rkeys, c->d_rlanes);
+        HIPCHK(hipGetLastError());
+        size_t bytes = c->rtemp_bytes;
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(c->d_rtemp, bytes, c->d_rkeys, c->d_rkeys2, c->d_rlanes,
+                                                  c->d_perm + first, (int)count, 0, 24, c->stream));
+        HIPCHK(hipMemsetAsync(c->d_stat + 2, 0, 8, c->stream));  // running lanes: the last launch's count
+      }
 #if WTFGPU_P_BYREF
-    k_run<<<(hwaves + 3) / 4, 256, 0, c->stream>>>(c->d_dev, first, count, steps);
+      k_run<<<(hwaves + 3) / 4, 256, 0, c->stream>>>(c->d_dev, first, count, steps);
 #else
-    k_run<<<(hwaves + 3) / 4, 256, 0, c->stream>>>(c->P, first, count, steps);
+      k_run<<<(hwaves + 3) / 4, 256, 0, c->stream>>>(Q, first, count, steps);
 #endif
-    HIPCHK(hipGetLastError());
+      HIPCHK(hipGetLastError());
+      done += steps;
+    }
     HIPCHK(hipEventRecord(c->ev1, c->stream));
     u64 s[16];
     HIPCHK(hipMemcpyAsync(s, c->d_stat, sizeof(s), hipMemcpyDeviceToHost, c->stream));
@@ -2060,7 +2104,7 @@ int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     ms_total += ms;
-    st.kernel_launches++;
+    st.kernel_launches += k;
     st.group_steps += s[0];
     st.lane_retired += s[1];
 #ifdef WTFGPU_STAMPS
@@ -2070,7 +2114,6 @@ int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps
             (unsigned long long)s[0], (double)s[4] / s[0], (double)s[6] / s[0], (double)s[7] / s[0],
             (double)s[5] / s[0], (double)s[9] / s[0]);
 #endif
-    done += steps;
     if (s[2] == 0 || done >= max_steps) break;
   }
   st.kernel_ms = ms_total;
@@ -2338,40 +2381,45 @@ int wtfgpu_read_dirty(wtfgpu_ctx *c, uint32_t lane, uint64_t *gpas, uint32_t cap
   return WTFGPU_OK;
 }
 
+// The coverage sets of a lane list (lanes == nullptr: first .. first+n),
+// compacted into (lane, rip) pairs; `clear` empties the sets read.
+static int collect_sets(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t first, uint32_t n, uint32_t *out_lanes,
+                        uint64_t *out_rips, uint64_t cap, uint64_t *total, uint32_t *overflow, int clear) {
+  HIPCHK(hipSetDevice(c->device));
+  const u64 room = std::max<u64>(cap, 1);
+  const u64 o_n = ((u64)(lanes ? n : 0) * 4 + 255) & ~255ull, o_l = o_n + 256, o_r = (o_l + room * 4 + 255) & ~255ull;
+  if (ensure_scratch(c, o_r + room * 8)) return WTFGPU_ERR_OOM;
+  if (lanes) HIPCHK(hipMemcpyAsync(c->d_scratch, lanes, (u64)n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_scratch + o_n, 0, 16, c->stream));
+  k_cov_collect<<<n, 256, 0, c->stream>>>(c->P, lanes ? (const u32 *)c->d_scratch : nullptr, first, n,
+                                          (u32 *)(c->d_scratch + o_l), (u64 *)(c->d_scratch + o_r), cap,
+                                          (unsigned long long *)(c->d_scratch + o_n), (u32 *)(c->d_scratch + o_n + 8));
+  HIPCHK(hipGetLastError());
+  u64 hdr[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(hdr, c->d_scratch + o_n, 16, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (clear && lanes && hdr[0] <= cap) {  // everything was read: the sets empty (ordered before later work)
+    k_cov_clear<<<(n + 255) / 256, 256, 0, c->stream>>>(c->P, (const u32 *)c->d_scratch, n);
+    HIPCHK(hipGetLastError());
+  }
+  const u64 m = std::min(hdr[0], cap);
+  if (m) {
+    HIPCHK(hipMemcpyAsync(out_lanes, c->d_scratch + o_l, m * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(out_rips, c->d_scratch + o_r, m * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
+  if (overflow) *overflow = (u32)hdr[1] & 1;
+  *total = hdr[0];
+  return WTFGPU_OK;
+}
+
 int wtfgpu_read_coverage(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint32_t *lanes, uint64_t *rips,
                          uint64_t cap, uint64_t *n, uint32_t *overflow) {
-  if (!lanes_ok(c, first, count) || !n) return WTFGPU_ERR_INVALID;
+  if (!lanes_ok(c, first, count) || !n || (cap && (!lanes || !rips))) return WTFGPU_ERR_INVALID;
   *n = 0;
   if (overflow) *overflow = 0;
   if (!c->d_covrip || count == 0) return WTFGPU_OK;
-  HIPCHK(hipSetDevice(c->device));
-  const u32 w0 = first / c->P.lpw, w1 = (first + count + c->P.lpw - 1) / c->P.lpw;
-  const u64 total = (u64)(w1 - w0) * c->P.H;
-  const u64 room = std::max<u64>(cap, 1);
-  const u64 o_rip = (room * 4 + 255) & ~255ull, o_n = (o_rip + room * 8 + 255) & ~255ull;
-  if (ensure_scratch(c, o_n + 64)) return WTFGPU_ERR_OOM;
-  HIPCHK(hipMemsetAsync(c->d_scratch + o_n, 0, 8, c->stream));
-  k_cov_collect<<<(u32)((total + 255) / 256), 256, 0, c->stream>>>(
-      c->P, first, count, (u32 *)c->d_scratch, (u64 *)(c->d_scratch + o_rip), cap,
-      (unsigned long long *)(c->d_scratch + o_n));
-  HIPCHK(hipGetLastError());
-  u64 got = 0;
-  HIPCHK(hipMemcpyAsync(&got, c->d_scratch + o_n, 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  const u64 m = std::min(got, cap);
-  if (m) {
-    HIPCHK(hipMemcpyAsync(lanes, c->d_scratch, m * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(rips, c->d_scratch + o_rip, m * 8, hipMemcpyDeviceToHost, c->stream));
-  }
-  if (overflow) {
-    std::vector<u32> ov(w1 - w0);
-    HIPCHK(hipMemcpyAsync(ov.data(), c->d_covovf + w0, (u64)(w1 - w0) * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    for (u32 v : ov) *overflow |= v;
-  }
-  HIPCHK(hipStreamSynchronize(c->stream));
-  *n = got;
-  return WTFGPU_OK;
+  return collect_sets(c, nullptr, first, count, lanes, rips, cap, n, overflow, 0);
 }
 
 int wtfgpu_collect_coverage_lanes(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, uint32_t *out_lanes,
@@ -2380,54 +2428,9 @@ int wtfgpu_collect_coverage_lanes(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t
   *total = 0;
   if (overflow) *overflow = 0;
   if (!c->d_covrip || n == 0) return WTFGPU_OK;
-  HIPCHK(hipSetDevice(c->device));
-  // per-wave request masks
-  std::vector<u32> waves;
-  std::vector<u64> masks;
-  {
-    std::vector<u32> sorted(lanes, lanes + n);
-    std::sort(sorted.begin(), sorted.end());
-    for (u32 l : sorted) {
-      if (l >= c->P.nlanes) return WTFGPU_ERR_INVALID;
-      const u32 w = l / c->P.lpw;
-      if (waves.empty() || waves.back() != w) {
-        waves.push_back(w);
-        masks.push_back(0);
-      }
-      masks.back() |= 1ull << (l % c->P.lpw);
-    }
-  }
-  const u32 nw = (u32)waves.size();
-  const u64 room = std::max<u64>(cap, 1);
-  const u64 o_m = ((u64)nw * 4 + 255) & ~255ull, o_n = (o_m + (u64)nw * 8 + 255) & ~255ull, o_l = o_n + 256,
-            o_r = (o_l + room * 4 + 255) & ~255ull;
-  if (ensure_scratch(c, o_r + room * 8)) return WTFGPU_ERR_OOM;
-  HIPCHK(hipMemcpyAsync(c->d_scratch, waves.data(), (u64)nw * 4, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipMemcpyAsync(c->d_scratch + o_m, masks.data(), (u64)nw * 8, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipMemsetAsync(c->d_scratch + o_n, 0, 8, c->stream));
-  const u64 threads = (u64)nw * c->P.H;
-  k_cov_collect_lanes<<<(u32)((threads + 255) / 256), 256, 0, c->stream>>>(
-      c->P, (const u32 *)c->d_scratch, (const u64 *)(c->d_scratch + o_m), nw, (u32 *)(c->d_scratch + o_l),
-      (u64 *)(c->d_scratch + o_r), cap, (unsigned long long *)(c->d_scratch + o_n), cap ? 1 : 0);
-  HIPCHK(hipGetLastError());
-  u64 got = 0;
-  HIPCHK(hipMemcpyAsync(&got, c->d_scratch + o_n, 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  const u64 m = std::min(got, cap);
-  if (m) {
-    HIPCHK(hipMemcpyAsync(out_lanes, c->d_scratch + o_l, m * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(out_rips, c->d_scratch + o_r, m * 8, hipMemcpyDeviceToHost, c->stream));
-  }
-  if (overflow) {
-    const u32 nall = (c->P.nlanes + c->P.lpw - 1) / c->P.lpw;
-    std::vector<u32> ov(nall);
-    HIPCHK(hipMemcpyAsync(ov.data(), c->d_covovf, (u64)nall * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    for (u32 w : waves) *overflow |= ov[w];
-  }
-  HIPCHK(hipStreamSynchronize(c->stream));
-  *total = got;
-  return WTFGPU_OK;
+  for (u32 i = 0; i < n; i++)
+    if (lanes[i] >= c->P.nlanes) return WTFGPU_ERR_INVALID;
+  return collect_sets(c, lanes, 0, n, out_lanes, out_rips, cap, total, overflow, 1);
 }
 
 int wtfgpu_commit_coverage(wtfgpu_ctx *c, const uint64_t *rips, uint64_t n) {

@@ -93,12 +93,19 @@ struct Dev {
   u32 code_mask;
   u8 *cov_map;           // [slots][4096]
   u8 *cov_shadow;        // [slots][4096]: the map as of the last absorb
-  u64 *cov_rip;          // per wave [nwaves][H]
-  u64 *cov_mask;
-  u32 *cov_ep;           // entry epoch
-  u32 *cov_wave_ep;      // current epoch per wave
-  u32 *cov_overflow;     // per wave
-  u32 H;                 // entries per wave (power of two)
+  // new-coverage logs: per lane, an open-addressing set of H rips the lane
+  // ran while they were absent from cov_map (bochscpu_backend.cc:501-504)
+  u64 *cov_rip;          // [nlanes][H]
+  u32 *cov_gen;          // [nlanes][H]: an entry is live when it equals the lane's generation
+  u32 *lane_gen;         // [nlanes]: bumped by restore / collection (empties the set in O(1))
+  u32 *cov_cnt;          // [nlanes]: live entries
+  u32 *cov_overflow;     // [nlanes]: the set filled up (entries were lost)
+  u32 H;                 // entries per lane (power of two)
+  // lane order of a k_run launch (cross-wave regrouping): hardware wave w runs
+  // lanes perm[first + w * lpw ...]; nullptr = identity
+  const u32 *perm;
+  wtfgpu_regs_t *full;   // [nlanes] cold architectural state (MSRs the hot LaneSys lacks)
+  u64 cr3_0;             // the testcases' initial cr3 (Cr3Change_t, bochscpu_backend.cc:628-657)
   u64 limit;
   u64 *stat;             // [0] group steps, [1] retired, [2] lanes still running
 };

@@ -19,6 +19,7 @@ struct Lane {
   u32 tnext, ovn, cpl, status, lane, exvec, exerr, exop;
   u32 miss, miss_acc, flush, pend;  // pend: bytes accessed by the attempt in flight
   u32 nodeliver;                    // this fault could not be delivered through the guest IDT
+  u32 cgen, ccnt;                   // coverage set: generation, live entries
 };
 
 // GPR r of the lane. r is wave-uniform and the halves live in two u32 arrays

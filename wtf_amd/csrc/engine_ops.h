@@ -18,7 +18,7 @@
 
 namespace wtfgpu_dev {
 
-enum { X_OK = 0, X_FAULT = 1, X_UNIMPL = 2, X_INT3 = 3, X_HLT = 4, X_KEEP = 6 };
+enum { X_OK = 0, X_FAULT = 1, X_UNIMPL = 2, X_INT3 = 3, X_HLT = 4, X_CR3 = 5, X_KEEP = 6 };
 
 // operations
 enum : u32 {
@@ -135,7 +135,7 @@ __constant__ u32 kMap1[256] = {
     E(O_RET, 0, L_POP, Z_Q, Z_Q, 0, 0, 0, 0, K_W, 0), E(O_RET, 0, L_POP, Z_Q, Z_Q, 0, 0, 0, 0, K_NONE, 0), UN, UN,
     E(O_MOV, L_RM, L_IMM, Z_B, Z_B, 0, 1, 0, 1, K_B, G_C6), E(O_MOV, L_RM, L_IMM, Z_V, Z_V, 0, 1, 0, 1, K_Z, G_C6),
     /*c8*/ UN, E(O_LEAVE, 0, L_RBPMEM, Z_Q, Z_Q, 0, 0, 0, 0, K_NONE, 0), UN, UN,
-    E(O_INT3, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, UN, UN,
+    E(O_INT3, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, UN, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0),
     /*d0*/ E(O_SHIFT, L_RM, L_ONE, Z_B, Z_B, 1, 1, 0, 1, K_NONE, G_2), E(O_SHIFT, L_RM, L_ONE, Z_V, Z_B, 1, 1, 0, 1, K_NONE, G_2),
     E(O_SHIFT, L_RM, L_CL, Z_B, Z_B, 1, 1, 0, 1, K_NONE, G_2), E(O_SHIFT, L_RM, L_CL, Z_V, Z_B, 1, 1, 0, 1, K_NONE, G_2),
     UN, UN, UN, E(O_MOV, L_RAX, L_XLAT, Z_B, Z_B, 0, 1, 0, 0, K_NONE, 0),
@@ -161,8 +161,10 @@ __constant__ u32 kMap2[256] = {
     /*00*/ UN, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 1, K_NONE, 0), UN, UN, UN, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN,
     E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, UN, UN, E(O_UD, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, NOPM, UN, UN,
     /*10*/ UN, UN, UN, UN, UN, UN, UN, UN, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM,
-    /*20*/ E(O_SYS, L_RM, 0, Z_Q, Z_Q, 0, 1, 0, 1, K_NONE, 0), UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN,
-    /*30*/ UN16,
+    /*20*/ E(O_SYS, L_RM, 0, Z_Q, Z_Q, 0, 1, 0, 1, K_NONE, 0), UN, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 1, K_NONE, 0), UN, UN,
+    UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN,
+    /*30*/ E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0),
+    E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN,
     /*40*/ CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV,
     /*50*/ UN16,
     /*60*/ UN16,
@@ -412,15 +414,21 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
     if (u.op == O_BSR && u.rep == 0xf3) u.op = O_LZCNT;
     if (u.op == O_SYS) {
       // 0 syscall, 1 sysret (64-bit form only), 2 swapgs (0f 01 f8), 3 rdrand r (0f c7 /6),
-      // 4 mov r64, crN (0f 20 /r)
-      u.sub = c == 0x05 ? 0 : c == 0x07 ? 1 : c == 0x01 ? 2 : c == 0x20 ? 4 : 3;
-      if (c == 0x20 && u.is_mem) u.op = O_UNIMPL;
+      // 4 mov r64, crN (0f 20 /r), 6 mov crN, r64 (0f 22 /r), 7 wrmsr, 8 rdtsc, 9 rdmsr,
+      // 10 rdtscp (0f 01 f9)
+      u.sub = c == 0x05 ? 0 : c == 0x07 ? 1 : c == 0x01 ? 2 : c == 0x20 ? 4 : c == 0x22 ? 6 : c == 0x30 ? 7
+              : c == 0x31 ? 8 : c == 0x32 ? 9 : 3;
+      if ((c == 0x20 || c == 0x22) && u.is_mem) u.op = O_UNIMPL;
       if (c == 0x07 && !rexw) u.op = O_UNIMPL;
-      if (c == 0x01 && (u.is_mem || (u.reg & 7) != 7 || (u.rm & 7) != 0)) u.op = O_UNIMPL;
+      if (c == 0x01 && (u.is_mem || (u.reg & 7) != 7 || (u.rm & 7) > 1)) u.op = O_UNIMPL;
+      if (c == 0x01 && (u.rm & 7) == 1) u.sub = 10;
       if (c == 0xc7 && (u.is_mem || (u.reg & 7) != 6 || p66 || u.rep)) u.op = O_UNIMPL;
     }
   } else if (u.op == O_FLAGOP) {
     u.sub = c;
+  } else if (u.op == O_SYS) {  // iretq (48 cf): 64-bit operand size only
+    u.sub = 5;
+    if (!rexw) u.op = O_UNIMPL;
   }
   u32 n = 0;
   switch (ik) {
@@ -1025,6 +1033,134 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
         else {
           set_fault(L, WTFGPU_VEC_UD, 0, 0);
           return X_FAULT;
+        }
+        break;
+      }
+      if (u.sub == 5) {  // iretq (U19): every frame read before any change
+        u64 f0, f1, f2, f3, f4;
+        if (!vread(L, rsp, 8, f0) || !vread(L, rsp + 8, 8, f1) || !vread(L, rsp + 16, 8, f2) ||
+            !vread(L, rsp + 24, 8, f3) || !vread(L, rsp + 32, 8, f4))
+          return X_FAULT;
+        const u32 ncpl = (u32)f1 & 3;
+        if ((f1 & 0xfffc) == 0 || ncpl < L.cpl) {
+          set_fault(L, WTFGPU_VEC_GP, (u32)f1 & 0xfffc, 0);
+          return X_FAULT;
+        }
+        if (!canonical(f0)) {
+          set_fault(L, WTFGPU_VEC_GP, 0, 0);
+          return X_FAULT;
+        }
+        // SDM IRET: status, TF, DF, NT, RF, AC, ID always; IF if CPL <= IOPL;
+        // IOPL, VIF, VIP at CPL 0 only
+        u64 mask = 0x254dd5ull;
+        if (L.cpl == 0) mask |= 0x200ull | 0x3000ull | 0x80000ull | 0x100000ull;
+        else if (L.cpl <= ((fl >> 12) & 3)) mask |= 0x200ull;
+        fl = (fl & ~mask) | (f2 & mask) | 2;
+        next = f0;
+        RS(L, 4, f3);
+        S.cs = (u16)f1;
+        S.ss = (u16)f4;
+        if (ncpl != L.cpl) L.flush = 1;  // translations were permission-checked at the old cpl
+        L.cpl = S.cpl = ncpl;
+        break;
+      }
+      if (u.sub >= 6) {  // mov crN, r64 / wrmsr / rdtsc / rdmsr / rdtscp (U20, U21)
+        if (u.sub == 8 || u.sub == 10) {
+          if ((S.cr4 & 4) && L.cpl != 0) {
+            set_fault(L, WTFGPU_VEC_GP, 0, 0);
+            return X_FAULT;
+          }
+          const u64 t = P.full[L.lane].tsc + L.icount;
+          RS(L, 0, t & 0xffffffffull);
+          RS(L, 2, t >> 32);
+          if (u.sub == 10) RS(L, 1, P.full[L.lane].tsc_aux & 0xffffffffull);
+          break;
+        }
+        if (L.cpl != 0) {
+          set_fault(L, WTFGPU_VEC_GP, 0, 0);
+          return X_FAULT;
+        }
+        if (u.sub == 6) {
+          const u32 n = u.reg & 15;
+          const u64 v = R(L, u.rm & 15);
+          if (n == 0) {
+            L.cr0 = S.cr0 = v;
+            L.flush = 1;
+          } else if (n == 2) {
+            S.cr2 = v;
+          } else if (n == 3) {
+            S.cr3 = v;
+            L.cr3 = v;
+            L.flush = 1;
+            if (v != P.cr3_0) {
+              L.rflags = fl;
+              return X_CR3;  // retires, then the lane stops with Cr3Change_t
+            }
+          } else if (n == 4) {
+            S.cr4 = v;
+            L.flush = 1;
+          } else if (n == 8) {
+            P.full[L.lane].cr8 = v & 15;
+          } else {
+            set_fault(L, WTFGPU_VEC_UD, 0, 0);
+            return X_FAULT;
+          }
+          break;
+        }
+        // rdmsr / wrmsr: the MSRs CpuState_t carries
+        wtfgpu_regs_t &F = P.full[L.lane];
+        const u32 idx = (u32)R(L, 1);
+        u64 cur = 0;
+        int canon = 0, lo32 = 0;
+        switch (idx) {
+          case 0x10: cur = F.tsc + L.icount; break;
+          case 0x1b: cur = F.apic_base; break;
+          case 0x174: cur = F.sysenter_cs; break;
+          case 0x175: cur = F.sysenter_esp; canon = 1; break;
+          case 0x176: cur = F.sysenter_eip; canon = 1; break;
+          case 0x277: cur = F.pat; break;
+          case 0xc0000080u: cur = L.efer; break;
+          case 0xc0000081u: cur = S.star; break;
+          case 0xc0000082u: cur = S.lstar; canon = 1; break;
+          case 0xc0000083u: cur = F.cstar; canon = 1; break;
+          case 0xc0000084u: cur = S.sfmask; lo32 = 1; break;
+          case 0xc0000100u: cur = P.fs_base[L.lane]; canon = 1; break;
+          case 0xc0000101u: cur = P.gs_base[L.lane]; canon = 1; break;
+          case 0xc0000102u: cur = S.kgs; canon = 1; break;
+          case 0xc0000103u: cur = F.tsc_aux; lo32 = 1; break;
+          default:
+            set_fault(L, WTFGPU_VEC_GP, 0, 0);
+            return X_FAULT;
+        }
+        if (u.sub == 9) {
+          RS(L, 0, cur & 0xffffffffull);
+          RS(L, 2, cur >> 32);
+          break;
+        }
+        const u64 v = (R(L, 0) & 0xffffffffull) | (R(L, 2) << 32);
+        if ((canon && !canonical(v)) || (lo32 && (v >> 32))) {
+          set_fault(L, WTFGPU_VEC_GP, 0, 0);
+          return X_FAULT;
+        }
+        switch (idx) {
+          case 0x10: F.tsc = v - L.icount; break;
+          case 0x1b: F.apic_base = v; break;
+          case 0x174: F.sysenter_cs = v; break;
+          case 0x175: F.sysenter_esp = v; break;
+          case 0x176: F.sysenter_eip = v; break;
+          case 0x277: F.pat = v; break;
+          case 0xc0000080u:
+            L.efer = S.efer = (v & ~0x400ull) | (L.efer & 0x400ull);  // LMA is read-only
+            L.flush = 1;
+            break;
+          case 0xc0000081u: S.star = v; break;
+          case 0xc0000082u: S.lstar = v; break;
+          case 0xc0000083u: F.cstar = v; break;
+          case 0xc0000084u: S.sfmask = v; break;
+          case 0xc0000100u: P.fs_base[L.lane] = v; break;
+          case 0xc0000101u: P.gs_base[L.lane] = v; break;
+          case 0xc0000102u: S.kgs = v; break;
+          default: F.tsc_aux = v; break;
         }
         break;
       }

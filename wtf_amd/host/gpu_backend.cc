@@ -1036,25 +1036,31 @@ void GpuBackend_t::collect_coverage(const std::vector<uint32_t> &lanes, std::vec
   const auto t0 = Clock::now();
   uint64_t total = 0;
   uint32_t ovf = 0;
-  wtfgpu_collect_coverage_lanes(ctx_, lanes.data(), (uint32_t)lanes.size(), nullptr, nullptr, 0, &total, &ovf);
-  std::vector<uint32_t> cl(total);
-  std::vector<uint64_t> cr(total);
-  if (total)
-    wtfgpu_collect_coverage_lanes(ctx_, lanes.data(), (uint32_t)lanes.size(), cl.data(), cr.data(), total, &total,
-                                  &ovf);
-  else  // nothing logged: still drop the lanes from the logs
-    wtfgpu_collect_coverage_lanes(ctx_, lanes.data(), (uint32_t)lanes.size(), cl.data(), cr.data(), 1, &total, &ovf);
+  // one call into buffers that persist (the sets empty when it all fits);
+  // a larger result is read again at its size
+  if (cov_lanes_.size() < (1u << 16)) {
+    cov_lanes_.resize(1u << 16);
+    cov_rips_.resize(1u << 16);
+  }
+  wtfgpu_collect_coverage_lanes(ctx_, lanes.data(), (uint32_t)lanes.size(), cov_lanes_.data(), cov_rips_.data(),
+                                cov_lanes_.size(), &total, &ovf);
+  if (total > cov_lanes_.size()) {
+    cov_lanes_.resize(total);
+    cov_rips_.resize(total);
+    wtfgpu_collect_coverage_lanes(ctx_, lanes.data(), (uint32_t)lanes.size(), cov_lanes_.data(), cov_rips_.data(),
+                                  cov_lanes_.size(), &total, &ovf);
+  }
+  const std::vector<uint32_t> &cl = cov_lanes_;
+  const std::vector<uint64_t> &cr = cov_rips_;
   const auto t1 = Clock::now();
   stats_.covlog_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
   stats_.cov_entries += total;
-  if (getenv("WTFGPU_DEBUG_COV") && total) {
-    size_t known = 0;
-    for (uint64_t i = 0; i < total && i < cr.size(); i++) known += aggregate_.count(cr[i]);
-    fprintf(stderr, "collect: %zu lanes, %llu entries (%zu already in the aggregate of %zu); first rip %#llx\n",
-            lanes.size(), (unsigned long long)total, known, aggregate_.size(), (unsigned long long)(cr.empty() ? 0 : cr[0]));
+  if (ovf && !cov_ovf_warned_) {
+    cov_ovf_warned_ = true;
+    fprintf(stderr, "wtfgpu: a lane's new-coverage set filled up (rips lost); raise the set size\n");
   }
   std::unordered_map<uint32_t, std::vector<uint64_t>> per;
-  for (uint64_t i = 0; i < total && i < cl.size(); i++) per[cl[i]].push_back(cr[i]);
+  for (uint64_t i = 0; i < total; i++) per[cl[i]].push_back(cr[i]);
   std::vector<uint64_t> fresh;
   last_new_coverage_.clear();
   for (uint32_t l : lanes) {

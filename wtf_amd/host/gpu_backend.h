@@ -178,6 +178,9 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   std::vector<uint8_t> busy_;
   std::vector<uint64_t> tag_;
   std::vector<LaneResult> lres_;
+  std::vector<uint32_t> cov_lanes_;  // coverage collection buffers (streaming)
+  std::vector<uint64_t> cov_rips_;
+  bool cov_ovf_warned_ = false;
   uint8_t *feed_pin_ = nullptr;  // pinned staging of streamed feeds
   uint64_t feed_pin_cap_ = 0;
   void finish_coverage(uint32_t n, std::vector<LaneResult> *out, std::vector<uint32_t> *timedout);

@@ -489,30 +489,30 @@ bool FuzzSession::StreamStep() {
 // The master's bookkeeping of one result (server.h:816-886).
 void FuzzSession::Account(const std::string &Tc, const LaneResult &L) {
   S_.execs++;
-    S_.retired += L.icount;
-    if (L.error) {  // the engine could not finish it: neither a crash nor coverage
-      S_.errors++;
-      S_.error_retired += L.icount;
-      return;
-    }
-    if (std::holds_alternative<Timedout_t>(L.result)) S_.timeouts++;
-    if (std::holds_alternative<Cr3Change_t>(L.result)) S_.cr3++;
-    if (const Crash_t *C = std::get_if<Crash_t>(&L.result)) {
-      S_.crashes++;
-      if (!C->CrashName.empty() && CrashNames_.insert(C->CrashName).second)
-        SaveFile(T_ / "crashes" / C->CrashName, (const uint8_t *)Tc.data(), Tc.size());
-    }
-    // a timed-out testcase reports no coverage (the client revokes it,
-    // client.cc:122-133); any other result with new coverage, crashes
-    // included, joins the corpus after arming the mutator's cross-over
-    // (server.h:816-853)
-    if (!L.new_coverage.empty() && !std::holds_alternative<Timedout_t>(L.result)) {
-      Testcase_t Tcase((const uint8_t *)Tc.data(), Tc.size());
-      Mutator_->OnNewCoverage(Tcase);
-      LastNewCov_ = Tc;
-      HaveNewCov_ = true;
-      Corpus_.SaveTestcase(L.result, std::move(Tcase));
-    }
+  S_.retired += L.icount;
+  if (L.error) {  // the engine could not finish it: neither a crash nor coverage
+    S_.errors++;
+    S_.error_retired += L.icount;
+    return;
+  }
+  if (std::holds_alternative<Timedout_t>(L.result)) S_.timeouts++;
+  if (std::holds_alternative<Cr3Change_t>(L.result)) S_.cr3++;
+  if (const Crash_t *C = std::get_if<Crash_t>(&L.result)) {
+    S_.crashes++;
+    if (!C->CrashName.empty() && CrashNames_.insert(C->CrashName).second)
+      SaveFile(T_ / "crashes" / C->CrashName, (const uint8_t *)Tc.data(), Tc.size());
+  }
+  // a timed-out testcase reports no coverage (the client revokes it,
+  // client.cc:122-133); any other result with new coverage, crashes
+  // included, joins the corpus after arming the mutator's cross-over
+  // (server.h:816-853)
+  if (!L.new_coverage.empty() && !std::holds_alternative<Timedout_t>(L.result)) {
+    Testcase_t Tcase((const uint8_t *)Tc.data(), Tc.size());
+    Mutator_->OnNewCoverage(Tcase);
+    LastNewCov_ = Tc;
+    HaveNewCov_ = true;
+    Corpus_.SaveTestcase(L.result, std::move(Tcase));
+  }
 }
 
 // every shard's coverage map, MAX-reduced over the shards; the

@@ -17,7 +17,11 @@
  *   0x22201F wait on an object -> nt!SwapContext (context switch)
  * Every handler logs through nt!DbgPrintEx, and the pool cookie comes from
  * nt!ExGenRandom, whose `rdrand rdx` sits at +0xe0 like the Windows build the
- * module checks (fuzzer_hevd.cc:96-101).
+ * module checks (fuzzer_hevd.cc:96-101), mixed with the time-stamp counter.
+ * As in HEVD, the handlers touch user memory inside __try / __except: a page
+ * fault on a user address there is dispatched to the handler (the trap
+ * returns through IRETQ into the guarded function's except path with
+ * STATUS_ACCESS_VIOLATION); a fault on a kernel address bugchecks.
  *
  * Compiled with gcc (-mabi=ms: Win64 argument registers) into a flat image at
  * KERNEL_BASE, mapped supervisor-only by wtf_amd/tools/hevd.py.
@@ -73,6 +77,29 @@ __attribute__((noipa, noreturn)) void KeBugCheckEx(u64 Code, u64 P1, u64 P2, u64
   for (;;) __asm__ volatile("hlt");
 }
 
+/* ---- __try / __except: a guarded region registers its resume context; the
+ * page-fault path (KiTrapHandler) sends a user-address fault inside it to
+ * KiTryResume through IRETQ, which unwinds to the region's except path. */
+#define STATUS_ACCESS_VIOLATION 0xC0000005u
+typedef struct {
+  void *Jmp[5];
+} KTRY;
+static KTRY *volatile CurrentTry;
+__attribute__((noipa, used)) void KiTryResume(void) { __builtin_longjmp(CurrentTry->Jmp, 1); }
+/* the barriers keep the guarded accesses between the two stores */
+static inline __attribute__((always_inline)) int TryEnter(KTRY *T) {
+  CurrentTry = T;
+  __asm__ volatile("" ::: "memory");
+  return 1;
+}
+static inline __attribute__((always_inline)) void TryLeave(void) {
+  __asm__ volatile("" ::: "memory");
+  CurrentTry = 0;
+}
+#define TRY(T) if (__builtin_setjmp((T).Jmp) == 0 && TryEnter(&(T)))
+#define EXCEPT else
+#define END_TRY() TryLeave()
+
 /* ---- /GS cookie */
 u64 __security_cookie = 0x00002B992DDFA232ull;
 __attribute__((noipa)) static void CheckCookie(u64 Saved, u64 Frame) {
@@ -93,7 +120,11 @@ struct {
 } Pool;
 
 static u64 PoolCookie(void) {
-  if (!Pool.Cookie) Pool.Cookie = ExGenRandom() | 1;
+  if (!Pool.Cookie) {
+    u32 lo, hi;
+    __asm__ volatile("rdtsc" : "=a"(lo), "=d"(hi));
+    Pool.Cookie = (ExGenRandom() ^ ((u64)hi << 32 | lo)) | 1;
+  }
   return Pool.Cookie;
 }
 __attribute__((noipa)) void *ExAllocatePoolWithTag(u32 Type, u64 Size, u32 Tag) {
@@ -127,9 +158,17 @@ __attribute__((noipa)) void ExFreePoolWithTag(void *P, u32 Tag) {
 
 __attribute__((noipa)) static u32 TriggerBufferOverflowStack(const u8 *User, u64 Size) {
   u8 Kernel[512];
+  KTRY T;
   memset(Kernel, 0, sizeof(Kernel));
   DbgPrintEx(77, 3, "[+] UserBuffer: 0x%p Size: 0x%zX\n", User, Size);
-  memcpy(Kernel, User, Size); /* the bug: Size is the user's, not sizeof(Kernel) */
+  TRY(T) {
+    memcpy(Kernel, User, Size); /* the bug: Size is the user's, not sizeof(Kernel) */
+    END_TRY();
+  }
+  EXCEPT {
+    END_TRY();
+    return STATUS_ACCESS_VIOLATION;
+  }
   return Kernel[0] == 0x41 ? STATUS_SUCCESS : STATUS_UNSUCCESSFUL;
 }
 
@@ -154,16 +193,32 @@ struct WhatWhere {
 __attribute__((noipa)) static u32 TriggerArbitraryWrite(const u8 *User, u64 Size) {
   if (Size < sizeof(struct WhatWhere)) return STATUS_UNSUCCESSFUL;
   const struct WhatWhere *W = (const struct WhatWhere *)User;
+  KTRY T;
   DbgPrintEx(77, 3, "[+] What: 0x%p Where: 0x%p\n", W->What, W->Where);
-  *(W->Where) = *(W->What);
+  TRY(T) {
+    *(W->Where) = *(W->What);
+    END_TRY();
+  }
+  EXCEPT {
+    END_TRY();
+    return STATUS_ACCESS_VIOLATION;
+  }
   return STATUS_SUCCESS;
 }
 
 __attribute__((noipa)) static u32 TriggerPoolOverflow(const u8 *User, u64 Size) {
   u8 *Chunk = ExAllocatePoolWithTag(0, 0x1f8, TAG);
   if (!Chunk) return STATUS_UNSUCCESSFUL;
+  KTRY T;
   DbgPrintEx(77, 3, "[+] Pool chunk: 0x%p Size: 0x%zX\n", Chunk, Size);
-  memcpy(Chunk, User, Size);
+  TRY(T) {
+    memcpy(Chunk, User, Size);
+    END_TRY();
+  }
+  EXCEPT {
+    END_TRY();
+    return STATUS_ACCESS_VIOLATION;
+  }
   ExFreePoolWithTag(Chunk, TAG);
   return STATUS_SUCCESS;
 }
@@ -281,11 +336,16 @@ __asm__(".globl KiSystemCall64\n"
 struct TrapFrame {
   u64 Error, Rip, Cs, Rflags, Rsp, Ss;
 };
-__attribute__((noipa, used)) void KiTrapHandler(u64 Vector, struct TrapFrame *F, u64 Cr2) {
+__attribute__((noipa, used)) u32 KiTrapHandler(u64 Vector, struct TrapFrame *F, u64 Cr2) {
   if (F->Cs & 3) ((void (*)(void))SwapContext)();
+  if (Vector == 14 && CurrentTry && Cr2 < 0x800000000000ull) {
+    F->Rip = (u64)KiTryResume; /* dispatched to the guarded region's handler */
+    return 1;
+  }
   if (Vector == 14)
     KeBugCheckEx(0x50, Cr2, (F->Error & 0x10) ? 0x10 : (F->Error & 2) ? 2 : 0, F->Rip, 0);
   KeBugCheckEx(0x1E, Vector == 0 ? 0xC0000094u : Vector == 6 ? 0xC000001Du : 0xC0000005u, F->Rip, 0, 0);
+  return 0;
 }
 /* stubs: faults without an error code push a zero so every frame is a TrapFrame */
 __asm__(".globl KiDivideErrorFault\n.globl KiInvalidOpcodeFault\n.globl KiGeneralProtectionFault\n"
@@ -298,6 +358,14 @@ __asm__(".globl KiDivideErrorFault\n.globl KiInvalidOpcodeFault\n.globl KiGenera
         "  mov %rsp, %rdx\n"
         "  mov %cr2, %r8\n"
         "  and $-16, %rsp\n"
+        "  push %rdx\n"
+        "  push %rdx\n"
         "  sub $0x20, %rsp\n"
         "  call KiTrapHandler\n"
-        "  hlt\n");
+        "  add $0x28, %rsp\n"
+        "  pop %rsp\n"          /* the trap frame */
+        "  test %eax, %eax\n"
+        "  jz 1f\n"
+        "  add $8, %rsp\n"      /* error code */
+        "  iretq\n"
+        "1: hlt\n");
