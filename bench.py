@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--lanes", type=int, default=65536)
+    ap.add_argument("--slice-steps", type=int, default=0, help="wave-steps per streaming slice (0: the node's 4096)")
+    ap.add_argument("--regroup-steps", type=int, default=-1,
+                    help="k_run launch length with lanes regrouped by rip (0: off; -1: engine default)")
     ap.add_argument("--limit", type=int, default=100000)
     ap.add_argument("--hevd-limit", type=int, default=10_000_000, help="BASELINE.md: HEVD runs --limit 10000000")
     ap.add_argument("--leg-seconds", type=float, default=10.0, help="GPU wall window of the hevd leg")
@@ -220,10 +223,21 @@ def node_fields(s0: dict, s1: dict) -> dict:
     }
 
 
-def hevd_leg(base: str, lanes: int, limit: int, seconds: float) -> dict:
+def sched_flags(a) -> list[str]:
+    """The node's scheduling flags from bench's (--slice-steps / --regroup-steps)."""
+    f = []
+    if a.slice_steps:
+        f += ["--slice-steps", str(a.slice_steps)]
+    if a.regroup_steps >= 0:
+        f += ["--regroup-steps", str(a.regroup_steps)]
+    return f
+
+
+def hevd_leg(base: str, lanes: int, limit: int, seconds: float, flags=()) -> dict:
     """`wtfgpu fuzz` (the product node binary) on HEVD for `seconds` of wall time."""
     out = subprocess.run([WTFGPU, "fuzz", "--name", "hevd", "--target", base, "--lanes", str(lanes),
-                          "--seconds", str(seconds), "--seed", "1337", "--limit", str(limit), "--max_len", "1028"],
+                          "--seconds", str(seconds), "--seed", "1337", "--limit", str(limit), "--max_len", "1028",
+                          *flags],
                          check=True, capture_output=True, text=True, timeout=seconds * 6 + 300).stdout
     g = json.loads([x for x in out.splitlines() if x.startswith("{")][-1])
     b = g["backend"]
@@ -330,13 +344,15 @@ def run(a, rank, world, local, tmp):
         rccl_id = shard.share_bytes(wn.rccl_unique_id() if rank == 0 else None, dist)
 
     node = wn.Node("tlv_server", tlv_dir, a.lanes, a.limit, seed=1337, max_len=TARGETS["tlv_server"][2],
-                   device=local, rank=rank, world=world, rccl_id=rccl_id)
+                   device=local, rank=rank, world=world, rccl_id=rccl_id, slice_steps=a.slice_steps,
+                   regroup_steps=None if a.regroup_steps < 0 else a.regroup_steps)
     for _ in range(a.warmup):
         node.step()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     s0 = node.stats()
+    sum0 = node.summary()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         node.step()
@@ -349,6 +365,10 @@ def run(a, rank, world, local, tmp):
     dt, execs, retired = shard.job_totals(dt, float(execs), float(retired), dist)
     fields = node_fields(s0, s1)
     summary = node.summary()
+    # the timed steps' share of every node / backend counter (summary - summary before)
+    timed = {k: round(v - sum0[k], 3) for k, v in summary.items() if isinstance(v, (int, float)) and k in sum0}
+    timed["backend"] = {k: round(v - sum0["backend"][k], 3) for k, v in summary["backend"].items()
+                        if isinstance(v, (int, float)) and k in sum0["backend"]}
     node.close()
 
     if rank == 0:
@@ -368,7 +388,8 @@ def run(a, rank, world, local, tmp):
             "data": "synthetic (tlv_server look-alike snapshot built in-process; the tlv module's CustomMutator_t "
                     "over its seed corpus)",
             "config": {"workload": TARGETS["tlv_server"][1], "lanes_per_gpu": a.lanes, "limit": a.limit,
-                       "max_len": TARGETS["tlv_server"][2],
+                       "max_len": TARGETS["tlv_server"][2], "slice_steps": a.slice_steps or 4096,
+                       "regroup_steps": a.regroup_steps,
                        "parallelism": f"shard{world}: one node per GPU (seed + rank), RCCL MAX coverage-map "
                                       f"merge per batch"},
             "instr_per_exec": retired / max(1.0, execs),
@@ -378,13 +399,14 @@ def run(a, rank, world, local, tmp):
             "node": {k: v for k, v in fields.items() if k not in ("lanes_per_wave_step", "gpu_retired_fraction")},
             "coverage": summary["coverage"], "unique_crashes": summary["unique_crashes"],
             "node_summary": summary,
+            "node_timed": timed,
             "cpu_baseline": cpu.get("tlv_server"),
             "host_cpus": core_info,
         }
         if out["cpu_baseline"]:
             out["vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
         if legs:
-            h = hevd_leg(hevd_dir, a.lanes, a.hevd_limit, a.leg_seconds)
+            h = hevd_leg(hevd_dir, a.lanes, a.hevd_limit, a.leg_seconds, sched_flags(a))
             if "hevd" in cpu:
                 h["cpu_baseline"] = cpu["hevd"]
                 h["vs_cpu"] = h["value"] / cpu["hevd"]["value"]

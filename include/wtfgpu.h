@@ -164,6 +164,11 @@ uint32_t wtfgpu_lane_count(wtfgpu_ctx *ctx);
 
 int wtfgpu_set_initial_state(wtfgpu_ctx *ctx, const wtfgpu_regs_t *regs);
 int wtfgpu_set_limit(wtfgpu_ctx *ctx, uint64_t limit);
+/* Cross-wave regrouping (no bochscpu counterpart: the SIMT schedule only):
+ * wtfgpu_run splits its wave-steps into k_run launches of `steps`, and before
+ * each one the running lanes are sorted by rip so that lanes at one rip share
+ * a wave. 0 = fixed lane order. Results are identical either way. */
+int wtfgpu_set_regroup(wtfgpu_ctx *ctx, uint64_t steps);
 int wtfgpu_set_breakpoints(wtfgpu_ctx *ctx, const uint64_t *gvas, uint32_t n);
 
 /* Device-side breakpoint actions (new; no bochscpu counterpart). A breakpoint

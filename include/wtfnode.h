@@ -38,6 +38,8 @@ typedef struct wtfnode_opts {
   int32_t device;           /* HIP device */
   int32_t rank, world;      /* shard rank of world; world 1 = alone */
   const uint8_t *rccl_id;   /* world > 1: WTFNODE_RCCL_ID_BYTES from wtfnode_rccl_unique_id on rank 0 */
+  uint64_t slice_steps;     /* wave-steps per streaming slice (0 = 4096) */
+  uint64_t regroup_steps;   /* k_run launch length with rip regrouping (0 = off, ~0 = engine default) */
 } wtfnode_opts_t;
 
 typedef struct wtfnode_stats {

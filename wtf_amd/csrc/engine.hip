@@ -71,18 +71,49 @@ __device__ __forceinline__ void load_lane(const Dev &P, u32 lane, Lane &L) {
   L.efer = s.efer;
   L.cpl = s.cpl;
   L.ovn = P.ov_count[lane];
-  L.bloom = 0;
-  for (u32 k = 0; k < L.ovn; k++) L.bloom |= bloom_bit(P.ov_gpfn[(u64)k * N + lane]);
   L.lane = lane;
   L.cgen = P.lane_gen ? P.lane_gen[lane] : 0;
   L.ccnt = P.cov_cnt ? P.cov_cnt[lane] : 0;
-  tlb_flush(L);
-  L.tnext = 0;
+  if (P.tlb_ok && P.tlb_ok[lane]) {
+    const LaneTlb &t = P.tlbs[lane];
+#pragma unroll
+    for (int i = 0; i < TLB_N; i++) {
+      L.tv[i] = t.tv[i];
+      L.td[i] = t.td[i];
+    }
+    L.cvpn = t.cvpn;
+    L.cptr = t.cptr;
+    L.bloom = t.bloom;
+    L.tnext = t.tnext;
+  } else {
+    L.bloom = 0;
+    for (u32 k = 0; k < L.ovn; k++) L.bloom |= bloom_bit(P.ov_gpfn[(u64)k * N + lane]);
+    tlb_flush(L);
+    L.tnext = 0;
+  }
   L.exvec = L.exerr = L.exop = 0;
   L.exaddr = 0;
   L.miss = L.miss_acc = L.flush = L.pend = 0;
   L.nodeliver = 0;
   L.miss_va = 0;
+}
+
+__device__ __forceinline__ void store_tlb(const Dev &P, const Lane &L) {
+  if (!P.tlb_ok) return;
+  LaneTlb &t = P.tlbs[L.lane];
+#pragma unroll
+  for (int i = 0; i < TLB_N; i++) {
+    t.tv[i] = L.tv[i];
+    t.td[i] = L.td[i];
+  }
+  t.cvpn = L.cvpn;
+  t.cptr = L.cptr;
+  t.bloom = L.bloom;
+  t.tnext = L.tnext;
+  P.tlb_ok[L.lane] = 1;
+}
+__device__ __forceinline__ void tlb_stale(const Dev &P, u32 lane) {
+  if (P.tlb_ok) P.tlb_ok[lane] = 0;
 }
 
 __device__ __forceinline__ void store_lane(const Dev &P, const Lane &L) {
@@ -334,7 +365,52 @@ __device__ __noinline__ bool deliver_fault(const Dev &P, Lane &L) {
   return ok;
 }
 
+constexpr u32 GUC_WORDS = 48;                                  // 3 lines x 16 dwords
+constexpr u32 GUC_PAYLOAD = (sizeof(UCEntry) - offsetof(UCEntry, flags)) / 4;  // flags .. UOp
+static_assert(GUC_PAYLOAD <= 3 * 14, "global uop cache entry: 3 lines of 14 payload dwords");
+__device__ __forceinline__ u32 guc_slot(const Dev &P, u64 key) {
+  return (u32)(mix64(key) & P.guc_mask);
+}
+// payload dword of lane lid (lines of 16 dwords: 14 payload, 2 key tag), or ~0u
+__device__ __forceinline__ u32 guc_payload_index(u32 lid) {
+  return (lid < GUC_WORDS && (lid & 15) < 14) ? (lid >> 4) * 14 + (lid & 15) : ~0u;
+}
+
+// COVERED: the rip's byte in the aggregate coverage map is set (dynamic: not
+// part of a shared entry)
+__device__ __forceinline__ u32 covered_flag(const Dev &P, u64 rip, u32 off) {
+  if (P.code_keys) {
+    u32 s;
+    if (hash_find(P.code_keys, P.code_mask, rip >> 12, s)) {
+      const u32 cs = rfl32(P.code_slot[s]);
+      if (rfl32(P.cov_map[(u64)cs * WTFGPU_PAGE_SIZE + off])) return UC_COVERED;
+    }
+  }
+  return 0;
+}
+
 __device__ __noinline__ void uc_fill(const Dev &P, UCEntry *e, u64 key, u64 lptr, u32 off, u64 rip, u32 lid) {
+  u32 *gw = nullptr;
+  const u32 pj = guc_payload_index(lid);
+  if (P.guc) {
+    // the shared cache first: one dword per lane, the six tag dwords checked
+    gw = P.guc + (u64)guc_slot(P, key) * GUC_WORDS;
+    const u32 w = lid < GUC_WORDS ? gw[lid] : 0;
+    const bool tag = lid < GUC_WORDS && (lid & 15) >= 14;
+    const bool bad = tag && w != ((lid & 1) ? (u32)(key >> 32) : (u32)key);
+    if (__ballot(bad) == 0) {
+      u32 *dst = (u32 *)&e->flags;
+      if (pj < GUC_PAYLOAD) dst[pj] = w;
+      const u32 flags = __builtin_amdgcn_readlane(w, 0) | covered_flag(P, rip, off);
+      __builtin_amdgcn_wave_barrier();
+      if (lid == 0) {
+        e->logged = 0;
+        e->flags = flags;
+        e->key = key;
+      }
+      return;
+    }
+  }
   IBytes ib;
   ib.avail = 4096 - off < 16 ? 4096 - off : 16;
   fetch_bytes(lptr, off, ib.avail, ib.lo, ib.hi);
@@ -346,21 +422,27 @@ __device__ __noinline__ void uc_fill(const Dev &P, UCEntry *e, u64 key, u64 lptr
     digest(d, f);
     if (!d.supported) flags |= UC_UNSUP;
     if (bp_lookup(P, rip)) flags |= UC_BP;
-    if (P.code_keys) {
-      u32 s;
-      if (hash_find(P.code_keys, P.code_mask, rip >> 12, s)) {
-        const u32 cs = rfl32(P.code_slot[s]);
-        if (rfl32(P.cov_map[(u64)cs * WTFGPU_PAGE_SIZE + off])) flags |= UC_COVERED;
-      }
-    }
   } else {
     f = FOp{};
   }
+  const u32 dyn = dr == 0 ? covered_flag(P, rip, off) : 0;
   if (lid == 0) {
     e->logged = 0;
-    e->flags = flags;
+    e->flags = flags;  // the static flags first: the shared copy is taken from here
     e->f = f;
     e->u = d;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  if (gw) {  // publish (static flags only); one coalesced store of 3 tagged lines
+    const u32 *src = (const u32 *)&e->flags;
+    u32 v = 0;
+    if (pj < GUC_PAYLOAD) v = src[pj];
+    else if (lid < GUC_WORDS && (lid & 15) >= 14) v = (lid & 1) ? (u32)(key >> 32) : (u32)key;
+    if (lid < GUC_WORDS) gw[lid] = v;
+  }
+  if (lid == 0) {
+    e->flags = flags | dyn;
     e->key = key;
   }
 }
@@ -761,7 +843,18 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     const u64 key = lptr | off;
     UCEntry *e = &uc[uc_slot(key)];
     const bool cacheable = lptr >= pool_lo && lptr < pool_hi;
-    if (cacheable && rfl64(e->key) != key) uc_fill(P, e, key, lptr, off, grip, lid);
+    if (cacheable && rfl64(e->key) != key) {
+      uc_fill(P, e, key, lptr, off, grip, lid);
+      // an entry the fast loop can run (a common op, nothing to log, no
+      // breakpoint): back to it, this pass was only the fill
+      const u32 ff = rfl32(e->flags);
+      if (!(ff & (UC_BP | UC_CROSS | UC_BADLEN | UC_UNSUP)) && (!P.cov_rip || (ff & UC_COVERED)) &&
+          fo_op(e->f) != FO_GENERIC) {
+        steps--;
+        STAMP(2);
+        continue;
+      }
+    }
     STAMP(2);
     const u32 flags = cacheable ? rfl32(e->flags) : UC_CROSS;
     if (flags & (UC_CROSS | UC_BADLEN)) {
@@ -826,6 +919,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
 
   if (valid) {
     store_lane(P, L);
+    store_tlb(P, L);
     if (L.status == WTFGPU_EXIT_FAULT || L.status == WTFGPU_EXIT_UNIMPLEMENTED) {
       ExitInfo ei;
       ei.vector = L.exvec;
@@ -874,6 +968,7 @@ __device__ __forceinline__ void restore_lane(const Dev &P, const InitState &s, c
   P.lflags[lane] = 0;
   P.sys[lane] = s.sys;
   P.ov_count[lane] = 0;
+  tlb_stale(P, lane);
   if (P.cov_rip) {
     P.lane_gen[lane] += 1;
     P.cov_cnt[lane] = 0;
@@ -910,6 +1005,7 @@ __global__ void k_restore(Dev P, const InitState *S, const wtfgpu_regs_t *full0,
   P.lflags[lane] = 0;
   P.sys[lane] = s.sys;
   P.ov_count[lane] = 0;  // the dirty-list reset: overlays dropped, nothing copied
+  tlb_stale(P, lane);
   if (P.cov_rip) {       // the lane's coverage set empties
     P.lane_gen[lane] += 1;
     P.cov_cnt[lane] = 0;
@@ -995,6 +1091,7 @@ __global__ void k_apply_writes(Dev P, const WriteRec *recs, const u32 *starts, u
     status_out[r] = st;
   }
   P.ov_count[lane] = L.ovn;
+  tlb_stale(P, lane);
 }
 
 // Host-injected exception per lane (PageFaultsMemoryIfNeeded): delivered
@@ -1016,6 +1113,7 @@ __global__ void k_inject_fault(Dev P, const u32 *lanes, const u64 *addrs, u32 n,
   ok[t] = d ? 1 : 0;
   if (d) {
     store_lane(P, L);
+    tlb_stale(P, lane);
     P.lflags[lane] = 0;
   }
 }
@@ -1073,6 +1171,7 @@ __global__ void k_lane_mem(Dev P, u32 lane, u32 op, u64 addr, u64 len, u8 *buf, 
       a += n;
     }
     P.ov_count[lane] = L.ovn;
+    tlb_stale(P, lane);
   }
   *result = rc;
 }
@@ -1153,6 +1252,29 @@ __global__ void k_cov_collect(Dev P, const u32 *lanes, u32 first, u32 n, u32 *ou
     }
   }
   if (threadIdx.x == 0 && P.cov_overflow[lane]) atomicOr(ovf, 1u);
+}
+
+// Exit records of lanes [first, first + count) (wtfgpu_read_exits).
+__global__ void k_pack_exits(Dev P, u32 first, u32 count, wtfgpu_exit_t *out) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const u32 lane = first + i;
+  wtfgpu_exit_t e;
+  e.status = P.status[lane];
+  e.vector = e.error = e.opcode = 0;
+  e.addr = 0;
+  if (e.status == WTFGPU_EXIT_FAULT) {
+    const ExitInfo x = P.exinfo[lane];
+    e.vector = x.vector;
+    e.error = x.error;
+    e.addr = x.addr;
+    e.opcode = x.cpl;
+  } else if (e.status == WTFGPU_EXIT_UNIMPLEMENTED) {
+    e.opcode = P.exinfo[lane].opcode;
+  }
+  e.rip = P.rip[lane];
+  e.icount = P.icount[lane];
+  out[i] = e;
 }
 
 // Regrouping keys: running lanes by rip (lanes at one rip become neighbours,
@@ -1257,6 +1379,9 @@ struct wtfgpu_ctx {
   u32 *d_status = nullptr, *d_lflags = nullptr, *d_ovcount = nullptr, *d_ovgpfn = nullptr;
   ExitInfo *d_exinfo = nullptr;
   LaneSys *d_sys = nullptr;
+  u32 *d_guc = nullptr;       // device-wide decoded-uop cache (Dev::guc)
+  LaneTlb *d_tlbs = nullptr;  // translation state kept between k_run launches
+  u32 *d_tlbok = nullptr;
   u8 *d_ovdata = nullptr;
   wtfgpu_regs_t *d_full = nullptr;  // full per-lane architectural state (cold fields)
   // breakpoints
@@ -1381,6 +1506,12 @@ int h2d(wtfgpu_ctx *c, T *dst, const T *src, u64 n) {
   return WTFGPU_OK;
 }
 
+// Entries depend on the pool pages and the breakpoint set: cleared with them.
+int guc_clear(wtfgpu_ctx *c) {
+  if (c->d_guc) HIPCHK(hipMemsetAsync(c->d_guc, 0, (u64)(c->P.guc_mask + 1) * GUC_WORDS * 4, c->stream));
+  return WTFGPU_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1403,6 +1534,20 @@ int wtfgpu_create(int device, wtfgpu_ctx **out) {
   if (!c) return WTFGPU_ERR_OOM;
   c->device = device;
   if (const char *e = getenv("WTFGPU_REGROUP_STEPS")) c->regroup_steps = strtoull(e, nullptr, 0);
+  {
+    // shared decoded-uop cache: 32K entries of 192 bytes (WTFGPU_GUC=0: off)
+    const char *e = getenv("WTFGPU_GUC");
+    const u32 n = e ? (u32)strtoul(e, nullptr, 0) : 32768u;
+    if (n && !(n & (n - 1))) {
+      if (dalloc(&c->d_guc, (u64)n * GUC_WORDS)) {
+        delete c;
+        return WTFGPU_ERR_OOM;
+      }
+      HIPCHK(hipMemset(c->d_guc, 0, (u64)n * GUC_WORDS * 4));
+      c->P.guc = c->d_guc;
+      c->P.guc_mask = n - 1;
+    }
+  }
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIPCHK(hipEventCreate(&c->ev0));
   HIPCHK(hipEventCreate(&c->ev1));
@@ -1433,6 +1578,8 @@ static void free_lanes(wtfgpu_ctx *c) {
   dfree(c->d_ovgpfn);
   dfree(c->d_exinfo);
   dfree(c->d_sys);
+  dfree(c->d_tlbs);
+  dfree(c->d_tlbok);
   dfree(c->d_ovdata);
   dfree(c->d_full);
   dfree(c->d_rkeys);
@@ -1454,6 +1601,7 @@ int wtfgpu_destroy(wtfgpu_ctx *c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   free_lanes(c);
+  dfree(c->d_guc);
   dfree(c->d_pool);
   dfree(c->d_pfnmap);
   dfree(c->d_ptbits);
@@ -1519,6 +1667,9 @@ int wtfgpu_load_pool(wtfgpu_ctx *c, const uint64_t *gpfns, const uint8_t *pages,
   c->P.pfn_map_len = maplen;
   c->P.npool = npages;
   c->P.ptbits = c->d_ptbits;
+  if (c->d_tlbok) HIPCHK(hipMemsetAsync(c->d_tlbok, 0, (u64)c->P.nlanes * 4, c->stream));  // old page pointers
+  if (guc_clear(c)) return WTFGPU_ERR_HIP;
+  HIPCHK(hipStreamSynchronize(c->stream));
   if (c->have_initial) return mark_pt_pages(c);
   return WTFGPU_OK;
 }
@@ -1557,6 +1708,8 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
     return WTFGPU_ERR_OOM;
   }
   rc |= dalloc(&c->d_full, N);
+  rc |= dalloc(&c->d_tlbs, N);
+  rc |= dalloc(&c->d_tlbok, N);
   if (cov_entries) {
     rc |= dalloc(&c->d_covrip, N * cov_entries);
     rc |= dalloc(&c->d_covgen, N * cov_entries);
@@ -1569,6 +1722,7 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
   HIPCHK(hipMemcpyAsync(c->d_status, idle.data(), N * 4, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemsetAsync(c->d_ovcount, 0, N * 4, c->stream));
   HIPCHK(hipMemsetAsync(c->d_lflags, 0, N * 4, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_tlbok, 0, N * 4, c->stream));
   HIPCHK(hipMemsetAsync(c->d_icount, 0, N * 8, c->stream));
   HIPCHK(hipMemsetAsync(c->d_nbytes, 0, N * 8, c->stream));
   HIPCHK(hipMemsetAsync(c->d_exinfo, 0, N * sizeof(ExitInfo), c->stream));
@@ -1595,6 +1749,8 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
   P.lflags = c->d_lflags;
   P.exinfo = c->d_exinfo;
   P.sys = c->d_sys;
+  P.tlbs = c->d_tlbs;
+  P.tlb_ok = c->d_tlbok;
   P.ov_count = c->d_ovcount;
   P.ov_gpfn = c->d_ovgpfn;
   P.ov_data = c->d_ovdata;
@@ -1653,11 +1809,18 @@ int wtfgpu_set_initial_state(wtfgpu_ctx *c, const wtfgpu_regs_t *regs) {
   c->initial = *regs;
   c->have_initial = true;
   c->P.cr3_0 = regs->cr3;
+  if (c->d_tlbok) HIPCHK(hipMemsetAsync(c->d_tlbok, 0, (u64)c->P.nlanes * 4, c->stream));  // page-table pages change
   const InitState s = make_init(*regs);
   HIPCHK(hipMemcpyAsync(c->d_init, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->d_init_full, regs, sizeof(*regs), hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return mark_pt_pages(c);
+}
+
+int wtfgpu_set_regroup(wtfgpu_ctx *c, uint64_t steps) {
+  if (!c) return WTFGPU_ERR_INVALID;
+  c->regroup_steps = steps;
+  return WTFGPU_OK;
 }
 
 int wtfgpu_set_limit(wtfgpu_ctx *c, uint64_t limit) {
@@ -1672,7 +1835,11 @@ int wtfgpu_set_breakpoints(wtfgpu_ctx *c, const uint64_t *gvas, uint32_t n) {
   dfree(c->d_bp);
   c->P.bp_keys = nullptr;
   c->P.bp_mask = 0;
-  if (n == 0) return WTFGPU_OK;
+  if (guc_clear(c)) return WTFGPU_ERR_HIP;  // shared entries carry the breakpoint flag
+  if (n == 0) {
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return WTFGPU_OK;
+  }
   const u32 sz = table_size(n);
   std::vector<u64> t(sz, EMPTY_KEY);
   for (u32 i = 0; i < n; i++) {
@@ -1973,6 +2140,7 @@ int wtfgpu_write_regs(wtfgpu_ctx *c, uint32_t first, uint32_t count, const wtfgp
   rc |= h2d(c, c->d_fsb + first, fsb.data(), count);
   rc |= h2d(c, c->d_gsb + first, gsb.data(), count);
   rc |= h2d(c, c->d_sys + first, sys.data(), count);
+  if (c->d_tlbok) HIPCHK(hipMemsetAsync(c->d_tlbok + first, 0, (u64)count * 4, c->stream));
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(c->stream));
   return WTFGPU_OK;
@@ -1980,31 +2148,15 @@ int wtfgpu_write_regs(wtfgpu_ctx *c, uint32_t first, uint32_t count, const wtfgp
 
 int wtfgpu_read_exits(wtfgpu_ctx *c, uint32_t first, uint32_t count, wtfgpu_exit_t *out) {
   if (!lanes_ok(c, first, count) || !out) return WTFGPU_ERR_INVALID;
+  if (count == 0) return WTFGPU_OK;
   HIPCHK(hipSetDevice(c->device));
-  std::vector<u32> st(count);
-  std::vector<ExitInfo> ex(count);
-  std::vector<u64> rip(count), ic(count);
-  int rc = 0;
-  rc |= d2h(c, st.data(), c->d_status + first, count);
-  rc |= d2h(c, ex.data(), c->d_exinfo + first, count);
-  rc |= d2h(c, rip.data(), c->d_rip + first, count);
-  rc |= d2h(c, ic.data(), c->d_icount + first, count);
-  if (rc) return rc;
+  // packed on the device, one copy back
+  const u64 bytes = (u64)count * sizeof(wtfgpu_exit_t);
+  if (ensure_scratch(c, bytes)) return WTFGPU_ERR_OOM;
+  k_pack_exits<<<(count + 255) / 256, 256, 0, c->stream>>>(c->P, first, count, (wtfgpu_exit_t *)c->d_scratch);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, c->d_scratch, bytes, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  for (u64 l = 0; l < count; l++) {
-    wtfgpu_exit_t &e = out[l];
-    memset(&e, 0, sizeof(e));
-    e.status = st[l];
-    if (st[l] == WTFGPU_EXIT_FAULT) {
-      e.vector = ex[l].vector;
-      e.error = ex[l].error;
-      e.addr = ex[l].addr;
-      e.opcode = ex[l].cpl;
-    }
-    if (st[l] == WTFGPU_EXIT_UNIMPLEMENTED) e.opcode = ex[l].opcode;
-    e.rip = rip[l];
-    e.icount = ic[l];
-  }
   return WTFGPU_OK;
 }
 
@@ -2348,6 +2500,7 @@ int wtfgpu_lane_set_cr(wtfgpu_ctx *c, uint32_t lane, uint32_t cr, uint64_t value
   if (lane_cr_ptr(c, lane, cr, &p)) return WTFGPU_ERR_INVALID;
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipMemcpyAsync(p, &value, 8, hipMemcpyHostToDevice, c->stream));
+  if (cr == 3) HIPCHK(hipMemsetAsync(c->d_tlbok + lane, 0, 4, c->stream));  // translations of the old cr3
   HIPCHK(hipStreamSynchronize(c->stream));
   return WTFGPU_OK;
 }

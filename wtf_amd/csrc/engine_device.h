@@ -51,6 +51,15 @@ struct LaneSys {   // rarely touched per-lane system state
   u16 cs, ss;                    // selectors after SYSCALL/SYSRET (64-bit mode, STAR)
 };
 
+// Translation state a lane keeps between k_run launches (regrouped launches
+// are short): TLB, code-page cache, overlay filter. tlb_ok[lane] == 0 means
+// stale (restore, host writes, injected faults, register / cr writes).
+struct LaneTlb {
+  u64 tv[TLB_N], td[TLB_N];
+  u64 cvpn, cptr, bloom;
+  u32 tnext, pad;
+};
+
 struct ExitInfo {
   u32 vector, error, opcode, cpl;  // cpl: privilege level the fault was raised at
   u64 addr;
@@ -104,6 +113,13 @@ struct Dev {
   // lane order of a k_run launch (cross-wave regrouping): hardware wave w runs
   // lanes perm[first + w * lpw ...]; nullptr = identity
   const u32 *perm;
+  // device-wide decoded-uop cache (shared by every wave and launch): entries
+  // of 3 x 64-byte lines, 14 payload dwords + the key in each line's last 8
+  // bytes (a reader takes an entry only when all three tags match)
+  u32 *guc;
+  u32 guc_mask;
+  LaneTlb *tlbs;          // [nlanes]
+  u32 *tlb_ok;            // [nlanes]
   wtfgpu_regs_t *full;   // [nlanes] cold architectural state (MSRs the hot LaneSys lacks)
   u64 cr3_0;             // the testcases' initial cr3 (Cr3Change_t, bochscpu_backend.cc:628-657)
   u64 limit;

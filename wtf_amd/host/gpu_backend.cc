@@ -604,7 +604,10 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
 
   for (;;) {
     wtfgpu_run_stats_t rs{};
+    const auto tk = Clock::now();
     if (wtfgpu_run(ctx_, first, count, sliced ? slice : ~0ull, &rs)) return false;
+    const auto te = Clock::now();
+    stats_.run_ms += std::chrono::duration<double, std::milli>(te - tk).count();
     stats_.kernel_launches += rs.kernel_launches;
     stats_.kernel_ms += rs.kernel_ms;
     stats_.retired += rs.lane_retired;
@@ -612,12 +615,15 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
     stats_.rounds++;
     if (wtfgpu_read_exits(ctx_, first, count, ex.data())) return false;
     std::vector<uint32_t> hits;
-    for (uint32_t l : pending) {
+    std::vector<uint8_t> hit(pending.size(), 0);
+#pragma omp parallel for schedule(static, 1024) if (pending.size() >= 8192)
+    for (size_t pi = 0; pi < pending.size(); pi++) {
+      const uint32_t l = pending[pi];
       if (done[l - first]) continue;
       const wtfgpu_exit_t &e = ex[l - first];
       LaneView &v = views_[l];
       switch (e.status) {
-        case WTFGPU_EXIT_BREAKPOINT: hits.push_back(l); continue;
+        case WTFGPU_EXIT_BREAKPOINT: hit[pi] = 1; continue;
         case WTFGPU_RUNNING: continue;  // sliced: still running when the slice ended
         case WTFGPU_EXIT_TIMEOUT: v.result = Timedout_t(); break;    // bochscpu_backend.cc:458-469
         case WTFGPU_EXIT_INT3:                                         // :595-619
@@ -637,6 +643,9 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
       }
       done[l - first] = 1;
     }
+    for (size_t pi = 0; pi < pending.size(); pi++)
+      if (hit[pi]) hits.push_back(pending[pi]);
+    stats_.exits_ms += ms_since(te);
     if (hits.empty()) break;
     if (!service_hits(hits, first, done, slots, per_lane_state)) return false;
     if (sliced) break;  // the serviced lanes resume in the next slice
@@ -647,23 +656,33 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
   if (finished)
     for (uint32_t l : lanes)
       if (done[l - first]) finished->push_back(l);
-  // final state of every finished lane
+  // final state of every finished lane (`ex` holds the last round's exits of
+  // every lane: a lane is final once it is done)
   if (out) {
+    const auto tg = Clock::now();
     std::vector<uint32_t> fin;
     for (uint32_t l : lanes)
       if (done[l - first]) fin.push_back(l);
-    std::vector<uint64_t> regs(fin.size() * 18);
-    if (!fin.empty() && wtfgpu_read_gprs_list(ctx_, fin.data(), (uint32_t)fin.size(), regs.data())) return false;
-    if (wtfgpu_read_exits(ctx_, first, count, ex.data())) return false;
+    std::vector<uint64_t> regs;
+    if (want_gprs_) {  // run mode prints them; the fuzz loop never reads them
+      regs.resize(fin.size() * 18);
+      if (!fin.empty() && wtfgpu_read_gprs_list(ctx_, fin.data(), (uint32_t)fin.size(), regs.data())) return false;
+    }
+#pragma omp parallel for schedule(static, 1024) if (fin.size() >= 8192)
     for (size_t i = 0; i < fin.size(); i++) {
       LaneResult &r = (*out)[fin[i]];
       const LaneView &v = views_[fin[i]];
       r.result = v.result ? *v.result : TestcaseResult_t(Ok_t());
-      memcpy(r.gprs, &regs[i * 18], 18 * 8);
-      r.rip = r.gprs[16];
+      if (want_gprs_) {
+        memcpy(r.gprs, &regs[i * 18], 18 * 8);
+        r.rip = r.gprs[16];
+      } else {
+        r.rip = ex[fin[i] - first].rip;
+      }
       r.icount = ex[fin[i] - first].icount;
       r.exit_status = ex[fin[i] - first].status;
     }
+    stats_.regs_ms += ms_since(tg);
   }
   return true;
 }
@@ -1190,8 +1209,12 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
   stats_.coverage_ms += std::chrono::duration<double, std::milli>(tr - tc).count();
   target_restore(Target, finished, Slots);
   stats_.target_restore_ms += ms_since(tr);
-  for (uint32_t l : finished) {
-    Out.push_back(StreamResult_t{tag_[l], std::move(lres_[l])});
+  const size_t base = Out.size();
+  Out.resize(base + finished.size());
+#pragma omp parallel for schedule(static, 1024) if (finished.size() >= 8192)
+  for (size_t i = 0; i < finished.size(); i++) {
+    const uint32_t l = finished[i];
+    Out[base + i] = StreamResult_t{tag_[l], std::move(lres_[l])};
     lres_[l] = LaneResult{};
     busy_[l] = 0;
     // not runnable until refilled (a finished lane keeps its exit status)
@@ -1215,7 +1238,8 @@ std::string GpuBackend_t::StatsJson() const {
            "\"prefetched_pages\":%llu,\"stack_windows\":%llu,\"staged_pages\":%llu,\"bulk_ms\":%.3f,\"prefetch_ms\":%.3f,"
            "\"handler_ms\":%.3f,\"fetch_ms\":%.3f,\"flush_ms\":%.3f,\"insert_ms\":%.3f,\"coverage_ms\":%.3f,"
            "\"target_restore_ms\":%.3f,\"alg_bytes\":%llu,\"restore_ms\":%.3f,\"module_ms\":%.3f,"
-           "\"upload_ms\":%.3f,\"bytes_ms\":%.3f,\"covlog_ms\":%.3f,\"attrib_ms\":%.3f,\"cov_entries\":%llu}",
+           "\"upload_ms\":%.3f,\"bytes_ms\":%.3f,\"covlog_ms\":%.3f,\"attrib_ms\":%.3f,\"cov_entries\":%llu,"
+           "\"run_ms\":%.3f,\"exits_ms\":%.3f,\"regs_ms\":%.3f}",
            (unsigned long long)stats_.group_steps, (unsigned long long)stats_.rounds,
            (unsigned long long)stats_.breakpoint_hits, (unsigned long long)stats_.kernel_launches, stats_.kernel_ms,
            stats_.service_ms, stats_.total_ms, (unsigned long long)stats_.page_fetches,
@@ -1223,7 +1247,8 @@ std::string GpuBackend_t::StatsJson() const {
            (unsigned long long)stats_.staged_pages, stats_.bulk_ms, stats_.prefetch_ms, stats_.handler_ms,
            stats_.fetch_ms, stats_.flush_ms, stats_.insert_ms, stats_.coverage_ms, stats_.target_restore_ms,
            (unsigned long long)stats_.alg_bytes, stats_.restore_ms, stats_.module_ms, stats_.upload_ms,
-           stats_.bytes_ms, stats_.covlog_ms, stats_.attrib_ms, (unsigned long long)stats_.cov_entries);
+           stats_.bytes_ms, stats_.covlog_ms, stats_.attrib_ms, (unsigned long long)stats_.cov_entries,
+           stats_.run_ms, stats_.exits_ms, stats_.regs_ms);
   std::string r(b);
   r.pop_back();
   r += ",\"fetch_by_bp\":{";

@@ -46,6 +46,8 @@ struct BatchStats {
   // streaming harvest split: per-lane byte counters, coverage logs, attribution
   double bytes_ms = 0, covlog_ms = 0, attrib_ms = 0;
   uint64_t cov_entries = 0;  // (lane, rip) new-coverage log entries collected
+  // run loop split: wtfgpu_run wall (launches + syncs), exit read-back + classification, final registers
+  double run_ms = 0, exits_ms = 0, regs_ms = 0;
 };
 
 class GpuBackend_t final : public Backend_t, public Executor_t {
@@ -95,6 +97,7 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
                   std::vector<StreamResult_t> &Out, ModuleSlots *Slots) override;
   void ResetCoverage() override;
   void SetFullCoverage(bool On) override { full_coverage_ = On; }
+  void SetWantRegisters(bool On) override { want_gprs_ = On; }
   size_t CoverageSize() const override { return aggregate_.size(); }
   std::string StatsJson() const override;
   bool CoverageMap(uint8_t **Map, uint64_t *Bytes, bool *Device) override;
@@ -181,6 +184,7 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   std::vector<uint32_t> cov_lanes_;  // coverage collection buffers (streaming)
   std::vector<uint64_t> cov_rips_;
   bool cov_ovf_warned_ = false;
+  bool want_gprs_ = true;
   uint8_t *feed_pin_ = nullptr;  // pinned staging of streamed feeds
   uint64_t feed_pin_cap_ = 0;
   void finish_coverage(uint32_t n, std::vector<LaneResult> *out, std::vector<uint32_t> *timedout);

@@ -24,6 +24,7 @@ int main(int argc, char **argv) {
     printf("Failed to initialize the gpu backend\n");
     return 1;
   }
+  if (O.regroup != ~0ull) wtfgpu_set_regroup(B->Engine(), O.regroup);
   std::unique_ptr<wtfgpu_host::RcclExchange_t> X;
   if (O.world > 1) {
     uint8_t Id[wtfgpu_host::kRcclIdBytes];

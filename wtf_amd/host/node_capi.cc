@@ -46,10 +46,13 @@ int wtfnode_open(const wtfnode_opts_t *o, wtfnode **out) {
   O.device = o->device;
   O.rank = o->rank;
   O.world = o->world;
+  if (o->slice_steps) O.slice = o->slice_steps;
+  O.regroup = o->regroup_steps;
   if (!LoadTarget(O, N->Opts, N->State)) return -2;
   N->B = new GpuBackend_t();
   g_Backend = N->B;
   if (!N->B->Initialize(N->Opts, N->State)) return -3;
+  if (O.regroup != ~0ull) wtfgpu_set_regroup(N->B->Engine(), O.regroup);
   if (O.world > 1) {
     N->X = std::make_unique<RcclExchange_t>(O.rank, O.world);
     if (!N->X->Init(o->rccl_id, wtfgpu_stream(N->B->Engine()))) return -4;

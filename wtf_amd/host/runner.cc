@@ -143,6 +143,7 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
     else if (a == "--quiet") O.quiet = true;
     else if (a == "--serial-mutation") O.serial_mutation = true;
     else if (a == "--slice-steps") O.slice = strtoull(next("--slice-steps"), nullptr, 0);
+    else if (a == "--regroup-steps") O.regroup = strtoull(next("--regroup-steps"), nullptr, 0);
     else if (a == "--stream-run") O.stream_run = true;
     else if (a == "--rank") O.rank = atoi(next("--rank"));
     else if (a == "--world") O.world = atoi(next("--world"));
@@ -160,7 +161,7 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
   if (O.name.empty() || O.target.empty()) {
     fprintf(stderr, "usage: [run|fuzz] --name <target> --target <dir> [--input p] [--results f] [--limit n]\n"
                     "       [--lanes n] [--overlay-pages k] [--runs n] [--seconds s] [--seed s] [--full-coverage]\n"
-                    "       [--serial-mutation] [--slice-steps s] [--rank r --world n [--exchange host:port | --nccl-id-file f]]\n");
+                    "       [--serial-mutation] [--slice-steps s] [--regroup-steps r] [--rank r --world n [--exchange host:port | --nccl-id-file f]]\n");
     return false;
   }
   return true;
@@ -310,6 +311,7 @@ FuzzSession::~FuzzSession() {
 }
 
 bool FuzzSession::Start() {
+  Exec_.SetWantRegisters(false);
   fs::create_directories(T_ / "outputs");
   fs::create_directories(T_ / "crashes");
   if (Target_.CreateMutator) Mutator_ = Target_.CreateMutator(Rng_, O_.max_len);
@@ -325,11 +327,21 @@ bool FuzzSession::Start() {
   t0_ = Clock::now();
   stream_ = O_.slice && Exec_.CanStream();
   if (stream_) {
-    for (std::string &S : MakeBatch(Budget(Exec_.Lanes()))) Ready_.push_back(std::move(S));
+    Adopt(MakeBatch(Budget(Exec_.Lanes())));
     return !Ready_.empty();
   }
   Batch_ = MakeBatch(Budget(Exec_.Lanes()));
   return !Batch_.empty();
+}
+
+void FuzzSession::Adopt(TcBatch &&B) {
+  for (std::unique_ptr<TcArena> &A : B) {
+    if (!A || A->Count() == 0) continue;
+    A->Live = A->Count();
+    for (size_t i = 0; i < A->Count(); i++) Ready_.push_back(TcRef{A.get(), (uint32_t)i});
+    TcArena *K = A.get();
+    Arenas_.emplace(K, std::move(A));
+  }
 }
 
 // at most n more testcases within the --runs budget
@@ -353,23 +365,28 @@ bool FuzzSession::More(uint64_t done) const {
 double FuzzSession::WallSeconds() const { return secs_since(t0_); }
 
 // The next n testcases: the corpus inputs first, then mutations of corpus picks.
-std::vector<std::string> FuzzSession::MakeBatch(uint64_t n) {
-  std::vector<std::string> Batch;
-  Batch.reserve(n);
-  while (Batch.size() < n && !Pending_.empty()) {
-    Batch.push_back(std::move(Pending_.back()));
+TcBatch FuzzSession::MakeBatch(uint64_t n) {
+  TcBatch Batch;
+  size_t Made = 0;
+  auto Tail = [&]() -> TcArena & {
+    if (Batch.empty()) Batch.push_back(std::make_unique<TcArena>());
+    return *Batch.back();
+  };
+  while (Made < n && !Pending_.empty()) {
+    Tail().Add(Pending_.back().data(), Pending_.back().size());
     Pending_.pop_back();
+    Made++;
   }
   // large batches: mutate in fixed chunks on the host threads; chunk c has
   // its own generator, seeded from Rng in chunk order, its own mutator and
   // a read-only view of the corpus (deterministic for a seed whatever the
   // thread count; the corpus does not change while the batch is built)
-  const size_t Need = n - Batch.size();
+  const size_t Need = n - Made;
   if (Corpus_.Size() && Need >= kParMutateMin && !O_.serial_mutation) {
     const size_t Chunks = (Need + kMutateChunk - 1) / kMutateChunk;
     std::vector<uint64_t> Seeds(Chunks);
     for (uint64_t &S : Seeds) S = Rng_();
-    std::vector<std::string> Out(Need);
+    std::vector<std::unique_ptr<TcArena>> Out(Chunks);
     std::atomic<size_t> NextChunk{0};
     auto Work = [&]() {
       for (size_t c; (c = NextChunk.fetch_add(1)) < Chunks;) {
@@ -379,24 +396,46 @@ std::vector<std::string> FuzzSession::MakeBatch(uint64_t n) {
         // the master mutator's cross-over partner (the last new-coverage
         // testcase) is every chunk mutator's too
         if (HaveNewCov_) M->OnNewCoverage(Testcase_t((const uint8_t *)LastNewCov_.data(), LastNewCov_.size()));
-        for (size_t i = c * kMutateChunk; i < std::min(Need, (c + 1) * kMutateChunk); i++) {
-          Out[i] = M->GetNewTestcase(View);
-          if (Out[i].size() > O_.max_len) Out[i].resize(O_.max_len);
+        auto A = std::make_unique<TcArena>();
+        const size_t End = std::min(Need, (c + 1) * kMutateChunk);
+        A->Off.reserve(End - c * kMutateChunk + 1);
+        for (size_t i = c * kMutateChunk; i < End; i++) {
+          const std::string S = M->GetNewTestcase(View);
+          A->Add(S.data(), std::min<size_t>(S.size(), O_.max_len));
         }
+        Out[c] = std::move(A);
       }
     };
     std::vector<std::thread> Pool;
     for (unsigned t = 1; t < host_threads(); t++) Pool.emplace_back(Work);
     Work();
     for (std::thread &Th : Pool) Th.join();
-    for (std::string &S : Out) Batch.push_back(std::move(S));
+    for (std::unique_ptr<TcArena> &A : Out) Batch.push_back(std::move(A));
+    Made += Need;
+    Batch.push_back(std::make_unique<TcArena>());  // the serial tail below
   }
-  while (Batch.size() < n) {
-    if (Corpus_.Size() == 0 && Batch.empty()) break;
-    std::string S = Corpus_.Size() ? Mutator_->GetNewTestcase(Corpus_) : Batch[Rng_() % Batch.size()];
-    if (S.size() > O_.max_len) S.resize(O_.max_len);
-    Batch.push_back(std::move(S));
+  while (Made < n) {
+    if (Corpus_.Size() == 0 && Made == 0) break;
+    if (Corpus_.Size()) {
+      const std::string S = Mutator_->GetNewTestcase(Corpus_);
+      Tail().Add(S.data(), std::min<size_t>(S.size(), O_.max_len));
+    } else {  // no corpus yet: repeat one of the batch's testcases so far
+      size_t k = Rng_() % Made;
+      const TcArena *F = nullptr;
+      for (const std::unique_ptr<TcArena> &A : Batch) {
+        if (k < A->Count()) {
+          F = A.get();
+          break;
+        }
+        k -= A->Count();
+      }
+      const std::vector<uint8_t> Copy(F->Ptr(k), F->Ptr(k) + F->Len(k));
+      Tail().Add(Copy.data(), Copy.size());
+    }
+    Made++;
   }
+  Batch.erase(std::remove_if(Batch.begin(), Batch.end(), [](const std::unique_ptr<TcArena> &A) { return A->Count() == 0; }),
+              Batch.end());
   return Batch;
 }
 
@@ -409,12 +448,15 @@ bool FuzzSession::Step() {
   // a shard that is done keeps joining the other shards' merges
   if (X_ && X_->World() > 1 && Done()) return MergeCoverage();
   if (stream_) return StreamStep();
-  if (Batch_.empty()) return true;
-  std::vector<std::pair<const uint8_t *, size_t>> Tc(Batch_.size());
-  for (size_t i = 0; i < Batch_.size(); i++) Tc[i] = {(const uint8_t *)Batch_[i].data(), Batch_[i].size()};
+  BatchRefs_.clear();
+  for (const std::unique_ptr<TcArena> &A : Batch_)
+    for (size_t i = 0; i < A->Count(); i++) BatchRefs_.push_back(TcRef{A.get(), (uint32_t)i});
+  if (BatchRefs_.empty()) return true;
+  std::vector<std::pair<const uint8_t *, size_t>> Tc(BatchRefs_.size());
+  for (size_t i = 0; i < BatchRefs_.size(); i++) Tc[i] = {BatchRefs_[i].data(), BatchRefs_[i].size()};
   std::vector<LaneResult> R;
   const auto tb = Clock::now();
-  const uint64_t after = S_.execs + Batch_.size();
+  const uint64_t after = S_.execs + BatchRefs_.size();
   if (More(after) && Corpus_.Size()) {
     const uint64_t n = O_.runs ? std::min<uint64_t>(Exec_.Lanes(), O_.runs - after) : Exec_.Lanes();
     Next_ = std::async(std::launch::async, &FuzzSession::MakeBatch, this, n);
@@ -422,9 +464,9 @@ bool FuzzSession::Step() {
   if (!Exec_.RunBatch(Target_, Tc, R, &Slots_)) return false;
   S_.run_s += secs_since(tb);
   S_.batches++;
-  std::vector<std::string> NextBatch;
+  TcBatch NextBatch;
   if (Next_.valid()) NextBatch = Next_.get();  // before the corpus / mutator change below
-  for (size_t i = 0; i < Batch_.size(); i++) Account(Batch_[i], R[i]);
+  for (size_t i = 0; i < BatchRefs_.size(); i++) Account(BatchRefs_[i].data(), BatchRefs_[i].size(), R[i]);
   if (X_ && X_->World() > 1 && !MergeCoverage()) return false;
   if (!NextBatch.empty() || !More(S_.execs))
     Batch_ = std::move(NextBatch);
@@ -439,12 +481,16 @@ bool FuzzSession::Step() {
 // corpus as it stood before this step's results.
 bool FuzzSession::StreamStep() {
   if (Done()) return true;
+  const auto t_step = Clock::now();
   std::vector<StreamTestcase_t> In;
   const bool open = More(S_.execs);
   if (open) {
     const uint32_t free = Exec_.FreeLanes();
-    if (Ready_.size() < free && !Next_.valid() && Corpus_.Size())  // nothing in the pipe: make them now
-      for (std::string &S : MakeBatch(Budget(free - Ready_.size()))) Ready_.push_back(std::move(S));
+    if (Ready_.size() < free && !Next_.valid() && Corpus_.Size()) {  // nothing in the pipe: make them now
+      const auto tm = Clock::now();
+      Adopt(MakeBatch(Budget(free - Ready_.size())));
+      S_.make_ms += secs_since(tm) * 1e3;
+    }
     const size_t take = std::min<size_t>(free, Ready_.size());
     In.reserve(take);
     for (size_t i = 0; i < take; i++) {
@@ -454,11 +500,11 @@ bool FuzzSession::StreamStep() {
       }
       const uint64_t tag = FreeSlot_.back();
       FreeSlot_.pop_back();
-      std::string &slot = Slot_[tag];
-      slot.swap(Ready_.front());
+      const TcRef R = Ready_.front();
       Ready_.pop_front();
+      Slot_[tag] = R;
       InFlight_++;
-      In.push_back(StreamTestcase_t{(const uint8_t *)slot.data(), slot.size(), tag});
+      In.push_back(StreamTestcase_t{R.data(), R.size(), tag});
     }
     const uint64_t want = Budget(Exec_.Lanes() > Ready_.size() ? Exec_.Lanes() - Ready_.size() : 0);
     if (want && Corpus_.Size() && !Next_.valid())
@@ -466,28 +512,32 @@ bool FuzzSession::StreamStep() {
   }
   std::vector<StreamResult_t> Out;
   const auto tb = Clock::now();
+  S_.fill_ms += std::chrono::duration<double, std::milli>(tb - t_step).count();
   const bool ok = Exec_.StreamStep(Target_, In, O_.slice, Out, &Slots_);
   S_.run_s += secs_since(tb);
   const auto tw = Clock::now();
-  if (Next_.valid())  // before the corpus / mutator change below
-    for (std::string &S : Next_.get()) Ready_.push_back(std::move(S));
+  if (Next_.valid()) Adopt(Next_.get());  // before the corpus / mutator change below
   const auto ta = Clock::now();
   S_.produce_wait_ms += std::chrono::duration<double, std::milli>(ta - tw).count();
   if (!ok) return false;
   S_.batches++;
   for (StreamResult_t &F : Out) {
     if (F.tag >= Slot_.size()) return false;
-    Account(Slot_[F.tag], F.r);
-    FreeSlot_.push_back(F.tag);  // the string keeps its buffer for the next testcase
+    const TcRef R = Slot_[F.tag];
+    Account(R.data(), R.size(), F.r);
+    if (--R.A->Live == 0) Arenas_.erase(R.A);  // every testcase of the arena accounted
+    Slot_[F.tag] = TcRef{};
+    FreeSlot_.push_back(F.tag);
     InFlight_--;
   }
   S_.account_ms += secs_since(ta) * 1e3;
   if (X_ && X_->World() > 1 && !MergeCoverage()) return false;
+  S_.step_ms += secs_since(t_step) * 1e3;
   return true;
 }
 
 // The master's bookkeeping of one result (server.h:816-886).
-void FuzzSession::Account(const std::string &Tc, const LaneResult &L) {
+void FuzzSession::Account(const uint8_t *Tc, size_t Size, const LaneResult &L) {
   S_.execs++;
   S_.retired += L.icount;
   if (L.error) {  // the engine could not finish it: neither a crash nor coverage
@@ -500,16 +550,16 @@ void FuzzSession::Account(const std::string &Tc, const LaneResult &L) {
   if (const Crash_t *C = std::get_if<Crash_t>(&L.result)) {
     S_.crashes++;
     if (!C->CrashName.empty() && CrashNames_.insert(C->CrashName).second)
-      SaveFile(T_ / "crashes" / C->CrashName, (const uint8_t *)Tc.data(), Tc.size());
+      SaveFile(T_ / "crashes" / C->CrashName, Tc, Size);
   }
   // a timed-out testcase reports no coverage (the client revokes it,
   // client.cc:122-133); any other result with new coverage, crashes
   // included, joins the corpus after arming the mutator's cross-over
   // (server.h:816-853)
   if (!L.new_coverage.empty() && !std::holds_alternative<Timedout_t>(L.result)) {
-    Testcase_t Tcase((const uint8_t *)Tc.data(), Tc.size());
+    Testcase_t Tcase(Tc, Size);
     Mutator_->OnNewCoverage(Tcase);
-    LastNewCov_ = Tc;
+    LastNewCov_.assign((const char *)Tc, Size);
     HaveNewCov_ = true;
     Corpus_.SaveTestcase(L.result, std::move(Tcase));
   }
@@ -538,7 +588,7 @@ std::string FuzzSession::SummaryJson() const {
            "\"execs\":%llu,\"retired\":%llu,\"wall_s\":%.6f,\"run_s\":%.6f,\"execs_per_s\":%.3f,"
            "\"instr_per_s\":%.3f,\"coverage\":%zu,\"corpus\":%zu,\"crashes\":%llu,\"unique_crashes\":%zu,"
            "\"timeouts\":%llu,\"cr3\":%llu,\"errors\":%llu,\"error_retired\":%llu,\"merged_rips\":%llu,"
-           "\"merge_ms\":%.3f,\"produce_wait_ms\":%.3f,\"account_ms\":%.3f,"
+           "\"merge_ms\":%.3f,\"produce_wait_ms\":%.3f,\"account_ms\":%.3f,\"make_ms\":%.3f,\"step_ms\":%.3f,\"fill_ms\":%.3f,"
            "\"backend\":",
            O_.name.c_str(), Exec_.Lanes(), X_ ? X_->Rank() : 0, X_ ? X_->World() : 1,
            (unsigned long long)S_.batches, (unsigned long long)S_.execs, (unsigned long long)S_.retired, Wall,
@@ -546,7 +596,7 @@ std::string FuzzSession::SummaryJson() const {
            Exec_.CoverageSize(), Corpus_.Size(), (unsigned long long)S_.crashes, CrashNames_.size(),
            (unsigned long long)S_.timeouts, (unsigned long long)S_.cr3, (unsigned long long)S_.errors,
            (unsigned long long)S_.error_retired, (unsigned long long)S_.merged_rips, S_.merge_ms, S_.produce_wait_ms,
-           S_.account_ms);
+           S_.account_ms, S_.make_ms, S_.step_ms, S_.fill_ms);
   return std::string(b) + Exec_.StatsJson() + "}";
 }
 

@@ -66,6 +66,8 @@ class Executor_t {
   // parity mode: LaneResult::new_coverage holds each testcase's full rip set
   // (as if it ran first), not the lane-order delta
   virtual void SetFullCoverage(bool On) = 0;
+  // LaneResult::gprs filled (run mode prints them; the fuzz loop does not read them)
+  virtual void SetWantRegisters(bool) {}
   virtual size_t CoverageSize() const = 0;
   virtual std::string StatsJson() const { return "{}"; }
   // The coverage map over the executable-page slot table (one byte per code
@@ -116,6 +118,10 @@ struct RunnerOptions {
   // occupied lane runs `slice` wave-steps per step, finished lanes are
   // refilled at once; 0 = whole batches (every lane runs to its end)
   uint64_t slice = 4096;
+  // GPU: k_run launches of this many wave-steps with the lanes regrouped by
+  // rip between them (wtfgpu_set_regroup); 0 = fixed lane order, ~0 = the
+  // engine's default (WTFGPU_REGROUP_STEPS)
+  uint64_t regroup = ~0ull;
   bool stream_run = false;  // run: replay the inputs through the streaming path
   int rank = 0, world = 1;         // fuzz: shard rank of world (one node per GPU)
   std::string exchange = "127.0.0.1:31337";  // TCP coverage exchange (CPU shards): rank 0 listens here
@@ -127,6 +133,32 @@ struct FuzzStats {
   uint64_t error_retired = 0;  // instructions retired by testcases the engine could not finish
   double run_s = 0, merge_ms = 0;
   double produce_wait_ms = 0, account_ms = 0;  // streaming: waiting on the mutator, master bookkeeping
+  double make_ms = 0, step_ms = 0;             // streaming: mutation on the step's own thread, whole steps
+  double fill_ms = 0;                          // streaming: taking the step's testcases (make_ms included)
+};
+
+// Testcases stored back to back: one allocation per chunk of mutations, so
+// handing 64K+ testcases per step to the lanes allocates and frees nothing
+// per testcase on the step's thread.
+struct TcArena {
+  std::vector<uint8_t> Data;
+  std::vector<uint64_t> Off{0};
+  size_t Live = 0;  // streaming: testcases of this arena not yet accounted
+  void Add(const void *P, size_t N) {
+    const uint8_t *B = (const uint8_t *)P;
+    Data.insert(Data.end(), B, B + N);
+    Off.push_back(Data.size());
+  }
+  size_t Count() const { return Off.size() - 1; }
+  const uint8_t *Ptr(size_t I) const { return Data.data() + Off[I]; }
+  size_t Len(size_t I) const { return Off[I + 1] - Off[I]; }
+};
+using TcBatch = std::vector<std::unique_ptr<TcArena>>;
+struct TcRef {
+  TcArena *A = nullptr;
+  uint32_t I = 0;
+  const uint8_t *data() const { return A->Ptr(I); }
+  size_t size() const { return A->Len(I); }
 };
 
 // The fuzz loop of one node / shard, one batch per Step(): an in-process
@@ -148,12 +180,13 @@ class FuzzSession {
   std::string SummaryJson() const;
 
  private:
-  std::vector<std::string> MakeBatch(uint64_t n);
+  TcBatch MakeBatch(uint64_t n);
+  void Adopt(TcBatch &&B);  // streaming: the batch's testcases join the ready queue
   uint64_t Budget(uint64_t n) const;
   bool More(uint64_t done) const;
   bool MergeCoverage();
   bool StreamStep();
-  void Account(const std::string &Tc, const LaneResult &L);
+  void Account(const uint8_t *Tc, size_t Size, const LaneResult &L);
 
   const RunnerOptions O_;
   Executor_t &Exec_;
@@ -164,17 +197,20 @@ class FuzzSession {
   fs::path T_;
   Corpus_t Corpus_;
   std::unique_ptr<Mutator_t> Mutator_;
-  std::vector<std::string> Pending_, Batch_;
+  std::vector<std::string> Pending_;
+  TcBatch Batch_;                // batch mode: the batch in the lanes
+  std::vector<TcRef> BatchRefs_;
   std::string LastNewCov_;  // the testcase last passed to Mutator_->OnNewCoverage
   bool HaveNewCov_ = false;
-  std::future<std::vector<std::string>> Next_;
+  std::future<TcBatch> Next_;
   std::unordered_set<std::string> CrashNames_;
   FuzzStats S_;
   std::chrono::steady_clock::time_point t0_;
   // streaming (RunnerOptions::slice != 0 on an executor that streams)
   bool stream_ = false;
-  std::deque<std::string> Ready_;                      // mutated, not yet in a lane
-  std::vector<std::string> Slot_;  // tag -> testcase in a lane (tags are slot indices)
+  std::deque<TcRef> Ready_;                                      // mutated, not yet in a lane
+  std::unordered_map<TcArena *, std::unique_ptr<TcArena>> Arenas_;  // owners of Ready_ / Slot_ testcases
+  std::vector<TcRef> Slot_;  // tag -> testcase in a lane (tags are slot indices)
   std::vector<uint64_t> FreeSlot_;
   size_t InFlight_ = 0;
 };

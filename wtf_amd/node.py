@@ -16,7 +16,8 @@ RCCL_ID_BYTES = 128
 class Opts(C.Structure):
     _fields_ = [("name", C.c_char_p), ("target", C.c_char_p), ("lanes", C.c_uint32), ("overlay_pages", C.c_uint32),
                 ("limit", C.c_uint64), ("seed", C.c_uint64), ("max_len", C.c_uint64), ("device", C.c_int32),
-                ("rank", C.c_int32), ("world", C.c_int32), ("rccl_id", C.POINTER(C.c_uint8))]
+                ("rank", C.c_int32), ("world", C.c_int32), ("rccl_id", C.POINTER(C.c_uint8)),
+                ("slice_steps", C.c_uint64), ("regroup_steps", C.c_uint64)]
 
 
 class Stats(C.Structure):
@@ -63,11 +64,12 @@ def rccl_unique_id() -> bytes:
 class Node:
     def __init__(self, name: str, target: str, lanes: int, limit: int, seed: int = 1337, max_len: int = 0x1000,
                  device: int = 0, rank: int = 0, world: int = 1, rccl_id: bytes | None = None,
-                 overlay_pages: int = 0):
+                 overlay_pages: int = 0, slice_steps: int = 0, regroup_steps: int | None = None):
         self.L = lib()
         self._id = (C.c_uint8 * RCCL_ID_BYTES)(*rccl_id) if rccl_id else None
         o = Opts(name.encode(), target.encode(), lanes, overlay_pages, limit, seed, max_len, device, rank, world,
-                 C.cast(self._id, C.POINTER(C.c_uint8)) if self._id is not None else None)
+                 C.cast(self._id, C.POINTER(C.c_uint8)) if self._id is not None else None,
+                 slice_steps, (1 << 64) - 1 if regroup_steps is None else regroup_steps)
         h = C.c_void_p()
         rc = self.L.wtfnode_open(C.byref(o), C.byref(h))
         if rc != 0:
