@@ -149,8 +149,15 @@ int wtfgpu_abi_version(void);
 int wtfgpu_device_count(void);
 int wtfgpu_create(int device, wtfgpu_ctx **out);
 int wtfgpu_destroy(wtfgpu_ctx *ctx);
-/* The HIP stream the context launches on (hipStream_t, as void*). */
+/* The HIP stream the context launches on (hipStream_t, as void*): the
+ * current queue's. */
 void *wtfgpu_stream(wtfgpu_ctx *ctx);
+/* Queues (no bochscpu counterpart: host/GPU overlap). Every later call is
+ * issued on queue `queue` (0 or 1) until the next selection: its own stream
+ * and staging scratch, so a slice queued with wtfgpu_run_async on one queue
+ * runs while the host services lanes on the other. Lane sets driven through
+ * different queues must be disjoint. */
+int wtfgpu_select_queue(wtfgpu_ctx *ctx, uint32_t queue);
 
 /* Snapshot physical memory: npages pages of 4096 bytes, page i backs gpfns[i]. */
 int wtfgpu_load_pool(wtfgpu_ctx *ctx, const uint64_t *gpfns, const uint8_t *pages,
@@ -253,6 +260,11 @@ int wtfgpu_stop(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, uint32_t sta
  * max_steps wave-steps elapse. Blocking. */
 int wtfgpu_run(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, uint64_t max_steps,
                wtfgpu_run_stats_t *stats);
+/* The same for exactly max_steps wave-steps (<= 2^32), queued on the current
+ * queue and returning at once; wtfgpu_run_wait blocks until it is done and
+ * returns its statistics. One run in flight per queue. */
+int wtfgpu_run_async(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, uint64_t max_steps);
+int wtfgpu_run_wait(wtfgpu_ctx *ctx, wtfgpu_run_stats_t *stats);
 
 /* Per-lane memory. gva translation uses the lane's cr3 and its overlays. */
 int wtfgpu_lane_translate(wtfgpu_ctx *ctx, uint32_t lane, uint64_t gva, uint64_t *gpa);

@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 for cfg in ${SWEEP:-65536:0:4096}; do
   IFS=: read L R S <<< "$cfg"
   log=gpurun_out/sw_${L}_${R}_${S}.log
-  timeout -k 10 240 python -u bench.py --steps ${STEPS:-10} --warmup 2 --no-cpu --no-legs --lanes $L --regroup-steps $R --slice-steps $S > $log 2>&1 || { echo FAIL $cfg; tail -20 $log; exit 1; }
+  timeout -k 10 240 python -u bench.py --steps ${STEPS:-20} --warmup 6 --no-cpu --no-legs --lanes $L --regroup-steps $R --slice-steps $S > $log 2>&1 || { echo FAIL $cfg; tail -20 $log; exit 1; }
   tail -1 $log | python -c "
 import json,sys; d=json.loads(sys.stdin.read()); n=d['node']; ns=d['node_timed']; b=ns['backend']
 print('$cfg', round(d['value']), round(d['ms_per_step'],1), round(d.get('lanes_per_wave_step'),1), round(n['kernel_ms'],1), n['kernel_launches'], round(n['insert_ms'],1), round(n['node_ms'],1))

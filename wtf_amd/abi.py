@@ -112,6 +112,9 @@ def load_hip_library(path: str = LIB_PATH) -> C.CDLL:
         "wtfgpu_set_initial_state": ([P, C.POINTER(Regs)], C.c_int),
         "wtfgpu_set_limit": ([P, U64], C.c_int),
         "wtfgpu_set_regroup": ([P, U64], C.c_int),
+        "wtfgpu_select_queue": ([P, U32], C.c_int),
+        "wtfgpu_run_async": ([P, U32, U32, U64], C.c_int),
+        "wtfgpu_run_wait": ([P, C.POINTER(RunStats)], C.c_int),
         "wtfgpu_set_breakpoints": ([P, C.POINTER(U64), U32], C.c_int),
         "wtfgpu_set_breakpoint_actions": ([P, C.POINTER(BpAction), U32], C.c_int),
         "wtfgpu_set_feed": ([P, U32, U32, C.POINTER(U64), C.c_char_p, C.c_char_p, U64], C.c_int),

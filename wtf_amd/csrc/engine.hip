@@ -1364,6 +1364,22 @@ __global__ void k_cov_commit(Dev P, const u64 *rips, u64 n) {
     }                                                                                    \
   } while (0)
 
+// What a queue owns (wtfgpu_select_queue): its stream and the scratch a call
+// on it stages through, so that work queued on one (a k_run slice) runs while
+// the host drives the other.
+struct QueueRes {
+  hipStream_t stream = nullptr;
+  u8 *d_scratch = nullptr;
+  u64 scratch_bytes = 0;
+  u64 *d_stat = nullptr;
+  Dev *d_dev = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  u32 *d_rkeys = nullptr, *d_rkeys2 = nullptr, *d_rlanes = nullptr;
+  void *d_rtemp = nullptr;
+  size_t rtemp_bytes = 0;
+  u32 async_launches = 0;  // wtfgpu_run_async in flight (0 = none)
+};
+
 struct wtfgpu_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -1419,6 +1435,10 @@ struct wtfgpu_ctx {
   u64 scratch_bytes = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   u64 regroup_steps = 0;
+  u32 async_launches = 0;
+  // the current queue's resources live in the members above; the others here
+  QueueRes queues[2];
+  u32 cur_queue = 0;
 };
 
 namespace {
@@ -1448,6 +1468,63 @@ int ensure_scratch(wtfgpu_ctx *c, u64 bytes) {
   if (dalloc(&c->d_scratch, bytes)) return WTFGPU_ERR_OOM;
   c->scratch_bytes = bytes;
   return WTFGPU_OK;
+}
+
+void queue_save(wtfgpu_ctx *c, QueueRes &q) {
+  q.stream = c->stream;
+  q.d_scratch = c->d_scratch;
+  q.scratch_bytes = c->scratch_bytes;
+  q.d_stat = c->d_stat;
+  q.d_dev = c->d_dev;
+  q.ev0 = c->ev0;
+  q.ev1 = c->ev1;
+  q.d_rkeys = c->d_rkeys;
+  q.d_rkeys2 = c->d_rkeys2;
+  q.d_rlanes = c->d_rlanes;
+  q.d_rtemp = c->d_rtemp;
+  q.rtemp_bytes = c->rtemp_bytes;
+  q.async_launches = c->async_launches;
+}
+void queue_load(wtfgpu_ctx *c, const QueueRes &q) {
+  c->stream = q.stream;
+  c->d_scratch = q.d_scratch;
+  c->scratch_bytes = q.scratch_bytes;
+  c->d_stat = q.d_stat;
+  c->d_dev = q.d_dev;
+  c->ev0 = q.ev0;
+  c->ev1 = q.ev1;
+  c->d_rkeys = q.d_rkeys;
+  c->d_rkeys2 = q.d_rkeys2;
+  c->d_rlanes = q.d_rlanes;
+  c->d_rtemp = q.d_rtemp;
+  c->rtemp_bytes = q.rtemp_bytes;
+  c->async_launches = q.async_launches;
+}
+int queue_create(QueueRes &q) {
+  HIPCHK(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreate(&q.ev0));
+  HIPCHK(hipEventCreate(&q.ev1));
+  if (dalloc(&q.d_stat, 16) || dalloc(&q.d_dev, 1)) return WTFGPU_ERR_OOM;
+  return WTFGPU_OK;
+}
+void regroup_free(u32 *&k, u32 *&k2, u32 *&l, void *&t, size_t &tb) {
+  dfree(k);
+  dfree(k2);
+  dfree(l);
+  if (t) (void)hipFree(t);
+  t = nullptr;
+  tb = 0;
+}
+void queue_destroy(QueueRes &q) {
+  if (q.stream) (void)hipStreamSynchronize(q.stream);
+  regroup_free(q.d_rkeys, q.d_rkeys2, q.d_rlanes, q.d_rtemp, q.rtemp_bytes);
+  dfree(q.d_stat);
+  dfree(q.d_dev);
+  dfree(q.d_scratch);
+  if (q.ev0) (void)hipEventDestroy(q.ev0);
+  if (q.ev1) (void)hipEventDestroy(q.ev1);
+  if (q.stream) (void)hipStreamDestroy(q.stream);
+  q = QueueRes{};
 }
 
 u64 hmix(u64 x) {
@@ -1548,11 +1625,11 @@ int wtfgpu_create(int device, wtfgpu_ctx **out) {
       c->P.guc_mask = n - 1;
     }
   }
-  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HIPCHK(hipEventCreate(&c->ev0));
-  HIPCHK(hipEventCreate(&c->ev1));
-  if (dalloc(&c->d_stat, 16) || dalloc(&c->d_init, 1) || dalloc(&c->d_init_full, 1) || dalloc(&c->d_dev, 1))
+  if (queue_create(c->queues[0]) || dalloc(&c->d_init, 1) || dalloc(&c->d_init_full, 1)) {
+    wtfgpu_destroy(c);
     return WTFGPU_ERR_OOM;
+  }
+  queue_load(c, c->queues[0]);
   *out = c;
   return WTFGPU_OK;
 }
@@ -1582,13 +1659,14 @@ static void free_lanes(wtfgpu_ctx *c) {
   dfree(c->d_tlbok);
   dfree(c->d_ovdata);
   dfree(c->d_full);
-  dfree(c->d_rkeys);
-  dfree(c->d_rkeys2);
-  dfree(c->d_rlanes);
   dfree(c->d_perm);
-  if (c->d_rtemp) (void)hipFree(c->d_rtemp);
-  c->d_rtemp = nullptr;
-  c->rtemp_bytes = 0;
+  // regrouping buffers are sized by the lane count: every queue's
+  regroup_free(c->d_rkeys, c->d_rkeys2, c->d_rlanes, c->d_rtemp, c->rtemp_bytes);
+  for (u32 q = 0; q < 2; q++)
+    if (q != c->cur_queue) {
+      QueueRes &Q = c->queues[q];
+      regroup_free(Q.d_rkeys, Q.d_rkeys2, Q.d_rlanes, Q.d_rtemp, Q.rtemp_bytes);
+    }
   dfree(c->d_covrip);
   dfree(c->d_covgen);
   dfree(c->d_lanegen);
@@ -1599,7 +1677,8 @@ static void free_lanes(wtfgpu_ctx *c) {
 int wtfgpu_destroy(wtfgpu_ctx *c) {
   if (!c) return WTFGPU_OK;
   (void)hipSetDevice(c->device);
-  (void)hipStreamSynchronize(c->stream);
+  for (QueueRes &q : c->queues)
+    if (q.stream) (void)hipStreamSynchronize(q.stream);
   free_lanes(c);
   dfree(c->d_guc);
   dfree(c->d_pool);
@@ -1615,14 +1694,10 @@ int wtfgpu_destroy(wtfgpu_ctx *c) {
   dfree(c->d_codeslot);
   dfree(c->d_covmap);
   dfree(c->d_covshadow);
-  dfree(c->d_stat);
   dfree(c->d_init);
   dfree(c->d_init_full);
-  dfree(c->d_dev);
-  dfree(c->d_scratch);
-  if (c->ev0) (void)hipEventDestroy(c->ev0);
-  if (c->ev1) (void)hipEventDestroy(c->ev1);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
+  queue_save(c, c->queues[c->cur_queue]);
+  for (QueueRes &q : c->queues) queue_destroy(q);
   delete c;
   return WTFGPU_OK;
 }
@@ -2191,40 +2266,73 @@ int wtfgpu_stop(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, uint32_t statu
   return set_status_list(c, lanes, n, status, nullptr);
 }
 
+// Regrouping buffers of the current queue (sized by the lane count).
+static int regroup_buffers(wtfgpu_ctx *c) {
+  if (c->d_rkeys) return WTFGPU_OK;
+  const u64 N = c->P.nlanes;
+  if (!c->d_perm && dalloc(&c->d_perm, N)) return WTFGPU_ERR_OOM;
+  if (dalloc(&c->d_rkeys, N) || dalloc(&c->d_rkeys2, N) || dalloc(&c->d_rlanes, N)) return WTFGPU_ERR_OOM;
+  size_t bytes = 0;
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, c->d_rkeys, c->d_rkeys2, c->d_rlanes, c->d_perm, (int)N, 0,
+                                            24, c->stream));
+  HIPCHK(hipMalloc(&c->d_rtemp, bytes));
+  c->rtemp_bytes = bytes;
+  return WTFGPU_OK;
+}
+
+// The kernel parameters of a run on the current queue.
+static Dev run_params(wtfgpu_ctx *c, bool regroup) {
+  Dev Q = c->P;
+  Q.perm = regroup ? c->d_perm : nullptr;
+  Q.stat = c->d_stat;
+  return Q;
+}
+
+// One k_run launch of `steps` wave-steps over [first, first + count), after
+// the regrouping sort when on.
+static int launch_chunk(wtfgpu_ctx *c, const Dev &Q, u32 first, u32 count, u64 steps, bool regroup) {
+  const u32 hwaves = (count + c->P.lpw - 1) / c->P.lpw;
+  if (regroup) {
+    k_regroup_keys<<<(count + 255) / 256, 256, 0, c->stream>>>(c->P, first, count, c->d_rkeys, c->d_rlanes);
+    HIPCHK(hipGetLastError());
+    size_t bytes = c->rtemp_bytes;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(c->d_rtemp, bytes, c->d_rkeys, c->d_rkeys2, c->d_rlanes,
+                                              c->d_perm + first, (int)count, 0, 24, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_stat + 2, 0, 8, c->stream));  // running lanes: the last launch's count
+  }
+#if WTFGPU_P_BYREF
+  k_run<<<(hwaves + 3) / 4, 256, 0, c->stream>>>(c->d_dev, first, count, steps);
+#else
+  k_run<<<(hwaves + 3) / 4, 256, 0, c->stream>>>(Q, first, count, steps);
+#endif
+  HIPCHK(hipGetLastError());
+  return WTFGPU_OK;
+}
+
 int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps, wtfgpu_run_stats_t *stats) {
   if (!lanes_ok(c, first, count) || (first % c->P.lpw)) return WTFGPU_ERR_INVALID;
   if (!c->P.pool) return WTFGPU_ERR_STATE;
+  if (c->async_launches) return WTFGPU_ERR_STATE;  // wtfgpu_run_wait first
   HIPCHK(hipSetDevice(c->device));
   wtfgpu_run_stats_t st{};
   u64 chunk = 1ull << 20;  // wave-steps per launch: keeps every launch short
   // Cross-wave regrouping: launches of `regroup` wave-steps, between them the
   // lanes are sorted by rip so that lanes that diverged from their wave
-  // neighbours meet lanes at the same rip in another wave (WTFGPU_REGROUP_STEPS
-  // sets it, 0 = fixed lane order).
+  // neighbours meet lanes at the same rip in another wave (wtfgpu_set_regroup,
+  // WTFGPU_REGROUP_STEPS; 0 = fixed lane order).
   u64 regroup = c->regroup_steps;
   if (count < 2 * c->P.lpw) regroup = 0;
   if (regroup) {
     chunk = regroup;
-    if (!c->d_perm) {
-      const u64 N = c->P.nlanes;
-      if (dalloc(&c->d_rkeys, N) || dalloc(&c->d_rkeys2, N) || dalloc(&c->d_rlanes, N) || dalloc(&c->d_perm, N))
-        return WTFGPU_ERR_OOM;
-      size_t bytes = 0;
-      HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, c->d_rkeys, c->d_rkeys2, c->d_rlanes, c->d_perm,
-                                                (int)N, 0, 24, c->stream));
-      HIPCHK(hipMalloc(&c->d_rtemp, bytes));
-      c->rtemp_bytes = bytes;
-    }
+    if (int rc = regroup_buffers(c)) return rc;
   }
-  Dev Q = c->P;
-  Q.perm = regroup ? c->d_perm : nullptr;
+  const Dev Q = run_params(c, regroup != 0);
 #if WTFGPU_P_BYREF
   HIPCHK(hipMemcpyAsync(c->d_dev, &Q, sizeof(Dev), hipMemcpyHostToDevice, c->stream));
 #endif
   // launches per host synchronisation: regrouped chunks are short, so a
   // group of them is queued at once (one stats read-back per group)
   const u32 group = regroup ? (u32)std::max<u64>(1, 1024 / regroup) : 1;
-  const u32 hwaves = (count + c->P.lpw - 1) / c->P.lpw;
   u64 done = 0;
   float ms_total = 0;
   for (;;) {
@@ -2233,20 +2341,7 @@ int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps
     u32 k = 0;
     for (; k < group && done < max_steps; k++) {
       const u64 steps = std::min<u64>(chunk, max_steps - done);
-      if (regroup) {
-        k_regroup_keys<<<(count + 255) / 256, 256, 0, c->stream>>>(c->P, first, count, c->d_rkeys, c->d_rlanes);
-        HIPCHK(hipGetLastError());
-        size_t bytes = c->rtemp_bytes;
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(c->d_rtemp, bytes, c->d_rkeys, c->d_rkeys2, c->d_rlanes,
-                                                  c->d_perm + first, (int)count, 0, 24, c->stream));
-        HIPCHK(hipMemsetAsync(c->d_stat + 2, 0, 8, c->stream));  // running lanes: the last launch's count
-      }
-#if WTFGPU_P_BYREF
-      k_run<<<(hwaves + 3) / 4, 256, 0, c->stream>>>(c->d_dev, first, count, steps);
-#else
-      k_run<<<(hwaves + 3) / 4, 256, 0, c->stream>>>(Q, first, count, steps);
-#endif
-      HIPCHK(hipGetLastError());
+      if (int rc = launch_chunk(c, Q, first, count, steps, regroup != 0)) return rc;
       done += steps;
     }
     HIPCHK(hipEventRecord(c->ev1, c->stream));
@@ -2270,6 +2365,65 @@ int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps
   }
   st.kernel_ms = ms_total;
   if (stats) *stats = st;
+  return WTFGPU_OK;
+}
+
+int wtfgpu_run_async(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps) {
+  if (!lanes_ok(c, first, count) || (first % c->P.lpw) || max_steps == 0 || max_steps > (1ull << 32))
+    return WTFGPU_ERR_INVALID;
+  if (!c->P.pool) return WTFGPU_ERR_STATE;
+  if (c->async_launches) return WTFGPU_ERR_STATE;
+  HIPCHK(hipSetDevice(c->device));
+  u64 regroup = c->regroup_steps;
+  if (count < 2 * c->P.lpw) regroup = 0;
+  const u64 chunk = regroup ? regroup : max_steps;
+  if (regroup)
+    if (int rc = regroup_buffers(c)) return rc;
+  const Dev Q = run_params(c, regroup != 0);
+#if WTFGPU_P_BYREF
+  HIPCHK(hipMemcpyAsync(c->d_dev, &Q, sizeof(Dev), hipMemcpyHostToDevice, c->stream));
+#endif
+  HIPCHK(hipMemsetAsync(c->d_stat, 0, 16 * 8, c->stream));
+  HIPCHK(hipEventRecord(c->ev0, c->stream));
+  u32 k = 0;
+  for (u64 done = 0; done < max_steps; done += chunk, k++) {
+    if (int rc = launch_chunk(c, Q, first, count, std::min<u64>(chunk, max_steps - done), regroup != 0)) return rc;
+  }
+  HIPCHK(hipEventRecord(c->ev1, c->stream));
+  c->async_launches = k;
+  return WTFGPU_OK;
+}
+
+int wtfgpu_run_wait(wtfgpu_ctx *c, wtfgpu_run_stats_t *stats) {
+  if (!c) return WTFGPU_ERR_INVALID;
+  wtfgpu_run_stats_t st{};
+  if (c->async_launches) {
+    HIPCHK(hipSetDevice(c->device));
+    u64 s[16];
+    HIPCHK(hipMemcpyAsync(s, c->d_stat, sizeof(s), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    st.kernel_launches = c->async_launches;
+    st.group_steps = s[0];
+    st.lane_retired = s[1];
+    st.kernel_ms = ms;
+    c->async_launches = 0;
+  }
+  if (stats) *stats = st;
+  return WTFGPU_OK;
+}
+
+int wtfgpu_select_queue(wtfgpu_ctx *c, uint32_t queue) {
+  if (!c || queue >= 2) return WTFGPU_ERR_INVALID;
+  if (queue == c->cur_queue) return WTFGPU_OK;
+  HIPCHK(hipSetDevice(c->device));
+  QueueRes &next = c->queues[queue];
+  if (!next.stream)
+    if (int rc = queue_create(next)) return rc;
+  queue_save(c, c->queues[c->cur_queue]);
+  queue_load(c, next);
+  c->cur_queue = queue;
   return WTFGPU_OK;
 }
 

@@ -53,7 +53,8 @@ int gpr_index(Registers_t r) {
 
 GpuBackend_t::GpuBackend_t() = default;
 GpuBackend_t::~GpuBackend_t() {
-  if (feed_pin_) wtfgpu_host_free(ctx_, feed_pin_);
+  for (Part &P : parts_)
+    if (P.pin) wtfgpu_host_free(ctx_, P.pin);
   if (ctx_) wtfgpu_destroy(ctx_);
 }
 
@@ -585,106 +586,121 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
   return rc;
 }
 
+// One round's exits: each pending lane that is not done is classified (a
+// result, or a breakpoint hit for the host, or still running).
+void GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first, const std::vector<wtfgpu_exit_t> &ex,
+                            std::vector<uint8_t> &done, std::vector<LaneResult> *out, std::vector<uint32_t> &hits) {
+  std::vector<uint8_t> hit(pending.size(), 0);
+#pragma omp parallel for schedule(static, 1024) if (pending.size() >= 8192)
+  for (size_t pi = 0; pi < pending.size(); pi++) {
+    const uint32_t l = pending[pi];
+    if (done[l - first]) continue;
+    const wtfgpu_exit_t &e = ex[l - first];
+    LaneView &v = views_[l];
+    switch (e.status) {
+      case WTFGPU_EXIT_BREAKPOINT: hit[pi] = 1; continue;
+      case WTFGPU_RUNNING: continue;  // sliced: still running when the slice ended
+      case WTFGPU_EXIT_TIMEOUT: v.result = Timedout_t(); break;    // bochscpu_backend.cc:458-469
+      case WTFGPU_EXIT_INT3:                                         // :595-619
+      case WTFGPU_EXIT_HLT: v.result = Crash_t(); break;             // :690-697
+      case WTFGPU_EXIT_CR3: v.result = Cr3Change_t(); break;         // :628-657
+      case WTFGPU_EXIT_FAULT: v.result = FaultToResult(e.vector, e.error, e.rip, e.addr, e.opcode); break;
+      case WTFGPU_EXIT_STOPPED: break;
+      case WTFGPU_EXIT_STOP_OK: v.result = Ok_t(); break;           // device Feed action: Stop(Ok_t())
+      default:
+        // unimplemented opcode / overlay full / a device Feed write that
+        // failed: the engine cannot finish the testcase. Not a target bug:
+        // flagged as an engine error, with an unnamed Crash_t (which no
+        // master saves, server.h:861-877) as its result
+        if (out) (*out)[l].error = true;
+        if (!v.result) v.result = Crash_t();
+        break;
+    }
+    done[l - first] = 1;
+  }
+  for (size_t pi = 0; pi < pending.size(); pi++)
+    if (hit[pi]) hits.push_back(pending[pi]);
+}
+
+// Final state of every finished lane (`ex` holds the last round's exits of
+// every lane: a lane is final once it is done).
+bool GpuBackend_t::fill_results(const std::vector<uint32_t> &lanes, uint32_t first,
+                                const std::vector<wtfgpu_exit_t> &ex, const std::vector<uint8_t> &done,
+                                std::vector<LaneResult> *out, std::vector<uint32_t> *finished) {
+  const auto tg = Clock::now();
+  std::vector<uint32_t> fin;
+  for (uint32_t l : lanes)
+    if (done[l - first]) fin.push_back(l);
+  if (finished) finished->insert(finished->end(), fin.begin(), fin.end());
+  if (!out) return true;
+  std::vector<uint64_t> regs;
+  if (want_gprs_) {  // run mode prints them; the fuzz loop never reads them
+    regs.resize(fin.size() * 18);
+    if (!fin.empty() && wtfgpu_read_gprs_list(ctx_, fin.data(), (uint32_t)fin.size(), regs.data())) return false;
+  }
+#pragma omp parallel for schedule(static, 1024) if (fin.size() >= 8192)
+  for (size_t i = 0; i < fin.size(); i++) {
+    LaneResult &r = (*out)[fin[i]];
+    const LaneView &v = views_[fin[i]];
+    r.result = v.result ? *v.result : TestcaseResult_t(Ok_t());
+    if (want_gprs_) {
+      memcpy(r.gprs, &regs[i * 18], 18 * 8);
+      r.rip = r.gprs[16];
+    } else {
+      r.rip = ex[fin[i] - first].rip;
+    }
+    r.icount = ex[fin[i] - first].icount;
+    r.exit_status = ex[fin[i] - first].status;
+  }
+  stats_.regs_ms += ms_since(tg);
+  return true;
+}
+
+// Lanes InsertTestcase stopped never run: marked STOPPED on the device, so
+// the next classification gives them their result.
+bool GpuBackend_t::stop_prestopped(const std::vector<uint32_t> &lanes) {
+  std::vector<uint32_t> pre;
+  for (uint32_t l : lanes)
+    if (views_[l].result) pre.push_back(l);
+  return pre.empty() || wtfgpu_stop(ctx_, pre.data(), (uint32_t)pre.size(), WTFGPU_EXIT_STOPPED) == WTFGPU_OK;
+}
+
 // The run loop over `lanes` (ascending): launch, classify exits, service
 // breakpoint hits on the host, resume; until every lane has a result.
 bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<LaneResult> *out, ModuleSlots *slots,
-                             bool per_lane_state, uint64_t slice, std::vector<uint32_t> *finished) {
+                             bool per_lane_state) {
   if (lanes.empty()) return true;
-  const bool sliced = finished != nullptr;  // one slice of `slice` wave-steps, then return
   const uint32_t first = lanes.front() & ~63u, count = lanes.back() + 1 - first;
   std::vector<wtfgpu_exit_t> ex(count);
   std::vector<uint8_t> done(count, 0);
   std::vector<uint32_t> pending = lanes;
-  // lanes stopped before running (InsertTestcase called Stop)
-  std::vector<uint32_t> pre_stopped;
-  for (uint32_t l : lanes)
-    if (views_[l].result) pre_stopped.push_back(l);
-  if (!pre_stopped.empty()) wtfgpu_stop(ctx_, pre_stopped.data(), (uint32_t)pre_stopped.size(), WTFGPU_EXIT_STOPPED);
-  for (uint32_t l : pre_stopped) done[l - first] = 1;
-
+  if (!stop_prestopped(lanes)) return false;
   for (;;) {
     wtfgpu_run_stats_t rs{};
     const auto tk = Clock::now();
-    if (wtfgpu_run(ctx_, first, count, sliced ? slice : ~0ull, &rs)) return false;
+    if (wtfgpu_run(ctx_, first, count, ~0ull, &rs)) return false;
     const auto te = Clock::now();
     stats_.run_ms += std::chrono::duration<double, std::milli>(te - tk).count();
-    stats_.kernel_launches += rs.kernel_launches;
-    stats_.kernel_ms += rs.kernel_ms;
-    stats_.retired += rs.lane_retired;
-    stats_.group_steps += rs.group_steps;
-    stats_.rounds++;
+    account_run(rs);
     if (wtfgpu_read_exits(ctx_, first, count, ex.data())) return false;
     std::vector<uint32_t> hits;
-    std::vector<uint8_t> hit(pending.size(), 0);
-#pragma omp parallel for schedule(static, 1024) if (pending.size() >= 8192)
-    for (size_t pi = 0; pi < pending.size(); pi++) {
-      const uint32_t l = pending[pi];
-      if (done[l - first]) continue;
-      const wtfgpu_exit_t &e = ex[l - first];
-      LaneView &v = views_[l];
-      switch (e.status) {
-        case WTFGPU_EXIT_BREAKPOINT: hit[pi] = 1; continue;
-        case WTFGPU_RUNNING: continue;  // sliced: still running when the slice ended
-        case WTFGPU_EXIT_TIMEOUT: v.result = Timedout_t(); break;    // bochscpu_backend.cc:458-469
-        case WTFGPU_EXIT_INT3:                                         // :595-619
-        case WTFGPU_EXIT_HLT: v.result = Crash_t(); break;             // :690-697
-        case WTFGPU_EXIT_CR3: v.result = Cr3Change_t(); break;         // :628-657
-        case WTFGPU_EXIT_FAULT: v.result = FaultToResult(e.vector, e.error, e.rip, e.addr, e.opcode); break;
-        case WTFGPU_EXIT_STOPPED: break;
-        case WTFGPU_EXIT_STOP_OK: v.result = Ok_t(); break;           // device Feed action: Stop(Ok_t())
-        default:
-          // unimplemented opcode / overlay full / a device Feed write that
-          // failed: the engine cannot finish the testcase. Not a target bug:
-          // flagged as an engine error, with an unnamed Crash_t (which no
-          // master saves, server.h:861-877) as its result
-          if (out) (*out)[l].error = true;
-          if (!v.result) v.result = Crash_t();
-          break;
-      }
-      done[l - first] = 1;
-    }
-    for (size_t pi = 0; pi < pending.size(); pi++)
-      if (hit[pi]) hits.push_back(pending[pi]);
+    classify(pending, first, ex, done, out, hits);
     stats_.exits_ms += ms_since(te);
     if (hits.empty()) break;
     if (!service_hits(hits, first, done, slots, per_lane_state)) return false;
-    if (sliced) break;  // the serviced lanes resume in the next slice
     pending.clear();
     for (uint32_t l : hits)
       if (!done[l - first]) pending.push_back(l);
   }
-  if (finished)
-    for (uint32_t l : lanes)
-      if (done[l - first]) finished->push_back(l);
-  // final state of every finished lane (`ex` holds the last round's exits of
-  // every lane: a lane is final once it is done)
-  if (out) {
-    const auto tg = Clock::now();
-    std::vector<uint32_t> fin;
-    for (uint32_t l : lanes)
-      if (done[l - first]) fin.push_back(l);
-    std::vector<uint64_t> regs;
-    if (want_gprs_) {  // run mode prints them; the fuzz loop never reads them
-      regs.resize(fin.size() * 18);
-      if (!fin.empty() && wtfgpu_read_gprs_list(ctx_, fin.data(), (uint32_t)fin.size(), regs.data())) return false;
-    }
-#pragma omp parallel for schedule(static, 1024) if (fin.size() >= 8192)
-    for (size_t i = 0; i < fin.size(); i++) {
-      LaneResult &r = (*out)[fin[i]];
-      const LaneView &v = views_[fin[i]];
-      r.result = v.result ? *v.result : TestcaseResult_t(Ok_t());
-      if (want_gprs_) {
-        memcpy(r.gprs, &regs[i * 18], 18 * 8);
-        r.rip = r.gprs[16];
-      } else {
-        r.rip = ex[fin[i] - first].rip;
-      }
-      r.icount = ex[fin[i] - first].icount;
-      r.exit_status = ex[fin[i] - first].status;
-    }
-    stats_.regs_ms += ms_since(tg);
-  }
-  return true;
+  return fill_results(lanes, first, ex, done, out, nullptr);
+}
+
+void GpuBackend_t::account_run(const wtfgpu_run_stats_t &rs) {
+  stats_.kernel_launches += rs.kernel_launches;
+  stats_.kernel_ms += rs.kernel_ms;
+  stats_.retired += rs.lane_retired;
+  stats_.group_steps += rs.group_steps;
+  stats_.rounds++;
 }
 
 // Services one round's breakpoint hits on the host (BeforeExecutionHook,
@@ -1106,36 +1122,63 @@ void GpuBackend_t::collect_coverage(const std::vector<uint32_t> &lanes, std::vec
 }
 
 uint32_t GpuBackend_t::FreeLanes() const {
-  if (busy_.empty()) return nlanes_;
+  if (busy_.empty()) return parts_n() > 1 ? nlanes_ / 2 : nlanes_;
+  const Part &P = parts_[next_part_];
+  if (P.launched) return P.hi - P.lo;  // its running lanes may all finish: an upper bound
   uint32_t n = 0;
-  for (uint8_t b : busy_) n += !b;
+  for (uint32_t l = P.lo; l < P.hi; l++) n += !busy_[l];
   return n;
 }
 
-// One streaming step: new testcases into free lanes (device reset of those
-// lanes + InsertTestcase + uploads), one slice over every occupied lane with
-// breakpoints serviced, then the finished lanes are harvested (results,
-// coverage attribution in lane order, Target.Restore) and freed.
+// Streaming parts: one (every lane, synchronous) or two halves on their own
+// queues, pipelined: StreamStep harvests and refills one half while the
+// other half's slice runs on the GPU (WTFGPU_STREAM_PARTS=1 turns it off).
+uint32_t GpuBackend_t::parts_n() const {
+  if (!parts_.empty()) return (uint32_t)parts_.size();
+  const char *e = getenv("WTFGPU_STREAM_PARTS");
+  const uint32_t want = e ? (uint32_t)atoi(e) : 2;
+  return (want >= 2 && nlanes_ >= 256 && nlanes_ % 128 == 0) ? 2 : 1;
+}
+
+// One streaming step on the next part: its finished slice is harvested (when
+// pipelined), its free lanes get testcases from `In` (restore +
+// InsertTestcase + uploads), and its occupied lanes start one slice of
+// `Slice` wave-steps (without the pipeline: harvested in the same call).
 bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTestcase_t> &In, uint64_t Slice,
-                              std::vector<StreamResult_t> &Out, ModuleSlots *Slots) {
+                              std::vector<StreamResult_t> &Out, ModuleSlots *Slots, size_t *Taken) {
   const auto t0 = Clock::now();
+  if (Taken) *Taken = 0;
   if (busy_.empty()) {
     busy_.assign(nlanes_, 0);
     tag_.assign(nlanes_, 0);
     lres_.assign(nlanes_, LaneResult{});
+    const uint32_t n = parts_n();
+    parts_.assign(n, Part{});
+    for (uint32_t p = 0; p < n; p++) {
+      parts_[p].lo = (uint32_t)((uint64_t)nlanes_ * p / n);
+      parts_[p].hi = (uint32_t)((uint64_t)nlanes_ * (p + 1) / n);
+    }
     // every lane idle until it gets a testcase
     std::vector<uint32_t> all(nlanes_);
     for (uint32_t l = 0; l < nlanes_; l++) all[l] = l;
     if (wtfgpu_stop(ctx_, all.data(), nlanes_, WTFGPU_EXIT_IDLE)) return false;
   }
+  const bool pipelined = parts_.size() > 1;
+  const uint32_t pi = next_part_;
+  next_part_ = (next_part_ + 1) % (uint32_t)parts_.size();
+  Part &P = parts_[pi];
+  if (pipelined && wtfgpu_select_queue(ctx_, pi)) return false;
+  if (pipelined && P.launched && !harvest_part(P, Target, Out, Slots)) return false;
+  const auto ti = Clock::now();
   // ---- refill
   std::vector<uint32_t> fresh;
   std::vector<std::pair<const uint8_t *, size_t>> tcs;
-  for (uint32_t l = 0; l < nlanes_ && fresh.size() < In.size(); l++)
+  for (uint32_t l = P.lo; l < P.hi && fresh.size() < In.size(); l++)
     if (!busy_[l]) {
       fresh.push_back(l);
       tcs.push_back({In[fresh.size() - 1].data, In[fresh.size() - 1].size});
     }
+  if (Taken) *Taken = fresh.size();
   if (!fresh.empty()) {
     if (wtfgpu_restore_lanes(ctx_, fresh.data(), (uint32_t)fresh.size())) return false;
 #pragma omp parallel for schedule(static)
@@ -1147,7 +1190,7 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
       lres_[l] = LaneResult{};
     }
     const auto tm = Clock::now();
-    stats_.restore_ms += std::chrono::duration<double, std::milli>(tm - t0).count();
+    stats_.restore_ms += std::chrono::duration<double, std::milli>(tm - ti).count();
     std::vector<uint8_t> ok;
     insert_lanes(Target, fresh, tcs, Slots, ok);
     for (size_t i = 0; i < fresh.size(); i++)
@@ -1164,38 +1207,66 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
         off[i + 1] = off[i] + v.feed.size();
         has[i] = v.has_feed;
       }
-      // packed into a pinned buffer on all host threads: one DMA to the device
-      if (off[n] > feed_pin_cap_) {
-        if (feed_pin_) wtfgpu_host_free(ctx_, feed_pin_);
-        feed_pin_ = nullptr;
-        feed_pin_cap_ = std::max<uint64_t>(off[n] * 2, 1 << 20);
+      // packed into the part's pinned buffer on all host threads: one DMA
+      if (off[n] > P.pin_cap) {
+        if (P.pin) wtfgpu_host_free(ctx_, P.pin);
+        P.pin = nullptr;
+        P.pin_cap = std::max<uint64_t>(off[n] * 2, 1 << 20);
         void *p = nullptr;
-        if (wtfgpu_host_alloc(ctx_, feed_pin_cap_, &p)) return false;
-        feed_pin_ = (uint8_t *)p;
+        if (wtfgpu_host_alloc(ctx_, P.pin_cap, &p)) return false;
+        P.pin = (uint8_t *)p;
       }
 #pragma omp parallel for schedule(static, 256)
       for (size_t i = 0; i < n; i++) {
         const LaneView &v = views_[fresh[i]];
-        if (!v.feed.empty()) memcpy(feed_pin_ + off[i], v.feed.data(), v.feed.size());
+        if (!v.feed.empty()) memcpy(P.pin + off[i], v.feed.data(), v.feed.size());
       }
-      if (wtfgpu_set_feed_lanes(ctx_, fresh.data(), (uint32_t)n, off.data(), has.data(), feed_pin_, off[n]))
+      if (wtfgpu_set_feed_lanes(ctx_, fresh.data(), (uint32_t)n, off.data(), has.data(), P.pin, off[n]))
         return false;
     }
+    if (!stop_prestopped(fresh)) return false;
     stats_.upload_ms += ms_since(tu);
     stats_.testcases += fresh.size();
   }
-  stats_.insert_ms += ms_since(t0);
-  // ---- one slice over the occupied lanes
-  std::vector<uint32_t> occupied, finished;
-  for (uint32_t l = 0; l < nlanes_; l++)
-    if (busy_[l]) occupied.push_back(l);
-  if (occupied.empty()) return true;
-  if (!run_lanes(occupied, &lres_, Slots, Slots != nullptr, Slice, &finished)) return false;
-  if (finished.empty()) {
-    stats_.total_ms += ms_since(t0);
-    return true;
+  stats_.insert_ms += ms_since(ti);
+  // ---- one slice over the part's occupied lanes
+  P.occ.clear();
+  for (uint32_t l = P.lo; l < P.hi; l++)
+    if (busy_[l]) P.occ.push_back(l);
+  if (!P.occ.empty()) {
+    const auto tk = Clock::now();
+    if (wtfgpu_run_async(ctx_, P.lo, P.hi - P.lo, Slice ? Slice : 4096)) return false;
+    stats_.run_ms += ms_since(tk);
+    P.launched = true;
+    if (!pipelined && !harvest_part(P, Target, Out, Slots)) return false;
   }
-  // ---- harvest
+  stats_.total_ms += ms_since(t0);
+  return true;
+}
+
+// The part's slice: wait for it, classify the exits, service breakpoint hits
+// (those lanes resume in the next slice), and harvest the finished lanes
+// (results, coverage attribution in lane order, Target.Restore).
+bool GpuBackend_t::harvest_part(Part &P, const Target_t &Target, std::vector<StreamResult_t> &Out,
+                                ModuleSlots *Slots) {
+  const auto tw = Clock::now();
+  wtfgpu_run_stats_t rs{};
+  if (wtfgpu_run_wait(ctx_, &rs)) return false;
+  const auto te = Clock::now();
+  stats_.run_ms += std::chrono::duration<double, std::milli>(te - tw).count();
+  account_run(rs);
+  P.launched = false;
+  const uint32_t first = P.lo, count = P.hi - P.lo;
+  if (P.ex.size() < count) P.ex.resize(count);
+  if (wtfgpu_read_exits(ctx_, first, count, P.ex.data())) return false;
+  std::vector<uint8_t> done(count, 0);
+  std::vector<uint32_t> hits;
+  classify(P.occ, first, P.ex, done, &lres_, hits);
+  stats_.exits_ms += ms_since(te);
+  if (!hits.empty() && !service_hits(hits, first, done, Slots, Slots != nullptr)) return false;
+  std::vector<uint32_t> finished;
+  if (!fill_results(P.occ, first, P.ex, done, &lres_, &finished)) return false;
+  if (finished.empty()) return true;
   const auto tc = Clock::now();
   {
     uint32_t lo = finished.front() & ~63u, hi = finished.back() + 1;
@@ -1219,7 +1290,6 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
     busy_[l] = 0;
     // not runnable until refilled (a finished lane keeps its exit status)
   }
-  stats_.total_ms += ms_since(t0);
   stats_.batches++;
   return true;
 }

@@ -94,7 +94,7 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   bool CanStream() const override { return true; }
   uint32_t FreeLanes() const override;
   bool StreamStep(const Target_t &Target, const std::vector<StreamTestcase_t> &In, uint64_t Slice,
-                  std::vector<StreamResult_t> &Out, ModuleSlots *Slots) override;
+                  std::vector<StreamResult_t> &Out, ModuleSlots *Slots, size_t *Taken) override;
   void ResetCoverage() override;
   void SetFullCoverage(bool On) override { full_coverage_ = On; }
   void SetWantRegisters(bool On) override { want_gprs_ = On; }
@@ -163,10 +163,15 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   void drop_staged(LaneView &v) const;
   bool in_overlay(const LaneView &v, uint64_t gpfn) const;
   int flush_lanes(const std::vector<uint32_t> &lanes);
-  // until every lane has a result; or, with `finished`, one slice of `slice`
-  // wave-steps (finished lanes appended to it, the others keep running)
+  // until every lane has a result
   bool run_lanes(const std::vector<uint32_t> &lanes, std::vector<LaneResult> *out, ModuleSlots *slots,
-                 bool per_lane_state, uint64_t slice = ~0ull, std::vector<uint32_t> *finished = nullptr);
+                 bool per_lane_state);
+  void classify(const std::vector<uint32_t> &pending, uint32_t first, const std::vector<wtfgpu_exit_t> &ex,
+                std::vector<uint8_t> &done, std::vector<LaneResult> *out, std::vector<uint32_t> &hits);
+  bool fill_results(const std::vector<uint32_t> &lanes, uint32_t first, const std::vector<wtfgpu_exit_t> &ex,
+                    const std::vector<uint8_t> &done, std::vector<LaneResult> *out, std::vector<uint32_t> *finished);
+  bool stop_prestopped(const std::vector<uint32_t> &lanes);
+  void account_run(const wtfgpu_run_stats_t &rs);
   bool service_hits(const std::vector<uint32_t> &hits, uint32_t first, std::vector<uint8_t> &done, ModuleSlots *slots,
                     bool per_lane_state);
   // InsertTestcase for `lanes` (restored views), module state per lane, on all
@@ -185,8 +190,20 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   std::vector<uint64_t> cov_rips_;
   bool cov_ovf_warned_ = false;
   bool want_gprs_ = true;
-  uint8_t *feed_pin_ = nullptr;  // pinned staging of streamed feeds
-  uint64_t feed_pin_cap_ = 0;
+  // streaming parts (see parts_n): lane range, slice in flight, its occupied
+  // lanes, exit read-back, pinned staging of the part's feeds
+  struct Part {
+    uint32_t lo = 0, hi = 0;
+    bool launched = false;
+    std::vector<uint32_t> occ;
+    std::vector<wtfgpu_exit_t> ex;
+    uint8_t *pin = nullptr;
+    uint64_t pin_cap = 0;
+  };
+  std::vector<Part> parts_;
+  uint32_t next_part_ = 0;
+  uint32_t parts_n() const;
+  bool harvest_part(Part &P, const Target_t &Target, std::vector<StreamResult_t> &Out, ModuleSlots *Slots);
   void finish_coverage(uint32_t n, std::vector<LaneResult> *out, std::vector<uint32_t> *timedout);
   bool set_code_pages();
 

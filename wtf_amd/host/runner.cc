@@ -240,10 +240,12 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
           In.push_back(StreamTestcase_t{Bufs[next].data(), Bufs[next].size(), next});
         }
         std::vector<StreamResult_t> R;
-        if (!Exec.StreamStep(*Target, In, O.slice ? O.slice : 4096, R, &Slots)) {
+        size_t Taken = 0;
+        if (!Exec.StreamStep(*Target, In, O.slice ? O.slice : 4096, R, &Slots, &Taken)) {
           printf("StreamStep failed\n");
           return 1;
         }
+        next -= In.size() - Taken;  // offered again next step
         for (StreamResult_t &F : R) {
           Res[F.tag] = std::move(F.r);
           Got[F.tag] = 1;
@@ -513,8 +515,16 @@ bool FuzzSession::StreamStep() {
   std::vector<StreamResult_t> Out;
   const auto tb = Clock::now();
   S_.fill_ms += std::chrono::duration<double, std::milli>(tb - t_step).count();
-  const bool ok = Exec_.StreamStep(Target_, In, O_.slice, Out, &Slots_);
+  size_t Taken = 0;
+  const bool ok = Exec_.StreamStep(Target_, In, O_.slice, Out, &Slots_, &Taken);
   S_.run_s += secs_since(tb);
+  // testcases the executor did not take go back to the front of the queue
+  for (size_t i = In.size(); i-- > Taken;) {
+    Ready_.push_front(Slot_[In[i].tag]);
+    Slot_[In[i].tag] = TcRef{};
+    FreeSlot_.push_back(In[i].tag);
+    InFlight_--;
+  }
   const auto tw = Clock::now();
   if (Next_.valid()) Adopt(Next_.get());  // before the corpus / mutator change below
   const auto ta = Clock::now();

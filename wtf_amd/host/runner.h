@@ -45,13 +45,16 @@ struct StreamResult_t {
 class Executor_t {
  public:
   // ---- streaming (continuous batching): lanes are slots. StreamStep puts
-  // testcases into free lanes (at most FreeLanes()), runs every occupied lane
-  // for one slice of `Slice` wave-steps and returns the testcases that
-  // finished, in lane order. A testcase's data is only read during the call.
+  // testcases into free lanes (In[0, *Taken): at most FreeLanes(), which is
+  // an upper bound), runs occupied lanes for one slice of `Slice` wave-steps
+  // and returns the testcases that finished, in lane order. A testcase's data
+  // is only read during the call. (A pipelined executor returns a slice's
+  // results one call later: its lanes run while the host serves others.)
   virtual bool CanStream() const { return false; }
   virtual uint32_t FreeLanes() const { return 0; }
   virtual bool StreamStep(const Target_t &, const std::vector<StreamTestcase_t> &, uint64_t,
-                          std::vector<StreamResult_t> &, ModuleSlots *) {
+                          std::vector<StreamResult_t> &, ModuleSlots *, size_t *Taken) {
+    if (Taken) *Taken = 0;
     return false;
   }
 
