@@ -67,7 +67,7 @@ TARGETS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=6)
     ap.add_argument("--lanes", type=int, default=65536)
     ap.add_argument("--slice-steps", type=int, default=0, help="wave-steps per streaming slice (0: the node's 4096)")

@@ -69,7 +69,7 @@ enum wtfgpu_status {
   WTFGPU_EXIT_OVERLAY_FULL = 8, /* lane ran out of copy-on-write pages */
   WTFGPU_EXIT_STOPPED = 9,    /* host called Stop(); result kept on the host */
   WTFGPU_EXIT_IDLE = 10,      /* lane holds no testcase */
-  WTFGPU_EXIT_STOP_OK = 11,   /* a device FEED action found the lane's feed drained: Stop(Ok_t()) */
+  WTFGPU_EXIT_STOP_OK = 11,   /* a device action stopped the lane with Ok_t() (feed drained, STOP_OK) */
   WTFGPU_EXIT_FEED_FAULT = 12 /* a device FEED action could not write its chunk (engine error) */
 };
 
@@ -198,6 +198,14 @@ enum wtfgpu_bp_action_kind {
    * and the hooked instruction runs (fuzzer_tlv_server.cc:83-166). A lane
    * without a feed exits to the host handler. */
   WTFGPU_BPACT_FEED = 3,
+  /* gpr[gprs[0]] = Rdrand(): the lane's BLAKE3 chain (h = blake3(le64(seed))
+   * [0..16), seed = h[0..8), value = h[8..16); bochscpu_backend.cc:874-885),
+   * seed reset to the initial state's at restore; rip is kept and the hooked
+   * instruction runs (fuzzer_hevd.cc:96-108). */
+  WTFGPU_BPACT_RDRAND = 4,
+  /* Stop(Ok_t()): the lane exits with WTFGPU_EXIT_STOP_OK (a handler that
+   * only ends the testcase, fuzzer_hevd.cc:64-73) */
+  WTFGPU_BPACT_STOP_OK = 5,
 };
 typedef struct wtfgpu_bp_action {
   uint64_t gva;
@@ -207,6 +215,10 @@ typedef struct wtfgpu_bp_action {
   uint64_t gprs[17];
 } wtfgpu_bp_action_t;
 int wtfgpu_set_breakpoint_actions(wtfgpu_ctx *ctx, const wtfgpu_bp_action_t *acts, uint32_t n);
+/* The Rdrand seeds of a lane list (BochscpuBackend_t::Seed_): read into
+ * seeds[i], or written from it (write != 0), so host handlers and the device
+ * action share one chain. Restore resets them to the initial seed. */
+int wtfgpu_lane_seeds(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, uint64_t *seeds, int write);
 /* Per-lane input feed of lanes [first, first+count): lane first+i owns
  * bytes[offsets[i] .. offsets[i+1]) (count+1 non-decreasing offsets), a
  * sequence of chunks each stored as a little-endian u32 size and that many

@@ -113,6 +113,7 @@ def load_hip_library(path: str = LIB_PATH) -> C.CDLL:
         "wtfgpu_set_limit": ([P, U64], C.c_int),
         "wtfgpu_set_regroup": ([P, U64], C.c_int),
         "wtfgpu_select_queue": ([P, U32], C.c_int),
+        "wtfgpu_lane_seeds": ([P, C.POINTER(U32), U32, C.POINTER(U64), C.c_int], C.c_int),
         "wtfgpu_run_async": ([P, U32, U32, U64], C.c_int),
         "wtfgpu_run_wait": ([P, C.POINTER(RunStats)], C.c_int),
         "wtfgpu_set_breakpoints": ([P, C.POINTER(U64), U32], C.c_int),

@@ -555,6 +555,44 @@ __device__ __noinline__ bool feed_apply(const Dev &P, Lane &L, const wtfgpu_bp_a
 // registers untouched. RETURN reads [rsp] as the host's
 // SimulateReturnFromFunction does (backend.cc:129-146); a read that would fault
 // is left to the host path, whose translation decides the outcome.
+// BLAKE3 of an 8-byte input, first 16 output bytes (one chunk, one block:
+// CHUNK_START | CHUNK_END | ROOT), for Rdrand's chain.
+__device__ __forceinline__ u32 rotr32(u32 x, u32 n) { return (x >> n) | (x << (32 - n)); }
+__device__ __forceinline__ void b3_g(u32 *v, int a, int b, int c, int d, u32 x, u32 y) {
+  v[a] = v[a] + v[b] + x;
+  v[d] = rotr32(v[d] ^ v[a], 16);
+  v[c] = v[c] + v[d];
+  v[b] = rotr32(v[b] ^ v[c], 12);
+  v[a] = v[a] + v[b] + y;
+  v[d] = rotr32(v[d] ^ v[a], 8);
+  v[c] = v[c] + v[d];
+  v[b] = rotr32(v[b] ^ v[c], 7);
+}
+__device__ __noinline__ void blake3_le64(u64 in, u64 &lo, u64 &hi) {
+  const u32 iv[8] = {0x6A09E667u, 0xBB67AE85u, 0x3C6EF372u, 0xA54FF53Au,
+                     0x510E527Fu, 0x9B05688Cu, 0x1F83D9ABu, 0x5BE0CD19u};
+  const u8 perm[16] = {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8};
+  u32 m[16] = {(u32)in, (u32)(in >> 32), 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  u32 v[16] = {iv[0], iv[1], iv[2], iv[3], iv[4], iv[5], iv[6], iv[7], iv[0], iv[1], iv[2], iv[3], 0, 0, 8, 1 | 2 | 8};
+  for (int r = 0; r < 7; r++) {
+    b3_g(v, 0, 4, 8, 12, m[0], m[1]);
+    b3_g(v, 1, 5, 9, 13, m[2], m[3]);
+    b3_g(v, 2, 6, 10, 14, m[4], m[5]);
+    b3_g(v, 3, 7, 11, 15, m[6], m[7]);
+    b3_g(v, 0, 5, 10, 15, m[8], m[9]);
+    b3_g(v, 1, 6, 11, 12, m[10], m[11]);
+    b3_g(v, 2, 7, 8, 13, m[12], m[13]);
+    b3_g(v, 3, 4, 9, 14, m[14], m[15]);
+    if (r < 6) {
+      u32 t[16];
+      for (int i = 0; i < 16; i++) t[i] = m[perm[i]];
+      for (int i = 0; i < 16; i++) m[i] = t[i];
+    }
+  }
+  lo = (u64)(v[0] ^ v[8]) | ((u64)(v[1] ^ v[9]) << 32);
+  hi = (u64)(v[2] ^ v[10]) | ((u64)(v[3] ^ v[11]) << 32);
+}
+
 __device__ __noinline__ bool bp_apply(const Dev &P, Lane &L, u64 grip) {
   u32 s;
   if (!P.act_keys || !hash_find(P.act_keys, P.act_mask, grip, s)) return false;
@@ -565,6 +603,18 @@ __device__ __noinline__ bool bp_apply(const Dev &P, Lane &L, u64 grip) {
     return true;
   }
   if (a.kind == WTFGPU_BPACT_FEED) return feed_apply(P, L, a);
+  if (a.kind == WTFGPU_BPACT_STOP_OK) {
+    L.status = WTFGPU_EXIT_STOP_OK;
+    return true;
+  }
+  if (a.kind == WTFGPU_BPACT_RDRAND) {  // Rdrand (bochscpu_backend.cc:874-885); the instruction then runs
+    if (!P.rd_seed) return false;
+    u64 lo, hi;
+    blake3_le64(P.rd_seed[L.lane], lo, hi);
+    P.rd_seed[L.lane] = lo;
+    RS(L, (u32)a.gprs[0] & 15, hi);
+    return true;
+  }
   if (a.kind != WTFGPU_BPACT_RETURN) return false;
   const u64 rsp = R(L, WTFGPU_RSP);
   u64 ra = 0;
@@ -723,6 +773,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(const Dev *__res
 #else
 __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first, u32 count, u64 max_steps) {
 #endif
+  if (P.perm && rfl64(P.stat[3]) == 0) return;  // regrouped launch with no running lane
   const u32 lid = threadIdx.x & 63;
   const u32 hw = rfl32(blockIdx.x * 4 + (threadIdx.x >> 6));  // hardware wave in the launch (uniform)
   const u32 tid = hw * P.lpw + lid;
@@ -969,6 +1020,7 @@ __device__ __forceinline__ void restore_lane(const Dev &P, const InitState &s, c
   P.sys[lane] = s.sys;
   P.ov_count[lane] = 0;
   tlb_stale(P, lane);
+  if (P.rd_seed) P.rd_seed[lane] = P.rd_seed0;  // bochscpu_backend.cc:1030
   if (P.cov_rip) {
     P.lane_gen[lane] += 1;
     P.cov_cnt[lane] = 0;
@@ -1006,6 +1058,7 @@ __global__ void k_restore(Dev P, const InitState *S, const wtfgpu_regs_t *full0,
   P.sys[lane] = s.sys;
   P.ov_count[lane] = 0;  // the dirty-list reset: overlays dropped, nothing copied
   tlb_stale(P, lane);
+  if (P.rd_seed) P.rd_seed[lane] = P.rd_seed0;  // bochscpu_backend.cc:1030
   if (P.cov_rip) {       // the lane's coverage set empties
     P.lane_gen[lane] += 1;
     P.cov_cnt[lane] = 0;
@@ -1058,9 +1111,40 @@ __device__ __forceinline__ bool host_walk(const Dev &P, Lane &L, u64 va, u64 &gp
   return true;
 }
 
+// The same write by one 64-thread block (the control is uniform, every
+// thread computes it; the page copy and the bytes are spread over the block).
+__device__ __forceinline__ bool lane_phys_write_block(const Dev &P, Lane &L, u64 gpa, const u8 *src, u64 len, u32 lid) {
+  while (len) {
+    const u64 off = gpa & 0xfff;
+    u64 n = 4096 - off;
+    if (n > len) n = len;
+    bool priv;
+    const u8 *pg = phys_page(P, L.lane, L.ovn, L.bloom, gpa >> 12, priv);
+    u8 *dst = (u8 *)pg;
+    if (!priv) {
+      if (L.ovn >= P.K) return false;
+      dst = P.ov_data + ((u64)L.lane * P.K + L.ovn) * WTFGPU_PAGE_SIZE;
+      const uint4 *s4 = (const uint4 *)pg;
+      uint4 *d4 = (uint4 *)dst;
+      for (u32 i = lid; i < 256; i += 64) d4[i] = s4[i];
+      if (lid == 0) P.ov_gpfn[(u64)L.ovn * P.nlanes + L.lane] = (u32)(gpa >> 12);
+      __syncthreads();  // the copy before the patch (and the slot before later lookups)
+      L.ovn++;
+      L.bloom |= bloom_bit(gpa >> 12);
+    }
+    for (u64 i = lid; i < n; i += 64) dst[off + i] = src[i];
+    __syncthreads();
+    src += n;
+    gpa += n;
+    len -= n;
+  }
+  return true;
+}
+
+// Host-handler writes, one 64-thread block per lane, records in order.
 __global__ void k_apply_writes(Dev P, const WriteRec *recs, const u32 *starts, u32 nlanes_w, const u8 *data,
                                i32 *status_out, u32 phys) {
-  const u32 t = blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 t = blockIdx.x, lid = threadIdx.x;
   if (t >= nlanes_w) return;
   const u32 r0 = starts[t], r1 = starts[t + 1];
   const u32 lane = recs[r0].lane;
@@ -1080,7 +1164,7 @@ __global__ void k_apply_writes(Dev P, const WriteRec *recs, const u32 *starts, u
         st = WTFGPU_ERR_TRANSLATE;
         break;
       }
-      if (!lane_phys_write(P, L, gpa, src, n)) {
+      if (!lane_phys_write_block(P, L, gpa, src, n, lid)) {
         st = WTFGPU_ERR_OOM;
         break;
       }
@@ -1088,10 +1172,12 @@ __global__ void k_apply_writes(Dev P, const WriteRec *recs, const u32 *starts, u
       src += n;
       left -= n;
     }
-    status_out[r] = st;
+    if (lid == 0) status_out[r] = st;
   }
-  P.ov_count[lane] = L.ovn;
-  tlb_stale(P, lane);
+  if (lid == 0) {
+    P.ov_count[lane] = L.ovn;
+    tlb_stale(P, lane);
+  }
 }
 
 // Host-injected exception per lane (PageFaultsMemoryIfNeeded): delivered
@@ -1254,6 +1340,14 @@ __global__ void k_cov_collect(Dev P, const u32 *lanes, u32 first, u32 n, u32 *ou
   if (threadIdx.x == 0 && P.cov_overflow[lane]) atomicOr(ovf, 1u);
 }
 
+// Rdrand seeds of a lane list: gathered into / scattered from buf.
+__global__ void k_lane_seeds(Dev P, const u32 *lanes, u32 n, u64 *buf, int write) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (write) P.rd_seed[lanes[i]] = buf[i];
+  else buf[i] = P.rd_seed[lanes[i]];
+}
+
 // Exit records of lanes [first, first + count) (wtfgpu_read_exits).
 __global__ void k_pack_exits(Dev P, u32 first, u32 count, wtfgpu_exit_t *out) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1280,12 +1374,17 @@ __global__ void k_pack_exits(Dev P, u32 first, u32 count, wtfgpu_exit_t *out) {
 // Regrouping keys: running lanes by rip (lanes at one rip become neighbours,
 // so one wave step serves them all), every other lane after them (their
 // waves find nothing to run and leave at once).
+// They also count the running lanes (P.stat[3]): a launch with none returns at once.
 __global__ void k_regroup_keys(Dev P, u32 first, u32 count, u32 *keys, u32 *lanes) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= count) return;
-  const u32 lane = first + i;
+  const bool in = i < count;
+  const u32 lane = first + (in ? i : 0);
+  const bool run = in && P.status[lane] == WTFGPU_RUNNING;
+  const u64 m = __ballot(run);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd((unsigned long long *)&P.stat[3], (unsigned long long)__popcll(m));
+  if (!in) return;
   const u32 r = (u32)P.rip[lane] & 0xffffffu;  // 24 key bits: three radix passes
-  keys[i] = P.status[lane] == WTFGPU_RUNNING ? (r == 0xffffffu ? r - 1 : r) : 0xffffffu;
+  keys[i] = run ? (r == 0xffffffu ? r - 1 : r) : 0xffffffu;
   lanes[i] = lane;
 }
 
@@ -1396,6 +1495,7 @@ struct wtfgpu_ctx {
   ExitInfo *d_exinfo = nullptr;
   LaneSys *d_sys = nullptr;
   u32 *d_guc = nullptr;       // device-wide decoded-uop cache (Dev::guc)
+  u64 *d_rdseed = nullptr;    // per-lane Rdrand seeds (Dev::rd_seed)
   LaneTlb *d_tlbs = nullptr;  // translation state kept between k_run launches
   u32 *d_tlbok = nullptr;
   u8 *d_ovdata = nullptr;
@@ -1434,7 +1534,7 @@ struct wtfgpu_ctx {
   size_t rtemp_bytes = 0;
   u64 scratch_bytes = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  u64 regroup_steps = 0;
+  u64 regroup_steps = 1024;
   u32 async_launches = 0;
   // the current queue's resources live in the members above; the others here
   QueueRes queues[2];
@@ -1610,6 +1710,9 @@ int wtfgpu_create(int device, wtfgpu_ctx **out) {
   wtfgpu_ctx *c = new (std::nothrow) wtfgpu_ctx();
   if (!c) return WTFGPU_ERR_OOM;
   c->device = device;
+  // regrouped launches of 1024 wave-steps by default (measured on MI355X:
+  // HEVD 0.73M -> 1.9M execs/s, tlv 2.0M -> 2.1-2.3M, SYN 0.88M -> 0.81M)
+  c->regroup_steps = 1024;
   if (const char *e = getenv("WTFGPU_REGROUP_STEPS")) c->regroup_steps = strtoull(e, nullptr, 0);
   {
     // shared decoded-uop cache: 32K entries of 192 bytes (WTFGPU_GUC=0: off)
@@ -1657,6 +1760,7 @@ static void free_lanes(wtfgpu_ctx *c) {
   dfree(c->d_sys);
   dfree(c->d_tlbs);
   dfree(c->d_tlbok);
+  dfree(c->d_rdseed);
   dfree(c->d_ovdata);
   dfree(c->d_full);
   dfree(c->d_perm);
@@ -1785,6 +1889,7 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
   rc |= dalloc(&c->d_full, N);
   rc |= dalloc(&c->d_tlbs, N);
   rc |= dalloc(&c->d_tlbok, N);
+  rc |= dalloc(&c->d_rdseed, N);
   if (cov_entries) {
     rc |= dalloc(&c->d_covrip, N * cov_entries);
     rc |= dalloc(&c->d_covgen, N * cov_entries);
@@ -1798,6 +1903,7 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
   HIPCHK(hipMemsetAsync(c->d_ovcount, 0, N * 4, c->stream));
   HIPCHK(hipMemsetAsync(c->d_lflags, 0, N * 4, c->stream));
   HIPCHK(hipMemsetAsync(c->d_tlbok, 0, N * 4, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_rdseed, 0, N * 8, c->stream));  // CpuState_t::Seed = 0 (globals.h:1084)
   HIPCHK(hipMemsetAsync(c->d_icount, 0, N * 8, c->stream));
   HIPCHK(hipMemsetAsync(c->d_nbytes, 0, N * 8, c->stream));
   HIPCHK(hipMemsetAsync(c->d_exinfo, 0, N * sizeof(ExitInfo), c->stream));
@@ -1826,6 +1932,8 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
   P.sys = c->d_sys;
   P.tlbs = c->d_tlbs;
   P.tlb_ok = c->d_tlbok;
+  P.rd_seed = c->d_rdseed;
+  P.rd_seed0 = 0;
   P.ov_count = c->d_ovcount;
   P.ov_gpfn = c->d_ovgpfn;
   P.ov_data = c->d_ovdata;
@@ -1933,7 +2041,7 @@ int wtfgpu_set_breakpoints(wtfgpu_ctx *c, const uint64_t *gvas, uint32_t n) {
 int wtfgpu_set_breakpoint_actions(wtfgpu_ctx *c, const wtfgpu_bp_action_t *acts, uint32_t n) {
   if (!c || (n && !acts)) return WTFGPU_ERR_INVALID;
   for (u32 i = 0; i < n; i++)
-    if (acts[i].kind > WTFGPU_BPACT_FEED || acts[i].gva == EMPTY_KEY) return WTFGPU_ERR_INVALID;
+    if (acts[i].kind > WTFGPU_BPACT_STOP_OK || acts[i].gva == EMPTY_KEY) return WTFGPU_ERR_INVALID;
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   dfree(c->d_actkeys);
@@ -2293,12 +2401,12 @@ static Dev run_params(wtfgpu_ctx *c, bool regroup) {
 static int launch_chunk(wtfgpu_ctx *c, const Dev &Q, u32 first, u32 count, u64 steps, bool regroup) {
   const u32 hwaves = (count + c->P.lpw - 1) / c->P.lpw;
   if (regroup) {
-    k_regroup_keys<<<(count + 255) / 256, 256, 0, c->stream>>>(c->P, first, count, c->d_rkeys, c->d_rlanes);
+    HIPCHK(hipMemsetAsync(c->d_stat + 2, 0, 16, c->stream));  // running lanes: this launch's (2: after, 3: before)
+    k_regroup_keys<<<(count + 255) / 256, 256, 0, c->stream>>>(Q, first, count, c->d_rkeys, c->d_rlanes);
     HIPCHK(hipGetLastError());
     size_t bytes = c->rtemp_bytes;
     HIPCHK(hipcub::DeviceRadixSort::SortPairs(c->d_rtemp, bytes, c->d_rkeys, c->d_rkeys2, c->d_rlanes,
                                               c->d_perm + first, (int)count, 0, 24, c->stream));
-    HIPCHK(hipMemsetAsync(c->d_stat + 2, 0, 8, c->stream));  // running lanes: the last launch's count
   }
 #if WTFGPU_P_BYREF
   k_run<<<(hwaves + 3) / 4, 256, 0, c->stream>>>(c->d_dev, first, count, steps);
@@ -2414,6 +2522,24 @@ int wtfgpu_run_wait(wtfgpu_ctx *c, wtfgpu_run_stats_t *stats) {
   return WTFGPU_OK;
 }
 
+int wtfgpu_lane_seeds(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, uint64_t *seeds, int write) {
+  if (!c || (n && (!lanes || !seeds)) || !c->d_rdseed) return WTFGPU_ERR_INVALID;
+  if (n == 0) return WTFGPU_OK;
+  for (u32 i = 0; i < n; i++)
+    if (lanes[i] >= c->P.nlanes) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  const u64 o_s = ((u64)n * 4 + 255) & ~255ull;
+  if (ensure_scratch(c, o_s + (u64)n * 8)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemcpyAsync(c->d_scratch, lanes, (u64)n * 4, hipMemcpyHostToDevice, c->stream));
+  if (write) HIPCHK(hipMemcpyAsync(c->d_scratch + o_s, seeds, (u64)n * 8, hipMemcpyHostToDevice, c->stream));
+  k_lane_seeds<<<(n + 255) / 256, 256, 0, c->stream>>>(c->P, (const u32 *)c->d_scratch, n, (u64 *)(c->d_scratch + o_s),
+                                                       write);
+  HIPCHK(hipGetLastError());
+  if (!write) HIPCHK(hipMemcpyAsync(seeds, c->d_scratch + o_s, (u64)n * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
 int wtfgpu_select_queue(wtfgpu_ctx *c, uint32_t queue) {
   if (!c || queue >= 2) return WTFGPU_ERR_INVALID;
   if (queue == c->cur_queue) return WTFGPU_OK;
@@ -2482,7 +2608,10 @@ static int apply_writes(wtfgpu_ctx *c, const wtfgpu_write_t *writes, uint32_t n,
     order[i] = i;
     if (writes[i].lane >= c->P.nlanes || writes[i].data_off + writes[i].len > data_len) return WTFGPU_ERR_INVALID;
   }
-  std::stable_sort(order.begin(), order.end(), [&](u32 a, u32 b) { return writes[a].lane < writes[b].lane; });
+  bool grouped = true;  // records of a lane already consecutive and lanes ascending: no sort
+  for (u32 i = 1; i < n && grouped; i++) grouped = writes[i - 1].lane <= writes[i].lane;
+  if (!grouped)
+    std::stable_sort(order.begin(), order.end(), [&](u32 a, u32 b) { return writes[a].lane < writes[b].lane; });
   std::vector<WriteRec> recs(n);
   std::vector<u32> starts;
   for (u32 i = 0; i < n; i++) {
@@ -2499,7 +2628,7 @@ static int apply_writes(wtfgpu_ctx *c, const wtfgpu_write_t *writes, uint32_t n,
   HIPCHK(hipMemcpyAsync(c->d_scratch, recs.data(), b_recs, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->d_scratch + o_starts, starts.data(), b_starts, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->d_scratch + o_data, data, data_len, hipMemcpyHostToDevice, c->stream));
-  k_apply_writes<<<(nl + 63) / 64, 64, 0, c->stream>>>(c->P, (const WriteRec *)c->d_scratch,
+  k_apply_writes<<<nl, 64, 0, c->stream>>>(c->P, (const WriteRec *)c->d_scratch,
                                                        (const u32 *)(c->d_scratch + o_starts), nl,
                                                        c->d_scratch + o_data, (i32 *)(c->d_scratch + o_st), phys);
   HIPCHK(hipGetLastError());

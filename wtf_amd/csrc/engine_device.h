@@ -118,6 +118,8 @@ struct Dev {
   // bytes (a reader takes an entry only when all three tags match)
   u32 *guc;
   u32 guc_mask;
+  u64 *rd_seed;           // [nlanes] Rdrand seeds (WTFGPU_BPACT_RDRAND)
+  u64 rd_seed0;           // the initial state's (restore)
   LaneTlb *tlbs;          // [nlanes]
   u32 *tlb_ok;            // [nlanes]
   wtfgpu_regs_t *full;   // [nlanes] cold architectural state (MSRs the hot LaneSys lacks)

@@ -55,6 +55,7 @@ GpuBackend_t::GpuBackend_t() = default;
 GpuBackend_t::~GpuBackend_t() {
   for (Part &P : parts_)
     if (P.pin) wtfgpu_host_free(ctx_, P.pin);
+  if (wpin_) wtfgpu_host_free(ctx_, wpin_);
   if (ctx_) wtfgpu_destroy(ctx_);
 }
 
@@ -201,6 +202,11 @@ bool GpuBackend_t::SetBreakpoint(const Gva_t Gva, const BreakpointHandler_t Hand
     A.gprs[0] = (uint64_t)gpr_index((Registers_t)Action.Gprs[0]);
     A.gprs[1] = (uint64_t)gpr_index((Registers_t)Action.Gprs[1]);
     feed_action_ = true;
+  } else if (Action.Kind == BreakpointAction_t::Kind_t::StopOk) {
+    A.kind = WTFGPU_BPACT_STOP_OK;
+  } else if (Action.Kind == BreakpointAction_t::Kind_t::Rdrand) {
+    A.kind = WTFGPU_BPACT_RDRAND;
+    A.gprs[0] = (uint64_t)gpr_index((Registers_t)Action.Gprs[0]);
   } else {
     A.kind = WTFGPU_BPACT_SET_GPRS;
     memcpy(A.gprs, Action.Gprs, sizeof(A.gprs));
@@ -553,36 +559,73 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
     cand[i].lo = (uint32_t)lo;
     cand[i].hi = (uint32_t)hi;
   }
-  std::vector<wtfgpu_write_t> writes;
-  std::vector<uint8_t> data;
-  for (uint32_t l : lanes) {
+  // the write records and their bytes, laid out per lane (prefix sums) and
+  // filled on all host threads into a pinned buffer: one DMA to the device
+  const size_t nl = lanes.size();
+  std::vector<uint64_t> roff(nl + 1, 0), boff(nl + 1, 0);
+  for (size_t i = 0; i < nl; i++) {
+    const LaneView &v = views_[lanes[i]];
+    uint64_t r = 0, b = 0;
+    for (const LaneView::Logged &w : v.wlog)
+      if (w.len) {
+        r++;
+        b += w.len;
+      }
+    roff[i + 1] = roff[i] + r;
+    boff[i + 1] = boff[i] + b;
+  }
+  uint64_t cbytes = 0, crecs = 0;
+  for (const Cand &c : cand)
+    if (c.lo != c.hi) {
+      crecs++;
+      cbytes += c.hi - c.lo;
+    }
+  std::vector<wtfgpu_write_t> writes(roff[nl] + crecs);
+  const uint64_t total = boff[nl] + cbytes;
+  if (total > wpin_cap_) {
+    if (wpin_) wtfgpu_host_free(ctx_, wpin_);
+    wpin_ = nullptr;
+    wpin_cap_ = std::max<uint64_t>(total * 2, 1 << 20);
+    void *p = nullptr;
+    if (wtfgpu_host_alloc(ctx_, wpin_cap_, &p)) return WTFGPU_ERR_OOM;
+    wpin_ = (uint8_t *)p;
+  }
+#pragma omp parallel for schedule(static, 256) if (nl >= 1024)
+  for (size_t i = 0; i < nl; i++) {
+    const uint32_t l = lanes[i];
     LaneView &v = views_[l];
+    uint64_t r = roff[i], b = boff[i];
     for (const LaneView::Logged &w : v.wlog) {
       if (!w.len) continue;
-      writes.push_back(wtfgpu_write_t{l, w.len, w.gpa, data.size()});
-      data.insert(data.end(), v.wdata.begin() + w.off, v.wdata.begin() + w.off + w.len);
+      writes[r++] = wtfgpu_write_t{l, w.len, w.gpa, b};
+      memcpy(wpin_ + b, v.wdata.data() + w.off, w.len);
+      b += w.len;
       v.dirty_known = false;
     }
     v.wlog.clear();
     v.wdata.clear();
   }
-  for (const Cand &c : cand) {
-    if (c.lo == c.hi) continue;
-    wtfgpu_write_t w{};
-    w.lane = c.lane;
-    w.len = c.hi - c.lo;
-    w.gva = (c.p->gpfn << 12) | c.lo;
-    w.data_off = data.size();
-    data.insert(data.end(), c.p->data + c.lo, c.p->data + c.hi);
-    writes.push_back(w);
-    views_[c.lane].dirty_known = false;  // the device overlay changed
+  {
+    uint64_t r = roff[nl], b = boff[nl];
+    for (const Cand &c : cand) {
+      if (c.lo == c.hi) continue;
+      wtfgpu_write_t w{};
+      w.lane = c.lane;
+      w.len = c.hi - c.lo;
+      w.gva = (c.p->gpfn << 12) | c.lo;
+      w.data_off = b;
+      memcpy(wpin_ + b, c.p->data + c.lo, w.len);
+      b += w.len;
+      writes[r++] = w;
+      views_[c.lane].dirty_known = false;  // the device overlay changed
+    }
   }
   stats_.staged_pages += cand.size();
   for (uint32_t l : lanes) drop_staged(views_[l]);
   int rc = WTFGPU_OK;
   if (!rl.empty()) rc = wtfgpu_write_gprs_list(ctx_, rl.data(), (uint32_t)rl.size(), regs.data());
   if (!rc && !writes.empty())
-    rc = wtfgpu_apply_phys_writes(ctx_, writes.data(), (uint32_t)writes.size(), data.data(), data.size(), nullptr);
+    rc = wtfgpu_apply_phys_writes(ctx_, writes.data(), (uint32_t)writes.size(), wpin_, total, nullptr);
   return rc;
 }
 
@@ -591,7 +634,7 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
 void GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first, const std::vector<wtfgpu_exit_t> &ex,
                             std::vector<uint8_t> &done, std::vector<LaneResult> *out, std::vector<uint32_t> &hits) {
   std::vector<uint8_t> hit(pending.size(), 0);
-#pragma omp parallel for schedule(static, 1024) if (pending.size() >= 8192)
+#pragma omp parallel for schedule(static, 1024) if (pending.size() >= 2048)
   for (size_t pi = 0; pi < pending.size(); pi++) {
     const uint32_t l = pending[pi];
     if (done[l - first]) continue;
@@ -614,6 +657,15 @@ void GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first
         // master saves, server.h:861-877) as its result
         if (out) (*out)[l].error = true;
         if (!v.result) v.result = Crash_t();
+        if (e.status == WTFGPU_EXIT_UNIMPLEMENTED) {
+          stats_.err_unimpl++;
+          stats_.last_unimpl_op = e.opcode;
+          stats_.last_unimpl_rip = e.rip;
+        } else if (e.status == WTFGPU_EXIT_OVERLAY_FULL) {
+          stats_.err_overlay++;
+        } else {
+          stats_.err_other++;
+        }
         break;
     }
     done[l - first] = 1;
@@ -638,7 +690,7 @@ bool GpuBackend_t::fill_results(const std::vector<uint32_t> &lanes, uint32_t fir
     regs.resize(fin.size() * 18);
     if (!fin.empty() && wtfgpu_read_gprs_list(ctx_, fin.data(), (uint32_t)fin.size(), regs.data())) return false;
   }
-#pragma omp parallel for schedule(static, 1024) if (fin.size() >= 8192)
+#pragma omp parallel for schedule(static, 1024) if (fin.size() >= 2048)
   for (size_t i = 0; i < fin.size(); i++) {
     LaneResult &r = (*out)[fin[i]];
     const LaneView &v = views_[fin[i]];
@@ -714,6 +766,9 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
     // ---- service the round's breakpoint hits
     std::vector<uint64_t> regs(hits.size() * 18);
     if (wtfgpu_read_gprs_list(ctx_, hits.data(), (uint32_t)hits.size(), regs.data())) return false;
+    // the lanes' Rdrand chains (a device Rdrand action may have advanced them)
+    std::vector<uint64_t> seeds(hits.size());
+    if (wtfgpu_lane_seeds(ctx_, hits.data(), (uint32_t)hits.size(), seeds.data(), 0)) return false;
     const uint32_t stride = overlay_pages_ + 1;
     std::vector<uint32_t> dl(hits.size() * stride);
     if (wtfgpu_read_dirty_list(ctx_, hits.data(), (uint32_t)hits.size(), dl.data())) return false;
@@ -729,6 +784,7 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
     for (size_t i = 0; i < hits.size(); i++) {
       LaneView &v = views_[hits[i]];
       memcpy(v.gpr, &regs[i * 18], 18 * 8);
+      v.seed = seeds[i];
       v.regs_dirty = false;
       v.cr_known = 0;  // an exception delivery or a cr write may have changed them
       v.win_len = 0;
@@ -864,6 +920,8 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
     const auto t3 = Clock::now();
     stats_.handler_ms += std::chrono::duration<double, std::milli>(t3 - t2).count();
     if (flush_lanes(hits)) return false;
+    for (size_t i = 0; i < hits.size(); i++) seeds[i] = views_[hits[i]].seed;
+    if (wtfgpu_lane_seeds(ctx_, hits.data(), (uint32_t)hits.size(), seeds.data(), 1)) return false;
     {  // PageFaultsMemoryIfNeeded requests: #PF through the guest IDT, resume at the handler
       std::vector<uint32_t> il;
       std::vector<uint64_t> ia;
@@ -1309,7 +1367,8 @@ std::string GpuBackend_t::StatsJson() const {
            "\"handler_ms\":%.3f,\"fetch_ms\":%.3f,\"flush_ms\":%.3f,\"insert_ms\":%.3f,\"coverage_ms\":%.3f,"
            "\"target_restore_ms\":%.3f,\"alg_bytes\":%llu,\"restore_ms\":%.3f,\"module_ms\":%.3f,"
            "\"upload_ms\":%.3f,\"bytes_ms\":%.3f,\"covlog_ms\":%.3f,\"attrib_ms\":%.3f,\"cov_entries\":%llu,"
-           "\"run_ms\":%.3f,\"exits_ms\":%.3f,\"regs_ms\":%.3f}",
+           "\"run_ms\":%.3f,\"exits_ms\":%.3f,\"regs_ms\":%.3f,\"err_unimpl\":%llu,\"err_overlay\":%llu,"
+           "\"err_other\":%llu,\"last_unimpl_op\":%llu,\"last_unimpl_rip\":%llu}",
            (unsigned long long)stats_.group_steps, (unsigned long long)stats_.rounds,
            (unsigned long long)stats_.breakpoint_hits, (unsigned long long)stats_.kernel_launches, stats_.kernel_ms,
            stats_.service_ms, stats_.total_ms, (unsigned long long)stats_.page_fetches,
@@ -1318,7 +1377,9 @@ std::string GpuBackend_t::StatsJson() const {
            stats_.fetch_ms, stats_.flush_ms, stats_.insert_ms, stats_.coverage_ms, stats_.target_restore_ms,
            (unsigned long long)stats_.alg_bytes, stats_.restore_ms, stats_.module_ms, stats_.upload_ms,
            stats_.bytes_ms, stats_.covlog_ms, stats_.attrib_ms, (unsigned long long)stats_.cov_entries,
-           stats_.run_ms, stats_.exits_ms, stats_.regs_ms);
+           stats_.run_ms, stats_.exits_ms, stats_.regs_ms, (unsigned long long)stats_.err_unimpl.load(),
+           (unsigned long long)stats_.err_overlay.load(), (unsigned long long)stats_.err_other.load(),
+           (unsigned long long)stats_.last_unimpl_op.load(), (unsigned long long)stats_.last_unimpl_rip.load());
   std::string r(b);
   r.pop_back();
   r += ",\"fetch_by_bp\":{";

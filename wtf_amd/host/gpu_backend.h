@@ -48,6 +48,9 @@ struct BatchStats {
   uint64_t cov_entries = 0;  // (lane, rip) new-coverage log entries collected
   // run loop split: wtfgpu_run wall (launches + syncs), exit read-back + classification, final registers
   double run_ms = 0, exits_ms = 0, regs_ms = 0;
+  // engine errors by exit status, the last unimplemented opcode and its rip
+  std::atomic<uint64_t> err_unimpl{0}, err_overlay{0}, err_other{0};
+  std::atomic<uint64_t> last_unimpl_op{0}, last_unimpl_rip{0};
 };
 
 class GpuBackend_t final : public Backend_t, public Executor_t {
@@ -201,6 +204,8 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
     uint64_t pin_cap = 0;
   };
   std::vector<Part> parts_;
+  uint8_t *wpin_ = nullptr;  // pinned staging of host-handler writes (flush_lanes; applied synchronously)
+  uint64_t wpin_cap_ = 0;
   uint32_t next_part_ = 0;
   uint32_t parts_n() const;
   bool harvest_part(Part &P, const Target_t &Target, std::vector<StreamResult_t> &Out, ModuleSlots *Slots);

@@ -3,10 +3,11 @@
 //  * InsertTestcase (:20-59): u32 IOCTL code -> rdx, the rest (<= 1024 bytes)
 //    -> the user buffer at r8, its size -> r9 and GetArgAddress(5);
 //  * the instruction after the 6-byte call to DeviceIoControl stops the
-//    testcase with Ok (:64-73);
+//    testcase with Ok (:64-73; also declared as BreakpointAction_t::StopOk);
 //  * nt!DbgPrintEx is skipped (return 0) after reading its format (:78-88);
 //  * nt!ExGenRandom: right after its `rdrand rdx` (+0xe0) rdx := Rdrand()
-//    (:96-108, the BLAKE3 chain of Backend_t::Rdrand);
+//    (:96-108, the BLAKE3 chain of Backend_t::Rdrand; also declared as data,
+//    BreakpointAction_t::Rdrand, which the gpu backend runs on the device);
 //  * nt!KeBugCheck2 -> Crash_t("crash-<code>-<p0>-<p1>-<p2>-<p3>-<p4>") (:114-128);
 //  * nt!SwapContext -> Cr3Change_t (:134-139).
 // The module keeps no per-testcase state, so nothing is registered with
@@ -44,7 +45,10 @@ bool InsertTestcase(const uint8_t *Buffer, const size_t BufferSize) {
 bool Init(const Options_t &, const CpuState_t &) {
   const Gva_t Rip = Gva_t(g_Backend->Rip());
   const Gva_t AfterCall = Rip + Gva_t(6);
-  if (!g_Backend->SetBreakpoint(AfterCall, [](Backend_t *Backend) { Backend->Stop(Ok_t()); })) return false;
+  if (!g_Backend->SetBreakpoint(
+          AfterCall, [](Backend_t *Backend) { Backend->Stop(Ok_t()); },
+          BreakpointAction_t::StopOk()))  // device-side on the gpu backend
+    return false;
   if (!g_Backend->SetBreakpoint("nt!DbgPrintEx", [](Backend_t *Backend) {
         const Gva_t FormatPtr = Backend->GetArgGva(2);
         const std::string Format = Backend->VirtReadString(FormatPtr);
@@ -58,7 +62,9 @@ bool Init(const Options_t &, const CpuState_t &) {
     printf("It seems that nt!ExGenRandom's code has changed, update the offset!\n");
     return false;
   }
-  if (!g_Backend->SetBreakpoint(ExGenRandom, [](Backend_t *Backend) { Backend->Rdx(Backend->Rdrand()); }))
+  if (!g_Backend->SetBreakpoint(
+          ExGenRandom, [](Backend_t *Backend) { Backend->Rdx(Backend->Rdrand()); },
+          BreakpointAction_t::Rdrand(Registers_t::Rdx)))  // device-side on the gpu backend
     return false;
   if (!g_Backend->SetBreakpoint("nt!KeBugCheck2", [](Backend_t *Backend) {
         const uint64_t BCode = Backend->GetArg(0), B0 = Backend->GetArg(1), B1 = Backend->GetArg(2),

@@ -551,6 +551,12 @@ void FuzzSession::Account(const uint8_t *Tc, size_t Size, const LaneResult &L) {
   S_.execs++;
   S_.retired += L.icount;
   if (L.error) {  // the engine could not finish it: neither a crash nor coverage
+    // the first ones are kept under errors/ for triage (engine gaps, not target bugs)
+    if (S_.errors < 256) {
+      std::error_code ec;
+      fs::create_directories(T_ / "errors", ec);
+      SaveFile(T_ / "errors" / ("engine-error-" + std::to_string(S_.errors)), Tc, Size);
+    }
     S_.errors++;
     S_.error_retired += L.icount;
     return;

@@ -206,7 +206,7 @@ using BreakpointHandler_t = void (*)(Backend_t *);
 // other backend calls the handler. The module guarantees the two are the same
 // register effect; the GPU-vs-twin parity tests check it testcase by testcase.
 struct BreakpointAction_t {
-  enum class Kind_t { Host, SimulateReturn, SetGprs, Feed };
+  enum class Kind_t { Host, SimulateReturn, SetGprs, Feed, Rdrand, StopOk };
   Kind_t Kind = Kind_t::Host;
   uint64_t Return = 0;  // SimulateReturn: SimulateReturnFromFunction(Return)
   uint64_t Gprs[17] = {};  // SetGprs: rax, rcx, rdx, rbx, rsp, rbp, rsi, rdi, r8..r15, rip
@@ -223,6 +223,20 @@ struct BreakpointAction_t {
   // Size >= Window -> Stop(Ok_t()); else write it so that it ends at
   // Base + Window (dirty), Base = its address, Len = its size; the hooked
   // instruction then runs (Gprs[0] / Gprs[1] hold the two Registers_t)
+  // Stop(Ok_t())
+  static BreakpointAction_t StopOk() {
+    BreakpointAction_t A;
+    A.Kind = Kind_t::StopOk;
+    return A;
+  }
+  // Reg := Backend_t::Rdrand() (the testcase's BLAKE3 chain); the hooked
+  // instruction then runs
+  static BreakpointAction_t Rdrand(const Registers_t Reg) {
+    BreakpointAction_t A;
+    A.Kind = Kind_t::Rdrand;
+    A.Gprs[0] = (uint64_t)Reg;
+    return A;
+  }
   static BreakpointAction_t Feed(const Registers_t Base, const Registers_t Len,
                                  const uint64_t Window) {
     BreakpointAction_t A;
