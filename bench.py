@@ -281,7 +281,8 @@ def syn_leg(lanes: int, limit: int, steps: int, device: int) -> dict:
             acc["kernel_ms"] += rs.kernel_ms
             acc["launches"] += rs.kernel_launches
             acc["steps"] += rs.group_steps
-            acc["bytes"] += int(eng.nbytes().sum())
+            # B_exec: instruction + data bytes, the 64-byte input, 2 x 4096 per dirty page
+            acc["bytes"] += int(eng.nbytes().sum()) + 64 * lanes + 2 * 4096 * int(eng.dirty_counts().sum())
             acc["bad"] += int(np.count_nonzero(ex["status"] != EXIT_BREAKPOINT))
 
     step(0, False)

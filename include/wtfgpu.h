@@ -363,6 +363,9 @@ int wtfgpu_coverage_rips(wtfgpu_ctx *ctx, uint64_t *rips, uint64_t cap, uint64_t
 /* Per-lane algorithmic byte counters (ilen + data bytes read/written),
  * for the roofline numerator. */
 int wtfgpu_read_bytes(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, uint64_t *out);
+/* Per-lane dirty (copy-on-write) page counts: the 2 x 4096 bytes per dirty
+ * page of the reference's restore memcpy in B_exec. */
+int wtfgpu_read_dirty_counts(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, uint32_t *out);
 
 #ifdef __cplusplus
 }

@@ -52,13 +52,14 @@ def test_hevd_parity_host_handlers_only(target, tmp_path):
     assert len(h) == len(t) and not bad, bad[:10]
 
 
-@pytest.mark.parametrize("slice_steps", [128, 4096])
-def test_hevd_streaming_parity(target, tmp_path, slice_steps):
-    """Continuous batching with host-serviced breakpoints (ExGenRandom,
-    KeBugCheck2, SwapContext) and ring-0 paths: every input as the twin."""
+@pytest.mark.parametrize("slice_steps,regroup", [(128, 0), (4096, 0), (4096, 256), (2048, 1024)])
+def test_hevd_streaming_parity(target, tmp_path, slice_steps, regroup):
+    """Continuous batching (two pipelined halves) with device actions (Rdrand,
+    Stop, DbgPrintEx), host-serviced breakpoints (KeBugCheck2, SwapContext) and
+    ring-0 paths, with and without cross-wave regrouping: every input as the twin."""
     inp = os.path.join(target, "parity")
     g = H.run(H.WTFGPU, target, inp, str(tmp_path / "g.jsonl"), lanes=256, name="hevd",
-              extra=("--stream-run", "--slice-steps", str(slice_steps)))
+              extra=("--stream-run", "--slice-steps", str(slice_steps), "--regroup-steps", str(regroup)))
     t = H.run(H.TWIN, target, inp, str(tmp_path / "t.jsonl"), lanes=512, name="hevd")
     bad = [(x["input"], k) for x, y in zip(g, t) for k in FIELDS if x[k] != y[k]]
     assert len(g) == len(t) and not bad, bad[:10]

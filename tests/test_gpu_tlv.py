@@ -66,15 +66,15 @@ def test_tlv_lane_order_coverage_attribution(target, tmp_path):
     assert not _diff(g, t)
 
 
-@pytest.mark.parametrize("slice_steps", [64, 2048])
-def test_tlv_streaming_parity(target, tmp_path, slice_steps):
+@pytest.mark.parametrize("slice_steps,regroup", [(64, 0), (2048, 0), (2048, 256), (4096, 1024)])
+def test_tlv_streaming_parity(target, tmp_path, slice_steps, regroup):
     """Continuous batching (lanes refilled as their testcases finish: per-lane
     restore, feed regions, per-lane coverage collection) replays every input
     exactly as the twin does; short slices force many refills and lanes that
     straddle slices."""
     inp = os.path.join(target, "parity")
     g = H.run(H.WTFGPU, target, inp, str(tmp_path / "g.jsonl"), lanes=256,
-              extra=("--stream-run", "--slice-steps", str(slice_steps)))
+              extra=("--stream-run", "--slice-steps", str(slice_steps), "--regroup-steps", str(regroup)))
     t = H.run(H.TWIN, target, inp, str(tmp_path / "t.jsonl"), lanes=512)
     assert len(g) == len(t)
     assert not _diff(g, t)

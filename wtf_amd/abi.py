@@ -144,6 +144,7 @@ def load_hip_library(path: str = LIB_PATH) -> C.CDLL:
         "wtfgpu_coverage_device_map": ([P, C.POINTER(P), C.POINTER(U64)], C.c_int),
         "wtfgpu_coverage_rips": ([P, C.POINTER(U64), U64, C.POINTER(U64)], C.c_int),
         "wtfgpu_read_bytes": ([P, U32, U32, C.POINTER(U64)], C.c_int),
+        "wtfgpu_read_dirty_counts": ([P, U32, U32, C.POINTER(U32)], C.c_int),
         "wtfgpu_gather_pages": ([P, C.POINTER(U32), C.POINTER(U64), U32, P], C.c_int),
         "wtfgpu_lane_get_cr": ([P, U32, U32, C.POINTER(U64)], C.c_int),
         "wtfgpu_lane_set_cr": ([P, U32, U32, U64], C.c_int),

@@ -2947,7 +2947,16 @@ int wtfgpu_coverage_rips(wtfgpu_ctx *c, uint64_t *rips, uint64_t cap, uint64_t *
 int wtfgpu_read_bytes(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t *out) {
   if (!lanes_ok(c, first, count) || !out) return WTFGPU_ERR_INVALID;
   HIPCHK(hipSetDevice(c->device));
-  HIPCHK(hipMemcpy(out, c->d_nbytes + first, (u64)count * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpyAsync(out, c->d_nbytes + first, (u64)count * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_read_dirty_counts(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint32_t *out) {
+  if (!lanes_ok(c, first, count) || !out) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemcpyAsync(out, c->d_ovcount + first, (u64)count * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
   return WTFGPU_OK;
 }
 

@@ -205,6 +205,13 @@ class Engine:
              "read_bytes")
         return out
 
+    def dirty_counts(self, first=0, count=None) -> np.ndarray:
+        count = self.nlanes - first if count is None else count
+        out = np.zeros(count, dtype=np.uint32)
+        _chk(self.L.wtfgpu_read_dirty_counts(self.ctx, first, count, out.ctypes.data_as(C.POINTER(C.c_uint32))),
+             "read_dirty_counts")
+        return out
+
     def gather_pages(self, lanes, gpas) -> np.ndarray:
         """[n, 4096] u8: each lane's current view of each guest-physical page."""
         lanes = np.ascontiguousarray(lanes, dtype=np.uint32)

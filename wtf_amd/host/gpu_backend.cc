@@ -1046,10 +1046,12 @@ bool GpuBackend_t::RunBatch(const Target_t &Target, const std::vector<std::pair<
   stats_.upload_ms += ms_since(tu);
   stats_.insert_ms += ms_since(t0);
   if (!run_lanes(lanes, &Out, Slots, Slots != nullptr)) return false;
-  {
+  {  // B_exec = instruction + data bytes, testcase bytes, 2 x 4096 per dirty page
     std::vector<uint64_t> nb(n);
-    if (wtfgpu_read_bytes(ctx_, 0, n, nb.data()) == WTFGPU_OK)
-      for (uint64_t b : nb) stats_.alg_bytes += b;
+    std::vector<uint32_t> dc(n);
+    if (wtfgpu_read_bytes(ctx_, 0, n, nb.data()) == WTFGPU_OK &&
+        wtfgpu_read_dirty_counts(ctx_, 0, n, dc.data()) == WTFGPU_OK)
+      for (uint32_t l = 0; l < n; l++) stats_.alg_bytes += nb[l] + 2ull * 4096 * dc[l] + Testcases[l].second;
   }
   const auto tc = Clock::now();
   std::vector<uint32_t> timedout;
@@ -1209,6 +1211,7 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
   if (busy_.empty()) {
     busy_.assign(nlanes_, 0);
     tag_.assign(nlanes_, 0);
+    tc_bytes_.assign(nlanes_, 0);
     lres_.assign(nlanes_, LaneResult{});
     const uint32_t n = parts_n();
     parts_.assign(n, Part{});
@@ -1245,6 +1248,7 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
       reset_view(l);
       busy_[l] = 1;
       tag_[l] = In[i].tag;
+      tc_bytes_[l] = In[i].size;
       lres_[l] = LaneResult{};
     }
     const auto tm = Clock::now();
@@ -1326,11 +1330,13 @@ bool GpuBackend_t::harvest_part(Part &P, const Target_t &Target, std::vector<Str
   if (!fill_results(P.occ, first, P.ex, done, &lres_, &finished)) return false;
   if (finished.empty()) return true;
   const auto tc = Clock::now();
-  {
+  {  // B_exec = instruction + data bytes, testcase bytes, 2 x 4096 per dirty page
     uint32_t lo = finished.front() & ~63u, hi = finished.back() + 1;
     std::vector<uint64_t> nb(hi - lo);
-    if (wtfgpu_read_bytes(ctx_, lo, hi - lo, nb.data()) == WTFGPU_OK)
-      for (uint32_t l : finished) stats_.alg_bytes += nb[l - lo];
+    std::vector<uint32_t> dc(hi - lo);
+    if (wtfgpu_read_bytes(ctx_, lo, hi - lo, nb.data()) == WTFGPU_OK &&
+        wtfgpu_read_dirty_counts(ctx_, lo, hi - lo, dc.data()) == WTFGPU_OK)
+      for (uint32_t l : finished) stats_.alg_bytes += nb[l - lo] + 2ull * 4096 * dc[l - lo] + tc_bytes_[l];
   }
   stats_.bytes_ms += ms_since(tc);
   collect_coverage(finished, lres_);

@@ -188,6 +188,7 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   // streaming state: slot occupancy, the caller's tag per lane, results
   std::vector<uint8_t> busy_;
   std::vector<uint64_t> tag_;
+  std::vector<uint64_t> tc_bytes_;  // the testcase size in each lane (B_exec)
   std::vector<LaneResult> lres_;
   std::vector<uint32_t> cov_lanes_;  // coverage collection buffers (streaming)
   std::vector<uint64_t> cov_rips_;
