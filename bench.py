@@ -390,7 +390,7 @@ def run(a, rank, world, local, tmp):
                     "over its seed corpus)",
             "config": {"workload": TARGETS["tlv_server"][1], "lanes_per_gpu": a.lanes, "limit": a.limit,
                        "max_len": TARGETS["tlv_server"][2], "slice_steps": a.slice_steps or 4096,
-                       "regroup_steps": a.regroup_steps,
+                       "regroup_steps": a.regroup_steps if a.regroup_steps >= 0 else 1024,  # engine default
                        "parallelism": f"shard{world}: one node per GPU (seed + rank), RCCL MAX coverage-map "
                                       f"merge per batch"},
             "instr_per_exec": retired / max(1.0, execs),
