@@ -49,6 +49,11 @@
  *       SYSENTER_*, PAT, EFER, STAR, LSTAR, CSTAR, SFMASK, FS/GS/KERNEL_GS
  *       base, TSC_AUX); any other MSR, a non-canonical base / entry point or
  *       upper bits in SFMASK / TSC_AUX is #GP(0); EFER.LMA is read-only.
+ *   U22 SSE / SSE2: the legacy-encoded integer and data-movement subset (see
+ *       exec_sse); MMX, SSE floating-point arithmetic, SSE3+ and VEX are
+ *       UNIMPLEMENTED. #UD if CR0.EM or !CR4.OSFXSR, #NM if CR0.TS, #GP(0) for a
+ *       misaligned 16-byte operand of an aligned form; the checks run in that
+ *       order, before any memory access.
  */
 #include "x86_oracle.h"
 #include <stdlib.h>
@@ -947,6 +952,429 @@ enum { X_OK = 0, X_FAULT = 1, X_UNIMPL = 2, X_INT3 = 3, X_HLT = 4, X_CR3 = 5, X_
     if (x) return X_FAULT;                                                                       \
   } while (0)
 
+/* ---------------- SSE / SSE2 (U22) ----------------
+ * The legacy-encoded integer and data-movement subset compilers emit for
+ * x86-64 (SSE2 baseline): 128-bit moves, scalar / half moves, movd / movq,
+ * logic, integer add / sub / saturate / compare / min / max / multiply,
+ * shifts, shuffles, unpacks, packs, mask extraction, ldmxcsr / stmxcsr, fences,
+ * movnti. MMX (no-prefix 0f 6x / dx-fx), SSE floating-point arithmetic, SSE3+
+ * and VEX are outside the subset (UNIMPLEMENTED). Faults: #UD when CR0.EM = 1
+ * or CR4.OSFXSR = 0, #NM when CR0.TS = 1, #GP(0) for a 16-byte memory operand
+ * that is not 16-byte aligned (all but movups / movupd / movdqu). */
+typedef struct { u8 b[16]; } x128;
+
+static x128 xreg(orc_machine *m, u32 r) {
+  x128 v;
+  memcpy(v.b, m->r.xmm[r & 15], 16);
+  return v;
+}
+static void xput(orc_machine *m, u32 r, x128 v) { memcpy(m->r.xmm[r & 15], v.b, 16); }
+static u64 el(const x128 *v, int i, int w) {
+  u64 x = 0;
+  memcpy(&x, v->b + i * w, (size_t)w);
+  return x;
+}
+static void elput(x128 *v, int i, int w, u64 x) { memcpy(v->b + i * w, &x, (size_t)w); }
+static i64 sel(const x128 *v, int i, int w) { return (i64)sxn(el(v, i, w), w); }
+static u64 satu(i64 x, int w) {
+  const i64 hi = (i64)szmask(w);
+  return (u64)(x < 0 ? 0 : x > hi ? hi : x);
+}
+static u64 sats(i64 x, int w) {
+  const i64 hi = (i64)(szmask(w) >> 1), lo = -hi - 1;
+  return (u64)(x < lo ? lo : x > hi ? hi : x) & szmask(w);
+}
+
+/* element-wise op `k` on w-byte elements */
+enum { EW_ADD, EW_SUB, EW_ADDUS, EW_SUBUS, EW_ADDS, EW_SUBS, EW_MINU, EW_MAXU, EW_MINS, EW_MAXS, EW_EQ, EW_GT,
+       EW_AVG, EW_MULLO, EW_MULHS, EW_MULHU };
+static x128 ewise(int k, int w, const x128 *a, const x128 *b) {
+  x128 r;
+  for (int i = 0; i < 16 / w; i++) {
+    const u64 x = el(a, i, w), y = el(b, i, w);
+    const i64 sx = sel(a, i, w), sy = sel(b, i, w);
+    u64 v = 0;
+    switch (k) {
+    case EW_ADD: v = x + y; break;
+    case EW_SUB: v = x - y; break;
+    case EW_ADDUS: v = satu((i64)(x + y), w); break;
+    case EW_SUBUS: v = satu((i64)x - (i64)y, w); break;
+    case EW_ADDS: v = sats(sx + sy, w); break;
+    case EW_SUBS: v = sats(sx - sy, w); break;
+    case EW_MINU: v = x < y ? x : y; break;
+    case EW_MAXU: v = x > y ? x : y; break;
+    case EW_MINS: v = sx < sy ? x : y; break;
+    case EW_MAXS: v = sx > sy ? x : y; break;
+    case EW_EQ: v = x == y ? ~0ULL : 0; break;
+    case EW_GT: v = sx > sy ? ~0ULL : 0; break;
+    case EW_AVG: v = (x + y + 1) >> 1; break;
+    case EW_MULLO: v = (u64)(sx * sy); break;
+    case EW_MULHS: v = (u64)((sx * sy) >> 16); break;
+    default: v = (x * y) >> 16; break;
+    }
+    elput(&r, i, w, v & szmask(w));
+  }
+  return r;
+}
+/* interleave the low (hi = 0) or high halves of a and b in w-byte elements */
+static x128 unpack(int w, int hi, const x128 *a, const x128 *b) {
+  x128 r;
+  const int n = 8 / w;
+  for (int i = 0; i < n; i++) {
+    elput(&r, 2 * i, w, el(a, i + hi * n, w));
+    elput(&r, 2 * i + 1, w, el(b, i + hi * n, w));
+  }
+  return r;
+}
+/* shift every w-byte element by cnt: 0 logical right, 1 arithmetic right, 2 left */
+static x128 shift_el(int kind, int w, const x128 *a, u64 cnt) {
+  x128 r;
+  const u64 bits = 8 * (u64)w;
+  for (int i = 0; i < 16 / w; i++) {
+    const u64 x = el(a, i, w);
+    u64 v;
+    if (kind == 1) v = (u64)(sel(a, i, w) >> (cnt >= bits ? bits - 1 : cnt));
+    else if (cnt >= bits) v = 0;
+    else v = kind == 0 ? x >> cnt : x << cnt;
+    elput(&r, i, w, v & szmask(w));
+  }
+  return r;
+}
+
+/* the r/m operand as 128 bits: an xmm register, or n bytes of memory
+ * (zero-extended; n = 16 needs 16-byte alignment when `align`) */
+static int xsrc(orc_machine *m, insn *d, int n, int align, x128 *v) {
+  memset(v->b, 0, 16);
+  if (!d->is_mem) {
+    *v = xreg(m, d->rm);
+    return 0;
+  }
+  if (align && (d->ea & 15)) {
+    fault(m, WTFGPU_VEC_GP, 0);
+    return -1;
+  }
+  return vread(m, d->ea, (u32)n, v->b);
+}
+static int xstore(orc_machine *m, insn *d, int n, int align, const x128 *v) {
+  if (align && (d->ea & 15)) {
+    fault(m, WTFGPU_VEC_GP, 0);
+    return -1;
+  }
+  return vwrite(m, d->ea, (u32)n, v->b);
+}
+
+static int sse_opcode(u32 op) {
+  return (op >= 0x10 && op <= 0x17) || op == 0x28 || op == 0x29 || op == 0x2b || (op >= 0x50 && op <= 0x7f) ||
+         op == 0xae || op == 0xc3 || (op >= 0xc4 && op <= 0xc6) || op >= 0xd0;
+}
+
+static int exec_sse(orc_machine *m, insn *d) {
+  const u32 op = d->op, r3 = d->reg & 7;
+  const int pc = d->rep == 0xf3 ? 2 : d->rep == 0xf2 ? 3 : d->pfx66 ? 1 : 0; /* none, 66, f3, f2 */
+  const int mem = d->is_mem;
+  const u8 imm = d->bytes[d->len - 1];
+  x128 a, b, r;
+  u64 v;
+  if (op == 0xc3) { /* movnti m32/64, r (SSE2 general-register store) */
+    if (pc != 0) return X_UNIMPL;
+    if (!mem) {
+      fault(m, WTFGPU_VEC_UD, 0);
+      return X_FAULT;
+    }
+    const int sz = d->rexw ? 8 : 4;
+    v = m->r.gpr[d->reg] & szmask(sz);
+    return vwrite(m, d->ea, (u32)sz, &v) ? X_FAULT : X_OK;
+  }
+  if (op == 0xae) {
+    if (pc != 0) return X_UNIMPL;
+    if (!mem) return r3 >= 5 ? X_OK : X_UNIMPL; /* lfence / mfence / sfence */
+    if (r3 != 2 && r3 != 3) return X_UNIMPL;
+  }
+  /* encodings outside the subset */
+  {
+    int ok;
+    if (op >= 0x60 && op <= 0x6d) ok = pc == 1;
+    else if (op == 0x6e || op == 0x74 || op == 0x75 || op == 0x76 || op == 0xc4 || op == 0xc5 || op == 0xd6)
+      ok = pc == 1;
+    else if (op == 0x6f || op == 0x7f) ok = pc == 1 || pc == 2;
+    else if (op == 0x70) ok = pc != 0;
+    else if (op >= 0x71 && op <= 0x73) ok = pc == 1;
+    else if (op == 0x7e) ok = pc == 1 || pc == 2;
+    else if (op == 0x10 || op == 0x11) ok = 1;
+    else if ((op >= 0x12 && op <= 0x17) || op == 0x28 || op == 0x29 || op == 0x2b || op == 0x50 || op == 0xc6 ||
+             (op >= 0x54 && op <= 0x57))
+      ok = pc <= 1;
+    else if (op == 0xae) ok = 1;
+    else if (op >= 0xd0) {
+      ok = pc == 1 && op != 0xd0 && op != 0xd6 && op != 0xe6 && op != 0xe7 && op != 0xf0 && op != 0xf7 &&
+           op != 0xff;
+      if (op == 0xd6 || op == 0xe7) ok = pc == 1;
+    } else ok = 0;
+    if (!ok) return X_UNIMPL;
+  }
+  /* register-only and memory-only forms */
+  {
+    const int reg_only = (op >= 0x71 && op <= 0x73) || op == 0x50 || op == 0xd7 || op == 0xc5;
+    const int mem_only = op == 0x13 || op == 0x17 || op == 0x2b || op == 0xe7 || op == 0xae ||
+                         ((op == 0x12 || op == 0x16) && pc == 1);
+    if ((reg_only && mem) || (mem_only && !mem)) {
+      fault(m, WTFGPU_VEC_UD, 0);
+      return X_FAULT;
+    }
+    if (op >= 0x71 && op <= 0x73 && !((r3 == 2 || r3 == 4 || r3 == 6) && op != 0x73) &&
+        !(op == 0x73 && (r3 == 2 || r3 == 3 || r3 == 6 || r3 == 7)))
+      return X_UNIMPL;
+  }
+  if (m->r.cr0 & 4 || !(m->r.cr4 & 0x200)) {
+    fault(m, WTFGPU_VEC_UD, 0);
+    return X_FAULT;
+  }
+  if (m->r.cr0 & 8) {
+    fault(m, 7, 0); /* #NM */
+    return X_FAULT;
+  }
+  a = xreg(m, d->reg);
+  switch (op) {
+  case 0x10: /* movups / movupd / movss / movsd load */
+    if (pc <= 1) {
+      if (xsrc(m, d, 16, 0, &b)) return X_FAULT;
+      xput(m, d->reg, b);
+    } else {
+      const int n = pc == 2 ? 4 : 8;
+      if (xsrc(m, d, n, 0, &b)) return X_FAULT;
+      if (mem) xput(m, d->reg, b); /* zero-extended */
+      else {
+        memcpy(a.b, b.b, (size_t)n);
+        xput(m, d->reg, a);
+      }
+    }
+    return X_OK;
+  case 0x11: /* stores of 0x10 */
+    if (pc <= 1) {
+      if (mem) return xstore(m, d, 16, 0, &a) ? X_FAULT : X_OK;
+      xput(m, d->rm, a);
+    } else {
+      const int n = pc == 2 ? 4 : 8;
+      if (mem) return xstore(m, d, n, 0, &a) ? X_FAULT : X_OK;
+      r = xreg(m, d->rm);
+      memcpy(r.b, a.b, (size_t)n);
+      xput(m, d->rm, r);
+    }
+    return X_OK;
+  case 0x12: /* movlps / movlpd m64; movhlps */
+  case 0x16: /* movhps / movhpd m64; movlhps */
+    if (xsrc(m, d, 8, 0, &b)) return X_FAULT;
+    if (op == 0x12) memcpy(a.b, b.b + (mem ? 0 : 8), 8);
+    else memcpy(a.b + 8, b.b, 8);
+    xput(m, d->reg, a);
+    return X_OK;
+  case 0x13:
+  case 0x17:
+    if (op == 0x17) memcpy(a.b, a.b + 8, 8);
+    return xstore(m, d, 8, 0, &a) ? X_FAULT : X_OK;
+  case 0x14:
+  case 0x15:
+    if (xsrc(m, d, 16, 1, &b)) return X_FAULT;
+    xput(m, d->reg, unpack(pc ? 8 : 4, op == 0x15, &a, &b));
+    return X_OK;
+  case 0x28:
+  case 0x6f:
+    if (xsrc(m, d, 16, op == 0x28 || pc == 1, &b)) return X_FAULT;
+    xput(m, d->reg, b);
+    return X_OK;
+  case 0x29:
+  case 0x2b:
+  case 0x7f:
+  case 0xe7:
+    if (mem) return xstore(m, d, 16, op != 0x7f || pc == 1, &a) ? X_FAULT : X_OK;
+    xput(m, d->rm, a);
+    return X_OK;
+  case 0x50: { /* movmskps / movmskpd */
+    b = xreg(m, d->rm);
+    const int w = pc ? 8 : 4;
+    v = 0;
+    for (int i = 0; i < 16 / w; i++) v |= (el(&b, i, w) >> (8 * w - 1)) << i;
+    m->r.gpr[d->reg] = v;
+    return X_OK;
+  }
+  case 0xd7: /* pmovmskb */
+    b = xreg(m, d->rm);
+    v = 0;
+    for (int i = 0; i < 16; i++) v |= (u64)(b.b[i] >> 7) << i;
+    m->r.gpr[d->reg] = v;
+    return X_OK;
+  case 0x54: case 0x55: case 0x56: case 0x57: case 0xdb: case 0xdf: case 0xeb: case 0xef:
+    if (xsrc(m, d, 16, 1, &b)) return X_FAULT;
+    for (int i = 0; i < 16; i++) {
+      const u8 x = a.b[i], y = b.b[i];
+      r.b[i] = (op == 0x54 || op == 0xdb) ? (u8)(x & y) : (op == 0x55 || op == 0xdf) ? (u8)(~x & y)
+             : (op == 0x56 || op == 0xeb) ? (u8)(x | y) : (u8)(x ^ y);
+    }
+    xput(m, d->reg, r);
+    return X_OK;
+  case 0x60: case 0x61: case 0x62: case 0x6c:
+  case 0x68: case 0x69: case 0x6a: case 0x6d: {
+    if (xsrc(m, d, 16, 1, &b)) return X_FAULT;
+    const u32 lo = op & 0xf7;
+    const int w = lo == 0x60 ? 1 : lo == 0x61 ? 2 : lo == 0x62 ? 4 : 8;
+    xput(m, d->reg, unpack(w, op == 0x68 || op == 0x69 || op == 0x6a || op == 0x6d, &a, &b));
+    return X_OK;
+  }
+  case 0x63: case 0x67: case 0x6b: { /* packsswb, packuswb, packssdw */
+    if (xsrc(m, d, 16, 1, &b)) return X_FAULT;
+    const int w = op == 0x6b ? 4 : 2, n = 16 / w;
+    for (int i = 0; i < 2 * n; i++) {
+      const i64 x = i < n ? sel(&a, i, w) : sel(&b, i - n, w);
+      elput(&r, i, w / 2, op == 0x67 ? satu(x, 1) : sats(x, w / 2));
+    }
+    xput(m, d->reg, r);
+    return X_OK;
+  }
+  case 0x64: case 0x65: case 0x66: case 0x74: case 0x75: case 0x76:
+    if (xsrc(m, d, 16, 1, &b)) return X_FAULT;
+    xput(m, d->reg, ewise(op >= 0x74 ? EW_EQ : EW_GT, 1 << ((op & 0xf) % 4), &a, &b));
+    return X_OK;
+  case 0x6e: /* movd / movq xmm, r/m */
+  case 0x7e: {
+    const int n = d->rexw ? 8 : 4;
+    if (op == 0x7e && pc == 2) { /* movq xmm, xmm/m64 */
+      if (xsrc(m, d, 8, 0, &b)) return X_FAULT;
+      memset(b.b + 8, 0, 8);
+      xput(m, d->reg, b);
+      return X_OK;
+    }
+    if (op == 0x6e) {
+      memset(r.b, 0, 16);
+      if (mem) {
+        if (vread(m, d->ea, (u32)n, r.b)) return X_FAULT;
+      } else {
+        v = m->r.gpr[d->rm] & szmask(n);
+        memcpy(r.b, &v, 8);
+      }
+      xput(m, d->reg, r);
+      return X_OK;
+    }
+    v = el(&a, 0, n);
+    if (mem) return vwrite(m, d->ea, (u32)n, &v) ? X_FAULT : X_OK;
+    m->r.gpr[d->rm] = v;
+    return X_OK;
+  }
+  case 0x70: { /* pshufd / pshufhw / pshuflw */
+    if (xsrc(m, d, 16, 1, &b)) return X_FAULT;
+    r = b;
+    if (pc == 1)
+      for (int i = 0; i < 4; i++) elput(&r, i, 4, el(&b, (imm >> (2 * i)) & 3, 4));
+    else
+      for (int i = 0; i < 4; i++) elput(&r, i + (pc == 2 ? 4 : 0), 2, el(&b, ((imm >> (2 * i)) & 3) + (pc == 2 ? 4 : 0), 2));
+    xput(m, d->reg, r);
+    return X_OK;
+  }
+  case 0x71: case 0x72: case 0x73: {
+    b = xreg(m, d->rm);
+    const int w = op == 0x71 ? 2 : op == 0x72 ? 4 : 8;
+    if (op == 0x73 && (r3 == 3 || r3 == 7)) { /* psrldq / pslldq: bytes */
+      memset(r.b, 0, 16);
+      for (int i = 0; i < 16; i++) {
+        const int src = r3 == 3 ? i + imm : i - imm;
+        if (src >= 0 && src < 16) r.b[i] = b.b[src];
+      }
+    } else {
+      r = shift_el(r3 == 2 ? 0 : r3 == 4 ? 1 : 2, w, &b, imm);
+    }
+    xput(m, d->rm, r);
+    return X_OK;
+  }
+  case 0xc4: /* pinsrw */
+    if (mem) {
+      v = 0;
+      if (vread(m, d->ea, 2, &v)) return X_FAULT;
+    } else {
+      v = m->r.gpr[d->rm];
+    }
+    elput(&a, imm & 7, 2, v & 0xffff);
+    xput(m, d->reg, a);
+    return X_OK;
+  case 0xc5: /* pextrw */
+    b = xreg(m, d->rm);
+    m->r.gpr[d->reg] = el(&b, imm & 7, 2);
+    return X_OK;
+  case 0xc6: /* shufps / shufpd */
+    if (xsrc(m, d, 16, 1, &b)) return X_FAULT;
+    if (pc == 0) {
+      elput(&r, 0, 4, el(&a, imm & 3, 4));
+      elput(&r, 1, 4, el(&a, (imm >> 2) & 3, 4));
+      elput(&r, 2, 4, el(&b, (imm >> 4) & 3, 4));
+      elput(&r, 3, 4, el(&b, (imm >> 6) & 3, 4));
+    } else {
+      elput(&r, 0, 8, el(&a, imm & 1, 8));
+      elput(&r, 1, 8, el(&b, (imm >> 1) & 1, 8));
+    }
+    xput(m, d->reg, r);
+    return X_OK;
+  case 0xd6: /* movq xmm/m64, xmm */
+    if (mem) return xstore(m, d, 8, 0, &a) ? X_FAULT : X_OK;
+    memset(a.b + 8, 0, 8);
+    xput(m, d->rm, a);
+    return X_OK;
+  case 0xae: { /* ldmxcsr / stmxcsr */
+    u32 mx = 0;
+    if (r3 == 3) return vwrite(m, d->ea, 4, &m->r.mxcsr) ? X_FAULT : X_OK;
+    if (vread(m, d->ea, 4, &mx)) return X_FAULT;
+    if (mx & ~(m->r.mxcsr_mask ? m->r.mxcsr_mask : 0xffbfu)) {
+      fault(m, WTFGPU_VEC_GP, 0);
+      return X_FAULT;
+    }
+    m->r.mxcsr = mx;
+    return X_OK;
+  }
+  default:
+    break;
+  }
+  /* 66 0f d1-fe: integer arithmetic on xmm, xmm/m128 */
+  if (xsrc(m, d, 16, 1, &b)) return X_FAULT;
+  switch (op) {
+  case 0xd1: case 0xd2: case 0xd3: r = shift_el(0, op == 0xd1 ? 2 : op == 0xd2 ? 4 : 8, &a, el(&b, 0, 8)); break;
+  case 0xe1: case 0xe2: r = shift_el(1, op == 0xe1 ? 2 : 4, &a, el(&b, 0, 8)); break;
+  case 0xf1: case 0xf2: case 0xf3: r = shift_el(2, op == 0xf1 ? 2 : op == 0xf2 ? 4 : 8, &a, el(&b, 0, 8)); break;
+  case 0xd4: r = ewise(EW_ADD, 8, &a, &b); break;
+  case 0xfb: r = ewise(EW_SUB, 8, &a, &b); break;
+  case 0xfc: case 0xfd: case 0xfe: r = ewise(EW_ADD, 1 << (op - 0xfc), &a, &b); break;
+  case 0xf8: case 0xf9: case 0xfa: r = ewise(EW_SUB, 1 << (op - 0xf8), &a, &b); break;
+  case 0xd5: r = ewise(EW_MULLO, 2, &a, &b); break;
+  case 0xe5: r = ewise(EW_MULHS, 2, &a, &b); break;
+  case 0xe4: r = ewise(EW_MULHU, 2, &a, &b); break;
+  case 0xd8: case 0xd9: r = ewise(EW_SUBUS, op - 0xd7, &a, &b); break;
+  case 0xdc: case 0xdd: r = ewise(EW_ADDUS, op - 0xdb, &a, &b); break;
+  case 0xe8: case 0xe9: r = ewise(EW_SUBS, op - 0xe7, &a, &b); break;
+  case 0xec: case 0xed: r = ewise(EW_ADDS, op - 0xeb, &a, &b); break;
+  case 0xda: r = ewise(EW_MINU, 1, &a, &b); break;
+  case 0xde: r = ewise(EW_MAXU, 1, &a, &b); break;
+  case 0xea: r = ewise(EW_MINS, 2, &a, &b); break;
+  case 0xee: r = ewise(EW_MAXS, 2, &a, &b); break;
+  case 0xe0: r = ewise(EW_AVG, 1, &a, &b); break;
+  case 0xe3: r = ewise(EW_AVG, 2, &a, &b); break;
+  case 0xf4: /* pmuludq */
+    elput(&r, 0, 8, el(&a, 0, 4) * el(&b, 0, 4));
+    elput(&r, 1, 8, el(&a, 2, 4) * el(&b, 2, 4));
+    break;
+  case 0xf5: /* pmaddwd */
+    for (int i = 0; i < 4; i++)
+      elput(&r, i, 4, (u64)(sel(&a, 2 * i, 2) * sel(&b, 2 * i, 2) + sel(&a, 2 * i + 1, 2) * sel(&b, 2 * i + 1, 2)) & 0xffffffffULL);
+    break;
+  case 0xf6: /* psadbw */
+    for (int h = 0; h < 2; h++) {
+      u64 s = 0;
+      for (int i = 8 * h; i < 8 * h + 8; i++) s += a.b[i] > b.b[i] ? a.b[i] - b.b[i] : b.b[i] - a.b[i];
+      elput(&r, h, 8, s);
+    }
+    break;
+  default:
+    return X_UNIMPL;
+  }
+  xput(m, d->reg, r);
+  return X_OK;
+}
+
 static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
   (void)mr;
   const u32 op = d->op;
@@ -1351,6 +1779,7 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
   }
 
   if (d->opmap == 1) {
+    if (sse_opcode(op)) return exec_sse(m, d);
     switch (op) {
     case 0x05: /* syscall (64-bit; SDM vol. 2B; U16) */
     case 0x07: /* sysretq */
@@ -1814,6 +2243,8 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
       imm = 1;
     }
     if (b >= 0x80 && b <= 0x8f) imm = 4;
+    if (sse_opcode(b)) has_modrm = 1;
+    if ((b >= 0x70 && b <= 0x73) || (b >= 0xc4 && b <= 0xc6)) imm = 1;
   }
   if (has_modrm) {
     decode_modrm(m, d, mr);

@@ -12,6 +12,8 @@ struct SimResult {
   uint32_t status, vector, error, ovn;
   uint64_t addr;
   uint64_t dirty[64];
+  uint64_t xmm[32];
+  uint32_t mxcsr, pad;
 };
 
 int sim_run(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, const wtfgpu_regs_t *r0,
@@ -42,6 +44,14 @@ int sim_run(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, const 
   P.fs_base = fsb.data();
   P.gs_base = gsb.data();
   P.limit = limit;
+  wtfgpu_regs_t full = *r0;  // cold state: XMM registers, MXCSR
+  LaneSys sys{};
+  sys.cr0 = r0->cr0;
+  sys.cr3 = r0->cr3;
+  sys.cr4 = r0->cr4;
+  sys.efer = r0->efer;
+  P.full = &full;
+  P.sys = &sys;
   uint32_t glo[16], ghi[16];
   Lane L{};
   L.glo = glo;
@@ -133,6 +143,8 @@ int sim_run(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, const 
   out->addr = L.exaddr;
   out->ovn = L.ovn;
   for (uint32_t k = 0; k < L.ovn && k < 64; k++) out->dirty[k] = (uint64_t)ovg[k] << 12;
+  for (int k = 0; k < 16; k++) out->xmm[2 * k] = full.xmm[k][0], out->xmm[2 * k + 1] = full.xmm[k][1];
+  out->mxcsr = full.mxcsr;
   free(pool);
   free(ov);
   return 0;

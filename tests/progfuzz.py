@@ -6,7 +6,9 @@ then runs one random form drawn from the native-vector generator's encodings
 (tests/golden/gen_native_vectors.py). Some blocks are guarded by a forward
 conditional jump, some jump backwards through a counted loop. Programs end in
 int3. Faults (#DE, #PF on a read-only page, ...) end a lane early; both
-engines must agree on that too.
+engines must agree on that too. With sse=True the SSE / SSE2 forms of
+tests/golden/gen_sse_vectors.py join the pool (aligned forms sometimes get a
+misaligned window: #GP) and every lane starts from its own XMM registers.
 """
 from __future__ import annotations
 
@@ -64,10 +66,15 @@ def make_program(rng: random.Random, forms, n_blocks=24) -> bytes:
     return bytes(code[:SLOT])
 
 
-def build(n_programs: int, seed: int):
+def build(n_programs: int, seed: int, sse: bool = False):
     """Returns (AddressSpace, base state, list of (code_va, regs dict))."""
     rng = random.Random(seed)
     forms = gen_forms(random.Random(seed ^ 0xABCDEF))
+    if sse:
+        from tests.golden.gen_sse_vectors import gen_forms as gen_sse_forms
+
+        sse_forms = gen_sse_forms(random.Random(seed ^ 0x55E))
+        forms = forms + sse_forms * 3  # mostly SSE
     sp = AddressSpace()
     progs = []
     for i in range(n_programs):
@@ -89,7 +96,13 @@ def build(n_programs: int, seed: int):
     return sp, st, lanes
 
 
-def oracle_run(sp: AddressSpace, st: dict, lanes, limit=20000, breakpoints=()):
+def lane_xmm(n: int, seed: int):
+    """Initial XMM registers per lane (32 u64 each)."""
+    rng = random.Random(seed ^ 0x3E3)
+    return [[rng.getrandbits(64) for _ in range(32)] for _ in range(n)]
+
+
+def oracle_run(sp: AddressSpace, st: dict, lanes, limit=20000, breakpoints=(), xmm=None):
     """Runs every lane on the CPU oracle; returns per-lane result dicts."""
     from tests.oracle_lib import Oracle
 
@@ -99,10 +112,13 @@ def oracle_run(sp: AddressSpace, st: dict, lanes, limit=20000, breakpoints=()):
     o.set_limit(limit)
     o.set_breakpoints(list(breakpoints))
     out = []
-    for va, regs, flags in lanes:
+    for i, (va, regs, flags) in enumerate(lanes):
         r = regs_from_state(st)
         for k in range(16):
             r.gpr[k] = regs[k]
+        if xmm is not None:
+            for k in range(16):
+                r.xmm[k][0], r.xmm[k][1] = xmm[i][2 * k], xmm[i][2 * k + 1]
         r.rip = va
         r.rflags = flags
         o.restore(base)
@@ -114,5 +130,6 @@ def oracle_run(sp: AddressSpace, st: dict, lanes, limit=20000, breakpoints=()):
             "icount": ex.icount, "gpr": list(rr.gpr), "rflags": rr.rflags, "cov": set(o.coverage()),
             "dirty": set(o.dirty()), "bytes": o.nbytes(),
             "win": o.read_virt(WIN_VA, 0x2000), "stack": o.read_virt(STACK_VA, 0x2000),
+            "xmm": [rr.xmm[k][h] for k in range(16) for h in range(2)], "mxcsr": rr.mxcsr,
         })
     return out

@@ -1,0 +1,190 @@
+"""GPU engine on the SSE / SSE2 subset.
+
+1. Every native SSE vector (tests/golden/sse_vectors.json.gz) as one lane:
+   GPRs, RFLAGS, all 16 XMM registers, MXCSR and the memory window.
+2. The fault / encoding cases of tests/test_sse.py, GPU vs oracle.
+3. Random programs mixing SSE and integer forms, GPU vs oracle lane by lane
+   (exit, registers, XMM, coverage, dirty pages, bytes, memory).
+"""
+import gzip
+import json
+import os
+
+import numpy as np
+import pytest
+
+from tests import progfuzz
+from tests.golden.gen_sse_vectors import window_in
+from tests.oracle_lib import Oracle
+from tests.test_sse import BUF, SSE_FAULT_CASES, layout
+from wtf_amd.abi import EXIT_INT3, regs_from_state
+from wtf_amd.tools.snapshot import AddressSpace, user_state
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CODE_VA = 0x140000000
+
+pytestmark = pytest.mark.gpu
+
+
+def set_xmm(r, xs):
+    for k in range(16):
+        r.xmm[k][0], r.xmm[k][1] = xs[2 * k], xs[2 * k + 1]
+
+
+def get_xmm(r):
+    return [r.xmm[k][h] for k in range(16) for h in range(2)]
+
+
+def test_gpu_matches_native_sse_vectors():
+    from wtf_amd.engine import Engine
+
+    with gzip.open(os.path.join(HERE, "golden", "sse_vectors.json.gz"), "rt") as f:
+        doc = json.load(f)
+    cases = doc["cases"]
+    codes = sorted({c["code"] for c in cases})
+    slot = {c: i for i, c in enumerate(codes)}
+    blob = bytearray(32 * len(codes))
+    for c, i in slot.items():
+        b = bytes.fromhex(c) + b"\xcc"
+        blob[32 * i: 32 * i + len(b)] = b
+    sp = AddressSpace()
+    sp.map_range(CODE_VA, bytes(blob), write=False)
+    buf_va = int(doc["buf_va"], 16)
+    page_va = buf_va & ~0xFFF
+    sp.map(page_va, b"", nx=True)
+    sp.map(page_va + 0x1000, b"", nx=True)
+    n = (len(cases) + 63) // 64 * 64
+    eng = Engine(0)
+    pfns, pblob = sp.phys()
+    eng.load_pool(pfns, pblob)
+    eng.alloc_lanes(n, overlay_pages=4, cov_entries=64)
+    base = regs_from_state(user_state(CODE_VA, 0, sp.cr3))
+    eng.set_initial_state(base)
+    eng.set_limit(0)
+    eng.restore()
+    regs = eng.read_regs(0, n)
+    writes = []
+    for i, c in enumerate(cases):
+        r = regs[i]
+        for k in range(16):
+            r.gpr[k] = int(c["in"][k], 16)
+        r.rip = CODE_VA + 32 * slot[c["code"]]
+        r.rflags = int(c["fl"], 16) | 0x200
+        set_xmm(r, [int(v, 16) for v in c["xin"]])
+        r.mxcsr = int(c["mx"], 16)
+        writes.append((i, buf_va, window_in(int(c["seed"], 16), c["ldmx"])))
+    for i in range(len(cases), n):  # padding lanes run a lone int3
+        regs[i].rip = CODE_VA + 32 * slot[cases[0]["code"]] + len(bytes.fromhex(cases[0]["code"]))
+    eng.write_regs(regs)
+    eng.apply_writes(writes)
+    eng.run()
+    ex = eng.exits()
+    out = eng.read_regs(0, n)
+    fails = []
+    for i, c in enumerate(cases):
+        r = out[i]
+        if ex[i].status != EXIT_INT3 or ex[i].icount != 1:
+            fails.append((c["name"], c["code"], "exit", ex[i].status, ex[i].vector))
+            continue
+        if [r.gpr[k] for k in range(16)] != [int(v, 16) for v in c["out"]]:
+            fails.append((c["name"], c["code"], "gpr"))
+            continue
+        if (r.rflags ^ int(c["flo"], 16)) & 0x8D5:
+            fails.append((c["name"], c["code"], "flags"))
+            continue
+        if get_xmm(r) != [int(v, 16) for v in c["xout"]] or r.mxcsr != int(c["mxo"], 16):
+            fails.append((c["name"], c["code"], "xmm"))
+            continue
+        win = bytearray(window_in(int(c["seed"], 16), c["ldmx"]))
+        for k, v in c["diff"]:
+            win[k] = v
+        if (c["diff"] or i % 5 == 0) and eng.read_virt(i, buf_va, 256) != bytes(win):
+            fails.append((c["name"], c["code"], "mem"))
+    assert not fails, f"{len(fails)}/{len(cases)} mismatches, first: {fails[:6]}"
+
+
+def test_gpu_sse_faults_match_oracle():
+    """Misaligned operands, register-only / memory-only forms, MMX / FP /
+    SSE3 encodings and CR0 / CR4 gating: GPU exits equal the oracle's."""
+    from wtf_amd.engine import Engine
+
+    variants = [(code, None, None) for code, _, _ in SSE_FAULT_CASES]
+    pxor = [0x66, 0x0F, 0xEF, 0xC1]
+    variants += [(pxor, None, 0x370678 & ~0x200), (pxor, 0x80050031 | 4, None), (pxor, 0x80050031 | 8, None),
+                 ([0x0F, 0xAE, 0xF0], 0x80050031 | 8, None)]
+    for code, cr0, cr4 in variants:
+        sp, regs = layout(bytes(code), BUF, bytes(range(256)), cr0=cr0, cr4=cr4)
+        regs.gpr[3] = BUF + 0x10
+        regs.gpr[6] = BUF + 0x13
+        pfns, blob = sp.phys()
+        o = Oracle(pfns=pfns, blob=blob)
+        o.restore(regs)
+        want = o.run()
+        eng = Engine(0)
+        eng.load_pool(pfns, blob)
+        eng.alloc_lanes(64, overlay_pages=4, cov_entries=64)
+        eng.set_initial_state(regs)
+        eng.set_limit(0)
+        eng.restore()
+        eng.run()
+        e = eng.exits(0, 1)[0]
+        got = (e.status, e.vector if e.status == 5 else 0, e.rip, e.icount)
+        exp = (want.status, want.vector if want.status == 5 else 0, want.rip, want.icount)
+        assert got == exp, (bytes(code).hex(), cr0, cr4, got, exp)
+        eng.close()
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_gpu_matches_oracle_on_random_sse_programs(seed):
+    from wtf_amd.engine import Engine
+
+    n = 512
+    sp, st, lanes = progfuzz.build(n, seed=seed, sse=True)
+    xmm = progfuzz.lane_xmm(n, seed)
+    want = progfuzz.oracle_run(sp, st, lanes, xmm=xmm)
+    eng = Engine(0)
+    pfns, blob = sp.phys()
+    eng.load_pool(pfns, blob)
+    eng.alloc_lanes(n, overlay_pages=8, cov_entries=4096)
+    eng.set_initial_state(regs_from_state(st))
+    eng.set_limit(20000)
+    eng.restore()
+    regs = eng.read_regs(0, n)
+    for i, (va, g, flags) in enumerate(lanes):
+        for k in range(16):
+            regs[i].gpr[k] = g[k]
+        regs[i].rip = va
+        regs[i].rflags = flags
+        set_xmm(regs[i], xmm[i])
+    eng.write_regs(regs)
+    stats = eng.run()
+    ex = eng.exits()
+    out = eng.read_regs(0, n)
+    cov, ovf = eng.coverage()
+    nb = eng.nbytes()
+    bad = []
+    for i, w in enumerate(want):
+        e, r = ex[i], out[i]
+        got = (e.status, e.vector if e.status == 5 else 0, e.addr if e.status == 5 else 0, r.rip, e.icount)
+        exp = (w["status"], w["vector"] if w["status"] == 5 else 0, w["addr"] if w["status"] == 5 else 0,
+               w["rip"], w["icount"])
+        if got != exp:
+            bad.append((i, "exit", got, exp))
+        elif [r.gpr[k] for k in range(16)] != w["gpr"] or r.rflags != w["rflags"]:
+            bad.append((i, "regs"))
+        elif get_xmm(r) != w["xmm"] or r.mxcsr != w["mxcsr"]:
+            bad.append((i, "xmm"))
+        elif cov.get(i, set()) != w["cov"]:
+            bad.append((i, "cov"))
+        elif set(eng.dirty(i)) != w["dirty"]:
+            bad.append((i, "dirty"))
+        elif int(nb[i]) != w["bytes"]:
+            bad.append((i, "bytes", int(nb[i]), w["bytes"]))
+        elif i % 8 == 0 and (eng.read_virt(i, progfuzz.WIN_VA, 0x2000) != w["win"] or
+                             eng.read_virt(i, progfuzz.STACK_VA, 0x2000) != w["stack"]):
+            bad.append((i, "memory"))
+    assert not ovf
+    assert stats.lane_retired == sum(w["icount"] for w in want)
+    statuses = np.bincount([w["status"] for w in want], minlength=13)
+    assert statuses[EXIT_INT3] > n // 8, statuses  # most programs run to the end
+    assert not bad, f"{len(bad)}/{n} lanes differ; first: {bad[:4]}"

@@ -27,7 +27,7 @@ enum : u32 {
   O_SHIFT, O_SHXD, O_MULDIV, O_IMUL, O_BT, O_BSF, O_BSR, O_TZCNT, O_LZCNT, O_POPCNT,
   O_CMOV, O_SETCC, O_BSWAP, O_CBW, O_CWD, O_LAHF, O_SAHF, O_FLAGOP, O_NOP, O_JCC, O_JMP,
   O_CALL, O_RET, O_PUSH, O_POP, O_PUSHF, O_POPF, O_LEAVE, O_STRING, O_INT3, O_HLT, O_UD,
-  O_LEA, O_SYS, O_UNIMPL
+  O_LEA, O_SYS, O_SSE, O_UNIMPL
 };
 // operand locations
 enum : u32 {
@@ -46,6 +46,9 @@ struct UOp {
   u64 disp, imm;
   u32 supported, opbytes;
 };
+}  // namespace wtfgpu_dev
+#include "engine_sse.h"  // the SSE / SSE2 subset: sse_valid (decode), sse_exec (exec)
+namespace wtfgpu_dev {
 
 // ---------------------------------------------------------------- registers
 __device__ __forceinline__ u64 getr(const Lane &L, u32 rex, u32 r, u32 sz) {
@@ -157,22 +160,25 @@ __constant__ u32 kMap1[256] = {
 #define BTRW E(O_BT, L_RM, L_GREG, Z_V, Z_V, 1, 1, 0, 1, K_NONE, 0)
 #define SHXD(ik) E(O_SHXD, L_RM, L_GREG, Z_V, Z_V, 1, 1, 0, 1, ik, 0)
 #define UN16 UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN
+#define SSEM E(O_SSE, 0, 0, 0, 0, 0, 0, 0, 1, K_NONE, 0)
+#define SSEI E(O_SSE, 0, 0, 0, 0, 0, 0, 0, 1, K_B, 0)
+#define SSE8 SSEM, SSEM, SSEM, SSEM, SSEM, SSEM, SSEM, SSEM
 __constant__ u32 kMap2[256] = {
     /*00*/ UN, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 1, K_NONE, 0), UN, UN, UN, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN,
     E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, UN, UN, E(O_UD, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, NOPM, UN, UN,
-    /*10*/ UN, UN, UN, UN, UN, UN, UN, UN, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM,
+    /*10*/ SSE8, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM,
     /*20*/ E(O_SYS, L_RM, 0, Z_Q, Z_Q, 0, 1, 0, 1, K_NONE, 0), UN, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 1, K_NONE, 0), UN, UN,
-    UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN,
+    UN, UN, UN, SSEM, SSEM, UN, SSEM, UN, UN, UN, UN,
     /*30*/ E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0),
     E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN,
     /*40*/ CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV,
-    /*50*/ UN16,
-    /*60*/ UN16,
-    /*70*/ UN16,
+    /*50*/ SSE8, SSE8,
+    /*60*/ SSE8, SSE8,
+    /*70*/ SSEI, SSEI, SSEI, SSEI, SSEM, SSEM, SSEM, SSEM, SSE8,
     /*80*/ JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32,
     /*90*/ SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC,
     /*a0*/ UN, UN, UN, E(O_BT, L_RM, L_GREG, Z_V, Z_V, 1, 0, 0, 1, K_NONE, 0), SHXD(K_B), SHXD(K_NONE), UN, UN,
-    /*a8*/ UN, UN, UN, BTRW, SHXD(K_B), SHXD(K_NONE), UN, E(O_IMUL, L_GREG, L_RM, Z_V, Z_V, 1, 1, 0, 1, K_NONE, 0),
+    /*a8*/ UN, UN, UN, BTRW, SHXD(K_B), SHXD(K_NONE), SSEM, E(O_IMUL, L_GREG, L_RM, Z_V, Z_V, 1, 1, 0, 1, K_NONE, 0),
     /*b0*/ E(O_CMPXCHG, L_RM, L_GREG, Z_B, Z_B, 1, 1, 0, 1, K_NONE, 0),
     E(O_CMPXCHG, L_RM, L_GREG, Z_V, Z_V, 1, 1, 0, 1, K_NONE, 0), UN, BTRW, UN, UN,
     E(O_MOVZX, L_GREG, L_RM, Z_V, Z_B, 0, 1, 0, 1, K_NONE, 0), E(O_MOVZX, L_GREG, L_RM, Z_V, Z_W, 0, 1, 0, 1, K_NONE, 0),
@@ -181,11 +187,11 @@ __constant__ u32 kMap2[256] = {
     E(O_BSF, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0), E(O_BSR, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0),
     E(O_MOVSX, L_GREG, L_RM, Z_V, Z_B, 0, 1, 0, 1, K_NONE, 0), E(O_MOVSX, L_GREG, L_RM, Z_V, Z_W, 0, 1, 0, 1, K_NONE, 0),
     /*c0*/ E(O_XADD, L_RM, L_GREG, Z_B, Z_B, 1, 1, 1, 1, K_NONE, 0), E(O_XADD, L_RM, L_GREG, Z_V, Z_V, 1, 1, 1, 1, K_NONE, 0),
-    UN, UN, UN, UN, UN, E(O_SYS, L_RM, 0, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0),
+    UN, SSEM, SSEI, SSEI, SSEI, E(O_SYS, L_RM, 0, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0),
     BSWAP, BSWAP, BSWAP, BSWAP, BSWAP, BSWAP, BSWAP, BSWAP,
-    /*d0*/ UN16,
-    /*e0*/ UN16,
-    /*f0*/ UN16,
+    /*d0*/ SSE8, SSE8,
+    /*e0*/ SSE8, SSE8,
+    /*f0*/ SSE8, SSE8,
 };
 #undef E
 #undef UN
@@ -206,6 +212,9 @@ __constant__ u32 kMap2[256] = {
 #undef BTRW
 #undef SHXD
 #undef UN16
+#undef SSEM
+#undef SSEI
+#undef SSE8
 
 // Instruction bytes as two uniform u64 (SGPR pairs).
 struct IBytes {
@@ -408,6 +417,11 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
   }
   if (u.op == O_ALU && u.sub == 7) u.awrite = 0;  // cmp reads its destination, never writes it
   if (map2) {
+    if (u.op == O_SSE) {  // engine_sse.h: opcode in sub, mandatory-prefix class in bsz
+      u.sub = c;
+      u.bsz = u.rep == 0xf3 ? 2 : u.rep == 0xf2 ? 3 : p66 ? 1 : 0;
+      if (!sse_valid(c, u.bsz, u.is_mem, u.reg & 7)) u.op = O_UNIMPL;
+    }
     if (u.op == O_BT && grp != G_BA) u.sub = c == 0xa3 ? 4 : c == 0xab ? 5 : c == 0xb3 ? 6 : 7;
     if (u.op == O_SHXD) u.sub = (c >= 0xac ? 1u : 0u) | ((c & 1) ? 2u : 0u);  // bit0 shrd, bit1 count in cl
     if (u.op == O_BSF && u.rep == 0xf3) u.op = O_TZCNT;
@@ -788,6 +802,7 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
   next = nrip;
   const u32 op = u.op;
   if (op == O_STRING) return string_op(P, L, u);
+  if (op == O_SSE) return sse_exec(P, L, u, nrip, next);
   if (op == O_LEA && !u.is_mem) {
     set_fault(L, WTFGPU_VEC_UD, 0, 0);
     return X_FAULT;
