@@ -15,7 +15,7 @@ IOCTLS = [0x222003, 0x222007, 0x22200B, 0x22200F, 0x222013, 0x222017, 0x22201B, 
 
 def crafted() -> dict[str, bytes]:
     return {
-        "stack_ret_overrun": testcase(0x222003, b"A" * 512 + b"B" * 80),    # return address -> 0x4242.. (#GP)
+        "stack_ret_overrun": testcase(0x222003, b"A" * 512 + b"B" * 240),   # return address -> 0x4242.. (#GP)
         "stack_gs_cookie": testcase(0x222007, b"A" * 520),                  # cookie -> KeBugCheck2(0xF7)
         "write_what_where_bad": testcase(0x22200B, struct.pack("<QQ", USER_BUF, 0xFFFF800000000000)),
         "write_what_where_ok": testcase(0x22200B, struct.pack("<QQ", USER_BUF + 0x10, USER_BUF + 0x20)),

@@ -26,6 +26,7 @@
  * Compiled with gcc (-mabi=ms: Win64 argument registers) into a flat image at
  * KERNEL_BASE, mapped supervisor-only by wtf_amd/tools/hevd.py.
  */
+#include "sse_rt.h"
 typedef unsigned long long u64;
 typedef unsigned int u32;
 typedef unsigned short u16;
@@ -37,14 +38,11 @@ typedef unsigned char u8;
 
 /* ---- freestanding helpers (gcc may emit calls to these) */
 __attribute__((used)) void *memcpy(void *d, const void *s, u64 n) {
-  u8 *dd = d;
-  const u8 *ss = s;
-  for (u64 i = 0; i < n; i++) dd[i] = ss[i];
+  sse_copy(d, s, n);
   return d;
 }
 __attribute__((used)) void *memset(void *d, int c, u64 n) {
-  u8 *dd = d;
-  for (u64 i = 0; i < n; i++) dd[i] = (u8)c;
+  sse_fill(d, c, n);
   return d;
 }
 
@@ -318,10 +316,10 @@ __asm__(".globl KiSystemCall64\n"
         "  mov %gs:0x1a8, %rsp\n"
         "  push %rcx\n"
         "  push %r11\n"
-        "  sub $0x28, %rsp\n"
+        "  sub $0x20, %rsp\n"        /* home space; rsp = 8 mod 16 at the callee's entry */
         "  mov %r10, %rcx\n"
         "  call NtDeviceIoControlFile\n"
-        "  add $0x28, %rsp\n"
+        "  add $0x20, %rsp\n"
         "  pop %r11\n"
         "  pop %rcx\n"
         "  mov %gs:0x10, %rsp\n"

@@ -17,6 +17,7 @@
  * failure routine (what __fastfail reaches in the kernel,
  * nt!KiRaiseSecurityCheckFailure, crash_detection_umode.cc:135-150).
  */
+#include "sse_rt.h"
 typedef unsigned long long u64;
 typedef unsigned int u32;
 typedef unsigned short u16;
@@ -79,7 +80,7 @@ __attribute__((noinline)) static void *Malloc(u64 Size) {
   G.FreeHead = *(u64 *)Page;
   *(u64 *)Page = 0;
   u8 *P = (u8 *)(((u64)Page + 0x1000 - Size) & ~7ull);
-  for (u64 i = 0; i < Size; i++) P[i] = 0;
+  sse_fill(P, 0, Size);
   return P;
 }
 
@@ -95,9 +96,7 @@ __attribute__((noinline)) static void Free(void *P) {
   G.FreeHead = Off / HEAP_STRIDE + 1;
 }
 
-static void Memcpy(u8 *Dst, const u8 *Src, u64 Size) {
-  for (u64 i = 0; i < Size; i++) Dst[i] = Src[i];
-}
+static void Memcpy(u8 *Dst, const u8 *Src, u64 Size) { sse_copy(Dst, Src, Size); }
 
 static void DeleteChunk(struct Chunk *C) {
   if (!C) return;

@@ -115,7 +115,7 @@ def build_space(work_dir: str):
     sp.map(KPCR, bytes(kpcr), user=False, nx=True)
     for i in range(KSTACK_PAGES):
         sp.map(KSTACK + i * PAGE, b"", user=False, nx=True)
-    rsp = STACK_TOP - 0x1000 - 0x48  # UserMain's frame: sub rsp, 0x48 before the call
+    rsp = STACK_TOP - 0x1000 - 0x50  # UserMain's frame (sub rsp, 0x48 from an entry rsp = 8 mod 16)
     # DeviceIoControl(handle, code, in, insize, out, outsize, &returned, NULL): args 4..7
     returned = rsp + 0x40
     sp.write(rsp + 0x20, struct.pack("<QQQQ", USER_BUF, 0x400, returned, 0))

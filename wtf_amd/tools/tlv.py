@@ -34,7 +34,9 @@ HEAP_SLOTS = 64
 HEAP_STRIDE = 0x2000
 PACKET_VA = 0x300000000
 STACK_TOP = 0x7FF000000000
-CFLAGS = ["-O2", "-ffreestanding", "-fpie", "-fvisibility=hidden", "-mabi=ms", "-mgeneral-regs-only",
+# gcc's default x86-64 code generation (SSE2 baseline): the engine runs the
+# SSE / SSE2 subset (U22), so the guests are not restricted to general registers
+CFLAGS = ["-O2", "-ffreestanding", "-fpie", "-fvisibility=hidden", "-mabi=ms",
           "-mno-red-zone", "-fno-stack-protector", "-fcf-protection=none", "-fno-tree-loop-distribute-patterns",
           "-fno-asynchronous-unwind-tables", "-nostdlib", "-static", "-Wl,--build-id=none"]
 
