@@ -31,6 +31,15 @@
 //   kdmp <dump> [gva...]      wtf_amd/host/kdmp.cc in oracle/ref_kdmp_dump.cc's
 //                             output format (TYPE / CR3 / RIP / PAGE / VT lines),
 //                             for comparison with oracle/_ref/kdmp_ref
+// Both builds (the reference through yas and socket.h's serializers, this
+// repository through wtf_amd/host/wire.cc):
+//   wire-testcase <hex>       the master's Testcase message (server.h:720-737)
+//   wire-result <hex> <idx> <crashname|-> [rip...]
+//                             the client's Result message (client.cc:187-200):
+//                             testcase, coverage set, TestcaseResult_t
+//   wire-decode <hex>         a Result message decoded: TC / RES / COV lines
+//                             (COV sorted)
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -43,8 +52,10 @@
 #ifdef WTF_AMD_HOST
 #include "../wtf_amd/host/blake3_lite.h"
 #include "../wtf_amd/host/kdmp.h"
+#include "../wtf_amd/host/wire.h"
 #include "../wtf_amd/host/wtf_api.h"
 #else
+#include "socket.h"
 #include "backend.h"
 #include "corpus.h"
 #include "mutator.h"
@@ -133,9 +144,85 @@ static std::vector<uint8_t> unhex(const char *p) {
   return b;
 }
 
+static TestcaseResult_t result_of(int idx, const char *name) {
+  switch (idx) {
+    case 0: return Ok_t();
+    case 1: return Timedout_t();
+    case 2: return Cr3Change_t();
+    default: return Crash_t(std::string(name) == "-" ? "" : name);
+  }
+}
+
+static std::string bytes_hex(const std::string &s) {
+  std::string o;
+  char b[3];
+  for (unsigned char c : s) {
+    snprintf(b, sizeof(b), "%02x", c);
+    o += b;
+  }
+  return o;
+}
+
+static int cmd_wire(int argc, char **argv) {
+  const std::string cmd = argv[1];
+  const auto tc = unhex(argv[2]);
+  const std::string T(tc.begin(), tc.end());
+  if (cmd == "wire-testcase") {
+#ifdef WTF_AMD_HOST
+    printf("%s\n", bytes_hex(wtfgpu_host::wire::EncodeTestcase(tc.data(), tc.size())).c_str());
+#else
+    yas::mem_ostream Os;
+    yas::binary_oarchive<decltype(Os), YasFlags> Oa(Os);
+    Oa &T;
+    const auto &Buf = Os.get_intrusive_buffer();
+    printf("%s\n", bytes_hex(std::string(Buf.data, Buf.size)).c_str());
+#endif
+    return 0;
+  }
+  if (cmd == "wire-result" && argc >= 5) {
+    const TestcaseResult_t R = result_of(atoi(argv[3]), argv[4]);
+    std::vector<uint64_t> Cov;
+    for (int i = 5; i < argc; i++) Cov.push_back(strtoull(argv[i], nullptr, 0));
+#ifdef WTF_AMD_HOST
+    printf("%s\n", bytes_hex(wtfgpu_host::wire::EncodeResult(tc.data(), tc.size(), Cov, R)).c_str());
+#else
+    tsl::robin_set<Gva_t> Set;
+    for (uint64_t g : Cov) Set.emplace(Gva_t(g));
+    yas::mem_ostream Os;
+    yas::binary_oarchive<decltype(Os), YasFlags> Oa(Os);
+    Oa &T &Set &R;
+    const auto &Buf = Os.get_intrusive_buffer();
+    printf("%s\n", bytes_hex(std::string(Buf.data, Buf.size)).c_str());
+#endif
+    return 0;
+  }
+  if (cmd == "wire-decode") {
+    std::string Tc;
+    std::vector<uint64_t> Cov;
+    TestcaseResult_t R;
+#ifdef WTF_AMD_HOST
+    if (!wtfgpu_host::wire::DecodeResult(T, Tc, Cov, R)) return 1;
+#else
+    tsl::robin_set<Gva_t> Set;
+    yas::mem_istream Is(tc.data(), tc.size());
+    yas::binary_iarchive<decltype(Is), YasFlags> Ia(Is);
+    Ia &Tc &Set &R;
+    for (const Gva_t &g : Set) Cov.push_back(g.U64());
+#endif
+    std::sort(Cov.begin(), Cov.end());
+    printf("TC %s\nRES %zu %s\nCOV", bytes_hex(Tc).c_str(), R.index(),
+           std::holds_alternative<Crash_t>(R) ? std::get<Crash_t>(R).CrashName.c_str() : "");
+    for (uint64_t g : Cov) printf(" %llx", (unsigned long long)g);
+    printf("\n");
+    return 0;
+  }
+  return 2;
+}
+
 int main(int argc, char **argv) {
   if (argc < 2) return 2;
   const std::string cmd = argv[1];
+  if (cmd.rfind("wire-", 0) == 0 && argc >= 3) return cmd_wire(argc, argv);
 #ifdef WTF_AMD_HOST
   if (cmd == "xof" && argc == 4) {
     const auto b = unhex(argv[2]);

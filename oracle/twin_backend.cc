@@ -14,6 +14,7 @@
 
 #include "../include/wtfgpu.h"
 #include "../wtf_amd/host/runner.h"
+#include "../wtf_amd/host/remote.h"
 #include "../wtf_amd/host/wtf_api.h"
 #include "x86_oracle.h"
 #include "../wtf_amd/host/kdmp.h"
@@ -328,6 +329,7 @@ int main(int argc, char **argv) {
   setvbuf(stdout, nullptr, _IOLBF, 0);
   RunnerOptions O;
   if (!ParseRunnerArgs(argc, argv, O)) return 2;
+  if (O.mode == "master") return MasterMain(O);
   Options_t Opts;
   CpuState_t State;
   if (!LoadTarget(O, Opts, State)) return 1;

@@ -3,18 +3,23 @@
 //   wtfgpu fuzz --name tlv_server --target targets/tlv --lanes 65536 --runs N --seed 1337
 //   wtfgpu fuzz ... --device r --rank r --world n --nccl-id-file /tmp/id   (one process per GPU:
 //       shard r mutates with seed + r; coverage maps merged with RCCL MAX after every batch)
+//   wtfgpu master --name tlv_server --target targets/tlv --address tcp://127.0.0.1:31337 --nodes 8 --batched
+//   wtfgpu fuzz --name tlv_server --target targets/tlv --lanes 65536 --address tcp://127.0.0.1:31337 --batched
+//       (a master process and one node per GPU over the wire protocol, remote.h / wire.h)
 // The same runner drives the oracle twin (oracle/twin_backend.cc) for parity.
 #include <cstdio>
 #include <memory>
 
 #include "gpu_backend.h"
 #include "rccl_exchange.h"
+#include "remote.h"
 #include "runner.h"
 
 int main(int argc, char **argv) {
   setvbuf(stdout, nullptr, _IOLBF, 0);
   wtfgpu_host::RunnerOptions O;
   if (!wtfgpu_host::ParseRunnerArgs(argc, argv, O)) return 2;
+  if (O.mode == "master") return wtfgpu_host::MasterMain(O);  // no GPU: corpus + mutator + nodes
   Options_t Opts;
   CpuState_t State;
   if (!wtfgpu_host::LoadTarget(O, Opts, State)) return 1;

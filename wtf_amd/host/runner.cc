@@ -1,5 +1,6 @@
 // runner.cc — see runner.h.
 #include "runner.h"
+#include "remote.h"
 
 #include <algorithm>
 #include <atomic>
@@ -126,7 +127,7 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
       }
       return argv[++i];
     };
-    if (a == "run" || a == "fuzz") O.mode = a;
+    if (a == "run" || a == "fuzz" || a == "master") O.mode = a;
     else if (a == "--name") O.name = next("--name");
     else if (a == "--target") O.target = next("--target");
     else if (a == "--input") O.input = next("--input");
@@ -149,6 +150,9 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
     else if (a == "--world") O.world = atoi(next("--world"));
     else if (a == "--exchange") O.exchange = next("--exchange");
     else if (a == "--nccl-id-file") O.nccl_id_file = next("--nccl-id-file");
+    else if (a == "--address") O.address = next("--address");
+    else if (a == "--nodes") O.nodes = atoi(next("--nodes"));
+    else if (a == "--batched") O.batched = true;
     else {
       fprintf(stderr, "unknown argument %s\n", a.c_str());
       return false;
@@ -158,10 +162,15 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
     fprintf(stderr, "--rank must be in [0, --world)\n");
     return false;
   }
+  if (O.mode == "master" && (O.address.empty() || O.nodes < 1)) {
+    fprintf(stderr, "master needs --address and --nodes >= 1\n");
+    return false;
+  }
   if (O.name.empty() || O.target.empty()) {
-    fprintf(stderr, "usage: [run|fuzz] --name <target> --target <dir> [--input p] [--results f] [--limit n]\n"
+    fprintf(stderr, "usage: [run|fuzz|master] --name <target> --target <dir> [--input p] [--results f] [--limit n]\n"
                     "       [--lanes n] [--overlay-pages k] [--runs n] [--seconds s] [--seed s] [--full-coverage]\n"
-                    "       [--serial-mutation] [--slice-steps s] [--regroup-steps r] [--rank r --world n [--exchange host:port | --nccl-id-file f]]\n");
+                    "       [--serial-mutation] [--slice-steps s] [--regroup-steps r] [--rank r --world n [--exchange host:port | --nccl-id-file f]]\n"
+                    "       [--address tcp://ip:port|unix://path [--batched] [--nodes k]]\n");
     return false;
   }
   return true;
@@ -282,6 +291,9 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
               secs_since(t0));
     return 0;
   }
+
+  // ---- fuzz against a remote master (wire.h): the client loop
+  if (!O.address.empty()) return NodeMain(O, Exec, *Target, Slots);
 
   // ---- fuzz: in-process master + batched node
   FuzzSession F(O, Exec, *Target, Slots, X);
@@ -573,6 +585,11 @@ void FuzzSession::Account(const uint8_t *Tc, size_t Size, const LaneResult &L) {
   // included, joins the corpus after arming the mutator's cross-over
   // (server.h:816-853)
   if (!L.new_coverage.empty() && !std::holds_alternative<Timedout_t>(L.result)) {
+    // admitted only if the master's aggregate grows: nodes attribute against
+    // their own aggregates, which lack what other nodes found
+    const size_t Before = Coverage_.size();
+    Coverage_.insert(L.new_coverage.begin(), L.new_coverage.end());
+    if (Coverage_.size() == Before) return;
     Testcase_t Tcase(Tc, Size);
     Mutator_->OnNewCoverage(Tcase);
     LastNewCov_.assign((const char *)Tc, Size);

@@ -101,7 +101,7 @@ class CoverageExchange_t {
 };
 
 struct RunnerOptions {
-  std::string mode = "run";  // run | fuzz
+  std::string mode = "run";  // run | fuzz | master
   std::string name;          // target name
   std::string target;        // dir with state/, inputs/, outputs/, crashes/
   std::string input;         // run: file or directory (default <target>/inputs)
@@ -129,6 +129,10 @@ struct RunnerOptions {
   int rank = 0, world = 1;         // fuzz: shard rank of world (one node per GPU)
   std::string exchange = "127.0.0.1:31337";  // TCP coverage exchange (CPU shards): rank 0 listens here
   std::string nccl_id_file;        // GPU shards: RCCL unique id file (rank 0 writes it)
+  // the wire protocol (remote.h, wire.h): `master` listens, `fuzz` dials
+  std::string address;             // tcp://ip:port or unix://path
+  int nodes = 1;                   // master: nodes to wait for
+  bool batched = false;            // N testcases per round trip (else the reference's one)
 };
 
 struct FuzzStats {
@@ -207,6 +211,7 @@ class FuzzSession {
   bool HaveNewCov_ = false;
   std::future<TcBatch> Next_;
   std::unordered_set<std::string> CrashNames_;
+  std::unordered_set<uint64_t> Coverage_;  // the master's aggregate (server.h:816-854)
   FuzzStats S_;
   std::chrono::steady_clock::time_point t0_;
   // streaming (RunnerOptions::slice != 0 on an executor that streams)
