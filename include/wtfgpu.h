@@ -70,7 +70,8 @@ enum wtfgpu_status {
   WTFGPU_EXIT_STOPPED = 9,    /* host called Stop(); result kept on the host */
   WTFGPU_EXIT_IDLE = 10,      /* lane holds no testcase */
   WTFGPU_EXIT_STOP_OK = 11,   /* a device action stopped the lane with Ok_t() (feed drained, STOP_OK) */
-  WTFGPU_EXIT_FEED_FAULT = 12 /* a device FEED action could not write its chunk (engine error) */
+  WTFGPU_EXIT_FEED_FAULT = 12, /* a device FEED action could not write its chunk (engine error) */
+  WTFGPU_EXIT_STOP_ARGS = 13   /* a STOP_ARGS action stopped the lane; its arguments: wtfgpu_read_stop_args */
 };
 
 /* x86 exception vectors reported in wtfgpu_exit_t.vector. */
@@ -206,6 +207,14 @@ enum wtfgpu_bp_action_kind {
   /* Stop(Ok_t()): the lane exits with WTFGPU_EXIT_STOP_OK (a handler that
    * only ends the testcase, fuzzer_hevd.cc:64-73) */
   WTFGPU_BPACT_STOP_OK = 5,
+  /* A handler that ends the testcase with a result computed from the hooked
+   * function's arguments (nt!KeBugCheck2 -> Crash_t("crash-<code>-<p0>..."),
+   * fuzzer_hevd.cc:114-128): the lane's first `value` (<= 6) Win64 arguments
+   * (rcx, rdx, r8, r9, [rsp+0x28], [rsp+0x30]; GetArg, backend.cc:168-192)
+   * are kept for wtfgpu_read_stop_args and the lane exits with
+   * WTFGPU_EXIT_STOP_ARGS at the breakpoint's rip; a stack argument that does
+   * not translate leaves the hit to the host handler. */
+  WTFGPU_BPACT_STOP_ARGS = 6,
 };
 typedef struct wtfgpu_bp_action {
   uint64_t gva;
@@ -219,6 +228,9 @@ int wtfgpu_set_breakpoint_actions(wtfgpu_ctx *ctx, const wtfgpu_bp_action_t *act
  * seeds[i], or written from it (write != 0), so host handlers and the device
  * action share one chain. Restore resets them to the initial seed. */
 int wtfgpu_lane_seeds(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, uint64_t *seeds, int write);
+/* The arguments a STOP_ARGS action kept: 6 u64 per lane of the list (lanes
+ * whose last exit is WTFGPU_EXIT_STOP_ARGS). */
+int wtfgpu_read_stop_args(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, uint64_t *out6);
 /* Per-lane input feed of lanes [first, first+count): lane first+i owns
  * bytes[offsets[i] .. offsets[i+1]) (count+1 non-decreasing offsets), a
  * sequence of chunks each stored as a little-endian u32 size and that many
@@ -350,6 +362,19 @@ int wtfgpu_read_coverage(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, uint32
 /* Add RIPs to the coverage map (aggregate coverage). */
 int wtfgpu_commit_coverage(wtfgpu_ctx *ctx, const uint64_t *rips, uint64_t n);
 int wtfgpu_reset_coverage(wtfgpu_ctx *ctx);
+/* Edge coverage (--edges; RecordEdge, bochscpu_backend.cc:699-728): every
+ * conditional near branch (taken or not) and indirect near jmp / call adds
+ * splitmix64_finaliser(rip) ^ next_rip to the coverage values, next to the
+ * rips. Values outside code pages (edges, rips elsewhere) live in a per-GPU
+ * set that wtfgpu_commit_coverage grows; they are not part of the RCCL map. */
+int wtfgpu_set_edges(wtfgpu_ctx *ctx, int on);
+/* Rip traces (`wtf run --trace-type rip`, BochscpuBackend_t::SetTraceFile /
+ * BeforeExecutionHook, bochscpu_backend.cc:506-520, :799-815): every lane logs
+ * the rips it is about to execute, up to per_lane of them (0 = off), reset by
+ * restore. wtfgpu_read_trace copies min(count, per_lane, cap) rips of a lane;
+ * *n gets the count (larger than per_lane: the trace was truncated). */
+int wtfgpu_set_trace(wtfgpu_ctx *ctx, uint32_t per_lane);
+int wtfgpu_read_trace(wtfgpu_ctx *ctx, uint32_t lane, uint64_t *rips, uint64_t cap, uint64_t *n);
 /* Device pointer + size of the uint8 coverage map (for an RCCL MAX all-reduce). */
 int wtfgpu_coverage_device_map(wtfgpu_ctx *ctx, void **dev_ptr, uint64_t *bytes);
 /* After a MAX all-reduce of the map (other shards' coverage merged in): the

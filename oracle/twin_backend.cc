@@ -65,6 +65,8 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
   std::unordered_set<uint64_t> aggregate_;
   std::unordered_set<Gva_t> last_new_;
   uint64_t retired_total_ = 0;
+  uint32_t trace_cap_ = 0;                      // rip traces (EnableTrace)
+  std::vector<std::vector<uint64_t>> traces_;   // per testcase of the last RunBatch
   uint64_t inject_ = ~0ull;  // page to #PF after the current handler
   // coverage map over the executable-page slots (ExecutablePages, as the gpu
   // backend builds it) and its shadow, for the shard merge
@@ -102,6 +104,7 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
     m_ = orc_create();
     for (auto &[gpfn, page] : dump_.Pages()) orc_add_page(m_, gpfn, page);
     if (Opts.Limit) orc_set_limit(m_, Opts.Limit);
+    orc_set_edges(m_, Opts.Edges ? 1 : 0);
     return Restore(CpuState);
   }
   // bochscpu_backend.cc:352-410 (+ the handler dispatch of :476-548)
@@ -281,9 +284,22 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
   bool engine_error_ = false;
   void SetFullCoverage(bool On) override { full_ = On; }
   size_t CoverageSize() const override { return aggregate_.size(); }
+  bool EnableTrace(uint32_t PerLane) override {
+    trace_cap_ = PerLane;
+    orc_set_trace(m_, PerLane != 0);
+    return true;
+  }
+  bool LaneTrace(uint32_t Lane, std::vector<uint64_t> &Rips, bool &Truncated) override {
+    if (Lane >= traces_.size()) return false;
+    Rips = traces_[Lane];
+    Truncated = Rips.size() > trace_cap_;
+    if (Truncated) Rips.resize(trace_cap_);
+    return true;
+  }
   bool RunBatch(const Target_t &Target, const std::vector<std::pair<const uint8_t *, size_t>> &Tc,
                 std::vector<LaneResult> &Out, ModuleSlots *) override {
     Out.assign(Tc.size(), LaneResult{});
+    if (trace_cap_) traces_.assign(Tc.size(), {});
     g_Backend = this;
     for (size_t i = 0; i < Tc.size(); i++) {
       LaneResult &L = Out[i];
@@ -312,6 +328,11 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
       L.gprs[17] = r.rflags;
       L.rip = r.rip;
       L.icount = orc_icount(m_);
+      if (trace_cap_) {  // this testcase's rip trace
+        std::vector<uint64_t> &T = traces_[i];
+        T.resize(orc_trace(m_, nullptr, 0));
+        orc_trace(m_, T.data(), T.size());
+      }
       Target.Restore();
     }
     Restore(initial_);
@@ -352,6 +373,8 @@ int main(int argc, char **argv) {
     std::string StatsJson() const override { return b->StatsJson(); }
     bool CoverageMap(uint8_t **M, uint64_t *N, bool *D) override { return b->CoverageMap(M, N, D); }
     size_t AbsorbCoverageMap() override { return b->AbsorbCoverageMap(); }
+    bool EnableTrace(uint32_t P) override { return b->EnableTrace(P); }
+    bool LaneTrace(uint32_t L, std::vector<uint64_t> &R, bool &T) override { return b->LaneTrace(L, R, T); }
   } E;
   E.b = B;
   E.n = O.lanes ? O.lanes : 1;

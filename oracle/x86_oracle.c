@@ -154,6 +154,9 @@ struct orc_machine {
   u64 bytes;
   u64 deliv_icount; /* retired count at the last IDT delivery (valid if deliv_valid) */
   int deliv_valid;
+  int edges; /* record branch edges into the coverage (RecordEdge) */
+  int trace, resumed; /* rip trace on; the next instruction resumes a breakpoint hit */
+  vec tracelist;
   /* per-instruction scratch */
   wtfgpu_exit_t *ex;
   int faulted;
@@ -193,6 +196,7 @@ void orc_destroy(orc_machine *m) {
   hm_free(&m->cov);
   free(m->dirty.v);
   free(m->covlist.v);
+  free(m->tracelist.v);
   free(m);
 }
 
@@ -206,6 +210,7 @@ int orc_add_page(orc_machine *m, u64 gpfn, const u8 *page) {
 void orc_set_regs(orc_machine *m, const wtfgpu_regs_t *r) { m->r = *r; }
 void orc_get_regs(orc_machine *m, wtfgpu_regs_t *r) { *r = m->r; }
 void orc_set_limit(orc_machine *m, u64 limit) { m->limit = limit; }
+void orc_set_edges(orc_machine *m, int on) { m->edges = on; }
 
 int orc_set_breakpoints(orc_machine *m, const u64 *gvas, u32 n) {
   hm_free(&m->bps);
@@ -223,6 +228,7 @@ void orc_restore(orc_machine *m, const wtfgpu_regs_t *r) {
   hm_free(&m->cov);
   hm_init(&m->cov, 1024);
   m->covlist.n = 0;
+  m->tracelist.n = 0;
   m->r = *r;
   m->initial_cr3 = r->cr3;
   m->icount = 0;
@@ -2359,6 +2365,8 @@ static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
     *hm_slot(&m->cov, m->r.rip, 1) = (void *)1;
     vec_push(&m->covlist, m->r.rip);
   }
+  if (m->trace && !m->resumed) vec_push(&m->tracelist, m->r.rip); /* bochscpu_backend.cc:506-520 */
+  m->resumed = 0;
   if (check_bp && hm_has(&m->bps, m->r.rip)) {
     fill_exit(m, ex, WTFGPU_EXIT_BREAKPOINT);
     return ex->status;
@@ -2372,6 +2380,23 @@ static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
   u64 saved_bytes = m->bytes;
   u64 next = 0;
   int x = exec_insn(m, &d, &mr, &next);
+  /* RecordEdge (bochscpu_backend.cc:699-728, hooks :235-257, :308-312): jcc
+   * taken or not, indirect near jmp / call; before the retire hook */
+  if (m->edges && x == X_OK &&
+      ((d.opmap == 0 && d.op >= 0x70 && d.op <= 0x7f) || (d.opmap == 1 && d.op >= 0x80 && d.op <= 0x8f) ||
+       (d.opmap == 0 && d.op == 0xff && ((d.reg & 7) == 2 || (d.reg & 7) == 4)))) {
+    u64 e = d.start;
+    e ^= e >> 30;
+    e *= 0xbf58476d1ce4e5b9ULL;
+    e ^= e >> 27;
+    e *= 0x94d049bb133111ebULL;
+    e ^= e >> 31;
+    e ^= next;
+    if (!hm_has(&m->cov, e)) {
+      *hm_slot(&m->cov, e, 1) = (void *)1;
+      vec_push(&m->covlist, e);
+    }
+  }
   if (x == X_OK || x == X_CR3) {
     m->r.rip = next;
     m->bytes += d.len;
@@ -2430,10 +2455,22 @@ int orc_inject_fault(orc_machine *m, uint32_t vector, uint32_t error, uint64_t a
 int orc_run(orc_machine *m, int skip_bp, wtfgpu_exit_t *ex) {
   int first = 1;
   for (;;) {
+    m->resumed = first && skip_bp; /* its before-execution hook ran at the hit */
     int st = one(m, !(first && skip_bp), ex);
     first = 0;
     if (st != WTFGPU_RUNNING) return st;
   }
 }
 
-int orc_step(orc_machine *m, wtfgpu_exit_t *ex) { return one(m, 0, ex); }
+int orc_step(orc_machine *m, wtfgpu_exit_t *ex) {
+  m->resumed = 0;
+  return one(m, 0, ex);
+}
+void orc_set_trace(orc_machine *m, int on) {
+  m->trace = on;
+  m->tracelist.n = 0;
+}
+uint64_t orc_trace(orc_machine *m, uint64_t *out, uint64_t cap) {
+  for (u64 i = 0; i < m->tracelist.n && i < cap; i++) out[i] = m->tracelist.v[i];
+  return m->tracelist.n;
+}

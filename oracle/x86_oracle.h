@@ -38,6 +38,15 @@ int orc_add_page(orc_machine *m, uint64_t gpfn, const uint8_t *page);
 void orc_set_regs(orc_machine *m, const wtfgpu_regs_t *r);
 void orc_get_regs(orc_machine *m, wtfgpu_regs_t *r);
 void orc_set_limit(orc_machine *m, uint64_t limit);
+/* Edge coverage (--edges): jcc and indirect jmp / call add
+ * splitmix64_finaliser(rip) ^ next_rip to the coverage (RecordEdge,
+ * bochscpu_backend.cc:699-728). */
+void orc_set_edges(orc_machine *m, int on);
+/* Rip trace (--trace-type rip, bochscpu_backend.cc:506-520): the rips about to
+ * execute, in order, since the last restore (a resumed breakpoint is logged
+ * once). orc_trace copies up to cap of them and returns the count. */
+void orc_set_trace(orc_machine *m, int on);
+uint64_t orc_trace(orc_machine *m, uint64_t *out, uint64_t cap);
 int orc_set_breakpoints(orc_machine *m, const uint64_t *gvas, uint32_t n);
 /* Restore: drop overlays, reload registers, zero counters and coverage. */
 void orc_restore(orc_machine *m, const wtfgpu_regs_t *r);

@@ -25,7 +25,7 @@ def lib() -> C.CDLL:
         "orc_create": ([], P), "orc_destroy": ([P], None),
         "orc_add_page": ([P, U64, C.c_char_p], C.c_int),
         "orc_set_regs": ([P, C.POINTER(Regs)], None), "orc_get_regs": ([P, C.POINTER(Regs)], None),
-        "orc_set_limit": ([P, U64], None),
+        "orc_set_limit": ([P, U64], None), "orc_set_edges": ([P, C.c_int], None),
         "orc_set_breakpoints": ([P, C.POINTER(U64), U32], C.c_int),
         "orc_restore": ([P, C.POINTER(Regs)], None),
         "orc_run": ([P, C.c_int, C.POINTER(Exit)], C.c_int),
@@ -76,6 +76,9 @@ class Oracle:
         r = Regs()
         self.L.orc_get_regs(self.m, C.byref(r))
         return r
+
+    def set_edges(self, on: bool):
+        self.L.orc_set_edges(self.m, 1 if on else 0)
 
     def set_limit(self, n):
         self.L.orc_set_limit(self.m, n)

@@ -1,0 +1,80 @@
+"""Rip traces (`run --trace-path --trace-type rip|cov`; SURVEY §8(f) rank 4,
+BochscpuBackend_t::SetTraceFile / BeforeExecutionHook, bochscpu_backend.cc:
+506-520, subcommands.cc:52-74): one `<input>.trace` per input, one "%#x" rip
+per line, every rip about to execute (rip) or only those new to the aggregate
+(cov). The GPU records them on the device (wtfgpu_set_trace); the twin from
+the oracle; their files must be identical.
+"""
+import os
+
+import pytest
+
+from tests import tlv_harness as H
+
+pytestmark = pytest.mark.skipif(not os.path.exists(H.TWIN), reason="oracle/wtf_twin not built")
+
+
+def read_trace(path):
+    with open(path) as f:
+        return [int(x, 16) for x in f.read().split()]
+
+
+def traces(exe, target, out, kind="rip", name="tlv_server", lanes=16):
+    res = H.run(exe, target, os.path.join(target, "inputs"), str(out) + ".jsonl", lanes=lanes, name=name,
+                extra=["--trace-path", str(out), "--trace-type", kind])
+    return res, {f[:-6]: read_trace(os.path.join(out, f)) for f in os.listdir(out)}
+
+
+@pytest.fixture(scope="module")
+def tlv(tmp_path_factory):
+    return H.build_target(str(tmp_path_factory.mktemp("tlvt")))
+
+
+@pytest.fixture(scope="module")
+def hevd(tmp_path_factory):
+    return H.build_hevd_target(str(tmp_path_factory.mktemp("hevdt")))
+
+
+def test_twin_rip_trace_is_the_executed_rips(tlv, tmp_path):
+    res, tr = traces(H.TWIN, tlv, tmp_path / "t")
+    assert set(tr) == {r["input"] for r in res}
+    for r in res:
+        t = tr[r["input"]]
+        assert t[0] == 0x140001000 or len(t) > 0
+        assert set(t) == set(r["coverage"])  # full coverage = every rip the hook saw
+        assert len(t) >= r["icount"]
+
+
+def test_cov_trace_is_first_occurrences_in_input_order(tlv, tmp_path):
+    _, rip = traces(H.TWIN, tlv, tmp_path / "r", "rip")
+    _, cov = traces(H.TWIN, tlv, tmp_path / "c", "cov")
+    seen = set()
+    for name in sorted(rip):
+        want = []
+        for v in rip[name]:
+            if v not in seen:
+                seen.add(v)
+                want.append(v)
+        assert cov[name] == want, name
+
+
+def test_existing_traces_are_skipped(tlv, tmp_path):
+    out = tmp_path / "s"
+    traces(H.TWIN, tlv, out)
+    first = sorted(os.listdir(out))
+    victim = os.path.join(out, first[0])
+    with open(victim, "w") as f:
+        f.write("0x1\n")
+    traces(H.TWIN, tlv, out)
+    assert read_trace(victim) == [1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["tlv", "hevd"])
+def test_gpu_traces_equal_twin(which, tlv, hevd, tmp_path):
+    target, name = (tlv, "tlv_server") if which == "tlv" else (hevd, "hevd")
+    for kind in ("rip", "cov"):
+        ra, a = traces(H.TWIN, target, tmp_path / f"twin_{kind}", kind, name=name)
+        rb, b = traces(H.WTFGPU, target, tmp_path / f"gpu_{kind}", kind, name=name)
+        assert a == b, kind
+        assert sum(len(t) for t in a.values()) > 100

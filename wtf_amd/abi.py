@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("WTFGPU_LIB") or os.path.join(HERE, "csrc", "libwtfgpu
 HOST_LIB_PATH = os.path.join(HERE, "host", "libwtf_host.so")
 
 RUNNING, EXIT_BREAKPOINT, EXIT_TIMEOUT, EXIT_INT3, EXIT_HLT, EXIT_FAULT, EXIT_UNIMPLEMENTED, \
-    EXIT_CR3, EXIT_OVERLAY_FULL, EXIT_STOPPED, EXIT_IDLE = range(11)
+    EXIT_CR3, EXIT_OVERLAY_FULL, EXIT_STOPPED, EXIT_IDLE, EXIT_STOP_OK, EXIT_FEED_FAULT, EXIT_STOP_ARGS = range(14)
 STATUS_NAMES = ["running", "breakpoint", "timeout", "int3", "hlt", "fault", "unimplemented",
                 "cr3", "overlay_full", "stopped", "idle", "stop_ok", "feed_fault"]
 
@@ -112,6 +112,10 @@ def load_hip_library(path: str = LIB_PATH) -> C.CDLL:
         "wtfgpu_set_initial_state": ([P, C.POINTER(Regs)], C.c_int),
         "wtfgpu_set_limit": ([P, U64], C.c_int),
         "wtfgpu_set_regroup": ([P, U64], C.c_int),
+        "wtfgpu_set_edges": ([P, C.c_int], C.c_int),
+        "wtfgpu_set_trace": ([P, U32], C.c_int),
+        "wtfgpu_read_trace": ([P, U32, C.POINTER(U64), U64, C.POINTER(U64)], C.c_int),
+        "wtfgpu_read_stop_args": ([P, C.POINTER(U32), U32, C.POINTER(U64)], C.c_int),
         "wtfgpu_select_queue": ([P, U32], C.c_int),
         "wtfgpu_lane_seeds": ([P, C.POINTER(U32), U32, C.POINTER(U64), C.c_int], C.c_int),
         "wtfgpu_run_async": ([P, U32, U32, U64], C.c_int),

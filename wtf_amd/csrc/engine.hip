@@ -56,6 +56,45 @@ __device__ __forceinline__ bool hash_find(const u64 *keys, u32 mask, u64 key, u3
   return false;
 }
 
+// Per-lane (non-uniform) lookup in an open-addressing u64 set.
+__device__ __forceinline__ bool set_has(const u64 *keys, u32 mask, u64 key) {
+  u32 h = (u32)mix64(key) & mask;
+  for (u32 i = 0; i <= mask; i++) {
+    const u64 k = keys[h];
+    if (k == key) return true;
+    if (k == EMPTY_KEY) return false;
+    h = (h + 1) & mask;
+  }
+  return false;
+}
+
+// Rip trace: the lane's next entry (the before-execution hook's trace write,
+// bochscpu_backend.cc:506-520).
+__device__ __forceinline__ void trace_rip(const Dev &P, u32 lane, u64 rip) {
+  const u32 n = P.trace_cnt[lane];
+  if (n < P.trace_cap) P.trace[(u64)lane * P.trace_cap + n] = rip;
+  P.trace_cnt[lane] = n + 1;
+}
+
+// RecordEdge's key (bochscpu_backend.cc:699-728): splitmix64's finaliser of
+// the branch's rip, xor the rip that follows it.
+__device__ __forceinline__ u64 edge_key(u64 rip, u64 next) {
+  u64 e = rip;
+  e ^= e >> 30;
+  e *= 0xbf58476d1ce4e5b9ull;
+  e ^= e >> 27;
+  e *= 0x94d049bb133111ebull;
+  e ^= e >> 31;
+  return e ^ next;
+}
+
+// The branches RecordEdge sees: conditional near branches taken or not
+// (cnear_branch_taken / _not_taken) and indirect near jmp / call
+// (ucnear_branch with JMP_INDIRECT / CALL_INDIRECT), :235-257.
+__device__ __forceinline__ bool edge_op(u32 op, u32 bsrc) {
+  return op == O_JCC || ((op == O_JMP || op == O_CALL) && bsrc != L_IMM);
+}
+
 __device__ __forceinline__ void load_lane(const Dev &P, u32 lane, Lane &L) {
   const u64 N = P.nlanes;
 #pragma unroll
@@ -130,6 +169,8 @@ __device__ __forceinline__ void store_lane(const Dev &P, const Lane &L) {
   if (P.cov_cnt) P.cov_cnt[lane] = L.ccnt;
 }
 
+__device__ __forceinline__ u32 log_value(const Dev &P, u64 v, bool mine, u32 lane, u32 gen, u32 cnt);
+
 // Coverage (bochscpu_backend.cc:501-504): a rip absent from the aggregate map
 // joins the set of every lane that ran it (`mine`). The map check is uniform;
 // the set insert is per lane (its own open-addressing table, no contention
@@ -140,8 +181,21 @@ __device__ __noinline__ u32 cover(const Dev &P, u64 rip, bool mine, u32 lane, u3
     if (hash_find(P.code_keys, P.code_mask, rip >> 12, s)) {
       const u32 cs = rfl32(P.code_slot[s]);
       if (rfl32(P.cov_map[(u64)cs * WTFGPU_PAGE_SIZE + (rip & 0xfff)])) return cnt;
+    } else if (P.extra_keys && set_has(P.extra_keys, P.extra_mask, rip)) {
+      return cnt;
     }
   }
+  return log_value(P, rip, mine, lane, gen, cnt);
+}
+
+// A branch edge (per-lane value): logged unless the aggregate has it.
+__device__ __noinline__ u32 cover_edge(const Dev &P, u64 e, bool mine, u32 lane, u32 gen, u32 cnt) {
+  if (!mine) return cnt;
+  if (P.extra_keys && set_has(P.extra_keys, P.extra_mask, e)) return cnt;
+  return log_value(P, e, true, lane, gen, cnt);
+}
+
+__device__ __forceinline__ u32 log_value(const Dev &P, u64 rip, bool mine, u32 lane, u32 gen, u32 cnt) {
   if (!mine) return cnt;
   const u32 H = P.H;
   const u64 base = (u64)lane * H;
@@ -420,6 +474,8 @@ __device__ __noinline__ void uc_fill(const Dev &P, UCEntry *e, u64 key, u64 lptr
   FOp f;
   if (dr == 0) {
     digest(d, f);
+    if (P.edges && edge_op(d.op, d.bsrc)) f = FOp{};  // branches whose edge is recorded run in the slow step
+    if (P.trace) f = FOp{};                           // traced lanes log every rip in the slow step
     if (!d.supported) flags |= UC_UNSUP;
     if (bp_lookup(P, rip)) flags |= UC_BP;
   } else {
@@ -615,6 +671,27 @@ __device__ __noinline__ bool bp_apply(const Dev &P, Lane &L, u64 grip) {
     RS(L, (u32)a.gprs[0] & 15, hi);
     return true;
   }
+  if (a.kind == WTFGPU_BPACT_STOP_ARGS) {  // Win64 arguments 0..5 (backend.cc:168-192), then stop
+    if (!P.stop_args) return false;
+    const u64 rsp = R(L, WTFGPU_RSP);
+    u64 v[6] = {R(L, 1), R(L, 2), R(L, 8), R(L, 9), 0, 0};
+    for (u32 i = 4; i < 6 && i < a.value; i++) {
+      for (int attempt = 0;; attempt++) {
+        L.miss = 0;
+        if (vread(L, rsp + 8 + 8 * (u64)i, 8, v[i])) break;
+        if (L.status != WTFGPU_RUNNING || !L.miss || !miss_service(P, L, attempt)) {
+          L.status = WTFGPU_RUNNING;  // undo a fault: the host handler decides
+          L.miss = 0;
+          L.pend = 0;
+          return false;
+        }
+      }
+    }
+    L.pend = 0;
+    for (u32 i = 0; i < 6; i++) P.stop_args[(u64)L.lane * 6 + i] = i < a.value ? v[i] : 0;
+    L.status = WTFGPU_EXIT_STOP_ARGS;
+    return true;
+  }
   if (a.kind != WTFGPU_BPACT_RETURN) return false;
   const u64 rsp = R(L, WTFGPU_RSP);
   u64 ra = 0;
@@ -681,6 +758,7 @@ __device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr
   const u64 gmask = __ballot(ing);
   if (gmask == 0) return;
   if (P.cov_rip) L.ccnt = cover(P, grip, ing, L.lane, L.cgen, L.ccnt);
+  if (P.trace && ing && !skip) trace_rip(P, L.lane, grip);  // a resumed breakpoint was logged at its hit
   const bool isbp = bp_lookup(P, grip);
   if (ing) {
     if (isbp && !skip) {
@@ -712,6 +790,9 @@ __device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr
       if (!miss_service(P, L, attempt)) break;
     }
     retire(P, L, x, d.len, next, d.opbytes);
+    // RecordEdge (bochscpu_backend.cc:699-728): the branch ran, whatever the retire hook decided
+    if (P.edges && P.cov_rip && edge_op(d.op, d.bsrc) && x == X_OK)
+      L.ccnt = cover_edge(P, edge_key(grip, next), true, L.lane, L.cgen, L.ccnt);
   }
 }
 
@@ -921,6 +1002,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     const u64 gmask = __ballot(ing);
 
     // ---- coverage, then breakpoint (bochscpu_backend.cc:501-547)
+    if (P.trace && ing && !skip) trace_rip(P, L.lane, grip);  // a resumed breakpoint was logged at its hit
     if (P.cov_rip && !(flags & UC_COVERED)) {
       const u64 logged = rfl64(e->logged);
       if (gmask & ~logged) {
@@ -964,6 +1046,9 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       u32 opbytes = 0;
       if (x == X_UNIMPL) opbytes = e->u.opbytes;
       retire(P, L, x, len, next, opbytes);
+      // RecordEdge (bochscpu_backend.cc:699-728): the branch ran, whatever the retire hook decided
+      if (P.edges && P.cov_rip && x == X_OK && edge_op(rfl32(e->u.op), rfl32(e->u.bsrc)))
+        L.ccnt = cover_edge(P, edge_key(grip, next), true, L.lane, L.cgen, L.ccnt);
     }
     STAMP(1);
   }
@@ -1021,6 +1106,7 @@ __device__ __forceinline__ void restore_lane(const Dev &P, const InitState &s, c
   P.ov_count[lane] = 0;
   tlb_stale(P, lane);
   if (P.rd_seed) P.rd_seed[lane] = P.rd_seed0;  // bochscpu_backend.cc:1030
+  if (P.trace_cnt) P.trace_cnt[lane] = 0;
   if (P.cov_rip) {
     P.lane_gen[lane] += 1;
     P.cov_cnt[lane] = 0;
@@ -1059,6 +1145,7 @@ __global__ void k_restore(Dev P, const InitState *S, const wtfgpu_regs_t *full0,
   P.ov_count[lane] = 0;  // the dirty-list reset: overlays dropped, nothing copied
   tlb_stale(P, lane);
   if (P.rd_seed) P.rd_seed[lane] = P.rd_seed0;  // bochscpu_backend.cc:1030
+  if (P.trace_cnt) P.trace_cnt[lane] = 0;
   if (P.cov_rip) {       // the lane's coverage set empties
     P.lane_gen[lane] += 1;
     P.cov_cnt[lane] = 0;
@@ -1348,6 +1435,13 @@ __global__ void k_lane_seeds(Dev P, const u32 *lanes, u32 n, u64 *buf, int write
   else buf[i] = P.rd_seed[lanes[i]];
 }
 
+// STOP_ARGS arguments of a lane list (6 u64 each).
+__global__ void k_stop_args(Dev P, const u32 *lanes, u32 n, u64 *out) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * 6) return;
+  out[i] = P.stop_args[(u64)lanes[i / 6] * 6 + i % 6];
+}
+
 // Exit records of lanes [first, first + count) (wtfgpu_read_exits).
 __global__ void k_pack_exits(Dev P, u32 first, u32 count, wtfgpu_exit_t *out) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1445,8 +1539,17 @@ __global__ void k_cov_commit(Dev P, const u64 *rips, u64 n) {
       P.cov_shadow[at] = 1;  // this shard's own find: not reported by absorb
       return;
     }
-    if (k == EMPTY_KEY) return;
+    if (k == EMPTY_KEY) break;
     h = (h + 1) & P.code_mask;
+  }
+  // not a code byte of a code page (a rip elsewhere, an edge): the extra set,
+  // kept at most 3/4 full (a value that does not fit is logged again later)
+  if (!P.extra_keys || rip == EMPTY_KEY) return;
+  u32 g = (u32)mix64(rip) & P.extra_mask;
+  for (u32 i = 0; i <= P.extra_mask / 4; i++) {
+    const unsigned long long prev = atomicCAS((unsigned long long *)&P.extra_keys[g], EMPTY_KEY, rip);
+    if (prev == EMPTY_KEY || prev == rip) return;
+    g = (g + 1) & P.extra_mask;
   }
 }
 
@@ -1496,6 +1599,10 @@ struct wtfgpu_ctx {
   LaneSys *d_sys = nullptr;
   u32 *d_guc = nullptr;       // device-wide decoded-uop cache (Dev::guc)
   u64 *d_rdseed = nullptr;    // per-lane Rdrand seeds (Dev::rd_seed)
+  u64 *d_stopargs = nullptr;  // per-lane STOP_ARGS arguments (Dev::stop_args)
+  u64 *d_extra = nullptr;     // coverage values outside code pages (Dev::extra_keys)
+  u64 *d_trace = nullptr;     // rip traces (Dev::trace)
+  u32 *d_tracecnt = nullptr;
   LaneTlb *d_tlbs = nullptr;  // translation state kept between k_run launches
   u32 *d_tlbok = nullptr;
   u8 *d_ovdata = nullptr;
@@ -1683,6 +1790,8 @@ int h2d(wtfgpu_ctx *c, T *dst, const T *src, u64 n) {
   return WTFGPU_OK;
 }
 
+constexpr u32 kExtraEntries = 1u << 20;
+
 // Entries depend on the pool pages and the breakpoint set: cleared with them.
 int guc_clear(wtfgpu_ctx *c) {
   if (c->d_guc) HIPCHK(hipMemsetAsync(c->d_guc, 0, (u64)(c->P.guc_mask + 1) * GUC_WORDS * 4, c->stream));
@@ -1761,6 +1870,15 @@ static void free_lanes(wtfgpu_ctx *c) {
   dfree(c->d_tlbs);
   dfree(c->d_tlbok);
   dfree(c->d_rdseed);
+  dfree(c->d_stopargs);
+  dfree(c->d_extra);
+  dfree(c->d_trace);
+  dfree(c->d_tracecnt);
+  c->d_trace = nullptr;
+  c->d_tracecnt = nullptr;
+  c->P.trace = nullptr;
+  c->P.trace_cnt = nullptr;
+  c->P.trace_cap = 0;
   dfree(c->d_ovdata);
   dfree(c->d_full);
   dfree(c->d_perm);
@@ -1890,6 +2008,11 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
   rc |= dalloc(&c->d_tlbs, N);
   rc |= dalloc(&c->d_tlbok, N);
   rc |= dalloc(&c->d_rdseed, N);
+  rc |= dalloc(&c->d_stopargs, 6 * N);
+  if (!c->d_extra) {  // the aggregate's values outside code pages (Dev::extra_keys): 1M entries
+    rc |= dalloc(&c->d_extra, (u64)kExtraEntries);
+    if (!rc) HIPCHK(hipMemset(c->d_extra, 0xff, (u64)kExtraEntries * 8));
+  }
   if (cov_entries) {
     rc |= dalloc(&c->d_covrip, N * cov_entries);
     rc |= dalloc(&c->d_covgen, N * cov_entries);
@@ -1933,6 +2056,9 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
   P.tlbs = c->d_tlbs;
   P.tlb_ok = c->d_tlbok;
   P.rd_seed = c->d_rdseed;
+  P.stop_args = c->d_stopargs;
+  P.extra_keys = c->d_extra;
+  P.extra_mask = kExtraEntries - 1;
   P.rd_seed0 = 0;
   P.ov_count = c->d_ovcount;
   P.ov_gpfn = c->d_ovgpfn;
@@ -2040,8 +2166,10 @@ int wtfgpu_set_breakpoints(wtfgpu_ctx *c, const uint64_t *gvas, uint32_t n) {
 
 int wtfgpu_set_breakpoint_actions(wtfgpu_ctx *c, const wtfgpu_bp_action_t *acts, uint32_t n) {
   if (!c || (n && !acts)) return WTFGPU_ERR_INVALID;
-  for (u32 i = 0; i < n; i++)
-    if (acts[i].kind > WTFGPU_BPACT_STOP_OK || acts[i].gva == EMPTY_KEY) return WTFGPU_ERR_INVALID;
+  for (u32 i = 0; i < n; i++) {
+    if (acts[i].kind > WTFGPU_BPACT_STOP_ARGS || acts[i].gva == EMPTY_KEY) return WTFGPU_ERR_INVALID;
+    if (acts[i].kind == WTFGPU_BPACT_STOP_ARGS && acts[i].value > 6) return WTFGPU_ERR_INVALID;
+  }
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   dfree(c->d_actkeys);
@@ -2540,6 +2668,23 @@ int wtfgpu_lane_seeds(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, uint64_t
   return WTFGPU_OK;
 }
 
+int wtfgpu_read_stop_args(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, uint64_t *out6) {
+  if (!c || (n && (!lanes || !out6)) || !c->d_stopargs) return WTFGPU_ERR_INVALID;
+  if (n == 0) return WTFGPU_OK;
+  for (u32 i = 0; i < n; i++)
+    if (lanes[i] >= c->P.nlanes) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  const u64 o_s = ((u64)n * 4 + 255) & ~255ull;
+  if (ensure_scratch(c, o_s + (u64)n * 48)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemcpyAsync(c->d_scratch, lanes, (u64)n * 4, hipMemcpyHostToDevice, c->stream));
+  k_stop_args<<<(n * 6 + 255) / 256, 256, 0, c->stream>>>(c->P, (const u32 *)c->d_scratch, n,
+                                                        (u64 *)(c->d_scratch + o_s));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out6, c->d_scratch + o_s, (u64)n * 48, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
 int wtfgpu_select_queue(wtfgpu_ctx *c, uint32_t queue) {
   if (!c || queue >= 2) return WTFGPU_ERR_INVALID;
   if (queue == c->cur_queue) return WTFGPU_OK;
@@ -2887,8 +3032,51 @@ int wtfgpu_reset_coverage(wtfgpu_ctx *c) {
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipMemsetAsync(c->d_covmap, 0, c->ncovslots * WTFGPU_PAGE_SIZE, c->stream));
   HIPCHK(hipMemsetAsync(c->d_covshadow, 0, c->ncovslots * WTFGPU_PAGE_SIZE, c->stream));
+  if (c->d_extra) HIPCHK(hipMemsetAsync(c->d_extra, 0xff, (u64)kExtraEntries * 8, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return WTFGPU_OK;
+}
+
+int wtfgpu_set_trace(wtfgpu_ctx *c, uint32_t per_lane) {
+  if (!c || !c->P.nlanes) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  dfree(c->d_trace);
+  dfree(c->d_tracecnt);
+  c->d_trace = nullptr;
+  c->d_tracecnt = nullptr;
+  c->P.trace = nullptr;
+  c->P.trace_cnt = nullptr;
+  c->P.trace_cap = 0;
+  if (per_lane) {
+    const u64 N = c->P.nlanes;
+    if (dalloc(&c->d_trace, N * per_lane) || dalloc(&c->d_tracecnt, N)) return WTFGPU_ERR_OOM;
+    HIPCHK(hipMemset(c->d_tracecnt, 0, N * 4));
+    c->P.trace = c->d_trace;
+    c->P.trace_cnt = c->d_tracecnt;
+    c->P.trace_cap = per_lane;
+  }
+  return guc_clear(c);  // cached entries were digested for the other setting
+}
+
+int wtfgpu_read_trace(wtfgpu_ctx *c, uint32_t lane, uint64_t *rips, uint64_t cap, uint64_t *n) {
+  if (!c || !n || (cap && !rips) || lane >= c->P.nlanes || !c->d_trace) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  u32 cnt = 0;
+  HIPCHK(hipMemcpyAsync(&cnt, c->d_tracecnt + lane, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  *n = cnt;
+  const u64 k = std::min<u64>(std::min<u64>(cnt, c->P.trace_cap), cap);
+  if (k) HIPCHK(hipMemcpyAsync(rips, c->d_trace + (u64)lane * c->P.trace_cap, k * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_set_edges(wtfgpu_ctx *c, int on) {
+  if (!c) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  c->P.edges = on ? 1 : 0;
+  return guc_clear(c);  // cached entries were digested for the other setting
 }
 
 int wtfgpu_coverage_absorb(wtfgpu_ctx *c, uint64_t *rips, uint64_t cap, uint64_t *n) {

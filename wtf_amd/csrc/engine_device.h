@@ -119,6 +119,18 @@ struct Dev {
   u32 *guc;
   u32 guc_mask;
   u64 *rd_seed;           // [nlanes] Rdrand seeds (WTFGPU_BPACT_RDRAND)
+  u64 *stop_args;         // [nlanes][6] arguments kept by WTFGPU_BPACT_STOP_ARGS
+  // values of the aggregate coverage that are not code bytes of a code page
+  // (rips elsewhere, --edges values): an open-addressing set, read-only
+  // during k_run, grown by k_cov_commit
+  u64 *extra_keys;
+  u32 extra_mask;
+  u32 edges;              // record branch edges (RecordEdge, bochscpu_backend.cc:699-728)
+  // rip trace (--trace-type rip / unique_rip, bochscpu_backend.cc:506-520):
+  // per lane, the rips about to execute in order, trace_cap of them at most
+  u64 *trace;             // [nlanes][trace_cap]
+  u32 *trace_cnt;         // [nlanes] rips logged (may exceed trace_cap: truncated)
+  u32 trace_cap;
   u64 rd_seed0;           // the initial state's (restore)
   LaneTlb *tlbs;          // [nlanes]
   u32 *tlb_ok;            // [nlanes]

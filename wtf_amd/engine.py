@@ -60,6 +60,9 @@ class Engine:
         arr = (C.c_uint64 * max(1, len(gvas)))(*gvas)
         _chk(self.L.wtfgpu_set_breakpoints(self.ctx, arr, len(gvas)), "set_breakpoints")
 
+    def set_edges(self, on: bool):
+        _chk(self.L.wtfgpu_set_edges(self.ctx, 1 if on else 0), "set_edges")
+
     def set_code_pages(self, vpns):
         arr = (C.c_uint64 * max(1, len(vpns)))(*vpns)
         _chk(self.L.wtfgpu_set_code_pages(self.ctx, arr, len(vpns)), "set_code_pages")

@@ -86,6 +86,7 @@ bool GpuBackend_t::Initialize(const Options_t &Opts, const CpuState_t &CpuState)
   views_.resize(nlanes_);
   arenas_.resize(omp_get_max_threads() + 1);
   if (Opts.Limit) SetLimit(Opts.Limit);
+  if (Opts.Edges && wtfgpu_set_edges(ctx_, 1) != WTFGPU_OK) return false;  // bochscpu_backend.cc:308-312
   if (!Restore(CpuState)) return false;
   return set_code_pages();
 }
@@ -207,6 +208,11 @@ bool GpuBackend_t::SetBreakpoint(const Gva_t Gva, const BreakpointHandler_t Hand
   } else if (Action.Kind == BreakpointAction_t::Kind_t::Rdrand) {
     A.kind = WTFGPU_BPACT_RDRAND;
     A.gprs[0] = (uint64_t)gpr_index((Registers_t)Action.Gprs[0]);
+  } else if (Action.Kind == BreakpointAction_t::Kind_t::StopWithArgs) {
+    if (!Action.ArgsResult || Action.Return > 6) return false;
+    A.kind = WTFGPU_BPACT_STOP_ARGS;
+    A.value = Action.Return;
+    args_results_[Gva.U64()] = Action.ArgsResult;
   } else {
     A.kind = WTFGPU_BPACT_SET_GPRS;
     memcpy(A.gprs, Action.Gprs, sizeof(A.gprs));
@@ -650,6 +656,7 @@ void GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first
       case WTFGPU_EXIT_FAULT: v.result = FaultToResult(e.vector, e.error, e.rip, e.addr, e.opcode); break;
       case WTFGPU_EXIT_STOPPED: break;
       case WTFGPU_EXIT_STOP_OK: v.result = Ok_t(); break;           // device Feed action: Stop(Ok_t())
+      case WTFGPU_EXIT_STOP_ARGS: hit[pi] = 2; continue;            // named below from the kept arguments
       default:
         // unimplemented opcode / overlay full / a device Feed write that
         // failed: the engine cannot finish the testcase. Not a target bug:
@@ -670,8 +677,28 @@ void GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first
     }
     done[l - first] = 1;
   }
-  for (size_t pi = 0; pi < pending.size(); pi++)
-    if (hit[pi]) hits.push_back(pending[pi]);
+  std::vector<uint32_t> named;
+  for (size_t pi = 0; pi < pending.size(); pi++) {
+    if (hit[pi] == 1) hits.push_back(pending[pi]);
+    if (hit[pi] == 2) named.push_back(pending[pi]);
+  }
+  if (named.empty()) return;
+  // device StopWithArgs actions: the handler's Stop(Result(GetArg(0..5)))
+  std::vector<uint64_t> args(named.size() * 6);
+  const bool ok = wtfgpu_read_stop_args(ctx_, named.data(), (uint32_t)named.size(), args.data()) == WTFGPU_OK;
+  for (size_t k = 0; k < named.size(); k++) {
+    const uint32_t l = named[k];
+    LaneView &v = views_[l];
+    const auto it = args_results_.find(ex[l - first].rip);
+    if (ok && it != args_results_.end()) {
+      v.result = it->second(&args[k * 6]);
+    } else {  // cannot happen unless the engine misbehaves: an engine error, not a target bug
+      if (out) (*out)[l].error = true;
+      if (!v.result) v.result = Crash_t();
+      stats_.err_other++;
+    }
+    done[l - first] = 1;
+  }
 }
 
 // Final state of every finished lane (`ex` holds the last round's exits of
@@ -1019,6 +1046,15 @@ std::optional<TestcaseResult_t> GpuBackend_t::Run(const uint8_t *, const uint64_
   stats_.total_ms += ms_since(t0);
   cur_ = 0;
   return out[0].result;
+}
+
+bool GpuBackend_t::LaneTrace(uint32_t Lane, std::vector<uint64_t> &Rips, bool &Truncated) {
+  uint64_t N = 0;
+  Rips.clear();
+  if (wtfgpu_read_trace(ctx_, Lane, nullptr, 0, &N) != WTFGPU_OK) return false;
+  Truncated = N > trace_cap_;
+  Rips.resize(std::min<uint64_t>(N, trace_cap_));
+  return wtfgpu_read_trace(ctx_, Lane, Rips.data(), Rips.size(), &N) == WTFGPU_OK;
 }
 
 bool GpuBackend_t::RunBatch(const Target_t &Target, const std::vector<std::pair<const uint8_t *, size_t>> &Testcases,

@@ -105,6 +105,11 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   std::string StatsJson() const override;
   bool CoverageMap(uint8_t **Map, uint64_t *Bytes, bool *Device) override;
   size_t AbsorbCoverageMap() override;
+  bool EnableTrace(uint32_t PerLane) override {
+    trace_cap_ = PerLane;
+    return ctx_ && wtfgpu_set_trace(ctx_, PerLane) == WTFGPU_OK;
+  }
+  bool LaneTrace(uint32_t Lane, std::vector<uint64_t> &Rips, bool &Truncated) override;
   const BatchStats &Stats() const { return stats_; }
   uint32_t Lanes() const override { return nlanes_; }
   wtfgpu_ctx *Engine() const { return ctx_; }
@@ -225,6 +230,8 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   static thread_local uint32_t cur_;
   std::unordered_map<uint64_t, BreakpointHandler_t> breakpoints_;
   std::vector<wtfgpu_bp_action_t> bp_actions_;  // device-side equivalents of some handlers
+  uint32_t trace_cap_ = 0;                       // rip-trace capacity per lane (EnableTrace)
+  std::unordered_map<uint64_t, BreakpointAction_t::ArgsResult_t> args_results_;  // StopWithArgs, by gva
   bool feed_action_ = false;                     // a Feed action is on the device
   int upload_feed(uint32_t n);                   // lanes [0, n)
   std::unordered_set<uint64_t> aggregate_;

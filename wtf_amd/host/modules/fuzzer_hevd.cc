@@ -8,7 +8,8 @@
 //  * nt!ExGenRandom: right after its `rdrand rdx` (+0xe0) rdx := Rdrand()
 //    (:96-108, the BLAKE3 chain of Backend_t::Rdrand; also declared as data,
 //    BreakpointAction_t::Rdrand, which the gpu backend runs on the device);
-//  * nt!KeBugCheck2 -> Crash_t("crash-<code>-<p0>-<p1>-<p2>-<p3>-<p4>") (:114-128);
+//  * nt!KeBugCheck2 -> Crash_t("crash-<code>-<p0>-<p1>-<p2>-<p3>-<p4>") (:114-128; also
+//    declared as BreakpointAction_t::StopWithArgs, named from the device-kept arguments);
 //  * nt!SwapContext -> Cr3Change_t (:134-139).
 // The module keeps no per-testcase state, so nothing is registered with
 // WTF_LANE_STATE.
@@ -24,6 +25,12 @@ static std::string Hex(const uint64_t V) {
   char B[24];
   snprintf(B, sizeof(B), "0x%llx", (unsigned long long)V);
   return B;
+}
+
+// nt!KeBugCheck2(BCode, B0, B1, B2, B3, B4) -> the crash name (:114-128)
+TestcaseResult_t BugCheckResult(const uint64_t *A) {
+  return Crash_t("crash-" + Hex(A[0]) + "-" + Hex(A[1]) + "-" + Hex(A[2]) + "-" + Hex(A[3]) + "-" + Hex(A[4]) + "-" +
+                 Hex(A[5]));
 }
 
 bool InsertTestcase(const uint8_t *Buffer, const size_t BufferSize) {
@@ -67,11 +74,11 @@ bool Init(const Options_t &, const CpuState_t &) {
           BreakpointAction_t::Rdrand(Registers_t::Rdx)))  // device-side on the gpu backend
     return false;
   if (!g_Backend->SetBreakpoint("nt!KeBugCheck2", [](Backend_t *Backend) {
-        const uint64_t BCode = Backend->GetArg(0), B0 = Backend->GetArg(1), B1 = Backend->GetArg(2),
-                       B2 = Backend->GetArg(3), B3 = Backend->GetArg(4), B4 = Backend->GetArg(5);
-        Backend->Stop(Crash_t("crash-" + Hex(BCode) + "-" + Hex(B0) + "-" + Hex(B1) + "-" + Hex(B2) + "-" + Hex(B3) +
-                              "-" + Hex(B4)));
-      }))
+        const uint64_t A[6] = {Backend->GetArg(0), Backend->GetArg(1), Backend->GetArg(2),
+                               Backend->GetArg(3), Backend->GetArg(4), Backend->GetArg(5)};
+        Backend->Stop(BugCheckResult(A));
+      },
+      BreakpointAction_t::StopWithArgs(6, BugCheckResult)))  // device-side on the gpu backend
     return false;
   if (!g_Backend->SetBreakpoint("nt!SwapContext", [](Backend_t *Backend) { Backend->Stop(Cr3Change_t()); }))
     return false;

@@ -141,6 +141,10 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
     else if (a == "--max_len") O.max_len = strtoull(next("--max_len"), nullptr, 0);
     else if (a == "--device") O.device = atoi(next("--device"));
     else if (a == "--full-coverage") O.full_coverage = true;
+    else if (a == "--edges") O.edges = true;
+    else if (a == "--trace-path") O.trace_path = next("--trace-path");
+    else if (a == "--trace-type") O.trace_type = next("--trace-type");
+    else if (a == "--trace-cap") O.trace_cap = (uint32_t)strtoul(next("--trace-cap"), nullptr, 0);
     else if (a == "--quiet") O.quiet = true;
     else if (a == "--serial-mutation") O.serial_mutation = true;
     else if (a == "--slice-steps") O.slice = strtoull(next("--slice-steps"), nullptr, 0);
@@ -170,7 +174,8 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
     fprintf(stderr, "usage: [run|fuzz|master] --name <target> --target <dir> [--input p] [--results f] [--limit n]\n"
                     "       [--lanes n] [--overlay-pages k] [--runs n] [--seconds s] [--seed s] [--full-coverage]\n"
                     "       [--serial-mutation] [--slice-steps s] [--regroup-steps r] [--rank r --world n [--exchange host:port | --nccl-id-file f]]\n"
-                    "       [--address tcp://ip:port|unix://path [--batched] [--nodes k]]\n");
+                    "       [--address tcp://ip:port|unix://path [--batched] [--nodes k]] [--edges]\n"
+                    "       [--trace-path dir [--trace-type rip|cov] [--trace-cap n]]\n");
     return false;
   }
   return true;
@@ -185,6 +190,7 @@ bool LoadTarget(const RunnerOptions &O, Options_t &Opts, CpuState_t &State) {
   Opts.CpuStatePath = Opts.StatePath / "regs.json";
   Opts.SymbolFilePath = Opts.StatePath / "symbol-store.json";
   Opts.Limit = O.limit;
+  Opts.Edges = O.edges;
   Opts.GpuDevice = O.device;
   Opts.GpuLanes = O.lanes;
   Opts.GpuOverlayPages = O.overlay_pages;
@@ -218,7 +224,41 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
   Exec.SetFullCoverage(O.full_coverage);
 
   if (O.mode == "run") {
-    const auto Inputs = list_inputs(O.input.empty() ? fs::path(O.target) / "inputs" : fs::path(O.input));
+    auto Inputs = list_inputs(O.input.empty() ? fs::path(O.target) / "inputs" : fs::path(O.input));
+    // traces (subcommands.cc:52-74): <trace-path>/<input name>.trace; an input
+    // whose trace exists is skipped
+    const bool Trace = !O.trace_path.empty();
+    std::unordered_set<uint64_t> TraceSeen;  // cov traces: rips not seen in earlier testcases
+    if (Trace) {
+      if (O.trace_type != "rip" && O.trace_type != "cov") {
+        printf("--trace-type %s is not supported by this backend (rip, cov)\n", O.trace_type.c_str());
+        return 1;
+      }
+      if (!Exec.EnableTrace(O.trace_cap)) {
+        printf("EnableTrace failed\n");
+        return 1;
+      }
+      fs::create_directories(O.trace_path);
+      std::vector<fs::path> Keep;
+      for (const fs::path &In : Inputs) {
+        if (fs::exists(fs::path(O.trace_path) / (In.filename().string() + ".trace")))
+          printf("Skipping %s as it already exists.\n", In.string().c_str());
+        else Keep.push_back(In);
+      }
+      Inputs = Keep;
+    }
+    auto write_trace = [&](const fs::path &In, uint32_t Lane) -> bool {
+      std::vector<uint64_t> Rips;
+      bool Truncated = false;
+      if (!Exec.LaneTrace(Lane, Rips, Truncated)) return false;
+      FILE *F = fopen((fs::path(O.trace_path) / (In.filename().string() + ".trace")).c_str(), "w");
+      if (!F) return false;
+      for (uint64_t R : Rips)
+        if (O.trace_type == "rip" || TraceSeen.insert(R).second) fprintf(F, "%#llx\n", (unsigned long long)R);
+      fclose(F);
+      if (Truncated) printf("trace of %s truncated at %zu rips (--trace-cap)\n", In.string().c_str(), Rips.size());
+      return true;
+    };
     FILE *Out = O.results.empty() ? stdout : fopen(O.results.c_str(), "w");
     if (!Out) return 1;
     const auto t0 = Clock::now();
@@ -235,7 +275,7 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
       for (size_t c = 0; c < Cov.size(); c++) fprintf(Out, "%s%llu", c ? "," : "", (unsigned long long)Cov[c]);
       fprintf(Out, "]}\n");
     };
-    if (O.stream_run && Exec.CanStream()) {
+    if (O.stream_run && Exec.CanStream() && !Trace) {
       // streaming replay: lanes refilled as testcases finish, results printed
       // in input order (parity with the batched replay, tests/test_gpu_tlv.py)
       std::vector<std::vector<uint8_t>> Bufs(Inputs.size());
@@ -266,7 +306,7 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
         print(Inputs[i], Res[i]);
       }
     }
-    for (size_t b = O.stream_run && Exec.CanStream() ? Inputs.size() : 0; b < Inputs.size(); b += N) {
+    for (size_t b = O.stream_run && Exec.CanStream() && !Trace ? Inputs.size() : 0; b < Inputs.size(); b += N) {
       const size_t n = std::min<size_t>(N, Inputs.size() - b);
       std::vector<std::vector<uint8_t>> Bufs(n);
       std::vector<std::pair<const uint8_t *, size_t>> Tc(n);
@@ -283,6 +323,10 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
       for (size_t i = 0; i < n; i++) {
         Retired += R[i].icount;
         print(Inputs[b + i], R[i]);
+        if (Trace && !write_trace(Inputs[b + i], (uint32_t)i)) {
+          printf("trace of %s failed\n", Inputs[b + i].string().c_str());
+          return 1;
+        }
       }
     }
     if (Out != stdout) fclose(Out);

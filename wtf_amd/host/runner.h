@@ -85,6 +85,12 @@ class Executor_t {
   // Rips set in the map (after a merge) that the aggregate lacks join it;
   // returns how many.
   virtual size_t AbsorbCoverageMap() { return 0; }
+  // Rip traces (wtf run --trace-type rip / cov, SetTraceFile,
+  // bochscpu_backend.cc:506-520): every testcase of the next RunBatch logs
+  // the rips it is about to execute, PerLane at most; LaneTrace(i) is
+  // testcase i's (Truncated: it logged more than PerLane).
+  virtual bool EnableTrace(uint32_t) { return false; }
+  virtual bool LaneTrace(uint32_t, std::vector<uint64_t> &, bool &) { return false; }
 };
 
 // The collective between shards (one node per GPU): an in-place MAX
@@ -115,6 +121,10 @@ struct RunnerOptions {
   uint64_t max_len = 0x1000;
   int device = 0;
   bool full_coverage = false;
+  bool edges = false;        // --edges: branch edges join the coverage (RecordEdge)
+  std::string trace_path;    // run: --trace-path dir (one <input>.trace per input, subcommands.cc:52-74)
+  std::string trace_type = "rip";  // run: --trace-type rip | cov (wtf.cc:197-200)
+  uint32_t trace_cap = 1u << 20;   // run: rips kept per testcase
   bool quiet = false;
   bool serial_mutation = false;  // one mutator, in order: the reference master's stream exactly
   // fuzz: continuous batching on executors that stream (the gpu node): every

@@ -206,10 +206,12 @@ using BreakpointHandler_t = void (*)(Backend_t *);
 // other backend calls the handler. The module guarantees the two are the same
 // register effect; the GPU-vs-twin parity tests check it testcase by testcase.
 struct BreakpointAction_t {
-  enum class Kind_t { Host, SimulateReturn, SetGprs, Feed, Rdrand, StopOk };
+  enum class Kind_t { Host, SimulateReturn, SetGprs, Feed, Rdrand, StopOk, StopWithArgs };
   Kind_t Kind = Kind_t::Host;
   uint64_t Return = 0;  // SimulateReturn: SimulateReturnFromFunction(Return)
   uint64_t Gprs[17] = {};  // SetGprs: rax, rcx, rdx, rbx, rsp, rbp, rsi, rdi, r8..r15, rip
+  using ArgsResult_t = TestcaseResult_t (*)(const uint64_t *Args);
+  ArgsResult_t ArgsResult = nullptr;  // StopWithArgs
 
   static BreakpointAction_t SimulateReturn(const uint64_t Value) {
     BreakpointAction_t A;
@@ -235,6 +237,16 @@ struct BreakpointAction_t {
     BreakpointAction_t A;
     A.Kind = Kind_t::Rdrand;
     A.Gprs[0] = (uint64_t)Reg;
+    return A;
+  }
+  // Stop(Result(Args)), Args = GetArg(0 .. NArgs - 1) of the hooked function
+  // (NArgs <= 6): a handler that only names the testcase's end from its
+  // arguments (nt!KeBugCheck2 -> Crash_t, fuzzer_hevd.cc:114-128)
+  static BreakpointAction_t StopWithArgs(const uint32_t NArgs, const ArgsResult_t Result) {
+    BreakpointAction_t A;
+    A.Kind = Kind_t::StopWithArgs;
+    A.Return = NArgs;
+    A.ArgsResult = Result;
     return A;
   }
   static BreakpointAction_t Feed(const Registers_t Base, const Registers_t Len,
