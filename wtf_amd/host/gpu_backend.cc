@@ -686,6 +686,8 @@ void GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first
   // device StopWithArgs actions: the handler's Stop(Result(GetArg(0..5)))
   std::vector<uint64_t> args(named.size() * 6);
   const bool ok = wtfgpu_read_stop_args(ctx_, named.data(), (uint32_t)named.size(), args.data()) == WTFGPU_OK;
+  uint64_t bad = 0;
+#pragma omp parallel for schedule(static, 512) reduction(+ : bad) if (named.size() >= 2048)
   for (size_t k = 0; k < named.size(); k++) {
     const uint32_t l = named[k];
     LaneView &v = views_[l];
@@ -695,10 +697,11 @@ void GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first
     } else {  // cannot happen unless the engine misbehaves: an engine error, not a target bug
       if (out) (*out)[l].error = true;
       if (!v.result) v.result = Crash_t();
-      stats_.err_other++;
+      bad++;
     }
     done[l - first] = 1;
   }
+  stats_.err_other += bad;
 }
 
 // Final state of every finished lane (`ex` holds the last round's exits of

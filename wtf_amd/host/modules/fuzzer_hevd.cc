@@ -21,16 +21,26 @@
 namespace Hevd {
 
 // fmt's {:#x}: "0x" + lowercase hex, "0x0" for zero
-static std::string Hex(const uint64_t V) {
-  char B[24];
-  snprintf(B, sizeof(B), "0x%llx", (unsigned long long)V);
-  return B;
+static void AppendHex(std::string &S, uint64_t V) {
+  char B[18];
+  int N = 0;
+  do {
+    B[N++] = "0123456789abcdef"[V & 15];
+    V >>= 4;
+  } while (V);
+  S += "0x";
+  while (N) S += B[--N];
 }
 
 // nt!KeBugCheck2(BCode, B0, B1, B2, B3, B4) -> the crash name (:114-128)
 TestcaseResult_t BugCheckResult(const uint64_t *A) {
-  return Crash_t("crash-" + Hex(A[0]) + "-" + Hex(A[1]) + "-" + Hex(A[2]) + "-" + Hex(A[3]) + "-" + Hex(A[4]) + "-" +
-                 Hex(A[5]));
+  std::string Name = "crash";
+  Name.reserve(6 * 19 + 5);
+  for (int i = 0; i < 6; i++) {
+    Name += '-';
+    AppendHex(Name, A[i]);
+  }
+  return Crash_t(std::move(Name));
 }
 
 bool InsertTestcase(const uint8_t *Buffer, const size_t BufferSize) {
