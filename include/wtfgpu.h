@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define WTFGPU_ABI_VERSION 1
+#define WTFGPU_ABI_VERSION 2
 #define WTFGPU_PAGE_SIZE 4096u
 
 /* Status codes. */
@@ -122,7 +122,8 @@ typedef struct wtfgpu_regs {
   uint16_t fpcw, fpsw, fptw, fpop;
   uint32_t pad0;
   uint64_t fpst[8];
-  uint64_t xmm[16][2];
+  uint64_t xmm[16][2];  /* bits 127:0 of ymm0..15 */
+  uint64_t ymmh[16][2]; /* bits 255:128 (CpuState_t::Zmm[i].Q[2..3]) */
 } wtfgpu_regs_t;
 
 /* Why a lane stopped. */

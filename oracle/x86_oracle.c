@@ -54,6 +54,11 @@
  *       UNIMPLEMENTED. #UD if CR0.EM or !CR4.OSFXSR, #NM if CR0.TS, #GP(0) for a
  *       misaligned 16-byte operand of an aligned form; the checks run in that
  *       order, before any memory access.
+ *   U23 AVX / AVX2 (VEX): the same subset at 128 / 256 bits plus vzeroupper,
+ *       vzeroall, vpshufb, vptest, vpbroadcast (see exec_vex); VEX.128 zeroes
+ *       bits 255:128; legacy SSE leaves them. 16- / 32-byte operands: every
+ *       page is checked before any byte moves, a fault is reported at the
+ *       operand's start or at the page boundary it crosses.
  */
 #include "x86_oracle.h"
 #include <stdlib.h>
@@ -452,6 +457,24 @@ static int vread_rmw(orc_machine *m, u64 va, u32 len, void *out) {
   return 0;
 }
 
+/* up to 32 bytes: every page checked before any byte moves (a 32-byte
+ * operand crosses at most one page boundary; the fault is at its start or
+ * at the boundary) */
+static int vread_n(orc_machine *m, u64 va, u32 len, void *out) {
+  if (len <= 16) return vread(m, va, len, out);
+  u64 pa[2];
+  u32 nn[2];
+  if (vprobe(m, va, 16, ACC_R, pa, nn) || vprobe(m, va + 16, len - 16, ACC_R, pa, nn)) return -1;
+  return vread(m, va, 16, out) || vread(m, va + 16, len - 16, (u8 *)out + 16);
+}
+static int vwrite_n(orc_machine *m, u64 va, u32 len, const void *in) {
+  if (len <= 16) return vwrite(m, va, len, in);
+  u64 pa[2];
+  u32 nn[2];
+  if (vprobe(m, va, 16, ACC_W, pa, nn) || vprobe(m, va + 16, len - 16, ACC_W, pa, nn)) return -1;
+  return vwrite(m, va, 16, in) || vwrite(m, va + 16, len - 16, (const u8 *)in + 16);
+}
+
 /* ---------------- decode ---------------- */
 typedef struct {
   u64 start;
@@ -459,6 +482,7 @@ typedef struct {
   u32 pfx66, pfx67, rep, lock, seg; /* seg: 0 none, 4 fs, 5 gs */
   u32 rex, rexw, rexr, rexx, rexb;
   u32 opmap; /* 0 one-byte, 1 = 0F, 2 = 0F38, 3 = 0F3A */
+  u32 vex, vl, vw, vvvv, vpp, vbad; /* VEX prefix: present, L, W, vvvv (decoded), pp; a legacy prefix before it */
   u32 op;
   u32 has_modrm, mod, reg, rm; /* reg, rm include REX extension */
   u32 is_mem;
@@ -1074,6 +1098,22 @@ static int sse_opcode(u32 op) {
          op == 0xae || op == 0xc3 || (op >= 0xc4 && op <= 0xc6) || op >= 0xd0;
 }
 
+/* pshufb of one lane */
+static x128 pshufb(const x128 *a, const x128 *b) {
+  x128 r;
+  for (int i = 0; i < 16; i++) r.b[i] = (b->b[i] & 0x80) ? 0 : a->b[b->b[i] & 15];
+  return r;
+}
+/* ptest over n bytes: ZF = (a & b) == 0, CF = (~a & b) == 0, AF OF PF SF = 0 */
+static void ptest(orc_machine *m, const u8 *a, const u8 *b, int n) {
+  int z = 1, c = 1;
+  for (int i = 0; i < n; i++) {
+    if (a[i] & b[i]) z = 0;
+    if (~a[i] & b[i]) c = 0;
+  }
+  m->r.rflags = (m->r.rflags & ~RF_STATUS) | (z ? RF_ZF : 0) | (c ? RF_CF : 0);
+}
+
 static int exec_sse(orc_machine *m, insn *d) {
   const u32 op = d->op, r3 = d->reg & 7;
   const int pc = d->rep == 0xf3 ? 2 : d->rep == 0xf2 ? 3 : d->pfx66 ? 1 : 0; /* none, 66, f3, f2 */
@@ -1081,6 +1121,22 @@ static int exec_sse(orc_machine *m, insn *d) {
   const u8 imm = d->bytes[d->len - 1];
   x128 a, b, r;
   u64 v;
+  if (d->opmap == 2) { /* 66 0f 38 00 pshufb, 66 0f 38 17 ptest */
+    if (pc != 1) return X_UNIMPL;
+    if (m->r.cr0 & 4 || !(m->r.cr4 & 0x200)) {
+      fault(m, WTFGPU_VEC_UD, 0);
+      return X_FAULT;
+    }
+    if (m->r.cr0 & 8) {
+      fault(m, 7, 0);
+      return X_FAULT;
+    }
+    a = xreg(m, d->reg);
+    if (xsrc(m, d, 16, 1, &b)) return X_FAULT;
+    if (op == 0x17) ptest(m, a.b, b.b, 16);
+    else xput(m, d->reg, pshufb(&a, &b));
+    return X_OK;
+  }
   if (op == 0xc3) { /* movnti m32/64, r (SSE2 general-register store) */
     if (pc != 0) return X_UNIMPL;
     if (!mem) {
@@ -1378,6 +1434,334 @@ static int exec_sse(orc_machine *m, insn *d) {
     return X_UNIMPL;
   }
   xput(m, d->reg, r);
+  return X_OK;
+}
+
+
+/* ---------------- AVX / AVX2 (U23) ----------------
+ * VEX-encoded forms of the same subset at 128 and 256 bits (three operands:
+ * dst = reg, first source = vvvv, second = r/m; lane-wise per 128 bits),
+ * vzeroupper / vzeroall, vpshufb, vptest, vpbroadcastb/w/d/q. VEX.128 zeroes
+ * bits 255:128 of the destination. #UD for a legacy 66/f2/f3/REX before VEX,
+ * CR4.OSXSAVE = 0, XCR0[2:1] != 11, vvvv != 1111 in two-operand forms, L = 1
+ * where only 128 bits exist, and register-only / memory-only violations; #NM
+ * if CR0.TS; #GP(0) when an aligned move (vmovaps/apd/dqa/ntdq/ntps/ntpd) is
+ * not aligned to its size. */
+typedef struct { x128 l, h; } y256;
+
+static y256 yreg(orc_machine *m, u32 r) {
+  y256 v;
+  memcpy(v.l.b, m->r.xmm[r & 15], 16);
+  memcpy(v.h.b, m->r.ymmh[r & 15], 16);
+  return v;
+}
+static void yput(orc_machine *m, u32 r, y256 v, int l256) {
+  memcpy(m->r.xmm[r & 15], v.l.b, 16);
+  if (l256) memcpy(m->r.ymmh[r & 15], v.h.b, 16);
+  else memset(m->r.ymmh[r & 15], 0, 16);
+}
+
+/* two-source ops of one 128-bit lane (the legacy semantics); 0 = not one */
+static int vlane(u32 op, int pc, const x128 *a, const x128 *b, u8 imm, u64 cnt, x128 *r) {
+  const u32 lo = op & 0xf7;
+  memset(r->b, 0, 16);
+  switch (op) {
+  case 0x14: case 0x15: *r = unpack(pc ? 8 : 4, op == 0x15, a, b); return 1;
+  case 0x54: case 0x55: case 0x56: case 0x57: case 0xdb: case 0xdf: case 0xeb: case 0xef:
+    for (int i = 0; i < 16; i++) {
+      const u8 x = a->b[i], y = b->b[i];
+      r->b[i] = (op == 0x54 || op == 0xdb) ? (u8)(x & y) : (op == 0x55 || op == 0xdf) ? (u8)(~x & y)
+              : (op == 0x56 || op == 0xeb) ? (u8)(x | y) : (u8)(x ^ y);
+    }
+    return 1;
+  case 0x60: case 0x61: case 0x62: case 0x6c: case 0x68: case 0x69: case 0x6a: case 0x6d:
+    *r = unpack(lo == 0x60 ? 1 : lo == 0x61 ? 2 : lo == 0x62 ? 4 : 8, op == 0x68 || op == 0x69 || op == 0x6a || op == 0x6d, a, b);
+    return 1;
+  case 0x63: case 0x67: case 0x6b: {
+    const int w = op == 0x6b ? 4 : 2, n = 16 / w;
+    for (int i = 0; i < 2 * n; i++) {
+      const i64 x = i < n ? sel(a, i, w) : sel(b, i - n, w);
+      elput(r, i, w / 2, op == 0x67 ? satu(x, 1) : sats(x, w / 2));
+    }
+    return 1;
+  }
+  case 0x64: case 0x65: case 0x66: case 0x74: case 0x75: case 0x76:
+    *r = ewise(op >= 0x74 ? EW_EQ : EW_GT, 1 << ((op & 0xf) % 4), a, b);
+    return 1;
+  case 0x70:
+    *r = *b;
+    if (pc == 1)
+      for (int i = 0; i < 4; i++) elput(r, i, 4, el(b, (imm >> (2 * i)) & 3, 4));
+    else
+      for (int i = 0; i < 4; i++) elput(r, i + (pc == 2 ? 4 : 0), 2, el(b, ((imm >> (2 * i)) & 3) + (pc == 2 ? 4 : 0), 2));
+    return 1;
+  case 0xc6:
+    if (pc == 0) {
+      elput(r, 0, 4, el(a, imm & 3, 4));
+      elput(r, 1, 4, el(a, (imm >> 2) & 3, 4));
+      elput(r, 2, 4, el(b, (imm >> 4) & 3, 4));
+      elput(r, 3, 4, el(b, (imm >> 6) & 3, 4));
+    } else {
+      elput(r, 0, 8, el(a, imm & 1, 8));
+      elput(r, 1, 8, el(b, (imm >> 1) & 1, 8));
+    }
+    return 1;
+  case 0xd1: case 0xd2: case 0xd3: *r = shift_el(0, op == 0xd1 ? 2 : op == 0xd2 ? 4 : 8, a, cnt); return 1;
+  case 0xe1: case 0xe2: *r = shift_el(1, op == 0xe1 ? 2 : 4, a, cnt); return 1;
+  case 0xf1: case 0xf2: case 0xf3: *r = shift_el(2, op == 0xf1 ? 2 : op == 0xf2 ? 4 : 8, a, cnt); return 1;
+  case 0xd4: *r = ewise(EW_ADD, 8, a, b); return 1;
+  case 0xfb: *r = ewise(EW_SUB, 8, a, b); return 1;
+  case 0xfc: case 0xfd: case 0xfe: *r = ewise(EW_ADD, 1 << (op - 0xfc), a, b); return 1;
+  case 0xf8: case 0xf9: case 0xfa: *r = ewise(EW_SUB, 1 << (op - 0xf8), a, b); return 1;
+  case 0xd5: *r = ewise(EW_MULLO, 2, a, b); return 1;
+  case 0xe5: *r = ewise(EW_MULHS, 2, a, b); return 1;
+  case 0xe4: *r = ewise(EW_MULHU, 2, a, b); return 1;
+  case 0xd8: case 0xd9: *r = ewise(EW_SUBUS, op - 0xd7, a, b); return 1;
+  case 0xdc: case 0xdd: *r = ewise(EW_ADDUS, op - 0xdb, a, b); return 1;
+  case 0xe8: case 0xe9: *r = ewise(EW_SUBS, op - 0xe7, a, b); return 1;
+  case 0xec: case 0xed: *r = ewise(EW_ADDS, op - 0xeb, a, b); return 1;
+  case 0xda: *r = ewise(EW_MINU, 1, a, b); return 1;
+  case 0xde: *r = ewise(EW_MAXU, 1, a, b); return 1;
+  case 0xea: *r = ewise(EW_MINS, 2, a, b); return 1;
+  case 0xee: *r = ewise(EW_MAXS, 2, a, b); return 1;
+  case 0xe0: *r = ewise(EW_AVG, 1, a, b); return 1;
+  case 0xe3: *r = ewise(EW_AVG, 2, a, b); return 1;
+  case 0xf4:
+    elput(r, 0, 8, el(a, 0, 4) * el(b, 0, 4));
+    elput(r, 1, 8, el(a, 2, 4) * el(b, 2, 4));
+    return 1;
+  case 0xf5:
+    for (int i = 0; i < 4; i++)
+      elput(r, i, 4, (u64)(sel(a, 2 * i, 2) * sel(b, 2 * i, 2) + sel(a, 2 * i + 1, 2) * sel(b, 2 * i + 1, 2)) & 0xffffffffULL);
+    return 1;
+  case 0xf6:
+    for (int h = 0; h < 2; h++) {
+      u64 sum = 0;
+      for (int i = 8 * h; i < 8 * h + 8; i++) sum += a->b[i] > b->b[i] ? a->b[i] - b->b[i] : b->b[i] - a->b[i];
+      elput(r, h, 8, sum);
+    }
+    return 1;
+  default: return 0;
+  }
+}
+
+static x128 vshift_imm(u32 op, u32 r3, const x128 *b, u8 imm) {
+  x128 r;
+  if (op == 0x73 && (r3 == 3 || r3 == 7)) {
+    memset(r.b, 0, 16);
+    for (int i = 0; i < 16; i++) {
+      const int src = r3 == 3 ? i + imm : i - imm;
+      if (src >= 0 && src < 16) r.b[i] = b->b[src];
+    }
+    return r;
+  }
+  return shift_el(r3 == 2 ? 0 : r3 == 4 ? 1 : 2, op == 0x71 ? 2 : op == 0x72 ? 4 : 8, b, imm);
+}
+
+static int vex_valid(u32 map, u32 op, int pp, int mem, u32 r3) {
+  if (map == 2) return pp == 1 && (op == 0x00 || op == 0x17 || op == 0x58 || op == 0x59 || op == 0x78 || op == 0x79);
+  if (map != 1) return 0;
+  if (op == 0x77) return pp == 0;
+  if (op >= 0x10 && op <= 0x17) return op <= 0x11 || pp <= 1;
+  if (op == 0x28 || op == 0x29 || op == 0x2b || op == 0x50 || op == 0xc6 || (op >= 0x54 && op <= 0x57)) return pp <= 1;
+  if ((op >= 0x60 && op <= 0x6e) && op != 0x6f) return pp == 1;
+  if (op == 0x6f || op == 0x7f || op == 0x7e) return pp == 1 || pp == 2;
+  if (op == 0x70) return pp != 0;
+  if (op >= 0x71 && op <= 0x73) {
+    if (pp != 1) return 0;
+    if (mem) return 1;
+    return op == 0x73 ? (r3 == 2 || r3 == 3 || r3 == 6 || r3 == 7) : (r3 == 2 || r3 == 4 || r3 == 6);
+  }
+  if (op == 0x74 || op == 0x75 || op == 0x76 || op == 0xc4 || op == 0xc5) return pp == 1;
+  if (op >= 0xd0) return pp == 1 && op != 0xd0 && op != 0xe6 && op != 0xf0 && op != 0xf7 && op != 0xff;
+  return 0;
+}
+
+static int exec_vex(orc_machine *m, insn *d) {
+  const u32 op = d->op, r3 = d->reg & 7, map = d->opmap, vv = d->vvvv;
+  const int pp = (int)d->vpp, l256 = (int)d->vl, mem = d->is_mem;
+  const u8 imm = d->bytes[d->len - 1];
+  if (!vex_valid(map, op, pp, mem, r3)) return X_UNIMPL;
+  int ud = d->vbad || !((m->r.cr4 >> 18) & 1) || (m->r.xcr0 & 6) != 6;
+  int two = 0, no256 = 0, reg_only = 0, mem_only = 0;
+  if (map == 1) {
+    two = ((op == 0x10 || op == 0x11) && (pp <= 1 || mem)) || op == 0x13 || op == 0x17 || op == 0x28 || op == 0x29 ||
+          op == 0x2b || op == 0x50 || op == 0x6e || op == 0x6f || op == 0x70 || op == 0x7e || op == 0x7f || op == 0xc5 ||
+          op == 0xd6 || op == 0xd7 || op == 0xe7 || op == 0x77;
+    no256 = op == 0x12 || op == 0x13 || op == 0x16 || op == 0x17 || op == 0x6e || op == 0x7e || op == 0xc4 ||
+            op == 0xc5 || op == 0xd6;
+    reg_only = (op >= 0x71 && op <= 0x73) || op == 0x50 || op == 0xd7 || op == 0xc5;
+    mem_only = op == 0x13 || op == 0x17 || op == 0x2b || op == 0xe7 || ((op == 0x12 || op == 0x16) && pp == 1);
+  } else {
+    two = op != 0x00;
+  }
+  if ((two && vv != 0) || (no256 && l256) || (reg_only && mem) || (mem_only && !mem)) ud = 1;
+  if (ud) {
+    fault(m, WTFGPU_VEC_UD, 0);
+    return X_FAULT;
+  }
+  if (m->r.cr0 & 8) {
+    fault(m, 7, 0);
+    return X_FAULT;
+  }
+  if (map == 1 && op == 0x77) { /* vzeroupper / vzeroall */
+    for (int i = 0; i < 16; i++) {
+      memset(m->r.ymmh[i], 0, 16);
+      if (l256) memset(m->r.xmm[i], 0, 16);
+    }
+    return X_OK;
+  }
+  const int vl = l256 ? 32 : 16;
+  int n = vl, align = 0;
+  if (map == 1) {
+    switch (op) {
+    case 0x10: case 0x11: n = pp <= 1 ? vl : pp == 2 ? 4 : 8; break;
+    case 0x12: case 0x13: case 0x16: case 0x17: case 0xd6: n = 8; break;
+    case 0x6e: case 0x7e: n = (pp == 2 || d->vw) ? 8 : 4; break;
+    case 0xc4: n = 2; break;
+    case 0x28: case 0x29: case 0x2b: case 0xe7: align = 1; break;
+    case 0x6f: case 0x7f: align = pp == 1; break;
+    case 0xd1: case 0xd2: case 0xd3: case 0xe1: case 0xe2: case 0xf1: case 0xf2: case 0xf3: n = 16; break;
+    default: break;
+    }
+  } else if (op == 0x58 || op == 0x59 || op == 0x78 || op == 0x79) {
+    n = op == 0x78 ? 1 : op == 0x79 ? 2 : op == 0x58 ? 4 : 8;
+  }
+  if (mem && align && (d->ea & (u64)(vl - 1))) {
+    fault(m, WTFGPU_VEC_GP, 0);
+    return X_FAULT;
+  }
+  const int store = map == 1 && (op == 0x11 || op == 0x13 || op == 0x17 || op == 0x29 || op == 0x2b || op == 0x7f ||
+                                 op == 0xe7 || op == 0xd6 || (op == 0x7e && pp == 1));
+  const y256 s = yreg(m, d->reg), a = yreg(m, vv);
+  y256 b, r;
+  memset(&b, 0, sizeof(b));
+  memset(&r, 0, sizeof(r));
+  if (!store) {
+    if (mem) {
+      if (vread_n(m, d->ea, (u32)n, b.l.b)) return X_FAULT;
+    } else if (map == 1 && (op == 0x6e || op == 0xc4)) {
+      const u64 g = m->r.gpr[d->rm];
+      memcpy(b.l.b, &g, 8);
+    } else {
+      b = yreg(m, d->rm);
+    }
+  }
+  u32 dst = d->reg;
+  if (map == 2) {
+    if (op == 0x17) { /* vptest */
+      u8 sa[32], sb[32];
+      memcpy(sa, s.l.b, 16);
+      memcpy(sa + 16, s.h.b, 16);
+      memcpy(sb, b.l.b, 16);
+      memcpy(sb + 16, b.h.b, 16);
+      ptest(m, sa, sb, vl);
+      return X_OK;
+    }
+    if (op == 0x00) { /* vpshufb */
+      r.l = pshufb(&a.l, &b.l);
+      r.h = pshufb(&a.h, &b.h);
+    } else { /* vpbroadcastb / w / d / q */
+      const int ew = op == 0x78 ? 1 : op == 0x79 ? 2 : op == 0x58 ? 4 : 8;
+      const u64 e = el(&b.l, 0, ew);
+      for (int i = 0; i < 16 / ew; i++) elput(&r.l, i, ew, e);
+      r.h = r.l;
+    }
+    yput(m, dst, r, l256);
+    return X_OK;
+  }
+  switch (op) {
+  case 0x10:
+    if (pp <= 1 || mem) r = b;
+    else {
+      r.l = a.l;
+      memcpy(r.l.b, b.l.b, pp == 2 ? 4 : 8);
+    }
+    break;
+  case 0x11: case 0x29: case 0x2b: case 0x7f: case 0xe7:
+    if (mem) {
+      u8 buf[32];
+      memcpy(buf, s.l.b, 16);
+      memcpy(buf + 16, s.h.b, 16);
+      return vwrite_n(m, d->ea, (u32)(op == 0x11 ? n : vl), buf) ? X_FAULT : X_OK;
+    }
+    if (op == 0x11 && pp >= 2) {
+      r.l = a.l;
+      memcpy(r.l.b, s.l.b, pp == 2 ? 4 : 8);
+      yput(m, d->rm, r, 0);
+    } else {
+      yput(m, d->rm, s, l256);
+    }
+    return X_OK;
+  case 0x12:
+    memcpy(r.l.b, mem ? b.l.b : b.l.b + 8, 8);
+    memcpy(r.l.b + 8, a.l.b + 8, 8);
+    break;
+  case 0x16:
+    memcpy(r.l.b, a.l.b, 8);
+    memcpy(r.l.b + 8, b.l.b, 8);
+    break;
+  case 0x13: return vwrite(m, d->ea, 8, s.l.b) ? X_FAULT : X_OK;
+  case 0x17: return vwrite(m, d->ea, 8, s.l.b + 8) ? X_FAULT : X_OK;
+  case 0x28: case 0x6f: r = b; break;
+  case 0x50: {
+    const int ew = pp ? 8 : 4;
+    u64 v = 0;
+    for (int i = 0; i < 16 / ew; i++) v |= (el(&b.l, i, ew) >> (8 * ew - 1)) << i;
+    if (l256)
+      for (int i = 0; i < 16 / ew; i++) v |= (el(&b.h, i, ew) >> (8 * ew - 1)) << (i + 16 / ew);
+    m->r.gpr[d->reg] = v;
+    return X_OK;
+  }
+  case 0xd7: {
+    u64 v = 0;
+    for (int i = 0; i < 16; i++) v |= (u64)(b.l.b[i] >> 7) << i;
+    if (l256)
+      for (int i = 0; i < 16; i++) v |= (u64)(b.h.b[i] >> 7) << (i + 16);
+    m->r.gpr[d->reg] = v;
+    return X_OK;
+  }
+  case 0x6e:
+    memset(b.l.b + n, 0, (size_t)(16 - n));
+    r.l = b.l;
+    break;
+  case 0x7e:
+    if (pp == 2) {
+      memcpy(r.l.b, b.l.b, 8);
+      break;
+    }
+    if (mem) return vwrite(m, d->ea, (u32)n, s.l.b) ? X_FAULT : X_OK;
+    m->r.gpr[d->rm] = el(&s.l, 0, n);
+    return X_OK;
+  case 0x70:
+    vlane(0x70, pp, &a.l, &b.l, imm, 0, &r.l);
+    vlane(0x70, pp, &a.h, &b.h, imm, 0, &r.h);
+    break;
+  case 0x71: case 0x72: case 0x73:
+    r.l = vshift_imm(op, r3, &b.l, imm);
+    r.h = vshift_imm(op, r3, &b.h, imm);
+    dst = vv;
+    break;
+  case 0xc4:
+    r.l = a.l;
+    elput(&r.l, imm & 7, 2, el(&b.l, 0, 2));
+    break;
+  case 0xc5:
+    m->r.gpr[d->reg] = el(&b.l, imm & 7, 2);
+    return X_OK;
+  case 0xd6:
+    if (mem) return vwrite(m, d->ea, 8, s.l.b) ? X_FAULT : X_OK;
+    memcpy(r.l.b, s.l.b, 8);
+    yput(m, d->rm, r, 0);
+    return X_OK;
+  default: {
+    const u64 cnt = el(&b.l, 0, 8);
+    if (!vlane(op, pp, &a.l, &b.l, imm, cnt, &r.l)) return X_UNIMPL;
+    vlane(op, pp, &a.h, &b.h, (u8)(op == 0xc6 && pp == 1 ? imm >> 2 : imm), cnt, &r.h);
+    break;
+  }
+  }
+  yput(m, dst, r, l256);
   return X_OK;
 }
 
@@ -1784,6 +2168,8 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
     }
   }
 
+  if (d->vex) return exec_vex(m, d);
+  if (d->opmap == 2) return exec_sse(m, d);
   if (d->opmap == 1) {
     if (sse_opcode(op)) return exec_sse(m, d);
     switch (op) {
@@ -2166,15 +2552,42 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
     d->rexx = (d->rex >> 1) & 1;
     d->rexb = d->rex & 1;
   }
-  if (b == 0x0f) {
+  if (b == 0xc4 || b == 0xc5) { /* VEX (always VEX in 64-bit mode) */
+    d->vex = 1;
+    d->vbad = d->pfx66 || d->rep || d->rex;
+    const u8 b1 = fetch8(m, d);
+    const u8 b2 = b == 0xc4 ? fetch8(m, d) : b1;
+    if (d->fetch_fail) return -1;
+    d->rexr = !((b1 >> 7) & 1);
+    d->rexx = b == 0xc4 ? !((b1 >> 6) & 1) : 0;
+    d->rexb = b == 0xc4 ? !((b1 >> 5) & 1) : 0;
+    d->opmap = b == 0xc4 ? (b1 & 31u) : 1;
+    d->vw = b == 0xc4 ? (b2 >> 7) & 1u : 0;
+    d->rexw = d->vw;
+    d->rex = 0x40 | (d->rexw << 3) | (d->rexr << 2) | (d->rexx << 1) | d->rexb;
+    d->vvvv = (~b2 >> 3) & 15u;
+    d->vl = (b2 >> 2) & 1u;
+    d->vpp = b2 & 3u;
+    b = fetch8(m, d);
+    if (d->fetch_fail) return -1;
+    if (d->opmap != 1 && d->opmap != 2) {
+      d->op = b;
+      d->len = d->pos;
+      return 1;
+    }
+  } else if (b == 0x0f) {
     d->opmap = 1;
     b = fetch8(m, d);
     if (d->fetch_fail) return -1;
     if (b == 0x38 || b == 0x3a) {
       d->opmap = b == 0x38 ? 2 : 3;
       d->op = fetch8(m, d);
-      d->len = d->pos;
-      return d->fetch_fail ? -1 : 1;
+      if (d->fetch_fail) return -1;
+      if (d->opmap == 3 || (d->op != 0x00 && d->op != 0x17)) { /* 0f 38 00 pshufb, 0f 38 17 ptest; the rest: outside */
+        d->len = d->pos;
+        return 1;
+      }
+      b = d->op;
     }
   }
   d->op = b;
@@ -2249,8 +2662,11 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
       imm = 1;
     }
     if (b >= 0x80 && b <= 0x8f) imm = 4;
-    if (sse_opcode(b)) has_modrm = 1;
-    if ((b >= 0x70 && b <= 0x73) || (b >= 0xc4 && b <= 0xc6)) imm = 1;
+    if (d->opmap == 2) has_modrm = 1;
+    else {
+      if (sse_opcode(b) && b != 0x77) has_modrm = 1;
+      if ((b >= 0x70 && b <= 0x73) || (b >= 0xc4 && b <= 0xc6)) imm = 1;
+    }
   }
   if (has_modrm) {
     decode_modrm(m, d, mr);

@@ -14,6 +14,7 @@ struct SimResult {
   uint64_t dirty[64];
   uint64_t xmm[32];
   uint32_t mxcsr, pad;
+  uint64_t ymmh[32];
 };
 
 int sim_run(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, const wtfgpu_regs_t *r0,
@@ -145,6 +146,7 @@ int sim_run(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, const 
   for (uint32_t k = 0; k < L.ovn && k < 64; k++) out->dirty[k] = (uint64_t)ovg[k] << 12;
   for (int k = 0; k < 16; k++) out->xmm[2 * k] = full.xmm[k][0], out->xmm[2 * k + 1] = full.xmm[k][1];
   out->mxcsr = full.mxcsr;
+  for (int k = 0; k < 16; k++) out->ymmh[2 * k] = full.ymmh[k][0], out->ymmh[2 * k + 1] = full.ymmh[k][1];
   free(pool);
   free(ov);
   return 0;

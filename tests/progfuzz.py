@@ -73,8 +73,10 @@ def build(n_programs: int, seed: int, sse: bool = False):
     if sse:
         from tests.golden.gen_sse_vectors import gen_forms as gen_sse_forms
 
-        sse_forms = gen_sse_forms(random.Random(seed ^ 0x55E))
-        forms = forms + sse_forms * 3  # mostly SSE
+        from tests.golden.gen_avx_vectors import gen_forms as gen_avx_forms
+
+        sse_forms = gen_sse_forms(random.Random(seed ^ 0x55E)) + gen_avx_forms(random.Random(seed ^ 0xA0C))
+        forms = forms + sse_forms * 3  # mostly SSE / AVX
     sp = AddressSpace()
     progs = []
     for i in range(n_programs):
@@ -96,13 +98,13 @@ def build(n_programs: int, seed: int, sse: bool = False):
     return sp, st, lanes
 
 
-def lane_xmm(n: int, seed: int):
-    """Initial XMM registers per lane (32 u64 each)."""
-    rng = random.Random(seed ^ 0x3E3)
+def lane_xmm(n: int, seed: int, salt: int = 0x3E3):
+    """Initial XMM registers per lane (32 u64 each); salt 0x4E4: the YMM upper halves."""
+    rng = random.Random(seed ^ salt)
     return [[rng.getrandbits(64) for _ in range(32)] for _ in range(n)]
 
 
-def oracle_run(sp: AddressSpace, st: dict, lanes, limit=20000, breakpoints=(), xmm=None):
+def oracle_run(sp: AddressSpace, st: dict, lanes, limit=20000, breakpoints=(), xmm=None, ymmh=None):
     """Runs every lane on the CPU oracle; returns per-lane result dicts."""
     from tests.oracle_lib import Oracle
 
@@ -119,6 +121,9 @@ def oracle_run(sp: AddressSpace, st: dict, lanes, limit=20000, breakpoints=(), x
         if xmm is not None:
             for k in range(16):
                 r.xmm[k][0], r.xmm[k][1] = xmm[i][2 * k], xmm[i][2 * k + 1]
+        if ymmh is not None:
+            for k in range(16):
+                r.ymmh[k][0], r.ymmh[k][1] = ymmh[i][2 * k], ymmh[i][2 * k + 1]
         r.rip = va
         r.rflags = flags
         o.restore(base)
@@ -131,5 +136,6 @@ def oracle_run(sp: AddressSpace, st: dict, lanes, limit=20000, breakpoints=(), x
             "dirty": set(o.dirty()), "bytes": o.nbytes(),
             "win": o.read_virt(WIN_VA, 0x2000), "stack": o.read_virt(STACK_VA, 0x2000),
             "xmm": [rr.xmm[k][h] for k in range(16) for h in range(2)], "mxcsr": rr.mxcsr,
+            "ymmh": [rr.ymmh[k][h] for k in range(16) for h in range(2)],
         })
     return out

@@ -1,0 +1,181 @@
+"""AVX / AVX2 (VEX) subset and the legacy pshufb / ptest.
+
+The oracle and the engine's own code built for the host (tests/native/
+sim_lane.cc) against native-execution vectors (tests/golden/gen_avx_vectors.py:
+16 GPRs, RFLAGS, 16 YMM registers at 256 bits and a 256-byte memory window),
+then the #UD / #NM / #GP rules native execution cannot show. The GPU runs the
+same vectors in tests/test_gpu_sse.py.
+"""
+import gzip
+import json
+import os
+
+import pytest
+
+from tests.golden.gen_native_vectors import splitmix_bytes
+from tests.test_sse import BUF, layout, sim_lib, sim_run
+from tests.oracle_lib import Oracle
+from wtf_amd.abi import EXIT_FAULT, EXIT_UNIMPLEMENTED, RUNNING
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CODE_VA = 0x140001000
+
+
+def load():
+    with gzip.open(os.path.join(HERE, "golden", "avx_vectors.json.gz"), "rt") as f:
+        return json.load(f)
+
+
+DOC = load()
+
+
+def set_ymm(regs, ys):
+    for i in range(16):
+        regs.xmm[i][0], regs.xmm[i][1] = ys[4 * i], ys[4 * i + 1]
+        regs.ymmh[i][0], regs.ymmh[i][1] = ys[4 * i + 2], ys[4 * i + 3]
+
+
+def get_ymm(xmm, ymmh):
+    """32 + 32 u64 (xmm / ymmh, reg-major) -> 64 u64 in native ymm order."""
+    out = []
+    for i in range(16):
+        out += [xmm[2 * i], xmm[2 * i + 1], ymmh[2 * i], ymmh[2 * i + 1]]
+    return out
+
+
+def case_regs(c, regs):
+    for i in range(16):
+        regs.gpr[i] = int(c["in"][i], 16)
+    regs.rflags = int(c["fl"], 16) | 0x200
+    set_ymm(regs, [int(v, 16) for v in c["yin"]])
+    return regs
+
+
+def window(c):
+    return splitmix_bytes(int(c["seed"], 16), 256)
+
+
+@pytest.mark.parametrize("chunk", range(4))
+def test_oracle_matches_native_avx(chunk):
+    buf_va = int(DOC["buf_va"], 16)
+    fails = []
+    cases = DOC["cases"][chunk::4]
+    for c in cases:
+        sp, regs = layout(bytes.fromhex(c["code"]), buf_va, window(c))
+        pfns, blob = sp.phys()
+        o = Oracle(pfns=pfns, blob=blob)
+        o.restore(case_regs(c, regs))
+        ex = o.step()
+        if ex.status != RUNNING:
+            fails.append((c["name"], c["code"], "exit", ex.status, ex.vector))
+            continue
+        r = o.regs()
+        if list(r.gpr) != [int(x, 16) for x in c["out"]] or (r.rflags ^ int(c["flo"], 16)) & 0x8D5:
+            fails.append((c["name"], c["code"], "regs"))
+            continue
+        got = get_ymm([r.xmm[i][h] for i in range(16) for h in range(2)],
+                      [r.ymmh[i][h] for i in range(16) for h in range(2)])
+        if got != [int(v, 16) for v in c["yout"]]:
+            fails.append((c["name"], c["code"], "ymm"))
+            continue
+        win = bytearray(window(c))
+        for i, v in c["diff"]:
+            win[i] = v
+        if o.read_virt(buf_va, 256) != bytes(win):
+            fails.append((c["name"], c["code"], "mem"))
+    assert not fails, f"{len(fails)}/{len(cases)} mismatches, first: {fails[:6]}"
+
+
+def test_engine_avx_code_matches_native_vectors():
+    L = sim_lib()
+    buf_va = int(DOC["buf_va"], 16)
+    fails = []
+    for c in DOC["cases"]:
+        sp, regs = layout(bytes.fromhex(c["code"]), buf_va, window(c))
+        out = sim_run(L, sp, case_regs(c, regs))
+        if out.status != 3 or out.icount != 1:
+            fails.append((c["name"], c["code"], "exit", out.status, out.vector))
+        elif list(out.gpr) != [int(x, 16) for x in c["out"]] or (out.rflags ^ int(c["flo"], 16)) & 0x8D5:
+            fails.append((c["name"], c["code"], "regs"))
+        elif get_ymm(list(out.xmm), list(out.ymmh)) != [int(v, 16) for v in c["yout"]]:
+            fails.append((c["name"], c["code"], "ymm"))
+    assert not fails, f"{len(fails)}/{len(DOC['cases'])} mismatches, first: {fails[:6]}"
+
+
+def test_avx_vector_file_is_substantial():
+    assert len(DOC["cases"]) > 2000
+    names = {c["name"].split(".")[0] for c in DOC["cases"]}
+    for n in ("vmovdqu", "vmovdqa", "vpmovmskb", "vzero", "vptest", "vpshufb", "vpbroadcast78", "pshufb", "ptest"):
+        assert n in names, n
+
+
+# ---- hand-checked: VEX #UD rules, alignment, AVX state
+AVX_FAULT_CASES = [
+    ([0xC5, 0xFE, 0x6F, 0x06], RUNNING, None),             # vmovdqu ymm0, [rsi]: unaligned is fine
+    ([0xC5, 0xFD, 0x6F, 0x03], EXIT_FAULT, 13),             # vmovdqa ymm0, [rbx]: rbx 16- but not 32-aligned
+    ([0xC5, 0xF9, 0x6F, 0x03], RUNNING, None),             # vmovdqa xmm0, [rbx]: 16-aligned
+    ([0xC5, 0xF9, 0x6F, 0x06], EXIT_FAULT, 13),             # vmovdqa xmm0, [rsi]: misaligned
+    ([0xC5, 0xF5, 0xEF, 0x06], RUNNING, None),             # vpxor ymm0, ymm1, [rsi]: VEX needs no alignment
+    ([0xC5, 0xF6, 0x6F, 0xC1], EXIT_FAULT, 6),              # vmovdqu with vvvv != 1111
+    ([0xC5, 0xFD, 0x6E, 0xC0], EXIT_FAULT, 6),              # vmovd with L = 1
+    ([0x66, 0xC5, 0xF9, 0xEF, 0xC1], EXIT_FAULT, 6),        # 66 before VEX
+    ([0x48, 0xC5, 0xF9, 0xEF, 0xC1], EXIT_FAULT, 6),        # REX before VEX
+    ([0xC5, 0xFD, 0xD7, 0x03], EXIT_FAULT, 6),              # vpmovmskb eax, [rbx]: register only
+    ([0xC5, 0xFC, 0x58, 0xC1], EXIT_UNIMPLEMENTED, None),   # vaddps (floating point)
+    ([0xC4, 0xE3, 0x79, 0x0F, 0xC1, 0x04], EXIT_UNIMPLEMENTED, None),  # vpalignr (0f 3a)
+    ([0xC4, 0xE2, 0x79, 0x1C, 0xC1], EXIT_UNIMPLEMENTED, None),        # vpabsb (0f 38 1c)
+    ([0x66, 0x0F, 0x38, 0x00, 0x06], EXIT_FAULT, 13),      # pshufb xmm0, [rsi]: legacy needs alignment
+    ([0x66, 0x0F, 0x38, 0x1C, 0xC1], EXIT_UNIMPLEMENTED, None),        # pabsb (outside)
+]
+
+
+def run1(code, cr0=None, cr4=None, xcr0=None, L=None):
+    sp, regs = layout(bytes(code), BUF, bytes(range(256)), cr0=cr0, cr4=cr4)
+    regs.gpr[3] = BUF + 0x10  # rbx: 16-aligned, not 32-aligned (BUF is 0x...800)
+    regs.gpr[6] = BUF + 0x13
+    if xcr0 is not None:
+        regs.xcr0 = xcr0
+    pfns, blob = sp.phys()
+    o = Oracle(pfns=pfns, blob=blob)
+    o.restore(regs)
+    ex = o.step()
+    sim = sim_run(L, sp, regs) if L is not None else None
+    return ex, sim
+
+
+@pytest.mark.parametrize("code,status,vector", AVX_FAULT_CASES)
+def test_avx_faults_oracle_and_engine(code, status, vector):
+    L = sim_lib()
+    ex, sim = run1(code, L=L)
+    assert ex.status == status, (bytes(code).hex(), ex.status, ex.vector)
+    if vector is not None:
+        assert ex.vector == vector
+    want_sim = 3 if status == RUNNING else status
+    assert sim.status == want_sim and (vector is None or sim.vector == vector), (sim.status, sim.vector)
+
+
+def test_avx_state_gating():
+    L = sim_lib()
+    vpxor = [0xC5, 0xF5, 0xEF, 0xC2]
+    for kw, vec in ((dict(cr4=0x370678 & ~0x40000), 6), (dict(xcr0=0x3), 6), (dict(cr0=0x80050031 | 8), 7)):
+        ex, sim = run1(vpxor, L=L, **kw)
+        assert (ex.status, ex.vector) == (EXIT_FAULT, vec), kw
+        assert (sim.status, sim.vector) == (EXIT_FAULT, vec), kw
+    ex, sim = run1(vpxor, L=L, cr0=0x80050031 | 4)  # CR0.EM does not gate VEX
+    assert ex.status == RUNNING and sim.status == 3
+
+
+def test_vzeroupper_keeps_low_halves_and_legacy_keeps_high():
+    # vzeroupper ; movaps xmm1, xmm2 (legacy: ymm1's upper half stays) ; vmovaps xmm3, xmm2 (VEX.128: zeroed)
+    code = [0xC5, 0xF8, 0x77, 0x0F, 0x28, 0xCA, 0xC5, 0xF8, 0x28, 0xDA]
+    sp, regs = layout(bytes(code), BUF, bytes(256))
+    for i in range(16):
+        regs.xmm[i][0], regs.xmm[i][1] = i + 1, i + 2
+        regs.ymmh[i][0], regs.ymmh[i][1] = 100 + i, 200 + i
+    pfns, blob = sp.phys()
+    o = Oracle(pfns=pfns, blob=blob)
+    o.restore(regs)
+    assert o.step().status == RUNNING
+    r = o.regs()
+    assert all(r.ymmh[i][0] == 0 and r.ymmh[i][1] == 0 for i in range(16))
+    assert all(r.xmm[i][0] == i + 1 for i in range(16))

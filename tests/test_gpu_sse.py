@@ -141,7 +141,8 @@ def test_gpu_matches_oracle_on_random_sse_programs(seed):
     n = 512
     sp, st, lanes = progfuzz.build(n, seed=seed, sse=True)
     xmm = progfuzz.lane_xmm(n, seed)
-    want = progfuzz.oracle_run(sp, st, lanes, xmm=xmm)
+    ymmh = progfuzz.lane_xmm(n, seed, 0x4E4)
+    want = progfuzz.oracle_run(sp, st, lanes, xmm=xmm, ymmh=ymmh)
     eng = Engine(0)
     pfns, blob = sp.phys()
     eng.load_pool(pfns, blob)
@@ -156,6 +157,8 @@ def test_gpu_matches_oracle_on_random_sse_programs(seed):
         regs[i].rip = va
         regs[i].rflags = flags
         set_xmm(regs[i], xmm[i])
+        for k in range(16):
+            regs[i].ymmh[k][0], regs[i].ymmh[k][1] = ymmh[i][2 * k], ymmh[i][2 * k + 1]
     eng.write_regs(regs)
     stats = eng.run()
     ex = eng.exits()
@@ -174,6 +177,8 @@ def test_gpu_matches_oracle_on_random_sse_programs(seed):
             bad.append((i, "regs"))
         elif get_xmm(r) != w["xmm"] or r.mxcsr != w["mxcsr"]:
             bad.append((i, "xmm"))
+        elif [r.ymmh[k][h] for k in range(16) for h in range(2)] != w["ymmh"]:
+            bad.append((i, "ymm"))
         elif cov.get(i, set()) != w["cov"]:
             bad.append((i, "cov"))
         elif set(eng.dirty(i)) != w["dirty"]:
@@ -188,3 +193,66 @@ def test_gpu_matches_oracle_on_random_sse_programs(seed):
     statuses = np.bincount([w["status"] for w in want], minlength=13)
     assert statuses[EXIT_INT3] > n // 8, statuses  # most programs run to the end
     assert not bad, f"{len(bad)}/{n} lanes differ; first: {bad[:4]}"
+
+
+def test_gpu_matches_native_avx_vectors():
+    """Every AVX / AVX2 vector (tests/golden/avx_vectors.json.gz) as one lane:
+    GPRs, RFLAGS, all 16 YMM registers and the memory window."""
+    from tests.test_avx import DOC, get_ymm, set_ymm, window
+    from wtf_amd.engine import Engine
+
+    cases = DOC["cases"]
+    codes = sorted({c["code"] for c in cases})
+    slot = {c: i for i, c in enumerate(codes)}
+    blob = bytearray(32 * len(codes))
+    for c, i in slot.items():
+        b = bytes.fromhex(c) + b"\xcc"
+        blob[32 * i: 32 * i + len(b)] = b
+    sp = AddressSpace()
+    sp.map_range(CODE_VA, bytes(blob), write=False)
+    buf_va = int(DOC["buf_va"], 16)
+    sp.map(buf_va & ~0xFFF, b"", nx=True)
+    sp.map((buf_va & ~0xFFF) + 0x1000, b"", nx=True)
+    n = (len(cases) + 63) // 64 * 64
+    eng = Engine(0)
+    pfns, pblob = sp.phys()
+    eng.load_pool(pfns, pblob)
+    eng.alloc_lanes(n, overlay_pages=4, cov_entries=64)
+    eng.set_initial_state(regs_from_state(user_state(CODE_VA, 0, sp.cr3)))
+    eng.set_limit(0)
+    eng.restore()
+    regs = eng.read_regs(0, n)
+    writes = []
+    for i, c in enumerate(cases):
+        r = regs[i]
+        for k in range(16):
+            r.gpr[k] = int(c["in"][k], 16)
+        r.rip = CODE_VA + 32 * slot[c["code"]]
+        r.rflags = int(c["fl"], 16) | 0x200
+        set_ymm(r, [int(v, 16) for v in c["yin"]])
+        writes.append((i, buf_va, window(c)))
+    for i in range(len(cases), n):
+        regs[i].rip = CODE_VA + 32 * slot[cases[0]["code"]] + len(bytes.fromhex(cases[0]["code"]))
+    eng.write_regs(regs)
+    eng.apply_writes(writes)
+    eng.run()
+    ex = eng.exits()
+    out = eng.read_regs(0, n)
+    fails = []
+    for i, c in enumerate(cases):
+        r = out[i]
+        if ex[i].status != EXIT_INT3 or ex[i].icount != 1:
+            fails.append((c["name"], c["code"], "exit", ex[i].status, ex[i].vector))
+        elif [r.gpr[k] for k in range(16)] != [int(v, 16) for v in c["out"]] or \
+                (r.rflags ^ int(c["flo"], 16)) & 0x8D5:
+            fails.append((c["name"], c["code"], "regs"))
+        elif get_ymm([r.xmm[k][h] for k in range(16) for h in range(2)],
+                     [r.ymmh[k][h] for k in range(16) for h in range(2)]) != [int(v, 16) for v in c["yout"]]:
+            fails.append((c["name"], c["code"], "ymm"))
+        else:
+            win = bytearray(window(c))
+            for k, v in c["diff"]:
+                win[k] = v
+            if (c["diff"] or i % 5 == 0) and eng.read_virt(i, buf_va, 256) != bytes(win):
+                fails.append((c["name"], c["code"], "mem"))
+    assert not fails, f"{len(fails)}/{len(cases)} mismatches, first: {fails[:6]}"

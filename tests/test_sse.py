@@ -205,7 +205,7 @@ class SimResult(C.Structure):
     _fields_ = [("gpr", C.c_uint64 * 16), ("rip", C.c_uint64), ("rflags", C.c_uint64), ("icount", C.c_uint64),
                 ("nbytes", C.c_uint64), ("status", C.c_uint32), ("vector", C.c_uint32), ("error", C.c_uint32),
                 ("ovn", C.c_uint32), ("addr", C.c_uint64), ("dirty", C.c_uint64 * 64), ("xmm", C.c_uint64 * 32),
-                ("mxcsr", C.c_uint32), ("pad", C.c_uint32)]
+                ("mxcsr", C.c_uint32), ("pad", C.c_uint32), ("ymmh", C.c_uint64 * 32)]
 
 
 def sim_lib():
@@ -261,13 +261,15 @@ def test_engine_sse_code_matches_oracle_on_random_programs():
     n = 160
     sp, st, lanes = progfuzz.build(n, seed=31, sse=True)
     xmm = progfuzz.lane_xmm(n, 31)
-    want = progfuzz.oracle_run(sp, st, lanes, xmm=xmm)
+    ymmh = progfuzz.lane_xmm(n, 31, 0x4E4)
+    want = progfuzz.oracle_run(sp, st, lanes, xmm=xmm, ymmh=ymmh)
     bad = []
     for i, ((va, g, flags), w) in enumerate(zip(lanes, want)):
         regs = regs_from_state(st)
         for k in range(16):
             regs.gpr[k] = g[k]
             regs.xmm[k][0], regs.xmm[k][1] = xmm[i][2 * k], xmm[i][2 * k + 1]
+            regs.ymmh[k][0], regs.ymmh[k][1] = ymmh[i][2 * k], ymmh[i][2 * k + 1]
         regs.rip, regs.rflags = va, flags
         out = sim_run(L, sp, regs, limit=20000)
         got = (out.status, out.vector if out.status == EXIT_FAULT else 0, out.rip, out.icount)
@@ -278,6 +280,8 @@ def test_engine_sse_code_matches_oracle_on_random_programs():
             bad.append((i, "regs"))
         elif list(out.xmm) != w["xmm"] or out.mxcsr != w["mxcsr"]:
             bad.append((i, "xmm"))
+        elif list(out.ymmh) != w["ymmh"]:
+            bad.append((i, "ymm"))
         elif out.nbytes != w["bytes"]:
             bad.append((i, "bytes", out.nbytes, w["bytes"]))
         elif {out.dirty[k] for k in range(min(out.ovn, 64))} != w["dirty"]:

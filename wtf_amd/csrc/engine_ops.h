@@ -174,7 +174,7 @@ __constant__ u32 kMap2[256] = {
     /*40*/ CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV,
     /*50*/ SSE8, SSE8,
     /*60*/ SSE8, SSE8,
-    /*70*/ SSEI, SSEI, SSEI, SSEI, SSEM, SSEM, SSEM, SSEM, SSE8,
+    /*70*/ SSEI, SSEI, SSEI, SSEI, SSEM, SSEM, SSEM, E(O_SSE, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), SSE8,
     /*80*/ JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32,
     /*90*/ SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC,
     /*a0*/ UN, UN, UN, E(O_BT, L_RM, L_GREG, Z_V, Z_V, 1, 0, 0, 1, K_NONE, 0), SHXD(K_B), SHXD(K_NONE), UN, UN,
@@ -193,6 +193,8 @@ __constant__ u32 kMap2[256] = {
     /*e0*/ SSE8, SSE8,
     /*f0*/ SSE8, SSE8,
 };
+constexpr u32 kSseModrm = E(O_SSE, 0, 0, 0, 0, 0, 0, 0, 1, K_NONE, 0);  // 0f 38 / VEX map 2 opcodes
+constexpr u32 kUnimpl = UN;
 #undef E
 #undef UN
 #undef ALU4
@@ -261,26 +263,57 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
     else if (c != 0xf0 && c != 0x26 && c != 0x2e && c != 0x36 && c != 0x3e) break;
     rex = 0;
   }
+  // VEX (c4 / c5; always VEX in 64-bit mode): its fields become the REX bits,
+  // the map and `vex` (engine_sse.h: UOp::opreg of an O_SSE op)
+  u32 vex = 0, vpp = 0;
+  if (c == 0xc4 || c == 0xc5) {
+    const u32 bad = (p66 || u.rep || rex) ? 1u : 0u;  // a legacy 66 / f2 / f3 / REX before VEX: #UD
+    const u32 nb = c == 0xc4 ? 2 : 1;
+    if (pos + nb + 1 > 15) return 2;
+    if (pos + nb + 1 > b.avail) return 1;
+    const u32 b1 = ib_at(b, pos), b2 = c == 0xc4 ? ib_at(b, pos + 1) : b1;
+    pos += nb;
+    const u32 vr = ((b1 >> 7) & 1) ^ 1;
+    const u32 vx = c == 0xc4 ? ((b1 >> 6) & 1) ^ 1 : 0, vb = c == 0xc4 ? ((b1 >> 5) & 1) ^ 1 : 0;
+    const u32 vmap = c == 0xc4 ? (b1 & 31) : 1, vw = c == 0xc4 ? (b2 >> 7) & 1 : 0;
+    vpp = b2 & 3;
+    vex = 1 | (((b2 >> 2) & 1) << 1) | (vw << 2) | ((((~b2) >> 3) & 15) << 4) | (vmap << 8) | (bad << 16);
+    rex = 0x40 | (vw << 3) | (vr << 2) | (vx << 1) | vb;
+    c = ib_at(b, pos++);  // the opcode
+  }
   u.rex = rex;
   const u32 rexw = (rex >> 3) & 1, rexr = (rex >> 2) & 1, rexx = (rex >> 1) & 1, rexb = rex & 1;
-  u32 e, map2 = 0;
-  if (c == 0x0f) {
+  u32 e, map2 = 0, smap = 1;
+  if (vex) {
+    smap = vex_map(vex);
+    map2 = 1;
+    e = smap == 1 ? kMap2[c] : smap == 2 ? kSseModrm : kUnimpl;
+    if (smap == 1 && (e & 63) != O_SSE) e = kUnimpl;
+  } else if (c == 0x0f) {
     if (pos >= 15) return 2;
     if (pos >= b.avail) return 1;
     c = ib_at(b, pos++);
-    if (c == 0x38 || c == 0x3a) {  // three-byte maps: outside the ISA subset
+    if (c == 0x38 || c == 0x3a) {  // three-byte maps: 0f 38 00 (pshufb), 0f 38 17 (ptest), the rest outside the subset
       if (pos >= 15) return 2;
       if (pos >= b.avail) return 1;
-      pos++;
-      u.len = pos;
-      u.op = O_UNIMPL;
-      u.supported = 0;
-      u.opbytes = pos >= 4 ? (u32)b.lo : ((u32)b.lo & ((1u << (8 * pos)) - 1));
-      return 0;
+      const u32 c3 = ib_at(b, pos++);
+      if (c == 0x38 && (c3 == 0x00 || c3 == 0x17)) {
+        c = c3;
+        smap = 2;
+        map2 = 1;
+        e = kSseModrm;
+      } else {
+        u.len = pos;
+        u.op = O_UNIMPL;
+        u.supported = 0;
+        u.opbytes = pos >= 4 ? (u32)b.lo : ((u32)b.lo & ((1u << (8 * pos)) - 1));
+        return 0;
+      }
+    } else {
+      map2 = 1;
+      e = kMap2[c];
+      if (c == 0xb8 && u.rep != 0xf3) e = O_UNIMPL;  // popcnt needs f3
     }
-    map2 = 1;
-    e = kMap2[c];
-    if (c == 0xb8 && u.rep != 0xf3) e = O_UNIMPL;  // popcnt needs f3
   } else {
     e = kMap1[c];
     if (c == 0x90 && !rexb) e = O_NOP;  // 90 is nop (no zero-extension), f3 90 pause
@@ -417,10 +450,17 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
   }
   if (u.op == O_ALU && u.sub == 7) u.awrite = 0;  // cmp reads its destination, never writes it
   if (map2) {
-    if (u.op == O_SSE) {  // engine_sse.h: opcode in sub, mandatory-prefix class in bsz
+    if (u.op == O_SSE) {  // engine_sse.h: opcode in sub, mandatory-prefix class in bsz, map / VEX in opreg
       u.sub = c;
-      u.bsz = u.rep == 0xf3 ? 2 : u.rep == 0xf2 ? 3 : p66 ? 1 : 0;
-      if (!sse_valid(c, u.bsz, u.is_mem, u.reg & 7)) u.op = O_UNIMPL;
+      if (vex) {
+        u.bsz = vpp;
+        u.opreg = vex;
+        if (!vex_valid(smap, c, vpp, u.is_mem, u.reg & 7)) u.op = O_UNIMPL;
+      } else {
+        u.bsz = u.rep == 0xf3 ? 2 : u.rep == 0xf2 ? 3 : p66 ? 1 : 0;
+        u.opreg = smap << 8;
+        if (!sse_valid(smap, c, u.bsz, u.is_mem, u.reg & 7)) u.op = O_UNIMPL;
+      }
     }
     if (u.op == O_BT && grp != G_BA) u.sub = c == 0xa3 ? 4 : c == 0xab ? 5 : c == 0xb3 ? 6 : 7;
     if (u.op == O_SHXD) u.sub = (c >= 0xac ? 1u : 0u) | ((c & 1) ? 2u : 0u);  // bit0 shrd, bit1 count in cl

@@ -1,19 +1,26 @@
-// engine_sse.h — the SSE / SSE2 subset (convention U22).
+// engine_sse.h — the SSE / SSE2 and AVX / AVX2 data-movement subset
+// (conventions U22 / U23).
 //
-// The legacy-encoded integer and data-movement instructions compilers emit
-// for x86-64 at the SSE2 baseline: 128-bit moves, scalar / half moves,
-// movd / movq, logic, integer add / sub / saturate / compare / min / max /
-// multiply, shifts, shuffles, unpacks, packs, mask extraction, ldmxcsr /
-// stmxcsr, fences, movnti. A UOp with op O_SSE carries the opcode byte in
-// `sub` and the mandatory-prefix class in `bsz` (0 none, 1 66, 2 f3, 3 f2);
-// `imm` is the imm8. Encodings outside the subset (MMX, floating point, SSE3+)
-// decode as O_UNIMPL (sse_valid), so lanes exit UNIMPLEMENTED as in the oracle.
+// Legacy encodings: the integer and data-movement instructions compilers emit
+// for x86-64 at the SSE2 baseline (128-bit moves, scalar / half moves, movd /
+// movq, logic, integer add / sub / saturate / compare / min / max / multiply,
+// shifts, shuffles, unpacks, packs, mask extraction, ldmxcsr / stmxcsr,
+// fences, movnti) plus pshufb and ptest (0f 38 00 / 17). VEX encodings: the
+// same operations with three operands at 128 and 256 bits (AVX / AVX2 integer),
+// vzeroupper / vzeroall, vpshufb, vptest, vpbroadcastb/w/d/q — what the
+// runtime's vectorised memcpy / memset / strlen paths run. A UOp with op
+// O_SSE carries the opcode byte in `sub`, the mandatory-prefix class in `bsz`
+// (0 none, 1 66, 2 f3, 3 f2), `imm` the imm8, and in `opreg` the map and the
+// VEX fields (vex_*). Encodings outside the subset (MMX, floating point, the
+// other SSE3+ / AVX opcodes) decode as O_UNIMPL, as in the oracle.
 //
-// The XMM registers and MXCSR live in the lane's cold state (P.full[lane],
-// wtfgpu_regs_t: read_regs / write_regs / restore already carry them). As in
-// exec(), nothing is committed before every access has succeeded: 16-byte
-// stores probe both ends for write permission first, so a fault or a
-// copy-on-write restart never leaves half an operand written.
+// The XMM registers, the YMM upper halves and MXCSR live in the lane's cold
+// state (P.full[lane], wtfgpu_regs_t: read_regs / write_regs / restore carry
+// them). As in exec(), nothing is committed before every access has
+// succeeded: 16- and 32-byte stores probe both ends for write permission
+// first, so a fault or a copy-on-write restart never leaves half an operand
+// written. Legacy SSE leaves bits 255:128 of a destination alone; VEX.128
+// zeroes them.
 #pragma once
 #include "engine_exec.h"
 
@@ -44,9 +51,16 @@ __device__ __forceinline__ u64 sat_s(i64 x, u32 w) {
   return (u64)(x < lo ? lo : x > hi ? hi : x) & szmask(w);
 }
 
+// UOp::opreg of an O_SSE op: bit 0 VEX, bit 1 VEX.L, bit 2 VEX.W, bits 4-7
+// VEX.vvvv, bits 8-12 the opcode map (1 = 0f, 2 = 0f 38), bit 16 a legacy
+// 66 / f2 / f3 / REX prefix before the VEX prefix (#UD).
+__device__ __forceinline__ u32 vex_map(u32 x) { return (x >> 8) & 31; }
+
 // Decode-time check: is (opcode, prefix class, modrm) inside the subset?
-// Register-only / memory-only violations are #UD at execution, not here.
-__device__ __forceinline__ bool sse_valid(u32 c, u32 pc, u32 is_mem, u32 r3) {
+// Register-only / memory-only / VEX.L / VEX.vvvv violations are #UD at
+// execution, not here.
+__device__ __forceinline__ bool sse_valid(u32 map, u32 c, u32 pc, u32 is_mem, u32 r3) {
+  if (map == 2) return pc == 1 && (c == 0x00 || c == 0x17);
   if (c == 0xc3) return pc == 0;
   if (c == 0xae) return pc == 0 && (is_mem ? (r3 == 2 || r3 == 3) : r3 >= 5);
   if (c >= 0x60 && c <= 0x6d) return pc == 1;
@@ -65,6 +79,13 @@ __device__ __forceinline__ bool sse_valid(u32 c, u32 pc, u32 is_mem, u32 r3) {
   if (c >= 0xd0)
     return pc == 1 && c != 0xd0 && c != 0xe6 && c != 0xf0 && c != 0xf7 && c != 0xff;
   return false;
+}
+__device__ __forceinline__ bool vex_valid(u32 map, u32 c, u32 pp, u32 is_mem, u32 r3) {
+  if (map == 2) return pp == 1 && (c == 0x00 || c == 0x17 || c == 0x58 || c == 0x59 || c == 0x78 || c == 0x79);
+  if (map != 1) return false;
+  if (c == 0x77) return pp == 0;
+  if (c == 0xc3 || c == 0xae) return false;  // movnti has no VEX form; vldmxcsr / vstmxcsr are outside the subset
+  return sse_valid(1, c, pp, is_mem, r3);
 }
 
 // element-wise ops on w-byte elements
@@ -132,39 +153,199 @@ __device__ __forceinline__ void xmm_put(const Dev &P, const Lane &L, u32 r, X128
   F.xmm[r & 15][1] = v.hi;
 }
 
-// n bytes (4, 8 or 16) at ea, zero-extended
+// The pages of [ea, ea + n) pass the access check before any byte moves; a
+// fault is reported at ea or at the page boundary the operand crosses (as the
+// oracle's vprobe, and as the 1-8 byte accesses do).
+__device__ __forceinline__ bool span_ok(Lane &L, u64 ea, u32 n, int acc) {
+  const u64 last = ea + n - 1;
+  if (!xlate(L, ea, acc)) return false;
+  return ((ea ^ last) >> 12) == 0 || xlate(L, last & ~0xfffull, acc);
+}
+// n bytes (1, 2, 4, 8 or 16) at ea, zero-extended
 __device__ __forceinline__ bool xload(Lane &L, u64 ea, u32 n, X128 &v) {
   v.lo = v.hi = 0;
   if (n <= 8) return vread(L, ea, n, v.lo);
-  return vread(L, ea, 8, v.lo) && vread(L, ea + 8, 8, v.hi);
+  return span_ok(L, ea, n, ACC_R) && vread(L, ea, 8, v.lo) && vread(L, ea + 8, 8, v.hi);
 }
-// n bytes of v to ea: both ends pass the write check before anything is written
+// n bytes of v to ea
 __device__ __forceinline__ bool xstore(Lane &L, u64 ea, u32 n, X128 v) {
   if (n <= 8) return vwrite(L, ea, n, v.lo);
-  if (!xlate(L, ea, ACC_WPROBE) || !xlate(L, ea + 15, ACC_WPROBE)) return false;
+  if (!span_ok(L, ea, n, ACC_WPROBE)) return false;
   return vwrite(L, ea, 8, v.lo) && vwrite(L, ea + 8, 8, v.hi);
 }
+
+
+// ---------------------------------------------------------------- 256-bit state
+struct Y256 {
+  X128 l, h;
+};
+__device__ __forceinline__ Y256 ymm_get(const Dev &P, const Lane &L, u32 r) {
+  const wtfgpu_regs_t &F = P.full[L.lane];
+  return Y256{X128{F.xmm[r & 15][0], F.xmm[r & 15][1]}, X128{F.ymmh[r & 15][0], F.ymmh[r & 15][1]}};
+}
+// a VEX destination: VEX.128 zeroes bits 255:128 (VLMAX)
+__device__ __forceinline__ void ymm_put(const Dev &P, const Lane &L, u32 r, Y256 v, u32 l256) {
+  wtfgpu_regs_t &F = P.full[L.lane];
+  F.xmm[r & 15][0] = v.l.lo;
+  F.xmm[r & 15][1] = v.l.hi;
+  F.ymmh[r & 15][0] = l256 ? v.h.lo : 0;
+  F.ymmh[r & 15][1] = l256 ? v.h.hi : 0;
+}
+__device__ __forceinline__ bool yload(Lane &L, u64 ea, u32 n, Y256 &v) {
+  v.h = X128{0, 0};
+  if (n <= 16) return xload(L, ea, n, v.l);
+  return span_ok(L, ea, n, ACC_R) && xload(L, ea, 16, v.l) && xload(L, ea + 16, 16, v.h);
+}
+__device__ __forceinline__ bool ystore(Lane &L, u64 ea, u32 n, Y256 v) {
+  if (n <= 16) return xstore(L, ea, n, v.l);
+  if (!span_ok(L, ea, n, ACC_WPROBE)) return false;
+  return vwrite(L, ea, 8, v.l.lo) && vwrite(L, ea + 8, 8, v.l.hi) && vwrite(L, ea + 16, 8, v.h.lo) &&
+         vwrite(L, ea + 24, 8, v.h.hi);
+}
+
+// The 128-bit lane of the two-source integer / logic / shuffle ops shared by
+// the legacy and the VEX encodings: a = first source (the destination for
+// legacy SSE, VEX.vvvv for VEX), b = second source (r/m), cnt = the shift
+// count of the shift-by-register forms (for VEX.256 the count register's low
+// quadword, the same for both lanes). map 2 = 0f 38. false = not such an op.
+__device__ __noinline__ bool sse_lane(u32 map, u32 c, u32 pc, X128 a, X128 b, u32 imm, u64 cnt, X128 &r) {
+  r = X128{0, 0};
+  if (map == 2) {
+    if (c != 0x00) return false;
+    for (u32 i = 0; i < 16; i++) {  // pshufb
+      const u32 s = (u32)xel(b, i, 1);
+      xset(r, i, 1, (s & 0x80) ? 0 : xel(a, s & 15, 1));
+    }
+    return true;
+  }
+  switch (c) {
+    case 0x14: case 0x15: r = sse_unpack(pc ? 8 : 4, c == 0x15, a, b); return true;
+    case 0x54: case 0xdb: r = X128{a.lo & b.lo, a.hi & b.hi}; return true;
+    case 0x55: case 0xdf: r = X128{~a.lo & b.lo, ~a.hi & b.hi}; return true;
+    case 0x56: case 0xeb: r = X128{a.lo | b.lo, a.hi | b.hi}; return true;
+    case 0x57: case 0xef: r = X128{a.lo ^ b.lo, a.hi ^ b.hi}; return true;
+    case 0x60: case 0x61: case 0x62: case 0x6c:
+      r = sse_unpack(c == 0x60 ? 1 : c == 0x61 ? 2 : c == 0x62 ? 4 : 8, 0, a, b);
+      return true;
+    case 0x68: case 0x69: case 0x6a: case 0x6d:
+      r = sse_unpack(c == 0x68 ? 1 : c == 0x69 ? 2 : c == 0x6a ? 4 : 8, 1, a, b);
+      return true;
+    case 0x63: case 0x67: case 0x6b: {  // packsswb, packuswb, packssdw
+      const u32 w = c == 0x6b ? 4 : 2, h = 16 / w;
+      for (u32 i = 0; i < 2 * h; i++) {
+        const i64 x = i < h ? xsel(a, i, w) : xsel(b, i - h, w);
+        xset(r, i, w / 2, c == 0x67 ? sat_u(x, 1) : sat_s(x, w / 2));
+      }
+      return true;
+    }
+    case 0x64: case 0x65: case 0x66: r = sse_ewise(EW_GT, 1u << (c - 0x64), a, b); return true;
+    case 0x74: case 0x75: case 0x76: r = sse_ewise(EW_EQ, 1u << (c - 0x74), a, b); return true;
+    case 0x70:  // pshufd / pshufhw / pshuflw (of b)
+      r = b;
+      if (pc == 1) {
+        for (u32 i = 0; i < 4; i++) xset(r, i, 4, xel(b, (imm >> (2 * i)) & 3, 4));
+      } else {
+        const u32 o = pc == 2 ? 4 : 0;
+        for (u32 i = 0; i < 4; i++) xset(r, i + o, 2, xel(b, ((imm >> (2 * i)) & 3) + o, 2));
+      }
+      return true;
+    case 0xc6:  // shufps / shufpd
+      if (pc == 0) {
+        xset(r, 0, 4, xel(a, imm & 3, 4));
+        xset(r, 1, 4, xel(a, (imm >> 2) & 3, 4));
+        xset(r, 2, 4, xel(b, (imm >> 4) & 3, 4));
+        xset(r, 3, 4, xel(b, (imm >> 6) & 3, 4));
+      } else {
+        r = X128{(imm & 1) ? a.hi : a.lo, (imm & 2) ? b.hi : b.lo};
+      }
+      return true;
+    case 0xd1: case 0xd2: case 0xd3: r = sse_shift(0, c == 0xd1 ? 2 : c == 0xd2 ? 4 : 8, a, cnt); return true;
+    case 0xe1: case 0xe2: r = sse_shift(1, c == 0xe1 ? 2 : 4, a, cnt); return true;
+    case 0xf1: case 0xf2: case 0xf3: r = sse_shift(2, c == 0xf1 ? 2 : c == 0xf2 ? 4 : 8, a, cnt); return true;
+    case 0xd4: r = X128{a.lo + b.lo, a.hi + b.hi}; return true;
+    case 0xfb: r = X128{a.lo - b.lo, a.hi - b.hi}; return true;
+    case 0xfc: case 0xfd: case 0xfe: r = sse_ewise(EW_ADD, 1u << (c - 0xfc), a, b); return true;
+    case 0xf8: case 0xf9: case 0xfa: r = sse_ewise(EW_SUB, 1u << (c - 0xf8), a, b); return true;
+    case 0xd5: r = sse_ewise(EW_MULLO, 2, a, b); return true;
+    case 0xe5: r = sse_ewise(EW_MULHS, 2, a, b); return true;
+    case 0xe4: r = sse_ewise(EW_MULHU, 2, a, b); return true;
+    case 0xd8: case 0xd9: r = sse_ewise(EW_SUBUS, c - 0xd7, a, b); return true;
+    case 0xdc: case 0xdd: r = sse_ewise(EW_ADDUS, c - 0xdb, a, b); return true;
+    case 0xe8: case 0xe9: r = sse_ewise(EW_SUBS, c - 0xe7, a, b); return true;
+    case 0xec: case 0xed: r = sse_ewise(EW_ADDS, c - 0xeb, a, b); return true;
+    case 0xda: r = sse_ewise(EW_MINU, 1, a, b); return true;
+    case 0xde: r = sse_ewise(EW_MAXU, 1, a, b); return true;
+    case 0xea: r = sse_ewise(EW_MINS, 2, a, b); return true;
+    case 0xee: r = sse_ewise(EW_MAXS, 2, a, b); return true;
+    case 0xe0: r = sse_ewise(EW_AVG, 1, a, b); return true;
+    case 0xe3: r = sse_ewise(EW_AVG, 2, a, b); return true;
+    case 0xf4:
+      r = X128{(a.lo & 0xffffffffull) * (b.lo & 0xffffffffull), (a.hi & 0xffffffffull) * (b.hi & 0xffffffffull)};
+      return true;
+    case 0xf5:  // pmaddwd
+      for (u32 i = 0; i < 4; i++)
+        xset(r, i, 4, (u64)(xsel(a, 2 * i, 2) * xsel(b, 2 * i, 2) + xsel(a, 2 * i + 1, 2) * xsel(b, 2 * i + 1, 2)));
+      return true;
+    case 0xf6: {  // psadbw
+      u64 s0 = 0, s1 = 0;
+      for (u32 i = 0; i < 8; i++) {
+        const u64 x0 = xel(a, i, 1), y0 = xel(b, i, 1), x1 = xel(a, i + 8, 1), y1 = xel(b, i + 8, 1);
+        s0 += x0 > y0 ? x0 - y0 : y0 - x0;
+        s1 += x1 > y1 ? x1 - y1 : y1 - x1;
+      }
+      r = X128{s0, s1};
+      return true;
+    }
+    default: return false;
+  }
+}
+
+// 71 / 72 / 73 by imm8 of one lane: /2 srl, /4 sra, /6 sll, 73 /3 srldq, /7 slldq
+__device__ __forceinline__ X128 sse_shift_imm(u32 c, u32 r3, X128 b, u32 imm) {
+  if (c == 0x73 && (r3 == 3 || r3 == 7)) {
+    X128 r{0, 0};
+    for (u32 i = 0; i < 16; i++) {
+      const i32 s = r3 == 3 ? (i32)(i + imm) : (i32)i - (i32)imm;
+      if (s >= 0 && s < 16) xset(r, i, 1, xel(b, (u32)s, 1));
+    }
+    return r;
+  }
+  return sse_shift(r3 == 2 ? 0 : r3 == 4 ? 1 : 2, c == 0x71 ? 2 : c == 0x72 ? 4 : 8, b, imm);
+}
+
+// ptest / vptest: ZF = (a & b) == 0, CF = (~a & b) == 0, AF OF PF SF = 0
+__device__ __forceinline__ u64 ptest_flags(u64 fl, Y256 a, Y256 b) {
+  const bool z = !((a.l.lo & b.l.lo) | (a.l.hi & b.l.hi) | (a.h.lo & b.h.lo) | (a.h.hi & b.h.hi));
+  const bool cf = !((~a.l.lo & b.l.lo) | (~a.l.hi & b.l.hi) | (~a.h.lo & b.h.lo) | (~a.h.hi & b.h.hi));
+  return (fl & ~F_STATUS) | (z ? F_ZF : 0) | (cf ? F_CF : 0);
+}
+
+__device__ __forceinline__ u64 sse_ea(const Dev &P, const Lane &L, const UOp &u, u64 nrip) {
+  u64 ea;
+  if (u.riprel) {
+    ea = nrip + u.disp;
+  } else {
+    ea = u.disp;
+    if (u.base >= 0) ea += R(L, u.base);
+    if (u.index >= 0) ea += R(L, u.index) << u.scale;
+  }
+  if (u.p67) ea &= 0xffffffffull;
+  if (u.seg) ea += u.seg == 4 ? P.fs_base[L.lane] : P.gs_base[L.lane];
+  return ea;
+}
+
+__device__ __noinline__ int vex_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next);
 
 // One attempt at an SSE instruction (exec() protocol: X_FAULT with L.miss set
 // asks for a translation service and a rerun).
 __device__ __noinline__ int sse_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next) {
+  if (u.opreg & 1) return vex_exec(P, L, u, nrip, next);
   next = nrip;
-  const u32 c = u.sub, pc = u.bsz, r3 = u.reg & 7;
+  const u32 c = u.sub, pc = u.bsz, r3 = u.reg & 7, map = vex_map(u.opreg);
   const bool mem = u.is_mem;
   const u32 imm = (u32)u.imm & 0xff;
-  u64 ea = 0;
-  if (mem) {
-    if (u.riprel) {
-      ea = nrip + u.disp;
-    } else {
-      ea = u.disp;
-      if (u.base >= 0) ea += R(L, u.base);
-      if (u.index >= 0) ea += R(L, u.index) << u.scale;
-    }
-    if (u.p67) ea &= 0xffffffffull;
-    if (u.seg) ea += u.seg == 4 ? P.fs_base[L.lane] : P.gs_base[L.lane];
-  }
-  if (c == 0xc3) {  // movnti m32/64, r
+  const u64 ea = mem ? sse_ea(P, L, u, nrip) : 0;
+  if (map == 1 && c == 0xc3) {  // movnti m32/64, r
     if (!mem) {
       set_fault(L, WTFGPU_VEC_UD, 0, 0);
       return X_FAULT;
@@ -172,10 +353,10 @@ __device__ __noinline__ int sse_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
     const u32 sz = (u.rex & 8) ? 8 : 4;
     return vwrite(L, ea, sz, R(L, u.reg) & szmask(sz)) ? X_OK : X_FAULT;
   }
-  if (c == 0xae && !mem) return X_OK;  // lfence / mfence / sfence
-  const bool reg_only = (c >= 0x71 && c <= 0x73) || c == 0x50 || c == 0xd7 || c == 0xc5;
-  const bool mem_only = c == 0x13 || c == 0x17 || c == 0x2b || c == 0xe7 || c == 0xae ||
-                        ((c == 0x12 || c == 0x16) && pc == 1);
+  if (map == 1 && c == 0xae && !mem) return X_OK;  // lfence / mfence / sfence
+  const bool reg_only = map == 1 && ((c >= 0x71 && c <= 0x73) || c == 0x50 || c == 0xd7 || c == 0xc5);
+  const bool mem_only = map == 1 && (c == 0x13 || c == 0x17 || c == 0x2b || c == 0xe7 || c == 0xae ||
+                                     ((c == 0x12 || c == 0x16) && pc == 1));
   if ((reg_only && mem) || (mem_only && !mem)) {
     set_fault(L, WTFGPU_VEC_UD, 0, 0);
     return X_FAULT;
@@ -192,34 +373,40 @@ __device__ __noinline__ int sse_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
   // the r/m operand: 16 bytes aligned unless an unaligned move / narrower form
   u32 n = 16;
   bool align = true;
-  switch (c) {
-    case 0x10:
-    case 0x11: n = pc <= 1 ? 16 : pc == 2 ? 4 : 8; align = false; break;
-    case 0x12: case 0x13: case 0x16: case 0x17: case 0xd6: n = 8; align = false; break;
-    case 0x6e: case 0x7e: n = (pc == 2 || (u.rex & 8)) ? 8 : 4; align = false; break;
-    case 0x6f: case 0x7f: align = pc == 1; break;
-    case 0xc4: n = 2; align = false; break;
-    case 0xae: n = 4; align = false; break;
-    default: break;
+  if (map == 1) {
+    switch (c) {
+      case 0x10:
+      case 0x11: n = pc <= 1 ? 16 : pc == 2 ? 4 : 8; align = false; break;
+      case 0x12: case 0x13: case 0x16: case 0x17: case 0xd6: n = 8; align = false; break;
+      case 0x6e: case 0x7e: n = (pc == 2 || (u.rex & 8)) ? 8 : 4; align = false; break;
+      case 0x6f: case 0x7f: align = pc == 1; break;
+      case 0xc4: n = 2; align = false; break;
+      case 0xae: n = 4; align = false; break;
+      default: break;
+    }
   }
   if (mem && n == 16 && align && (ea & 15)) {
     set_fault(L, WTFGPU_VEC_GP, 0, 0);
     return X_FAULT;
   }
-  const bool store = c == 0x11 || c == 0x13 || c == 0x17 || c == 0x29 || c == 0x2b || c == 0x7f || c == 0xe7 ||
-                     c == 0xd6 || (c == 0x7e && pc == 1) || (c == 0xae && r3 == 3);
+  const bool store = map == 1 && (c == 0x11 || c == 0x13 || c == 0x17 || c == 0x29 || c == 0x2b || c == 0x7f ||
+                                  c == 0xe7 || c == 0xd6 || (c == 0x7e && pc == 1) || (c == 0xae && r3 == 3));
   X128 a = xmm_get(P, L, u.reg), b{0, 0}, r{0, 0};
   if (!store) {
     if (mem) {
       if (!xload(L, ea, n, b)) return X_FAULT;
-    } else if (c == 0x6e || c == 0xc4) {
+    } else if (map == 1 && (c == 0x6e || c == 0xc4)) {
       b.lo = R(L, u.rm);
     } else {
       b = xmm_get(P, L, u.rm);
     }
   }
+  if (map == 2 && c == 0x17) {  // ptest
+    L.rflags = ptest_flags(L.rflags, Y256{a, X128{0, 0}}, Y256{b, X128{0, 0}});
+    return X_OK;
+  }
   // ---- compute: r goes to xmm[reg] unless a case returns itself
-  switch (c) {
+  switch (map == 1 ? c : 0x100) {
     case 0x10:
       if (pc <= 1 || mem) r = b;
       else if (pc == 2) r = X128{(a.lo & ~0xffffffffull) | (b.lo & 0xffffffffull), a.hi};
@@ -238,7 +425,6 @@ __device__ __noinline__ int sse_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
     case 0x16: r = X128{a.lo, b.lo}; break;               // movhps / movhpd; movlhps
     case 0x13: return xstore(L, ea, 8, a) ? X_OK : X_FAULT;
     case 0x17: return xstore(L, ea, 8, X128{a.hi, 0}) ? X_OK : X_FAULT;
-    case 0x14: case 0x15: r = sse_unpack(pc ? 8 : 4, c == 0x15, a, b); break;
     case 0x28: case 0x6f: r = b; break;
     case 0x50: {  // movmskps / movmskpd
       const u32 w = pc ? 8 : 4;
@@ -253,22 +439,6 @@ __device__ __noinline__ int sse_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
       RS(L, u.reg, v);
       return X_OK;
     }
-    case 0x54: case 0xdb: r = X128{a.lo & b.lo, a.hi & b.hi}; break;
-    case 0x55: case 0xdf: r = X128{~a.lo & b.lo, ~a.hi & b.hi}; break;
-    case 0x56: case 0xeb: r = X128{a.lo | b.lo, a.hi | b.hi}; break;
-    case 0x57: case 0xef: r = X128{a.lo ^ b.lo, a.hi ^ b.hi}; break;
-    case 0x60: case 0x61: case 0x62: case 0x6c: r = sse_unpack(c == 0x60 ? 1 : c == 0x61 ? 2 : c == 0x62 ? 4 : 8, 0, a, b); break;
-    case 0x68: case 0x69: case 0x6a: case 0x6d: r = sse_unpack(c == 0x68 ? 1 : c == 0x69 ? 2 : c == 0x6a ? 4 : 8, 1, a, b); break;
-    case 0x63: case 0x67: case 0x6b: {  // packsswb, packuswb, packssdw
-      const u32 w = c == 0x6b ? 4 : 2, h = 16 / w;
-      for (u32 i = 0; i < 2 * h; i++) {
-        const i64 x = i < h ? xsel(a, i, w) : xsel(b, i - h, w);
-        xset(r, i, w / 2, c == 0x67 ? sat_u(x, 1) : sat_s(x, w / 2));
-      }
-      break;
-    }
-    case 0x64: case 0x65: case 0x66: r = sse_ewise(EW_GT, 1u << (c - 0x64), a, b); break;
-    case 0x74: case 0x75: case 0x76: r = sse_ewise(EW_EQ, 1u << (c - 0x74), a, b); break;
     case 0x6e: r = X128{b.lo & szmask(n), 0}; break;  // movd / movq xmm, r/m
     case 0x7e:
       if (pc == 2) {  // movq xmm, xmm/m64
@@ -279,39 +449,11 @@ __device__ __noinline__ int sse_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
       if (mem) return vwrite(L, ea, n, a.lo & szmask(n)) ? X_OK : X_FAULT;
       RS(L, u.rm, a.lo & szmask(n));
       return X_OK;
-    case 0x70:
-      r = b;
-      if (pc == 1) {
-        for (u32 i = 0; i < 4; i++) xset(r, i, 4, xel(b, (imm >> (2 * i)) & 3, 4));
-      } else {
-        const u32 o = pc == 2 ? 4 : 0;
-        for (u32 i = 0; i < 4; i++) xset(r, i + o, 2, xel(b, ((imm >> (2 * i)) & 3) + o, 2));
-      }
-      break;
-    case 0x71: case 0x72: case 0x73: {
-      if (c == 0x73 && (r3 == 3 || r3 == 7)) {  // psrldq / pslldq (bytes)
-        for (u32 i = 0; i < 16; i++) {
-          const i32 s = r3 == 3 ? (i32)(i + imm) : (i32)i - (i32)imm;
-          if (s >= 0 && s < 16) xset(r, i, 1, xel(b, (u32)s, 1));
-        }
-      } else {
-        r = sse_shift(r3 == 2 ? 0 : r3 == 4 ? 1 : 2, c == 0x71 ? 2 : c == 0x72 ? 4 : 8, b, imm);
-      }
-      xmm_put(P, L, u.rm, r);
+    case 0x71: case 0x72: case 0x73:
+      xmm_put(P, L, u.rm, sse_shift_imm(c, r3, b, imm));
       return X_OK;
-    }
     case 0xc4: r = a; xset(r, imm & 7, 2, b.lo & 0xffff); break;  // pinsrw
     case 0xc5: RS(L, u.reg, xel(b, imm & 7, 2)); return X_OK;     // pextrw
-    case 0xc6:
-      if (pc == 0) {
-        xset(r, 0, 4, xel(a, imm & 3, 4));
-        xset(r, 1, 4, xel(a, (imm >> 2) & 3, 4));
-        xset(r, 2, 4, xel(b, (imm >> 4) & 3, 4));
-        xset(r, 3, 4, xel(b, (imm >> 6) & 3, 4));
-      } else {
-        r = X128{(imm & 1) ? a.hi : a.lo, (imm & 2) ? b.hi : b.lo};
-      }
-      break;
     case 0xd6:  // movq xmm/m64, xmm
       if (mem) return xstore(L, ea, 8, a) ? X_OK : X_FAULT;
       xmm_put(P, L, u.rm, X128{a.lo, 0});
@@ -327,44 +469,176 @@ __device__ __noinline__ int sse_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
       F.mxcsr = (u32)b.lo;
       return X_OK;
     }
-    case 0xd1: case 0xd2: case 0xd3: r = sse_shift(0, c == 0xd1 ? 2 : c == 0xd2 ? 4 : 8, a, b.lo); break;
-    case 0xe1: case 0xe2: r = sse_shift(1, c == 0xe1 ? 2 : 4, a, b.lo); break;
-    case 0xf1: case 0xf2: case 0xf3: r = sse_shift(2, c == 0xf1 ? 2 : c == 0xf2 ? 4 : 8, a, b.lo); break;
-    case 0xd4: r = X128{a.lo + b.lo, a.hi + b.hi}; break;
-    case 0xfb: r = X128{a.lo - b.lo, a.hi - b.hi}; break;
-    case 0xfc: case 0xfd: case 0xfe: r = sse_ewise(EW_ADD, 1u << (c - 0xfc), a, b); break;
-    case 0xf8: case 0xf9: case 0xfa: r = sse_ewise(EW_SUB, 1u << (c - 0xf8), a, b); break;
-    case 0xd5: r = sse_ewise(EW_MULLO, 2, a, b); break;
-    case 0xe5: r = sse_ewise(EW_MULHS, 2, a, b); break;
-    case 0xe4: r = sse_ewise(EW_MULHU, 2, a, b); break;
-    case 0xd8: case 0xd9: r = sse_ewise(EW_SUBUS, c - 0xd7, a, b); break;
-    case 0xdc: case 0xdd: r = sse_ewise(EW_ADDUS, c - 0xdb, a, b); break;
-    case 0xe8: case 0xe9: r = sse_ewise(EW_SUBS, c - 0xe7, a, b); break;
-    case 0xec: case 0xed: r = sse_ewise(EW_ADDS, c - 0xeb, a, b); break;
-    case 0xda: r = sse_ewise(EW_MINU, 1, a, b); break;
-    case 0xde: r = sse_ewise(EW_MAXU, 1, a, b); break;
-    case 0xea: r = sse_ewise(EW_MINS, 2, a, b); break;
-    case 0xee: r = sse_ewise(EW_MAXS, 2, a, b); break;
-    case 0xe0: r = sse_ewise(EW_AVG, 1, a, b); break;
-    case 0xe3: r = sse_ewise(EW_AVG, 2, a, b); break;
-    case 0xf4: r = X128{(a.lo & 0xffffffffull) * (b.lo & 0xffffffffull), (a.hi & 0xffffffffull) * (b.hi & 0xffffffffull)}; break;
-    case 0xf5:  // pmaddwd
-      for (u32 i = 0; i < 4; i++)
-        xset(r, i, 4, (u64)(xsel(a, 2 * i, 2) * xsel(b, 2 * i, 2) + xsel(a, 2 * i + 1, 2) * xsel(b, 2 * i + 1, 2)));
+    default:
+      if (!sse_lane(map, c, pc, a, b, imm, b.lo, r)) return X_UNIMPL;
       break;
-    case 0xf6: {  // psadbw
-      u64 s0 = 0, s1 = 0;
-      for (u32 i = 0; i < 8; i++) {
-        const u64 x0 = xel(a, i, 1), y0 = xel(b, i, 1), x1 = xel(a, i + 8, 1), y1 = xel(b, i + 8, 1);
-        s0 += x0 > y0 ? x0 - y0 : y0 - x0;
-        s1 += x1 > y1 ? x1 - y1 : y1 - x1;
-      }
-      r = X128{s0, s1};
-      break;
-    }
-    default: return X_UNIMPL;
   }
   xmm_put(P, L, u.reg, r);
+  return X_OK;
+}
+
+// One attempt at a VEX instruction (U23). dst = reg, a = VEX.vvvv, b = r/m.
+__device__ __noinline__ int vex_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next) {
+  next = nrip;
+  const u32 x = u.opreg, c = u.sub, pp = u.bsz, r3 = u.reg & 7, map = vex_map(x);
+  const u32 l256 = (x >> 1) & 1, w = (x >> 2) & 1, vvvv = (x >> 4) & 15;
+  const bool mem = u.is_mem;
+  const u32 imm = (u32)u.imm & 0xff;
+  const u64 ea = mem ? sse_ea(P, L, u, nrip) : 0;
+  // ---- #UD: a legacy prefix before VEX, AVX state off, operand-form rules
+  bool ud = (x >> 16) & 1;
+  const u64 cr4 = P.sys[L.lane].cr4;
+  if (!((cr4 >> 18) & 1) || (P.full[L.lane].xcr0 & 6) != 6) ud = true;
+  bool two_op = false, no256 = false, reg_only = false, mem_only = false;
+  if (map == 1) {
+    two_op = ((c == 0x10 || c == 0x11) && (pp <= 1 || mem)) || c == 0x13 || c == 0x17 || c == 0x28 || c == 0x29 ||
+             c == 0x2b || c == 0x50 || c == 0x6e || c == 0x6f || c == 0x70 || c == 0x7e || c == 0x7f || c == 0xc5 ||
+             c == 0xd6 || c == 0xd7 || c == 0xe7 || c == 0x77;
+    no256 = c == 0x12 || c == 0x13 || c == 0x16 || c == 0x17 || c == 0x6e || c == 0x7e || c == 0xc4 || c == 0xc5 ||
+            c == 0xd6;
+    reg_only = (c >= 0x71 && c <= 0x73) || c == 0x50 || c == 0xd7 || c == 0xc5;
+    mem_only = c == 0x13 || c == 0x17 || c == 0x2b || c == 0xe7 || ((c == 0x12 || c == 0x16) && pp == 1);
+  } else {
+    two_op = c != 0x00;
+  }
+  if ((two_op && vvvv != 0) || (no256 && l256) || (reg_only && mem) || (mem_only && !mem)) ud = true;
+  if (ud) {
+    set_fault(L, WTFGPU_VEC_UD, 0, 0);
+    return X_FAULT;
+  }
+  if (L.cr0 & 8) {
+    set_fault(L, 7, 0, 0);  // #NM
+    return X_FAULT;
+  }
+  if (map == 1 && c == 0x77) {  // vzeroupper / vzeroall
+    wtfgpu_regs_t &F = P.full[L.lane];
+    for (u32 i = 0; i < 16; i++) {
+      F.ymmh[i][0] = F.ymmh[i][1] = 0;
+      if (l256) F.xmm[i][0] = F.xmm[i][1] = 0;
+    }
+    return X_OK;
+  }
+  // ---- the r/m operand's size; aligned moves need 16 / 32-byte alignment
+  const u32 vl = l256 ? 32 : 16;
+  u32 n = vl;
+  bool align = false;
+  if (map == 1) {
+    switch (c) {
+      case 0x10: case 0x11: n = pp <= 1 ? vl : pp == 2 ? 4 : 8; break;
+      case 0x12: case 0x13: case 0x16: case 0x17: case 0xd6: n = 8; break;
+      case 0x6e: case 0x7e: n = (pp == 2 || w) ? 8 : 4; break;
+      case 0xc4: n = 2; break;
+      case 0x28: case 0x29: case 0x2b: case 0xe7: align = true; break;
+      case 0x6f: case 0x7f: align = pp == 1; break;
+      case 0xd1: case 0xd2: case 0xd3: case 0xe1: case 0xe2: case 0xf1: case 0xf2: case 0xf3: n = 16; break;
+      default: break;
+    }
+  } else if (c == 0x58 || c == 0x59 || c == 0x78 || c == 0x79) {
+    n = c == 0x78 ? 1 : c == 0x79 ? 2 : c == 0x58 ? 4 : 8;
+  }
+  if (mem && align && (ea & (vl - 1))) {
+    set_fault(L, WTFGPU_VEC_GP, 0, 0);
+    return X_FAULT;
+  }
+  const bool store = map == 1 && (c == 0x11 || c == 0x13 || c == 0x17 || c == 0x29 || c == 0x2b || c == 0x7f ||
+                                  c == 0xe7 || c == 0xd6 || (c == 0x7e && pp == 1));
+  const Y256 s = ymm_get(P, L, u.reg);  // the reg operand (a store's source, vptest's first source)
+  const Y256 a = ymm_get(P, L, vvvv);
+  Y256 b{X128{0, 0}, X128{0, 0}}, r{X128{0, 0}, X128{0, 0}};
+  if (!store) {
+    if (mem) {
+      if (!yload(L, ea, n, b)) return X_FAULT;
+    } else if (map == 1 && (c == 0x6e || c == 0xc4)) {
+      b.l.lo = R(L, u.rm);
+    } else {
+      b = ymm_get(P, L, u.rm);
+    }
+  }
+  u32 dst = u.reg;
+  if (map == 2) {
+    if (c == 0x17) {  // vptest (VEX.128: the low halves only)
+      L.rflags = l256 ? ptest_flags(L.rflags, s, b) : ptest_flags(L.rflags, Y256{s.l, X128{0, 0}}, Y256{b.l, X128{0, 0}});
+      return X_OK;
+    }
+    if (c == 0x00) {  // vpshufb
+      sse_lane(2, 0, 1, a.l, b.l, 0, 0, r.l);
+      if (l256) sse_lane(2, 0, 1, a.h, b.h, 0, 0, r.h);
+    } else {  // vpbroadcastb / w / d / q
+      const u32 ew = c == 0x78 ? 1 : c == 0x79 ? 2 : c == 0x58 ? 4 : 8;
+      const u64 e = xel(b.l, 0, ew);
+      for (u32 i = 0; i < 16 / ew; i++) xset(r.l, i, ew, e);
+      r.h = r.l;
+    }
+    ymm_put(P, L, dst, r, l256);
+    return X_OK;
+  }
+  switch (c) {
+    case 0x10:
+      if (pp <= 1 || mem) r = b;
+      else if (pp == 2) r.l = X128{(a.l.lo & ~0xffffffffull) | (b.l.lo & 0xffffffffull), a.l.hi};
+      else r.l = X128{b.l.lo, a.l.hi};
+      break;
+    case 0x11: case 0x29: case 0x2b: case 0x7f: case 0xe7:  // stores / register moves to rm
+      if (mem) return ystore(L, ea, c == 0x11 ? n : vl, s) ? X_OK : X_FAULT;
+      if (c == 0x11 && pp == 2) r.l = X128{(a.l.lo & ~0xffffffffull) | (s.l.lo & 0xffffffffull), a.l.hi};
+      else if (c == 0x11 && pp == 3) r.l = X128{s.l.lo, a.l.hi};
+      else r = s;
+      ymm_put(P, L, u.rm, r, c == 0x11 && pp >= 2 ? 0 : l256);
+      return X_OK;
+    case 0x12: r.l = X128{mem ? b.l.lo : b.l.hi, a.l.hi}; break;  // vmovlps / vmovlpd; vmovhlps
+    case 0x16: r.l = X128{a.l.lo, b.l.lo}; break;                 // vmovhps / vmovhpd; vmovlhps
+    case 0x13: return xstore(L, ea, 8, s.l) ? X_OK : X_FAULT;
+    case 0x17: return xstore(L, ea, 8, X128{s.l.hi, 0}) ? X_OK : X_FAULT;
+    case 0x28: case 0x6f: r = b; break;
+    case 0x50: {  // vmovmskps / vmovmskpd
+      const u32 ew = pp ? 8 : 4;
+      u64 v = 0;
+      for (u32 i = 0; i < 16 / ew; i++) v |= (xel(b.l, i, ew) >> (8 * ew - 1)) << i;
+      if (l256)
+        for (u32 i = 0; i < 16 / ew; i++) v |= (xel(b.h, i, ew) >> (8 * ew - 1)) << (i + 16 / ew);
+      RS(L, u.reg, v);
+      return X_OK;
+    }
+    case 0xd7: {  // vpmovmskb
+      u64 v = 0;
+      for (u32 i = 0; i < 16; i++) v |= ((xel(b.l, i, 1) >> 7) & 1) << i;
+      if (l256)
+        for (u32 i = 0; i < 16; i++) v |= ((xel(b.h, i, 1) >> 7) & 1) << (i + 16);
+      RS(L, u.reg, v);
+      return X_OK;
+    }
+    case 0x6e: r.l = X128{b.l.lo & szmask(n), 0}; break;  // vmovd / vmovq xmm, r/m
+    case 0x7e:
+      if (pp == 2) {  // vmovq xmm, xmm/m64
+        r.l = X128{b.l.lo, 0};
+        break;
+      }
+      if (mem) return vwrite(L, ea, n, s.l.lo & szmask(n)) ? X_OK : X_FAULT;
+      RS(L, u.rm, s.l.lo & szmask(n));
+      return X_OK;
+    case 0x70:
+      sse_lane(1, 0x70, pp, a.l, b.l, imm, 0, r.l);
+      if (l256) sse_lane(1, 0x70, pp, a.h, b.h, imm, 0, r.h);
+      break;
+    case 0x71: case 0x72: case 0x73:  // the destination is VEX.vvvv
+      r.l = sse_shift_imm(c, r3, b.l, imm);
+      if (l256) r.h = sse_shift_imm(c, r3, b.h, imm);
+      dst = vvvv;
+      break;
+    case 0xc4: r.l = a.l; xset(r.l, imm & 7, 2, b.l.lo & 0xffff); break;  // vpinsrw
+    case 0xc5: RS(L, u.reg, xel(b.l, imm & 7, 2)); return X_OK;           // vpextrw
+    case 0xd6:  // vmovq xmm/m64, xmm
+      if (mem) return xstore(L, ea, 8, s.l) ? X_OK : X_FAULT;
+      ymm_put(P, L, u.rm, Y256{X128{s.l.lo, 0}, X128{0, 0}}, 0);
+      return X_OK;
+    default: {
+      // two-source lane ops: vshufpd's high lane takes imm bits 2-3
+      if (!sse_lane(1, c, pp, a.l, b.l, imm, b.l.lo, r.l)) return X_UNIMPL;
+      if (l256) sse_lane(1, c, pp, a.h, b.h, c == 0xc6 && pp == 1 ? imm >> 2 : imm, b.l.lo, r.h);
+      break;
+    }
+  }
+  ymm_put(P, L, dst, r, l256);
   return X_OK;
 }
 

@@ -86,7 +86,10 @@ wtfgpu_regs_t RegsFromCpuState(const CpuState_t &S) {
   r.mxcsr = S.Mxcsr, r.mxcsr_mask = S.MxcsrMask;
   r.fpcw = S.Fpcw, r.fpsw = S.Fpsw, r.fptw = S.Fptw, r.fpop = S.Fpop;
   memcpy(r.fpst, S.Fpst, sizeof(r.fpst));
-  for (int i = 0; i < 16; i++) r.xmm[i][0] = S.Zmm[i].Q[0], r.xmm[i][1] = S.Zmm[i].Q[1];
+  for (int i = 0; i < 16; i++) {
+    r.xmm[i][0] = S.Zmm[i].Q[0], r.xmm[i][1] = S.Zmm[i].Q[1];
+    r.ymmh[i][0] = S.Zmm[i].Q[2], r.ymmh[i][1] = S.Zmm[i].Q[3];
+  }
   return r;
 }
 
