@@ -50,8 +50,8 @@
  *       base, TSC_AUX); any other MSR, a non-canonical base / entry point or
  *       upper bits in SFMASK / TSC_AUX is #GP(0); EFER.LMA is read-only.
  *   U22 SSE / SSE2: the legacy-encoded integer and data-movement subset (see
- *       exec_sse); MMX, SSE floating-point arithmetic, SSE3+ and VEX are
- *       UNIMPLEMENTED. #UD if CR0.EM or !CR4.OSFXSR, #NM if CR0.TS, #GP(0) for a
+ *       exec_sse) plus pshufb and ptest; MMX, SSE floating-point arithmetic
+ *       and the rest of SSE3+ are UNIMPLEMENTED. #UD if CR0.EM or !CR4.OSFXSR, #NM if CR0.TS, #GP(0) for a
  *       misaligned 16-byte operand of an aligned form; the checks run in that
  *       order, before any memory access.
  *   U23 AVX / AVX2 (VEX): the same subset at 128 / 256 bits plus vzeroupper,
@@ -987,8 +987,9 @@ enum { X_OK = 0, X_FAULT = 1, X_UNIMPL = 2, X_INT3 = 3, X_HLT = 4, X_CR3 = 5, X_
  * x86-64 (SSE2 baseline): 128-bit moves, scalar / half moves, movd / movq,
  * logic, integer add / sub / saturate / compare / min / max / multiply,
  * shifts, shuffles, unpacks, packs, mask extraction, ldmxcsr / stmxcsr, fences,
- * movnti. MMX (no-prefix 0f 6x / dx-fx), SSE floating-point arithmetic, SSE3+
- * and VEX are outside the subset (UNIMPLEMENTED). Faults: #UD when CR0.EM = 1
+ * movnti, plus pshufb (0f 38 00) and ptest (0f 38 17). MMX (no-prefix 0f 6x /
+ * dx-fx), SSE floating-point arithmetic and the rest of SSE3+ are outside the
+ * subset (UNIMPLEMENTED); VEX forms are exec_vex's. Faults: #UD when CR0.EM = 1
  * or CR4.OSFXSR = 0, #NM when CR0.TS = 1, #GP(0) for a 16-byte memory operand
  * that is not 16-byte aligned (all but movups / movupd / movdqu). */
 typedef struct { u8 b[16]; } x128;
