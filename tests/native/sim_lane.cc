@@ -1,9 +1,11 @@
 // sim_lane.cc — TEST INFRASTRUCTURE ONLY: one lane of the GPU interpreter's
 // per-step logic (engine.hip k_run: code translation, fetch, decode, exec with
-// miss/retry, retire) compiled for the host, for divergence debugging.
+// miss/retry, retire) compiled for the host, for divergence debugging. With
+// `fast` set, each instruction first tries the fast loop's form (digest +
+// fast_exec, engine_fast.h) and falls back to exec() on a miss, as k_run does.
 #include <cstdlib>
 #include <vector>
-#include "../../wtf_amd/csrc/engine_ops.h"
+#include "../../wtf_amd/csrc/engine_fast.h"
 using namespace wtfgpu_dev;
 
 extern "C" {
@@ -15,10 +17,11 @@ struct SimResult {
   uint64_t xmm[32];
   uint32_t mxcsr, pad;
   uint64_t ymmh[32];
+  uint8_t win[512];  // the lane's view of [win_va, win_va + 512) at the end (zeros where unmapped)
 };
 
-int sim_run(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, const wtfgpu_regs_t *r0,
-            uint64_t limit, SimResult *out) {
+int sim_run_mode(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, const wtfgpu_regs_t *r0,
+                 uint64_t limit, SimResult *out, int fast, uint64_t *fast_count, uint64_t win_va) {
   uint64_t maxpfn = 0;
   for (uint64_t i = 0; i < npages; i++) maxpfn = gpfns[i] > maxpfn ? gpfns[i] : maxpfn;
   // page pointers carry flags in their low 12 bits: storage must be 4 KiB aligned
@@ -65,6 +68,7 @@ int sim_run(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, const 
   L.efer = r0->efer;
   L.cpl = r0->seg[WTFGPU_CS].selector & 3;
   L.status = WTFGPU_RUNNING;
+  L.simd = simd_bits(r0->cr0, r0->cr4, r0->xcr0);
   tlb_flush(L);
   for (uint64_t steps = 0; steps < 100000000 && L.status == WTFGPU_RUNNING; steps++) {
     const uint64_t grip = L.rip;
@@ -107,6 +111,23 @@ int sim_run(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, const 
       break;
     }
     uint64_t next = 0;
+    if (fast) {
+      FOp f;
+      digest(d, f);
+      if (fo_op(f) != FO_GENERIC) {
+        L.miss = 0;
+        L.pend = 0;
+        fast_exec(P, L, f, grip + d.len, next);
+        if (!L.miss) {
+          if (fast_count) ++*fast_count;
+          L.rip = next;
+          L.icount++;
+          L.nbytes += d.len + L.pend;
+          if (P.limit && L.icount > P.limit) L.status = WTFGPU_EXIT_TIMEOUT;
+          continue;
+        }
+      }
+    }
     int x;
     for (int attempt = 0;; attempt++) {
       L.miss = 0;
@@ -147,8 +168,23 @@ int sim_run(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, const 
   for (int k = 0; k < 16; k++) out->xmm[2 * k] = full.xmm[k][0], out->xmm[2 * k + 1] = full.xmm[k][1];
   out->mxcsr = full.mxcsr;
   for (int k = 0; k < 16; k++) out->ymmh[2 * k] = full.ymmh[k][0], out->ymmh[2 * k + 1] = full.ymmh[k][1];
+  memset(out->win, 0, sizeof(out->win));
+  if (win_va) {
+    L.cpl = 0;
+    const uint32_t st = L.status;
+    for (uint32_t i = 0; i < sizeof(out->win); i++) {
+      uint64_t td, gpfn;
+      if (walk(P, L, win_va + i, ACC_R, td, gpfn)) out->win[i] = ((const uint8_t *)(uintptr_t)(td & ~0xfffull))[(win_va + i) & 0xfff];
+    }
+    L.status = st;
+  }
   free(pool);
   free(ov);
   return 0;
+}
+
+int sim_run(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, const wtfgpu_regs_t *r0,
+            uint64_t limit, SimResult *out) {
+  return sim_run_mode(gpfns, pages, npages, r0, limit, out, 0, nullptr, 0);
 }
 }

@@ -1,0 +1,249 @@
+"""The fast loop's forms (engine_fast.h: digest + fast_exec) on the CPU.
+
+k_run runs an instruction through its FOp digest first and falls back to the
+generic exec() only on a miss. tests/native/sim_lane.cc, in fast mode, runs the
+same order on the host-built device code, so every native-execution vector
+(integer, SSE, AVX2) is checked through the fast forms too, including the
+memory window, and the vector moves the guests' memcpy / memset loops run
+(FO_VLD / FO_VST / FO_VMOV / FO_VZU) are checked at every alignment, at page
+ends and with the SSE / AVX state switched off, against the generic path and
+the oracle.
+"""
+import ctypes as C
+import gzip
+import json
+import os
+
+import pytest
+
+from tests.golden.gen_native_vectors import splitmix_bytes
+from tests.golden.gen_sse_vectors import window_in
+from tests.oracle_lib import Oracle
+from tests.test_sse import BUF, layout, sim_lib, sim_run
+from wtf_amd.abi import EXIT_FAULT
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+INT3 = 3
+
+
+def vectors(name):
+    with gzip.open(os.path.join(HERE, "golden", name), "rt") as f:
+        return json.load(f)
+
+
+def run_both(L, sp, regs, win_va, limit=0):
+    """(slow result, fast result, instructions the fast forms retired)."""
+    cnt = C.c_uint64(0)
+    slow = sim_run(L, sp, regs, limit=limit, win_va=win_va)
+    fast = sim_run(L, sp, regs, limit=limit, fast=True, counter=cnt, win_va=win_va)
+    return slow, fast, cnt.value
+
+
+def same(a, b):
+    return (a.status == b.status and a.vector == b.vector and a.rip == b.rip and a.icount == b.icount and
+            list(a.gpr) == list(b.gpr) and a.rflags == b.rflags and list(a.xmm) == list(b.xmm) and
+            list(a.ymmh) == list(b.ymmh) and a.nbytes == b.nbytes and bytes(a.win) == bytes(b.win))
+
+
+def test_integer_vectors_through_fast_forms():
+    doc = vectors("native_vectors.json.gz")
+    L = sim_lib()
+    buf_va = int(doc["buf_va"], 16)
+    fails, fast_total = [], 0
+    for c in doc["cases"]:
+        sp, regs = layout(bytes.fromhex(c["code"]), buf_va, splitmix_bytes(int(c["seed"], 16), 256))
+        for i in range(16):
+            regs.gpr[i] = int(c["in"][i], 16)
+        regs.rflags = int(c["fl"], 16) | 0x200
+        cnt = C.c_uint64(0)
+        out = sim_run(L, sp, regs, fast=True, counter=cnt, win_va=buf_va)
+        fast_total += cnt.value
+        want = [int(x, 16) for x in c["out"]]
+        got = list(out.gpr)
+        if c["cls"] == "bsx" and (int(c["flo"], 16) & 0x40):
+            got[c["dst"]] = want[c["dst"]]
+        win = bytearray(splitmix_bytes(int(c["seed"], 16), 256))
+        for i, v in c["diff"]:
+            win[i] = v
+        if out.status != INT3 or out.icount != 1:
+            fails.append((c["name"], "exit", out.status))
+        elif got != want or (out.rflags ^ int(c["flo"], 16)) & int(c["fmask"], 16):
+            fails.append((c["name"], "regs"))
+        elif bytes(out.win[:256]) != bytes(win):
+            fails.append((c["name"], "mem"))
+    assert not fails, f"{len(fails)} mismatches, first: {fails[:6]}"
+    assert fast_total > len(doc["cases"]) // 3, fast_total
+
+
+@pytest.mark.parametrize("name", ["sse_vectors.json.gz", "avx_vectors.json.gz"])
+def test_vector_vectors_fast_equals_slow(name):
+    doc = vectors(name)
+    L = sim_lib()
+    buf_va = int(doc["buf_va"], 16)
+    avx = name.startswith("avx")
+    fails, fast_total = [], 0
+    for c in doc["cases"]:
+        win = splitmix_bytes(int(c["seed"], 16), 256) if avx else window_in(int(c["seed"], 16), c["ldmx"])
+        sp, regs = layout(bytes.fromhex(c["code"]), buf_va, win)
+        for i in range(16):
+            regs.gpr[i] = int(c["in"][i], 16)
+        regs.rflags = int(c["fl"], 16) | 0x200
+        if avx:
+            ys = [int(v, 16) for v in c["yin"]]
+            for i in range(16):
+                regs.xmm[i][0], regs.xmm[i][1] = ys[4 * i], ys[4 * i + 1]
+                regs.ymmh[i][0], regs.ymmh[i][1] = ys[4 * i + 2], ys[4 * i + 3]
+        else:
+            xs = [int(v, 16) for v in c["xin"]]
+            for i in range(16):
+                regs.xmm[i][0], regs.xmm[i][1] = xs[2 * i], xs[2 * i + 1]
+            regs.mxcsr = int(c["mx"], 16)
+        slow, fast, n = run_both(L, sp, regs, buf_va)
+        fast_total += n
+        want = bytearray(win)
+        for i, v in c["diff"]:
+            want[i] = v
+        if not same(slow, fast):
+            fails.append((c["name"], c["code"], "fast != slow"))
+        elif bytes(fast.win[:256]) != bytes(want):
+            fails.append((c["name"], c["code"], "mem"))
+    assert not fails, f"{len(fails)} mismatches, first: {fails[:6]}"
+    assert fast_total > 50, fast_total
+
+
+# ---- the memcpy / memset forms at every alignment and at page ends
+MOVES = {
+    "movdqu load": "f30f6f0e",            # movdqu xmm1, [rsi]
+    "movdqu store": "f30f7f0f",           # movdqu [rdi], xmm1
+    "movups load": "0f100e",
+    "movups store": "0f110f",
+    "movdqa load": "660f6f0e",            # aligned: #GP when misaligned
+    "movdqa store": "660f7f0f",
+    "movaps store": "0f290f",
+    "vmovdqu ymm load": "c5fe6f0e",
+    "vmovdqu ymm store": "c5fe7f0f",
+    "vmovdqu xmm load": "c5fa6f0e",       # VEX.128: zeroes bits 255:128
+    "vmovdqu xmm store": "c5fa7f0f",
+    "vmovdqa ymm load": "c5fd6f0e",
+    "vmovdqa ymm store": "c5fd7f0f",
+    "vmovups ymm store": "c5fc110f",
+    "vmovaps ymm load": "c5fc280e",
+    "movdqa reg": "660f6fca",             # movdqa xmm1, xmm2
+    "movdqu reg store form": "f30f7fd1",  # movdqu xmm1, xmm2 (0f 7f, r/m = xmm1)
+    "vmovdqu ymm reg": "c5fe6fca",
+    "vmovdqu xmm reg": "c5fa6fca",
+    "pxor zero": "660fefc9",
+    "xorps zero": "0f57c9",
+    "vpxor zero 128": "c5f1efc9",
+    "vpxor zero 256": "c5f5efc9",
+    "pxor other": "660fefca",             # not the idiom: generic path
+    "vzeroupper": "c5f877",
+}
+
+
+PRIV = "8a078807"  # mov al, [rdi]; mov [rdi], al: the destination page becomes the lane's own first
+
+
+def move_case(code_hex, off_src, off_dst, cr0=None, cr4=None, xcr0=None):
+    code = bytes.fromhex(code_hex)
+    page = BUF & ~0xFFF
+    sp, regs = layout(code, page, bytes((i * 7 + 3) & 0xFF for i in range(4096)), cr0=cr0, cr4=cr4)
+    regs.gpr[6] = page + off_src  # rsi
+    regs.gpr[7] = page + off_dst  # rdi
+    for k in range(16):
+        regs.xmm[k][0], regs.xmm[k][1] = 0x1111111111111111 * (k + 1), 0x0101010101010101 * (k + 3)
+        regs.ymmh[k][0], regs.ymmh[k][1] = 0xA0A0A0A0A0A0A0A0 + k, 0xB0B0B0B0B0B0B0B0 + k
+    if xcr0 is not None:
+        regs.xcr0 = xcr0
+    return sp, regs
+
+
+@pytest.mark.parametrize("name", sorted(MOVES))
+def test_moves_fast_equals_slow_and_oracle(name):
+    L = sim_lib()
+    page = BUF & ~0xFFF
+    offsets = [(s, d) for s in (0, 1, 3, 7, 8, 13, 16, 24, 31) for d in (0, 2, 5, 8, 9, 16, 30)]
+    offsets += [(4096 - 32, 4096 - 16), (4096 - 16, 4096 - 32), (4096 - 20, 4096 - 9), (4096 - 1, 4096 - 33)]
+    fast_runs = 0
+    for s, d in offsets:
+        sp, regs = move_case(PRIV + MOVES[name], s, d)
+        slow, fast, n = run_both(L, sp, regs, page + 0x100 if max(s, d) < 0x100 else page + 4096 - 256)
+        fast_runs += n
+        assert same(slow, fast), (name, s, d, slow.status, fast.status)
+        # the priming moves always take the slow step (cold TLB, copy-on-write);
+        # the vector form runs fast unless it faults, crosses a page or is generic
+        size = 32 if name.startswith("v") and "ymm" in name else 16
+        off = (d if "store" in name and "reg" not in name else s) if ("load" in name or "store" in name) else 0
+        crosses = "reg" not in name and ("load" in name or "store" in name) and off + size > 4096
+        assert n == (0 if slow.status != INT3 or crosses or name == "pxor other" else 1), (name, s, d, n)
+        pfns, blob = sp.phys()
+        o = Oracle(pfns=pfns, blob=blob)
+        o.restore(regs)
+        ex = o.run()
+        r = o.regs()
+        if slow.status == INT3:
+            assert ex.status == INT3 and o.icount() == slow.icount, (name, s, d)
+            assert [r.xmm[i][h] for i in range(16) for h in range(2)] == list(fast.xmm), (name, s, d)
+            assert [r.ymmh[i][h] for i in range(16) for h in range(2)] == list(fast.ymmh), (name, s, d)
+            wv = page + 0x100 if max(s, d) < 0x100 else page + 4096 - 256
+            assert o.read_virt(wv, 256) == bytes(fast.win[:256]), (name, s, d)
+        else:
+            assert (ex.status, ex.vector) == (slow.status, slow.vector), (name, s, d)
+    assert (fast_runs == 0) if name == "pxor other" else fast_runs >= 5, (name, fast_runs)
+
+
+def test_vector_moves_defer_to_generic_when_state_is_off():
+    """CR0.TS (#NM), CR0.EM / no OSFXSR (#UD), no OSXSAVE or XCR0 (#UD): the
+    fast forms leave the lane to exec(), which raises the fault."""
+    L = sim_lib()
+    cases = [
+        ("f30f6f0e", dict(cr0=0x80050031 | 8), 7),
+        ("f30f6f0e", dict(cr0=0x80050031 | 4), 6),
+        ("f30f6f0e", dict(cr4=0x370678 & ~0x200), 6),
+        ("c5fe6f0e", dict(cr4=0x370678 & ~0x40000), 6),
+        ("c5fe6f0e", dict(xcr0=3), 6),
+        ("c5fe7f0f", dict(cr0=0x80050031 | 8), 7),
+        ("c5f877", dict(xcr0=3), 6),
+        ("660fefc9", dict(cr0=0x80050031 | 8), 7),
+    ]
+    for code, kw, vec in cases:
+        sp, regs = move_case(code, 0, 64, **kw)
+        slow, fast, n = run_both(L, sp, regs, 0)
+        assert (fast.status, fast.vector) == (EXIT_FAULT, vec), (code, kw, fast.status, fast.vector)
+        assert same(slow, fast) and n == 0, (code, kw)
+
+
+def test_aligned_forms_fault_when_misaligned_on_fast_path():
+    L = sim_lib()
+    for code in ("660f6f0e", "660f7f0f", "0f290f", "c5fd6f0e", "c5fd7f0f", "c5fc280e"):
+        sp, regs = move_case(code, 8 if code.endswith("0e") else 0, 8)
+        slow, fast, _ = run_both(L, sp, regs, 0)
+        assert (fast.status, fast.vector) == (EXIT_FAULT, 13), code
+        assert same(slow, fast), code
+
+
+def test_copy_loop_program_fast_equals_slow():
+    """The guests' memcpy shape: 32-byte vmovdqu blocks, 16-byte movdqu blocks,
+    vzeroupper, at several misalignments, with copy-on-write on first writes."""
+    # rcx = count of 32-byte blocks; rsi, rdi
+    prog = bytes.fromhex(
+        "c5fe6f06"      # vmovdqu ymm0, [rsi]
+        "c5fe7f07"      # vmovdqu [rdi], ymm0
+        "4883c620"      # add rsi, 32
+        "4883c720"      # add rdi, 32
+        "48ffc9"        # dec rcx
+        "75eb"          # jnz loop
+        "c5f877"        # vzeroupper
+        "f30f6f06"      # movdqu xmm0, [rsi]
+        "f30f7f07"      # movdqu [rdi], xmm0
+    )
+    L = sim_lib()
+    page = BUF & ~0xFFF
+    for s, d in ((0, 0), (1, 0), (3, 9), (16, 7), (5, 37)):
+        sp, regs = move_case(prog.hex(), s, 0x400 + d)
+        regs.gpr[1] = 20
+        slow, fast, n = run_both(L, sp, regs, page + 0x400)
+        assert same(slow, fast), (s, d)
+        assert fast.status == INT3 and n > 60, (s, d, fast.status, n)
+        src = bytes((i * 7 + 3) & 0xFF for i in range(4096))
+        assert bytes(fast.win[d:d + 656]) == src[s:s + 656][:512 - d], (s, d)

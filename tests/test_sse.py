@@ -205,7 +205,7 @@ class SimResult(C.Structure):
     _fields_ = [("gpr", C.c_uint64 * 16), ("rip", C.c_uint64), ("rflags", C.c_uint64), ("icount", C.c_uint64),
                 ("nbytes", C.c_uint64), ("status", C.c_uint32), ("vector", C.c_uint32), ("error", C.c_uint32),
                 ("ovn", C.c_uint32), ("addr", C.c_uint64), ("dirty", C.c_uint64 * 64), ("xmm", C.c_uint64 * 32),
-                ("mxcsr", C.c_uint32), ("pad", C.c_uint32), ("ymmh", C.c_uint64 * 32)]
+                ("mxcsr", C.c_uint32), ("pad", C.c_uint32), ("ymmh", C.c_uint64 * 32), ("win", C.c_uint8 * 512)]
 
 
 def sim_lib():
@@ -214,14 +214,20 @@ def sim_lib():
     L = C.CDLL(os.path.join(d, "libsimlane.so"))
     L.sim_run.argtypes = [C.POINTER(C.c_uint64), C.c_char_p, C.c_uint64, C.POINTER(Regs), C.c_uint64,
                           C.POINTER(SimResult)]
+    L.sim_run_mode.argtypes = L.sim_run.argtypes + [C.c_int, C.POINTER(C.c_uint64), C.c_uint64]
     return L
 
 
-def sim_run(L, sp, regs, limit=0):
+def sim_run(L, sp, regs, limit=0, fast=False, counter=None, win_va=0):
+    """One lane from `regs` until it stops; fast=True tries the fast loop's
+    form of each instruction first (k_run's order). `counter` (a c_uint64)
+    counts the instructions the fast form retired; `win_va` selects the 512
+    bytes returned in `win`."""
     pfns, blob = sp.phys()
     arr = (C.c_uint64 * len(pfns))(*pfns)
     out = SimResult()
-    L.sim_run(arr, blob, len(pfns), C.byref(regs), limit, C.byref(out))
+    cnt = counter if counter is not None else C.c_uint64(0)
+    L.sim_run_mode(arr, blob, len(pfns), C.byref(regs), limit, C.byref(out), 1 if fast else 0, C.byref(cnt), win_va)
     return out
 
 
@@ -254,7 +260,8 @@ def test_engine_sse_code_faults(code, status, vector):
         assert out.vector == vector
 
 
-def test_engine_sse_code_matches_oracle_on_random_programs():
+@pytest.mark.parametrize("fast", [False, True])
+def test_engine_sse_code_matches_oracle_on_random_programs(fast):
     from tests import progfuzz
 
     L = sim_lib()
@@ -271,7 +278,7 @@ def test_engine_sse_code_matches_oracle_on_random_programs():
             regs.xmm[k][0], regs.xmm[k][1] = xmm[i][2 * k], xmm[i][2 * k + 1]
             regs.ymmh[k][0], regs.ymmh[k][1] = ymmh[i][2 * k], ymmh[i][2 * k + 1]
         regs.rip, regs.rflags = va, flags
-        out = sim_run(L, sp, regs, limit=20000)
+        out = sim_run(L, sp, regs, limit=20000, fast=fast)
         got = (out.status, out.vector if out.status == EXIT_FAULT else 0, out.rip, out.icount)
         exp = (w["status"], w["vector"] if w["status"] == EXIT_FAULT else 0, w["rip"], w["icount"])
         if got != exp:

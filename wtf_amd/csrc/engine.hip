@@ -109,6 +109,7 @@ __device__ __forceinline__ void load_lane(const Dev &P, u32 lane, Lane &L) {
   L.cr3 = s.cr3;
   L.efer = s.efer;
   L.cpl = s.cpl;
+  L.simd = simd_bits(s.cr0, s.cr4, P.full[lane].xcr0);
   L.ovn = P.ov_count[lane];
   L.lane = lane;
   L.cgen = P.lane_gen ? P.lane_gen[lane] : 0;
@@ -930,7 +931,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
         L.pend = 0;
         const u32 len = fo_len(f);
         u64 next;
-        fast_exec(L, f, grip + len, next);
+        fast_exec(P, L, f, grip + len, next);
         if (!L.miss) {
           L.rip = next;
           L.icount++;
@@ -1166,6 +1167,7 @@ __device__ __forceinline__ void lane_min_load(const Dev &P, u32 lane, Lane &L) {
   L.cr3 = s.cr3;
   L.efer = s.efer;
   L.cpl = 0;  // host accesses are not subject to user checks (VirtTranslate has none)
+  L.simd = 0;
   L.ovn = P.ov_count[lane];
   L.bloom = 0;
   for (u32 k = 0; k < L.ovn; k++) L.bloom |= bloom_bit(P.ov_gpfn[(u64)k * P.nlanes + lane]);

@@ -20,7 +20,18 @@ struct Lane {
   u32 miss, miss_acc, flush, pend;  // pend: bytes accessed by the attempt in flight
   u32 nodeliver;                    // this fault could not be delivered through the guest IDT
   u32 cgen, ccnt;                   // coverage set: generation, live entries
+  u32 simd;                         // bit 0: SSE usable, bit 1: AVX usable (simd_bits)
 };
+
+// Which vector state the lane's cr0 / cr4 / xcr0 enable without a fault: bit 0
+// legacy SSE (CR0.EM = 0, CR0.TS = 0, CR4.OSFXSR), bit 1 VEX (CR4.OSXSAVE,
+// XCR0[2:1] = 11, CR0.TS = 0). The fast path runs vector moves only then.
+__device__ __forceinline__ u32 simd_bits(u64 cr0, u64 cr4, u64 xcr0) {
+  const bool ts = (cr0 >> 3) & 1;
+  const u32 sse = !((cr0 >> 2) & 1) && !ts && ((cr4 >> 9) & 1);
+  const u32 avx = !ts && ((cr4 >> 18) & 1) && (xcr0 & 6) == 6;
+  return sse | avx << 1;
+}
 
 // GPR r of the lane. r is wave-uniform and the halves live in two u32 arrays
 // that the compiler keeps in VGPRs, indexed with s_set_gpr_idx (32-bit moves

@@ -39,6 +39,13 @@ enum : u32 {
   FO_SHIFT,   // res = shift_op(sub, a, imm)
   FO_CMOV,    // res = cond(sub) ? b : a
   FO_SETCC,   // res = cond(sub)
+  // SSE / AVX data movement (engine_sse.h semantics), ra = the xmm / ymm
+  // register, sz = operand bytes / 8; sub bit 0: aligned form, bit 1: VEX
+  // (VEX.128 zeroes bits 255:128), bit 2 (FO_VMOV): the zeroing xor idiom
+  FO_VLD,     // ymm[ra] = mem
+  FO_VST,     // mem = ymm[ra]
+  FO_VMOV,    // ymm[ra] = ymm[rb] (or 0)
+  FO_VZU,     // vzeroupper
 };
 // pipeline flags
 enum : u32 {
@@ -87,6 +94,34 @@ __device__ __forceinline__ u32 loc_regno(const UOp &u, u32 loc) {
   }
 }
 
+// The moves memcpy / memset loops run (legacy and VEX movdqu / movdqa /
+// movups / movaps loads, stores and register moves, the pxor / xorps zeroing
+// idiom, vzeroupper); every other O_SSE form stays generic.
+__device__ __forceinline__ void digest_sse(const UOp &u, u32 &op, u32 &sub, u32 &ra, u32 &rb, u32 &sz) {
+  const u32 x = u.opreg, c = u.sub, pp = u.bsz;
+  const bool vex = x & 1;
+  if (vex_map(x) != 1 || (x & 0x10000)) return;
+  const u32 vvvv = vex ? (x >> 4) & 15 : 0;
+  sz = vex && ((x >> 1) & 1) ? 4 : 2;
+  sub = vex ? 2 : 0;
+  if (vex && c == 0x77) {  // vzeroupper (vzeroall stays generic)
+    if (sz == 2) op = FO_VZU;
+    return;
+  }
+  const bool load = ((c == 0x6f) && (pp == 1 || pp == 2)) || ((c == 0x10 || c == 0x28) && pp <= 1);
+  const bool store = ((c == 0x7f) && (pp == 1 || pp == 2)) || ((c == 0x11 || c == 0x29) && pp <= 1);
+  const bool aligned = c == 0x28 || c == 0x29 || (pp == 1 && (c == 0x6f || c == 0x7f));
+  if ((load || store) && vvvv == 0) {
+    if (aligned) sub |= 1;
+    if (!u.is_mem) op = FO_VMOV, ra = load ? u.reg : u.rm, rb = load ? u.rm : u.reg;
+    else op = load ? FO_VLD : FO_VST, ra = u.reg;
+    return;
+  }
+  // pxor / xorps / xorpd x, x (VEX: vvvv == r/m): zero
+  if (((c == 0xef && pp == 1) || (c == 0x57 && pp <= 1)) && !u.is_mem && (vex ? vvvv : u.reg) == u.rm)
+    op = FO_VMOV, sub |= 4, ra = u.reg, rb = u.rm;
+}
+
 __device__ __forceinline__ void digest(const UOp &u, FOp &f) {
   u32 op = FO_GENERIC, fl = 0, sub = u.sub;
   const u32 ra = loc_regno(u, u.asrc), rb = loc_regno(u, u.bsrc);
@@ -96,7 +131,10 @@ __device__ __forceinline__ void digest(const UOp &u, FOp &f) {
   // high-byte registers (ah/ch/dh/bh) stay on the generic path
   const bool hb = !u.rex && ((u.asz == 1 && areg && ra >= 4 && ra < 8) || (u.bsz == 1 && breg && rb >= 4 && rb < 8));
   u64 imm = u.imm;
-  if (u.supported && !u.seg && !u.p67 && !u.rep && !hb) {
+  u32 ra_ = ra, rb_ = rb, sz_ = u.asz;
+  if (u.op == O_SSE && u.supported && !u.seg && !u.p67) {
+    digest_sse(u, op, sub, ra_, rb_, sz_);
+  } else if (u.supported && !u.seg && !u.p67 && !u.rep && !hb) {
     switch (u.op) {
       case O_NOP: op = FO_NOP; break;
       case O_MOV:
@@ -163,10 +201,10 @@ __device__ __forceinline__ void digest(const UOp &u, FOp &f) {
     }
   }
   const u32 base = u.base >= 0 ? (u32)u.base : NOREG, index = u.index >= 0 ? (u32)u.index : NOREG;
-  f.w0 = op | (sub & 0xf) << 8 | (u.asz & 0xf) << 12 | (u.bsz & 0xf) << 16 | (u.len & 0x3f) << 20 |
+  f.w0 = op | (sub & 0xf) << 8 | (sz_ & 0xf) << 12 | (u.bsz & 0xf) << 16 | (u.len & 0x3f) << 20 |
          (u.scale & 3) << 26 | (u.riprel & 1) << 28;
   f.fl = fl;
-  f.w2 = (ra & 0xff) | (rb & 0xff) << 8 | (base & 0xff) << 16 | (index & 0xff) << 24;
+  f.w2 = (ra_ & 0xff) | (rb_ & 0xff) << 8 | (base & 0xff) << 16 | (index & 0xff) << 24;
   f.pad = 0;
   f.disp = u.disp;
   f.imm = imm;
@@ -195,9 +233,90 @@ __device__ __forceinline__ u8 *fxlate(Lane &L, u64 va, u32 sz, int acc) {
   return (u8 *)(uintptr_t)(td & ~0xfffull) + (va & 0xfff);
 }
 
-__device__ __forceinline__ int fast_exec(Lane &L, const FOp &f, u64 nrip, u64 &next) {
+// 16 / 32 bytes at p (inside one page): aligned words, funnel-shifted when p
+// is not 8-byte aligned (the word past the operand is read only then, and it
+// lies in the same page).
+__device__ __forceinline__ void vload(const u8 *p, u32 k, u64 *v) {
+  const u64 *w = (const u64 *)((uintptr_t)p & ~(uintptr_t)7);
+  const u32 sh = 8 * (u32)((uintptr_t)p & 7);
+  if (!sh) {
+    for (u32 i = 0; i < k; i++) v[i] = w[i];
+    return;
+  }
+  u64 prev = w[0];
+  for (u32 i = 0; i < k; i++) {
+    const u64 nx = w[i + 1];
+    v[i] = (prev >> sh) | (nx << (64 - sh));
+    prev = nx;
+  }
+}
+// The store side: whole words in the middle, the two partial end words merged
+// (the page is the lane's own overlay copy, no other lane writes it).
+__device__ __forceinline__ void vstore(u8 *p, u32 k, const u64 *v) {
+  u64 *w = (u64 *)((uintptr_t)p & ~(uintptr_t)7);
+  const u32 sh = 8 * (u32)((uintptr_t)p & 7);
+  if (!sh) {
+    for (u32 i = 0; i < k; i++) w[i] = v[i];
+    return;
+  }
+  const u64 keep = (1ull << sh) - 1;
+  const u64 first = w[0], last = w[k];
+  w[0] = (first & keep) | (v[0] << sh);
+  for (u32 i = 1; i < k; i++) w[i] = (v[i - 1] >> (64 - sh)) | (v[i] << sh);
+  w[k] = (last & ~keep) | (v[k - 1] >> (64 - sh));
+}
+
+// The FO_V* ops. Anything the generic path would check or fault on (SSE / AVX
+// state off in cr0 / cr4 / xcr0, a misaligned aligned form, a TLB miss, a first
+// write, a page-crossing operand) leaves through L.miss to exec().
+__device__ __forceinline__ int fast_vec(const Dev &P, Lane &L, const FOp &f, u64 nrip) {
+  const u32 op = fo_op(f), sub = fo_sub(f), k = fo_sz(f), n = 8 * k;
+  if (!((L.simd >> ((sub >> 1) & 1)) & 1)) {
+    L.miss = 1;
+    return X_FAULT;
+  }
+  wtfgpu_regs_t &F = P.full[L.lane];
+  if (op == FO_VZU) {
+    for (u32 i = 0; i < 16; i++) F.ymmh[i][0] = F.ymmh[i][1] = 0;
+    return X_OK;
+  }
+  const u32 ra = fo_ra(f) & 15;
+  u64 v[4] = {0, 0, 0, 0};
+  if (op == FO_VMOV) {
+    const u32 rb = fo_rb(f) & 15;
+    if (!(sub & 4)) v[0] = F.xmm[rb][0], v[1] = F.xmm[rb][1];
+    if (!(sub & 4) && n == 32) v[2] = F.ymmh[rb][0], v[3] = F.ymmh[rb][1];
+  } else {
+    u64 addr = f.disp + (fo_riprel(f) ? nrip : 0);
+    if (fo_base(f) != NOREG) addr += R(L, fo_base(f));
+    if (fo_index(f) != NOREG) addr += R(L, fo_index(f)) << fo_scale(f);
+    if ((sub & 1) && (addr & (n - 1))) {
+      L.miss = 1;
+      return X_FAULT;
+    }
+    u8 *mp = fxlate(L, addr, n, op == FO_VST ? ACC_W : ACC_R);
+    if (!mp) return X_FAULT;
+    L.pend += n;
+    if (op == FO_VST) {
+      v[0] = F.xmm[ra][0], v[1] = F.xmm[ra][1], v[2] = F.ymmh[ra][0], v[3] = F.ymmh[ra][1];
+      vstore(mp, k, v);
+      return X_OK;
+    }
+    vload(mp, k, v);
+  }
+  F.xmm[ra][0] = v[0];
+  F.xmm[ra][1] = v[1];
+  if (n == 32 || (sub & 2)) {  // VEX.128 zeroes the upper half, legacy SSE keeps it
+    F.ymmh[ra][0] = v[2];
+    F.ymmh[ra][1] = v[3];
+  }
+  return X_OK;
+}
+
+__device__ __forceinline__ int fast_exec(const Dev &P, Lane &L, const FOp &f, u64 nrip, u64 &next) {
   next = nrip;
   const u32 F = f.fl, op = fo_op(f), sub = fo_sub(f), sz = fo_sz(f);
+  if (op >= FO_VLD) return fast_vec(P, L, f, nrip);
   const u64 rsp = R(L, 4);
   u64 a = (F & FF_AREG) ? R(L, fo_ra(f)) : 0;
   u64 b = (F & FF_BREG) ? R(L, fo_rb(f)) : f.imm;

@@ -1140,6 +1140,7 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
           const u64 v = R(L, u.rm & 15);
           if (n == 0) {
             L.cr0 = S.cr0 = v;
+            L.simd = simd_bits(v, S.cr4, P.full[L.lane].xcr0);
             L.flush = 1;
           } else if (n == 2) {
             S.cr2 = v;
@@ -1153,6 +1154,7 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
             }
           } else if (n == 4) {
             S.cr4 = v;
+            L.simd = simd_bits(L.cr0, v, P.full[L.lane].xcr0);
             L.flush = 1;
           } else if (n == 8) {
             P.full[L.lane].cr8 = v & 15;
