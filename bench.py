@@ -5,7 +5,9 @@ HEVD) at 1/2/4/8 GPUs").
 Headline (`value`): fuzzer_tlv_server on the gpu backend (BASELINE.json
 configs[2] at N=1, configs[3] at N>1): the synthetic tlv_server snapshot
 (wtf_amd/tools/tlv.py; the real one cannot be fetched), the tlv
-module and its custom mutator, seed 1337, 65,536 lanes per GPU, --limit 100000.
+module and its custom mutator, seed 1337, 131,072 lanes per GPU (two waves per
+SIMD: the most the k_run register budget keeps resident; configs[2] names no
+batch), --limit 100000.
 One step = one fuzz batch of the node (include/wtfnode.h, libwtfnode.so, the
 same C++ as `wtfgpu fuzz`): mutate (overlapped with the previous batch) ->
 InsertTestcase x N -> k_run with breakpoints serviced -> lane-order coverage
@@ -69,7 +71,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=6)
-    ap.add_argument("--lanes", type=int, default=65536)
+    ap.add_argument("--lanes", type=int, default=131072, help="lanes per GPU of the tlv and hevd legs")
+    ap.add_argument("--syn-lanes", type=int, default=65536, help="BASELINE.json configs[1]: 64K lanes")
     ap.add_argument("--slice-steps", type=int, default=0, help="wave-steps per streaming slice (0: the node's 4096)")
     ap.add_argument("--regroup-steps", type=int, default=-1,
                     help="k_run launch length with lanes regrouped by rip (0: off; -1: engine default)")
@@ -412,7 +415,7 @@ def run(a, rank, world, local, tmp):
                 h["cpu_baseline"] = cpu["hevd"]
                 h["vs_cpu"] = h["value"] / cpu["hevd"]["value"]
             out["hevd"] = h
-            s = syn_leg(a.lanes, a.limit, 10, local)
+            s = syn_leg(a.syn_lanes, a.limit, 10, local)
             if "syn" in cpu:
                 s["cpu_baseline"] = cpu["syn"]
             out["syn"] = s

@@ -257,7 +257,9 @@ int wtfgpu_restore_lanes(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n);
 /* Feeds of a lane list, each in a fixed per-lane region (running lanes keep
  * theirs): lane lanes[i] gets bytes[offsets[i] .. offsets[i+1]); has_feed[i]
  * == 0, or a feed larger than the region, sends that lane's FEED hits to the
- * host handler. */
+ * host handler. Asynchronous on the current queue: `bytes` (pinned memory,
+ * wtfgpu_host_alloc, for a DMA) must stay unchanged until the queue's next
+ * synchronising call (wtfgpu_run_wait, or any call that returns data). */
 int wtfgpu_set_feed_lanes(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, const uint64_t *offsets,
                           const uint8_t *has_feed, const uint8_t *bytes, uint64_t nbytes);
 /* New-coverage sets of a lane list (as wtfgpu_read_coverage); a call whose

@@ -31,6 +31,13 @@
 //   kdmp <dump> [gva...]      wtf_amd/host/kdmp.cc in oracle/ref_kdmp_dump.cc's
 //                             output format (TYPE / CR3 / RIP / PAGE / VT lines),
 //                             for comparison with oracle/_ref/kdmp_ref
+//   tlv-feed <file>           each testcase of <file> (u32 length + bytes, repeated)
+//                             deserialized as fuzzer_tlv_server's InsertTestcase
+//                             does (fuzzer_tlv_server.cc:36-40, 67-75; this
+//                             repository: TlvServer::TestcaseFeed) and printed as
+//                             its packet chunks "F <hex>" (u32 Size, u32 Command,
+//                             u16 Id, u16 BodySize, Body), or "F -" when it does
+//                             not deserialize (the reference throws)
 // Both builds (the reference through yas and socket.h's serializers, this
 // repository through wtf_amd/host/wire.cc):
 //   wire-testcase <hex>       the master's Testcase message (server.h:720-737)
@@ -107,6 +114,66 @@ static int cmd_cpustate(const char *path) {
            (unsigned long long)segs[i]->Base, (unsigned)segs[i]->Limit, (unsigned)segs[i]->Attr);
   for (int i = 0; i < 8; i++) printf("fpst%d %llx\n", i, (unsigned long long)S.Fpst[i]);
 #undef P
+  return 0;
+}
+
+#ifdef WTF_AMD_HOST
+namespace TlvServer {
+bool TestcaseFeedBytes(const uint8_t *Buffer, const size_t BufferSize, std::vector<uint8_t> &Feed);
+}  // namespace TlvServer
+#else
+namespace TlvServer {  // the reference's types (fuzzer_tlv_server.cc:23-34), same layout
+struct Packet_t {
+  uint32_t Command;
+  uint16_t Id;
+  uint16_t BodySize;
+  std::vector<uint8_t> Body;
+};
+struct Packets_t {
+  std::vector<Packet_t> Packets;
+};
+Packets_t Deserialize(const uint8_t *Buffer, const size_t BufferSize);
+}  // namespace TlvServer
+#endif
+
+static int cmd_tlv_feed(const char *path) {
+  const auto all = read_all(path);
+  for (size_t o = 0; o + 4 <= all.size();) {
+    uint32_t n;
+    memcpy(&n, &all[o], 4);
+    if (o + 4 + n > all.size()) return 1;
+    const uint8_t *tc = all.data() + o + 4;
+    o += 4 + n;
+    std::vector<uint8_t> Feed;
+    bool ok = true;
+#ifdef WTF_AMD_HOST
+    ok = TlvServer::TestcaseFeedBytes(tc, n, Feed);
+#else
+    try {
+      const TlvServer::Packets_t P = TlvServer::Deserialize(tc, n);
+      for (const TlvServer::Packet_t &Pk : P.Packets) {
+        const uint32_t Size = uint32_t(8 + Pk.Body.size());
+        const size_t At = Feed.size();
+        Feed.resize(At + 4 + Size);
+        uint8_t *Q = Feed.data() + At;
+        memcpy(Q, &Size, 4);
+        memcpy(Q + 4, &Pk.Command, 4);
+        memcpy(Q + 8, &Pk.Id, 2);
+        memcpy(Q + 10, &Pk.BodySize, 2);
+        if (!Pk.Body.empty()) memcpy(Q + 12, Pk.Body.data(), Pk.Body.size());
+      }
+    } catch (const std::exception &) {
+      ok = false;
+    }
+#endif
+    if (!ok) {
+      printf("F -\n");
+      continue;
+    }
+    printf("F ");
+    for (uint8_t c : Feed) printf("%02x", c);
+    printf("\n");
+  }
   return 0;
 }
 
@@ -223,6 +290,7 @@ int main(int argc, char **argv) {
   if (argc < 2) return 2;
   const std::string cmd = argv[1];
   if (cmd.rfind("wire-", 0) == 0 && argc >= 3) return cmd_wire(argc, argv);
+  if (cmd == "tlv-feed" && argc == 3) return cmd_tlv_feed(argv[2]);
 #ifdef WTF_AMD_HOST
   if (cmd == "xof" && argc == 4) {
     const auto b = unhex(argv[2]);

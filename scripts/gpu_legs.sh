@@ -2,7 +2,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 for R in ${RG_LIST:-0 256}; do
-  WTFGPU_REGROUP_STEPS=$R timeout -k 10 400 python -u bench.py --no-cpu --regroup-steps $R --lanes ${LANES:-65536} > gpurun_out/legs_$R.log 2>&1 || { echo FAIL $R; tail -20 gpurun_out/legs_$R.log; exit 1; }
+  WTFGPU_REGROUP_STEPS=$R timeout -k 10 400 python -u bench.py --no-cpu --regroup-steps $R --lanes ${LANES:-131072} > gpurun_out/legs_$R.log 2>&1 || { echo FAIL $R; tail -20 gpurun_out/legs_$R.log; exit 1; }
   tail -1 gpurun_out/legs_$R.log | python -c "
 import json,sys; d=json.loads(sys.stdin.read())
 print('R=$R tlv', round(d['value']), 'lpws', round(d['lanes_per_wave_step'],1))

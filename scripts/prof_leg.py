@@ -14,7 +14,8 @@ import bench  # noqa: E402
 def main():
     leg = sys.argv[1]
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-    lanes, limit = 65536, 100000
+    limit = 100000
+    lanes = 65536 if leg == "syn" else 131072  # bench.py's --syn-lanes / --lanes defaults
     if leg == "syn":
         s = bench.syn_leg(lanes, limit, steps, 0)
         print(json.dumps({"leg": "syn", "lanes": lanes, "limit": limit, "launches": s.get("launches"),

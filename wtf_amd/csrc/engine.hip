@@ -1575,6 +1575,8 @@ struct QueueRes {
   hipStream_t stream = nullptr;
   u8 *d_scratch = nullptr;
   u64 scratch_bytes = 0;
+  u8 *h_stage = nullptr;  // pinned host staging of the queue's asynchronous uploads
+  u64 stage_bytes = 0;
   u64 *d_stat = nullptr;
   Dev *d_dev = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -1637,6 +1639,8 @@ struct wtfgpu_ctx {
   wtfgpu_regs_t initial{};
   bool have_initial = false;
   u8 *d_scratch = nullptr;
+  u8 *h_stage = nullptr;
+  u64 stage_bytes = 0;
   // cross-wave regrouping (wtfgpu_run): sort keys, the lane order, radix-sort scratch
   u32 *d_rkeys = nullptr, *d_rkeys2 = nullptr, *d_rlanes = nullptr, *d_perm = nullptr;
   void *d_rtemp = nullptr;
@@ -1679,10 +1683,25 @@ int ensure_scratch(wtfgpu_ctx *c, u64 bytes) {
   return WTFGPU_OK;
 }
 
+// The current queue's pinned staging buffer, at least `bytes`. Only for a
+// call that synchronised the queue's stream first (no DMA still reads it).
+int ensure_stage(wtfgpu_ctx *c, u64 bytes) {
+  if (bytes <= c->stage_bytes) return WTFGPU_OK;
+  if (c->h_stage) HIPCHK(hipHostFree(c->h_stage));
+  c->h_stage = nullptr;
+  c->stage_bytes = 0;
+  const u64 want = std::max<u64>(bytes * 2, 1 << 20);
+  if (hipHostMalloc((void **)&c->h_stage, want, hipHostMallocDefault) != hipSuccess) return WTFGPU_ERR_OOM;
+  c->stage_bytes = want;
+  return WTFGPU_OK;
+}
+
 void queue_save(wtfgpu_ctx *c, QueueRes &q) {
   q.stream = c->stream;
   q.d_scratch = c->d_scratch;
   q.scratch_bytes = c->scratch_bytes;
+  q.h_stage = c->h_stage;
+  q.stage_bytes = c->stage_bytes;
   q.d_stat = c->d_stat;
   q.d_dev = c->d_dev;
   q.ev0 = c->ev0;
@@ -1698,6 +1717,8 @@ void queue_load(wtfgpu_ctx *c, const QueueRes &q) {
   c->stream = q.stream;
   c->d_scratch = q.d_scratch;
   c->scratch_bytes = q.scratch_bytes;
+  c->h_stage = q.h_stage;
+  c->stage_bytes = q.stage_bytes;
   c->d_stat = q.d_stat;
   c->d_dev = q.d_dev;
   c->ev0 = q.ev0;
@@ -1730,6 +1751,8 @@ void queue_destroy(QueueRes &q) {
   dfree(q.d_stat);
   dfree(q.d_dev);
   dfree(q.d_scratch);
+  if (q.h_stage) (void)hipHostFree(q.h_stage);
+  q.h_stage = nullptr;
   if (q.ev0) (void)hipEventDestroy(q.ev0);
   if (q.ev1) (void)hipEventDestroy(q.ev1);
   if (q.stream) (void)hipStreamDestroy(q.stream);
@@ -2343,20 +2366,22 @@ int wtfgpu_set_feed_lanes(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, cons
   const u64 o_off = ((u64)n * 4 + 255) & ~255ull, o_len = o_off + a8, o_pos = o_len + a8, o_end = o_pos + a8,
             o_data = o_end + a8;
   if (ensure_scratch(c, o_data + nbytes)) return WTFGPU_ERR_OOM;
-  std::vector<u8> stage(o_data);
-  memcpy(stage.data(), lanes, (u64)n * 4);
-  memcpy(stage.data() + o_off, off.data(), (u64)n * 8);
-  memcpy(stage.data() + o_len, len.data(), (u64)n * 8);
-  memcpy(stage.data() + o_pos, pos.data(), (u64)n * 8);
-  memcpy(stage.data() + o_end, end.data(), (u64)n * 8);
-  HIPCHK(hipMemcpyAsync(c->d_scratch, stage.data(), stage.size(), hipMemcpyHostToDevice, c->stream));
+  if (ensure_stage(c, o_data)) return WTFGPU_ERR_OOM;
+  u8 *stage = c->h_stage;
+  memcpy(stage, lanes, (u64)n * 4);
+  memcpy(stage + o_off, off.data(), (u64)n * 8);
+  memcpy(stage + o_len, len.data(), (u64)n * 8);
+  memcpy(stage + o_pos, pos.data(), (u64)n * 8);
+  memcpy(stage + o_end, end.data(), (u64)n * 8);
+  HIPCHK(hipMemcpyAsync(c->d_scratch, stage, o_data, hipMemcpyHostToDevice, c->stream));
   if (nbytes) HIPCHK(hipMemcpyAsync(c->d_scratch + o_data, bytes, nbytes, hipMemcpyHostToDevice, c->stream));
   k_feed_scatter<<<n, 256, 0, c->stream>>>(c->d_feeddata, S, (const u32 *)c->d_scratch,
                                            (const u64 *)(c->d_scratch + o_off), (const u64 *)(c->d_scratch + o_len), n,
                                            c->d_scratch + o_data, c->d_feedpos, c->d_feedend,
                                            (const u64 *)(c->d_scratch + o_pos), (const u64 *)(c->d_scratch + o_end));
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(c->stream));
+  // no wait: the queue's later work (its k_run slice) is ordered after the
+  // scatter, and the next call on this queue synchronises first
   c->P.feed_pos = c->d_feedpos;
   c->P.feed_end = c->d_feedend;
   c->P.feed_data = c->d_feeddata;
@@ -2547,6 +2572,20 @@ static int launch_chunk(wtfgpu_ctx *c, const Dev &Q, u32 first, u32 count, u64 s
   return WTFGPU_OK;
 }
 
+// Diagnostic build only: the per-phase cycle totals of one run (stat[4..11]).
+static void print_stamps(const u64 *s) {
+#ifdef WTFGPU_STAMPS
+  if (s[0])
+    fprintf(stderr,
+            "wtfgpu stamps (cycles per wave-step, %llu steps): fast loop %.0f, slow: xlate+fill %.0f, coverage %.0f, "
+            "exec %.0f, cross-page %.0f\n",
+            (unsigned long long)s[0], (double)s[4] / s[0], (double)s[6] / s[0], (double)s[7] / s[0],
+            (double)s[5] / s[0], (double)s[9] / s[0]);
+#else
+  (void)s;
+#endif
+}
+
 int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps, wtfgpu_run_stats_t *stats) {
   if (!lanes_ok(c, first, count) || (first % c->P.lpw)) return WTFGPU_ERR_INVALID;
   if (!c->P.pool) return WTFGPU_ERR_STATE;
@@ -2592,13 +2631,7 @@ int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps
     st.kernel_launches += k;
     st.group_steps += s[0];
     st.lane_retired += s[1];
-#ifdef WTFGPU_STAMPS
-    fprintf(stderr,
-            "wtfgpu stamps (cycles per wave-step, %llu steps): fast loop %.0f, slow: xlate+fill %.0f, coverage %.0f, "
-            "exec %.0f, cross-page %.0f\n",
-            (unsigned long long)s[0], (double)s[4] / s[0], (double)s[6] / s[0], (double)s[7] / s[0],
-            (double)s[5] / s[0], (double)s[9] / s[0]);
-#endif
+    print_stamps(s);
     if (s[2] == 0 || done >= max_steps) break;
   }
   st.kernel_ms = ms_total;
@@ -2647,6 +2680,7 @@ int wtfgpu_run_wait(wtfgpu_ctx *c, wtfgpu_run_stats_t *stats) {
     st.lane_retired = s[1];
     st.kernel_ms = ms;
     c->async_launches = 0;
+    print_stamps(s);
   }
   if (stats) *stats = st;
   return WTFGPU_OK;

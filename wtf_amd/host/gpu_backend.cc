@@ -530,28 +530,64 @@ bool GpuBackend_t::RevokeLastNewCoverage() {
 // their original content in parallel; each changed byte range becomes one
 // write record (copy-on-write + dirty on the device).
 int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
-  std::vector<uint32_t> rl;
-  std::vector<uint64_t> regs;
+  const auto tp = Clock::now();
+  const size_t nl = lanes.size();
+  const bool par = nl >= 1024;
+  // per lane: registers to upload, staged pages, logged write records / bytes
+  // (counted on all host threads, then prefix sums)
+  std::vector<uint64_t> rcnt(nl + 1, 0), pcnt(nl + 1, 0), roff(nl + 1, 0), boff(nl + 1, 0);
+  bool any_cr = false;
+#pragma omp parallel for schedule(static, 256) if (par) reduction(|| : any_cr)
+  for (size_t i = 0; i < nl; i++) {
+    const LaneView &v = views_[lanes[i]];
+    rcnt[i + 1] = v.regs_dirty ? 1 : 0;
+    pcnt[i + 1] = v.pages.size();
+    uint64_t r = 0, b = 0;
+    for (const LaneView::Logged &w : v.wlog)
+      if (w.len) {
+        r++;
+        b += w.len;
+      }
+    roff[i + 1] = r;
+    boff[i + 1] = b;
+    any_cr = any_cr || v.cr_dirty;
+  }
+  for (size_t i = 0; i < nl; i++) {
+    rcnt[i + 1] += rcnt[i];
+    pcnt[i + 1] += pcnt[i];
+    roff[i + 1] += roff[i];
+    boff[i + 1] += boff[i];
+  }
+  if (any_cr)
+    for (uint32_t l : lanes) {
+      LaneView &v = views_[l];
+      for (int k = 0; k < 2; k++)
+        if (v.cr_dirty & (1 << k)) {
+          std::lock_guard<std::mutex> g(engine_mu_);
+          if (wtfgpu_lane_set_cr(ctx_, l, k ? 3 : 2, v.cr[k]) != WTFGPU_OK) return WTFGPU_ERR_INVALID;
+        }
+      v.cr_dirty = 0;
+    }
+  std::vector<uint32_t> rl(rcnt[nl]);
+  std::vector<uint64_t> regs(rcnt[nl] * 18);
+  // staged pages: diffed against their original content, only the changed span is written
   struct Cand {
     uint32_t lane;
     const Staged *p;
     uint32_t lo, hi;
   };
-  std::vector<Cand> cand;
-  for (uint32_t l : lanes) {
+  std::vector<Cand> cand(pcnt[nl]);
+#pragma omp parallel for schedule(static, 256) if (par)
+  for (size_t i = 0; i < nl; i++) {
+    const uint32_t l = lanes[i];
     LaneView &v = views_[l];
     if (v.regs_dirty) {
-      rl.push_back(l);
-      regs.insert(regs.end(), v.gpr, v.gpr + 18);
+      rl[rcnt[i]] = l;
+      memcpy(&regs[rcnt[i] * 18], v.gpr, 18 * 8);
       v.regs_dirty = false;
     }
-    for (const Staged &p : v.pages) cand.push_back(Cand{l, &p, 0, 0});
-    for (int k = 0; k < 2; k++)
-      if (v.cr_dirty & (1 << k)) {
-        std::lock_guard<std::mutex> g(engine_mu_);
-        if (wtfgpu_lane_set_cr(ctx_, l, k ? 3 : 2, v.cr[k]) != WTFGPU_OK) return WTFGPU_ERR_INVALID;
-      }
-    v.cr_dirty = 0;
+    uint64_t k = pcnt[i];
+    for (const Staged &p : v.pages) cand[k++] = Cand{l, &p, 0, 0};
   }
 #pragma omp parallel for schedule(dynamic, 64)
   for (size_t i = 0; i < cand.size(); i++) {
@@ -565,21 +601,8 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
     cand[i].lo = (uint32_t)lo;
     cand[i].hi = (uint32_t)hi;
   }
-  // the write records and their bytes, laid out per lane (prefix sums) and
-  // filled on all host threads into a pinned buffer: one DMA to the device
-  const size_t nl = lanes.size();
-  std::vector<uint64_t> roff(nl + 1, 0), boff(nl + 1, 0);
-  for (size_t i = 0; i < nl; i++) {
-    const LaneView &v = views_[lanes[i]];
-    uint64_t r = 0, b = 0;
-    for (const LaneView::Logged &w : v.wlog)
-      if (w.len) {
-        r++;
-        b += w.len;
-      }
-    roff[i + 1] = roff[i] + r;
-    boff[i + 1] = boff[i] + b;
-  }
+  // the write records and their bytes, laid out per lane and filled on all
+  // host threads into a pinned buffer: one DMA to the device
   uint64_t cbytes = 0, crecs = 0;
   for (const Cand &c : cand)
     if (c.lo != c.hi) {
@@ -596,7 +619,7 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
     if (wtfgpu_host_alloc(ctx_, wpin_cap_, &p)) return WTFGPU_ERR_OOM;
     wpin_ = (uint8_t *)p;
   }
-#pragma omp parallel for schedule(static, 256) if (nl >= 1024)
+#pragma omp parallel for schedule(static, 256) if (par)
   for (size_t i = 0; i < nl; i++) {
     const uint32_t l = lanes[i];
     LaneView &v = views_[l];
@@ -627,11 +650,17 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
     }
   }
   stats_.staged_pages += cand.size();
-  for (uint32_t l : lanes) drop_staged(views_[l]);
+  if (!cand.empty())
+    for (uint32_t l : lanes) drop_staged(views_[l]);
   int rc = WTFGPU_OK;
+  const auto tr = Clock::now();
+  stats_.up_prep_ms += std::chrono::duration<double, std::milli>(tr - tp).count();
   if (!rl.empty()) rc = wtfgpu_write_gprs_list(ctx_, rl.data(), (uint32_t)rl.size(), regs.data());
+  const auto ta = Clock::now();
+  stats_.up_regs_ms += std::chrono::duration<double, std::milli>(ta - tr).count();
   if (!rc && !writes.empty())
     rc = wtfgpu_apply_phys_writes(ctx_, writes.data(), (uint32_t)writes.size(), wpin_, total, nullptr);
+  stats_.up_apply_ms += ms_since(ta);
   return rc;
 }
 
@@ -1281,6 +1310,7 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
   if (Taken) *Taken = fresh.size();
   if (!fresh.empty()) {
     if (wtfgpu_restore_lanes(ctx_, fresh.data(), (uint32_t)fresh.size())) return false;
+    stats_.restore_dev_ms += ms_since(ti);
 #pragma omp parallel for schedule(static)
     for (size_t i = 0; i < fresh.size(); i++) {
       const uint32_t l = fresh[i];
@@ -1300,6 +1330,7 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
     stats_.module_ms += std::chrono::duration<double, std::milli>(tu - tm).count();
     if (flush_lanes(fresh)) return false;
     if (feed_action_) {
+      const auto tf = Clock::now();
       const size_t n = fresh.size();
       std::vector<uint64_t> off(n + 1, 0);
       std::vector<uint8_t> has(n);
@@ -1324,6 +1355,7 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
       }
       if (wtfgpu_set_feed_lanes(ctx_, fresh.data(), (uint32_t)n, off.data(), has.data(), P.pin, off[n]))
         return false;
+      stats_.up_feed_ms += ms_since(tf);
     }
     if (!stop_prestopped(fresh)) return false;
     stats_.upload_ms += ms_since(tu);
@@ -1427,6 +1459,10 @@ std::string GpuBackend_t::StatsJson() const {
            (unsigned long long)stats_.last_unimpl_op.load(), (unsigned long long)stats_.last_unimpl_rip.load());
   std::string r(b);
   r.pop_back();
+  snprintf(b, sizeof(b), ",\"up_prep_ms\":%.3f,\"up_regs_ms\":%.3f,\"up_apply_ms\":%.3f,\"up_feed_ms\":%.3f,"
+           "\"restore_dev_ms\":%.3f", stats_.up_prep_ms, stats_.up_regs_ms, stats_.up_apply_ms, stats_.up_feed_ms,
+           stats_.restore_dev_ms);
+  r += b;
   r += ",\"fetch_by_bp\":{";
   bool first = true;
   for (const auto &[bp, n] : fetch_by_bp_) {

@@ -43,6 +43,9 @@ struct BatchStats {
   // insert_ms split: device restore + host views, module InsertTestcase calls,
   // register / memory / feed uploads
   double restore_ms = 0, module_ms = 0, upload_ms = 0;
+  // upload split: write-record preparation on the host, register upload,
+  // memory-write apply, feed upload; device restore within restore_ms
+  double up_prep_ms = 0, up_regs_ms = 0, up_apply_ms = 0, up_feed_ms = 0, restore_dev_ms = 0;
   // streaming harvest split: per-lane byte counters, coverage logs, attribution
   double bytes_ms = 0, covlog_ms = 0, attrib_ms = 0;
   uint64_t cov_entries = 0;  // (lane, rip) new-coverage log entries collected

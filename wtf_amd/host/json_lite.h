@@ -34,6 +34,16 @@ struct Value {
     if (!v) throw std::runtime_error("json: missing key " + k);
     return *v;
   }
+  // nlohmann's get<unsigned integer>: numbers (cast) and booleans, nothing else
+  uint64_t num_u64() const {
+    if (kind == Number) return str.empty() ? (uint64_t)num : (uint64_t)std::strtoull(str.c_str(), nullptr, 10);
+    if (kind == Bool) return b ? 1 : 0;
+    throw std::runtime_error("json: not a number");
+  }
+  const std::vector<Value> &array() const {
+    if (kind != Array) throw std::runtime_error("json: not an array");
+    return arr;
+  }
   // integer view: numbers (exact when written as integers) or "0x.." strings
   uint64_t u64() const {
     if (kind == Number) return str.empty() ? (uint64_t)num : (uint64_t)std::strtoull(str.c_str(), nullptr, 0);
@@ -157,11 +167,29 @@ class Parser {
       p_ += 4;
       return v;
     }
+    // RFC 8259 number: -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]+)? (nlohmann's
+    // lexer rejects anything else, leading zeros included)
     const char *s = p_;
-    while (p_ < e_ && (std::isdigit((unsigned char)*p_) || *p_ == '-' || *p_ == '+' || *p_ == '.' || *p_ == 'e' ||
-                       *p_ == 'E'))
+    auto digits = [&]() {
+      const char *d = p_;
+      while (p_ < e_ && std::isdigit((unsigned char)*p_)) p_++;
+      return p_ > d;
+    };
+    if (p_ < e_ && *p_ == '-') p_++;
+    if (p_ < e_ && *p_ == '0') {
       p_++;
-    if (s == p_) fail("bad value");
+    } else if (!digits()) {
+      fail("bad value");
+    }
+    if (p_ < e_ && *p_ == '.') {
+      p_++;
+      if (!digits()) fail("bad number");
+    }
+    if (p_ < e_ && (*p_ == 'e' || *p_ == 'E')) {
+      p_++;
+      if (p_ < e_ && (*p_ == '+' || *p_ == '-')) p_++;
+      if (!digits()) fail("bad number");
+    }
     v.kind = Value::Number;
     v.str.assign(s, p_);
     v.num = std::strtod(v.str.c_str(), nullptr);
@@ -175,6 +203,7 @@ class Parser {
   Value parse() {
     Value v = value();
     ws();
+    if (p_ != e_) fail("trailing characters");
     return v;
   }
 };

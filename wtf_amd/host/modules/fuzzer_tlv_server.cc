@@ -56,7 +56,7 @@ struct Cursor {
     const char *s = p;
     v = 0;
     while (p < e && *p >= '0' && *p <= '9' && p - s < 19) v = v * 10 + uint64_t(*p++ - '0');
-    return p > s && (p == e || *p < '0' || *p > '9');
+    return p > s && (p == e || *p < '0' || *p > '9') && !(*s == '0' && p - s > 1);
   }
 };
 }  // namespace
@@ -111,12 +111,12 @@ bool Deserialize(const uint8_t *Buffer, const size_t BufferSize, std::vector<Pac
   Out.clear();
   try {
     const jsonl::Value Root = jsonl::parse(Buffer, BufferSize);
-    for (const jsonl::Value &P : Root.at("Packets").arr) {
+    for (const jsonl::Value &P : Root.at("Packets").array()) {
       Packet_t Pk;
-      Pk.Command = (uint32_t)P.at("Command").u64();
-      Pk.Id = (uint16_t)P.at("Id").u64();
-      Pk.BodySize = (uint16_t)P.at("BodySize").u64();
-      for (const jsonl::Value &B : P.at("Body").arr) Pk.Body.push_back((uint8_t)B.u64());
+      Pk.Command = (uint32_t)P.at("Command").num_u64();
+      Pk.Id = (uint16_t)P.at("Id").num_u64();
+      Pk.BodySize = (uint16_t)P.at("BodySize").num_u64();
+      for (const jsonl::Value &B : P.at("Body").array()) Pk.Body.push_back((uint8_t)B.num_u64());
       Out.push_back(std::move(Pk));
     }
   } catch (const std::exception &) {
@@ -158,14 +158,125 @@ thread_local struct {
 } GlobalState;
 WTF_LANE_STATE_TLS(GlobalState);
 
-bool InsertTestcase(const uint8_t *Buffer, const size_t BufferSize) {
-  GlobalState.Packets.clear();
-  std::vector<Packet_t> Packets;
+// FastDeserialize's grammar, written straight into the Feed layout
+// InsertTestcase hands the backend (per packet: u32 Size, u32 Command, u16 Id,
+// u16 BodySize, Body): no Packet_t vectors. Same acceptance and the same bytes
+// as FastDeserialize + the loop in InsertTestcase; false -> that path decides.
+// `Out` must hold BufferSize bytes (a packet takes at least as many JSON
+// characters as Feed bytes).
+namespace {
+inline bool Lit(const char *&p, const char *e, const char *s, size_t n) {
+  if ((size_t)(e - p) < n || memcmp(p, s, n)) return false;
+  p += n;
+  return true;
+}
+// JSON forbids leading zeros ("007"): such a number goes to the general parser
+inline bool Num(const char *&p, const char *e, uint64_t &v) {
+  const char *s = p;
+  v = 0;
+  while (p < e && (unsigned)(*p - '0') < 10 && p - s < 19) v = v * 10 + uint64_t(*p++ - '0');
+  return p > s && (p == e || (unsigned)(*p - '0') >= 10) && !(*s == '0' && p - s > 1);
+}
+}  // namespace
+
+bool FastFeed(const uint8_t *Buffer, const size_t BufferSize, uint8_t *Out, size_t &OutSize) {
+  const char *p = (const char *)Buffer, *e = p + BufferSize;
+  uint8_t *o = Out;
+  if (!Lit(p, e, "{\"Packets\":[", 12)) return false;
+  if (Lit(p, e, "]}", 2)) {
+    OutSize = 0;
+    return p == e;
+  }
+  for (;;) {
+    if (!Lit(p, e, "{", 1)) return false;
+    uint8_t *h = o;  // header, filled once the packet is closed
+    uint8_t *be = o + 12;
+    uint32_t Command = 0;
+    uint16_t Id = 0, BodySize = 0;
+    unsigned seen = 0;
+    for (;;) {
+      uint64_t v;
+      if (Lit(p, e, "\"Body\":[", 8)) {
+        if (seen & 1) return false;
+        seen |= 1;
+        if (!Lit(p, e, "]", 1)) {
+          for (;;) {
+            // 1-3 digits and a separator (the usual byte): no general number loop
+            if (e - p >= 4 && (unsigned)(p[0] - '0') < 10) {
+              const unsigned d0 = (unsigned)(p[0] - '0'), d1 = (unsigned)(p[1] - '0');
+              unsigned n = 1, x = d0;
+              if (d1 < 10) {
+                if (d0 == 0) return false;
+                const unsigned d2 = (unsigned)(p[2] - '0');
+                x = x * 10 + d1, n = 2;
+                if (d2 < 10) x = x * 10 + d2, n = 3;
+              }
+              if ((unsigned)(p[n] - '0') >= 10) {
+                p += n;
+                v = x;
+              } else if (!Num(p, e, v)) {
+                return false;
+              }
+            } else if (!Num(p, e, v)) {
+              return false;
+            }
+            *be++ = (uint8_t)v;
+            if (p < e && *p == ',') {
+              p++;
+              continue;
+            }
+            if (p < e && *p == ']') {
+              p++;
+              break;
+            }
+            return false;
+          }
+        }
+      } else if (Lit(p, e, "\"BodySize\":", 11)) {
+        if ((seen & 2) || !Num(p, e, v)) return false;
+        seen |= 2, BodySize = (uint16_t)v;
+      } else if (Lit(p, e, "\"Command\":", 10)) {
+        if ((seen & 4) || !Num(p, e, v)) return false;
+        seen |= 4, Command = (uint32_t)v;
+      } else if (Lit(p, e, "\"Id\":", 5)) {
+        if ((seen & 8) || !Num(p, e, v)) return false;
+        seen |= 8, Id = (uint16_t)v;
+      } else {
+        return false;
+      }
+      if (Lit(p, e, "}", 1)) break;
+      if (!Lit(p, e, ",", 1)) return false;
+    }
+    if (seen != 15) return false;
+    const uint32_t Size = uint32_t(8 + (be - (o + 12)));
+    memcpy(h, &Size, 4);
+    memcpy(h + 4, &Command, 4);
+    memcpy(h + 8, &Id, 2);
+    memcpy(h + 10, &BodySize, 2);
+    o = be;
+    if (Lit(p, e, "]}", 2)) {
+      OutSize = (size_t)(o - Out);
+      return p == e;
+    }
+    if (!Lit(p, e, ",", 1)) return false;
+  }
+}
+
+// The Feed of a testcase (the packets InsertTestcase queues, as the chunks
+// OnProcessPacket writes: u32 Size, u32 Command, u16 Id, u16 BodySize, Body),
+// canonical JSON parsed straight into it; `Packets` is filled only when the
+// general parser ran. false: the testcase does not deserialize.
+bool TestcaseFeed(const uint8_t *Buffer, const size_t BufferSize, std::vector<uint8_t> &Feed,
+                  std::vector<Packet_t> &Packets) {
+  Packets.clear();
+  Feed.resize(BufferSize + 16);
+  size_t FeedSize = 0;
+  if (FastFeed(Buffer, BufferSize, Feed.data(), FeedSize)) {
+    Feed.resize(FeedSize);
+    return true;
+  }
+  Feed.clear();
   if (!Deserialize(Buffer, BufferSize, Packets)) return false;
-  // the same packets as Feed chunks (Command, Id, BodySize, Body: the bytes
-  // OnProcessPacket writes); a backend that takes them serves ProcessPacket
-  // itself, the deque then stays unused
-  std::vector<uint8_t> Feed;
   for (const Packet_t &P : Packets) {
     const uint32_t Size = uint32_t(sizeof(P.Command) + sizeof(P.Id) + sizeof(P.BodySize) + P.Body.size());
     const size_t At = Feed.size();
@@ -177,9 +288,24 @@ bool InsertTestcase(const uint8_t *Buffer, const size_t BufferSize) {
     memcpy(Q + 10, &P.BodySize, 2);
     if (!P.Body.empty()) memcpy(Q + 12, P.Body.data(), P.Body.size());
   }
+  return true;
+}
+
+// TestcaseFeed without the packets (oracle/hostcheck.cc tlv-feed)
+bool TestcaseFeedBytes(const uint8_t *Buffer, const size_t BufferSize, std::vector<uint8_t> &Feed) {
+  std::vector<Packet_t> Packets;
+  return TestcaseFeed(Buffer, BufferSize, Feed, Packets);
+}
+
+bool InsertTestcase(const uint8_t *Buffer, const size_t BufferSize) {
+  GlobalState.Packets.clear();
+  thread_local std::vector<uint8_t> Feed;
+  std::vector<Packet_t> Packets;
+  if (!TestcaseFeed(Buffer, BufferSize, Feed, Packets)) return false;
   // a backend that serves ProcessPacket from the feed never runs the handler
   // for this testcase: the queue stays empty
   if (g_Backend->SetFeed(Feed.data(), Feed.size())) return true;
+  if (Packets.empty() && !Deserialize(Buffer, BufferSize, Packets)) return false;  // the fast path kept none
   for (Packet_t &P : Packets) GlobalState.Packets.emplace_back(std::move(P));
   return true;
 }

@@ -590,10 +590,19 @@ bool FuzzSession::StreamStep() {
   S_.produce_wait_ms += std::chrono::duration<double, std::milli>(ta - tw).count();
   if (!ok) return false;
   S_.batches++;
-  for (StreamResult_t &F : Out) {
+  for (const StreamResult_t &F : Out)
     if (F.tag >= Slot_.size()) return false;
+  // crash names already seen, looked up on all host threads (read-only) so
+  // that the serial bookkeeping below only hashes the new ones
+  std::vector<uint8_t> Known(Out.size(), 0);
+#pragma omp parallel for schedule(static, 512) if (Out.size() >= 4096)
+  for (size_t i = 0; i < Out.size(); i++)
+    if (const Crash_t *C = std::get_if<Crash_t>(&Out[i].r.result))
+      Known[i] = !Out[i].r.error && CrashNames_.count(C->CrashName) != 0;
+  for (size_t i = 0; i < Out.size(); i++) {
+    StreamResult_t &F = Out[i];
     const TcRef R = Slot_[F.tag];
-    Account(R.data(), R.size(), F.r);
+    Account(R.data(), R.size(), F.r, Known[i]);
     if (--R.A->Live == 0) Arenas_.erase(R.A);  // every testcase of the arena accounted
     Slot_[F.tag] = TcRef{};
     FreeSlot_.push_back(F.tag);
@@ -606,7 +615,7 @@ bool FuzzSession::StreamStep() {
 }
 
 // The master's bookkeeping of one result (server.h:816-886).
-void FuzzSession::Account(const uint8_t *Tc, size_t Size, const LaneResult &L) {
+void FuzzSession::Account(const uint8_t *Tc, size_t Size, const LaneResult &L, bool KnownCrash) {
   S_.execs++;
   S_.retired += L.icount;
   if (L.error) {  // the engine could not finish it: neither a crash nor coverage
@@ -624,7 +633,7 @@ void FuzzSession::Account(const uint8_t *Tc, size_t Size, const LaneResult &L) {
   if (std::holds_alternative<Cr3Change_t>(L.result)) S_.cr3++;
   if (const Crash_t *C = std::get_if<Crash_t>(&L.result)) {
     S_.crashes++;
-    if (!C->CrashName.empty() && CrashNames_.insert(C->CrashName).second)
+    if (!KnownCrash && !C->CrashName.empty() && CrashNames_.insert(C->CrashName).second)
       SaveFile(T_ / "crashes" / C->CrashName, Tc, Size);
   }
   // a timed-out testcase reports no coverage (the client revokes it,

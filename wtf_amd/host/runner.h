@@ -203,7 +203,7 @@ class FuzzSession {
   bool More(uint64_t done) const;
   bool MergeCoverage();
   bool StreamStep();
-  void Account(const uint8_t *Tc, size_t Size, const LaneResult &L);
+  void Account(const uint8_t *Tc, size_t Size, const LaneResult &L, bool KnownCrash = false);
 
   const RunnerOptions O_;
   Executor_t &Exec_;
