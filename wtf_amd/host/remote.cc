@@ -128,6 +128,7 @@ int MasterMain(const RunnerOptions &O) {
       printf("a node failed\n");
       return 1;
     }
+  F.FlushFiles();
   printf("%s\n", F.SummaryJson().c_str());
   return 0;  // the node sockets close with Exec: the nodes' loops end
 }

@@ -357,8 +357,50 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
       return 1;
     }
   }
+  F.FlushFiles();
   printf("%s\n", F.SummaryJson().c_str());
   return 0;
+}
+
+// ------------------------------------------------------------------ FileWriter
+FileWriter::FileWriter() : Th_([this] { Loop(); }) {}
+
+FileWriter::~FileWriter() {
+  {
+    std::lock_guard<std::mutex> g(Mu_);
+    Stop_ = true;
+  }
+  Cv_.notify_all();
+  Th_.join();
+}
+
+void FileWriter::Save(std::filesystem::path Path, const uint8_t *Data, size_t Size) {
+  {
+    std::lock_guard<std::mutex> g(Mu_);
+    Q_.emplace_back(std::move(Path), std::vector<uint8_t>(Data, Data + Size));
+  }
+  Cv_.notify_one();
+}
+
+void FileWriter::Flush() {
+  std::unique_lock<std::mutex> g(Mu_);
+  Idle_.wait(g, [this] { return Q_.empty() && !Busy_; });
+}
+
+void FileWriter::Loop() {
+  std::unique_lock<std::mutex> g(Mu_);
+  for (;;) {
+    Cv_.wait(g, [this] { return Stop_ || !Q_.empty(); });
+    if (Q_.empty()) return;  // stopping with nothing left
+    auto F = std::move(Q_.front());
+    Q_.pop_front();
+    Busy_ = true;
+    g.unlock();
+    SaveFile(F.first, F.second.data(), F.second.size());
+    g.lock();
+    Busy_ = false;
+    if (Q_.empty()) Idle_.notify_all();
+  }
 }
 
 // ------------------------------------------------------------------ FuzzSession
@@ -369,6 +411,7 @@ FuzzSession::FuzzSession(const RunnerOptions &O, Executor_t &Exec, Target_t &Tar
 
 FuzzSession::~FuzzSession() {
   if (Next_.valid()) Next_.wait();
+  Writer_.Flush();
 }
 
 bool FuzzSession::Start() {
@@ -634,7 +677,7 @@ void FuzzSession::Account(const uint8_t *Tc, size_t Size, const LaneResult &L, b
   if (const Crash_t *C = std::get_if<Crash_t>(&L.result)) {
     S_.crashes++;
     if (!KnownCrash && !C->CrashName.empty() && CrashNames_.insert(C->CrashName).second)
-      SaveFile(T_ / "crashes" / C->CrashName, Tc, Size);
+      Writer_.Save(T_ / "crashes" / C->CrashName, Tc, Size);
   }
   // a timed-out testcase reports no coverage (the client revokes it,
   // client.cc:122-133); any other result with new coverage, crashes

@@ -5,6 +5,10 @@
 // batched N testcases per executor call.
 #pragma once
 #include <chrono>
+#include <condition_variable>
+#include <filesystem>
+#include <mutex>
+#include <thread>
 #include <cstdint>
 #include <deque>
 #include <unordered_map>
@@ -183,6 +187,25 @@ struct TcRef {
 // executor N testcases at a time (client.cc:187-258, batched). With a
 // CoverageExchange_t of world > 1, shard r mutates with seed + r and merges
 // coverage maps after every batch.
+// Saves files on a background thread in the order given (the master's
+// crashes/ writes, server.h:839-847: off the bookkeeping thread; flushed
+// before the session ends).
+class FileWriter {
+ public:
+  FileWriter();
+  ~FileWriter();
+  void Save(std::filesystem::path Path, const uint8_t *Data, size_t Size);
+  void Flush();
+
+ private:
+  void Loop();
+  std::mutex Mu_;
+  std::condition_variable Cv_, Idle_;
+  std::deque<std::pair<std::filesystem::path, std::vector<uint8_t>>> Q_;
+  bool Stop_ = false, Busy_ = false;
+  std::thread Th_;
+};
+
 class FuzzSession {
  public:
   FuzzSession(const RunnerOptions &O, Executor_t &Exec, Target_t &Target, ModuleSlots &Slots,
@@ -195,6 +218,7 @@ class FuzzSession {
   size_t CorpusSize() const { return Corpus_.Size(); }
   double WallSeconds() const;
   std::string SummaryJson() const;
+  void FlushFiles() { Writer_.Flush(); }  // crash files written so far are on disk
 
  private:
   TcBatch MakeBatch(uint64_t n);
@@ -220,6 +244,7 @@ class FuzzSession {
   std::string LastNewCov_;  // the testcase last passed to Mutator_->OnNewCoverage
   bool HaveNewCov_ = false;
   std::future<TcBatch> Next_;
+  FileWriter Writer_;
   std::unordered_set<std::string> CrashNames_;
   std::unordered_set<uint64_t> Coverage_;  // the master's aggregate (server.h:816-854)
   FuzzStats S_;
