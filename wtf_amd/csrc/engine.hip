@@ -253,9 +253,10 @@ __device__ __forceinline__ void fetch_bytes(u64 pageptr, u32 off, u32 n, u64 &lo
 // already in the aggregate coverage map, and the lanes this wave has already
 // logged for it in this launch.
 #ifndef WTFGPU_UC_N
-#define WTFGPU_UC_N 64  // 128 (with a packed UOp) measured: no tlv gain, SYN k_run +3 %
+#define WTFGPU_UC_N 256  // head-only entries (the UOp lives in the uop slots below)
 #endif
 constexpr u32 UC_N = WTFGPU_UC_N;  // entries per wave (power of two)
+constexpr u32 UC_U = 8;            // uop slots per wave (power of two)
 constexpr u32 UC_BP = 1, UC_COVERED = 2, UC_CROSS = 4, UC_BADLEN = 8, UC_UNSUP = 16;
 struct UCHead {
   u64 key;
@@ -263,6 +264,8 @@ struct UCHead {
   u32 flags, pad;
   FOp f;
 };
+// What the fast loop reads: one LDS entry per cached rip (64 bytes, so a wave
+// keeps UC_N of them within the CU's LDS budget at two blocks per CU).
 struct UCEntry {
   union {
     UCHead h;
@@ -273,11 +276,34 @@ struct UCEntry {
       FOp f;
     };
   };
+  u64 rip;  // the rip that filled it (a warm image re-checks UC_COVERED with it)
+};
+// The decoded UOp, which only the slow step's generic exec needs: a few
+// slots per wave, refilled from the shared cache (or decoded) on demand.
+struct UCUop {
+  u64 key;
   UOp u;
 };
+// The shared (device-wide) cache's payload: static flags, FOp, UOp.
+struct GPayload {
+  u32 flags, pad;
+  FOp f;
+  UOp u;
+};
+constexpr u32 GP_HEAD = (sizeof(u32) * 2 + sizeof(FOp)) / 4;  // dwords of flags, pad, FOp
 static_assert(sizeof(UOp) % 4 == 0 && sizeof(FOp) % 4 == 0, "copied as dwords");
+static_assert(sizeof(UCEntry) == 64, "LDS entry size");
+// Warm start: at the end of a launch, hardware waves 0..UC_IMAGES-1 store their
+// LDS uop cache as an image; at the start of the next launch on the same
+// queue, wave w loads image w % UC_IMAGES (logged masks cleared, UC_COVERED
+// re-checked against the coverage map) instead of starting empty. UC_COVERED
+// stays true until the coverage map is reset; images are dropped with the
+// shared cache (pool, breakpoints, edges / trace) and on a coverage reset.
+constexpr u32 UC_IMAGES = 64, UC_QUEUES = 8;
+constexpr u64 UC_IMAGE_SET = (u64)UC_IMAGES * UC_N * sizeof(UCEntry);  // bytes per queue
 
 __device__ __forceinline__ u32 uc_slot(u64 key) { return (u32)((key ^ (key >> 12) * 0x9E3779B1u) & (UC_N - 1)); }
+__device__ __forceinline__ u32 uu_slot(u64 key) { return (u32)((key ^ (key >> 12) * 0x9E3779B1u) & (UC_U - 1)); }
 
 template <typename T>
 __device__ __forceinline__ void lds_uniform_read(const T *src, T &dst) {
@@ -421,7 +447,7 @@ __device__ __noinline__ bool deliver_fault(const Dev &P, Lane &L) {
 }
 
 constexpr u32 GUC_WORDS = 48;                                  // 3 lines x 16 dwords
-constexpr u32 GUC_PAYLOAD = (sizeof(UCEntry) - offsetof(UCEntry, flags)) / 4;  // flags .. UOp
+constexpr u32 GUC_PAYLOAD = sizeof(GPayload) / 4;  // flags, pad, FOp, UOp
 static_assert(GUC_PAYLOAD <= 3 * 14, "global uop cache entry: 3 lines of 14 payload dwords");
 __device__ __forceinline__ u32 guc_slot(const Dev &P, u64 key) {
   return (u32)(mix64(key) & P.guc_mask);
@@ -444,9 +470,34 @@ __device__ __forceinline__ u32 covered_flag(const Dev &P, u64 rip, u32 off) {
   return 0;
 }
 
-__device__ __noinline__ void uc_fill(const Dev &P, UCEntry *e, u64 key, u64 lptr, u32 off, u64 rip, u32 lid) {
+// The same per lane (non-uniform rips: a warm image's entries).
+__device__ __forceinline__ u32 covered_flag_lane(const Dev &P, u64 rip, u32 off) {
+  if (!P.code_keys) return 0;
+  u32 h = (u32)mix64(rip >> 12) & P.code_mask;
+  for (u32 i = 0; i <= P.code_mask; i++) {
+    const u64 k = P.code_keys[h];
+    if (k == (rip >> 12)) return P.cov_map[(u64)P.code_slot[h] * WTFGPU_PAGE_SIZE + off] ? UC_COVERED : 0;
+    if (k == EMPTY_KEY) return 0;
+    h = (h + 1) & P.code_mask;
+  }
+  return 0;
+}
+
+// The FOp of an instruction that always runs in the slow step (its length kept).
+__device__ __forceinline__ FOp generic_fop(const UOp &d) {
+  FOp f{};
+  f.w0 = (d.len & 0x3f) << 20;
+  return f;
+}
+
+// Fill one entry (uniform): from the shared cache when it holds the key, else
+// fetch + decode from the pool page, digest, lookups, and publish. The head
+// goes to `e` (when given), the UOp to the uop slot `us`.
+__device__ __noinline__ void uc_fill(const Dev &P, UCEntry *e, UCUop *us, u64 key, u64 lptr, u32 off, u64 rip,
+                                     u32 lid) {
   u32 *gw = nullptr;
   const u32 pj = guc_payload_index(lid);
+  u32 *head = e ? (u32 *)&e->flags : nullptr, *uop = (u32 *)&us->u;
   if (P.guc) {
     // the shared cache first: one dword per lane, the six tag dwords checked
     gw = P.guc + (u64)guc_slot(P, key) * GUC_WORDS;
@@ -454,14 +505,21 @@ __device__ __noinline__ void uc_fill(const Dev &P, UCEntry *e, u64 key, u64 lptr
     const bool tag = lid < GUC_WORDS && (lid & 15) >= 14;
     const bool bad = tag && w != ((lid & 1) ? (u32)(key >> 32) : (u32)key);
     if (__ballot(bad) == 0) {
-      u32 *dst = (u32 *)&e->flags;
-      if (pj < GUC_PAYLOAD) dst[pj] = w;
-      const u32 flags = __builtin_amdgcn_readlane(w, 0) | covered_flag(P, rip, off);
+      if (pj < GP_HEAD) {
+        if (head) head[pj] = w;
+      } else if (pj < GUC_PAYLOAD) {
+        uop[pj - GP_HEAD] = w;
+      }
+      const u32 flags = __builtin_amdgcn_readlane(w, 0) | (e ? covered_flag(P, rip, off) : 0);
       __builtin_amdgcn_wave_barrier();
       if (lid == 0) {
-        e->logged = 0;
-        e->flags = flags;
-        e->key = key;
+        us->key = key;
+        if (e) {
+          e->logged = 0;
+          e->flags = flags;
+          e->rip = rip;
+          e->key = key;
+        }
       }
       return;
     }
@@ -475,33 +533,41 @@ __device__ __noinline__ void uc_fill(const Dev &P, UCEntry *e, u64 key, u64 lptr
   FOp f;
   if (dr == 0) {
     digest(d, f);
-    if (P.edges && edge_op(d.op, d.bsrc)) f = FOp{};  // branches whose edge is recorded run in the slow step
-    if (P.trace) f = FOp{};                           // traced lanes log every rip in the slow step
+    if (P.edges && edge_op(d.op, d.bsrc)) f = generic_fop(d);  // branches whose edge is recorded run in the slow step
+    if (P.trace) f = generic_fop(d);                           // traced lanes log every rip in the slow step
     if (!d.supported) flags |= UC_UNSUP;
     if (bp_lookup(P, rip)) flags |= UC_BP;
   } else {
     f = FOp{};
   }
-  const u32 dyn = dr == 0 ? covered_flag(P, rip, off) : 0;
+  const u32 dyn = (dr == 0 && e) ? covered_flag(P, rip, off) : 0;
   if (lid == 0) {
-    e->logged = 0;
-    e->flags = flags;  // the static flags first: the shared copy is taken from here
-    e->f = f;
-    e->u = d;
+    us->u = d;
+    us->key = key;
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   if (gw) {  // publish (static flags only); one coalesced store of 3 tagged lines
-    const u32 *src = (const u32 *)&e->flags;
     u32 v = 0;
-    if (pj < GUC_PAYLOAD) v = src[pj];
+    if (pj < GP_HEAD) v = pj == 0 ? flags : pj == 1 ? 0u : ((const u32 *)&f)[pj - 2];
+    else if (pj < GUC_PAYLOAD) v = uop[pj - GP_HEAD];
     else if (lid < GUC_WORDS && (lid & 15) >= 14) v = (lid & 1) ? (u32)(key >> 32) : (u32)key;
     if (lid < GUC_WORDS) gw[lid] = v;
   }
-  if (lid == 0) {
+  if (lid == 0 && e) {
+    e->logged = 0;
+    e->f = f;
     e->flags = flags | dyn;
+    e->rip = rip;
     e->key = key;
   }
+}
+
+// The UOp of `key` in the wave's uop slots (the slow step's generic path).
+__device__ __forceinline__ const UOp *uc_uop(const Dev &P, UCUop *uu, u64 key, u64 lptr, u32 off, u64 rip, u32 lid) {
+  UCUop *us = &uu[uu_slot(key)];
+  if (rfl64(us->key) != key) uc_fill(P, nullptr, us, key, lptr, off, rip, lid);
+  return &us->u;
 }
 
 // Instruction-page translation for lanes whose code-page cache missed.
@@ -829,9 +895,17 @@ __device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr
     stamp_[k] += t_ - tprev_;                      \
     tprev_ = t_;                                   \
   } while (0)
+// why the fast loop handed the wave to the slow step, counted in stat[12..15]:
+// 0 a fast attempt missed (TLB, first write, page crossing, state), 1 the
+// code page changed, 2 the rip is not in the wave's LDS uop cache, 3 other
+// (generic op, breakpoint, coverage, code outside the pool)
+#define WHY(k) why_ = (k)
 #else
 #define STAMP(k) \
   do {           \
+  } while (0)
+#define WHY(k) \
+  do {         \
   } while (0)
 #endif
 
@@ -867,8 +941,24 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
   // host): it is neither loaded nor stored
   const bool valid = inrange && P.status[lane] == WTFGPU_RUNNING;
   __shared__ UCEntry sUC[4][UC_N];
+  __shared__ UCUop sUU[4][UC_U];
   UCEntry *uc = sUC[threadIdx.x >> 6];
-  for (u32 i = lid; i < UC_N; i += 64) uc[i].key = EMPTY_KEY;
+  UCUop *uu = sUU[threadIdx.x >> 6];
+  // the LDS uop cache: the warm image of an earlier launch, or empty
+  const bool wave_live = __ballot(valid) != 0;
+  const UCEntry *img = (P.warm && wave_live) ? (const UCEntry *)P.warm + (u64)(hw % UC_IMAGES) * UC_N : nullptr;
+  if (img) {
+    for (u32 i = lid; i < UC_N; i += 64) {
+      UCEntry t = img[i];
+      t.logged = 0;
+      if (P.cov_rip && t.key != EMPTY_KEY && !(t.flags & (UC_COVERED | UC_CROSS | UC_BADLEN)))
+        t.flags |= covered_flag_lane(P, t.rip, (u32)(t.rip & 0xfff));
+      uc[i] = t;
+    }
+  } else {
+    for (u32 i = lid; i < UC_N; i += 64) uc[i].key = EMPTY_KEY;
+  }
+  if (lid < UC_U) uu[lid].key = EMPTY_KEY;
   u32 glo[16], ghi[16];
   Lane L;
   L.glo = glo;
@@ -889,6 +979,8 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
 #ifdef WTFGPU_STAMPS
   u64 stamp_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u64 tprev_ = __builtin_amdgcn_s_memtime();
+  u64 whyc_[4] = {0, 0, 0, 0};
+  u32 why_ = 3;
 #endif
 
   for (;;) {
@@ -907,7 +999,9 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       if (__ballot(active && L.rip == grip) != am) grip = rfl64(wave_min(active ? L.rip : EMPTY_KEY));
       have = true;
       const bool cand = active && L.rip == grip;
+      WHY(1);
       if (__ballot(cand && (grip >> 12) != L.cvpn)) break;
+      WHY(3);
       const int leader = __ffsll((long long)__ballot(cand)) - 1;
       const u64 lptr = readlane64(L.cptr, leader);
       if (lptr < pool_lo || lptr >= pool_hi) break;
@@ -917,7 +1011,9 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       // one LDS round trip: key, logged mask, flags and the FOp are contiguous
       UCHead h;
       lds_uniform_read(&e->h, h);
+      WHY(2);
       if (h.key != key) break;
+      WHY(3);
       const u32 flags = h.flags;
       if (flags & (UC_BP | UC_CROSS | UC_BADLEN | UC_UNSUP)) break;
       if (P.cov_rip && !(flags & UC_COVERED) && (__ballot(ing) & ~h.logged)) break;
@@ -941,6 +1037,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       }
       // lanes that missed keep their rip: the slow step services them
       if (__ballot(ing && L.miss)) {
+        WHY(0);
         have = true;
         break;
       }
@@ -962,6 +1059,9 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     // fills, page-crossing / overlay code, coverage logging, breakpoints,
     // generic instructions, TLB misses and copy-on-write
     steps++;
+#ifdef WTFGPU_STAMPS
+    whyc_[why_ & 3]++;
+#endif
     const bool active = valid && L.status == WTFGPU_RUNNING;
     bool cand = active && L.rip == grip;
     if (cand && (grip >> 12) != L.cvpn) WITH_LANE_COPY(code_xlate(P, T, grip));
@@ -977,7 +1077,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     UCEntry *e = &uc[uc_slot(key)];
     const bool cacheable = lptr >= pool_lo && lptr < pool_hi;
     if (cacheable && rfl64(e->key) != key) {
-      uc_fill(P, e, key, lptr, off, grip, lid);
+      uc_fill(P, e, &uu[uu_slot(key)], key, lptr, off, grip, lid);
       // an entry the fast loop can run (a common op, nothing to log, no
       // breakpoint): back to it, this pass was only the fill
       const u32 ff = rfl32(e->flags);
@@ -999,7 +1099,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       STAMP(5);
       continue;
     }
-    const u32 len = rfl32(e->u.len);
+    const u32 len = (rfl32(e->f.w0) >> 20) & 0x3f;  // fo_len, read once for the wave
     const u64 gmask = __ballot(ing);
 
     // ---- coverage, then breakpoint (bochscpu_backend.cc:501-547)
@@ -1024,8 +1124,11 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
         skip = false;
       }
     }
+    // the UOp for the generic path (wave-uniform: the slot fill is a wave operation)
+    const UOp *u = nullptr;
+    if (__ballot(ing)) u = uc_uop(P, uu, key, lptr, off, grip, lid);
     if (ing && (flags & UC_UNSUP)) {
-      const u32 ob = e->u.opbytes, n = len;
+      const u32 ob = u->opbytes, n = len;
       L.status = WTFGPU_EXIT_UNIMPLEMENTED;
       L.exop = n >= 4 ? ob : (ob & ((1u << (8 * n)) - 1));
       ing = false;
@@ -1038,22 +1141,28 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       for (int attempt = 0;; attempt++) {
         L.miss = 0;
         L.pend = 0;
-        WITH_LANE_COPY(x = exec_generic(P, T, &e->u, next));
+        WITH_LANE_COPY(x = exec_generic(P, T, u, next));
         if (!L.miss || L.status != WTFGPU_RUNNING) break;
         bool ok;
         WITH_LANE_COPY(ok = miss_service(P, T, attempt));
         if (!ok) break;
       }
       u32 opbytes = 0;
-      if (x == X_UNIMPL) opbytes = e->u.opbytes;
+      if (x == X_UNIMPL) opbytes = u->opbytes;
       retire(P, L, x, len, next, opbytes);
       // RecordEdge (bochscpu_backend.cc:699-728): the branch ran, whatever the retire hook decided
-      if (P.edges && P.cov_rip && x == X_OK && edge_op(rfl32(e->u.op), rfl32(e->u.bsrc)))
+      if (P.edges && P.cov_rip && x == X_OK && edge_op(rfl32(u->op), rfl32(u->bsrc)))
         L.ccnt = cover_edge(P, edge_key(grip, next), true, L.lane, L.cgen, L.ccnt);
     }
     STAMP(1);
   }
 
+  if (P.warm && wave_live && hw < UC_IMAGES) {  // this wave's cache for the next launch
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    UCEntry *out = (UCEntry *)P.warm + (u64)hw * UC_N;
+    for (u32 i = lid; i < UC_N; i += 64) out[i] = uc[i];
+  }
   if (valid) {
     store_lane(P, L);
     store_tlb(P, L);
@@ -1076,6 +1185,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     if (running) atomicAdd((unsigned long long *)&P.stat[2], (unsigned long long)running);
 #ifdef WTFGPU_STAMPS
     for (int k = 0; k < 8; k++) atomicAdd((unsigned long long *)&P.stat[4 + k], (unsigned long long)stamp_[k]);
+    for (int k = 0; k < 4; k++) atomicAdd((unsigned long long *)&P.stat[12 + k], (unsigned long long)whyc_[k]);
 #endif
   }
 }
@@ -1602,6 +1712,7 @@ struct wtfgpu_ctx {
   ExitInfo *d_exinfo = nullptr;
   LaneSys *d_sys = nullptr;
   u32 *d_guc = nullptr;       // device-wide decoded-uop cache (Dev::guc)
+  u8 *d_warm = nullptr;       // LDS uop-cache images, UC_QUEUES sets (Dev::warm)
   u64 *d_rdseed = nullptr;    // per-lane Rdrand seeds (Dev::rd_seed)
   u64 *d_stopargs = nullptr;  // per-lane STOP_ARGS arguments (Dev::stop_args)
   u64 *d_extra = nullptr;     // coverage values outside code pages (Dev::extra_keys)
@@ -1817,10 +1928,20 @@ int h2d(wtfgpu_ctx *c, T *dst, const T *src, u64 n) {
 
 constexpr u32 kExtraEntries = 1u << 20;
 
+// The warm images of every queue dropped (rare: setup-time changes). Every
+// queue is drained first: a launch in flight on another queue reads or
+// writes its set.
+int warm_clear(wtfgpu_ctx *c) {
+  if (!c->d_warm) return WTFGPU_OK;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemset(c->d_warm, 0xff, UC_IMAGE_SET * UC_QUEUES));
+  return WTFGPU_OK;
+}
+
 // Entries depend on the pool pages and the breakpoint set: cleared with them.
 int guc_clear(wtfgpu_ctx *c) {
   if (c->d_guc) HIPCHK(hipMemsetAsync(c->d_guc, 0, (u64)(c->P.guc_mask + 1) * GUC_WORDS * 4, c->stream));
-  return WTFGPU_OK;
+  return warm_clear(c);
 }
 
 }  // namespace
@@ -1928,6 +2049,7 @@ int wtfgpu_destroy(wtfgpu_ctx *c) {
     if (q.stream) (void)hipStreamSynchronize(q.stream);
   free_lanes(c);
   dfree(c->d_guc);
+  if (c->d_warm) (void)hipFree(c->d_warm);
   dfree(c->d_pool);
   dfree(c->d_pfnmap);
   dfree(c->d_ptbits);
@@ -2293,6 +2415,7 @@ int wtfgpu_set_code_pages(wtfgpu_ctx *c, const uint64_t *vpns, uint32_t n) {
   HIPCHK(hipMemsetAsync(c->d_covmap, 0, (u64)n * WTFGPU_PAGE_SIZE, c->stream));
   HIPCHK(hipMemsetAsync(c->d_covshadow, 0, (u64)n * WTFGPU_PAGE_SIZE, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  if (int rc = warm_clear(c)) return rc;  // images carry UC_COVERED
   c->P.cov_shadow = c->d_covshadow;
   c->P.code_keys = c->d_codekeys;
   c->P.code_slot = c->d_codeslot;
@@ -2548,6 +2671,22 @@ static Dev run_params(wtfgpu_ctx *c, bool regroup) {
   Dev Q = c->P;
   Q.perm = regroup ? c->d_perm : nullptr;
   Q.stat = c->d_stat;
+  // warm-started LDS uop caches (WTFGPU_WARM=0: every launch starts empty)
+  const char *w = getenv("WTFGPU_WARM");
+  if (!(w && atoi(w) == 0)) {
+    if (!c->d_warm) {
+      if (hipMalloc((void **)&c->d_warm, UC_IMAGE_SET * UC_QUEUES) != hipSuccess) {
+        c->d_warm = nullptr;
+      } else if (hipMemset(c->d_warm, 0xff, UC_IMAGE_SET * UC_QUEUES) != hipSuccess ||
+                 hipDeviceSynchronize() != hipSuccess) {
+        (void)hipFree(c->d_warm);
+        c->d_warm = nullptr;
+      }
+    }
+    Q.warm = c->d_warm ? c->d_warm + (u64)(c->cur_queue % UC_QUEUES) * UC_IMAGE_SET : nullptr;
+  } else {
+    Q.warm = nullptr;
+  }
   return Q;
 }
 
@@ -2578,9 +2717,10 @@ static void print_stamps(const u64 *s) {
   if (s[0])
     fprintf(stderr,
             "wtfgpu stamps (cycles per wave-step, %llu steps): fast loop %.0f, slow: xlate+fill %.0f, coverage %.0f, "
-            "exec %.0f, cross-page %.0f\n",
+            "exec %.0f, cross-page %.0f; slow steps: miss %llu, codepage %llu, ucmiss %llu, other %llu\n",
             (unsigned long long)s[0], (double)s[4] / s[0], (double)s[6] / s[0], (double)s[7] / s[0],
-            (double)s[5] / s[0], (double)s[9] / s[0]);
+            (double)s[5] / s[0], (double)s[9] / s[0], (unsigned long long)s[12], (unsigned long long)s[13],
+            (unsigned long long)s[14], (unsigned long long)s[15]);
 #else
   (void)s;
 #endif
@@ -3070,7 +3210,7 @@ int wtfgpu_reset_coverage(wtfgpu_ctx *c) {
   HIPCHK(hipMemsetAsync(c->d_covshadow, 0, c->ncovslots * WTFGPU_PAGE_SIZE, c->stream));
   if (c->d_extra) HIPCHK(hipMemsetAsync(c->d_extra, 0xff, (u64)kExtraEntries * 8, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  return WTFGPU_OK;
+  return warm_clear(c);  // images carry UC_COVERED
 }
 
 int wtfgpu_set_trace(wtfgpu_ctx *c, uint32_t per_lane) {

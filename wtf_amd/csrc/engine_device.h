@@ -118,6 +118,7 @@ struct Dev {
   // bytes (a reader takes an entry only when all three tags match)
   u32 *guc;
   u32 guc_mask;
+  u8 *warm;  // k_run: per-wave images of the LDS uop cache carried between launches (null: cold start)
   u64 *rd_seed;           // [nlanes] Rdrand seeds (WTFGPU_BPACT_RDRAND)
   u64 *stop_args;         // [nlanes][6] arguments kept by WTFGPU_BPACT_STOP_ARGS
   // values of the aggregate coverage that are not code bytes of a code page
