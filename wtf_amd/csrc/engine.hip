@@ -600,6 +600,21 @@ __device__ __noinline__ int exec_generic(const Dev &P, Lane &L, const UOp *ul, u
   return exec(P, L, d, L.rip + d.len, next);
 }
 
+// The restartable attempts at one instruction on one lane copy: a TLB miss /
+// first write abandons the attempt, miss_service fills the TLB or copies the
+// page, the attempt reruns.
+__device__ __noinline__ int exec_retry(const Dev &P, Lane &L, const UOp *ul, u64 &next) {
+  int x;
+  for (int attempt = 0;; attempt++) {
+    L.miss = 0;
+    L.pend = 0;
+    x = exec_generic(P, L, ul, next);
+    if (!L.miss || L.status != WTFGPU_RUNNING) break;
+    if (!miss_service(P, L, attempt)) break;
+  }
+  return x;
+}
+
 // Retire / exit bookkeeping after the last attempt at an instruction.
 __device__ __forceinline__ void retire(const Dev &P, Lane &L, int x, u32 len, u64 next, u32 opbytes) {
   if (L.flush) {
@@ -1134,19 +1149,10 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       ing = false;
     }
     if (ing) {
-      // restartable attempts: a TLB miss / first write abandons the attempt,
-      // miss_service fills the TLB or copies the page, the attempt reruns
+      // restartable attempts (exec_retry), all on one copy of the lane
       u64 next = 0;
       int x;
-      for (int attempt = 0;; attempt++) {
-        L.miss = 0;
-        L.pend = 0;
-        WITH_LANE_COPY(x = exec_generic(P, T, u, next));
-        if (!L.miss || L.status != WTFGPU_RUNNING) break;
-        bool ok;
-        WITH_LANE_COPY(ok = miss_service(P, T, attempt));
-        if (!ok) break;
-      }
+      WITH_LANE_COPY(x = exec_retry(P, T, u, next));
       u32 opbytes = 0;
       if (x == X_UNIMPL) opbytes = u->opbytes;
       retire(P, L, x, len, next, opbytes);
