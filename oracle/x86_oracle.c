@@ -2099,6 +2099,13 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
       return X_OK;
     case 0xf4:
       return X_HLT;
+    /* invalid in 64-bit mode: push / pop es cs ss ds, daa das aaa aas, pusha
+     * popa, 82 (alias of 80), far call / jmp, aam aad salc (SDM opcode map, i64) */
+    case 0x06: case 0x07: case 0x0e: case 0x16: case 0x17: case 0x1e: case 0x1f: case 0x27:
+    case 0x2f: case 0x37: case 0x3f: case 0x60: case 0x61: case 0x82: case 0x9a: case 0xd4:
+    case 0xd5: case 0xd6: case 0xea:
+      fault(m, WTFGPU_VEC_UD, 0);
+      return X_FAULT;
     case 0xf5:
       m->r.rflags ^= RF_CF;
       return X_OK;

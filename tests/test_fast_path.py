@@ -247,3 +247,21 @@ def test_copy_loop_program_fast_equals_slow():
         assert fast.status == INT3 and n > 60, (s, d, fast.status, n)
         src = bytes((i * 7 + 3) & 0xFF for i in range(4096))
         assert bytes(fast.win[d:d + 656]) == src[s:s + 656][:512 - d], (s, d)
+
+
+@pytest.mark.parametrize("op", [0x06, 0x07, 0x0E, 0x16, 0x17, 0x1E, 0x1F, 0x27, 0x2F, 0x37, 0x3F, 0x60, 0x61,
+                                0x82, 0x9A, 0xD4, 0xD5, 0xD6, 0xEA])
+def test_opcodes_invalid_in_64bit_mode_raise_ud(op):
+    """SDM opcode map (i64): #UD on the oracle and the engine's code, at the
+    instruction, nothing retired (they were engine errors before)."""
+    L = sim_lib()
+    code = bytes([op, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00])
+    sp, regs = layout(code, BUF, bytes(256))
+    pfns, blob = sp.phys()
+    o = Oracle(pfns=pfns, blob=blob)
+    o.restore(regs)
+    ex = o.step()
+    assert (ex.status, ex.vector) == (EXIT_FAULT, 6), hex(op)
+    for fast in (False, True):
+        out = sim_run(L, sp, regs, fast=fast)
+        assert (out.status, out.vector, out.icount, out.rip) == (EXIT_FAULT, 6, 0, regs.rip), (hex(op), fast)

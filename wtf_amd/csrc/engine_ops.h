@@ -87,6 +87,9 @@ __device__ __forceinline__ u64 segbase(const Dev &P, const Lane &L, u32 seg) {
    ((u32)(ar) << 20) | ((u32)(aw) << 21) | ((u32)(bw) << 22) | ((u32)(m) << 23) | ((u32)(ik) << 24) | \
    ((u32)(grp) << 27))
 #define UN E(O_UNIMPL, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
+// invalid in 64-bit mode (push / pop of es cs ss ds, daa das aaa aas, pusha
+// popa, the 82 alias of 80, far call / jmp, aam aad salc): #UD
+#define UDE E(O_UD, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0)
 enum : u32 { K_NONE = 0, K_B, K_W, K_Z, K_V, K_MOFFS, K_D };
 enum : u32 { G_NONE = 0, G_1, G_2, G_3, G_4, G_5, G_8F, G_C6, G_BA, G_ALU };
 
@@ -96,7 +99,7 @@ enum : u32 { G_NONE = 0, G_1, G_2, G_3, G_4, G_5, G_8F, G_C6, G_BA, G_ALU };
       E(O_ALU, L_GREG, L_RM, Z_B, Z_B, 1, 1, 0, 1, K_NONE, G_ALU),                        \
       E(O_ALU, L_GREG, L_RM, Z_V, Z_V, 1, 1, 0, 1, K_NONE, G_ALU),                        \
       E(O_ALU, L_RAX, L_IMM, Z_B, Z_B, 1, 1, 0, 0, K_B, G_ALU),                           \
-      E(O_ALU, L_RAX, L_IMM, Z_V, Z_V, 1, 1, 0, 0, K_Z, G_ALU), UN, UN
+      E(O_ALU, L_RAX, L_IMM, Z_V, Z_V, 1, 1, 0, 0, K_Z, G_ALU), UDE, UDE
 #define JCC E(O_JCC, 0, L_IMM, 0, Z_Q, 0, 0, 0, 0, K_B, 0)
 #define PUSHR E(O_PUSH, L_PUSH, L_OPREG, Z_STK, Z_STK, 0, 1, 0, 0, K_NONE, 0)
 #define POPR E(O_POP, L_OPREG, L_POP, Z_STK, Z_STK, 0, 1, 0, 0, K_NONE, 0)
@@ -110,14 +113,14 @@ __constant__ u32 kMap1[256] = {
     /*00*/ ALU4, ALU4, ALU4, ALU4, ALU4, ALU4, ALU4, ALU4,
     /*40*/ UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN,
     /*50*/ PUSHR, PUSHR, PUSHR, PUSHR, PUSHR, PUSHR, PUSHR, PUSHR, POPR, POPR, POPR, POPR, POPR, POPR, POPR, POPR,
-    /*60*/ UN, UN, UN, E(O_MOVSX, L_GREG, L_RM, Z_V, Z_D, 0, 1, 0, 1, K_NONE, 0), UN, UN, UN, UN,
+    /*60*/ UDE, UDE, UN, E(O_MOVSX, L_GREG, L_RM, Z_V, Z_D, 0, 1, 0, 1, K_NONE, 0), UN, UN, UN, UN,
     /*68*/ E(O_PUSH, L_PUSH, L_IMM, Z_STK, Z_STK, 0, 1, 0, 0, K_Z, 0),
     E(O_IMUL, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_Z, 0),
     E(O_PUSH, L_PUSH, L_IMM, Z_STK, Z_STK, 0, 1, 0, 0, K_B, 0),
     E(O_IMUL, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_B, 0), UN, UN, UN, UN,
     /*70*/ JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC,
     /*80*/ E(O_ALU, L_RM, L_IMM, Z_B, Z_B, 1, 1, 0, 1, K_B, G_1), E(O_ALU, L_RM, L_IMM, Z_V, Z_V, 1, 1, 0, 1, K_Z, G_1),
-    UN, E(O_ALU, L_RM, L_IMM, Z_V, Z_V, 1, 1, 0, 1, K_B, G_1),
+    UDE, E(O_ALU, L_RM, L_IMM, Z_V, Z_V, 1, 1, 0, 1, K_B, G_1),
     E(O_TEST, L_RM, L_GREG, Z_B, Z_B, 1, 0, 0, 1, K_NONE, 0), E(O_TEST, L_RM, L_GREG, Z_V, Z_V, 1, 0, 0, 1, K_NONE, 0),
     E(O_XCHG, L_RM, L_GREG, Z_B, Z_B, 1, 1, 1, 1, K_NONE, 0), E(O_XCHG, L_RM, L_GREG, Z_V, Z_V, 1, 1, 1, 1, K_NONE, 0),
     /*88*/ E(O_MOV, L_RM, L_GREG, Z_B, Z_B, 0, 1, 0, 1, K_NONE, 0), E(O_MOV, L_RM, L_GREG, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0),
@@ -125,7 +128,7 @@ __constant__ u32 kMap1[256] = {
     UN, E(O_LEA, L_GREG, 0, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0), UN,
     E(O_POP, L_RM, L_POP, Z_STK, Z_STK, 0, 1, 0, 1, K_NONE, G_8F),
     /*90*/ XCHGR, XCHGR, XCHGR, XCHGR, XCHGR, XCHGR, XCHGR, XCHGR,
-    /*98*/ E(O_CBW, 0, 0, Z_V, Z_V, 0, 0, 0, 0, K_NONE, 0), E(O_CWD, 0, 0, Z_V, Z_V, 0, 0, 0, 0, K_NONE, 0), UN, UN,
+    /*98*/ E(O_CBW, 0, 0, Z_V, Z_V, 0, 0, 0, 0, K_NONE, 0), E(O_CWD, 0, 0, Z_V, Z_V, 0, 0, 0, 0, K_NONE, 0), UDE, UN,
     E(O_PUSHF, L_PUSH, 0, Z_STK, Z_STK, 0, 1, 0, 0, K_NONE, 0), E(O_POPF, 0, L_POP, Z_STK, Z_STK, 0, 0, 0, 0, K_NONE, 0),
     E(O_SAHF, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), E(O_LAHF, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0),
     /*a0*/ E(O_MOV, L_RAX, L_MOFFS, Z_B, Z_B, 0, 1, 0, 0, K_MOFFS, 0), E(O_MOV, L_RAX, L_MOFFS, Z_V, Z_V, 0, 1, 0, 0, K_MOFFS, 0),
@@ -141,10 +144,10 @@ __constant__ u32 kMap1[256] = {
     E(O_INT3, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, UN, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0),
     /*d0*/ E(O_SHIFT, L_RM, L_ONE, Z_B, Z_B, 1, 1, 0, 1, K_NONE, G_2), E(O_SHIFT, L_RM, L_ONE, Z_V, Z_B, 1, 1, 0, 1, K_NONE, G_2),
     E(O_SHIFT, L_RM, L_CL, Z_B, Z_B, 1, 1, 0, 1, K_NONE, G_2), E(O_SHIFT, L_RM, L_CL, Z_V, Z_B, 1, 1, 0, 1, K_NONE, G_2),
-    UN, UN, UN, E(O_MOV, L_RAX, L_XLAT, Z_B, Z_B, 0, 1, 0, 0, K_NONE, 0),
+    UDE, UDE, UDE, E(O_MOV, L_RAX, L_XLAT, Z_B, Z_B, 0, 1, 0, 0, K_NONE, 0),
     /*d8*/ UN, UN, UN, UN, UN, UN, UN, UN,
     /*e0*/ UN, UN, UN, UN, UN, UN, UN, UN,
-    /*e8*/ E(O_CALL, L_PUSH, L_IMM, Z_Q, Z_Q, 0, 1, 0, 0, K_D, 0), E(O_JMP, 0, L_IMM, Z_Q, Z_Q, 0, 0, 0, 0, K_D, 0), UN,
+    /*e8*/ E(O_CALL, L_PUSH, L_IMM, Z_Q, Z_Q, 0, 1, 0, 0, K_D, 0), E(O_JMP, 0, L_IMM, Z_Q, Z_Q, 0, 0, 0, 0, K_D, 0), UDE,
     E(O_JMP, 0, L_IMM, Z_Q, Z_Q, 0, 0, 0, 0, K_B, 0), UN, UN, UN, UN,
     /*f0*/ UN, UN, UN, UN, E(O_HLT, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), FLG,
     E(O_TEST, L_RM, L_IMM, Z_B, Z_B, 1, 0, 0, 1, K_NONE, G_3), E(O_TEST, L_RM, L_IMM, Z_V, Z_V, 1, 0, 0, 1, K_NONE, G_3),
@@ -197,6 +200,7 @@ constexpr u32 kSseModrm = E(O_SSE, 0, 0, 0, 0, 0, 0, 0, 1, K_NONE, 0);  // 0f 38
 constexpr u32 kUnimpl = UN;
 #undef E
 #undef UN
+#undef UDE
 #undef ALU4
 #undef JCC
 #undef PUSHR
