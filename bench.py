@@ -252,8 +252,8 @@ def hevd_leg(base: str, lanes: int, limit: int, seconds: float, flags=()) -> dic
             "gpu_retired_fraction": (g["retired"] - g["error_retired"]) / max(1, g["retired"]),
             "lanes_per_wave_step": g["retired"] / max(1, b["group_steps"]),
             "roofline": roofline(b["alg_bytes"], b["kernel_launches"], b["kernel_ms"], pmc), "backend": b,
-            "node": {k: g.get(k) for k in ("step_ms", "account_ms", "produce_wait_ms", "make_ms", "fill_ms", "run_s",
-                                           "batches", "crashes")}}
+            "node": {k: g.get(k) for k in ("step_ms", "account_ms", "newcov_ms", "crashsave_ms", "produce_wait_ms",
+                                           "make_ms", "fill_ms", "run_s", "batches", "crashes")}}
 
 
 def syn_leg(lanes: int, limit: int, steps: int, device: int) -> dict:

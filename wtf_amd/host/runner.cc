@@ -676,8 +676,11 @@ void FuzzSession::Account(const uint8_t *Tc, size_t Size, const LaneResult &L, b
   if (std::holds_alternative<Cr3Change_t>(L.result)) S_.cr3++;
   if (const Crash_t *C = std::get_if<Crash_t>(&L.result)) {
     S_.crashes++;
-    if (!KnownCrash && !C->CrashName.empty() && CrashNames_.insert(C->CrashName).second)
-      Writer_.Save(T_ / "crashes" / C->CrashName, Tc, Size);
+    if (!KnownCrash && !C->CrashName.empty()) {
+      const auto tc = Clock::now();
+      if (CrashNames_.insert(C->CrashName).second) Writer_.Save(T_ / "crashes" / C->CrashName, Tc, Size);
+      S_.crashsave_ms += secs_since(tc) * 1e3;
+    }
   }
   // a timed-out testcase reports no coverage (the client revokes it,
   // client.cc:122-133); any other result with new coverage, crashes
@@ -686,14 +689,17 @@ void FuzzSession::Account(const uint8_t *Tc, size_t Size, const LaneResult &L, b
   if (!L.new_coverage.empty() && !std::holds_alternative<Timedout_t>(L.result)) {
     // admitted only if the master's aggregate grows: nodes attribute against
     // their own aggregates, which lack what other nodes found
+    const auto tn = Clock::now();
     const size_t Before = Coverage_.size();
     Coverage_.insert(L.new_coverage.begin(), L.new_coverage.end());
-    if (Coverage_.size() == Before) return;
-    Testcase_t Tcase(Tc, Size);
-    Mutator_->OnNewCoverage(Tcase);
-    LastNewCov_.assign((const char *)Tc, Size);
-    HaveNewCov_ = true;
-    Corpus_.SaveTestcase(L.result, std::move(Tcase));
+    if (Coverage_.size() != Before) {
+      Testcase_t Tcase(Tc, Size);
+      Mutator_->OnNewCoverage(Tcase);
+      LastNewCov_.assign((const char *)Tc, Size);
+      HaveNewCov_ = true;
+      Corpus_.SaveTestcase(L.result, std::move(Tcase));
+    }
+    S_.newcov_ms += secs_since(tn) * 1e3;
   }
 }
 
@@ -721,6 +727,7 @@ std::string FuzzSession::SummaryJson() const {
            "\"instr_per_s\":%.3f,\"coverage\":%zu,\"corpus\":%zu,\"crashes\":%llu,\"unique_crashes\":%zu,"
            "\"timeouts\":%llu,\"cr3\":%llu,\"errors\":%llu,\"error_retired\":%llu,\"merged_rips\":%llu,"
            "\"merge_ms\":%.3f,\"produce_wait_ms\":%.3f,\"account_ms\":%.3f,\"make_ms\":%.3f,\"step_ms\":%.3f,\"fill_ms\":%.3f,"
+           "\"newcov_ms\":%.3f,\"crashsave_ms\":%.3f,"
            "\"backend\":",
            O_.name.c_str(), Exec_.Lanes(), X_ ? X_->Rank() : 0, X_ ? X_->World() : 1,
            (unsigned long long)S_.batches, (unsigned long long)S_.execs, (unsigned long long)S_.retired, Wall,
@@ -728,7 +735,7 @@ std::string FuzzSession::SummaryJson() const {
            Exec_.CoverageSize(), Corpus_.Size(), (unsigned long long)S_.crashes, CrashNames_.size(),
            (unsigned long long)S_.timeouts, (unsigned long long)S_.cr3, (unsigned long long)S_.errors,
            (unsigned long long)S_.error_retired, (unsigned long long)S_.merged_rips, S_.merge_ms, S_.produce_wait_ms,
-           S_.account_ms, S_.make_ms, S_.step_ms, S_.fill_ms);
+           S_.account_ms, S_.make_ms, S_.step_ms, S_.fill_ms, S_.newcov_ms, S_.crashsave_ms);
   return std::string(b) + Exec_.StatsJson() + "}";
 }
 

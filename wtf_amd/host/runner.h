@@ -156,6 +156,7 @@ struct FuzzStats {
   double produce_wait_ms = 0, account_ms = 0;  // streaming: waiting on the mutator, master bookkeeping
   double make_ms = 0, step_ms = 0;             // streaming: mutation on the step's own thread, whole steps
   double fill_ms = 0;                          // streaming: taking the step's testcases (make_ms included)
+  double newcov_ms = 0, crashsave_ms = 0;      // account_ms split: corpus admissions, new crash names
 };
 
 // Testcases stored back to back: one allocation per chunk of mutations, so
