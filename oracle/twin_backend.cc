@@ -8,6 +8,7 @@
 // retired counts, final registers and coverage sets can be compared lane by
 // lane (tests/test_gpu_tlv.py), and it is the CPU baseline of the TLV bench
 // (one process per host core, bench.py). The product never links this file.
+#include "../wtf_amd/host/unimpl_hist.h"
 #include <cstdio>
 #include <cstring>
 #include <unordered_map>
@@ -93,6 +94,7 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
 
  public:
   ~TwinBackend_t() override {
+    if (getenv("WTF_UNIMPL_HIST")) fprintf(stderr, "unimpl_ops %s\n", unimpl_.json(64).c_str());
     if (m_) orc_destroy(m_);
   }
   bool Initialize(const Options_t &Opts, const CpuState_t &CpuState) override {
@@ -141,6 +143,7 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
         default:  // outside the engine subset: an engine error, not a target crash
           result_ = Crash_t();
           engine_error_ = true;
+          if (e.status == WTFGPU_EXIT_UNIMPLEMENTED) unimpl_.add(e.opcode);
           break;
       }
       break;
@@ -282,6 +285,7 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
   }
   bool full_ = false;
   bool engine_error_ = false;
+  UnimplHist unimpl_;  // WTF_UNIMPL_HIST=1: printed to stderr at exit
   void SetFullCoverage(bool On) override { full_ = On; }
   size_t CoverageSize() const override { return aggregate_.size(); }
   bool EnableTrace(uint32_t PerLane) override {

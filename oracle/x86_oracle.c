@@ -1766,6 +1766,8 @@ static int exec_vex(orc_machine *m, insn *d) {
   return X_OK;
 }
 
+#include "x86_oracle_sys.inc"
+
 static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
   (void)mr;
   const u32 op = d->op;
@@ -1773,6 +1775,10 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
   u64 nrip = d->start + d->len;
   u64 a = 0, b = 0, res = 0;
   *next_rip = nrip;
+  if (d->lock && !lockable(d)) { /* U34 */
+    fault(m, WTFGPU_VEC_UD, 0);
+    return X_FAULT;
+  }
 
   if (d->opmap == 0) {
     /* ALU ops 00-3f */
@@ -1910,7 +1916,10 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
       setreg(m, d, d->reg, osz, d->ea - seg_base(m, d->seg));
       return X_OK;
     case 0x8f: {
-      if ((d->reg & 7) != 0) return X_UNIMPL;
+      if ((d->reg & 7) != 0) { /* XOP on AMD; #UD here */
+        fault(m, WTFGPU_VEC_UD, 0);
+        return X_FAULT;
+      }
       const int sz = d->pfx66 ? 2 : 8;
       /* pop r/m: the address is computed with rsp already incremented */
       u64 rsp0 = m->r.gpr[WTFGPU_RSP];
@@ -2030,7 +2039,10 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
     }
     case 0xc6:
     case 0xc7: {
-      if ((d->reg & 7) != 0) return X_UNIMPL;
+      if ((d->reg & 7) != 0) { /* xabort / xbegin (no RTM) and the reserved forms */
+        fault(m, WTFGPU_VEC_UD, 0);
+        return X_FAULT;
+      }
       const int sz = op == 0xc6 ? 1 : osz;
       int isz = op == 0xc6 ? 1 : (osz == 2 ? 2 : 4);
       b = 0;
@@ -2047,8 +2059,8 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
     }
     case 0xcc:
       return X_INT3;
-    case 0xcf: { /* iretq (64-bit operand size only; U19) */
-      if (!d->rexw) return X_UNIMPL;
+    case 0xcf: { /* iretq (U19); iret / iretd with 16- / 32-bit slots (U29) */
+      if (!d->rexw) return far_pop(m, osz, 0, next_rip, 1);
       u64 f[5]; /* rip, cs, rflags, rsp, ss: every read before any change */
       for (int i = 0; i < 5; i++) CHK(vread(m, m->r.gpr[WTFGPU_RSP] + 8 * (u64)i, 8, &f[i]));
       const u32 ocpl = (u32)cpl(m), ncpl = (u32)f[1] & 3;
@@ -2106,6 +2118,116 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
     case 0xd5: case 0xd6: case 0xea:
       fault(m, WTFGPU_VEC_UD, 0);
       return X_FAULT;
+    case 0x62: /* EVEX (no AVX-512) */
+    case 0xce: /* into: invalid in 64-bit mode */
+      fault(m, WTFGPU_VEC_UD, 0);
+      return X_FAULT;
+    case 0x6c: case 0x6d: case 0x6e: case 0x6f: { /* ins / outs (U31) */
+      const int sz = (op & 1) ? (osz == 2 ? 2 : 4) : 1;
+      if (io_string(m, d, sz)) return X_FAULT_KEEP;
+      return X_OK;
+    }
+    case 0xe4: case 0xe5: case 0xec: case 0xed: /* in: all ones (U31) */
+      if (!io_allowed(m)) return X_FAULT;
+      setreg(m, d, 0, (op & 1) ? (osz == 2 ? 2 : 4) : 1, ~0ULL);
+      return X_OK;
+    case 0xe6: case 0xe7: case 0xee: case 0xef: /* out */
+      if (!io_allowed(m)) return X_FAULT;
+      return X_OK;
+    case 0x8c: { /* mov r/m, Sreg (U30) */
+      const u32 sr = d->reg & 7;
+      if (sr > 5) {
+        fault(m, WTFGPU_VEC_UD, 0);
+        return X_FAULT;
+      }
+      a = m->r.seg[sr].selector;
+      if (d->is_mem) {
+        CHK(vwrite(m, d->ea, 2, &a));
+      } else {
+        setreg(m, d, d->rm, osz, a);
+      }
+      return X_OK;
+    }
+    case 0x8e: { /* mov Sreg, r/m16 */
+      const u32 sr = d->reg & 7;
+      if (sr == WTFGPU_CS || sr > 5) {
+        fault(m, WTFGPU_VEC_UD, 0);
+        return X_FAULT;
+      }
+      CHK(rd_rm(m, d, 2, &a));
+      if (load_sreg(m, sr, (u16)a)) return X_FAULT;
+      return X_OK;
+    }
+    case 0x9b: /* fwait (U32) */
+      if ((m->r.cr0 & 0xa) == 0xa) { /* TS and MP */
+        fault(m, VEC_NM, 0);
+        return X_FAULT;
+      }
+      if (m->r.fpsw & 0x80) {
+        fault(m, VEC_MF, 0);
+        return X_FAULT;
+      }
+      return X_OK;
+    case 0xc8: { /* enter (U29): bochs' ENTER64 order */
+      if (d->pfx66) return X_UNIMPL;
+      const u64 size = (u64)d->bytes[d->len - 3] | ((u64)d->bytes[d->len - 2] << 8);
+      const u32 level = d->bytes[d->len - 1] & 31;
+      u64 rsp = m->r.gpr[WTFGPU_RSP], rbp = m->r.gpr[WTFGPU_RBP];
+      CHK(span_check(m, rsp - 8 * (level + 1), 8 * (level + 1), ACC_W));
+      rsp -= 8;
+      CHK(vwrite(m, rsp, 8, &rbp));
+      const u64 frame = rsp;
+      if (level > 0) {
+        for (u32 i = 1; i < level; i++) {
+          rbp -= 8;
+          u64 t = 0;
+          CHK(vread(m, rbp, 8, &t));
+          rsp -= 8;
+          CHK(vwrite(m, rsp, 8, &t));
+        }
+        rsp -= 8;
+        CHK(vwrite(m, rsp, 8, &frame));
+      }
+      m->r.gpr[WTFGPU_RBP] = frame;
+      m->r.gpr[WTFGPU_RSP] = rsp - size;
+      return X_OK;
+    }
+    case 0xca: case 0xcb: { /* far ret (U29): 32-bit operand size unless REX.W / 66 */
+      const u64 imm = op == 0xca ? ((u64)d->bytes[d->len - 2] | ((u64)d->bytes[d->len - 1] << 8)) : 0;
+      return far_pop(m, osz, imm, next_rip, 0);
+    }
+    case 0xcd: { /* int n (U24) */
+      const u32 vec = d->bytes[d->len - 1];
+      if (vec == 3) return X_INT3;
+      return soft_int(m, vec, 1, nrip, next_rip);
+    }
+    case 0xf1: /* int1 (icebp): #DB through the IDT, no DPL check */
+      return soft_int(m, VEC_DB, 0, nrip, next_rip);
+    case 0xfa: case 0xfb: /* cli / sti (U25) */
+      if ((u32)cpl(m) > iopl(m)) {
+        fault(m, WTFGPU_VEC_GP, 0);
+        return X_FAULT;
+      }
+      if (op == 0xfa) m->r.rflags &= ~RF_IF;
+      else m->r.rflags |= RF_IF;
+      return X_OK;
+    case 0xe0: case 0xe1: case 0xe2: case 0xe3: { /* loopne / loope / loop / jrcxz (U26) */
+      const u64 amask = d->pfx67 ? 0xffffffffULL : ~0ULL;
+      const u64 rel = sxn(d->bytes[d->len - 1], 1);
+      int taken;
+      if (op == 0xe3) {
+        taken = (m->r.gpr[WTFGPU_RCX] & amask) == 0;
+      } else {
+        const u64 cnt = (m->r.gpr[WTFGPU_RCX] - 1) & amask;
+        m->r.gpr[WTFGPU_RCX] = cnt;
+        const int zf = (m->r.rflags & RF_ZF) != 0;
+        taken = cnt != 0 && (op == 0xe2 || (op == 0xe1 ? zf : !zf));
+      }
+      if (taken) *next_rip = nrip + rel;
+      return X_OK;
+    }
+    case 0xd8: case 0xd9: case 0xda: case 0xdb: case 0xdc: case 0xdd: case 0xde: case 0xdf:
+      return exec_x87(m, d);
     case 0xf5:
       m->r.rflags ^= RF_CF;
       return X_OK;
@@ -2156,7 +2278,40 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
         }
         return X_OK;
       }
-      if (op == 0xfe) return X_UNIMPL;
+      if (op == 0xfe || sub == 7) {
+        fault(m, WTFGPU_VEC_UD, 0);
+        return X_FAULT;
+      }
+      if (sub == 3 || sub == 5) { /* far call / jmp m16:osz (U29): the CPL is kept */
+        if (!d->is_mem) {
+          fault(m, WTFGPU_VEC_UD, 0);
+          return X_FAULT;
+        }
+        u64 off = 0, sel = 0;
+        CHK(vread(m, d->ea, (u32)osz, &off));
+        CHK(vread(m, d->ea + (u64)osz, 2, &sel));
+        if ((sel & 0xfffc) == 0) {
+          fault(m, WTFGPU_VEC_GP, 0);
+          return X_FAULT;
+        }
+        if (osz == 2) off &= 0xffff;
+        if (!is_canonical(off)) {
+          fault(m, WTFGPU_VEC_GP, 0);
+          return X_FAULT;
+        }
+        const u16 ncs = (u16)((sel & 0xfffc) | (u32)cpl(m));
+        if (sub == 3) {
+          const u64 rsp = m->r.gpr[WTFGPU_RSP];
+          const u64 ocs = m->r.seg[WTFGPU_CS].selector;
+          CHK(span_check(m, rsp - 2 * (u64)osz, 2 * (u32)osz, ACC_W));
+          CHK(vwrite(m, rsp - (u64)osz, (u32)osz, &ocs));
+          CHK(vwrite(m, rsp - 2 * (u64)osz, (u32)osz, &nrip));
+          m->r.gpr[WTFGPU_RSP] = rsp - 2 * (u64)osz;
+        }
+        m->r.seg[WTFGPU_CS].selector = ncs;
+        *next_rip = off;
+        return X_OK;
+      }
       if (sub == 2 || sub == 4) { /* call / jmp near indirect (64-bit) */
         CHK(rd_rm(m, d, 8, &a));
         if (sub == 2) CHK(push64(m, nrip, 8));
@@ -2179,8 +2334,25 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
   if (d->vex) return exec_vex(m, d);
   if (d->opmap == 2) return exec_sse(m, d);
   if (d->opmap == 1) {
+    if (op == 0xae && !(!d->pfx66 && !d->rep && (d->is_mem ? ((d->reg & 7) == 2 || (d->reg & 7) == 3) : (d->reg & 7) >= 5)))
+      return exec_sys0f(m, d, next_rip);
+    if (op == 0xff) { /* ud0 */
+      fault(m, WTFGPU_VEC_UD, 0);
+      return X_FAULT;
+    }
     if (sse_opcode(op)) return exec_sse(m, d);
     switch (op) {
+    case 0x00: case 0x02: case 0x03: case 0x06: case 0x08: case 0x09: case 0x21: case 0x23: case 0x33:
+    case 0x34: case 0x35: case 0xa0: case 0xa1: case 0xa2: case 0xa8: case 0xa9: case 0xb2: case 0xb4:
+    case 0xb5: case 0xc7:
+      return exec_sys0f(m, d, next_rip);
+    /* #UD: 3DNow! / femms, mov to / from test registers, GETSEC (no SMX), RSM
+     * outside SMM, UD0 / UD1, the undefined 0f opcodes */
+    case 0x04: case 0x0a: case 0x0c: case 0x0e: case 0x0f: case 0x24: case 0x25: case 0x26: case 0x27:
+    case 0x36: case 0x37: case 0x39: case 0x3b: case 0x3c: case 0x3d: case 0x3e: case 0x3f: case 0xa6:
+    case 0xa7: case 0xaa: case 0xb9: case 0xff:
+      fault(m, WTFGPU_VEC_UD, 0);
+      return X_FAULT;
     case 0x05: /* syscall (64-bit; SDM vol. 2B; U16) */
     case 0x07: /* sysretq */
       if (op == 0x07 && !d->rexw) return X_UNIMPL;
@@ -2206,8 +2378,8 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
         m->r.seg[WTFGPU_SS].selector = (u16)((((m->r.star >> 48) & 0xffff) + 8) | 3);
       }
       return X_OK;
-    case 0x01: /* swapgs (0f 01 f8), rdtscp (0f 01 f9) */
-      if (d->is_mem || (d->reg & 7) != 7 || (d->rm & 7) > 1) return X_UNIMPL;
+    case 0x01: /* swapgs (0f 01 f8), rdtscp (0f 01 f9); the rest of group 7: exec_sys0f */
+      if (d->is_mem || (d->reg & 7) != 7 || (d->rm & 7) > 1) return exec_sys0f(m, d, next_rip);
       if ((d->rm & 7) == 1) {
         if ((m->r.cr4 & 4) && cpl(m) != 0) {
           fault(m, WTFGPU_VEC_GP, 0);
@@ -2327,11 +2499,6 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
       if (idx == 0xc0000103) m->r.tsc_aux = v;
       return X_OK;
     }
-    case 0xc7: /* rdrand r: deterministic 0 with CF=1 (U15) */
-      if (d->is_mem || (d->reg & 7) != 6 || d->pfx66 || d->rep) return X_UNIMPL;
-      setreg(m, d, d->rm, osz, 0);
-      set_flags(m, RF_STATUS, RF_CF);
-      return X_OK;
     case 0x0b:
       fault(m, WTFGPU_VEC_UD, 0);
       return X_FAULT;
@@ -2477,8 +2644,11 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
       setreg(m, d, d->reg, osz, a & szmask(osz));
       return X_OK;
     }
-    case 0xb8: /* popcnt (f3) */
-      if (d->rep != 0xf3) return X_UNIMPL;
+    case 0xb8: /* popcnt (f3); without f3 JMPE: #UD */
+      if (d->rep != 0xf3) {
+        fault(m, WTFGPU_VEC_UD, 0);
+        return X_FAULT;
+      }
       CHK(rd_rm(m, d, osz, &a));
       res = (u64)__builtin_popcountll(a & szmask(osz));
       setreg(m, d, d->reg, osz, res);
@@ -2610,8 +2780,18 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
     case 0x30: case 0x31: case 0x32: case 0x33: case 0x38: case 0x39: case 0x3a: case 0x3b:
     case 0x63: case 0x84: case 0x85: case 0x86: case 0x87: case 0x88: case 0x89: case 0x8a:
     case 0x8b: case 0x8d: case 0x8f: case 0xd0: case 0xd1: case 0xd2: case 0xd3: case 0xfe:
-    case 0xff:
+    case 0xff: case 0x8c: case 0x8e: case 0xd8: case 0xd9: case 0xda: case 0xdb: case 0xdc: case 0xdd:
+    case 0xde: case 0xdf:
       has_modrm = 1;
+      break;
+    case 0xc8:
+      imm = 3;
+      break;
+    case 0xca:
+      imm = 2;
+      break;
+    case 0xcd: case 0xe0: case 0xe1: case 0xe2: case 0xe3: case 0xe4: case 0xe5: case 0xe6: case 0xe7:
+      imm = 1;
       break;
     case 0x04: case 0x0c: case 0x14: case 0x1c: case 0x24: case 0x2c: case 0x34: case 0x3c:
     case 0x6a: case 0xa8: case 0xb0: case 0xb1: case 0xb2: case 0xb3: case 0xb4: case 0xb5:
@@ -2662,8 +2842,8 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
         b == 0xb3 || b == 0xbb || b == 0xaf || b == 0xb0 || b == 0xb1 || b == 0xb6 ||
         b == 0xb7 || b == 0xbe || b == 0xbf || b == 0xbc || b == 0xbd || b == 0xb8 ||
         b == 0xc0 || b == 0xc1 || b == 0xa5 || b == 0xad || b == 0x0d || b == 0x01 || b == 0xc7 || b == 0x20 ||
-        b == 0x22 ||
-        (b >= 0x18 && b <= 0x1f))
+        b == 0x22 || b == 0x00 || b == 0x02 || b == 0x03 || b == 0x21 || b == 0x23 || b == 0xb2 || b == 0xb4 ||
+        b == 0xb5 || (b >= 0x18 && b <= 0x1f))
       has_modrm = 1;
     if (b == 0xa4 || b == 0xac || b == 0xba) {
       has_modrm = 1;
@@ -2795,7 +2975,7 @@ static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
     fill_exit(m, ex, WTFGPU_EXIT_BREAKPOINT);
     return ex->status;
   }
-  if (rc == 1) {
+  if (rc == 1 && !d.lock) {
     memcpy(&ex->opcode, d.bytes, 4);
     fill_exit(m, ex, WTFGPU_EXIT_UNIMPLEMENTED);
     return ex->status;
@@ -2808,6 +2988,7 @@ static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
    * taken or not, indirect near jmp / call; before the retire hook */
   if (m->edges && x == X_OK &&
       ((d.opmap == 0 && d.op >= 0x70 && d.op <= 0x7f) || (d.opmap == 1 && d.op >= 0x80 && d.op <= 0x8f) ||
+       (d.opmap == 0 && !d.vex && d.op >= 0xe0 && d.op <= 0xe3) ||
        (d.opmap == 0 && d.op == 0xff && ((d.reg & 7) == 2 || (d.reg & 7) == 4)))) {
     u64 e = d.start;
     e ^= e >> 30;

@@ -340,6 +340,21 @@ def gen_forms(rng):
             for rep in ([], [0xF3], [0xF2]) if opc in (0xA6, 0xA7, 0xAE, 0xAF) else ([], [0xF3]):
                 code = rep + pfx(size) + ([0x48] if size == 8 else []) + [opc]
                 forms.append(Enc(code, f"str{opc:x}.{size}.{len(rep)}", cls="string", size=size))
+    # (round 3, appended so the earlier forms keep their random streams)
+    # loopne / loope / loop / jrcxz with a zero displacement: the counter update
+    # (rcx, or ecx zero-extended under 67) and untouched flags (U26)
+    for opc in (0xE0, 0xE1, 0xE2, 0xE3):
+        for p67 in ([], [0x67]):
+            forms.append(Enc(p67 + [opc, 0x00], f"loop{opc:x}.{len(p67)}", smalls={RCX: (0, 3)}))
+            forms.append(Enc(p67 + [opc, 0x00], f"loopr{opc:x}.{len(p67)}"))
+    # cmpxchg8b / cmpxchg16b [rdi] (U28): half the cases compare equal
+    forms.append(Enc([0x0F, 0xC7, 0x0F], "cmpxchg8b", ptrs={RDI: 0x40}, fmask=ZF, cls="cx"))
+    forms.append(Enc([0xF0, 0x0F, 0xC7, 0x0F], "lockcmpxchg8b", ptrs={RDI: 0x48}, fmask=ZF, cls="cx"))
+    forms.append(Enc([0x48, 0x0F, 0xC7, 0x0F], "cmpxchg16b", ptrs={RDI: 0x40}, fmask=ZF, cls="cx"))
+    # enter iw, ib at nesting levels 0..3 (U29): rbp points into the window above rsp
+    for level in (0, 1, 2, 3):
+        forms.append(Enc([0xC8, 0x18, 0x00, level], f"enter.{level}", ptrs={RBP: 0xC0}, cls="stack"))
+    forms.append(Enc([0xC8, 0x00, 0x01, 0x21], "enter.33", ptrs={RBP: 0xE0}, cls="stack"))
     return forms
 
 
@@ -464,6 +479,16 @@ def make_cases(forms, rng, per_form=6):
                     if not (v & ((1 << 8) | (1 << 18) | (1 << 14))):
                         break
                     seed = rng.getrandbits(63)
+            if f.cls == "cx" and rng.random() < 0.5:  # rdx:rax = the operand: the equal case
+                off = f.ptrs[RDI]
+                w = splitmix_bytes(seed, WIN)
+                lo = int.from_bytes(w[off:off + 8], "little")
+                hi = int.from_bytes(w[off + 8:off + 16], "little")
+                if f.code[0] == 0x48:
+                    regs[RAX], regs[RDX] = lo, hi
+                else:
+                    regs[RAX] = (regs[RAX] & ~0xFFFFFFFF) | (lo & 0xFFFFFFFF)
+                    regs[RDX] = (regs[RDX] & ~0xFFFFFFFF) | (lo >> 32)
             cases.append({
                 "name": f.name,
                 "code": f.code.hex(),

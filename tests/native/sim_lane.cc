@@ -20,8 +20,11 @@ struct SimResult {
   uint8_t win[512];  // the lane's view of [win_va, win_va + 512) at the end (zeros where unmapped)
 };
 
-int sim_run_mode(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, const wtfgpu_regs_t *r0,
-                 uint64_t limit, SimResult *out, int fast, uint64_t *fast_count, uint64_t win_va) {
+// final (optional): the lane's whole architectural state at the end, hot
+// fields merged into the cold copy as wtfgpu_read_regs does
+int sim_run_full(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, const wtfgpu_regs_t *r0,
+                 uint64_t limit, SimResult *out, int fast, uint64_t *fast_count, uint64_t win_va,
+                 wtfgpu_regs_t *final, uint8_t *ovpages) {
   uint64_t maxpfn = 0;
   for (uint64_t i = 0; i < npages; i++) maxpfn = gpfns[i] > maxpfn ? gpfns[i] : maxpfn;
   // page pointers carry flags in their low 12 bits: storage must be 4 KiB aligned
@@ -49,11 +52,23 @@ int sim_run_mode(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, c
   P.gs_base = gsb.data();
   P.limit = limit;
   wtfgpu_regs_t full = *r0;  // cold state: XMM registers, MXCSR
-  LaneSys sys{};
+  LaneSys sys{};  // as engine.hip make_init
   sys.cr0 = r0->cr0;
   sys.cr3 = r0->cr3;
   sys.cr4 = r0->cr4;
   sys.efer = r0->efer;
+  sys.cpl = r0->seg[WTFGPU_CS].selector & 3;
+  sys.star = r0->star;
+  sys.lstar = r0->lstar;
+  sys.sfmask = r0->sfmask;
+  sys.kgs = r0->kernel_gs_base;
+  sys.cs = r0->seg[WTFGPU_CS].selector;
+  sys.ss = r0->seg[WTFGPU_SS].selector;
+  sys.idtr = r0->idtr_base;
+  sys.idtr_limit = r0->idtr_limit;
+  sys.tss = r0->seg[WTFGPU_TR].base;
+  sys.cr2 = r0->cr2;
+  sys.deliv_icount = ~0ull;
   P.full = &full;
   P.sys = &sys;
   uint32_t glo[16], ghi[16];
@@ -168,6 +183,27 @@ int sim_run_mode(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, c
   for (int k = 0; k < 16; k++) out->xmm[2 * k] = full.xmm[k][0], out->xmm[2 * k + 1] = full.xmm[k][1];
   out->mxcsr = full.mxcsr;
   for (int k = 0; k < 16; k++) out->ymmh[2 * k] = full.ymmh[k][0], out->ymmh[2 * k + 1] = full.ymmh[k][1];
+  if (ovpages) memcpy(ovpages, ov, (size_t)(L.ovn < 64 ? L.ovn : 64) * 4096);  // the dirty pages, in out->dirty order
+  if (final) {
+    wtfgpu_regs_t f = full;
+    for (int i = 0; i < 16; i++) f.gpr[i] = R(L, i);
+    f.rip = L.rip;
+    f.rflags = L.rflags;
+    f.seg[WTFGPU_FS].base = fsb[0];
+    f.seg[WTFGPU_GS].base = gsb[0];
+    f.cr0 = sys.cr0;
+    f.cr3 = sys.cr3;
+    f.cr4 = sys.cr4;
+    f.efer = sys.efer;
+    f.kernel_gs_base = sys.kgs;
+    f.star = sys.star;
+    f.lstar = sys.lstar;
+    f.sfmask = sys.sfmask;
+    f.cr2 = sys.cr2;
+    f.seg[WTFGPU_CS].selector = sys.cs;
+    f.seg[WTFGPU_SS].selector = sys.ss;
+    *final = f;
+  }
   memset(out->win, 0, sizeof(out->win));
   if (win_va) {
     L.cpl = 0;
@@ -183,6 +219,10 @@ int sim_run_mode(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, c
   return 0;
 }
 
+int sim_run_mode(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, const wtfgpu_regs_t *r0,
+                 uint64_t limit, SimResult *out, int fast, uint64_t *fast_count, uint64_t win_va) {
+  return sim_run_full(gpfns, pages, npages, r0, limit, out, fast, fast_count, win_va, nullptr, nullptr);
+}
 int sim_run(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, const wtfgpu_regs_t *r0,
             uint64_t limit, SimResult *out) {
   return sim_run_mode(gpfns, pages, npages, r0, limit, out, 0, nullptr, 0);

@@ -43,6 +43,11 @@ def test_tlv_full_coverage_parity(target, tmp_path):
     assert not bad, bad[:10]
     assert sum(r["result"] == "crash" for r in g) > 10
     assert not any(r["error"] for r in g)
+    # __fastfail: int 0x29 through the snapshot's IDT gate (DPL 3, stack switch to
+    # RSP0) to nt!KiRaiseSecurityCheckFailure, named from the address at [rsp]
+    # (crash_detection_umode.cc:131-152), identical on both backends
+    ff = [r for r in g if r["input"] == "edge_fastfail"]
+    assert ff and ff[0]["crash"].startswith("crash-EXCEPTION_STACK_BUFFER_OVERRUN-0x"), ff
 
 
 def test_tlv_parity_host_handlers_only(target, tmp_path):

@@ -33,6 +33,10 @@ def edge_cases() -> dict[str, bytes]:
         "edge_header_only": packets_json([(0, 1, 0, b"")]),
         "edge_big_edit": packets_json([(0, 1, 4, b"abcd"), (1, 1, 64, b"y" * 64)]),
         "edge_delete_twice": packets_json([(0, 1, 4, b"abcd"), (2, 1, 0, b""), (2, 1, 0, b"")]),
+        # the stale LastFreed deleted by an allocation past the table: a free of a
+        # pointer the heap does not own -> __fastfail -> int 0x29 -> nt!KiRaiseSecurityCheckFailure
+        "edge_fastfail": packets_json([(0, i, 16, bytes([0x30 + i] * 16)) for i in range(1, 5)] + [(2, 1, 0, b"")] +
+                                      [(0, 5, 16, b"5" * 16), (0, 6, 16, b"6" * 16)]),
     }
 
 

@@ -92,7 +92,7 @@ __device__ __forceinline__ u64 edge_key(u64 rip, u64 next) {
 // (cnear_branch_taken / _not_taken) and indirect near jmp / call
 // (ucnear_branch with JMP_INDIRECT / CALL_INDIRECT), :235-257.
 __device__ __forceinline__ bool edge_op(u32 op, u32 bsrc) {
-  return op == O_JCC || ((op == O_JMP || op == O_CALL) && bsrc != L_IMM);
+  return op == O_JCC || op == O_LOOP || ((op == O_JMP || op == O_CALL) && bsrc != L_IMM);
 }
 
 __device__ __forceinline__ void load_lane(const Dev &P, u32 lane, Lane &L) {

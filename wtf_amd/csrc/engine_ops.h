@@ -27,7 +27,9 @@ enum : u32 {
   O_SHIFT, O_SHXD, O_MULDIV, O_IMUL, O_BT, O_BSF, O_BSR, O_TZCNT, O_LZCNT, O_POPCNT,
   O_CMOV, O_SETCC, O_BSWAP, O_CBW, O_CWD, O_LAHF, O_SAHF, O_FLAGOP, O_NOP, O_JCC, O_JMP,
   O_CALL, O_RET, O_PUSH, O_POP, O_PUSHF, O_POPF, O_LEAVE, O_STRING, O_INT3, O_HLT, O_UD,
-  O_LEA, O_SYS, O_SSE, O_UNIMPL
+  O_LEA, O_SYS, O_SSE, O_UNIMPL,
+  O_SYS2,  // engine_sys.h: system / far-transfer / I/O / x87-control (sub = opcode | 0x100 for 0f)
+  O_LOOP   // loopne / loope / loop / jrcxz (sub = opcode & 3)
 };
 // operand locations
 enum : u32 {
@@ -90,7 +92,7 @@ __device__ __forceinline__ u64 segbase(const Dev &P, const Lane &L, u32 seg) {
 // invalid in 64-bit mode (push / pop of es cs ss ds, daa das aaa aas, pusha
 // popa, the 82 alias of 80, far call / jmp, aam aad salc): #UD
 #define UDE E(O_UD, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0)
-enum : u32 { K_NONE = 0, K_B, K_W, K_Z, K_V, K_MOFFS, K_D };
+enum : u32 { K_NONE = 0, K_B, K_W, K_Z, K_V, K_MOFFS, K_D, K_ENTER /* iw ib */ };
 enum : u32 { G_NONE = 0, G_1, G_2, G_3, G_4, G_5, G_8F, G_C6, G_BA, G_ALU };
 
 #define ALU4                                                                             \
@@ -108,16 +110,21 @@ enum : u32 { G_NONE = 0, G_1, G_2, G_3, G_4, G_5, G_8F, G_C6, G_BA, G_ALU };
 #define MOVRV E(O_MOV, L_OPREG, L_IMM, Z_V, Z_V, 0, 1, 0, 0, K_V, 0)
 #define STR(sz) E(O_STRING, 0, 0, sz, sz, 0, 0, 0, 0, K_NONE, 0)
 #define FLG E(O_FLAGOP, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0)
+// engine_sys.h instructions: asz = the operand size, bsz = 2 with a 66 prefix
+#define S2 E(O_SYS2, 0, 0, Z_V, Z_STK, 0, 0, 0, 0, K_NONE, 0)
+#define S2M E(O_SYS2, 0, 0, Z_V, Z_STK, 0, 0, 0, 1, K_NONE, 0)
+#define S2B E(O_SYS2, 0, 0, Z_V, Z_STK, 0, 0, 0, 0, K_B, 0)
+#define LOOPX E(O_LOOP, 0, L_IMM, 0, Z_Q, 0, 0, 0, 0, K_B, 0)
 
 __constant__ u32 kMap1[256] = {
     /*00*/ ALU4, ALU4, ALU4, ALU4, ALU4, ALU4, ALU4, ALU4,
     /*40*/ UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN,
     /*50*/ PUSHR, PUSHR, PUSHR, PUSHR, PUSHR, PUSHR, PUSHR, PUSHR, POPR, POPR, POPR, POPR, POPR, POPR, POPR, POPR,
-    /*60*/ UDE, UDE, UN, E(O_MOVSX, L_GREG, L_RM, Z_V, Z_D, 0, 1, 0, 1, K_NONE, 0), UN, UN, UN, UN,
+    /*60*/ UDE, UDE, UDE, E(O_MOVSX, L_GREG, L_RM, Z_V, Z_D, 0, 1, 0, 1, K_NONE, 0), UN, UN, UN, UN,
     /*68*/ E(O_PUSH, L_PUSH, L_IMM, Z_STK, Z_STK, 0, 1, 0, 0, K_Z, 0),
     E(O_IMUL, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_Z, 0),
     E(O_PUSH, L_PUSH, L_IMM, Z_STK, Z_STK, 0, 1, 0, 0, K_B, 0),
-    E(O_IMUL, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_B, 0), UN, UN, UN, UN,
+    E(O_IMUL, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_B, 0), STR(Z_B), STR(Z_V), STR(Z_B), STR(Z_V),
     /*70*/ JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC, JCC,
     /*80*/ E(O_ALU, L_RM, L_IMM, Z_B, Z_B, 1, 1, 0, 1, K_B, G_1), E(O_ALU, L_RM, L_IMM, Z_V, Z_V, 1, 1, 0, 1, K_Z, G_1),
     UDE, E(O_ALU, L_RM, L_IMM, Z_V, Z_V, 1, 1, 0, 1, K_B, G_1),
@@ -125,10 +132,10 @@ __constant__ u32 kMap1[256] = {
     E(O_XCHG, L_RM, L_GREG, Z_B, Z_B, 1, 1, 1, 1, K_NONE, 0), E(O_XCHG, L_RM, L_GREG, Z_V, Z_V, 1, 1, 1, 1, K_NONE, 0),
     /*88*/ E(O_MOV, L_RM, L_GREG, Z_B, Z_B, 0, 1, 0, 1, K_NONE, 0), E(O_MOV, L_RM, L_GREG, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0),
     E(O_MOV, L_GREG, L_RM, Z_B, Z_B, 0, 1, 0, 1, K_NONE, 0), E(O_MOV, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0),
-    UN, E(O_LEA, L_GREG, 0, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0), UN,
+    S2M, E(O_LEA, L_GREG, 0, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0), S2M,
     E(O_POP, L_RM, L_POP, Z_STK, Z_STK, 0, 1, 0, 1, K_NONE, G_8F),
     /*90*/ XCHGR, XCHGR, XCHGR, XCHGR, XCHGR, XCHGR, XCHGR, XCHGR,
-    /*98*/ E(O_CBW, 0, 0, Z_V, Z_V, 0, 0, 0, 0, K_NONE, 0), E(O_CWD, 0, 0, Z_V, Z_V, 0, 0, 0, 0, K_NONE, 0), UDE, UN,
+    /*98*/ E(O_CBW, 0, 0, Z_V, Z_V, 0, 0, 0, 0, K_NONE, 0), E(O_CWD, 0, 0, Z_V, Z_V, 0, 0, 0, 0, K_NONE, 0), UDE, S2,
     E(O_PUSHF, L_PUSH, 0, Z_STK, Z_STK, 0, 1, 0, 0, K_NONE, 0), E(O_POPF, 0, L_POP, Z_STK, Z_STK, 0, 0, 0, 0, K_NONE, 0),
     E(O_SAHF, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), E(O_LAHF, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0),
     /*a0*/ E(O_MOV, L_RAX, L_MOFFS, Z_B, Z_B, 0, 1, 0, 0, K_MOFFS, 0), E(O_MOV, L_RAX, L_MOFFS, Z_V, Z_V, 0, 1, 0, 0, K_MOFFS, 0),
@@ -140,18 +147,19 @@ __constant__ u32 kMap1[256] = {
     /*c0*/ E(O_SHIFT, L_RM, L_IMM, Z_B, Z_B, 1, 1, 0, 1, K_B, G_2), E(O_SHIFT, L_RM, L_IMM, Z_V, Z_B, 1, 1, 0, 1, K_B, G_2),
     E(O_RET, 0, L_POP, Z_Q, Z_Q, 0, 0, 0, 0, K_W, 0), E(O_RET, 0, L_POP, Z_Q, Z_Q, 0, 0, 0, 0, K_NONE, 0), UN, UN,
     E(O_MOV, L_RM, L_IMM, Z_B, Z_B, 0, 1, 0, 1, K_B, G_C6), E(O_MOV, L_RM, L_IMM, Z_V, Z_V, 0, 1, 0, 1, K_Z, G_C6),
-    /*c8*/ UN, E(O_LEAVE, 0, L_RBPMEM, Z_Q, Z_Q, 0, 0, 0, 0, K_NONE, 0), UN, UN,
-    E(O_INT3, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, UN, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0),
+    /*c8*/ E(O_SYS2, 0, 0, Z_V, Z_STK, 0, 0, 0, 0, K_ENTER, 0), E(O_LEAVE, 0, L_RBPMEM, Z_Q, Z_Q, 0, 0, 0, 0, K_NONE, 0),
+    E(O_SYS2, 0, 0, Z_V, Z_STK, 0, 0, 0, 0, K_W, 0), S2,
+    E(O_INT3, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), S2B, UDE, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0),
     /*d0*/ E(O_SHIFT, L_RM, L_ONE, Z_B, Z_B, 1, 1, 0, 1, K_NONE, G_2), E(O_SHIFT, L_RM, L_ONE, Z_V, Z_B, 1, 1, 0, 1, K_NONE, G_2),
     E(O_SHIFT, L_RM, L_CL, Z_B, Z_B, 1, 1, 0, 1, K_NONE, G_2), E(O_SHIFT, L_RM, L_CL, Z_V, Z_B, 1, 1, 0, 1, K_NONE, G_2),
     UDE, UDE, UDE, E(O_MOV, L_RAX, L_XLAT, Z_B, Z_B, 0, 1, 0, 0, K_NONE, 0),
-    /*d8*/ UN, UN, UN, UN, UN, UN, UN, UN,
-    /*e0*/ UN, UN, UN, UN, UN, UN, UN, UN,
+    /*d8*/ S2M, S2M, S2M, S2M, S2M, S2M, S2M, S2M,
+    /*e0*/ LOOPX, LOOPX, LOOPX, LOOPX, S2B, S2B, S2B, S2B,
     /*e8*/ E(O_CALL, L_PUSH, L_IMM, Z_Q, Z_Q, 0, 1, 0, 0, K_D, 0), E(O_JMP, 0, L_IMM, Z_Q, Z_Q, 0, 0, 0, 0, K_D, 0), UDE,
-    E(O_JMP, 0, L_IMM, Z_Q, Z_Q, 0, 0, 0, 0, K_B, 0), UN, UN, UN, UN,
-    /*f0*/ UN, UN, UN, UN, E(O_HLT, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), FLG,
+    E(O_JMP, 0, L_IMM, Z_Q, Z_Q, 0, 0, 0, 0, K_B, 0), S2, S2, S2, S2,
+    /*f0*/ UN, S2, UN, UN, E(O_HLT, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), FLG,
     E(O_TEST, L_RM, L_IMM, Z_B, Z_B, 1, 0, 0, 1, K_NONE, G_3), E(O_TEST, L_RM, L_IMM, Z_V, Z_V, 1, 0, 0, 1, K_NONE, G_3),
-    /*f8*/ FLG, FLG, UN, UN, FLG, FLG,
+    /*f8*/ FLG, FLG, S2, S2, FLG, FLG,
     E(O_INCDEC, L_RM, 0, Z_B, Z_B, 1, 1, 0, 1, K_NONE, G_4), E(O_INCDEC, L_RM, 0, Z_V, Z_V, 1, 1, 0, 1, K_NONE, G_5),
 };
 
@@ -167,25 +175,25 @@ __constant__ u32 kMap1[256] = {
 #define SSEI E(O_SSE, 0, 0, 0, 0, 0, 0, 0, 1, K_B, 0)
 #define SSE8 SSEM, SSEM, SSEM, SSEM, SSEM, SSEM, SSEM, SSEM
 __constant__ u32 kMap2[256] = {
-    /*00*/ UN, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 1, K_NONE, 0), UN, UN, UN, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN,
-    E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, UN, UN, E(O_UD, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, NOPM, UN, UN,
+    /*00*/ S2M, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 1, K_NONE, 0), S2M, S2M, UDE, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), S2,
+    E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), S2, S2, UDE, E(O_UD, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UDE, NOPM, UDE, UDE,
     /*10*/ SSE8, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM,
-    /*20*/ E(O_SYS, L_RM, 0, Z_Q, Z_Q, 0, 1, 0, 1, K_NONE, 0), UN, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 1, K_NONE, 0), UN, UN,
-    UN, UN, UN, SSEM, SSEM, UN, SSEM, UN, UN, UN, UN,
+    /*20*/ E(O_SYS, L_RM, 0, Z_Q, Z_Q, 0, 1, 0, 1, K_NONE, 0), S2M, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 1, K_NONE, 0), S2M, UDE,
+    UDE, UDE, UDE, SSEM, SSEM, UN, SSEM, UN, UN, UN, UN,
     /*30*/ E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0),
-    E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN,
+    E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), S2, S2, S2, UDE, UDE, UN, UDE, UN, UDE, UDE, UDE, UDE, UDE,
     /*40*/ CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV,
     /*50*/ SSE8, SSE8,
     /*60*/ SSE8, SSE8,
     /*70*/ SSEI, SSEI, SSEI, SSEI, SSEM, SSEM, SSEM, E(O_SSE, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), SSE8,
     /*80*/ JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32, JCC32,
     /*90*/ SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC, SETCC,
-    /*a0*/ UN, UN, UN, E(O_BT, L_RM, L_GREG, Z_V, Z_V, 1, 0, 0, 1, K_NONE, 0), SHXD(K_B), SHXD(K_NONE), UN, UN,
-    /*a8*/ UN, UN, UN, BTRW, SHXD(K_B), SHXD(K_NONE), SSEM, E(O_IMUL, L_GREG, L_RM, Z_V, Z_V, 1, 1, 0, 1, K_NONE, 0),
+    /*a0*/ S2, S2, S2, E(O_BT, L_RM, L_GREG, Z_V, Z_V, 1, 0, 0, 1, K_NONE, 0), SHXD(K_B), SHXD(K_NONE), UDE, UDE,
+    /*a8*/ S2, S2, UDE, BTRW, SHXD(K_B), SHXD(K_NONE), SSEM, E(O_IMUL, L_GREG, L_RM, Z_V, Z_V, 1, 1, 0, 1, K_NONE, 0),
     /*b0*/ E(O_CMPXCHG, L_RM, L_GREG, Z_B, Z_B, 1, 1, 0, 1, K_NONE, 0),
-    E(O_CMPXCHG, L_RM, L_GREG, Z_V, Z_V, 1, 1, 0, 1, K_NONE, 0), UN, BTRW, UN, UN,
+    E(O_CMPXCHG, L_RM, L_GREG, Z_V, Z_V, 1, 1, 0, 1, K_NONE, 0), S2M, BTRW, S2M, S2M,
     E(O_MOVZX, L_GREG, L_RM, Z_V, Z_B, 0, 1, 0, 1, K_NONE, 0), E(O_MOVZX, L_GREG, L_RM, Z_V, Z_W, 0, 1, 0, 1, K_NONE, 0),
-    /*b8*/ E(O_POPCNT, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0), UN,
+    /*b8*/ E(O_POPCNT, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0), UDE,
     E(O_BT, L_RM, L_IMM, Z_V, Z_B, 1, 1, 0, 1, K_B, G_BA), BTRW,
     E(O_BSF, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0), E(O_BSR, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0),
     E(O_MOVSX, L_GREG, L_RM, Z_V, Z_B, 0, 1, 0, 1, K_NONE, 0), E(O_MOVSX, L_GREG, L_RM, Z_V, Z_W, 0, 1, 0, 1, K_NONE, 0),
@@ -210,6 +218,10 @@ constexpr u32 kUnimpl = UN;
 #undef MOVRV
 #undef STR
 #undef FLG
+#undef S2
+#undef S2M
+#undef S2B
+#undef LOOPX
 #undef NOPM
 #undef CMOV
 #undef JCC32
@@ -249,7 +261,7 @@ __device__ __forceinline__ u32 zsize(u32 z, u32 osz, u32 p66) {
 
 // Decode (uniform). 0 ok, 1 needs bytes beyond avail, 2 longer than 15 (#GP).
 __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
-  u32 pos = 0, p66 = 0, rex = 0, c;
+  u32 pos = 0, p66 = 0, rex = 0, lock = 0, c;
   u.p67 = u.rep = u.seg = 0;
   for (;;) {
     if (pos >= 15) return 2;
@@ -264,7 +276,8 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
     else if (c == 0xf2 || c == 0xf3) u.rep = c;
     else if (c == 0x64) u.seg = 4;
     else if (c == 0x65) u.seg = 5;
-    else if (c != 0xf0 && c != 0x26 && c != 0x2e && c != 0x36 && c != 0x3e) break;
+    else if (c == 0xf0) lock = 1;
+    else if (c != 0x26 && c != 0x2e && c != 0x36 && c != 0x3e) break;
     rex = 0;
   }
   // VEX (c4 / c5; always VEX in 64-bit mode): its fields become the REX bits,
@@ -308,15 +321,15 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
         e = kSseModrm;
       } else {
         u.len = pos;
-        u.op = O_UNIMPL;
-        u.supported = 0;
+        u.op = lock ? O_UD : O_UNIMPL;  // U34: lock is #UD first
+        u.supported = lock;
         u.opbytes = pos >= 4 ? (u32)b.lo : ((u32)b.lo & ((1u << (8 * pos)) - 1));
         return 0;
       }
     } else {
       map2 = 1;
       e = kMap2[c];
-      if (c == 0xb8 && u.rep != 0xf3) e = O_UNIMPL;  // popcnt needs f3
+      if ((c == 0xb8 && u.rep != 0xf3) || c == 0xff) e = O_UD;  // popcnt needs f3 (jmpe: #UD); ud0
     }
   } else {
     e = kMap1[c];
@@ -415,7 +428,7 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
         }
         break;
       case G_4:
-        if (r3 > 1) u.op = O_UNIMPL;
+        if (r3 > 1) u.op = O_UD;
         u.sub = r3;
         break;
       case G_5:
@@ -435,16 +448,20 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
           u.aread = 0;
           u.awrite = 1;
           u.bsrc = L_RM;
-        } else if (r3 > 1) {
-          u.op = O_UNIMPL;
+        } else if (r3 == 3 || r3 == 5) {  // far call / jmp m16:osz (engine_sys.h)
+          u.op = O_SYS2;
+          u.asz = osz;
+          u.bsz = p66 ? 2 : 8;
+        } else if (r3 == 7) {
+          u.op = O_UD;
         }
         break;
       case G_8F:
       case G_C6:
-        if (r3 != 0) u.op = O_UNIMPL;
+        if (r3 != 0) u.op = O_UD;  // xop / xabort / xbegin and the reserved forms: #UD
         break;
       case G_BA:
-        if (r3 < 4) u.op = O_UNIMPL;
+        if (r3 < 4) u.op = O_UD;
         u.sub = r3;
         if (r3 == 4) u.awrite = 0;
         break;
@@ -463,7 +480,11 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
       } else {
         u.bsz = u.rep == 0xf3 ? 2 : u.rep == 0xf2 ? 3 : p66 ? 1 : 0;
         u.opreg = smap << 8;
-        if (!sse_valid(smap, c, u.bsz, u.is_mem, u.reg & 7)) u.op = O_UNIMPL;
+        if (!sse_valid(smap, c, u.bsz, u.is_mem, u.reg & 7)) u.op = (c == 0xae && smap == 1) ? O_SYS2 : O_UNIMPL;
+      }
+      if (u.op == O_SYS2) {  // group 15 beyond ldmxcsr / stmxcsr / the fences: engine_sys.h
+        u.asz = osz;
+        u.bsz = p66 ? 2 : 8;
       }
     }
     if (u.op == O_BT && grp != G_BA) u.sub = c == 0xa3 ? 4 : c == 0xab ? 5 : c == 0xb3 ? 6 : 7;
@@ -478,15 +499,34 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
               : c == 0x31 ? 8 : c == 0x32 ? 9 : 3;
       if ((c == 0x20 || c == 0x22) && u.is_mem) u.op = O_UNIMPL;
       if (c == 0x07 && !rexw) u.op = O_UNIMPL;
-      if (c == 0x01 && (u.is_mem || (u.reg & 7) != 7 || (u.rm & 7) > 1)) u.op = O_UNIMPL;
       if (c == 0x01 && (u.rm & 7) == 1) u.sub = 10;
-      if (c == 0xc7 && (u.is_mem || (u.reg & 7) != 6 || p66 || u.rep)) u.op = O_UNIMPL;
+      // the rest of groups 7 and 9 (rdrand / rdseed r stay here): engine_sys.h
+      if ((c == 0x01 && (u.is_mem || (u.reg & 7) != 7 || (u.rm & 7) > 1)) ||
+          (c == 0xc7 && (u.is_mem || (u.reg & 7) < 6 || u.rep))) {
+        u.op = O_SYS2;
+        u.asz = osz;
+        u.bsz = p66 ? 2 : 8;
+      }
     }
   } else if (u.op == O_FLAGOP) {
     u.sub = c;
-  } else if (u.op == O_SYS) {  // iretq (48 cf): 64-bit operand size only
+  } else if (u.op == O_SYS) {  // iretq (48 cf); iret / iretd: engine_sys.h
     u.sub = 5;
-    if (!rexw) u.op = O_UNIMPL;
+    if (!rexw) {
+      u.op = O_SYS2;
+      u.asz = osz;
+      u.bsz = p66 ? 2 : 8;
+    }
+  } else if (u.op == O_STRING && c < 0x80) {
+    u.sub |= 0x10;  // ins / outs (6c-6f)
+  }
+  if (u.op == O_SYS2) u.sub = (map2 ? 0x100u : 0u) | c;
+  if (lock) {  // U34: lock only on a memory read-modify-write of the lockable forms
+    const bool ok = u.is_mem && !vex &&
+                    ((u.op == O_ALU && u.asrc == L_RM && u.sub != 7) || (u.op == O_XCHG && u.asrc == L_RM) ||
+                     u.op == O_NOT || u.op == O_NEG || u.op == O_INCDEC || (u.op == O_BT && u.sub >= 5) ||
+                     u.op == O_CMPXCHG || u.op == O_XADD || (u.op == O_SYS2 && u.sub == 0x1c7 && (u.reg & 7) == 1));
+    if (!ok) u.op = O_UD;
   }
   u32 n = 0;
   switch (ik) {
@@ -496,6 +536,7 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
     case K_V: n = osz; break;
     case K_MOFFS: n = u.p67 ? 4 : 8; break;
     case K_D: n = 4; break;
+    case K_ENTER: n = 3; break;
     default: n = 0;
   }
   if (pos + n > 15) return 2;
@@ -503,7 +544,7 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
   const u64 raw = ib_get(b, pos, n);
   // the immediates x86 sign-extends: Ib/Iz of alu/test/push/imul, branch displacements, c7 Iz
   const bool sx = n && (u.op == O_ALU || u.op == O_TEST || u.op == O_PUSH || u.op == O_IMUL || u.op == O_JCC ||
-                        u.op == O_JMP || u.op == O_CALL || (u.op == O_MOV && c == 0xc7 && !map2));
+                        u.op == O_LOOP || u.op == O_JMP || u.op == O_CALL || (u.op == O_MOV && c == 0xc7 && !map2));
   u.imm = sx ? sext(raw, n) : raw;
   pos += n;
   u.len = pos;
@@ -785,18 +826,25 @@ __device__ __forceinline__ bool muldiv(const Lane &L, u32 sub, u32 sz, u64 src, 
 
 // ---------------------------------------------------------------- string ops
 __device__ __forceinline__ int string_op(const Dev &P, Lane &L, const UOp &u) {
-  const u32 op = 0xa0 | (u.sub & 0xe);
-  const u32 sz = u.asz;
+  // a4 movs, a6 cmps, aa stos, ac lods, ae scas; 6c ins, 6e outs (U31: all
+  // ones in, nothing out, #GP(0) at CPL > IOPL checked per iteration)
+  const bool io = u.sub & 0x10;
+  const u32 op = io ? (0x60 | (u.sub & 0xe)) : (0xa0 | (u.sub & 0xe));
+  const u32 sz = io && u.asz == 8 ? 4 : u.asz;
   const u64 amask = u.p67 ? 0xffffffffull : ~0ull;
   const u64 step = (L.rflags & F_DF) ? (u64)(-(i64)sz) : (u64)sz;
   const u64 sb = segbase(P, L, u.seg);
-  const bool src = op == 0xa4 || op == 0xa6 || op == 0xac;
-  const bool dstw = op == 0xa4 || op == 0xaa;
+  const bool src = op == 0xa4 || op == 0xa6 || op == 0xac || op == 0x6e;
+  const bool dstw = op == 0xa4 || op == 0xaa || op == 0x6c;
   const bool dstr = op == 0xa6 || op == 0xae;
   for (;;) {
     if (u.rep && (R(L, 1) & amask) == 0) break;
+    if (io && L.cpl > ((L.rflags >> 12) & 3)) {
+      set_fault(L, WTFGPU_VEC_GP, 0, 0);
+      return X_KEEP;
+    }
     const u64 rsi = R(L, 6) & amask, rdi = R(L, 7) & amask;
-    u64 a = R(L, 0), b = 0;
+    u64 a = op == 0x6c ? ~0ull : R(L, 0), b = 0;
     if (src && !vread(L, sb + rsi, sz, a)) return X_KEEP;
     if (dstr && !vread(L, rdi, sz, b)) return X_KEEP;
     if (dstw && !vwrite(L, rdi, sz, a)) return X_KEEP;
@@ -807,7 +855,7 @@ __device__ __forceinline__ int string_op(const Dev &P, Lane &L, const UOp &u) {
     }
     if (op == 0xac) setr(L, u.rex, 0, sz, a);
     if (src) RS(L, 6, (rsi + step) & amask);
-    if (op != 0xac) RS(L, 7, (rdi + step) & amask);
+    if (op != 0xac && op != 0x6e) RS(L, 7, (rdi + step) & amask);
     L.nbytes += L.pend;  // the iteration is architecturally complete
     L.pend = 0;
     if (!u.rep) break;
@@ -820,6 +868,10 @@ __device__ __forceinline__ int string_op(const Dev &P, Lane &L, const UOp &u) {
   }
   return X_OK;
 }
+
+}  // namespace wtfgpu_dev
+#include "engine_sys.h"  // sys2_exec: system, far-transfer, I/O and x87-control instructions
+namespace wtfgpu_dev {
 
 // ---------------------------------------------------------------- execute
 __device__ __forceinline__ bool loc_is_mem(const UOp &u, u32 loc) {
@@ -864,6 +916,7 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
     }
     if (u.p67) ea &= 0xffffffffull;
   }
+  if (op == O_SYS2) return sys2_exec(P, L, u, nrip, next, ea + sb);
   const u64 rsp = R(L, 4);
   // ---- register / immediate operands
   u64 a = (u.aread && !loc_is_mem(u, u.asrc)) ? loc_reg_read(L, u, u.asrc, u.asz) : 0;
@@ -1038,6 +1091,20 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
       if (cond(fl, u.sub)) next = nrip + b;
       break;
     case O_JMP: next = u.bsrc == L_IMM ? nrip + b : b; break;
+    case O_LOOP: {  // U26: e0 loopne, e1 loope, e2 loop, e3 jrcxz; rcx (ecx with 67), flags untouched
+      const u64 amask = u.p67 ? 0xffffffffull : ~0ull;
+      bool taken;
+      if (u.sub == 3) {
+        taken = (R(L, 1) & amask) == 0;
+      } else {
+        const u64 cnt = (R(L, 1) - 1) & amask;
+        RS(L, 1, cnt);
+        const bool zf = fl & F_ZF;
+        taken = cnt != 0 && (u.sub == 2 || (u.sub == 1 ? zf : !zf));
+      }
+      if (taken) next = nrip + b;
+      break;
+    }
     case O_CALL:
       res = nrip;
       next = u.bsrc == L_IMM ? nrip + b : b;

@@ -695,6 +695,7 @@ void GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first
         if (!v.result) v.result = Crash_t();
         if (e.status == WTFGPU_EXIT_UNIMPLEMENTED) {
           stats_.err_unimpl++;
+          stats_.unimpl_ops.add(e.opcode);
           stats_.last_unimpl_op = e.opcode;
           stats_.last_unimpl_rip = e.rip;
         } else if (e.status == WTFGPU_EXIT_OVERLAY_FULL) {
@@ -1462,6 +1463,9 @@ std::string GpuBackend_t::StatsJson() const {
   snprintf(b, sizeof(b), ",\"up_prep_ms\":%.3f,\"up_regs_ms\":%.3f,\"up_apply_ms\":%.3f,\"up_feed_ms\":%.3f,"
            "\"restore_dev_ms\":%.3f", stats_.up_prep_ms, stats_.up_regs_ms, stats_.up_apply_ms, stats_.up_feed_ms,
            stats_.restore_dev_ms);
+  r += b;
+  r += ",\"unimpl_ops\":" + stats_.unimpl_ops.json();
+  b[0] = 0;
   r += b;
   r += ",\"fetch_by_bp\":{";
   bool first = true;

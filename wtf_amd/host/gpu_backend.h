@@ -13,6 +13,7 @@
 //    the lane (registers gathered in bulk, pages fetched on demand or
 //    prefetched for the stack, writes staged and applied in bulk).
 #pragma once
+#include "unimpl_hist.h"
 #include <atomic>
 #include <memory>
 #include <mutex>
@@ -53,6 +54,7 @@ struct BatchStats {
   double run_ms = 0, exits_ms = 0, regs_ms = 0;
   // engine errors by exit status, the last unimplemented opcode and its rip
   std::atomic<uint64_t> err_unimpl{0}, err_overlay{0}, err_other{0};
+  UnimplHist unimpl_ops;  // opcode histogram of the UNIMPLEMENTED exits
   std::atomic<uint64_t> last_unimpl_op{0}, last_unimpl_rip{0};
 };
 

@@ -13,9 +13,10 @@
  * rcx) into a flat image placed in the snapshot by wtf_amd/tools/tlv.py.
  * The heap is a page heap: every allocation ends at the end of its own page,
  * followed by an unmapped guard page, so overflows fault like under a
- * page-heap-enabled Windows process; a bad free calls the security-check
- * failure routine (what __fastfail reaches in the kernel,
- * nt!KiRaiseSecurityCheckFailure, crash_detection_umode.cc:135-150).
+ * page-heap-enabled Windows process; a bad free is a __fastfail: `int 0x29`
+ * with the failure code in ecx, which the snapshot's IDT (gate 0x29, DPL 3)
+ * delivers to nt!KiRaiseSecurityCheckFailure in ring 0 with the address after
+ * the int at [rsp] (crash_detection_umode.cc:131-152).
  */
 #include "sse_rt.h"
 typedef unsigned long long u64;
@@ -42,11 +43,16 @@ struct Chunk {
   u8 *Buf;
 };
 
-/* One object so the layout is fixed: the entry past ChunkList is the heap's
- * free-list head (what a write past the table lands on in this image). */
+/* One object so the layout is fixed: the entry past ChunkList is LastFreed,
+ * a stale pointer to the buffer of the chunk deleted last (what a write past
+ * the table lands on in this image): Allocate into a full table deletes it as
+ * a Chunk, freeing whatever its bytes 8..15 hold, and the heap's free check
+ * fails fast on a pointer it does not own. */
 struct Globals {
   struct Chunk *ChunkList[4];
+  struct Chunk *LastFreed;
   u64 FreeHead; /* 1 + index of the first free slot, 0 = none */
+  u64 InUse;    /* bit per slot: allocated */
   u64 Initialised;
 };
 struct Globals G;
@@ -56,7 +62,6 @@ __attribute__((noipa, used)) int printf(const char *Format, ...) {
   (void)Format;
   return 0;
 }
-__attribute__((noipa, used, naked)) void KiRaiseSecurityCheckFailure(void) { __asm__ volatile("hlt"); }
 __attribute__((noipa, used, naked)) void RtlDispatchException(void) { __asm__ volatile("hlt"); }
 __attribute__((noipa, used, naked)) void KeBugCheck2(void) { __asm__ volatile("hlt"); }
 __attribute__((noipa, used, naked)) void SwapContext(void) { __asm__ volatile("hlt"); }
@@ -69,6 +74,7 @@ static void heap_init(void) {
   /* free list threaded through the first 8 bytes of each slot page */
   for (u64 i = 0; i < HEAP_SLOTS; i++) *(u64 *)slot_page(i) = (i + 1 < HEAP_SLOTS) ? i + 2 : 0;
   G.FreeHead = 1;
+  G.InUse = 0;
   G.Initialised = 1;
 }
 
@@ -78,6 +84,7 @@ __attribute__((noinline)) static void *Malloc(u64 Size) {
   const u64 Slot = G.FreeHead - 1;
   u8 *Page = slot_page(Slot);
   G.FreeHead = *(u64 *)Page;
+  G.InUse |= 1ull << Slot;
   *(u64 *)Page = 0;
   u8 *P = (u8 *)(((u64)Page + 0x1000 - Size) & ~7ull);
   sse_fill(P, 0, Size);
@@ -87,10 +94,13 @@ __attribute__((noinline)) static void *Malloc(u64 Size) {
 __attribute__((noinline)) static void Free(void *P) {
   if (!P) return;
   const u64 Off = (u64)P - HEAP_BASE;
-  if ((u64)P < HEAP_BASE || Off >= HEAP_SLOTS * HEAP_STRIDE || (Off & 0x1fff) >= 0x1000) {
-    KiRaiseSecurityCheckFailure(); /* heap corruption: __fastfail */
-    return;
+  if ((u64)P < HEAP_BASE || Off >= HEAP_SLOTS * HEAP_STRIDE || (Off & 0x1fff) >= 0x1000 ||
+      !((G.InUse >> (Off / HEAP_STRIDE)) & 1)) {
+    /* a block the heap does not own (a double free): __fastfail(FAST_FAIL_INVALID_FREE) */
+    __asm__ volatile("mov $0x3e, %%ecx\n\tint $0x29" ::: "rcx", "memory");
+    __builtin_unreachable();
   }
+  G.InUse &= ~(1ull << (Off / HEAP_STRIDE));
   u8 *Page = slot_page(Off / HEAP_STRIDE);
   *(u64 *)Page = G.FreeHead;
   G.FreeHead = Off / HEAP_STRIDE + 1;
@@ -100,8 +110,10 @@ static void Memcpy(u8 *Dst, const u8 *Src, u64 Size) { sse_copy(Dst, Src, Size);
 
 static void DeleteChunk(struct Chunk *C) {
   if (!C) return;
-  Free(C->Buf);
+  u8 *Buf = C->Buf;
+  Free(Buf);
   Free(C);
+  G.LastFreed = (struct Chunk *)Buf;
 }
 
 /* tlv_server.cc:31-94 */

@@ -16,6 +16,14 @@ Layout (guest virtual):
   0x200000000  page heap: 64 slots of [page rw-][guard, unmapped]
   0x300000000  packet page (rw-), 0x300001000 guard (unmapped)
   STACK_TOP-0x4000 .. STACK_TOP   stack (rw-)
+  0xFFFFF80000004000  IDT (supervisor): gate 0x29 only (64-bit interrupt gate,
+                      DPL 3) -> nt!KiRaiseSecurityCheckFailure
+  0xFFFFF80000002000  TSS (RSP0 = the kernel stack)
+  0xFFFFF80000100000  nt!KiRaiseSecurityCheckFailure (supervisor code: hlt)
+  0xFFFFF80000300000  kernel stack, 2 pages (supervisor rw-)
+The guest's __fastfail (`int 0x29`, tlv_server.c Free) reaches the kernel
+routine through that gate, as on Windows; no other vector has a gate, so a
+fault ends the testcase with the fault (user-mode crash naming, U14).
 """
 from __future__ import annotations
 
@@ -34,6 +42,11 @@ HEAP_SLOTS = 64
 HEAP_STRIDE = 0x2000
 PACKET_VA = 0x300000000
 STACK_TOP = 0x7FF000000000
+IDT = 0xFFFFF80000004000     # user_state's idtr
+TSS = 0xFFFFF80000002000     # user_state's tr.base
+KI_RAISE = 0xFFFFF80000100000
+KSTACK = 0xFFFFF80000300000
+FASTFAIL_VECTOR = 0x29
 # gcc's default x86-64 code generation (SSE2 baseline): the engine runs the
 # SSE / SSE2 subset (U22), so the guests are not restricted to general registers
 CFLAGS = ["-O2", "-ffreestanding", "-fpie", "-fvisibility=hidden", "-mabi=ms",
@@ -84,10 +97,11 @@ def build(state_dir: str, work_dir: str | None = None) -> dict:
         assert vaddr % PAGE == 0
         img = data + b"\0" * (memsz - len(data))
         if vaddr == syms["G"] & ~0xFFF:
-            # heap ready at snapshot time: free list 1 -> 2 -> ... -> 64, G.Initialised = 1
+            # heap ready at snapshot time: free list 1 -> 2 -> ... -> 64, nothing in
+            # use, no chunk freed yet, G.Initialised = 1 (tlv_server.c struct Globals)
             goff = syms["G"] - vaddr
-            img = bytearray(img.ljust(goff + 0x30, b"\0"))
-            struct.pack_into("<QQ", img, goff + 0x20, 1, 1)
+            img = bytearray(img.ljust(goff + 0x40, b"\0"))
+            struct.pack_into("<QQQQ", img, goff + 0x20, 0, 1, 0, 1)
             img = bytes(img)
         sp.map_range(vaddr, img, user=True, write=bool(flags & 2), nx=not (flags & 1))
     for i in range(HEAP_SLOTS):
@@ -96,6 +110,17 @@ def build(state_dir: str, work_dir: str | None = None) -> dict:
     sp.map(PACKET_VA, b"", nx=True)
     for va in range(STACK_TOP - 0x4000, STACK_TOP, PAGE):
         sp.map(va, b"", nx=True)
+    # ring 0 pieces the __fastfail path runs through (SDM vol. 3 6.14)
+    sp.map(KI_RAISE, b"\xf4" * 16, user=False, write=False, nx=False)
+    idt = bytearray(PAGE)
+    lo = (KI_RAISE & 0xFFFF) | (0x10 << 16) | (0xEE << 40) | (((KI_RAISE >> 16) & 0xFFFF) << 48)
+    struct.pack_into("<QQ", idt, FASTFAIL_VECTOR * 16, lo, KI_RAISE >> 32)
+    sp.map(IDT, bytes(idt), user=False, write=False, nx=True)
+    tss = bytearray(PAGE)
+    struct.pack_into("<Q", tss, 4, KSTACK + 2 * PAGE - 0x40)  # RSP0
+    sp.map(TSS, bytes(tss), user=False, nx=True)
+    for i in range(2):
+        sp.map(KSTACK + i * PAGE, b"", user=False, nx=True)
     rsp = STACK_TOP - 0x108  # rsp = 8 mod 16 at function entry
     sp.write(rsp, struct.pack("<Q", syms["ServerLoopReturn"]))
     st = user_state(syms["ProcessPacket"], rsp, sp.cr3, rcx=PACKET_VA, rdx=0x1000)
@@ -108,7 +133,7 @@ def build(state_dir: str, work_dir: str | None = None) -> dict:
         "nt!KeBugCheck2": syms["KeBugCheck2"],
         "nt!SwapContext": syms["SwapContext"],
         "ntdll!RtlDispatchException": syms["RtlDispatchException"],
-        "nt!KiRaiseSecurityCheckFailure": syms["KiRaiseSecurityCheckFailure"],
+        "nt!KiRaiseSecurityCheckFailure": KI_RAISE,
         "verifier": 0,
     }
     write_snapshot(state_dir, sp, st, symbols)
