@@ -76,7 +76,10 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
   std::vector<uint8_t> map_, shadow_;
   void map_set(uint64_t rip) {
     auto it = slot_.find(rip >> 12);
-    if (it == slot_.end()) return;
+    if (it == slot_.end()) {  // outside the map: the overflow list other shards gather
+      extra_new_.push_back(rip);
+      return;
+    }
     const uint64_t at = (uint64_t)it->second * 4096 + (rip & 0xfff);
     map_[at] = shadow_[at] = 1;
   }
@@ -112,6 +115,7 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
   // bochscpu_backend.cc:352-410 (+ the handler dispatch of :476-548)
   std::optional<TestcaseResult_t> Run(const uint8_t *, const uint64_t) override {
     flush();
+    engine_error_ = false;
     int skip = 0;
     for (;;) {
       wtfgpu_exit_t e{};
@@ -274,6 +278,16 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
     *Device = false;
     return true;
   }
+  void TakeNewExtra(std::vector<uint64_t> &Out) override {
+    Out.swap(extra_new_);
+    extra_new_.clear();
+  }
+  size_t AbsorbExtra(const std::vector<uint64_t> &All) override {
+    size_t added = 0;
+    for (uint64_t v : All) added += aggregate_.insert(v).second;
+    return added;
+  }
+  std::vector<uint64_t> extra_new_;  // aggregate values outside the map since TakeNewExtra
   size_t AbsorbCoverageMap() override {
     size_t added = 0;
     for (size_t i = 0; i < map_.size(); i++)
@@ -283,6 +297,7 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
       }
     return added;
   }
+  uint64_t Icount() const { return orc_icount(m_); }
   bool full_ = false;
   bool engine_error_ = false;
   UnimplHist unimpl_;  // WTF_UNIMPL_HIST=1: printed to stderr at exit
@@ -377,7 +392,11 @@ int main(int argc, char **argv) {
     std::string StatsJson() const override { return b->StatsJson(); }
     bool CoverageMap(uint8_t **M, uint64_t *N, bool *D) override { return b->CoverageMap(M, N, D); }
     size_t AbsorbCoverageMap() override { return b->AbsorbCoverageMap(); }
+    void TakeNewExtra(std::vector<uint64_t> &O) override { b->TakeNewExtra(O); }
+    size_t AbsorbExtra(const std::vector<uint64_t> &A) override { return b->AbsorbExtra(A); }
     bool EnableTrace(uint32_t P) override { return b->EnableTrace(P); }
+    uint64_t LastIcount() const override { return b->Icount(); }
+    bool LastError() const override { return b->engine_error_; }
     bool LaneTrace(uint32_t L, std::vector<uint64_t> &R, bool &T) override { return b->LaneTrace(L, R, T); }
   } E;
   E.b = B;

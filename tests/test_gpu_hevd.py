@@ -12,6 +12,7 @@ from tests.hevd_inputs import write_inputs
 pytestmark = pytest.mark.gpu
 
 FIELDS = ("result", "crash", "error", "icount", "gprs", "coverage")
+LIMIT = 10_000_000  # BASELINE.md / README.md:58: HEVD runs --limit 10000000
 
 
 @pytest.fixture(scope="module")
@@ -24,8 +25,8 @@ def target(tmp_path_factory):
 
 def test_hevd_full_coverage_parity(target, tmp_path):
     inp = os.path.join(target, "parity")
-    g = H.run(H.WTFGPU, target, inp, str(tmp_path / "g.jsonl"), lanes=512, name="hevd")
-    t = H.run(H.TWIN, target, inp, str(tmp_path / "t.jsonl"), lanes=512, name="hevd")
+    g = H.run(H.WTFGPU, target, inp, str(tmp_path / "g.jsonl"), lanes=512, name="hevd", limit=LIMIT)
+    t = H.run(H.TWIN, target, inp, str(tmp_path / "t.jsonl"), lanes=512, name="hevd", limit=LIMIT)
     assert len(g) == len(t) == len(os.listdir(inp))
     bad = []
     for x, y in zip(g, t):
@@ -45,9 +46,9 @@ def test_hevd_parity_host_handlers_only(target, tmp_path):
     """nt!DbgPrintEx carries a device-side SimulateReturn action; with device
     actions off every hit is a host handler. Both must match the twin."""
     inp = os.path.join(target, "parity")
-    h = H.run(H.WTFGPU, target, inp, str(tmp_path / "h.jsonl"), lanes=512, name="hevd",
+    h = H.run(H.WTFGPU, target, inp, str(tmp_path / "h.jsonl"), lanes=512, name="hevd", limit=LIMIT,
               env={"WTFGPU_DEVICE_BP_ACTIONS": "0"})
-    t = H.run(H.TWIN, target, inp, str(tmp_path / "t.jsonl"), lanes=512, name="hevd")
+    t = H.run(H.TWIN, target, inp, str(tmp_path / "t.jsonl"), lanes=512, name="hevd", limit=LIMIT)
     bad = [(x["input"], k) for x, y in zip(h, t) for k in FIELDS if x[k] != y[k]]
     assert len(h) == len(t) and not bad, bad[:10]
 
@@ -58,13 +59,13 @@ def test_hevd_streaming_parity(target, tmp_path, slice_steps, regroup):
     Stop, DbgPrintEx), host-serviced breakpoints (KeBugCheck2, SwapContext) and
     ring-0 paths, with and without cross-wave regrouping: every input as the twin."""
     inp = os.path.join(target, "parity")
-    g = H.run(H.WTFGPU, target, inp, str(tmp_path / "g.jsonl"), lanes=256, name="hevd",
+    g = H.run(H.WTFGPU, target, inp, str(tmp_path / "g.jsonl"), lanes=256, name="hevd", limit=LIMIT,
               extra=("--stream-run", "--slice-steps", str(slice_steps), "--regroup-steps", str(regroup)))
-    t = H.run(H.TWIN, target, inp, str(tmp_path / "t.jsonl"), lanes=512, name="hevd")
+    t = H.run(H.TWIN, target, inp, str(tmp_path / "t.jsonl"), lanes=512, name="hevd", limit=LIMIT)
     bad = [(x["input"], k) for x, y in zip(g, t) for k in FIELDS if x[k] != y[k]]
     assert len(g) == len(t) and not bad, bad[:10]
 
 
 def test_hevd_fuzz_smoke(target):
-    st = H.fuzz(H.WTFGPU, target, runs=8192, lanes=4096, name="hevd", max_len=1028)
+    st = H.fuzz(H.WTFGPU, target, runs=8192, lanes=4096, name="hevd", max_len=1028, limit=LIMIT)
     assert st["execs"] == 8192 and st["errors"] == 0

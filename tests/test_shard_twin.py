@@ -71,3 +71,44 @@ def test_two_twin_shards_merge_coverage(base, tmp_path):
     shutil.copytree(base, solo, ignore=shutil.ignore_patterns("outputs", "crashes", "work"))
     one = subprocess.run(_fuzz_cmd(solo, 0, 1, port), capture_output=True, text=True, timeout=300, check=True)
     assert _last_json(one.stdout)["coverage"] <= res[0]["coverage"]
+
+
+def test_two_twin_shards_merge_edges_outside_the_map(base, tmp_path):
+    """--edges: branch edge values live outside the code-page map (SURVEY
+    8(e)'s overflow list); every merge all-gathers each shard's new ones
+    (CoverageExchange_t::AllGatherV) and both shards end with the same
+    aggregate, edges included."""
+    dirs = []
+    for r in range(2):
+        d = str(tmp_path / f"e{r}")
+        shutil.copytree(base, d, ignore=shutil.ignore_patterns("outputs", "crashes", "work"))
+        dirs.append(d)
+    port = _free_port()
+    procs = [subprocess.Popen(_fuzz_cmd(dirs[r], r, 2, port, runs=2048) + ["--edges", "--seed", str(1337 + r)],
+                              stdout=subprocess.PIPE, text=True) for r in range(2)]
+    res = [_last_json(p.communicate(timeout=300)[0]) for p in procs]
+    assert all(p.returncode == 0 for p in procs)
+    assert res[0]["coverage"] == res[1]["coverage"]
+    # edges make the aggregate larger than the rips alone
+    solo = str(tmp_path / "solo_noedges")
+    shutil.copytree(base, solo, ignore=shutil.ignore_patterns("outputs", "crashes", "work"))
+    one = subprocess.run(_fuzz_cmd(solo, 0, 1, port, runs=2048), capture_output=True, text=True, timeout=300,
+                         check=True)
+    assert res[0]["coverage"] > _last_json(one.stdout)["coverage"]
+
+
+def test_shards_stopping_at_different_times(base, tmp_path):
+    """--seconds budgets that end at different moments: a finished shard keeps
+    joining the other's merges (Done() is read once per step) until every
+    shard is done; neither hangs nor mismatches a collective."""
+    dirs = []
+    for r in range(2):
+        d = str(tmp_path / f"t{r}")
+        shutil.copytree(base, d, ignore=shutil.ignore_patterns("outputs", "crashes", "work"))
+        dirs.append(d)
+    port = _free_port()
+    cmds = [_fuzz_cmd(dirs[r], r, 2, port, runs=0, lanes=64) + ["--seconds", str(1.0 + 2.0 * r)] for r in range(2)]
+    procs = [subprocess.Popen(c, stdout=subprocess.PIPE, text=True) for c in cmds]
+    res = [_last_json(p.communicate(timeout=120)[0]) for p in procs]
+    assert all(p.returncode == 0 for p in procs)
+    assert res[0]["coverage"] == res[1]["coverage"]

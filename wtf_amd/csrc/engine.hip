@@ -1791,12 +1791,19 @@ void dfree(T *&p) {
   p = nullptr;
 }
 
+// The current queue's device scratch, at least `bytes`. Growth is geometric
+// and stream-ordered (hipFreeAsync / hipMallocAsync on the queue's stream):
+// the old buffer is released after the queue's earlier work that reads it
+// (e.g. an asynchronous k_feed_scatter) and nothing synchronises the device,
+// so the other queue's k_run slice keeps running.
 int ensure_scratch(wtfgpu_ctx *c, u64 bytes) {
   if (c->scratch_bytes >= bytes) return WTFGPU_OK;
-  dfree(c->d_scratch);
+  const u64 want = std::max<u64>(std::max<u64>(bytes, 2 * c->scratch_bytes), 1ull << 20);
+  if (c->d_scratch) HIPCHK(hipFreeAsync(c->d_scratch, c->stream));
+  c->d_scratch = nullptr;
   c->scratch_bytes = 0;
-  if (dalloc(&c->d_scratch, bytes)) return WTFGPU_ERR_OOM;
-  c->scratch_bytes = bytes;
+  if (hipMallocAsync((void **)&c->d_scratch, want, c->stream) != hipSuccess) return WTFGPU_ERR_OOM;
+  c->scratch_bytes = want;
   return WTFGPU_OK;
 }
 

@@ -1046,6 +1046,8 @@ void GpuBackend_t::finish_coverage(uint32_t n, std::vector<LaneResult> *out, std
     per[l].erase(std::unique(per[l].begin(), per[l].end()), per[l].end());
     if (full_coverage_) {
       if (out) (*out)[l].new_coverage = per[l];
+      if (n == 1)
+        for (uint64_t rip : per[l]) last_new_coverage_.insert(Gva_t(rip));
       continue;
     }
     const bool revoke = timedout && std::find(timedout->begin(), timedout->end(), l) != timedout->end();
@@ -1062,7 +1064,7 @@ void GpuBackend_t::finish_coverage(uint32_t n, std::vector<LaneResult> *out, std
     wtfgpu_reset_coverage(ctx_);
     return;
   }
-  if (!fresh.empty()) wtfgpu_commit_coverage(ctx_, fresh.data(), fresh.size());
+  commit_fresh(fresh);
 }
 
 // bochscpu_backend.cc:352-410: one testcase on lane 0; the caller already ran
@@ -1073,8 +1075,14 @@ std::optional<TestcaseResult_t> GpuBackend_t::Run(const uint8_t *, const uint64_
   if (flush_lanes({0}) || upload_feed(1)) return std::nullopt;
   std::vector<LaneResult> out(1);
   if (!run_lanes({0}, &out, nullptr, false)) return std::nullopt;
-  std::vector<uint32_t> to;
-  if (std::holds_alternative<Timedout_t>(out[0].result)) to.push_back(0);
+  // the lane's final registers back into its view: GetReg after Run reads
+  // them (the client's own code and Target.Restore may do so)
+  LaneView &v = views_[0];
+  if (wtfgpu_read_gprs_list(ctx_, &cur_, 1, v.gpr)) return std::nullopt;
+  v.regs_dirty = false;
+  v.cr_known = 0;
+  last_icount_ = out[0].icount;
+  last_error_ = out[0].error;
   finish_coverage(1, nullptr, nullptr);  // Timedout revocation is the client's call (RevokeLastNewCoverage)
   stats_.total_ms += ms_since(t0);
   cur_ = 0;
@@ -1246,7 +1254,7 @@ void GpuBackend_t::collect_coverage(const std::vector<uint32_t> &lanes, std::vec
       fresh.push_back(rip);
     }
   }
-  if (!fresh.empty()) wtfgpu_commit_coverage(ctx_, fresh.data(), fresh.size());
+  commit_fresh(fresh);
   stats_.attrib_ms += ms_since(t1);
 }
 
@@ -1483,6 +1491,8 @@ std::string GpuBackend_t::StatsJson() const {
 // every GPU, so the maps can be merged with a MAX all-reduce.
 bool GpuBackend_t::set_code_pages() {
   const std::vector<uint64_t> vpns = ExecutablePages(dump_, initial_.Cr3);
+  code_vpns_.clear();
+  code_vpns_.insert(vpns.begin(), vpns.end());
   if (vpns.empty()) return true;
   return wtfgpu_set_code_pages(ctx_, vpns.data(), (uint32_t)vpns.size()) == WTFGPU_OK;
 }
@@ -1505,6 +1515,31 @@ size_t GpuBackend_t::AbsorbCoverageMap() {
   size_t added = 0;
   for (uint64_t i = 0; i < n && i < rips.size(); i++) added += aggregate_.insert(rips[i]).second;
   return added;
+}
+
+// New aggregate values go to the device map (code pages) or its extra set
+// (wtfgpu_commit_coverage); the ones outside the map are also kept for the
+// cross-shard overflow merge.
+void GpuBackend_t::commit_fresh(const std::vector<uint64_t> &fresh) {
+  if (fresh.empty()) return;
+  for (uint64_t v : fresh)
+    if (!code_vpns_.count(v >> 12)) extra_new_.push_back(v);
+  wtfgpu_commit_coverage(ctx_, fresh.data(), fresh.size());
+}
+
+void GpuBackend_t::TakeNewExtra(std::vector<uint64_t> &Out) {
+  Out.swap(extra_new_);
+  extra_new_.clear();
+}
+
+// Other shards' values outside the map join the aggregate and the device set
+// (so lanes stop logging them); returns how many were new here.
+size_t GpuBackend_t::AbsorbExtra(const std::vector<uint64_t> &All) {
+  std::vector<uint64_t> add;
+  for (uint64_t v : All)
+    if (aggregate_.insert(v).second) add.push_back(v);
+  if (!add.empty()) wtfgpu_commit_coverage(ctx_, add.data(), add.size());
+  return add.size();
 }
 
 }  // namespace wtfgpu_host

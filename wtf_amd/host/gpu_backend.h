@@ -106,7 +106,11 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   void ResetCoverage() override;
   void SetFullCoverage(bool On) override { full_coverage_ = On; }
   void SetWantRegisters(bool On) override { want_gprs_ = On; }
+  uint64_t LastIcount() const override { return last_icount_; }
+  bool LastError() const override { return last_error_; }
   size_t CoverageSize() const override { return aggregate_.size(); }
+  void TakeNewExtra(std::vector<uint64_t> &Out) override;
+  size_t AbsorbExtra(const std::vector<uint64_t> &All) override;
   std::string StatsJson() const override;
   bool CoverageMap(uint8_t **Map, uint64_t *Bytes, bool *Device) override;
   size_t AbsorbCoverageMap() override;
@@ -204,6 +208,8 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   std::vector<uint64_t> cov_rips_;
   bool cov_ovf_warned_ = false;
   bool want_gprs_ = true;
+  uint64_t last_icount_ = 0;  // of the last Run
+  bool last_error_ = false;
   // streaming parts (see parts_n): lane range, slice in flight, its occupied
   // lanes, exit read-back, pinned staging of the part's feeds
   struct Part {
@@ -240,6 +246,9 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   bool feed_action_ = false;                     // a Feed action is on the device
   int upload_feed(uint32_t n);                   // lanes [0, n)
   std::unordered_set<uint64_t> aggregate_;
+  std::unordered_set<uint64_t> code_vpns_;  // the map's pages (set_code_pages)
+  std::vector<uint64_t> extra_new_;         // aggregate values outside them since TakeNewExtra
+  void commit_fresh(const std::vector<uint64_t> &fresh);
   std::unordered_set<Gva_t> last_new_coverage_;
   mutable BatchStats stats_;
   // staging arena: blocks of slots, each slot a pinned 4 KiB page (device

@@ -127,4 +127,28 @@ bool TcpExchange_t::AllDone(bool Mine, bool *All) {
   return true;
 }
 
+// rank 0 concatenates every rank's list in rank order and sends it back
+bool TcpExchange_t::AllGatherV(const std::vector<uint64_t> &Mine, std::vector<uint64_t> &All) {
+  All = Mine;
+  if (world_ <= 1) return true;
+  std::vector<uint8_t> buf;
+  if (rank_ != 0) {
+    if (!send_frame(peers_[0], (const uint8_t *)Mine.data(), Mine.size() * 8) || !recv_frame(peers_[0], buf) ||
+        buf.size() % 8)
+      return false;
+    All.resize(buf.size() / 8);
+    memcpy(All.data(), buf.data(), buf.size());
+    return true;
+  }
+  for (int r = 1; r < world_; r++) {
+    if (!recv_frame(peers_[r], buf) || buf.size() % 8) return false;
+    const size_t at = All.size();
+    All.resize(at + buf.size() / 8);
+    memcpy(All.data() + at, buf.data(), buf.size());
+  }
+  for (int r = 1; r < world_; r++)
+    if (!send_frame(peers_[r], (const uint8_t *)All.data(), All.size() * 8)) return false;
+  return true;
+}
+
 }  // namespace wtfgpu_host

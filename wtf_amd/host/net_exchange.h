@@ -18,6 +18,7 @@ class TcpExchange_t final : public CoverageExchange_t {
   int World() const override { return world_; }
   bool AllReduceMax(uint8_t *Map, uint64_t Bytes, bool Device) override;
   bool AllDone(bool Mine, bool *All) override;
+  bool AllGatherV(const std::vector<uint64_t> &Mine, std::vector<uint64_t> &All) override;
 
  private:
   int rank_, world_;

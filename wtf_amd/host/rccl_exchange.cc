@@ -1,11 +1,15 @@
 // rccl_exchange.cc — CoverageExchange_t for GPU shards: one RCCL
 // communicator over the node's GPUs (xGMI), an in-place
-// ncclAllReduce(uint8, ncclMax) of the device coverage map on the engine's
-// stream. The unique id travels out of band: through a file
+// ncclAllReduce(uint8, ncclMax) of the device coverage map and
+// an all-gather of the values outside it. The collectives run on a stream of
+// their own: the engine's commits are synchronous, so the map is final when a
+// merge starts, and the host waits only for the collective, never for a k_run
+// slice another queue has in flight. The unique id travels out of band: through a file
 // (`wtfgpu fuzz --world n --rank r --nccl-id-file f`, rank 0 writes it) or
 // from the caller (libwtfnode, bench.py broadcasts it).
 #include "rccl_exchange.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <filesystem>
@@ -19,8 +23,10 @@ namespace wtfgpu_host {
 
 struct RcclExchange_t::Impl {
   ncclComm_t comm = nullptr;
-  hipStream_t stream = nullptr;
-  uint8_t *flag = nullptr;  // device byte for AllDone
+  hipStream_t stream = nullptr;  // the collectives' own stream
+  uint8_t *flag = nullptr;       // device byte for AllDone
+  uint64_t *gbuf = nullptr;      // AllGatherV staging: world counts, then world * cap values
+  uint64_t gcap = 0;             // u64 slots in gbuf
 };
 
 bool RcclUniqueId(uint8_t Out[kRcclIdBytes]) {
@@ -57,12 +63,15 @@ RcclExchange_t::RcclExchange_t(int Rank, int World) : rank_(Rank), world_(World)
 RcclExchange_t::~RcclExchange_t() {
   if (impl_->comm) ncclCommDestroy(impl_->comm);
   if (impl_->flag) (void)hipFree(impl_->flag);
+  if (impl_->gbuf) (void)hipFree(impl_->gbuf);
+  if (impl_->stream) (void)hipStreamDestroy(impl_->stream);
   delete impl_;
 }
 
 bool RcclExchange_t::Init(const uint8_t Id[kRcclIdBytes], void *Stream) {
-  impl_->stream = (hipStream_t)Stream;
+  (void)Stream;  // the engine's stream: the collectives use their own (see above)
   if (world_ <= 1) return true;
+  if (hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking) != hipSuccess) return false;
   ncclUniqueId id;
   memcpy(&id, Id, sizeof(id));
   const ncclResult_t r = ncclCommInitRank(&impl_->comm, world_, id, rank_);
@@ -93,6 +102,46 @@ bool RcclExchange_t::AllDone(bool Mine, bool *All) {
       hipStreamSynchronize(impl_->stream) != hipSuccess)
     return false;
   *All = notdone == 0;
+  return true;
+}
+
+// counts first (one u64 per rank), then every list padded to the longest
+bool RcclExchange_t::AllGatherV(const std::vector<uint64_t> &Mine, std::vector<uint64_t> &All) {
+  All = Mine;
+  if (world_ <= 1) return true;
+  if (!impl_->comm) return false;
+  auto grow = [&](uint64_t slots) {
+    if (slots <= impl_->gcap) return true;
+    if (impl_->gbuf) (void)hipFree(impl_->gbuf);
+    impl_->gbuf = nullptr;
+    impl_->gcap = 0;
+    if (hipMalloc((void **)&impl_->gbuf, slots * 8) != hipSuccess) return false;
+    impl_->gcap = slots;
+    return true;
+  };
+  const uint64_t W = (uint64_t)world_;
+  std::vector<uint64_t> counts(W, 0);
+  uint64_t mine = Mine.size();
+  if (!grow(W + 1)) return false;
+  if (hipMemcpyAsync(impl_->gbuf + W, &mine, 8, hipMemcpyHostToDevice, impl_->stream) != hipSuccess ||
+      ncclAllGather(impl_->gbuf + W, impl_->gbuf, 1, ncclUint64, impl_->comm, impl_->stream) != ncclSuccess ||
+      hipMemcpyAsync(counts.data(), impl_->gbuf, W * 8, hipMemcpyDeviceToHost, impl_->stream) != hipSuccess ||
+      hipStreamSynchronize(impl_->stream) != hipSuccess)
+    return false;
+  uint64_t cap = 0;
+  for (uint64_t c : counts) cap = std::max(cap, c);
+  if (cap == 0) return true;  // every rank sees the same counts: all skip together
+  if (!grow(W * cap + cap)) return false;
+  uint64_t *send = impl_->gbuf + W * cap;
+  if ((mine && hipMemcpyAsync(send, Mine.data(), mine * 8, hipMemcpyHostToDevice, impl_->stream) != hipSuccess) ||
+      ncclAllGather(send, impl_->gbuf, cap, ncclUint64, impl_->comm, impl_->stream) != ncclSuccess)
+    return false;
+  std::vector<uint64_t> got(W * cap);
+  if (hipMemcpyAsync(got.data(), impl_->gbuf, W * cap * 8, hipMemcpyDeviceToHost, impl_->stream) != hipSuccess ||
+      hipStreamSynchronize(impl_->stream) != hipSuccess)
+    return false;
+  All.clear();
+  for (uint64_t r = 0; r < W; r++) All.insert(All.end(), got.begin() + r * cap, got.begin() + r * cap + counts[r]);
   return true;
 }
 

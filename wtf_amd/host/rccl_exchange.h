@@ -3,6 +3,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "runner.h"
 
@@ -25,6 +26,7 @@ class RcclExchange_t final : public CoverageExchange_t {
   int World() const override { return world_; }
   bool AllReduceMax(uint8_t *Map, uint64_t Bytes, bool Device) override;
   bool AllDone(bool Mine, bool *All) override;
+  bool AllGatherV(const std::vector<uint64_t> &Mine, std::vector<uint64_t> &All) override;
 
  private:
   struct Impl;

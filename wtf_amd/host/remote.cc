@@ -25,7 +25,7 @@ bool RemoteExecutor_t::Accept(int ListenFd, int Nodes, bool Batched) {
     if (N.Fd < 0) return false;
     if (Batched) {
       std::string Msg;
-      if (!wire::ReceiveFrame(N.Fd, Msg) || !wire::DecodeHello(Msg, N.Lanes)) {
+      if (!wire::ReceiveFrame(N.Fd, Msg, 4096) || !wire::DecodeHello(Msg, N.Lanes)) {
         printf("node %d: no batched hello\n", i);
         return false;
       }

@@ -153,6 +153,7 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
     else if (a == "--slice-steps") O.slice = strtoull(next("--slice-steps"), nullptr, 0);
     else if (a == "--regroup-steps") O.regroup = strtoull(next("--regroup-steps"), nullptr, 0);
     else if (a == "--stream-run") O.stream_run = true;
+    else if (a == "--serial") O.serial = true;
     else if (a == "--rank") O.rank = atoi(next("--rank"));
     else if (a == "--world") O.world = atoi(next("--world"));
     else if (a == "--exchange") O.exchange = next("--exchange");
@@ -160,6 +161,8 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
     else if (a == "--address") O.address = next("--address");
     else if (a == "--nodes") O.nodes = atoi(next("--nodes"));
     else if (a == "--batched") O.batched = true;
+    else if (a == "--sample") O.sample = next("--sample");
+    else if (a == "--sample-every") O.sample_every = strtoull(next("--sample-every"), nullptr, 0);
     else {
       fprintf(stderr, "unknown argument %s\n", a.c_str());
       return false;
@@ -278,6 +281,46 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
       for (size_t c = 0; c < Cov.size(); c++) fprintf(Out, "%s%llu", c ? "," : "", (unsigned long long)Cov[c]);
       fprintf(Out, "]}\n");
     };
+    if (O.serial && !Trace) {
+      // RunTestcaseAndRestore (client.cc:88-180) restated over the Backend_t
+      // interface: InsertTestcase -> Run -> a timeout's new coverage revoked
+      // (RevokeLastNewCoverage, :122-125) -> Target.Restore -> Backend.Restore.
+      // The module's globals are used as they are (one testcase at a time).
+      Backend_t *B = Exec.AsBackend();
+      static const Registers_t Order[18] = {
+          Registers_t::Rax, Registers_t::Rcx, Registers_t::Rdx, Registers_t::Rbx, Registers_t::Rsp, Registers_t::Rbp,
+          Registers_t::Rsi, Registers_t::Rdi, Registers_t::R8,  Registers_t::R9,  Registers_t::R10, Registers_t::R11,
+          Registers_t::R12, Registers_t::R13, Registers_t::R14, Registers_t::R15, Registers_t::Rip, Registers_t::Rflags};
+      for (const fs::path &In : Inputs) {
+        g_Backend = B;
+        const std::vector<uint8_t> Buf = ReadFile(In);
+        LaneResult L;
+        if (!Target->InsertTestcase(Buf.data(), Buf.size())) {
+          L.result = Crash_t("insert-testcase-failed");
+        } else {
+          const std::optional<TestcaseResult_t> Res = B->Run(Buf.data(), Buf.size());
+          if (!Res) {  // client.cc:112-115: a backend failure ends the client
+            printf("Run failed\n");
+            return 1;
+          }
+          L.result = *Res;
+          // printed as the batch path prints it: what the testcase found, even
+          // when a timeout then revokes it from the aggregate
+          for (const Gva_t &G : B->LastNewCoverage()) L.new_coverage.push_back(G.U64());
+          if (std::holds_alternative<Timedout_t>(*Res)) B->RevokeLastNewCoverage();
+          L.icount = Exec.LastIcount();
+          L.error = Exec.LastError();
+        }
+        for (int g = 0; g < 18; g++) L.gprs[g] = B->GetReg(Order[g]);
+        L.rip = L.gprs[16];
+        if (!Target->Restore() || !B->Restore(State)) {
+          printf("Restore failed\n");
+          return 1;
+        }
+        Retired += L.icount;
+        print(In, L);
+      }
+    }
     if (O.stream_run && Exec.CanStream() && !Trace) {
       // streaming replay: lanes refilled as testcases finish, results printed
       // in input order (parity with the batched replay, tests/test_gpu_tlv.py)
@@ -309,7 +352,8 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
         print(Inputs[i], Res[i]);
       }
     }
-    for (size_t b = O.stream_run && Exec.CanStream() && !Trace ? Inputs.size() : 0; b < Inputs.size(); b += N) {
+    for (size_t b = (O.stream_run && Exec.CanStream() && !Trace) || (O.serial && !Trace) ? Inputs.size() : 0;
+         b < Inputs.size(); b += N) {
       const size_t n = std::min<size_t>(N, Inputs.size() - b);
       std::vector<std::vector<uint8_t>> Bufs(n);
       std::vector<std::pair<const uint8_t *, size_t>> Tc(n);
@@ -412,10 +456,33 @@ FuzzSession::FuzzSession(const RunnerOptions &O, Executor_t &Exec, Target_t &Tar
 FuzzSession::~FuzzSession() {
   if (Next_.valid()) Next_.wait();
   Writer_.Flush();
+  if (Sample_) fclose(Sample_);
+}
+
+void FuzzSession::WriteSample(const uint8_t *Tc, size_t Size, const LaneResult &L) {
+  static const char *hex = "0123456789abcdef";
+  std::string H(2 * Size, '0');
+  for (size_t i = 0; i < Size; i++) {
+    H[2 * i] = hex[Tc[i] >> 4];
+    H[2 * i + 1] = hex[Tc[i] & 15];
+  }
+  std::vector<uint64_t> Cov = L.new_coverage;
+  std::sort(Cov.begin(), Cov.end());
+  fprintf(Sample_, "{\"tc\":\"%s\",\"result\":\"%s\",\"crash\":\"%s\",\"error\":%d,\"icount\":%llu,\"gprs\":[",
+          H.c_str(), TestcaseResultName(L.result).c_str(), json_escape(crash_name(L.result)).c_str(), (int)L.error,
+          (unsigned long long)L.icount);
+  for (int g = 0; g < 18; g++) fprintf(Sample_, "%s%llu", g ? "," : "", (unsigned long long)L.gprs[g]);
+  fprintf(Sample_, "],\"coverage\":[");
+  for (size_t c = 0; c < Cov.size(); c++) fprintf(Sample_, "%s%llu", c ? "," : "", (unsigned long long)Cov[c]);
+  fprintf(Sample_, "]}\n");
 }
 
 bool FuzzSession::Start() {
-  Exec_.SetWantRegisters(false);
+  Exec_.SetWantRegisters(!O_.sample.empty());
+  if (!O_.sample.empty()) {
+    Sample_ = fopen(O_.sample.c_str(), "w");
+    if (!Sample_) return false;
+  }
   fs::create_directories(T_ / "outputs");
   fs::create_directories(T_ / "crashes");
   if (Target_.CreateMutator) Mutator_ = Target_.CreateMutator(Rng_, O_.max_len);
@@ -549,9 +616,12 @@ TcBatch FuzzSession::MakeBatch(uint64_t n) {
 // master's bookkeeping in lane order (server.h:816-886) and, across shards,
 // the coverage-map merge.
 bool FuzzSession::Step() {
-  // a shard that is done keeps joining the other shards' merges
-  if (X_ && X_->World() > 1 && Done()) return MergeCoverage();
-  if (stream_) return StreamStep();
+  // Done() is read once per step: a shard that is done keeps joining the other
+  // shards' merges, and one that is not always reaches its own merge below
+  // (two reads could disagree under --seconds and skip a collective)
+  const bool done = Done();
+  if (X_ && X_->World() > 1 && done) return MergeCoverage();
+  if (stream_) return StreamStep(done);
   BatchRefs_.clear();
   for (const std::unique_ptr<TcArena> &A : Batch_)
     for (size_t i = 0; i < A->Count(); i++) BatchRefs_.push_back(TcRef{A.get(), (uint32_t)i});
@@ -583,8 +653,8 @@ bool FuzzSession::Step() {
 // ready queue, every occupied lane runs one slice, the finished testcases are
 // accounted. The producer mutates the next testcases meanwhile, from the
 // corpus as it stood before this step's results.
-bool FuzzSession::StreamStep() {
-  if (Done()) return true;
+bool FuzzSession::StreamStep(bool Done) {
+  if (Done) return true;
   const auto t_step = Clock::now();
   std::vector<StreamTestcase_t> In;
   const bool open = More(S_.execs);
@@ -659,6 +729,7 @@ bool FuzzSession::StreamStep() {
 
 // The master's bookkeeping of one result (server.h:816-886).
 void FuzzSession::Account(const uint8_t *Tc, size_t Size, const LaneResult &L, bool KnownCrash) {
+  if (Sample_ && S_.execs % std::max<uint64_t>(1, O_.sample_every) == 0) WriteSample(Tc, Size, L);
   S_.execs++;
   S_.retired += L.icount;
   if (L.error) {  // the engine could not finish it: neither a crash nor coverage
@@ -714,6 +785,12 @@ bool FuzzSession::MergeCoverage() {
   if (!Exec_.CoverageMap(&Map, &Bytes, &Device)) return false;
   if (Bytes && !X_->AllReduceMax(Map, Bytes, Device)) return false;
   S_.merged_rips += Exec_.AbsorbCoverageMap();
+  // the values outside the map (SURVEY 8(e)'s overflow list): every shard's
+  // new ones, gathered, joined on the host
+  std::vector<uint64_t> Mine, All;
+  Exec_.TakeNewExtra(Mine);
+  if (!X_->AllGatherV(Mine, All)) return false;
+  S_.merged_rips += Exec_.AbsorbExtra(All);
   S_.merge_ms += secs_since(t) * 1e3;
   return true;
 }

@@ -75,6 +75,9 @@ class Executor_t {
   virtual void SetFullCoverage(bool On) = 0;
   // LaneResult::gprs filled (run mode prints them; the fuzz loop does not read them)
   virtual void SetWantRegisters(bool) {}
+  // the retired count / engine-error flag of the last Backend_t::Run
+  virtual uint64_t LastIcount() const { return 0; }
+  virtual bool LastError() const { return false; }
   virtual size_t CoverageSize() const = 0;
   virtual std::string StatsJson() const { return "{}"; }
   // The coverage map over the executable-page slot table (one byte per code
@@ -89,6 +92,12 @@ class Executor_t {
   // Rips set in the map (after a merge) that the aggregate lacks join it;
   // returns how many.
   virtual size_t AbsorbCoverageMap() { return 0; }
+  // Coverage values outside the map (rips on pages outside the slot table,
+  // --edges values; SURVEY 8(e)'s overflow list): the ones this shard added
+  // to its aggregate since the last call are moved into Out; AbsorbExtra adds
+  // other shards' to the aggregate (and returns how many were new).
+  virtual void TakeNewExtra(std::vector<uint64_t> &Out) { Out.clear(); }
+  virtual size_t AbsorbExtra(const std::vector<uint64_t> &) { return 0; }
   // Rip traces (wtf run --trace-type rip / cov, SetTraceFile,
   // bochscpu_backend.cc:506-520): every testcase of the next RunBatch logs
   // the rips it is about to execute, PerLane at most; LaneTrace(i) is
@@ -108,6 +117,9 @@ class CoverageExchange_t {
   virtual bool AllReduceMax(uint8_t *Map, uint64_t Bytes, bool Device) = 0;
   // *All = every shard's Mine is true
   virtual bool AllDone(bool Mine, bool *All) = 0;
+  // All = the concatenation of every shard's Mine, in rank order (the
+  // overflow list of coverage values outside the map)
+  virtual bool AllGatherV(const std::vector<uint64_t> &Mine, std::vector<uint64_t> &All) = 0;
 };
 
 struct RunnerOptions {
@@ -140,6 +152,9 @@ struct RunnerOptions {
   // engine's default (WTFGPU_REGROUP_STEPS)
   uint64_t regroup = ~0ull;
   bool stream_run = false;  // run: replay the inputs through the streaming path
+  // run: the reference client's RunTestcaseAndRestore (client.cc:88-180), one
+  // testcase at a time through Backend_t::Run / Restore (no batching)
+  bool serial = false;
   int rank = 0, world = 1;         // fuzz: shard rank of world (one node per GPU)
   std::string exchange = "127.0.0.1:31337";  // TCP coverage exchange (CPU shards): rank 0 listens here
   std::string nccl_id_file;        // GPU shards: RCCL unique id file (rank 0 writes it)
@@ -147,6 +162,12 @@ struct RunnerOptions {
   std::string address;             // tcp://ip:port or unix://path
   int nodes = 1;                   // master: nodes to wait for
   bool batched = false;            // N testcases per round trip (else the reference's one)
+  // fuzz: every sample_every-th testcase (in accounting order) is written to
+  // `sample` as a JSON line (testcase bytes, result, crash name, retired
+  // count, final GPRs, new coverage) so a run at the bench's configuration
+  // can be replayed on the twin (tests/test_gpu_bench_parity.py)
+  std::string sample;
+  uint64_t sample_every = 0;
 };
 
 struct FuzzStats {
@@ -227,7 +248,9 @@ class FuzzSession {
   uint64_t Budget(uint64_t n) const;
   bool More(uint64_t done) const;
   bool MergeCoverage();
-  bool StreamStep();
+  void WriteSample(const uint8_t *Tc, size_t Size, const LaneResult &L);
+  FILE *Sample_ = nullptr;
+  bool StreamStep(bool Done);
   void Account(const uint8_t *Tc, size_t Size, const LaneResult &L, bool KnownCrash = false);
 
   const RunnerOptions O_;

@@ -216,9 +216,10 @@ bool SendFrame(int Fd, const std::string &Msg) {
   return all(Fd, &N, 4, true) && all(Fd, Msg.data(), Msg.size(), true);
 }
 
-bool ReceiveFrame(int Fd, std::string &Msg) {
+bool ReceiveFrame(int Fd, std::string &Msg, uint64_t MaxBytes) {
   uint32_t N = 0;
   if (!all(Fd, &N, 4, false)) return false;
+  if (N > MaxBytes) return false;  // as the reference's Receive rejects frames beyond its buffer (socket.cc:335-340)
   Msg.resize(N);
   return all(Fd, Msg.data(), N, false);
 }

@@ -109,7 +109,10 @@ int Accept(int ListenFd);
 int Dial(const std::string &Address);
 bool SendFrame(int Fd, const std::string &Msg);
 // false on a closed connection or an error
-bool ReceiveFrame(int Fd, std::string &Msg);
+// A frame longer than MaxBytes is refused (the peer is dropped), so a bad or
+// hostile length cannot force a huge allocation.
+constexpr uint64_t kMaxFrameBytes = 256ull << 20;
+bool ReceiveFrame(int Fd, std::string &Msg, uint64_t MaxBytes = kMaxFrameBytes);
 void Close(int Fd);
 
 }  // namespace wtfgpu_host::wire
