@@ -9,6 +9,7 @@
 // lane (tests/test_gpu_tlv.py), and it is the CPU baseline of the TLV bench
 // (one process per host core, bench.py). The product never links this file.
 #include "../wtf_amd/host/unimpl_hist.h"
+#include "../wtf_amd/host/module_instances.h"
 #include <cstdio>
 #include <cstring>
 #include <unordered_map>
@@ -123,9 +124,15 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
       skip = 0;
       if (e.status == WTFGPU_EXIT_BREAKPOINT) {
         const uint64_t rip0 = regs().rip;
-        auto it = bps_.find(rip0);
+        BreakpointHandler_t handler = nullptr;
+        if (route_) {
+          handler = route_->HandlerOf(route_lane_, rip0);  // the lane's module copy (module_instances.h)
+        } else {
+          const auto it = bps_.find(rip0);
+          if (it != bps_.end()) handler = it->second;
+        }
         inject_ = ~0ull;
-        if (it != bps_.end()) it->second(this);
+        if (handler) handler(this);
         flush();
         if (result_) break;
         skip = regs().rip == rip0;  // U10: a moved rip cancels the hooked instruction
@@ -198,6 +205,10 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
   uint64_t Rdrand() override;
   void PrintRunStats() override {}
   bool SetBreakpoint(const Gva_t Gva, const BreakpointHandler_t Handler) override {
+    if (ModuleInstances *I = ModuleInstances::Registering()) {  // a module copy's Init
+      I->AddHandler(Gva.U64(), Handler);
+      if (I->RegisteringIndex() > 0) return bps_.count(Gva.U64()) != 0;
+    }
     if (bps_.count(Gva.U64())) return false;
     bps_[Gva.U64()] = Handler;
     std::vector<uint64_t> v;
@@ -298,6 +309,8 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
     return added;
   }
   uint64_t Icount() const { return orc_icount(m_); }
+  const ModuleInstances *route_ = nullptr;  // RunBatch over per-lane module copies
+  uint32_t route_lane_ = 0;
   bool full_ = false;
   bool engine_error_ = false;
   UnimplHist unimpl_;  // WTF_UNIMPL_HIST=1: printed to stderr at exit
@@ -316,14 +329,17 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
     return true;
   }
   bool RunBatch(const Target_t &Target, const std::vector<std::pair<const uint8_t *, size_t>> &Tc,
-                std::vector<LaneResult> &Out, ModuleSlots *) override {
+                std::vector<LaneResult> &Out, ModuleSlots *Slots) override {
     Out.assign(Tc.size(), LaneResult{});
+    route_ = Slots ? Slots->Instances() : nullptr;
     if (trace_cap_) traces_.assign(Tc.size(), {});
     g_Backend = this;
     for (size_t i = 0; i < Tc.size(); i++) {
       LaneResult &L = Out[i];
       Restore(initial_);
-      if (!Target.InsertTestcase(Tc[i].first, Tc[i].second)) result_ = Crash_t("insert-testcase-failed");
+      route_lane_ = (uint32_t)i;
+      const Target_t &T = route_ ? route_->TargetOf((uint32_t)i) : Target;
+      if (!T.InsertTestcase(Tc[i].first, Tc[i].second)) result_ = Crash_t("insert-testcase-failed");
       std::optional<TestcaseResult_t> R;
       if (result_) {
         R = result_;
@@ -352,9 +368,10 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
         T.resize(orc_trace(m_, nullptr, 0));
         orc_trace(m_, T.data(), T.size());
       }
-      Target.Restore();
+      T.Restore();
     }
     Restore(initial_);
+    route_ = nullptr;
     return true;
   }
   std::string StatsJson() const override {

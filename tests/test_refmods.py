@@ -14,11 +14,14 @@ device-side breakpoint actions, so on the GPU every one of its breakpoints is a
 host round trip (the host service path, exercised by an unmodified module).
 
 The reference's fuzzer_tlv_server.cc keeps its packet queue in a plain
-global: it is linked the same way and runs unchanged wherever one testcase is
-in flight at a time (the twin; the gpu node at one lane per batch), and must
-match the restated module there. Batching it over many lanes needs the
-one-line WTF_LANE_STATE annotation (module_slots.h). Malformed-JSON inputs are
-left out: the reference module throws on them (nlohmann parse, uncaught).
+global: linked into the executable it runs unchanged wherever one testcase is
+in flight at a time (the twin; the gpu node at one lane per batch). Batched,
+it runs unchanged too as per-lane copies (module_instances.h):
+oracle/Makefile also builds it as oracle/_ref/fuzzer_tlv_server_ref.so, and
+`--module-so` loads one private copy per lane (own globals, own handlers),
+512 lanes per batch on the GPU. Either way it must match the restated module.
+Malformed-JSON inputs are left out: the reference module throws on them
+(nlohmann parse, uncaught).
 """
 import os
 import subprocess
@@ -32,6 +35,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = "/root/reference/src"
 TWIN_REF = os.path.join(ROOT, "oracle", "_ref", "wtf_twin_refmods")
 GPU_REF = os.path.join(ROOT, "oracle", "_ref", "wtfgpu_refmods")
+TLV_SO = os.path.join(ROOT, "oracle", "_ref", "fuzzer_tlv_server_ref.so")
 FIELDS = ("result", "crash", "error", "icount", "gprs", "coverage")
 
 
@@ -65,7 +69,7 @@ def tlv_target(tmp_path_factory):
     d = str(tmp_path_factory.mktemp("tlv_refmods"))
     H.build_target(d)
     inp = os.path.join(d, "parity")
-    tlv_inputs(inp, 250)
+    tlv_inputs(inp, 1100)
     os.remove(os.path.join(inp, "edge_bad_json"))
     return d
 
@@ -111,4 +115,26 @@ def test_reference_tlv_module_on_gpu_one_lane(tlv_target, tmp_path):
         (sub / n).write_bytes(open(os.path.join(inp, n), "rb").read())
     g = H.run(GPU_REF, tlv_target, str(sub), str(tmp_path / "g.jsonl"), lanes=1)
     t = H.run(H.TWIN, tlv_target, str(sub), str(tmp_path / "t.jsonl"), lanes=1)
+    assert not _diff(g, t)
+
+
+@pytest.mark.skipif(not os.path.exists(TLV_SO), reason="reference build absent (oracle/_ref)")
+def test_reference_tlv_module_copies_on_twin(tlv_target, tmp_path):
+    inp = os.path.join(tlv_target, "parity")
+    ref = H.run(TWIN_REF, tlv_target, inp, str(tmp_path / "ref.jsonl"), lanes=512, extra=("--module-so", TLV_SO))
+    ours = H.run(H.TWIN, tlv_target, inp, str(tmp_path / "ours.jsonl"), lanes=512)
+    assert not _diff(ref, ours)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(GPU_REF) or not os.path.exists(TLV_SO), reason="oracle/_ref not built")
+@pytest.mark.parametrize("lanes", [512, 1024])
+def test_reference_tlv_module_batched_on_gpu(tlv_target, tmp_path, lanes):
+    """The unchanged module, one copy per lane, `lanes` testcases in flight:
+    every copy's packet queue is its own lane's (a shared queue would hand
+    one lane's packets to another and change results)."""
+    inp = os.path.join(tlv_target, "parity")
+    g = H.run(GPU_REF, tlv_target, inp, str(tmp_path / "g.jsonl"), lanes=lanes, extra=("--module-so", TLV_SO))
+    t = H.run(H.TWIN, tlv_target, inp, str(tmp_path / "t.jsonl"), lanes=512)
+    assert len(g) > lanes
     assert not _diff(g, t)

@@ -642,7 +642,11 @@ __device__ __forceinline__ void retire(const Dev &P, Lane &L, int x, u32 len, u6
 // FEED action: the next chunk of the lane's feed goes to gpr[b] + window -
 // size, as fuzzer_tlv_server.cc:83-166 writes the next packet. Writes go
 // through the copy-on-write path (the pages are dirtied as VirtWriteDirty
-// does); 8-byte stores, then single bytes.
+// does); 8-byte stores, then single bytes. Like Backend_t::VirtWrite
+// (backend.cc:91-121, translation with ValidateRead) only a missing
+// translation stops it: the stores run as supervisor with CR0.WP clear, so
+// U/S and R/W are not checked. A missing page ends the lane with
+// WTFGPU_EXIT_FEED_FAULT, where the module's handler aborts.
 __device__ __noinline__ bool feed_apply(const Dev &P, Lane &L, const wtfgpu_bp_action_t &a) {
   if (!P.feed_pos) return false;
   const u64 pos = P.feed_pos[L.lane];
@@ -661,6 +665,10 @@ __device__ __noinline__ bool feed_apply(const Dev &P, Lane &L, const wtfgpu_bp_a
   }
   const u32 rb = (u32)a.gprs[0] & 15, rn = (u32)a.gprs[1] & 15;
   const u64 dst = R(L, rb) + a.value - n;
+  const u32 cpl0 = L.cpl;
+  const u64 cr00 = L.cr0;
+  L.cpl = 0;
+  L.cr0 &= ~(1ull << 16);
   for (u32 o = 0; o < n;) {
     const u32 sz = n - o >= 8 ? 8 : 1;
     u64 v = 0;
@@ -672,11 +680,15 @@ __device__ __noinline__ bool feed_apply(const Dev &P, Lane &L, const wtfgpu_bp_a
         if (L.status == WTFGPU_RUNNING || L.status == WTFGPU_EXIT_FAULT) L.status = WTFGPU_EXIT_FEED_FAULT;
         L.miss = 0;
         L.pend = 0;
+        L.cpl = cpl0;
+        L.cr0 = cr00;
         return true;
       }
     }
     o += sz;
   }
+  L.cpl = cpl0;
+  L.cr0 = cr00;
   L.pend = 0;
   if (L.flush) {
     tlb_flush(L);

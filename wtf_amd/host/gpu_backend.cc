@@ -1,5 +1,6 @@
 // gpu_backend.cc — see gpu_backend.h. Reference functions are cited per method.
 #include "gpu_backend.h"
+#include "module_instances.h"
 
 #include <algorithm>
 #include <chrono>
@@ -176,6 +177,10 @@ void GpuBackend_t::PrintRunStats() {
 
 // bochscpu_backend.cc:337-346
 bool GpuBackend_t::SetBreakpoint(const Gva_t Gva, const BreakpointHandler_t Handler) {
+  if (ModuleInstances *I = ModuleInstances::Registering()) {  // a module copy's Init (module_instances.h)
+    I->AddHandler(Gva.U64(), Handler);
+    if (I->RegisteringIndex() > 0) return breakpoints_.count(Gva.U64()) != 0;
+  }
   if (breakpoints_.count(Gva.U64())) {
     printf("/!\\ There is already a breakpoint at %#llx\n", (unsigned long long)Gva.U64());
     return false;
@@ -189,6 +194,7 @@ bool GpuBackend_t::SetBreakpoint(const Gva_t Gva, const BreakpointHandler_t Hand
 bool GpuBackend_t::SetBreakpoint(const Gva_t Gva, const BreakpointHandler_t Handler,
                                  const BreakpointAction_t &Action) {
   if (!SetBreakpoint(Gva, Handler)) return false;
+  if (ModuleInstances::Registering() && ModuleInstances::Registering()->RegisteringIndex() > 0) return true;
   const char *Env = getenv("WTFGPU_DEVICE_BP_ACTIONS");
   if (Action.Kind == BreakpointAction_t::Kind_t::Host || (Env && Env[0] == '0')) return true;
   wtfgpu_bp_action_t A;
@@ -665,10 +671,19 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
 }
 
 // One round's exits: each pending lane that is not done is classified (a
-// result, or a breakpoint hit for the host, or still running).
-void GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first, const std::vector<wtfgpu_exit_t> &ex,
+// result, or a breakpoint hit for the host, or still running). false: a
+// device Feed action could not write its chunk; the module's handler would
+// std::abort() on that failed VirtWriteDirty (fuzzer_tlv_server.cc:130-158),
+// the backend fails the run instead (RunBatch / Run return an error).
+bool GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first, const std::vector<wtfgpu_exit_t> &ex,
                             std::vector<uint8_t> &done, std::vector<LaneResult> *out, std::vector<uint32_t> &hits) {
   std::vector<uint8_t> hit(pending.size(), 0);
+  for (uint32_t l : pending)
+    if (!done[l - first] && ex[l - first].status == WTFGPU_EXIT_FEED_FAULT) {
+      fprintf(stderr, "VirtWriteDirty failed: the device Feed action of lane %u could not write its chunk (rip %#llx)\n",
+              l, (unsigned long long)ex[l - first].rip);
+      return false;
+    }
 #pragma omp parallel for schedule(static, 1024) if (pending.size() >= 2048)
   for (size_t pi = 0; pi < pending.size(); pi++) {
     const uint32_t l = pending[pi];
@@ -712,7 +727,7 @@ void GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first
     if (hit[pi] == 1) hits.push_back(pending[pi]);
     if (hit[pi] == 2) named.push_back(pending[pi]);
   }
-  if (named.empty()) return;
+  if (named.empty()) return true;
   // device StopWithArgs actions: the handler's Stop(Result(GetArg(0..5)))
   std::vector<uint64_t> args(named.size() * 6);
   const bool ok = wtfgpu_read_stop_args(ctx_, named.data(), (uint32_t)named.size(), args.data()) == WTFGPU_OK;
@@ -732,6 +747,7 @@ void GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first
     done[l - first] = 1;
   }
   stats_.err_other += bad;
+  return true;
 }
 
 // Final state of every finished lane (`ex` holds the last round's exits of
@@ -796,7 +812,7 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
     account_run(rs);
     if (wtfgpu_read_exits(ctx_, first, count, ex.data())) return false;
     std::vector<uint32_t> hits;
-    classify(pending, first, ex, done, out, hits);
+    if (!classify(pending, first, ex, done, out, hits)) return false;
     stats_.exits_ms += ms_since(te);
     if (hits.empty()) break;
     if (!service_hits(hits, first, done, slots, per_lane_state)) return false;
@@ -875,11 +891,17 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
       cur_ = l;
       const uint64_t rip0 = v.gpr[16];
       servicing_sp_ = sp_gpfn[h];
-      auto it = breakpoints_.find(rip0);
+      BreakpointHandler_t handler = nullptr;
+      if (slots && slots->Instances()) {
+        handler = slots->Instances()->HandlerOf(l, rip0);  // lane l's module copy
+      } else {
+        const auto it = breakpoints_.find(rip0);
+        if (it != breakpoints_.end()) handler = it->second;
+      }
       if (per_lane_state && slots) slots->SwapIn(l);
       servicing_bp_ = rip0;
       v.inject = ~0ull;
-      if (it != breakpoints_.end()) it->second(this);  // BeforeExecutionHook (bochscpu_backend.cc:545-547)
+      if (handler) handler(this);  // BeforeExecutionHook (bochscpu_backend.cc:545-547)
       servicing_bp_ = ~0ull;
       if (per_lane_state && slots) slots->SwapOut(l);
       action[h] = v.result ? 0 : (v.gpr[16] == rip0 ? 2 : 1);  // U10: a moved rip cancels the hooked instruction
@@ -1159,7 +1181,8 @@ void GpuBackend_t::insert_lanes(const Target_t &Target, const std::vector<uint32
       Slots->ResetLane(l);
       Slots->SwapIn(l);
     }
-    ok[i] = Target.InsertTestcase(tcs[i].first, tcs[i].second);
+    const Target_t &T = Slots && Slots->Instances() ? Slots->Instances()->TargetOf(l) : Target;
+    ok[i] = T.InsertTestcase(tcs[i].first, tcs[i].second);
     if (Slots) Slots->SwapOut(l);
   };
   if (parallel_service(Slots)) {
@@ -1182,7 +1205,7 @@ void GpuBackend_t::target_restore(const Target_t &Target, const std::vector<uint
   auto restore = [&](uint32_t l) {
     cur_ = l;
     if (Slots) Slots->SwapIn(l);
-    Target.Restore();
+    (Slots && Slots->Instances() ? Slots->Instances()->TargetOf(l) : Target).Restore();
     if (Slots) Slots->SwapOut(l);
   };
   if (parallel_service(Slots)) {
@@ -1403,7 +1426,7 @@ bool GpuBackend_t::harvest_part(Part &P, const Target_t &Target, std::vector<Str
   if (wtfgpu_read_exits(ctx_, first, count, P.ex.data())) return false;
   std::vector<uint8_t> done(count, 0);
   std::vector<uint32_t> hits;
-  classify(P.occ, first, P.ex, done, &lres_, hits);
+  if (!classify(P.occ, first, P.ex, done, &lres_, hits)) return false;
   stats_.exits_ms += ms_since(te);
   if (!hits.empty() && !service_hits(hits, first, done, Slots, Slots != nullptr)) return false;
   std::vector<uint32_t> finished;

@@ -183,7 +183,7 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   // until every lane has a result
   bool run_lanes(const std::vector<uint32_t> &lanes, std::vector<LaneResult> *out, ModuleSlots *slots,
                  bool per_lane_state);
-  void classify(const std::vector<uint32_t> &pending, uint32_t first, const std::vector<wtfgpu_exit_t> &ex,
+  bool classify(const std::vector<uint32_t> &pending, uint32_t first, const std::vector<wtfgpu_exit_t> &ex,
                 std::vector<uint8_t> &done, std::vector<LaneResult> *out, std::vector<uint32_t> &hits);
   bool fill_results(const std::vector<uint32_t> &lanes, uint32_t first, const std::vector<wtfgpu_exit_t> &ex,
                     const std::vector<uint8_t> &done, std::vector<LaneResult> *out, std::vector<uint32_t> *finished);

@@ -20,7 +20,7 @@ ModuleSlots::~ModuleSlots() { release(); }
 bool ModuleSlots::ThreadSafe() const {
   for (const auto &ops : LaneStateRegistry())
     if (!ops.tls) return false;
-  return !LaneStateRegistry().empty();
+  return inst_ || !LaneStateRegistry().empty();
 }
 
 void ModuleSlots::release() {

@@ -37,6 +37,8 @@
 
 namespace wtfgpu_host {
 
+class ModuleInstances;
+
 // Type-erased operations over one registered global.
 struct LaneStateOps {
   void *(*object)();                     // the calling thread's instance
@@ -81,14 +83,19 @@ class ModuleSlots {
   void SwapIn(uint32_t lane);
   void SwapOut(uint32_t lane);
   size_t Objects() const { return initial_.size(); }
-  // every registered object is thread_local: lanes may be serviced in parallel
+  // every registered object is thread_local (or every lane runs its own copy
+  // of the module, module_instances.h): lanes may be serviced in parallel
   bool ThreadSafe() const;
+  // per-lane module copies: lane l runs copy l's Target_t and handlers
+  void AttachInstances(ModuleInstances *I) { inst_ = I; }
+  ModuleInstances *Instances() const { return inst_; }
 
  private:
   void release();
   std::vector<void *> initial_;             // per registered object
   std::vector<std::vector<void *>> lanes_;  // [lane][object], nullptr = not materialised
   std::vector<uint8_t> dirty_;              // lane copy differs from initial
+  ModuleInstances *inst_ = nullptr;
 };
 
 }  // namespace wtfgpu_host

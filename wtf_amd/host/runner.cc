@@ -1,6 +1,7 @@
 // runner.cc — see runner.h.
 #include "runner.h"
 #include "remote.h"
+#include "module_instances.h"
 
 #include <algorithm>
 #include <atomic>
@@ -154,6 +155,7 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
     else if (a == "--regroup-steps") O.regroup = strtoull(next("--regroup-steps"), nullptr, 0);
     else if (a == "--stream-run") O.stream_run = true;
     else if (a == "--serial") O.serial = true;
+    else if (a == "--module-so") O.module_so = next("--module-so");
     else if (a == "--rank") O.rank = atoi(next("--rank"));
     else if (a == "--world") O.world = atoi(next("--world"));
     else if (a == "--exchange") O.exchange = next("--exchange");
@@ -181,7 +183,7 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
                     "       [--lanes n] [--overlay-pages k] [--runs n] [--seconds s] [--seed s] [--full-coverage]\n"
                     "       [--serial-mutation] [--slice-steps s] [--regroup-steps r] [--rank r --world n [--exchange host:port | --nccl-id-file f]]\n"
                     "       [--address tcp://ip:port|unix://path [--batched] [--nodes k]] [--edges]\n"
-                    "       [--trace-path dir [--trace-type rip|cov] [--trace-cap n]]\n");
+                    "       [--trace-path dir [--trace-type rip|cov] [--trace-cap n]] [--module-so m.so] [--serial]\n");
     return false;
   }
   return true;
@@ -213,20 +215,33 @@ bool LoadTarget(const RunnerOptions &O, Options_t &Opts, CpuState_t &State) {
 
 int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, const CpuState_t &State,
                CoverageExchange_t *X) {
-  Target_t *Target = Targets_t::Instance().Get(O.name);
+  // --module-so: one private copy of an unchanged module per lane
+  // (module_instances.h); lane l runs copy l
+  std::unique_ptr<ModuleInstances> Inst;
+  Target_t *Target = nullptr;
+  std::unique_ptr<Target_t> Copy0;  // a copy: Target_t's own constructor would register it
+  if (!O.module_so.empty()) {
+    Inst = std::make_unique<ModuleInstances>();
+    if (!Inst->Load(O.module_so, O.name, Exec.Lanes())) return 1;
+    Copy0 = std::make_unique<Target_t>(Inst->TargetOf(0));
+    Target = Copy0.get();
+  } else {
+    Target = Targets_t::Instance().Get(O.name);
+  }
   if (!Target) {
     printf("Target %s not found\n", O.name.c_str());
     Targets_t::Instance().DisplayRegisteredTargets();
     return 1;
   }
   g_Backend = Exec.AsBackend();
-  if (!Target->Init(Opts, State)) {
+  if (Inst ? !Inst->InitAll(Opts, State) : !Target->Init(Opts, State)) {
     printf("Failed to initialize the target\n");
     return 1;
   }
   const uint32_t N = Exec.Lanes();
   ModuleSlots Slots;
   Slots.Capture(N);
+  Slots.AttachInstances(Inst.get());
   Exec.SetFullCoverage(O.full_coverage);
 
   if (O.mode == "run") {

@@ -155,6 +155,7 @@ struct RunnerOptions {
   // run: the reference client's RunTestcaseAndRestore (client.cc:88-180), one
   // testcase at a time through Backend_t::Run / Restore (no batching)
   bool serial = false;
+  std::string module_so;  // an unchanged module built as a shared object, one copy per lane
   int rank = 0, world = 1;         // fuzz: shard rank of world (one node per GPU)
   std::string exchange = "127.0.0.1:31337";  // TCP coverage exchange (CPU shards): rank 0 listens here
   std::string nccl_id_file;        // GPU shards: RCCL unique id file (rank 0 writes it)

@@ -84,9 +84,13 @@ def _elf(path: str):
     return segs, syms
 
 
-def build(state_dir: str, work_dir: str | None = None) -> dict:
+def build(state_dir: str, work_dir: str | None = None, packet: str = "rw") -> dict:
     """Compiles the guest and writes mem.dmp / regs.json / symbol-store.json
-    into state_dir. Returns the guest symbol table."""
+    into state_dir. Returns the guest symbol table. `packet` maps the packet
+    buffer page read-write ("rw", the real server), read-only ("ro": the
+    module's writes still land, Backend_t::VirtWrite translates without a
+    permission check, backend.cc:91-121) or not at all ("none": the module's
+    write fails and its handler aborts)."""
     work_dir = work_dir or state_dir
     os.makedirs(work_dir, exist_ok=True)
     elf = os.path.join(work_dir, "tlv_server_guest.elf")
@@ -107,7 +111,8 @@ def build(state_dir: str, work_dir: str | None = None) -> dict:
     for i in range(HEAP_SLOTS):
         link = (i + 2) if i + 1 < HEAP_SLOTS else 0
         sp.map(HEAP_BASE + i * HEAP_STRIDE, struct.pack("<Q", link), nx=True)
-    sp.map(PACKET_VA, b"", nx=True)
+    if packet != "none":
+        sp.map(PACKET_VA, b"", nx=True, write=packet == "rw")
     for va in range(STACK_TOP - 0x4000, STACK_TOP, PAGE):
         sp.map(va, b"", nx=True)
     # ring 0 pieces the __fastfail path runs through (SDM vol. 3 6.14)
