@@ -154,7 +154,10 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
         default:  // outside the engine subset: an engine error, not a target crash
           result_ = Crash_t();
           engine_error_ = true;
-          if (e.status == WTFGPU_EXIT_UNIMPLEMENTED) unimpl_.add(e.opcode);
+          if (e.status == WTFGPU_EXIT_UNIMPLEMENTED) {
+            unimpl_.add(e.opcode);
+            if (getenv("WTF_UNIMPL_RAW")) fprintf(stderr, "unimpl_raw %08x rip %llx\n", e.opcode, (unsigned long long)e.rip);
+          }
           break;
       }
       break;

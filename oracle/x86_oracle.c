@@ -482,6 +482,7 @@ typedef struct {
   u32 pfx66, pfx67, rep, lock, seg; /* seg: 0 none, 4 fs, 5 gs */
   u32 rex, rexw, rexr, rexx, rexb;
   u32 opmap; /* 0 one-byte, 1 = 0F, 2 = 0F38, 3 = 0F3A */
+  u32 undef; /* U36: an encoding the emulated CPU does not define (#UD) */
   u32 vex, vl, vw, vvvv, vpp, vbad; /* VEX prefix: present, L, W, vvvv (decoded), pp; a legacy prefix before it */
   u32 op;
   u32 has_modrm, mod, reg, rm; /* reg, rm include REX extension */
@@ -1578,10 +1579,69 @@ static int vex_valid(u32 map, u32 op, int pp, int mem, u32 r3) {
   return 0;
 }
 
+/* U36: which encodings exist on the emulated CPU (SDM vol. 2 appendix A,
+ * restricted to the features leaf 1 / leaf 7 of cpuid_leaf enumerate: SSE,
+ * SSE2, SSSE3, SSE4.1, AVX, AVX2). An opcode no such instruction defines, a
+ * VEX map other than 0f / 0f 38 / 0f 3a, and the forms of features CPUID does
+ * not enumerate (SSE3 and SSE4.2 aside from their VEX forms, FMA, F16C,
+ * BMI1/2, ADX, MOVBE, AES, PCLMULQDQ, SHA, VMX, INVPCID, AVX-512 mask ops) are
+ * #UD, decided from the opcode byte (no ModRM / immediate fetched). A defined
+ * form outside the executed subset stays UNIMPLEMENTED. pp / pfx: 0 none,
+ * 1 66, 2 f3, 3 f2. */
+static int vex_defined(u32 map, u32 op, int pp) {
+  if (map == 1) {
+    switch (op) {
+    case 0x10: case 0x11: case 0x12: case 0x51: case 0x58: case 0x59: case 0x5a: case 0x5c: case 0x5d:
+    case 0x5e: case 0x5f: case 0xc2: case 0xae:
+      return 1;
+    case 0x13: case 0x14: case 0x15: case 0x17: case 0x28: case 0x29: case 0x2b: case 0x2e: case 0x2f:
+    case 0x50: case 0x54: case 0x55: case 0x56: case 0x57: case 0xc6:
+      return pp <= 1;
+    case 0x16: case 0x5b: return pp <= 2;
+    case 0x2a: case 0x2c: case 0x2d: return pp >= 2;
+    case 0x52: case 0x53: return pp == 0 || pp == 2;
+    case 0x6f: case 0x7e: case 0x7f: return pp == 1 || pp == 2;
+    case 0x70: case 0xe6: return pp >= 1;
+    case 0x77: return pp == 0;
+    case 0x7c: case 0x7d: case 0xd0: return pp == 1 || pp == 3;
+    case 0xf0: return pp == 3;
+    default:
+      return pp == 1 && ((op >= 0x60 && op <= 0x6e) || (op >= 0x71 && op <= 0x76) || op == 0xc4 || op == 0xc5 ||
+                         (op >= 0xd1 && op <= 0xfe));
+    }
+  }
+  if (pp != 1) return 0;
+  if (map == 2)
+    return op <= 0x0f || (op >= 0x16 && op <= 0x1a) || (op >= 0x1c && op <= 0x1e) || (op >= 0x20 && op <= 0x25) ||
+           (op >= 0x28 && op <= 0x41) || (op >= 0x45 && op <= 0x47) || (op >= 0x58 && op <= 0x5a) || op == 0x78 ||
+           op == 0x79 || op == 0x8c || op == 0x8e || (op >= 0x90 && op <= 0x93);
+  if (map == 3)
+    return op == 0x00 || op == 0x01 || op == 0x02 || op == 0x04 || op == 0x05 || op == 0x06 ||
+           (op >= 0x08 && op <= 0x0f) || (op >= 0x14 && op <= 0x19) || (op >= 0x20 && op <= 0x22) || op == 0x38 ||
+           op == 0x39 || (op >= 0x40 && op <= 0x42) || op == 0x46 || (op >= 0x4a && op <= 0x4c) ||
+           (op >= 0x60 && op <= 0x63);
+  return 0;
+}
+
+/* the legacy (non-VEX) 0f 38 / 0f 3a maps, same rule */
+static int legacy_3byte_defined(u32 map, u32 op, int pfx) {
+  if (map == 2)
+    return ((op <= 0x0b || (op >= 0x1c && op <= 0x1e)) && pfx <= 1) ||
+           (pfx == 1 && (op == 0x10 || op == 0x14 || op == 0x15 || op == 0x17 || (op >= 0x20 && op <= 0x25) ||
+                         (op >= 0x28 && op <= 0x2b) || (op >= 0x30 && op <= 0x35) || (op >= 0x38 && op <= 0x41)));
+  return (op == 0x0f && pfx <= 1) ||
+         (pfx == 1 && ((op >= 0x08 && op <= 0x0e) || (op >= 0x14 && op <= 0x17) || (op >= 0x20 && op <= 0x22) ||
+                       (op >= 0x40 && op <= 0x42)));
+}
+
 static int exec_vex(orc_machine *m, insn *d) {
   const u32 op = d->op, r3 = d->reg & 7, map = d->opmap, vv = d->vvvv;
   const int pp = (int)d->vpp, l256 = (int)d->vl, mem = d->is_mem;
   const u8 imm = d->bytes[d->len - 1];
+  if (map == 1 && op == 0xae && !(pp == 0 && mem && (r3 == 2 || r3 == 3))) { /* U36: vldmxcsr / vstmxcsr only */
+    fault(m, WTFGPU_VEC_UD, 0);
+    return X_FAULT;
+  }
   if (!vex_valid(map, op, pp, mem, r3)) return X_UNIMPL;
   int ud = d->vbad || !((m->r.cr4 >> 18) & 1) || (m->r.xcr0 & 6) != 6;
   int two = 0, no256 = 0, reg_only = 0, mem_only = 0;
@@ -1775,7 +1835,7 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
   u64 nrip = d->start + d->len;
   u64 a = 0, b = 0, res = 0;
   *next_rip = nrip;
-  if (d->lock && !lockable(d)) { /* U34 */
+  if ((d->lock && !lockable(d)) || d->undef) { /* U34, U36 */
     fault(m, WTFGPU_VEC_UD, 0);
     return X_FAULT;
   }
@@ -2748,7 +2808,13 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
     d->vpp = b2 & 3u;
     b = fetch8(m, d);
     if (d->fetch_fail) return -1;
+    d->undef = d->vbad || d->opmap < 1 || d->opmap > 3 || !vex_defined(d->opmap, b, (int)d->vpp);
     if (d->opmap != 1 && d->opmap != 2) {
+      d->op = b;
+      d->len = d->pos;
+      return 1;
+    }
+    if (d->undef) {
       d->op = b;
       d->len = d->pos;
       return 1;
@@ -2762,6 +2828,8 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
       d->op = fetch8(m, d);
       if (d->fetch_fail) return -1;
       if (d->opmap == 3 || (d->op != 0x00 && d->op != 0x17)) { /* 0f 38 00 pshufb, 0f 38 17 ptest; the rest: outside */
+        const int pfx = d->rep == 0xf3 ? 2 : d->rep == 0xf2 ? 3 : d->pfx66 ? 1 : 0;
+        d->undef = !legacy_3byte_defined(d->opmap, d->op, pfx);
         d->len = d->pos;
         return 1;
       }
@@ -2975,7 +3043,7 @@ static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
     fill_exit(m, ex, WTFGPU_EXIT_BREAKPOINT);
     return ex->status;
   }
-  if (rc == 1 && !d.lock) {
+  if (rc == 1 && !d.lock && !d.undef) {
     memcpy(&ex->opcode, d.bytes, 4);
     fill_exit(m, ex, WTFGPU_EXIT_UNIMPLEMENTED);
     return ex->status;

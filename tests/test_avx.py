@@ -15,7 +15,7 @@ import pytest
 from tests.golden.gen_native_vectors import splitmix_bytes
 from tests.test_sse import BUF, layout, sim_lib, sim_run
 from tests.oracle_lib import Oracle
-from wtf_amd.abi import EXIT_FAULT, EXIT_UNIMPLEMENTED, RUNNING
+from wtf_amd.abi import EXIT_FAULT, EXIT_TIMEOUT, EXIT_UNIMPLEMENTED, RUNNING
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CODE_VA = 0x140001000
@@ -126,6 +126,29 @@ AVX_FAULT_CASES = [
     ([0xC4, 0xE2, 0x79, 0x1C, 0xC1], EXIT_UNIMPLEMENTED, None),        # vpabsb (0f 38 1c)
     ([0x66, 0x0F, 0x38, 0x00, 0x06], EXIT_FAULT, 13),      # pshufb xmm0, [rsi]: legacy needs alignment
     ([0x66, 0x0F, 0x38, 0x1C, 0xC1], EXIT_UNIMPLEMENTED, None),        # pabsb (outside)
+    # U36: encodings the emulated CPU does not define
+    ([0xC4, 0x30, 0x02, 0x00], EXIT_FAULT, 6),              # VEX map 0x10 (runaway HEVD bytes)
+    ([0xC4, 0xE0, 0x79, 0x58, 0xC1], EXIT_FAULT, 6),        # VEX map 0
+    ([0xC4, 0xE4, 0x79, 0x58, 0xC1], EXIT_FAULT, 6),        # VEX map 4
+    ([0xC5, 0xF8, 0x00, 0xC1], EXIT_FAULT, 6),              # VEX 0f 00: no AVX form
+    ([0xC5, 0xF8, 0x60, 0xC1], EXIT_FAULT, 6),              # VEX.NP 0f 60: MMX only
+    ([0xC5, 0xFA, 0x14, 0xC1], EXIT_FAULT, 6),              # VEX.F3 0f 14
+    ([0xC4, 0xE2, 0x79, 0xA8, 0xC1], EXIT_FAULT, 6),        # vfmadd213ps: FMA not enumerated
+    ([0xC4, 0xE2, 0x78, 0xF2, 0xC1], EXIT_FAULT, 6),        # andn: BMI1 not enumerated
+    ([0xC4, 0xE2, 0x79, 0x13, 0xC1], EXIT_FAULT, 6),        # vcvtph2ps: F16C not enumerated
+    ([0xC4, 0xE3, 0x79, 0x44, 0xC1, 0x00], EXIT_FAULT, 6),  # vpclmulqdq: PCLMULQDQ not enumerated
+    ([0xC4, 0xE3, 0x7B, 0xF0, 0xC1, 0x01], EXIT_FAULT, 6),  # rorx: BMI2 not enumerated
+    ([0xC5, 0xF8, 0xAE, 0x16], EXIT_UNIMPLEMENTED, None),   # vldmxcsr [rsi]: defined, outside the subset
+    ([0xC5, 0xF8, 0xAE, 0xC1], EXIT_FAULT, 6),              # VEX 0f ae, register form
+    ([0xC5, 0xF8, 0xAE, 0x06], EXIT_FAULT, 6),              # VEX 0f ae /0 (fxsave has no VEX form)
+    ([0xC4, 0xE3, 0x79, 0x0F, 0x06, 0x04], EXIT_UNIMPLEMENTED, None),  # vpalignr xmm, [rsi]
+    ([0x66, 0x0F, 0x38, 0x37, 0xC1], EXIT_FAULT, 6),        # pcmpgtq: SSE4.2 not enumerated
+    ([0x0F, 0x38, 0xF0, 0x06], EXIT_FAULT, 6),              # movbe: not enumerated
+    ([0x66, 0x0F, 0x38, 0xDC, 0xC1], EXIT_FAULT, 6),        # aesenc: not enumerated
+    ([0x66, 0x0F, 0x38, 0x50, 0xC1], EXIT_FAULT, 6),        # 0f 38 50: undefined
+    ([0x66, 0x0F, 0x3A, 0x44, 0xC1, 0x00], EXIT_FAULT, 6),  # pclmulqdq
+    ([0x0F, 0x38, 0x00, 0xC1], EXIT_UNIMPLEMENTED, None),   # pshufb mm, mm (MMX form, defined)
+    ([0x0F, 0x3A, 0x0F, 0xC1, 0x01], EXIT_UNIMPLEMENTED, None),  # palignr mm, mm, 1
 ]
 
 
@@ -179,3 +202,36 @@ def test_vzeroupper_keeps_low_halves_and_legacy_keeps_high():
     r = o.regs()
     assert all(r.ymmh[i][0] == 0 and r.ymmh[i][1] == 0 for i in range(16))
     assert all(r.xmm[i][0] == i + 1 for i in range(16))
+
+
+def test_encoding_space_oracle_equals_engine():
+    """U36 over the whole opcode space of VEX maps 0-4 (each pp) and of the
+    legacy 0f 38 / 0f 3a maps (each mandatory prefix): the oracle and the
+    engine's decode agree on #UD / UNIMPLEMENTED / executed for every opcode,
+    register and memory ModRM forms alike."""
+    L = sim_lib()
+    codes = []
+    for modrm in (0xC1, 0x06):
+        for m in range(5):
+            for pp in range(4):
+                for op in range(256):
+                    codes.append([0xC4, 0xE0 | m, 0x78 | pp, op, modrm, 0x01, 0xCC])
+        for pfx in ([], [0x66], [0xF3], [0xF2]):
+            for esc in (0x38, 0x3A):
+                for op in range(256):
+                    codes.append(pfx + [0x0F, esc, op, modrm, 0x01, 0xCC])
+    bad = []
+    for code in codes:
+        sp, regs = layout(bytes(code), BUF, bytes(range(256)))
+        regs.gpr[3], regs.gpr[6] = BUF + 0x10, BUF + 0x13
+        pfns, blob = sp.phys()
+        o = Oracle(pfns=pfns, blob=blob)
+        o.restore(regs)
+        ex = o.step()
+        if ex.status == RUNNING:  # the limit stops the lane after its second instruction
+            ex = o.step()
+        sim = sim_run(L, sp, regs, limit=1)
+        want = (EXIT_TIMEOUT, 3) if ex.status == RUNNING else (ex.status,)
+        if sim.status not in want or (ex.status == EXIT_FAULT and sim.vector != ex.vector):
+            bad.append((bytes(code).hex(), ex.status, ex.vector, sim.status, sim.vector))
+    assert not bad, (len(bad), bad[:8])

@@ -263,6 +263,15 @@ __device__ __forceinline__ u32 zsize(u32 z, u32 osz, u32 p66) {
 __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
   u32 pos = 0, p66 = 0, rex = 0, lock = 0, c;
   u.p67 = u.rep = u.seg = 0;
+  // operand fields exec reads before it dispatches on the op: defined for the
+  // early returns below (#UD / UNIMPLEMENTED decided before the ModRM)
+  u.asrc = u.bsrc = L_NONE;
+  u.aread = u.awrite = u.bwrite = 0;
+  u.is_mem = u.riprel = 0;
+  u.reg = u.rm = u.opreg = u.rex = 0;
+  u.base = u.index = -1;
+  u.scale = 0;
+  u.disp = 0;
   for (;;) {
     if (pos >= 15) return 2;
     if (pos >= b.avail) return 1;
@@ -297,6 +306,14 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
     vex = 1 | (((b2 >> 2) & 1) << 1) | (vw << 2) | ((((~b2) >> 3) & 15) << 4) | (vmap << 8) | (bad << 16);
     rex = 0x40 | (vw << 3) | (vr << 2) | (vx << 1) | vb;
     c = ib_at(b, pos++);  // the opcode
+    const bool def = !bad && vmap >= 1 && vmap <= 3 && vex_defined(vmap, c, vpp);
+    if (!def || vmap == 3) {  // U36: #UD from the opcode byte; a defined 0f 3a form is outside the subset
+      u.len = pos;
+      u.op = (lock || !def) ? O_UD : O_UNIMPL;
+      u.supported = lock || !def;
+      u.opbytes = pos >= 4 ? (u32)b.lo : ((u32)b.lo & ((1u << (8 * pos)) - 1));
+      return 0;
+    }
   }
   u.rex = rex;
   const u32 rexw = (rex >> 3) & 1, rexr = (rex >> 2) & 1, rexx = (rex >> 1) & 1, rexb = rex & 1;
@@ -320,9 +337,10 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
         map2 = 1;
         e = kSseModrm;
       } else {
+        const bool def = legacy_3byte_defined(c == 0x38 ? 2 : 3, c3, u.rep == 0xf3 ? 2 : u.rep == 0xf2 ? 3 : p66 ? 1 : 0);
         u.len = pos;
-        u.op = lock ? O_UD : O_UNIMPL;  // U34: lock is #UD first
-        u.supported = lock;
+        u.op = (lock || !def) ? O_UD : O_UNIMPL;  // U34: lock is #UD first; U36: undefined is #UD
+        u.supported = lock || !def;
         u.opbytes = pos >= 4 ? (u32)b.lo : ((u32)b.lo & ((1u << (8 * pos)) - 1));
         return 0;
       }
@@ -476,7 +494,10 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
       if (vex) {
         u.bsz = vpp;
         u.opreg = vex;
-        if (!vex_valid(smap, c, vpp, u.is_mem, u.reg & 7)) u.op = O_UNIMPL;
+        if (smap == 1 && c == 0xae && !(vpp == 0 && u.is_mem && ((u.reg & 7) == 2 || (u.reg & 7) == 3)))
+          u.op = O_UD;  // U36: vldmxcsr / vstmxcsr are the only VEX group-15 forms
+        else if (!vex_valid(smap, c, vpp, u.is_mem, u.reg & 7))
+          u.op = O_UNIMPL;
       } else {
         u.bsz = u.rep == 0xf3 ? 2 : u.rep == 0xf2 ? 3 : p66 ? 1 : 0;
         u.opreg = smap << 8;

@@ -80,6 +80,56 @@ __device__ __forceinline__ bool sse_valid(u32 map, u32 c, u32 pc, u32 is_mem, u3
     return pc == 1 && c != 0xd0 && c != 0xe6 && c != 0xf0 && c != 0xf7 && c != 0xff;
   return false;
 }
+// U36: the encodings the emulated CPU defines, i.e. SSE .. SSE4.1,
+// SSSE3, AVX and AVX2 as cpuid_leaf enumerates them. Anything else (an
+// undefined opcode / prefix pair, a VEX map other than 0f / 0f 38 / 0f 3a,
+// FMA, F16C, BMI, AES, PCLMULQDQ, SHA, SSE4.2 legacy forms, ...) is #UD,
+// decided from the opcode byte before any ModRM fetch. pp: 0 none, 1 66,
+// 2 f3, 3 f2.
+__host__ __device__ inline bool vex_defined(u32 map, u32 op, u32 pp) {
+  if (map == 1) {
+    switch (op) {
+      case 0x10: case 0x11: case 0x12: case 0x51: case 0x58: case 0x59: case 0x5a: case 0x5c: case 0x5d:
+      case 0x5e: case 0x5f: case 0xc2: case 0xae:
+        return true;
+      case 0x13: case 0x14: case 0x15: case 0x17: case 0x28: case 0x29: case 0x2b: case 0x2e: case 0x2f:
+      case 0x50: case 0x54: case 0x55: case 0x56: case 0x57: case 0xc6:
+        return pp <= 1;
+      case 0x16: case 0x5b: return pp <= 2;
+      case 0x2a: case 0x2c: case 0x2d: return pp >= 2;
+      case 0x52: case 0x53: return pp == 0 || pp == 2;
+      case 0x6f: case 0x7e: case 0x7f: return pp == 1 || pp == 2;
+      case 0x70: case 0xe6: return pp >= 1;
+      case 0x77: return pp == 0;
+      case 0x7c: case 0x7d: case 0xd0: return pp == 1 || pp == 3;
+      case 0xf0: return pp == 3;
+      default:
+        return pp == 1 && ((op >= 0x60 && op <= 0x6e) || (op >= 0x71 && op <= 0x76) || op == 0xc4 || op == 0xc5 ||
+                           (op >= 0xd1 && op <= 0xfe));
+    }
+  }
+  if (pp != 1) return false;
+  if (map == 2)
+    return op <= 0x0f || (op >= 0x16 && op <= 0x1a) || (op >= 0x1c && op <= 0x1e) || (op >= 0x20 && op <= 0x25) ||
+           (op >= 0x28 && op <= 0x41) || (op >= 0x45 && op <= 0x47) || (op >= 0x58 && op <= 0x5a) || op == 0x78 ||
+           op == 0x79 || op == 0x8c || op == 0x8e || (op >= 0x90 && op <= 0x93);
+  if (map == 3)
+    return op <= 0x02 || (op >= 0x04 && op <= 0x06) || (op >= 0x08 && op <= 0x0f) || (op >= 0x14 && op <= 0x19) ||
+           (op >= 0x20 && op <= 0x22) || op == 0x38 || op == 0x39 || (op >= 0x40 && op <= 0x42) || op == 0x46 ||
+           (op >= 0x4a && op <= 0x4c) || (op >= 0x60 && op <= 0x63);
+  return false;
+}
+// the legacy 0f 38 (map 2) / 0f 3a (map 3) opcodes, same rule
+__host__ __device__ inline bool legacy_3byte_defined(u32 map, u32 op, u32 pfx) {
+  if (map == 2)
+    return ((op <= 0x0b || (op >= 0x1c && op <= 0x1e)) && pfx <= 1) ||
+           (pfx == 1 && (op == 0x10 || op == 0x14 || op == 0x15 || op == 0x17 || (op >= 0x20 && op <= 0x25) ||
+                         (op >= 0x28 && op <= 0x2b) || (op >= 0x30 && op <= 0x35) || (op >= 0x38 && op <= 0x41)));
+  return (op == 0x0f && pfx <= 1) ||
+         (pfx == 1 && ((op >= 0x08 && op <= 0x0e) || (op >= 0x14 && op <= 0x17) || (op >= 0x20 && op <= 0x22) ||
+                       (op >= 0x40 && op <= 0x42)));
+}
+
 __device__ __forceinline__ bool vex_valid(u32 map, u32 c, u32 pp, u32 is_mem, u32 r3) {
   if (map == 2) return pp == 1 && (c == 0x00 || c == 0x17 || c == 0x58 || c == 0x59 || c == 0x78 || c == 0x79);
   if (map != 1) return false;

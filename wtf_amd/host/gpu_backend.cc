@@ -1496,6 +1496,7 @@ std::string GpuBackend_t::StatsJson() const {
            stats_.restore_dev_ms);
   r += b;
   r += ",\"unimpl_ops\":" + stats_.unimpl_ops.json();
+  r += ",\"unimpl_raw\":" + stats_.unimpl_ops.raw_json();
   b[0] = 0;
   r += b;
   r += ",\"fetch_by_bp\":{";

@@ -14,6 +14,10 @@
 
 struct UnimplHist {
   std::atomic<uint64_t> n[512] = {};
+  // the first kRaw exits' four opcode bytes as they were (diagnostic)
+  static constexpr uint32_t kRaw = 96;
+  std::atomic<uint32_t> nraw{0};
+  uint32_t raw[kRaw] = {};
   static uint32_t key(uint32_t opbytes) {
     for (int i = 0; i < 4; i++) {
       const uint32_t b = (opbytes >> (8 * i)) & 0xff;
@@ -28,7 +32,23 @@ struct UnimplHist {
     }
     return 0x1ff;
   }
-  void add(uint32_t opbytes) { n[key(opbytes)].fetch_add(1, std::memory_order_relaxed); }
+  void add(uint32_t opbytes) {
+    n[key(opbytes)].fetch_add(1, std::memory_order_relaxed);
+    const uint32_t i = nraw.fetch_add(1, std::memory_order_relaxed);
+    if (i < kRaw) raw[i] = opbytes;
+  }
+  // ["c4e27d18",...]: the sampled exits' bytes in memory order
+  std::string raw_json() const {
+    std::string s = "[";
+    char buf[16];
+    const uint32_t m = std::min<uint32_t>(nraw.load(), kRaw);
+    for (uint32_t i = 0; i < m; i++) {
+      snprintf(buf, sizeof(buf), "%s\"%02x%02x%02x%02x\"", i ? "," : "", raw[i] & 0xff, (raw[i] >> 8) & 0xff,
+               (raw[i] >> 16) & 0xff, raw[i] >> 24);
+      s += buf;
+    }
+    return s + "]";
+  }
   // {"d9":12,"0f58":3,...}: the `top` most frequent keys
   std::string json(size_t top = 16) const {
     std::vector<std::pair<uint64_t, uint32_t>> v;
