@@ -86,6 +86,31 @@ def parse():
     return ap.parse_args()
 
 
+GPUS_PER_NODE = 8  # an MI355X node (BASELINE.json: 1/2/4/8 GPUs)
+MUTATION = ("batches of >= 8192 testcases are mutated in parallel chunks of 2048, each chunk with its own "
+            "mutator and a generator seeded from the node's seed-1337 stream in chunk order (runner.cc "
+            "kParMutateMin / kMutateChunk): deterministic, but not server.h's single-mutator stream "
+            "(--serial-mutation restores that)")
+
+
+def node_extrapolation(value: float, cpu: dict, core_info: dict) -> dict | None:
+    """The reference runs one wtf client per core of the node; the box gives
+    this job a 16-core share (OMP_NUM_THREADS) of a 256-CPU, 8-GPU machine, so
+    the whole-node CPU figure is extrapolated linearly from the measured
+    per-core rate (labelled as such), and set against 8 GPUs at this line's
+    per-GPU rate (also linear: weak scaling, the driver's SCALE run measures
+    the real one)."""
+    node_cores = core_info.get("os_cpu_count") or 0
+    if not cpu or not node_cores or cpu["cores"] >= node_cores:
+        return None
+    per_core = cpu["value"] / cpu["cores"]
+    return {"kind": "extrapolated", "cores": node_cores, "value": per_core * node_cores,
+            "per_core": per_core, "gpus": GPUS_PER_NODE,
+            "vs_cpu_node": value * GPUS_PER_NODE / (per_core * node_cores),
+            "basis": f"linear in cores from {cpu['cores']} measured cores (the job's CPU share; a process per "
+                     f"machine core would exceed it) and linear in GPUs from this 1-GPU value"}
+
+
 def cpu_cores() -> tuple[int, dict]:
     """Host threads the CPU baselines use: the CPU share the job may use
     (OMP_NUM_THREADS when the environment sets it, as the GPU box does, else
@@ -252,6 +277,9 @@ def hevd_leg(base: str, lanes: int, limit: int, seconds: float, flags=()) -> dic
             "gpu_retired_fraction": (g["retired"] - g["error_retired"]) / max(1, g["retired"]),
             "lanes_per_wave_step": g["retired"] / max(1, b["group_steps"]),
             "roofline": roofline(b["alg_bytes"], b["kernel_launches"], b["kernel_ms"], pmc), "backend": b,
+            "kernel_busy_frac": b["kernel_ms"] / (g["wall_s"] * 1e3),
+            "note": "the HEVD look-alike's IOCTL path is ~300 instructions per exec: no IO manager (SURVEY F3), so "
+                    "this leg says little about a real HEVD snapshot's throughput",
             "node": {k: g.get(k) for k in ("step_ms", "account_ms", "newcov_ms", "crashsave_ms", "produce_wait_ms",
                                            "make_ms", "fill_ms", "run_s", "batches", "crashes")}}
 
@@ -396,6 +424,8 @@ def run(a, rank, world, local, tmp):
             "config": {"workload": TARGETS["tlv_server"][1], "lanes_per_gpu": a.lanes, "limit": a.limit,
                        "max_len": TARGETS["tlv_server"][2], "slice_steps": a.slice_steps or 4096,
                        "regroup_steps": a.regroup_steps if a.regroup_steps >= 0 else 1024,  # engine default
+                       "regroup_auto": "off while a run retires >= 56 lanes per wave-step, on again below 40",
+                       "mutation": MUTATION,
                        "parallelism": f"shard{world}: one node per GPU (seed + rank), RCCL MAX coverage-map "
                                       f"merge per batch"},
             "instr_per_exec": retired / max(1.0, execs),
@@ -409,13 +439,20 @@ def run(a, rank, world, local, tmp):
             "cpu_baseline": cpu.get("tlv_server"),
             "host_cpus": core_info,
         }
+        out["kernel_busy_frac"] = fields["kernel_ms"] / (dt * 1e3)  # sum of k_run time / wall
         if out["cpu_baseline"]:
             out["vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+            out["cpu_node"] = node_extrapolation(out["value"], out["cpu_baseline"], core_info)
+            if out["cpu_node"]:
+                out["vs_cpu_node"] = out["cpu_node"]["vs_cpu_node"]
         if legs:
             h = hevd_leg(hevd_dir, a.lanes, a.hevd_limit, a.leg_seconds, sched_flags(a))
             if "hevd" in cpu:
                 h["cpu_baseline"] = cpu["hevd"]
                 h["vs_cpu"] = h["value"] / cpu["hevd"]["value"]
+                h["cpu_node"] = node_extrapolation(h["value"], cpu["hevd"], core_info)
+                if h["cpu_node"]:
+                    h["vs_cpu_node"] = h["cpu_node"]["vs_cpu_node"]
             out["hevd"] = h
             s = syn_leg(a.syn_lanes, a.limit, 10, local)
             if "syn" in cpu:

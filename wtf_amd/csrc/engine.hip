@@ -1777,6 +1777,11 @@ struct wtfgpu_ctx {
   u64 scratch_bytes = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   u64 regroup_steps = 1024;
+  // regrouping pays only while lanes diverge from their wave neighbours:
+  // regroup_now() turns it off while the last run retired >= 56 lanes per
+  // wave-step and back on below 40 (WTFGPU_REGROUP_AUTO=0: never)
+  bool regroup_auto = true, regroup_off = false;
+  double lanes_per_step = 0;
   u32 async_launches = 0;
   // the current queue's resources live in the members above; the others here
   QueueRes queues[2];
@@ -1994,6 +1999,7 @@ int wtfgpu_create(int device, wtfgpu_ctx **out) {
   // HEVD 0.73M -> 1.9M execs/s, tlv 2.0M -> 2.1-2.3M, SYN 0.88M -> 0.81M)
   c->regroup_steps = 1024;
   if (const char *e = getenv("WTFGPU_REGROUP_STEPS")) c->regroup_steps = strtoull(e, nullptr, 0);
+  if (const char *e = getenv("WTFGPU_REGROUP_AUTO")) c->regroup_auto = e[0] != '0';
   {
     // shared decoded-uop cache: 32K entries of 192 bytes (WTFGPU_GUC=0: off)
     const char *e = getenv("WTFGPU_GUC");
@@ -2715,6 +2721,20 @@ static Dev run_params(wtfgpu_ctx *c, bool regroup) {
   return Q;
 }
 
+// Whether this run regroups (see wtfgpu_ctx::regroup_auto), and the
+// measurement the next decision uses.
+static u64 regroup_now(wtfgpu_ctx *c, u32 count) {
+  if (!c->regroup_steps || count < 2 * c->P.lpw) return 0;
+  if (!c->regroup_auto) return c->regroup_steps;
+  static constexpr double kOff = 56, kOn = 40;
+  if (c->lanes_per_step >= kOff) c->regroup_off = true;
+  else if (c->lanes_per_step < kOn) c->regroup_off = false;
+  return c->regroup_off ? 0 : c->regroup_steps;
+}
+static void regroup_observe(wtfgpu_ctx *c, u64 group_steps, u64 retired) {
+  if (group_steps >= 64) c->lanes_per_step = (double)retired / (double)group_steps;
+}
+
 // One k_run launch of `steps` wave-steps over [first, first + count), after
 // the regrouping sort when on.
 static int launch_chunk(wtfgpu_ctx *c, const Dev &Q, u32 first, u32 count, u64 steps, bool regroup) {
@@ -2761,9 +2781,8 @@ int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps
   // Cross-wave regrouping: launches of `regroup` wave-steps, between them the
   // lanes are sorted by rip so that lanes that diverged from their wave
   // neighbours meet lanes at the same rip in another wave (wtfgpu_set_regroup,
-  // WTFGPU_REGROUP_STEPS; 0 = fixed lane order).
-  u64 regroup = c->regroup_steps;
-  if (count < 2 * c->P.lpw) regroup = 0;
+  // WTFGPU_REGROUP_STEPS; 0 = fixed lane order; regroup_now).
+  const u64 regroup = regroup_now(c, count);
   if (regroup) {
     chunk = regroup;
     if (int rc = regroup_buffers(c)) return rc;
@@ -2799,6 +2818,7 @@ int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps
     print_stamps(s);
     if (s[2] == 0 || done >= max_steps) break;
   }
+  regroup_observe(c, st.group_steps, st.lane_retired);
   st.kernel_ms = ms_total;
   if (stats) *stats = st;
   return WTFGPU_OK;
@@ -2810,8 +2830,7 @@ int wtfgpu_run_async(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max
   if (!c->P.pool) return WTFGPU_ERR_STATE;
   if (c->async_launches) return WTFGPU_ERR_STATE;
   HIPCHK(hipSetDevice(c->device));
-  u64 regroup = c->regroup_steps;
-  if (count < 2 * c->P.lpw) regroup = 0;
+  const u64 regroup = regroup_now(c, count);
   const u64 chunk = regroup ? regroup : max_steps;
   if (regroup)
     if (int rc = regroup_buffers(c)) return rc;
@@ -2845,6 +2864,7 @@ int wtfgpu_run_wait(wtfgpu_ctx *c, wtfgpu_run_stats_t *stats) {
     st.lane_retired = s[1];
     st.kernel_ms = ms;
     c->async_launches = 0;
+    regroup_observe(c, st.group_steps, st.lane_retired);
     print_stamps(s);
   }
   if (stats) *stats = st;
