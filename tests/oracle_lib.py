@@ -8,7 +8,7 @@ import subprocess
 from wtf_amd.abi import Exit, Regs
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+from tests.cpu_bins import ALT, ORACLE_SO  # noqa: E402
 
 _lib = None
 
@@ -17,7 +17,7 @@ def lib() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(ORACLE_SO):
+    if not ALT and not os.path.exists(ORACLE_SO):
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "liboracle.so"])
     L = C.CDLL(ORACLE_SO)
     P, U32, U64 = C.c_void_p, C.c_uint32, C.c_uint64

@@ -6,7 +6,7 @@ import pytest
 
 import bench
 
-TWIN = os.path.join(bench.ROOT, "oracle", "wtf_twin")
+from tests.cpu_bins import TWIN  # noqa: E402
 
 
 @pytest.mark.skipif(not os.path.exists(TWIN), reason="oracle/wtf_twin not built")

@@ -34,14 +34,14 @@ sys.path.insert(0, ROOT)
 
 from wtf_amd.tools import snapshot, syn  # noqa: E402
 
-TOOL = os.path.join(ROOT, "oracle", "hostcheck")
+from tests.cpu_bins import ALT, HOSTCHECK as TOOL  # noqa: E402
 REF = os.path.join(ROOT, "oracle", "_ref", "kdmp_ref")
 FIXTURES = os.path.join(ROOT, "tests", "golden", "kdmp_fixtures.json")
 PREFIXES = ("TYPE ", "CR3 ", "RIP ", "PAGE ", "VT ", "PARSE_FAIL")
 
 
 def _tool():
-    if not os.path.exists(TOOL):
+    if not ALT and not os.path.exists(TOOL):
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "hostcheck"])
     return TOOL
 

@@ -196,8 +196,8 @@ def test_oracle_page_crossing_movdqu_store_faults_whole():
 # against the native vectors and the oracle, so the device semantics are
 # checked on CPU before any GPU run.
 import ctypes as C  # noqa: E402
-import subprocess  # noqa: E402
 
+from tests.cpu_bins import SIMLANE_SO, ensure  # noqa: E402
 from wtf_amd.abi import Regs  # noqa: E402
 
 
@@ -209,9 +209,7 @@ class SimResult(C.Structure):
 
 
 def sim_lib():
-    d = os.path.join(HERE, "native")
-    subprocess.check_call(["make", "-s", "-C", d])
-    L = C.CDLL(os.path.join(d, "libsimlane.so"))
+    L = C.CDLL(ensure(SIMLANE_SO, os.path.join(HERE, "native")))
     L.sim_run.argtypes = [C.POINTER(C.c_uint64), C.c_char_p, C.c_uint64, C.POINTER(Regs), C.c_uint64,
                           C.POINTER(SimResult)]
     L.sim_run_mode.argtypes = L.sim_run.argtypes + [C.c_int, C.POINTER(C.c_uint64), C.c_uint64]

@@ -8,11 +8,11 @@ table state, XMM / YMM registers and the contents of every dirty page."""
 import ctypes as C
 import os
 import struct
-import subprocess
 
 import pytest
 
 from tests import sysprog2 as S
+from tests.cpu_bins import SIMLANE_SO, ensure
 from wtf_amd import abi
 from wtf_amd.abi import Regs, regs_from_state
 
@@ -149,9 +149,7 @@ class SimResult(C.Structure):
 
 
 def sim_lib():
-    d = os.path.join(HERE, "native")
-    subprocess.check_call(["make", "-s", "-C", d])
-    L = C.CDLL(os.path.join(d, "libsimlane.so"))
+    L = C.CDLL(ensure(SIMLANE_SO, os.path.join(HERE, "native")))
     L.sim_run_full.argtypes = [C.POINTER(C.c_uint64), C.c_char_p, C.c_uint64, C.POINTER(Regs), C.c_uint64,
                                C.POINTER(SimResult), C.c_int, C.POINTER(C.c_uint64), C.c_uint64, C.POINTER(Regs),
                                C.c_char_p]

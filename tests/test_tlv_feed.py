@@ -16,7 +16,7 @@ from tests.golden.gen_tlv_feed_fixtures import canonical, feeds, packet
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-OURS = os.path.join(ROOT, "oracle", "hostcheck")
+from tests.cpu_bins import HOSTCHECK as OURS  # noqa: E402
 REF = os.path.join(ROOT, "oracle", "_ref", "ref_hostcheck")
 
 pytestmark = pytest.mark.skipif(not os.path.exists(OURS), reason="oracle/hostcheck not built")

@@ -23,7 +23,7 @@ import pytest
 from tests import tlv_harness as H
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-TOOL = os.path.join(ROOT, "oracle", "hostcheck")
+from tests.cpu_bins import HOSTCHECK as TOOL  # noqa: E402
 REF_TOOL = os.path.join(ROOT, "oracle", "_ref", "ref_hostcheck")
 FX = json.load(open(os.path.join(ROOT, "tests", "golden", "wire_fixtures.json")))
 

@@ -8,7 +8,7 @@ import subprocess
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WTFGPU = os.path.join(ROOT, "wtf_amd", "host", "wtfgpu")
-TWIN = os.path.join(ROOT, "oracle", "wtf_twin")
+from tests.cpu_bins import TWIN  # noqa: E402
 
 
 def build_hevd_target(d: str) -> str:

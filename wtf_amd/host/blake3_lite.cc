@@ -57,7 +57,7 @@ void compress(const uint32_t cv[8], const uint32_t block[16], uint64_t counter, 
 
 void load_block(const uint8_t *p, size_t n, uint32_t w[16]) {
   uint8_t b[kBlock] = {0};
-  memcpy(b, p, n);
+  if (n) memcpy(b, p, n);  // an empty input may come with a null pointer
   for (int i = 0; i < 16; i++)
     w[i] = (uint32_t)b[4 * i] | (uint32_t)b[4 * i + 1] << 8 | (uint32_t)b[4 * i + 2] << 16 |
            (uint32_t)b[4 * i + 3] << 24;

@@ -137,14 +137,14 @@ bool TcpExchange_t::AllGatherV(const std::vector<uint64_t> &Mine, std::vector<ui
         buf.size() % 8)
       return false;
     All.resize(buf.size() / 8);
-    memcpy(All.data(), buf.data(), buf.size());
+    if (!buf.empty()) memcpy(All.data(), buf.data(), buf.size());
     return true;
   }
   for (int r = 1; r < world_; r++) {
     if (!recv_frame(peers_[r], buf) || buf.size() % 8) return false;
     const size_t at = All.size();
     All.resize(at + buf.size() / 8);
-    memcpy(All.data() + at, buf.data(), buf.size());
+    if (!buf.empty()) memcpy(All.data() + at, buf.data(), buf.size());
   }
   for (int r = 1; r < world_; r++)
     if (!send_frame(peers_[r], (const uint8_t *)All.data(), All.size() * 8)) return false;

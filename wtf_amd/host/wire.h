@@ -74,7 +74,7 @@ struct Reader {
     std::vector<uint64_t> S;
     if (!Need(N * 8)) return S;
     S.resize(N);
-    memcpy(S.data(), P, N * 8);
+    if (N) memcpy(S.data(), P, N * 8);
     P += N * 8;
     return S;
   }
