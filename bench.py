@@ -440,6 +440,8 @@ def run(a, rank, world, local, tmp):
             "host_cpus": core_info,
         }
         out["kernel_busy_frac"] = fields["kernel_ms"] / (dt * 1e3)  # sum of k_run time / wall
+        if timed.get("cpu_s") is not None and timed.get("wall_s"):  # host cores busy over the timed steps
+            out["host_cpu_frac"] = timed["cpu_s"] / (timed["wall_s"] * cores)
         if out["cpu_baseline"]:
             out["vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
             out["cpu_node"] = node_extrapolation(out["value"], out["cpu_baseline"], core_info)

@@ -25,9 +25,8 @@ bool ModuleSlots::ThreadSafe() const {
 
 void ModuleSlots::release() {
   const auto &R = LaneStateRegistry();
-  for (auto &objs : lanes_)
-    for (size_t i = 0; i < objs.size(); i++)
-      if (objs[i]) R[i].destroy(objs[i]);
+  for (size_t k = 0; k < lanes_.size(); k++)
+    if (lanes_[k]) R[k % R.size()].destroy(lanes_[k]);
   for (size_t i = 0; i < initial_.size(); i++) R[i].destroy(initial_[i]);
   lanes_.clear();
   initial_.clear();
@@ -38,20 +37,21 @@ void ModuleSlots::Capture(uint32_t lanes) {
   release();
   const auto &R = LaneStateRegistry();
   for (const auto &ops : R) initial_.push_back(ops.clone(ops.object()));
-  lanes_.assign(lanes, std::vector<void *>(R.size(), nullptr));
+  lanes_.assign((size_t)lanes * R.size(), nullptr);
   dirty_.assign(lanes, 0);
   t_in = -1;
 }
 
 void ModuleSlots::ResetAll() {
-  for (size_t l = 0; l < lanes_.size(); l++) ResetLane((uint32_t)l);
+  for (size_t l = 0; l < dirty_.size(); l++) ResetLane((uint32_t)l);
 }
 
 void ModuleSlots::ResetLane(uint32_t l) {
-  if (l >= lanes_.size() || !dirty_[l]) return;
+  if (l >= dirty_.size() || !dirty_[l]) return;
   const auto &R = LaneStateRegistry();
+  void **objs = lanes_.data() + (size_t)l * R.size();
   for (size_t i = 0; i < R.size(); i++)
-    if (lanes_[l][i]) R[i].assign(lanes_[l][i], initial_[i]);
+    if (objs[i]) R[i].assign(objs[i], initial_[i]);
   dirty_[l] = 0;
 }
 
@@ -61,7 +61,11 @@ void ModuleSlots::SwapIn(uint32_t lane) {
     std::abort();
   }
   const auto &R = LaneStateRegistry();
-  auto &objs = lanes_.at(lane);
+  if (lane >= dirty_.size()) {
+    fprintf(stderr, "ModuleSlots: lane %u out of range\n", lane);
+    std::abort();
+  }
+  void **objs = lanes_.data() + (size_t)lane * R.size();
   for (size_t i = 0; i < R.size(); i++) {
     if (!objs[i]) objs[i] = R[i].clone(initial_[i]);
     R[i].swap(R[i].object(), objs[i]);
@@ -76,7 +80,7 @@ void ModuleSlots::SwapOut(uint32_t lane) {
     std::abort();
   }
   const auto &R = LaneStateRegistry();
-  auto &objs = lanes_[lane];
+  void **objs = lanes_.data() + (size_t)lane * R.size();
   for (size_t i = 0; i < R.size(); i++) R[i].swap(R[i].object(), objs[i]);
   t_in = -1;
 }

@@ -93,7 +93,7 @@ class ModuleSlots {
  private:
   void release();
   std::vector<void *> initial_;             // per registered object
-  std::vector<std::vector<void *>> lanes_;  // [lane][object], nullptr = not materialised
+  std::vector<void *> lanes_;  // [lane * objects + object], nullptr = not materialised
   std::vector<uint8_t> dirty_;              // lane copy differs from initial
   ModuleInstances *inst_ = nullptr;
 };

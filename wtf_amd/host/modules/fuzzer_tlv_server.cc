@@ -22,6 +22,8 @@
 // are read-only after Init). The packet queue is per testcase, so per lane,
 // and lanes are serviced on several host threads at once. A backend that
 // takes the packets as a Feed (SetFeed true) leaves the queue empty.
+#include <cstdio>
+#include <cstring>
 #include <deque>
 #include <string>
 #include <vector>
@@ -125,21 +127,62 @@ bool Deserialize(const uint8_t *Buffer, const size_t BufferSize, std::vector<Pac
   return true;
 }
 
-// packets -> JSON as nlohmann's dump() writes it (sorted keys, no spaces)
+// packets -> JSON as nlohmann's dump() writes it (sorted keys, no spaces).
+// Written into one preallocated buffer with a digit table (the mutator calls
+// it for every testcase: the node's hottest host loop), same bytes as
+// appending std::to_string of each field.
+namespace {
+struct Digits {
+  char s[256][4];
+  uint8_t n[256];
+  Digits() {
+    for (int v = 0; v < 256; v++) n[v] = (uint8_t)snprintf(s[v], sizeof(s[v]), "%d", v);
+  }
+};
+const Digits kDigits;
+inline char *PutU64(char *o, uint64_t v) {
+  char t[20];
+  int n = 0;
+  do {
+    t[n++] = char('0' + v % 10);
+    v /= 10;
+  } while (v);
+  while (n) *o++ = t[--n];
+  return o;
+}
+inline char *PutLit(char *o, const char *s, size_t n) {
+  memcpy(o, s, n);
+  return o + n;
+}
+}  // namespace
+
 std::string Serialize(const std::vector<Packet_t> &Packets) {
-  std::string S = "{\"Packets\":[";
+  size_t Cap = 16;
+  for (const Packet_t &P : Packets) Cap += 72 + 4 * P.Body.size();
+  std::string S(Cap, '\0');
+  char *o = S.data();
+  o = PutLit(o, "{\"Packets\":[", 12);
   for (size_t i = 0; i < Packets.size(); i++) {
     const Packet_t &P = Packets[i];
-    if (i) S += ',';
-    S += "{\"Body\":[";
+    if (i) *o++ = ',';
+    o = PutLit(o, "{\"Body\":[", 9);
     for (size_t j = 0; j < P.Body.size(); j++) {
-      if (j) S += ',';
-      S += std::to_string(P.Body[j]);
+      if (j) *o++ = ',';
+      const uint8_t b = P.Body[j];
+      memcpy(o, kDigits.s[b], 4);  // the table entry is 4 bytes; only n of them count
+      o += kDigits.n[b];
     }
-    S += "],\"BodySize\":" + std::to_string(P.BodySize) + ",\"Command\":" + std::to_string(P.Command) +
-         ",\"Id\":" + std::to_string(P.Id) + "}";
+    o = PutLit(o, "],\"BodySize\":", 13);
+    o = PutU64(o, P.BodySize);
+    o = PutLit(o, ",\"Command\":", 11);
+    o = PutU64(o, P.Command);
+    o = PutLit(o, ",\"Id\":", 6);
+    o = PutU64(o, P.Id);
+    *o++ = '}';
   }
-  return S + "]}";
+  o = PutLit(o, "]}", 2);
+  S.resize((size_t)(o - S.data()));
+  return S;
 }
 
 // The snapshot's registers (Init): read-only once set, so kept out of the
@@ -153,8 +196,26 @@ void RestoreGprs(Backend_t *B) {
   B->R12(C.R12), B->R13(C.R13), B->R14(C.R14), B->R15(C.R15);
 }
 
+// The packet queue (the reference's std::deque, :42-65) as a vector and a head
+// index: ModuleSlots swaps it in and out around every call for a lane, and a
+// vector moves without allocating (a deque's move constructor allocates).
+struct PacketQueue {
+  std::vector<Packet_t> Items;
+  size_t Head = 0;
+  bool empty() const { return Head == Items.size(); }
+  const Packet_t &front() const { return Items[Head]; }
+  void pop_front() {
+    if (++Head == Items.size()) clear();
+  }
+  void clear() {
+    Items.clear();
+    Head = 0;
+  }
+  void emplace_back(Packet_t &&P) { Items.emplace_back(std::move(P)); }
+};
+
 thread_local struct {
-  std::deque<Packet_t> Packets;
+  PacketQueue Packets;
 } GlobalState;
 WTF_LANE_STATE_TLS(GlobalState);
 

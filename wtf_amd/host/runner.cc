@@ -3,6 +3,8 @@
 #include "remote.h"
 #include "module_instances.h"
 
+#include <sys/resource.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -810,6 +812,14 @@ bool FuzzSession::MergeCoverage() {
   return true;
 }
 
+// user + system CPU time of the process so far (all threads): with wall_s,
+// how busy the host cores were
+static double ProcessCpuSeconds() {
+  struct rusage u {};
+  getrusage(RUSAGE_SELF, &u);
+  return (double)u.ru_utime.tv_sec + u.ru_utime.tv_usec * 1e-6 + (double)u.ru_stime.tv_sec + u.ru_stime.tv_usec * 1e-6;
+}
+
 std::string FuzzSession::SummaryJson() const {
   const double Wall = WallSeconds();
   char b[2048];
@@ -819,7 +829,7 @@ std::string FuzzSession::SummaryJson() const {
            "\"instr_per_s\":%.3f,\"coverage\":%zu,\"corpus\":%zu,\"crashes\":%llu,\"unique_crashes\":%zu,"
            "\"timeouts\":%llu,\"cr3\":%llu,\"errors\":%llu,\"error_retired\":%llu,\"merged_rips\":%llu,"
            "\"merge_ms\":%.3f,\"produce_wait_ms\":%.3f,\"account_ms\":%.3f,\"make_ms\":%.3f,\"step_ms\":%.3f,\"fill_ms\":%.3f,"
-           "\"newcov_ms\":%.3f,\"crashsave_ms\":%.3f,"
+           "\"newcov_ms\":%.3f,\"crashsave_ms\":%.3f,\"cpu_s\":%.3f,"
            "\"backend\":",
            O_.name.c_str(), Exec_.Lanes(), X_ ? X_->Rank() : 0, X_ ? X_->World() : 1,
            (unsigned long long)S_.batches, (unsigned long long)S_.execs, (unsigned long long)S_.retired, Wall,
@@ -827,7 +837,7 @@ std::string FuzzSession::SummaryJson() const {
            Exec_.CoverageSize(), Corpus_.Size(), (unsigned long long)S_.crashes, CrashNames_.size(),
            (unsigned long long)S_.timeouts, (unsigned long long)S_.cr3, (unsigned long long)S_.errors,
            (unsigned long long)S_.error_retired, (unsigned long long)S_.merged_rips, S_.merge_ms, S_.produce_wait_ms,
-           S_.account_ms, S_.make_ms, S_.step_ms, S_.fill_ms, S_.newcov_ms, S_.crashsave_ms);
+           S_.account_ms, S_.make_ms, S_.step_ms, S_.fill_ms, S_.newcov_ms, S_.crashsave_ms, ProcessCpuSeconds());
   return std::string(b) + Exec_.StatsJson() + "}";
 }
 
