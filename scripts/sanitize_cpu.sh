@@ -14,7 +14,7 @@ CXX="g++ -std=c++20 -fPIC -fopenmp $SAN"
 CC="gcc -std=gnu99 -fPIC $SAN"
 H=$ROOT/wtf_amd/host
 cd "$H"
-SRCS="wtf_api.cc kdmp.cc blake3_lite.cc module_slots.cc module_instances.cc runner.cc mutator_lite.cc net_exchange.cc
+SRCS="wtf_api.cc kdmp.cc blake3_lite.cc host_pool.cc module_slots.cc module_instances.cc runner.cc mutator_lite.cc net_exchange.cc
       wire.cc remote.cc modules/fuzzer_tlv_server.cc modules/crash_detection_umode.cc modules/fuzzer_hevd.cc"
 objs=()
 pids=()

@@ -7,7 +7,7 @@
 #include <cstdio>
 #include <cstring>
 
-#include <omp.h>
+#include "host_pool.h"
 
 #include "blake3_lite.h"
 
@@ -85,7 +85,7 @@ bool GpuBackend_t::Initialize(const Options_t &Opts, const CpuState_t &CpuState)
   if (wtfgpu_alloc_lanes(ctx_, nlanes_, overlay_pages_, 1024)) return false;
   views_.clear();
   views_.resize(nlanes_);
-  arenas_.resize(omp_get_max_threads() + 1);
+  arenas_.resize(HostPool::Get().Threads() + 1);
   if (Opts.Limit) SetLimit(Opts.Limit);
   if (Opts.Edges && wtfgpu_set_edges(ctx_, 1) != WTFGPU_OK) return false;  // bochscpu_backend.cc:308-312
   if (!Restore(CpuState)) return false;
@@ -266,7 +266,7 @@ const uint8_t kZeroPage[Page::Size] = {};
 }  // namespace
 
 size_t GpuBackend_t::alloc_slots(size_t n, uint8_t **orig, uint8_t **data) const {
-  Arena &A = arenas_[omp_in_parallel() ? omp_get_thread_num() : 0];
+  Arena &A = arenas_[HostPool::InLoop() ? HostPool::ThreadIndex() : 0];
   while (A.cur < A.blocks.size() && A.blocks[A.cur].cap - A.blocks[A.cur].used < n) A.cur++;
   if (A.cur == A.blocks.size()) {
     Block b;
@@ -294,7 +294,7 @@ size_t GpuBackend_t::alloc_slots(size_t n, uint8_t **orig, uint8_t **data) const
 }
 
 bool GpuBackend_t::parallel_service(const ModuleSlots *slots) const {
-  return slots && slots->ThreadSafe() && omp_get_max_threads() > 1;
+  return slots && slots->ThreadSafe() && HostPool::Get().Threads() > 1;
 }
 
 uint8_t *GpuBackend_t::stage(uint32_t lane, uint64_t gpfn, const uint8_t *orig, uint8_t *data) const {
@@ -372,7 +372,7 @@ void GpuBackend_t::drop_staged(LaneView &v) const {
   if (v.pages.empty()) return;
   live_staged_ -= v.pages.size();
   v.pages.clear();
-  if (live_staged_ == 0 && !omp_in_parallel()) {  // every staged page consumed: recycle the arenas
+  if (live_staged_ == 0 && !HostPool::InLoop()) {  // every staged page consumed: recycle the arenas
     for (Arena &A : arenas_) {
       for (Block &b : A.blocks) b.used = 0;
       A.cur = 0;
@@ -542,9 +542,8 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
   // per lane: registers to upload, staged pages, logged write records / bytes
   // (counted on all host threads, then prefix sums)
   std::vector<uint64_t> rcnt(nl + 1, 0), pcnt(nl + 1, 0), roff(nl + 1, 0), boff(nl + 1, 0);
-  bool any_cr = false;
-#pragma omp parallel for schedule(static, 256) if (par) reduction(|| : any_cr)
-  for (size_t i = 0; i < nl; i++) {
+  std::atomic<bool> any_cr{false};
+  HostPool::Get().For(nl, 256, [&](size_t i) {
     const LaneView &v = views_[lanes[i]];
     rcnt[i + 1] = v.regs_dirty ? 1 : 0;
     pcnt[i + 1] = v.pages.size();
@@ -556,8 +555,8 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
       }
     roff[i + 1] = r;
     boff[i + 1] = b;
-    any_cr = any_cr || v.cr_dirty;
-  }
+    if (v.cr_dirty) any_cr.store(true, std::memory_order_relaxed);
+  }, par);
   for (size_t i = 0; i < nl; i++) {
     rcnt[i + 1] += rcnt[i];
     pcnt[i + 1] += pcnt[i];
@@ -583,8 +582,7 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
     uint32_t lo, hi;
   };
   std::vector<Cand> cand(pcnt[nl]);
-#pragma omp parallel for schedule(static, 256) if (par)
-  for (size_t i = 0; i < nl; i++) {
+  HostPool::Get().For(nl, 256, [&](size_t i) {
     const uint32_t l = lanes[i];
     LaneView &v = views_[l];
     if (v.regs_dirty) {
@@ -594,11 +592,10 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
     }
     uint64_t k = pcnt[i];
     for (const Staged &p : v.pages) cand[k++] = Cand{l, &p, 0, 0};
-  }
-#pragma omp parallel for schedule(dynamic, 64)
-  for (size_t i = 0; i < cand.size(); i++) {
+  }, par);
+  HostPool::Get().For(cand.size(), 64, [&](size_t i) {
     const uint8_t *d = cand[i].p->data, *o = cand[i].p->orig;
-    if (!memcmp(d, o, Page::Size)) continue;
+    if (!memcmp(d, o, Page::Size)) return;
     size_t lo = 0, hi = Page::Size;
     while (lo + 8 <= hi && !memcmp(d + lo, o + lo, 8)) lo += 8;
     while (lo < hi && d[lo] == o[lo]) lo++;
@@ -606,7 +603,7 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
     while (hi > lo && d[hi - 1] == o[hi - 1]) hi--;
     cand[i].lo = (uint32_t)lo;
     cand[i].hi = (uint32_t)hi;
-  }
+  });
   // the write records and their bytes, laid out per lane and filled on all
   // host threads into a pinned buffer: one DMA to the device
   uint64_t cbytes = 0, crecs = 0;
@@ -625,8 +622,7 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
     if (wtfgpu_host_alloc(ctx_, wpin_cap_, &p)) return WTFGPU_ERR_OOM;
     wpin_ = (uint8_t *)p;
   }
-#pragma omp parallel for schedule(static, 256) if (par)
-  for (size_t i = 0; i < nl; i++) {
+  HostPool::Get().For(nl, 256, [&](size_t i) {
     const uint32_t l = lanes[i];
     LaneView &v = views_[l];
     uint64_t r = roff[i], b = boff[i];
@@ -639,7 +635,7 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
     }
     v.wlog.clear();
     v.wdata.clear();
-  }
+  }, par);
   {
     uint64_t r = roff[nl], b = boff[nl];
     for (const Cand &c : cand) {
@@ -684,15 +680,14 @@ bool GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first
               l, (unsigned long long)ex[l - first].rip);
       return false;
     }
-#pragma omp parallel for schedule(static, 1024) if (pending.size() >= 2048)
-  for (size_t pi = 0; pi < pending.size(); pi++) {
+  HostPool::Get().For(pending.size(), 1024, [&](size_t pi) {
     const uint32_t l = pending[pi];
-    if (done[l - first]) continue;
+    if (done[l - first]) return;
     const wtfgpu_exit_t &e = ex[l - first];
     LaneView &v = views_[l];
     switch (e.status) {
-      case WTFGPU_EXIT_BREAKPOINT: hit[pi] = 1; continue;
-      case WTFGPU_RUNNING: continue;  // sliced: still running when the slice ended
+      case WTFGPU_EXIT_BREAKPOINT: hit[pi] = 1; return;
+      case WTFGPU_RUNNING: return;  // sliced: still running when the slice ended
       case WTFGPU_EXIT_TIMEOUT: v.result = Timedout_t(); break;    // bochscpu_backend.cc:458-469
       case WTFGPU_EXIT_INT3:                                         // :595-619
       case WTFGPU_EXIT_HLT: v.result = Crash_t(); break;             // :690-697
@@ -700,7 +695,7 @@ bool GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first
       case WTFGPU_EXIT_FAULT: v.result = FaultToResult(e.vector, e.error, e.rip, e.addr, e.opcode); break;
       case WTFGPU_EXIT_STOPPED: break;
       case WTFGPU_EXIT_STOP_OK: v.result = Ok_t(); break;           // device Feed action: Stop(Ok_t())
-      case WTFGPU_EXIT_STOP_ARGS: hit[pi] = 2; continue;            // named below from the kept arguments
+      case WTFGPU_EXIT_STOP_ARGS: hit[pi] = 2; return;            // named below from the kept arguments
       default:
         // unimplemented opcode / overlay full / a device Feed write that
         // failed: the engine cannot finish the testcase. Not a target bug:
@@ -721,7 +716,7 @@ bool GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first
         break;
     }
     done[l - first] = 1;
-  }
+  }, pending.size() >= 2048);
   std::vector<uint32_t> named;
   for (size_t pi = 0; pi < pending.size(); pi++) {
     if (hit[pi] == 1) hits.push_back(pending[pi]);
@@ -731,9 +726,8 @@ bool GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first
   // device StopWithArgs actions: the handler's Stop(Result(GetArg(0..5)))
   std::vector<uint64_t> args(named.size() * 6);
   const bool ok = wtfgpu_read_stop_args(ctx_, named.data(), (uint32_t)named.size(), args.data()) == WTFGPU_OK;
-  uint64_t bad = 0;
-#pragma omp parallel for schedule(static, 512) reduction(+ : bad) if (named.size() >= 2048)
-  for (size_t k = 0; k < named.size(); k++) {
+  std::atomic<uint64_t> bad{0};
+  HostPool::Get().For(named.size(), 512, [&](size_t k) {
     const uint32_t l = named[k];
     LaneView &v = views_[l];
     const auto it = args_results_.find(ex[l - first].rip);
@@ -745,7 +739,7 @@ bool GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first
       bad++;
     }
     done[l - first] = 1;
-  }
+  }, named.size() >= 2048);
   stats_.err_other += bad;
   return true;
 }
@@ -766,8 +760,7 @@ bool GpuBackend_t::fill_results(const std::vector<uint32_t> &lanes, uint32_t fir
     regs.resize(fin.size() * 18);
     if (!fin.empty() && wtfgpu_read_gprs_list(ctx_, fin.data(), (uint32_t)fin.size(), regs.data())) return false;
   }
-#pragma omp parallel for schedule(static, 1024) if (fin.size() >= 2048)
-  for (size_t i = 0; i < fin.size(); i++) {
+  HostPool::Get().For(fin.size(), 1024, [&](size_t i) {
     LaneResult &r = (*out)[fin[i]];
     const LaneView &v = views_[fin[i]];
     r.result = v.result ? *v.result : TestcaseResult_t(Ok_t());
@@ -779,7 +772,7 @@ bool GpuBackend_t::fill_results(const std::vector<uint32_t> &lanes, uint32_t fir
     }
     r.icount = ex[fin[i] - first].icount;
     r.exit_status = ex[fin[i] - first].status;
-  }
+  }, fin.size() >= 2048);
   stats_.regs_ms += ms_since(tg);
   return true;
 }
@@ -856,8 +849,7 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
     // fixed frames (e.g. the tlv packet buffer, bp_pages_)
     std::vector<uint64_t> sp_gpfn(hits.size(), ~0ull), sp_gpa(hits.size(), ~0ull);
     // lane views of the hits (independent per lane: all host threads)
-#pragma omp parallel for schedule(static)
-    for (size_t i = 0; i < hits.size(); i++) {
+    HostPool::Get().For(hits.size(), 256, [&](size_t i) {
       LaneView &v = views_[hits[i]];
       memcpy(v.gpr, &regs[i * 18], 18 * 8);
       v.seed = seeds[i];
@@ -879,7 +871,7 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
           sp_gpfn[i] = sp.U64() >> 12;
         }
       }
-    }
+    });
     // the handlers: lane by lane, or on all host threads when the module keeps
     // its per-testcase state thread_local (each thread services its own lanes
     // with g_Backend = this and its own swapped-in module state). The order of
@@ -929,13 +921,12 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
     std::vector<uint32_t> pf_lanes, win_lanes;
     std::vector<uint64_t> pf_gpas, win_gpas;
     std::vector<uint8_t> use_win(hits.size(), 0);
-#pragma omp parallel for schedule(static)
-    for (size_t i = 0; i < hits.size(); i++) {
-      if (scouted[i] || sp_gpfn[i] == ~0ull) continue;
+    HostPool::Get().For(hits.size(), 256, [&](size_t i) {
+      if (scouted[i] || sp_gpfn[i] == ~0ull) return;
       const LaneView &v = views_[hits[i]];
       if (bp_stack_.count(v.gpr[16]) && in_overlay(v, sp_gpfn[i]))
         use_win[i] = (sp_gpa[i] & 0xfff) + LaneView::kWin <= Page::Size ? 1 : 2;  // 2: whole page
-    }
+    });
     for (size_t i = 0; i < hits.size(); i++) {
       if (scouted[i]) continue;
       const LaneView &v = views_[hits[i]];
@@ -963,13 +954,12 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
       std::vector<uint8_t> buf(nw * LaneView::kWin);
       if (wtfgpu_gather_bytes(ctx_, win_lanes.data(), win_gpas.data(), (uint32_t)nw, LaneView::kWin, buf.data()))
         return false;
-#pragma omp parallel for schedule(static)
-      for (size_t i = 0; i < nw; i++) {
+      HostPool::Get().For(nw, 256, [&](size_t i) {
         LaneView &v = views_[win_lanes[i]];
         v.win_gpa = win_gpas[i];
         v.win_len = LaneView::kWin;
         memcpy(v.win, buf.data() + i * LaneView::kWin, LaneView::kWin);
-      }
+      });
       stats_.stack_windows += nw;
     }
     if (!pf_lanes.empty()) {
@@ -977,8 +967,7 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
       uint8_t *o, *d;
       alloc_slots(np, &o, &d);
       if (wtfgpu_gather_pages(ctx_, pf_lanes.data(), pf_gpas.data(), (uint32_t)np, o)) return false;
-#pragma omp parallel for schedule(static)
-      for (size_t i = 0; i < np; i++) memcpy(d + i * Page::Size, o + i * Page::Size, Page::Size);
+      HostPool::Get().For(np, 256, [&](size_t i) { memcpy(d + i * Page::Size, o + i * Page::Size, Page::Size); });
       for (size_t i = 0; i < np; i++)
         stage(pf_lanes[i], pf_gpas[i] >> 12, o + i * Page::Size, d + i * Page::Size);
       stats_.prefetched_pages += np;
@@ -986,13 +975,10 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
     const auto t2 = Clock::now();
     stats_.prefetch_ms += std::chrono::duration<double, std::milli>(t2 - t1).count();
     if (per_lane_state && parallel_service(slots)) {
-#pragma omp parallel
-      {
+      HostPool::Get().For(hits.size(), 64, [&](size_t h) {
         g_Backend = this;
-#pragma omp for schedule(dynamic, 64)
-        for (size_t h = 0; h < hits.size(); h++)
-          if (!scouted[h]) service(h);
-      }
+        if (!scouted[h]) service(h);
+      });
     } else {
       for (size_t h = 0; h < hits.size(); h++)
         if (!scouted[h]) service(h);
@@ -1186,12 +1172,10 @@ void GpuBackend_t::insert_lanes(const Target_t &Target, const std::vector<uint32
     if (Slots) Slots->SwapOut(l);
   };
   if (parallel_service(Slots)) {
-#pragma omp parallel
-    {
+    HostPool::Get().For(lanes.size(), 256, [&](size_t i) {
       g_Backend = this;
-#pragma omp for schedule(dynamic, 256)
-      for (size_t i = 0; i < lanes.size(); i++) insert(i);
-    }
+      insert(i);
+    });
   } else {
     g_Backend = this;
     for (size_t i = 0; i < lanes.size(); i++) insert(i);
@@ -1209,12 +1193,10 @@ void GpuBackend_t::target_restore(const Target_t &Target, const std::vector<uint
     if (Slots) Slots->SwapOut(l);
   };
   if (parallel_service(Slots)) {
-#pragma omp parallel
-    {
+    HostPool::Get().For(lanes.size(), 256, [&](size_t i) {
       g_Backend = this;
-#pragma omp for schedule(dynamic, 256)
-      for (size_t i = 0; i < lanes.size(); i++) restore(lanes[i]);
-    }
+      restore(lanes[i]);
+    });
   } else {
     g_Backend = this;
     for (uint32_t l : lanes) restore(l);
@@ -1343,15 +1325,14 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
   if (!fresh.empty()) {
     if (wtfgpu_restore_lanes(ctx_, fresh.data(), (uint32_t)fresh.size())) return false;
     stats_.restore_dev_ms += ms_since(ti);
-#pragma omp parallel for schedule(static)
-    for (size_t i = 0; i < fresh.size(); i++) {
+    HostPool::Get().For(fresh.size(), 256, [&](size_t i) {
       const uint32_t l = fresh[i];
       reset_view(l);
       busy_[l] = 1;
       tag_[l] = In[i].tag;
       tc_bytes_[l] = In[i].size;
       lres_[l] = LaneResult{};
-    }
+    });
     const auto tm = Clock::now();
     stats_.restore_ms += std::chrono::duration<double, std::milli>(tm - ti).count();
     std::vector<uint8_t> ok;
@@ -1380,11 +1361,10 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
         if (wtfgpu_host_alloc(ctx_, P.pin_cap, &p)) return false;
         P.pin = (uint8_t *)p;
       }
-#pragma omp parallel for schedule(static, 256)
-      for (size_t i = 0; i < n; i++) {
+      HostPool::Get().For(n, 256, [&](size_t i) {
         const LaneView &v = views_[fresh[i]];
         if (!v.feed.empty()) memcpy(P.pin + off[i], v.feed.data(), v.feed.size());
-      }
+      });
       if (wtfgpu_set_feed_lanes(ctx_, fresh.data(), (uint32_t)n, off.data(), has.data(), P.pin, off[n]))
         return false;
       stats_.up_feed_ms += ms_since(tf);
@@ -1449,14 +1429,13 @@ bool GpuBackend_t::harvest_part(Part &P, const Target_t &Target, std::vector<Str
   stats_.target_restore_ms += ms_since(tr);
   const size_t base = Out.size();
   Out.resize(base + finished.size());
-#pragma omp parallel for schedule(static, 1024) if (finished.size() >= 8192)
-  for (size_t i = 0; i < finished.size(); i++) {
+  HostPool::Get().For(finished.size(), 1024, [&](size_t i) {
     const uint32_t l = finished[i];
     Out[base + i] = StreamResult_t{tag_[l], std::move(lres_[l])};
     lres_[l] = LaneResult{};
     busy_[l] = 0;
     // not runnable until refilled (a finished lane keeps its exit status)
-  }
+  }, finished.size() >= 8192);
   stats_.batches++;
   return true;
 }

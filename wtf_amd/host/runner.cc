@@ -1,6 +1,7 @@
 // runner.cc — see runner.h.
 #include "runner.h"
 #include "remote.h"
+#include "host_pool.h"
 #include "module_instances.h"
 
 #include <sys/resource.h>
@@ -25,13 +26,6 @@ namespace {
 // kParMutateMin new testcases, kMutateChunk testcases per generator
 constexpr size_t kParMutateMin = 8192, kMutateChunk = 2048;
 
-// host threads for batch mutation: OMP_NUM_THREADS when set, else up to 16
-unsigned host_threads() {
-  if (const char *E = getenv("OMP_NUM_THREADS"))
-    if (atoi(E) > 0) return (unsigned)atoi(E);
-  const unsigned H = std::thread::hardware_concurrency();
-  return H == 0 ? 1 : std::min(H, 16u);
-}
 using Clock = std::chrono::steady_clock;
 double secs_since(Clock::time_point t0) { return std::chrono::duration<double>(Clock::now() - t0).count(); }
 
@@ -725,10 +719,10 @@ bool FuzzSession::StreamStep(bool Done) {
   // crash names already seen, looked up on all host threads (read-only) so
   // that the serial bookkeeping below only hashes the new ones
   std::vector<uint8_t> Known(Out.size(), 0);
-#pragma omp parallel for schedule(static, 512) if (Out.size() >= 4096)
-  for (size_t i = 0; i < Out.size(); i++)
+  HostPool::Get().For(Out.size(), 512, [&](size_t i) {
     if (const Crash_t *C = std::get_if<Crash_t>(&Out[i].r.result))
       Known[i] = !Out[i].r.error && CrashNames_.count(C->CrashName) != 0;
+  }, Out.size() >= 4096);
   for (size_t i = 0; i < Out.size(); i++) {
     StreamResult_t &F = Out[i];
     const TcRef R = Slot_[F.tag];
