@@ -50,8 +50,8 @@
  *       base, TSC_AUX); any other MSR, a non-canonical base / entry point or
  *       upper bits in SFMASK / TSC_AUX is #GP(0); EFER.LMA is read-only.
  *   U22 SSE / SSE2: the legacy-encoded integer and data-movement subset (see
- *       exec_sse) plus pshufb and ptest; MMX, SSE floating-point arithmetic
- *       and the rest of SSE3+ are UNIMPLEMENTED. #UD if CR0.EM or !CR4.OSFXSR, #NM if CR0.TS, #GP(0) for a
+ *       exec_sse) plus pshufb and ptest; SSE floating-point arithmetic and
+ *       the rest of SSE3+ are UNIMPLEMENTED. MMX: U37 (exec_mmx). #UD if CR0.EM or !CR4.OSFXSR, #NM if CR0.TS, #GP(0) for a
  *       misaligned 16-byte operand of an aligned form; the checks run in that
  *       order, before any memory access.
  *   U23 AVX / AVX2 (VEX): the same subset at 128 / 256 bits plus vzeroupper,
@@ -1116,6 +1116,242 @@ static void ptest(orc_machine *m, const u8 *a, const u8 *b, int n) {
   m->r.rflags = (m->r.rflags & ~RF_STATUS) | (z ? RF_ZF : 0) | (c ? RF_CF : 0);
 }
 
+/* ---------------- MMX (U37) ----------------
+ * The MMX and SSE-integer-on-MMX forms of 0f 60-7f, c4 / c5, d1-fe (no
+ * mandatory prefix), emms, and movq2dq / movdq2q (f3 / f2 0f d6). mm i is
+ * physical x87 register R(i); fpst holds ST(0..7), so mm i = fpst[(i - TOS) & 7].
+ * A completed MMX instruction sets TOS = 0 (fpst rotated to R order) and every
+ * tag valid (fptw = 0); emms sets every tag empty (fptw = 0xffff). Checks in
+ * order: #UD if CR0.EM, #NM if CR0.TS, #MF if FSW.ES, then the operand's
+ * memory faults (8-byte operands, no alignment check). ModRM's mm fields
+ * ignore REX. maskmovq, the SSSE3 (0f 38 / 0f 3a) and the floating-point
+ * MMX forms are UNIMPLEMENTED; 0f 6c / 6d / d0 / d6 / e6 / f0 without a prefix
+ * are #UD. */
+static int mmx_opcode(u32 op) {
+  return (op >= 0x60 && op <= 0x7f && op != 0x78 && op != 0x79 && op != 0x7a && op != 0x7b && op != 0x7c &&
+          op != 0x7d) ||
+         op == 0xc4 || op == 0xc5 || (op >= 0xd0 && op <= 0xfe);
+}
+static u64 mmx_read(const orc_machine *m, u32 i) { return m->r.fpst[(i - ((m->r.fpsw >> 11) & 7)) & 7]; }
+/* a completed MMX instruction: TOS = 0 (fpst rotated to R order), tags valid */
+static void mmx_commit(orc_machine *m) {
+  const u32 tos = (m->r.fpsw >> 11) & 7;
+  if (tos) {
+    u64 t[8];
+    for (u32 j = 0; j < 8; j++) t[j] = m->r.fpst[(j - tos) & 7];
+    memcpy(m->r.fpst, t, sizeof(t));
+  }
+  m->r.fpsw &= (u16)~0x3800;
+  m->r.fptw = 0;
+}
+static x128 x64(u64 v) {
+  x128 r;
+  memset(r.b, 0, 16);
+  memcpy(r.b, &v, 8);
+  return r;
+}
+
+static int exec_mmx(orc_machine *m, insn *d, int pc) {
+  const u32 op = d->op, r3 = d->reg & 7, mr = d->reg & 7, mm_rm = d->rm & 7;
+  const int mem = d->is_mem;
+  const u8 imm = d->bytes[d->len - 1];
+  if (pc == 0 && (op == 0xd0 || op == 0xd6 || op == 0xe6 || op == 0xf0 || op == 0x6c || op == 0x6d)) {
+    fault(m, WTFGPU_VEC_UD, 0);
+    return X_FAULT;
+  }
+  if (op == 0xf7) return X_UNIMPL; /* maskmovq */
+  if ((op >= 0x71 && op <= 0x73) && (mem || !((op == 0x73) ? (r3 == 2 || r3 == 6) : (r3 == 2 || r3 == 4 || r3 == 6)))) {
+    fault(m, WTFGPU_VEC_UD, 0); /* register forms /2 /4 /6 (73: /2 /6) only */
+    return X_FAULT;
+  }
+  if ((op == 0xc5 || op == 0xd7 || (op == 0xd6 && pc)) && mem) {
+    fault(m, WTFGPU_VEC_UD, 0);
+    return X_FAULT;
+  }
+  if (op == 0xe7 && !mem) {
+    fault(m, WTFGPU_VEC_UD, 0);
+    return X_FAULT;
+  }
+  if (m->r.cr0 & 4) { /* CR0.EM */
+    fault(m, WTFGPU_VEC_UD, 0);
+    return X_FAULT;
+  }
+  if (m->r.cr0 & 8) { /* CR0.TS */
+    fault(m, 7, 0);
+    return X_FAULT;
+  }
+  if (m->r.fpsw & 0x80) { /* a pending unmasked x87 exception */
+    fault(m, 16, 0);
+    return X_FAULT;
+  }
+  if (op == 0x77) { /* emms */
+    m->r.fptw = 0xffff;
+    return X_OK;
+  }
+  if (op == 0xd6) { /* f3: movq2dq xmm, mm; f2: movdq2q mm, xmm */
+    if (pc == 2) {
+      const u64 v = mmx_read(m, mm_rm);
+      mmx_commit(m);
+      xput(m, d->reg, x64(v));
+    } else {
+      const x128 x = xreg(m, d->rm);
+      mmx_commit(m);
+      m->r.fpst[mr] = el(&x, 0, 8);
+    }
+    return X_OK;
+  }
+  const u64 av = mmx_read(m, mr);
+  u64 bv = 0;
+  /* the r/m source (not for the forms whose r/m is a destination or a GPR) */
+  const int rm_src = !(op == 0x7e || op == 0x7f || op == 0xe7 || op == 0x6e || op == 0xc4);
+  if (rm_src) {
+    if (mem) {
+      if (vread(m, d->ea, 8, &bv)) return X_FAULT;
+    } else {
+      bv = mmx_read(m, mm_rm);
+    }
+  }
+  x128 a = x64(av), b = x64(bv), r;
+  u64 res;
+  int to_gpr = -1;
+  switch (op) {
+  case 0x6e: { /* movd / movq mm, r/m */
+    const int n = d->rexw ? 8 : 4;
+    u64 v = 0;
+    if (mem) {
+      if (vread(m, d->ea, (u32)n, &v)) return X_FAULT;
+    } else {
+      v = m->r.gpr[d->rm] & szmask(n);
+    }
+    res = v;
+    break;
+  }
+  case 0x7e: { /* movd / movq r/m, mm */
+    const int n = d->rexw ? 8 : 4;
+    const u64 v = av & szmask(n);
+    if (mem) {
+      if (vwrite(m, d->ea, (u32)n, &v)) return X_FAULT;
+      mmx_commit(m);
+      return X_OK;
+    }
+    mmx_commit(m);
+    m->r.gpr[d->rm] = v;
+    return X_OK;
+  }
+  case 0x6f: res = bv; break;
+  case 0x7f: case 0xe7: /* movq mm/m64, mm; movntq m64, mm */
+    if (mem) {
+      if (vwrite(m, d->ea, 8, &av)) return X_FAULT;
+      mmx_commit(m);
+      return X_OK;
+    }
+    mmx_commit(m);
+    m->r.fpst[mm_rm] = av;
+    return X_OK;
+  case 0x60: case 0x61: case 0x62: /* punpckl*: the low halves */
+    r = unpack(1 << (op - 0x60), 0, &a, &b);
+    res = el(&r, 0, 8);
+    break;
+  case 0x68: case 0x69: case 0x6a: { /* punpckh*: the high halves */
+    const x128 ah = x64(av >> 32), bh = x64(bv >> 32);
+    r = unpack(1 << (op - 0x68), 0, &ah, &bh);
+    res = el(&r, 0, 8);
+    break;
+  }
+  case 0x63: case 0x67: case 0x6b: { /* packsswb, packuswb, packssdw: a's elements, then b's */
+    const int w = op == 0x6b ? 4 : 2, n = 8 / w;
+    r = x64(0);
+    for (int i = 0; i < 2 * n; i++) {
+      const i64 x = i < n ? sel(&a, i, w) : sel(&b, i - n, w);
+      elput(&r, i, w / 2, op == 0x67 ? satu(x, 1) : sats(x, w / 2));
+    }
+    res = el(&r, 0, 8);
+    break;
+  }
+  case 0x64: case 0x65: case 0x66: case 0x74: case 0x75: case 0x76:
+    r = ewise(op >= 0x74 ? EW_EQ : EW_GT, 1 << ((op & 0xf) % 4), &a, &b);
+    res = el(&r, 0, 8);
+    break;
+  case 0x70: /* pshufw */
+    res = 0;
+    for (int i = 0; i < 4; i++) res |= ((bv >> (16 * ((imm >> (2 * i)) & 3))) & 0xffff) << (16 * i);
+    break;
+  case 0x71: case 0x72: case 0x73: { /* shifts by imm8 of mm (r/m) */
+    const int w = op == 0x71 ? 2 : op == 0x72 ? 4 : 8;
+    r = shift_el(r3 == 2 ? 0 : r3 == 4 ? 1 : 2, w, &b, imm);
+    mmx_commit(m);
+    m->r.fpst[mm_rm] = el(&r, 0, 8);
+    return X_OK;
+  }
+  case 0xc4: { /* pinsrw mm, r32/m16, imm8 */
+    u64 v = 0;
+    if (mem) {
+      if (vread(m, d->ea, 2, &v)) return X_FAULT;
+    } else {
+      v = m->r.gpr[d->rm];
+    }
+    const int k = imm & 3;
+    res = (av & ~(0xffffULL << (16 * k))) | ((v & 0xffff) << (16 * k));
+    break;
+  }
+  case 0xc5: /* pextrw r32, mm, imm8 */
+    to_gpr = 1;
+    res = (bv >> (16 * (imm & 3))) & 0xffff;
+    break;
+  case 0xd7: /* pmovmskb r32, mm */
+    to_gpr = 1;
+    res = 0;
+    for (int i = 0; i < 8; i++) res |= ((bv >> (8 * i + 7)) & 1) << i;
+    break;
+  case 0xd1: case 0xd2: case 0xd3: r = shift_el(0, op == 0xd1 ? 2 : op == 0xd2 ? 4 : 8, &a, bv); res = el(&r, 0, 8); break;
+  case 0xe1: case 0xe2: r = shift_el(1, op == 0xe1 ? 2 : 4, &a, bv); res = el(&r, 0, 8); break;
+  case 0xf1: case 0xf2: case 0xf3: r = shift_el(2, op == 0xf1 ? 2 : op == 0xf2 ? 4 : 8, &a, bv); res = el(&r, 0, 8); break;
+  case 0xd4: res = av + bv; break;
+  case 0xfb: res = av - bv; break;
+  case 0xfc: case 0xfd: case 0xfe: r = ewise(EW_ADD, 1 << (op - 0xfc), &a, &b); res = el(&r, 0, 8); break;
+  case 0xf8: case 0xf9: case 0xfa: r = ewise(EW_SUB, 1 << (op - 0xf8), &a, &b); res = el(&r, 0, 8); break;
+  case 0xd5: r = ewise(EW_MULLO, 2, &a, &b); res = el(&r, 0, 8); break;
+  case 0xe5: r = ewise(EW_MULHS, 2, &a, &b); res = el(&r, 0, 8); break;
+  case 0xe4: r = ewise(EW_MULHU, 2, &a, &b); res = el(&r, 0, 8); break;
+  case 0xd8: case 0xd9: r = ewise(EW_SUBUS, op - 0xd7, &a, &b); res = el(&r, 0, 8); break;
+  case 0xdc: case 0xdd: r = ewise(EW_ADDUS, op - 0xdb, &a, &b); res = el(&r, 0, 8); break;
+  case 0xe8: case 0xe9: r = ewise(EW_SUBS, op - 0xe7, &a, &b); res = el(&r, 0, 8); break;
+  case 0xec: case 0xed: r = ewise(EW_ADDS, op - 0xeb, &a, &b); res = el(&r, 0, 8); break;
+  case 0xda: r = ewise(EW_MINU, 1, &a, &b); res = el(&r, 0, 8); break;
+  case 0xde: r = ewise(EW_MAXU, 1, &a, &b); res = el(&r, 0, 8); break;
+  case 0xea: r = ewise(EW_MINS, 2, &a, &b); res = el(&r, 0, 8); break;
+  case 0xee: r = ewise(EW_MAXS, 2, &a, &b); res = el(&r, 0, 8); break;
+  case 0xe0: r = ewise(EW_AVG, 1, &a, &b); res = el(&r, 0, 8); break;
+  case 0xe3: r = ewise(EW_AVG, 2, &a, &b); res = el(&r, 0, 8); break;
+  case 0xdb: res = av & bv; break;
+  case 0xdf: res = ~av & bv; break;
+  case 0xeb: res = av | bv; break;
+  case 0xef: res = av ^ bv; break;
+  case 0xf4: res = (av & 0xffffffffULL) * (bv & 0xffffffffULL); break; /* pmuludq */
+  case 0xf5: /* pmaddwd */
+    r = x64(0);
+    for (int i = 0; i < 2; i++)
+      elput(&r, i, 4, (u64)(sel(&a, 2 * i, 2) * sel(&b, 2 * i, 2) + sel(&a, 2 * i + 1, 2) * sel(&b, 2 * i + 1, 2)) & 0xffffffffULL);
+    res = el(&r, 0, 8);
+    break;
+  case 0xf6: { /* psadbw */
+    u64 sum = 0;
+    for (int i = 0; i < 8; i++) {
+      const u32 x = (u32)((av >> (8 * i)) & 0xff), y = (u32)((bv >> (8 * i)) & 0xff);
+      sum += x > y ? x - y : y - x;
+    }
+    res = sum;
+    break;
+  }
+  default:
+    return X_UNIMPL;
+  }
+  mmx_commit(m);
+  if (to_gpr >= 0) m->r.gpr[d->reg] = res; /* zero-extended into the 64-bit register */
+  else m->r.fpst[mr] = res;
+  return X_OK;
+}
+
 static int exec_sse(orc_machine *m, insn *d) {
   const u32 op = d->op, r3 = d->reg & 7;
   const int pc = d->rep == 0xf3 ? 2 : d->rep == 0xf2 ? 3 : d->pfx66 ? 1 : 0; /* none, 66, f3, f2 */
@@ -1123,6 +1359,7 @@ static int exec_sse(orc_machine *m, insn *d) {
   const u8 imm = d->bytes[d->len - 1];
   x128 a, b, r;
   u64 v;
+  if (d->opmap == 1 && ((pc == 0 && mmx_opcode(op)) || (op == 0xd6 && pc >= 2))) return exec_mmx(m, d, pc);
   if (d->opmap == 2) { /* 66 0f 38 00 pshufb, 66 0f 38 17 ptest */
     if (pc != 1) return X_UNIMPL;
     if (m->r.cr0 & 4 || !(m->r.cr4 & 0x200)) {

@@ -1,7 +1,9 @@
-"""GPU engine on the SSE / SSE2 subset.
+"""GPU engine on the SSE / SSE2 subset and MMX (U37).
 
 1. Every native SSE vector (tests/golden/sse_vectors.json.gz) as one lane:
-   GPRs, RFLAGS, all 16 XMM registers, MXCSR and the memory window.
+   GPRs, RFLAGS, all 16 XMM registers, MXCSR and the memory window; every
+   native MMX vector (mmx_vectors.json.gz) likewise, with mm0-7, FSW and the
+   tags.
 2. The fault / encoding cases of tests/test_sse.py, GPU vs oracle.
 3. Random programs mixing SSE and integer forms, GPU vs oracle lane by lane
    (exit, registers, XMM, coverage, dirty pages, bytes, memory).
@@ -100,6 +102,74 @@ def test_gpu_matches_native_sse_vectors():
             win[k] = v
         if (c["diff"] or i % 5 == 0) and eng.read_virt(i, buf_va, 256) != bytes(win):
             fails.append((c["name"], c["code"], "mem"))
+    assert not fails, f"{len(fails)}/{len(cases)} mismatches, first: {fails[:6]}"
+
+
+def test_gpu_matches_native_mmx_vectors():
+    from tests.golden.gen_native_vectors import splitmix_bytes
+    from tests.test_mmx import DOC, abridged
+    from wtf_amd.engine import Engine
+
+    cases = DOC["cases"]
+    codes = sorted({c["code"] for c in cases})
+    slot = {c: i for i, c in enumerate(codes)}
+    blob = bytearray(32 * len(codes))
+    for c, i in slot.items():
+        b = bytes.fromhex(c) + b"\xcc"
+        blob[32 * i: 32 * i + len(b)] = b
+    sp = AddressSpace()
+    sp.map_range(CODE_VA, bytes(blob), write=False)
+    buf_va = int(DOC["buf_va"], 16)
+    page_va = buf_va & ~0xFFF
+    sp.map(page_va, b"", nx=True)
+    sp.map(page_va + 0x1000, b"", nx=True)
+    n = (len(cases) + 63) // 64 * 64
+    eng = Engine(0)
+    pfns, pblob = sp.phys()
+    eng.load_pool(pfns, pblob)
+    eng.alloc_lanes(n, overlay_pages=4, cov_entries=64)
+    eng.set_initial_state(regs_from_state(user_state(CODE_VA, 0, sp.cr3)))
+    eng.set_limit(0)
+    eng.restore()
+    regs = eng.read_regs(0, n)
+    writes = []
+    for i, c in enumerate(cases):
+        r = regs[i]
+        for k in range(16):
+            r.gpr[k] = int(c["in"][k], 16)
+        r.rip = CODE_VA + 32 * slot[c["code"]]
+        r.rflags = int(c["fl"], 16) | 0x200
+        set_xmm(r, [int(v, 16) for v in c["xin"]])
+        for k in range(8):
+            r.fpst[k] = int(c["mmin"][k], 16)
+        r.fpsw, r.fptw = 0, 0
+        writes.append((i, buf_va, splitmix_bytes(int(c["seed"], 16), 256)))
+    for i in range(len(cases), n):  # padding lanes run a lone int3
+        regs[i].rip = CODE_VA + 32 * slot[cases[0]["code"]] + len(bytes.fromhex(cases[0]["code"]))
+    eng.write_regs(regs)
+    eng.apply_writes(writes)
+    eng.run()
+    ex = eng.exits()
+    out = eng.read_regs(0, n)
+    fails = []
+    for i, c in enumerate(cases):
+        r = out[i]
+        if ex[i].status != EXIT_INT3 or ex[i].icount != 1:
+            fails.append((c["name"], c["code"], "exit", ex[i].status, ex[i].vector))
+        elif [r.gpr[k] for k in range(16)] != [int(v, 16) for v in c["out"]] or (r.rflags ^ int(c["flo"], 16)) & 0x8D5:
+            fails.append((c["name"], c["code"], "gpr"))
+        elif get_xmm(r) != [int(v, 16) for v in c["xout"]]:
+            fails.append((c["name"], c["code"], "xmm"))
+        elif [r.fpst[k] for k in range(8)] != [int(v, 16) for v in c["mmout"]]:
+            fails.append((c["name"], c["code"], "mm"))
+        elif r.fpsw != int(c["fsw"], 16) or abridged(r.fptw) != int(c["ftw"], 16):
+            fails.append((c["name"], c["code"], "x87"))
+        else:
+            win = bytearray(splitmix_bytes(int(c["seed"], 16), 256))
+            for k, v in c["diff"]:
+                win[k] = v
+            if c["diff"] and eng.read_virt(i, buf_va, 256) != bytes(win):
+                fails.append((c["name"], c["code"], "mem"))
     assert not fails, f"{len(fails)}/{len(cases)} mismatches, first: {fails[:6]}"
 
 

@@ -256,7 +256,10 @@ __device__ __forceinline__ void fetch_bytes(u64 pageptr, u32 off, u32 n, u64 &lo
 #define WTFGPU_UC_N 256  // head-only entries (the UOp lives in the uop slots below)
 #endif
 constexpr u32 UC_N = WTFGPU_UC_N;  // entries per wave (power of two)
-constexpr u32 UC_U = 8;            // uop slots per wave (power of two)
+#ifndef WTFGPU_UC_U
+#define WTFGPU_UC_U 4  // 4 x 120 bytes per wave: k_run's LDS (uop cache + lane copies) fits 160 KiB
+#endif
+constexpr u32 UC_U = WTFGPU_UC_U;  // uop slots per wave (power of two)
 constexpr u32 UC_BP = 1, UC_COVERED = 2, UC_CROSS = 4, UC_BADLEN = 8, UC_UNSUP = 16;
 struct UCHead {
   u64 key;
@@ -892,15 +895,35 @@ __device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr
 
 // Runs `call` on a copy T of lane L whose registers live in arrays of their
 // own, so the kernel's register arrays never escape into a called function
-// (they stay in VGPRs); the copy goes through scratch, which only rare paths pay.
+// (they stay in VGPRs). The copy lives in LDS (sLane / sRegs, one slot per
+// thread; WTFGPU_LANE_LDS=0: on the stack, i.e. scratch, whose write-backs
+// were most of k_run's HBM traffic).
+#ifndef WTFGPU_LANE_LDS
+#define WTFGPU_LANE_LDS 1
+#endif
+#if WTFGPU_LANE_LDS
+// the register slots take an odd stride (33 dwords) so a wave's copies spread
+// over the LDS banks; the Lane slots (60 dwords) conflict 4-way at most
+#define LANE_COPY_DECL            \
+  __shared__ Lane sLane[256];     \
+  __shared__ u32 sRegs[256][33];
+#define LANE_COPY_SLOT                                  \
+  Lane &T = sLane[threadIdx.x];                         \
+  u32 *const tlo_ = sRegs[threadIdx.x], *const thi_ = sRegs[threadIdx.x] + 16;
+#else
+#define LANE_COPY_DECL
+#define LANE_COPY_SLOT    \
+  u32 tlo_[16], thi_[16]; \
+  Lane T;
+#endif
 #define WITH_LANE_COPY(call)                      \
   do {                                            \
-    u32 tlo_[16], thi_[16];                       \
+    LANE_COPY_SLOT                                \
     _Pragma("unroll") for (int i_ = 0; i_ < 16; i_++) { \
       tlo_[i_] = glo[i_];                         \
       thi_[i_] = ghi[i_];                         \
     }                                             \
-    Lane T = L;                                   \
+    T = L;                                        \
     T.glo = tlo_;                                 \
     T.ghi = thi_;                                 \
     call;                                         \
@@ -969,6 +992,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
   const bool valid = inrange && P.status[lane] == WTFGPU_RUNNING;
   __shared__ UCEntry sUC[4][UC_N];
   __shared__ UCUop sUU[4][UC_U];
+  LANE_COPY_DECL
   UCEntry *uc = sUC[threadIdx.x >> 6];
   UCUop *uu = sUU[threadIdx.x >> 6];
   // the LDS uop cache: the warm image of an earlier launch, or empty

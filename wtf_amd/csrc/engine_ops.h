@@ -501,7 +501,10 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
       } else {
         u.bsz = u.rep == 0xf3 ? 2 : u.rep == 0xf2 ? 3 : p66 ? 1 : 0;
         u.opreg = smap << 8;
-        if (!sse_valid(smap, c, u.bsz, u.is_mem, u.reg & 7)) u.op = (c == 0xae && smap == 1) ? O_SYS2 : O_UNIMPL;
+        if (smap == 1 && ((u.bsz == 0 && mmx_opcode(c)) || (c == 0xd6 && u.bsz >= 2)))
+          u.opreg |= kMmxForm;  // U37: engine_sse.h mmx_exec
+        else if (!sse_valid(smap, c, u.bsz, u.is_mem, u.reg & 7))
+          u.op = (c == 0xae && smap == 1) ? O_SYS2 : O_UNIMPL;
       }
       if (u.op == O_SYS2) {  // group 15 beyond ldmxcsr / stmxcsr / the fences: engine_sys.h
         u.asz = osz;

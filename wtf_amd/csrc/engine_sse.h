@@ -386,10 +386,174 @@ __device__ __forceinline__ u64 sse_ea(const Dev &P, const Lane &L, const UOp &u,
 
 __device__ __noinline__ int vex_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next);
 
+// ---------------------------------------------------------------- MMX (U37)
+// The oracle's exec_mmx: mm i is physical x87 register R(i) = fpst[(i - TOS)
+// & 7] (fpst holds ST order); a completed MMX instruction rotates fpst to R
+// order (TOS = 0) and marks every tag valid, emms every tag empty. #UD if
+// CR0.EM, #NM if CR0.TS, #MF if FSW.ES, then the operand's memory faults;
+// nothing is committed before every access succeeded (exec protocol).
+// UOp::opreg bit 20 marks an MMX form (decode).
+constexpr u32 kMmxForm = 1u << 20;
+__host__ __device__ inline bool mmx_opcode(u32 c) {
+  return (c >= 0x60 && c <= 0x7f && !(c >= 0x78 && c <= 0x7d)) || c == 0xc4 || c == 0xc5 || (c >= 0xd0 && c <= 0xfe);
+}
+__device__ __forceinline__ u64 mmx_get(const wtfgpu_regs_t &F, u32 i) { return F.fpst[(i - ((F.fpsw >> 11) & 7)) & 7]; }
+__device__ __forceinline__ void mmx_commit(wtfgpu_regs_t &F) {
+  const u32 tos = (F.fpsw >> 11) & 7;
+  if (tos) {
+    u64 t[8];
+    for (u32 j = 0; j < 8; j++) t[j] = F.fpst[(j - tos) & 7];
+    for (u32 j = 0; j < 8; j++) F.fpst[j] = t[j];
+  }
+  F.fpsw = (u16)(F.fpsw & ~0x3800);
+  F.fptw = 0;
+}
+
+__device__ __noinline__ int mmx_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next) {
+  next = nrip;
+  const u32 c = u.sub, pc = u.bsz, r3 = u.reg & 7, mr = u.reg & 7, mrm = u.rm & 7;
+  const bool mem = u.is_mem;
+  const u32 imm = (u32)u.imm & 0xff;
+  const u64 ea = mem ? sse_ea(P, L, u, nrip) : 0;
+  wtfgpu_regs_t &F = P.full[L.lane];
+  bool ud = pc == 0 && (c == 0xd0 || c == 0xd6 || c == 0xe6 || c == 0xf0 || c == 0x6c || c == 0x6d);
+  if (!ud && c == 0xf7) return X_UNIMPL;  // maskmovq
+  if (c >= 0x71 && c <= 0x73)
+    ud = ud || mem || !(c == 0x73 ? (r3 == 2 || r3 == 6) : (r3 == 2 || r3 == 4 || r3 == 6));
+  ud = ud || ((c == 0xc5 || c == 0xd7 || (c == 0xd6 && pc)) && mem) || (c == 0xe7 && !mem) || (L.cr0 & 4);
+  if (ud) {
+    set_fault(L, WTFGPU_VEC_UD, 0, 0);
+    return X_FAULT;
+  }
+  if (L.cr0 & 8) {
+    set_fault(L, 7, 0, 0);  // #NM
+    return X_FAULT;
+  }
+  if (F.fpsw & 0x80) {
+    set_fault(L, 16, 0, 0);  // #MF: a pending unmasked x87 exception
+    return X_FAULT;
+  }
+  if (c == 0x77) {  // emms
+    F.fptw = 0xffff;
+    return X_OK;
+  }
+  if (c == 0xd6) {  // f3: movq2dq xmm, mm; f2: movdq2q mm, xmm
+    if (pc == 2) {
+      const u64 v = mmx_get(F, mrm);
+      mmx_commit(F);
+      xmm_put(P, L, u.reg, X128{v, 0});
+    } else {
+      const u64 v = xmm_get(P, L, u.rm).lo;
+      mmx_commit(F);
+      F.fpst[mr] = v;
+    }
+    return X_OK;
+  }
+  const u64 av = mmx_get(F, mr);
+  u64 bv = 0;
+  const bool rm_src = !(c == 0x7e || c == 0x7f || c == 0xe7 || c == 0x6e || c == 0xc4);
+  if (rm_src) {
+    if (mem) {
+      if (!vread(L, ea, 8, bv)) return X_FAULT;
+    } else {
+      bv = mmx_get(F, mrm);
+    }
+  }
+  const X128 a{av, 0}, b{bv, 0};
+  X128 r{0, 0};
+  u64 res = 0;
+  bool to_gpr = false;
+  switch (c) {
+    case 0x6e: {  // movd / movq mm, r/m
+      const u32 n = (u.rex & 8) ? 8 : 4;
+      u64 v = 0;
+      if (mem) {
+        if (!vread(L, ea, n, v)) return X_FAULT;
+      } else {
+        v = R(L, u.rm) & szmask(n);
+      }
+      res = v;
+      break;
+    }
+    case 0x7e: {  // movd / movq r/m, mm
+      const u32 n = (u.rex & 8) ? 8 : 4;
+      const u64 v = av & szmask(n);
+      if (mem && !vwrite(L, ea, n, v)) return X_FAULT;
+      mmx_commit(F);
+      if (!mem) RS(L, u.rm, v);
+      return X_OK;
+    }
+    case 0x6f: res = bv; break;
+    case 0x7f: case 0xe7:  // movq mm/m64, mm; movntq m64, mm
+      if (mem && !vwrite(L, ea, 8, av)) return X_FAULT;
+      mmx_commit(F);
+      if (!mem) F.fpst[mrm] = av;
+      return X_OK;
+    case 0x68: case 0x69: case 0x6a:  // punpckh*: the high halves
+      r = sse_unpack(1u << (c - 0x68), 0, X128{av >> 32, 0}, X128{bv >> 32, 0});
+      res = r.lo;
+      break;
+    case 0x63: case 0x67: case 0x6b: {  // packs: a's elements, then b's
+      const u32 w = c == 0x6b ? 4 : 2, h = 8 / w;
+      for (u32 i = 0; i < 2 * h; i++) {
+        const i64 x = i < h ? xsel(a, i, w) : xsel(b, i - h, w);
+        xset(r, i, w / 2, c == 0x67 ? sat_u(x, 1) : sat_s(x, w / 2));
+      }
+      res = r.lo;
+      break;
+    }
+    case 0x70:  // pshufw
+      for (u32 i = 0; i < 4; i++) res |= ((bv >> (16 * ((imm >> (2 * i)) & 3))) & 0xffff) << (16 * i);
+      break;
+    case 0x71: case 0x72: case 0x73:  // by imm8, of mm (r/m)
+      r = sse_shift_imm(c, r3, b, imm);
+      mmx_commit(F);
+      F.fpst[mrm] = r.lo;
+      return X_OK;
+    case 0xc4: {  // pinsrw mm, r32/m16, imm8
+      u64 v = 0;
+      if (mem) {
+        if (!vread(L, ea, 2, v)) return X_FAULT;
+      } else {
+        v = R(L, u.rm);
+      }
+      const u32 k = imm & 3;
+      res = (av & ~(0xffffull << (16 * k))) | ((v & 0xffff) << (16 * k));
+      break;
+    }
+    case 0xc5: to_gpr = true; res = (bv >> (16 * (imm & 3))) & 0xffff; break;  // pextrw
+    case 0xd7:  // pmovmskb r32, mm
+      to_gpr = true;
+      for (u32 i = 0; i < 8; i++) res |= ((bv >> (8 * i + 7)) & 1) << i;
+      break;
+    case 0xf4: res = (av & 0xffffffffull) * (bv & 0xffffffffull); break;  // pmuludq
+    case 0xf5:  // pmaddwd
+      for (u32 i = 0; i < 2; i++)
+        xset(r, i, 4, (u64)(xsel(a, 2 * i, 2) * xsel(b, 2 * i, 2) + xsel(a, 2 * i + 1, 2) * xsel(b, 2 * i + 1, 2)));
+      res = r.lo;
+      break;
+    case 0xf6:  // psadbw
+      for (u32 i = 0; i < 8; i++) {
+        const u64 x = (av >> (8 * i)) & 0xff, y = (bv >> (8 * i)) & 0xff;
+        res += x > y ? x - y : y - x;
+      }
+      break;
+    default:  // the rest: the 128-bit lane op on the low quadwords (counts: the source quadword)
+      if (!sse_lane(1, c, 0, a, b, imm, bv, r)) return X_UNIMPL;
+      res = r.lo;
+      break;
+  }
+  mmx_commit(F);
+  if (to_gpr) RS(L, u.reg, res);
+  else F.fpst[mr] = res;
+  return X_OK;
+}
+
 // One attempt at an SSE instruction (exec() protocol: X_FAULT with L.miss set
 // asks for a translation service and a rerun).
 __device__ __noinline__ int sse_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next) {
   if (u.opreg & 1) return vex_exec(P, L, u, nrip, next);
+  if (u.opreg & kMmxForm) return mmx_exec(P, L, u, nrip, next);
   next = nrip;
   const u32 c = u.sub, pc = u.bsz, r3 = u.reg & 7, map = vex_map(u.opreg);
   const bool mem = u.is_mem;
