@@ -378,6 +378,21 @@ int wtfgpu_set_edges(wtfgpu_ctx *ctx, int on);
  * *n gets the count (larger than per_lane: the trace was truncated). */
 int wtfgpu_set_trace(wtfgpu_ctx *ctx, uint32_t per_lane);
 int wtfgpu_read_trace(wtfgpu_ctx *ctx, uint32_t lane, uint64_t *rips, uint64_t cap, uint64_t *n);
+
+/* Tenet traces (`wtf run --trace-type tenet`, BochscpuBackend_t::DumpTenetDelta,
+ * bochscpu_backend.cc:1215-1323): per lane a stream of bytes_per_lane bytes of
+ * 8-byte-aligned entries (0 turns tracing off):
+ *   ACC  {u64 va; u64 meta = 1 << 56 | type << 32 | len; data (len bytes,
+ *        rounded up to 8)}: one data access of an instruction, type 1 read,
+ *        2 write, 3 read-modify-write; data = the memory after the instruction;
+ *   REGS {u64 meta = 2 << 56; u64 gpr[16] (rax, rcx, ... r15); u64 rip}: the
+ *        registers at the start, after each retired instruction, delivered
+ *        exception, breakpoint action or handler that moved rip, and when the
+ *        lane stops with accesses open.
+ * The stream restarts at restore. wtfgpu_read_tenet copies min(bytes, per_lane,
+ * cap) bytes of a lane; *n gets the bytes written (past per_lane: truncated). */
+int wtfgpu_set_tenet(wtfgpu_ctx *ctx, uint64_t bytes_per_lane);
+int wtfgpu_read_tenet(wtfgpu_ctx *ctx, uint32_t lane, uint8_t *buf, uint64_t cap, uint64_t *n);
 /* Device pointer + size of the uint8 coverage map (for an RCCL MAX all-reduce). */
 int wtfgpu_coverage_device_map(wtfgpu_ctx *ctx, void **dev_ptr, uint64_t *bytes);
 /* After a MAX all-reduce of the map (other shards' coverage merged in): the

@@ -143,6 +143,7 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
           }
           skip = 0;
         }
+        if (!skip) orc_tenet_event(m_);  // Tenet: the handler moved rip (or injected a #PF)
         continue;
       }
       switch (e.status) {
@@ -331,11 +332,26 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
     if (Truncated) Rips.resize(trace_cap_);
     return true;
   }
+  uint64_t tenet_cap_ = 0;                       // Tenet stream bytes per lane (EnableTenet)
+  std::vector<std::vector<uint8_t>> tenets_;     // per testcase of the last RunBatch, untruncated
+  bool EnableTenet(uint64_t BytesPerLane) override {
+    tenet_cap_ = BytesPerLane;
+    orc_set_tenet(m_, BytesPerLane != 0);
+    return true;
+  }
+  bool LaneTenet(uint32_t Lane, std::vector<uint8_t> &Bytes, bool &Truncated) override {
+    if (Lane >= tenets_.size()) return false;
+    Bytes = tenets_[Lane];
+    Truncated = Bytes.size() > tenet_cap_;
+    if (Truncated) Bytes.resize(tenet_cap_);
+    return true;
+  }
   bool RunBatch(const Target_t &Target, const std::vector<std::pair<const uint8_t *, size_t>> &Tc,
                 std::vector<LaneResult> &Out, ModuleSlots *Slots) override {
     Out.assign(Tc.size(), LaneResult{});
     route_ = Slots ? Slots->Instances() : nullptr;
     if (trace_cap_) traces_.assign(Tc.size(), {});
+    if (tenet_cap_) tenets_.assign(Tc.size(), {});
     g_Backend = this;
     for (size_t i = 0; i < Tc.size(); i++) {
       LaneResult &L = Out[i];
@@ -370,6 +386,11 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
         std::vector<uint64_t> &T = traces_[i];
         T.resize(orc_trace(m_, nullptr, 0));
         orc_trace(m_, T.data(), T.size());
+      }
+      if (tenet_cap_) {  // and its Tenet stream
+        std::vector<uint64_t> W(orc_tenet(m_, nullptr, 0));
+        orc_tenet(m_, W.data(), W.size());
+        tenets_[i].assign((const uint8_t *)W.data(), (const uint8_t *)(W.data() + W.size()));
       }
       T.Restore();
     }
@@ -418,6 +439,8 @@ int main(int argc, char **argv) {
     uint64_t LastIcount() const override { return b->Icount(); }
     bool LastError() const override { return b->engine_error_; }
     bool LaneTrace(uint32_t L, std::vector<uint64_t> &R, bool &T) override { return b->LaneTrace(L, R, T); }
+    bool EnableTenet(uint64_t P) override { return b->EnableTenet(P); }
+    bool LaneTenet(uint32_t L, std::vector<uint8_t> &R, bool &T) override { return b->LaneTenet(L, R, T); }
   } E;
   E.b = B;
   E.n = O.lanes ? O.lanes : 1;

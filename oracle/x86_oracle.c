@@ -162,6 +162,10 @@ struct orc_machine {
   int edges; /* record branch edges into the coverage (RecordEdge) */
   int trace, resumed; /* rip trace on; the next instruction resumes a breakpoint hit */
   vec tracelist;
+  /* Tenet (U38, wtfgpu_set_tenet's stream): entries as u64 words */
+  int tn, tn_mute;
+  vec tnlist;
+  u64 tn_ipos, tn_last; /* the current instruction's first entry / latest ACC entry (~0: none) */
   /* per-instruction scratch */
   wtfgpu_exit_t *ex;
   int faulted;
@@ -202,6 +206,7 @@ void orc_destroy(orc_machine *m) {
   free(m->dirty.v);
   free(m->covlist.v);
   free(m->tracelist.v);
+  free(m->tnlist.v);
   free(m);
 }
 
@@ -234,6 +239,10 @@ void orc_restore(orc_machine *m, const wtfgpu_regs_t *r) {
   hm_init(&m->cov, 1024);
   m->covlist.n = 0;
   m->tracelist.n = 0;
+  m->tnlist.n = 0;
+  m->tn_ipos = 0;
+  m->tn_last = ~0ULL;
+  m->tn_mute = 0;
   m->r = *r;
   m->initial_cr3 = r->cr3;
   m->icount = 0;
@@ -412,6 +421,48 @@ int orc_write_virt(orc_machine *m, u64 gva, const void *buf, u64 len) {
   return 0;
 }
 
+/* ---------------- Tenet (U38) ----------------
+ * The stream wtfgpu_set_tenet documents (include/wtfgpu.h), as u64 words:
+ * ACC {va, 1 << 56 | type << 32 | len, data words} for each data access of an
+ * instruction (an operand as a whole, an RMW operand once as type 3), REGS
+ * {2 << 56, gpr[16], rip} at the start, after each retired instruction,
+ * delivered exception and rip-moving breakpoint handler, and when the run
+ * stops with accesses open. ACC data = the memory after the instruction, read
+ * byte by byte through present-bit translation (zero where none). Implicit
+ * supervisor accesses (descriptor tables, exception frames) are not logged. */
+#define TN_R 1u
+#define TN_W 2u
+#define TN_RW 3u
+static void tn_access(orc_machine *m, u64 va, u32 len, u32 type) {
+  if (!m->tn || m->tn_mute) return;
+  if (type == TN_W && m->tn_last != ~0ULL && m->tnlist.v[m->tn_last] == va &&
+      m->tnlist.v[m->tn_last + 1] == ((1ULL << 56) | ((u64)TN_RW << 32) | len))
+    return; /* the write of a read-modify-write operand */
+  m->tn_last = m->tnlist.n;
+  vec_push(&m->tnlist, va);
+  vec_push(&m->tnlist, (1ULL << 56) | ((u64)type << 32) | len);
+  for (u32 i = 0; i < (len + 7) / 8; i++) vec_push(&m->tnlist, 0);
+}
+static void tn_regs(orc_machine *m) {
+  if (!m->tn) return;
+  for (u64 q = m->tn_ipos; q + 2 <= m->tnlist.n;) {
+    const u64 va = m->tnlist.v[q], len = m->tnlist.v[q + 1] & 0xffffffffULL;
+    u8 *out = (u8 *)&m->tnlist.v[q + 2];
+    for (u64 i = 0; i < len; i++) {
+      u64 pa;
+      u8 b = 0;
+      if (orc_translate(m, va + i, &pa) == 0) orc_read_phys(m, pa, &b, 1);
+      out[i] = b;
+    }
+    q += 2 + (len + 7) / 8;
+  }
+  vec_push(&m->tnlist, 2ULL << 56);
+  for (int i = 0; i < 16; i++) vec_push(&m->tnlist, m->r.gpr[i]);
+  vec_push(&m->tnlist, m->r.rip);
+  m->tn_ipos = m->tnlist.n;
+  m->tn_last = ~0ULL;
+}
+
 /* ---------------- guest virtual access with permission checks ---------------- */
 /* Translate [va, va+len) (len <= 16) for acc; fills up to two physical spans. */
 static int vprobe(orc_machine *m, u64 va, u32 len, int acc, u64 pa[2], u32 n[2]) {
@@ -434,6 +485,7 @@ static int vread(orc_machine *m, u64 va, u32 len, void *out) {
   orc_read_phys(m, pa[0], out, n[0]);
   if (n[1]) orc_read_phys(m, pa[1], (u8 *)out + n[0], n[1]);
   m->bytes += len;
+  tn_access(m, va, len, TN_R);
   return 0;
 }
 static int vwrite(orc_machine *m, u64 va, u32 len, const void *in) {
@@ -443,6 +495,7 @@ static int vwrite(orc_machine *m, u64 va, u32 len, const void *in) {
   orc_write_phys(m, pa[0], in, n[0]);
   if (n[1]) orc_write_phys(m, pa[1], (const u8 *)in + n[0], n[1]);
   m->bytes += len;
+  tn_access(m, va, len, TN_W);
   return 0;
 }
 /* Read for a read-modify-write: write permission required, pages dirtied at
@@ -454,6 +507,7 @@ static int vread_rmw(orc_machine *m, u64 va, u32 len, void *out) {
   memcpy(out, phys_rw(m, pa[0] >> 12) + (pa[0] & 0xfff), n[0]);
   if (n[1]) memcpy((u8 *)out + n[0], phys_rw(m, pa[1] >> 12) + (pa[1] & 0xfff), n[1]);
   m->bytes += len;
+  tn_access(m, va, len, TN_RW);
   return 0;
 }
 
@@ -465,14 +519,22 @@ static int vread_n(orc_machine *m, u64 va, u32 len, void *out) {
   u64 pa[2];
   u32 nn[2];
   if (vprobe(m, va, 16, ACC_R, pa, nn) || vprobe(m, va + 16, len - 16, ACC_R, pa, nn)) return -1;
-  return vread(m, va, 16, out) || vread(m, va + 16, len - 16, (u8 *)out + 16);
+  m->tn_mute++; /* Tenet: one access of len bytes */
+  const int rc = vread(m, va, 16, out) || vread(m, va + 16, len - 16, (u8 *)out + 16);
+  m->tn_mute--;
+  if (!rc) tn_access(m, va, len, TN_R);
+  return rc;
 }
 static int vwrite_n(orc_machine *m, u64 va, u32 len, const void *in) {
   if (len <= 16) return vwrite(m, va, len, in);
   u64 pa[2];
   u32 nn[2];
   if (vprobe(m, va, 16, ACC_W, pa, nn) || vprobe(m, va + 16, len - 16, ACC_W, pa, nn)) return -1;
-  return vwrite(m, va, 16, in) || vwrite(m, va + 16, len - 16, (const u8 *)in + 16);
+  m->tn_mute++;
+  const int rc = vwrite(m, va, 16, in) || vwrite(m, va + 16, len - 16, (const u8 *)in + 16);
+  m->tn_mute--;
+  if (!rc) tn_access(m, va, len, TN_W);
+  return rc;
 }
 
 /* ---------------- decode ---------------- */
@@ -3266,7 +3328,10 @@ static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
       ex->addr = 0;
     }
     fill_exit(m, ex, WTFGPU_EXIT_FAULT);
-    if (deliver(m, ex->vector, ex->error, ex->addr)) return ex->status = WTFGPU_RUNNING;
+    if (deliver(m, ex->vector, ex->error, ex->addr)) {
+      tn_regs(m);
+      return ex->status = WTFGPU_RUNNING;
+    }
     return ex->status;
   }
   /* coverage (bochscpu_backend.cc:501-504) then breakpoint lookup (:545-547) */
@@ -3288,6 +3353,9 @@ static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
   wtfgpu_regs_t saved = m->r;
   u64 saved_bytes = m->bytes;
   u64 next = 0;
+  m->tn_ipos = m->tnlist.n; /* Tenet: this instruction's accesses */
+  m->tn_last = ~0ULL;
+  m->tn_mute = 0;
   int x = exec_insn(m, &d, &mr, &next);
   /* RecordEdge (bochscpu_backend.cc:699-728, hooks :235-257, :308-312): jcc
    * taken or not, indirect near jmp / call; before the retire hook */
@@ -3311,6 +3379,7 @@ static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
     m->r.rip = next;
     m->bytes += d.len;
     m->icount++;
+    tn_regs(m);
     /* the limit check of the retire hook runs after the cr3 hook and wins */
     if (m->limit > 0 && m->icount > m->limit) {
       fill_exit(m, ex, WTFGPU_EXIT_TIMEOUT);
@@ -3339,7 +3408,10 @@ static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
     ex->vector = keep.vector;
     ex->error = keep.error;
     ex->addr = keep.addr;
-    if (deliver(m, ex->vector, ex->error, ex->addr)) return ex->status = WTFGPU_RUNNING;
+    if (deliver(m, ex->vector, ex->error, ex->addr)) {
+      tn_regs(m);
+      return ex->status = WTFGPU_RUNNING;
+    }
     break;
   }
   case X_UNIMPL:
@@ -3359,22 +3431,46 @@ int orc_inject_fault(orc_machine *m, uint32_t vector, uint32_t error, uint64_t a
   wtfgpu_exit_t ex;
   memset(&ex, 0, sizeof(ex));
   m->ex = &ex;
-  return deliver(m, vector, error, addr);
+  const int d = deliver(m, vector, error, addr);
+  if (d) {
+    m->tn_ipos = m->tnlist.n;
+    tn_regs(m);
+  }
+  return d;
 }
 
 int orc_run(orc_machine *m, int skip_bp, wtfgpu_exit_t *ex) {
   int first = 1;
+  if (m->tn && m->tnlist.n == 0) tn_regs(m); /* Tenet: the registers at the start */
   for (;;) {
     m->resumed = first && skip_bp; /* its before-execution hook ran at the hit */
     int st = one(m, !(first && skip_bp), ex);
     first = 0;
-    if (st != WTFGPU_RUNNING) return st;
+    if (st != WTFGPU_RUNNING) {
+      if (st != WTFGPU_EXIT_BREAKPOINT && m->tn && m->tnlist.n > m->tn_ipos) tn_regs(m); /* open accesses */
+      return st;
+    }
   }
 }
 
 int orc_step(orc_machine *m, wtfgpu_exit_t *ex) {
   m->resumed = 0;
   return one(m, 0, ex);
+}
+void orc_set_tenet(orc_machine *m, int on) {
+  m->tn = on;
+  m->tnlist.n = 0;
+  m->tn_ipos = 0;
+  m->tn_last = ~0ULL;
+}
+void orc_tenet_event(orc_machine *m) {
+  if (!m->tn) return;
+  m->tn_ipos = m->tnlist.n;
+  tn_regs(m);
+}
+uint64_t orc_tenet(orc_machine *m, uint64_t *out, uint64_t cap_words) {
+  for (u64 i = 0; i < m->tnlist.n && i < cap_words; i++) out[i] = m->tnlist.v[i];
+  return m->tnlist.n;
 }
 void orc_set_trace(orc_machine *m, int on) {
   m->trace = on;

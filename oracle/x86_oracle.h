@@ -45,6 +45,12 @@ void orc_set_edges(orc_machine *m, int on);
 /* Rip trace (--trace-type rip, bochscpu_backend.cc:506-520): the rips about to
  * execute, in order, since the last restore (a resumed breakpoint is logged
  * once). orc_trace copies up to cap of them and returns the count. */
+/* Tenet trace (U38): the stream wtfgpu_set_tenet documents, as u64 words;
+ * orc_tenet_event appends a REGS entry (a handler moved rip); orc_tenet copies
+ * up to cap words and returns the count. Restarts at orc_restore. */
+void orc_set_tenet(orc_machine *m, int on);
+void orc_tenet_event(orc_machine *m);
+uint64_t orc_tenet(orc_machine *m, uint64_t *out, uint64_t cap_words);
 void orc_set_trace(orc_machine *m, int on);
 uint64_t orc_trace(orc_machine *m, uint64_t *out, uint64_t cap);
 int orc_set_breakpoints(orc_machine *m, const uint64_t *gvas, uint32_t n);

@@ -8,7 +8,19 @@
 #include "../../wtf_amd/csrc/engine_fast.h"
 using namespace wtfgpu_dev;
 
+// Tenet stream of the next sim_run_full (sim_set_tenet; engine_exec.h TenetDev)
+static std::vector<uint8_t> g_tn_store;
+static uint64_t g_tn_pos, g_tn_cpos, g_tn_ipos, g_tn_last;
+static uint32_t g_tn_mute;
+
 extern "C" {
+void sim_set_tenet(uint64_t cap) { g_tn_store.assign(cap, 0); }
+uint64_t sim_tenet(uint8_t *out, uint64_t cap) {
+  const uint64_t n = g_tn_pos < g_tn_store.size() ? g_tn_pos : g_tn_store.size();
+  memcpy(out, g_tn_store.data(), n < cap ? n : cap);
+  return g_tn_pos;
+}
+
 struct SimResult {
   uint64_t gpr[16], rip, rflags, icount, nbytes;
   uint32_t status, vector, error, ovn;
@@ -85,6 +97,14 @@ int sim_run_full(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, c
   L.status = WTFGPU_RUNNING;
   L.simd = simd_bits(r0->cr0, r0->cr4, r0->xcr0);
   tlb_flush(L);
+  g_tn = TenetDev{};
+  if (!g_tn_store.empty()) {
+    g_tn_pos = g_tn_cpos = g_tn_ipos = 0;
+    g_tn_last = ~0ull;
+    g_tn_mute = 0;
+    g_tn = TenetDev{g_tn_store.data(), g_tn_store.size(), &g_tn_pos, &g_tn_cpos, &g_tn_ipos, &g_tn_last, &g_tn_mute};
+    tn_regs(P, L);  // the registers at the start
+  }
   for (uint64_t steps = 0; steps < 100000000 && L.status == WTFGPU_RUNNING; steps++) {
     const uint64_t grip = L.rip;
     uint64_t td;
@@ -144,9 +164,11 @@ int sim_run_full(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, c
       }
     }
     int x;
+    tn_insn_begin(L.lane);
     for (int attempt = 0;; attempt++) {
       L.miss = 0;
       L.pend = 0;
+      tn_rollback(L.lane);
       x = exec(P, L, d, grip + d.len, next);
       if (!L.miss || L.status != WTFGPU_RUNNING) break;
       if (attempt >= 16 || !service_miss(P, L, L.miss_va, (int)L.miss_acc)) break;
@@ -160,6 +182,7 @@ int sim_run_full(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, c
       L.icount++;
       L.nbytes += d.len + L.pend;
       if (P.limit && L.icount > P.limit) L.status = WTFGPU_EXIT_TIMEOUT;
+      if (g_tn.buf) tn_regs(P, L);
     } else if (L.status != WTFGPU_RUNNING) {
     } else if (x == X_UNIMPL) {
       L.status = WTFGPU_EXIT_UNIMPLEMENTED;
@@ -169,6 +192,8 @@ int sim_run_full(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, c
       L.status = WTFGPU_EXIT_HLT;
     }
   }
+  if (g_tn.buf && g_tn_pos > g_tn_ipos) tn_regs(P, L);  // open accesses of the stopping instruction
+  g_tn = TenetDev{};
   for (int i = 0; i < 16; i++) out->gpr[i] = R(L, i);
   out->rip = L.rip;
   out->rflags = L.rflags;

@@ -39,6 +39,8 @@ def lib() -> C.CDLL:
         "orc_read_virt": ([P, U64, P, U64], C.c_int),
         "orc_write_virt": ([P, U64, P, U64], C.c_int),
         "orc_inject_fault": ([P, U32, U32, U64], C.c_int),
+        "orc_set_tenet": ([P, C.c_int], None), "orc_tenet_event": ([P], None),
+        "orc_tenet": ([P, C.POINTER(U64), U64], U64),
     }
     for n, (a, r) in sig.items():
         f = getattr(L, n)
@@ -96,6 +98,16 @@ class Oracle:
         e = Exit()
         self.L.orc_step(self.m, C.byref(e))
         return e
+
+    def set_tenet(self, on: bool):
+        self.L.orc_set_tenet(self.m, 1 if on else 0)
+
+    def tenet(self) -> bytes:
+        """The Tenet stream (U38) as bytes."""
+        n = self.L.orc_tenet(self.m, None, 0)
+        arr = (C.c_uint64 * max(1, n))()
+        self.L.orc_tenet(self.m, arr, n)
+        return bytes(arr)[:8 * n]
 
     def icount(self):
         return self.L.orc_icount(self.m)

@@ -3,7 +3,9 @@ BochscpuBackend_t::SetTraceFile / BeforeExecutionHook, bochscpu_backend.cc:
 506-520, subcommands.cc:52-74): one `<input>.trace` per input, one "%#x" rip
 per line, every rip about to execute (rip) or only those new to the aggregate
 (cov). The GPU records them on the device (wtfgpu_set_trace); the twin from
-the oracle; their files must be identical.
+the oracle; their files must be identical. Tenet traces (`--trace-type
+tenet`, bochscpu_backend.cc:1215-1323; the format is checked in
+tests/test_tenet.py) likewise, byte for byte.
 """
 import os
 
@@ -78,3 +80,29 @@ def test_gpu_traces_equal_twin(which, tlv, hevd, tmp_path):
         rb, b = traces(H.WTFGPU, target, tmp_path / f"gpu_{kind}", kind, name=name)
         assert a == b, kind
         assert sum(len(t) for t in a.values()) > 100
+
+
+def tenet_files(exe, target, out, name):
+    H.run(exe, target, os.path.join(target, "inputs"), str(out) + ".jsonl", lanes=16, name=name,
+          extra=["--trace-path", str(out), "--trace-type", "tenet"])
+    files = {}
+    for f in os.listdir(out):
+        with open(os.path.join(out, f), "rb") as fh:
+            files[f] = fh.read()
+    return files
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["tlv", "hevd"])
+def test_gpu_tenet_traces_equal_twin(which, tlv, hevd, tmp_path):
+    target, name = (tlv, "tlv_server") if which == "tlv" else (hevd, "hevd")
+    a = tenet_files(H.TWIN, target, tmp_path / "twin", name)
+    b = tenet_files(H.WTFGPU, target, tmp_path / "gpu", name)
+    assert sorted(a) == sorted(b)
+    for f in sorted(a):
+        if a[f] != b[f]:
+            la, lb = a[f].split(b"\n"), b[f].split(b"\n")
+            k = next((i for i, (x, y) in enumerate(zip(la, lb)) if x != y), min(len(la), len(lb)))
+            pytest.fail(f"{f}: line {k}: twin {la[k:k + 2]} gpu {lb[k:k + 2]}")
+    assert sum(x.count(b"\n") for x in a.values()) > 200
+    assert sum(x.count(b",mw=") for x in a.values()) > 20

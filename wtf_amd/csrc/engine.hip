@@ -537,7 +537,7 @@ __device__ __noinline__ void uc_fill(const Dev &P, UCEntry *e, UCUop *us, u64 ke
   if (dr == 0) {
     digest(d, f);
     if (P.edges && edge_op(d.op, d.bsrc)) f = generic_fop(d);  // branches whose edge is recorded run in the slow step
-    if (P.trace) f = generic_fop(d);                           // traced lanes log every rip in the slow step
+    if (P.trace || g_tn.buf) f = generic_fop(d);               // traced lanes log every rip in the slow step
     if (!d.supported) flags |= UC_UNSUP;
     if (bp_lookup(P, rip)) flags |= UC_BP;
   } else {
@@ -608,9 +608,11 @@ __device__ __noinline__ int exec_generic(const Dev &P, Lane &L, const UOp *ul, u
 // page, the attempt reruns.
 __device__ __noinline__ int exec_retry(const Dev &P, Lane &L, const UOp *ul, u64 &next) {
   int x;
+  tn_insn_begin(L.lane);
   for (int attempt = 0;; attempt++) {
     L.miss = 0;
     L.pend = 0;
+    tn_rollback(L.lane);
     x = exec_generic(P, L, ul, next);
     if (!L.miss || L.status != WTFGPU_RUNNING) break;
     if (!miss_service(P, L, attempt)) break;
@@ -864,6 +866,7 @@ __device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr
       const bool applied = bp_apply(P, L, grip);
       if (!applied) L.status = WTFGPU_EXIT_BREAKPOINT;
       skip = applied && L.rip == grip;
+      if (applied && !skip && g_tn.buf) tn_regs(P, L);  // Tenet: the action moved rip
       ing = false;
     } else {
       skip = false;
@@ -879,14 +882,17 @@ __device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr
   if (ing) {
     u64 next = 0;
     int x;
+    tn_insn_begin(L.lane);
     for (int attempt = 0;; attempt++) {
       L.miss = 0;
       L.pend = 0;
+      tn_rollback(L.lane);
       x = exec(P, L, d, grip + d.len, next);
       if (!L.miss || L.status != WTFGPU_RUNNING) break;
       if (!miss_service(P, L, attempt)) break;
     }
     retire(P, L, x, d.len, next, d.opbytes);
+    if (g_tn.buf && (x == X_OK || x == X_CR3)) tn_regs(P, L);
     // RecordEdge (bochscpu_backend.cc:699-728): the branch ran, whatever the retire hook decided
     if (P.edges && P.cov_rip && edge_op(d.op, d.bsrc) && x == X_OK)
       L.ccnt = cover_edge(P, edge_key(grip, next), true, L.lane, L.cgen, L.ccnt);
@@ -1025,6 +1031,9 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
   }
   const u64 icount0 = L.icount;
   bool skip = valid && (P.lflags[lane] & 1);
+  // Tenet: the registers at the start (first entry), or after a host handler
+  // moved rip (resume without skip, lflags bit 1)
+  if (valid && g_tn.buf && (g_tn.pos[lane] == 0 || (P.lflags[lane] & 2))) WITH_LANE_COPY(tn_regs(P, T));
   const u64 pool_lo = (u64)(uintptr_t)P.pool, pool_hi = pool_lo + (P.npool + 1) * WTFGPU_PAGE_SIZE;
   u64 steps = 0;
 #ifdef WTFGPU_STAMPS
@@ -1100,7 +1109,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       if (valid && L.status == WTFGPU_EXIT_FAULT && !L.nodeliver) {
         bool dv;
         WITH_LANE_COPY(dv = deliver_fault(P, T));
-        (void)dv;
+        if (dv && g_tn.buf) WITH_LANE_COPY(tn_regs(P, T));  // Tenet: the delivered exception
       }
       continue;
     }
@@ -1170,6 +1179,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
         if (P.act_keys) WITH_LANE_COPY(applied = bp_apply(P, T, grip));
         if (!applied) L.status = WTFGPU_EXIT_BREAKPOINT;
         skip = applied && L.rip == grip;
+        if (applied && !skip && g_tn.buf) WITH_LANE_COPY(tn_regs(P, T));  // Tenet: the action moved rip
         ing = false;
       } else {
         skip = false;
@@ -1192,6 +1202,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       u32 opbytes = 0;
       if (x == X_UNIMPL) opbytes = u->opbytes;
       retire(P, L, x, len, next, opbytes);
+      if (g_tn.buf && (x == X_OK || x == X_CR3)) WITH_LANE_COPY(tn_regs(P, T));  // Tenet: the retired instruction
       // RecordEdge (bochscpu_backend.cc:699-728): the branch ran, whatever the retire hook decided
       if (P.edges && P.cov_rip && x == X_OK && edge_op(rfl32(u->op), rfl32(u->bsrc)))
         L.ccnt = cover_edge(P, edge_key(grip, next), true, L.lane, L.cgen, L.ccnt);
@@ -1205,6 +1216,11 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     UCEntry *out = (UCEntry *)P.warm + (u64)hw * UC_N;
     for (u32 i = lid; i < UC_N; i += 64) out[i] = uc[i];
   }
+  // Tenet: a lane that stopped with accesses still open (an undelivered fault,
+  // an unimplemented instruction) closes them with a REGS entry
+  if (valid && g_tn.buf && L.status != WTFGPU_RUNNING && L.status != WTFGPU_EXIT_BREAKPOINT &&
+      g_tn.pos[lane] > g_tn.ipos[lane])
+    WITH_LANE_COPY(tn_regs(P, T));
   if (valid) {
     store_lane(P, L);
     store_tlb(P, L);
@@ -1260,6 +1276,11 @@ __device__ __forceinline__ void restore_lane(const Dev &P, const InitState &s, c
   tlb_stale(P, lane);
   if (P.rd_seed) P.rd_seed[lane] = P.rd_seed0;  // bochscpu_backend.cc:1030
   if (P.trace_cnt) P.trace_cnt[lane] = 0;
+  if (g_tn.buf) {
+    g_tn.pos[lane] = g_tn.ipos[lane] = g_tn.cpos[lane] = 0;
+    g_tn.last[lane] = ~0ull;
+    g_tn.mute[lane] = 0;
+  }
   if (P.cov_rip) {
     P.lane_gen[lane] += 1;
     P.cov_cnt[lane] = 0;
@@ -1299,6 +1320,11 @@ __global__ void k_restore(Dev P, const InitState *S, const wtfgpu_regs_t *full0,
   tlb_stale(P, lane);
   if (P.rd_seed) P.rd_seed[lane] = P.rd_seed0;  // bochscpu_backend.cc:1030
   if (P.trace_cnt) P.trace_cnt[lane] = 0;
+  if (g_tn.buf) {
+    g_tn.pos[lane] = g_tn.ipos[lane] = g_tn.cpos[lane] = 0;
+    g_tn.last[lane] = ~0ull;
+    g_tn.mute[lane] = 0;
+  }
   if (P.cov_rip) {       // the lane's coverage set empties
     P.lane_gen[lane] += 1;
     P.cov_cnt[lane] = 0;
@@ -1438,6 +1464,10 @@ __global__ void k_inject_fault(Dev P, const u32 *lanes, const u64 *addrs, u32 n,
   L.exaddr = addrs[t];
   const bool d = deliver_fault(P, L);
   ok[t] = d ? 1 : 0;
+  if (d && g_tn.buf) {  // Tenet: the injected exception
+    g_tn.ipos[lane] = g_tn.pos[lane];
+    tn_regs(P, L);
+  }
   if (d) {
     store_lane(P, L);
     tlb_stale(P, lane);
@@ -1451,7 +1481,7 @@ __global__ void k_set_status(Dev P, const u32 *lanes, u32 n, u32 status, const u
   if (t >= n) return;
   const u32 lane = lanes[t];
   P.status[lane] = status;
-  if (skip) P.lflags[lane] = skip[t] ? 1u : 0u;
+  if (skip) P.lflags[lane] = skip[t] ? 1u : (g_tn.buf ? 2u : 0u);  // 2: Tenet entry at the next launch
 }
 
 // Single-lane memory services for the host proxy.
@@ -1758,6 +1788,10 @@ struct wtfgpu_ctx {
   u64 *d_rdseed = nullptr;    // per-lane Rdrand seeds (Dev::rd_seed)
   u64 *d_stopargs = nullptr;  // per-lane STOP_ARGS arguments (Dev::stop_args)
   u64 *d_extra = nullptr;     // coverage values outside code pages (Dev::extra_keys)
+  u8 *d_tn_buf = nullptr;     // Tenet traces (g_tn)
+  u64 *d_tn_pos = nullptr, *d_tn_cpos = nullptr, *d_tn_ipos = nullptr, *d_tn_last = nullptr;
+  u32 *d_tn_mute = nullptr;
+  u64 tn_cap = 0;
   u64 *d_trace = nullptr;     // rip traces (Dev::trace)
   u32 *d_tracecnt = nullptr;
   LaneTlb *d_tlbs = nullptr;  // translation state kept between k_run launches
@@ -2080,6 +2114,18 @@ static void free_lanes(wtfgpu_ctx *c) {
   c->P.trace = nullptr;
   c->P.trace_cnt = nullptr;
   c->P.trace_cap = 0;
+  if (c->d_tn_buf) {  // Tenet buffers are sized by the lane count
+    dfree(c->d_tn_buf);
+    dfree(c->d_tn_pos);
+    dfree(c->d_tn_cpos);
+    dfree(c->d_tn_ipos);
+    dfree(c->d_tn_last);
+    dfree(c->d_tn_mute);
+    c->d_tn_buf = nullptr, c->d_tn_pos = c->d_tn_cpos = c->d_tn_ipos = c->d_tn_last = nullptr, c->d_tn_mute = nullptr;
+    c->tn_cap = 0;
+    const TenetDev T{};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tn), &T, sizeof(T));
+  }
   dfree(c->d_ovdata);
   dfree(c->d_full);
   dfree(c->d_perm);
@@ -3313,6 +3359,50 @@ int wtfgpu_read_trace(wtfgpu_ctx *c, uint32_t lane, uint64_t *rips, uint64_t cap
   *n = cnt;
   const u64 k = std::min<u64>(std::min<u64>(cnt, c->P.trace_cap), cap);
   if (k) HIPCHK(hipMemcpyAsync(rips, c->d_trace + (u64)lane * c->P.trace_cap, k * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+// Tenet traces (engine_exec.h TenetDev): bytes_per_lane of entries per lane, 0 = off.
+int wtfgpu_set_tenet(wtfgpu_ctx *c, uint64_t bytes_per_lane) {
+  if (!c || !c->d_gpr || (bytes_per_lane & 7)) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  dfree(c->d_tn_buf);
+  dfree(c->d_tn_pos);
+  dfree(c->d_tn_cpos);
+  dfree(c->d_tn_ipos);
+  dfree(c->d_tn_last);
+  dfree(c->d_tn_mute);
+  c->d_tn_buf = nullptr, c->d_tn_pos = c->d_tn_cpos = c->d_tn_ipos = c->d_tn_last = nullptr, c->d_tn_mute = nullptr;
+  TenetDev T{};
+  c->tn_cap = 0;
+  if (bytes_per_lane) {
+    const u64 N = c->P.nlanes;
+    if (dalloc(&c->d_tn_buf, N * bytes_per_lane) || dalloc(&c->d_tn_pos, N) || dalloc(&c->d_tn_cpos, N) ||
+        dalloc(&c->d_tn_ipos, N) || dalloc(&c->d_tn_last, N) || dalloc(&c->d_tn_mute, N))
+      return WTFGPU_ERR_OOM;
+    HIPCHK(hipMemset(c->d_tn_pos, 0, N * 8));
+    HIPCHK(hipMemset(c->d_tn_cpos, 0, N * 8));
+    HIPCHK(hipMemset(c->d_tn_ipos, 0, N * 8));
+    HIPCHK(hipMemset(c->d_tn_last, 0xff, N * 8));
+    HIPCHK(hipMemset(c->d_tn_mute, 0, N * 4));
+    T = TenetDev{c->d_tn_buf, bytes_per_lane, c->d_tn_pos, c->d_tn_cpos, c->d_tn_ipos, c->d_tn_last, c->d_tn_mute};
+    c->tn_cap = bytes_per_lane;
+  }
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_tn), &T, sizeof(T)));
+  return guc_clear(c);  // cached entries were digested for the other setting
+}
+
+int wtfgpu_read_tenet(wtfgpu_ctx *c, uint32_t lane, uint8_t *buf, uint64_t cap, uint64_t *n) {
+  if (!c || !n || (cap && !buf) || lane >= c->P.nlanes || !c->d_tn_buf) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  u64 pos = 0;
+  HIPCHK(hipMemcpyAsync(&pos, c->d_tn_pos + lane, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  *n = pos;
+  const u64 k = std::min<u64>(std::min<u64>(pos, c->tn_cap), cap);
+  if (k) HIPCHK(hipMemcpyAsync(buf, c->d_tn_buf + (u64)lane * c->tn_cap, k, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return WTFGPU_OK;
 }

@@ -248,6 +248,79 @@ __device__ __forceinline__ u8 *xlate(Lane &L, u64 va, int acc, u64 *tdo = nullpt
   return (u8 *)(uintptr_t)(td & ~0xfffull) + (va & 0xfff);
 }
 
+// ------------------------------------------------------------------ Tenet trace
+// (wtfgpu_set_tenet; bochscpu_backend.cc:1215-1323; U38 in DESIGN.md). Per
+// lane a byte stream of 8-byte-aligned entries:
+//   ACC  {u64 va; u64 meta = 1 << 56 | type << 32 | len; data, len bytes
+//         rounded up to 8}: one data access of an instruction (the operand as
+//         a whole, up to 32 bytes; an RMW operand once, as read-write); the
+//         data is the memory after the instruction, filled at its REGS entry;
+//   REGS {u64 meta = 2 << 56; u64 gpr[16]; u64 rip}: the registers at the
+//         start, after each retired instruction, after each delivered
+//         exception, after a breakpoint action that moved rip, and when a
+//         lane stops with accesses still open.
+// pos: bytes written (past cap: truncated); cpos: the committed position a
+// restarted attempt rolls back to (string ops commit per iteration); ipos: the
+// current instruction's first ACC entry; mute: nested accesses of an operand
+// already logged as a whole.
+struct TenetDev {
+  u8 *buf;
+  u64 cap;
+  u64 *pos, *cpos, *ipos, *last;  // last: the instruction's latest ACC entry (~0: none)
+  u32 *mute;
+};
+__device__ TenetDev g_tn;
+enum : u32 { TN_R = 1, TN_W = 2, TN_RW = 3 };
+constexpr u64 TN_ACC = 1ull << 56, TN_REGS = 2ull << 56;
+
+__device__ __noinline__ void tn_access(u32 lane, u64 va, u32 len, u32 type) {
+  if (g_tn.mute[lane]) return;
+  const u64 p = g_tn.pos[lane], last = g_tn.last[lane];
+  u8 *const base = g_tn.buf + (u64)lane * g_tn.cap;
+  // the write of a read-modify-write operand: its read entry is the latest one
+  if (type == TN_W && last != ~0ull && last + 16 <= g_tn.cap && *(const u64 *)(base + last) == va &&
+      *(const u64 *)(base + last + 8) == (TN_ACC | (u64)TN_RW << 32 | len))
+    return;
+  const u64 n = 16 + ((u64)len + 7) / 8 * 8;
+  if (p + n <= g_tn.cap) {
+    *(u64 *)(base + p) = va;
+    *(u64 *)(base + p + 8) = TN_ACC | (u64)type << 32 | len;
+  } else if (p + 16 <= g_tn.cap) {
+    *(u64 *)(base + p) = 0;  // truncated here: readers stop at this zero header
+    *(u64 *)(base + p + 8) = 0;
+  }
+  g_tn.last[lane] = p;
+  g_tn.pos[lane] = p + n;
+}
+// An operand wider than one vread / vwrite (16 / 32 bytes): its pieces are
+// muted and, once every piece succeeded, it is logged once as a whole.
+__device__ __forceinline__ void tn_mute(u32 lane) {
+  if (g_tn.buf) g_tn.mute[lane]++;
+}
+__device__ __forceinline__ bool tn_unmute(u32 lane, u64 va, u32 len, u32 type, bool ok) {
+  if (g_tn.buf) {
+    g_tn.mute[lane]--;
+    if (ok) tn_access(lane, va, len, type);
+  }
+  return ok;
+}
+// instruction start / attempt restart / iteration commit
+__device__ __forceinline__ void tn_insn_begin(u32 lane) {
+  if (!g_tn.buf) return;
+  g_tn.ipos[lane] = g_tn.cpos[lane] = g_tn.pos[lane];
+  g_tn.last[lane] = ~0ull;
+  g_tn.mute[lane] = 0;
+}
+__device__ __forceinline__ void tn_rollback(u32 lane) {
+  if (!g_tn.buf) return;
+  g_tn.pos[lane] = g_tn.cpos[lane];
+  g_tn.last[lane] = ~0ull;
+  g_tn.mute[lane] = 0;
+}
+__device__ __forceinline__ void tn_commit(u32 lane) {
+  if (g_tn.buf) g_tn.cpos[lane] = g_tn.pos[lane];
+}
+
 // Guest virtual reads / writes of 1..8 bytes (page crossing handled).
 __device__ __forceinline__ bool vread(Lane &L, u64 va, u32 sz, u64 &out, int acc = ACC_R) {
   const u32 off = (u32)(va & 0xfff);
@@ -269,6 +342,7 @@ __device__ __forceinline__ bool vread(Lane &L, u64 va, u32 sz, u64 &out, int acc
     out = v;
   }
   L.pend += sz;
+  if (g_tn.buf) tn_access(L.lane, va, sz, acc == ACC_W ? TN_RW : TN_R);
   return true;
 }
 
@@ -295,7 +369,61 @@ __device__ __forceinline__ bool vwrite(Lane &L, u64 va, u32 sz, u64 v) {
   // when the instruction retires, so a restart cannot livelock)
   if ((td0 | td1) & T_PT) L.flush = 1;
   L.pend += sz;
+  if (g_tn.buf) tn_access(L.lane, va, sz, TN_W);
   return true;
+}
+
+// Tenet (engine_exec.h TenetDev): fills the data of the ACC entries the
+// current instruction logged with the memory as it is now (translation by
+// present bits, as the oracle's orc_read_virt; a page that no longer
+// translates reads as zeros), then appends a REGS entry with the lane's
+// registers. The lane's state is left as it was.
+__device__ __noinline__ void tn_regs(const Dev &P, Lane &L) {
+  const u32 lane = L.lane;
+  const u64 cap = g_tn.cap, end = g_tn.pos[lane];
+  u8 *const base = g_tn.buf + (u64)lane * cap;
+  const u32 st = L.status, ev = L.exvec, ee = L.exerr, cpl = L.cpl, pend = L.pend, miss = L.miss;
+  const u64 ea = L.exaddr, cr0 = L.cr0;
+  L.cpl = 0;  // supervisor reads, CR0.WP clear: only the present bits decide
+  L.cr0 &= ~(1ull << 16);
+  for (u64 q = g_tn.ipos[lane]; q + 16 <= end && q + 16 <= cap;) {
+    const u64 va = *(const u64 *)(base + q), meta = *(const u64 *)(base + q + 8);
+    if (meta >> 56 != 1) break;  // the truncation mark (tn_access)
+    const u32 len = (u32)(meta & 0xffffffffull);
+    const u64 n = 16 + ((u64)len + 7) / 8 * 8;
+    if (q + n > cap) break;
+    {
+      u8 *out = base + q + 16;
+      for (u32 i = 0; i < len; i++) {
+        u8 b = 0;
+        for (int attempt = 0;; attempt++) {
+          L.miss = 0;
+          L.status = WTFGPU_RUNNING;
+          const u8 *p = xlate(L, va + i, ACC_R);
+          if (p) {
+            b = *p;
+            break;
+          }
+          if (!L.miss || attempt >= 16 || !service_miss(P, L, L.miss_va, (int)L.miss_acc)) break;
+        }
+        out[i] = b;
+      }
+    }
+    q += n;
+  }
+  L.status = st, L.exvec = ev, L.exerr = ee, L.exaddr = ea, L.cpl = cpl, L.pend = pend, L.miss = miss, L.cr0 = cr0;
+  const u64 n = 8 + 17 * 8;
+  if (end + n <= cap) {
+    u64 *r = (u64 *)(base + end);
+    r[0] = TN_REGS;
+    for (u32 i = 0; i < 16; i++) r[1 + i] = R(L, i);
+    r[17] = L.rip;
+  } else if (end + 16 <= cap) {
+    *(u64 *)(base + end) = 0;  // truncation mark
+    *(u64 *)(base + end + 8) = 0;
+  }
+  g_tn.pos[lane] = g_tn.ipos[lane] = g_tn.cpos[lane] = end + n;
+  g_tn.last[lane] = ~0ull;
 }
 
 }  // namespace wtfgpu_dev

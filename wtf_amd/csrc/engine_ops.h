@@ -882,6 +882,7 @@ __device__ __forceinline__ int string_op(const Dev &P, Lane &L, const UOp &u) {
     if (op != 0xac && op != 0x6e) RS(L, 7, (rdi + step) & amask);
     L.nbytes += L.pend;  // the iteration is architecturally complete
     L.pend = 0;
+    tn_commit(L.lane);   // and so are its Tenet accesses
     if (!u.rep) break;
     RS(L, 1, (R(L, 1) - 1) & amask);
     if (dstr) {

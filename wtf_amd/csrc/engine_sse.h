@@ -215,13 +215,17 @@ __device__ __forceinline__ bool span_ok(Lane &L, u64 ea, u32 n, int acc) {
 __device__ __forceinline__ bool xload(Lane &L, u64 ea, u32 n, X128 &v) {
   v.lo = v.hi = 0;
   if (n <= 8) return vread(L, ea, n, v.lo);
-  return span_ok(L, ea, n, ACC_R) && vread(L, ea, 8, v.lo) && vread(L, ea + 8, 8, v.hi);
+  tn_mute(L.lane);  // Tenet: one 16-byte access
+  const bool ok = span_ok(L, ea, n, ACC_R) && vread(L, ea, 8, v.lo) && vread(L, ea + 8, 8, v.hi);
+  return tn_unmute(L.lane, ea, n, TN_R, ok);
 }
 // n bytes of v to ea
 __device__ __forceinline__ bool xstore(Lane &L, u64 ea, u32 n, X128 v) {
   if (n <= 8) return vwrite(L, ea, n, v.lo);
   if (!span_ok(L, ea, n, ACC_WPROBE)) return false;
-  return vwrite(L, ea, 8, v.lo) && vwrite(L, ea + 8, 8, v.hi);
+  tn_mute(L.lane);
+  const bool ok = vwrite(L, ea, 8, v.lo) && vwrite(L, ea + 8, 8, v.hi);
+  return tn_unmute(L.lane, ea, n, TN_W, ok);
 }
 
 
@@ -244,13 +248,17 @@ __device__ __forceinline__ void ymm_put(const Dev &P, const Lane &L, u32 r, Y256
 __device__ __forceinline__ bool yload(Lane &L, u64 ea, u32 n, Y256 &v) {
   v.h = X128{0, 0};
   if (n <= 16) return xload(L, ea, n, v.l);
-  return span_ok(L, ea, n, ACC_R) && xload(L, ea, 16, v.l) && xload(L, ea + 16, 16, v.h);
+  tn_mute(L.lane);  // Tenet: one 32-byte access
+  const bool ok = span_ok(L, ea, n, ACC_R) && xload(L, ea, 16, v.l) && xload(L, ea + 16, 16, v.h);
+  return tn_unmute(L.lane, ea, n, TN_R, ok);
 }
 __device__ __forceinline__ bool ystore(Lane &L, u64 ea, u32 n, Y256 v) {
   if (n <= 16) return xstore(L, ea, n, v.l);
   if (!span_ok(L, ea, n, ACC_WPROBE)) return false;
-  return vwrite(L, ea, 8, v.l.lo) && vwrite(L, ea + 8, 8, v.l.hi) && vwrite(L, ea + 16, 8, v.h.lo) &&
-         vwrite(L, ea + 24, 8, v.h.hi);
+  tn_mute(L.lane);
+  const bool ok = vwrite(L, ea, 8, v.l.lo) && vwrite(L, ea + 8, 8, v.l.hi) && vwrite(L, ea + 16, 8, v.h.lo) &&
+                  vwrite(L, ea + 24, 8, v.h.hi);
+  return tn_unmute(L.lane, ea, n, TN_W, ok);
 }
 
 // The 128-bit lane of the two-source integer / logic / shuffle ops shared by

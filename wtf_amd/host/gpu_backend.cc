@@ -1106,6 +1106,15 @@ bool GpuBackend_t::LaneTrace(uint32_t Lane, std::vector<uint64_t> &Rips, bool &T
   return wtfgpu_read_trace(ctx_, Lane, Rips.data(), Rips.size(), &N) == WTFGPU_OK;
 }
 
+bool GpuBackend_t::LaneTenet(uint32_t Lane, std::vector<uint8_t> &Bytes, bool &Truncated) {
+  uint64_t N = 0;
+  Bytes.clear();
+  if (wtfgpu_read_tenet(ctx_, Lane, nullptr, 0, &N) != WTFGPU_OK) return false;
+  Truncated = N > tenet_cap_;
+  Bytes.resize(std::min<uint64_t>(N, tenet_cap_));
+  return wtfgpu_read_tenet(ctx_, Lane, Bytes.data(), Bytes.size(), &N) == WTFGPU_OK;
+}
+
 bool GpuBackend_t::RunBatch(const Target_t &Target, const std::vector<std::pair<const uint8_t *, size_t>> &Testcases,
                             std::vector<LaneResult> &Out, ModuleSlots *Slots) {
   const auto t0 = Clock::now();

@@ -119,6 +119,11 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
     return ctx_ && wtfgpu_set_trace(ctx_, PerLane) == WTFGPU_OK;
   }
   bool LaneTrace(uint32_t Lane, std::vector<uint64_t> &Rips, bool &Truncated) override;
+  bool EnableTenet(uint64_t BytesPerLane) override {
+    tenet_cap_ = BytesPerLane;
+    return ctx_ && wtfgpu_set_tenet(ctx_, BytesPerLane) == WTFGPU_OK;
+  }
+  bool LaneTenet(uint32_t Lane, std::vector<uint8_t> &Bytes, bool &Truncated) override;
   const BatchStats &Stats() const { return stats_; }
   uint32_t Lanes() const override { return nlanes_; }
   wtfgpu_ctx *Engine() const { return ctx_; }
@@ -242,6 +247,7 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   std::unordered_map<uint64_t, BreakpointHandler_t> breakpoints_;
   std::vector<wtfgpu_bp_action_t> bp_actions_;  // device-side equivalents of some handlers
   uint32_t trace_cap_ = 0;                       // rip-trace capacity per lane (EnableTrace)
+  uint64_t tenet_cap_ = 0;                       // Tenet stream bytes per lane (EnableTenet)
   std::unordered_map<uint64_t, BreakpointAction_t::ArgsResult_t> args_results_;  // StopWithArgs, by gva
   bool feed_action_ = false;                     // a Feed action is on the device
   int upload_feed(uint32_t n);                   // lanes [0, n)

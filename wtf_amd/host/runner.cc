@@ -63,6 +63,67 @@ std::vector<fs::path> list_inputs(const fs::path &P) {
 }
 }  // namespace
 
+void FormatTenet(const uint8_t *S, size_t Bytes, FILE *F) {
+  // reference print order (rax, rbx, rcx, rdx, rbp, rsp, rsi, rdi, r8..r15)
+  // over the stream's x86 order (rax, rcx, rdx, rbx, rsp, rbp, rsi, rdi, ...)
+  static const int Order[16] = {0, 3, 1, 2, 5, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+  static const char *Name[17] = {"rax", "rcx", "rdx", "rbx", "rsp", "rbp", "rsi", "rdi", "r8",
+                                 "r9",  "r10", "r11", "r12", "r13", "r14", "r15", "rip"};
+  static const char *Type[4] = {"", "mr", "mw", "mrw"};
+  static const char Hex[] = "0123456789ABCDEF";
+  uint64_t Prev[17] = {};
+  bool First = true;
+  std::string Line, Mem;
+  auto word = [&](size_t q) {
+    uint64_t v;
+    memcpy(&v, S + q, 8);
+    return v;
+  };
+  size_t q = 0;
+  while (q + 16 <= Bytes) {
+    const uint64_t w0 = word(q), w1 = word(q + 8);
+    if (w0 == 2ull << 56) {  // REGS
+      if (q + 8 + 17 * 8 > Bytes) break;
+      uint64_t Cur[17];
+      memcpy(Cur, S + q + 8, sizeof(Cur));
+      Line.clear();
+      char Buf[48];
+      for (int k = 0; k < 17; k++) {
+        const int r = k < 16 ? Order[k] : 16;
+        if (!First && Cur[r] == Prev[r]) continue;
+        snprintf(Buf, sizeof(Buf), "%s=0x%llx%s", Name[r], (unsigned long long)Cur[r], k < 16 ? "," : "");
+        Line += Buf;
+      }
+      Line += Mem;
+      if (!Line.empty()) {
+        Line += '\n';
+        fwrite(Line.data(), 1, Line.size(), F);
+      }
+      Mem.clear();
+      memcpy(Prev, Cur, sizeof(Prev));
+      First = false;
+      q += 8 + 17 * 8;
+      continue;
+    }
+    const uint32_t Ty = (uint32_t)(w1 >> 32) & 0xff, Len = (uint32_t)w1;
+    if (w1 >> 56 != 1 || Ty == 0 || Ty > 3) break;  // a truncation mark
+    const size_t n = 16 + ((size_t)Len + 7) / 8 * 8;
+    if (q + n > Bytes) break;
+    char Buf[40];
+    snprintf(Buf, sizeof(Buf), ",%s=0x%llx:", Type[Ty], (unsigned long long)w0);
+    Mem += Buf;
+    for (uint32_t i = 0; i < Len; i++) {
+      Mem += Hex[S[q + 16 + i] >> 4];
+      Mem += Hex[S[q + 16 + i] & 15];
+    }
+    q += n;
+  }
+  if (!Mem.empty()) {  // accesses of a truncated stream's last instruction
+    Mem += '\n';
+    fwrite(Mem.data(), 1, Mem.size(), F);
+  }
+}
+
 // The ring-3 CpuState_t -> wtfgpu_regs_t mapping (LoadState, bochscpu_backend.cc:1026-1122).
 wtfgpu_regs_t RegsFromCpuState(const CpuState_t &S) {
   wtfgpu_regs_t r{};
@@ -145,6 +206,7 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
     else if (a == "--trace-path") O.trace_path = next("--trace-path");
     else if (a == "--trace-type") O.trace_type = next("--trace-type");
     else if (a == "--trace-cap") O.trace_cap = (uint32_t)strtoul(next("--trace-cap"), nullptr, 0);
+    else if (a == "--tenet-cap") O.tenet_cap = strtoull(next("--tenet-cap"), nullptr, 0) & ~7ull;
     else if (a == "--quiet") O.quiet = true;
     else if (a == "--serial-mutation") O.serial_mutation = true;
     else if (a == "--slice-steps") O.slice = strtoull(next("--slice-steps"), nullptr, 0);
@@ -179,7 +241,7 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
                     "       [--lanes n] [--overlay-pages k] [--runs n] [--seconds s] [--seed s] [--full-coverage]\n"
                     "       [--serial-mutation] [--slice-steps s] [--regroup-steps r] [--rank r --world n [--exchange host:port | --nccl-id-file f]]\n"
                     "       [--address tcp://ip:port|unix://path [--batched] [--nodes k]] [--edges]\n"
-                    "       [--trace-path dir [--trace-type rip|cov] [--trace-cap n]] [--module-so m.so] [--serial]\n");
+                    "       [--trace-path dir [--trace-type rip|cov|tenet] [--trace-cap n] [--tenet-cap bytes]] [--module-so m.so] [--serial]\n");
     return false;
   }
   return true;
@@ -247,11 +309,18 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
     const bool Trace = !O.trace_path.empty();
     std::unordered_set<uint64_t> TraceSeen;  // cov traces: rips not seen in earlier testcases
     if (Trace) {
-      if (O.trace_type != "rip" && O.trace_type != "cov") {
-        printf("--trace-type %s is not supported by this backend (rip, cov)\n", O.trace_type.c_str());
+      if (O.trace_type != "rip" && O.trace_type != "cov" && O.trace_type != "tenet") {
+        printf("--trace-type %s is not supported by this backend (rip, cov, tenet)\n", O.trace_type.c_str());
         return 1;
       }
-      if (!Exec.EnableTrace(O.trace_cap)) {
+      if (O.trace_type == "tenet") {
+        // the device holds lanes x cap bytes: the default is clamped to 32 GiB in all
+        const uint64_t Cap = O.tenet_cap ? O.tenet_cap : std::min<uint64_t>(1ull << 24, (32ull << 30) / N) & ~7ull;
+        if (!Exec.EnableTenet(Cap)) {
+          printf("EnableTenet failed (%u lanes x %llu bytes)\n", N, (unsigned long long)Cap);
+          return 1;
+        }
+      } else if (!Exec.EnableTrace(O.trace_cap)) {
         printf("EnableTrace failed\n");
         return 1;
       }
@@ -265,6 +334,17 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
       Inputs = Keep;
     }
     auto write_trace = [&](const fs::path &In, uint32_t Lane) -> bool {
+      if (O.trace_type == "tenet") {
+        std::vector<uint8_t> Bytes;
+        bool Truncated = false;
+        if (!Exec.LaneTenet(Lane, Bytes, Truncated)) return false;
+        FILE *F = fopen((fs::path(O.trace_path) / (In.filename().string() + ".trace")).c_str(), "w");
+        if (!F) return false;
+        FormatTenet(Bytes.data(), Bytes.size(), F);
+        fclose(F);
+        if (Truncated) printf("tenet trace of %s truncated at %zu bytes (--tenet-cap)\n", In.string().c_str(), Bytes.size());
+        return true;
+      }
       std::vector<uint64_t> Rips;
       bool Truncated = false;
       if (!Exec.LaneTrace(Lane, Rips, Truncated)) return false;

@@ -104,6 +104,13 @@ class Executor_t {
   // testcase i's (Truncated: it logged more than PerLane).
   virtual bool EnableTrace(uint32_t) { return false; }
   virtual bool LaneTrace(uint32_t, std::vector<uint64_t> &, bool &) { return false; }
+  // Tenet traces (wtf run --trace-type tenet, bochscpu_backend.cc:1215-1323):
+  // every testcase of the next RunBatch logs the entry stream wtfgpu_set_tenet
+  // documents (include/wtfgpu.h), BytesPerLane at most; LaneTenet(i) is
+  // testcase i's (Truncated: it logged more). FormatTenet (runner.cc) turns it
+  // into the reference's text.
+  virtual bool EnableTenet(uint64_t) { return false; }
+  virtual bool LaneTenet(uint32_t, std::vector<uint8_t> &, bool &) { return false; }
 };
 
 // The collective between shards (one node per GPU): an in-place MAX
@@ -139,8 +146,9 @@ struct RunnerOptions {
   bool full_coverage = false;
   bool edges = false;        // --edges: branch edges join the coverage (RecordEdge)
   std::string trace_path;    // run: --trace-path dir (one <input>.trace per input, subcommands.cc:52-74)
-  std::string trace_type = "rip";  // run: --trace-type rip | cov (wtf.cc:197-200)
+  std::string trace_type = "rip";  // run: --trace-type rip | cov | tenet (wtf.cc:197-200)
   uint32_t trace_cap = 1u << 20;   // run: rips kept per testcase
+  uint64_t tenet_cap = 0;          // run: Tenet stream bytes per testcase (0: 16 MiB, at most 32 GiB / lanes)
   bool quiet = false;
   bool serial_mutation = false;  // one mutator, in order: the reference master's stream exactly
   // fuzz: continuous batching on executors that stream (the gpu node): every
@@ -284,6 +292,13 @@ class FuzzSession {
 };
 
 bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O);
+// A Tenet entry stream (include/wtfgpu.h wtfgpu_set_tenet) as the reference's
+// text (BochscpuBackend_t::DumpTenetDelta, bochscpu_backend.cc:1215-1323): the
+// first REGS entry sets every register, each later one the registers that
+// changed since the previous one, then the accesses logged before it as
+// ,mr= / ,mw= / ,mrw= 0x<va>:<HEX>; a line only when something was printed.
+// Stops at a truncated or incomplete entry.
+void FormatTenet(const uint8_t *Stream, size_t Bytes, FILE *F);
 // Loads the snapshot, initialises the executor and the module, runs the mode.
 // make_executor is called after the options are parsed; returns the exit code.
 int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, const CpuState_t &State,
