@@ -748,7 +748,7 @@ __device__ __noinline__ void blake3_le64(u64 in, u64 &lo, u64 &hi) {
   hi = (u64)(v[2] ^ v[10]) | ((u64)(v[3] ^ v[11]) << 32);
 }
 
-__device__ __noinline__ bool bp_apply(const Dev &P, Lane &L, u64 grip) {
+__device__ __forceinline__ bool bp_apply_action(const Dev &P, Lane &L, u64 grip) {
   u32 s;
   if (!P.act_keys || !hash_find(P.act_keys, P.act_mask, grip, s)) return false;
   const wtfgpu_bp_action_t &a = P.act[s];
@@ -809,6 +809,16 @@ __device__ __noinline__ bool bp_apply(const Dev &P, Lane &L, u64 grip) {
   RS(L, WTFGPU_RSP, rsp + 8);
   L.rip = ra;
   return true;
+}
+
+// The action stands in for a host handler, whose guest-memory reads and writes
+// (VirtRead / VirtWrite) are no CPU accesses: Tenet does not log them
+// (bochscpu_backend.cc:1215-1323 logs the lin_access hook only).
+__device__ __noinline__ bool bp_apply(const Dev &P, Lane &L, u64 grip) {
+  tn_mute(L.lane);
+  const bool r = bp_apply_action(P, L, grip);
+  tn_unmute(L.lane, 0, 0, 0, false);
+  return r;
 }
 
 // A step the uop cache cannot serve: code on a lane overlay page, or an
