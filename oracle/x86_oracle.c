@@ -1158,7 +1158,7 @@ static int xstore(orc_machine *m, insn *d, int n, int align, const x128 *v) {
 }
 
 static int sse_opcode(u32 op) {
-  return (op >= 0x10 && op <= 0x17) || op == 0x28 || op == 0x29 || op == 0x2b || (op >= 0x50 && op <= 0x7f) ||
+  return (op >= 0x10 && op <= 0x17) || (op >= 0x28 && op <= 0x2f) || op == 0xc2 || (op >= 0x50 && op <= 0x7f) ||
          op == 0xae || op == 0xc3 || (op >= 0xc4 && op <= 0xc6) || op >= 0xd0;
 }
 
@@ -1414,6 +1414,9 @@ static int exec_mmx(orc_machine *m, insn *d, int pc) {
   return X_OK;
 }
 
+static int fp_form_o(u32 map, u32 c, int pp, int vex); /* x86_oracle_fp.inc */
+static int exec_fp(orc_machine *m, insn *d);
+
 static int exec_sse(orc_machine *m, insn *d) {
   const u32 op = d->op, r3 = d->reg & 7;
   const int pc = d->rep == 0xf3 ? 2 : d->rep == 0xf2 ? 3 : d->pfx66 ? 1 : 0; /* none, 66, f3, f2 */
@@ -1422,6 +1425,7 @@ static int exec_sse(orc_machine *m, insn *d) {
   x128 a, b, r;
   u64 v;
   if (d->opmap == 1 && ((pc == 0 && mmx_opcode(op)) || (op == 0xd6 && pc >= 2))) return exec_mmx(m, d, pc);
+  if (fp_form_o(d->opmap, op, pc, 0)) return exec_fp(m, d); /* U39 / U40 */
   if (d->opmap == 2) { /* 66 0f 38 00 pshufb, 66 0f 38 17 ptest */
     if (pc != 1) return X_UNIMPL;
     if (m->r.cr0 & 4 || !(m->r.cr4 & 0x200)) {
@@ -1762,6 +1766,8 @@ static void yput(orc_machine *m, u32 r, y256 v, int l256) {
   else memset(m->r.ymmh[r & 15], 0, 16);
 }
 
+#include "x86_oracle_fp.inc" /* SSE / AVX floating point (U39 / U40) */
+
 /* two-source ops of one 128-bit lane (the legacy semantics); 0 = not one */
 static int vlane(u32 op, int pc, const x128 *a, const x128 *b, u8 imm, u64 cnt, x128 *r) {
   const u32 lo = op & 0xf7;
@@ -1937,6 +1943,7 @@ static int exec_vex(orc_machine *m, insn *d) {
   const u32 op = d->op, r3 = d->reg & 7, map = d->opmap, vv = d->vvvv;
   const int pp = (int)d->vpp, l256 = (int)d->vl, mem = d->is_mem;
   const u8 imm = d->bytes[d->len - 1];
+  if (fp_form_o(map, op, pp, 1)) return exec_fp(m, d); /* U39 / U40 */
   if (map == 1 && op == 0xae && !(pp == 0 && mem && (r3 == 2 || r3 == 3))) { /* U36: vldmxcsr / vstmxcsr only */
     fault(m, WTFGPU_VEC_UD, 0);
     return X_FAULT;
@@ -2691,7 +2698,7 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
   }
 
   if (d->vex) return exec_vex(m, d);
-  if (d->opmap == 2) return exec_sse(m, d);
+  if (d->opmap == 2 || d->opmap == 3) return exec_sse(m, d);
   if (d->opmap == 1) {
     if (op == 0xae && !(!d->pfx66 && !d->rep && (d->is_mem ? ((d->reg & 7) == 2 || (d->reg & 7) == 3) : (d->reg & 7) >= 5)))
       return exec_sys0f(m, d, next_rip);
@@ -3108,7 +3115,7 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
     b = fetch8(m, d);
     if (d->fetch_fail) return -1;
     d->undef = d->vbad || d->opmap < 1 || d->opmap > 3 || !vex_defined(d->opmap, b, (int)d->vpp);
-    if (d->opmap != 1 && d->opmap != 2) {
+    if (d->opmap != 1 && d->opmap != 2 && !(d->opmap == 3 && !d->undef && fp_form_o(3, b, (int)d->vpp, 1))) {
       d->op = b;
       d->len = d->pos;
       return 1;
@@ -3126,8 +3133,9 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
       d->opmap = b == 0x38 ? 2 : 3;
       d->op = fetch8(m, d);
       if (d->fetch_fail) return -1;
-      if (d->opmap == 3 || (d->op != 0x00 && d->op != 0x17)) { /* 0f 38 00 pshufb, 0f 38 17 ptest; the rest: outside */
-        const int pfx = d->rep == 0xf3 ? 2 : d->rep == 0xf2 ? 3 : d->pfx66 ? 1 : 0;
+      const int pfx = d->rep == 0xf3 ? 2 : d->rep == 0xf2 ? 3 : d->pfx66 ? 1 : 0;
+      /* 0f 38 00 pshufb, 0f 38 17 ptest, the floating-point forms; the rest: outside */
+      if ((d->opmap == 3 || (d->op != 0x00 && d->op != 0x17)) && !fp_form_o(d->opmap, d->op, pfx, 0)) {
         d->undef = !legacy_3byte_defined(d->opmap, d->op, pfx);
         d->len = d->pos;
         return 1;
@@ -3218,9 +3226,10 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
     }
     if (b >= 0x80 && b <= 0x8f) imm = 4;
     if (d->opmap == 2) has_modrm = 1;
+    else if (d->opmap == 3) has_modrm = imm = 1;
     else {
       if (sse_opcode(b) && b != 0x77) has_modrm = 1;
-      if ((b >= 0x70 && b <= 0x73) || (b >= 0xc4 && b <= 0xc6)) imm = 1;
+      if ((b >= 0x70 && b <= 0x73) || b == 0xc2 || (b >= 0xc4 && b <= 0xc6)) imm = 1;
     }
   }
   if (has_modrm) {

@@ -121,7 +121,7 @@ AVX_FAULT_CASES = [
     ([0x66, 0xC5, 0xF9, 0xEF, 0xC1], EXIT_FAULT, 6),        # 66 before VEX
     ([0x48, 0xC5, 0xF9, 0xEF, 0xC1], EXIT_FAULT, 6),        # REX before VEX
     ([0xC5, 0xFD, 0xD7, 0x03], EXIT_FAULT, 6),              # vpmovmskb eax, [rbx]: register only
-    ([0xC5, 0xFC, 0x58, 0xC1], EXIT_UNIMPLEMENTED, None),   # vaddps (floating point)
+    ([0xC5, 0xFC, 0x58, 0xC1], RUNNING, None),              # vaddps (floating point, U39)
     ([0xC4, 0xE3, 0x79, 0x0F, 0xC1, 0x04], EXIT_UNIMPLEMENTED, None),  # vpalignr (0f 3a)
     ([0xC4, 0xE2, 0x79, 0x1C, 0xC1], EXIT_UNIMPLEMENTED, None),        # vpabsb (0f 38 1c)
     ([0x66, 0x0F, 0x38, 0x00, 0x06], EXIT_FAULT, 13),      # pshufb xmm0, [rsi]: legacy needs alignment

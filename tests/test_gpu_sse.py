@@ -326,3 +326,73 @@ def test_gpu_matches_native_avx_vectors():
             if (c["diff"] or i % 5 == 0) and eng.read_virt(i, buf_va, 256) != bytes(win):
                 fails.append((c["name"], c["code"], "mem"))
     assert not fails, f"{len(fails)}/{len(cases)} mismatches, first: {fails[:6]}"
+
+
+@pytest.mark.gpu
+def test_gpu_matches_native_fp_vectors():
+    """Every SSE / AVX floating-point vector (tests/golden/fp_vectors.json.gz,
+    U39 / U40) as one lane: GPRs, RFLAGS, all 16 YMM registers, MXCSR, and for
+    the unmasked-exception cases the #XM exit with the trap's MXCSR."""
+    from tests.test_avx import get_ymm, set_ymm
+    from tests.test_fp import DOC, VEC_XM, expected, inputs
+    from wtf_amd.abi import EXIT_FAULT
+    from wtf_amd.engine import Engine
+
+    cases = DOC["cases"]
+    codes = sorted({c["code"] for c in cases})
+    slot = {c: i for i, c in enumerate(codes)}
+    blob = bytearray(32 * len(codes))
+    for c, i in slot.items():
+        b = bytes.fromhex(c) + b"\xcc"
+        blob[32 * i: 32 * i + len(b)] = b
+    sp = AddressSpace()
+    sp.map_range(CODE_VA, bytes(blob), write=False)
+    buf_va = int(DOC["buf_va"], 16)
+    sp.map(buf_va & ~0xFFF, b"", nx=True)
+    sp.map((buf_va & ~0xFFF) + 0x1000, b"", nx=True)
+    n = (len(cases) + 63) // 64 * 64
+    eng = Engine(0)
+    pfns, pblob = sp.phys()
+    eng.load_pool(pfns, pblob)
+    eng.alloc_lanes(n, overlay_pages=4, cov_entries=64)
+    eng.set_initial_state(regs_from_state(user_state(CODE_VA, 0, sp.cr3)))
+    eng.set_limit(0)
+    eng.restore()
+    regs = eng.read_regs(0, n)
+    writes, ins = [], []
+    for i, c in enumerate(cases):
+        yin, win = inputs(c)
+        ins.append(yin)
+        r = regs[i]
+        for k in range(16):
+            r.gpr[k] = int(c["in"][k], 16)
+        r.rip = CODE_VA + 32 * slot[c["code"]]
+        r.rflags = int(c["fl"], 16) | 0x200
+        r.mxcsr = int(c["mx"], 16)
+        set_ymm(r, yin)
+        writes.append((i, buf_va, win))
+    for i in range(len(cases), n):
+        regs[i].rip = CODE_VA + 32 * slot[cases[0]["code"]] + len(bytes.fromhex(cases[0]["code"]))
+    eng.write_regs(regs)
+    eng.apply_writes(writes)
+    eng.run()
+    ex = eng.exits()
+    out = eng.read_regs(0, n)
+    fails = []
+    for i, c in enumerate(cases):
+        r = out[i]
+        if "trap_mx" in c:
+            if ex[i].status != EXIT_FAULT or ex[i].vector != VEC_XM or r.mxcsr != int(c["trap_mx"], 16):
+                fails.append((c["name"], c["code"], "trap", ex[i].status, ex[i].vector, hex(r.mxcsr)))
+            continue
+        g, y = expected(c, ins[i])
+        if ex[i].status != EXIT_INT3 or ex[i].icount != 1:
+            fails.append((c["name"], c["code"], "exit", ex[i].status, ex[i].vector))
+        elif [r.gpr[k] for k in range(16)] != g or (r.rflags ^ int(c["flo"], 16)) & 0x8D5:
+            fails.append((c["name"], c["code"], "regs"))
+        elif get_ymm([r.xmm[k][h] for k in range(16) for h in range(2)],
+                     [r.ymmh[k][h] for k in range(16) for h in range(2)]) != y:
+            fails.append((c["name"], c["code"], "ymm"))
+        elif r.mxcsr != int(c["mxo"], 16):
+            fails.append((c["name"], c["code"], "mxcsr", hex(r.mxcsr), c["mxo"]))
+    assert not fails, f"{len(fails)}/{len(cases)} mismatches, first: {fails[:6]}"

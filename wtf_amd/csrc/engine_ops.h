@@ -179,7 +179,7 @@ __constant__ u32 kMap2[256] = {
     E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), S2, S2, UDE, E(O_UD, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), UDE, NOPM, UDE, UDE,
     /*10*/ SSE8, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM, NOPM,
     /*20*/ E(O_SYS, L_RM, 0, Z_Q, Z_Q, 0, 1, 0, 1, K_NONE, 0), S2M, E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 1, K_NONE, 0), S2M, UDE,
-    UDE, UDE, UDE, SSEM, SSEM, UN, SSEM, UN, UN, UN, UN,
+    UDE, UDE, UDE, SSEM, SSEM, SSEM, SSEM, SSEM, SSEM, SSEM, SSEM,
     /*30*/ E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0),
     E(O_SYS, 0, 0, 0, 0, 0, 0, 0, 0, K_NONE, 0), S2, S2, S2, UDE, UDE, UN, UDE, UN, UDE, UDE, UDE, UDE, UDE,
     /*40*/ CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV, CMOV,
@@ -198,13 +198,14 @@ __constant__ u32 kMap2[256] = {
     E(O_BSF, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0), E(O_BSR, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0),
     E(O_MOVSX, L_GREG, L_RM, Z_V, Z_B, 0, 1, 0, 1, K_NONE, 0), E(O_MOVSX, L_GREG, L_RM, Z_V, Z_W, 0, 1, 0, 1, K_NONE, 0),
     /*c0*/ E(O_XADD, L_RM, L_GREG, Z_B, Z_B, 1, 1, 1, 1, K_NONE, 0), E(O_XADD, L_RM, L_GREG, Z_V, Z_V, 1, 1, 1, 1, K_NONE, 0),
-    UN, SSEM, SSEI, SSEI, SSEI, E(O_SYS, L_RM, 0, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0),
+    SSEI, SSEM, SSEI, SSEI, SSEI, E(O_SYS, L_RM, 0, Z_V, Z_V, 0, 1, 0, 1, K_NONE, 0),
     BSWAP, BSWAP, BSWAP, BSWAP, BSWAP, BSWAP, BSWAP, BSWAP,
     /*d0*/ SSE8, SSE8,
     /*e0*/ SSE8, SSE8,
     /*f0*/ SSE8, SSE8,
 };
 constexpr u32 kSseModrm = E(O_SSE, 0, 0, 0, 0, 0, 0, 0, 1, K_NONE, 0);  // 0f 38 / VEX map 2 opcodes
+constexpr u32 kSseModrmImm = E(O_SSE, 0, 0, 0, 0, 0, 0, 0, 1, K_B, 0);  // 0f 3a / VEX map 3 opcodes (imm8)
 constexpr u32 kUnimpl = UN;
 #undef E
 #undef UN
@@ -307,7 +308,7 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
     rex = 0x40 | (vw << 3) | (vr << 2) | (vx << 1) | vb;
     c = ib_at(b, pos++);  // the opcode
     const bool def = !bad && vmap >= 1 && vmap <= 3 && vex_defined(vmap, c, vpp);
-    if (!def || vmap == 3) {  // U36: #UD from the opcode byte; a defined 0f 3a form is outside the subset
+    if (!def || (vmap == 3 && !fp_form(3, c, vpp, true))) {  // U36: #UD from the opcode byte; 0f 3a: fp forms only
       u.len = pos;
       u.op = (lock || !def) ? O_UD : O_UNIMPL;
       u.supported = lock || !def;
@@ -321,7 +322,7 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
   if (vex) {
     smap = vex_map(vex);
     map2 = 1;
-    e = smap == 1 ? kMap2[c] : smap == 2 ? kSseModrm : kUnimpl;
+    e = smap == 1 ? kMap2[c] : smap == 2 ? kSseModrm : kSseModrmImm;
     if (smap == 1 && (e & 63) != O_SSE) e = kUnimpl;
   } else if (c == 0x0f) {
     if (pos >= 15) return 2;
@@ -331,11 +332,12 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
       if (pos >= 15) return 2;
       if (pos >= b.avail) return 1;
       const u32 c3 = ib_at(b, pos++);
-      if (c == 0x38 && (c3 == 0x00 || c3 == 0x17)) {
+      const u32 pfx3 = u.rep == 0xf3 ? 2 : u.rep == 0xf2 ? 3 : p66 ? 1 : 0;
+      if ((c == 0x38 && (c3 == 0x00 || c3 == 0x17)) || fp_form(c == 0x38 ? 2 : 3, c3, pfx3, false)) {
+        smap = c == 0x38 ? 2 : 3;
+        e = smap == 3 ? kSseModrmImm : kSseModrm;
         c = c3;
-        smap = 2;
         map2 = 1;
-        e = kSseModrm;
       } else {
         const bool def = legacy_3byte_defined(c == 0x38 ? 2 : 3, c3, u.rep == 0xf3 ? 2 : u.rep == 0xf2 ? 3 : p66 ? 1 : 0);
         u.len = pos;

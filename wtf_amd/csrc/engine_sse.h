@@ -23,6 +23,7 @@
 // zeroes them.
 #pragma once
 #include "engine_exec.h"
+#include "engine_fp.h"
 
 namespace wtfgpu_dev {
 
@@ -60,6 +61,7 @@ __device__ __forceinline__ u32 vex_map(u32 x) { return (x >> 8) & 31; }
 // Register-only / memory-only / VEX.L / VEX.vvvv violations are #UD at
 // execution, not here.
 __device__ __forceinline__ bool sse_valid(u32 map, u32 c, u32 pc, u32 is_mem, u32 r3) {
+  if (fp_form(map, c, pc, false)) return true;  // engine_ssefp.h
   if (map == 2) return pc == 1 && (c == 0x00 || c == 0x17);
   if (c == 0xc3) return pc == 0;
   if (c == 0xae) return pc == 0 && (is_mem ? (r3 == 2 || r3 == 3) : r3 >= 5);
@@ -131,6 +133,7 @@ __host__ __device__ inline bool legacy_3byte_defined(u32 map, u32 op, u32 pfx) {
 }
 
 __device__ __forceinline__ bool vex_valid(u32 map, u32 c, u32 pp, u32 is_mem, u32 r3) {
+  if (fp_form(map, c, pp, true)) return true;  // engine_ssefp.h
   if (map == 2) return pp == 1 && (c == 0x00 || c == 0x17 || c == 0x58 || c == 0x59 || c == 0x78 || c == 0x79);
   if (map != 1) return false;
   if (c == 0x77) return pp == 0;
@@ -394,6 +397,10 @@ __device__ __forceinline__ u64 sse_ea(const Dev &P, const Lane &L, const UOp &u,
 
 __device__ __noinline__ int vex_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next);
 
+}  // namespace wtfgpu_dev
+#include "engine_ssefp.h"  // SSE / AVX floating point: fp_exec
+namespace wtfgpu_dev {
+
 // ---------------------------------------------------------------- MMX (U37)
 // The oracle's exec_mmx: mm i is physical x87 register R(i) = fpst[(i - TOS)
 // & 7] (fpst holds ST order); a completed MMX instruction rotates fpst to R
@@ -592,6 +599,7 @@ __device__ __noinline__ int sse_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
     set_fault(L, 7, 0, 0);  // #NM
     return X_FAULT;
   }
+  if (fp_form(map, c, pc, false)) return fp_exec(P, L, u, nrip, next);
   // the r/m operand: 16 bytes aligned unless an unaligned move / narrower form
   u32 n = 16;
   bool align = true;
@@ -703,6 +711,7 @@ __device__ __noinline__ int sse_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
 __device__ __noinline__ int vex_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next) {
   next = nrip;
   const u32 x = u.opreg, c = u.sub, pp = u.bsz, r3 = u.reg & 7, map = vex_map(x);
+  if (fp_form(map, c, pp, true)) return fp_exec(P, L, u, nrip, next);  // its own VEX checks
   const u32 l256 = (x >> 1) & 1, w = (x >> 2) & 1, vvvv = (x >> 4) & 15;
   const bool mem = u.is_mem;
   const u32 imm = (u32)u.imm & 0xff;

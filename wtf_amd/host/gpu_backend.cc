@@ -763,7 +763,7 @@ bool GpuBackend_t::fill_results(const std::vector<uint32_t> &lanes, uint32_t fir
   HostPool::Get().For(fin.size(), 1024, [&](size_t i) {
     LaneResult &r = (*out)[fin[i]];
     const LaneView &v = views_[fin[i]];
-    r.result = v.result ? *v.result : TestcaseResult_t(Ok_t());
+    r.result = v.result ? std::move(*v.result) : TestcaseResult_t(Ok_t());  // the view is reset at refill
     if (want_gprs_) {
       memcpy(r.gprs, &regs[i * 18], 18 * 8);
       r.rip = r.gprs[16];
@@ -1304,6 +1304,7 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
     tag_.assign(nlanes_, 0);
     tc_bytes_.assign(nlanes_, 0);
     lres_.assign(nlanes_, LaneResult{});
+    lres_stale_.assign(nlanes_, 0);
     const uint32_t n = parts_n();
     parts_.assign(n, Part{});
     for (uint32_t p = 0; p < n; p++) {
@@ -1322,6 +1323,7 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
   if (pipelined && wtfgpu_select_queue(ctx_, pi)) return false;
   if (pipelined && P.launched && !harvest_part(P, Target, Out, Slots)) return false;
   const auto ti = Clock::now();
+  stats_.harvest_ms += std::chrono::duration<double, std::milli>(ti - t0).count();
   // ---- refill
   std::vector<uint32_t> fresh;
   std::vector<std::pair<const uint8_t *, size_t>> tcs;
@@ -1331,6 +1333,7 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
       tcs.push_back({In[fresh.size() - 1].data, In[fresh.size() - 1].size});
     }
   if (Taken) *Taken = fresh.size();
+  stats_.fresh_ms += ms_since(ti);
   if (!fresh.empty()) {
     if (wtfgpu_restore_lanes(ctx_, fresh.data(), (uint32_t)fresh.size())) return false;
     stats_.restore_dev_ms += ms_since(ti);
@@ -1340,7 +1343,7 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
       busy_[l] = 1;
       tag_[l] = In[i].tag;
       tc_bytes_[l] = In[i].size;
-      lres_[l] = LaneResult{};
+      lres_stale_[l] = 1;  // its last result may not be consumed yet (this call's Out)
     });
     const auto tm = Clock::now();
     stats_.restore_ms += std::chrono::duration<double, std::milli>(tm - ti).count();
@@ -1384,9 +1387,11 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
   }
   stats_.insert_ms += ms_since(ti);
   // ---- one slice over the part's occupied lanes
+  const auto to = Clock::now();
   P.occ.clear();
   for (uint32_t l = P.lo; l < P.hi; l++)
     if (busy_[l]) P.occ.push_back(l);
+  stats_.occ_ms += ms_since(to);
   if (!P.occ.empty()) {
     const auto tk = Clock::now();
     if (wtfgpu_run_async(ctx_, P.lo, P.hi - P.lo, Slice ? Slice : 4096)) return false;
@@ -1411,6 +1416,20 @@ bool GpuBackend_t::harvest_part(Part &P, const Target_t &Target, std::vector<Str
   account_run(rs);
   P.launched = false;
   const uint32_t first = P.lo, count = P.hi - P.lo;
+  // the results handed out for these lanes' previous testcases were consumed
+  // before this call: clear them (capacity kept) before this slice's go in
+  HostPool::Get().For(P.occ.size(), 1024, [&](size_t i) {
+    const uint32_t l = P.occ[i];
+    if (!lres_stale_[l]) return;
+    lres_stale_[l] = 0;
+    LaneResult &r = lres_[l];
+    r.result = Ok_t();
+    r.error = false;
+    r.exit_status = 0;
+    r.icount = 0;
+    r.rip = 0;
+    r.new_coverage.clear();
+  }, P.occ.size() >= 8192);
   if (P.ex.size() < count) P.ex.resize(count);
   if (wtfgpu_read_exits(ctx_, first, count, P.ex.data())) return false;
   std::vector<uint8_t> done(count, 0);
@@ -1436,15 +1455,15 @@ bool GpuBackend_t::harvest_part(Part &P, const Target_t &Target, std::vector<Str
   stats_.coverage_ms += std::chrono::duration<double, std::milli>(tr - tc).count();
   target_restore(Target, finished, Slots);
   stats_.target_restore_ms += ms_since(tr);
+  const auto tout = Clock::now();
   const size_t base = Out.size();
   Out.resize(base + finished.size());
-  HostPool::Get().For(finished.size(), 1024, [&](size_t i) {
+  for (size_t i = 0; i < finished.size(); i++) {
     const uint32_t l = finished[i];
-    Out[base + i] = StreamResult_t{tag_[l], std::move(lres_[l])};
-    lres_[l] = LaneResult{};
-    busy_[l] = 0;
-    // not runnable until refilled (a finished lane keeps its exit status)
-  }, finished.size() >= 8192);
+    Out[base + i] = StreamResult_t{tag_[l], &lres_[l]};
+    busy_[l] = 0;  // not runnable until refilled (a finished lane keeps its exit status)
+  }
+  stats_.out_ms += ms_since(tout);
   stats_.batches++;
   return true;
 }
@@ -1480,8 +1499,9 @@ std::string GpuBackend_t::StatsJson() const {
   std::string r(b);
   r.pop_back();
   snprintf(b, sizeof(b), ",\"up_prep_ms\":%.3f,\"up_regs_ms\":%.3f,\"up_apply_ms\":%.3f,\"up_feed_ms\":%.3f,"
-           "\"restore_dev_ms\":%.3f", stats_.up_prep_ms, stats_.up_regs_ms, stats_.up_apply_ms, stats_.up_feed_ms,
-           stats_.restore_dev_ms);
+           "\"restore_dev_ms\":%.3f,\"out_ms\":%.3f,\"fresh_ms\":%.3f,\"occ_ms\":%.3f,\"harvest_ms\":%.3f",
+           stats_.up_prep_ms, stats_.up_regs_ms, stats_.up_apply_ms, stats_.up_feed_ms, stats_.restore_dev_ms,
+           stats_.out_ms, stats_.fresh_ms, stats_.occ_ms, stats_.harvest_ms);
   r += b;
   r += ",\"unimpl_ops\":" + stats_.unimpl_ops.json();
   r += ",\"unimpl_raw\":" + stats_.unimpl_ops.raw_json();

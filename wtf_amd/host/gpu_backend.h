@@ -47,6 +47,7 @@ struct BatchStats {
   // upload split: write-record preparation on the host, register upload,
   // memory-write apply, feed upload; device restore within restore_ms
   double up_prep_ms = 0, up_regs_ms = 0, up_apply_ms = 0, up_feed_ms = 0, restore_dev_ms = 0;
+  double out_ms = 0, fresh_ms = 0, occ_ms = 0, harvest_ms = 0;  // streaming: result hand-over, refill list, slice list, whole harvest
   // streaming harvest split: per-lane byte counters, coverage logs, attribution
   double bytes_ms = 0, covlog_ms = 0, attrib_ms = 0;
   uint64_t cov_entries = 0;  // (lane, rip) new-coverage log entries collected
@@ -209,6 +210,7 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   std::vector<uint64_t> tag_;
   std::vector<uint64_t> tc_bytes_;  // the testcase size in each lane (B_exec)
   std::vector<LaneResult> lres_;
+  std::vector<uint8_t> lres_stale_;  // lres_[l] still holds a handed-out result: reset at the lane's next harvest
   std::vector<uint32_t> cov_lanes_;  // coverage collection buffers (streaming)
   std::vector<uint64_t> cov_rips_;
   bool cov_ovf_warned_ = false;

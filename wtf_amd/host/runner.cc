@@ -433,7 +433,7 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
         }
         next -= In.size() - Taken;  // offered again next step
         for (StreamResult_t &F : R) {
-          Res[F.tag] = std::move(F.r);
+          Res[F.tag] = std::move(*F.r);
           Got[F.tag] = 1;
           got++;
         }
@@ -712,7 +712,12 @@ bool FuzzSession::Step() {
   // (two reads could disagree under --seconds and skip a collective)
   const bool done = Done();
   if (X_ && X_->World() > 1 && done) return MergeCoverage();
-  if (stream_) return StreamStep(done);
+  if (stream_) {
+    const auto tc = Clock::now();
+    const bool ok = StreamStep(done);
+    S_.call_ms += secs_since(tc) * 1e3;
+    return ok;
+  }
   BatchRefs_.clear();
   for (const std::unique_ptr<TcArena> &A : Batch_)
     for (size_t i = 0; i < A->Count(); i++) BatchRefs_.push_back(TcRef{A.get(), (uint32_t)i});
@@ -800,13 +805,13 @@ bool FuzzSession::StreamStep(bool Done) {
   // that the serial bookkeeping below only hashes the new ones
   std::vector<uint8_t> Known(Out.size(), 0);
   HostPool::Get().For(Out.size(), 512, [&](size_t i) {
-    if (const Crash_t *C = std::get_if<Crash_t>(&Out[i].r.result))
-      Known[i] = !Out[i].r.error && CrashNames_.count(C->CrashName) != 0;
+    if (const Crash_t *C = std::get_if<Crash_t>(&Out[i].r->result))
+      Known[i] = !Out[i].r->error && CrashNames_.count(C->CrashName) != 0;
   }, Out.size() >= 4096);
   for (size_t i = 0; i < Out.size(); i++) {
     StreamResult_t &F = Out[i];
     const TcRef R = Slot_[F.tag];
-    Account(R.data(), R.size(), F.r, Known[i]);
+    Account(R.data(), R.size(), *F.r, Known[i]);
     if (--R.A->Live == 0) Arenas_.erase(R.A);  // every testcase of the arena accounted
     Slot_[F.tag] = TcRef{};
     FreeSlot_.push_back(F.tag);
@@ -903,7 +908,7 @@ std::string FuzzSession::SummaryJson() const {
            "\"instr_per_s\":%.3f,\"coverage\":%zu,\"corpus\":%zu,\"crashes\":%llu,\"unique_crashes\":%zu,"
            "\"timeouts\":%llu,\"cr3\":%llu,\"errors\":%llu,\"error_retired\":%llu,\"merged_rips\":%llu,"
            "\"merge_ms\":%.3f,\"produce_wait_ms\":%.3f,\"account_ms\":%.3f,\"make_ms\":%.3f,\"step_ms\":%.3f,\"fill_ms\":%.3f,"
-           "\"newcov_ms\":%.3f,\"crashsave_ms\":%.3f,\"cpu_s\":%.3f,"
+           "\"newcov_ms\":%.3f,\"crashsave_ms\":%.3f,\"call_ms\":%.3f,\"cpu_s\":%.3f,"
            "\"backend\":",
            O_.name.c_str(), Exec_.Lanes(), X_ ? X_->Rank() : 0, X_ ? X_->World() : 1,
            (unsigned long long)S_.batches, (unsigned long long)S_.execs, (unsigned long long)S_.retired, Wall,
@@ -911,7 +916,7 @@ std::string FuzzSession::SummaryJson() const {
            Exec_.CoverageSize(), Corpus_.Size(), (unsigned long long)S_.crashes, CrashNames_.size(),
            (unsigned long long)S_.timeouts, (unsigned long long)S_.cr3, (unsigned long long)S_.errors,
            (unsigned long long)S_.error_retired, (unsigned long long)S_.merged_rips, S_.merge_ms, S_.produce_wait_ms,
-           S_.account_ms, S_.make_ms, S_.step_ms, S_.fill_ms, S_.newcov_ms, S_.crashsave_ms, ProcessCpuSeconds());
+           S_.account_ms, S_.make_ms, S_.step_ms, S_.fill_ms, S_.newcov_ms, S_.crashsave_ms, S_.call_ms, ProcessCpuSeconds());
   return std::string(b) + Exec_.StatsJson() + "}";
 }
 

@@ -39,9 +39,12 @@ struct StreamTestcase_t {
   size_t size;
   uint64_t tag;  // the caller's name for it, returned with its result
 };
+// A finished testcase: its tag and its result, which stays in the executor's
+// storage and is valid until the executor's next StreamStep (no per-result
+// copies of the ~250-byte LaneResult on the step's thread).
 struct StreamResult_t {
   uint64_t tag;
-  LaneResult r;
+  LaneResult *r;
 };
 
 // A backend that runs many testcases per call (GpuBackend_t; the oracle twin
@@ -186,6 +189,7 @@ struct FuzzStats {
   double produce_wait_ms = 0, account_ms = 0;  // streaming: waiting on the mutator, master bookkeeping
   double make_ms = 0, step_ms = 0;             // streaming: mutation on the step's own thread, whole steps
   double fill_ms = 0;                          // streaming: taking the step's testcases (make_ms included)
+  double call_ms = 0;                          // streaming: whole StreamStep calls, destructors included
   double newcov_ms = 0, crashsave_ms = 0;      // account_ms split: corpus admissions, new crash names
 };
 
