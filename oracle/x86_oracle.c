@@ -1416,6 +1416,8 @@ static int exec_mmx(orc_machine *m, insn *d, int pc) {
 
 static int fp_form_o(u32 map, u32 c, int pp, int vex); /* x86_oracle_fp.inc */
 static int exec_fp(orc_machine *m, insn *d);
+static int s4_form_o(u32 map, u32 c, int pp, int vex); /* x86_oracle_sse4.inc */
+static int exec_s4(orc_machine *m, insn *d);
 
 static int exec_sse(orc_machine *m, insn *d) {
   const u32 op = d->op, r3 = d->reg & 7;
@@ -1426,6 +1428,7 @@ static int exec_sse(orc_machine *m, insn *d) {
   u64 v;
   if (d->opmap == 1 && ((pc == 0 && mmx_opcode(op)) || (op == 0xd6 && pc >= 2))) return exec_mmx(m, d, pc);
   if (fp_form_o(d->opmap, op, pc, 0)) return exec_fp(m, d); /* U39 / U40 */
+  if (s4_form_o(d->opmap, op, pc, 0)) return exec_s4(m, d); /* U41 */
   if (d->opmap == 2) { /* 66 0f 38 00 pshufb, 66 0f 38 17 ptest */
     if (pc != 1) return X_UNIMPL;
     if (m->r.cr0 & 4 || !(m->r.cr4 & 0x200)) {
@@ -1767,6 +1770,7 @@ static void yput(orc_machine *m, u32 r, y256 v, int l256) {
 }
 
 #include "x86_oracle_fp.inc" /* SSE / AVX floating point (U39 / U40) */
+#include "x86_oracle_sse4.inc" /* SSSE3 / SSE4.1 integer, AVX2 lane crossing (U41) */
 
 /* two-source ops of one 128-bit lane (the legacy semantics); 0 = not one */
 static int vlane(u32 op, int pc, const x128 *a, const x128 *b, u8 imm, u64 cnt, x128 *r) {
@@ -1944,6 +1948,7 @@ static int exec_vex(orc_machine *m, insn *d) {
   const int pp = (int)d->vpp, l256 = (int)d->vl, mem = d->is_mem;
   const u8 imm = d->bytes[d->len - 1];
   if (fp_form_o(map, op, pp, 1)) return exec_fp(m, d); /* U39 / U40 */
+  if (s4_form_o(map, op, pp, 1)) return exec_s4(m, d); /* U41 */
   if (map == 1 && op == 0xae && !(pp == 0 && mem && (r3 == 2 || r3 == 3))) { /* U36: vldmxcsr / vstmxcsr only */
     fault(m, WTFGPU_VEC_UD, 0);
     return X_FAULT;
@@ -3115,7 +3120,8 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
     b = fetch8(m, d);
     if (d->fetch_fail) return -1;
     d->undef = d->vbad || d->opmap < 1 || d->opmap > 3 || !vex_defined(d->opmap, b, (int)d->vpp);
-    if (d->opmap != 1 && d->opmap != 2 && !(d->opmap == 3 && !d->undef && fp_form_o(3, b, (int)d->vpp, 1))) {
+    if (d->opmap != 1 && d->opmap != 2 &&
+        !(d->opmap == 3 && !d->undef && (fp_form_o(3, b, (int)d->vpp, 1) || s4_form_o(3, b, (int)d->vpp, 1)))) {
       d->op = b;
       d->len = d->pos;
       return 1;
@@ -3135,7 +3141,8 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
       if (d->fetch_fail) return -1;
       const int pfx = d->rep == 0xf3 ? 2 : d->rep == 0xf2 ? 3 : d->pfx66 ? 1 : 0;
       /* 0f 38 00 pshufb, 0f 38 17 ptest, the floating-point forms; the rest: outside */
-      if ((d->opmap == 3 || (d->op != 0x00 && d->op != 0x17)) && !fp_form_o(d->opmap, d->op, pfx, 0)) {
+      if ((d->opmap == 3 || (d->op != 0x00 && d->op != 0x17)) && !fp_form_o(d->opmap, d->op, pfx, 0) &&
+          !s4_form_o(d->opmap, d->op, pfx, 0)) {
         d->undef = !legacy_3byte_defined(d->opmap, d->op, pfx);
         d->len = d->pos;
         return 1;

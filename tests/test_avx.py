@@ -122,10 +122,11 @@ AVX_FAULT_CASES = [
     ([0x48, 0xC5, 0xF9, 0xEF, 0xC1], EXIT_FAULT, 6),        # REX before VEX
     ([0xC5, 0xFD, 0xD7, 0x03], EXIT_FAULT, 6),              # vpmovmskb eax, [rbx]: register only
     ([0xC5, 0xFC, 0x58, 0xC1], RUNNING, None),              # vaddps (floating point, U39)
-    ([0xC4, 0xE3, 0x79, 0x0F, 0xC1, 0x04], EXIT_UNIMPLEMENTED, None),  # vpalignr (0f 3a)
-    ([0xC4, 0xE2, 0x79, 0x1C, 0xC1], EXIT_UNIMPLEMENTED, None),        # vpabsb (0f 38 1c)
+    ([0xC4, 0xE3, 0x79, 0x0F, 0xC1, 0x04], RUNNING, None),  # vpalignr (0f 3a, U41)
+    ([0xC4, 0xE2, 0x79, 0x1C, 0xC1], RUNNING, None),        # vpabsb (0f 38 1c, U41)
     ([0x66, 0x0F, 0x38, 0x00, 0x06], EXIT_FAULT, 13),      # pshufb xmm0, [rsi]: legacy needs alignment
-    ([0x66, 0x0F, 0x38, 0x1C, 0xC1], EXIT_UNIMPLEMENTED, None),        # pabsb (outside)
+    ([0x66, 0x0F, 0x38, 0x1C, 0xC1], RUNNING, None),        # pabsb (U41)
+    ([0x66, 0x0F, 0x3A, 0x42, 0xC1, 0x00], EXIT_UNIMPLEMENTED, None),  # mpsadbw (outside)
     # U36: encodings the emulated CPU does not define
     ([0xC4, 0x30, 0x02, 0x00], EXIT_FAULT, 6),              # VEX map 0x10 (runaway HEVD bytes)
     ([0xC4, 0xE0, 0x79, 0x58, 0xC1], EXIT_FAULT, 6),        # VEX map 0
@@ -141,7 +142,7 @@ AVX_FAULT_CASES = [
     ([0xC5, 0xF8, 0xAE, 0x16], EXIT_UNIMPLEMENTED, None),   # vldmxcsr [rsi]: defined, outside the subset
     ([0xC5, 0xF8, 0xAE, 0xC1], EXIT_FAULT, 6),              # VEX 0f ae, register form
     ([0xC5, 0xF8, 0xAE, 0x06], EXIT_FAULT, 6),              # VEX 0f ae /0 (fxsave has no VEX form)
-    ([0xC4, 0xE3, 0x79, 0x0F, 0x06, 0x04], EXIT_UNIMPLEMENTED, None),  # vpalignr xmm, [rsi]
+    ([0xC4, 0xE3, 0x79, 0x0F, 0x06, 0x04], RUNNING, None),  # vpalignr xmm, [rsi] (U41)
     ([0x66, 0x0F, 0x38, 0x37, 0xC1], EXIT_FAULT, 6),        # pcmpgtq: SSE4.2 not enumerated
     ([0x0F, 0x38, 0xF0, 0x06], EXIT_FAULT, 6),              # movbe: not enumerated
     ([0x66, 0x0F, 0x38, 0xDC, 0xC1], EXIT_FAULT, 6),        # aesenc: not enumerated

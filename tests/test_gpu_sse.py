@@ -328,13 +328,12 @@ def test_gpu_matches_native_avx_vectors():
     assert not fails, f"{len(fails)}/{len(cases)} mismatches, first: {fails[:6]}"
 
 
-@pytest.mark.gpu
-def test_gpu_matches_native_fp_vectors():
-    """Every SSE / AVX floating-point vector (tests/golden/fp_vectors.json.gz,
-    U39 / U40) as one lane: GPRs, RFLAGS, all 16 YMM registers, MXCSR, and for
-    the unmasked-exception cases the #XM exit with the trap's MXCSR."""
+def _run_vector_doc(DOC, inputs, mem=False):
+    """Every case of a native-vector document (gen_fp_vectors.run_native's
+    format) as one lane: GPRs, RFLAGS, all 16 YMM registers, MXCSR, the window
+    (mem), and for the unmasked-exception cases the #XM exit with the trap's MXCSR."""
     from tests.test_avx import get_ymm, set_ymm
-    from tests.test_fp import DOC, VEC_XM, expected, inputs
+    from tests.test_fp import VEC_XM, expected
     from wtf_amd.abi import EXIT_FAULT
     from wtf_amd.engine import Engine
 
@@ -359,10 +358,11 @@ def test_gpu_matches_native_fp_vectors():
     eng.set_limit(0)
     eng.restore()
     regs = eng.read_regs(0, n)
-    writes, ins = [], []
+    writes, ins, wins = [], [], []
     for i, c in enumerate(cases):
         yin, win = inputs(c)
         ins.append(yin)
+        wins.append(win)
         r = regs[i]
         for k in range(16):
             r.gpr[k] = int(c["in"][k], 16)
@@ -395,4 +395,22 @@ def test_gpu_matches_native_fp_vectors():
             fails.append((c["name"], c["code"], "ymm"))
         elif r.mxcsr != int(c["mxo"], 16):
             fails.append((c["name"], c["code"], "mxcsr", hex(r.mxcsr), c["mxo"]))
+        elif mem and c.get("mdiff"):
+            w = bytearray(wins[i])
+            for k, v in c["mdiff"]:
+                w[k] = v
+            if eng.read_virt(i, buf_va, 256) != bytes(w):
+                fails.append((c["name"], c["code"], "mem"))
     assert not fails, f"{len(fails)}/{len(cases)} mismatches, first: {fails[:6]}"
+
+
+def test_gpu_matches_native_fp_vectors():
+    """SSE / AVX floating point (tests/golden/fp_vectors.json.gz, U39 / U40)."""
+    from tests.test_fp import DOC, inputs
+    _run_vector_doc(DOC, inputs)
+
+
+def test_gpu_matches_native_sse4_vectors():
+    """SSSE3 / SSE4.1 integer and AVX2 lane-crossing forms (tests/golden/sse4_vectors.json.gz, U41)."""
+    from tests.test_sse4 import DOC, inputs
+    _run_vector_doc(DOC, inputs, mem=True)

@@ -308,7 +308,7 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
     rex = 0x40 | (vw << 3) | (vr << 2) | (vx << 1) | vb;
     c = ib_at(b, pos++);  // the opcode
     const bool def = !bad && vmap >= 1 && vmap <= 3 && vex_defined(vmap, c, vpp);
-    if (!def || (vmap == 3 && !fp_form(3, c, vpp, true))) {  // U36: #UD from the opcode byte; 0f 3a: fp forms only
+    if (!def || (vmap == 3 && !fp_form(3, c, vpp, true) && !s4_form(3, c, vpp, true))) {  // U36: #UD from the opcode byte
       u.len = pos;
       u.op = (lock || !def) ? O_UD : O_UNIMPL;
       u.supported = lock || !def;
@@ -333,7 +333,8 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
       if (pos >= b.avail) return 1;
       const u32 c3 = ib_at(b, pos++);
       const u32 pfx3 = u.rep == 0xf3 ? 2 : u.rep == 0xf2 ? 3 : p66 ? 1 : 0;
-      if ((c == 0x38 && (c3 == 0x00 || c3 == 0x17)) || fp_form(c == 0x38 ? 2 : 3, c3, pfx3, false)) {
+      if ((c == 0x38 && (c3 == 0x00 || c3 == 0x17)) || fp_form(c == 0x38 ? 2 : 3, c3, pfx3, false) ||
+          s4_form(c == 0x38 ? 2 : 3, c3, pfx3, false)) {
         smap = c == 0x38 ? 2 : 3;
         e = smap == 3 ? kSseModrmImm : kSseModrm;
         c = c3;

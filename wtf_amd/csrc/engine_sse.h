@@ -27,6 +27,8 @@
 
 namespace wtfgpu_dev {
 
+__host__ __device__ inline bool s4_form(u32 map, u32 c, u32 pp, bool vex);  // engine_sse4.h
+
 struct X128 {
   u64 lo, hi;
 };
@@ -61,7 +63,7 @@ __device__ __forceinline__ u32 vex_map(u32 x) { return (x >> 8) & 31; }
 // Register-only / memory-only / VEX.L / VEX.vvvv violations are #UD at
 // execution, not here.
 __device__ __forceinline__ bool sse_valid(u32 map, u32 c, u32 pc, u32 is_mem, u32 r3) {
-  if (fp_form(map, c, pc, false)) return true;  // engine_ssefp.h
+  if (fp_form(map, c, pc, false) || s4_form(map, c, pc, false)) return true;  // engine_ssefp.h, engine_sse4.h
   if (map == 2) return pc == 1 && (c == 0x00 || c == 0x17);
   if (c == 0xc3) return pc == 0;
   if (c == 0xae) return pc == 0 && (is_mem ? (r3 == 2 || r3 == 3) : r3 >= 5);
@@ -133,7 +135,7 @@ __host__ __device__ inline bool legacy_3byte_defined(u32 map, u32 op, u32 pfx) {
 }
 
 __device__ __forceinline__ bool vex_valid(u32 map, u32 c, u32 pp, u32 is_mem, u32 r3) {
-  if (fp_form(map, c, pp, true)) return true;  // engine_ssefp.h
+  if (fp_form(map, c, pp, true) || s4_form(map, c, pp, true)) return true;  // engine_ssefp.h, engine_sse4.h
   if (map == 2) return pp == 1 && (c == 0x00 || c == 0x17 || c == 0x58 || c == 0x59 || c == 0x78 || c == 0x79);
   if (map != 1) return false;
   if (c == 0x77) return pp == 0;
@@ -399,6 +401,7 @@ __device__ __noinline__ int vex_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
 
 }  // namespace wtfgpu_dev
 #include "engine_ssefp.h"  // SSE / AVX floating point: fp_exec
+#include "engine_sse4.h"  // SSSE3 / SSE4.1 integer, AVX2 lane-crossing: s4_exec
 namespace wtfgpu_dev {
 
 // ---------------------------------------------------------------- MMX (U37)
@@ -600,6 +603,7 @@ __device__ __noinline__ int sse_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
     return X_FAULT;
   }
   if (fp_form(map, c, pc, false)) return fp_exec(P, L, u, nrip, next);
+  if (s4_form(map, c, pc, false)) return s4_exec(P, L, u, nrip, next);
   // the r/m operand: 16 bytes aligned unless an unaligned move / narrower form
   u32 n = 16;
   bool align = true;
@@ -712,6 +716,7 @@ __device__ __noinline__ int vex_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
   next = nrip;
   const u32 x = u.opreg, c = u.sub, pp = u.bsz, r3 = u.reg & 7, map = vex_map(x);
   if (fp_form(map, c, pp, true)) return fp_exec(P, L, u, nrip, next);  // its own VEX checks
+  if (s4_form(map, c, pp, true)) return s4_exec(P, L, u, nrip, next);
   const u32 l256 = (x >> 1) & 1, w = (x >> 2) & 1, vvvv = (x >> 4) & 15;
   const bool mem = u.is_mem;
   const u32 imm = (u32)u.imm & 0xff;
