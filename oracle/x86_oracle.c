@@ -164,6 +164,7 @@ struct orc_machine {
   vec tracelist;
   /* Tenet (U38, wtfgpu_set_tenet's stream): entries as u64 words */
   int tn, tn_mute;
+  u32 xm_flags; /* MXCSR flags of an instruction that faulted with #XM (U40) */
   vec tnlist;
   u64 tn_ipos, tn_last; /* the current instruction's first entry / latest ACC entry (~0: none) */
   /* per-instruction scratch */
@@ -3417,6 +3418,8 @@ static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
     m->r = saved;
     m->bytes = saved_bytes;
   }
+  m->r.mxcsr |= m->xm_flags; /* a SIMD FP exception keeps the flags it set (U40) */
+  m->xm_flags = 0;
   switch (x) {
   case X_FAULT: {
     wtfgpu_exit_t keep = *ex;

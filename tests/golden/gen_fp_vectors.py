@@ -45,6 +45,7 @@ class Form:
         self.ptrs = dict(ptrs)
         self.smalls = dict(smalls)
         self.ints = ints  # sources are integers (cvtdq2ps, cvtdq2pd)
+        self.cls = "sse"  # tests/progfuzz.py's block kind
 
 
 def leg_rr(pp, op, reg, rm, w=0, map3=None):

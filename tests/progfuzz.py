@@ -66,10 +66,17 @@ def make_program(rng: random.Random, forms, n_blocks=24) -> bytes:
     return bytes(code[:SLOT])
 
 
-def build(n_programs: int, seed: int, sse: bool = False):
-    """Returns (AddressSpace, base state, list of (code_va, regs dict))."""
+def build(n_programs: int, seed: int, sse: bool = False, fp: bool = False):
+    """Returns (AddressSpace, base state, list of (code_va, regs dict)). fp:
+    the SSE / AVX floating-point (U39 / U40) and SSE4 / AVX2 (U41) forms join
+    the SSE pool."""
     rng = random.Random(seed)
     forms = gen_forms(random.Random(seed ^ 0xABCDEF))
+    if fp:
+        from tests.golden.gen_fp_vectors import gen_forms as gen_fp_forms
+        from tests.golden.gen_sse4_vectors import gen_forms as gen_sse4_forms
+
+        forms = forms + (gen_fp_forms(random.Random(seed ^ 0xF9)) + gen_sse4_forms(random.Random(seed ^ 0x54))) * 2
     if sse:
         from tests.golden.gen_sse_vectors import gen_forms as gen_sse_forms
 
@@ -104,7 +111,19 @@ def lane_xmm(n: int, seed: int, salt: int = 0x3E3):
     return [[rng.getrandbits(64) for _ in range(32)] for _ in range(n)]
 
 
-def oracle_run(sp: AddressSpace, st: dict, lanes, limit=20000, breakpoints=(), xmm=None, ymmh=None):
+def lane_mxcsr(n: int, seed: int):
+    """Initial MXCSR per lane: rounding control, DAZ, FTZ, sometimes unmasked exceptions."""
+    rng = random.Random(seed ^ 0x3C5)
+    out = []
+    for _ in range(n):
+        mx = 0x1F80 | (rng.randrange(4) << 13) | (0x40 if rng.random() < 0.3 else 0) | (0x8000 if rng.random() < 0.3 else 0)
+        if rng.random() < 0.2:
+            mx &= ~(rng.getrandbits(6) << 7)
+        out.append(mx)
+    return out
+
+
+def oracle_run(sp: AddressSpace, st: dict, lanes, limit=20000, breakpoints=(), xmm=None, ymmh=None, mxcsr=None):
     """Runs every lane on the CPU oracle; returns per-lane result dicts."""
     from tests.oracle_lib import Oracle
 
@@ -124,6 +143,8 @@ def oracle_run(sp: AddressSpace, st: dict, lanes, limit=20000, breakpoints=(), x
         if ymmh is not None:
             for k in range(16):
                 r.ymmh[k][0], r.ymmh[k][1] = ymmh[i][2 * k], ymmh[i][2 * k + 1]
+        if mxcsr is not None:
+            r.mxcsr = mxcsr[i]
         r.rip = va
         r.rflags = flags
         o.restore(base)

@@ -204,15 +204,17 @@ def test_gpu_sse_faults_match_oracle():
         eng.close()
 
 
-@pytest.mark.parametrize("seed", [21, 22])
-def test_gpu_matches_oracle_on_random_sse_programs(seed):
+@pytest.mark.parametrize("seed,fp", [(21, False), (22, False), (23, True), (24, True)])
+def test_gpu_matches_oracle_on_random_sse_programs(seed, fp):
+    """fp: with the floating-point and SSE4 / AVX2 forms and a random MXCSR per lane."""
     from wtf_amd.engine import Engine
 
     n = 512
-    sp, st, lanes = progfuzz.build(n, seed=seed, sse=True)
+    sp, st, lanes = progfuzz.build(n, seed=seed, sse=True, fp=fp)
     xmm = progfuzz.lane_xmm(n, seed)
     ymmh = progfuzz.lane_xmm(n, seed, 0x4E4)
-    want = progfuzz.oracle_run(sp, st, lanes, xmm=xmm, ymmh=ymmh)
+    mx = progfuzz.lane_mxcsr(n, seed) if fp else None
+    want = progfuzz.oracle_run(sp, st, lanes, xmm=xmm, ymmh=ymmh, mxcsr=mx)
     eng = Engine(0)
     pfns, blob = sp.phys()
     eng.load_pool(pfns, blob)
@@ -229,6 +231,8 @@ def test_gpu_matches_oracle_on_random_sse_programs(seed):
         set_xmm(regs[i], xmm[i])
         for k in range(16):
             regs[i].ymmh[k][0], regs[i].ymmh[k][1] = ymmh[i][2 * k], ymmh[i][2 * k + 1]
+        if mx is not None:
+            regs[i].mxcsr = mx[i]
     eng.write_regs(regs)
     stats = eng.run()
     ex = eng.exits()

@@ -260,16 +260,19 @@ def test_engine_sse_code_faults(code, status, vector):
         assert out.vector == vector
 
 
-@pytest.mark.parametrize("fast", [False, True])
-def test_engine_sse_code_matches_oracle_on_random_programs(fast):
+@pytest.mark.parametrize("fast,fp", [(False, False), (True, False), (True, True)])
+def test_engine_sse_code_matches_oracle_on_random_programs(fast, fp):
+    """fp: with the floating-point and SSE4 / AVX2 forms and a random MXCSR per lane."""
     from tests import progfuzz
 
     L = sim_lib()
     n = 160
-    sp, st, lanes = progfuzz.build(n, seed=31, sse=True)
-    xmm = progfuzz.lane_xmm(n, 31)
-    ymmh = progfuzz.lane_xmm(n, 31, 0x4E4)
-    want = progfuzz.oracle_run(sp, st, lanes, xmm=xmm, ymmh=ymmh)
+    seed = 33 if fp else 31
+    sp, st, lanes = progfuzz.build(n, seed=seed, sse=True, fp=fp)
+    xmm = progfuzz.lane_xmm(n, seed)
+    ymmh = progfuzz.lane_xmm(n, seed, 0x4E4)
+    mx = progfuzz.lane_mxcsr(n, seed) if fp else None
+    want = progfuzz.oracle_run(sp, st, lanes, xmm=xmm, ymmh=ymmh, mxcsr=mx)
     bad = []
     for i, ((va, g, flags), w) in enumerate(zip(lanes, want)):
         regs = regs_from_state(st)
@@ -278,6 +281,8 @@ def test_engine_sse_code_matches_oracle_on_random_programs(fast):
             regs.xmm[k][0], regs.xmm[k][1] = xmm[i][2 * k], xmm[i][2 * k + 1]
             regs.ymmh[k][0], regs.ymmh[k][1] = ymmh[i][2 * k], ymmh[i][2 * k + 1]
         regs.rip, regs.rflags = va, flags
+        if mx is not None:
+            regs.mxcsr = mx[i]
         out = sim_run(L, sp, regs, limit=20000, fast=fast)
         got = (out.status, out.vector if out.status == EXIT_FAULT else 0, out.rip, out.icount)
         exp = (w["status"], w["vector"] if w["status"] == EXIT_FAULT else 0, w["rip"], w["icount"])

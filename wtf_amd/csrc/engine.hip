@@ -917,7 +917,7 @@ __device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr
 #ifndef WTFGPU_LANE_LDS
 #define WTFGPU_LANE_LDS 1
 #endif
-#if WTFGPU_LANE_LDS
+#if WTFGPU_LANE_LDS == 1
 // the register slots take an odd stride (33 dwords) so a wave's copies spread
 // over the LDS banks; the Lane slots (60 dwords) conflict 4-way at most
 #define LANE_COPY_DECL            \
@@ -926,6 +926,18 @@ __device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr
 #define LANE_COPY_SLOT                                  \
   Lane &T = sLane[threadIdx.x];                         \
   u32 *const tlo_ = sRegs[threadIdx.x], *const thi_ = sRegs[threadIdx.x] + 16;
+#elif WTFGPU_LANE_LDS == 2
+// in HBM, one slot per lane (L2-resident while the lane runs): the LDS the
+// copy took is left to a second wave per SIMD (measured variant)
+struct LaneCopy {
+  Lane l;
+  u32 r[32];
+};
+#define LANE_COPY_DECL
+#define LANE_COPY_SLOT                                       \
+  LaneCopy &C_ = ((LaneCopy *)P.lcopy)[lane];                \
+  Lane &T = C_.l;                                            \
+  u32 *const tlo_ = C_.r, *const thi_ = C_.r + 16;
 #else
 #define LANE_COPY_DECL
 #define LANE_COPY_SLOT    \
@@ -1805,6 +1817,7 @@ struct wtfgpu_ctx {
   u64 *d_trace = nullptr;     // rip traces (Dev::trace)
   u32 *d_tracecnt = nullptr;
   LaneTlb *d_tlbs = nullptr;  // translation state kept between k_run launches
+  u8 *d_lcopy = nullptr;      // WTFGPU_LANE_LDS=2: the rare path's lane copies
   u32 *d_tlbok = nullptr;
   u8 *d_ovdata = nullptr;
   wtfgpu_regs_t *d_full = nullptr;  // full per-lane architectural state (cold fields)
@@ -2113,6 +2126,7 @@ static void free_lanes(wtfgpu_ctx *c) {
   dfree(c->d_exinfo);
   dfree(c->d_sys);
   dfree(c->d_tlbs);
+  dfree(c->d_lcopy);
   dfree(c->d_tlbok);
   dfree(c->d_rdseed);
   dfree(c->d_stopargs);
@@ -2264,6 +2278,9 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
   }
   rc |= dalloc(&c->d_full, N);
   rc |= dalloc(&c->d_tlbs, N);
+#if WTFGPU_LANE_LDS == 2
+  rc |= dalloc(&c->d_lcopy, N * sizeof(LaneCopy));
+#endif
   rc |= dalloc(&c->d_tlbok, N);
   rc |= dalloc(&c->d_rdseed, N);
   rc |= dalloc(&c->d_stopargs, 6 * N);
@@ -2312,6 +2329,7 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
   P.exinfo = c->d_exinfo;
   P.sys = c->d_sys;
   P.tlbs = c->d_tlbs;
+  P.lcopy = c->d_lcopy;
   P.tlb_ok = c->d_tlbok;
   P.rd_seed = c->d_rdseed;
   P.stop_args = c->d_stopargs;

@@ -134,6 +134,7 @@ struct Dev {
   u32 trace_cap;
   u64 rd_seed0;           // the initial state's (restore)
   LaneTlb *tlbs;          // [nlanes]
+  void *lcopy;            // [nlanes] Lane + 32 u32: the rare path's lane copy (build WTFGPU_LANE_LDS=2 only)
   u32 *tlb_ok;            // [nlanes]
   wtfgpu_regs_t *full;   // [nlanes] cold architectural state (MSRs the hot LaneSys lacks)
   u64 cr3_0;             // the testcases' initial cr3 (Cr3Change_t, bochscpu_backend.cc:628-657)
