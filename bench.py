@@ -71,7 +71,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=6)
-    ap.add_argument("--lanes", type=int, default=131072, help="lanes per GPU of the tlv and hevd legs")
+    ap.add_argument("--lanes", type=int, default=262144, help="lanes per GPU of the tlv headline (two waves per SIMD "
+                    "per pipelined half)")
+    ap.add_argument("--hevd-lanes", type=int, default=131072, help="lanes per GPU of the hevd leg")
     ap.add_argument("--syn-lanes", type=int, default=65536, help="BASELINE.json configs[1]: 64K lanes")
     ap.add_argument("--slice-steps", type=int, default=0, help="wave-steps per streaming slice (0: the node's 4096)")
     ap.add_argument("--regroup-steps", type=int, default=-1,
@@ -448,7 +450,7 @@ def run(a, rank, world, local, tmp):
             if out["cpu_node"]:
                 out["vs_cpu_node"] = out["cpu_node"]["vs_cpu_node"]
         if legs:
-            h = hevd_leg(hevd_dir, a.lanes, a.hevd_limit, a.leg_seconds, sched_flags(a))
+            h = hevd_leg(hevd_dir, a.hevd_lanes, a.hevd_limit, a.leg_seconds, sched_flags(a))
             if "hevd" in cpu:
                 h["cpu_baseline"] = cpu["hevd"]
                 h["vs_cpu"] = h["value"] / cpu["hevd"]["value"]

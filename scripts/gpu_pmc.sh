@@ -28,7 +28,7 @@ for leg in ${LEGS:-tlv hevd syn}; do
   run $leg write 180 --pmc WRITE_SIZE
   run $leg mix 180 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR
   run $leg wait 180 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES
-  cd $R && python3 scripts/pmc_summary.py /tmp/pmc/$leg $leg $([ $leg = syn ] && echo 65536 || echo 131072) $([ $leg = hevd ] && echo 10000000 || echo 100000) > gpurun_out/pmc/pmc_${leg}_k_run${TAG}.json && cd /tmp || { echo SUMMARY_FAIL $leg; exit 1; }
+  cd $R && python3 scripts/pmc_summary.py /tmp/pmc/$leg $leg $([ $leg = syn ] && echo 65536 || ([ $leg = hevd ] && echo 131072 || echo 262144)) $([ $leg = hevd ] && echo 10000000 || echo 100000) > gpurun_out/pmc/pmc_${leg}_k_run${TAG}.json && cd /tmp || { echo SUMMARY_FAIL $leg; exit 1; }
   # the raw CSVs stay on the box (large); the kernel statistics and logs come back
   cp $(find /tmp/pmc/$leg/stats -name '*kernel_stats.csv' | head -1) $R/gpurun_out/pmc/${leg}_kernel_stats${TAG}.csv
   cp /tmp/pmc/$leg/stats.log $R/gpurun_out/pmc/${leg}_stats${TAG}.log

@@ -15,7 +15,7 @@ def main():
     leg = sys.argv[1]
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     limit = 100000
-    lanes = 65536 if leg == "syn" else 131072  # bench.py's --syn-lanes / --lanes defaults
+    lanes = 65536 if leg == "syn" else 262144  # bench.py's --syn-lanes / --lanes defaults
     if leg == "syn":
         s = bench.syn_leg(lanes, limit, steps, 0)
         print(json.dumps({"leg": "syn", "lanes": lanes, "limit": limit, "launches": s.get("launches"),

@@ -911,11 +911,14 @@ __device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr
 
 // Runs `call` on a copy T of lane L whose registers live in arrays of their
 // own, so the kernel's register arrays never escape into a called function
-// (they stay in VGPRs). The copy lives in LDS (sLane / sRegs, one slot per
-// thread; WTFGPU_LANE_LDS=0: on the stack, i.e. scratch, whose write-backs
-// were most of k_run's HBM traffic).
+// (they stay in VGPRs). WTFGPU_LANE_LDS picks where the copy lives:
+//   2 (default) a per-lane slot in HBM (L2-resident while the lane runs),
+//     which leaves LDS to a second resident wave per SIMD: k_run launches
+//     take 1.25-1.35x less time per lane than with 1 (MI355X, tlv);
+//   1 LDS (sLane / sRegs, one slot per thread): one wave per SIMD;
+//   0 the stack, i.e. scratch, whose write-backs were most of k_run's HBM traffic.
 #ifndef WTFGPU_LANE_LDS
-#define WTFGPU_LANE_LDS 1
+#define WTFGPU_LANE_LDS 2
 #endif
 #if WTFGPU_LANE_LDS == 1
 // the register slots take an odd stride (33 dwords) so a wave's copies spread
