@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define WTFGPU_ABI_VERSION 2
+#define WTFGPU_ABI_VERSION 3
 #define WTFGPU_PAGE_SIZE 4096u
 
 /* Status codes. */
@@ -124,6 +124,9 @@ typedef struct wtfgpu_regs {
   uint64_t fpst[8];
   uint64_t xmm[16][2];  /* bits 127:0 of ymm0..15 */
   uint64_t ymmh[16][2]; /* bits 255:128 (CpuState_t::Zmm[i].Q[2..3]) */
+  uint16_t fpse[8];     /* sign / exponent words of ST(0..7) (ABI 3): CpuState_t::Fpst
+                           carries the 64-bit significands only (globals.h:1067), so a
+                           snapshot loads these as 0 */
 } wtfgpu_regs_t;
 
 /* Why a lane stopped. */

@@ -1201,11 +1201,18 @@ static void mmx_commit(orc_machine *m) {
   const u32 tos = (m->r.fpsw >> 11) & 7;
   if (tos) {
     u64 t[8];
-    for (u32 j = 0; j < 8; j++) t[j] = m->r.fpst[(j - tos) & 7];
+    u16 e[8];
+    for (u32 j = 0; j < 8; j++) t[j] = m->r.fpst[(j - tos) & 7], e[j] = m->r.fpse[(j - tos) & 7];
     memcpy(m->r.fpst, t, sizeof(t));
+    memcpy(m->r.fpse, e, sizeof(e));
   }
   m->r.fpsw &= (u16)~0x3800;
   m->r.fptw = 0;
+}
+/* an MMX register write: the significand, sign and exponent all ones */
+static void mmx_put(orc_machine *m, u32 i, u64 v) {
+  m->r.fpst[i] = v;
+  m->r.fpse[i] = 0xffff;
 }
 static x128 x64(u64 v) {
   x128 r;
@@ -1243,7 +1250,7 @@ static int exec_mmx(orc_machine *m, insn *d, int pc) {
     fault(m, 7, 0);
     return X_FAULT;
   }
-  if (m->r.fpsw & 0x80) { /* a pending unmasked x87 exception */
+  if (m->r.fpsw & ~m->r.fpcw & 0x3f) { /* a pending unmasked x87 exception */
     fault(m, 16, 0);
     return X_FAULT;
   }
@@ -1259,7 +1266,7 @@ static int exec_mmx(orc_machine *m, insn *d, int pc) {
     } else {
       const x128 x = xreg(m, d->rm);
       mmx_commit(m);
-      m->r.fpst[mr] = el(&x, 0, 8);
+      mmx_put(m, mr, el(&x, 0, 8));
     }
     return X_OK;
   }
@@ -1309,7 +1316,7 @@ static int exec_mmx(orc_machine *m, insn *d, int pc) {
       return X_OK;
     }
     mmx_commit(m);
-    m->r.fpst[mm_rm] = av;
+    mmx_put(m, mm_rm, av);
     return X_OK;
   case 0x60: case 0x61: case 0x62: /* punpckl*: the low halves */
     r = unpack(1 << (op - 0x60), 0, &a, &b);
@@ -1343,7 +1350,7 @@ static int exec_mmx(orc_machine *m, insn *d, int pc) {
     const int w = op == 0x71 ? 2 : op == 0x72 ? 4 : 8;
     r = shift_el(r3 == 2 ? 0 : r3 == 4 ? 1 : 2, w, &b, imm);
     mmx_commit(m);
-    m->r.fpst[mm_rm] = el(&r, 0, 8);
+    mmx_put(m, mm_rm, el(&r, 0, 8));
     return X_OK;
   }
   case 0xc4: { /* pinsrw mm, r32/m16, imm8 */
@@ -1411,7 +1418,7 @@ static int exec_mmx(orc_machine *m, insn *d, int pc) {
   }
   mmx_commit(m);
   if (to_gpr >= 0) m->r.gpr[d->reg] = res; /* zero-extended into the 64-bit register */
-  else m->r.fpst[mr] = res;
+  else mmx_put(m, mr, res);
   return X_OK;
 }
 
@@ -2535,7 +2542,7 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
         fault(m, VEC_NM, 0);
         return X_FAULT;
       }
-      if (m->r.fpsw & 0x80) {
+      if (m->r.fpsw & ~m->r.fpcw & 0x3f) { /* a pending unmasked exception */
         fault(m, VEC_MF, 0);
         return X_FAULT;
       }

@@ -418,3 +418,66 @@ def test_gpu_matches_native_sse4_vectors():
     """SSSE3 / SSE4.1 integer and AVX2 lane-crossing forms (tests/golden/sse4_vectors.json.gz, U41)."""
     from tests.test_sse4 import DOC, inputs
     _run_vector_doc(DOC, inputs, mem=True)
+
+
+def test_gpu_matches_x87_vectors():
+    """x87 arithmetic (tests/golden/x87_vectors.json.gz, U42): every case one
+    lane; its x87 state, status flags and 16-byte memory operand in, the
+    host CPU's answer out (registers, sign / exponent words, FCW / FSW / tags,
+    RFLAGS, the operand bytes, #MF / #UD / stack-fault outcomes)."""
+    from tests.golden.gen_x87_vectors import case_regs
+    from tests.test_x87 import DOC
+    from wtf_amd.abi import EXIT_FAULT
+    from wtf_amd.engine import Engine
+
+    cases = DOC["cases"]
+    codes = sorted({c["code"] for c in cases})
+    slot = {c: i for i, c in enumerate(codes)}
+    blob = bytearray(32 * len(codes))
+    for c, i in slot.items():
+        b = bytes.fromhex(c) + b"\xcc"
+        blob[32 * i: 32 * i + len(b)] = b
+    sp = AddressSpace()
+    sp.map_range(CODE_VA, bytes(blob), write=False)
+    buf_va = int(DOC["buf_va"], 16)
+    sp.map(buf_va & ~0xFFF, b"", nx=True)
+    sp.map((buf_va & ~0xFFF) + 0x1000, b"", nx=True)
+    n = (len(cases) + 63) // 64 * 64
+    eng = Engine(0)
+    pfns, pblob = sp.phys()
+    eng.load_pool(pfns, pblob)
+    eng.alloc_lanes(n, overlay_pages=4, cov_entries=64)
+    eng.set_initial_state(regs_from_state(user_state(CODE_VA, 0, sp.cr3)))
+    eng.set_limit(0)
+    eng.restore()
+    regs = eng.read_regs(0, n)
+    writes = []
+    for i, c in enumerate(cases):
+        r = regs[i]
+        case_regs(c, r)
+        r.gpr[6] = buf_va
+        r.rip = CODE_VA + 32 * slot[c["code"]]
+        writes.append((i, buf_va, bytes.fromhex(c["mem"])))
+    for i in range(len(cases), n):
+        regs[i].rip = CODE_VA + 32 * slot[cases[0]["code"]] + len(bytes.fromhex(cases[0]["code"]))
+    eng.write_regs(regs)
+    eng.apply_writes(writes)
+    eng.run()
+    ex = eng.exits()
+    out = eng.read_regs(0, n)
+    fails = []
+    for i, c in enumerate(cases):
+        w, r = c["out"], out[i]
+        if w["status"] == EXIT_FAULT:
+            if ex[i].status != EXIT_FAULT or ex[i].vector != w["vector"]:
+                fails.append((c["code"], "fault", ex[i].status, ex[i].vector))
+            continue
+        if ex[i].status != EXIT_INT3 or ex[i].icount != 1:
+            fails.append((c["code"], "exit", ex[i].status, ex[i].vector))
+        elif (r.fpcw, r.fpsw, r.fptw, r.rflags & 0x8D5) != (w["fcw"], w["fsw"], w["ftw"], w["fl"]):
+            fails.append((c["code"], "status", hex(r.fpsw), hex(w["fsw"])))
+        elif [(r.fpst[k], r.fpse[k]) for k in range(8)] != [tuple(x) for x in w["st"]]:
+            fails.append((c["code"], "st"))
+        elif eng.read_virt(i, buf_va, 16).hex() != w["mem"]:
+            fails.append((c["code"], "mem"))
+    assert not fails, f"{len(fails)}/{len(cases)} mismatches, first: {fails[:6]}"

@@ -144,8 +144,10 @@ def test_engine_mmx_code_matches_native_vectors():
 FAULT_CASES = [
     ([0x0F, 0xFC, 0xC1], dict(cr0=0x80050031 | 4), EXIT_FAULT, 6),    # CR0.EM: #UD
     ([0x0F, 0xFC, 0xC1], dict(cr0=0x80050031 | 8), EXIT_FAULT, 7),    # CR0.TS: #NM
-    ([0x0F, 0xFC, 0xC1], dict(fsw=0x80), EXIT_FAULT, 16),             # FSW.ES: #MF
-    ([0x0F, 0x77], dict(fsw=0x80), EXIT_FAULT, 16),                   # emms too
+    ([0x0F, 0xFC, 0xC1], dict(fsw=0x8081, fcw=0x37E), EXIT_FAULT, 16),  # an unmasked flag pending: #MF
+    ([0x0F, 0x77], dict(fsw=0x8081, fcw=0x37E), EXIT_FAULT, 16),      # emms too
+    ([0x0F, 0x77], dict(fsw=0x0001, fcw=0x37E), EXIT_FAULT, 16),      # the host's rule: ES not needed
+    ([0x0F, 0x77], dict(fsw=0x0080, fcw=0x37F), RUNNING, None),       # ES with every flag masked: none
     ([0x0F, 0x73, 0xD9, 0x01], {}, EXIT_FAULT, 6),                    # psrldq has no MMX form
     ([0x0F, 0x71, 0xC1, 0x01], {}, EXIT_FAULT, 6),                    # 71 /0
     ([0x0F, 0x71, 0x16, 0x01], {}, EXIT_FAULT, 6),                    # shift-by-imm of memory
@@ -158,9 +160,10 @@ FAULT_CASES = [
 ]
 
 
-def run_one(code, L=None, cr0=None, fsw=0, tos=0, fptw=0xFFFF, mm=None):
+def run_one(code, L=None, cr0=None, fsw=0, tos=0, fptw=0xFFFF, mm=None, fcw=0x37F):
     sp, regs = layout(bytes(code), BUF, bytes(range(256)), cr0=cr0)
     regs.gpr[6] = BUF + 0x13
+    regs.fpcw = fcw
     regs.fpsw = fsw | (tos << 11)
     regs.fptw = fptw
     for i in range(8):

@@ -36,7 +36,7 @@ class Regs(C.Structure):
         ("idtr_limit", C.c_uint32), ("mxcsr", C.c_uint32), ("mxcsr_mask", C.c_uint32),
         ("fpcw", C.c_uint16), ("fpsw", C.c_uint16), ("fptw", C.c_uint16), ("fpop", C.c_uint16),
         ("pad0", C.c_uint32), ("fpst", C.c_uint64 * 8), ("xmm", (C.c_uint64 * 2) * 16),
-        ("ymmh", (C.c_uint64 * 2) * 16),
+        ("ymmh", (C.c_uint64 * 2) * 16), ("fpse", C.c_uint16 * 8),
     ]
 
 

@@ -420,11 +420,17 @@ __device__ __forceinline__ void mmx_commit(wtfgpu_regs_t &F) {
   const u32 tos = (F.fpsw >> 11) & 7;
   if (tos) {
     u64 t[8];
-    for (u32 j = 0; j < 8; j++) t[j] = F.fpst[(j - tos) & 7];
-    for (u32 j = 0; j < 8; j++) F.fpst[j] = t[j];
+    u16 e[8];
+    for (u32 j = 0; j < 8; j++) t[j] = F.fpst[(j - tos) & 7], e[j] = F.fpse[(j - tos) & 7];
+    for (u32 j = 0; j < 8; j++) F.fpst[j] = t[j], F.fpse[j] = e[j];
   }
   F.fpsw = (u16)(F.fpsw & ~0x3800);
   F.fptw = 0;
+}
+// an MMX register write: the significand, sign and exponent all ones (after mmx_commit: ST = R order)
+__device__ __forceinline__ void mmx_put(wtfgpu_regs_t &F, u32 i, u64 v) {
+  F.fpst[i] = v;
+  F.fpse[i] = 0xffff;
 }
 
 __device__ __noinline__ int mmx_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next) {
@@ -447,7 +453,7 @@ __device__ __noinline__ int mmx_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
     set_fault(L, 7, 0, 0);  // #NM
     return X_FAULT;
   }
-  if (F.fpsw & 0x80) {
+  if (F.fpsw & ~F.fpcw & 0x3f) {
     set_fault(L, 16, 0, 0);  // #MF: a pending unmasked x87 exception
     return X_FAULT;
   }
@@ -463,7 +469,7 @@ __device__ __noinline__ int mmx_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
     } else {
       const u64 v = xmm_get(P, L, u.rm).lo;
       mmx_commit(F);
-      F.fpst[mr] = v;
+      mmx_put(F, mr, v);
     }
     return X_OK;
   }
@@ -505,7 +511,7 @@ __device__ __noinline__ int mmx_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
     case 0x7f: case 0xe7:  // movq mm/m64, mm; movntq m64, mm
       if (mem && !vwrite(L, ea, 8, av)) return X_FAULT;
       mmx_commit(F);
-      if (!mem) F.fpst[mrm] = av;
+      if (!mem) mmx_put(F, mrm, av);
       return X_OK;
     case 0x68: case 0x69: case 0x6a:  // punpckh*: the high halves
       r = sse_unpack(1u << (c - 0x68), 0, X128{av >> 32, 0}, X128{bv >> 32, 0});
@@ -526,7 +532,7 @@ __device__ __noinline__ int mmx_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
     case 0x71: case 0x72: case 0x73:  // by imm8, of mm (r/m)
       r = sse_shift_imm(c, r3, b, imm);
       mmx_commit(F);
-      F.fpst[mrm] = r.lo;
+      mmx_put(F, mrm, r.lo);
       return X_OK;
     case 0xc4: {  // pinsrw mm, r32/m16, imm8
       u64 v = 0;
@@ -563,7 +569,7 @@ __device__ __noinline__ int mmx_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
   }
   mmx_commit(F);
   if (to_gpr) RS(L, u.reg, res);
-  else F.fpst[mr] = res;
+  else mmx_put(F, mr, res);
   return X_OK;
 }
 

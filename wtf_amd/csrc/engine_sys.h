@@ -226,6 +226,13 @@ __device__ __forceinline__ u32 tag_of(u64 mant, u32 se) {
   if (e == 0) return mant ? 2 : 1;
   return (mant >> 63) ? 0 : 2;
 }
+// FSW after loading a status / control pair: ES and B follow the unmasked
+// flags (what the host's FXRSTOR / FRSTOR / FLDENV do, U42)
+__device__ __forceinline__ u32 fsw_norm(u32 fsw, u32 fcw) {
+  return (fsw & 0x7f7fu) | ((fsw & ~fcw & 0x3fu) ? 0x8080u : 0u);
+}
+// a waiting x87 instruction takes #MF while an unmasked exception flag is set
+__device__ __forceinline__ bool x87_pending(const wtfgpu_regs_t &F) { return (F.fpsw & ~F.fpcw & 0x3f) != 0; }
 __device__ __forceinline__ u32 mxcsr_mask_of(const wtfgpu_regs_t &F) { return F.mxcsr_mask ? F.mxcsr_mask : 0xffbfu; }
 
 // 8 bytes of the legacy (FXSAVE) image at offset off (a multiple of 8, < 416)
@@ -237,7 +244,7 @@ __device__ __noinline__ u64 legacy_q(const Dev &P, const Lane &L, u32 off) {
   if (off == 24) return (u64)F.mxcsr | ((u64)mxcsr_mask_of(F) << 32);
   if (off < 160) {
     const u32 k = (off - 32) >> 4;
-    return (off & 8) ? 0 : F.fpst[k];
+    return (off & 8) ? (u64)F.fpse[k] : F.fpst[k];
   }
   const u32 k = (off - 160) >> 4;
   return F.xmm[k][(off >> 3) & 1];
@@ -248,7 +255,21 @@ __device__ __forceinline__ void x87_init(wtfgpu_regs_t &F) {
   F.fpsw = 0;
   F.fptw = 0xffff;
   F.fpop = 0;
-  for (int i = 0; i < 8; i++) F.fpst[i] = 0;
+  for (int i = 0; i < 8; i++) F.fpst[i] = 0, F.fpse[i] = 0;
+}
+
+// FNINIT: control / status / tags reset, TOP = 0 (ST order rotated to R order),
+// the register contents kept
+__device__ __forceinline__ void x87_fninit(wtfgpu_regs_t &F) {
+  const u32 top = (F.fpsw >> 11) & 7;
+  u64 t[8];
+  u16 e[8];
+  for (u32 j = 0; j < 8; j++) t[j] = F.fpst[(j - top) & 7], e[j] = F.fpse[(j - top) & 7];
+  for (u32 j = 0; j < 8; j++) F.fpst[j] = t[j], F.fpse[j] = e[j];
+  F.fpcw = 0x37f;
+  F.fpsw = 0;
+  F.fptw = 0xffff;
+  F.fpop = 0;
 }
 
 // bytes [off, off + n) of the legacy region written with vwrite (n a multiple of 8)
@@ -283,10 +304,10 @@ __device__ __noinline__ bool x87_load(const Dev &P, Lane &L, u64 va, bool commit
     w |= t << (2 * p);
   }
   F.fpcw = (u16)q0;
-  F.fpsw = (u16)fsw;
+  F.fpsw = (u16)fsw_norm(fsw, (u32)q0 & 0xffff);
   F.fptw = (u16)w;
   F.fpop = (u16)((q0 >> 48) & 0x7ff);
-  for (u32 i = 0; i < 8; i++) F.fpst[i] = mant[i];
+  for (u32 i = 0; i < 8; i++) F.fpst[i] = mant[i], F.fpse[i] = (u16)se[i];
   return true;
 }
 
@@ -429,6 +450,10 @@ __device__ __forceinline__ u64 env_q(const wtfgpu_regs_t &F, u32 off) {
   return 0;
 }
 
+}  // namespace wtfgpu_dev
+#include "engine_x87.h"
+namespace wtfgpu_dev {
+
 __device__ __noinline__ int exec_x87(const Dev &P, Lane &L, const UOp &u, u64 va) {
   wtfgpu_regs_t &F = P.full[L.lane];
   const u32 op = u.sub & 0xff, r3 = u.reg & 7, mem = u.is_mem;
@@ -438,11 +463,11 @@ __device__ __noinline__ int exec_x87(const Dev &P, Lane &L, const UOp &u, u64 va
   if (op == 0xdb && !mem && (modrm == 0xe2 || modrm == 0xe3)) ctl = true;
   if (op == 0xdd && mem && (r3 == 4 || r3 == 6 || r3 == 7)) ctl = true;
   if (op == 0xdf && !mem && modrm == 0xe0) ctl = true;
-  if (!ctl) return X_UNIMPL;
+  if (!ctl) return x87_arith(P, L, u, va);
   if (mem && (r3 == 4 || r3 == 6) && u.bsz == 2) return X_UNIMPL;  // 16-bit environment formats
   if (L.cr0 & 0xc) return fault_x(L, VEC_NM, 0);
   if (op == 0xdb) {
-    if (modrm == 0xe3) x87_init(F);
+    if (modrm == 0xe3) x87_fninit(F);
     else F.fpsw &= 0x7f00;
     return X_OK;
   }
@@ -456,7 +481,7 @@ __device__ __noinline__ int exec_x87(const Dev &P, Lane &L, const UOp &u, u64 va
       if (!vread(L, va, 8, q0) || !vread(L, va + 8, 8, q1) || !vread(L, va + 16, 8, q2) || !vread(L, va + 24, 4, q3))
         return X_FAULT;
       F.fpcw = (u16)q0;
-      F.fpsw = (u16)(q0 >> 32);
+      F.fpsw = (u16)fsw_norm((u32)(q0 >> 32) & 0xffff, (u32)q0 & 0xffff);
       F.fptw = (u16)q1;
       F.fpop = (u16)((q2 >> 16) & 0x7ff);
       return X_OK;
@@ -484,16 +509,14 @@ __device__ __noinline__ int exec_x87(const Dev &P, Lane &L, const UOp &u, u64 va
     u64 q0, q1, q2, q3;
     if (!vread(L, va, 8, q0) || !vread(L, va + 8, 8, q1) || !vread(L, va + 16, 8, q2) || !vread(L, va + 24, 4, q3))
       return X_FAULT;
-    u64 st[8];
-    for (u32 i = 0; i < 8; i++) {
-      u64 se;
-      if (!vread(L, va + 28 + 10 * i, 8, st[i]) || !vread(L, va + 36 + 10 * i, 2, se)) return X_FAULT;
-    }
+    u64 st[8], se[8];
+    for (u32 i = 0; i < 8; i++)
+      if (!vread(L, va + 28 + 10 * i, 8, st[i]) || !vread(L, va + 36 + 10 * i, 2, se[i])) return X_FAULT;
     F.fpcw = (u16)q0;
-    F.fpsw = (u16)(q0 >> 32);
+    F.fpsw = (u16)fsw_norm((u32)(q0 >> 32) & 0xffff, (u32)q0 & 0xffff);
     F.fptw = (u16)q1;
     F.fpop = (u16)((q2 >> 16) & 0x7ff);
-    for (u32 i = 0; i < 8; i++) F.fpst[i] = st[i];
+    for (u32 i = 0; i < 8; i++) F.fpst[i] = st[i], F.fpse[i] = (u16)se[i];
     return X_OK;
   }
   if (r3 == 6) {  // fnsave, then fninit
@@ -502,8 +525,8 @@ __device__ __noinline__ int exec_x87(const Dev &P, Lane &L, const UOp &u, u64 va
         !vwrite(L, va + 24, 4, 0))
       return X_FAULT;
     for (u32 i = 0; i < 8; i++)
-      if (!vwrite(L, va + 28 + 10 * i, 8, F.fpst[i]) || !vwrite(L, va + 36 + 10 * i, 2, 0)) return X_FAULT;
-    x87_init(F);
+      if (!vwrite(L, va + 28 + 10 * i, 8, F.fpst[i]) || !vwrite(L, va + 36 + 10 * i, 2, F.fpse[i])) return X_FAULT;
+    x87_fninit(F);
     return X_OK;
   }
   return vwrite(L, va, 2, F.fpsw) ? X_OK : X_FAULT;  // fnstsw m16
@@ -586,7 +609,7 @@ __device__ __noinline__ int sys2_exec(const Dev &P, Lane &L, const UOp &u, u64 n
       }
       case 0x9b:  // fwait (U32)
         if ((L.cr0 & 0xa) == 0xa) return fault_x(L, VEC_NM, 0);
-        if (F.fpsw & 0x80) return fault_x(L, VEC_MF, 0);
+        if (x87_pending(F)) return fault_x(L, VEC_MF, 0);
         return X_OK;
       case 0xc8: {  // enter (U29), 64-bit operand size
         if (p66) return X_UNIMPL;
