@@ -1185,7 +1185,7 @@ static void ptest(orc_machine *m, const u8 *a, const u8 *b, int n) {
  * physical x87 register R(i); fpst holds ST(0..7), so mm i = fpst[(i - TOS) & 7].
  * A completed MMX instruction sets TOS = 0 (fpst rotated to R order) and every
  * tag valid (fptw = 0); emms sets every tag empty (fptw = 0xffff). Checks in
- * order: #UD if CR0.EM, #NM if CR0.TS, #MF if FSW.ES, then the operand's
+ * order: #UD if CR0.EM, #NM if CR0.TS, #MF if an unmasked x87 flag is set, then the operand's
  * memory faults (8-byte operands, no alignment check). ModRM's mm fields
  * ignore REX. maskmovq, the SSSE3 (0f 38 / 0f 3a) and the floating-point
  * MMX forms are UNIMPLEMENTED; 0f 6c / 6d / d0 / d6 / e6 / f0 without a prefix
@@ -2734,7 +2734,6 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
       return X_FAULT;
     case 0x05: /* syscall (64-bit; SDM vol. 2B; U16) */
     case 0x07: /* sysretq */
-      if (op == 0x07 && !d->rexw) return X_UNIMPL;
       if (!(m->r.efer & 1)) {
         fault(m, WTFGPU_VEC_UD, 0);
         return X_FAULT;
@@ -2747,6 +2746,7 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
         m->r.seg[WTFGPU_CS].selector = (u16)((m->r.star >> 32) & 0xfffc);
         m->r.seg[WTFGPU_SS].selector = (u16)(m->r.seg[WTFGPU_CS].selector + 8);
       } else {
+        if (cpl(m) == 0 && !d->rexw) return X_UNIMPL; /* sysret to compatibility mode */
         if (cpl(m) != 0 || !is_canonical(m->r.gpr[1])) {
           fault(m, WTFGPU_VEC_GP, 0);
           return X_FAULT;

@@ -176,6 +176,9 @@ U = {  # ring 3, entered through to_user (each ends with int3)
     "u_movfs": "mov fs, r8w\n rdfsbase rax\n int3",
     "u_cpuid": "mov eax, r8d\n cpuid\n int3",
     "u_x87": "fninit\n fnstcw [rdi]\n int3",
+    "u_x87a": "fld1\n fldpi\n faddp\n fild dword ptr [rsi]\n fmul st(0), st(1)\n fstp qword ptr [rdi]\n fistp word ptr [rdi+8]\n"
+              " fnstsw ax\n int3",
+    "u_sysret32": ".byte 0x0f, 0x07\n int3",
     "u_wbinvd": "wbinvd\n int3",
 }
 HANDLER_AT = KCODE + 0x5E00

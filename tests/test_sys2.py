@@ -135,6 +135,17 @@ def test_xsave_header(space):
     assert r["exit"][0] == HLT
 
 
+def test_sysret_forms(space):
+    # ring 3: #GP(0) whatever the operand size; ring 0 without REX.W returns to
+    # compatibility mode, outside the engine (UNIMPLEMENTED)
+    assert _one(space, "u_sysret32")["exit"][:3] == (FAULT, 13, 0)
+
+
+def test_x87_arithmetic_in_a_program(space):
+    r = _one(space, "u_x87a", rdi=S.DATA + 0x40, rsi=S.DATA + 0x100)
+    assert r["exit"][0] == INT3 and r["gpr"][0] & 0x3800 == 0
+
+
 def test_ud_opcodes(space):
     for n in ("ud_evex", "ud_0f", "ud_b9", "ud_0e", "ud_xbegin", "ud_8f", "ud_fe", "ud_jmpe", "ud_getsec", "movcs"):
         assert _one(space, n)["exit"][:2] == (FAULT, 6), n

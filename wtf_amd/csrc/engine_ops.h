@@ -519,13 +519,13 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
     if (u.op == O_BSF && u.rep == 0xf3) u.op = O_TZCNT;
     if (u.op == O_BSR && u.rep == 0xf3) u.op = O_LZCNT;
     if (u.op == O_SYS) {
-      // 0 syscall, 1 sysret (64-bit form only), 2 swapgs (0f 01 f8), 3 rdrand r (0f c7 /6),
+      // 0 syscall, 1 sysret (its checks; the return to compatibility mode without REX.W is
+      // outside), 2 swapgs (0f 01 f8), 3 rdrand r (0f c7 /6),
       // 4 mov r64, crN (0f 20 /r), 6 mov crN, r64 (0f 22 /r), 7 wrmsr, 8 rdtsc, 9 rdmsr,
       // 10 rdtscp (0f 01 f9)
       u.sub = c == 0x05 ? 0 : c == 0x07 ? 1 : c == 0x01 ? 2 : c == 0x20 ? 4 : c == 0x22 ? 6 : c == 0x30 ? 7
               : c == 0x31 ? 8 : c == 0x32 ? 9 : 3;
       if ((c == 0x20 || c == 0x22) && u.is_mem) u.op = O_UNIMPL;
-      if (c == 0x07 && !rexw) u.op = O_UNIMPL;
       if (c == 0x01 && (u.rm & 7) == 1) u.sub = 10;
       // the rest of groups 7 and 9 (rdrand / rdseed r stay here): engine_sys.h
       if ((c == 0x01 && (u.is_mem || (u.reg & 7) != 7 || (u.rm & 7) > 1)) ||
@@ -1352,6 +1352,7 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
           set_fault(L, WTFGPU_VEC_GP, 0, 0);
           return X_FAULT;
         }
+        if (!(u.rex & 8)) return X_UNIMPL;  // sysret to compatibility mode
         const u64 target = R(L, 1);
         if (!canonical(target)) {
           set_fault(L, WTFGPU_VEC_GP, 0, 0);

@@ -408,7 +408,7 @@ namespace wtfgpu_dev {
 // The oracle's exec_mmx: mm i is physical x87 register R(i) = fpst[(i - TOS)
 // & 7] (fpst holds ST order); a completed MMX instruction rotates fpst to R
 // order (TOS = 0) and marks every tag valid, emms every tag empty. #UD if
-// CR0.EM, #NM if CR0.TS, #MF if FSW.ES, then the operand's memory faults;
+// CR0.EM, #NM if CR0.TS, #MF if an unmasked x87 flag is set, then the operand's memory faults;
 // nothing is committed before every access succeeded (exec protocol).
 // UOp::opreg bit 20 marks an MMX form (decode).
 constexpr u32 kMmxForm = 1u << 20;
