@@ -29,7 +29,7 @@ UD_REG = {
     0xDE: lambda m: 0xD8 <= m <= 0xDF and m != 0xD9,
     0xDF: lambda m: (0xE1 <= m <= 0xE7) or m >= 0xF8,
 }
-UNIMPL_D9 = {0xF0, 0xF1, 0xF2, 0xF3, 0xF5, 0xF8, 0xF9, 0xFB, 0xFE, 0xFF}
+UNIMPL_D9 = {0xF0, 0xF1, 0xF2, 0xF3, 0xF9, 0xFB, 0xFE, 0xFF}
 CONTROL_REG = {(0xDB, 0xE2), (0xDB, 0xE3), (0xDF, 0xE0)}
 
 

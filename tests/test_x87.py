@@ -107,7 +107,7 @@ X87_FAULT_CASES = [
     ([0xD9, 0x0E], EXIT_FAULT, 6, {}),                        # d9 /1 m: reserved
     ([0xDB, 0x26], EXIT_FAULT, 6, {}),                        # db /4 m: reserved
     ([0xD9, 0xFE], EXIT_UNIMPLEMENTED, None, {}),             # fsin: outside
-    ([0xD9, 0xF8], EXIT_UNIMPLEMENTED, None, {}),             # fprem: outside
+    ([0xD9, 0xFF], EXIT_UNIMPLEMENTED, None, {}),             # fcos: outside
     ([0xDF, 0x26], EXIT_UNIMPLEMENTED, None, {}),             # fbld: outside
     ([0xD8, 0xC1], EXIT_FAULT, 16, dict(fcw=0x37E, fsw=0x8081)),  # pending unmasked IE: #MF
     ([0xD8, 0xC1], EXIT_FAULT, 16, dict(fcw=0x37E, fsw=0x0001)),  # pending even with ES clear

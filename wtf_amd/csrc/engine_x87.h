@@ -85,6 +85,10 @@ __device__ __noinline__ F80 x_round(XEnv &v, u32 s, i32 exp, u128 W, u32 prec) {
   bool wrapped = false;
   if (exp <= 0) {
     const bool tiny = exp < 0 || (W + inc) >= W;  // no carry out of bit 127: still below 2^-16382
+    if (tiny && !(v.masks & SW_UE) && exp + 24576 <= 0) {  // unmasked, beyond the wrap: a zero
+      v.fl |= SW_UE | SW_PE;
+      return x_zero(s);
+    }
     if (tiny && !(v.masks & SW_UE)) {  // unmasked: the exponent wrapped into range
       exp += 24576;
       v.fl |= SW_UE;
@@ -107,7 +111,7 @@ __device__ __noinline__ F80 x_round(XEnv &v, u32 s, i32 exp, u128 W, u32 prec) {
     }
   }
   if (!wrapped && (exp >= 0x7fff || (exp == 0x7ffe && (W + inc) < W))) {
-    if (!(v.masks & SW_OE)) {
+    if (!(v.masks & SW_OE) && exp - 24576 < 0x7fff) {
       exp -= 24576;
       v.fl |= SW_OE;
     } else {
@@ -609,6 +613,81 @@ __device__ __noinline__ F80 x_fscale(XEnv &v, F80 a, F80 b) {
   return x_scale(v, a, b);
 }
 
+// ---------------------------------------------------------------- FPREM / FPREM1
+// ST0 - q * ST1, exact; q truncated (fprem) or to nearest even (fprem1). With
+// an exponent difference D >= 64 the reduction is partial: q's top N bits,
+// q * 2^(D - N) with N = 32 + D mod 32 (the host's choice; C2 = 1). cc: raw
+// C3 (2) C2 (4) C0 (1) with C0 = q bit 2, C3 = q bit 1, C1 = q bit 0;
+// kPremC2Only: C2 = 0, C0 / C3 kept.
+constexpr u32 kPremC2Only = 0x100;
+__device__ __noinline__ F80 x_fprem(XEnv &v, F80 a, F80 b, bool near, u32 &cc) {
+  const u32 ca = x_class(a), cb = x_class(b);
+  cc = kPremC2Only;
+  v.c1 = 0;
+  if (ca == XC_UNSUP || cb == XC_UNSUP) {
+    v.fl |= SW_IE;
+    return x_indef();
+  }
+  if (x_nan(ca) || x_nan(cb)) return x_nan2(v, a, ca, b, cb);
+  if (ca == XC_INF || cb == XC_ZERO) {  // IE alone, beside a denormal too
+    v.fl |= SW_IE;
+    return x_indef();
+  }
+  if (ca == XC_DEN || cb == XC_DEN) v.fl |= SW_DE;
+  cc = 0;
+  if (ca == XC_ZERO) return a;
+  i32 ea, eb;
+  u64 ma, mb;
+  x_unpack(a, ea, ma);
+  u32 s = x_sign(a);
+  // q = 0: a itself (a pseudo-denormal comes back with exponent 1)
+  const F80 a1 = (x_exp(a) == 0 && (a.m >> 63)) ? F80{a.m, a.se | 1} : a;
+  if (cb == XC_INF) return a1;
+  x_unpack(b, eb, mb);
+  const i32 D = ea - eb;
+  if (D < -1 || (D == -1 && !near)) return x_round(v, s, ea, (u128)ma << 64, 64);  // tiny: UE rules
+  const bool partial = D >= 64;
+  const i32 steps = partial ? 32 + (D & 31) : D;  // quotient bits below the top one
+  // long division of ma by mb at the scale of mb * 2^(D - steps)
+  u128 r = ma;
+  u64 q = 0;
+  if (D >= 0) {
+    for (i32 i = steps; i >= 0; i--) {
+      q <<= 1;
+      if (r >= mb) {
+        r -= mb;
+        q |= 1;
+      }
+      if (i) r <<= 1;
+    }
+  }
+  // r < mb: the remainder is r * 2^(eb + D - steps - 63) (D >= 0), or a itself (D = -1)
+  i32 re = D >= 0 ? eb + D - steps : ea;
+  if (near && !partial) {
+    // compare 2r with mb at the same scale (D = -1: r = ma at 2^(ea), mb at 2^(ea + 1))
+    const u128 twice = D >= 0 ? r << 1 : r;
+    if (twice > mb || (twice == mb && (q & 1))) {
+      q++;
+      r = (D >= 0 ? (u128)mb : (u128)mb << 1) - (D >= 0 ? r : r);
+      if (D < 0) re = ea;  // |b| - |a| at a's scale: (2 mb - ma) * 2^(ea - 63)
+      s ^= 1;
+    }
+  }
+  if (partial) cc = 4;
+  else {
+    cc = ((q >> 2) & 1) | (((q >> 1) & 1) << 1);
+    v.c1 = q & 1;
+  }
+  if (r == 0) return x_zero(x_sign(a) ^ 0);
+  // normalise r (< 2^65) to bit 127 and round (exact; only a tiny result can raise UE)
+  const u32 lz = (u64)(r >> 64) ? (u32)__builtin_clzll((u64)(r >> 64)) : 64 + (u32)__builtin_clzll((u64)r);
+  const u128 W = r << lz;
+  XEnv w = v;
+  const F80 res = x_round(w, s, re + 127 - (i32)lz - 63 + 0, W, 64);
+  v.fl = w.fl;
+  return res;
+}
+
 // ---------------------------------------------------------------- memory operands
 enum : u32 { XM_NONE, XM_F32, XM_F64, XM_F80, XM_I16, XM_I32, XM_I64 };
 __device__ __forceinline__ u32 xm_bytes(u32 k) {
@@ -678,9 +757,9 @@ __device__ __noinline__ int x87_arith(const Dev &P, Lane &L, const UOp &u, u64 v
     bool ud = false;
     switch (op) {
       case 0xd9:
-        if (modrm >= 0xf0 && !(modrm == 0xf4 || modrm == 0xf6 || modrm == 0xf7 || modrm == 0xfa || modrm == 0xfc ||
-                               modrm == 0xfd))
-          return X_UNIMPL;  // transcendental, fprem, fprem1
+        if (modrm >= 0xf0 && !(modrm == 0xf4 || modrm == 0xf5 || modrm == 0xf6 || modrm == 0xf7 || modrm == 0xf8 ||
+                               modrm == 0xfa || modrm == 0xfc || modrm == 0xfd))
+          return X_UNIMPL;  // transcendental
         ud = (modrm >= 0xd1 && modrm <= 0xd7) || modrm == 0xe2 || modrm == 0xe3 || modrm == 0xe6 || modrm == 0xe7 ||
              modrm == 0xef;
         break;
@@ -949,8 +1028,9 @@ __device__ __noinline__ int x87_arith(const Dev &P, Lane &L, const UOp &u, u64 v
       v.c1 = x_sign(a);
     } else {
       // the one-operand ST0 forms: fchs fabs ftst fxtract fsqrt frndint fscale
-      if (st_empty(F, 0) || (modrm == 0xfd && st_empty(F, 1))) {
+      if (st_empty(F, 0) || ((modrm == 0xfd || modrm == 0xf5 || modrm == 0xf8) && st_empty(F, 1))) {
         underflow();
+        if (modrm == 0xf5 || modrm == 0xf8) cc = 0x40000000u;  // fprem: C2 = 0
         if (modrm == 0xe4) cc = 3;
         else if (!suppress) {
           st_wr(F, 0, x_indef());
@@ -1003,6 +1083,14 @@ __device__ __noinline__ int x87_arith(const Dev &P, Lane &L, const UOp &u, u64 v
             if (!pre_unmasked()) st_wr(F, 0, r);
             break;
           }
+          case 0xf5: case 0xf8: {  // fprem1, fprem
+            u32 qb;
+            const F80 r = x_fprem(v, a, st_rd(F, 1), modrm == 0xf5, qb);
+            cc = (qb & kPremC2Only) ? 0x40000000u : 0x80000000u | qb;
+            if (!pre_unmasked()) st_wr(F, 0, r);
+            else cc = 0x40000000u;  // no result: C2 = 0, C0 / C3 kept
+            break;
+          }
           default: {  // fxtract (f4)
             const u32 c = x_class(a);
             F80 sig, ex;
@@ -1043,7 +1131,9 @@ __device__ __noinline__ int x87_arith(const Dev &P, Lane &L, const UOp &u, u64 v
   // status word: sticky flags, C1, condition codes, ES / B
   u32 sw = F.fpsw | (v.fl & 0x7fu);
   if (c1mode == 0) sw = (sw & ~SW_C1) | (v.c1 ? SW_C1 : 0);
-  if (cc != 0xffffffffu) {
+  if (cc == 0x40000000u) {
+    sw &= ~SW_C2;
+  } else if (cc != 0xffffffffu) {
     if (cc & 0x80000000u) {
       sw = (sw & ~(SW_C0 | SW_C2 | SW_C3)) | ((cc & 1) ? SW_C0 : 0) | ((cc & 4) ? SW_C2 : 0) | ((cc & 2) ? SW_C3 : 0);
     } else {
