@@ -288,6 +288,7 @@ static u64 phys_read64(orc_machine *m, u64 pa) {
   return v;
 }
 
+
 int orc_read_phys(orc_machine *m, u64 gpa, void *buf, u64 len) {
   u8 *o = (u8 *)buf;
   while (len) {
@@ -327,6 +328,26 @@ static int cpl(orc_machine *m) { return m->r.seg[WTFGPU_CS].selector & 3; }
 static int is_canonical(u64 va) {
   i64 s = (i64)(va << 16) >> 16;
   return (u64)s == va;
+}
+
+/* would a ring-3 instruction fetch at va translate (present, user,
+ * executable)? SYSRET without REX.W enters compatibility mode at ecx: the
+ * oracle runs no 32-bit code, so that SYSRET is UNIMPLEMENTED when the fetch
+ * would succeed, and otherwise its first fetch faults as the host's would (U29) */
+static int user_fetch_ok(orc_machine *m, u64 va) {
+  if (!is_canonical(va)) return 0;
+  const int nxe = (m->r.efer >> 11) & 1;
+  u64 table = m->r.cr3 & 0x000ffffffffff000ULL, e = 0;
+  int u = 1, nx = 0;
+  for (int level = 3; level >= 0; level--) {
+    e = phys_read64(m, table + ((va >> (12 + 9 * level)) & 0x1ff) * 8);
+    if (!(e & 1)) return 0;
+    u &= (e & 4) != 0;
+    if (nxe && (e >> 63)) nx = 1;
+    if (level > 0 && level < 3 && (e & 0x80)) break;
+    table = e & 0x000ffffffffff000ULL;
+  }
+  return u && !nx;
 }
 
 /* 4-level walk; check: perform permission checks. Returns 0 ok, else sets fault. */
@@ -2746,7 +2767,15 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
         m->r.seg[WTFGPU_CS].selector = (u16)((m->r.star >> 32) & 0xfffc);
         m->r.seg[WTFGPU_SS].selector = (u16)(m->r.seg[WTFGPU_CS].selector + 8);
       } else {
-        if (cpl(m) == 0 && !d->rexw) return X_UNIMPL; /* sysret to compatibility mode */
+        if (cpl(m) == 0 && !d->rexw) { /* to compatibility mode (U29): see user_fetch_ok */
+          const u64 t32 = m->r.gpr[1] & 0xffffffffULL;
+          if (user_fetch_ok(m, t32)) return X_UNIMPL;
+          *next_rip = t32;
+          m->r.rflags = (m->r.gpr[11] & 0x3c7fd7ULL) | 2;
+          m->r.seg[WTFGPU_CS].selector = (u16)(((m->r.star >> 48) & 0xffff) | 3);
+          m->r.seg[WTFGPU_SS].selector = (u16)((((m->r.star >> 48) & 0xffff) + 8) | 3);
+          return X_OK;
+        }
         if (cpl(m) != 0 || !is_canonical(m->r.gpr[1])) {
           fault(m, WTFGPU_VEC_GP, 0);
           return X_FAULT;

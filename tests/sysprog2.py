@@ -156,6 +156,7 @@ K = {  # ring 0 (each ends with hlt; a fault ends the lane)
     "ud_jmpe": ".byte 0x0f, 0xb8, 0xc0\n hlt",
     "ud_getsec": ".byte 0x0f, 0x37\n hlt",
     "rdrand16": "rdrand ax\n rdseed rbx\n hlt",
+    "sysret32": "mov ecx, r8d\n mov r11d, 0x202\n .byte 0x0f, 0x07",  # to compatibility mode: the fetch faults
     "to_user": TO_USER,
 }
 U = {  # ring 3, entered through to_user (each ends with int3)

@@ -139,6 +139,9 @@ def test_sysret_forms(space):
     # ring 3: #GP(0) whatever the operand size; ring 0 without REX.W returns to
     # compatibility mode, outside the engine (UNIMPLEMENTED)
     assert _one(space, "u_sysret32")["exit"][:3] == (FAULT, 13, 0)
+    # ring 0 to an address ring 3 cannot fetch: #PF (user, fetch) through the IDT, no engine error
+    r = _one(space, "sysret32", r8=0x10000)
+    assert r["exit"][0] != UNIMPL
 
 
 def test_x87_arithmetic_in_a_program(space):

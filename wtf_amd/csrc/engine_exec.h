@@ -182,6 +182,25 @@ __device__ __forceinline__ bool walk(const Dev &P, Lane &L, u64 va, int acc, u64
   return true;
 }
 
+// Would a ring-3 instruction fetch at va translate (present, user, executable)?
+// No side effects (SYSRET to compatibility mode, U29).
+__device__ __noinline__ bool user_fetch_ok(const Dev &P, const Lane &L, u64 va) {
+  if (!canonical(va)) return false;
+  const bool nxe = (L.efer >> 11) & 1;
+  u64 table = L.cr3 & 0x000ffffffffff000ull;
+  bool u = true, nx = false, priv;
+  for (int level = 3; level >= 0; level--) {
+    const u8 *pg = phys_page(P, L.lane, L.ovn, L.bloom, table >> 12, priv);
+    const u64 e = *(const u64 *)(pg + ((va >> (12 + 9 * level)) & 0x1ff) * 8);
+    if (!(e & 1)) return false;
+    u &= (e & 4) != 0;
+    if (nxe && (e >> 63)) nx = true;
+    if ((level == 2 || level == 1) && (e & 0x80)) break;
+    table = e & 0x000ffffffffff000ull;
+  }
+  return u && !nx;
+}
+
 // Copy-on-write into overlay slot `slot` of `lane`: the page joins the dirty
 // list (bochscpu_backend.cc:887-889 DirtyGpa; dropped again by restore :751-772).
 __device__ __forceinline__ u8 *cow_copy(const Dev &P, u32 lane, u32 slot, u64 gpfn, const u8 *src) {

@@ -519,8 +519,8 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
     if (u.op == O_BSF && u.rep == 0xf3) u.op = O_TZCNT;
     if (u.op == O_BSR && u.rep == 0xf3) u.op = O_LZCNT;
     if (u.op == O_SYS) {
-      // 0 syscall, 1 sysret (its checks; the return to compatibility mode without REX.W is
-      // outside), 2 swapgs (0f 01 f8), 3 rdrand r (0f c7 /6),
+      // 0 syscall, 1 sysret (without REX.W: to compatibility mode, U29), 2 swapgs (0f 01 f8),
+      // 3 rdrand r (0f c7 /6),
       // 4 mov r64, crN (0f 20 /r), 6 mov crN, r64 (0f 22 /r), 7 wrmsr, 8 rdtsc, 9 rdmsr,
       // 10 rdtscp (0f 01 f9)
       u.sub = c == 0x05 ? 0 : c == 0x07 ? 1 : c == 0x01 ? 2 : c == 0x20 ? 4 : c == 0x22 ? 6 : c == 0x30 ? 7
@@ -1352,7 +1352,20 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
           set_fault(L, WTFGPU_VEC_GP, 0, 0);
           return X_FAULT;
         }
-        if (!(u.rex & 8)) return X_UNIMPL;  // sysret to compatibility mode
+        if (!(u.rex & 8)) {
+          // to compatibility mode at ecx: its first fetch faults (#PF through the
+          // IDT, as the host's would) unless ring 3 could fetch there: then
+          // 32-bit code would run, which is outside (U29)
+          const u64 t32 = R(L, 1) & 0xffffffffull;
+          if (user_fetch_ok(P, L, t32)) return X_UNIMPL;
+          fl = (R(L, 11) & 0x3c7fd7ull) | 2;
+          next = t32;
+          L.cpl = S.cpl = 3;
+          S.cs = (u16)(((S.star >> 48) & 0xffff) | 3);
+          S.ss = (u16)((((S.star >> 48) & 0xffff) + 8) | 3);
+          L.flush = 1;
+          break;
+        }
         const u64 target = R(L, 1);
         if (!canonical(target)) {
           set_fault(L, WTFGPU_VEC_GP, 0, 0);

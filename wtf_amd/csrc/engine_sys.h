@@ -555,6 +555,8 @@ __device__ __noinline__ int far_pop(const Dev &P, Lane &L, u32 osz, u64 imm, boo
     if ((nss & 0xfffc) == 0 && ncpl == 3) return fault_x(L, WTFGPU_VEC_GP, 0);
   }
   if (!canonical(f0)) return fault_x(L, WTFGPU_VEC_GP, 0);
+  // back to SYSRET's compatibility-mode selector where ring 3 could fetch: 32-bit code (U29)
+  if (cs == ((((u32)(S.star >> 48)) & 0xffff) | 3) && user_fetch_ok(P, L, f0 & 0xffffffffull)) return X_UNIMPL;
   if (iret) {
     u64 mask = 0x254dd5ull;
     if (ocpl == 0) mask |= 0x200ull | 0x3000ull | 0x80000ull | 0x100000ull;
