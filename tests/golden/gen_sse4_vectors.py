@@ -65,7 +65,7 @@ def gen_forms(rng):
     c, p, s = leg_mem(rng, 1, 0x41, x(), 16, map3=2)
     add(c, "phminposuw.m", p, s)
     # 0f 3a
-    for op, nm in ((0x0E, "pblendw"), (0x0F, "palignr")):
+    for op, nm in ((0x0E, "pblendw"), (0x0F, "palignr"), (0x42, "mpsadbw")):
         for _ in range(3):
             add(leg_rr(1, op, x(), x(), map3=3) + [rng.choice([0, 1, 4, 8, 15, 16, 17, 31, 32, 40, rng.randrange(256)])],
                 nm + ".rr")
@@ -109,7 +109,7 @@ def gen_forms(rng):
         add(vrr(rng, 0x18, x(), 0, x(), l, 1, mmmmm=2), f"vbroadcastss.L{l}.rr")
         c, p, s = vmem(rng, 0x18, x(), 0, l, 1, 1, mmmmm=2)
         add(c, f"vbroadcastss.L{l}.m", p, s)
-        for op, nm in ((0x0E, "vpblendw"), (0x0F, "vpalignr"), (0x02, "vpblendd")):
+        for op, nm in ((0x0E, "vpblendw"), (0x0F, "vpalignr"), (0x02, "vpblendd"), (0x42, "vmpsadbw")):
             add(vrr(rng, op, x(), x(), x(), l, 1, mmmmm=3) + imm(), f"{nm}.L{l}.rr")
         for op, nm in ((0x04, "vpermilps.i"), (0x05, "vpermilpd.i")):
             add(vrr(rng, op, x(), 0, x(), l, 1, mmmmm=3) + imm(), f"{nm}.L{l}.rr")

@@ -96,7 +96,8 @@ def test_sse4_vector_file_is_substantial():
     assert len(DOC["cases"]) > 1900
     for n in ("phaddw", "pmaddubsw", "pabsd", "pmovzx30", "pmovsx25", "pminud", "pmulld", "packusdw", "palignr",
               "pextrd", "pinsrb", "insertps", "movntdqa", "vpermq", "vpermd", "vperm2i128", "vinserti128",
-              "vextracti128", "vpsllv", "vpsrav", "vpblendvb", "vbroadcastss", "vbroadcasti128", "vtestps"):
+              "vextracti128", "vpsllv", "vpsrav", "vpblendvb", "vbroadcastss", "vbroadcasti128", "vtestps",
+              "mpsadbw", "vmpsadbw"):
         assert n in names, n
 
 
@@ -115,7 +116,7 @@ SSE4_FAULT_CASES = [
     ([0xC4, 0xE2, 0x7D, 0x1A, 0xC1], EXIT_FAULT, 6),                # vbroadcastf128 ymm0, xmm1: memory only
     ([0xC4, 0xE2, 0x79, 0x1A, 0x06], EXIT_FAULT, 6),                # vbroadcastf128 with VEX.L = 0
     ([0xC4, 0xE2, 0xF9, 0x46, 0xC1], EXIT_FAULT, 6),                # vpsravq (AVX-512 only): #UD
-    ([0x66, 0x0F, 0x3A, 0x42, 0xC1, 0x00], EXIT_UNIMPLEMENTED, None),  # mpsadbw: outside
+    ([0x66, 0x0F, 0x3A, 0x42, 0x06, 0x00], EXIT_FAULT, 13),          # mpsadbw xmm0, [rsi]: misaligned
     ([0xC4, 0xE2, 0x79, 0x2C, 0x06], EXIT_UNIMPLEMENTED, None),     # vmaskmovps: outside
     ([0x0F, 0x38, 0x00, 0xC1], EXIT_UNIMPLEMENTED, None),           # pshufb mm0, mm1: outside
 ]

@@ -60,7 +60,7 @@ __host__ __device__ inline S4Form s4_desc(u32 map, u32 c, u32 pp, bool vex, u32 
   }
   if (map != 3) return S4Form{0, 0, 0, 0, 0, 0, 0};
   switch (c) {
-    case 0x0e: case 0x0f: return f;  // pblendw, palignr
+    case 0x0e: case 0x0f: case 0x42: return f;  // pblendw, palignr, mpsadbw
     case 0x14: f.shape = S4_B; f.align = 0; f.two = 1; f.l = 1; f.store = 1; return f;  // pextrb
     case 0x15: f.shape = S4_W; f.align = 0; f.two = 1; f.l = 1; f.store = 1; return f;  // pextrw
     case 0x16: f.shape = w ? S4_Q : S4_D; f.align = 0; f.two = 1; f.l = 1; f.store = 1; return f;  // pextrd / q
@@ -312,6 +312,23 @@ __device__ __noinline__ int s4_exec(const Dev &P, Lane &L, const UOp &u, u64 nri
         for (u32 i = 0; i < vl / ew; i++) yset(r, i, ew, ((imm >> (i & 7)) & 1) ? yel(b, i, ew) : yel(a, i, ew));
         break;
       }
+      case 0x42:  // mpsadbw: per lane, 8 sums of 4 absolute byte differences (the upper lane: imm[5:3])
+        for (u32 h = 0; h < vl / 16; h++) {
+          const X128 al = h ? a.h : a.l, bl = h ? b.h : b.l;
+          const u32 im = h ? (imm >> 3) : imm, o1 = ((im >> 2) & 1) * 4, o2 = (im & 3) * 4;
+          X128 o{0, 0};
+          for (u32 j = 0; j < 8; j++) {
+            u32 s = 0;
+            for (u32 k = 0; k < 4; k++) {
+              const i32 d = (i32)xel(al, o1 + j + k, 1) - (i32)xel(bl, o2 + k, 1);
+              s += (u32)(d < 0 ? -d : d);
+            }
+            xset(o, j, 2, s);
+          }
+          if (h) r.h = o;
+          else r.l = o;
+        }
+        break;
       case 0x0f:  // palignr: per lane, (a:b) >> 8 * imm
         for (u32 h = 0; h < vl / 16; h++) {
           const X128 al = h ? a.h : a.l, bl = h ? b.h : b.l;
