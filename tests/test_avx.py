@@ -126,7 +126,8 @@ AVX_FAULT_CASES = [
     ([0xC4, 0xE2, 0x79, 0x1C, 0xC1], RUNNING, None),        # vpabsb (0f 38 1c, U41)
     ([0x66, 0x0F, 0x38, 0x00, 0x06], EXIT_FAULT, 13),      # pshufb xmm0, [rsi]: legacy needs alignment
     ([0x66, 0x0F, 0x38, 0x1C, 0xC1], RUNNING, None),        # pabsb (U41)
-    ([0x66, 0x0F, 0x3A, 0x42, 0xC1, 0x00], EXIT_UNIMPLEMENTED, None),  # mpsadbw (outside)
+    ([0x66, 0x0F, 0x3A, 0x42, 0xC1, 0x00], RUNNING, None),  # mpsadbw (U41)
+    ([0x66, 0x0F, 0x3A, 0x40, 0xC1, 0x00], EXIT_UNIMPLEMENTED, None),  # dpps (outside)
     # U36: encodings the emulated CPU does not define
     ([0xC4, 0x30, 0x02, 0x00], EXIT_FAULT, 6),              # VEX map 0x10 (runaway HEVD bytes)
     ([0xC4, 0xE0, 0x79, 0x58, 0xC1], EXIT_FAULT, 6),        # VEX map 0
