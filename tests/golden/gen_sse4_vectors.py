@@ -117,6 +117,12 @@ def gen_forms(rng):
     for op, nm in ((0x16, "vpermps"), (0x36, "vpermd")):
         add(vrr(rng, op, x(), x(), x(), 1, 1, mmmmm=2), nm + ".rr")
     add(vrr(rng, 0x19, x(), 0, x(), 1, 1, mmmmm=2), "vbroadcastsd.rr")
+    for l in (0, 1):
+        for op, nm, w in ((0x2C, "vmaskmovps", 0), (0x2D, "vmaskmovpd", 0), (0x2E, "vmaskmovps.st", 0),
+                          (0x2F, "vmaskmovpd.st", 0)):
+            for _ in range(2):
+                c, p, s = vmem(rng, op, x(), x(), l, 1, 1, mmmmm=2, w=w)
+                add(c, f"{nm}.L{l}.m", p, s)
     for op, nm in ((0x1A, "vbroadcastf128"), (0x5A, "vbroadcasti128")):
         c, p, s = vmem(rng, op, x(), 0, 1, 1, 1, mmmmm=2)
         add(c, nm + ".m", p, s)

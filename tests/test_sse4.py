@@ -97,7 +97,7 @@ def test_sse4_vector_file_is_substantial():
     for n in ("phaddw", "pmaddubsw", "pabsd", "pmovzx30", "pmovsx25", "pminud", "pmulld", "packusdw", "palignr",
               "pextrd", "pinsrb", "insertps", "movntdqa", "vpermq", "vpermd", "vperm2i128", "vinserti128",
               "vextracti128", "vpsllv", "vpsrav", "vpblendvb", "vbroadcastss", "vbroadcasti128", "vtestps",
-              "mpsadbw", "vmpsadbw"):
+              "mpsadbw", "vmpsadbw", "vmaskmovps", "vmaskmovpd"):
         assert n in names, n
 
 
@@ -117,7 +117,9 @@ SSE4_FAULT_CASES = [
     ([0xC4, 0xE2, 0x79, 0x1A, 0x06], EXIT_FAULT, 6),                # vbroadcastf128 with VEX.L = 0
     ([0xC4, 0xE2, 0xF9, 0x46, 0xC1], EXIT_FAULT, 6),                # vpsravq (AVX-512 only): #UD
     ([0x66, 0x0F, 0x3A, 0x42, 0x06, 0x00], EXIT_FAULT, 13),          # mpsadbw xmm0, [rsi]: misaligned
-    ([0xC4, 0xE2, 0x79, 0x2C, 0x06], EXIT_UNIMPLEMENTED, None),     # vmaskmovps: outside
+    ([0xC4, 0xE2, 0x79, 0x2C, 0xC1], EXIT_FAULT, 6),                # vmaskmovps xmm0, xmm0, xmm1: memory only
+    ([0xC4, 0xE2, 0xF9, 0x2C, 0x06], EXIT_FAULT, 6),                # vmaskmovps with VEX.W = 1
+    ([0xC4, 0xE2, 0x79, 0x2C, 0x86, 0x00, 0x40, 0x00, 0x00], RUNNING, None),  # mask 0: no access, no fault
     ([0x0F, 0x38, 0x00, 0xC1], EXIT_UNIMPLEMENTED, None),           # pshufb mm0, mm1: outside
 ]
 

@@ -267,6 +267,16 @@ __device__ __forceinline__ u8 *xlate(Lane &L, u64 va, int acc, u64 *tdo = nullpt
   return (u8 *)(uintptr_t)(td & ~0xfffull) + (va & 0xfff);
 }
 
+// [va, va + n) (n <= 4096) writable and in the lane's overlay: false = a miss
+// (the caller restarts after service_miss) or a fault. Every page passes the
+// write check before any of them is copied (a fault dirties nothing).
+__device__ __forceinline__ bool span_w(Lane &L, u64 va, u32 n) {
+  const u64 last = (va + n - 1) & ~0xfffull;
+  const bool two = ((va ^ (va + n - 1)) >> 12) != 0;
+  if (!xlate(L, va, ACC_WPROBE) || (two && !xlate(L, last, ACC_WPROBE))) return false;
+  return xlate(L, va, ACC_W) && (!two || xlate(L, last, ACC_W));
+}
+
 // ------------------------------------------------------------------ Tenet trace
 // (wtfgpu_set_tenet; bochscpu_backend.cc:1215-1323; U38 in DESIGN.md). Per
 // lane a byte stream of 8-byte-aligned entries:

@@ -22,15 +22,6 @@ constexpr u64 XS_SUPPORTED = 0x1f;  // x87, SSE, AVX, BNDREGS, BNDCSR
 
 __device__ __forceinline__ u32 lane_iopl(const Lane &L) { return (u32)(L.rflags >> 12) & 3; }
 
-// [va, va + n) (n <= 4096) writable and in the lane's overlay: false = a miss
-// (the caller restarts after service_miss) or a fault. Every page passes the
-// write check before any of them is copied (a fault dirties nothing).
-__device__ __forceinline__ bool span_w(Lane &L, u64 va, u32 n) {
-  const u64 last = (va + n - 1) & ~0xfffull;
-  const bool two = ((va ^ (va + n - 1)) >> 12) != 0;
-  if (!xlate(L, va, ACC_WPROBE) || (two && !xlate(L, last, ACC_WPROBE))) return false;
-  return xlate(L, va, ACC_W) && (!two || xlate(L, last, ACC_W));
-}
 
 // implicit supervisor access: the walk without permission checks; a
 // non-canonical address or a missing page is #PF(err) at va
