@@ -3268,7 +3268,7 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
       has_modrm = 1;
       imm = 1;
     }
-    if (b >= 0x80 && b <= 0x8f) imm = 4;
+    if (d->opmap == 1 && b >= 0x80 && b <= 0x8f) imm = 4; /* jcc rel32 (0f 38 8x has none) */
     if (d->opmap == 2) has_modrm = 1;
     else if (d->opmap == 3) has_modrm = imm = 1;
     else {

@@ -119,7 +119,8 @@ def gen_forms(rng):
     add(vrr(rng, 0x19, x(), 0, x(), 1, 1, mmmmm=2), "vbroadcastsd.rr")
     for l in (0, 1):
         for op, nm, w in ((0x2C, "vmaskmovps", 0), (0x2D, "vmaskmovpd", 0), (0x2E, "vmaskmovps.st", 0),
-                          (0x2F, "vmaskmovpd.st", 0)):
+                          (0x2F, "vmaskmovpd.st", 0), (0x8C, "vpmaskmovd", 0), (0x8C, "vpmaskmovq", 1),
+                          (0x8E, "vpmaskmovd.st", 0), (0x8E, "vpmaskmovq.st", 1)):
             for _ in range(2):
                 c, p, s = vmem(rng, op, x(), x(), l, 1, 1, mmmmm=2, w=w)
                 add(c, f"{nm}.L{l}.m", p, s)

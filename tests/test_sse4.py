@@ -97,7 +97,7 @@ def test_sse4_vector_file_is_substantial():
     for n in ("phaddw", "pmaddubsw", "pabsd", "pmovzx30", "pmovsx25", "pminud", "pmulld", "packusdw", "palignr",
               "pextrd", "pinsrb", "insertps", "movntdqa", "vpermq", "vpermd", "vperm2i128", "vinserti128",
               "vextracti128", "vpsllv", "vpsrav", "vpblendvb", "vbroadcastss", "vbroadcasti128", "vtestps",
-              "mpsadbw", "vmpsadbw", "vmaskmovps", "vmaskmovpd"):
+              "mpsadbw", "vmpsadbw", "vmaskmovps", "vmaskmovpd", "vpmaskmovq", "vpmaskmovd"):
         assert n in names, n
 
 

@@ -57,6 +57,7 @@ __host__ __device__ inline S4Form s4_desc(u32 map, u32 c, u32 pp, bool vex, u32 
       case 0x2c: case 0x2d: case 0x2e: case 0x2f:                                      // vmaskmovps / pd
         f.memonly = 1;
         return w ? S4Form{0, 0, 0, 0, 0, 0, 0} : f;
+      case 0x8c: case 0x8e: f.memonly = 1; return f;                                   // vpmaskmovd / q
       case 0x46: return w ? S4Form{0, 0, 0, 0, 0, 0, 0} : f;                           // vpsravd
       default: return S4Form{0, 0, 0, 0, 0, 0, 0};
     }
@@ -219,11 +220,11 @@ __device__ __noinline__ int s4_exec(const Dev &P, Lane &L, const UOp &u, u64 nri
   }
   const Y256 s = vex ? ymm_get(P, L, u.reg) : Y256{xmm_get(P, L, u.reg), X128{0, 0}};  // reg operand
   const Y256 a = vex ? ymm_get(P, L, vvvv) : s;                                         // first source
-  // ---- vmaskmovps / pd: only the elements whose mask (vvvv) sign bit is set
+  // ---- vmaskmovps / pd, vpmaskmovd / q: only the elements whose mask (vvvv) sign bit is set
   // touch memory, so only they fault; a store checks them all before it writes
-  if (map == 2 && c >= 0x2c && c <= 0x2f) {
-    const u32 ew = (c == 0x2d || c == 0x2f) ? 8 : 4, ne = vl / ew;
-    if (c == 0x2e || c == 0x2f) {
+  if (map == 2 && ((c >= 0x2c && c <= 0x2f) || c == 0x8c || c == 0x8e)) {
+    const u32 ew = (c == 0x2d || c == 0x2f || (c >= 0x8c && W)) ? 8 : 4, ne = vl / ew;
+    if (c == 0x2e || c == 0x2f || c == 0x8e) {
       for (u32 i = 0; i < ne; i++)
         if ((yel(a, i, ew) >> (8 * ew - 1)) && !span_w(L, ea + i * ew, ew)) return X_FAULT;
       for (u32 i = 0; i < ne; i++)
