@@ -194,7 +194,11 @@ int wtfgpu_set_breakpoints(wtfgpu_ctx *ctx, const uint64_t *gvas, uint32_t n);
  * runs. Actions apply only at gvas also passed to wtfgpu_set_breakpoints. */
 enum wtfgpu_bp_action_kind {
   WTFGPU_BPACT_HOST = 0,           /* exit to the host (default) */
-  WTFGPU_BPACT_RETURN = 1,         /* rax = value; rip = [rsp]; rsp += 8 */
+  /* rax = value; rip = [rsp]; rsp += 8. gprs[0] != 0: the handler first reads
+   * a C string at gpr[gprs[0] - 1] (at most gprs[1] bytes, VirtReadString):
+   * a byte before its terminator that does not translate leaves the hit to
+   * the host handler. */
+  WTFGPU_BPACT_RETURN = 1,
   WTFGPU_BPACT_SET_GPRS = 2,       /* gprs[0..15] (WTFGPU_RAX order), rip = gprs[16] */
   /* Pop the lane's next feed chunk (wtfgpu_set_feed): none left, or a chunk of
    * `value` bytes or more -> the lane stops with WTFGPU_EXIT_STOP_OK; else the

@@ -132,7 +132,14 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
           if (it != bps_.end()) handler = it->second;
         }
         inject_ = ~0ull;
-        if (handler) handler(this);
+        try {
+          if (handler) handler(this);
+        } catch (const HandlerFault_t &) {  // U43: the handler ends at the failed access, the testcase as an engine error
+          flush();
+          result_ = Crash_t();
+          engine_error_ = true;
+          break;
+        }
         flush();
         if (result_) break;
         skip = regs().rip == rip0;  // U10: a moved rip cancels the hooked instruction
@@ -358,7 +365,13 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
       Restore(initial_);
       route_lane_ = (uint32_t)i;
       const Target_t &T = route_ ? route_->TargetOf((uint32_t)i) : Target;
-      if (!T.InsertTestcase(Tc[i].first, Tc[i].second)) result_ = Crash_t("insert-testcase-failed");
+      bool inserted = false;
+      try {
+        inserted = T.InsertTestcase(Tc[i].first, Tc[i].second);
+      } catch (const HandlerFault_t &) {  // U43
+        engine_error_ = true;
+      }
+      if (!inserted) result_ = Crash_t(engine_error_ ? "" : "insert-testcase-failed");
       std::optional<TestcaseResult_t> R;
       if (result_) {
         R = result_;
@@ -368,6 +381,7 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
       }
       L.result = *R;
       L.error = engine_error_;
+      if (L.error) L.result = Crash_t();
       engine_error_ = false;
       if (std::holds_alternative<Timedout_t>(*R)) {
         L.new_coverage.assign(0, 0);

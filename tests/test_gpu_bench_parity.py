@@ -1,5 +1,6 @@
 """Parity at the configurations as benchmarked (bench.py): `wtfgpu fuzz` at
-131,072 lanes per GPU with the bench's scheduling (two pipelined halves,
+the bench's lane counts (tlv 262,144 lanes per GPU, the headline; HEVD
+131,072) with the bench's scheduling (two pipelined halves,
 4096-wave-step slices, regrouping every 1024 wave-steps, mutation in parallel
 chunks) records every k-th testcase it accounted (--sample: the testcase
 bytes, result, crash name, retired count, final GPRs and the coverage it
@@ -7,9 +8,19 @@ reported as new); each sampled testcase is then replayed alone through the
 oracle twin (`wtf_twin run`, one testcase after the other like the reference
 client) and must end identically: result, crash name, retired count, GPRs,
 rip and rflags, and every rip the GPU reported must be in the twin's set.
-tlv_server at --limit 100000 and HEVD at --limit 10000000."""
+tlv_server at --limit 100000 and HEVD at --limit 10000000.
+
+Engine errors are replayed too: every testcase the node kept under errors/
+must be an engine error on the twin as well (a handler whose guest access
+does not translate, U43, is the guest's doing; an opcode outside the engine
+would be the engine's, and is one on the twin too).
+
+Reproducibility (U44): the same fixed-seed `--runs` campaign twice at the
+headline lane count gives the same summary, the same crash names and the same
+corpus."""
 import json
 import os
+import shutil
 
 import pytest
 
@@ -17,16 +28,32 @@ from tests import tlv_harness as H
 
 pytestmark = pytest.mark.gpu
 
-LANES = 131072
+TLV_LANES = 262144  # bench.py's headline leg
+HEVD_LANES = 131072  # bench.py's hevd leg
 
 
-def _sample_and_replay(tmp, target, name, runs, every, limit, max_len):
+def _replay_errors(tmp, target, name, limit):
+    """Every testcase kept under errors/ is an engine error on the twin too."""
+    err = os.path.join(target, "errors")
+    if not os.path.isdir(err) or not os.listdir(err):
+        return 0
+    want = H.run(H.TWIN, target, err, os.path.join(tmp, "twin_errors.jsonl"), lanes=1024, limit=limit, name=name,
+                 timeout=900)
+    bad = [w["input"] for w in want if not w["error"]]
+    assert not bad, f"{len(bad)} of {len(want)} GPU engine errors are not errors on the twin: {bad[:5]}"
+    return len(want)
+
+
+def _sample_and_replay(tmp, target, name, runs, every, limit, max_len, lanes):
     sample = os.path.join(tmp, "sample.jsonl")
-    st = H.fuzz(H.WTFGPU, target, runs=runs, lanes=LANES, name=name, limit=limit, max_len=max_len,
+    st = H.fuzz(H.WTFGPU, target, runs=runs, lanes=lanes, name=name, limit=limit, max_len=max_len,
                 extra=("--sample", sample, "--sample-every", str(every)), timeout=600)
-    # engine errors (opcodes outside the engine, e.g. x87 arithmetic in runaway
-    # HEVD code) stay rare; a sampled one must be an error on the twin too
+    # engine errors stay rare, and none is an opcode outside the engine or a
+    # full overlay; a sampled one must be an error on the twin too
+    b = st["backend"]
     assert st["execs"] == runs and st["errors"] <= runs // 10000, st
+    assert b["err_unimpl"] == 0 and b["err_overlay"] == 0 and b["err_other"] == 0, b
+    _replay_errors(tmp, target, name, limit)
     with open(sample) as f:
         got = [json.loads(line) for line in f]
     inp = os.path.join(tmp, "replay")
@@ -51,8 +78,8 @@ def _sample_and_replay(tmp, target, name, runs, every, limit, max_len):
 
 def test_tlv_bench_config_parity(tmp_path):
     target = H.build_target(str(tmp_path / "tlv"))
-    got = _sample_and_replay(str(tmp_path), target, "tlv_server", runs=655360, every=128, limit=100000,
-                             max_len=0x1000)
+    got = _sample_and_replay(str(tmp_path), target, "tlv_server", runs=5 * TLV_LANES, every=256, limit=100000,
+                             max_len=0x1000, lanes=TLV_LANES)
     assert len(got) >= 4096
     assert sum(g["result"] == "crash" for g in got) > 10 and sum(g["result"] == "ok" for g in got) > 100
 
@@ -60,6 +87,29 @@ def test_tlv_bench_config_parity(tmp_path):
 def test_hevd_bench_config_parity(tmp_path):
     target = H.build_hevd_target(str(tmp_path / "hevd"))
     got = _sample_and_replay(str(tmp_path), target, "hevd", runs=655360, every=128, limit=10_000_000,
-                             max_len=1028)
+                             max_len=1028, lanes=HEVD_LANES)
     assert len(got) >= 4096
     assert {g["result"] for g in got} >= {"ok", "crash"}
+
+
+_SAME = ("execs", "retired", "coverage", "corpus", "crashes", "unique_crashes", "timeouts", "cr3", "errors")
+
+
+def test_tlv_fixed_seed_campaign_reproduces(tmp_path):
+    """U44: two runs of the same `wtfgpu fuzz --seed 1337 --runs N` at the
+    headline lane count agree on every count, every crash name and every
+    corpus entry (slices end after a fixed number of wave-steps whichever
+    path ran each group; coverage is attributed in lane order on the host)."""
+    base = H.build_target(str(tmp_path / "tlv"))
+    runs = 6 * TLV_LANES
+    out = []
+    for k in (1, 2):
+        t = str(tmp_path / f"tlv{k}")
+        shutil.copytree(base, t)
+        st = H.fuzz(H.WTFGPU, t, runs=runs, lanes=TLV_LANES, name="tlv_server", limit=100000, timeout=600)
+        out.append((st, sorted(os.listdir(os.path.join(t, "crashes"))), sorted(os.listdir(os.path.join(t, "outputs")))))
+    (a, ca, oa), (b, cb, ob) = out
+    assert a["execs"] == runs
+    assert {k: a[k] for k in _SAME} == {k: b[k] for k in _SAME}
+    assert a["backend"]["group_steps"] == b["backend"]["group_steps"]
+    assert ca == cb and oa == ob

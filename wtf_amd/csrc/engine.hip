@@ -792,6 +792,27 @@ __device__ __forceinline__ bool bp_apply_action(const Dev &P, Lane &L, u64 grip)
     return true;
   }
   if (a.kind != WTFGPU_BPACT_RETURN) return false;
+  if (a.gprs[0]) {
+    // the handler first reads a C string at gpr[gprs[0] - 1], at most gprs[1]
+    // bytes (VirtReadString, backend.h:333-430): a byte that does not
+    // translate before the terminator leaves the hit to the host handler,
+    // whose read then decides (U43)
+    const u64 s = R(L, (u32)(a.gprs[0] - 1) & 15);
+    for (u64 i = 0; i < a.gprs[1]; i++) {
+      u64 c = 0;
+      for (int attempt = 0;; attempt++) {
+        L.miss = 0;
+        if (vread(L, s + i, 1, c)) break;
+        if (L.status != WTFGPU_RUNNING || !L.miss || !miss_service(P, L, attempt)) {
+          L.status = WTFGPU_RUNNING;  // undo a fault: the host handler decides
+          L.miss = 0;
+          L.pend = 0;
+          return false;
+        }
+      }
+      if ((c & 0xff) == 0) break;
+    }
+  }
   const u64 rsp = R(L, WTFGPU_RSP);
   u64 ra = 0;
   for (int attempt = 0;; attempt++) {
@@ -1120,9 +1141,14 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
           if (P.limit && L.icount > P.limit) L.status = WTFGPU_EXIT_TIMEOUT;
         }
       }
-      // lanes that missed keep their rip: the slow step services them
+      // lanes that missed keep their rip: the slow step services them. The
+      // attempt is not a wave-step of its own (the slow step counts the
+      // group once): a slice's length in wave-steps must not depend on which
+      // path ran a group, since that depends on when other queues' coverage
+      // commits landed (U44: fixed-seed campaigns reproduce)
       if (__ballot(ing && L.miss)) {
         WHY(0);
+        steps--;
         have = true;
         break;
       }

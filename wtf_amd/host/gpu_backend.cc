@@ -115,6 +115,7 @@ void GpuBackend_t::reset_view(uint32_t lane) {
   v.cr_known = 3;
   v.cr_dirty = 0;
   v.result.reset();
+  v.handler_fault = false;
   v.seed = initial_.Seed;  // Rdrand seed (bochscpu_backend.cc:1030)
   v.has_feed = false;
   v.feed.clear();
@@ -203,6 +204,12 @@ bool GpuBackend_t::SetBreakpoint(const Gva_t Gva, const BreakpointHandler_t Hand
   if (Action.Kind == BreakpointAction_t::Kind_t::SimulateReturn) {
     A.kind = WTFGPU_BPACT_RETURN;
     A.value = Action.Return;
+    if (Action.StringReg >= 0) {
+      const int g = gpr_index((Registers_t)Action.StringReg);
+      if (g < 0) return false;
+      A.gprs[0] = (uint64_t)g + 1;
+      A.gprs[1] = Action.StringMax;
+    }
   } else if (Action.Kind == BreakpointAction_t::Kind_t::Feed) {
     A.kind = WTFGPU_BPACT_FEED;
     A.value = Action.Return;
@@ -667,19 +674,13 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
 }
 
 // One round's exits: each pending lane that is not done is classified (a
-// result, or a breakpoint hit for the host, or still running). false: a
-// device Feed action could not write its chunk; the module's handler would
-// std::abort() on that failed VirtWriteDirty (fuzzer_tlv_server.cc:130-158),
-// the backend fails the run instead (RunBatch / Run return an error).
+// result, or a breakpoint hit for the host, or still running). A device Feed
+// action that could not write its chunk (WTFGPU_EXIT_FEED_FAULT) is the
+// module handler's failed VirtWriteDirty (fuzzer_tlv_server.cc:130-158): a
+// handler fault, the testcase an engine error (U43).
 bool GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first, const std::vector<wtfgpu_exit_t> &ex,
                             std::vector<uint8_t> &done, std::vector<LaneResult> *out, std::vector<uint32_t> &hits) {
   std::vector<uint8_t> hit(pending.size(), 0);
-  for (uint32_t l : pending)
-    if (!done[l - first] && ex[l - first].status == WTFGPU_EXIT_FEED_FAULT) {
-      fprintf(stderr, "VirtWriteDirty failed: the device Feed action of lane %u could not write its chunk (rip %#llx)\n",
-              l, (unsigned long long)ex[l - first].rip);
-      return false;
-    }
   HostPool::Get().For(pending.size(), 1024, [&](size_t pi) {
     const uint32_t l = pending[pi];
     if (done[l - first]) return;
@@ -696,6 +697,7 @@ bool GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first
       case WTFGPU_EXIT_STOPPED: break;
       case WTFGPU_EXIT_STOP_OK: v.result = Ok_t(); break;           // device Feed action: Stop(Ok_t())
       case WTFGPU_EXIT_STOP_ARGS: hit[pi] = 2; return;            // named below from the kept arguments
+      case WTFGPU_EXIT_FEED_FAULT: v.handler_fault = true; break;  // U43: fill_results makes it an engine error
       default:
         // unimplemented opcode / overlay full / a device Feed write that
         // failed: the engine cannot finish the testcase. Not a target bug:
@@ -764,6 +766,11 @@ bool GpuBackend_t::fill_results(const std::vector<uint32_t> &lanes, uint32_t fir
     LaneResult &r = (*out)[fin[i]];
     const LaneView &v = views_[fin[i]];
     r.result = v.result ? std::move(*v.result) : TestcaseResult_t(Ok_t());  // the view is reset at refill
+    if (v.handler_fault) {  // U43: an engine error, never a named crash
+      r.result = Crash_t();
+      r.error = true;
+      stats_.err_handler++;
+    }
     if (want_gprs_) {
       memcpy(r.gprs, &regs[i * 18], 18 * 8);
       r.rip = r.gprs[16];
@@ -893,7 +900,12 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
       if (per_lane_state && slots) slots->SwapIn(l);
       servicing_bp_ = rip0;
       v.inject = ~0ull;
-      if (handler) handler(this);  // BeforeExecutionHook (bochscpu_backend.cc:545-547)
+      try {
+        if (handler) handler(this);  // BeforeExecutionHook (bochscpu_backend.cc:545-547)
+      } catch (const HandlerFault_t &) {  // the reference node stops here (backend.cc:39-42): this lane does
+        v.handler_fault = true;
+        v.result = Crash_t();
+      }
       servicing_bp_ = ~0ull;
       if (per_lane_state && slots) slots->SwapOut(l);
       action[h] = v.result ? 0 : (v.gpr[16] == rip0 ? 2 : 1);  // U10: a moved rip cancels the hooked instruction
@@ -1177,7 +1189,12 @@ void GpuBackend_t::insert_lanes(const Target_t &Target, const std::vector<uint32
       Slots->SwapIn(l);
     }
     const Target_t &T = Slots && Slots->Instances() ? Slots->Instances()->TargetOf(l) : Target;
-    ok[i] = T.InsertTestcase(tcs[i].first, tcs[i].second);
+    try {
+      ok[i] = T.InsertTestcase(tcs[i].first, tcs[i].second);
+    } catch (const HandlerFault_t &) {  // see service_hits
+      views_[l].handler_fault = true;
+      ok[i] = 0;
+    }
     if (Slots) Slots->SwapOut(l);
   };
   if (parallel_service(Slots)) {
@@ -1484,7 +1501,7 @@ std::string GpuBackend_t::StatsJson() const {
            "\"target_restore_ms\":%.3f,\"alg_bytes\":%llu,\"restore_ms\":%.3f,\"module_ms\":%.3f,"
            "\"upload_ms\":%.3f,\"bytes_ms\":%.3f,\"covlog_ms\":%.3f,\"attrib_ms\":%.3f,\"cov_entries\":%llu,"
            "\"run_ms\":%.3f,\"exits_ms\":%.3f,\"regs_ms\":%.3f,\"err_unimpl\":%llu,\"err_overlay\":%llu,"
-           "\"err_other\":%llu,\"last_unimpl_op\":%llu,\"last_unimpl_rip\":%llu}",
+           "\"err_other\":%llu,\"err_handler\":%llu,\"last_unimpl_op\":%llu,\"last_unimpl_rip\":%llu}",
            (unsigned long long)stats_.group_steps, (unsigned long long)stats_.rounds,
            (unsigned long long)stats_.breakpoint_hits, (unsigned long long)stats_.kernel_launches, stats_.kernel_ms,
            stats_.service_ms, stats_.total_ms, (unsigned long long)stats_.page_fetches,
@@ -1495,7 +1512,7 @@ std::string GpuBackend_t::StatsJson() const {
            stats_.bytes_ms, stats_.covlog_ms, stats_.attrib_ms, (unsigned long long)stats_.cov_entries,
            stats_.run_ms, stats_.exits_ms, stats_.regs_ms, (unsigned long long)stats_.err_unimpl.load(),
            (unsigned long long)stats_.err_overlay.load(), (unsigned long long)stats_.err_other.load(),
-           (unsigned long long)stats_.last_unimpl_op.load(), (unsigned long long)stats_.last_unimpl_rip.load());
+           (unsigned long long)stats_.err_handler.load(), (unsigned long long)stats_.last_unimpl_op.load(), (unsigned long long)stats_.last_unimpl_rip.load());
   std::string r(b);
   r.pop_back();
   snprintf(b, sizeof(b), ",\"up_prep_ms\":%.3f,\"up_regs_ms\":%.3f,\"up_apply_ms\":%.3f,\"up_feed_ms\":%.3f,"

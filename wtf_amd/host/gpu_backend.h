@@ -54,7 +54,7 @@ struct BatchStats {
   // run loop split: wtfgpu_run wall (launches + syncs), exit read-back + classification, final registers
   double run_ms = 0, exits_ms = 0, regs_ms = 0;
   // engine errors by exit status, the last unimplemented opcode and its rip
-  std::atomic<uint64_t> err_unimpl{0}, err_overlay{0}, err_other{0};
+  std::atomic<uint64_t> err_unimpl{0}, err_overlay{0}, err_other{0}, err_handler{0};
   UnimplHist unimpl_ops;  // opcode histogram of the UNIMPLEMENTED exits
   std::atomic<uint64_t> last_unimpl_op{0}, last_unimpl_rip{0};
 };
@@ -147,6 +147,9 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
     uint64_t cr[2] = {};
     uint8_t cr_known = 0, cr_dirty = 0;
     std::optional<TestcaseResult_t> result;
+    // a handler or InsertTestcase access did not translate (HandlerFault_t):
+    // the testcase ends as an engine error (DESIGN U43)
+    bool handler_fault = false;
     uint64_t seed = 0;
     uint64_t inject = ~0ull;  // PageFaultsMemoryIfNeeded: page to #PF after the handler
     bool has_feed = false;    // SetFeed: chunks for the device Feed action

@@ -72,7 +72,7 @@ bool Init(const Options_t &, const CpuState_t &) {
         (void)Format;
         Backend->SimulateReturnFromFunction(0);
       },
-      BreakpointAction_t::SimulateReturn(0)))  // device-side on the gpu backend
+      BreakpointAction_t::SimulateReturn(0).AfterReadingString(Registers_t::R8)))  // device-side on the gpu backend
     return false;
   const Gva_t ExGenRandom = Gva_t(g_Dbg.GetSymbol("nt!ExGenRandom") + 0xe0 + 4);
   if (g_Backend->VirtRead4(ExGenRandom - Gva_t(4)) != 0xf2c70f48) {

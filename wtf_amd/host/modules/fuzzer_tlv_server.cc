@@ -413,7 +413,7 @@ bool Init(const Options_t &, const CpuState_t &State) {
         (void)Format;
         Backend->SimulateReturnFromFunction(0);
       },
-      BreakpointAction_t::SimulateReturn(0))) {
+      BreakpointAction_t::SimulateReturn(0).AfterReadingString(Registers_t::Rcx))) {
     printf("Failed to SetBreakpoint on printf\n");
     return false;
   }

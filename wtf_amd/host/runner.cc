@@ -386,8 +386,14 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
         g_Backend = B;
         const std::vector<uint8_t> Buf = ReadFile(In);
         LaneResult L;
-        if (!Target->InsertTestcase(Buf.data(), Buf.size())) {
-          L.result = Crash_t("insert-testcase-failed");
+        bool Inserted = false;
+        try {
+          Inserted = Target->InsertTestcase(Buf.data(), Buf.size());
+        } catch (const HandlerFault_t &) {  // U43: an engine error for this testcase
+          L.error = true;
+        }
+        if (!Inserted) {
+          L.result = L.error ? Crash_t() : Crash_t("insert-testcase-failed");
         } else {
           const std::optional<TestcaseResult_t> Res = B->Run(Buf.data(), Buf.size());
           if (!Res) {  // client.cc:112-115: a backend failure ends the client

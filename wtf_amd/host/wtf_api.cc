@@ -31,15 +31,20 @@ bool Backend_t::PhysWrite(const Gpa_t Gpa, const uint8_t *Buffer, const uint64_t
   return true;
 }
 
-// backend.cc:30-56: page-chunked translate + copy; a failed translation is fatal
+// A failed translation under a helper: the reference's __debugbreak
+// (backend.cc:39-42), here the end of the calling handler (HandlerFault_t).
+[[noreturn]] static void handler_fault(const uint64_t Gva) {
+  printf("Translation of GVA %#llx failed\n", (unsigned long long)Gva);
+  throw HandlerFault_t{Gva};
+}
+
+// backend.cc:30-56: page-chunked translate + copy; a failed translation ends
+// the handler (HandlerFault_t), it never returns false
 bool Backend_t::VirtRead(const Gva_t Gva, uint8_t *Buffer, const uint64_t BufferSize) const {
   uint64_t Left = BufferSize, Cur = Gva.U64();
   while (Left) {
     Gpa_t Gpa;
-    if (!VirtTranslate(Gva_t(Cur), Gpa, MemoryValidate_t::ValidateRead)) {
-      printf("Translation of GVA %#llx failed\n", (unsigned long long)Cur);
-      return false;
-    }
+    if (!VirtTranslate(Gva_t(Cur), Gpa, MemoryValidate_t::ValidateRead)) handler_fault(Cur);
     const uint64_t Chunk = std::min<uint64_t>(Left, Page::Size - (Cur & 0xfff));
     if (!PhysReadDirect(Gpa, Buffer, Chunk)) {
       const uint8_t *Hva = PhysTranslate(Gpa);
@@ -66,14 +71,16 @@ uint64_t Backend_t::VirtRead8(const Gva_t Gva) const {
 Gva_t Backend_t::VirtReadGva(const Gva_t Gva) const { return Gva_t(VirtRead8(Gva)); }
 Gpa_t Backend_t::VirtReadGpa(const Gva_t Gva) const { return Gpa_t(VirtRead8(Gva)); }
 
-// backend.h:281-330: read up to MaxLength bytes, stop at the terminator
+// backend.h:333-430: read up to MaxLength bytes, stop at the terminator; a
+// page the string reaches that does not translate ends the handler
+// (:352-356, HandlerFault_t)
 template <typename Ch>
 static std::basic_string<Ch> read_cstring(const Backend_t *B, const Gva_t Gva, const uint64_t MaxLength) {
   std::basic_string<Ch> S;
   uint64_t Cur = Gva.U64();
   for (uint64_t i = 0; i + sizeof(Ch) <= MaxLength; i += sizeof(Ch), Cur += sizeof(Ch)) {
     Ch C = 0;
-    if (!B->VirtRead(Gva_t(Cur), (uint8_t *)&C, sizeof(Ch))) break;
+    if (!B->VirtRead(Gva_t(Cur), (uint8_t *)&C, sizeof(Ch))) break;  // PhysTranslate failed (no frame)
     if (C == 0) break;
     S.push_back(C);
   }
@@ -91,10 +98,7 @@ bool Backend_t::VirtWrite(const Gva_t Gva, const uint8_t *Buffer, const uint64_t
   uint64_t Left = BufferSize, Cur = Gva.U64();
   while (Left) {
     Gpa_t Gpa;
-    if (!VirtTranslate(Gva_t(Cur), Gpa, MemoryValidate_t::ValidateRead)) {
-      printf("Translation of GVA %#llx failed\n", (unsigned long long)Cur);
-      return false;
-    }
+    if (!VirtTranslate(Gva_t(Cur), Gpa, MemoryValidate_t::ValidateRead)) handler_fault(Cur);
     const uint64_t Chunk = std::min<uint64_t>(Left, Page::Size - (Cur & 0xfff));
     if (!PhysWrite(Gpa, Buffer, Chunk, Dirty)) return false;
     Buffer += Chunk;

@@ -199,6 +199,18 @@ struct Options_t {
 class Backend_t;
 using BreakpointHandler_t = void (*)(Backend_t *);
 
+// A guest access of a handler (VirtRead / VirtWrite / the string readers) whose
+// translation failed. The reference stops the whole node there: it prints the
+// GVA and executes `int3` (__debugbreak, platform.h:35; backend.cc:39-42,
+// 58-72, 101-104; backend.h:352-356). Here the helper throws this instead, and
+// the backend that called the handler (or InsertTestcase) catches it: the
+// handler is abandoned at that access, exactly where the reference stops, and
+// only that testcase ends, as an engine error (DESIGN U43; a batched node must
+// not lose its other lanes to one testcase).
+struct HandlerFault_t {
+  uint64_t Gva;
+};
+
 // What a breakpoint handler does, stated as data (this repository's
 // extension; the reference only has the handler). A backend that can apply it
 // without leaving the execution engine (the gpu backend does it on the device,
@@ -219,6 +231,17 @@ struct BreakpointAction_t {
     A.Return = Value;
     return A;
   }
+  // ... after a VirtReadString(Reg, MaxLength) whose result the handler drops
+  // (tlv printf's format): the read's translations are part of the handler
+  // (a failing one ends the testcase, U43), so the backend checks them too
+  BreakpointAction_t AfterReadingString(const Registers_t Reg, const uint64_t MaxLength = 256) const {
+    BreakpointAction_t A = *this;
+    A.StringReg = (int)Reg;
+    A.StringMax = MaxLength;
+    return A;
+  }
+  int StringReg = -1;  // SimulateReturn: Registers_t of the string read first, -1 none
+  uint64_t StringMax = 0;
   // the 16 GPRs and rip of a CpuState_t (registers only; rflags untouched)
   static BreakpointAction_t SetGprs(const struct CpuState_t &State);
   // pop the testcase's next input chunk (Backend_t::SetFeed): none left, or
