@@ -1447,6 +1447,10 @@ static int fp_form_o(u32 map, u32 c, int pp, int vex); /* x86_oracle_fp.inc */
 static int exec_fp(orc_machine *m, insn *d);
 static int s4_form_o(u32 map, u32 c, int pp, int vex); /* x86_oracle_sse4.inc */
 static int exec_s4(orc_machine *m, insn *d);
+static int gx_form_o(u32 map, u32 c, int pp, int vex); /* x86_oracle_ext.inc */
+static int x42_form_o(u32 map, u32 c, int pp, int vex);
+static int exec_gext(orc_machine *m, insn *d);
+static int exec_x42(orc_machine *m, insn *d);
 
 static int exec_sse(orc_machine *m, insn *d) {
   const u32 op = d->op, r3 = d->reg & 7;
@@ -1458,6 +1462,8 @@ static int exec_sse(orc_machine *m, insn *d) {
   if (d->opmap == 1 && ((pc == 0 && mmx_opcode(op)) || (op == 0xd6 && pc >= 2))) return exec_mmx(m, d, pc);
   if (fp_form_o(d->opmap, op, pc, 0)) return exec_fp(m, d); /* U39 / U40 */
   if (s4_form_o(d->opmap, op, pc, 0)) return exec_s4(m, d); /* U41 */
+  if (gx_form_o(d->opmap, op, pc, 0)) return exec_gext(m, d); /* U45 */
+  if (x42_form_o(d->opmap, op, pc, 0)) return exec_x42(m, d);
   if (d->opmap == 2) { /* 66 0f 38 00 pshufb, 66 0f 38 17 ptest */
     if (pc != 1) return X_UNIMPL;
     if (m->r.cr0 & 4 || !(m->r.cr4 & 0x200)) {
@@ -1800,6 +1806,7 @@ static void yput(orc_machine *m, u32 r, y256 v, int l256) {
 
 #include "x86_oracle_fp.inc" /* SSE / AVX floating point (U39 / U40) */
 #include "x86_oracle_sse4.inc" /* SSSE3 / SSE4.1 integer, AVX2 lane crossing (U41) */
+#include "x86_oracle_ext.inc"  /* BMI1 / BMI2 / ADX / MOVBE / CRC32, SSE4.2, AES, PCLMULQDQ (U45) */
 
 /* two-source ops of one 128-bit lane (the legacy semantics); 0 = not one */
 static int vlane(u32 op, int pc, const x128 *a, const x128 *b, u8 imm, u64 cnt, x128 *r) {
@@ -1917,15 +1924,17 @@ static int vex_valid(u32 map, u32 op, int pp, int mem, u32 r3) {
   return 0;
 }
 
-/* U36: which encodings exist on the emulated CPU (SDM vol. 2 appendix A,
- * restricted to the features leaf 1 / leaf 7 of cpuid_leaf enumerate: SSE,
- * SSE2, SSSE3, SSE4.1, AVX, AVX2). An opcode no such instruction defines, a
- * VEX map other than 0f / 0f 38 / 0f 3a, and the forms of features CPUID does
- * not enumerate (SSE3 and SSE4.2 aside from their VEX forms, FMA, F16C,
- * BMI1/2, ADX, MOVBE, AES, PCLMULQDQ, SHA, VMX, INVPCID, AVX-512 mask ops) are
- * #UD, decided from the opcode byte (no ModRM / immediate fetched). A defined
- * form outside the executed subset stays UNIMPLEMENTED. pp / pfx: 0 none,
- * 1 66, 2 f3, 3 f2. */
+/* U36 / U45: which encodings some x86-64 CPU defines (SDM vol. 2 appendix A
+ * and the extension references). The emulated CPU enumerates and executes
+ * SSE .. SSE4.2, SSSE3, AVX, AVX2, AES, PCLMULQDQ, BMI1 / BMI2, ADX and MOVBE;
+ * the other defined forms (FMA, F16C, AVX-VNNI / -IFMA / -NE-CONVERT /
+ * -VNNI-INT8 / -INT16, GFNI, the 256-bit VAES / VPCLMULQDQ, SHA, CET shadow
+ * stack writes, MOVDIRI / MOVDIR64B, ENQCMD, Key Locker, INVEPT / INVVPID /
+ * INVPCID, EVEX) are UNIMPLEMENTED: a guest chooses its code from the capture
+ * host's CPUID, so such a form is an engine gap, never a crash. An opcode no
+ * CPU assigns, or a VEX map other than 0f / 0f 38 / 0f 3a, is #UD, decided
+ * from the opcode byte (no ModRM / immediate fetched). pp / pfx: 0 none, 1 66,
+ * 2 f3, 3 f2. */
 static int vex_defined(u32 map, u32 op, int pp) {
   if (map == 1) {
     switch (op) {
@@ -1948,28 +1957,59 @@ static int vex_defined(u32 map, u32 op, int pp) {
                          (op >= 0xd1 && op <= 0xfe));
     }
   }
-  if (pp != 1) return 0;
-  if (map == 2)
-    return op <= 0x0f || (op >= 0x16 && op <= 0x1a) || (op >= 0x1c && op <= 0x1e) || (op >= 0x20 && op <= 0x25) ||
-           (op >= 0x28 && op <= 0x41) || (op >= 0x45 && op <= 0x47) || (op >= 0x58 && op <= 0x5a) || op == 0x78 ||
-           op == 0x79 || op == 0x8c || op == 0x8e || (op >= 0x90 && op <= 0x93);
-  if (map == 3)
+  if (map == 2) {
+    switch (op) { /* every prefix: BMI2 / BEXTR (f5 f7), AVX-VNNI-INT8 (50 51), NE-CONVERT (b0), VNNI-INT16 (d2 d3) */
+    case 0xf5: case 0xf7: case 0x50: case 0x51: case 0xb0: case 0xd2: case 0xd3: return 1;
+    case 0xf2: case 0xf3: return pp == 0;             /* andn, group 17 */
+    case 0x72: return pp == 2;                        /* vcvtneps2bf16 */
+    case 0xb1: return pp == 1 || pp == 2;             /* vbcstnesh2ps / vbcstnebf162ps */
+    case 0xf6: return pp == 3;                        /* mulx */
+    default: break;
+    }
+    if (pp != 1) return 0;
+    return op <= 0x0f || op == 0x13 || (op >= 0x16 && op <= 0x1a) || (op >= 0x1c && op <= 0x1e) ||
+           (op >= 0x20 && op <= 0x25) || (op >= 0x28 && op <= 0x41) || (op >= 0x45 && op <= 0x47) || op == 0x52 ||
+           op == 0x53 || (op >= 0x58 && op <= 0x5a) || op == 0x78 || op == 0x79 || op == 0x8c || op == 0x8e ||
+           (op >= 0x90 && op <= 0x93) || (op >= 0x96 && op <= 0x9f) || (op >= 0xa6 && op <= 0xaf) ||
+           (op >= 0xb4 && op <= 0xbf) || op == 0xcf || (op >= 0xdb && op <= 0xdf);
+  }
+  if (map == 3) {
+    if (pp == 3) return op == 0xf0; /* rorx */
+    if (pp != 1) return 0;
     return op == 0x00 || op == 0x01 || op == 0x02 || op == 0x04 || op == 0x05 || op == 0x06 ||
-           (op >= 0x08 && op <= 0x0f) || (op >= 0x14 && op <= 0x19) || (op >= 0x20 && op <= 0x22) || op == 0x38 ||
-           op == 0x39 || (op >= 0x40 && op <= 0x42) || op == 0x46 || (op >= 0x4a && op <= 0x4c) ||
-           (op >= 0x60 && op <= 0x63);
+           (op >= 0x08 && op <= 0x0f) || (op >= 0x14 && op <= 0x19) || op == 0x1d || (op >= 0x20 && op <= 0x22) ||
+           op == 0x38 || op == 0x39 || (op >= 0x40 && op <= 0x42) || op == 0x44 || op == 0x46 ||
+           (op >= 0x4a && op <= 0x4c) || (op >= 0x60 && op <= 0x63) || op == 0xce || op == 0xcf || op == 0xdf;
+  }
   return 0;
 }
 
 /* the legacy (non-VEX) 0f 38 / 0f 3a maps, same rule */
 static int legacy_3byte_defined(u32 map, u32 op, int pfx) {
-  if (map == 2)
+  if (map == 2) {
+    switch (pfx) {
+    case 0: /* sha1 / sha256 (c8-cd), movbe, wrss, movdiri */
+      if ((op >= 0xc8 && op <= 0xcd) || op == 0xf0 || op == 0xf1 || op == 0xf6 || op == 0xf9) return 1;
+      break;
+    case 1: /* pcmpgtq, invept / invvpid / invpcid, gf2p8mulb, aes, movbe r16, wruss, adcx, movdir64b */
+      if (op == 0x37 || (op >= 0x80 && op <= 0x82) || op == 0xcf || (op >= 0xdb && op <= 0xdf) || op == 0xf0 ||
+          op == 0xf1 || op == 0xf5 || op == 0xf6 || op == 0xf8)
+        return 1;
+      break;
+    case 2: /* Key Locker (d8 dc-df), adox, enqcmds */
+      return op == 0xd8 || (op >= 0xdc && op <= 0xdf) || op == 0xf6 || op == 0xf8;
+    default: /* crc32, enqcmd */
+      return op == 0xf0 || op == 0xf1 || op == 0xf8;
+    }
     return ((op <= 0x0b || (op >= 0x1c && op <= 0x1e)) && pfx <= 1) ||
            (pfx == 1 && (op == 0x10 || op == 0x14 || op == 0x15 || op == 0x17 || (op >= 0x20 && op <= 0x25) ||
                          (op >= 0x28 && op <= 0x2b) || (op >= 0x30 && op <= 0x35) || (op >= 0x38 && op <= 0x41)));
+  }
+  if (op == 0xcc) return pfx == 0; /* sha1rnds4 */
   return (op == 0x0f && pfx <= 1) ||
          (pfx == 1 && ((op >= 0x08 && op <= 0x0e) || (op >= 0x14 && op <= 0x17) || (op >= 0x20 && op <= 0x22) ||
-                       (op >= 0x40 && op <= 0x42)));
+                       (op >= 0x40 && op <= 0x42) || op == 0x44 || (op >= 0x60 && op <= 0x63) || op == 0xce ||
+                       op == 0xcf || op == 0xdf));
 }
 
 static int exec_vex(orc_machine *m, insn *d) {
@@ -1978,6 +2018,8 @@ static int exec_vex(orc_machine *m, insn *d) {
   const u8 imm = d->bytes[d->len - 1];
   if (fp_form_o(map, op, pp, 1)) return exec_fp(m, d); /* U39 / U40 */
   if (s4_form_o(map, op, pp, 1)) return exec_s4(m, d); /* U41 */
+  if (gx_form_o(map, op, pp, 1)) return exec_gext(m, d); /* U45 */
+  if (x42_form_o(map, op, pp, 1)) return exec_x42(m, d);
   if (map == 1 && op == 0xae && !(pp == 0 && mem && (r3 == 2 || r3 == 3))) { /* U36: vldmxcsr / vstmxcsr only */
     fault(m, WTFGPU_VEC_UD, 0);
     return X_FAULT;
@@ -2439,7 +2481,8 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
     }
     case 0xc6:
     case 0xc7: {
-      if ((d->reg & 7) != 0) { /* xabort / xbegin (no RTM) and the reserved forms */
+      if ((d->reg & 7) != 0) { /* the reserved forms; xabort / xbegin: RTM, defined, not executed (U45) */
+        if ((d->reg & 7) == 7 && !d->is_mem && (d->rm & 7) == 0) return X_UNIMPL;
         fault(m, WTFGPU_VEC_UD, 0);
         return X_FAULT;
       }
@@ -2518,7 +2561,8 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
     case 0xd5: case 0xd6: case 0xea:
       fault(m, WTFGPU_VEC_UD, 0);
       return X_FAULT;
-    case 0x62: /* EVEX (no AVX-512) */
+    case 0x62: /* EVEX: AVX-512, defined, not executed (U45) */
+      return X_UNIMPL;
     case 0xce: /* into: invalid in 64-bit mode */
       fault(m, WTFGPU_VEC_UD, 0);
       return X_FAULT;
@@ -3158,7 +3202,8 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
     if (d->fetch_fail) return -1;
     d->undef = d->vbad || d->opmap < 1 || d->opmap > 3 || !vex_defined(d->opmap, b, (int)d->vpp);
     if (d->opmap != 1 && d->opmap != 2 &&
-        !(d->opmap == 3 && !d->undef && (fp_form_o(3, b, (int)d->vpp, 1) || s4_form_o(3, b, (int)d->vpp, 1)))) {
+        !(d->opmap == 3 && !d->undef && (fp_form_o(3, b, (int)d->vpp, 1) || s4_form_o(3, b, (int)d->vpp, 1) ||
+                                         x42_form_o(3, b, (int)d->vpp, 1) || gx_form_o(3, b, (int)d->vpp, 1)))) {
       d->op = b;
       d->len = d->pos;
       return 1;
@@ -3179,7 +3224,8 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
       const int pfx = d->rep == 0xf3 ? 2 : d->rep == 0xf2 ? 3 : d->pfx66 ? 1 : 0;
       /* 0f 38 00 pshufb, 0f 38 17 ptest, the floating-point forms; the rest: outside */
       if ((d->opmap == 3 || (d->op != 0x00 && d->op != 0x17)) && !fp_form_o(d->opmap, d->op, pfx, 0) &&
-          !s4_form_o(d->opmap, d->op, pfx, 0)) {
+          !s4_form_o(d->opmap, d->op, pfx, 0) && !x42_form_o(d->opmap, d->op, pfx, 0) &&
+          !gx_form_o(d->opmap, d->op, pfx, 0)) {
         d->undef = !legacy_3byte_defined(d->opmap, d->op, pfx);
         d->len = d->pos;
         return 1;

@@ -431,6 +431,8 @@ def run_native(cases, generator, out_path, mem_writes=False):
         # inputs: the GPRs, RFLAGS, MXCSR; YMM and window from (seed, ew, ints) by case_inputs
         e = {"name": c["name"], "code": c["code"], "in": ["%x" % v for v in inregs], "fl": "%x" % c["flags"],
              "mx": "%x" % c["mx"], "seed": "%x" % c["seed"], "ew": c["ew"], "ints": c["ints"]}
+        if "flm" in c:  # the flags the SDM defines for this form (gen_ext_vectors.py)
+            e["flm"] = c["flm"]
         if out[k].startswith("T"):
             e["trap_mx"] = out[k].split()[1]
             traps += 1

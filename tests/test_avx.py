@@ -128,27 +128,42 @@ AVX_FAULT_CASES = [
     ([0x66, 0x0F, 0x38, 0x1C, 0xC1], RUNNING, None),        # pabsb (U41)
     ([0x66, 0x0F, 0x3A, 0x42, 0xC1, 0x00], RUNNING, None),  # mpsadbw (U41)
     ([0x66, 0x0F, 0x3A, 0x40, 0xC1, 0x00], EXIT_UNIMPLEMENTED, None),  # dpps (outside)
-    # U36: encodings the emulated CPU does not define
+    # U36 / U45: encodings no CPU defines are #UD; defined ones outside the engine are UNIMPLEMENTED
     ([0xC4, 0x30, 0x02, 0x00], EXIT_FAULT, 6),              # VEX map 0x10 (runaway HEVD bytes)
     ([0xC4, 0xE0, 0x79, 0x58, 0xC1], EXIT_FAULT, 6),        # VEX map 0
     ([0xC4, 0xE4, 0x79, 0x58, 0xC1], EXIT_FAULT, 6),        # VEX map 4
     ([0xC5, 0xF8, 0x00, 0xC1], EXIT_FAULT, 6),              # VEX 0f 00: no AVX form
     ([0xC5, 0xF8, 0x60, 0xC1], EXIT_FAULT, 6),              # VEX.NP 0f 60: MMX only
     ([0xC5, 0xFA, 0x14, 0xC1], EXIT_FAULT, 6),              # VEX.F3 0f 14
-    ([0xC4, 0xE2, 0x79, 0xA8, 0xC1], EXIT_FAULT, 6),        # vfmadd213ps: FMA not enumerated
-    ([0xC4, 0xE2, 0x78, 0xF2, 0xC1], EXIT_FAULT, 6),        # andn: BMI1 not enumerated
-    ([0xC4, 0xE2, 0x79, 0x13, 0xC1], EXIT_FAULT, 6),        # vcvtph2ps: F16C not enumerated
-    ([0xC4, 0xE3, 0x79, 0x44, 0xC1, 0x00], EXIT_FAULT, 6),  # vpclmulqdq: PCLMULQDQ not enumerated
-    ([0xC4, 0xE3, 0x7B, 0xF0, 0xC1, 0x01], EXIT_FAULT, 6),  # rorx: BMI2 not enumerated
+    ([0xC4, 0xE2, 0x79, 0xA8, 0xC1], EXIT_UNIMPLEMENTED, None),  # vfmadd213ps: FMA defined, not executed
+    ([0xC4, 0xE2, 0x78, 0xF2, 0xC1], RUNNING, None),        # andn (BMI1)
+    ([0xC4, 0xE2, 0x79, 0x13, 0xC1], EXIT_UNIMPLEMENTED, None),  # vcvtph2ps: F16C defined, not executed
+    ([0xC4, 0xE3, 0x79, 0x44, 0xC1, 0x00], RUNNING, None),  # vpclmulqdq xmm (PCLMULQDQ)
+    ([0xC4, 0xE3, 0x7D, 0x44, 0xC1, 0x00], EXIT_UNIMPLEMENTED, None),  # vpclmulqdq ymm: VPCLMULQDQ
+    ([0xC4, 0xE2, 0x7D, 0xDC, 0xC1], EXIT_UNIMPLEMENTED, None),  # vaesenc ymm: VAES
+    ([0xC4, 0xE3, 0x7B, 0xF0, 0xC1, 0x01], RUNNING, None),  # rorx (BMI2)
+    ([0xC4, 0xE2, 0x7C, 0xF2, 0xC1], EXIT_FAULT, 6),        # andn with VEX.L = 1
+    ([0xC4, 0xE2, 0x78, 0xF3, 0xC1], EXIT_FAULT, 6),        # group 17 /0: undefined
+    ([0xC4, 0xE2, 0x70, 0xF3, 0xC9], RUNNING, None),        # blsr ecx, ecx
+    ([0xC4, 0xE3, 0x79, 0x63, 0xC1, 0x0C], RUNNING, None),  # vpcmpistri
+    ([0xC4, 0xE3, 0x7D, 0x63, 0xC1, 0x0C], EXIT_FAULT, 6),  # vpcmpistri with VEX.L = 1
     ([0xC5, 0xF8, 0xAE, 0x16], EXIT_UNIMPLEMENTED, None),   # vldmxcsr [rsi]: defined, outside the subset
     ([0xC5, 0xF8, 0xAE, 0xC1], EXIT_FAULT, 6),              # VEX 0f ae, register form
     ([0xC5, 0xF8, 0xAE, 0x06], EXIT_FAULT, 6),              # VEX 0f ae /0 (fxsave has no VEX form)
     ([0xC4, 0xE3, 0x79, 0x0F, 0x06, 0x04], RUNNING, None),  # vpalignr xmm, [rsi] (U41)
-    ([0x66, 0x0F, 0x38, 0x37, 0xC1], EXIT_FAULT, 6),        # pcmpgtq: SSE4.2 not enumerated
-    ([0x0F, 0x38, 0xF0, 0x06], EXIT_FAULT, 6),              # movbe: not enumerated
-    ([0x66, 0x0F, 0x38, 0xDC, 0xC1], EXIT_FAULT, 6),        # aesenc: not enumerated
+    ([0x66, 0x0F, 0x38, 0x37, 0xC1], RUNNING, None),        # pcmpgtq (SSE4.2)
+    ([0x66, 0x0F, 0x38, 0x37, 0x06], EXIT_FAULT, 13),       # pcmpgtq xmm0, [rsi]: legacy needs alignment
+    ([0x66, 0x0F, 0x3A, 0x61, 0x06, 0x00], RUNNING, None),  # pcmpestri xmm0, [rsi]: no alignment
+    ([0x0F, 0x38, 0xF0, 0x06], RUNNING, None),              # movbe eax, [rsi]
+    ([0x0F, 0x38, 0xF0, 0xC1], EXIT_FAULT, 6),              # movbe eax, ecx: memory only
+    ([0xF2, 0x0F, 0x38, 0xF1, 0xC1], RUNNING, None),        # crc32 eax, ecx
+    ([0x66, 0x0F, 0x38, 0xF6, 0xC1], RUNNING, None),        # adcx eax, ecx
+    ([0xF0, 0x66, 0x0F, 0x38, 0xF6, 0x06], EXIT_FAULT, 6),  # lock adcx: #UD (U34)
+    ([0x66, 0x0F, 0x38, 0xDC, 0xC1], RUNNING, None),        # aesenc (AES)
     ([0x66, 0x0F, 0x38, 0x50, 0xC1], EXIT_FAULT, 6),        # 0f 38 50: undefined
-    ([0x66, 0x0F, 0x3A, 0x44, 0xC1, 0x00], EXIT_FAULT, 6),  # pclmulqdq
+    ([0x0F, 0x38, 0xC9, 0xC1], EXIT_UNIMPLEMENTED, None),   # sha1msg1: SHA defined, not executed
+    ([0x66, 0x0F, 0x3A, 0x44, 0xC1, 0x00], RUNNING, None),  # pclmulqdq
+    ([0x62, 0xF1, 0x7C, 0x48, 0x58, 0xC1], EXIT_UNIMPLEMENTED, None),  # EVEX vaddps zmm: AVX-512
     ([0x0F, 0x38, 0x00, 0xC1], EXIT_UNIMPLEMENTED, None),   # pshufb mm, mm (MMX form, defined)
     ([0x0F, 0x3A, 0x0F, 0xC1, 0x01], EXIT_UNIMPLEMENTED, None),  # palignr mm, mm, 1
 ]

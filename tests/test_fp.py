@@ -73,7 +73,7 @@ def check(c, status, vector, gpr, rflags, ymm, mxcsr, yin):
     g, y = expected(c, yin)
     if list(gpr) != g:
         return ("gprs", [(i, hex(gpr[i]), hex(g[i])) for i in range(16) if gpr[i] != g[i]])
-    if (rflags ^ int(c["flo"], 16)) & 0x8D5:
+    if (rflags ^ int(c["flo"], 16)) & int(c.get("flm", "8d5"), 16):
         return ("rflags", hex(rflags), c["flo"])
     if ymm != y:
         return ("ymm", [(i // 4, i % 4, hex(ymm[i]), hex(y[i])) for i in range(64) if ymm[i] != y[i]][:4])

@@ -392,7 +392,7 @@ def _run_vector_doc(DOC, inputs, mem=False):
         g, y = expected(c, ins[i])
         if ex[i].status != EXIT_INT3 or ex[i].icount != 1:
             fails.append((c["name"], c["code"], "exit", ex[i].status, ex[i].vector))
-        elif [r.gpr[k] for k in range(16)] != g or (r.rflags ^ int(c["flo"], 16)) & 0x8D5:
+        elif [r.gpr[k] for k in range(16)] != g or (r.rflags ^ int(c["flo"], 16)) & int(c.get("flm", "8d5"), 16):
             fails.append((c["name"], c["code"], "regs"))
         elif get_ymm([r.xmm[k][h] for k in range(16) for h in range(2)],
                      [r.ymmh[k][h] for k in range(16) for h in range(2)]) != y:
@@ -481,3 +481,9 @@ def test_gpu_matches_x87_vectors():
         elif eng.read_virt(i, buf_va, 16).hex() != w["mem"]:
             fails.append((c["code"], "mem"))
     assert not fails, f"{len(fails)}/{len(cases)} mismatches, first: {fails[:6]}"
+
+
+def test_gpu_matches_native_ext_vectors():
+    """BMI1 / BMI2 / ADX / MOVBE / CRC32, SSE4.2, AES, PCLMULQDQ (tests/golden/ext_vectors.json.gz, U45)."""
+    from tests.test_ext import DOC, inputs
+    _run_vector_doc(DOC, inputs, mem=True)

@@ -150,8 +150,11 @@ def test_x87_arithmetic_in_a_program(space):
 
 
 def test_ud_opcodes(space):
-    for n in ("ud_evex", "ud_0f", "ud_b9", "ud_0e", "ud_xbegin", "ud_8f", "ud_fe", "ud_jmpe", "ud_getsec", "movcs"):
+    for n in ("ud_0f", "ud_b9", "ud_0e", "ud_8f", "ud_fe", "ud_jmpe", "ud_getsec", "movcs"):
         assert _one(space, n)["exit"][:2] == (FAULT, 6), n
+    # defined on some CPU, not executed: an engine error, never a #UD crash (U45)
+    for n in ("ud_evex", "ud_xbegin"):
+        assert _one(space, n)["exit"][0] == UNIMPL, n
 
 
 # ---------------------------------------------------------------- engine code on the host vs the oracle
@@ -208,7 +211,9 @@ def test_engine_code_matches_oracle(space):
     # the programs reach every outcome class
     kinds = {(w["exit"][0], w["exit"][1]) for w in want}
     assert {(HLT, 0), (INT3, 0), (FAULT, 6), (FAULT, 13), (FAULT, 14), (FAULT, 11), (FAULT, 7)} <= kinds, kinds
-    assert not any(w["exit"][0] == UNIMPL for w in want)
+    # nothing leaves the engine but the defined-not-executed forms (U45)
+    unimpl = {names.get(ln[i][0]) or names.get(ln[i][1][3]) for i, w in enumerate(want) if w["exit"][0] == UNIMPL}
+    assert unimpl <= {"ud_evex", "ud_xbegin"}, unimpl
 
 
 # ---------------------------------------------------------------- GPU vs the oracle

@@ -29,7 +29,8 @@ enum : u32 {
   O_CALL, O_RET, O_PUSH, O_POP, O_PUSHF, O_POPF, O_LEAVE, O_STRING, O_INT3, O_HLT, O_UD,
   O_LEA, O_SYS, O_SSE, O_UNIMPL,
   O_SYS2,  // engine_sys.h: system / far-transfer / I/O / x87-control (sub = opcode | 0x100 for 0f)
-  O_LOOP   // loopne / loope / loop / jrcxz (sub = opcode & 3)
+  O_LOOP,  // loopne / loope / loop / jrcxz (sub = opcode & 3)
+  O_GEXT   // engine_ext.h: BMI1 / BMI2 / ADX / MOVBE / CRC32 (sub = opcode, fields as O_SSE)
 };
 // operand locations
 enum : u32 {
@@ -75,6 +76,9 @@ __device__ __forceinline__ void setr(Lane &L, u32 rex, u32 r, u32 sz, u64 v) {
     RS(L, r, v);
   }
 }
+}  // namespace wtfgpu_dev
+#include "engine_ext.h"  // the extensions beyond SSE4.1 / AVX2 (U45): gext_exec, x42_exec
+namespace wtfgpu_dev {
 
 // fs / gs bases are cold: read from lane memory when an override appears
 __device__ __forceinline__ u64 segbase(const Dev &P, const Lane &L, u32 seg) {
@@ -120,7 +124,7 @@ __constant__ u32 kMap1[256] = {
     /*00*/ ALU4, ALU4, ALU4, ALU4, ALU4, ALU4, ALU4, ALU4,
     /*40*/ UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN, UN,
     /*50*/ PUSHR, PUSHR, PUSHR, PUSHR, PUSHR, PUSHR, PUSHR, PUSHR, POPR, POPR, POPR, POPR, POPR, POPR, POPR, POPR,
-    /*60*/ UDE, UDE, UDE, E(O_MOVSX, L_GREG, L_RM, Z_V, Z_D, 0, 1, 0, 1, K_NONE, 0), UN, UN, UN, UN,
+    /*60*/ UDE, UDE, UN /* EVEX (U45) */, E(O_MOVSX, L_GREG, L_RM, Z_V, Z_D, 0, 1, 0, 1, K_NONE, 0), UN, UN, UN, UN,
     /*68*/ E(O_PUSH, L_PUSH, L_IMM, Z_STK, Z_STK, 0, 1, 0, 0, K_Z, 0),
     E(O_IMUL, L_GREG, L_RM, Z_V, Z_V, 0, 1, 0, 1, K_Z, 0),
     E(O_PUSH, L_PUSH, L_IMM, Z_STK, Z_STK, 0, 1, 0, 0, K_B, 0),
@@ -308,7 +312,8 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
     rex = 0x40 | (vw << 3) | (vr << 2) | (vx << 1) | vb;
     c = ib_at(b, pos++);  // the opcode
     const bool def = !bad && vmap >= 1 && vmap <= 3 && vex_defined(vmap, c, vpp);
-    if (!def || (vmap == 3 && !fp_form(3, c, vpp, true) && !s4_form(3, c, vpp, true))) {  // U36: #UD from the opcode byte
+    if (!def || (vmap == 3 && !fp_form(3, c, vpp, true) && !s4_form(3, c, vpp, true) && !x42_form(3, c, vpp, true) &&
+                 !gx_form(3, c, vpp, true))) {  // U36: #UD from the opcode byte
       u.len = pos;
       u.op = (lock || !def) ? O_UD : O_UNIMPL;
       u.supported = lock || !def;
@@ -333,8 +338,9 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
       if (pos >= b.avail) return 1;
       const u32 c3 = ib_at(b, pos++);
       const u32 pfx3 = u.rep == 0xf3 ? 2 : u.rep == 0xf2 ? 3 : p66 ? 1 : 0;
-      if ((c == 0x38 && (c3 == 0x00 || c3 == 0x17)) || fp_form(c == 0x38 ? 2 : 3, c3, pfx3, false) ||
-          s4_form(c == 0x38 ? 2 : 3, c3, pfx3, false)) {
+      const u32 m3 = c == 0x38 ? 2 : 3;
+      if ((c == 0x38 && (c3 == 0x00 || c3 == 0x17)) || fp_form(m3, c3, pfx3, false) || s4_form(m3, c3, pfx3, false) ||
+          x42_form(m3, c3, pfx3, false) || gx_form(m3, c3, pfx3, false)) {
         smap = c == 0x38 ? 2 : 3;
         e = smap == 3 ? kSseModrmImm : kSseModrm;
         c = c3;
@@ -479,7 +485,8 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
         break;
       case G_8F:
       case G_C6:
-        if (r3 != 0) u.op = O_UD;  // xop / xabort / xbegin and the reserved forms: #UD
+        if (r3 != 0) u.op = O_UD;  // xop and the reserved forms: #UD
+        if (grp == G_C6 && r3 == 7 && !u.is_mem && (u.rm & 7) == 0) u.op = O_UNIMPL;  // xabort / xbegin: RTM (U45)
         break;
       case G_BA:
         if (r3 < 4) u.op = O_UD;
@@ -492,7 +499,14 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
   }
   if (u.op == O_ALU && u.sub == 7) u.awrite = 0;  // cmp reads its destination, never writes it
   if (map2) {
-    if (u.op == O_SSE) {  // engine_sse.h: opcode in sub, mandatory-prefix class in bsz, map / VEX in opreg
+    const u32 gpc = vex ? vpp : (u.rep == 0xf3 ? 2 : u.rep == 0xf2 ? 3 : p66 ? 1 : 0);
+    if (u.op == O_SSE && smap >= 2 && gx_form(smap, c, gpc, vex != 0)) {  // engine_ext.h (U45)
+      u.op = O_GEXT;
+      u.sub = c;
+      u.bsz = gpc;
+      u.opreg = vex ? vex : (smap << 8);
+      u.asz = osz;
+    } else if (u.op == O_SSE) {  // engine_sse.h: opcode in sub, mandatory-prefix class in bsz, map / VEX in opreg
       u.sub = c;
       if (vex) {
         u.bsz = vpp;
@@ -927,6 +941,7 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
   const u32 op = u.op;
   if (op == O_STRING) return string_op(P, L, u);
   if (op == O_SSE) return sse_exec(P, L, u, nrip, next);
+  if (op == O_GEXT) return gext_exec(P, L, u, nrip, next);
   if (op == O_LEA && !u.is_mem) {
     set_fault(L, WTFGPU_VEC_UD, 0, 0);
     return X_FAULT;

@@ -28,6 +28,9 @@
 namespace wtfgpu_dev {
 
 __host__ __device__ inline bool s4_form(u32 map, u32 c, u32 pp, bool vex);  // engine_sse4.h
+__host__ __device__ inline bool x42_form(u32 map, u32 c, u32 pp, bool vex);  // engine_ext.h
+struct UOp;
+__device__ __noinline__ int x42_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next);
 
 struct X128 {
   u64 lo, hi;
@@ -63,7 +66,8 @@ __device__ __forceinline__ u32 vex_map(u32 x) { return (x >> 8) & 31; }
 // Register-only / memory-only / VEX.L / VEX.vvvv violations are #UD at
 // execution, not here.
 __device__ __forceinline__ bool sse_valid(u32 map, u32 c, u32 pc, u32 is_mem, u32 r3) {
-  if (fp_form(map, c, pc, false) || s4_form(map, c, pc, false)) return true;  // engine_ssefp.h, engine_sse4.h
+  if (fp_form(map, c, pc, false) || s4_form(map, c, pc, false) || x42_form(map, c, pc, false))
+    return true;  // engine_ssefp.h, engine_sse4.h, engine_ext.h
   if (map == 2) return pc == 1 && (c == 0x00 || c == 0x17);
   if (c == 0xc3) return pc == 0;
   if (c == 0xae) return pc == 0 && (is_mem ? (r3 == 2 || r3 == 3) : r3 >= 5);
@@ -84,10 +88,14 @@ __device__ __forceinline__ bool sse_valid(u32 map, u32 c, u32 pc, u32 is_mem, u3
     return pc == 1 && c != 0xd0 && c != 0xe6 && c != 0xf0 && c != 0xf7 && c != 0xff;
   return false;
 }
-// U36: the encodings the emulated CPU defines, i.e. SSE .. SSE4.1,
-// SSSE3, AVX and AVX2 as cpuid_leaf enumerates them. Anything else (an
-// undefined opcode / prefix pair, a VEX map other than 0f / 0f 38 / 0f 3a,
-// FMA, F16C, BMI, AES, PCLMULQDQ, SHA, SSE4.2 legacy forms, ...) is #UD,
+// U36: the encodings some x86-64 CPU defines. Those the engine
+// executes are what cpuid_leaf enumerates (SSE .. SSE4.2, SSSE3, AVX, AVX2,
+// AES, PCLMULQDQ, BMI1 / BMI2, ADX, MOVBE); the other defined ones (FMA, F16C,
+// AVX-VNNI, AVX-IFMA, AVX-NE-CONVERT, GFNI, VAES / VPCLMULQDQ's 256-bit forms,
+// SHA, CET, MOVDIR*, ENQCMD, Key Locker, EVEX, ...) are UNIMPLEMENTED (U45: a
+// guest picks its paths from the capture host's CPUID, so they are an engine
+// gap, never a crash). Only an encoding no CPU defines (a VEX map other than
+// 0f / 0f 38 / 0f 3a, an opcode / prefix pair no extension assigns) is #UD,
 // decided from the opcode byte before any ModRM fetch. pp: 0 none, 1 66,
 // 2 f3, 3 f2.
 __host__ __device__ inline bool vex_defined(u32 map, u32 op, u32 pp) {
@@ -112,30 +120,52 @@ __host__ __device__ inline bool vex_defined(u32 map, u32 op, u32 pp) {
                            (op >= 0xd1 && op <= 0xfe));
     }
   }
-  if (pp != 1) return false;
-  if (map == 2)
-    return op <= 0x0f || (op >= 0x16 && op <= 0x1a) || (op >= 0x1c && op <= 0x1e) || (op >= 0x20 && op <= 0x25) ||
-           (op >= 0x28 && op <= 0x41) || (op >= 0x45 && op <= 0x47) || (op >= 0x58 && op <= 0x5a) || op == 0x78 ||
-           op == 0x79 || op == 0x8c || op == 0x8e || (op >= 0x90 && op <= 0x93);
-  if (map == 3)
+  if (map == 2) {
+    // BMI1 / BMI2, AVX-VNNI-INT8 (50 51), AVX-NE-CONVERT (72 b0 b1), AVX-VNNI-INT16 (d2 d3)
+    if (op == 0xf5 || op == 0xf7 || op == 0x50 || op == 0x51 || op == 0xb0 || op == 0xd2 || op == 0xd3) return true;
+    if (pp == 0) return op == 0xf2 || op == 0xf3;
+    if (pp == 2) return op == 0x72 || op == 0xb1;
+    if (pp == 3) return op == 0xf6;
+    return op <= 0x0f || op == 0x13 || (op >= 0x16 && op <= 0x1a) || (op >= 0x1c && op <= 0x1e) ||
+           (op >= 0x20 && op <= 0x25) || (op >= 0x28 && op <= 0x41) || (op >= 0x45 && op <= 0x47) ||
+           (op >= 0x52 && op <= 0x53) || (op >= 0x58 && op <= 0x5a) || op == 0x78 || op == 0x79 || op == 0x8c ||
+           op == 0x8e || (op >= 0x90 && op <= 0x93) || (op >= 0x96 && op <= 0x9f) || (op >= 0xa6 && op <= 0xaf) ||
+           op == 0xb1 || (op >= 0xb4 && op <= 0xbf) ||
+           op == 0xcf || (op >= 0xdb && op <= 0xdf);
+  }
+  if (map == 3) {
+    if (pp == 3) return op == 0xf0;  // rorx
+    if (pp != 1) return false;
     return op <= 0x02 || (op >= 0x04 && op <= 0x06) || (op >= 0x08 && op <= 0x0f) || (op >= 0x14 && op <= 0x19) ||
-           (op >= 0x20 && op <= 0x22) || op == 0x38 || op == 0x39 || (op >= 0x40 && op <= 0x42) || op == 0x46 ||
-           (op >= 0x4a && op <= 0x4c) || (op >= 0x60 && op <= 0x63);
+           op == 0x1d || (op >= 0x20 && op <= 0x22) || op == 0x38 || op == 0x39 || (op >= 0x40 && op <= 0x42) ||
+           op == 0x44 || op == 0x46 || (op >= 0x4a && op <= 0x4c) || (op >= 0x60 && op <= 0x63) || op == 0xce ||
+           op == 0xcf || op == 0xdf;
+  }
   return false;
 }
 // the legacy 0f 38 (map 2) / 0f 3a (map 3) opcodes, same rule
 __host__ __device__ inline bool legacy_3byte_defined(u32 map, u32 op, u32 pfx) {
-  if (map == 2)
+  if (map == 2) {
+    if (pfx == 0 && ((op >= 0xc8 && op <= 0xcd) || op == 0xf0 || op == 0xf1 || op == 0xf6 || op == 0xf9)) return true;
+    if (pfx == 2 && (op == 0xf6 || op == 0xf8 || op == 0xd8 || (op >= 0xdc && op <= 0xdf))) return true;
+    if (pfx == 3 && (op == 0xf0 || op == 0xf1 || op == 0xf8)) return true;
+    if (pfx == 1 && (op == 0x37 || (op >= 0x80 && op <= 0x82) || op == 0xcf || (op >= 0xdb && op <= 0xdf) ||
+                     op == 0xf0 || op == 0xf1 || op == 0xf5 || op == 0xf6 || op == 0xf8))
+      return true;
     return ((op <= 0x0b || (op >= 0x1c && op <= 0x1e)) && pfx <= 1) ||
            (pfx == 1 && (op == 0x10 || op == 0x14 || op == 0x15 || op == 0x17 || (op >= 0x20 && op <= 0x25) ||
                          (op >= 0x28 && op <= 0x2b) || (op >= 0x30 && op <= 0x35) || (op >= 0x38 && op <= 0x41)));
+  }
+  if (pfx == 0 && op == 0xcc) return true;  // sha1rnds4
   return (op == 0x0f && pfx <= 1) ||
          (pfx == 1 && ((op >= 0x08 && op <= 0x0e) || (op >= 0x14 && op <= 0x17) || (op >= 0x20 && op <= 0x22) ||
-                       (op >= 0x40 && op <= 0x42)));
+                       (op >= 0x40 && op <= 0x42) || op == 0x44 || (op >= 0x60 && op <= 0x63) || op == 0xce ||
+                       op == 0xcf || op == 0xdf));
 }
 
 __device__ __forceinline__ bool vex_valid(u32 map, u32 c, u32 pp, u32 is_mem, u32 r3) {
-  if (fp_form(map, c, pp, true) || s4_form(map, c, pp, true)) return true;  // engine_ssefp.h, engine_sse4.h
+  if (fp_form(map, c, pp, true) || s4_form(map, c, pp, true) || x42_form(map, c, pp, true))
+    return true;  // engine_ssefp.h, engine_sse4.h, engine_ext.h
   if (map == 2) return pp == 1 && (c == 0x00 || c == 0x17 || c == 0x58 || c == 0x59 || c == 0x78 || c == 0x79);
   if (map != 1) return false;
   if (c == 0x77) return pp == 0;
@@ -610,6 +640,7 @@ __device__ __noinline__ int sse_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
   }
   if (fp_form(map, c, pc, false)) return fp_exec(P, L, u, nrip, next);
   if (s4_form(map, c, pc, false)) return s4_exec(P, L, u, nrip, next);
+  if (x42_form(map, c, pc, false)) return x42_exec(P, L, u, nrip, next);
   // the r/m operand: 16 bytes aligned unless an unaligned move / narrower form
   u32 n = 16;
   bool align = true;
@@ -723,6 +754,7 @@ __device__ __noinline__ int vex_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
   const u32 x = u.opreg, c = u.sub, pp = u.bsz, r3 = u.reg & 7, map = vex_map(x);
   if (fp_form(map, c, pp, true)) return fp_exec(P, L, u, nrip, next);  // its own VEX checks
   if (s4_form(map, c, pp, true)) return s4_exec(P, L, u, nrip, next);
+  if (x42_form(map, c, pp, true)) return x42_exec(P, L, u, nrip, next);  // its own VEX checks
   const u32 l256 = (x >> 1) & 1, w = (x >> 2) & 1, vvvv = (x >> 4) & 15;
   const bool mem = u.is_mem;
   const u32 imm = (u32)u.imm & 0xff;
