@@ -416,6 +416,11 @@ int wtfgpu_read_bytes(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, uint64_t 
 /* Per-lane dirty (copy-on-write) page counts: the 2 x 4096 bytes per dirty
  * page of the reference's restore memcpy in B_exec. */
 int wtfgpu_read_dirty_counts(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, uint32_t *out);
+/* With edges on (wtfgpu_set_edges): per lane of [first, first+count) two
+ * counts, RecordEdge calls of its testcase and those whose edge was new to its
+ * coverage set (BochscpuRunStats_t::NumberEdges / NumberUniqueEdges,
+ * bochscpu_backend.h:17-45); zeros with edges off. Reset by restore. */
+int wtfgpu_read_edge_counts(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, uint32_t *out2);
 
 #ifdef __cplusplus
 }

@@ -214,7 +214,6 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
     return Value;
   }
   uint64_t Rdrand() override;
-  void PrintRunStats() override {}
   bool SetBreakpoint(const Gva_t Gva, const BreakpointHandler_t Handler) override {
     if (ModuleInstances *I = ModuleInstances::Registering()) {  // a module copy's Init
       I->AddHandler(Gva.U64(), Handler);
@@ -320,6 +319,17 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
     return added;
   }
   uint64_t Icount() const { return orc_icount(m_); }
+  void RunStats(LaneResult &L) const {
+    L.bytes = orc_bytes(m_);
+    L.dirty = (uint32_t)orc_dirty(m_, nullptr, 0);
+    L.edges = orc_edges(m_, &L.edges_new);
+  }
+  void PrintRunStats() override {
+    LaneResult L;
+    L.icount = orc_icount(m_);
+    RunStats(L);
+    PrintTestcaseRunStats(L, aggregate_.size());
+  }
   const ModuleInstances *route_ = nullptr;  // RunBatch over per-lane module copies
   uint32_t route_lane_ = 0;
   bool full_ = false;
@@ -396,6 +406,9 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
       L.gprs[17] = r.rflags;
       L.rip = r.rip;
       L.icount = orc_icount(m_);
+      L.bytes = orc_bytes(m_);
+      L.dirty = (uint32_t)orc_dirty(m_, nullptr, 0);
+      L.edges = orc_edges(m_, &L.edges_new);
       if (trace_cap_) {  // this testcase's rip trace
         std::vector<uint64_t> &T = traces_[i];
         T.resize(orc_trace(m_, nullptr, 0));
@@ -452,6 +465,7 @@ int main(int argc, char **argv) {
     bool EnableTrace(uint32_t P) override { return b->EnableTrace(P); }
     uint64_t LastIcount() const override { return b->Icount(); }
     bool LastError() const override { return b->engine_error_; }
+    void LastRunStats(LaneResult &L) const override { b->RunStats(L); }
     bool LaneTrace(uint32_t L, std::vector<uint64_t> &R, bool &T) override { return b->LaneTrace(L, R, T); }
     bool EnableTenet(uint64_t P) override { return b->EnableTenet(P); }
     bool LaneTenet(uint32_t L, std::vector<uint8_t> &R, bool &T) override { return b->LaneTenet(L, R, T); }

@@ -160,6 +160,7 @@ struct orc_machine {
   u64 deliv_icount; /* retired count at the last IDT delivery (valid if deliv_valid) */
   int deliv_valid;
   int edges; /* record branch edges into the coverage (RecordEdge) */
+  u64 edges_run, edges_new; /* RecordEdge calls of the testcase, and those whose edge joined its set (run stats) */
   int trace, resumed; /* rip trace on; the next instruction resumes a breakpoint hit */
   vec tracelist;
   /* Tenet (U38, wtfgpu_set_tenet's stream): entries as u64 words */
@@ -248,11 +249,16 @@ void orc_restore(orc_machine *m, const wtfgpu_regs_t *r) {
   m->initial_cr3 = r->cr3;
   m->icount = 0;
   m->bytes = 0;
+  m->edges_run = m->edges_new = 0;
   m->deliv_valid = 0;
 }
 
 uint64_t orc_icount(orc_machine *m) { return m->icount; }
 uint64_t orc_bytes(orc_machine *m) { return m->bytes; }
+uint64_t orc_edges(orc_machine *m, uint64_t *unique) {
+  if (unique) *unique = m->edges_new;
+  return m->edges_run;
+}
 
 uint64_t orc_coverage(orc_machine *m, u64 *out, u64 cap) {
   for (u64 i = 0; i < m->covlist.n && i < cap; i++) out[i] = m->covlist.v[i];
@@ -3469,9 +3475,11 @@ static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
     e *= 0x94d049bb133111ebULL;
     e ^= e >> 31;
     e ^= next;
+    m->edges_run++;
     if (!hm_has(&m->cov, e)) {
       *hm_slot(&m->cov, e, 1) = (void *)1;
       vec_push(&m->covlist, e);
+      m->edges_new++;
     }
   }
   if (x == X_OK || x == X_CR3) {

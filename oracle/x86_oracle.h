@@ -63,6 +63,8 @@ int orc_run(orc_machine *m, int skip_bp, wtfgpu_exit_t *exit);
 int orc_step(orc_machine *m, wtfgpu_exit_t *exit);
 uint64_t orc_icount(orc_machine *m);
 uint64_t orc_bytes(orc_machine *m);
+/* RecordEdge calls of the current testcase; *unique: those whose edge was new to its coverage set */
+uint64_t orc_edges(orc_machine *m, uint64_t *unique);
 /* Unique rips executed since the last restore, in first-execution order. */
 uint64_t orc_coverage(orc_machine *m, uint64_t *out, uint64_t cap);
 /* Dirty (copy-on-write) GPAs since the last restore, in first-write order. */

@@ -189,6 +189,14 @@ __device__ __noinline__ u32 cover(const Dev &P, u64 rip, bool mine, u32 lane, u3
   return log_value(P, rip, mine, lane, gen, cnt);
 }
 
+// Run stats (BochscpuRunStats_t::NumberEdges / NumberUniqueEdges,
+// bochscpu_backend.h:17-45): edges recorded, and those new to the lane's set.
+__device__ __forceinline__ void count_edge(const Dev &P, u32 lane, bool fresh) {
+  if (!P.edge_cnt) return;
+  P.edge_cnt[2 * (u64)lane] += 1;
+  if (fresh) P.edge_cnt[2 * (u64)lane + 1] += 1;
+}
+
 // A branch edge (per-lane value): logged unless the aggregate has it.
 __device__ __noinline__ u32 cover_edge(const Dev &P, u64 e, bool mine, u32 lane, u32 gen, u32 cnt) {
   if (!mine) return cnt;
@@ -925,8 +933,11 @@ __device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr
     retire(P, L, x, d.len, next, d.opbytes);
     if (g_tn.buf && (x == X_OK || x == X_CR3)) tn_regs(P, L);
     // RecordEdge (bochscpu_backend.cc:699-728): the branch ran, whatever the retire hook decided
-    if (P.edges && P.cov_rip && edge_op(d.op, d.bsrc) && x == X_OK)
+    if (P.edges && P.cov_rip && edge_op(d.op, d.bsrc) && x == X_OK) {
+      const u32 c0 = L.ccnt;
       L.ccnt = cover_edge(P, edge_key(grip, next), true, L.lane, L.cgen, L.ccnt);
+      count_edge(P, L.lane, L.ccnt != c0);
+    }
   }
 }
 
@@ -1255,8 +1266,11 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       retire(P, L, x, len, next, opbytes);
       if (g_tn.buf && (x == X_OK || x == X_CR3)) WITH_LANE_COPY(tn_regs(P, T));  // Tenet: the retired instruction
       // RecordEdge (bochscpu_backend.cc:699-728): the branch ran, whatever the retire hook decided
-      if (P.edges && P.cov_rip && x == X_OK && edge_op(rfl32(u->op), rfl32(u->bsrc)))
+      if (P.edges && P.cov_rip && x == X_OK && edge_op(rfl32(u->op), rfl32(u->bsrc))) {
+        const u32 c0 = L.ccnt;
         L.ccnt = cover_edge(P, edge_key(grip, next), true, L.lane, L.cgen, L.ccnt);
+        count_edge(P, L.lane, L.ccnt != c0);
+      }
     }
     STAMP(1);
   }
@@ -1327,6 +1341,7 @@ __device__ __forceinline__ void restore_lane(const Dev &P, const InitState &s, c
   tlb_stale(P, lane);
   if (P.rd_seed) P.rd_seed[lane] = P.rd_seed0;  // bochscpu_backend.cc:1030
   if (P.trace_cnt) P.trace_cnt[lane] = 0;
+  if (P.edge_cnt) P.edge_cnt[2 * (u64)lane] = P.edge_cnt[2 * (u64)lane + 1] = 0;
   if (g_tn.buf) {
     g_tn.pos[lane] = g_tn.ipos[lane] = g_tn.cpos[lane] = 0;
     g_tn.last[lane] = ~0ull;
@@ -1371,6 +1386,7 @@ __global__ void k_restore(Dev P, const InitState *S, const wtfgpu_regs_t *full0,
   tlb_stale(P, lane);
   if (P.rd_seed) P.rd_seed[lane] = P.rd_seed0;  // bochscpu_backend.cc:1030
   if (P.trace_cnt) P.trace_cnt[lane] = 0;
+  if (P.edge_cnt) P.edge_cnt[2 * (u64)lane] = P.edge_cnt[2 * (u64)lane + 1] = 0;
   if (g_tn.buf) {
     g_tn.pos[lane] = g_tn.ipos[lane] = g_tn.cpos[lane] = 0;
     g_tn.last[lane] = ~0ull;
@@ -1845,6 +1861,7 @@ struct wtfgpu_ctx {
   u64 tn_cap = 0;
   u64 *d_trace = nullptr;     // rip traces (Dev::trace)
   u32 *d_tracecnt = nullptr;
+  u32 *d_edgecnt = nullptr;  // [nlanes][2] (wtfgpu_set_edges)
   LaneTlb *d_tlbs = nullptr;  // translation state kept between k_run launches
   u8 *d_lcopy = nullptr;      // WTFGPU_LANE_LDS=2: the rare path's lane copies
   u32 *d_tlbok = nullptr;
@@ -2162,10 +2179,13 @@ static void free_lanes(wtfgpu_ctx *c) {
   dfree(c->d_extra);
   dfree(c->d_trace);
   dfree(c->d_tracecnt);
+  dfree(c->d_edgecnt);
   c->d_trace = nullptr;
   c->d_tracecnt = nullptr;
+  c->d_edgecnt = nullptr;
   c->P.trace = nullptr;
   c->P.trace_cnt = nullptr;
+  c->P.edge_cnt = nullptr;
   c->P.trace_cap = 0;
   if (c->d_tn_buf) {  // Tenet buffers are sized by the lane count
     dfree(c->d_tn_buf);
@@ -2376,6 +2396,7 @@ int wtfgpu_alloc_lanes(wtfgpu_ctx *c, uint32_t nlanes, uint32_t overlay_pages, u
   P.cov_overflow = c->d_covovf;
   P.H = cov_entries;
   P.stat = c->d_stat;
+  if (P.edges) return wtfgpu_set_edges(c, 1);  // the counters follow the lane count
   return WTFGPU_OK;
 }
 
@@ -3468,6 +3489,11 @@ int wtfgpu_set_edges(wtfgpu_ctx *c, int on) {
   if (!c) return WTFGPU_ERR_INVALID;
   HIPCHK(hipSetDevice(c->device));
   c->P.edges = on ? 1 : 0;
+  if (on && !c->d_edgecnt && c->P.nlanes) {
+    if (dalloc(&c->d_edgecnt, 2ull * c->P.nlanes)) return WTFGPU_ERR_OOM;
+    HIPCHK(hipMemset(c->d_edgecnt, 0, 8ull * c->P.nlanes));
+  }
+  c->P.edge_cnt = on ? c->d_edgecnt : nullptr;
   return guc_clear(c);  // cached entries were digested for the other setting
 }
 
@@ -3528,6 +3554,18 @@ int wtfgpu_read_bytes(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t *o
   if (!lanes_ok(c, first, count) || !out) return WTFGPU_ERR_INVALID;
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipMemcpyAsync(out, c->d_nbytes + first, (u64)count * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_read_edge_counts(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint32_t *out2) {
+  if (!lanes_ok(c, first, count) || !out2) return WTFGPU_ERR_INVALID;
+  if (!c->d_edgecnt) {
+    memset(out2, 0, 8ull * count);
+    return WTFGPU_OK;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemcpyAsync(out2, c->d_edgecnt + 2ull * first, 8ull * count, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return WTFGPU_OK;
 }

@@ -127,6 +127,7 @@ struct Dev {
   u64 *extra_keys;
   u32 extra_mask;
   u32 edges;              // record branch edges (RecordEdge, bochscpu_backend.cc:699-728)
+  u32 *edge_cnt;          // [nlanes][2] with edges: RecordEdge calls, and those new to the lane's set (run stats)
   // rip trace (--trace-type rip / unique_rip, bochscpu_backend.cc:506-520):
   // per lane, the rips about to execute in order, trace_cap of them at most
   u64 *trace;             // [nlanes][trace_cap]

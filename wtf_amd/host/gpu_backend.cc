@@ -167,10 +167,10 @@ uint64_t GpuBackend_t::SetReg(const Registers_t Reg, const uint64_t Value) {
 // bochscpu_backend.cc:874-885, per-lane seed
 uint64_t GpuBackend_t::Rdrand() { return wtf_rdrand(cur().seed); }
 
+// BochscpuRunStats_t::Print (bochscpu_backend.h:25-37) of the last testcase
+// Run() ran, then the engine's own counters
 void GpuBackend_t::PrintRunStats() {
-  printf("--------------------------------------------------\n");
-  printf("Run stats (gpu):\n");
-  printf("Instructions executed: %llu\n", (unsigned long long)stats_.retired);
+  PrintTestcaseRunStats(last_run_, aggregate_.size());
   printf("  Breakpoint services: %llu in %llu rounds\n", (unsigned long long)stats_.breakpoint_hits,
          (unsigned long long)stats_.rounds);
   printf("       Kernel time ms: %.2f\n", stats_.kernel_ms);
@@ -758,9 +758,23 @@ bool GpuBackend_t::fill_results(const std::vector<uint32_t> &lanes, uint32_t fir
   if (finished) finished->insert(finished->end(), fin.begin(), fin.end());
   if (!out) return true;
   std::vector<uint64_t> regs;
+  // run stats of [lo, hi) (run mode): byte, dirty-page and edge counters
+  uint32_t lo = 0, hi = 0;
+  std::vector<uint64_t> nb;
+  std::vector<uint32_t> dc, ec;
   if (want_gprs_) {  // run mode prints them; the fuzz loop never reads them
     regs.resize(fin.size() * 18);
     if (!fin.empty() && wtfgpu_read_gprs_list(ctx_, fin.data(), (uint32_t)fin.size(), regs.data())) return false;
+    if (!fin.empty()) {
+      lo = *std::min_element(fin.begin(), fin.end());
+      hi = *std::max_element(fin.begin(), fin.end()) + 1;
+      nb.resize(hi - lo);
+      dc.resize(hi - lo);
+      ec.resize(2 * (hi - lo));
+      if (wtfgpu_read_bytes(ctx_, lo, hi - lo, nb.data()) || wtfgpu_read_dirty_counts(ctx_, lo, hi - lo, dc.data()) ||
+          wtfgpu_read_edge_counts(ctx_, lo, hi - lo, ec.data()))
+        return false;
+    }
   }
   HostPool::Get().For(fin.size(), 1024, [&](size_t i) {
     LaneResult &r = (*out)[fin[i]];
@@ -774,6 +788,11 @@ bool GpuBackend_t::fill_results(const std::vector<uint32_t> &lanes, uint32_t fir
     if (want_gprs_) {
       memcpy(r.gprs, &regs[i * 18], 18 * 8);
       r.rip = r.gprs[16];
+      const uint32_t k = fin[i] - lo;
+      r.bytes = nb[k];
+      r.dirty = std::min(dc[k], overlay_pages_);
+      r.edges = ec[2 * k];
+      r.edges_new = ec[2 * k + 1];
     } else {
       r.rip = ex[fin[i] - first].rip;
     }
@@ -1103,6 +1122,18 @@ std::optional<TestcaseResult_t> GpuBackend_t::Run(const uint8_t *, const uint64_
   v.cr_known = 0;
   last_icount_ = out[0].icount;
   last_error_ = out[0].error;
+  {  // run stats of this testcase (PrintRunStats)
+    uint64_t nbytes = 0;
+    uint32_t dcount = 0, ecount[2] = {0, 0};
+    wtfgpu_read_bytes(ctx_, 0, 1, &nbytes);
+    wtfgpu_read_dirty_counts(ctx_, 0, 1, &dcount);
+    wtfgpu_read_edge_counts(ctx_, 0, 1, ecount);
+    last_run_ = out[0];
+    last_run_.bytes = nbytes;
+    last_run_.dirty = std::min(dcount, overlay_pages_);
+    last_run_.edges = ecount[0];
+    last_run_.edges_new = ecount[1];
+  }
   finish_coverage(1, nullptr, nullptr);  // Timedout revocation is the client's call (RevokeLastNewCoverage)
   stats_.total_ms += ms_since(t0);
   cur_ = 0;

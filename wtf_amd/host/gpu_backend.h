@@ -109,6 +109,12 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   void SetWantRegisters(bool On) override { want_gprs_ = On; }
   uint64_t LastIcount() const override { return last_icount_; }
   bool LastError() const override { return last_error_; }
+  void LastRunStats(LaneResult &L) const override {
+    L.bytes = last_run_.bytes;
+    L.dirty = last_run_.dirty;
+    L.edges = last_run_.edges;
+    L.edges_new = last_run_.edges_new;
+  }
   size_t CoverageSize() const override { return aggregate_.size(); }
   void TakeNewExtra(std::vector<uint64_t> &Out) override;
   size_t AbsorbExtra(const std::vector<uint64_t> &All) override;
@@ -219,6 +225,7 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   bool cov_ovf_warned_ = false;
   bool want_gprs_ = true;
   uint64_t last_icount_ = 0;  // of the last Run
+  LaneResult last_run_;       // the last Run's result and run stats (PrintRunStats)
   bool last_error_ = false;
   // streaming parts (see parts_n): lane range, slice in flight, its occupied
   // lanes, exit read-back, pinned staging of the part's feeds

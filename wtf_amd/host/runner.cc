@@ -178,6 +178,39 @@ TestcaseResult_t FaultToResult(uint32_t vector, uint32_t error, uint64_t rip, ui
   return Crash_t(name);
 }
 
+// human.cc:38-72
+static std::string bytes_to_human(uint64_t B) {
+  const char *Unit = "b";
+  double V = double(B);
+  const double K = 1024, M = K * K, G = M * K;
+  if (V >= G) Unit = "gb", V /= G;
+  else if (V >= M) Unit = "mb", V /= M;
+  else if (V >= K) Unit = "kb", V /= K;
+  char b[64];
+  snprintf(b, sizeof(b), "%.1f%s", V, Unit);
+  return b;
+}
+static std::string number_to_human(uint64_t N) {
+  const char *Unit = "";
+  double V = double(N);
+  if (V > 1e6) Unit = "m", V /= 1e6;
+  else if (V > 1e3) Unit = "k", V /= 1e3;
+  char b[64];
+  snprintf(b, sizeof(b), "%.1f%s", V, Unit);
+  return b;
+}
+
+void PrintTestcaseRunStats(const LaneResult &L, size_t AggregateCoverage) {
+  printf("--------------------------------------------------\n");
+  printf("Run stats:\n");
+  printf("Instructions executed: %s (%s unique)\n", number_to_human(L.icount).c_str(),
+         number_to_human(AggregateCoverage).c_str());
+  printf("          Dirty pages: %s\n", bytes_to_human((uint64_t)L.dirty * Page::Size).c_str());
+  printf("      Memory accesses: %s\n", bytes_to_human(L.bytes).c_str());
+  printf("       Edges executed: %s (%s unique)\n", number_to_human(L.edges).c_str(),
+         number_to_human(L.edges_new).c_str());
+}
+
 bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
   for (int i = 1; i < argc; i++) {
     const std::string a = argv[i];
@@ -304,6 +337,18 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
 
   if (O.mode == "run") {
     auto Inputs = list_inputs(O.input.empty() ? fs::path(O.target) / "inputs" : fs::path(O.input));
+    // --runs R: each input R times in a row (subcommands.cc:85-88); the run
+    // stats are printed for a single input run once (:48)
+    const uint64_t Runs = O.runs ? O.runs : 1;
+    const bool Stats = Inputs.size() == 1 && Runs == 1 && !O.quiet;
+    if (Runs > 1) {
+      std::vector<fs::path> Rep;
+      Rep.reserve(Inputs.size() * Runs);
+      for (const fs::path &In : Inputs)
+        for (uint64_t k = 0; k < Runs; k++) Rep.push_back(In);
+      Inputs.swap(Rep);
+    }
+    LaneResult Last;
     // traces (subcommands.cc:52-74): <trace-path>/<input name>.trace; an input
     // whose trace exists is skipped
     const bool Trace = !O.trace_path.empty();
@@ -370,7 +415,9 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
       for (int g = 0; g < 18; g++) fprintf(Out, "%s%llu", g ? "," : "", (unsigned long long)L.gprs[g]);
       fprintf(Out, "],\"coverage\":[");
       for (size_t c = 0; c < Cov.size(); c++) fprintf(Out, "%s%llu", c ? "," : "", (unsigned long long)Cov[c]);
-      fprintf(Out, "]}\n");
+      fprintf(Out, "],\"bytes\":%llu,\"dirty\":%u,\"edges\":%llu,\"edges_new\":%llu}\n", (unsigned long long)L.bytes,
+              L.dirty, (unsigned long long)L.edges, (unsigned long long)L.edges_new);
+      Last = L;
     };
     if (O.serial && !Trace) {
       // RunTestcaseAndRestore (client.cc:88-180) restated over the Backend_t
@@ -407,6 +454,7 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
           if (std::holds_alternative<Timedout_t>(*Res)) B->RevokeLastNewCoverage();
           L.icount = Exec.LastIcount();
           L.error = Exec.LastError();
+          Exec.LastRunStats(L);
         }
         for (int g = 0; g < 18; g++) L.gprs[g] = B->GetReg(Order[g]);
         L.rip = L.gprs[16];
@@ -474,6 +522,7 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
       }
     }
     if (Out != stdout) fclose(Out);
+    if (Stats) PrintTestcaseRunStats(Last, Exec.CoverageSize());
     if (!O.quiet)
       fprintf(stderr, "run: %zu testcases, %llu instructions, %.3f s\n", Inputs.size(), (unsigned long long)Retired,
               secs_since(t0));

@@ -32,6 +32,11 @@ struct LaneResult {
   uint64_t rip = 0;
   uint64_t gprs[18] = {};    // final gprs (wtfgpu order) + rip + rflags
   std::vector<uint64_t> new_coverage;  // LastNewCoverage, attributed in lane order
+  // run stats (BochscpuRunStats_t, bochscpu_backend.h:17-45), filled when the
+  // executor is asked for registers (run mode): instruction + data bytes
+  // (B_insn), dirty pages, RecordEdge calls and those new to the testcase's set
+  uint64_t bytes = 0, edges = 0, edges_new = 0;
+  uint32_t dirty = 0;
 };
 
 struct StreamTestcase_t {
@@ -81,6 +86,8 @@ class Executor_t {
   // the retired count / engine-error flag of the last Backend_t::Run
   virtual uint64_t LastIcount() const { return 0; }
   virtual bool LastError() const { return false; }
+  // the run stats (LaneResult::bytes / dirty / edges / edges_new) of the last Backend_t::Run
+  virtual void LastRunStats(LaneResult &) const {}
   virtual size_t CoverageSize() const = 0;
   virtual std::string StatsJson() const { return "{}"; }
   // The coverage map over the executable-page slot table (one byte per code
@@ -132,6 +139,11 @@ class CoverageExchange_t {
   virtual bool AllGatherV(const std::vector<uint64_t> &Mine, std::vector<uint64_t> &All) = 0;
 };
 
+// BochscpuRunStats_t::Print (bochscpu_backend.h:25-37; NumberToHuman /
+// BytesToHuman, human.cc:38-72): one testcase's instructions (the aggregate's
+// size as the unique count), dirty pages, memory-access bytes and edges.
+void PrintTestcaseRunStats(const LaneResult &L, size_t AggregateCoverage);
+
 struct RunnerOptions {
   std::string mode = "run";  // run | fuzz | master
   std::string name;          // target name
@@ -141,7 +153,7 @@ struct RunnerOptions {
   uint64_t limit = 0;
   uint32_t lanes = 1;
   uint32_t overlay_pages = 32;
-  uint64_t runs = 0;         // fuzz: testcases
+  uint64_t runs = 0;         // fuzz: testcases; run: repetitions of each input (subcommands.cc:85-88)
   double seconds = 0;        // fuzz: wall-clock budget (0 = none)
   uint64_t seed = 1337;
   uint64_t max_len = 0x1000;
