@@ -407,6 +407,10 @@ int wtfgpu_coverage_device_map(wtfgpu_ctx *ctx, void **dev_ptr, uint64_t *bytes)
  * wtfgpu_commit_coverage calls, sorted; *n gets the count. cap = 0 only
  * counts; a call with cap >= that count also marks them seen. */
 int wtfgpu_coverage_absorb(wtfgpu_ctx *ctx, uint64_t *rips, uint64_t cap, uint64_t *n);
+/* MAX a device buffer of the map's size (another shard set's merged map,
+ * RCCL all-reduce result) into the coverage map; wtfgpu_coverage_absorb then
+ * reports what it added. Returns when done. */
+int wtfgpu_coverage_merge_in(wtfgpu_ctx *ctx, const void *dev_src, uint64_t bytes);
 /* Host copy of the coverage map's set bytes as RIPs. */
 int wtfgpu_coverage_rips(wtfgpu_ctx *ctx, uint64_t *rips, uint64_t cap, uint64_t *n);
 

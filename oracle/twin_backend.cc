@@ -10,6 +10,7 @@
 // (one process per host core, bench.py). The product never links this file.
 #include "../wtf_amd/host/unimpl_hist.h"
 #include "../wtf_amd/host/module_instances.h"
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <unordered_map>
@@ -309,6 +310,11 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
     return added;
   }
   std::vector<uint64_t> extra_new_;  // aggregate values outside the map since TakeNewExtra
+  size_t MergeCoverageMap(const uint8_t *Merged, uint64_t Bytes, bool Device) override {
+    if (Device || Bytes != map_.size()) return 0;
+    for (uint64_t i = 0; i < Bytes; i++) map_[i] = std::max(map_[i], Merged[i]);
+    return AbsorbCoverageMap();
+  }
   size_t AbsorbCoverageMap() override {
     size_t added = 0;
     for (size_t i = 0; i < map_.size(); i++)
@@ -460,6 +466,7 @@ int main(int argc, char **argv) {
     std::string StatsJson() const override { return b->StatsJson(); }
     bool CoverageMap(uint8_t **M, uint64_t *N, bool *D) override { return b->CoverageMap(M, N, D); }
     size_t AbsorbCoverageMap() override { return b->AbsorbCoverageMap(); }
+    size_t MergeCoverageMap(const uint8_t *M, uint64_t N, bool D) override { return b->MergeCoverageMap(M, N, D); }
     void TakeNewExtra(std::vector<uint64_t> &O) override { b->TakeNewExtra(O); }
     size_t AbsorbExtra(const std::vector<uint64_t> &A) override { return b->AbsorbExtra(A); }
     bool EnableTrace(uint32_t P) override { return b->EnableTrace(P); }

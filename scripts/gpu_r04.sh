@@ -2,7 +2,7 @@
 #   scripts/gpu_r04.sh <tag> ["<pytest selection>"] [bench args...]
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
-tag=$1; sel=${2:-tests}; shift 2
+tag=$1; sel=${2:-tests}; shift; [ $# -gt 0 ] && shift
 timeout -k 10 900 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu $sel > gpurun_out/${tag}_pytest.txt 2>&1
 rc=$?
 echo "pytest rc=$rc"; grep -E " passed| failed" gpurun_out/${tag}_pytest.txt | tail -2

@@ -75,7 +75,10 @@ def test_gpu_missing_packet_page_is_engine_error(targets, tmp_path):
     t = targets["none"]
     a = H.run(H.TWIN, t, os.path.join(t, "parity"), str(tmp_path / "t.jsonl"), lanes=64)
     b = H.run(H.WTFGPU, t, os.path.join(t, "parity"), str(tmp_path / "g.jsonl"), lanes=512)
-    _cmp(a, b, ("result", "crash", "error", "icount", "gprs"))
+    _cmp(a, b, ("result", "crash", "error", "icount"))
+    # the registers of a testcase abandoned mid-handler are the handler's
+    # partial work (the reference node stops there): compared where it finished
+    _cmp([r for r in a if not r["error"]], [r for r in b if not r["error"]], ("gprs",))
     # the fuzz loop goes on, and keeps the testcases under errors/
     st = H.fuzz(H.WTFGPU, t, runs=4096, lanes=512, timeout=120)
     assert st["execs"] == 4096 and st["errors"] > 0 and st["backend"]["err_handler"] == st["errors"]

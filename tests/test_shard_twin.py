@@ -4,8 +4,9 @@ RCCL, rccl_exchange.cc): two `wtf_twin fuzz` ranks, each an independent shard
 through the node's CoverageExchange_t (TCP on the CPU, net_exchange.cc).
 
   * both ranks end with the same aggregate coverage: the union;
-  * each rank absorbed rips the other one found (merged_rips > 0) and kept
-    only its own testcases in its corpus;
+  * rips one rank found reached the other (merged_rips > 0 somewhere; merges
+    are absorbed one step after they start), and each kept only its own
+    testcases in its corpus;
   * the union is at least what either shard alone covers.
 """
 import json
@@ -62,7 +63,9 @@ def test_two_twin_shards_merge_coverage(base, tmp_path):
     assert all(p.returncode == 0 for p in procs)
     assert [r["rank"] for r in res] == [0, 1] and all(r["world"] == 2 for r in res)
     assert res[0]["coverage"] == res[1]["coverage"]
-    assert all(r["merged_rips"] > 0 for r in res)
+    # merges are absorbed one step after they start: a shard may find what the
+    # other found in the meantime itself, but the two cannot both miss out
+    assert sum(r["merged_rips"] for r in res) > 0
     # corpora stay per shard: rank 1's seed differs, so its corpus differs
     c0, c1 = (set(os.listdir(os.path.join(d, "outputs"))) for d in dirs)
     assert c0 != c1

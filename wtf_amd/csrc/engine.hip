@@ -1762,6 +1762,16 @@ __global__ void k_cov_absorb(const u8 *map, u8 *shadow, u64 n16, u64 *out_idx, u
   if (write) ((uint4 *)shadow)[t] = m;
 }
 
+// A merged map from the other shards (bytes are 0 / 1, so OR is the MAX):
+// the deferred shard merge (CoverageExchange_t::MergeEnd); k_cov_absorb then
+// reports what it added.
+__global__ void k_cov_merge_in(uint4 *map, const uint4 *src, u64 n16) {
+  const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n16) return;
+  const uint4 a = map[t], b = src[t];
+  if ((b.x & ~a.x) | (b.y & ~a.y) | (b.z & ~a.z) | (b.w & ~a.w)) map[t] = uint4{a.x | b.x, a.y | b.y, a.z | b.z, a.w | b.w};
+}
+
 // Per-lane feed regions (streaming): `n` lanes, lane lanes[i] gets
 // len[i] bytes from src + off[i] at its region.
 __global__ void k_feed_scatter(u8 *feed, u64 stride, const u32 *lanes, const u64 *off, const u64 *len, u32 n,
@@ -3522,6 +3532,18 @@ int wtfgpu_coverage_absorb(wtfgpu_ctx *c, uint64_t *rips, uint64_t cap, uint64_t
     for (u64 i = 0; i < m; i++) rips[i] = (c->code_vpns[idx[i] / WTFGPU_PAGE_SIZE] << 12) | (idx[i] % WTFGPU_PAGE_SIZE);
   }
   *n = total;
+  return WTFGPU_OK;
+}
+
+int wtfgpu_coverage_merge_in(wtfgpu_ctx *c, const void *dev_src, uint64_t bytes) {
+  if (!c || (bytes && !dev_src)) return WTFGPU_ERR_INVALID;
+  if (!c->d_covmap || !c->ncovslots) return bytes ? WTFGPU_ERR_INVALID : WTFGPU_OK;
+  const u64 mb = c->ncovslots * WTFGPU_PAGE_SIZE, n16 = mb / 16;
+  if (bytes != mb) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  k_cov_merge_in<<<(u32)((n16 + 255) / 256), 256, 0, c->stream>>>((uint4 *)c->d_covmap, (const uint4 *)dev_src, n16);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
   return WTFGPU_OK;
 }
 

@@ -121,6 +121,10 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   std::string StatsJson() const override;
   bool CoverageMap(uint8_t **Map, uint64_t *Bytes, bool *Device) override;
   size_t AbsorbCoverageMap() override;
+  size_t MergeCoverageMap(const uint8_t *Merged, uint64_t Bytes, bool Device) override {
+    if (!Device || wtfgpu_coverage_merge_in(ctx_, Merged, Bytes) != WTFGPU_OK) return 0;
+    return AbsorbCoverageMap();
+  }
   bool EnableTrace(uint32_t PerLane) override {
     trace_cap_ = PerLane;
     return ctx_ && wtfgpu_set_trace(ctx_, PerLane) == WTFGPU_OK;

@@ -100,6 +100,7 @@ int wtfnode_summary_json(wtfnode *n, char *buf, uint64_t cap) {
 
 int wtfnode_close(wtfnode *n) {
   if (!n) return 0;
+  if (n->F && n->X && n->X->World() > 1) n->F->FinishMerge();  // the merge the last step started (collective)
   n->F.reset();
   n->X.reset();
   delete n;  // the backend stays (process lifetime, as g_Backend in the reference)

@@ -27,6 +27,15 @@ struct RcclExchange_t::Impl {
   uint8_t *flag = nullptr;       // device byte for AllDone
   uint64_t *gbuf = nullptr;      // AllGatherV staging: world counts, then world * cap values
   uint64_t gcap = 0;             // u64 slots in gbuf
+  // deferred merge: the reduced map, the (flag | count, values) blocks sent /
+  // received (device and pinned host), the event MergeEnd waits for, and the
+  // overflow values still to send
+  uint8_t *merged = nullptr;
+  uint64_t merged_bytes = 0, merged_cap = 0;
+  uint64_t *dsend = nullptr, *drecv = nullptr, *hsend = nullptr, *hrecv = nullptr;
+  hipEvent_t ev = nullptr;
+  bool inflight = false;
+  std::vector<uint64_t> carry;
 };
 
 bool RcclUniqueId(uint8_t Out[kRcclIdBytes]) {
@@ -61,7 +70,14 @@ bool RcclIdViaFile(const std::string &Path, int Rank, uint8_t Id[kRcclIdBytes], 
 RcclExchange_t::RcclExchange_t(int Rank, int World) : rank_(Rank), world_(World), impl_(new Impl) {}
 
 RcclExchange_t::~RcclExchange_t() {
+  if (impl_->stream) (void)hipStreamSynchronize(impl_->stream);  // a merge still in flight completes (every rank issued it)
   if (impl_->comm) ncclCommDestroy(impl_->comm);
+  if (impl_->merged) (void)hipFree(impl_->merged);
+  if (impl_->dsend) (void)hipFree(impl_->dsend);
+  if (impl_->drecv) (void)hipFree(impl_->drecv);
+  if (impl_->hsend) (void)hipHostFree(impl_->hsend);
+  if (impl_->hrecv) (void)hipHostFree(impl_->hrecv);
+  if (impl_->ev) (void)hipEventDestroy(impl_->ev);
   if (impl_->flag) (void)hipFree(impl_->flag);
   if (impl_->gbuf) (void)hipFree(impl_->gbuf);
   if (impl_->stream) (void)hipStreamDestroy(impl_->stream);
@@ -142,6 +158,78 @@ bool RcclExchange_t::AllGatherV(const std::vector<uint64_t> &Mine, std::vector<u
     return false;
   All.clear();
   for (uint64_t r = 0; r < W; r++) All.insert(All.end(), got.begin() + r * cap, got.begin() + r * cap + counts[r]);
+  return true;
+}
+
+bool RcclExchange_t::MergeBegin(const uint8_t *Map, uint64_t Bytes, bool Device, const std::vector<uint64_t> &Extras,
+                                bool Done) {
+  Impl &I = *impl_;
+  if (world_ <= 1) {  // nothing to exchange: the result is this shard's own
+    merged_extra_ = Extras;
+    merged_done_ = Done;
+    I.merged_bytes = 0;
+    I.inflight = true;
+    return true;
+  }
+  if (!Device || !I.comm || I.inflight) return false;
+  const uint64_t W = (uint64_t)world_, B = kMergeCap + 1;
+  if (!I.dsend) {  // sized once: no allocation (and no device-wide sync) during a run
+    if (hipMalloc((void **)&I.dsend, B * 8) != hipSuccess || hipMalloc((void **)&I.drecv, W * B * 8) != hipSuccess ||
+        hipHostMalloc((void **)&I.hsend, B * 8) != hipSuccess || hipHostMalloc((void **)&I.hrecv, W * B * 8) != hipSuccess ||
+        hipEventCreateWithFlags(&I.ev, hipEventDisableTiming) != hipSuccess)
+      return false;
+  }
+  if (Bytes > I.merged_cap) {  // the map's size is fixed after set_code_pages: the first merge sizes it
+    if (I.merged) (void)hipFree(I.merged);
+    I.merged = nullptr;
+    I.merged_cap = 0;
+    if (hipMalloc((void **)&I.merged, Bytes) != hipSuccess) return false;
+    I.merged_cap = Bytes;
+  }
+  I.merged_bytes = Bytes;
+  I.carry.insert(I.carry.end(), Extras.begin(), Extras.end());
+  const uint64_t k = std::min<uint64_t>(I.carry.size(), kMergeCap);
+  // done only once nothing is left to send
+  I.hsend[0] = k | ((Done && I.carry.size() == k) ? 1ull << 63 : 0);
+  if (k) memcpy(I.hsend + 1, I.carry.data(), k * 8);
+  I.carry.erase(I.carry.begin(), I.carry.begin() + (std::ptrdiff_t)k);
+  if (hipMemcpyAsync(I.dsend, I.hsend, (1 + k) * 8, hipMemcpyHostToDevice, I.stream) != hipSuccess) return false;
+  if (ncclGroupStart() != ncclSuccess) return false;
+  if (Bytes && ncclAllReduce(Map, I.merged, Bytes, ncclUint8, ncclMax, I.comm, I.stream) != ncclSuccess) return false;
+  if (ncclAllGather(I.dsend, I.drecv, B, ncclUint64, I.comm, I.stream) != ncclSuccess) return false;
+  if (ncclGroupEnd() != ncclSuccess) return false;
+  if (hipMemcpyAsync(I.hrecv, I.drecv, W * B * 8, hipMemcpyDeviceToHost, I.stream) != hipSuccess ||
+      hipEventRecord(I.ev, I.stream) != hipSuccess)
+    return false;
+  I.inflight = true;
+  return true;
+}
+
+bool RcclExchange_t::MergeEnd(const uint8_t **Merged, uint64_t *Bytes, std::vector<uint64_t> &AllExtras,
+                              bool *AllDone) {
+  Impl &I = *impl_;
+  if (!I.inflight) return false;
+  I.inflight = false;
+  if (world_ <= 1) {
+    AllExtras.swap(merged_extra_);
+    merged_extra_.clear();
+    *AllDone = merged_done_;
+    *Merged = nullptr;
+    *Bytes = 0;
+    return true;
+  }
+  if (hipEventSynchronize(I.ev) != hipSuccess) return false;
+  const uint64_t W = (uint64_t)world_, B = kMergeCap + 1;
+  AllExtras.clear();
+  bool all = true;
+  for (uint64_t r = 0; r < W; r++) {
+    const uint64_t h = I.hrecv[r * B], k = std::min<uint64_t>(h & ~(1ull << 63), kMergeCap);
+    all = all && (h >> 63);
+    AllExtras.insert(AllExtras.end(), I.hrecv + r * B + 1, I.hrecv + r * B + 1 + k);
+  }
+  *AllDone = all;
+  *Merged = I.merged;
+  *Bytes = I.merged_bytes;
   return true;
 }
 

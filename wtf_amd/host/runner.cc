@@ -538,15 +538,17 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
     printf("Nothing to run: empty corpus and no inputs\n");
     return 1;
   }
+  const bool Shards = X && X->World() > 1;
   for (;;) {
-    bool done = F.Done();
-    if (X && X->World() > 1 && !X->AllDone(done, &done)) return 1;  // every shard stops together
-    if (done) break;
+    // shards stop together, on the consensus of the last merge absorbed
+    // (every shard absorbs the same one at the same step)
+    if (Shards ? F.AllDone() : F.Done()) break;
     if (!F.Step()) {
       printf("RunBatch failed\n");
       return 1;
     }
   }
+  if (Shards && !F.FinishMerge()) return 1;
   F.FlushFiles();
   printf("%s\n", F.SummaryJson().c_str());
   return 0;
@@ -766,7 +768,7 @@ bool FuzzSession::Step() {
   // shards' merges, and one that is not always reaches its own merge below
   // (two reads could disagree under --seconds and skip a collective)
   const bool done = Done();
-  if (X_ && X_->World() > 1 && done) return MergeCoverage();
+  if (X_ && X_->World() > 1 && done) return MergeCoverage(true);
   if (stream_) {
     const auto tc = Clock::now();
     const bool ok = StreamStep(done);
@@ -792,7 +794,7 @@ bool FuzzSession::Step() {
   TcBatch NextBatch;
   if (Next_.valid()) NextBatch = Next_.get();  // before the corpus / mutator change below
   for (size_t i = 0; i < BatchRefs_.size(); i++) Account(BatchRefs_[i].data(), BatchRefs_[i].size(), R[i]);
-  if (X_ && X_->World() > 1 && !MergeCoverage()) return false;
+  if (X_ && X_->World() > 1 && !MergeCoverage(false)) return false;
   if (!NextBatch.empty() || !More(S_.execs))
     Batch_ = std::move(NextBatch);
   else
@@ -873,7 +875,7 @@ bool FuzzSession::StreamStep(bool Done) {
     InFlight_--;
   }
   S_.account_ms += secs_since(ta) * 1e3;
-  if (X_ && X_->World() > 1 && !MergeCoverage()) return false;
+  if (X_ && X_->World() > 1 && !MergeCoverage(false)) return false;
   S_.step_ms += secs_since(t_step) * 1e3;
   return true;
 }
@@ -928,21 +930,68 @@ void FuzzSession::Account(const uint8_t *Tc, size_t Size, const LaneResult &L, b
 // every shard's coverage map, MAX-reduced over the shards; the
 // rips other shards found join this shard's aggregate (so its lanes stop
 // reporting them as new). Testcases stay with the shard that found them.
-bool FuzzSession::MergeCoverage() {
+// Deferred by one step (CoverageExchange_t::MergeBegin / MergeEnd): the merge
+// a step starts runs while the next step's kernels do, and is absorbed at the
+// start of the following merge. Every shard starts one merge per step.
+bool FuzzSession::MergeCoverage(bool Done) {
   const auto t = Clock::now();
+  if (!AbsorbMerge()) return false;
   uint8_t *Map = nullptr;
   uint64_t Bytes = 0;
   bool Device = false;
   if (!Exec_.CoverageMap(&Map, &Bytes, &Device)) return false;
-  if (Bytes && !X_->AllReduceMax(Map, Bytes, Device)) return false;
-  S_.merged_rips += Exec_.AbsorbCoverageMap();
-  // the values outside the map (SURVEY 8(e)'s overflow list): every shard's
-  // new ones, gathered, joined on the host
-  std::vector<uint64_t> Mine, All;
+  // the values outside the map (SURVEY 8(e)'s overflow list): this shard's new ones
+  std::vector<uint64_t> Mine;
   Exec_.TakeNewExtra(Mine);
-  if (!X_->AllGatherV(Mine, All)) return false;
-  S_.merged_rips += Exec_.AbsorbExtra(All);
+  if (!X_->MergeBegin(Map, Bytes, Device, Mine, Done)) return false;
+  MergePending_ = true;
   S_.merge_ms += secs_since(t) * 1e3;
+  return true;
+}
+
+bool FuzzSession::AbsorbMerge() {
+  if (!MergePending_) return true;
+  MergePending_ = false;
+  const uint8_t *Merged = nullptr;
+  uint64_t Bytes = 0;
+  std::vector<uint64_t> All;
+  bool Every = false;
+  if (!X_->MergeEnd(&Merged, &Bytes, All, &Every)) return false;
+  uint8_t *Map = nullptr;
+  uint64_t MapBytes = 0;
+  bool Device = false;
+  if (!Exec_.CoverageMap(&Map, &MapBytes, &Device)) return false;
+  if (Bytes && Bytes == MapBytes) S_.merged_rips += Exec_.MergeCoverageMap(Merged, Bytes, Device);
+  S_.merged_rips += Exec_.AbsorbExtra(All);
+  AllDone_ = Every;
+  return true;
+}
+
+bool FuzzSession::FinishMerge() {
+  const auto t = Clock::now();
+  const bool ok = AbsorbMerge();
+  S_.merge_ms += secs_since(t) * 1e3;
+  return ok;
+}
+
+// ---- CoverageExchange_t's default deferred merge: the synchronous collectives
+bool CoverageExchange_t::MergeBegin(const uint8_t *Map, uint64_t Bytes, bool Device,
+                                    const std::vector<uint64_t> &Extras, bool Done) {
+  if (Device) return false;  // device maps: an exchange with its own MergeBegin (RCCL)
+  merged_.assign(Map, Map + Bytes);
+  merged_device_ = false;
+  if (Bytes && !AllReduceMax(merged_.data(), Bytes, false)) return false;
+  if (!AllGatherV(Extras, merged_extra_)) return false;
+  return AllDone(Done, &merged_done_);
+}
+
+bool CoverageExchange_t::MergeEnd(const uint8_t **Merged, uint64_t *Bytes, std::vector<uint64_t> &AllExtras,
+                                  bool *AllDone) {
+  *Merged = merged_.data();
+  *Bytes = merged_.size();
+  AllExtras.swap(merged_extra_);
+  merged_extra_.clear();
+  *AllDone = merged_done_;
   return true;
 }
 

@@ -102,6 +102,9 @@ class Executor_t {
   // Rips set in the map (after a merge) that the aggregate lacks join it;
   // returns how many.
   virtual size_t AbsorbCoverageMap() { return 0; }
+  // A merged map (CoverageExchange_t::MergeEnd: host or device memory, as
+  // CoverageMap's) is MAX-ed into this executor's map, then absorbed as above.
+  virtual size_t MergeCoverageMap(const uint8_t *, uint64_t, bool) { return 0; }
   // Coverage values outside the map (rips on pages outside the slot table,
   // --edges values; SURVEY 8(e)'s overflow list): the ones this shard added
   // to its aggregate since the last call are moved into Out; AbsorbExtra adds
@@ -137,6 +140,24 @@ class CoverageExchange_t {
   // All = the concatenation of every shard's Mine, in rank order (the
   // overflow list of coverage values outside the map)
   virtual bool AllGatherV(const std::vector<uint64_t> &Mine, std::vector<uint64_t> &All) = 0;
+
+  // The deferred merge of one node step (collective, every shard every step):
+  // MergeBegin starts the MAX all-reduce of Map into the exchange's own buffer
+  // and the all-gather of (Done, Extras); MergeEnd, called before the next
+  // MergeBegin, waits for them and hands out the merged map (host or device
+  // memory like Map, valid until the next MergeBegin), every shard's extras
+  // in rank order and whether every shard was done. Nothing waits in the step
+  // that starts a merge; its result is absorbed one step later. This default
+  // runs the synchronous collectives above inside MergeBegin (the TCP twins);
+  // RcclExchange_t overlaps them with the step on a stream of their own.
+  virtual bool MergeBegin(const uint8_t *Map, uint64_t Bytes, bool Device, const std::vector<uint64_t> &Extras,
+                          bool Done);
+  virtual bool MergeEnd(const uint8_t **Merged, uint64_t *Bytes, std::vector<uint64_t> &AllExtras, bool *AllDone);
+
+ protected:
+  std::vector<uint8_t> merged_;       // the default MergeBegin's result
+  std::vector<uint64_t> merged_extra_;
+  bool merged_done_ = false, merged_device_ = false;
 };
 
 // BochscpuRunStats_t::Print (bochscpu_backend.h:25-37; NumberToHuman /
@@ -261,6 +282,11 @@ class FuzzSession {
   bool Start();      // corpus inputs + the first batch; false = nothing to run
   bool Step();       // one batch; false = the executor failed
   bool Done() const;
+  // shards (world > 1): every shard was done as of the last merge absorbed
+  // (the loop's collective stop decision); FinishMerge absorbs the merge
+  // still in flight (collective: every shard calls it once, at the end)
+  bool AllDone() const { return AllDone_; }
+  bool FinishMerge();
   const FuzzStats &Stats() const { return S_; }
   size_t CorpusSize() const { return Corpus_.Size(); }
   double WallSeconds() const;
@@ -272,7 +298,9 @@ class FuzzSession {
   void Adopt(TcBatch &&B);  // streaming: the batch's testcases join the ready queue
   uint64_t Budget(uint64_t n) const;
   bool More(uint64_t done) const;
-  bool MergeCoverage();
+  bool MergeCoverage(bool Done);
+  bool AbsorbMerge();  // MergeEnd of the merge in flight, absorbed
+  bool MergePending_ = false, AllDone_ = false;
   void WriteSample(const uint8_t *Tc, size_t Size, const LaneResult &L);
   FILE *Sample_ = nullptr;
   bool StreamStep(bool Done);
