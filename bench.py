@@ -132,15 +132,25 @@ def build_target(name: str, d: str) -> str:
     return d
 
 
+def engine_sha16() -> str:
+    """The engine build (libwtfgpu.so) this run uses: PMC summaries carry the
+    hash of the build they were measured on."""
+    import hashlib
+
+    with open(os.path.join(ROOT, "wtf_amd", "csrc", "libwtfgpu.so"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def load_pmc(name: str, lanes: int, limit: int) -> dict | None:
     """The committed rocprofv3 PMC summary of k_run on this workload (made by
-    scripts/pmc_summary.py from the profiles/ CSVs), if its config matches."""
+    scripts/pmc_summary.py), if its config matches and it was measured on this
+    very engine build (engine_sha16); else None (traffic / valu / wait null)."""
     p = os.path.join(PROFILES, f"pmc_{name}_k_run.json")
     try:
         pmc = json.load(open(p))
     except (OSError, ValueError):
         return None
-    if pmc.get("lanes") != lanes or pmc.get("limit") != limit:
+    if pmc.get("lanes") != lanes or pmc.get("limit") != limit or pmc.get("engine_sha16") != engine_sha16():
         return None
     return pmc
 
@@ -402,7 +412,9 @@ def run(a, rank, world, local, tmp):
     fields = node_fields(s0, s1)
     summary = node.summary()
     # the timed steps' share of every node / backend counter (summary - summary before)
-    timed = {k: round(v - sum0[k], 3) for k, v in summary.items() if isinstance(v, (int, float)) and k in sum0}
+    # (counters only: a difference of two rates means nothing)
+    timed = {k: round(v - sum0[k], 3) for k, v in summary.items()
+             if isinstance(v, (int, float)) and k in sum0 and not k.endswith("_per_s")}
     timed["backend"] = {k: round(v - sum0["backend"][k], 3) for k, v in summary["backend"].items()
                         if isinstance(v, (int, float)) and k in sum0["backend"]}
     node.close()
@@ -429,7 +441,8 @@ def run(a, rank, world, local, tmp):
                        "regroup_auto": "off while a run retires >= 56 lanes per wave-step, on again below 40",
                        "mutation": MUTATION,
                        "parallelism": f"shard{world}: one node per GPU (seed + rank), RCCL MAX coverage-map "
-                                      f"merge per batch"},
+                                      f"merge started every step, absorbed the next"},
+            "build": {"engine_sha16": engine_sha16()},
             "instr_per_exec": retired / max(1.0, execs),
             "roofline": roofline(fields["alg_bytes"], fields["kernel_launches"], fields["kernel_ms"],
                                  load_pmc("tlv", a.lanes, a.limit)),

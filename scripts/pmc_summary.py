@@ -6,9 +6,11 @@ WRITE_SIZE are in KB; on gfx950 FETCH_SIZE reports half the bytes of a wide
 coalesced read, so it is doubled (k_run's reads are not all wide streams: the
 corrected read side is an upper bound, the raw one a lower bound).
 valu_util = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES, wait_frac = SQ_WAIT_ANY /
-SQ_WAVE_CYCLES (both summed over k_run dispatches)."""
+SQ_WAVE_CYCLES (both summed over k_run dispatches). engine_sha16 binds the
+summary to the libwtfgpu.so it was measured on."""
 import csv
 import glob
+import hashlib
 import json
 import os
 import sys
@@ -39,8 +41,11 @@ for f in glob.glob(os.path.join(d, "stats", "**", "*kernel_stats.csv"), recursiv
 fetch_b = fetch.get("FETCH_SIZE", 0) * 1024 / nf
 write_b = write.get("WRITE_SIZE", 0) * 1024 / nw
 cyc = wait.get("SQ_WAVE_CYCLES", 0)
+ENGINE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "wtf_amd", "csrc", "libwtfgpu.so")
 summary = {
     "kernel": "k_run",
+    # the engine build these counters were taken on (bench.py drops a summary of another build)
+    "engine_sha16": hashlib.sha256(open(ENGINE, "rb").read()).hexdigest()[:16],
     "leg": leg,
     "lanes": lanes,
     "limit": limit,
