@@ -150,10 +150,18 @@ int sim_run_full(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, c
       FOp f;
       digest(d, f);
       if (fo_op(f) != FO_GENERIC) {
-        L.miss = 0;
-        L.pend = 0;
-        fast_exec(P, L, f, grip + d.len, next);
-        if (!L.miss) {
+        bool done = false;
+        for (int fills = 0;; fills++) {  // k_run: a TLB miss / first write served in place (fast_fill)
+          L.miss = 0;
+          L.pend = 0;
+          fast_exec(P, L, f, grip + d.len, next);
+          if (!L.miss) {
+            done = true;
+            break;
+          }
+          if (L.miss != 2 || fills >= 3 || !fast_fill(P, L)) break;
+        }
+        if (done) {
           if (fast_count) ++*fast_count;
           L.rip = next;
           L.icount++;

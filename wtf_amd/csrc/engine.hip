@@ -1140,11 +1140,19 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       have = false;
       if (ing) {
         skip = false;
-        L.miss = 0;
-        L.pend = 0;
         const u32 len = fo_len(f);
         u64 next;
-        fast_exec(P, L, f, grip + len, next);
+        // a TLB miss or a first write (fxlate: miss 2) is served here, on the
+        // lane in registers, and the instruction retried at once, so the group
+        // still takes one wave-step (at most 3 fills); anything else (a fault
+        // to raise, a page-table write, a page-crossing operand, ...) is left
+        // to the slow step, whose exec() raises what it raises
+        for (u32 fills = 0;; fills++) {
+          L.miss = 0;
+          L.pend = 0;
+          fast_exec(P, L, f, grip + len, next);
+          if (!L.miss || L.miss != 2 || fills >= 3 || !fast_fill(P, L)) break;
+        }
         if (!L.miss) {
           L.rip = next;
           L.icount++;
@@ -1152,8 +1160,8 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
           if (P.limit && L.icount > P.limit) L.status = WTFGPU_EXIT_TIMEOUT;
         }
       }
-      // lanes that missed keep their rip: the slow step services them. The
-      // attempt is not a wave-step of its own (the slow step counts the
+      // lanes that still missed keep their rip: the slow step services them.
+      // The attempt is not a wave-step of its own (the slow step counts the
       // group once): a slice's length in wave-steps must not depend on which
       // path ran a group, since that depends on when other queues' coverage
       // commits landed (U44: fixed-seed campaigns reproduce)
@@ -1215,7 +1223,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     if (flags & (UC_CROSS | UC_BADLEN)) {
       if (flags & UC_BADLEN) {
         if (ing) set_fault(L, WTFGPU_VEC_GP, 0, 0);
-      } else {
+      } else if (valid) {  // a position with no lane has no copy slot of its own
         WITH_LANE_COPY(slow_step(P, T, grip, lptr, ing, skip));
       }
       STAMP(5);

@@ -146,11 +146,13 @@ __device__ __forceinline__ bool perm_ok(const Lane &L, u64 td, int acc) {
 }
 
 // 4-level walk through the lane's physical view (kdmp-parser.h:269-345 shape,
-// SDM permission bits accumulated). No A/D updates (U8). Faults set on L.
+// SDM permission bits accumulated). No A/D updates (U8). Faults set on L
+// (kFault); without kFault a walk that would fault only returns false.
+template <bool kFault = true>
 __device__ __forceinline__ bool walk(const Dev &P, Lane &L, u64 va, int acc, u64 &td, u64 &gpfn) {
   const bool nxe = (L.efer >> 11) & 1;
   if (!canonical(va)) {
-    set_fault(L, WTFGPU_VEC_GP, 0, va);
+    if (kFault) set_fault(L, WTFGPU_VEC_GP, 0, va);
     return false;
   }
   u64 table = L.cr3 & 0x000ffffffffff000ull;
@@ -162,7 +164,7 @@ __device__ __forceinline__ bool walk(const Dev &P, Lane &L, u64 va, int acc, u64
     const u8 *pg = phys_page(P, L.lane, L.ovn, L.bloom, table >> 12, priv);
     e = *(const u64 *)(pg + idx * 8);
     if (!(e & 1)) {
-      set_fault(L, WTFGPU_VEC_PF, pf_error(L, acc, false), va);
+      if (kFault) set_fault(L, WTFGPU_VEC_PF, pf_error(L, acc, false), va);
       return false;
     }
     aw &= (e & 2) != 0;
@@ -232,6 +234,28 @@ __device__ __forceinline__ bool service_miss(const Dev &P, Lane &L, u64 va, int 
       L.status = WTFGPU_EXIT_OVERLAY_FULL;
       return false;
     }
+    u8 *np = cow_copy(P, L.lane, L.ovn, gpfn, (const u8 *)(uintptr_t)(td & ~0xfffull));
+    L.ovn++;
+    L.bloom |= bloom_bit(gpfn);
+    tlb_flush(L);  // other vpns may alias the old page
+    td = (u64)(uintptr_t)np | (td & 0xfff) | T_PRIV;
+  }
+  tlb_put(L, va >> 12, td);
+  return true;
+}
+
+// The fast loop's own miss service (k_run): the TLB fill or first-write copy
+// service_miss would make, done in registers when it raises nothing. false =
+// the walk or the permission check would fault, the page is a page-table page
+// (exec() flushes after such a write) or the overlay is full: exec() in the
+// slow step then takes the instruction and raises exactly what it raises.
+__device__ __forceinline__ bool fast_fill(const Dev &P, Lane &L) {
+  const u64 va = L.miss_va;
+  const int acc = (int)L.miss_acc;
+  u64 td, gpfn;
+  if (!walk<false>(P, L, va, acc, td, gpfn) || !perm_ok(L, td, acc)) return false;
+  if (acc == ACC_W && !(td & T_PRIV)) {
+    if ((td & T_PT) || L.ovn >= P.K) return false;
     u8 *np = cow_copy(P, L.lane, L.ovn, gpfn, (const u8 *)(uintptr_t)(td & ~0xfffull));
     L.ovn++;
     L.bloom |= bloom_bit(gpfn);

@@ -221,12 +221,24 @@ __device__ __forceinline__ void wr(Lane &L, u32 r, u32 sz, u64 v) {
 
 // Fast translation: TLB hit with the permission already granted, and for a
 // write a private (copy-on-write done) page that is not a page-table page.
-// Everything else -> L.miss, the slow step takes over.
+// A TLB miss or a first write to a shared page -> L.miss = 2 with the address:
+// k_run serves it in registers (fast_fill) and retries. Everything else ->
+// L.miss = 1, the slow step takes over.
 __device__ __forceinline__ u8 *fxlate(Lane &L, u64 va, u32 sz, int acc) {
   u64 td;
   const bool w = acc == ACC_W;
-  if ((va & 0xfff) + sz > 4096 || !tlb_get(L, va >> 12, td) || !perm_ok(L, td, acc) ||
-      (w && ((td & (T_PRIV | T_PT)) != T_PRIV))) {
+  if ((va & 0xfff) + sz > 4096) {
+    L.miss = 1;
+    return nullptr;
+  }
+  const bool hit = tlb_get(L, va >> 12, td);
+  if (!hit || (perm_ok(L, td, acc) && w && (td & (T_PRIV | T_PT)) == 0)) {
+    L.miss = 2;
+    L.miss_va = va;
+    L.miss_acc = (u32)acc;
+    return nullptr;
+  }
+  if (!perm_ok(L, td, acc) || (w && ((td & (T_PRIV | T_PT)) != T_PRIV))) {
     L.miss = 1;
     return nullptr;
   }
