@@ -248,6 +248,27 @@ int wtfgpu_read_stop_args(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n, ui
 int wtfgpu_set_feed(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, const uint64_t *offsets,
                     const uint8_t *has_feed, const uint8_t *bytes, uint64_t nbytes);
 
+/* Declared insert (no bochscpu counterpart; the data form of an
+ * InsertTestcase that only moves the testcase into registers and guest memory,
+ * fuzzer_hevd.cc:20-59). Once set (NULL: none), every feed upload
+ * (wtfgpu_set_feed, wtfgpu_set_feed_lanes) also inserts the feed of each lane
+ * that has one and is RUNNING, before it runs: the feed's first chunk is the
+ * testcase; its first 4 bytes (u32, zero-extended) go to gpr[head_reg], the
+ * rest (the payload) is written at gpr[ptr_reg] (dirty; as Backend_t::
+ * VirtWriteDirty: supervisor stores, only a missing translation fails), its
+ * size goes to gpr[len_reg] and, when len_arg != 0, as a u64 to
+ * rsp + 8 + 8 * len_arg (GetArgAddress(len_arg), backend.cc:160-168). A write
+ * that fails ends the lane with WTFGPU_EXIT_FEED_FAULT (an engine error, as
+ * the module's failed VirtWrite). The feed is consumed. Chunks shorter than 4
+ * bytes are left alone. */
+typedef struct wtfgpu_insert {
+  uint32_t head_reg;
+  uint32_t ptr_reg;
+  uint32_t len_reg;
+  uint32_t len_arg;
+} wtfgpu_insert_t;
+int wtfgpu_set_insert(wtfgpu_ctx *ctx, const wtfgpu_insert_t *ins);
+
 /* Coverage index space: code pages (gva >> 12) that get a 4096-byte slot in
  * the per-GPU coverage map. Pages outside it are still logged per lane. */
 int wtfgpu_set_code_pages(wtfgpu_ctx *ctx, const uint64_t *vpns, uint32_t n);

@@ -1,15 +1,26 @@
-"""Sums the per-launch `wtfgpu stamps` lines of a stamps build into cycles per wave-step."""
+"""Sums the per-launch `wtfgpu stamps` lines of a stamps build into cycles per
+wave-step, and the generic ops the slow step ran (O_* numbers of engine_ops.h)."""
 import re
 import sys
 
 PAT = re.compile(r"wtfgpu stamps \(cycles per wave-step, (\d+) steps\): fast loop (\S+), slow: xlate\+fill (\S+), "
                  r"coverage (\S+), exec (\S+), cross-page ([^;\s]+)(?:; slow steps: miss (\d+), codepage (\d+), "
                  r"ucmiss (\d+), other (\d+))?")
+OPS = ("ALU TEST MOV MOVZX MOVSX XCHG XADD CMPXCHG INCDEC NOT NEG SHIFT SHXD MULDIV IMUL BT BSF BSR TZCNT LZCNT "
+       "POPCNT CMOV SETCC BSWAP CBW CWD LAHF SAHF FLAGOP NOP JCC JMP CALL RET PUSH POP PUSHF POPF LEAVE STRING INT3 "
+       "HLT UD LEA SYS SSE UNIMPL SYS2 LOOP GEXT").split()
 for path in sys.argv[1:]:
     steps = 0
     tot = [0.0] * 5
     why = [0] * 4
+    ops = {}
     for line in open(path):
+        if line.startswith("wtfgpu stamps generic ops:"):
+            for kv in line.split(":", 1)[1].split():
+                k, v = kv.split(":")
+                name = OPS[int(k)] if int(k) < len(OPS) else k
+                ops[name] = ops.get(name, 0) + int(v)
+            continue
         m = PAT.search(line)
         if not m:
             continue
@@ -23,3 +34,5 @@ for path in sys.argv[1:]:
     names = ("fast", "xlate+fill", "coverage", "exec", "cross-page")
     print(path, "wave-steps", steps, {k: round(v / max(1, steps)) for k, v in zip(names, tot)},
           "slow steps", dict(zip(("miss", "codepage", "ucmiss", "other"), why)))
+    if ops:
+        print("  generic ops", dict(sorted(ops.items(), key=lambda kv: -kv[1])))

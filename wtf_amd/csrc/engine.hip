@@ -660,6 +660,44 @@ __device__ __forceinline__ void retire(const Dev &P, Lane &L, int x, u32 len, u6
 // translation stops it: the stores run as supervisor with CR0.WP clear, so
 // U/S and R/W are not checked. A missing page ends the lane with
 // WTFGPU_EXIT_FEED_FAULT, where the module's handler aborts.
+// A host-side VirtWriteDirty of n bytes at va (backend.cc:91-121): the stores
+// run as supervisor with CR0.WP clear (translation with ValidateRead: only a
+// missing translation stops it), through copy-on-write, 8 bytes at a time and
+// then single bytes. false = a page did not translate: the lane ends with
+// WTFGPU_EXIT_FEED_FAULT (the host handler's failed write, U43).
+__device__ __noinline__ bool host_write(const Dev &P, Lane &L, u64 va, const u8 *src, u64 n) {
+  const u32 cpl0 = L.cpl;
+  const u64 cr00 = L.cr0;
+  L.cpl = 0;
+  L.cr0 &= ~(1ull << 16);
+  for (u64 o = 0; o < n;) {
+    const u32 sz = n - o >= 8 ? 8 : 1;
+    u64 v = 0;
+    for (u32 i = 0; i < sz; i++) v |= (u64)src[o + i] << (8 * i);
+    for (int attempt = 0;; attempt++) {
+      L.miss = 0;
+      if (vwrite(L, va + o, sz, v)) break;
+      if (L.status != WTFGPU_RUNNING || !L.miss || !miss_service(P, L, attempt)) {
+        if (L.status == WTFGPU_RUNNING || L.status == WTFGPU_EXIT_FAULT) L.status = WTFGPU_EXIT_FEED_FAULT;
+        L.miss = 0;
+        L.pend = 0;
+        L.cpl = cpl0;
+        L.cr0 = cr00;
+        return false;
+      }
+    }
+    o += sz;
+  }
+  L.cpl = cpl0;
+  L.cr0 = cr00;
+  L.pend = 0;
+  if (L.flush) {
+    tlb_flush(L);
+    L.flush = 0;
+  }
+  return true;
+}
+
 __device__ __noinline__ bool feed_apply(const Dev &P, Lane &L, const wtfgpu_bp_action_t &a) {
   if (!P.feed_pos) return false;
   const u64 pos = P.feed_pos[L.lane];
@@ -678,38 +716,38 @@ __device__ __noinline__ bool feed_apply(const Dev &P, Lane &L, const wtfgpu_bp_a
   }
   const u32 rb = (u32)a.gprs[0] & 15, rn = (u32)a.gprs[1] & 15;
   const u64 dst = R(L, rb) + a.value - n;
-  const u32 cpl0 = L.cpl;
-  const u64 cr00 = L.cr0;
-  L.cpl = 0;
-  L.cr0 &= ~(1ull << 16);
-  for (u32 o = 0; o < n;) {
-    const u32 sz = n - o >= 8 ? 8 : 1;
-    u64 v = 0;
-    for (u32 i = 0; i < sz; i++) v |= (u64)src[4 + o + i] << (8 * i);
-    for (int attempt = 0;; attempt++) {
-      L.miss = 0;
-      if (vwrite(L, dst + o, sz, v)) break;
-      if (L.status != WTFGPU_RUNNING || !L.miss || !miss_service(P, L, attempt)) {
-        if (L.status == WTFGPU_RUNNING || L.status == WTFGPU_EXIT_FAULT) L.status = WTFGPU_EXIT_FEED_FAULT;
-        L.miss = 0;
-        L.pend = 0;
-        L.cpl = cpl0;
-        L.cr0 = cr00;
-        return true;
-      }
-    }
-    o += sz;
-  }
-  L.cpl = cpl0;
-  L.cr0 = cr00;
-  L.pend = 0;
-  if (L.flush) {
-    tlb_flush(L);
-    L.flush = 0;
-  }
+  if (!host_write(P, L, dst, src + 4, n)) return true;  // WTFGPU_EXIT_FEED_FAULT
   RS(L, rn, n);
   RS(L, rb, dst);
   return true;
+}
+
+// Declared insert (wtfgpu_set_insert; the data form of fuzzer_hevd.cc:20-59's
+// InsertTestcase): the lane's feed holds one chunk, the testcase; its first 4
+// bytes go to gpr[head_reg], the rest (the payload) is written at
+// gpr[ptr_reg], its size goes to gpr[len_reg] and, with len_arg, to
+// [rsp + 8 + 8 * len_arg] (GetArgAddress, backend.cc:160-168), in the order
+// the module does it. The feed is consumed. A write that does not translate
+// ends the lane with WTFGPU_EXIT_FEED_FAULT, where the host handler would
+// have failed (U43).
+__device__ __noinline__ void insert_apply(const Dev &P, Lane &L, const wtfgpu_insert_t &ins) {
+  const u64 pos = P.feed_pos[L.lane], end = P.feed_end[L.lane];
+  if (pos == ~0ull) return;
+  P.feed_pos[L.lane] = end;
+  if (pos + 8 > end) return;
+  const u8 *src = P.feed_data + pos;
+  const u32 n = (u32)src[0] | ((u32)src[1] << 8) | ((u32)src[2] << 16) | ((u32)src[3] << 24);
+  if (n < 4 || pos + 4 + n > end) return;
+  const u32 head = (u32)src[4] | ((u32)src[5] << 8) | ((u32)src[6] << 16) | ((u32)src[7] << 24);
+  const u64 m = n - 4;
+  RS(L, ins.head_reg & 15, head);
+  if (!host_write(P, L, R(L, ins.ptr_reg & 15), src + 8, m)) return;
+  RS(L, ins.len_reg & 15, m);
+  if (ins.len_arg) {
+    u8 le[8];
+    for (int i = 0; i < 8; i++) le[i] = (u8)(m >> (8 * i));
+    host_write(P, L, R(L, WTFGPU_RSP) + 8 + 8 * (u64)ins.len_arg, le, 8);
+  }
 }
 
 // Device-side breakpoint action (wtfgpu_set_breakpoint_actions) at `grip`.
@@ -1013,7 +1051,15 @@ struct LaneCopy {
 // code page changed, 2 the rip is not in the wave's LDS uop cache, 3 other
 // (generic op, breakpoint, coverage, code outside the pool)
 #define WHY(k) why_ = (k)
+// and which generic ops the slow step executed (O_* / O_SYS2 etc.), one count per
+// group, in stat[16..80)
+#define OPHIST(op) ophist_[(op) & 63]++
+constexpr u32 STAT_N = 80;
 #else
+constexpr u32 STAT_N = 16;
+#define OPHIST(op) \
+  do {             \
+  } while (0)
 #define STAMP(k) \
   do {           \
   } while (0)
@@ -1098,6 +1144,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
   u64 tprev_ = __builtin_amdgcn_s_memtime();
   u64 whyc_[4] = {0, 0, 0, 0};
   u32 why_ = 3;
+  u32 ophist_[64] = {};
 #endif
 
   for (;;) {
@@ -1258,6 +1305,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     // the UOp for the generic path (wave-uniform: the slot fill is a wave operation)
     const UOp *u = nullptr;
     if (__ballot(ing)) u = uc_uop(P, uu, key, lptr, off, grip, lid);
+    if (__ballot(ing) && !(flags & UC_UNSUP)) OPHIST(rfl32(u->op));
     if (ing && (flags & UC_UNSUP)) {
       const u32 ob = u->opbytes, n = len;
       L.status = WTFGPU_EXIT_UNIMPLEMENTED;
@@ -1317,6 +1365,8 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
 #ifdef WTFGPU_STAMPS
     for (int k = 0; k < 8; k++) atomicAdd((unsigned long long *)&P.stat[4 + k], (unsigned long long)stamp_[k]);
     for (int k = 0; k < 4; k++) atomicAdd((unsigned long long *)&P.stat[12 + k], (unsigned long long)whyc_[k]);
+    for (int k = 0; k < 64; k++)
+      if (ophist_[k]) atomicAdd((unsigned long long *)&P.stat[16 + k], (unsigned long long)ophist_[k]);
 #endif
   }
 }
@@ -1548,6 +1598,26 @@ __global__ void k_inject_fault(Dev P, const u32 *lanes, const u64 *addrs, u32 n,
     tlb_stale(P, lane);
     P.lflags[lane] = 0;
   }
+}
+
+// The declared insert of a lane list (wtfgpu_set_insert), after the feed
+// scatter: lanes without a feed are left alone. The writes are not CPU
+// accesses (Tenet does not log them).
+__global__ void k_insert(Dev P, wtfgpu_insert_t ins, const u32 *lanes, u32 first, u32 n) {
+  const u32 t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const u32 lane = lanes ? lanes[t] : first + t;
+  if (P.feed_pos[lane] == ~0ull || P.status[lane] != WTFGPU_RUNNING) return;
+  u32 glo[16], ghi[16];
+  Lane L;
+  L.glo = glo;
+  L.ghi = ghi;
+  load_lane(P, lane, L);
+  if (g_tn.buf) tn_mute(lane);
+  insert_apply(P, L, ins);
+  if (g_tn.buf) tn_unmute(lane, 0, 0, 0, false);
+  store_lane(P, L);
+  store_tlb(P, L);
 }
 
 // Lane status (+ skip-breakpoint-once flag) for a lane list (resume / stop).
@@ -1893,6 +1963,8 @@ struct wtfgpu_ctx {
   u8 *d_feeddata = nullptr;
   u64 feed_cap = 0;
   u64 feed_stride = 0;  // streaming: bytes of feed region per lane (0 = one packed feed)
+  bool ins_on = false;  // a declared insert (wtfgpu_set_insert) runs after each feed upload
+  wtfgpu_insert_t ins{};
   // coverage
   u64 *d_codekeys = nullptr;
   u32 *d_codeslot = nullptr;
@@ -2020,7 +2092,7 @@ int queue_create(QueueRes &q) {
   HIPCHK(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
   HIPCHK(hipEventCreate(&q.ev0));
   HIPCHK(hipEventCreate(&q.ev1));
-  if (dalloc(&q.d_stat, 16) || dalloc(&q.d_dev, 1)) return WTFGPU_ERR_OOM;
+  if (dalloc(&q.d_stat, STAT_N) || dalloc(&q.d_dev, 1)) return WTFGPU_ERR_OOM;
   return WTFGPU_OK;
 }
 void regroup_free(u32 *&k, u32 *&k2, u32 *&l, void *&t, size_t &tb) {
@@ -2573,10 +2645,23 @@ int wtfgpu_set_feed(wtfgpu_ctx *c, uint32_t first, uint32_t count, const uint64_
   if (nbytes) HIPCHK(hipMemcpyAsync(c->d_feeddata, bytes, nbytes, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->d_feedpos + first, pos.data(), count * 8ull, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->d_feedend + first, end.data(), count * 8ull, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
   c->P.feed_pos = c->d_feedpos;
   c->P.feed_end = c->d_feedend;
   c->P.feed_data = c->d_feeddata;
+  if (c->ins_on && count) {
+    k_insert<<<(count + 63) / 64, 64, 0, c->stream>>>(c->P, c->ins, nullptr, first, count);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_set_insert(wtfgpu_ctx *c, const wtfgpu_insert_t *ins) {
+  if (!c) return WTFGPU_ERR_INVALID;
+  if (ins && (ins->head_reg > 15 || ins->ptr_reg > 15 || ins->len_reg > 15 || ins->len_arg > 64))
+    return WTFGPU_ERR_INVALID;
+  c->ins_on = ins != nullptr;
+  if (ins) c->ins = *ins;
   return WTFGPU_OK;
 }
 
@@ -2705,6 +2790,10 @@ int wtfgpu_set_feed_lanes(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, cons
   c->P.feed_pos = c->d_feedpos;
   c->P.feed_end = c->d_feedend;
   c->P.feed_data = c->d_feeddata;
+  if (c->ins_on) {  // the declared insert of the listed lanes, ordered after the scatter
+    k_insert<<<(n + 63) / 64, 64, 0, c->stream>>>(c->P, c->ins, (const u32 *)c->d_scratch, 0, n);
+    HIPCHK(hipGetLastError());
+  }
   return WTFGPU_OK;
 }
 
@@ -2932,6 +3021,10 @@ static void print_stamps(const u64 *s) {
             (unsigned long long)s[0], (double)s[4] / s[0], (double)s[6] / s[0], (double)s[7] / s[0],
             (double)s[5] / s[0], (double)s[9] / s[0], (unsigned long long)s[12], (unsigned long long)s[13],
             (unsigned long long)s[14], (unsigned long long)s[15]);
+  fprintf(stderr, "wtfgpu stamps generic ops:");
+  for (int k = 0; k < 64; k++)
+    if (s[16 + k]) fprintf(stderr, " %d:%llu", k, (unsigned long long)s[16 + k]);
+  fprintf(stderr, "\n");
 #else
   (void)s;
 #endif
@@ -2963,7 +3056,7 @@ int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps
   u64 done = 0;
   float ms_total = 0;
   for (;;) {
-    HIPCHK(hipMemsetAsync(c->d_stat, 0, 16 * 8, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_stat, 0, STAT_N * 8, c->stream));
     HIPCHK(hipEventRecord(c->ev0, c->stream));
     u32 k = 0;
     for (; k < group && done < max_steps; k++) {
@@ -2972,7 +3065,7 @@ int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps
       done += steps;
     }
     HIPCHK(hipEventRecord(c->ev1, c->stream));
-    u64 s[16];
+    u64 s[STAT_N];
     HIPCHK(hipMemcpyAsync(s, c->d_stat, sizeof(s), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     float ms = 0;
@@ -3004,7 +3097,7 @@ int wtfgpu_run_async(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max
 #if WTFGPU_P_BYREF
   HIPCHK(hipMemcpyAsync(c->d_dev, &Q, sizeof(Dev), hipMemcpyHostToDevice, c->stream));
 #endif
-  HIPCHK(hipMemsetAsync(c->d_stat, 0, 16 * 8, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_stat, 0, STAT_N * 8, c->stream));
   HIPCHK(hipEventRecord(c->ev0, c->stream));
   u32 k = 0;
   for (u64 done = 0; done < max_steps; done += chunk, k++) {
@@ -3020,7 +3113,7 @@ int wtfgpu_run_wait(wtfgpu_ctx *c, wtfgpu_run_stats_t *stats) {
   wtfgpu_run_stats_t st{};
   if (c->async_launches) {
     HIPCHK(hipSetDevice(c->device));
-    u64 s[16];
+    u64 s[STAT_N];
     HIPCHK(hipMemcpyAsync(s, c->d_stat, sizeof(s), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     float ms = 0;

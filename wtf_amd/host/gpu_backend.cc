@@ -245,10 +245,37 @@ bool GpuBackend_t::SetFeed(const uint8_t *Data, const uint64_t Size) {
   return true;
 }
 
+// InsertAction_t on the device (wtfgpu_set_insert): every feed upload also
+// inserts the lanes' testcases. Off with device actions off.
+bool GpuBackend_t::DeclareInsert(const InsertAction_t &Action) {
+  if (ModuleInstances::Registering() && ModuleInstances::Registering()->RegisteringIndex() > 0) return insert_action_;
+  const char *Env = getenv("WTFGPU_DEVICE_BP_ACTIONS");
+  if (Env && Env[0] == '0') return false;
+  const int h = gpr_index(Action.HeadReg), p = gpr_index(Action.PtrReg), l = gpr_index(Action.LenReg);
+  if (h < 0 || p < 0 || l < 0 || Action.LenArg > 64) return false;
+  const wtfgpu_insert_t I = {(uint32_t)h, (uint32_t)p, (uint32_t)l, Action.LenArg};
+  if (wtfgpu_set_insert(ctx_, &I) != WTFGPU_OK) return false;
+  insert_action_ = true;
+  return true;
+}
+
+// The testcase as the feed's one chunk (u32 size, bytes); the device applies
+// the declared insert to it before the lane runs.
+bool GpuBackend_t::SetInsert(const uint8_t *Data, const uint64_t Size) {
+  if (!insert_action_ || Size + 4 > kFeedRegion) return false;
+  LaneView &v = cur();
+  v.has_feed = true;
+  v.feed.resize(Size + 4);
+  const uint32_t n = (uint32_t)Size;
+  memcpy(v.feed.data(), &n, 4);
+  if (Size) memcpy(v.feed.data() + 4, Data, Size);
+  return true;
+}
+
 // One wtfgpu_set_feed call for lanes [0, n); lanes without SetFeed keep the
 // host handler.
 int GpuBackend_t::upload_feed(uint32_t n) {
-  if (!feed_action_ || n == 0) return WTFGPU_OK;
+  if (!(feed_action_ || insert_action_) || n == 0) return WTFGPU_OK;
   std::vector<uint64_t> off(n + 1);
   std::vector<uint8_t> has(n);
   uint64_t total = 0;
@@ -1402,7 +1429,7 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
     const auto tu = Clock::now();
     stats_.module_ms += std::chrono::duration<double, std::milli>(tu - tm).count();
     if (flush_lanes(fresh)) return false;
-    if (feed_action_) {
+    if (feed_action_ || insert_action_) {
       const auto tf = Clock::now();
       const size_t n = fresh.size();
       std::vector<uint64_t> off(n + 1, 0);

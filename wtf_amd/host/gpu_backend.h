@@ -88,6 +88,8 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   bool PhysWriteDirect(const Gpa_t Gpa, const uint8_t *Buffer, const uint64_t Size) override;
   bool PhysReadDirect(const Gpa_t Gpa, uint8_t *Buffer, const uint64_t Size) const override;
   bool SetFeed(const uint8_t *Data, const uint64_t Size) override;
+  bool DeclareInsert(const InsertAction_t &Action) override;
+  bool SetInsert(const uint8_t *Data, const uint64_t Size) override;
   const std::unordered_set<Gva_t> &LastNewCoverage() const override;
   bool RevokeLastNewCoverage() override;
   using Backend_t::SetBreakpoint;
@@ -162,7 +164,7 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
     bool handler_fault = false;
     uint64_t seed = 0;
     uint64_t inject = ~0ull;  // PageFaultsMemoryIfNeeded: page to #PF after the handler
-    bool has_feed = false;    // SetFeed: chunks for the device Feed action
+    bool has_feed = false;    // SetFeed / SetInsert: chunks for the device Feed action / insert
     std::vector<uint8_t> feed;
     bool dirty_known = false;
     std::vector<uint32_t> dirty;  // gpfns the lane's overlay holds
@@ -266,6 +268,7 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   uint64_t tenet_cap_ = 0;                       // Tenet stream bytes per lane (EnableTenet)
   std::unordered_map<uint64_t, BreakpointAction_t::ArgsResult_t> args_results_;  // StopWithArgs, by gva
   bool feed_action_ = false;                     // a Feed action is on the device
+  bool insert_action_ = false;                   // the declared insert is on the device (wtfgpu_set_insert)
   int upload_feed(uint32_t n);                   // lanes [0, n)
   std::unordered_set<uint64_t> aggregate_;
   std::unordered_set<uint64_t> code_vpns_;  // the map's pages (set_code_pages)

@@ -1,7 +1,8 @@
 // fuzzer_hevd.cc — the hevd fuzzer module (reference src/wtf/fuzzer_hevd.cc),
 // written against wtf_api.h with the same handlers, symbols and result names:
 //  * InsertTestcase (:20-59): u32 IOCTL code -> rdx, the rest (<= 1024 bytes)
-//    -> the user buffer at r8, its size -> r9 and GetArgAddress(5);
+//    -> the user buffer at r8, its size -> r9 and GetArgAddress(5) (also
+//    declared as InsertAction_t, which the gpu backend applies on the device);
 //  * the instruction after the 6-byte call to DeviceIoControl stops the
 //    testcase with Ok (:64-73; also declared as BreakpointAction_t::StopOk);
 //  * nt!DbgPrintEx is skipped (return 0) after reading its format (:78-88);
@@ -50,6 +51,9 @@ bool InsertTestcase(const uint8_t *Buffer, const size_t BufferSize) {
   const size_t IoctlBufferSize = BufferSize - sizeof(uint32_t);
   const uint8_t *IoctlBuffer = Buffer + sizeof(uint32_t);
   if (IoctlBufferSize > 1024) return false;
+  // the declared form below (Init): a backend that applies it on the device
+  // takes the whole testcase
+  if (g_Backend->SetInsert(Buffer, BufferSize)) return true;
   g_Backend->Rdx(Ioctl);
   const Gva_t IoctlBufferPtr = Gva_t(g_Backend->R8());
   if (!g_Backend->VirtWriteDirty(IoctlBufferPtr, IoctlBuffer, IoctlBufferSize)) return false;
@@ -60,6 +64,9 @@ bool InsertTestcase(const uint8_t *Buffer, const size_t BufferSize) {
 }
 
 bool Init(const Options_t &, const CpuState_t &) {
+  // InsertTestcase as data (device-side on the gpu backend)
+  g_Backend->DeclareInsert(
+      InsertAction_t::HeadAndPayload(Registers_t::Rdx, Registers_t::R8, Registers_t::R9, /*LenArg=*/5));
   const Gva_t Rip = Gva_t(g_Backend->Rip());
   const Gva_t AfterCall = Rip + Gva_t(6);
   if (!g_Backend->SetBreakpoint(

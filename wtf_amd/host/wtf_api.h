@@ -283,6 +283,30 @@ struct BreakpointAction_t {
   }
 };
 
+// What an InsertTestcase does, stated as data (this repository's extension,
+// like BreakpointAction_t): the testcase's first 4 bytes (u32) go to HeadReg,
+// the rest (the payload) is written, dirty, at the address in PtrReg, its size
+// goes to LenReg and, with LenArg != 0, as a u64 to GetArgAddress(LenArg)
+// (fuzzer_hevd.cc:20-59 exactly). A backend that applies it on the device says
+// so from DeclareInsert at Init; the module's InsertTestcase then hands it the
+// testcase (SetInsert) instead of writing it itself. The module keeps its own
+// size checks (what it rejects is never handed over).
+struct InsertAction_t {
+  Registers_t HeadReg = Registers_t::Rdx;
+  Registers_t PtrReg = Registers_t::R8;
+  Registers_t LenReg = Registers_t::R9;
+  uint32_t LenArg = 0;
+  static InsertAction_t HeadAndPayload(const Registers_t Head, const Registers_t Ptr, const Registers_t Len,
+                                       const uint32_t LenArg) {
+    InsertAction_t A;
+    A.HeadReg = Head;
+    A.PtrReg = Ptr;
+    A.LenReg = Len;
+    A.LenArg = LenArg;
+    return A;
+  }
+};
+
 class Backend_t {
  public:
   virtual ~Backend_t() = default;
@@ -315,6 +339,11 @@ class Backend_t {
   // (u32 little-endian size, bytes) records. true = the backend serves that
   // breakpoint from them; false (default) = its handler runs.
   virtual bool SetFeed(const uint8_t *, const uint64_t) { return false; }
+  // The declared insert (InsertAction_t): true = this backend applies it to
+  // every testcase the module hands over with SetInsert (which then returns
+  // true); false (default) = InsertTestcase writes the testcase itself.
+  virtual bool DeclareInsert(const InsertAction_t &) { return false; }
+  virtual bool SetInsert(const uint8_t *, const uint64_t) { return false; }
 
   // helpers implemented on top of the virtuals (backend.cc)
   bool SaveCrash(const Gva_t ExceptionAddress, const uint32_t ExceptionCode);
