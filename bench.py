@@ -438,7 +438,7 @@ def run(a, rank, world, local, tmp):
             "config": {"workload": TARGETS["tlv_server"][1], "lanes_per_gpu": a.lanes, "limit": a.limit,
                        "max_len": TARGETS["tlv_server"][2], "slice_steps": a.slice_steps or 4096,
                        "regroup_steps": a.regroup_steps if a.regroup_steps >= 0 else 1024,  # engine default
-                       "regroup_auto": "off while a run retires >= 56 lanes per wave-step, on again below 40",
+                       "regroup_auto": "the schedule (regrouped or fixed lane order) that retires more lanes per wave-step, measured; the other probed every 32nd run",
                        "mutation": MUTATION,
                        "parallelism": f"shard{world}: one node per GPU (seed + rank), RCCL MAX coverage-map "
                                       f"merge started every step, absorbed the next"},

@@ -1995,10 +1995,14 @@ struct wtfgpu_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   u64 regroup_steps = 1024;
   // regrouping pays only while lanes diverge from their wave neighbours:
-  // regroup_now() turns it off while the last run retired >= 56 lanes per
-  // wave-step and back on below 40 (WTFGPU_REGROUP_AUTO=0: never)
-  bool regroup_auto = true, regroup_off = false;
-  double lanes_per_step = 0;
+  // regroup_now() measures both schedules (lanes retired per wave-step) and
+  // runs the better one, probing the other every kProbe-th run; all counts,
+  // no clocks, so a fixed-seed campaign schedules the same way every time
+  // (WTFGPU_REGROUP_AUTO=0: always regroup)
+  bool regroup_auto = true;
+  double lps_sched[2] = {0, 0};  // lanes per wave-step, EMA: [0] fixed order, [1] regrouped
+  u64 rg_runs = 0;
+  u8 rg_used[2] = {2, 2};  // per queue: its run in flight regroups (1), not (0), unmeasured (2)
   u32 async_launches = 0;
   // the current queue's resources live in the members above; the others here
   QueueRes queues[2];
@@ -2976,18 +2980,33 @@ static Dev run_params(wtfgpu_ctx *c, bool regroup) {
   return Q;
 }
 
-// Whether this run regroups (see wtfgpu_ctx::regroup_auto), and the
-// measurement the next decision uses.
+// Whether this run regroups (see wtfgpu_ctx::regroup_auto): measure each
+// schedule once, then run the one that retires more lanes per wave-step
+// (regrouping must win by kMargin: its sorts and shorter launches cost time a
+// wave-step count does not show), probing the other every kProbe-th run.
 static u64 regroup_now(wtfgpu_ctx *c, u32 count) {
+  c->rg_used[c->cur_queue & 1] = 2;  // not a measured choice
   if (!c->regroup_steps || count < 2 * c->P.lpw) return 0;
   if (!c->regroup_auto) return c->regroup_steps;
-  static constexpr double kOff = 56, kOn = 40;
-  if (c->lanes_per_step >= kOff) c->regroup_off = true;
-  else if (c->lanes_per_step < kOn) c->regroup_off = false;
-  return c->regroup_off ? 0 : c->regroup_steps;
+  static constexpr double kMargin = 1.1;
+  static constexpr u64 kProbe = 32;
+  const u64 i = c->rg_runs++;
+  bool on;
+  if (c->lps_sched[1] == 0) on = true;
+  else if (c->lps_sched[0] == 0) on = false;
+  else {
+    on = c->lps_sched[1] > kMargin * c->lps_sched[0];
+    if (i % kProbe == kProbe - 1) on = !on;
+  }
+  c->rg_used[c->cur_queue & 1] = on;
+  return on ? c->regroup_steps : 0;
 }
 static void regroup_observe(wtfgpu_ctx *c, u64 group_steps, u64 retired) {
-  if (group_steps >= 64) c->lanes_per_step = (double)retired / (double)group_steps;
+  const u8 used = c->rg_used[c->cur_queue & 1];
+  if (used > 1 || group_steps < 64) return;
+  const double lps = (double)retired / (double)group_steps;
+  double &e = c->lps_sched[used];
+  e = e == 0 ? lps : 0.75 * e + 0.25 * lps;
 }
 
 // One k_run launch of `steps` wave-steps over [first, first + count), after
