@@ -336,8 +336,10 @@ def lanes(n: int, seed: int, st: dict, lay: dict, data: bytes):
         elif name.startswith("enter"):
             g[6] = KSP - rng.choice([0x100, 0x10, 0x800, 0x7000 - 0x80])
         elif name in ("retfq", "u_retf"):
-            g[8] = rng.choice([0x10, 0x33, 0x13, 0, 0x2B]) if name == "retfq" else rng.choice([0x33, 0x10, 0x30])
-            g[9] = rng.choice([KSLOT["cpuid"], USLOT["u_cpuid"], 1 << 47, USLOT["u_int1"]])
+            g[8] = rng.choice([0x10, 0x33, 0x13, 0, 0x2B, 0x23]) if name == "retfq" else rng.choice([0x33, 0x10, 0x30])
+            # 0x23: SYSRET's compatibility-mode selector (a rip past 4 GiB is #GP(0), U29)
+            g[9] = rng.choice([KSLOT["cpuid"], USLOT["u_cpuid"], 1 << 47, USLOT["u_int1"], USLOT["u_cpuid"] & 0xFFFFFFFF,
+                               (1 << 32) | 0x1000])
         elif name == "retf_imm":
             g[8], g[9] = rng.choice([(KSLOT["cpuid"], 0x10), (USLOT["u_cpuid"], 0x33), (USLOT["u_cpuid"], 0x33)])
             g[10], g[11] = rng.choice([USP, KSP - 0x200, 1 << 50]), rng.choice([0x2B, 0, 0x18])

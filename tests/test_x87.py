@@ -200,6 +200,40 @@ def test_fxrstor_normalises_es():
     assert o.regs().gpr[0] & 0xFFFF == 0x8081
 
 
+def _env_prog(code, data):
+    L = sim_lib()
+    sp, regs = layout(bytes(code), BUF, bytes(data) + bytes(256 - len(data)))
+    regs.gpr[6], regs.gpr[7] = BUF, BUF + 0x80
+    regs.fpcw, regs.fptw = 0x37F, 0xFFFF
+    out, fin = sim_run(L, sp, regs, win_va=BUF)
+    pfns, blob = sp.phys()
+    o = Oracle(pfns=pfns, blob=blob)
+    o.restore(regs)
+    for _ in range(16):
+        if o.step().status != 0:
+            break
+    env = bytes(out.win[0x80:0x80 + 28])
+    assert env == o.read_virt(BUF + 0x80, 28)
+    return [int.from_bytes(env[i:i + 2], "little") for i in (0, 4, 8)]
+
+
+def test_fldenv_frstor_normalise_fcw_and_retag():
+    """FLDENV / FRSTOR load FCW as FLDCW does and recompute every non-empty
+    tag from the register contents; the values are this host's (fnstenv after
+    the load): fldz / fld1 / fldpi, fldenv of fcw 0 / ftw 0 -> 0040 / 4155;
+    fcw ffff / ftw aaaa -> 1f7f / 4155; frstor of fcw ffff, ST0 = 1.0 -> 1f7f / 5554."""
+    ld3 = [0xD9, 0xEE, 0xD9, 0xE8, 0xD9, 0xEB]           # fldz; fld1; fldpi
+    fldenv_fnstenv = [0xD9, 0x26, 0xD9, 0x37, 0xCC]     # fldenv [rsi]; fnstenv [rdi]; int3
+    assert _env_prog(ld3 + fldenv_fnstenv, bytes(28)) == [0x0040, 0, 0x4155]
+    env = bytearray(28)
+    env[0:2], env[8:10] = (0xFFFF).to_bytes(2, "little"), (0xAAAA).to_bytes(2, "little")
+    assert _env_prog(ld3 + fldenv_fnstenv, env) == [0x1F7F, 0, 0x4155]
+    img = bytearray(108)
+    img[0:2] = (0xFFFF).to_bytes(2, "little")
+    img[28:36], img[36:38] = (1 << 63).to_bytes(8, "little"), (0x3FFF).to_bytes(2, "little")
+    assert _env_prog([0xDD, 0x26, 0xD9, 0x37, 0xCC], img) == [0x1F7F, 0, 0x5554]   # frstor [rsi]; fnstenv [rdi]
+
+
 def test_x87_store_fault_leaves_the_stack():
     # fstp dword [rsi + 0x2000] (unmapped): #PF (write), TOP and ST0 unchanged
     L = sim_lib()

@@ -473,10 +473,20 @@ __device__ __noinline__ int exec_x87(const Dev &P, Lane &L, const UOp &u, u64 va
       u64 q0, q1, q2, q3;
       if (!vread(L, va, 8, q0) || !vread(L, va + 8, 8, q1) || !vread(L, va + 16, 8, q2) || !vread(L, va + 24, 4, q3))
         return X_FAULT;
-      F.fpcw = (u16)q0;
-      F.fpsw = (u16)fsw_norm((u32)(q0 >> 32) & 0xffff, (u32)q0 & 0xffff);
+      // FCW as FLDCW loads it; the physical registers stay where they are
+      // under the loaded TOP (fpst is kept in ST order: rotated as FNINIT
+      // does); every tag not empty recomputed from the register's contents
+      // (what the host's FNSTENV shows afterwards)
+      const u32 ot = (F.fpsw >> 11) & 7, nt = (u32)(q0 >> 43) & 7;
+      u64 t[8];
+      u16 e[8];
+      for (u32 j = 0; j < 8; j++) t[j] = F.fpst[(nt + j - ot) & 7], e[j] = F.fpse[(nt + j - ot) & 7];
+      for (u32 j = 0; j < 8; j++) F.fpst[j] = t[j], F.fpse[j] = e[j];
+      F.fpcw = (u16)((q0 & ~0xe0c0ull) | 0x40);
+      F.fpsw = (u16)fsw_norm((u32)(q0 >> 32) & 0xffff, F.fpcw);
       F.fptw = (u16)q1;
       F.fpop = (u16)((q2 >> 16) & 0x7ff);
+      x87_retag(F);
       return X_OK;
     }
     if (r3 == 5) {  // fldcw
@@ -505,11 +515,12 @@ __device__ __noinline__ int exec_x87(const Dev &P, Lane &L, const UOp &u, u64 va
     u64 st[8], se[8];
     for (u32 i = 0; i < 8; i++)
       if (!vread(L, va + 28 + 10 * i, 8, st[i]) || !vread(L, va + 36 + 10 * i, 2, se[i])) return X_FAULT;
-    F.fpcw = (u16)q0;
-    F.fpsw = (u16)fsw_norm((u32)(q0 >> 32) & 0xffff, (u32)q0 & 0xffff);
+    F.fpcw = (u16)((q0 & ~0xe0c0ull) | 0x40);
+    F.fpsw = (u16)fsw_norm((u32)(q0 >> 32) & 0xffff, F.fpcw);
     F.fptw = (u16)q1;
     F.fpop = (u16)((q2 >> 16) & 0x7ff);
     for (u32 i = 0; i < 8; i++) F.fpst[i] = st[i], F.fpse[i] = (u16)se[i];
+    x87_retag(F);
     return X_OK;
   }
   if (r3 == 6) {  // fnsave, then fninit
@@ -548,8 +559,11 @@ __device__ __noinline__ int far_pop(const Dev &P, Lane &L, u32 osz, u64 imm, boo
     if ((nss & 0xfffc) == 0 && ncpl == 3) return fault_x(L, WTFGPU_VEC_GP, 0);
   }
   if (!canonical(f0)) return fault_x(L, WTFGPU_VEC_GP, 0);
-  // back to SYSRET's compatibility-mode selector where ring 3 could fetch: 32-bit code (U29)
-  if (cs == ((((u32)(S.star >> 48)) & 0xffff) | 3) && user_fetch_ok(P, L, f0 & 0xffffffffull)) return X_UNIMPL;
+  // back to SYSRET's compatibility-mode selector (U29): a rip past the 32-bit
+  // segment's limit is #GP(0); where ring 3 could fetch, 32-bit code runs
+  const bool compat = cs == ((((u32)(S.star >> 48)) & 0xffff) | 3);
+  if (compat && (f0 >> 32)) return fault_x(L, WTFGPU_VEC_GP, 0);
+  if (compat && user_fetch_ok(P, L, f0)) return X_UNIMPL;
   if (iret) {
     u64 mask = 0x254dd5ull;
     if (ocpl == 0) mask |= 0x200ull | 0x3000ull | 0x80000ull | 0x100000ull;
