@@ -300,7 +300,14 @@ const uint8_t kZeroPage[Page::Size] = {};
 }  // namespace
 
 size_t GpuBackend_t::alloc_slots(size_t n, uint8_t **orig, uint8_t **data) const {
-  Arena &A = arenas_[HostPool::InLoop() ? HostPool::ThreadIndex() : 0];
+  // a thread inside a HostPool loop has its own arena (its index); any call
+  // outside a loop takes the spare arena (index Threads()) under a lock, so a
+  // second driver thread, whose loop ran serially because another thread held
+  // the pool, never shares arena 0 with that loop's caller
+  const bool in_loop = HostPool::InLoop();
+  std::unique_lock<std::mutex> spare(spare_mu_, std::defer_lock);
+  if (!in_loop) spare.lock();
+  Arena &A = arenas_[in_loop ? HostPool::ThreadIndex() : arenas_.size() - 1];
   while (A.cur < A.blocks.size() && A.blocks[A.cur].cap - A.blocks[A.cur].used < n) A.cur++;
   if (A.cur == A.blocks.size()) {
     Block b;
@@ -406,11 +413,16 @@ void GpuBackend_t::drop_staged(LaneView &v) const {
   if (v.pages.empty()) return;
   live_staged_ -= v.pages.size();
   v.pages.clear();
-  if (live_staged_ == 0 && !HostPool::InLoop()) {  // every staged page consumed: recycle the arenas
-    for (Arena &A : arenas_) {
-      for (Block &b : A.blocks) b.used = 0;
-      A.cur = 0;
-    }
+  if (!HostPool::InLoop()) recycle_arenas();
+}
+
+// Every staged page consumed: the arenas start over (outside HostPool loops
+// only; callers of parallel drop_staged call it after their loop).
+void GpuBackend_t::recycle_arenas() const {
+  if (live_staged_ != 0 || HostPool::InLoop()) return;
+  for (Arena &A : arenas_) {
+    for (Block &b : A.blocks) b.used = 0;
+    A.cur = 0;
   }
 }
 
@@ -925,6 +937,7 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
         }
       }
     });
+    recycle_arenas();  // drop_staged ran inside the loop
     // the handlers: lane by lane, or on all host threads when the module keeps
     // its per-testcase state thread_local (each thread services its own lanes
     // with g_Backend = this and its own swapped-in module state). The order of
@@ -1420,6 +1433,7 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
       tc_bytes_[l] = In[i].size;
       lres_stale_[l] = 1;  // its last result may not be consumed yet (this call's Out)
     });
+    recycle_arenas();  // reset_view's drop_staged ran inside the loop
     const auto tm = Clock::now();
     stats_.restore_ms += std::chrono::duration<double, std::milli>(tm - ti).count();
     std::vector<uint8_t> ok;

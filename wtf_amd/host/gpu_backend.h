@@ -288,7 +288,9 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
     std::vector<Block> blocks;
     size_t cur = 0;
   };
-  mutable std::vector<Arena> arenas_;
+  mutable std::vector<Arena> arenas_;  // [0, Threads()): HostPool threads in a loop; the last: calls outside loops
+  mutable std::mutex spare_mu_;        // the last arena's lock
+  void recycle_arenas() const;
   mutable std::atomic<size_t> live_staged_{0};
   // serialises engine calls made from handler threads (shared scratch buffers)
   // and the learned-prefetch tables
