@@ -62,6 +62,7 @@
  */
 #include "x86_oracle.h"
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
 
 typedef uint64_t u64;
@@ -3418,6 +3419,25 @@ static int deliver(orc_machine *m, u32 vec, u32 err, u64 cr2) {
   return ok;
 }
 
+/* Diagnostic: executed instructions by (opcode map, opcode, ModRM reg,
+ * memory operand), for the engine's fast-path coverage study
+ * (scripts/op_mix.py via WTF_OPHIST on the twin). Process-wide, not thread-safe. */
+static u64 g_ophist[4 * 256 * 8 * 2];
+static int g_ophist_on = -1;
+void orc_ophist(u64 *out, int reset) {
+  memcpy(out, g_ophist, sizeof(g_ophist));
+  if (reset) memset(g_ophist, 0, sizeof(g_ophist));
+}
+
+static void ophist_dump(void) { /* "map opcode reg mem count" lines to $WTF_OPHIST */
+  FILE *f = fopen(getenv("WTF_OPHIST"), "w");
+  if (!f) return;
+  for (size_t i = 0; i < sizeof(g_ophist) / 8; i++)
+    if (g_ophist[i]) fprintf(f, "%zu %zu %zu %zu %llu\n", i / 4096, (i / 16) % 256, (i / 2) % 8, i % 2,
+                             (unsigned long long)g_ophist[i]);
+  fclose(f);
+}
+
 static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
   insn d;
   memref mr;
@@ -3425,6 +3445,12 @@ static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
   m->ex = ex;
   m->faulted = 0;
   int rc = decode(m, &d, &mr);
+  if (g_ophist_on < 0) {
+    g_ophist_on = getenv("WTF_OPHIST") != NULL;
+    if (g_ophist_on) atexit(ophist_dump);
+  }
+  if (g_ophist_on && rc >= 0)
+    g_ophist[(((d.opmap & 3) * 256 + (d.op & 0xff)) * 8 + (d.has_modrm ? (d.reg & 7) : 0)) * 2 + (d.is_mem ? 1 : 0)]++;
   if (rc < 0) {
     if (d.fetch_fail == 2) {
       ex->status = WTFGPU_EXIT_FAULT;

@@ -61,6 +61,10 @@ int orc_inject_fault(orc_machine *m, uint32_t vector, uint32_t error, uint64_t a
 int orc_run(orc_machine *m, int skip_bp, wtfgpu_exit_t *exit);
 /* Execute exactly one instruction (no breakpoint check); returns status. */
 int orc_step(orc_machine *m, wtfgpu_exit_t *exit);
+/* Diagnostic (WTF_OPHIST set): executed instructions counted by
+ * ((map * 256 + opcode) * 8 + ModRM.reg) * 2 + memory operand; out holds 16384
+ * counters. */
+void orc_ophist(uint64_t *out, int reset);
 uint64_t orc_icount(orc_machine *m);
 uint64_t orc_bytes(orc_machine *m);
 /* RecordEdge calls of the current testcase; *unique: those whose edge was new to its coverage set */
