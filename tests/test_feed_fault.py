@@ -79,7 +79,9 @@ def test_gpu_missing_packet_page_is_engine_error(targets, tmp_path):
     # the registers of a testcase abandoned mid-handler are the handler's
     # partial work (the reference node stops there): compared where it finished
     _cmp([r for r in a if not r["error"]], [r for r in b if not r["error"]], ("gprs",))
-    # the fuzz loop goes on, and keeps the testcases under errors/
+    # the node finishes the batch and keeps the testcases under errors/; then
+    # it stops where the reference's mutator does ("The corpus is empty,
+    # exiting", mutator.cc:27-31): every testcase errored, none joined the corpus
     st = H.fuzz(H.WTFGPU, t, runs=4096, lanes=512, timeout=120)
-    assert st["execs"] == 4096 and st["errors"] > 0 and st["backend"]["err_handler"] == st["errors"]
+    assert st["execs"] >= 512 and st["errors"] > 0 and st["backend"]["err_handler"] == st["errors"]
     assert os.listdir(os.path.join(t, "errors"))
