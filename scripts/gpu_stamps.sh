@@ -6,6 +6,7 @@ python -c "
 from tests import tlv_harness as H
 H.build_target('/tmp/st_tlv'); H.build_hevd_target('/tmp/st_hevd')" || exit 1
 export LD_LIBRARY_PATH=$PWD/${STAMPLIB:-stampslib}
-timeout -k 10 120 wtf_amd/host/wtfgpu fuzz --name tlv_server --target /tmp/st_tlv --lanes ${LANES:-131072} --seconds 4 --seed 1337 --limit 100000 --max_len 4096 > gpurun_out/stamps_tlv.log 2>&1 || exit 1
+WTFGPU_COVLOG_TOP=1 timeout -k 10 120 wtf_amd/host/wtfgpu fuzz --name tlv_server --target /tmp/st_tlv --lanes ${LANES:-131072} --seconds 4 --seed 1337 --limit 100000 --max_len 4096 > gpurun_out/stamps_tlv.log 2>&1 || exit 1
 timeout -k 10 120 wtf_amd/host/wtfgpu fuzz --name hevd --target /tmp/st_hevd --lanes ${LANES:-131072} --seconds 4 --seed 1337 --limit 10000000 --max_len 1028 > gpurun_out/stamps_hevd.log 2>&1 || exit 1
 python scripts/stamps_summary.py gpurun_out/stamps_tlv.log gpurun_out/stamps_hevd.log
+grep "covlog top" gpurun_out/stamps_tlv.log | tail -1 | cut -c1-900

@@ -1335,6 +1335,18 @@ void GpuBackend_t::collect_coverage(const std::vector<uint32_t> &lanes, std::vec
   }
   std::unordered_map<uint32_t, std::vector<uint64_t>> per;
   for (uint64_t i = 0; i < total; i++) per[cl[i]].push_back(cr[i]);
+  if (getenv("WTFGPU_COVLOG_TOP")) {  // diagnostic: which logged values keep coming back
+    for (uint64_t i = 0; i < total; i++) covlog_count_[cr[i]]++;
+    if (++covlog_calls_ % 64 == 0) {
+      std::vector<std::pair<uint64_t, uint64_t>> v(covlog_count_.begin(), covlog_count_.end());
+      std::sort(v.begin(), v.end(), [](auto &a, auto &b) { return a.second > b.second; });
+      fprintf(stderr, "covlog top:");
+      for (size_t i = 0; i < v.size() && i < 24; i++)
+        fprintf(stderr, " %llx:%llu%s", (unsigned long long)v[i].first, (unsigned long long)v[i].second,
+                aggregate_.count(v[i].first) ? "*" : "");
+      fprintf(stderr, " (%zu values)\n", v.size());
+    }
+  }
   std::vector<uint64_t> fresh;
   last_new_coverage_.clear();
   for (uint32_t l : lanes) {

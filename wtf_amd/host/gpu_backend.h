@@ -290,6 +290,8 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   };
   mutable std::vector<Arena> arenas_;  // [0, Threads()): HostPool threads in a loop; the last: calls outside loops
   mutable std::mutex spare_mu_;        // the last arena's lock
+  std::unordered_map<uint64_t, uint64_t> covlog_count_;  // WTFGPU_COVLOG_TOP diagnostic
+  uint64_t covlog_calls_ = 0;
   void recycle_arenas() const;
   mutable std::atomic<size_t> live_staged_{0};
   // serialises engine calls made from handler threads (shared scratch buffers)
