@@ -18,7 +18,7 @@ for path in sys.argv[1:]:
         if line.startswith("wtfgpu stamps generic ops:"):
             for kv in line.split(":", 1)[1].split():
                 k, v = kv.split(":")
-                name = OPS[int(k)] if int(k) < len(OPS) else k
+                name = (OPS[int(k) & 63] if (int(k) & 63) < len(OPS) else k) + ("" if int(k) < 64 else "(cov)")
                 ops[name] = ops.get(name, 0) + int(v)
             continue
         m = PAT.search(line)

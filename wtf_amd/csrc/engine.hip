@@ -264,6 +264,9 @@ __device__ __forceinline__ void fetch_bytes(u64 pageptr, u32 off, u32 n, u64 &lo
 #define WTFGPU_UC_N 256  // head-only entries (the UOp lives in the uop slots below)
 #endif
 constexpr u32 UC_N = WTFGPU_UC_N;  // entries per wave (power of two)
+#ifndef WTFGPU_FILL_INLINE
+#define WTFGPU_FILL_INLINE 1  // k_run's fills take the shared-cache hit path inline (uc_fill_shared)
+#endif
 #ifndef WTFGPU_UC_U
 #define WTFGPU_UC_U 4  // 4 x 120 bytes per wave: k_run's LDS (uop cache + lane copies) fits 160 KiB
 #endif
@@ -501,40 +504,49 @@ __device__ __forceinline__ FOp generic_fop(const UOp &d) {
   return f;
 }
 
+// The shared (device-wide) cache's side of a fill (uniform): one dword per
+// lane, the six tag dwords checked; on a hit the head goes to `e` (when
+// given) and the UOp to the uop slot `us`. Inline at k_run's fill site (a
+// fill is about a fifth of tlv's wave-steps, and a call spills the caller's
+// live registers); false = a miss, uc_fill decodes.
+__device__ __forceinline__ bool uc_fill_shared(const Dev &P, UCEntry *e, UCUop *us, u64 key, u32 off, u64 rip,
+                                               u32 lid) {
+  if (!P.guc) return false;
+  const u32 pj = guc_payload_index(lid);
+  u32 *head = e ? (u32 *)&e->flags : nullptr, *uop = (u32 *)&us->u;
+  const u32 *gw = P.guc + (u64)guc_slot(P, key) * GUC_WORDS;
+  const u32 w = lid < GUC_WORDS ? gw[lid] : 0;
+  const bool tag = lid < GUC_WORDS && (lid & 15) >= 14;
+  const bool bad = tag && w != ((lid & 1) ? (u32)(key >> 32) : (u32)key);
+  if (__ballot(bad) != 0) return false;
+  if (pj < GP_HEAD) {
+    if (head) head[pj] = w;
+  } else if (pj < GUC_PAYLOAD) {
+    uop[pj - GP_HEAD] = w;
+  }
+  const u32 flags = __builtin_amdgcn_readlane(w, 0) | (e ? covered_flag(P, rip, off) : 0);
+  __builtin_amdgcn_wave_barrier();
+  if (lid == 0) {
+    us->key = key;
+    if (e) {
+      e->logged = 0;
+      e->flags = flags;
+      e->rip = rip;
+      e->key = key;
+    }
+  }
+  return true;
+}
+
 // Fill one entry (uniform): from the shared cache when it holds the key, else
 // fetch + decode from the pool page, digest, lookups, and publish. The head
 // goes to `e` (when given), the UOp to the uop slot `us`.
 __device__ __noinline__ void uc_fill(const Dev &P, UCEntry *e, UCUop *us, u64 key, u64 lptr, u32 off, u64 rip,
-                                     u32 lid) {
-  u32 *gw = nullptr;
+                                     u32 lid, bool shared_checked = false) {
   const u32 pj = guc_payload_index(lid);
-  u32 *head = e ? (u32 *)&e->flags : nullptr, *uop = (u32 *)&us->u;
-  if (P.guc) {
-    // the shared cache first: one dword per lane, the six tag dwords checked
-    gw = P.guc + (u64)guc_slot(P, key) * GUC_WORDS;
-    const u32 w = lid < GUC_WORDS ? gw[lid] : 0;
-    const bool tag = lid < GUC_WORDS && (lid & 15) >= 14;
-    const bool bad = tag && w != ((lid & 1) ? (u32)(key >> 32) : (u32)key);
-    if (__ballot(bad) == 0) {
-      if (pj < GP_HEAD) {
-        if (head) head[pj] = w;
-      } else if (pj < GUC_PAYLOAD) {
-        uop[pj - GP_HEAD] = w;
-      }
-      const u32 flags = __builtin_amdgcn_readlane(w, 0) | (e ? covered_flag(P, rip, off) : 0);
-      __builtin_amdgcn_wave_barrier();
-      if (lid == 0) {
-        us->key = key;
-        if (e) {
-          e->logged = 0;
-          e->flags = flags;
-          e->rip = rip;
-          e->key = key;
-        }
-      }
-      return;
-    }
-  }
+  u32 *uop = (u32 *)&us->u;
+  if (!shared_checked && uc_fill_shared(P, e, us, key, off, rip, lid)) return;
+  u32 *gw = P.guc ? P.guc + (u64)guc_slot(P, key) * GUC_WORDS : nullptr;
   IBytes ib;
   ib.avail = 4096 - off < 16 ? 4096 - off : 16;
   fetch_bytes(lptr, off, ib.avail, ib.lo, ib.hi);
@@ -1053,8 +1065,8 @@ struct LaneCopy {
 #define WHY(k) why_ = (k)
 // and which generic ops the slow step executed (O_* / O_SYS2 etc.), one count per
 // group, in stat[16..80)
-#define OPHIST(op) ophist_[(op) & 63]++
-constexpr u32 STAT_N = 80;
+#define OPHIST(op) ophist_[(op) & 127]++
+constexpr u32 STAT_N = 144;
 #else
 constexpr u32 STAT_N = 16;
 #define OPHIST(op) \
@@ -1144,7 +1156,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
   u64 tprev_ = __builtin_amdgcn_s_memtime();
   u64 whyc_[4] = {0, 0, 0, 0};
   u32 why_ = 3;
-  u32 ophist_[64] = {};
+  u32 ophist_[128] = {};
 #endif
 
   for (;;) {
@@ -1254,7 +1266,12 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     UCEntry *e = &uc[uc_slot(key)];
     const bool cacheable = lptr >= pool_lo && lptr < pool_hi;
     if (cacheable && rfl64(e->key) != key) {
+#if WTFGPU_FILL_INLINE
+      if (!uc_fill_shared(P, e, &uu[uu_slot(key)], key, off, grip, lid))
+        uc_fill(P, e, &uu[uu_slot(key)], key, lptr, off, grip, lid, true);
+#else
       uc_fill(P, e, &uu[uu_slot(key)], key, lptr, off, grip, lid);
+#endif
       // an entry the fast loop can run (a common op, nothing to log, no
       // breakpoint): back to it, this pass was only the fill
       const u32 ff = rfl32(e->flags);
@@ -1305,7 +1322,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     // the UOp for the generic path (wave-uniform: the slot fill is a wave operation)
     const UOp *u = nullptr;
     if (__ballot(ing)) u = uc_uop(P, uu, key, lptr, off, grip, lid);
-    if (__ballot(ing) && !(flags & UC_UNSUP)) OPHIST(rfl32(u->op));
+    if (__ballot(ing) && !(flags & UC_UNSUP)) OPHIST(rfl32(u->op) + (flags & UC_COVERED ? 64 : 0));
     if (ing && (flags & UC_UNSUP)) {
       const u32 ob = u->opbytes, n = len;
       L.status = WTFGPU_EXIT_UNIMPLEMENTED;
@@ -1365,7 +1382,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
 #ifdef WTFGPU_STAMPS
     for (int k = 0; k < 8; k++) atomicAdd((unsigned long long *)&P.stat[4 + k], (unsigned long long)stamp_[k]);
     for (int k = 0; k < 4; k++) atomicAdd((unsigned long long *)&P.stat[12 + k], (unsigned long long)whyc_[k]);
-    for (int k = 0; k < 64; k++)
+    for (int k = 0; k < 128; k++)
       if (ophist_[k]) atomicAdd((unsigned long long *)&P.stat[16 + k], (unsigned long long)ophist_[k]);
 #endif
   }
@@ -3041,7 +3058,7 @@ static void print_stamps(const u64 *s) {
             (double)s[5] / s[0], (double)s[9] / s[0], (unsigned long long)s[12], (unsigned long long)s[13],
             (unsigned long long)s[14], (unsigned long long)s[15]);
   fprintf(stderr, "wtfgpu stamps generic ops:");
-  for (int k = 0; k < 64; k++)
+  for (int k = 0; k < 128; k++)
     if (s[16 + k]) fprintf(stderr, " %d:%llu", k, (unsigned long long)s[16 + k]);
   fprintf(stderr, "\n");
 #else
