@@ -5,13 +5,13 @@ import sys
 
 PAT = re.compile(r"wtfgpu stamps \(cycles per wave-step, (\d+) steps\): fast loop (\S+), slow: xlate\+fill (\S+), "
                  r"coverage (\S+), exec (\S+), cross-page ([^;\s]+)(?:; slow steps: miss (\d+), codepage (\d+), "
-                 r"ucmiss (\d+), other (\d+))?")
+                 r"ucmiss (\d+), other (\d+))?(?:; fast lookup (\S+), fast exec (\S+))?")
 OPS = ("ALU TEST MOV MOVZX MOVSX XCHG XADD CMPXCHG INCDEC NOT NEG SHIFT SHXD MULDIV IMUL BT BSF BSR TZCNT LZCNT "
        "POPCNT CMOV SETCC BSWAP CBW CWD LAHF SAHF FLAGOP NOP JCC JMP CALL RET PUSH POP PUSHF POPF LEAVE STRING INT3 "
        "HLT UD LEA SYS SSE UNIMPL SYS2 LOOP GEXT").split()
 for path in sys.argv[1:]:
     steps = 0
-    tot = [0.0] * 5
+    tot = [0.0] * 7
     why = [0] * 4
     ops = {}
     for line in open(path):
@@ -28,10 +28,13 @@ for path in sys.argv[1:]:
         steps += n
         for i in range(5):
             tot[i] += float(m.group(2 + i)) * n
+        if m.group(11):
+            tot[5] += float(m.group(11)) * n
+            tot[6] += float(m.group(12)) * n
         if m.group(7):
             for i in range(4):
                 why[i] += int(m.group(7 + i))
-    names = ("fast", "xlate+fill", "coverage", "exec", "cross-page")
+    names = ("fast", "xlate+fill", "coverage", "exec", "cross-page", "fast: lookup part", "fast: exec part")
     print(path, "wave-steps", steps, {k: round(v / max(1, steps)) for k, v in zip(names, tot)},
           "slow steps", dict(zip(("miss", "codepage", "ucmiss", "other"), why)))
     if ops:

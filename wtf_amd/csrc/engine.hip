@@ -23,14 +23,6 @@ using namespace wtfgpu_dev;
 // ====================================================================== device
 namespace {
 
-__device__ __forceinline__ u64 wave_min(u64 v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const u64 o = __shfl_xor(v, off, 64);
-    v = o < v ? o : v;
-  }
-  return v;
-}
 __device__ __forceinline__ u64 wave_sum(u64 v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -40,6 +32,18 @@ __device__ __forceinline__ u64 readlane64(u64 v, int l) {
   const u32 lo = __builtin_amdgcn_readlane((u32)v, l);
   const u32 hi = __builtin_amdgcn_readlane((u32)(v >> 32), l);
   return ((u64)hi << 32) | lo;
+}
+// The lowest v among the lanes with act, from a start value some such lane
+// holds: move to any lane below the current value until none is (a compare,
+// a ballot and a readlane per round, no LDS round trips; lanes regrouped by
+// rip are in ascending order, so one or two rounds).
+__device__ __forceinline__ u64 active_min(bool act, u64 v, u64 start) {
+  u64 g = start;
+  for (;;) {
+    const u64 m = __ballot(act && v < g);
+    if (m == 0) return g;
+    g = readlane64(v, __ffsll((long long)m) - 1);
+  }
 }
 
 __device__ __forceinline__ bool hash_find(const u64 *keys, u32 mask, u64 key, u32 &slot) {
@@ -1150,6 +1154,13 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
   // moved rip (resume without skip, lflags bit 1)
   if (valid && g_tn.buf && (g_tn.pos[lane] == 0 || (P.lflags[lane] & 2))) WITH_LANE_COPY(tn_regs(P, T));
   const u64 pool_lo = (u64)(uintptr_t)P.pool, pool_hi = pool_lo + (P.npool + 1) * WTFGPU_PAGE_SIZE;
+  // the fields the fast loop reads, once: P is address-taken (the rare-path
+  // calls take it by reference), so a field read in the loop would be a
+  // scratch load each step, and its vmcnt(0) wait would also wait for the
+  // previous step's guest stores
+  const bool cov_on = P.cov_rip != nullptr;
+  const u64 limit = P.limit;
+  wtfgpu_regs_t *const full = P.full;
   u64 steps = 0;
 #ifdef WTFGPU_STAMPS
   u64 stamp_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1172,7 +1183,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       // group = lanes at the min rip; when the wave is converged (the common
       // case) the first active lane's rip is that min and the reduction is skipped
       grip = readlane64(L.rip, __ffsll((long long)am) - 1);
-      if (__ballot(active && L.rip == grip) != am) grip = rfl64(wave_min(active ? L.rip : EMPTY_KEY));
+      if (__ballot(active && L.rip == grip) != am) grip = active_min(active, L.rip, grip);
       have = true;
       const bool cand = active && L.rip == grip;
       WHY(1);
@@ -1192,11 +1203,12 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       WHY(3);
       const u32 flags = h.flags;
       if (flags & (UC_BP | UC_CROSS | UC_BADLEN | UC_UNSUP)) break;
-      if (P.cov_rip && !(flags & UC_COVERED) && (__ballot(ing) & ~h.logged)) break;
+      if (cov_on && !(flags & UC_COVERED) && (__ballot(ing) & ~h.logged)) break;
       const FOp &f = h.f;
       if (fo_op(f) == FO_GENERIC) break;
       steps++;
       have = false;
+      STAMP(6);
       if (ing) {
         skip = false;
         const u32 len = fo_len(f);
@@ -1209,16 +1221,17 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
         for (u32 fills = 0;; fills++) {
           L.miss = 0;
           L.pend = 0;
-          fast_exec(P, L, f, grip + len, next);
+          fast_exec(full, L, f, grip + len, next);
           if (!L.miss || L.miss != 2 || fills >= 3 || !fast_fill(P, L)) break;
         }
         if (!L.miss) {
           L.rip = next;
           L.icount++;
           L.nbytes += len + L.pend;
-          if (P.limit && L.icount > P.limit) L.status = WTFGPU_EXIT_TIMEOUT;
+          if (limit && L.icount > limit) L.status = WTFGPU_EXIT_TIMEOUT;
         }
       }
+      STAMP(7);
       // lanes that still missed keep their rip: the slow step services them.
       // The attempt is not a wave-step of its own (the slow step counts the
       // group once): a slice's length in wave-steps must not depend on which
@@ -1288,7 +1301,9 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       if (flags & UC_BADLEN) {
         if (ing) set_fault(L, WTFGPU_VEC_GP, 0, 0);
       } else if (valid) {  // a position with no lane has no copy slot of its own
-        WITH_LANE_COPY(slow_step(P, T, grip, lptr, ing, skip));
+        bool sk = skip;  // skip stays a register (a reference would put it in scratch for the whole loop)
+        WITH_LANE_COPY(slow_step(P, T, grip, lptr, ing, sk));
+        skip = sk;
       }
       STAMP(5);
       continue;
@@ -3053,10 +3068,11 @@ static void print_stamps(const u64 *s) {
   if (s[0])
     fprintf(stderr,
             "wtfgpu stamps (cycles per wave-step, %llu steps): fast loop %.0f, slow: xlate+fill %.0f, coverage %.0f, "
-            "exec %.0f, cross-page %.0f; slow steps: miss %llu, codepage %llu, ucmiss %llu, other %llu\n",
+            "exec %.0f, cross-page %.0f; slow steps: miss %llu, codepage %llu, ucmiss %llu, other %llu; "
+            "fast lookup %.0f, fast exec %.0f\n",
             (unsigned long long)s[0], (double)s[4] / s[0], (double)s[6] / s[0], (double)s[7] / s[0],
             (double)s[5] / s[0], (double)s[9] / s[0], (unsigned long long)s[12], (unsigned long long)s[13],
-            (unsigned long long)s[14], (unsigned long long)s[15]);
+            (unsigned long long)s[14], (unsigned long long)s[15], (double)s[10] / s[0], (double)s[11] / s[0]);
   fprintf(stderr, "wtfgpu stamps generic ops:");
   for (int k = 0; k < 128; k++)
     if (s[16 + k]) fprintf(stderr, " %d:%llu", k, (unsigned long long)s[16 + k]);

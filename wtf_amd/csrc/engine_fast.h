@@ -281,13 +281,13 @@ __device__ __forceinline__ void vstore(u8 *p, u32 k, const u64 *v) {
 // The FO_V* ops. Anything the generic path would check or fault on (SSE / AVX
 // state off in cr0 / cr4 / xcr0, a misaligned aligned form, a TLB miss, a first
 // write, a page-crossing operand) leaves through L.miss to exec().
-__device__ __forceinline__ int fast_vec(const Dev &P, Lane &L, const FOp &f, u64 nrip) {
+__device__ __forceinline__ int fast_vec(wtfgpu_regs_t *full, Lane &L, const FOp &f, u64 nrip) {
   const u32 op = fo_op(f), sub = fo_sub(f), k = fo_sz(f), n = 8 * k;
   if (!((L.simd >> ((sub >> 1) & 1)) & 1)) {
     L.miss = 1;
     return X_FAULT;
   }
-  wtfgpu_regs_t &F = P.full[L.lane];
+  wtfgpu_regs_t &F = full[L.lane];
   if (op == FO_VZU) {
     for (u32 i = 0; i < 16; i++) F.ymmh[i][0] = F.ymmh[i][1] = 0;
     return X_OK;
@@ -325,10 +325,12 @@ __device__ __forceinline__ int fast_vec(const Dev &P, Lane &L, const FOp &f, u64
   return X_OK;
 }
 
-__device__ __forceinline__ int fast_exec(const Dev &P, Lane &L, const FOp &f, u64 nrip, u64 &next) {
+// `full`: Dev::full, read once by the caller (k_run keeps it in a register
+// rather than reloading it from the kernel argument's scratch copy each step).
+__device__ __forceinline__ int fast_exec(wtfgpu_regs_t *full, Lane &L, const FOp &f, u64 nrip, u64 &next) {
   next = nrip;
   const u32 F = f.fl, op = fo_op(f), sub = fo_sub(f), sz = fo_sz(f);
-  if (op >= FO_VLD) return fast_vec(P, L, f, nrip);
+  if (op >= FO_VLD) return fast_vec(full, L, f, nrip);
   const u64 rsp = R(L, 4);
   u64 a = (F & FF_AREG) ? R(L, fo_ra(f)) : 0;
   u64 b = (F & FF_BREG) ? R(L, fo_rb(f)) : f.imm;
@@ -405,6 +407,9 @@ __device__ __forceinline__ int fast_exec(const Dev &P, Lane &L, const FOp &f, u6
   if (F & FF_WRA) wr(L, fo_ra(f), sz, res);
   if (F & FF_FLAGS) L.rflags = fl;
   return X_OK;
+}
+__device__ __forceinline__ int fast_exec(const Dev &P, Lane &L, const FOp &f, u64 nrip, u64 &next) {
+  return fast_exec(P.full, L, f, nrip, next);
 }
 
 }  // namespace wtfgpu_dev
