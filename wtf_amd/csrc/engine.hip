@@ -311,14 +311,18 @@ struct GPayload {
 constexpr u32 GP_HEAD = (sizeof(u32) * 2 + sizeof(FOp)) / 4;  // dwords of flags, pad, FOp
 static_assert(sizeof(UOp) % 4 == 0 && sizeof(FOp) % 4 == 0, "copied as dwords");
 static_assert(sizeof(UCEntry) == 64, "LDS entry size");
-// Warm start: at the end of a launch, hardware waves 0..UC_IMAGES-1 store their
-// LDS uop cache as an image; at the start of the next launch on the same
-// queue, wave w loads image w % UC_IMAGES (logged masks cleared, UC_COVERED
+// Warm start: at the end of a launch, every hardware wave stores its LDS uop
+// cache as an image; at the start of the next launch on the same queue, wave
+// w loads image w (logged masks cleared, UC_COVERED
 // re-checked against the coverage map) instead of starting empty. UC_COVERED
 // stays true until the coverage map is reset; images are dropped with the
 // shared cache (pool, breakpoints, edges / trace) and on a coverage reset.
-constexpr u32 UC_IMAGES = 64, UC_QUEUES = 8;
-constexpr u64 UC_IMAGE_SET = (u64)UC_IMAGES * UC_N * sizeof(UCEntry);  // bytes per queue
+// One image per wave a launch can have (Dev::warm_n per queue): regrouping
+// keeps lanes in rip order, so wave w of the next launch runs much the code
+// wave w ran (measured: 64 shared images left tlv's fills at a fifth of
+// wave-steps). 16 KB a wave: 32 MB a queue at 131,072 lanes.
+constexpr u32 UC_QUEUES = 2;
+constexpr u64 UC_IMAGE_BYTES = (u64)UC_N * sizeof(UCEntry);
 
 __device__ __forceinline__ u32 uc_slot(u64 key) { return (u32)((key ^ (key >> 12) * 0x9E3779B1u) & (UC_N - 1)); }
 __device__ __forceinline__ u32 uu_slot(u64 key) { return (u32)((key ^ (key >> 12) * 0x9E3779B1u) & (UC_U - 1)); }
@@ -1122,7 +1126,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
   UCUop *uu = sUU[threadIdx.x >> 6];
   // the LDS uop cache: the warm image of an earlier launch, or empty
   const bool wave_live = __ballot(valid) != 0;
-  const UCEntry *img = (P.warm && wave_live) ? (const UCEntry *)P.warm + (u64)(hw % UC_IMAGES) * UC_N : nullptr;
+  const UCEntry *img = (P.warm && wave_live) ? (const UCEntry *)P.warm + (u64)(hw % P.warm_n) * UC_N : nullptr;
   if (img) {
     for (u32 i = lid; i < UC_N; i += 64) {
       UCEntry t = img[i];
@@ -1187,7 +1191,24 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       have = true;
       const bool cand = active && L.rip == grip;
       WHY(1);
-      if (__ballot(cand && (grip >> 12) != L.cvpn)) break;
+      // a new code page: the lane's TLB, else a walk, in registers (what
+      // code_xlate does); a translation that would fault goes to the slow step
+      const bool cx = cand && (grip >> 12) != L.cvpn;
+      if (__ballot(cx)) {
+        if (cx) {
+          u64 td, gp;
+          bool ok = tlb_get(L, grip >> 12, td) && perm_ok(L, td, ACC_X);
+          if (!ok && walk<false>(P, L, grip & ~0xfffull, ACC_X, td, gp) && perm_ok(L, td, ACC_X)) {
+            tlb_put(L, grip >> 12, td);
+            ok = true;
+          }
+          if (ok) {
+            L.cvpn = grip >> 12;
+            L.cptr = td & ~0xfffull;
+          }
+        }
+        if (__ballot(cand && (grip >> 12) != L.cvpn)) break;
+      }
       WHY(3);
       const int leader = __ffsll((long long)__ballot(cand)) - 1;
       const u64 lptr = readlane64(L.cptr, leader);
@@ -1209,27 +1230,46 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       steps++;
       have = false;
       STAMP(6);
-      if (ing) {
-        skip = false;
-        const u32 len = fo_len(f);
-        u64 next;
-        // a TLB miss or a first write (fxlate: miss 2) is served here, on the
-        // lane in registers, and the instruction retried at once, so the group
-        // still takes one wave-step (at most 3 fills); anything else (a fault
-        // to raise, a page-table write, a page-crossing operand, ...) is left
-        // to the slow step, whose exec() raises what it raises
-        for (u32 fills = 0;; fills++) {
+      // a TLB miss or a first write (fxlate: miss 2) is served here, on the
+      // lane in registers, and the instruction retried at once, so the group
+      // still takes one wave-step (at most 3 fill rounds); anything else (a
+      // fault to raise, a page-table write, a page-crossing operand, ...) is
+      // left to the slow step, whose exec() raises what it raises. A first
+      // write's page copy is made by the whole wave, 64 bytes a position: one
+      // memory round trip instead of a lane's 64 dependent ones
+      const u32 len = fo_len(f);
+      u64 next = 0;
+      bool want = ing;
+      if (ing) skip = false;
+      for (u32 round = 0;; round++) {
+        if (want) {
           L.miss = 0;
           L.pend = 0;
           fast_exec(full, L, f, grip + len, next);
-          if (!L.miss || L.miss != 2 || fills >= 3 || !fast_fill(P, L)) break;
+          if (!L.miss || L.miss != 2 || round >= 3) want = false;
         }
-        if (!L.miss) {
-          L.rip = next;
-          L.icount++;
-          L.nbytes += len + L.pend;
-          if (limit && L.icount > limit) L.status = WTFGPU_EXIT_TIMEOUT;
+        if (__ballot(want) == 0) break;
+        u64 csrc = 0, cdst = 0, cgpfn = 0, ctd = 0;
+        if (want && !fast_fill_prep(P, L, csrc, cdst, cgpfn, ctd)) want = false;
+        for (u64 cm = __ballot(want && cdst); cm; cm &= cm - 1) {
+          const int l = __ffsll((long long)cm) - 1;
+          const uint4 *s4 = (const uint4 *)(uintptr_t)readlane64(csrc, l) + lid * 4;
+          uint4 *d4 = (uint4 *)(uintptr_t)readlane64(cdst, l) + lid * 4;
+          const uint4 a = s4[0], b = s4[1], c = s4[2], d = s4[3];
+          d4[0] = a;
+          d4[1] = b;
+          d4[2] = c;
+          d4[3] = d;
         }
+        // the copies land before the lanes read their pages (one wave, one CU)
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        if (want && cdst) fast_fill_finish(P, L, cdst, cgpfn, ctd);
+      }
+      if (ing && !L.miss) {
+        L.rip = next;
+        L.icount++;
+        L.nbytes += len + L.pend;
+        if (limit && L.icount > limit) L.status = WTFGPU_EXIT_TIMEOUT;
       }
       STAMP(7);
       // lanes that still missed keep their rip: the slow step services them.
@@ -1363,7 +1403,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     STAMP(1);
   }
 
-  if (P.warm && wave_live && hw < UC_IMAGES) {  // this wave's cache for the next launch
+  if (P.warm && wave_live && hw < P.warm_n) {  // this wave's cache for the next launch
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     UCEntry *out = (UCEntry *)P.warm + (u64)hw * UC_N;
@@ -1971,7 +2011,8 @@ struct wtfgpu_ctx {
   ExitInfo *d_exinfo = nullptr;
   LaneSys *d_sys = nullptr;
   u32 *d_guc = nullptr;       // device-wide decoded-uop cache (Dev::guc)
-  u8 *d_warm = nullptr;       // LDS uop-cache images, UC_QUEUES sets (Dev::warm)
+  u8 *d_warm = nullptr;       // LDS uop-cache images, UC_QUEUES sets of warm_n (Dev::warm)
+  u32 warm_n = 0;
   u64 *d_rdseed = nullptr;    // per-lane Rdrand seeds (Dev::rd_seed)
   u64 *d_stopargs = nullptr;  // per-lane STOP_ARGS arguments (Dev::stop_args)
   u64 *d_extra = nullptr;     // coverage values outside code pages (Dev::extra_keys)
@@ -2217,7 +2258,7 @@ constexpr u32 kExtraEntries = 1u << 20;
 int warm_clear(wtfgpu_ctx *c) {
   if (!c->d_warm) return WTFGPU_OK;
   HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemset(c->d_warm, 0xff, UC_IMAGE_SET * UC_QUEUES));
+  HIPCHK(hipMemset(c->d_warm, 0xff, UC_IMAGE_BYTES * c->warm_n * UC_QUEUES));
   return WTFGPU_OK;
 }
 
@@ -2996,16 +3037,24 @@ static Dev run_params(wtfgpu_ctx *c, bool regroup) {
   // warm-started LDS uop caches (WTFGPU_WARM=0: every launch starts empty)
   const char *w = getenv("WTFGPU_WARM");
   if (!(w && atoi(w) == 0)) {
+    const u32 need = (u32)((c->P.nlanes + c->P.lpw - 1) / c->P.lpw);  // the most waves a launch can have
+    if (c->d_warm && c->warm_n < need) {
+      (void)hipDeviceSynchronize();
+      (void)hipFree(c->d_warm);
+      c->d_warm = nullptr;
+    }
     if (!c->d_warm) {
-      if (hipMalloc((void **)&c->d_warm, UC_IMAGE_SET * UC_QUEUES) != hipSuccess) {
+      c->warm_n = need;
+      const u64 bytes = UC_IMAGE_BYTES * need * UC_QUEUES;
+      if (hipMalloc((void **)&c->d_warm, bytes) != hipSuccess) {
         c->d_warm = nullptr;
-      } else if (hipMemset(c->d_warm, 0xff, UC_IMAGE_SET * UC_QUEUES) != hipSuccess ||
-                 hipDeviceSynchronize() != hipSuccess) {
+      } else if (hipMemset(c->d_warm, 0xff, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
         (void)hipFree(c->d_warm);
         c->d_warm = nullptr;
       }
     }
-    Q.warm = c->d_warm ? c->d_warm + (u64)(c->cur_queue % UC_QUEUES) * UC_IMAGE_SET : nullptr;
+    Q.warm = c->d_warm ? c->d_warm + (u64)(c->cur_queue % UC_QUEUES) * UC_IMAGE_BYTES * c->warm_n : nullptr;
+    Q.warm_n = c->warm_n;
   } else {
     Q.warm = nullptr;
   }

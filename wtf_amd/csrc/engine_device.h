@@ -119,6 +119,7 @@ struct Dev {
   u32 *guc;
   u32 guc_mask;
   u8 *warm;  // k_run: per-wave images of the LDS uop cache carried between launches (null: cold start)
+  u32 warm_n;  // images in the set (waves a launch can have)
   u64 *rd_seed;           // [nlanes] Rdrand seeds (WTFGPU_BPACT_RDRAND)
   u64 *stop_args;         // [nlanes][6] arguments kept by WTFGPU_BPACT_STOP_ARGS
   // values of the aggregate coverage that are not code bytes of a code page

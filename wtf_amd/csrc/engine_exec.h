@@ -205,16 +205,18 @@ __device__ __noinline__ bool user_fetch_ok(const Dev &P, const Lane &L, u64 va) 
 
 // Copy-on-write into overlay slot `slot` of `lane`: the page joins the dirty
 // list (bochscpu_backend.cc:887-889 DirtyGpa; dropped again by restore :751-772).
+// One lane's copy (the slow path; k_run's fast loop copies with the whole
+// wave): 256 bytes in flight per round, 16 rounds.
 __device__ __forceinline__ u8 *cow_copy(const Dev &P, u32 lane, u32 slot, u64 gpfn, const u8 *src) {
   u8 *dst = P.ov_data + ((u64)lane * P.K + slot) * WTFGPU_PAGE_SIZE;
-  const uint4 *s4 = (const uint4 *)src;
-  uint4 *d4 = (uint4 *)dst;
-  for (int i = 0; i < 256; i += 4) {
-    const uint4 a = s4[i], b = s4[i + 1], c = s4[i + 2], d = s4[i + 3];
-    d4[i] = a;
-    d4[i + 1] = b;
-    d4[i + 2] = c;
-    d4[i + 3] = d;
+  const uint4 *__restrict__ s4 = (const uint4 *)src;
+  uint4 *__restrict__ d4 = (uint4 *)dst;
+  for (int i = 0; i < 256; i += 16) {
+    uint4 t[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) t[j] = s4[i + j];
+#pragma unroll
+    for (int j = 0; j < 16; j++) d4[i + j] = t[j];
   }
   P.ov_gpfn[(u64)slot * P.nlanes + lane] = (u32)gpfn;
   return dst;
@@ -264,6 +266,33 @@ __device__ __forceinline__ bool fast_fill(const Dev &P, Lane &L) {
   }
   tlb_put(L, va >> 12, td);
   return true;
+}
+
+// fast_fill in two halves around a copy the whole wave makes (k_run): the
+// walk and checks, then either the TLB fill (nothing to copy: dst = 0) or the
+// page to copy (src, dst: the lane's next overlay slot, taken now); after the
+// copy, fast_fill_finish records the page as the lane's own. false = as
+// fast_fill's false.
+__device__ __forceinline__ bool fast_fill_prep(const Dev &P, Lane &L, u64 &src, u64 &dst, u64 &gpfn, u64 &td) {
+  const u64 va = L.miss_va;
+  const int acc = (int)L.miss_acc;
+  dst = 0;
+  if (!walk<false>(P, L, va, acc, td, gpfn) || !perm_ok(L, td, acc)) return false;
+  if (acc == ACC_W && !(td & T_PRIV)) {
+    if ((td & T_PT) || L.ovn >= P.K) return false;
+    src = td & ~0xfffull;
+    dst = (u64)(uintptr_t)(P.ov_data + ((u64)L.lane * P.K + L.ovn) * WTFGPU_PAGE_SIZE);
+    return true;
+  }
+  tlb_put(L, va >> 12, td);
+  return true;
+}
+__device__ __forceinline__ void fast_fill_finish(const Dev &P, Lane &L, u64 dst, u64 gpfn, u64 td) {
+  P.ov_gpfn[(u64)L.ovn * P.nlanes + L.lane] = (u32)gpfn;
+  L.ovn++;
+  L.bloom |= bloom_bit(gpfn);
+  tlb_flush(L);  // other vpns may alias the old page
+  tlb_put(L, L.miss_va >> 12, dst | (td & 0xfff) | T_PRIV);
 }
 
 // Fast path: TLB hit + permission check. A miss (or a write to a shared page)
