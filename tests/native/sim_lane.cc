@@ -252,6 +252,25 @@ int sim_run_full(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, c
   return 0;
 }
 
+// Decode + digest of up to 16 instruction bytes (diagnostic: which forms the
+// fast path leaves generic). out: decode result, UOp op, sub, FOp op, length,
+// seg, p67, rep, rex, asz, bsz, asrc, bsrc, is_mem, supported.
+int sim_digest(const uint8_t *bytes, uint32_t avail, uint32_t *out) {
+  IBytes ib;
+  ib.avail = avail > 16 ? 16 : avail;
+  uint8_t b[16] = {};
+  memcpy(b, bytes, ib.avail);
+  memcpy(&ib.lo, b, 8);
+  memcpy(&ib.hi, b + 8, 8);
+  UOp d;
+  const int dr = decode(ib, d);
+  FOp f{};
+  if (dr == 0) digest(d, f);
+  const uint32_t v[15] = {(uint32_t)dr, d.op, d.sub, fo_op(f), d.len, d.seg, d.p67, d.rep, d.rex,
+                          d.asz, d.bsz, d.asrc, d.bsrc, d.is_mem, d.supported};
+  memcpy(out, v, sizeof(v));
+  return dr;
+}
 int sim_run_mode(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, const wtfgpu_regs_t *r0,
                  uint64_t limit, SimResult *out, int fast, uint64_t *fast_count, uint64_t win_va) {
   return sim_run_full(gpfns, pages, npages, r0, limit, out, fast, fast_count, win_va, nullptr, nullptr);

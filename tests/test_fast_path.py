@@ -268,3 +268,48 @@ def test_opcodes_invalid_in_64bit_mode_raise_ud(op):
     for fast in (False, True):
         out = sim_run(L, sp, regs, fast=fast)
         assert (out.status, out.vector, out.icount, out.rip) == (EXIT_FAULT, 6, 0, regs.rip), (hex(op), fast)
+
+
+def test_indirect_branches_unary_bit_and_segment_forms_fast_equals_slow():
+    """The forms added to the fast path for tlv / HEVD's hot code: fs / gs
+    relative moves, not / neg, test with a memory operand, shifts by cl,
+    bt / bts with register and immediate bit numbers, call [mem], call reg,
+    jmp reg: the fast form gives the generic path's lane, and runs."""
+    from tests.test_sse import CODE_VA
+    code = bytes.fromhex(
+        "65488b042510000000"   # 0  mov rax, gs:[0x10]
+        "6548890425 18000000"  # 9  mov gs:[0x18], rax
+        "48f7d0"               # 18 not rax
+        "48f7d8"               # 21 neg rax
+        "48f70705000000"       # 24 test qword [rdi], 5
+        "48854708"             # 31 test [rdi+8], rax
+        "48d3e0"               # 35 shl rax, cl
+        "480fabc8"             # 38 bts rax, rcx
+        "480fbae203"           # 42 bt rdx, 3
+        "ff5710"               # 47 call qword [rdi+16] -> 60
+        .replace(" ", "")) + b"\xcc" * 10
+    code += bytes.fromhex(
+        "5b"                   # 60 pop rbx
+        "488d1d04000000"       # 61 lea rbx, [rip+4] -> 72
+        "ffd3"                 # 68 call rbx
+        "cccc"                 # 70
+        "59"                   # 72 pop rcx
+        "488d1503000000"       # 73 lea rdx, [rip+3] -> 83
+        "ffe2"                 # 80 jmp rdx
+        "cc")                  # 82; 83 is layout's trailing int3
+    assert len(code) == 83
+    page = BUF & ~0xFFF
+    win = bytearray(512)
+    win[0:8] = (0x1234).to_bytes(8, "little")
+    win[8:16] = (0xF0F0).to_bytes(8, "little")
+    win[16:24] = (CODE_VA + 60).to_bytes(8, "little")
+    win[0x110:0x118] = (0xDEADBEEF).to_bytes(8, "little")
+    L = sim_lib()
+    sp, regs = layout(code, page, bytes(win))
+    regs.gpr[4], regs.gpr[7], regs.gpr[1], regs.gpr[2] = page + 0x800, page, 5, 0xFF
+    regs.seg[5].base = page + 0x100  # gs
+    slow, fast, n = run_both(L, sp, regs, page)
+    assert same(slow, fast)
+    assert fast.status == INT3 and fast.rip == CODE_VA + 83, (fast.status, hex(fast.rip))
+    assert n == 16, n  # every instruction but the trailing int3 ran on the fast path
+    assert bytes(fast.win[0x118:0x120]) == (0xDEADBEEF).to_bytes(8, "little")

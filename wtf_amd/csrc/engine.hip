@@ -324,7 +324,19 @@ static_assert(sizeof(UCEntry) == 64, "LDS entry size");
 constexpr u32 UC_QUEUES = 2;
 constexpr u64 UC_IMAGE_BYTES = (u64)UC_N * sizeof(UCEntry);
 
-__device__ __forceinline__ u32 uc_slot(u64 key) { return (u32)((key ^ (key >> 12) * 0x9E3779B1u) & (UC_N - 1)); }
+// WTFGPU_UC_WAYS = 2: two-way sets (entries 2s, 2s + 1), a fill replaces the
+// way a per-wave counter picks; tlv's 228-instruction loop missed a fifth of
+// its wave-steps direct-mapped (scripts: a trace replay gives 23 % direct,
+// 14 % two-way at 256 entries).
+#ifndef WTFGPU_UC_WAYS
+#define WTFGPU_UC_WAYS 2
+#endif
+constexpr u32 UC_WAYS = WTFGPU_UC_WAYS;
+__device__ __forceinline__ u32 uc_slot(u64 key) {
+  if (UC_WAYS == 1) return (u32)((key ^ (key >> 12) * 0x9E3779B1u) & (UC_N - 1));
+  // multiplicative hash: the offset bits mix into the set index too
+  return (u32)((key * 0x9E3779B97F4A7C15ull) >> (64 - __builtin_ctz(UC_N / UC_WAYS))) * UC_WAYS;
+}
 __device__ __forceinline__ u32 uu_slot(u64 key) { return (u32)((key ^ (key >> 12) * 0x9E3779B1u) & (UC_U - 1)); }
 
 template <typename T>
@@ -522,7 +534,7 @@ __device__ __forceinline__ bool uc_fill_shared(const Dev &P, UCEntry *e, UCUop *
   if (!P.guc) return false;
   const u32 pj = guc_payload_index(lid);
   u32 *head = e ? (u32 *)&e->flags : nullptr, *uop = (u32 *)&us->u;
-  const u32 *gw = P.guc + (u64)guc_slot(P, key) * GUC_WORDS;
+  u32 *gw = P.guc + (u64)guc_slot(P, key) * GUC_WORDS;
   const u32 w = lid < GUC_WORDS ? gw[lid] : 0;
   const bool tag = lid < GUC_WORDS && (lid & 15) >= 14;
   const bool bad = tag && w != ((lid & 1) ? (u32)(key >> 32) : (u32)key);
@@ -532,7 +544,15 @@ __device__ __forceinline__ bool uc_fill_shared(const Dev &P, UCEntry *e, UCUop *
   } else if (pj < GUC_PAYLOAD) {
     uop[pj - GP_HEAD] = w;
   }
-  const u32 flags = __builtin_amdgcn_readlane(w, 0) | (e ? covered_flag(P, rip, off) : 0);
+  // UC_COVERED is cached in the shared entry once seen (coverage only grows
+  // until wtfgpu_reset_coverage, which clears the shared cache): most fills
+  // skip the map lookup's dependent loads
+  const u32 sflags = __builtin_amdgcn_readlane(w, 0);
+  u32 flags = sflags;
+  if (e && !(sflags & UC_COVERED)) {
+    flags |= covered_flag(P, rip, off);
+    if ((flags & UC_COVERED) && lid == 0) gw[0] = flags;
+  }
   __builtin_amdgcn_wave_barrier();
   if (lid == 0) {
     us->key = key;
@@ -580,7 +600,7 @@ __device__ __noinline__ void uc_fill(const Dev &P, UCEntry *e, UCUop *us, u64 ke
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   if (gw) {  // publish (static flags only); one coalesced store of 3 tagged lines
     u32 v = 0;
-    if (pj < GP_HEAD) v = pj == 0 ? flags : pj == 1 ? 0u : ((const u32 *)&f)[pj - 2];
+    if (pj < GP_HEAD) v = pj == 0 ? (flags | dyn) : pj == 1 ? 0u : ((const u32 *)&f)[pj - 2];
     else if (pj < GUC_PAYLOAD) v = uop[pj - GP_HEAD];
     else if (lid < GUC_WORDS && (lid & 15) >= 14) v = (lid & 1) ? (u32)(key >> 32) : (u32)key;
     if (lid < GUC_WORDS) gw[lid] = v;
@@ -1164,8 +1184,9 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
   // previous step's guest stores
   const bool cov_on = P.cov_rip != nullptr;
   const u64 limit = P.limit;
-  wtfgpu_regs_t *const full = P.full;
+  const FastMem fm = fast_mem(P);
   u64 steps = 0;
+  u32 fill_way = 0;  // two-way uop cache: the way the next fill replaces (wave-uniform)
 #ifdef WTFGPU_STAMPS
   u64 stamp_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u64 tprev_ = __builtin_amdgcn_s_memtime();
@@ -1217,8 +1238,14 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       const u64 key = lptr | (grip & 0xfff);
       UCEntry *e = &uc[uc_slot(key)];
       // one LDS round trip: key, logged mask, flags and the FOp are contiguous
+      // (both ways of the set read at once)
       UCHead h;
       lds_uniform_read(&e->h, h);
+      if (UC_WAYS == 2) {
+        UCHead h1;
+        lds_uniform_read(&e[1].h, h1);
+        if (h.key != key) h = h1;
+      }
       WHY(2);
       if (h.key != key) break;
       WHY(3);
@@ -1245,7 +1272,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
         if (want) {
           L.miss = 0;
           L.pend = 0;
-          fast_exec(full, L, f, grip + len, next);
+          fast_exec(fm, L, f, grip + len, next);
           if (!L.miss || L.miss != 2 || round >= 3) want = false;
         }
         if (__ballot(want) == 0) break;
@@ -1317,6 +1344,10 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     const u32 off = (u32)(grip & 0xfff);
     const u64 key = lptr | off;
     UCEntry *e = &uc[uc_slot(key)];
+    if (UC_WAYS == 2 && rfl64(e->key) != key) {
+      if (rfl64(e[1].key) == key) e += 1;
+      else e += (fill_way++ & 1);  // the way a fill replaces
+    }
     const bool cacheable = lptr >= pool_lo && lptr < pool_hi;
     if (cacheable && rfl64(e->key) != key) {
 #if WTFGPU_FILL_INLINE
@@ -3615,7 +3646,7 @@ int wtfgpu_reset_coverage(wtfgpu_ctx *c) {
   HIPCHK(hipMemsetAsync(c->d_covshadow, 0, c->ncovslots * WTFGPU_PAGE_SIZE, c->stream));
   if (c->d_extra) HIPCHK(hipMemsetAsync(c->d_extra, 0xff, (u64)kExtraEntries * 8, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  return warm_clear(c);  // images carry UC_COVERED
+  return guc_clear(c);  // shared entries and images carry UC_COVERED
 }
 
 int wtfgpu_set_trace(wtfgpu_ctx *c, uint32_t per_lane) {

@@ -32,13 +32,15 @@ enum : u32 {
   FO_LEA,     // res = ea
   FO_INCDEC,  // res = a +/- 1, CF kept
   FO_JCC,     // next = nrip + imm if cond(sub)
-  FO_JMP,     // next = nrip + imm
-  FO_CALL,    // res = nrip (pushed), next = nrip + imm
+  FO_JMP,     // next = nrip + imm, or b (FF_BREG)
+  FO_CALL,    // res = nrip (pushed), next = nrip + imm, or b (FF_BREG)
   FO_RET,     // next = b (popped)
   FO_MOVX,    // res = zext/sext(b, szb), sub 1 = sign
   FO_SHIFT,   // res = shift_op(sub, a, imm)
   FO_CMOV,    // res = cond(sub) ? b : a
   FO_SETCC,   // res = cond(sub)
+  FO_BT,      // bt / bts / btr / btc (sub 4..7) of register a, bit b: CF, res
+  FO_UNARY,   // sub 0: res = ~a (not); sub 1: res = 0 - a, flags (neg)
   // SSE / AVX data movement (engine_sse.h semantics), ra = the xmm / ymm
   // register, sz = operand bytes / 8; sub bit 0: aligned form, bit 1: VEX
   // (VEX.128 zeroes bits 255:128), bit 2 (FO_VMOV): the zeroing xor idiom
@@ -64,7 +66,7 @@ enum : u32 {
 constexpr u32 NOREG = 16;
 
 struct FOp {
-  u32 w0;  // op | sub << 8 | sz << 12 | szb << 16 | len << 20 | scale << 26 | riprel << 28
+  u32 w0;  // op | sub << 8 | sz << 12 | szb << 16 | len << 20 | scale << 26 | riprel << 28 | seg << 29 (1 fs, 2 gs)
   u32 fl;  // FF_*
   u32 w2;  // ra | rb << 8 | base << 16 | index << 24
   u32 pad;
@@ -78,6 +80,7 @@ __device__ __forceinline__ u32 fo_szb(const FOp &f) { return (f.w0 >> 16) & 0xf;
 __device__ __forceinline__ u32 fo_len(const FOp &f) { return (f.w0 >> 20) & 0x3f; }
 __device__ __forceinline__ u32 fo_scale(const FOp &f) { return (f.w0 >> 26) & 3; }
 __device__ __forceinline__ u32 fo_riprel(const FOp &f) { return (f.w0 >> 28) & 1; }
+__device__ __forceinline__ u32 fo_seg(const FOp &f) { return (f.w0 >> 29) & 3; }
 __device__ __forceinline__ u32 fo_ra(const FOp &f) { return f.w2 & 0xff; }
 __device__ __forceinline__ u32 fo_rb(const FOp &f) { return (f.w2 >> 8) & 0xff; }
 __device__ __forceinline__ u32 fo_base(const FOp &f) { return (f.w2 >> 16) & 0xff; }
@@ -134,7 +137,7 @@ __device__ __forceinline__ void digest(const UOp &u, FOp &f) {
   u32 ra_ = ra, rb_ = rb, sz_ = u.asz;
   if (u.op == O_SSE && u.supported && !u.seg && !u.p67) {
     digest_sse(u, op, sub, ra_, rb_, sz_);
-  } else if (u.supported && !u.seg && !u.p67 && !u.rep && !hb) {
+  } else if (u.supported && !u.p67 && !u.rep && !hb) {
     switch (u.op) {
       case O_NOP: op = FO_NOP; break;
       case O_MOV:
@@ -158,6 +161,15 @@ __device__ __forceinline__ void digest(const UOp &u, FOp &f) {
         sub = 4;
         if (areg && breg) op = FO_ALU, fl = FF_AREG | FF_BREG | FF_FLAGS;
         else if (areg && bimm) op = FO_ALU, fl = FF_AREG | FF_FLAGS;
+        else if (amem && breg) op = FO_ALU, fl = FF_BREG | FF_EA | FF_MR_A | FF_FLAGS;
+        else if (amem && bimm) op = FO_ALU, fl = FF_EA | FF_MR_A | FF_FLAGS;
+        break;
+      case O_NOT:
+      case O_NEG:
+        sub = u.op == O_NEG ? 1 : 0;
+        if (areg) op = FO_UNARY, fl = FF_AREG | FF_WRA;
+        else if (amem) op = FO_UNARY, fl = FF_EA | FF_MR_A | FF_MW;
+        if (op && u.op == O_NEG) fl |= FF_FLAGS;
         break;
       case O_LEA:
         if (areg && u.is_mem) op = FO_LEA, fl = FF_EA | FF_WRA;
@@ -166,11 +178,14 @@ __device__ __forceinline__ void digest(const UOp &u, FOp &f) {
         if (areg) op = FO_INCDEC, fl = FF_AREG | FF_WRA | FF_FLAGS;
         break;
       case O_JCC: op = FO_JCC; break;
-      case O_JMP:
+      case O_JMP:  // relative, or a 64-bit register (the memory forms stay generic)
         if (bimm) op = FO_JMP;
+        else if (breg && u.bsz == 8) op = FO_JMP, fl = FF_BREG;
         break;
       case O_CALL:
         if (bimm) op = FO_CALL, fl = FF_PUSH | FF_MW;
+        else if (breg && u.bsz == 8) op = FO_CALL, fl = FF_BREG | FF_PUSH | FF_MW;
+        else if (bmem && u.bsz == 8) op = FO_CALL, fl = FF_EA | FF_MR_B | FF_PUSH | FF_MW;  // call [mem]
         break;
       case O_RET: op = FO_RET, fl = FF_POP | FF_MR_B; break;
       case O_PUSH:
@@ -189,7 +204,13 @@ __device__ __forceinline__ void digest(const UOp &u, FOp &f) {
         if (areg && (bimm || u.bsrc == L_ONE)) {
           op = FO_SHIFT, fl = FF_AREG | FF_WRA | FF_FLAGS;
           if (u.bsrc == L_ONE) imm = 1;
+        } else if (areg && u.bsrc == L_CL) {  // the count in cl (shift_op masks it)
+          op = FO_SHIFT, fl = FF_AREG | FF_BREG | FF_WRA | FF_FLAGS, rb_ = 1;
         }
+        break;
+      case O_BT:  // register forms only (a memory bit string reaches past the operand)
+        if (areg && (breg || bimm) && u.sub >= 4)
+          op = FO_BT, fl = FF_AREG | (breg ? FF_BREG : 0) | (u.sub != 4 ? FF_WRA : 0) | FF_FLAGS;
         break;
       case O_CMOV:
         if (areg && breg) op = FO_CMOV, fl = FF_AREG | FF_BREG | FF_WRA;
@@ -199,10 +220,15 @@ __device__ __forceinline__ void digest(const UOp &u, FOp &f) {
         break;
       default: break;
     }
+    // an fs / gs override only matters to a memory operand's address; any
+    // other fast form with one stays generic
+    // (lea computes the offset alone: generic too)
+    if (u.seg && (!(fl & FF_EA) || op == FO_LEA)) op = FO_GENERIC;
   }
   const u32 base = u.base >= 0 ? (u32)u.base : NOREG, index = u.index >= 0 ? (u32)u.index : NOREG;
+  const u32 fseg = u.seg == 4 ? 1 : u.seg == 5 ? 2 : 0;
   f.w0 = op | (sub & 0xf) << 8 | (sz_ & 0xf) << 12 | (u.bsz & 0xf) << 16 | (u.len & 0x3f) << 20 |
-         (u.scale & 3) << 26 | (u.riprel & 1) << 28;
+         (u.scale & 3) << 26 | (u.riprel & 1) << 28 | fseg << 29;
   f.fl = fl;
   f.w2 = (ra_ & 0xff) | (rb_ & 0xff) << 8 | (base & 0xff) << 16 | (index & 0xff) << 24;
   f.pad = 0;
@@ -325,12 +351,19 @@ __device__ __forceinline__ int fast_vec(wtfgpu_regs_t *full, Lane &L, const FOp 
   return X_OK;
 }
 
-// `full`: Dev::full, read once by the caller (k_run keeps it in a register
-// rather than reloading it from the kernel argument's scratch copy each step).
-__device__ __forceinline__ int fast_exec(wtfgpu_regs_t *full, Lane &L, const FOp &f, u64 nrip, u64 &next) {
+// The Dev arrays the fast path reads, taken once by the caller (k_run keeps
+// them in registers rather than reloading them from the kernel argument's
+// scratch copy each step).
+struct FastMem {
+  wtfgpu_regs_t *full;
+  const u64 *fs_base, *gs_base;
+};
+__device__ __forceinline__ FastMem fast_mem(const Dev &P) { return FastMem{P.full, P.fs_base, P.gs_base}; }
+
+__device__ __forceinline__ int fast_exec(const FastMem &M, Lane &L, const FOp &f, u64 nrip, u64 &next) {
   next = nrip;
   const u32 F = f.fl, op = fo_op(f), sub = fo_sub(f), sz = fo_sz(f);
-  if (op >= FO_VLD) return fast_vec(full, L, f, nrip);
+  if (op >= FO_VLD) return fast_vec(M.full, L, f, nrip);
   const u64 rsp = R(L, 4);
   u64 a = (F & FF_AREG) ? R(L, fo_ra(f)) : 0;
   u64 b = (F & FF_BREG) ? R(L, fo_rb(f)) : f.imm;
@@ -339,6 +372,7 @@ __device__ __forceinline__ int fast_exec(wtfgpu_regs_t *full, Lane &L, const FOp
     addr = f.disp + (fo_riprel(f) ? nrip : 0);
     if (fo_base(f) != NOREG) addr += R(L, fo_base(f));
     if (fo_index(f) != NOREG) addr += R(L, fo_index(f)) << fo_scale(f);
+    if (fo_seg(f)) addr += (fo_seg(f) == 1 ? M.fs_base : M.gs_base)[L.lane];
   } else if (F & FF_PUSH) {
     addr = rsp - 8;
   } else {
@@ -346,9 +380,12 @@ __device__ __forceinline__ int fast_exec(wtfgpu_regs_t *full, Lane &L, const FOp
   }
   // ---- the memory read
   u8 *mp = nullptr;
+  // (a write to the read's own address makes it a read-modify-write; call
+  // [mem] reads its target and writes the stack)
+  const bool rmw = (F & FF_MW) && (F & (FF_MR_A | FF_MR_B)) && !(F & FF_PUSH);
   if (F & (FF_MR_A | FF_MR_B)) {
     const u32 rsz = (F & (FF_PUSH | FF_POP)) ? 8 : (op == FO_MOVX ? fo_szb(f) : sz);
-    mp = fxlate(L, addr, rsz, (F & FF_MW) ? ACC_W : ACC_R);
+    mp = fxlate(L, addr, rsz, rmw ? ACC_W : ACC_R);
     if (!mp) return X_FAULT;
     const u64 v = load_le(mp, rsz);
     L.pend += rsz;
@@ -371,10 +408,18 @@ __device__ __forceinline__ int fast_exec(wtfgpu_regs_t *full, Lane &L, const FOp
     case FO_JCC:
       if (cond(fl, sub)) next = nrip + f.imm;
       break;
-    case FO_JMP: next = nrip + f.imm; break;
-    case FO_CALL:
+    case FO_JMP: next = (F & FF_BREG) ? b : nrip + b; break;
+    case FO_CALL:  // indirect: the target in a register or read from memory
       res = nrip;
-      next = nrip + f.imm;
+      next = (F & (FF_BREG | FF_MR_B)) ? b : nrip + b;
+      break;
+    case FO_UNARY:
+      if (sub) {
+        res = alu2(5, 0, a, sz, fl, fo);
+        fl = with_status(fl, fo);
+      } else {
+        res = ~a;
+      }
       break;
     case FO_RET: next = b; break;
     case FO_MOVX: {
@@ -383,7 +428,13 @@ __device__ __forceinline__ int fast_exec(wtfgpu_regs_t *full, Lane &L, const FOp
       res = sub ? sext(b, szb) : b;
       break;
     }
-    case FO_SHIFT: res = shift_op(sub, a, (u32)f.imm, sz, fl); break;
+    case FO_SHIFT: res = shift_op(sub, a, (u32)b, sz, fl); break;  // b: the immediate, or rcx
+    case FO_BT: {
+      const u64 bitoff = b & (8 * sz - 1);
+      res = sub == 5 ? (a | (1ull << bitoff)) : sub == 6 ? (a & ~(1ull << bitoff)) : (a ^ (1ull << bitoff));
+      fl = (fl & ~F_CF) | ((a >> bitoff) & 1);
+      break;
+    }
     case FO_CMOV:
       // a false condition still zero-extends a 32-bit destination
       res = cond(fl, sub) ? b : a;
@@ -394,8 +445,8 @@ __device__ __forceinline__ int fast_exec(wtfgpu_regs_t *full, Lane &L, const FOp
   // ---- the memory write
   if (F & FF_MW) {
     const u32 wsz = (F & FF_PUSH) ? 8 : sz;
-    if (!mp) {
-      mp = fxlate(L, addr, wsz, ACC_W);
+    if (!rmw) {
+      mp = fxlate(L, (F & FF_PUSH) ? rsp - 8 : addr, wsz, ACC_W);
       if (!mp) return X_FAULT;
     }
     store_le(mp, wsz, res & szmask(wsz));
@@ -409,7 +460,7 @@ __device__ __forceinline__ int fast_exec(wtfgpu_regs_t *full, Lane &L, const FOp
   return X_OK;
 }
 __device__ __forceinline__ int fast_exec(const Dev &P, Lane &L, const FOp &f, u64 nrip, u64 &next) {
-  return fast_exec(P.full, L, f, nrip, next);
+  return fast_exec(fast_mem(P), L, f, nrip, next);
 }
 
 }  // namespace wtfgpu_dev
