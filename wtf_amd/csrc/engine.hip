@@ -1272,7 +1272,14 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
         if (want) {
           L.miss = 0;
           L.pend = 0;
-          fast_exec(fm, L, f, grip + len, next);
+          // the FOp as an opaque value each round: otherwise everything
+          // fast_exec derives from it (masks, shift counts, every op's
+          // conditions) is hoisted out of this loop as invariant, stays live
+          // across it and spills to VGPR lanes: ~100 v_writelane and ~280
+          // v_readlane on every wave-step
+          FOp fr = f;
+          asm volatile("" : "+s"(fr.w0), "+s"(fr.fl), "+s"(fr.w2), "+s"(fr.disp), "+s"(fr.imm));
+          fast_exec(fm, L, fr, grip + len, next);
           if (!L.miss || L.miss != 2 || round >= 3) want = false;
         }
         if (__ballot(want) == 0) break;
