@@ -2,7 +2,7 @@
 # $STAMPLIB, default exp/stamps), fixed lane order and regrouped.
 set -o pipefail
 mkdir -p gpurun_out
-for mode in "WTFGPU_REGROUP_STEPS=0" "WTFGPU_REGROUP_AUTO=0"; do
+for mode in ${MODES:-"WTFGPU_REGROUP_STEPS=0" "WTFGPU_REGROUP_AUTO=0"}; do
   echo "== $mode"
   timeout -k 10 180 env $mode WTFGPU_LIB=$PWD/${STAMPLIB:-exp/stamps}/libwtfgpu.so python -u -c "
 import bench

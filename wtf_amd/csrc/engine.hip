@@ -2110,10 +2110,17 @@ struct wtfgpu_ctx {
   // runs the better one, probing the other every kProbe-th run; all counts,
   // no clocks, so a fixed-seed campaign schedules the same way every time
   // (WTFGPU_REGROUP_AUTO=0: always regroup)
+  // A synchronous run to completion (wtfgpu_run with no step bound) ends
+  // with the same lane states in either order, so there the choice is by
+  // measured kernel time per retired instruction instead: a run whose longest
+  // lane sets its length (SYN) gains nothing from denser wave-steps and pays
+  // for the sorts and the shorter launches.
   bool regroup_auto = true;
   double lps_sched[2] = {0, 0};  // lanes per wave-step, EMA: [0] fixed order, [1] regrouped
   u64 rg_runs = 0;
   u8 rg_used[2] = {2, 2};  // per queue: its run in flight regroups (1), not (0), unmeasured (2)
+  double nspi_sched[2] = {0, 0};  // run-to-completion runs: kernel ns per retired instruction, EMA
+  u64 rg_sync_runs = 0;
   u32 async_launches = 0;
   // the current queue's resources live in the members above; the others here
   QueueRes queues[2];
@@ -3120,6 +3127,30 @@ static u64 regroup_now(wtfgpu_ctx *c, u32 count) {
   c->rg_used[c->cur_queue & 1] = on;
   return on ? c->regroup_steps : 0;
 }
+// The same choice for a synchronous run to completion, by kernel time per
+// retired instruction (its result does not depend on the lane order).
+static u64 regroup_now_timed(wtfgpu_ctx *c, u32 count, int &used) {
+  used = 2;
+  if (!c->regroup_steps || count < 2 * c->P.lpw) return 0;
+  if (!c->regroup_auto) return c->regroup_steps;
+  static constexpr u64 kProbe = 32;
+  const u64 i = c->rg_sync_runs++;
+  bool on;
+  if (c->nspi_sched[1] == 0) on = true;
+  else if (c->nspi_sched[0] == 0) on = false;
+  else {
+    on = c->nspi_sched[1] < c->nspi_sched[0];
+    if (i % kProbe == kProbe - 1) on = !on;
+  }
+  used = on;
+  return on ? c->regroup_steps : 0;
+}
+static void regroup_observe_timed(wtfgpu_ctx *c, int used, double ms, u64 retired) {
+  if (used > 1 || retired < 4096) return;
+  const double v = ms * 1e6 / (double)retired;
+  double &e = c->nspi_sched[used];
+  e = e == 0 ? v : 0.75 * e + 0.25 * v;
+}
 static void regroup_observe(wtfgpu_ctx *c, u64 group_steps, u64 retired) {
   const u8 used = c->rg_used[c->cur_queue & 1];
   if (used > 1 || group_steps < 64) return;
@@ -3180,7 +3211,10 @@ int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps
   // lanes are sorted by rip so that lanes that diverged from their wave
   // neighbours meet lanes at the same rip in another wave (wtfgpu_set_regroup,
   // WTFGPU_REGROUP_STEPS; 0 = fixed lane order; regroup_now).
-  const u64 regroup = regroup_now(c, count);
+  // (no step bound: a run to completion, see wtfgpu_ctx::nspi_sched)
+  const bool to_end = max_steps >= (1ull << 32);
+  int used_timed = 2;
+  const u64 regroup = to_end ? regroup_now_timed(c, count, used_timed) : regroup_now(c, count);
   if (regroup) {
     chunk = regroup;
     if (int rc = regroup_buffers(c)) return rc;
@@ -3191,7 +3225,7 @@ int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps
 #endif
   // launches per host synchronisation: regrouped chunks are short, so a
   // group of them is queued at once (one stats read-back per group)
-  const u32 group = regroup ? (u32)std::max<u64>(1, 1024 / regroup) : 1;
+  const u32 group = regroup ? (u32)std::max<u64>(1, 4096 / regroup) : 1;
   u64 done = 0;
   float ms_total = 0;
   for (;;) {
@@ -3216,7 +3250,8 @@ int wtfgpu_run(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max_steps
     print_stamps(s);
     if (s[2] == 0 || done >= max_steps) break;
   }
-  regroup_observe(c, st.group_steps, st.lane_retired);
+  if (to_end) regroup_observe_timed(c, used_timed, ms_total, st.lane_retired);
+  else regroup_observe(c, st.group_steps, st.lane_retired);
   st.kernel_ms = ms_total;
   if (stats) *stats = st;
   return WTFGPU_OK;

@@ -360,104 +360,122 @@ struct FastMem {
 };
 __device__ __forceinline__ FastMem fast_mem(const Dev &P) { return FastMem{P.full, P.fs_base, P.gs_base}; }
 
+// One exit and one commit on every path: a failed attempt (ok = false, L.miss
+// set) writes the unchanged values back. The guest registers are an array the
+// compiler keeps in VGPRs and indexes with s_set_gpr_idx; a register write
+// under a uniform branch, or an early return that skips the writes, makes that
+// array a phi of copies (~80 v_mov per wave-step). Here rsp and the
+// destination are written exactly once each, unconditionally.
 __device__ __forceinline__ int fast_exec(const FastMem &M, Lane &L, const FOp &f, u64 nrip, u64 &next) {
   next = nrip;
   const u32 F = f.fl, op = fo_op(f), sub = fo_sub(f), sz = fo_sz(f);
-  if (op >= FO_VLD) return fast_vec(M.full, L, f, nrip);
   const u64 rsp = R(L, 4);
-  u64 a = (F & FF_AREG) ? R(L, fo_ra(f)) : 0;
-  u64 b = (F & FF_BREG) ? R(L, fo_rb(f)) : f.imm;
-  u64 addr = 0;
-  if (F & FF_EA) {
-    addr = f.disp + (fo_riprel(f) ? nrip : 0);
-    if (fo_base(f) != NOREG) addr += R(L, fo_base(f));
-    if (fo_index(f) != NOREG) addr += R(L, fo_index(f)) << fo_scale(f);
-    if (fo_seg(f)) addr += (fo_seg(f) == 1 ? M.fs_base : M.gs_base)[L.lane];
-  } else if (F & FF_PUSH) {
-    addr = rsp - 8;
-  } else {
-    addr = rsp;
-  }
-  // ---- the memory read
-  u8 *mp = nullptr;
-  // (a write to the read's own address makes it a read-modify-write; call
-  // [mem] reads its target and writes the stack)
-  const bool rmw = (F & FF_MW) && (F & (FF_MR_A | FF_MR_B)) && !(F & FF_PUSH);
-  if (F & (FF_MR_A | FF_MR_B)) {
-    const u32 rsz = (F & (FF_PUSH | FF_POP)) ? 8 : (op == FO_MOVX ? fo_szb(f) : sz);
-    mp = fxlate(L, addr, rsz, rmw ? ACC_W : ACC_R);
-    if (!mp) return X_FAULT;
-    const u64 v = load_le(mp, rsz);
-    L.pend += rsz;
-    if (F & FF_MR_A) a = v;
-    else b = v;
-  }
-  // ---- compute (pure)
   u64 res = 0, fl = L.rflags, fo;
-  switch (op) {
-    case FO_MOV: res = b; break;
-    case FO_ALU:
-      res = alu2(sub, a, b, sz, fl, fo);
-      fl = with_status(fl, fo);
-      break;
-    case FO_LEA: res = addr; break;
-    case FO_INCDEC:
-      res = alu2(sub ? 5 : 0, a, 1, sz, fl, fo);
-      fl = (fl & ~(F_STATUS & ~F_CF)) | (fo & ~F_CF);
-      break;
-    case FO_JCC:
-      if (cond(fl, sub)) next = nrip + f.imm;
-      break;
-    case FO_JMP: next = (F & FF_BREG) ? b : nrip + b; break;
-    case FO_CALL:  // indirect: the target in a register or read from memory
-      res = nrip;
-      next = (F & (FF_BREG | FF_MR_B)) ? b : nrip + b;
-      break;
-    case FO_UNARY:
-      if (sub) {
-        res = alu2(5, 0, a, sz, fl, fo);
-        fl = with_status(fl, fo);
+  bool ok = true;
+  if (op >= FO_VLD) {
+    ok = fast_vec(M.full, L, f, nrip) == X_OK;  // xmm / ymm state only (memory), no GPR
+  } else {
+    u64 a = (F & FF_AREG) ? R(L, fo_ra(f)) : 0;
+    u64 b = (F & FF_BREG) ? R(L, fo_rb(f)) : f.imm;
+    u64 addr = 0;
+    if (F & FF_EA) {
+      addr = f.disp + (fo_riprel(f) ? nrip : 0);
+      if (fo_base(f) != NOREG) addr += R(L, fo_base(f));
+      if (fo_index(f) != NOREG) addr += R(L, fo_index(f)) << fo_scale(f);
+      if (fo_seg(f)) addr += (fo_seg(f) == 1 ? M.fs_base : M.gs_base)[L.lane];
+    } else if (F & FF_PUSH) {
+      addr = rsp - 8;
+    } else {
+      addr = rsp;
+    }
+    // ---- the memory read
+    u8 *mp = nullptr;
+    // (a write to the read's own address makes it a read-modify-write; call
+    // [mem] reads its target and writes the stack)
+    const bool rmw = (F & FF_MW) && (F & (FF_MR_A | FF_MR_B)) && !(F & FF_PUSH);
+    if (F & (FF_MR_A | FF_MR_B)) {
+      const u32 rsz = (F & (FF_PUSH | FF_POP)) ? 8 : (op == FO_MOVX ? fo_szb(f) : sz);
+      mp = fxlate(L, addr, rsz, rmw ? ACC_W : ACC_R);
+      if (mp) {
+        const u64 v = load_le(mp, rsz);
+        L.pend += rsz;
+        if (F & FF_MR_A) a = v;
+        else b = v;
       } else {
-        res = ~a;
+        ok = false;
       }
-      break;
-    case FO_RET: next = b; break;
-    case FO_MOVX: {
-      const u32 szb = fo_szb(f);
-      b &= szmask(szb);
-      res = sub ? sext(b, szb) : b;
-      break;
     }
-    case FO_SHIFT: res = shift_op(sub, a, (u32)b, sz, fl); break;  // b: the immediate, or rcx
-    case FO_BT: {
-      const u64 bitoff = b & (8 * sz - 1);
-      res = sub == 5 ? (a | (1ull << bitoff)) : sub == 6 ? (a & ~(1ull << bitoff)) : (a ^ (1ull << bitoff));
-      fl = (fl & ~F_CF) | ((a >> bitoff) & 1);
-      break;
+    // ---- compute (pure)
+    switch (op) {
+      case FO_MOV: res = b; break;
+      case FO_ALU:
+        res = alu2(sub, a, b, sz, fl, fo);
+        fl = with_status(fl, fo);
+        break;
+      case FO_LEA: res = addr; break;
+      case FO_INCDEC:
+        res = alu2(sub ? 5 : 0, a, 1, sz, fl, fo);
+        fl = (fl & ~(F_STATUS & ~F_CF)) | (fo & ~F_CF);
+        break;
+      case FO_JCC:
+        if (cond(fl, sub)) next = nrip + f.imm;
+        break;
+      case FO_JMP: next = (F & FF_BREG) ? b : nrip + b; break;
+      case FO_CALL:  // indirect: the target in a register or read from memory
+        res = nrip;
+        next = (F & (FF_BREG | FF_MR_B)) ? b : nrip + b;
+        break;
+      case FO_UNARY:
+        if (sub) {
+          res = alu2(5, 0, a, sz, fl, fo);
+          fl = with_status(fl, fo);
+        } else {
+          res = ~a;
+        }
+        break;
+      case FO_RET: next = b; break;
+      case FO_MOVX: {
+        const u32 szb = fo_szb(f);
+        b &= szmask(szb);
+        res = sub ? sext(b, szb) : b;
+        break;
+      }
+      case FO_SHIFT: res = shift_op(sub, a, (u32)b, sz, fl); break;  // b: the immediate, or rcx
+      case FO_BT: {
+        const u64 bitoff = b & (8 * sz - 1);
+        res = sub == 5 ? (a | (1ull << bitoff)) : sub == 6 ? (a & ~(1ull << bitoff)) : (a ^ (1ull << bitoff));
+        fl = (fl & ~F_CF) | ((a >> bitoff) & 1);
+        break;
+      }
+      case FO_CMOV:
+        // a false condition still zero-extends a 32-bit destination
+        res = cond(fl, sub) ? b : a;
+        break;
+      case FO_SETCC: res = cond(fl, sub) ? 1 : 0; break;
+      default: break;
     }
-    case FO_CMOV:
-      // a false condition still zero-extends a 32-bit destination
-      res = cond(fl, sub) ? b : a;
-      break;
-    case FO_SETCC: res = cond(fl, sub) ? 1 : 0; break;
-    default: break;
+    // ---- the memory write
+    if (ok && (F & FF_MW)) {
+      const u32 wsz = (F & FF_PUSH) ? 8 : sz;
+      if (!rmw) mp = fxlate(L, (F & FF_PUSH) ? rsp - 8 : addr, wsz, ACC_W);
+      if (mp) {
+        store_le(mp, wsz, res & szmask(wsz));
+        L.pend += wsz;
+      } else {
+        ok = false;
+      }
+    }
   }
-  // ---- the memory write
-  if (F & FF_MW) {
-    const u32 wsz = (F & FF_PUSH) ? 8 : sz;
-    if (!rmw) {
-      mp = fxlate(L, (F & FF_PUSH) ? rsp - 8 : addr, wsz, ACC_W);
-      if (!mp) return X_FAULT;
-    }
-    store_le(mp, wsz, res & szmask(wsz));
-    L.pend += wsz;
-  }
-  // ---- commit
-  if (F & FF_PUSH) RS(L, 4, rsp - 8);
-  if (F & FF_POP) RS(L, 4, rsp + 8 + (op == FO_RET ? f.imm : 0));
-  if (F & FF_WRA) wr(L, fo_ra(f), sz, res);
-  if (F & FF_FLAGS) L.rflags = fl;
-  return X_OK;
+  // ---- commit (rsp first: pop rsp ends with the popped value)
+  const u64 nrsp = !ok ? rsp : (F & FF_PUSH) ? rsp - 8 : (F & FF_POP) ? rsp + 8 + (op == FO_RET ? f.imm : 0) : rsp;
+  RS(L, 4, nrsp);
+  const u32 wi = fo_ra(f) & 15;
+  const u64 old = R(L, wi), mk = szmask(sz);
+  // wr(): 8 / 4 bytes replace (4 zero-extends), 2 / 1 merge into the old value
+  const u64 nv = (ok && (F & FF_WRA)) ? (sz >= 4 ? (res & mk) : ((old & ~mk) | (res & mk))) : old;
+  RS(L, wi, nv);
+  if (ok && (F & FF_FLAGS)) L.rflags = fl;
+  return ok ? X_OK : X_FAULT;
 }
 __device__ __forceinline__ int fast_exec(const Dev &P, Lane &L, const FOp &f, u64 nrip, u64 &next) {
   return fast_exec(fast_mem(P), L, f, nrip, next);
