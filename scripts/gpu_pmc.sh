@@ -15,7 +15,7 @@ run() {  # leg pass-name timeout rocprof-args...
   local out=/tmp/pmc/$leg/$pass
   mkdir -p $out
   if [ $leg = hevd ]; then
-    timeout -s KILL $t rocprofv3 "$@" --output-format csv -d $out -o run -- $R/wtf_amd/host/wtfgpu fuzz --name hevd --target /tmp/hevdp --lanes 131072 --seconds ${HEVD_SECS:-3} --seed 1337 --limit 10000000 --max_len 1028 > $out.log 2>&1
+    timeout -s KILL $t rocprofv3 "$@" --output-format csv -d $out -o run -- $R/wtf_amd/host/wtfgpu fuzz --name hevd --target /tmp/hevdp --lanes 131072 --seconds ${HEVD_SECS:-10} --seed 1337 --limit 10000000 --max_len 1028 > $out.log 2>&1
   else
     timeout -s KILL $t rocprofv3 "$@" --output-format csv -d $out -o run -- python3 $R/scripts/prof_leg.py $leg ${STEPS:-20} > $out.log 2>&1
   fi
@@ -23,6 +23,10 @@ run() {  # leg pass-name timeout rocprof-args...
   [ $rc -eq 0 ] || { echo "FAIL $leg $pass rc=$rc"; tail -5 $out.log; exit 1; }
 }
 for leg in ${LEGS:-tlv hevd syn}; do
+  # SYN's runs go to completion: after one probe of each schedule the run
+  # policy keeps the fixed lane order (wtfgpu_ctx::nspi_sched), so every
+  # profiled launch is measured in that steady state
+  if [ $leg = syn ]; then export WTFGPU_REGROUP_STEPS=0; else unset WTFGPU_REGROUP_STEPS; fi
   run $leg stats 240 --kernel-trace --stats
   run $leg fetch 180 --pmc FETCH_SIZE
   run $leg write 180 --pmc WRITE_SIZE
