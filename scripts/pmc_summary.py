@@ -6,8 +6,11 @@ WRITE_SIZE are in KB; on gfx950 FETCH_SIZE reports half the bytes of a wide
 coalesced read, so it is doubled (k_run's reads are not all wide streams: the
 corrected read side is an upper bound, the raw one a lower bound).
 valu_util = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES, wait_frac = SQ_WAIT_ANY /
-SQ_WAVE_CYCLES (both summed over k_run dispatches). engine_sha16 binds the
-summary to the libwtfgpu.so it was measured on."""
+SQ_WAVE_CYCLES (both summed over k_run dispatches). The launches of the
+workload's warm-up (prof_leg.py prints how many) are left out of the counters,
+as bench.py's timed window leaves them out; kernel_trace keeps rocprof's
+all-launch statistics and adds the after-warm-up average. engine_sha16 binds
+the summary to the libwtfgpu.so it was measured on."""
 import csv
 import glob
 import hashlib
@@ -18,15 +21,32 @@ import sys
 d, leg, lanes, limit = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
 
 
+def warm_launches(sub):
+    """k_run launches of the workload's warm-up in this pass (prof_leg.py
+    prints them; 0 for a run without one): left out, as bench.py's timed
+    window leaves its warm-up steps out."""
+    try:
+        for line in reversed(open(os.path.join(d, sub + ".log")).read().splitlines()):
+            if line.startswith("{") and "warm_launches" in line:
+                return int(json.loads(line)["warm_launches"])
+    except (OSError, ValueError):
+        pass
+    return 0
+
+
 def per_kernel(sub):
-    out, disp = {}, set()
+    rows = {}
     for f in glob.glob(os.path.join(d, sub, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if "k_run" not in r["Kernel_Name"]:
                 continue
-            disp.add((f, r["Dispatch_Id"]))
-            out[r["Counter_Name"]] = out.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    return out, max(1, len(disp))
+            rows.setdefault(int(r["Dispatch_Id"]), []).append((r["Counter_Name"], float(r["Counter_Value"])))
+    keep = sorted(rows)[warm_launches(sub):]
+    out = {}
+    for i in keep:
+        for k, v in rows[i]:
+            out[k] = out.get(k, 0.0) + v
+    return out, max(1, len(keep))
 
 
 fetch, nf = per_kernel("fetch")
@@ -38,6 +58,17 @@ for f in glob.glob(os.path.join(d, "stats", "**", "*kernel_stats.csv"), recursiv
     for r in csv.DictReader(open(f)):
         if "k_run" in r["Name"]:
             stats = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "pct": float(r["Percentage"])}
+# the same average over the launches after the warm-up (the kernel trace)
+durs = {}
+for f in glob.glob(os.path.join(d, "stats", "**", "*kernel_trace.csv"), recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "k_run" in r["Kernel_Name"]:
+            durs[int(r["Dispatch_Id"])] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+if durs:
+    kept = [durs[i] for i in sorted(durs)[warm_launches("stats"):]]
+    if kept:
+        stats["after_warmup"] = {"calls": len(kept), "avg_ns": sum(kept) / len(kept),
+                                 "warm_launches": warm_launches("stats")}
 fetch_b = fetch.get("FETCH_SIZE", 0) * 1024 / nf
 write_b = write.get("WRITE_SIZE", 0) * 1024 / nw
 cyc = wait.get("SQ_WAVE_CYCLES", 0)

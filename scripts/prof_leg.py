@@ -18,17 +18,24 @@ def main():
     lanes = 65536 if leg == "syn" else 262144  # bench.py's --syn-lanes / --lanes defaults
     if leg == "syn":
         s = bench.syn_leg(lanes, limit, steps, 0)
+        # syn_leg's one untimed step: one launch in the fixed order (gpu_pmc.sh)
         print(json.dumps({"leg": "syn", "lanes": lanes, "limit": limit, "launches": s.get("launches"),
-                          "value": s.get("value")}))
+                          "warm_launches": 1, "value": s.get("value")}))
         return
     from wtf_amd import node as wn
     d = bench.build_target("tlv_server", tempfile.mkdtemp())
     n = wn.Node("tlv_server", d, lanes, limit, seed=1337, max_len=bench.TARGETS["tlv_server"][2])
+    # bench.py's warm-up first: the summary leaves these launches out, as the
+    # bench's timed window does (the cold start logs every new rip per lane)
+    warm = int(os.environ.get("PROF_WARMUP", "6"))
+    for _ in range(warm):
+        n.step()
+    warm_launches = n.stats()["kernel_launches"]
     for _ in range(steps):
         n.step()
     s = n.stats()
     print(json.dumps({"leg": "tlv", "lanes": lanes, "limit": limit, "launches": s["kernel_launches"],
-                      "execs": s["execs"]}))
+                      "warm_launches": warm_launches, "execs": s["execs"]}))
     n.close()
 
 
