@@ -1427,6 +1427,8 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
   // ---- refill
   std::vector<uint32_t> fresh;
   std::vector<std::pair<const uint8_t *, size_t>> tcs;
+  fresh.reserve(std::min<size_t>(In.size(), P.hi - P.lo));
+  tcs.reserve(fresh.capacity());
   for (uint32_t l = P.lo; l < P.hi && fresh.size() < In.size(); l++)
     if (!busy_[l]) {
       fresh.push_back(l);
