@@ -179,7 +179,12 @@ int wtfgpu_set_limit(wtfgpu_ctx *ctx, uint64_t limit);
 /* Cross-wave regrouping (no bochscpu counterpart: the SIMT schedule only):
  * wtfgpu_run splits its wave-steps into k_run launches of `steps`, and before
  * each one the running lanes are sorted by rip so that lanes at one rip share
- * a wave. 0 = fixed lane order. Results are identical either way. */
+ * a wave. 0 = fixed lane order. Results are identical either way. Unless
+ * WTFGPU_REGROUP_AUTO=0, each run picks regrouping or the fixed order from
+ * measurements of both (probing the other every 32nd run): sliced runs by
+ * lanes retired per wave-step (counts only: fixed-seed campaigns reproduce),
+ * runs to completion (max_steps >= 2^32) by kernel time per retired
+ * instruction. */
 int wtfgpu_set_regroup(wtfgpu_ctx *ctx, uint64_t steps);
 int wtfgpu_set_breakpoints(wtfgpu_ctx *ctx, const uint64_t *gvas, uint32_t n);
 
