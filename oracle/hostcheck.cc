@@ -20,6 +20,9 @@
 //       printed as "T <hex>"; every `newcov_every`-th output (1-based, 0 =
 //       never) is fed back through OnNewCoverage (server.h:816-853), which
 //       arms libFuzzer's CrossOver.
+//   mutate-grow <...same...>  as mutate, and every `newcov_every`-th output
+//       also joins the corpus (this repository only: the tlv mutator's
+//       parsed-testcase cache over a growing corpus)
 //   blake3 <hexbytes>
 //       Blake3HexDigest (utils.cc) of the bytes.
 // This repository's build only (the reference exposes neither as a function
@@ -177,7 +180,7 @@ static int cmd_tlv_feed(const char *path) {
   return 0;
 }
 
-static int cmd_mutate(int argc, char **argv) {
+static int cmd_mutate(int argc, char **argv, bool grow = false) {
   if (argc < 7) return 2;
   const std::string name = argv[2];
   std::mt19937_64 Rng(strtoull(argv[3], nullptr, 0));
@@ -200,7 +203,10 @@ static int cmd_mutate(int argc, char **argv) {
   for (size_t i = 1; i <= count; i++) {
     std::string s = M->GetNewTestcase(Corpus);
     hexline("T", s);
-    if (every && i % every == 0) M->OnNewCoverage(Testcase_t((const uint8_t *)s.data(), s.size()));
+    if (every && i % every == 0) {
+      M->OnNewCoverage(Testcase_t((const uint8_t *)s.data(), s.size()));
+      if (grow) Corpus.SaveTestcase(Ok_t(), Testcase_t((const uint8_t *)s.data(), s.size()));
+    }
   }
   return 0;
 }
@@ -332,6 +338,7 @@ int main(int argc, char **argv) {
 #endif
   if (cmd == "cpustate" && argc == 3) return cmd_cpustate(argv[2]);
   if (cmd == "mutate") return cmd_mutate(argc, argv);
+  if (cmd == "mutate-grow") return cmd_mutate(argc, argv, true);
   if (cmd == "blake3" && argc == 3) {
     const auto b = unhex(argv[2]);
     printf("%s\n", Blake3HexDigest(b.data(), b.size()).c_str());

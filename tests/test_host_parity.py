@@ -128,3 +128,36 @@ def test_live_reference_agrees_with_fixtures():
     with tempfile.TemporaryDirectory() as d:
         outs = _mutate(REF_TOOL, dict(case, count=300), _corpus_files(d, case["corpus"]))
     assert [hashlib.sha256(bytes.fromhex(o)).hexdigest()[:32] for o in outs] == case["sha256"][:300]
+
+
+ODD_TLV = [
+    # the general parser's forms: whitespace, reordered keys, a leading zero
+    b'{ "Packets" : [ {"Id":2,"Command":3,"BodySize":1,"Body":[7]} ] }',
+    b'{"Packets":[{"Body":[1,2,300],"BodySize":070,"Command":1,"Id":1}]}',
+    # no packets, one packet too many to insert into, a truncated testcase
+    b'{"Packets":[]}',
+    b'{"Packets":[' + b",".join(b'{"Body":[%d],"BodySize":1,"Command":%d,"Id":%d}' % (i, i, i)
+                                for i in range(12)) + b']}',
+    b'{"Packets":[{"Body":[65,65],"BodySize":2,"Command":0,"Id":0},{"Body":[6',
+    b'not json at all',
+]
+
+
+@pytest.mark.parametrize("seed", [1, 1337, 0xC0FFEE])
+def test_tlv_mutator_parsed_cache_matches_plain(seed, tmp_path):
+    """The tlv mutator's fast path (corpus testcases parsed once, outputs
+    written from packet references) gives the stream of the plain path, which
+    parses and rewrites every pick as the reference does (the reference-pinned
+    one above), over a corpus that grows as the campaign's does and holds
+    testcases only the general parser reads."""
+    files = _corpus_files(str(tmp_path), "tlv")
+    for i, b in enumerate(ODD_TLV):
+        p = tmp_path / f"odd_{i}"
+        p.write_bytes(b)
+        files.append(str(p))
+    args = ["mutate-grow", "tlv_server", str(seed), "4096", "6000", "7", *files]
+    fast = run(_tool(), *args)
+    plain = subprocess.run([_tool(), *args], check=True, capture_output=True, text=True,
+                           env={**os.environ, "WTF_TLV_MUTATOR_PLAIN": "1"}).stdout
+    assert fast.count("\n") == 6000
+    assert fast == plain

@@ -119,6 +119,9 @@ void GpuBackend_t::reset_view(uint32_t lane) {
   v.seed = initial_.Seed;  // Rdrand seed (bochscpu_backend.cc:1030)
   v.has_feed = false;
   v.feed.clear();
+  v.ext = nullptr;
+  v.ext_len = 0;
+  v.ext_insert = false;
   v.dirty_known = true;    // a restored lane has an empty overlay
   v.dirty.clear();
   v.wlog.clear();
@@ -1439,6 +1442,10 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
   if (!fresh.empty()) {
     if (wtfgpu_restore_lanes(ctx_, fresh.data(), (uint32_t)fresh.size())) return false;
     stats_.restore_dev_ms += ms_since(ti);
+    // a prepared insert (Target_t::PrepareInsert) the backend takes is applied
+    // here, with the lane's module state reset as before an InsertTestcase;
+    // the other lanes call InsertTestcase below
+    std::vector<uint8_t> prepared(fresh.size(), 0);
     HostPool::Get().For(fresh.size(), 256, [&](size_t i) {
       const uint32_t l = fresh[i];
       reset_view(l);
@@ -1446,17 +1453,44 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
       tag_[l] = In[i].tag;
       tc_bytes_[l] = In[i].size;
       lres_stale_[l] = 1;  // its last result may not be consumed yet (this call's Out)
+      const StreamTestcase_t &T = In[i];
+      LaneView &v = views_[l];
+      switch (T.prep) {
+        case PreparedInsert_t::Call: return;
+        case PreparedInsert_t::Failed: v.result = Crash_t("insert-testcase-failed"); break;
+        case PreparedInsert_t::Nothing: break;
+        case PreparedInsert_t::Feed:  // SetFeed would refuse it: InsertTestcase keeps its host path
+          if (!feed_action_ || T.prep_size > kFeedRegion) return;
+          v.has_feed = true, v.ext = T.prep_data, v.ext_len = (uint32_t)T.prep_size;
+          break;
+        case PreparedInsert_t::Insert:  // as SetInsert
+          if (!insert_action_ || T.size + 4 > kFeedRegion) return;
+          v.has_feed = true, v.ext = T.data, v.ext_len = (uint32_t)T.size, v.ext_insert = true;
+          break;
+      }
+      if (Slots) Slots->ResetLane(l);
+      prepared[i] = 1;
     });
     recycle_arenas();  // reset_view's drop_staged ran inside the loop
     const auto tm = Clock::now();
     stats_.restore_ms += std::chrono::duration<double, std::milli>(tm - ti).count();
-    std::vector<uint8_t> ok;
-    insert_lanes(Target, fresh, tcs, Slots, ok);
+    std::vector<uint32_t> call;
+    std::vector<std::pair<const uint8_t *, size_t>> call_tcs;
     for (size_t i = 0; i < fresh.size(); i++)
-      if (!ok[i]) views_[fresh[i]].result = Crash_t("insert-testcase-failed");
+      if (!prepared[i]) {
+        call.push_back(fresh[i]);
+        call_tcs.push_back(tcs[i]);
+      }
+    stats_.prepared += fresh.size() - call.size();
+    if (!call.empty()) {
+      std::vector<uint8_t> ok;
+      insert_lanes(Target, call, call_tcs, Slots, ok);
+      for (size_t i = 0; i < call.size(); i++)
+        if (!ok[i]) views_[call[i]].result = Crash_t("insert-testcase-failed");
+    }
     const auto tu = Clock::now();
     stats_.module_ms += std::chrono::duration<double, std::milli>(tu - tm).count();
-    if (flush_lanes(fresh)) return false;
+    if (flush_lanes(call)) return false;
     if (feed_action_ || insert_action_) {
       const auto tf = Clock::now();
       const size_t n = fresh.size();
@@ -1464,7 +1498,7 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
       std::vector<uint8_t> has(n);
       for (size_t i = 0; i < n; i++) {
         const LaneView &v = views_[fresh[i]];
-        off[i + 1] = off[i] + v.feed.size();
+        off[i + 1] = off[i] + v.feed_size();
         has[i] = v.has_feed;
       }
       // packed into the part's pinned buffer on all host threads: one DMA
@@ -1478,7 +1512,16 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
       }
       HostPool::Get().For(n, 256, [&](size_t i) {
         const LaneView &v = views_[fresh[i]];
-        if (!v.feed.empty()) memcpy(P.pin + off[i], v.feed.data(), v.feed.size());
+        uint8_t *o = P.pin + off[i];
+        if (v.ext) {
+          if (v.ext_insert) {
+            memcpy(o, &v.ext_len, 4);
+            o += 4;
+          }
+          if (v.ext_len) memcpy(o, v.ext, v.ext_len);
+        } else if (!v.feed.empty()) {
+          memcpy(o, v.feed.data(), v.feed.size());
+        }
       });
       if (wtfgpu_set_feed_lanes(ctx_, fresh.data(), (uint32_t)n, off.data(), has.data(), P.pin, off[n]))
         return false;
@@ -1602,9 +1645,10 @@ std::string GpuBackend_t::StatsJson() const {
   std::string r(b);
   r.pop_back();
   snprintf(b, sizeof(b), ",\"up_prep_ms\":%.3f,\"up_regs_ms\":%.3f,\"up_apply_ms\":%.3f,\"up_feed_ms\":%.3f,"
-           "\"restore_dev_ms\":%.3f,\"out_ms\":%.3f,\"fresh_ms\":%.3f,\"occ_ms\":%.3f,\"harvest_ms\":%.3f",
+           "\"restore_dev_ms\":%.3f,\"out_ms\":%.3f,\"fresh_ms\":%.3f,\"occ_ms\":%.3f,\"harvest_ms\":%.3f,"
+           "\"prepared\":%llu",
            stats_.up_prep_ms, stats_.up_regs_ms, stats_.up_apply_ms, stats_.up_feed_ms, stats_.restore_dev_ms,
-           stats_.out_ms, stats_.fresh_ms, stats_.occ_ms, stats_.harvest_ms);
+           stats_.out_ms, stats_.fresh_ms, stats_.occ_ms, stats_.harvest_ms, (unsigned long long)stats_.prepared);
   r += b;
   r += ",\"unimpl_ops\":" + stats_.unimpl_ops.json();
   r += ",\"unimpl_raw\":" + stats_.unimpl_ops.raw_json();

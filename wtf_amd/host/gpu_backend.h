@@ -32,6 +32,7 @@ namespace wtfgpu_host {
 struct BatchStats {
   uint64_t rounds = 0, breakpoint_hits = 0, kernel_launches = 0, retired = 0, group_steps = 0;
   uint64_t page_fetches = 0, prefetched_pages = 0, batches = 0, testcases = 0, staged_pages = 0, stack_windows = 0;
+  uint64_t prepared = 0;  // streaming: testcases whose prepared insert the backend took (no InsertTestcase call)
   double kernel_ms = 0, service_ms = 0, total_ms = 0;
   // service_ms split: bulk reads (regs, dirty lists), stack/learned prefetch,
   // module handlers (incl. on-demand page fetches), flush (writes + resume/stop)
@@ -103,6 +104,7 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   Backend_t *AsBackend() override { return this; }
   // streaming (continuous batching): see Executor_t
   bool CanStream() const override { return true; }
+  bool TakesPrepared() const override { return feed_action_ || insert_action_; }
   uint32_t FreeLanes() const override;
   bool StreamStep(const Target_t &Target, const std::vector<StreamTestcase_t> &In, uint64_t Slice,
                   std::vector<StreamResult_t> &Out, ModuleSlots *Slots, size_t *Taken) override;
@@ -166,6 +168,13 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
     uint64_t inject = ~0ull;  // PageFaultsMemoryIfNeeded: page to #PF after the handler
     bool has_feed = false;    // SetFeed / SetInsert: chunks for the device Feed action / insert
     std::vector<uint8_t> feed;
+    // a prepared insert's bytes instead of `feed` (StreamTestcase_t::prep,
+    // valid during the StreamStep call): the feed itself, or with ext_insert
+    // the testcase the feed's one chunk (u32 size, bytes) holds
+    const uint8_t *ext = nullptr;
+    uint32_t ext_len = 0;
+    bool ext_insert = false;
+    uint64_t feed_size() const { return ext ? ext_len + (ext_insert ? 4 : 0) : feed.size(); }
     bool dirty_known = false;
     std::vector<uint32_t> dirty;  // gpfns the lane's overlay holds
     std::vector<Staged> pages;    // staged pages (few per lane: linear search)

@@ -63,6 +63,14 @@ bool InsertTestcase(const uint8_t *Buffer, const size_t BufferSize) {
   return true;
 }
 
+// InsertTestcase ahead of time (PrepareInsert_t): its size checks, then the
+// declared insert of the whole testcase
+PreparedInsert_t PrepareInsert(const uint8_t *, const size_t BufferSize, std::vector<uint8_t> &) {
+  if (BufferSize < sizeof(uint32_t)) return PreparedInsert_t::Nothing;
+  if (BufferSize - sizeof(uint32_t) > 1024) return PreparedInsert_t::Failed;
+  return PreparedInsert_t::Insert;
+}
+
 bool Init(const Options_t &, const CpuState_t &) {
   // InsertTestcase as data (device-side on the gpu backend)
   g_Backend->DeclareInsert(
@@ -102,6 +110,6 @@ bool Init(const Options_t &, const CpuState_t &) {
   return true;
 }
 
-Target_t Hevd("hevd", Init, InsertTestcase);
+Target_t Hevd("hevd", Init, InsertTestcase, []() { return true; }, LibfuzzerMutator_t::Create, PrepareInsert);
 
 }  // namespace Hevd

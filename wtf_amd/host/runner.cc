@@ -25,6 +25,13 @@ namespace {
 // parallel mutation of a fuzz batch (make_batch): batches of at least
 // kParMutateMin new testcases, kMutateChunk testcases per generator
 constexpr size_t kParMutateMin = 8192, kMutateChunk = 2048;
+// CPU time of the calling thread (ns)
+uint64_t ThreadCpuNs() {
+  timespec t{};
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &t);
+  return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+
 
 using Clock = std::chrono::steady_clock;
 double secs_since(Clock::time_point t0) { return std::chrono::duration<double>(Clock::now() - t0).count(); }
@@ -645,6 +652,10 @@ bool FuzzSession::Start() {
   }
   t0_ = Clock::now();
   stream_ = O_.slice && Exec_.CanStream();
+  // inserts prepared where the testcases are made (not for per-lane module
+  // copies: each lane calls its own copy's InsertTestcase)
+  if (stream_ && Exec_.TakesPrepared() && !Slots_.Instances() && !getenv("WTF_NO_PREPARED_INSERT"))
+    Prepare_ = Target_.PrepareInsert;
   if (stream_) {
     Adopt(MakeBatch(Budget(Exec_.Lanes())));
     return !Ready_.empty();
@@ -707,7 +718,9 @@ TcBatch FuzzSession::MakeBatch(uint64_t n) {
     for (uint64_t &S : Seeds) S = Rng_();
     std::vector<std::unique_ptr<TcArena>> Out(Chunks);
     std::atomic<size_t> NextChunk{0};
+    std::atomic<uint64_t> CpuNs{0};
     auto Work = [&]() {
+      const uint64_t c0 = ThreadCpuNs();
       for (size_t c; (c = NextChunk.fetch_add(1)) < Chunks;) {
         std::mt19937_64 R(Seeds[c]);
         Corpus_t View(Corpus_, R);
@@ -718,17 +731,21 @@ TcBatch FuzzSession::MakeBatch(uint64_t n) {
         auto A = std::make_unique<TcArena>();
         const size_t End = std::min(Need, (c + 1) * kMutateChunk);
         A->Off.reserve(End - c * kMutateChunk + 1);
+        std::vector<uint8_t> Scratch;
         for (size_t i = c * kMutateChunk; i < End; i++) {
           const std::string S = M->GetNewTestcase(View);
           A->Add(S.data(), std::min<size_t>(S.size(), O_.max_len));
+          if (Prepare_) A->Prepare(Prepare_, Scratch);
         }
         Out[c] = std::move(A);
       }
+      CpuNs += ThreadCpuNs() - c0;
     };
     std::vector<std::thread> Pool;
     for (unsigned t = 1; t < host_threads(); t++) Pool.emplace_back(Work);
     Work();
     for (std::thread &Th : Pool) Th.join();
+    MutateCpuNs_ += CpuNs.load();
     for (std::unique_ptr<TcArena> &A : Out) Batch.push_back(std::move(A));
     Made += Need;
     Batch.push_back(std::make_unique<TcArena>());  // the serial tail below
@@ -831,7 +848,13 @@ bool FuzzSession::StreamStep(bool Done) {
       Ready_.pop_front();
       Slot_[tag] = R;
       InFlight_++;
-      In.push_back(StreamTestcase_t{R.data(), R.size(), tag});
+      StreamTestcase_t T{R.data(), R.size(), tag};
+      if (R.A->Prep.size() == R.A->Count()) {
+        T.prep = R.prep();
+        T.prep_data = R.prep_data();
+        T.prep_size = R.prep_size();
+      }
+      In.push_back(T);
     }
     const uint64_t want = Budget(Exec_.Lanes() > Ready_.size() ? Exec_.Lanes() - Ready_.size() : 0);
     if (want && Corpus_.Size() && !Next_.valid())
@@ -1012,7 +1035,7 @@ std::string FuzzSession::SummaryJson() const {
            "\"instr_per_s\":%.3f,\"coverage\":%zu,\"corpus\":%zu,\"crashes\":%llu,\"unique_crashes\":%zu,"
            "\"timeouts\":%llu,\"cr3\":%llu,\"errors\":%llu,\"error_retired\":%llu,\"merged_rips\":%llu,"
            "\"merge_ms\":%.3f,\"produce_wait_ms\":%.3f,\"account_ms\":%.3f,\"make_ms\":%.3f,\"step_ms\":%.3f,\"fill_ms\":%.3f,"
-           "\"newcov_ms\":%.3f,\"crashsave_ms\":%.3f,\"call_ms\":%.3f,\"cpu_s\":%.3f,"
+           "\"newcov_ms\":%.3f,\"crashsave_ms\":%.3f,\"call_ms\":%.3f,\"cpu_s\":%.3f,\"mutate_cpu_ms\":%.3f,"
            "\"backend\":",
            O_.name.c_str(), Exec_.Lanes(), X_ ? X_->Rank() : 0, X_ ? X_->World() : 1,
            (unsigned long long)S_.batches, (unsigned long long)S_.execs, (unsigned long long)S_.retired, Wall,
@@ -1020,7 +1043,8 @@ std::string FuzzSession::SummaryJson() const {
            Exec_.CoverageSize(), Corpus_.Size(), (unsigned long long)S_.crashes, CrashNames_.size(),
            (unsigned long long)S_.timeouts, (unsigned long long)S_.cr3, (unsigned long long)S_.errors,
            (unsigned long long)S_.error_retired, (unsigned long long)S_.merged_rips, S_.merge_ms, S_.produce_wait_ms,
-           S_.account_ms, S_.make_ms, S_.step_ms, S_.fill_ms, S_.newcov_ms, S_.crashsave_ms, S_.call_ms, ProcessCpuSeconds());
+           S_.account_ms, S_.make_ms, S_.step_ms, S_.fill_ms, S_.newcov_ms, S_.crashsave_ms, S_.call_ms, ProcessCpuSeconds(),
+           MutateCpuNs_.load() * 1e-6);
   return std::string(b) + Exec_.StatsJson() + "}";
 }
 

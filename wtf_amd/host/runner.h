@@ -4,6 +4,7 @@
 // mutate, run, keep testcases that found new coverage, save crashes), both
 // batched N testcases per executor call.
 #pragma once
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <filesystem>
@@ -43,6 +44,11 @@ struct StreamTestcase_t {
   const uint8_t *data;
   size_t size;
   uint64_t tag;  // the caller's name for it, returned with its result
+  // Target_t::PrepareInsert's outcome for it, when the node prepared it
+  // (PreparedInsert_t; Call = not prepared) and its bytes (Feed)
+  PreparedInsert_t prep = PreparedInsert_t::Call;
+  const uint8_t *prep_data = nullptr;
+  size_t prep_size = 0;
 };
 // A finished testcase: its tag and its result, which stays in the executor's
 // storage and is valid until the executor's next StreamStep (no per-result
@@ -63,6 +69,8 @@ class Executor_t {
   // is only read during the call. (A pipelined executor returns a slice's
   // results one call later: its lanes run while the host serves others.)
   virtual bool CanStream() const { return false; }
+  // StreamStep uses prepared inserts (StreamTestcase_t::prep)
+  virtual bool TakesPrepared() const { return false; }
   virtual uint32_t FreeLanes() const { return 0; }
   virtual bool StreamStep(const Target_t &, const std::vector<StreamTestcase_t> &, uint64_t,
                           std::vector<StreamResult_t> &, ModuleSlots *, size_t *Taken) {
@@ -233,10 +241,23 @@ struct TcArena {
   std::vector<uint8_t> Data;
   std::vector<uint64_t> Off{0};
   size_t Live = 0;  // streaming: testcases of this arena not yet accounted
+  // prepared inserts (Target_t::PrepareInsert), one per testcase when present
+  std::vector<PreparedInsert_t> Prep;
+  std::vector<uint8_t> PrepData;
+  std::vector<uint64_t> PrepOff{0};
   void Add(const void *P, size_t N) {
     const uint8_t *B = (const uint8_t *)P;
     Data.insert(Data.end(), B, B + N);
     Off.push_back(Data.size());
+  }
+  // the last testcase added, prepared by F (every testcase of a prepared arena is)
+  void Prepare(PrepareInsert_t F, std::vector<uint8_t> &Scratch) {
+    const size_t I = Count() - 1;
+    Scratch.clear();
+    const PreparedInsert_t K = F(Ptr(I), Len(I), Scratch);
+    Prep.push_back(K);
+    if (K == PreparedInsert_t::Feed) PrepData.insert(PrepData.end(), Scratch.begin(), Scratch.end());
+    PrepOff.push_back(PrepData.size());
   }
   size_t Count() const { return Off.size() - 1; }
   const uint8_t *Ptr(size_t I) const { return Data.data() + Off[I]; }
@@ -248,6 +269,9 @@ struct TcRef {
   uint32_t I = 0;
   const uint8_t *data() const { return A->Ptr(I); }
   size_t size() const { return A->Len(I); }
+  PreparedInsert_t prep() const { return I < A->Prep.size() ? A->Prep[I] : PreparedInsert_t::Call; }
+  const uint8_t *prep_data() const { return A->PrepData.data() + A->PrepOff[I]; }
+  size_t prep_size() const { return A->PrepOff[I + 1] - A->PrepOff[I]; }
 };
 
 // The fuzz loop of one node / shard, one batch per Step(): an in-process
@@ -295,6 +319,8 @@ class FuzzSession {
 
  private:
   TcBatch MakeBatch(uint64_t n);
+  PrepareInsert_t Prepare_ = nullptr;  // the target's PrepareInsert when the executor takes it
+  std::atomic<uint64_t> MutateCpuNs_{0};  // CPU time of the parallel mutation (and preparation) threads
   void Adopt(TcBatch &&B);  // streaming: the batch's testcases join the ready queue
   uint64_t Budget(uint64_t n) const;
   bool More(uint64_t done) const;

@@ -206,8 +206,10 @@ void Backend_t::PrintRegisters() {
 
 // ------------------------------------------------------------------ targets (targets.cc:11-38)
 Target_t::Target_t(const std::string &Name_, const Init_t Init_, const InsertTestcase_t InsertTestcase_,
-                   const Restore_t Restore_, const CreateMutator_t CreateMutator_)
-    : Name(Name_), Init(Init_), InsertTestcase(InsertTestcase_), Restore(Restore_), CreateMutator(CreateMutator_) {
+                   const Restore_t Restore_, const CreateMutator_t CreateMutator_,
+                   const PrepareInsert_t PrepareInsert_)
+    : Name(Name_), Init(Init_), InsertTestcase(InsertTestcase_), Restore(Restore_), CreateMutator(CreateMutator_),
+      PrepareInsert(PrepareInsert_) {
   Targets_t::Instance().Registers(*this);
 }
 Targets_t &Targets_t::Instance() {

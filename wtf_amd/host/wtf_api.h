@@ -502,6 +502,22 @@ class LibfuzzerMutator_t : public Mutator_t {
 
 // ------------------------------------------------------------------ targets
 
+// InsertTestcase prepared ahead (this repository's extension, like
+// InsertAction_t): what a module's InsertTestcase does on a backend that takes
+// the testcase as data (Backend_t::SetFeed / SetInsert returning true), as a
+// function of the testcase bytes alone. The fuzz node runs it on the threads
+// that make the testcases; the backend then takes its bytes for the lane
+// without calling InsertTestcase (and calls InsertTestcase after all if it
+// would refuse them). The lane's module state must be what a reset left.
+enum class PreparedInsert_t : int8_t {
+  Failed = -1,   // InsertTestcase returns false
+  Call = 0,      // not preparable: call InsertTestcase
+  Nothing = 1,   // InsertTestcase returns true and hands the backend nothing
+  Feed = 2,      // ... does only SetFeed(Out) and returns true
+  Insert = 3,    // ... does only SetInsert(testcase) and returns true (Out unused)
+};
+using PrepareInsert_t = PreparedInsert_t (*)(const uint8_t *, size_t, std::vector<uint8_t> &Out);
+
 struct Target_t {
   using Init_t = bool (*)(const Options_t &, const CpuState_t &);
   using InsertTestcase_t = bool (*)(const uint8_t *, const size_t);
@@ -510,13 +526,15 @@ struct Target_t {
 
   explicit Target_t(const std::string &Name, const Init_t Init, const InsertTestcase_t InsertTestcase,
                     const Restore_t Restore = []() { return true; },
-                    const CreateMutator_t CreateMutator = LibfuzzerMutator_t::Create);
+                    const CreateMutator_t CreateMutator = LibfuzzerMutator_t::Create,
+                    const PrepareInsert_t PrepareInsert = nullptr);
 
   std::string Name;
   Init_t Init = nullptr;
   InsertTestcase_t InsertTestcase = nullptr;
   Restore_t Restore = nullptr;
   CreateMutator_t CreateMutator = nullptr;
+  PrepareInsert_t PrepareInsert = nullptr;  // optional (above)
 };
 
 struct Targets_t {
