@@ -23,6 +23,13 @@
 //   mutate-grow <...same...>  as mutate, and every `newcov_every`-th output
 //       also joins the corpus (this repository only: the tlv mutator's
 //       parsed-testcase cache over a growing corpus)
+//   merge-blocks <cap> <world> <step>...
+//       (this repository: merge_block.h) each step is one token per rank,
+//       "<n><d|->" joined by ',': rank r queues n new overflow values
+//       (r << 32 | running index) and says done with 'd'. Every rank packs
+//       its block, the blocks are read back in rank order as the collective
+//       delivers them (fixed stride, as RCCL does), and each step prints
+//       "S <all done 0|1> <values...>" (hex)
 //   blake3 <hexbytes>
 //       Blake3HexDigest (utils.cc) of the bytes.
 // This repository's build only (the reference exposes neither as a function
@@ -60,6 +67,7 @@
 #include <vector>
 
 #ifdef WTF_AMD_HOST
+#include "../wtf_amd/host/merge_block.h"
 #include "../wtf_amd/host/blake3_lite.h"
 #include "../wtf_amd/host/kdmp.h"
 #include "../wtf_amd/host/wire.h"
@@ -211,6 +219,38 @@ static int cmd_mutate(int argc, char **argv, bool grow = false) {
   return 0;
 }
 
+static int cmd_merge_blocks(int argc, char **argv) {
+  if (argc < 4) return 2;
+  const uint64_t cap = strtoull(argv[2], nullptr, 0), world = strtoull(argv[3], nullptr, 0);
+  std::vector<wtfgpu_host::MergeBlocks> ranks;
+  for (uint64_t r = 0; r < world; r++) ranks.emplace_back(cap);
+  std::vector<uint64_t> next(world, 0);
+  for (int a = 4; a < argc; a++) {
+    std::vector<uint64_t> blocks(world * (1 + cap), 0);
+    const char *p = argv[a];
+    for (uint64_t r = 0; r < world; r++) {
+      char *e = nullptr;
+      const uint64_t n = strtoull(p, &e, 10);
+      const bool done = *e == 'd';
+      p = e + 1;
+      if (*p == ',') p++;
+      std::vector<uint64_t> mine;
+      for (uint64_t i = 0; i < n; i++) mine.push_back(r << 32 | next[r]++);
+      ranks[r].Pack(mine, done, &blocks[r * (1 + cap)]);
+    }
+    std::vector<uint64_t> all;
+    bool every = false;
+    if (!wtfgpu_host::MergeBlocks::Unpack(blocks.data(), blocks.size(), world, 1 + cap, cap, all, &every)) {
+      printf("BAD\n");
+      return 1;
+    }
+    printf("S %d", every ? 1 : 0);
+    for (uint64_t v : all) printf(" %llx", (unsigned long long)v);
+    printf("\n");
+  }
+  return 0;
+}
+
 static std::vector<uint8_t> unhex(const char *p) {
   std::vector<uint8_t> b;
   for (; p[0] && p[1]; p += 2) b.push_back((uint8_t)strtoul(std::string(p, 2).c_str(), nullptr, 16));
@@ -339,6 +379,7 @@ int main(int argc, char **argv) {
   if (cmd == "cpustate" && argc == 3) return cmd_cpustate(argv[2]);
   if (cmd == "mutate") return cmd_mutate(argc, argv);
   if (cmd == "mutate-grow") return cmd_mutate(argc, argv, true);
+  if (cmd == "merge-blocks") return cmd_merge_blocks(argc, argv);
   if (cmd == "blake3" && argc == 3) {
     const auto b = unhex(argv[2]);
     printf("%s\n", Blake3HexDigest(b.data(), b.size()).c_str());

@@ -9,6 +9,8 @@
 // from the caller (libwtfnode, bench.py broadcasts it).
 #include "rccl_exchange.h"
 
+#include "merge_block.h"
+
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -27,15 +29,15 @@ struct RcclExchange_t::Impl {
   uint8_t *flag = nullptr;       // device byte for AllDone
   uint64_t *gbuf = nullptr;      // AllGatherV staging: world counts, then world * cap values
   uint64_t gcap = 0;             // u64 slots in gbuf
-  // deferred merge: the reduced map, the (flag | count, values) blocks sent /
-  // received (device and pinned host), the event MergeEnd waits for, and the
-  // overflow values still to send
-  uint8_t *merged = nullptr;
+  // deferred merge: the frozen copy of the map and the reduced map, the
+  // MergeBlocks blocks sent / received (device and pinned host), the event
+  // MergeEnd waits for, and the overflow values still to send
+  uint8_t *frozen = nullptr, *merged = nullptr;
   uint64_t merged_bytes = 0, merged_cap = 0;
   uint64_t *dsend = nullptr, *drecv = nullptr, *hsend = nullptr, *hrecv = nullptr;
   hipEvent_t ev = nullptr;
   bool inflight = false;
-  std::vector<uint64_t> carry;
+  MergeBlocks blocks{kMergeCap};
 };
 
 bool RcclUniqueId(uint8_t Out[kRcclIdBytes]) {
@@ -73,6 +75,7 @@ RcclExchange_t::~RcclExchange_t() {
   if (impl_->stream) (void)hipStreamSynchronize(impl_->stream);  // a merge still in flight completes (every rank issued it)
   if (impl_->comm) ncclCommDestroy(impl_->comm);
   if (impl_->merged) (void)hipFree(impl_->merged);
+  if (impl_->frozen) (void)hipFree(impl_->frozen);
   if (impl_->dsend) (void)hipFree(impl_->dsend);
   if (impl_->drecv) (void)hipFree(impl_->drecv);
   if (impl_->hsend) (void)hipHostFree(impl_->hsend);
@@ -181,21 +184,26 @@ bool RcclExchange_t::MergeBegin(const uint8_t *Map, uint64_t Bytes, bool Device,
   }
   if (Bytes > I.merged_cap) {  // the map's size is fixed after set_code_pages: the first merge sizes it
     if (I.merged) (void)hipFree(I.merged);
-    I.merged = nullptr;
+    if (I.frozen) (void)hipFree(I.frozen);
+    I.merged = I.frozen = nullptr;
     I.merged_cap = 0;
-    if (hipMalloc((void **)&I.merged, Bytes) != hipSuccess) return false;
+    if (hipMalloc((void **)&I.merged, Bytes) != hipSuccess || hipMalloc((void **)&I.frozen, Bytes) != hipSuccess)
+      return false;
     I.merged_cap = Bytes;
   }
   I.merged_bytes = Bytes;
-  I.carry.insert(I.carry.end(), Extras.begin(), Extras.end());
-  const uint64_t k = std::min<uint64_t>(I.carry.size(), kMergeCap);
-  // done only once nothing is left to send
-  I.hsend[0] = k | ((Done && I.carry.size() == k) ? 1ull << 63 : 0);
-  if (k) memcpy(I.hsend + 1, I.carry.data(), k * 8);
-  I.carry.erase(I.carry.begin(), I.carry.begin() + (std::ptrdiff_t)k);
-  if (hipMemcpyAsync(I.dsend, I.hsend, (1 + k) * 8, hipMemcpyHostToDevice, I.stream) != hipSuccess) return false;
+  // The map as of this step, frozen before the call returns: the engine's
+  // coverage commits are synchronous (so the live map is final here), and the
+  // next step's commits may write it while the all-reduce below still runs.
+  // Every shard reduces what it had at the same step: a fixed-seed campaign
+  // merges the same maps whatever the collective's timing (DESIGN U44).
+  if (Bytes && (hipMemcpyAsync(I.frozen, Map, Bytes, hipMemcpyDeviceToDevice, I.stream) != hipSuccess ||
+                hipStreamSynchronize(I.stream) != hipSuccess))
+    return false;
+  const uint64_t words = I.blocks.Pack(Extras, Done, I.hsend);
+  if (hipMemcpyAsync(I.dsend, I.hsend, words * 8, hipMemcpyHostToDevice, I.stream) != hipSuccess) return false;
   if (ncclGroupStart() != ncclSuccess) return false;
-  if (Bytes && ncclAllReduce(Map, I.merged, Bytes, ncclUint8, ncclMax, I.comm, I.stream) != ncclSuccess) return false;
+  if (Bytes && ncclAllReduce(I.frozen, I.merged, Bytes, ncclUint8, ncclMax, I.comm, I.stream) != ncclSuccess) return false;
   if (ncclAllGather(I.dsend, I.drecv, B, ncclUint64, I.comm, I.stream) != ncclSuccess) return false;
   if (ncclGroupEnd() != ncclSuccess) return false;
   if (hipMemcpyAsync(I.hrecv, I.drecv, W * B * 8, hipMemcpyDeviceToHost, I.stream) != hipSuccess ||
@@ -220,14 +228,7 @@ bool RcclExchange_t::MergeEnd(const uint8_t **Merged, uint64_t *Bytes, std::vect
   }
   if (hipEventSynchronize(I.ev) != hipSuccess) return false;
   const uint64_t W = (uint64_t)world_, B = kMergeCap + 1;
-  AllExtras.clear();
-  bool all = true;
-  for (uint64_t r = 0; r < W; r++) {
-    const uint64_t h = I.hrecv[r * B], k = std::min<uint64_t>(h & ~(1ull << 63), kMergeCap);
-    all = all && (h >> 63);
-    AllExtras.insert(AllExtras.end(), I.hrecv + r * B + 1, I.hrecv + r * B + 1 + k);
-  }
-  *AllDone = all;
+  if (!MergeBlocks::Unpack(I.hrecv, W * B, W, B, kMergeCap, AllExtras, AllDone)) return false;
   *Merged = I.merged;
   *Bytes = I.merged_bytes;
   return true;

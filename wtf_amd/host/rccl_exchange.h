@@ -27,13 +27,14 @@ class RcclExchange_t final : public CoverageExchange_t {
   bool AllReduceMax(uint8_t *Map, uint64_t Bytes, bool Device) override;
   bool AllDone(bool Mine, bool *All) override;
   bool AllGatherV(const std::vector<uint64_t> &Mine, std::vector<uint64_t> &All) override;
-  // the deferred merge on the exchange's stream: MAX all-reduce of the map
-  // into a buffer of its own, one all-gather of (done flag, up to kMergeCap
-  // overflow values) per rank, fused in one group; nothing waits before MergeEnd
+  // the deferred merge on the exchange's stream: a frozen copy of the map (the
+  // next step's commits write the live one), MAX all-reduce of that copy into
+  // a buffer of its own, one all-gather of every rank's MergeBlocks block
+  // (merge_block.h), fused in one group; nothing waits on the collectives
+  // before MergeEnd
   bool MergeBegin(const uint8_t *Map, uint64_t Bytes, bool Device, const std::vector<uint64_t> &Extras,
                   bool Done) override;
   bool MergeEnd(const uint8_t **Merged, uint64_t *Bytes, std::vector<uint64_t> &AllExtras, bool *AllDone) override;
-  static constexpr uint64_t kMergeCap = 4096;  // overflow values per rank per merge (the rest wait their turn)
 
  private:
   struct Impl;

@@ -540,6 +540,12 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
   if (!O.address.empty()) return NodeMain(O, Exec, *Target, Slots);
 
   // ---- fuzz: in-process master + batched node
+  if (X && X->World() > 1 && O.full_coverage) {
+    // parity mode resets the map every batch: a merge in flight reads a copy
+    // taken when it started, but the shards' maps would mean nothing
+    printf("--full-coverage is a single-node parity mode (not with --world > 1)\n");
+    return 1;
+  }
   FuzzSession F(O, Exec, *Target, Slots, X);
   if (!F.Start()) {
     printf("Nothing to run: empty corpus and no inputs\n");
@@ -1004,8 +1010,11 @@ bool CoverageExchange_t::MergeBegin(const uint8_t *Map, uint64_t Bytes, bool Dev
   merged_.assign(Map, Map + Bytes);
   merged_device_ = false;
   if (Bytes && !AllReduceMax(merged_.data(), Bytes, false)) return false;
-  if (!AllGatherV(Extras, merged_extra_)) return false;
-  return AllDone(Done, &merged_done_);
+  std::vector<uint64_t> Block(1 + blocks_.Cap()), Blocks;
+  Block.resize(blocks_.Pack(Extras, Done, Block.data()));
+  if (!AllGatherV(Block, Blocks)) return false;
+  return MergeBlocks::Unpack(Blocks.data(), Blocks.size(), (uint64_t)World(), 0, kMergeCap, merged_extra_,
+                             &merged_done_);
 }
 
 bool CoverageExchange_t::MergeEnd(const uint8_t **Merged, uint64_t *Bytes, std::vector<uint64_t> &AllExtras,

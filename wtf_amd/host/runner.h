@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/wtfgpu.h"
+#include "merge_block.h"
 #include "wtf_api.h"
 
 namespace wtfgpu_host {
@@ -155,9 +156,12 @@ class CoverageExchange_t {
   // MergeBegin, waits for them and hands out the merged map (host or device
   // memory like Map, valid until the next MergeBegin), every shard's extras
   // in rank order and whether every shard was done. Nothing waits in the step
-  // that starts a merge; its result is absorbed one step later. This default
-  // runs the synchronous collectives above inside MergeBegin (the TCP twins);
-  // RcclExchange_t overlaps them with the step on a stream of their own.
+  // that starts a merge; its result is absorbed one step later. The overflow
+  // values and the done flags travel as MergeBlocks blocks (merge_block.h: at
+  // most kMergeCap values per shard per merge, done only once a shard's queue
+  // is empty). This default runs the synchronous collectives above inside
+  // MergeBegin on a copy of the map (the TCP twins); RcclExchange_t overlaps
+  // them with the step on a stream of their own.
   virtual bool MergeBegin(const uint8_t *Map, uint64_t Bytes, bool Device, const std::vector<uint64_t> &Extras,
                           bool Done);
   virtual bool MergeEnd(const uint8_t **Merged, uint64_t *Bytes, std::vector<uint64_t> &AllExtras, bool *AllDone);
@@ -166,6 +170,7 @@ class CoverageExchange_t {
   std::vector<uint8_t> merged_;       // the default MergeBegin's result
   std::vector<uint64_t> merged_extra_;
   bool merged_done_ = false, merged_device_ = false;
+  MergeBlocks blocks_{kMergeCap};
 };
 
 // BochscpuRunStats_t::Print (bochscpu_backend.h:25-37; NumberToHuman /
