@@ -67,8 +67,8 @@
 #include <vector>
 
 #ifdef WTF_AMD_HOST
-#include "../wtf_amd/host/merge_block.h"
 #include "../wtf_amd/host/blake3_lite.h"
+#include "../wtf_amd/host/merge_block.h"
 #include "../wtf_amd/host/kdmp.h"
 #include "../wtf_amd/host/wire.h"
 #include "../wtf_amd/host/wtf_api.h"
@@ -219,6 +219,7 @@ static int cmd_mutate(int argc, char **argv, bool grow = false) {
   return 0;
 }
 
+#ifdef WTF_AMD_HOST
 static int cmd_merge_blocks(int argc, char **argv) {
   if (argc < 4) return 2;
   const uint64_t cap = strtoull(argv[2], nullptr, 0), world = strtoull(argv[3], nullptr, 0);
@@ -250,6 +251,8 @@ static int cmd_merge_blocks(int argc, char **argv) {
   }
   return 0;
 }
+
+#endif
 
 static std::vector<uint8_t> unhex(const char *p) {
   std::vector<uint8_t> b;
@@ -379,7 +382,9 @@ int main(int argc, char **argv) {
   if (cmd == "cpustate" && argc == 3) return cmd_cpustate(argv[2]);
   if (cmd == "mutate") return cmd_mutate(argc, argv);
   if (cmd == "mutate-grow") return cmd_mutate(argc, argv, true);
+#ifdef WTF_AMD_HOST
   if (cmd == "merge-blocks") return cmd_merge_blocks(argc, argv);
+#endif
   if (cmd == "blake3" && argc == 3) {
     const auto b = unhex(argv[2]);
     printf("%s\n", Blake3HexDigest(b.data(), b.size()).c_str());

@@ -2,7 +2,9 @@
 BochscpuBackend_t::SetTraceFile / BeforeExecutionHook, bochscpu_backend.cc:
 506-520, subcommands.cc:52-74): one `<input>.trace` per input, one "%#x" rip
 per line, every rip about to execute (rip) or only those new to the aggregate
-(cov). The GPU records them on the device (wtfgpu_set_trace); the twin from
+(cov), which the Restore after a traced run empties (bochscpu_backend.cc:
+778-789): a cov trace holds the rips unique within its run. Under --runs only
+an input's first run is traced (the same Restore closes the file). The GPU records them on the device (wtfgpu_set_trace); the twin from
 the oracle; their files must be identical. Tenet traces (`--trace-type
 tenet`, bochscpu_backend.cc:1215-1323; the format is checked in
 tests/test_tenet.py) likewise, byte for byte.
@@ -21,9 +23,9 @@ def read_trace(path):
         return [int(x, 16) for x in f.read().split()]
 
 
-def traces(exe, target, out, kind="rip", name="tlv_server", lanes=16):
+def traces(exe, target, out, kind="rip", name="tlv_server", lanes=16, runs=1):
     res = H.run(exe, target, os.path.join(target, "inputs"), str(out) + ".jsonl", lanes=lanes, name=name,
-                extra=["--trace-path", str(out), "--trace-type", kind])
+                extra=["--trace-path", str(out), "--trace-type", kind] + (["--runs", str(runs)] if runs > 1 else []))
     return res, {f[:-6]: read_trace(os.path.join(out, f)) for f in os.listdir(out)}
 
 
@@ -47,17 +49,34 @@ def test_twin_rip_trace_is_the_executed_rips(tlv, tmp_path):
         assert len(t) >= r["icount"]
 
 
-def test_cov_trace_is_first_occurrences_in_input_order(tlv, tmp_path):
+def _first_occurrences(rips, seen):
+    want = []
+    for v in rips:
+        if v not in seen:
+            seen.add(v)
+            want.append(v)
+    return want
+
+
+def test_cov_trace_is_the_run_s_unique_rips(tlv, tmp_path):
     _, rip = traces(H.TWIN, tlv, tmp_path / "r", "rip")
     _, cov = traces(H.TWIN, tlv, tmp_path / "c", "cov")
-    seen = set()
     for name in sorted(rip):
-        want = []
-        for v in rip[name]:
-            if v not in seen:
-                seen.add(v)
-                want.append(v)
-        assert cov[name] == want, name
+        assert cov[name] == _first_occurrences(rip[name], set()), name
+
+
+def test_runs_trace_the_first_run_only(tlv, tmp_path):
+    """--runs 3: each input's first run is traced; its other two runs add
+    their rips to the aggregate the next input's cov trace starts from (the
+    reference empties it only after a traced run)."""
+    _, rip = traces(H.TWIN, tlv, tmp_path / "r", "rip")
+    res3, rip3 = traces(H.TWIN, tlv, tmp_path / "r3", "rip", runs=3)
+    assert rip3 == rip and len(res3) == 3 * len(rip)
+    _, cov3 = traces(H.TWIN, tlv, tmp_path / "c3", "cov", runs=3)
+    prev = set()
+    for name in sorted(rip):
+        assert cov3[name] == _first_occurrences(rip[name], set(prev)), name
+        prev = set(rip[name])
 
 
 def test_existing_traces_are_skipped(tlv, tmp_path):
@@ -75,9 +94,9 @@ def test_existing_traces_are_skipped(tlv, tmp_path):
 @pytest.mark.parametrize("which", ["tlv", "hevd"])
 def test_gpu_traces_equal_twin(which, tlv, hevd, tmp_path):
     target, name = (tlv, "tlv_server") if which == "tlv" else (hevd, "hevd")
-    for kind in ("rip", "cov"):
-        ra, a = traces(H.TWIN, target, tmp_path / f"twin_{kind}", kind, name=name)
-        rb, b = traces(H.WTFGPU, target, tmp_path / f"gpu_{kind}", kind, name=name)
+    for kind, runs in (("rip", 1), ("cov", 1), ("cov", 2)):
+        ra, a = traces(H.TWIN, target, tmp_path / f"twin_{kind}{runs}", kind, name=name, runs=runs)
+        rb, b = traces(H.WTFGPU, target, tmp_path / f"gpu_{kind}{runs}", kind, name=name, runs=runs)
         assert a == b, kind
         assert sum(len(t) for t in a.values()) > 100
 

@@ -308,6 +308,9 @@ size_t GpuBackend_t::alloc_slots(size_t n, uint8_t **orig, uint8_t **data) const
   // second driver thread, whose loop ran serially because another thread held
   // the pool, never shares arena 0 with that loop's caller
   const bool in_loop = HostPool::InLoop();
+  // shared with other allocations, exclusive with recycle_arenas: the slots
+  // are counted as live (live_staged_) before a recycle can look
+  std::shared_lock<std::shared_mutex> recycling(recycle_mu_);
   std::unique_lock<std::mutex> spare(spare_mu_, std::defer_lock);
   if (!in_loop) spare.lock();
   Arena &A = arenas_[in_loop ? HostPool::ThreadIndex() : arenas_.size() - 1];
@@ -334,15 +337,19 @@ size_t GpuBackend_t::alloc_slots(size_t n, uint8_t **orig, uint8_t **data) const
   *data = b.data.get() + b.used * Page::Size;
   const size_t first = b.used;
   b.used += n;
+  live_staged_ += n;  // reserved here, each one staged (stage) or released (release_slots)
   return first;
 }
+
+void GpuBackend_t::release_slots(size_t n) const { live_staged_ -= n; }
 
 bool GpuBackend_t::parallel_service(const ModuleSlots *slots) const {
   return slots && slots->ThreadSafe() && HostPool::Get().Threads() > 1;
 }
 
 uint8_t *GpuBackend_t::stage(uint32_t lane, uint64_t gpfn, const uint8_t *orig, uint8_t *data) const {
-  live_staged_++;
+  // orig / data: slots alloc_slots counted as live, or (orig only) a dump or
+  // zero page with a fresh slot for data
   LaneView &v = views_[lane];
   v.pages.push_back(Staged{gpfn, data, orig});
   for (LaneView::Logged &w : v.wlog)  // logged writes to this page move into it
@@ -423,6 +430,9 @@ void GpuBackend_t::drop_staged(LaneView &v) const {
 // only; callers of parallel drop_staged call it after their loop).
 void GpuBackend_t::recycle_arenas() const {
   if (live_staged_ != 0 || HostPool::InLoop()) return;
+  std::unique_lock<std::shared_mutex> recycling(recycle_mu_);
+  if (live_staged_ != 0) return;  // an allocation came in between
+  std::lock_guard<std::mutex> spare(spare_mu_);
   for (Arena &A : arenas_) {
     for (Block &b : A.blocks) b.used = 0;
     A.cur = 0;
@@ -1040,7 +1050,10 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
       const size_t np = pf_lanes.size();
       uint8_t *o, *d;
       alloc_slots(np, &o, &d);
-      if (wtfgpu_gather_pages(ctx_, pf_lanes.data(), pf_gpas.data(), (uint32_t)np, o)) return false;
+      if (wtfgpu_gather_pages(ctx_, pf_lanes.data(), pf_gpas.data(), (uint32_t)np, o)) {
+        release_slots(np);
+        return false;
+      }
       HostPool::Get().For(np, 256, [&](size_t i) { memcpy(d + i * Page::Size, o + i * Page::Size, Page::Size); });
       for (size_t i = 0; i < np; i++)
         stage(pf_lanes[i], pf_gpas[i] >> 12, o + i * Page::Size, d + i * Page::Size);

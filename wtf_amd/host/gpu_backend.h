@@ -17,6 +17,7 @@
 #include <atomic>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -299,6 +300,8 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   };
   mutable std::vector<Arena> arenas_;  // [0, Threads()): HostPool threads in a loop; the last: calls outside loops
   mutable std::mutex spare_mu_;        // the last arena's lock
+  mutable std::shared_mutex recycle_mu_;  // allocations (shared) vs recycle_arenas (exclusive)
+  void release_slots(size_t n) const;     // slots alloc_slots reserved that were never staged
   std::unordered_map<uint64_t, uint64_t> covlog_count_;  // WTFGPU_COVLOG_TOP diagnostic
   uint64_t covlog_calls_ = 0;
   void recycle_arenas() const;

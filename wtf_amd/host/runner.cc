@@ -348,18 +348,15 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
     // stats are printed for a single input run once (:48)
     const uint64_t Runs = O.runs ? O.runs : 1;
     const bool Stats = Inputs.size() == 1 && Runs == 1 && !O.quiet;
-    if (Runs > 1) {
-      std::vector<fs::path> Rep;
-      Rep.reserve(Inputs.size() * Runs);
-      for (const fs::path &In : Inputs)
-        for (uint64_t k = 0; k < Runs; k++) Rep.push_back(In);
-      Inputs.swap(Rep);
-    }
     LaneResult Last;
     // traces (subcommands.cc:52-74): <trace-path>/<input name>.trace; an input
     // whose trace exists is skipped
     const bool Trace = !O.trace_path.empty();
-    std::unordered_set<uint64_t> TraceSeen;  // cov traces: rips not seen in earlier testcases
+    // cov traces: the reference logs a rip absent from its aggregate coverage
+    // (bochscpu_backend.cc:501-516), which the Restore after a traced run
+    // empties (:778-789): a traced run's rips unique within it, plus, under
+    // --runs, the rips the previous input's untraced repetitions added
+    std::unordered_set<uint64_t> TraceSeen;
     if (Trace) {
       if (O.trace_type != "rip" && O.trace_type != "cov" && O.trace_type != "tenet") {
         printf("--trace-type %s is not supported by this backend (rip, cov, tenet)\n", O.trace_type.c_str());
@@ -385,7 +382,29 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
       }
       Inputs = Keep;
     }
-    auto write_trace = [&](const fs::path &In, uint32_t Lane) -> bool {
+    // the repetition of each input (0 = its first run: the only one traced,
+    // since the reference's Restore closes the trace file after it)
+    std::vector<uint64_t> RepOf(Inputs.size(), 0);
+    if (Runs > 1) {
+      std::vector<fs::path> Rep;
+      Rep.reserve(Inputs.size() * Runs);
+      RepOf.clear();
+      for (const fs::path &In : Inputs)
+        for (uint64_t k = 0; k < Runs; k++) {
+          Rep.push_back(In);
+          RepOf.push_back(k);
+        }
+      Inputs.swap(Rep);
+    }
+    auto write_trace = [&](const fs::path &In, uint32_t Lane, uint64_t Rep) -> bool {
+      if (Rep) {  // an untraced repetition: its rips join the aggregate the next cov trace starts from
+        if (O.trace_type != "cov") return true;
+        std::vector<uint64_t> Rips;
+        bool Truncated = false;
+        if (!Exec.LaneTrace(Lane, Rips, Truncated)) return false;
+        TraceSeen.insert(Rips.begin(), Rips.end());
+        return true;
+      }
       if (O.trace_type == "tenet") {
         std::vector<uint8_t> Bytes;
         bool Truncated = false;
@@ -404,6 +423,7 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
       if (!F) return false;
       for (uint64_t R : Rips)
         if (O.trace_type == "rip" || TraceSeen.insert(R).second) fprintf(F, "%#llx\n", (unsigned long long)R);
+      TraceSeen.clear();
       fclose(F);
       if (Truncated) printf("trace of %s truncated at %zu rips (--trace-cap)\n", In.string().c_str(), Rips.size());
       return true;
@@ -522,7 +542,7 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
       for (size_t i = 0; i < n; i++) {
         Retired += R[i].icount;
         print(Inputs[b + i], R[i]);
-        if (Trace && !write_trace(Inputs[b + i], (uint32_t)i)) {
+        if (Trace && !write_trace(Inputs[b + i], (uint32_t)i, RepOf[b + i])) {
           printf("trace of %s failed\n", Inputs[b + i].string().c_str());
           return 1;
         }
