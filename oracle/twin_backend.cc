@@ -118,6 +118,7 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
   std::optional<TestcaseResult_t> Run(const uint8_t *, const uint64_t) override {
     flush();
     engine_error_ = false;
+    handler_fault_ = false;
     int skip = 0;
     for (;;) {
       wtfgpu_exit_t e{};
@@ -139,6 +140,7 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
           flush();
           result_ = Crash_t();
           engine_error_ = true;
+          handler_fault_ = true;
           break;
         }
         flush();
@@ -340,6 +342,7 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
   uint32_t route_lane_ = 0;
   bool full_ = false;
   bool engine_error_ = false;
+  bool handler_fault_ = false;  // U43 (within engine_error_)
   UnimplHist unimpl_;  // WTF_UNIMPL_HIST=1: printed to stderr at exit
   void SetFullCoverage(bool On) override { full_ = On; }
   size_t CoverageSize() const override { return aggregate_.size(); }
@@ -386,6 +389,7 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
         inserted = T.InsertTestcase(Tc[i].first, Tc[i].second);
       } catch (const HandlerFault_t &) {  // U43
         engine_error_ = true;
+        handler_fault_ = true;
       }
       if (!inserted) result_ = Crash_t(engine_error_ ? "" : "insert-testcase-failed");
       std::optional<TestcaseResult_t> R;
@@ -397,8 +401,10 @@ class TwinBackend_t final : public Backend_t, public Executor_t {
       }
       L.result = *R;
       L.error = engine_error_;
+      L.handler_fault = handler_fault_;
       if (L.error) L.result = Crash_t();
       engine_error_ = false;
+      handler_fault_ = false;
       if (std::holds_alternative<Timedout_t>(*R)) {
         L.new_coverage.assign(0, 0);
         for (const Gva_t &g : last_new_) L.new_coverage.push_back(g.U64());
@@ -472,6 +478,7 @@ int main(int argc, char **argv) {
     bool EnableTrace(uint32_t P) override { return b->EnableTrace(P); }
     uint64_t LastIcount() const override { return b->Icount(); }
     bool LastError() const override { return b->engine_error_; }
+    bool LastHandlerFault() const override { return b->handler_fault_; }
     void LastRunStats(LaneResult &L) const override { b->RunStats(L); }
     bool LaneTrace(uint32_t L, std::vector<uint64_t> &R, bool &T) override { return b->LaneTrace(L, R, T); }
     bool EnableTenet(uint64_t P) override { return b->EnableTenet(P); }

@@ -835,6 +835,7 @@ bool GpuBackend_t::fill_results(const std::vector<uint32_t> &lanes, uint32_t fir
     if (v.handler_fault) {  // U43: an engine error, never a named crash
       r.result = Crash_t();
       r.error = true;
+      r.handler_fault = true;
       stats_.err_handler++;
     }
     if (want_gprs_) {
@@ -1584,6 +1585,7 @@ bool GpuBackend_t::harvest_part(Part &P, const Target_t &Target, std::vector<Str
     LaneResult &r = lres_[l];
     r.result = Ok_t();
     r.error = false;
+    r.handler_fault = false;
     r.exit_status = 0;
     r.icount = 0;
     r.rip = 0;

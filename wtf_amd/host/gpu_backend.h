@@ -114,6 +114,7 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   void SetWantRegisters(bool On) override { want_gprs_ = On; }
   uint64_t LastIcount() const override { return last_icount_; }
   bool LastError() const override { return last_error_; }
+  bool LastHandlerFault() const override { return last_run_.handler_fault; }
   void LastRunStats(LaneResult &L) const override {
     L.bytes = last_run_.bytes;
     L.dirty = last_run_.dirty;

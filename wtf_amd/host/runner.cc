@@ -442,8 +442,9 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
       for (int g = 0; g < 18; g++) fprintf(Out, "%s%llu", g ? "," : "", (unsigned long long)L.gprs[g]);
       fprintf(Out, "],\"coverage\":[");
       for (size_t c = 0; c < Cov.size(); c++) fprintf(Out, "%s%llu", c ? "," : "", (unsigned long long)Cov[c]);
-      fprintf(Out, "],\"bytes\":%llu,\"dirty\":%u,\"edges\":%llu,\"edges_new\":%llu}\n", (unsigned long long)L.bytes,
-              L.dirty, (unsigned long long)L.edges, (unsigned long long)L.edges_new);
+      fprintf(Out, "],\"bytes\":%llu,\"dirty\":%u,\"edges\":%llu,\"edges_new\":%llu,\"handler_fault\":%d}\n",
+              (unsigned long long)L.bytes, L.dirty, (unsigned long long)L.edges, (unsigned long long)L.edges_new,
+              (int)L.handler_fault);
       Last = L;
     };
     if (O.serial && !Trace) {
@@ -465,6 +466,7 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
           Inserted = Target->InsertTestcase(Buf.data(), Buf.size());
         } catch (const HandlerFault_t &) {  // U43: an engine error for this testcase
           L.error = true;
+          L.handler_fault = true;
         }
         if (!Inserted) {
           L.result = L.error ? Crash_t() : Crash_t("insert-testcase-failed");
@@ -481,6 +483,7 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
           if (std::holds_alternative<Timedout_t>(*Res)) B->RevokeLastNewCoverage();
           L.icount = Exec.LastIcount();
           L.error = Exec.LastError();
+          L.handler_fault = Exec.LastHandlerFault();
           Exec.LastRunStats(L);
         }
         for (int g = 0; g < 18; g++) L.gprs[g] = B->GetReg(Order[g]);

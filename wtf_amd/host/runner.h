@@ -29,6 +29,7 @@ namespace wtfgpu_host {
 struct LaneResult {
   TestcaseResult_t result;
   bool error = false;        // the engine could not finish the testcase (unimplemented opcode, overlay full)
+  bool handler_fault = false;  // ... because a handler's guest access did not translate (DESIGN U43)
   uint32_t exit_status = 0;  // last engine exit status (wtfgpu_status)
   uint64_t icount = 0;       // retired instructions
   uint64_t rip = 0;
@@ -95,6 +96,7 @@ class Executor_t {
   // the retired count / engine-error flag of the last Backend_t::Run
   virtual uint64_t LastIcount() const { return 0; }
   virtual bool LastError() const { return false; }
+  virtual bool LastHandlerFault() const { return false; }
   // the run stats (LaneResult::bytes / dirty / edges / edges_new) of the last Backend_t::Run
   virtual void LastRunStats(LaneResult &) const {}
   virtual size_t CoverageSize() const = 0;
