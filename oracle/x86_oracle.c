@@ -579,6 +579,9 @@ typedef struct {
   u32 has_modrm, mod, reg, rm; /* reg, rm include REX extension */
   u32 is_mem;
   u64 ea; /* effective address (linear, seg base included) */
+  int vsib_idx, vsib_base; /* the SIB's raw index register (-1: no SIB) and base (-1: none), for VSIB */
+  u32 vsib_ss;
+  u64 vsib_disp;
   u8 bytes[16];
   u32 pos;
   int fetch_fail;
@@ -632,6 +635,7 @@ static void decode_modrm(orc_machine *m, insn *d, memref *mr) {
   memset(mr, 0, sizeof(*mr));
   mr->base = -1;
   mr->index = -1;
+  d->vsib_idx = -1;
   if (d->mod == 3) {
     d->rm = rm | (d->rexb << 3);
     d->is_mem = 0;
@@ -641,6 +645,8 @@ static void decode_modrm(orc_machine *m, insn *d, memref *mr) {
   if (rm == 4) {
     u8 sib = fetch8(m, d);
     u32 ss = sib >> 6, idx = ((sib >> 3) & 7) | (d->rexx << 3), base = sib & 7;
+    d->vsib_idx = (int)idx;
+    d->vsib_ss = ss;
     if (idx != 4) {
       mr->index = (int)idx;
       mr->scale = 1 << ss;
@@ -658,6 +664,8 @@ static void decode_modrm(orc_machine *m, insn *d, memref *mr) {
   }
   if (d->mod == 1) mr->disp = sxn(fetchn(m, d, 1), 1);
   if (d->mod == 2) mr->disp = sxn(fetchn(m, d, 4), 4);
+  d->vsib_base = mr->base;
+  d->vsib_disp = mr->disp;
 }
 
 static void finish_ea(orc_machine *m, insn *d, memref *mr) {
@@ -1067,7 +1075,9 @@ static int muldiv(orc_machine *m, insn *d, int sub, int sz, u64 src) {
 }
 
 /* ---------------- execute one instruction ---------------- */
-enum { X_OK = 0, X_FAULT = 1, X_UNIMPL = 2, X_INT3 = 3, X_HLT = 4, X_CR3 = 5, X_FAULT_KEEP = 6 };
+/* X_FAULT_KEEP: rep progress stays; X_FAULT_PARTIAL: a gather's completed
+ * elements stay in its registers (U46), its bytes are not counted */
+enum { X_OK = 0, X_FAULT = 1, X_UNIMPL = 2, X_INT3 = 3, X_HLT = 4, X_CR3 = 5, X_FAULT_KEEP = 6, X_FAULT_PARTIAL = 7 };
 
 #define CHK(x)                                                                                   \
   do {                                                                                           \
@@ -1458,6 +1468,8 @@ static int gx_form_o(u32 map, u32 c, int pp, int vex); /* x86_oracle_ext.inc */
 static int x42_form_o(u32 map, u32 c, int pp, int vex);
 static int exec_gext(orc_machine *m, insn *d);
 static int exec_x42(orc_machine *m, insn *d);
+static int ax_form_o(u32 map, u32 c, int pp, int vex); /* x86_oracle_avx2x.inc */
+static int exec_ax(orc_machine *m, insn *d);
 
 static int exec_sse(orc_machine *m, insn *d) {
   const u32 op = d->op, r3 = d->reg & 7;
@@ -1814,6 +1826,7 @@ static void yput(orc_machine *m, u32 r, y256 v, int l256) {
 #include "x86_oracle_fp.inc" /* SSE / AVX floating point (U39 / U40) */
 #include "x86_oracle_sse4.inc" /* SSSE3 / SSE4.1 integer, AVX2 lane crossing (U41) */
 #include "x86_oracle_ext.inc"  /* BMI1 / BMI2 / ADX / MOVBE / CRC32, SSE4.2, AES, PCLMULQDQ (U45) */
+#include "x86_oracle_avx2x.inc" /* FMA3, F16C, AVX2 gathers (U46) */
 
 /* two-source ops of one 128-bit lane (the legacy semantics); 0 = not one */
 static int vlane(u32 op, int pc, const x128 *a, const x128 *b, u8 imm, u64 cnt, x128 *r) {
@@ -2027,6 +2040,7 @@ static int exec_vex(orc_machine *m, insn *d) {
   if (s4_form_o(map, op, pp, 1)) return exec_s4(m, d); /* U41 */
   if (gx_form_o(map, op, pp, 1)) return exec_gext(m, d); /* U45 */
   if (x42_form_o(map, op, pp, 1)) return exec_x42(m, d);
+  if (ax_form_o(map, op, pp, 1)) return exec_ax(m, d); /* U46 */
   if (map == 1 && op == 0xae && !(pp == 0 && mem && (r3 == 2 || r3 == 3))) { /* U36: vldmxcsr / vstmxcsr only */
     fault(m, WTFGPU_VEC_UD, 0);
     return X_FAULT;
@@ -3210,7 +3224,8 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
     d->undef = d->vbad || d->opmap < 1 || d->opmap > 3 || !vex_defined(d->opmap, b, (int)d->vpp);
     if (d->opmap != 1 && d->opmap != 2 &&
         !(d->opmap == 3 && !d->undef && (fp_form_o(3, b, (int)d->vpp, 1) || s4_form_o(3, b, (int)d->vpp, 1) ||
-                                         x42_form_o(3, b, (int)d->vpp, 1) || gx_form_o(3, b, (int)d->vpp, 1)))) {
+                                         x42_form_o(3, b, (int)d->vpp, 1) || gx_form_o(3, b, (int)d->vpp, 1) ||
+                                         ax_form_o(3, b, (int)d->vpp, 1)))) {
       d->op = b;
       d->len = d->pos;
       return 1;
@@ -3317,7 +3332,7 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
         b == 0x22 || b == 0x00 || b == 0x02 || b == 0x03 || b == 0x21 || b == 0x23 || b == 0xb2 || b == 0xb4 ||
         b == 0xb5 || (b >= 0x18 && b <= 0x1f))
       has_modrm = 1;
-    if (b == 0xa4 || b == 0xac || b == 0xba) {
+    if (d->opmap == 1 && (b == 0xa4 || b == 0xac || b == 0xba)) { /* shld / shrd imm8, group 8 (not 0f 38 ac / ba: FMA3) */
       has_modrm = 1;
       imm = 1;
     }
@@ -3529,6 +3544,10 @@ static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
    * except rep string progress which is architecturally committed */
   if (x == X_FAULT_KEEP) {
     m->r.rip = saved.rip;
+    x = X_FAULT;
+  } else if (x == X_FAULT_PARTIAL) {
+    m->r.rip = saved.rip;
+    m->bytes = saved_bytes;
     x = X_FAULT;
   } else {
     m->r = saved;

@@ -433,6 +433,9 @@ def run_native(cases, generator, out_path, mem_writes=False):
              "mx": "%x" % c["mx"], "seed": "%x" % c["seed"], "ew": c["ew"], "ints": c["ints"]}
         if "flm" in c:  # the flags the SDM defines for this form (gen_ext_vectors.py)
             e["flm"] = c["flm"]
+        for key in ("kind", "yset"):  # gen_avx2x_vectors.py: the input family and YMM overrides
+            if key in c:
+                e[key] = c[key]
         if out[k].startswith("T"):
             e["trap_mx"] = out[k].split()[1]
             traps += 1

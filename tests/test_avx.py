@@ -135,9 +135,11 @@ AVX_FAULT_CASES = [
     ([0xC5, 0xF8, 0x00, 0xC1], EXIT_FAULT, 6),              # VEX 0f 00: no AVX form
     ([0xC5, 0xF8, 0x60, 0xC1], EXIT_FAULT, 6),              # VEX.NP 0f 60: MMX only
     ([0xC5, 0xFA, 0x14, 0xC1], EXIT_FAULT, 6),              # VEX.F3 0f 14
-    ([0xC4, 0xE2, 0x79, 0xA8, 0xC1], EXIT_UNIMPLEMENTED, None),  # vfmadd213ps: FMA defined, not executed
+    ([0xC4, 0xE2, 0x79, 0x50, 0xC1], EXIT_UNIMPLEMENTED, None),  # vpdpbusd: AVX-VNNI defined, not executed
     ([0xC4, 0xE2, 0x78, 0xF2, 0xC1], RUNNING, None),        # andn (BMI1)
-    ([0xC4, 0xE2, 0x79, 0x13, 0xC1], EXIT_UNIMPLEMENTED, None),  # vcvtph2ps: F16C defined, not executed
+    ([0xC4, 0xE2, 0x79, 0x13, 0xC1], RUNNING, None),        # vcvtph2ps (F16C, U46)
+    ([0xC4, 0xE2, 0x79, 0xA8, 0xC1], RUNNING, None),        # vfmadd213ps (FMA3, U46)
+    ([0xC4, 0xE2, 0x71, 0x92, 0xC1], EXIT_FAULT, 6),        # vgatherdps with a register operand (U46)
     ([0xC4, 0xE3, 0x79, 0x44, 0xC1, 0x00], RUNNING, None),  # vpclmulqdq xmm (PCLMULQDQ)
     ([0xC4, 0xE3, 0x7D, 0x44, 0xC1, 0x00], EXIT_UNIMPLEMENTED, None),  # vpclmulqdq ymm: VPCLMULQDQ
     ([0xC4, 0xE2, 0x7D, 0xDC, 0xC1], EXIT_UNIMPLEMENTED, None),  # vaesenc ymm: VAES

@@ -487,3 +487,9 @@ def test_gpu_matches_native_ext_vectors():
     """BMI1 / BMI2 / ADX / MOVBE / CRC32, SSE4.2, AES, PCLMULQDQ (tests/golden/ext_vectors.json.gz, U45)."""
     from tests.test_ext import DOC, inputs
     _run_vector_doc(DOC, inputs, mem=True)
+
+
+def test_gpu_matches_native_avx2x_vectors():
+    """FMA3, F16C and the AVX2 gathers (tests/golden/avx2x_vectors.json.gz, U46)."""
+    from tests.test_avx2x import DOC, inputs
+    _run_vector_doc(DOC, inputs, mem=True)

@@ -61,11 +61,11 @@ __device__ __forceinline__ FEnv fenv_mx(u32 mx) {
   return FEnv{(mx >> 13) & 3, (mx >> 6) & 1, (mx >> 15) & 1, (mx >> 7) & 63, 0};
 }
 
-// w: 0 binary32 (value in the low 32 bits), 1 binary64
-__device__ __forceinline__ u32 fF(u32 w) { return w ? 52 : 23; }
-__device__ __forceinline__ i32 fEmax(u32 w) { return w ? 0x7ff : 0xff; }
-__device__ __forceinline__ i32 fBias(u32 w) { return w ? 1023 : 127; }
-__device__ __forceinline__ u32 fSb(u32 w) { return w ? 63 : 31; }
+// w: 0 binary32 (value in the low 32 bits), 1 binary64, 2 binary16 (F16C)
+__device__ __forceinline__ u32 fF(u32 w) { return w == 1 ? 52 : w == 2 ? 10 : 23; }
+__device__ __forceinline__ i32 fEmax(u32 w) { return w == 1 ? 0x7ff : w == 2 ? 0x1f : 0xff; }
+__device__ __forceinline__ i32 fBias(u32 w) { return w == 1 ? 1023 : w == 2 ? 15 : 127; }
+__device__ __forceinline__ u32 fSb(u32 w) { return w == 1 ? 63 : w == 2 ? 15 : 31; }
 __device__ __forceinline__ u32 f_sign(u64 x, u32 w) { return (u32)(x >> fSb(w)) & 1; }
 __device__ __forceinline__ i32 f_exp(u64 x, u32 w) { return (i32)((x >> fF(w)) & (u64)fEmax(w)); }
 __device__ __forceinline__ u64 f_frac(u64 x, u32 w) { return x & ((1ull << fF(w)) - 1); }
@@ -76,7 +76,7 @@ __device__ __forceinline__ bool f_inf(u64 x, u32 w) { return f_exp(x, w) == fEma
 __device__ __forceinline__ bool f_zero(u64 x, u32 w) { return f_mag(x, w) == 0; }
 __device__ __forceinline__ bool f_den(u64 x, u32 w) { return f_exp(x, w) == 0 && f_frac(x, w); }
 __device__ __forceinline__ u64 f_quiet(u64 x, u32 w) { return x | (1ull << (fF(w) - 1)); }
-__device__ __forceinline__ u64 f_indef(u32 w) { return w ? 0xfff8000000000000ull : 0xffc00000ull; }
+__device__ __forceinline__ u64 f_indef(u32 w) { return w == 1 ? 0xfff8000000000000ull : w == 2 ? 0xfe00ull : 0xffc00000ull; }
 __device__ __forceinline__ u64 f_signed(u32 s, u32 w) { return (u64)s << fSb(w); }
 __device__ __forceinline__ u64 f_infv(u32 s, u32 w) { return f_signed(s, w) | ((u64)fEmax(w) << fF(w)); }
 // DAZ reads a denormal source as a zero of its sign

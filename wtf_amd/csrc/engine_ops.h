@@ -313,7 +313,7 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
     c = ib_at(b, pos++);  // the opcode
     const bool def = !bad && vmap >= 1 && vmap <= 3 && vex_defined(vmap, c, vpp);
     if (!def || (vmap == 3 && !fp_form(3, c, vpp, true) && !s4_form(3, c, vpp, true) && !x42_form(3, c, vpp, true) &&
-                 !gx_form(3, c, vpp, true))) {  // U36: #UD from the opcode byte
+                 !gx_form(3, c, vpp, true) && !ax_form(3, c, vpp, true))) {  // U36: #UD from the opcode byte
       u.len = pos;
       u.op = (lock || !def) ? O_UD : O_UNIMPL;
       u.supported = lock || !def;
@@ -382,6 +382,8 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
   u.base = u.index = -1;
   u.scale = 0;
   u.disp = 0;
+  i32 vsib = -1;  // the SIB's raw index register (VSIB: a vector register, 4 included) and scale
+  u32 vsib_scale = 0;
   if (hasm) {
     if (pos >= 15) return 2;
     if (pos >= b.avail) return 1;
@@ -397,6 +399,8 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
         if (pos >= b.avail) return 1;
         const u32 sib = ib_at(b, pos++);
         const u32 idx = ((sib >> 3) & 7) | (rexx << 3), base = sib & 7;
+        vsib = (i32)idx;
+        vsib_scale = sib >> 6;
         if (idx != 4) {
           u.index = (i32)idx;
           u.scale = sib >> 6;
@@ -498,6 +502,10 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
     }
   }
   if (u.op == O_ALU && u.sub == 7) u.awrite = 0;  // cmp reads its destination, never writes it
+  if (vex && smap == 2 && vpp == 1 && c >= 0x90 && c <= 0x93) {  // gathers (engine_avx2x.h): index -1 = no SIB
+    u.index = vsib;
+    u.scale = vsib_scale;
+  }
   if (map2) {
     const u32 gpc = vex ? vpp : (u.rep == 0xf3 ? 2 : u.rep == 0xf2 ? 3 : p66 ? 1 : 0);
     if (u.op == O_SSE && smap >= 2 && gx_form(smap, c, gpc, vex != 0)) {  // engine_ext.h (U45)

@@ -29,6 +29,7 @@ namespace wtfgpu_dev {
 
 __host__ __device__ inline bool s4_form(u32 map, u32 c, u32 pp, bool vex);  // engine_sse4.h
 __host__ __device__ inline bool x42_form(u32 map, u32 c, u32 pp, bool vex);  // engine_ext.h
+__host__ __device__ inline u32 ax_form(u32 map, u32 c, u32 pp, bool vex);    // engine_avx2x.h
 struct UOp;
 __device__ __noinline__ int x42_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next);
 
@@ -164,8 +165,8 @@ __host__ __device__ inline bool legacy_3byte_defined(u32 map, u32 op, u32 pfx) {
 }
 
 __device__ __forceinline__ bool vex_valid(u32 map, u32 c, u32 pp, u32 is_mem, u32 r3) {
-  if (fp_form(map, c, pp, true) || s4_form(map, c, pp, true) || x42_form(map, c, pp, true))
-    return true;  // engine_ssefp.h, engine_sse4.h, engine_ext.h
+  if (fp_form(map, c, pp, true) || s4_form(map, c, pp, true) || x42_form(map, c, pp, true) || ax_form(map, c, pp, true))
+    return true;  // engine_ssefp.h, engine_sse4.h, engine_ext.h, engine_avx2x.h
   if (map == 2) return pp == 1 && (c == 0x00 || c == 0x17 || c == 0x58 || c == 0x59 || c == 0x78 || c == 0x79);
   if (map != 1) return false;
   if (c == 0x77) return pp == 0;
@@ -432,6 +433,7 @@ __device__ __noinline__ int vex_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
 }  // namespace wtfgpu_dev
 #include "engine_ssefp.h"  // SSE / AVX floating point: fp_exec
 #include "engine_sse4.h"  // SSSE3 / SSE4.1 integer, AVX2 lane-crossing: s4_exec
+#include "engine_avx2x.h"  // FMA3, F16C, AVX2 gathers: ax_exec
 namespace wtfgpu_dev {
 
 // ---------------------------------------------------------------- MMX (U37)
@@ -755,6 +757,7 @@ __device__ __noinline__ int vex_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
   if (fp_form(map, c, pp, true)) return fp_exec(P, L, u, nrip, next);  // its own VEX checks
   if (s4_form(map, c, pp, true)) return s4_exec(P, L, u, nrip, next);
   if (x42_form(map, c, pp, true)) return x42_exec(P, L, u, nrip, next);  // its own VEX checks
+  if (ax_form(map, c, pp, true)) return ax_exec(P, L, u, nrip, next);    // its own VEX checks
   const u32 l256 = (x >> 1) & 1, w = (x >> 2) & 1, vvvv = (x >> 4) & 15;
   const bool mem = u.is_mem;
   const u32 imm = (u32)u.imm & 0xff;

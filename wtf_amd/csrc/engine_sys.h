@@ -129,9 +129,9 @@ __device__ __noinline__ void cpuid_leaf(u64 cr4, u64 xcr0, u32 leaf, u32 sub, u3
   } else if (leaf == 1) {
     r[0] = 0x000906ea;
     r[1] = 0x00000800;
-    // SSE3, PCLMULQDQ, SSSE3, CX16, SSE4.1, SSE4.2, MOVBE, POPCNT, AES, XSAVE, OSXSAVE, AVX, RDRAND
-    r[2] = (1u << 0) | (1u << 1) | (1u << 9) | (1u << 13) | (1u << 19) | (1u << 20) | (1u << 22) | (1u << 23) |
-           (1u << 25) | (1u << 26) | (osxsave << 27) | (1u << 28) | (1u << 30);
+    // SSE3, PCLMULQDQ, SSSE3, FMA, CX16, SSE4.1, SSE4.2, MOVBE, POPCNT, AES, XSAVE, OSXSAVE, AVX, F16C, RDRAND
+    r[2] = (1u << 0) | (1u << 1) | (1u << 9) | (1u << 12) | (1u << 13) | (1u << 19) | (1u << 20) | (1u << 22) |
+           (1u << 23) | (1u << 25) | (1u << 26) | (osxsave << 27) | (1u << 28) | (1u << 29) | (1u << 30);
     r[3] = 0x078bfbfd;
   } else if (leaf == 7) {
     if (sub == 0) r[1] = (1u << 0) | (1u << 3) | (1u << 5) | (1u << 8) | (1u << 9) | (1u << 19);  // FSGSBASE BMI1 AVX2 BMI2 ERMS ADX
