@@ -54,8 +54,10 @@ int gpr_index(Registers_t r) {
 
 GpuBackend_t::GpuBackend_t() = default;
 GpuBackend_t::~GpuBackend_t() {
-  for (Part &P : parts_)
+  for (Part &P : parts_) {
     if (P.pin) wtfgpu_host_free(ctx_, P.pin);
+    if (P.ex) wtfgpu_host_free(ctx_, P.ex);
+  }
   if (wpin_) wtfgpu_host_free(ctx_, wpin_);
   if (ctx_) wtfgpu_destroy(ctx_);
 }
@@ -730,7 +732,7 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
 // action that could not write its chunk (WTFGPU_EXIT_FEED_FAULT) is the
 // module handler's failed VirtWriteDirty (fuzzer_tlv_server.cc:130-158): a
 // handler fault, the testcase an engine error (U43).
-bool GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first, const std::vector<wtfgpu_exit_t> &ex,
+bool GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first, const wtfgpu_exit_t *ex,
                             std::vector<uint8_t> &done, std::vector<LaneResult> *out, std::vector<uint32_t> &hits) {
   std::vector<uint8_t> hit(pending.size(), 0);
   HostPool::Get().For(pending.size(), 1024, [&](size_t pi) {
@@ -801,7 +803,7 @@ bool GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first
 // Final state of every finished lane (`ex` holds the last round's exits of
 // every lane: a lane is final once it is done).
 bool GpuBackend_t::fill_results(const std::vector<uint32_t> &lanes, uint32_t first,
-                                const std::vector<wtfgpu_exit_t> &ex, const std::vector<uint8_t> &done,
+                                const wtfgpu_exit_t *ex, const std::vector<uint8_t> &done,
                                 std::vector<LaneResult> *out, std::vector<uint32_t> *finished) {
   const auto tg = Clock::now();
   std::vector<uint32_t> fin;
@@ -884,7 +886,7 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
     account_run(rs);
     if (wtfgpu_read_exits(ctx_, first, count, ex.data())) return false;
     std::vector<uint32_t> hits;
-    if (!classify(pending, first, ex, done, out, hits)) return false;
+    if (!classify(pending, first, ex.data(), done, out, hits)) return false;
     stats_.exits_ms += ms_since(te);
     if (hits.empty()) break;
     if (!service_hits(hits, first, done, slots, per_lane_state)) return false;
@@ -892,7 +894,7 @@ bool GpuBackend_t::run_lanes(const std::vector<uint32_t> &lanes, std::vector<Lan
     for (uint32_t l : hits)
       if (!done[l - first]) pending.push_back(l);
   }
-  return fill_results(lanes, first, ex, done, out, nullptr);
+  return fill_results(lanes, first, ex.data(), done, out, nullptr);
 }
 
 void GpuBackend_t::account_run(const wtfgpu_run_stats_t &rs) {
@@ -1591,8 +1593,16 @@ bool GpuBackend_t::harvest_part(Part &P, const Target_t &Target, std::vector<Str
     r.rip = 0;
     r.new_coverage.clear();
   }, P.occ.size() >= 8192);
-  if (P.ex.size() < count) P.ex.resize(count);
-  if (wtfgpu_read_exits(ctx_, first, count, P.ex.data())) return false;
+  if (P.ex_cap < count) {
+    if (P.ex) wtfgpu_host_free(ctx_, P.ex);
+    P.ex = nullptr;
+    P.ex_cap = 0;
+    void *p = nullptr;
+    if (wtfgpu_host_alloc(ctx_, (uint64_t)count * sizeof(wtfgpu_exit_t), &p)) return false;
+    P.ex = (wtfgpu_exit_t *)p;
+    P.ex_cap = count;
+  }
+  if (wtfgpu_read_exits(ctx_, first, count, P.ex)) return false;
   std::vector<uint8_t> done(count, 0);
   std::vector<uint32_t> hits;
   if (!classify(P.occ, first, P.ex, done, &lres_, hits)) return false;

@@ -215,9 +215,9 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   // until every lane has a result
   bool run_lanes(const std::vector<uint32_t> &lanes, std::vector<LaneResult> *out, ModuleSlots *slots,
                  bool per_lane_state);
-  bool classify(const std::vector<uint32_t> &pending, uint32_t first, const std::vector<wtfgpu_exit_t> &ex,
+  bool classify(const std::vector<uint32_t> &pending, uint32_t first, const wtfgpu_exit_t *ex,
                 std::vector<uint8_t> &done, std::vector<LaneResult> *out, std::vector<uint32_t> &hits);
-  bool fill_results(const std::vector<uint32_t> &lanes, uint32_t first, const std::vector<wtfgpu_exit_t> &ex,
+  bool fill_results(const std::vector<uint32_t> &lanes, uint32_t first, const wtfgpu_exit_t *ex,
                     const std::vector<uint8_t> &done, std::vector<LaneResult> *out, std::vector<uint32_t> *finished);
   bool stop_prestopped(const std::vector<uint32_t> &lanes);
   void account_run(const wtfgpu_run_stats_t &rs);
@@ -250,7 +250,8 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
     uint32_t lo = 0, hi = 0;
     bool launched = false;
     std::vector<uint32_t> occ;
-    std::vector<wtfgpu_exit_t> ex;
+    wtfgpu_exit_t *ex = nullptr;  // the slice's exit records: pinned (one DMA of 40 B per lane)
+    uint64_t ex_cap = 0;
     uint8_t *pin = nullptr;
     uint64_t pin_cap = 0;
   };
