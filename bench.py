@@ -155,7 +155,29 @@ def load_pmc(name: str, lanes: int, limit: int) -> dict | None:
     return pmc
 
 
-def roofline(alg_bytes: float, launches: float, kernel_ms: float, pmc: dict | None) -> dict:
+SIMDS = 256 * 4        # MI355X_MICROARCH.md: 256 CUs x 4 SIMDs
+CLOCK_HZ = 2.4e9       # MI355X_MICROARCH.md: max clock 2400 MHz
+
+
+def issue_roofline(pmc: dict | None, avg_s: float, steps_per_launch: float, retired_per_launch: float) -> dict | None:
+    """The bound that binds k_run (latency and issue, not HBM): wave
+    instructions issued per launch (the PMC summary's SQ_INSTS_* mix) against
+    the sequencer's ceiling of one instruction per SIMD per cycle, plus the
+    same count per wave-step and per lane-retired guest instruction."""
+    mix = (pmc or {}).get("instruction_mix_per_launch")
+    if not mix or avg_s <= 0:
+        return None
+    insts = sum(v for k, v in mix.items() if k.startswith("SQ_INSTS_"))
+    achieved = insts / (SIMDS * CLOCK_HZ * avg_s)
+    return {"unit": "wave instructions / SIMD-cycle", "achieved": achieved, "peak": 1.0, "frac": achieved,
+            "insts_per_launch": insts,
+            "per_wave_step": insts / steps_per_launch if steps_per_launch else None,
+            "per_retired_instr": insts / retired_per_launch if retired_per_launch else None,
+            "salu_valu_branch": [mix.get("SQ_INSTS_SALU"), mix.get("SQ_INSTS_VALU"), mix.get("SQ_INSTS_BRANCH")]}
+
+
+def roofline(alg_bytes: float, launches: float, kernel_ms: float, pmc: dict | None, steps: float = 0,
+             retired: float = 0) -> dict:
     avg_s = kernel_ms / 1e3 / max(1.0, launches)
     per_launch = alg_bytes / max(1.0, launches)
     achieved = per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
@@ -163,7 +185,8 @@ def roofline(alg_bytes: float, launches: float, kernel_ms: float, pmc: dict | No
             "frac": achieved / HBM_PEAK_GBS, "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
             "kernel": "k_run", "alg_bytes_per_launch": per_launch, "avg_launch_ms": avg_s * 1e3,
             "valu_util": pmc.get("valu_util") if pmc else None,
-            "wait_frac": pmc.get("wait_frac") if pmc else None}
+            "wait_frac": pmc.get("wait_frac") if pmc else None,
+            "issue": issue_roofline(pmc, avg_s, steps / max(1.0, launches), retired / max(1.0, launches))}
 
 
 # ----------------------------------------------------------------- CPU baselines
@@ -288,7 +311,8 @@ def hevd_leg(base: str, lanes: int, limit: int, seconds: float, flags=()) -> dic
             "unique_crashes": g["unique_crashes"], "coverage": g["coverage"], "errors": g["errors"],
             "gpu_retired_fraction": (g["retired"] - g["error_retired"]) / max(1, g["retired"]),
             "lanes_per_wave_step": g["retired"] / max(1, b["group_steps"]),
-            "roofline": roofline(b["alg_bytes"], b["kernel_launches"], b["kernel_ms"], pmc), "backend": b,
+            "roofline": roofline(b["alg_bytes"], b["kernel_launches"], b["kernel_ms"], pmc, b["group_steps"],
+                                 g["retired"]), "backend": b,
             "kernel_busy_frac": b["kernel_ms"] / (g["wall_s"] * 1e3),
             "note": "the HEVD look-alike's IOCTL path is ~300 instructions per exec: no IO manager (SURVEY F3), so "
                     "this leg says little about a real HEVD snapshot's throughput",
@@ -344,7 +368,8 @@ def syn_leg(lanes: int, limit: int, steps: int, device: int) -> dict:
             "instr_per_s": acc["retired"] / dt, "instr_per_exec": acc["retired"] / max(1, acc["execs"]),
             "ms_per_step": dt * 1e3 / steps, "lanes_per_wave_step": acc["retired"] / max(1, acc["steps"]),
             "gpu_retired_fraction": 1.0,
-            "roofline": roofline(acc["bytes"], acc["launches"], acc["kernel_ms"], load_pmc("syn", lanes, limit))}
+            "roofline": roofline(acc["bytes"], acc["launches"], acc["kernel_ms"], load_pmc("syn", lanes, limit),
+                                 acc["steps"], acc["retired"])}
 
 
 def main():
@@ -445,7 +470,7 @@ def run(a, rank, world, local, tmp):
             "build": {"engine_sha16": engine_sha16()},
             "instr_per_exec": retired / max(1.0, execs),
             "roofline": roofline(fields["alg_bytes"], fields["kernel_launches"], fields["kernel_ms"],
-                                 load_pmc("tlv", a.lanes, a.limit)),
+                                 load_pmc("tlv", a.lanes, a.limit), fields["group_steps"], retired),
             **{k: fields[k] for k in ("lanes_per_wave_step", "gpu_retired_fraction")},
             "node": {k: v for k, v in fields.items() if k not in ("lanes_per_wave_step", "gpu_retired_fraction")},
             "coverage": summary["coverage"], "unique_crashes": summary["unique_crashes"],
