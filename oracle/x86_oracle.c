@@ -1947,7 +1947,7 @@ static int vex_valid(u32 map, u32 op, int pp, int mem, u32 r3) {
 /* U36 / U45: which encodings some x86-64 CPU defines (SDM vol. 2 appendix A
  * and the extension references). The emulated CPU enumerates and executes
  * SSE .. SSE4.2, SSSE3, AVX, AVX2, AES, PCLMULQDQ, BMI1 / BMI2, ADX and MOVBE;
- * the other defined forms (FMA, F16C, AVX-VNNI / -IFMA / -NE-CONVERT /
+ * the other defined forms (AVX-VNNI / -IFMA / -NE-CONVERT /
  * -VNNI-INT8 / -INT16, GFNI, the 256-bit VAES / VPCLMULQDQ, SHA, CET shadow
  * stack writes, MOVDIRI / MOVDIR64B, ENQCMD, Key Locker, INVEPT / INVVPID /
  * INVPCID, EVEX) are UNIMPLEMENTED: a guest chooses its code from the capture

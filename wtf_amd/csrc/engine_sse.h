@@ -91,7 +91,7 @@ __device__ __forceinline__ bool sse_valid(u32 map, u32 c, u32 pc, u32 is_mem, u3
 }
 // U36: the encodings some x86-64 CPU defines. Those the engine
 // executes are what cpuid_leaf enumerates (SSE .. SSE4.2, SSSE3, AVX, AVX2,
-// AES, PCLMULQDQ, BMI1 / BMI2, ADX, MOVBE); the other defined ones (FMA, F16C,
+// AES, PCLMULQDQ, BMI1 / BMI2, ADX, MOVBE, FMA, F16C); the other defined ones (
 // AVX-VNNI, AVX-IFMA, AVX-NE-CONVERT, GFNI, VAES / VPCLMULQDQ's 256-bit forms,
 // SHA, CET, MOVDIR*, ENQCMD, Key Locker, EVEX, ...) are UNIMPLEMENTED (U45: a
 // guest picks its paths from the capture host's CPUID, so they are an engine

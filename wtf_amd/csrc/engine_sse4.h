@@ -5,8 +5,8 @@
 // by engine_sse.h; sse_exec / vex_exec hand every form s4_form() accepts to
 // s4_exec.
 //
-// Outside (UNIMPLEMENTED): the SSSE3 MMX-register forms, mpsadbw, vmaskmov /
-// vpmaskmov and the gathers (masked element accesses).
+// Outside (UNIMPLEMENTED): the SSSE3 MMX-register forms (the gathers are in
+// engine_avx2x.h).
 #pragma once
 #include "engine_fp.h"
 
