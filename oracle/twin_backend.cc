@@ -483,9 +483,30 @@ int main(int argc, char **argv) {
     bool LaneTrace(uint32_t L, std::vector<uint64_t> &R, bool &T) override { return b->LaneTrace(L, R, T); }
     bool EnableTenet(uint64_t P) override { return b->EnableTenet(P); }
     bool LaneTenet(uint32_t L, std::vector<uint8_t> &R, bool &T) override { return b->LaneTenet(L, R, T); }
+    // WTF_TWIN_STREAM=1: the streaming interface of the gpu node (continuous
+    // batching), served synchronously (every lane free at every step, each
+    // step's testcases run to their end), so the CPU tests drive the fuzz
+    // loop's streaming bookkeeping (runner.cc FuzzSession::StreamStep)
+    bool stream = false;
+    std::vector<LaneResult> res;  // the last step's results (valid until the next step)
+    bool CanStream() const override { return stream; }
+    uint32_t FreeLanes() const override { return n; }
+    bool StreamStep(const Target_t &T, const std::vector<StreamTestcase_t> &In, uint64_t,
+                    std::vector<StreamResult_t> &Out, ModuleSlots *S, size_t *Taken) override {
+      const size_t k = std::min<size_t>(In.size(), n);
+      if (Taken) *Taken = k;
+      std::vector<std::pair<const uint8_t *, size_t>> Tc(k);
+      for (size_t i = 0; i < k; i++) Tc[i] = {In[i].data, In[i].size};
+      Out.clear();
+      if (k == 0) return true;
+      if (!b->RunBatch(T, Tc, res, S)) return false;
+      for (size_t i = 0; i < k; i++) Out.push_back(StreamResult_t{In[i].tag, &res[i]});
+      return true;
+    }
   } E;
   E.b = B;
   E.n = O.lanes ? O.lanes : 1;
+  E.stream = getenv("WTF_TWIN_STREAM") && getenv("WTF_TWIN_STREAM")[0] == '1';
   // CPU shards merge their host coverage maps over TCP (net_exchange.cc)
   std::unique_ptr<TcpExchange_t> X;
   if (O.world > 1) {

@@ -1959,17 +1959,24 @@ __global__ void k_cov_merge_in(uint4 *map, const uint4 *src, u64 n16) {
 
 // Per-lane feed regions (streaming): `n` lanes, lane lanes[i] gets
 // len[i] bytes from src + off[i] at its region.
-__global__ void k_feed_scatter(u8 *feed, u64 stride, const u32 *lanes, const u64 *off, const u64 *len, u32 n,
-                               const u8 *src, u64 *feed_pos, u64 *feed_end, const u64 *pos, const u64 *end) {
+// Lane i's feed: bytes [off[i], off[i + 1]) of src into the lane's region, its
+// read position and end set; a lane without a feed (has[i] = 0) or with one
+// larger than its region keeps none (the host handler serves it).
+__global__ void k_feed_scatter(u8 *feed, u64 stride, const u32 *lanes, const u64 *off, const u8 *has, u32 n,
+                               const u8 *src, u64 *feed_pos, u64 *feed_end) {
   const u32 i = blockIdx.x;
   if (i >= n) return;
+  const u32 lane = lanes[i];
+  const u64 o = off[i], len = off[i + 1] - o;
+  const bool keep = (!has || has[i]) && len <= stride;
   if (threadIdx.x == 0) {
-    feed_pos[lanes[i]] = pos[i];
-    feed_end[lanes[i]] = end[i];
+    feed_pos[lane] = keep ? (u64)lane * stride : ~0ull;
+    feed_end[lane] = keep ? (u64)lane * stride + len : 0;
   }
-  u8 *dst = feed + (u64)lanes[i] * stride;
-  const u8 *s = src + off[i];
-  for (u64 k = threadIdx.x; k < len[i]; k += blockDim.x) dst[k] = s[k];
+  if (!keep) return;
+  u8 *dst = feed + (u64)lane * stride;
+  const u8 *sp = src + o;
+  for (u64 k = threadIdx.x; k < len; k += blockDim.x) dst[k] = sp[k];
 }
 
 __global__ void k_cov_commit(Dev P, const u64 *rips, u64 n) {
@@ -2853,8 +2860,12 @@ int wtfgpu_restore_lanes(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n) {
 int wtfgpu_set_feed_lanes(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, const uint64_t *offsets,
                           const uint8_t *has_feed, const uint8_t *bytes, uint64_t nbytes) {
   if (!c || !c->d_gpr || (n && (!lanes || !offsets)) || (nbytes && !bytes)) return WTFGPU_ERR_INVALID;
-  for (u32 i = 0; i < n; i++)
-    if (lanes[i] >= c->P.nlanes || offsets[i + 1] < offsets[i] || offsets[i + 1] > nbytes) return WTFGPU_ERR_INVALID;
+  {  // one branch-light pass: lanes in range, offsets ascending within the bytes
+    u32 bad = 0;
+    for (u32 i = 0; i < n; i++)
+      bad |= (u32)(lanes[i] >= c->P.nlanes) | (u32)(offsets[i + 1] < offsets[i]) | (u32)(offsets[i + 1] > nbytes);
+    if (bad) return WTFGPU_ERR_INVALID;
+  }
   if (n == 0) return WTFGPU_OK;
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -2873,36 +2884,22 @@ int wtfgpu_set_feed_lanes(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, cons
     c->feed_cap = N * stride;
     c->feed_stride = stride;
   }
-  const u64 S = c->feed_stride;
-  std::vector<u64> pos(n), end(n), off(n), len(n);
-  for (u32 i = 0; i < n; i++) {
-    const u64 L = offsets[i + 1] - offsets[i];
-    const bool has = (!has_feed || has_feed[i]) && L <= S;  // a feed too big for its region: host handler
-    off[i] = offsets[i];
-    len[i] = has ? L : 0;
-    pos[i] = has ? (u64)lanes[i] * S : ~0ull;
-    end[i] = has ? (u64)lanes[i] * S + L : 0;
-  }
-  // one staging upload of the lane metadata (lanes | off | len | pos | end),
-  // one of the bytes (straight from the caller's buffer: pinned memory DMAs),
-  // then one scatter
-  const u64 a8 = ((u64)n * 8 + 255) & ~255ull;
-  const u64 o_off = ((u64)n * 4 + 255) & ~255ull, o_len = o_off + a8, o_pos = o_len + a8, o_end = o_pos + a8,
-            o_data = o_end + a8;
+  // one staging upload of the lane list, the offsets and the flags (the
+  // scatter derives each lane's length, position and end), one of the bytes
+  // (straight from the caller's buffer: pinned memory DMAs), then one scatter
+  const u64 o_off = ((u64)n * 4 + 255) & ~255ull, o_has = (o_off + (u64)(n + 1) * 8 + 255) & ~255ull,
+            o_data = (o_has + n + 255) & ~255ull;
   if (ensure_scratch(c, o_data + nbytes)) return WTFGPU_ERR_OOM;
   if (ensure_stage(c, o_data)) return WTFGPU_ERR_OOM;
   u8 *stage = c->h_stage;
   memcpy(stage, lanes, (u64)n * 4);
-  memcpy(stage + o_off, off.data(), (u64)n * 8);
-  memcpy(stage + o_len, len.data(), (u64)n * 8);
-  memcpy(stage + o_pos, pos.data(), (u64)n * 8);
-  memcpy(stage + o_end, end.data(), (u64)n * 8);
+  memcpy(stage + o_off, offsets, (u64)(n + 1) * 8);
+  if (has_feed) memcpy(stage + o_has, has_feed, n);
   HIPCHK(hipMemcpyAsync(c->d_scratch, stage, o_data, hipMemcpyHostToDevice, c->stream));
   if (nbytes) HIPCHK(hipMemcpyAsync(c->d_scratch + o_data, bytes, nbytes, hipMemcpyHostToDevice, c->stream));
-  k_feed_scatter<<<n, 256, 0, c->stream>>>(c->d_feeddata, S, (const u32 *)c->d_scratch,
-                                           (const u64 *)(c->d_scratch + o_off), (const u64 *)(c->d_scratch + o_len), n,
-                                           c->d_scratch + o_data, c->d_feedpos, c->d_feedend,
-                                           (const u64 *)(c->d_scratch + o_pos), (const u64 *)(c->d_scratch + o_end));
+  k_feed_scatter<<<n, 128, 0, c->stream>>>(c->d_feeddata, c->feed_stride, (const u32 *)c->d_scratch,
+                                           (const u64 *)(c->d_scratch + o_off), has_feed ? c->d_scratch + o_has : nullptr,
+                                           n, c->d_scratch + o_data, c->d_feedpos, c->d_feedend);
   HIPCHK(hipGetLastError());
   // no wait: the queue's later work (its k_run slice) is ordered after the
   // scatter, and the next call on this queue synchronises first

@@ -861,9 +861,12 @@ bool GpuBackend_t::fill_results(const std::vector<uint32_t> &lanes, uint32_t fir
 // Lanes InsertTestcase stopped never run: marked STOPPED on the device, so
 // the next classification gives them their result.
 bool GpuBackend_t::stop_prestopped(const std::vector<uint32_t> &lanes) {
+  std::vector<uint8_t> has(lanes.size());
+  HostPool::Get().For(lanes.size(), 1024, [&](size_t i) { has[i] = views_[lanes[i]].result.has_value(); },
+                      lanes.size() >= 4096);
   std::vector<uint32_t> pre;
-  for (uint32_t l : lanes)
-    if (views_[l].result) pre.push_back(l);
+  for (size_t i = 0; i < lanes.size(); i++)
+    if (has[i]) pre.push_back(lanes[i]);
   return pre.empty() || wtfgpu_stop(ctx_, pre.data(), (uint32_t)pre.size(), WTFGPU_EXIT_STOPPED) == WTFGPU_OK;
 }
 
@@ -1352,8 +1355,13 @@ void GpuBackend_t::collect_coverage(const std::vector<uint32_t> &lanes, std::vec
     cov_ovf_warned_ = true;
     fprintf(stderr, "wtfgpu: a lane's new-coverage set filled up (rips lost); raise the set size\n");
   }
-  std::unordered_map<uint32_t, std::vector<uint64_t>> per;
-  for (uint64_t i = 0; i < total; i++) per[cl[i]].push_back(cr[i]);
+  // the entries come back in no order: sorted by (lane, rip) and unique, each
+  // lane's set is one run, found by binary search in the order given
+  std::vector<std::pair<uint32_t, uint64_t>> &ent = cov_sorted_;
+  ent.resize(total);
+  for (uint64_t i = 0; i < total; i++) ent[i] = {cl[i], cr[i]};
+  std::sort(ent.begin(), ent.end());
+  ent.erase(std::unique(ent.begin(), ent.end()), ent.end());
   if (getenv("WTFGPU_COVLOG_TOP")) {  // diagnostic: which logged values keep coming back
     for (uint64_t i = 0; i < total; i++) covlog_count_[cr[i]]++;
     if (++covlog_calls_ % 64 == 0) {
@@ -1368,23 +1376,30 @@ void GpuBackend_t::collect_coverage(const std::vector<uint32_t> &lanes, std::vec
   }
   std::vector<uint64_t> fresh;
   last_new_coverage_.clear();
-  for (uint32_t l : lanes) {
-    auto it = per.find(l);
-    if (it == per.end()) continue;
-    std::vector<uint64_t> &v = it->second;
-    std::sort(v.begin(), v.end());
-    v.erase(std::unique(v.begin(), v.end()), v.end());
-    if (full_coverage_) {  // parity mode: the lane's whole rip set, nothing committed
-      res[l].new_coverage = v;
-      continue;
-    }
+  // one lane's run of entries, attributed against the aggregate (lanes in order)
+  auto attribute = [&](uint32_t l, size_t at) {
     const bool revoke = std::holds_alternative<Timedout_t>(res[l].result);
-    for (uint64_t rip : v) {
+    for (; at < ent.size() && ent[at].first == l; at++) {
+      const uint64_t rip = ent[at].second;
+      if (full_coverage_) {  // parity mode: the lane's whole rip set, nothing committed
+        res[l].new_coverage.push_back(rip);
+        continue;
+      }
       if (aggregate_.count(rip)) continue;
       res[l].new_coverage.push_back(rip);
       if (revoke) continue;
       aggregate_.insert(rip);
       fresh.push_back(rip);
+    }
+    return at;
+  };
+  if (std::is_sorted(lanes.begin(), lanes.end())) {
+    // the entries' lane order is the given order: one pass over the runs
+    for (size_t at = 0; at < ent.size();) at = attribute(ent[at].first, at);
+  } else {
+    for (uint32_t l : lanes) {
+      const auto it = std::lower_bound(ent.begin(), ent.end(), std::pair<uint32_t, uint64_t>{l, 0});
+      if (it != ent.end() && it->first == l) attribute(l, (size_t)(it - ent.begin()));
     }
   }
   commit_fresh(fresh);
@@ -1512,11 +1527,12 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
       const size_t n = fresh.size();
       std::vector<uint64_t> off(n + 1, 0);
       std::vector<uint8_t> has(n);
-      for (size_t i = 0; i < n; i++) {
+      HostPool::Get().For(n, 1024, [&](size_t i) {  // the views are scattered: read them on all threads
         const LaneView &v = views_[fresh[i]];
-        off[i + 1] = off[i] + v.feed_size();
+        off[i + 1] = v.feed_size();
         has[i] = v.has_feed;
-      }
+      });
+      for (size_t i = 0; i < n; i++) off[i + 1] += off[i];
       // packed into the part's pinned buffer on all host threads: one DMA
       if (off[n] > P.pin_cap) {
         if (P.pin) wtfgpu_host_free(ctx_, P.pin);

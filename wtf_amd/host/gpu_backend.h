@@ -239,6 +239,7 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   std::vector<uint8_t> lres_stale_;  // lres_[l] still holds a handed-out result: reset at the lane's next harvest
   std::vector<uint32_t> cov_lanes_;  // coverage collection buffers (streaming)
   std::vector<uint64_t> cov_rips_;
+  std::vector<std::pair<uint32_t, uint64_t>> cov_sorted_;  // the same, sorted by (lane, rip)
   bool cov_ovf_warned_ = false;
   bool want_gprs_ = true;
   uint64_t last_icount_ = 0;  // of the last Run

@@ -728,7 +728,7 @@ TcBatch FuzzSession::MakeBatch(uint64_t n) {
   TcBatch Batch;
   size_t Made = 0;
   auto Tail = [&]() -> TcArena & {
-    if (Batch.empty()) Batch.push_back(std::make_unique<TcArena>());
+    if (Batch.empty()) Batch.push_back(NewArena());
     return *Batch.back();
   };
   while (Made < n && !Pending_.empty()) {
@@ -757,7 +757,7 @@ TcBatch FuzzSession::MakeBatch(uint64_t n) {
         // the master mutator's cross-over partner (the last new-coverage
         // testcase) is every chunk mutator's too
         if (HaveNewCov_) M->OnNewCoverage(Testcase_t((const uint8_t *)LastNewCov_.data(), LastNewCov_.size()));
-        auto A = std::make_unique<TcArena>();
+        auto A = NewArena();
         const size_t End = std::min(Need, (c + 1) * kMutateChunk);
         A->Off.reserve(End - c * kMutateChunk + 1);
         std::vector<uint8_t> Scratch;
@@ -777,7 +777,7 @@ TcBatch FuzzSession::MakeBatch(uint64_t n) {
     MutateCpuNs_ += CpuNs.load();
     for (std::unique_ptr<TcArena> &A : Out) Batch.push_back(std::move(A));
     Made += Need;
-    Batch.push_back(std::make_unique<TcArena>());  // the serial tail below
+    Batch.push_back(NewArena());  // the serial tail below
   }
   while (Made < n) {
     if (Corpus_.Size() == 0 && Made == 0) break;
@@ -864,27 +864,31 @@ bool FuzzSession::StreamStep(bool Done) {
       Adopt(MakeBatch(Budget(free - Ready_.size())));
       S_.make_ms += secs_since(tm) * 1e3;
     }
+    // the next `take` ready testcases, each in a free slot (its tag): taken in
+    // bulk, the slots and the executor's descriptors filled on all host threads
     const size_t take = std::min<size_t>(free, Ready_.size());
-    In.reserve(take);
-    for (size_t i = 0; i < take; i++) {
-      if (FreeSlot_.empty()) {
-        FreeSlot_.push_back(Slot_.size());
-        Slot_.emplace_back();
-      }
-      const uint64_t tag = FreeSlot_.back();
-      FreeSlot_.pop_back();
-      const TcRef R = Ready_.front();
-      Ready_.pop_front();
+    while (FreeSlot_.size() < take) {
+      FreeSlot_.push_back(Slot_.size());
+      Slot_.emplace_back();
+    }
+    const size_t base = FreeSlot_.size() - take;
+    std::vector<TcRef> Refs(Ready_.begin(), Ready_.begin() + (std::ptrdiff_t)take);
+    Ready_.erase(Ready_.begin(), Ready_.begin() + (std::ptrdiff_t)take);
+    In.resize(take);
+    HostPool::Get().For(take, 1024, [&](size_t i) {
+      const uint64_t tag = FreeSlot_[base + i];
+      const TcRef R = Refs[i];
       Slot_[tag] = R;
-      InFlight_++;
       StreamTestcase_t T{R.data(), R.size(), tag};
       if (R.A->Prep.size() == R.A->Count()) {
         T.prep = R.prep();
         T.prep_data = R.prep_data();
         T.prep_size = R.prep_size();
       }
-      In.push_back(T);
-    }
+      In[i] = T;
+    }, take >= 4096);
+    FreeSlot_.resize(base);
+    InFlight_ += take;
     const uint64_t want = Budget(Exec_.Lanes() > Ready_.size() ? Exec_.Lanes() - Ready_.size() : 0);
     if (want && Corpus_.Size() && !Next_.valid())
       Next_ = std::async(std::launch::async, &FuzzSession::MakeBatch, this, want);
@@ -910,26 +914,114 @@ bool FuzzSession::StreamStep(bool Done) {
   S_.batches++;
   for (const StreamResult_t &F : Out)
     if (F.tag >= Slot_.size()) return false;
-  // crash names already seen, looked up on all host threads (read-only) so
-  // that the serial bookkeeping below only hashes the new ones
-  std::vector<uint8_t> Known(Out.size(), 0);
-  HostPool::Get().For(Out.size(), 512, [&](size_t i) {
-    if (const Crash_t *C = std::get_if<Crash_t>(&Out[i].r->result))
-      Known[i] = !Out[i].r->error && CrashNames_.count(C->CrashName) != 0;
-  }, Out.size() >= 4096);
-  for (size_t i = 0; i < Out.size(); i++) {
-    StreamResult_t &F = Out[i];
-    const TcRef R = Slot_[F.tag];
-    Account(R.data(), R.size(), *F.r, Known[i]);
-    if (--R.A->Live == 0) Arenas_.erase(R.A);  // every testcase of the arena accounted
-    Slot_[F.tag] = TcRef{};
-    FreeSlot_.push_back(F.tag);
-    InFlight_--;
-  }
+  AccountStep(Out);
   S_.account_ms += secs_since(ta) * 1e3;
   if (X_ && X_->World() > 1 && !MergeCoverage(false)) return false;
   S_.step_ms += secs_since(t_step) * 1e3;
   return true;
+}
+
+std::unique_ptr<TcArena> FuzzSession::NewArena() {
+  {
+    std::lock_guard<std::mutex> g(ArenaPoolMu_);
+    if (!ArenaPool_.empty()) {
+      std::unique_ptr<TcArena> A = std::move(ArenaPool_.back());
+      ArenaPool_.pop_back();
+      return A;
+    }
+  }
+  return std::make_unique<TcArena>();
+}
+
+void FuzzSession::ReleaseArena(TcArena *A) {
+  auto it = Arenas_.find(A);
+  if (it == Arenas_.end()) return;
+  std::unique_ptr<TcArena> Own = std::move(it->second);
+  Arenas_.erase(it);
+  Own->Data.clear();
+  Own->Off.assign(1, 0);
+  Own->Live = 0;
+  Own->Prep.clear();
+  Own->PrepData.clear();
+  Own->PrepOff.assign(1, 0);
+  std::lock_guard<std::mutex> g(ArenaPoolMu_);
+  if (ArenaPool_.size() < 512) ArenaPool_.push_back(std::move(Own));
+}
+
+// The master's bookkeeping of one step's results, in their order (Account for
+// each): the counts every result adds are summed on all host threads; only the
+// results whose bookkeeping depends on the order (engine errors kept as files,
+// crash names not seen yet, new coverage) go through Account one by one. The
+// results' slots are freed and their arenas released in bulk.
+void FuzzSession::AccountStep(std::vector<StreamResult_t> &Out) {
+  const size_t n = Out.size();
+  enum : uint8_t { K_SERIAL = 1, K_TIMEOUT = 2, K_CR3 = 4, K_CRASH = 8 };
+  std::vector<uint8_t> Kind(n, 0);
+  std::vector<TcArena *> Ar(n);
+  struct Sum {
+    uint64_t retired = 0, timeouts = 0, cr3 = 0, crashes = 0;
+  };
+  const unsigned T = HostPool::Get().Threads();
+  std::vector<Sum> Part(T + 1);
+  const bool every = Sample_ != nullptr;  // samples follow the accounting order: all of it serial
+  HostPool::Get().For(n, 1024, [&](size_t i) {
+    const LaneResult &L = *Out[i].r;
+    const TcRef R = Slot_[Out[i].tag];
+    Ar[i] = R.A;
+    uint8_t k = 0;
+    if (every || L.error) {
+      k = K_SERIAL;
+    } else {
+      if (std::holds_alternative<Timedout_t>(L.result)) k |= K_TIMEOUT;
+      if (std::holds_alternative<Cr3Change_t>(L.result)) k |= K_CR3;
+      if (const Crash_t *C = std::get_if<Crash_t>(&L.result)) {
+        k |= K_CRASH;
+        if (!C->CrashName.empty() && !CrashNames_.count(C->CrashName)) k = K_SERIAL;  // a new name
+      }
+      if (!L.new_coverage.empty() && !std::holds_alternative<Timedout_t>(L.result)) k = K_SERIAL;
+    }
+    Kind[i] = k;
+    if (k != K_SERIAL) {
+      Sum &s = Part[HostPool::ThreadIndex()];
+      s.retired += L.icount;
+      s.timeouts += (k & K_TIMEOUT) != 0;
+      s.cr3 += (k & K_CR3) != 0;
+      s.crashes += (k & K_CRASH) != 0;
+    }
+  }, n >= 4096);
+  // the order-dependent results, in order (counts included: Account adds them)
+  uint64_t bulk = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (Kind[i] != K_SERIAL) {
+      bulk++;
+      continue;
+    }
+    const TcRef R = Slot_[Out[i].tag];
+    Account(R.data(), R.size(), *Out[i].r, false);
+  }
+  S_.execs += bulk;
+  for (const Sum &s : Part) {
+    S_.retired += s.retired;
+    S_.timeouts += s.timeouts;
+    S_.cr3 += s.cr3;
+    S_.crashes += s.crashes;
+  }
+  // slots back, arenas whose testcases are all accounted released (runs of one arena)
+  const size_t fs = FreeSlot_.size();
+  FreeSlot_.resize(fs + n);
+  HostPool::Get().For(n, 4096, [&](size_t i) {
+    Slot_[Out[i].tag] = TcRef{};
+    FreeSlot_[fs + i] = Out[i].tag;
+  }, n >= 8192);
+  InFlight_ -= n;
+  for (size_t i = 0; i < n;) {
+    size_t j = i + 1;
+    while (j < n && Ar[j] == Ar[i]) j++;
+    TcArena *A = Ar[i];
+    A->Live -= j - i;
+    if (A->Live == 0) ReleaseArena(A);  // every testcase of the arena accounted
+    i = j;
+  }
 }
 
 // The master's bookkeeping of one result (server.h:816-886).

@@ -338,6 +338,14 @@ class FuzzSession {
   FILE *Sample_ = nullptr;
   bool StreamStep(bool Done);
   void Account(const uint8_t *Tc, size_t Size, const LaneResult &L, bool KnownCrash = false);
+  void AccountStep(std::vector<StreamResult_t> &Out);
+  // arenas: a released one (every testcase accounted) is kept for the next
+  // batch (its buffers keep their capacity: no allocation and no first-touch
+  // page faults per batch)
+  void ReleaseArena(TcArena *A);
+  std::unique_ptr<TcArena> NewArena();
+  std::mutex ArenaPoolMu_;
+  std::vector<std::unique_ptr<TcArena>> ArenaPool_;
 
   const RunnerOptions O_;
   Executor_t &Exec_;
