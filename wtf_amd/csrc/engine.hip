@@ -33,6 +33,20 @@ __device__ __forceinline__ u64 readlane64(u64 v, int l) {
   const u32 hi = __builtin_amdgcn_readlane((u32)(v >> 32), l);
   return ((u64)hi << 32) | lo;
 }
+// Lane masks straight from a compare (one v_cmp writing an SGPR pair), and a
+// mask back to a per-lane condition (used as the exec mask as it is): the
+// step loop tests and combines groups as masks, where a per-lane bool fed to
+// __ballot costs a v_cndmask + v_cmp pair to become a mask again. Every lane
+// of the wave runs the step loop, so a compare's mask is the ballot's.
+__device__ __forceinline__ u64 m_eq32(u32 a, u32 b) { return __builtin_amdgcn_uicmp(a, b, 32); }
+__device__ __forceinline__ u64 m_ne32(u32 a, u32 b) { return __builtin_amdgcn_uicmp(a, b, 33); }
+__device__ __forceinline__ u64 m_eq64(u64 a, u64 b) { return __builtin_amdgcn_uicmpl(a, b, 32); }
+__device__ __forceinline__ u64 m_ne64(u64 a, u64 b) { return __builtin_amdgcn_uicmpl(a, b, 33); }
+__device__ __forceinline__ u64 m_lt64(u64 a, u64 b) { return __builtin_amdgcn_uicmpl(a, b, 36); }
+__device__ __forceinline__ u64 m_ge64(u64 a, u64 b) { return __builtin_amdgcn_uicmpl(a, b, 35); }
+__device__ __forceinline__ u64 m_ge32(u32 a, u32 b) { return __builtin_amdgcn_uicmp(a, b, 35); }
+__device__ __forceinline__ bool in_mask(u64 m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+
 // The lowest v among the lanes with act, from a start value some such lane
 // holds: move to any lane below the current value until none is (a compare,
 // a ballot and a readlane per round, no LDS round trips; lanes regrouped by
@@ -1108,6 +1122,13 @@ constexpr u32 STAT_N = 16;
   } while (0)
 #endif
 
+// The lanes of a per-lane `if` meet again here, before a `continue` or the
+// end of the step loop's body. Without it the loop latch is the join of that
+// divergent branch, which makes every value the latch merges (the step count,
+// the group, `have`) divergent to the compiler, and the step loops become
+// exec-masked divergent loops. No instruction is emitted.
+#define RECONVERGE() __builtin_amdgcn_wave_barrier()
+
 // ---------------------------------------------------------------- main kernel
 // One hardware wave runs P.lpw lanes (64, or 32 / 16 to put more waves on
 // each SIMD when the batch is small: the step loop is latency-bound).
@@ -1177,15 +1198,24 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
   // Tenet: the registers at the start (first entry), or after a host handler
   // moved rip (resume without skip, lflags bit 1)
   if (valid && g_tn.buf && (g_tn.pos[lane] == 0 || (P.lflags[lane] & 2))) WITH_LANE_COPY(tn_regs(P, T));
-  const u64 pool_lo = (u64)(uintptr_t)P.pool, pool_hi = pool_lo + (P.npool + 1) * WTFGPU_PAGE_SIZE;
-  // the fields the fast loop reads, once: P is address-taken (the rare-path
+  // The fields the step loops read, once: P is address-taken (the rare-path
   // calls take it by reference), so a field read in the loop would be a
   // scratch load each step, and its vmcnt(0) wait would also wait for the
-  // previous step's guest stores
-  const bool cov_on = P.cov_rip != nullptr;
-  const u64 limit = P.limit;
+  // previous step's guest stores. A flag that steers uniform control flow
+  // goes through readfirstlane (a load from that private copy counts as
+  // divergent, and a loop exit on one made the step loop an exec-masked
+  // divergent loop). The loop-invariant bounds are kept in VGPRs (the
+  // compiler is told nothing of their uniformity) and compared as lane
+  // masks: SGPRs are the step loop's scarce registers, and these were
+  // spilled to VGPR lanes and reloaded on every wave-step.
+  const bool cov_on = rfl32(P.cov_rip != nullptr ? 1u : 0u) != 0;
+  u64 pool_lo = (u64)(uintptr_t)P.pool, pool_span = (P.npool + 1) * WTFGPU_PAGE_SIZE;
+  u64 limit_v = P.limit ? P.limit : ~0ull;  // icount above it: timeout
+  // wave-steps of this launch (a launch is bounded far below 2^32 wave-steps)
+  u32 max32 = max_steps > 0xffffffffull ? 0xffffffffu : (u32)max_steps;
+  asm volatile("" : "+v"(pool_lo), "+v"(pool_span), "+v"(limit_v), "+v"(max32));
   const FastMem fm = fast_mem(P);
-  u64 steps = 0;
+  u32 steps = 0;
   u32 fill_way = 0;  // two-way uop cache: the way the next fill replaces (wave-uniform)
 #ifdef WTFGPU_STAMPS
   u64 stamp_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1201,22 +1231,25 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     u64 grip = 0;
     bool have = false;
     for (;;) {
-      if (steps >= max_steps) break;
-      const bool active = valid && L.status == WTFGPU_RUNNING;
-      const u64 am = __ballot(active);
+      if (m_ge32(steps, max32)) break;
+      // (a position with no lane is EXIT_IDLE, never running)
+      const u64 am = m_eq32(L.status, WTFGPU_RUNNING);
       if (am == 0) break;
       // group = lanes at the min rip; when the wave is converged (the common
       // case) the first active lane's rip is that min and the reduction is skipped
       grip = readlane64(L.rip, __ffsll((long long)am) - 1);
-      if (__ballot(active && L.rip == grip) != am) grip = active_min(active, L.rip, grip);
+      u64 gm = am & m_eq64(L.rip, grip);
+      if (gm != am) {
+        for (u64 lo = am & m_lt64(L.rip, grip); lo; lo = am & m_lt64(L.rip, grip))
+          grip = readlane64(L.rip, __ffsll((long long)lo) - 1);
+        gm = am & m_eq64(L.rip, grip);
+      }
       have = true;
-      const bool cand = active && L.rip == grip;
       WHY(1);
       // a new code page: the lane's TLB, else a walk, in registers (what
       // code_xlate does); a translation that would fault goes to the slow step
-      const bool cx = cand && (grip >> 12) != L.cvpn;
-      if (__ballot(cx)) {
-        if (cx) {
+      if (const u64 cxm = gm & m_ne64(L.cvpn, grip >> 12)) {
+        if (in_mask(cxm)) {
           u64 td, gp;
           bool ok = tlb_get(L, grip >> 12, td) && perm_ok(L, td, ACC_X);
           if (!ok && walk<false>(P, L, grip & ~0xfffull, ACC_X, td, gp) && perm_ok(L, td, ACC_X)) {
@@ -1228,13 +1261,13 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
             L.cptr = td & ~0xfffull;
           }
         }
-        if (__ballot(cand && (grip >> 12) != L.cvpn)) break;
+        if (gm & m_ne64(L.cvpn, grip >> 12)) break;
       }
       WHY(3);
-      const int leader = __ffsll((long long)__ballot(cand)) - 1;
-      const u64 lptr = readlane64(L.cptr, leader);
-      if (lptr < pool_lo || lptr >= pool_hi) break;
-      const bool ing = cand && L.cptr == lptr;
+      const u64 lptr = readlane64(L.cptr, __ffsll((long long)gm) - 1);
+      if (m_ge64(lptr - pool_lo, pool_span)) break;
+      const u64 ingm = gm & m_eq64(L.cptr, lptr);
+      const bool ing = in_mask(ingm);
       const u64 key = lptr | (grip & 0xfff);
       UCEntry *e = &uc[uc_slot(key)];
       // one LDS round trip: key, logged mask, flags and the FOp are contiguous;
@@ -1248,9 +1281,24 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       WHY(3);
       const u32 flags = h.flags;
       if (flags & (UC_BP | UC_CROSS | UC_BADLEN | UC_UNSUP)) break;
-      if (cov_on && !(flags & UC_COVERED) && (__ballot(ing) & ~h.logged)) break;
+      if (cov_on && !(flags & UC_COVERED) && (ingm & ~h.logged)) break;
       const FOp &f = h.f;
       if (fo_op(f) == FO_GENERIC) break;
+#if WTFGPU_PROBE == 1
+      // diagnostic build only: a nop retires without the exec pipeline
+      if (fo_op(f) == FO_NOP) {
+        steps++;
+        have = false;
+        if (ing) {
+          skip = false;
+          L.rip = grip + fo_len(f);
+          L.icount++;
+          L.nbytes += fo_len(f);
+          if (L.icount > limit_v) L.status = WTFGPU_EXIT_TIMEOUT;
+        }
+        continue;
+      }
+#endif
       steps++;
       have = false;
       STAMP(6);
@@ -1263,10 +1311,10 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       // memory round trip instead of a lane's 64 dependent ones
       const u32 len = fo_len(f);
       u64 next = 0;
-      bool want = ing;
+      u64 wantm = ingm;
       if (ing) skip = false;
       for (u32 round = 0;; round++) {
-        if (want) {
+        if (in_mask(wantm)) {
           L.miss = 0;
           L.pend = 0;
           // the FOp as an opaque value each round: otherwise everything
@@ -1277,10 +1325,13 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
           FOp fr = f;
           asm volatile("" : "+s"(fr.w0), "+s"(fr.fl), "+s"(fr.w2), "+s"(fr.disp), "+s"(fr.imm));
           fast_exec(fm, L, fr, grip + len, next);
-          if (!L.miss || L.miss != 2 || round >= 3) want = false;
         }
-        if (__ballot(want) == 0) break;
+        RECONVERGE();
+        // lanes to serve and retry: a TLB miss or first write (miss 2), 3 rounds at most
+        wantm = round >= 3 ? 0 : wantm & m_eq32(L.miss, 2);
+        if (wantm == 0) break;
         u64 csrc = 0, cdst = 0, cgpfn = 0, ctd = 0;
+        bool want = in_mask(wantm);
         if (want && !fast_fill_prep(P, L, csrc, cdst, cgpfn, ctd)) want = false;
         for (u64 cm = __ballot(want && cdst); cm; cm &= cm - 1) {
           const int l = __ffsll((long long)cm) - 1;
@@ -1295,20 +1346,23 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
         // the copies land before the lanes read their pages (one wave, one CU)
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
         if (want && cdst) fast_fill_finish(P, L, cdst, cgpfn, ctd);
+        wantm = __ballot(want);
       }
-      if (ing && !L.miss) {
+      const u64 missm = ingm & m_ne32(L.miss, 0);
+      if (in_mask(ingm & ~missm)) {
         L.rip = next;
         L.icount++;
         L.nbytes += len + L.pend;
-        if (limit && L.icount > limit) L.status = WTFGPU_EXIT_TIMEOUT;
+        if (L.icount > limit_v) L.status = WTFGPU_EXIT_TIMEOUT;
       }
+      RECONVERGE();
       STAMP(7);
       // lanes that still missed keep their rip: the slow step services them.
       // The attempt is not a wave-step of its own (the slow step counts the
       // group once): a slice's length in wave-steps must not depend on which
       // path ran a group, since that depends on when other queues' coverage
       // commits landed (U44: fixed-seed campaigns reproduce)
-      if (__ballot(ing && L.miss)) {
+      if (missm) {
         WHY(0);
         steps--;
         have = true;
@@ -1318,12 +1372,13 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     STAMP(0);
     // faults raised by the last slow step: deliver through the guest IDT when
     // it has a gate (the lane resumes at the handler), else the lane exits
-    if (__ballot(valid && L.status == WTFGPU_EXIT_FAULT && !L.nodeliver)) {
-      if (valid && L.status == WTFGPU_EXIT_FAULT && !L.nodeliver) {
+    if (__ballot(L.status == WTFGPU_EXIT_FAULT && !L.nodeliver)) {
+      if (L.status == WTFGPU_EXIT_FAULT && !L.nodeliver) {
         bool dv;
         WITH_LANE_COPY(dv = deliver_fault(P, T));
         if (dv && g_tn.buf) WITH_LANE_COPY(tn_regs(P, T));  // Tenet: the delivered exception
       }
+      RECONVERGE();
       continue;
     }
     if (!have) break;
@@ -1335,7 +1390,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
 #ifdef WTFGPU_STAMPS
     whyc_[why_ & 3]++;
 #endif
-    const bool active = valid && L.status == WTFGPU_RUNNING;
+    const bool active = L.status == WTFGPU_RUNNING;
     bool cand = active && L.rip == grip;
     if (cand && (grip >> 12) != L.cvpn) WITH_LANE_COPY(code_xlate(P, T, grip));
     cand = cand && (grip >> 12) == L.cvpn;
@@ -1352,7 +1407,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       if (rfl64(e[1].key) == key) e += 1;
       else e += (fill_way++ & 1);  // the way a fill replaces
     }
-    const bool cacheable = lptr >= pool_lo && lptr < pool_hi;
+    const bool cacheable = !m_ge64(lptr - pool_lo, pool_span);
     if (cacheable && rfl64(e->key) != key) {
 #if WTFGPU_FILL_INLINE
       if (!uc_fill_shared(P, e, &uu[uu_slot(key)], key, off, grip, lid))
@@ -1363,8 +1418,8 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       // an entry the fast loop can run (a common op, nothing to log, no
       // breakpoint): back to it, this pass was only the fill
       const u32 ff = rfl32(e->flags);
-      if (!(ff & (UC_BP | UC_CROSS | UC_BADLEN | UC_UNSUP)) && (!P.cov_rip || (ff & UC_COVERED)) &&
-          fo_op(e->f) != FO_GENERIC) {
+      if (!(ff & (UC_BP | UC_CROSS | UC_BADLEN | UC_UNSUP)) && (!cov_on || (ff & UC_COVERED)) &&
+          (rfl32(e->f.w0) & 0xff) != FO_GENERIC) {  // read uniformly: a divergent exit here made the whole step loop divergent
         steps--;
         STAMP(2);
         continue;
@@ -1375,11 +1430,12 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     if (flags & (UC_CROSS | UC_BADLEN)) {
       if (flags & UC_BADLEN) {
         if (ing) set_fault(L, WTFGPU_VEC_GP, 0, 0);
-      } else if (valid) {  // a position with no lane has no copy slot of its own
+      } else if (L.status != WTFGPU_EXIT_IDLE) {  // a position with no lane has no copy slot of its own
         bool sk = skip;  // skip stays a register (a reference would put it in scratch for the whole loop)
         WITH_LANE_COPY(slow_step(P, T, grip, lptr, ing, sk));
         skip = sk;
       }
+      RECONVERGE();
       STAMP(5);
       continue;
     }
@@ -1388,7 +1444,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
 
     // ---- coverage, then breakpoint (bochscpu_backend.cc:501-547)
     if (P.trace && ing && !skip) trace_rip(P, L.lane, grip);  // a resumed breakpoint was logged at its hit
-    if (P.cov_rip && !(flags & UC_COVERED)) {
+    if (cov_on && !(flags & UC_COVERED)) {
       const u64 logged = rfl64(e->logged);
       if (gmask & ~logged) {
         L.ccnt = cover(P, grip, ing && !((logged >> lid) & 1), L.lane, L.cgen, L.ccnt);
@@ -1435,6 +1491,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
         count_edge(P, L.lane, L.ccnt != c0);
       }
     }
+    RECONVERGE();
     STAMP(1);
   }
 

@@ -356,9 +356,9 @@ __device__ __forceinline__ int fast_vec(wtfgpu_regs_t *full, Lane &L, const FOp 
 // scratch copy each step).
 struct FastMem {
   wtfgpu_regs_t *full;
-  const u64 *fs_base, *gs_base;
+  const Dev *P;  // the rest (fs / gs bases: segment-override operands only) read when needed
 };
-__device__ __forceinline__ FastMem fast_mem(const Dev &P) { return FastMem{P.full, P.fs_base, P.gs_base}; }
+__device__ __forceinline__ FastMem fast_mem(const Dev &P) { return FastMem{P.full, &P}; }
 
 // One exit and one commit on every path: a failed attempt (ok = false, L.miss
 // set) writes the unchanged values back. The guest registers are an array the
@@ -382,7 +382,7 @@ __device__ __forceinline__ int fast_exec(const FastMem &M, Lane &L, const FOp &f
       addr = f.disp + (fo_riprel(f) ? nrip : 0);
       if (fo_base(f) != NOREG) addr += R(L, fo_base(f));
       if (fo_index(f) != NOREG) addr += R(L, fo_index(f)) << fo_scale(f);
-      if (fo_seg(f)) addr += (fo_seg(f) == 1 ? M.fs_base : M.gs_base)[L.lane];
+      if (fo_seg(f)) addr += (fo_seg(f) == 1 ? M.P->fs_base : M.P->gs_base)[L.lane];
     } else if (F & FF_PUSH) {
       addr = rsp - 8;
     } else {
