@@ -47,19 +47,6 @@ __device__ __forceinline__ u64 m_ge64(u64 a, u64 b) { return __builtin_amdgcn_ui
 __device__ __forceinline__ u64 m_ge32(u32 a, u32 b) { return __builtin_amdgcn_uicmp(a, b, 35); }
 __device__ __forceinline__ bool in_mask(u64 m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 
-// The lowest v among the lanes with act, from a start value some such lane
-// holds: move to any lane below the current value until none is (a compare,
-// a ballot and a readlane per round, no LDS round trips; lanes regrouped by
-// rip are in ascending order, so one or two rounds).
-__device__ __forceinline__ u64 active_min(bool act, u64 v, u64 start) {
-  u64 g = start;
-  for (;;) {
-    const u64 m = __ballot(act && v < g);
-    if (m == 0) return g;
-    g = readlane64(v, __ffsll((long long)m) - 1);
-  }
-}
-
 __device__ __forceinline__ bool hash_find(const u64 *keys, u32 mask, u64 key, u32 &slot) {
   u32 h = (u32)mix64(key) & mask;
   for (u32 i = 0; i <= mask; i++) {
@@ -359,6 +346,18 @@ __device__ __forceinline__ void lds_uniform_read(const T *src, T &dst) {
   u32 *d = (u32 *)&dst;
 #pragma unroll
   for (u32 i = 0; i < sizeof(T) / 4; i++) d[i] = rfl32(s[i]);
+}
+
+// The uop-cache head as the fast loop reads it (wave-uniform): key, flags
+// and the FOp words fast_exec uses (not `logged` or the pads).
+__device__ __forceinline__ void uc_head_read(const UCEntry *e, UCHead &h) {
+  h.key = rfl64(e->key);
+  h.flags = rfl32(e->flags);
+  h.f.w0 = rfl32(e->f.w0);
+  h.f.fl = rfl32(e->f.fl);
+  h.f.w2 = rfl32(e->f.w2);
+  h.f.disp = rfl64(e->f.disp);
+  h.f.imm = rfl64(e->f.imm);
 }
 
 __device__ __forceinline__ bool bp_lookup(const Dev &P, u64 rip) {
@@ -1139,6 +1138,9 @@ constexpr u32 STAT_N = 16;
 #ifndef WTFGPU_KRUN_WAVES
 #define WTFGPU_KRUN_WAVES 2
 #endif
+#ifndef WTFGPU_FAST_REGOPS
+#define WTFGPU_FAST_REGOPS 1  // register-only forms skip the fast loop's memory retry rounds
+#endif
 #ifndef WTFGPU_P_BYREF
 #define WTFGPU_P_BYREF 0
 #endif
@@ -1273,15 +1275,17 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       // one LDS round trip: key, logged mask, flags and the FOp are contiguous;
       // the second way only when the first misses (reading both at once kept
       // twice the head in flight on every step: SYN 8 % slower than one way)
+      // (the words the step needs only: the logged mask is read when the rip
+      // is not yet covered, the pads never)
       UCHead h;
-      lds_uniform_read(&e->h, h);
-      if (UC_WAYS == 2 && h.key != key) lds_uniform_read(&e[1].h, h);
+      uc_head_read(e, h);
+      if (UC_WAYS == 2 && h.key != key) uc_head_read(++e, h);
       WHY(2);
       if (h.key != key) break;
       WHY(3);
       const u32 flags = h.flags;
       if (flags & (UC_BP | UC_CROSS | UC_BADLEN | UC_UNSUP)) break;
-      if (cov_on && !(flags & UC_COVERED) && (ingm & ~h.logged)) break;
+      if (cov_on && !(flags & UC_COVERED) && (ingm & ~rfl64(e->logged))) break;
       const FOp &f = h.f;
       if (fo_op(f) == FO_GENERIC) break;
 #if WTFGPU_PROBE == 1
@@ -1296,6 +1300,27 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
           L.nbytes += fo_len(f);
           if (L.icount > limit_v) L.status = WTFGPU_EXIT_TIMEOUT;
         }
+        continue;
+      }
+#endif
+#if WTFGPU_FAST_REGOPS
+      // a form that touches no memory cannot miss: one pass, no retry rounds
+      if (!(f.fl & (FF_PUSH | FF_POP | FF_MR_A | FF_MR_B | FF_MW)) && fo_op(f) < FO_VLD) {
+        steps++;
+        have = false;
+        if (ing) {
+          skip = false;
+          const u32 len = fo_len(f);
+          FOp fr = f;
+          asm volatile("" : "+s"(fr.w0), "+s"(fr.fl), "+s"(fr.w2), "+s"(fr.disp), "+s"(fr.imm));
+          u64 next;
+          fast_exec<true>(fm, L, fr, grip + len, next);
+          L.rip = next;
+          L.icount++;
+          L.nbytes += len;
+          if (L.icount > limit_v) L.status = WTFGPU_EXIT_TIMEOUT;
+        }
+        RECONVERGE();
         continue;
       }
 #endif

@@ -366,13 +366,17 @@ __device__ __forceinline__ FastMem fast_mem(const Dev &P) { return FastMem{P.ful
 // under a uniform branch, or an early return that skips the writes, makes that
 // array a phi of copies (~80 v_mov per wave-step). Here rsp and the
 // destination are written exactly once each, unconditionally.
+// kRegOnly: the caller knows the form touches no memory (no FF_PUSH / FF_POP
+// / FF_MR_* / FF_MW, not a vector move): the memory stages compile out and
+// the attempt cannot miss.
+template <bool kRegOnly = false>
 __device__ __forceinline__ int fast_exec(const FastMem &M, Lane &L, const FOp &f, u64 nrip, u64 &next) {
   next = nrip;
   const u32 F = f.fl, op = fo_op(f), sub = fo_sub(f), sz = fo_sz(f);
   const u64 rsp = R(L, 4);
   u64 res = 0, fl = L.rflags, fo;
   bool ok = true;
-  if (op >= FO_VLD) {
+  if (!kRegOnly && op >= FO_VLD) {
     ok = fast_vec(M.full, L, f, nrip) == X_OK;  // xmm / ymm state only (memory), no GPR
   } else {
     u64 a = (F & FF_AREG) ? R(L, fo_ra(f)) : 0;
@@ -393,7 +397,7 @@ __device__ __forceinline__ int fast_exec(const FastMem &M, Lane &L, const FOp &f
     // (a write to the read's own address makes it a read-modify-write; call
     // [mem] reads its target and writes the stack)
     const bool rmw = (F & FF_MW) && (F & (FF_MR_A | FF_MR_B)) && !(F & FF_PUSH);
-    if (F & (FF_MR_A | FF_MR_B)) {
+    if (!kRegOnly && (F & (FF_MR_A | FF_MR_B))) {
       const u32 rsz = (F & (FF_PUSH | FF_POP)) ? 8 : (op == FO_MOVX ? fo_szb(f) : sz);
       mp = fxlate(L, addr, rsz, rmw ? ACC_W : ACC_R);
       if (mp) {
@@ -455,7 +459,7 @@ __device__ __forceinline__ int fast_exec(const FastMem &M, Lane &L, const FOp &f
       default: break;
     }
     // ---- the memory write
-    if (ok && (F & FF_MW)) {
+    if (!kRegOnly && ok && (F & FF_MW)) {
       const u32 wsz = (F & FF_PUSH) ? 8 : sz;
       if (!rmw) mp = fxlate(L, (F & FF_PUSH) ? rsp - 8 : addr, wsz, ACC_W);
       if (mp) {
@@ -467,6 +471,7 @@ __device__ __forceinline__ int fast_exec(const FastMem &M, Lane &L, const FOp &f
     }
   }
   // ---- commit (rsp first: pop rsp ends with the popped value)
+#if WTFGPU_FAST_WB_ALWAYS
   const u64 nrsp = !ok ? rsp : (F & FF_PUSH) ? rsp - 8 : (F & FF_POP) ? rsp + 8 + (op == FO_RET ? f.imm : 0) : rsp;
   RS(L, 4, nrsp);
   const u32 wi = fo_ra(f) & 15;
@@ -474,6 +479,17 @@ __device__ __forceinline__ int fast_exec(const FastMem &M, Lane &L, const FOp &f
   // wr(): 8 / 4 bytes replace (4 zero-extends), 2 / 1 merge into the old value
   const u64 nv = (ok && (F & FF_WRA)) ? (sz >= 4 ? (res & mk) : ((old & ~mk) | (res & mk))) : old;
   RS(L, wi, nv);
+#else
+  // (written under the op's uniform flags: ops that write no register skip
+  // the indexed read-back and write)
+  if (F & (FF_PUSH | FF_POP)) RS(L, 4, !ok ? rsp : (F & FF_PUSH) ? rsp - 8 : rsp + 8 + (op == FO_RET ? f.imm : 0));
+  if (F & FF_WRA) {
+    const u32 wi = fo_ra(f) & 15;
+    const u64 old = R(L, wi), mk = szmask(sz);
+    // wr(): 8 / 4 bytes replace (4 zero-extends), 2 / 1 merge into the old value
+    RS(L, wi, ok ? (sz >= 4 ? (res & mk) : ((old & ~mk) | (res & mk))) : old);
+  }
+#endif
   if (ok && (F & FF_FLAGS)) L.rflags = fl;
   return ok ? X_OK : X_FAULT;
 }
