@@ -250,6 +250,39 @@ __device__ __forceinline__ void wr(Lane &L, u32 r, u32 sz, u64 v) {
 // A TLB miss or a first write to a shared page -> L.miss = 2 with the address:
 // k_run serves it in registers (fast_fill) and retries. Everything else ->
 // L.miss = 1, the slow step takes over.
+#ifndef WTFGPU_FAST_NB
+#define WTFGPU_FAST_NB 1  // branch-free translation and unconditional loads in the fast path
+#endif
+#if WTFGPU_FAST_NB
+// The same decisions as selects, without per-lane branches (each early return
+// was an exec-mask region): the first failure of the attempt sets L.miss.
+__device__ __forceinline__ u8 *fxlate(Lane &L, u64 va, u32 sz, int acc) {
+  u64 td;
+  const bool w = acc == ACC_W;
+  const bool cross = (va & 0xfff) + sz > 4096;
+  const bool hit = tlb_get(L, va >> 12, td);
+  const bool pok = perm_ok(L, td, acc);
+  const u64 kind = td & (T_PRIV | T_PT);
+  const bool m2 = !cross && (!hit || (pok && w && kind == 0));
+  const bool ok = !cross && hit && pok && (!w || kind == T_PRIV);
+  const bool first = !ok && L.miss == 0;
+  L.miss = first ? (m2 ? 2u : 1u) : L.miss;
+  L.miss_va = first && m2 ? va : L.miss_va;
+  L.miss_acc = first && m2 ? (u32)acc : L.miss_acc;
+  return ok ? (u8 *)(uintptr_t)(td & ~0xfffull) + (va & 0xfff) : nullptr;
+}
+// sz bytes at p, read as the two aligned words around it, both loads issued
+// whatever the alignment (the second stays in p's page: at a page's last word
+// it re-reads the first, and is then unused); p may be the safe zero page.
+__device__ __forceinline__ u64 load_le2(const u8 *p, u32 sz) {
+  const uintptr_t a = (uintptr_t)p & ~(uintptr_t)7;
+  const u32 off = (u32)((uintptr_t)p & 7);
+  const u64 lo = *(const u64 *)a;
+  const u64 hi = *(const u64 *)((a & 0xff8) != 0xff8 ? a + 8 : a);
+  const u64 v = off ? (lo >> (8 * off)) | (hi << (64 - 8 * off)) : lo;
+  return v & szmask(sz);
+}
+#else
 __device__ __forceinline__ u8 *fxlate(Lane &L, u64 va, u32 sz, int acc) {
   u64 td;
   const bool w = acc == ACC_W;
@@ -270,6 +303,7 @@ __device__ __forceinline__ u8 *fxlate(Lane &L, u64 va, u32 sz, int acc) {
   }
   return (u8 *)(uintptr_t)(td & ~0xfffull) + (va & 0xfff);
 }
+#endif
 
 // 16 / 32 bytes at p (inside one page): aligned words, funnel-shifted when p
 // is not 8-byte aligned (the word past the operand is read only then, and it
@@ -356,9 +390,10 @@ __device__ __forceinline__ int fast_vec(wtfgpu_regs_t *full, Lane &L, const FOp 
 // scratch copy each step).
 struct FastMem {
   wtfgpu_regs_t *full;
-  const Dev *P;  // the rest (fs / gs bases: segment-override operands only) read when needed
+  const Dev *P;    // the rest (fs / gs bases: segment-override operands only) read when needed
+  const u8 *safe;  // the pool's zero page: what a lane whose access missed reads instead
 };
-__device__ __forceinline__ FastMem fast_mem(const Dev &P) { return FastMem{P.full, &P}; }
+__device__ __forceinline__ FastMem fast_mem(const Dev &P) { return FastMem{P.full, &P, P.pool}; }
 
 // One exit and one commit on every path: a failed attempt (ok = false, L.miss
 // set) writes the unchanged values back. The guest registers are an array the
@@ -400,6 +435,13 @@ __device__ __forceinline__ int fast_exec(const FastMem &M, Lane &L, const FOp &f
     if (!kRegOnly && (F & (FF_MR_A | FF_MR_B))) {
       const u32 rsz = (F & (FF_PUSH | FF_POP)) ? 8 : (op == FO_MOVX ? fo_szb(f) : sz);
       mp = fxlate(L, addr, rsz, rmw ? ACC_W : ACC_R);
+#if WTFGPU_FAST_NB
+      const u64 v = load_le2(mp ? mp : M.safe, rsz);  // a missed lane reads the zero page, unused
+      L.pend += mp ? rsz : 0;
+      if (F & FF_MR_A) a = mp ? v : a;
+      else b = mp ? v : b;
+      ok = mp != nullptr;
+#else
       if (mp) {
         const u64 v = load_le(mp, rsz);
         L.pend += rsz;
@@ -408,6 +450,7 @@ __device__ __forceinline__ int fast_exec(const FastMem &M, Lane &L, const FOp &f
       } else {
         ok = false;
       }
+#endif
     }
     // ---- compute (pure)
     switch (op) {
