@@ -30,6 +30,8 @@ CASES = {
     "pushpop": "5058",             # push rax; pop rax
     "cmp_jz": "4839d87400",        # cmp rax, rbx; jz +0
     "movaps_ld": "0f2807",         # movaps xmm0, [rdi]
+    "bswap": "480fc8",             # bswap rax       (generic: the slow step's exec)
+    "imul_rr": "480fafc3",         # imul rax, rbx   (generic)
 }
 SYN_LOOP = ("4889c2" "81e2f8010000" "4c8b0417" "4c01c0" "4831c3" "4929d9" "4c8d545810" "4181e2f80f0000" "4e890c16")
 

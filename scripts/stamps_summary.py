@@ -18,7 +18,11 @@ for path in sys.argv[1:]:
         if line.startswith("wtfgpu stamps generic ops:"):
             for kv in line.split(":", 1)[1].split():
                 k, v = kv.split(":")
-                name = (OPS[int(k) & 63] if (int(k) & 63) < len(OPS) else k) + ("" if int(k) < 64 else "(cov)")
+                # index: op | why << 6 | covered << 8 (why the fast loop left the
+                # group: miss, codepage, ucmiss, other)
+                i = int(k)
+                name = (OPS[i & 63] if (i & 63) < len(OPS) else str(i & 63)) + ("(cov)" if i & 256 else "") + \
+                    "/" + ("miss", "codepage", "ucmiss", "other")[(i >> 6) & 3]
                 ops[name] = ops.get(name, 0) + int(v)
             continue
         m = PAT.search(line)

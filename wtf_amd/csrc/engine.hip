@@ -1105,9 +1105,9 @@ struct LaneCopy {
 // (generic op, breakpoint, coverage, code outside the pool)
 #define WHY(k) why_ = (k)
 // and which generic ops the slow step executed (O_* / O_SYS2 etc.), one count per
-// group, in stat[16..80)
-#define OPHIST(op) ophist_[(op) & 127]++
-constexpr u32 STAT_N = 144;
+// group, in stat[16..528): index op | why << 6 | covered << 8
+#define OPHIST(op) ophist_[((op) & 63) | (why_ & 3) << 6 | ((op) & 64 ? 256 : 0)]++
+constexpr u32 STAT_N = 528;
 #else
 constexpr u32 STAT_N = 16;
 #define OPHIST(op) \
@@ -1140,6 +1140,15 @@ constexpr u32 STAT_N = 16;
 #endif
 #ifndef WTFGPU_FAST_REGOPS
 #define WTFGPU_FAST_REGOPS 1  // register-only forms skip the fast loop's memory retry rounds
+#endif
+#ifndef WTFGPU_BP_RESUME_FAST
+#define WTFGPU_BP_RESUME_FAST 1  // lanes resuming at a breakpoint run its instruction in the fast loop
+#endif
+#ifndef WTFGPU_INLINE_ACTIONS
+#define WTFGPU_INLINE_ACTIONS 3  // SetGprs (1) / StopOk (2) actions applied without the lane copy
+#endif
+#ifndef WTFGPU_FAST_FAULTS
+#define WTFGPU_FAST_FAULTS 1  // a fast attempt whose fill would fault raises the fault itself
 #endif
 #ifndef WTFGPU_P_BYREF
 #define WTFGPU_P_BYREF 0
@@ -1224,7 +1233,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
   u64 tprev_ = __builtin_amdgcn_s_memtime();
   u64 whyc_[4] = {0, 0, 0, 0};
   u32 why_ = 3;
-  u32 ophist_[128] = {};
+  u32 ophist_[512] = {};
 #endif
 
   for (;;) {
@@ -1284,7 +1293,16 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       if (h.key != key) break;
       WHY(3);
       const u32 flags = h.flags;
-      if (flags & (UC_BP | UC_CROSS | UC_BADLEN | UC_UNSUP)) break;
+      if (flags & (UC_CROSS | UC_BADLEN | UC_UNSUP)) break;
+      // a breakpoint: the slow step runs its handler; lanes that resume at it
+      // (skip: a device action that left rip there, or a host handler's
+      // resume) run the instruction here, as the slow step would without
+      // calling the handler again
+#if WTFGPU_BP_RESUME_FAST
+      if ((flags & UC_BP) && (ingm & ~__ballot(skip))) break;
+#else
+      if (flags & UC_BP) break;
+#endif
       if (cov_on && !(flags & UC_COVERED) && (ingm & ~rfl64(e->logged))) break;
       const FOp &f = h.f;
       if (fo_op(f) == FO_GENERIC) break;
@@ -1357,7 +1375,12 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
         if (wantm == 0) break;
         u64 csrc = 0, cdst = 0, cgpfn = 0, ctd = 0;
         bool want = in_mask(wantm);
-        if (want && !fast_fill_prep(P, L, csrc, cdst, cgpfn, ctd)) want = false;
+        if (want && !fast_fill_prep(P, L, csrc, cdst, cgpfn, ctd)) {
+          want = false;
+#if WTFGPU_FAST_FAULTS
+          fast_fault(P, L);  // the lane stops with the fault (delivered after the loop)
+#endif
+        }
         for (u64 cm = __ballot(want && cdst); cm; cm &= cm - 1) {
           const int l = __ffsll((long long)cm) - 1;
           const uint4 *s4 = (const uint4 *)(uintptr_t)readlane64(csrc, l) + lid * 4;
@@ -1387,12 +1410,15 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       // group once): a slice's length in wave-steps must not depend on which
       // path ran a group, since that depends on when other queues' coverage
       // commits landed (U44: fixed-seed campaigns reproduce)
-      if (missm) {
+      if (missm & m_eq32(L.status, WTFGPU_RUNNING)) {
         WHY(0);
         steps--;
         have = true;
         break;
       }
+      // lanes whose fill raised a fault here (fast_fault): the step counted
+      // (as the slow step's would have), the fault is delivered next
+      if (missm) break;
     }
     STAMP(0);
     // faults raised by the last slow step: deliver through the guest IDT when
@@ -1477,6 +1503,32 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       }
     }
     STAMP(3);
+    // a register-only device action (SetGprs, StopOk: the same for every lane)
+    // is applied here, without the lane copy and call the others take
+    u32 act_kind = ~0u;
+    const wtfgpu_bp_action_t *act = nullptr;
+    if (WTFGPU_INLINE_ACTIONS && (flags & UC_BP) && P.act_keys && !g_tn.buf) {
+      u32 slot;
+      if (hash_find(P.act_keys, P.act_mask, grip, slot)) {
+        act = &P.act[slot];
+        act_kind = rfl32(act->kind);
+      }
+    }
+    // (one block per kind: with the two kinds nested in one per-lane if/else
+    // the build ran wrong on MI355X, tlv's lanes stopping Ok at their SetGprs
+    // breakpoint, although either kind alone ran right)
+    if ((WTFGPU_INLINE_ACTIONS & 1) && act_kind == WTFGPU_BPACT_SET_GPRS && ing && !skip) {
+#pragma unroll
+      for (u32 i = 0; i < 16; i++) RS(L, i, act->gprs[i]);
+      L.rip = act->gprs[16];
+      skip = L.rip == grip;
+      ing = false;
+    }
+    if ((WTFGPU_INLINE_ACTIONS & 2) && act_kind == WTFGPU_BPACT_STOP_OK && ing && !skip) {
+      L.status = WTFGPU_EXIT_STOP_OK;
+      skip = true;
+      ing = false;
+    }
     if (ing) {
       if ((flags & UC_BP) && !skip) {
         // breakpoint hit: device action (the lane keeps running) or host exit
@@ -1554,7 +1606,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
 #ifdef WTFGPU_STAMPS
     for (int k = 0; k < 8; k++) atomicAdd((unsigned long long *)&P.stat[4 + k], (unsigned long long)stamp_[k]);
     for (int k = 0; k < 4; k++) atomicAdd((unsigned long long *)&P.stat[12 + k], (unsigned long long)whyc_[k]);
-    for (int k = 0; k < 128; k++)
+    for (int k = 0; k < 512; k++)
       if (ophist_[k]) atomicAdd((unsigned long long *)&P.stat[16 + k], (unsigned long long)ophist_[k]);
 #endif
   }
@@ -3268,7 +3320,7 @@ static void print_stamps(const u64 *s) {
             (double)s[5] / s[0], (double)s[9] / s[0], (unsigned long long)s[12], (unsigned long long)s[13],
             (unsigned long long)s[14], (unsigned long long)s[15], (double)s[10] / s[0], (double)s[11] / s[0]);
   fprintf(stderr, "wtfgpu stamps generic ops:");
-  for (int k = 0; k < 128; k++)
+  for (int k = 0; k < 512; k++)
     if (s[16 + k]) fprintf(stderr, " %d:%llu", k, (unsigned long long)s[16 + k]);
   fprintf(stderr, "\n");
 #else

@@ -287,6 +287,18 @@ __device__ __forceinline__ bool fast_fill_prep(const Dev &P, Lane &L, u64 &src, 
   tlb_put(L, va >> 12, td);
   return true;
 }
+// When fast_fill_prep declines because the access faults (the walk fails or
+// the permission check does), raise the fault service_miss would raise for
+// the same access, so the lane leaves the step loop with it instead of
+// re-running the instruction through exec() only to fault there (a
+// page-table page or a full overlay stays for the slow step: no fault).
+__device__ __forceinline__ void fast_fault(const Dev &P, Lane &L) {
+  const u64 va = L.miss_va;
+  const int acc = (int)L.miss_acc;
+  u64 td, gpfn;
+  if (!walk(P, L, va, acc, td, gpfn)) return;  // (walk<true> set the fault)
+  if (!perm_ok(L, td, acc)) set_fault(L, WTFGPU_VEC_PF, pf_error(L, acc, true), va);
+}
 __device__ __forceinline__ void fast_fill_finish(const Dev &P, Lane &L, u64 dst, u64 gpfn, u64 td) {
   P.ov_gpfn[(u64)L.ovn * P.nlanes + L.lane] = (u32)gpfn;
   L.ovn++;
