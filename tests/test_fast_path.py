@@ -313,3 +313,51 @@ def test_indirect_branches_unary_bit_and_segment_forms_fast_equals_slow():
     assert fast.status == INT3 and fast.rip == CODE_VA + 83, (fast.status, hex(fast.rip))
     assert n == 16, n  # every instruction but the trailing int3 ran on the fast path
     assert bytes(fast.win[0x118:0x120]) == (0xDEADBEEF).to_bytes(8, "little")
+
+
+def test_high_byte_register_forms_fast_equals_slow_and_oracle():
+    """ah / ch / dh / bh operands (8-bit registers 4..7 without REX) on the fast
+    path: read as bits 15:8 of rax..rbx, written merged into those bits, for
+    mov / ALU / test / inc / not / neg / shifts / setcc / movzx / movsx and the
+    memory forms; the fast forms give the generic path's and the oracle's lane."""
+    from tests.test_sse import CODE_VA
+    code = bytes.fromhex(
+        "f6c510"        # test ch, 0x10
+        "88e0"          # mov al, ah
+        "88c4"          # mov ah, al
+        "8ae1"          # mov ah, cl
+        "80c47f"        # add ah, 0x7f
+        "28fc"          # sub ah, bh
+        "30d6"          # xor dh, dl
+        "38ec"          # cmp ah, ch
+        "fec4"          # inc ah
+        "f6d7"          # not bh
+        "f6de"          # neg dh
+        "d0e4"          # shl ah, 1
+        "c0ef03"        # shr bh, 3
+        "0f94c4"        # sete ah
+        "0fb6c4"        # movzx eax, ah
+        "480fbecd"      # movsx rcx, ch
+        "8827"          # mov [rdi], ah
+        "8a7701"        # mov dh, [rdi+1]
+        "0067 02"       # add [rdi+2], ah
+        "8467 03"       # test [rdi+3], ah
+        .replace(" ", ""))
+    page = BUF & ~0xFFF
+    win = bytearray(range(256)) * 2
+    L = sim_lib()
+    sp, regs = layout(code, page, bytes(win))
+    regs.gpr[0], regs.gpr[1], regs.gpr[2], regs.gpr[3] = (0x1122334455667788, 0x99AABBCCDDEEFF10,
+                                                          0x0F1E2D3C4B5A6978, 0x8070605040302010)
+    regs.gpr[7] = page
+    slow, fast, n = run_both(L, sp, regs, page)
+    assert same(slow, fast)
+    assert n == 20, n  # every form ran fast
+    pfns, blob = sp.phys()
+    o = Oracle(pfns=pfns, blob=blob)
+    o.restore(regs)
+    ex = o.run()
+    r = o.regs()
+    assert ex.status == INT3 and o.icount() == fast.icount
+    assert [int(x) for x in fast.gpr] == list(r.gpr) and fast.rflags == r.rflags
+    assert o.read_virt(page, 256) == bytes(fast.win[:256])

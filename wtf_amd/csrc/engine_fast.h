@@ -64,6 +64,7 @@ enum : u32 {
 };
 
 constexpr u32 NOREG = 16;
+constexpr u32 FR_HB = 32;  // register field flag: the high byte (bits 15:8) of register & 3
 
 struct FOp {
   u32 w0;  // op | sub << 8 | sz << 12 | szb << 16 | len << 20 | scale << 26 | riprel << 28 | seg << 29 (1 fs, 2 gs)
@@ -132,7 +133,15 @@ __device__ __forceinline__ void digest(const UOp &u, FOp &f) {
   const bool bmem = u.bsrc == L_RM && u.is_mem;
   const bool areg = ra != NOREG, breg = rb != NOREG, bimm = u.bsrc == L_IMM;
   // high-byte registers (ah/ch/dh/bh) stay on the generic path
-  const bool hb = !u.rex && ((u.asz == 1 && areg && ra >= 4 && ra < 8) || (u.bsz == 1 && breg && rb >= 4 && rb < 8));
+  // high-byte registers (ah / ch / dh / bh: an 8-bit register 4..7 without
+  // REX) are register (r & 3) with bit FR_HB: read shifted down by 8, written
+  // merged into bits 15:8 (ops whose a / b / destination go through the
+  // pipeline below; the rest stay generic)
+  const bool hba = !u.rex && u.asz == 1 && areg && ra >= 4 && ra < 8;
+  const bool hbb = !u.rex && u.bsz == 1 && breg && rb >= 4 && rb < 8;
+  const bool hb = (hba || hbb) &&
+                  !(u.op == O_ALU || u.op == O_TEST || u.op == O_MOV || u.op == O_MOVZX || u.op == O_MOVSX ||
+                    u.op == O_INCDEC || u.op == O_NOT || u.op == O_NEG || u.op == O_SETCC || u.op == O_SHIFT);
   u64 imm = u.imm;
   u32 ra_ = ra, rb_ = rb, sz_ = u.asz;
   if (u.op == O_SSE && u.supported && !u.seg && !u.p67) {
@@ -225,6 +234,8 @@ __device__ __forceinline__ void digest(const UOp &u, FOp &f) {
     // (lea computes the offset alone: generic too)
     if (u.seg && (!(fl & FF_EA) || op == FO_LEA)) op = FO_GENERIC;
   }
+  if (hba) ra_ = (ra - 4) | FR_HB;
+  if (hbb) rb_ = (rb - 4) | FR_HB;
   const u32 base = u.base >= 0 ? (u32)u.base : NOREG, index = u.index >= 0 ? (u32)u.index : NOREG;
   const u32 fseg = u.seg == 4 ? 1 : u.seg == 5 ? 2 : 0;
   f.w0 = op | (sub & 0xf) << 8 | (sz_ & 0xf) << 12 | (u.bsz & 0xf) << 16 | (u.len & 0x3f) << 20 |
@@ -414,8 +425,8 @@ __device__ __forceinline__ int fast_exec(const FastMem &M, Lane &L, const FOp &f
   if (!kRegOnly && op >= FO_VLD) {
     ok = fast_vec(M.full, L, f, nrip) == X_OK;  // xmm / ymm state only (memory), no GPR
   } else {
-    u64 a = (F & FF_AREG) ? R(L, fo_ra(f)) : 0;
-    u64 b = (F & FF_BREG) ? R(L, fo_rb(f)) : f.imm;
+    u64 a = (F & FF_AREG) ? R(L, fo_ra(f)) >> ((fo_ra(f) & FR_HB) >> 2) : 0;
+    u64 b = (F & FF_BREG) ? R(L, fo_rb(f)) >> ((fo_rb(f) & FR_HB) >> 2) : f.imm;
     u64 addr = 0;
     if (F & FF_EA) {
       addr = f.disp + (fo_riprel(f) ? nrip : 0);
@@ -517,20 +528,20 @@ __device__ __forceinline__ int fast_exec(const FastMem &M, Lane &L, const FOp &f
 #if WTFGPU_FAST_WB_ALWAYS
   const u64 nrsp = !ok ? rsp : (F & FF_PUSH) ? rsp - 8 : (F & FF_POP) ? rsp + 8 + (op == FO_RET ? f.imm : 0) : rsp;
   RS(L, 4, nrsp);
-  const u32 wi = fo_ra(f) & 15;
-  const u64 old = R(L, wi), mk = szmask(sz);
+  const u32 wi = fo_ra(f) & 15, hs = (fo_ra(f) & FR_HB) >> 2;
+  const u64 old = R(L, wi), mk = szmask(sz) << hs;
   // wr(): 8 / 4 bytes replace (4 zero-extends), 2 / 1 merge into the old value
-  const u64 nv = (ok && (F & FF_WRA)) ? (sz >= 4 ? (res & mk) : ((old & ~mk) | (res & mk))) : old;
+  const u64 nv = (ok && (F & FF_WRA)) ? (sz >= 4 ? (res & mk) : ((old & ~mk) | ((res << hs) & mk))) : old;
   RS(L, wi, nv);
 #else
   // (written under the op's uniform flags: ops that write no register skip
   // the indexed read-back and write)
   if (F & (FF_PUSH | FF_POP)) RS(L, 4, !ok ? rsp : (F & FF_PUSH) ? rsp - 8 : rsp + 8 + (op == FO_RET ? f.imm : 0));
   if (F & FF_WRA) {
-    const u32 wi = fo_ra(f) & 15;
-    const u64 old = R(L, wi), mk = szmask(sz);
+    const u32 wi = fo_ra(f) & 15, hs = (fo_ra(f) & FR_HB) >> 2;  // hs: 8 for a high-byte register
+    const u64 old = R(L, wi), mk = szmask(sz) << hs;
     // wr(): 8 / 4 bytes replace (4 zero-extends), 2 / 1 merge into the old value
-    RS(L, wi, ok ? (sz >= 4 ? (res & mk) : ((old & ~mk) | (res & mk))) : old);
+    RS(L, wi, ok ? (sz >= 4 ? (res & mk) : ((old & ~mk) | ((res << hs) & mk))) : old);
   }
 #endif
   if (ok && (F & FF_FLAGS)) L.rflags = fl;
