@@ -361,3 +361,44 @@ def test_high_byte_register_forms_fast_equals_slow_and_oracle():
     assert ex.status == INT3 and o.icount() == fast.icount
     assert [int(x) for x in fast.gpr] == list(r.gpr) and fast.rflags == r.rflags
     assert o.read_virt(page, 256) == bytes(fast.win[:256])
+
+
+def test_system_call_forms_fast_equals_slow_and_oracle():
+    """syscall, swapgs and sysretq (REX.W) on the fast path (FO_SYS): a user
+    syscall into a kernel stub that swaps gs twice and returns; registers, rip,
+    rflags match the generic path and the oracle, and the forms run fast. At
+    ring 3, swapgs and sysretq leave the fast attempt: the slow step raises
+    #GP as exec() does."""
+    from tests.test_sse import CODE_VA
+    code = bytes.fromhex(
+        "0f05"                  # 0  syscall -> lstar = 8
+        "cc" "cccccccccc"       # 2  int3 (sysretq returns here)
+        "0f01f8"                # 8  swapgs
+        "48c7c034120000"        # 11 mov rax, 0x1234
+        "0f01f8"                # 18 swapgs
+        "480f07")               # 21 sysretq
+    page = BUF & ~0xFFF
+    L = sim_lib()
+    sp, regs = layout(code, page, bytes(256))
+    regs.cr4 &= ~(3 << 20)  # no SMEP / SMAP: the stub runs on the test's user code page
+    regs.lstar = CODE_VA + 8
+    regs.kernel_gs_base = 0xAAAA000
+    regs.seg[5].base = 0xBBBB000
+    regs.gpr[11] = 0x55
+    slow, fast, n = run_both(L, sp, regs, page)
+    assert same(slow, fast)
+    assert fast.status == INT3 and fast.rip == CODE_VA + 2, (fast.status, hex(fast.rip))
+    assert fast.gpr[0] == 0x1234 and fast.gpr[1] == CODE_VA + 2
+    assert n == 5, n
+    pfns, blob = sp.phys()
+    o = Oracle(pfns=pfns, blob=blob)
+    o.restore(regs)
+    ex = o.run()
+    r = o.regs()
+    assert ex.status == INT3 and o.icount() == fast.icount
+    assert [int(x) for x in fast.gpr] == list(r.gpr) and fast.rflags == r.rflags
+    # ring 3: swapgs / sysretq are #GP(0), raised by the slow step
+    for op in ("0f01f8", "480f07"):
+        sp, regs = layout(bytes.fromhex(op), page, bytes(256))
+        slow, fast, n = run_both(L, sp, regs, page)
+        assert same(slow, fast) and (fast.status, fast.vector) == (EXIT_FAULT, 13) and n == 0, (op, fast.status)
