@@ -1323,7 +1323,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
 #endif
 #if WTFGPU_FAST_REGOPS
       // a form that touches no memory cannot miss: one pass, no retry rounds
-      if (!(f.fl & (FF_PUSH | FF_POP | FF_MR_A | FF_MR_B | FF_MW | FF_MAYMISS)) && fo_op(f) < FO_VLD) {
+      if (!(f.fl & (FF_PUSH | FF_POP | FF_MR_A | FF_MR_B | FF_MW)) && fo_op(f) < FO_VLD) {
         steps++;
         have = false;
         if (ing) {

@@ -41,8 +41,6 @@ enum : u32 {
   FO_SETCC,   // res = cond(sub)
   FO_BT,      // bt / bts / btr / btc (sub 4..7) of register a, bit b: CF, res
   FO_UNARY,   // sub 0: res = ~a (not); sub 1: res = 0 - a, flags (neg)
-  FO_SYS,     // sub 0 syscall, 1 sysretq (REX.W), 2 swapgs: exec()'s O_SYS forms; a lane that
-              // would fault (#GP / #UD) leaves the attempt (miss 1) for the slow step to raise it
   // SSE / AVX data movement (engine_sse.h semantics), ra = the xmm / ymm
   // register, sz = operand bytes / 8; sub bit 0: aligned form, bit 1: VEX
   // (VEX.128 zeroes bits 255:128), bit 2 (FO_VMOV): the zeroing xor idiom
@@ -63,7 +61,6 @@ enum : u32 {
   FF_MW = 128,      // memory write of res at the address
   FF_WRA = 256,     // register write of res into ra
   FF_FLAGS = 512,   // rflags updated by the op
-  FF_MAYMISS = 1024,  // no memory operand, but the attempt can leave for the slow step (FO_SYS)
 };
 
 constexpr u32 NOREG = 16;
@@ -229,9 +226,6 @@ __device__ __forceinline__ void digest(const UOp &u, FOp &f) {
         break;
       case O_SETCC:
         if (areg) op = FO_SETCC, fl = FF_WRA;
-        break;
-      case O_SYS:  // the kernel-entry / exit forms of a system-call path (HEVD's KiSystemCall64)
-        if (u.sub == 0 || u.sub == 2 || (u.sub == 1 && (u.rex & 8))) op = FO_SYS, fl = FF_FLAGS | FF_MAYMISS;
         break;
       default: break;
     }
@@ -516,43 +510,6 @@ __device__ __forceinline__ int fast_exec(const FastMem &M, Lane &L, const FOp &f
         res = cond(fl, sub) ? b : a;
         break;
       case FO_SETCC: res = cond(fl, sub) ? 1 : 0; break;
-      case FO_SYS: {  // exec()'s O_SYS sub 0 / 1 / 2 (engine_ops.h), the checks first
-        LaneSys &S = M.P->sys[L.lane];
-        if (sub == 2) {  // swapgs
-          if (L.cpl != 0) {
-            L.miss = 1;
-            ok = false;
-            break;
-          }
-          u64 *gs = M.P->gs_base;
-          const u64 g = gs[L.lane];
-          gs[L.lane] = S.kgs;
-          S.kgs = g;
-          break;
-        }
-        if (!(L.efer & 1) || (sub == 1 && (L.cpl != 0 || !canonical(R(L, 1))))) {
-          L.miss = 1;
-          ok = false;
-          break;
-        }
-        if (sub == 0) {  // syscall
-          RS(L, 1, nrip);
-          RS(L, 11, fl & ~0x10000ull);
-          fl = ((fl & ~S.sfmask) & ~0x10000ull) | 2;
-          next = S.lstar;
-          L.cpl = S.cpl = 0;
-          S.cs = (u16)((S.star >> 32) & 0xfffc);
-          S.ss = (u16)(S.cs + 8);
-        } else {  // sysretq
-          fl = (R(L, 11) & 0x3c7fd7ull) | 2;
-          next = R(L, 1);
-          L.cpl = S.cpl = 3;
-          S.cs = (u16)((((S.star >> 48) & 0xffff) + 16) | 3);
-          S.ss = (u16)((((S.star >> 48) & 0xffff) + 8) | 3);
-        }
-        tlb_flush(L);  // exec()'s L.flush: cached translations were checked at the old cpl
-        break;
-      }
       default: break;
     }
     // ---- the memory write
