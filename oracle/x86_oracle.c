@@ -331,31 +331,19 @@ enum { ACC_R = 0, ACC_W = 1, ACC_X = 2 };
 #define PTE_ADDR 0x000ffffffffff000ULL
 
 static int cpl(orc_machine *m) { return m->r.seg[WTFGPU_CS].selector & 3; }
+/* 32-bit code (compatibility mode, U29): CS is SYSRET's 32-bit selector,
+ * STAR[63:48] (the one CS.L = 0 code segment of Windows' and Linux' GDTs;
+ * descriptors are not read, U19). bochscpu.hpp:119-182 carries the segment
+ * cache whose CS.L the reference's core reads. */
+static int is_m32(orc_machine *m) {
+  return ((m->r.seg[WTFGPU_CS].selector ^ (u32)(m->r.star >> 48)) & 0xfffc) == 0;
+}
 
 static int is_canonical(u64 va) {
   i64 s = (i64)(va << 16) >> 16;
   return (u64)s == va;
 }
 
-/* would a ring-3 instruction fetch at va translate (present, user,
- * executable)? SYSRET without REX.W enters compatibility mode at ecx: the
- * oracle runs no 32-bit code, so that SYSRET is UNIMPLEMENTED when the fetch
- * would succeed, and otherwise its first fetch faults as the host's would (U29) */
-static int user_fetch_ok(orc_machine *m, u64 va) {
-  if (!is_canonical(va)) return 0;
-  const int nxe = (m->r.efer >> 11) & 1;
-  u64 table = m->r.cr3 & 0x000ffffffffff000ULL, e = 0;
-  int u = 1, nx = 0;
-  for (int level = 3; level >= 0; level--) {
-    e = phys_read64(m, table + ((va >> (12 + 9 * level)) & 0x1ff) * 8);
-    if (!(e & 1)) return 0;
-    u &= (e & 4) != 0;
-    if (nxe && (e >> 63)) nx = 1;
-    if (level > 0 && level < 3 && (e & 0x80)) break;
-    table = e & 0x000ffffffffff000ULL;
-  }
-  return u && !nx;
-}
 
 /* 4-level walk; check: perform permission checks. Returns 0 ok, else sets fault. */
 static int walk(orc_machine *m, u64 va, int acc, int check, u64 *pa) {
@@ -573,6 +561,7 @@ typedef struct {
   u32 pfx66, pfx67, rep, lock, seg; /* seg: 0 none, 4 fs, 5 gs */
   u32 rex, rexw, rexr, rexx, rexb;
   u32 opmap; /* 0 one-byte, 1 = 0F, 2 = 0F38, 3 = 0F3A */
+  u32 m32, a16; /* 32-bit code (U29); a 67 prefix there (16-bit addresses: outside) */
   u32 undef; /* U36: an encoding the emulated CPU does not define (#UD) */
   u32 vex, vl, vw, vvvv, vpp, vbad; /* VEX prefix: present, L, W, vvvv (decoded), pp; a legacy prefix before it */
   u32 op;
@@ -657,7 +646,7 @@ static void decode_modrm(orc_machine *m, insn *d, memref *mr) {
       mr->base = (int)(base | (d->rexb << 3));
     }
   } else if (rm == 5 && d->mod == 0) {
-    mr->riprel = 1;
+    mr->riprel = !d->m32; /* 32-bit code: disp32 absolute */
     mr->disp = sxn(fetchn(m, d, 4), 4);
   } else {
     mr->base = (int)(rm | (d->rexb << 3));
@@ -888,16 +877,19 @@ static u64 shift_op(orc_machine *m, int op, u64 v, u32 count, int sz) {
 }
 
 /* ---------------- stack ---------------- */
+/* 32-bit code addresses the stack with esp (U29: the result zero-extends) */
+static u64 smask(orc_machine *m) { return is_m32(m) ? 0xffffffffULL : ~0ULL; }
 static int push64(orc_machine *m, u64 v, int sz) {
-  u64 rsp = m->r.gpr[WTFGPU_RSP] - (u64)sz;
+  u64 rsp = (m->r.gpr[WTFGPU_RSP] - (u64)sz) & smask(m);
   if (vwrite(m, rsp, (u32)sz, &v)) return -1;
   m->r.gpr[WTFGPU_RSP] = rsp;
   return 0;
 }
 static int pop64(orc_machine *m, u64 *v, int sz) {
   u64 t = 0;
-  if (vread(m, m->r.gpr[WTFGPU_RSP], (u32)sz, &t)) return -1;
-  m->r.gpr[WTFGPU_RSP] += (u64)sz;
+  const u64 sm = smask(m);
+  if (vread(m, m->r.gpr[WTFGPU_RSP] & sm, (u32)sz, &t)) return -1;
+  m->r.gpr[WTFGPU_RSP] = ((m->r.gpr[WTFGPU_RSP] & sm) + (u64)sz) & sm;
   *v = t;
   return 0;
 }
@@ -2242,6 +2234,35 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
     fault(m, WTFGPU_VEC_UD, 0);
     return X_FAULT;
   }
+  /* 32-bit code (U29): stack slots and near branch targets are 32-bit; 16-bit
+   * addresses (67) and 16-bit instruction pointers (66 on a near branch) are outside */
+  const int stk = d->pfx66 ? 2 : (d->m32 ? 4 : 8), nsz = d->m32 ? 4 : 8;
+  const u64 sm = d->m32 ? 0xffffffffULL : ~0ULL;
+  if (d->m32 && (d->a16 || (d->pfx66 && ((d->opmap == 0 && ((op >= 0x70 && op <= 0x7f) || (op >= 0xe0 && op <= 0xe3) ||
+                                                         op == 0xe8 || op == 0xe9 || op == 0xeb || op == 0xc2 ||
+                                                         op == 0xc3 || (op == 0xff && ((d->reg & 7) == 2 || (d->reg & 7) == 4)))) ||
+                                        (d->opmap == 1 && op >= 0x80 && op <= 0x8f)))))
+    return X_UNIMPL;
+  if (d->m32 && d->opmap == 0 && !d->vex) {
+    if (op >= 0x40 && op <= 0x4f) { /* inc / dec r32 */
+      const u32 r = op & 7;
+      a = getreg(m, d, r, osz);
+      const u64 cf = m->r.rflags & RF_CF;
+      res = alu2(m, op < 0x48 ? 0 : 5, a, 1, osz);
+      m->r.rflags = (m->r.rflags & ~RF_CF) | cf;
+      setreg(m, d, r, osz, res);
+      return X_OK;
+    }
+    switch (op) {
+    case 0x06: case 0x07: case 0x0e: case 0x16: case 0x17: case 0x1e: case 0x1f: case 0x27: case 0x2f:
+    case 0x37: case 0x3f: case 0x60: case 0x61: case 0x9a: case 0xce: case 0xd4: case 0xd5: case 0xea:
+      return exec_sys32(m, d, next_rip);
+    case 0x62: case 0x63: case 0xc4: case 0xc5: case 0xd6: /* bound, arpl, les / lds, salc */
+      return X_UNIMPL;
+    default:
+      break;
+    }
+  }
 
   if (d->opmap == 0) {
     /* ALU ops 00-3f */
@@ -2277,13 +2298,13 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
     }
     switch (op) {
     case 0x50: case 0x51: case 0x52: case 0x53: case 0x54: case 0x55: case 0x56: case 0x57: {
-      const int sz = d->pfx66 ? 2 : 8;
+      const int sz = stk;
       const u32 r = (op & 7) | (d->rexb << 3);
       CHK(push64(m, m->r.gpr[r] & szmask(sz), sz));
       return X_OK;
     }
     case 0x58: case 0x59: case 0x5a: case 0x5b: case 0x5c: case 0x5d: case 0x5e: case 0x5f: {
-      const int sz = d->pfx66 ? 2 : 8;
+      const int sz = stk;
       const u32 r = (op & 7) | (d->rexb << 3);
       CHK(pop64(m, &a, sz));
       setreg(m, d, r, sz, a);
@@ -2295,7 +2316,7 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
       return X_OK;
     case 0x68:
     case 0x6a: {
-      const int sz = d->pfx66 ? 2 : 8;
+      const int sz = stk;
       int isz = op == 0x6a ? 1 : (d->pfx66 ? 2 : 4);
       memcpy(&a, d->bytes + d->len - isz, (size_t)isz);
       a = sxn(a, isz) & szmask(sz);
@@ -2383,11 +2404,11 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
         fault(m, WTFGPU_VEC_UD, 0);
         return X_FAULT;
       }
-      const int sz = d->pfx66 ? 2 : 8;
+      const int sz = stk;
       /* pop r/m: the address is computed with rsp already incremented */
       u64 rsp0 = m->r.gpr[WTFGPU_RSP];
-      CHK(vread(m, rsp0, (u32)sz, &a) ? 1 : 0);
-      m->r.gpr[WTFGPU_RSP] = rsp0 + (u64)sz;
+      CHK(vread(m, rsp0 & sm, (u32)sz, &a) ? 1 : 0);
+      m->r.gpr[WTFGPU_RSP] = ((rsp0 & sm) + (u64)sz) & sm;
       if (d->is_mem) finish_ea(m, d, mr);
       if (wr_rm(m, d, sz, a)) {
         m->r.gpr[WTFGPU_RSP] = rsp0;
@@ -2418,12 +2439,12 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
       setreg(m, d, WTFGPU_RDX, osz, msb(m->r.gpr[0], osz) ? ~0ULL : 0);
       return X_OK;
     case 0x9c: { /* pushf */
-      const int sz = d->pfx66 ? 2 : 8;
+      const int sz = stk;
       CHK(push64(m, m->r.rflags & 0xfcffffULL & szmask(sz), sz));
       return X_OK;
     }
     case 0x9d: { /* popf */
-      const int sz = d->pfx66 ? 2 : 8;
+      const int sz = stk;
       CHK(pop64(m, &a, sz));
       u64 mask = RF_STATUS | RF_TF | RF_DF | 0x4000ULL /*NT*/ | 0x40000ULL /*AC*/ | 0x200000ULL /*ID*/;
       if (cpl(m) == 0) mask |= RF_IF | 0x3000ULL;
@@ -2493,10 +2514,11 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
     }
     case 0xc2:
     case 0xc3: {
-      CHK(vread(m, m->r.gpr[WTFGPU_RSP], 8, &a));
+      a = 0;
+      CHK(vread(m, m->r.gpr[WTFGPU_RSP] & sm, (u32)nsz, &a));
       u64 extra = 0;
       if (op == 0xc2) extra = (u64)d->bytes[d->len - 2] | ((u64)d->bytes[d->len - 1] << 8);
-      m->r.gpr[WTFGPU_RSP] += 8 + extra;
+      m->r.gpr[WTFGPU_RSP] = ((m->r.gpr[WTFGPU_RSP] & sm) + (u64)nsz + extra) & sm;
       *next_rip = a;
       return X_OK;
     }
@@ -2515,16 +2537,17 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
       return X_OK;
     }
     case 0xc9: { /* leave */
-      u64 rbp = m->r.gpr[WTFGPU_RBP];
-      CHK(vread(m, rbp, 8, &a));
-      m->r.gpr[WTFGPU_RSP] = rbp + 8;
+      u64 rbp = m->r.gpr[WTFGPU_RBP] & sm;
+      a = 0;
+      CHK(vread(m, rbp, (u32)nsz, &a));
+      m->r.gpr[WTFGPU_RSP] = (rbp + (u64)nsz) & sm;
       m->r.gpr[WTFGPU_RBP] = a;
       return X_OK;
     }
     case 0xcc:
       return X_INT3;
     case 0xcf: { /* iretq (U19); iret / iretd with 16- / 32-bit slots (U29) */
-      if (!d->rexw) return far_pop(m, osz, 0, next_rip, 1);
+      if (!d->rexw) return far_pop(m, osz, 0, next_rip, 1, (int)d->m32);
       u64 f[5]; /* rip, cs, rflags, rsp, ss: every read before any change */
       for (int i = 0; i < 5; i++) CHK(vread(m, m->r.gpr[WTFGPU_RSP] + 8 * (u64)i, 8, &f[i]));
       const u32 ocpl = (u32)cpl(m), ncpl = (u32)f[1] & 3;
@@ -2560,7 +2583,7 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
     case 0xe8: {
       u64 rel = 0;
       memcpy(&rel, d->bytes + d->len - 4, 4);
-      CHK(push64(m, nrip, 8));
+      CHK(push64(m, nrip, nsz));
       *next_rip = nrip + sxn(rel, 4);
       return X_OK;
     }
@@ -2578,10 +2601,32 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
     /* invalid in 64-bit mode: push / pop es cs ss ds, daa das aaa aas, pusha
      * popa, 82 (alias of 80), far call / jmp, aam aad salc (SDM opcode map, i64) */
     case 0x06: case 0x07: case 0x0e: case 0x16: case 0x17: case 0x1e: case 0x1f: case 0x27:
-    case 0x2f: case 0x37: case 0x3f: case 0x60: case 0x61: case 0x82: case 0x9a: case 0xd4:
+    case 0x2f: case 0x37: case 0x3f: case 0x60: case 0x61: case 0x9a: case 0xd4:
     case 0xd5: case 0xd6: case 0xea:
       fault(m, WTFGPU_VEC_UD, 0);
       return X_FAULT;
+    case 0x82: /* 80's alias in 32-bit code */
+      if (!d->m32) {
+        fault(m, WTFGPU_VEC_UD, 0);
+        return X_FAULT;
+      }
+      {
+        b = sxn(d->bytes[d->len - 1], 1);
+        const int aluop = (int)(d->reg & 7);
+        if (aluop == 7) {
+          CHK(rd_rm(m, d, 1, &a));
+          alu2(m, 7, a, b, 1);
+        } else {
+          CHK(rd_rm_rmw(m, d, 1, &a));
+          const u64 saved = m->r.rflags;
+          res = alu2(m, aluop, a, b, 1);
+          if (wr_rm(m, d, 1, res)) {
+            m->r.rflags = saved;
+            return X_FAULT;
+          }
+        }
+      }
+      return X_OK;
     case 0x62: /* EVEX: AVX-512, defined, not executed (U45) */
       return X_UNIMPL;
     case 0xce: /* into: invalid in 64-bit mode */
@@ -2633,33 +2678,34 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
         return X_FAULT;
       }
       return X_OK;
-    case 0xc8: { /* enter (U29): bochs' ENTER64 order */
+    case 0xc8: { /* enter (U29): bochs' ENTER64 order (32-bit slots in 32-bit code) */
       if (d->pfx66) return X_UNIMPL;
       const u64 size = (u64)d->bytes[d->len - 3] | ((u64)d->bytes[d->len - 2] << 8);
       const u32 level = d->bytes[d->len - 1] & 31;
-      u64 rsp = m->r.gpr[WTFGPU_RSP], rbp = m->r.gpr[WTFGPU_RBP];
-      CHK(span_check(m, rsp - 8 * (level + 1), 8 * (level + 1), ACC_W));
-      rsp -= 8;
-      CHK(vwrite(m, rsp, 8, &rbp));
+      const u32 w = (u32)nsz;
+      u64 rsp = m->r.gpr[WTFGPU_RSP] & sm, rbp = m->r.gpr[WTFGPU_RBP] & sm;
+      CHK(span_check(m, (rsp - w * (level + 1)) & sm, w * (level + 1), ACC_W));
+      rsp = (rsp - w) & sm;
+      CHK(vwrite(m, rsp, w, &rbp));
       const u64 frame = rsp;
       if (level > 0) {
         for (u32 i = 1; i < level; i++) {
-          rbp -= 8;
+          rbp = (rbp - w) & sm;
           u64 t = 0;
-          CHK(vread(m, rbp, 8, &t));
-          rsp -= 8;
-          CHK(vwrite(m, rsp, 8, &t));
+          CHK(vread(m, rbp, w, &t));
+          rsp = (rsp - w) & sm;
+          CHK(vwrite(m, rsp, w, &t));
         }
-        rsp -= 8;
-        CHK(vwrite(m, rsp, 8, &frame));
+        rsp = (rsp - w) & sm;
+        CHK(vwrite(m, rsp, w, &frame));
       }
       m->r.gpr[WTFGPU_RBP] = frame;
-      m->r.gpr[WTFGPU_RSP] = rsp - size;
+      m->r.gpr[WTFGPU_RSP] = (rsp - size) & sm;
       return X_OK;
     }
     case 0xca: case 0xcb: { /* far ret (U29): 32-bit operand size unless REX.W / 66 */
       const u64 imm = op == 0xca ? ((u64)d->bytes[d->len - 2] | ((u64)d->bytes[d->len - 1] << 8)) : 0;
-      return far_pop(m, osz, imm, next_rip, 0);
+      return far_pop(m, osz, imm, next_rip, 0, (int)d->m32);
     }
     case 0xcd: { /* int n (U24) */
       const u32 vec = d->bytes[d->len - 1];
@@ -2766,25 +2812,25 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
         }
         const u16 ncs = (u16)((sel & 0xfffc) | (u32)cpl(m));
         if (sub == 3) {
-          const u64 rsp = m->r.gpr[WTFGPU_RSP];
+          const u64 rsp = m->r.gpr[WTFGPU_RSP] & sm;
           const u64 ocs = m->r.seg[WTFGPU_CS].selector;
-          CHK(span_check(m, rsp - 2 * (u64)osz, 2 * (u32)osz, ACC_W));
-          CHK(vwrite(m, rsp - (u64)osz, (u32)osz, &ocs));
-          CHK(vwrite(m, rsp - 2 * (u64)osz, (u32)osz, &nrip));
-          m->r.gpr[WTFGPU_RSP] = rsp - 2 * (u64)osz;
+          CHK(span_check(m, (rsp - 2 * (u64)osz) & sm, 2 * (u32)osz, ACC_W));
+          CHK(vwrite(m, (rsp - (u64)osz) & sm, (u32)osz, &ocs));
+          CHK(vwrite(m, (rsp - 2 * (u64)osz) & sm, (u32)osz, &nrip));
+          m->r.gpr[WTFGPU_RSP] = (rsp - 2 * (u64)osz) & sm;
         }
         m->r.seg[WTFGPU_CS].selector = ncs;
         *next_rip = off;
         return X_OK;
       }
-      if (sub == 2 || sub == 4) { /* call / jmp near indirect (64-bit) */
-        CHK(rd_rm(m, d, 8, &a));
-        if (sub == 2) CHK(push64(m, nrip, 8));
+      if (sub == 2 || sub == 4) { /* call / jmp near indirect (64-bit; 32-bit in 32-bit code) */
+        CHK(rd_rm(m, d, nsz, &a));
+        if (sub == 2) CHK(push64(m, nrip, nsz));
         *next_rip = a;
         return X_OK;
       }
       if (sub == 6) { /* push r/m */
-        const int psz = d->pfx66 ? 2 : 8;
+        const int psz = stk;
         CHK(rd_rm(m, d, psz, &a));
         CHK(push64(m, a, psz));
         return X_OK;
@@ -2828,13 +2874,12 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
         m->r.gpr[1] = nrip;
         m->r.gpr[11] = m->r.rflags & ~0x10000ULL;
         m->r.rflags = ((m->r.rflags & ~m->r.sfmask) & ~0x10000ULL) | 2;
-        *next_rip = m->r.lstar;
+        *next_rip = d->m32 ? m->r.cstar : m->r.lstar; /* from 32-bit code: CSTAR (U29) */
         m->r.seg[WTFGPU_CS].selector = (u16)((m->r.star >> 32) & 0xfffc);
         m->r.seg[WTFGPU_SS].selector = (u16)(m->r.seg[WTFGPU_CS].selector + 8);
       } else {
-        if (cpl(m) == 0 && !d->rexw) { /* to compatibility mode (U29): see user_fetch_ok */
+        if (cpl(m) == 0 && !d->rexw) { /* to compatibility mode at ecx (U29) */
           const u64 t32 = m->r.gpr[1] & 0xffffffffULL;
-          if (user_fetch_ok(m, t32)) return X_UNIMPL;
           *next_rip = t32;
           m->r.rflags = (m->r.gpr[11] & 0x3c7fd7ULL) | 2;
           m->r.seg[WTFGPU_CS].selector = (u16)(((m->r.star >> 48) & 0xffff) | 3);
@@ -3178,12 +3223,13 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
   memset(d, 0, sizeof(*d));
   memset(mr, 0, sizeof(*mr));
   d->start = m->r.rip;
+  d->m32 = (u32)is_m32(m);
   u8 b;
   /* legacy prefixes and REX; a REX not immediately before the opcode is ignored */
   for (;;) {
     b = fetch8(m, d);
     if (d->fetch_fail) return -1;
-    if ((b & 0xf0) == 0x40) {
+    if ((b & 0xf0) == 0x40 && !d->m32) {
       d->rex = b;
       continue;
     }
@@ -3203,7 +3249,19 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
     d->rexx = (d->rex >> 1) & 1;
     d->rexb = d->rex & 1;
   }
-  if (b == 0xc4 || b == 0xc5) { /* VEX (always VEX in 64-bit mode) */
+  if (d->m32) { /* 32-bit addresses; 67 would make them 16-bit (outside) */
+    d->a16 = d->pfx67;
+    d->pfx67 = 1;
+  }
+  int les = 0; /* 32-bit code: c4 / c5 are les / lds unless the next byte's mod is 11 */
+  if (d->m32 && (b == 0xc4 || b == 0xc5)) {
+    const u64 save = d->pos;
+    const u8 nb = fetch8(m, d);
+    if (d->fetch_fail) return -1;
+    les = (nb & 0xc0) != 0xc0;
+    d->pos = (u32)save;
+  }
+  if ((b == 0xc4 || b == 0xc5) && !les) { /* VEX (always VEX in 64-bit mode) */
     d->vex = 1;
     d->vbad = d->pfx66 || d->rep || d->rex;
     const u8 b1 = fetch8(m, d);
@@ -3211,12 +3269,12 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
     if (d->fetch_fail) return -1;
     d->rexr = !((b1 >> 7) & 1);
     d->rexx = b == 0xc4 ? !((b1 >> 6) & 1) : 0;
-    d->rexb = b == 0xc4 ? !((b1 >> 5) & 1) : 0;
+    d->rexb = (b == 0xc4 && !d->m32) ? !((b1 >> 5) & 1) : 0;
     d->opmap = b == 0xc4 ? (b1 & 31u) : 1;
     d->vw = b == 0xc4 ? (b2 >> 7) & 1u : 0;
     d->rexw = d->vw;
     d->rex = 0x40 | (d->rexw << 3) | (d->rexr << 2) | (d->rexx << 1) | d->rexb;
-    d->vvvv = (~b2 >> 3) & 15u;
+    d->vvvv = (~b2 >> 3) & (d->m32 ? 7u : 15u);
     d->vl = (b2 >> 2) & 1u;
     d->vpp = b2 & 3u;
     b = fetch8(m, d);
@@ -3313,6 +3371,15 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
     case 0x6b: case 0x80: case 0x83: case 0xc0: case 0xc1: case 0xc6:
       has_modrm = 1;
       imm = 1;
+      break;
+    case 0x82: /* 32-bit code: 80's alias */
+      if (d->m32) has_modrm = imm = 1;
+      break;
+    case 0x9a: case 0xea: /* 32-bit code: far call / jmp ptr16:32 */
+      if (d->m32) imm = osz + 2;
+      break;
+    case 0xd4: case 0xd5: /* 32-bit code: aam / aad imm8 */
+      if (d->m32) imm = 1;
       break;
     case 0x81: case 0xc7:
       has_modrm = 1;
@@ -3503,6 +3570,7 @@ static int one(orc_machine *m, int check_bp, wtfgpu_exit_t *ex) {
   m->tn_last = ~0ULL;
   m->tn_mute = 0;
   int x = exec_insn(m, &d, &mr, &next);
+  if (d.m32 && x == X_OK && is_m32(m)) next &= 0xffffffffULL; /* 32-bit code stays below 4 GiB (U29) */
   /* RecordEdge (bochscpu_backend.cc:699-728, hooks :235-257, :308-312): jcc
    * taken or not, indirect near jmp / call; before the retire hook */
   if (m->edges && x == X_OK &&

@@ -68,7 +68,7 @@ int sim_run_full(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, c
   sys.cr0 = r0->cr0;
   sys.cr3 = r0->cr3;
   sys.cr4 = r0->cr4;
-  sys.efer = r0->efer;
+  sys.efer = (r0->efer & ~EFER_M32) | (compat_sel(r0->star, r0->seg[WTFGPU_CS].selector) ? EFER_M32 : 0);  // make_init
   sys.cpl = r0->seg[WTFGPU_CS].selector & 3;
   sys.star = r0->star;
   sys.lstar = r0->lstar;
@@ -92,7 +92,7 @@ int sim_run_full(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, c
   L.rflags = r0->rflags;
   L.cr0 = r0->cr0;
   L.cr3 = r0->cr3;
-  L.efer = r0->efer;
+  L.efer = sys.efer;  // as load_lane (U29)
   L.cpl = r0->seg[WTFGPU_CS].selector & 3;
   L.status = WTFGPU_RUNNING;
   L.simd = simd_bits(r0->cr0, r0->cr4, r0->xcr0);
@@ -123,7 +123,8 @@ int sim_run_full(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, c
     UOp d;
     memcpy(&ib.lo, bytes, 8);
     memcpy(&ib.hi, bytes + 8, 8);
-    int dr = decode(ib, d);
+    const bool m32 = (L.efer & EFER_M32) != 0;  // 32-bit code: slow_step's decode, never the fast path (U29)
+    int dr = decode(ib, d, m32);
     if (dr == 1) {
       const uint64_t va2 = (grip & ~0xfffull) + 4096;
       if (!tlb_get(L, va2 >> 12, td) || !perm_ok(L, td, ACC_X)) {
@@ -135,7 +136,7 @@ int sim_run_full(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, c
       memcpy(&ib.lo, bytes, 8);
       memcpy(&ib.hi, bytes + 8, 8);
       ib.avail = 16;
-      dr = decode(ib, d);
+      dr = decode(ib, d, m32);
     }
     if (dr == 2) {
       set_fault(L, WTFGPU_VEC_GP, 0, 0);
@@ -146,7 +147,7 @@ int sim_run_full(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, c
       break;
     }
     uint64_t next = 0;
-    if (fast) {
+    if (fast && !m32) {
       FOp f;
       digest(d, f);
       if (fo_op(f) != FO_GENERIC) {
@@ -227,7 +228,7 @@ int sim_run_full(const uint64_t *gpfns, const uint8_t *pages, uint64_t npages, c
     f.cr0 = sys.cr0;
     f.cr3 = sys.cr3;
     f.cr4 = sys.cr4;
-    f.efer = sys.efer;
+    f.efer = sys.efer & ~EFER_M32;
     f.kernel_gs_base = sys.kgs;
     f.star = sys.star;
     f.lstar = sys.lstar;

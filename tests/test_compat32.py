@@ -1,0 +1,157 @@
+"""32-bit code in compatibility mode: SYSRET without REX.W
+enters it, far transfers and interrupts leave it and come back. Hand-checked
+oracle cases (the SDM's arithmetic for the BCD forms, stack and branch widths,
+the mode switches), the engine's device code built for the host against the
+oracle lane by lane, and the GPU engine against the oracle lane by lane (-m gpu).
+
+Parity unpinned against real hardware: this container cannot execute 32-bit
+code natively (no 32-bit code segment for user processes here), so the
+restatement is pinned by the SDM's definitions checked below and by the
+engine / oracle agreement."""
+import pytest
+
+from tests import compat32 as T
+from tests import sysprog2 as S
+from tests.test_sys2 import _diff, sim_lanes, sim_lib
+from wtf_amd import abi
+from wtf_amd.abi import regs_from_state
+
+HLT, INT3, FAULT, UNIMPL = abi.EXIT_HLT, abi.EXIT_INT3, abi.EXIT_FAULT, abi.EXIT_UNIMPLEMENTED
+M32 = 0xFFFFFFFF
+
+
+@pytest.fixture(scope="module")
+def space():
+    return T.build_space()
+
+
+def _one(space, name, flags=0x202, esp=T.ESP32, **regs):
+    sp, st, lay, data = space
+    g = [0] * 16
+    for k, v in regs.items():
+        g[abi.GPR_ORDER.index(k)] = v
+    g[3], g[14], g[15] = T.SLOT32[name], esp, flags
+    g[13] = regs.get("rbx", 0)
+    return S.oracle_run(sp, st, [(T.KC32, g, 0x2)], limit=500)[0]
+
+
+def test_sysret_enters_32_bit_code(space):
+    r = _one(space, "incdec", rax=0xFFFFFFFF_00000010, rcx=0xFFFFFFFF, rsi=0, rdi=5, rbx=0x100000000)
+    g = r["gpr"]
+    assert r["exit"][0] == INT3 and r["exit"][4] == T.SLOT32["incdec"] + 5 and r["sel"][1] == 0x23
+    # 32-bit results zero-extend (ecx held the entry point: the stub's sysret target)
+    assert g[0] == 0x11 and g[1] == T.SLOT32["incdec"] + 1 and g[3] == 0xFFFFFFFF and g[6] == 0xFFFFFFFF
+    assert g[7] == 6
+
+
+def test_stack_and_branch_widths(space):
+    r = _one(space, "pushpop", rax=0xAABBCCDD_11223344, rsi=0x77778888_99990000)
+    g = r["gpr"]
+    assert r["exit"][0] == INT3
+    assert g[3] == 0x12345678 and g[1] == 0x11223344 and g[2] == T.ESP32  # push esp: the value before
+    assert g[6] == 0x77778888_99991234 and g[4] == T.ESP32  # pop si keeps the upper bits; esp balanced
+    r = _one(space, "callret")
+    assert r["exit"][0] == INT3 and r["gpr"][0] == 7 and r["gpr"][4] == T.ESP32  # ret 4 releases the argument
+    r = _one(space, "loop", rbx=1)
+    assert r["exit"][0] == INT3 and r["gpr"][0] == 10 and r["gpr"][3] == 2
+    r = _one(space, "pusha", rax=1, rbp=3, rdi=4)
+    g = r["gpr"]
+    assert (g[0], g[1], g[5], g[7], g[4]) == (1, T.SLOT32["pusha"], 3, 4, T.ESP32)
+    r = _one(space, "enter", rbp=T.ESP32 - 0x100)  # level 2: one frame pointer copied from [ebp - 4]
+    assert r["exit"][0] == INT3 and r["gpr"][5] == T.ESP32 - 0x100 and r["gpr"][4] == T.ESP32
+
+
+def test_bcd_adjustments_follow_the_sdm(space):
+    AF, CF = 0x10, 0x1
+    r = _one(space, "bcd2", rax=0x7B)  # 0x35 + 0x46 = 0x7B -> daa -> 0x81, AF
+    assert r["gpr"][0] & 0xFF == 0x81 and r["rflags"] & AF and not r["rflags"] & CF
+    r = _one(space, "bcd2", rax=0x9A, flags=0x202)  # both nibbles adjust: 0x00, CF, ZF
+    assert r["gpr"][0] & 0xFF == 0x00 and r["rflags"] & CF and r["rflags"] & 0x40
+    r = _one(space, "aas", rax=0x0203, flags=0x202 | AF)  # AX - 6 borrows into AH, then AH - 1
+    assert r["gpr"][0] & 0xFFFF == 0x000D and r["rflags"] & CF and r["rflags"] & AF
+    r = _one(space, "aad7", rax=0x0305)  # 3 * 7 + 5 = 26
+    assert r["gpr"][0] & 0xFFFF == 26
+    r = _one(space, "aam0")
+    assert r["exit"][:2] == (FAULT, 0)
+
+
+def test_mode_switches(space):
+    r = _one(space, "farcall")  # 32 -> 64 (call far 0x33:stub) -> retf -> 32
+    assert r["exit"][0] == INT3 and r["exit"][4] == T.SLOT32["farcall"] + 7
+    assert r["gpr"][9] == 0x1122334455667788 and r["sel"][1] == 0x23 and r["gpr"][4] == T.ESP32
+    r = _one(space, "farjmp")
+    assert r["exit"][0] == INT3 and r["gpr"][10] == 0x55 and r["sel"][1] == 0x33
+    r = _one(space, "syscall", flags=0x203)  # from 32-bit code: CSTAR
+    assert r["exit"][0] == HLT and r["gpr"][8] == T.SLOT32["syscall"] + 2 and r["gpr"][9] & 1
+    assert r["sel"][1] == 0x10
+    r = _one(space, "int29")  # a 64-bit gate: 64-bit frame on RSP0, cs 0x23 in it
+    assert r["exit"][0] == HLT and r["gpr"][8] == T.SLOT32["int29"] + 2 and r["gpr"][9] == 0x23
+    assert r["gpr"][11] == T.ESP32
+    r = _one(space, "iretd")  # iret at the same privilege from 32-bit code: no SS:ESP
+    assert r["exit"][0] == INT3 and r["gpr"][4] == T.ESP32 and r["sel"][1] == 0x23
+    r = _one(space, "retf")
+    assert r["exit"][0] == INT3 and r["gpr"][4] == T.ESP32
+
+
+def test_outside_forms_and_ud(space):
+    for n in ("les", "a16", "bound", "arpl", "jmp16"):
+        assert _one(space, n, rsi=T.DATA32)["exit"][0] == UNIMPL, n
+    assert _one(space, "ud2")["exit"][:2] == (FAULT, 6)
+
+
+def test_engine_code_matches_oracle(space):
+    sp, st, lay, data = space
+    ln = T.lanes(37 * 24, 21)
+    want = S.oracle_run(sp, st, ln, limit=500)
+    got = sim_lanes(sim_lib(), sp, st, ln, limit=500)
+    names = {v: k for k, v in T.SLOT32.items()}
+    bad = []
+    for i, (w, g) in enumerate(zip(want, got)):
+        d = _diff(g, w)
+        if d:
+            bad.append((i, names[ln[i][1][3]], d, {k: (g[k], w[k]) for k in d if k not in ("pages", "xmm", "ymmh")}))
+    assert not bad, f"{len(bad)}/{len(ln)} lanes differ; first: {bad[:3]}"
+    kinds = {(w["exit"][0], w["exit"][1]) for w in want}
+    assert {(HLT, 0), (INT3, 0), (UNIMPL, 0), (FAULT, 0), (FAULT, 6), (FAULT, 14)} <= kinds, kinds
+    # most lanes run their snippet to its int3
+    assert sum(w["exit"][0] == INT3 for w in want) > len(ln) // 2
+
+
+@pytest.mark.gpu
+def test_gpu_matches_oracle(space):
+    import numpy as np
+    from wtf_amd.engine import Engine
+
+    sp, st, lay, data = space
+    n = 37 * 32
+    ln = T.lanes(n, 22)
+    want = S.oracle_run(sp, st, ln, limit=500)
+    eng = Engine(0)
+    try:
+        pfns, blob = sp.phys()
+        eng.load_pool(pfns, blob)
+        eng.alloc_lanes(n, overlay_pages=16, cov_entries=256)
+        eng.set_initial_state(regs_from_state(st))
+        eng.set_limit(500)
+        eng.restore()
+        g = eng.read_gprs()
+        for i, (va, regs, flags) in enumerate(ln):
+            g[i, :16] = np.array(regs, dtype=np.uint64)
+            g[i, 16], g[i, 17] = va, flags
+        eng.write_gprs(g)
+        eng.run()
+        ex = eng.exits()
+        regs = eng.read_regs(0, n)
+        nb = eng.nbytes()
+        bad = []
+        for i, w in enumerate(want):
+            e = ex[i]
+            pg = {gpa: eng.read_phys(i, gpa, 4096) for gpa in eng.dirty(i)}
+            got = S.lane_view(e.status, e.vector, e.error, e.addr, e.icount, int(nb[i]), regs[i], pg)
+            d = _diff(got, w)
+            if d:
+                bad.append((i, d, {k: (got[k], w[k]) for k in d if k not in ("pages", "xmm", "ymmh")}))
+        assert not bad, f"{len(bad)}/{n} lanes differ; first: {bad[:3]}"
+        assert sum(w["exit"][0] == INT3 for w in want) > n // 2
+    finally:
+        eng.close()

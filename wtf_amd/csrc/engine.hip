@@ -112,7 +112,7 @@ __device__ __forceinline__ void load_lane(const Dev &P, u32 lane, Lane &L) {
   const LaneSys s = P.sys[lane];
   L.cr0 = s.cr0;
   L.cr3 = s.cr3;
-  L.efer = s.efer;
+  L.efer = s.efer;  // with the 32-bit-code bit (U29)
   L.cpl = s.cpl;
   L.simd = simd_bits(s.cr0, s.cr4, P.full[lane].xcr0);
   L.ovn = P.ov_count[lane];
@@ -468,7 +468,7 @@ __device__ __noinline__ bool deliver_fault(const Dev &P, Lane &L) {
     }
     if (!wr) break;
     if (ncpl < cpl0) S.ss = (u16)ncpl;  // SS := NULL selector at the new privilege level
-    S.cs = sel;
+    set_cs(L, S, sel);
     if (vec == WTFGPU_VEC_PF) S.cr2 = cr2;
     L.cpl = S.cpl = ncpl;
     S.deliv_icount = L.icount;
@@ -646,7 +646,7 @@ __device__ __noinline__ void code_xlate(const Dev &P, Lane &L, u64 rip) {
   }
   if (td) {
     L.cvpn = vpn;
-    L.cptr = td & ~0xfffull;
+    L.cptr = (td & ~0xfffull) | (L.efer & EFER_M32);  // 32-bit code: outside the pool (U29)
   }
 }
 
@@ -945,11 +945,13 @@ __device__ __noinline__ bool bp_apply(const Dev &P, Lane &L, u64 grip) {
 // instruction that crosses into the next page (translated per lane).
 __device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr, bool ing, bool &skip) {
   const u32 off = (u32)(grip & 0xfff);
+  const bool m32 = (lptr & EFER_M32) != 0;  // the group's lanes run 32-bit code (U29)
+  lptr &= ~EFER_M32;
   IBytes ib;
   ib.avail = 4096 - off < 16 ? 4096 - off : 16;
   fetch_bytes(lptr, off, ib.avail, ib.lo, ib.hi);
   UOp d;
-  int dr = decode(ib, d);
+  int dr = decode(ib, d, m32);
   if (dr == 1) {
     u64 nptr = 0;
     if (ing) {
@@ -978,7 +980,7 @@ __device__ __noinline__ void slow_step(const Dev &P, Lane &L, u64 grip, u64 lptr
       ib.hi = (lo2 >> (64 - 8 * n0)) | (hi2 << (8 * n0));
     }
     ib.avail = 16;
-    dr = decode(ib, d);
+    dr = decode(ib, d, m32);
   }
   if (dr == 2) {
     if (ing) set_fault(L, WTFGPU_VEC_GP, 0, 0);
@@ -1269,7 +1271,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
           }
           if (ok) {
             L.cvpn = grip >> 12;
-            L.cptr = td & ~0xfffull;
+            L.cptr = (td & ~0xfffull) | (L.efer & EFER_M32);  // 32-bit code: to slow_step (U29)
           }
         }
         if (gm & m_ne64(L.cvpn, grip >> 12)) break;
@@ -2402,7 +2404,7 @@ InitState make_init(const wtfgpu_regs_t &r) {
   s.sys.cr0 = r.cr0;
   s.sys.cr3 = r.cr3;
   s.sys.cr4 = r.cr4;
-  s.sys.efer = r.efer;
+  s.sys.efer = (r.efer & ~EFER_M32) | (compat_sel(r.star, r.seg[WTFGPU_CS].selector) ? EFER_M32 : 0);  // U29
   s.sys.cpl = r.seg[WTFGPU_CS].selector & 3;
   s.sys.star = r.star;
   s.sys.lstar = r.lstar;
@@ -3105,7 +3107,7 @@ int wtfgpu_read_regs(wtfgpu_ctx *c, uint32_t first, uint32_t count, wtfgpu_regs_
     r.cr0 = sys[l].cr0;
     r.cr3 = sys[l].cr3;
     r.cr4 = sys[l].cr4;
-    r.efer = sys[l].efer;
+    r.efer = sys[l].efer & ~EFER_M32;
     r.kernel_gs_base = sys[l].kgs;
     r.star = sys[l].star;
     r.lstar = sys[l].lstar;

@@ -72,6 +72,33 @@ __device__ __forceinline__ void tlb_flush(Lane &L) {
   L.cvpn = EMPTY_KEY;
 }
 
+// ------------------------------------------------------------------ compatibility mode (U29)
+// A lane runs 32-bit code when CS is SYSRET's 32-bit selector, STAR[63:48]
+// (Windows' and Linux' layout: the only CS.L = 0 code segment; descriptors are
+// not read, U19). The mode is bit 63 of the lane's efer copy (never of
+// LaneSys::efer, never reported: EFER bits 63:16 are reserved) and of its code
+// pointer L.cptr, which puts the pointer outside the page pool: the fast loop's
+// pool check and the slow step's cacheable test send every 32-bit instruction
+// to slow_step, which decodes it in 32-bit mode. LaneSys::efer carries the
+// bit too (set by make_init from the snapshot's CS, stripped from every
+// register read-back), so load_lane copies it with efer. (bochscpu.hpp:119-182:
+// the reference state is the full segment cache; its CS.L picks the mode.)
+constexpr u64 EFER_M32 = 1ull << 63;
+__host__ __device__ __forceinline__ bool compat_sel(u64 star, u32 sel) {
+  return ((sel ^ (u32)(star >> 48)) & 0xfffc) == 0;
+}
+// CS := sel, with the mode it selects; a mode change drops the code-page cache
+// (its pointer carries the mode)
+__device__ __forceinline__ void set_cs(Lane &L, LaneSys &S, u32 sel) {
+  S.cs = (u16)sel;
+  const u64 m = compat_sel(S.star, sel) ? EFER_M32 : 0;
+  if ((L.efer & EFER_M32) != m) {
+    L.efer ^= EFER_M32;
+    S.efer ^= EFER_M32;
+    L.cvpn = EMPTY_KEY;
+  }
+}
+
 // ------------------------------------------------------------------ physical memory
 __device__ __forceinline__ u64 bloom_bit(u64 gpfn) { return 1ull << ((gpfn * 0x9E3779B97F4A7C15ull) >> 58); }
 
@@ -182,25 +209,6 @@ __device__ __forceinline__ bool walk(const Dev &P, Lane &L, u64 va, int acc, u64
   td = (u64)(uintptr_t)pg | (aw ? T_W : 0) | (au ? T_U : 0) | (nx ? T_NX : 0) | (priv ? T_PRIV : 0) |
        (is_ptpage(P, gpfn) ? T_PT : 0);
   return true;
-}
-
-// Would a ring-3 instruction fetch at va translate (present, user, executable)?
-// No side effects (SYSRET to compatibility mode, U29).
-__device__ __noinline__ bool user_fetch_ok(const Dev &P, const Lane &L, u64 va) {
-  if (!canonical(va)) return false;
-  const bool nxe = (L.efer >> 11) & 1;
-  u64 table = L.cr3 & 0x000ffffffffff000ull;
-  bool u = true, nx = false, priv;
-  for (int level = 3; level >= 0; level--) {
-    const u8 *pg = phys_page(P, L.lane, L.ovn, L.bloom, table >> 12, priv);
-    const u64 e = *(const u64 *)(pg + ((va >> (12 + 9 * level)) & 0x1ff) * 8);
-    if (!(e & 1)) return false;
-    u &= (e & 4) != 0;
-    if (nxe && (e >> 63)) nx = true;
-    if ((level == 2 || level == 1) && (e & 0x80)) break;
-    table = e & 0x000ffffffffff000ull;
-  }
-  return u && !nx;
 }
 
 // Copy-on-write into overlay slot `slot` of `lane`: the page joins the dirty

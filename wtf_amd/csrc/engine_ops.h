@@ -43,7 +43,7 @@ enum : u32 { Z_B = 0, Z_V, Z_STK, Z_Q, Z_W, Z_D };
 struct UOp {
   u32 len, op, sub, asrc, bsrc, asz, bsz;
   u32 aread, awrite, bwrite;
-  u32 reg, rm, opreg, is_mem, riprel, p67, rex, rep, seg;
+  u32 reg, rm, opreg, is_mem, riprel, p67, rex, rep, seg;  // p67: bit 0 32-bit addresses, bit 1 32-bit code (U29)
   i32 base, index;
   u32 scale;
   u64 disp, imm;
@@ -211,6 +211,11 @@ __constant__ u32 kMap2[256] = {
 constexpr u32 kSseModrm = E(O_SSE, 0, 0, 0, 0, 0, 0, 0, 1, K_NONE, 0);  // 0f 38 / VEX map 2 opcodes
 constexpr u32 kSseModrmImm = E(O_SSE, 0, 0, 0, 0, 0, 0, 0, 1, K_B, 0);  // 0f 3a / VEX map 3 opcodes (imm8)
 constexpr u32 kUnimpl = UN;
+// 32-bit code (U29): 40-4f inc / dec r32, and the one-byte forms 64-bit mode
+// leaves #UD that engine_sys.h runs (push / pop es cs ss ds, pusha / popa,
+// daa das aaa aas, far call / jmp ptr16:32, into, aam / aad)
+constexpr u32 kIncDec32 = E(O_INCDEC, L_OPREG, 0, Z_V, Z_V, 1, 1, 0, 0, K_NONE, 0);
+constexpr u32 kSys32 = S2, kSys32B = S2B;
 #undef E
 #undef UN
 #undef UDE
@@ -253,19 +258,21 @@ __device__ __forceinline__ u64 ib_get(const IBytes &b, u32 pos, u32 n) {
   return v;
 }
 
-__device__ __forceinline__ u32 zsize(u32 z, u32 osz, u32 p66) {
+__device__ __forceinline__ u32 zsize(u32 z, u32 osz, u32 p66, bool m32) {
   switch (z) {
     case Z_B: return 1;
     case Z_V: return osz;
-    case Z_STK: return p66 ? 2 : 8;
-    case Z_Q: return 8;
+    case Z_STK: return p66 ? 2 : (m32 ? 4 : 8);
+    case Z_Q: return m32 ? 4 : 8;  // near branch targets, return addresses, rbp of leave
     case Z_W: return 2;
     default: return 4;
   }
 }
 
 // Decode (uniform). 0 ok, 1 needs bytes beyond avail, 2 longer than 15 (#GP).
-__device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
+// m32: 32-bit code (compatibility mode, U29): no REX, 32-bit operand and
+// address size, 32-bit stack slots and branch targets, disp32 absolute.
+__device__ __forceinline__ int decode(const IBytes &b, UOp &u, bool m32 = false) {
   u32 pos = 0, p66 = 0, rex = 0, lock = 0, c;
   u.p67 = u.rep = u.seg = 0;
   // operand fields exec reads before it dispatches on the op: defined for the
@@ -281,7 +288,7 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
     if (pos >= 15) return 2;
     if (pos >= b.avail) return 1;
     c = ib_at(b, pos++);
-    if ((c & 0xf0) == 0x40) {  // REX; ignored unless it is the last prefix
+    if ((c & 0xf0) == 0x40 && !m32) {  // REX; ignored unless it is the last prefix
       rex = c;
       continue;
     }
@@ -297,7 +304,13 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
   // VEX (c4 / c5; always VEX in 64-bit mode): its fields become the REX bits,
   // the map and `vex` (engine_sse.h: UOp::opreg of an O_SSE op)
   u32 vex = 0, vpp = 0;
-  if (c == 0xc4 || c == 0xc5) {
+  const bool a16 = m32 && u.p67;  // 16-bit addresses in 32-bit code: outside (U29)
+  if (m32) u.p67 = 3;
+  if (m32 && (c == 0xc4 || c == 0xc5)) {  // les / lds unless the next byte's mod is 11 (VEX)
+    if (pos >= 15) return 2;
+    if (pos >= b.avail) return 1;
+  }
+  if ((c == 0xc4 || c == 0xc5) && (!m32 || (ib_at(b, pos) & 0xc0) == 0xc0)) {
     const u32 bad = (p66 || u.rep || rex) ? 1u : 0u;  // a legacy 66 / f2 / f3 / REX before VEX: #UD
     const u32 nb = c == 0xc4 ? 2 : 1;
     if (pos + nb + 1 > 15) return 2;
@@ -305,10 +318,10 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
     const u32 b1 = ib_at(b, pos), b2 = c == 0xc4 ? ib_at(b, pos + 1) : b1;
     pos += nb;
     const u32 vr = ((b1 >> 7) & 1) ^ 1;
-    const u32 vx = c == 0xc4 ? ((b1 >> 6) & 1) ^ 1 : 0, vb = c == 0xc4 ? ((b1 >> 5) & 1) ^ 1 : 0;
+    const u32 vx = c == 0xc4 ? ((b1 >> 6) & 1) ^ 1 : 0, vb = (c == 0xc4 && !m32) ? ((b1 >> 5) & 1) ^ 1 : 0;
     const u32 vmap = c == 0xc4 ? (b1 & 31) : 1, vw = c == 0xc4 ? (b2 >> 7) & 1 : 0;
     vpp = b2 & 3;
-    vex = 1 | (((b2 >> 2) & 1) << 1) | (vw << 2) | ((((~b2) >> 3) & 15) << 4) | (vmap << 8) | (bad << 16);
+    vex = 1 | (((b2 >> 2) & 1) << 1) | (vw << 2) | ((((~b2) >> 3) & (m32 ? 7 : 15)) << 4) | (vmap << 8) | (bad << 16);
     rex = 0x40 | (vw << 3) | (vr << 2) | (vx << 1) | vb;
     c = ib_at(b, pos++);  // the opcode
     const bool def = !bad && vmap >= 1 && vmap <= 3 && vex_defined(vmap, c, vpp);
@@ -361,13 +374,25 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
   } else {
     e = kMap1[c];
     if (c == 0x90 && !rexb) e = O_NOP;  // 90 is nop (no zero-extension), f3 90 pause
+    if (m32) {
+      if (c >= 0x40 && c <= 0x4f) e = kIncDec32;
+      else if (c == 0x82) e = kMap1[0x80];
+      else if (c == 0xd4 || c == 0xd5) e = kSys32B;
+      else if (c == 0x06 || c == 0x07 || c == 0x0e || c == 0x16 || c == 0x17 || c == 0x1e || c == 0x1f ||
+               c == 0x27 || c == 0x2f || c == 0x37 || c == 0x3f || c == 0x60 || c == 0x61 || c == 0x9a ||
+               c == 0xce || c == 0xea)
+        e = kSys32;
+      else if (c == 0x62 || c == 0x63 || c == 0xc4 || c == 0xc5 || c == 0xd6)
+        e = kUnimpl;  // bound, arpl, les / lds, salc (U29)
+    }
   }
   const u32 osz = rexw ? 8 : (p66 ? 2 : 4);
+  const u32 sstk = p66 ? 2 : (m32 ? 4 : 8);  // a stack slot
   u.op = e & 63;
   u.asrc = (e >> 6) & 15;
   u.bsrc = (e >> 10) & 15;
-  u.asz = zsize((e >> 14) & 7, osz, p66);
-  u.bsz = zsize((e >> 17) & 7, osz, p66);
+  u.asz = zsize((e >> 14) & 7, osz, p66, m32);
+  u.bsz = zsize((e >> 17) & 7, osz, p66, m32);
   u.aread = (e >> 20) & 1;
   u.awrite = (e >> 21) & 1;
   u.bwrite = (e >> 22) & 1;
@@ -376,6 +401,7 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
   const u32 grp = (e >> 27) & 15;
   u.sub = c & 0xf;  // cc for jcc/cmov/setcc, string opcode low bits
   if (grp == G_ALU) u.sub = (c >> 3) & 7;
+  if (e == kIncDec32 && !map2) u.sub = (c >> 3) & 1;  // 40-47 inc, 48-4f dec
   u.opreg = (c & 7) | (rexb << 3);
   u.is_mem = u.riprel = 0;
   u.reg = u.rm = 0;
@@ -416,7 +442,7 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
       } else if (rm == 5 && mod == 0) {
         if (pos + 4 > 15) return 2;
         if (pos + 4 > b.avail) return 1;
-        u.riprel = 1;
+        u.riprel = m32 ? 0 : 1;  // 32-bit code: disp32 absolute
         u.disp = sext(ib_get(b, pos, 4), 4);
         pos += 4;
       } else {
@@ -467,22 +493,22 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
         if (r3 == 2 || r3 == 4) {  // call / jmp near indirect: 64-bit target
           u.op = r3 == 2 ? O_CALL : O_JMP;
           u.asrc = r3 == 2 ? L_PUSH : L_NONE;
-          u.asz = 8;
+          u.asz = m32 ? 4 : 8;
           u.aread = 0;
           u.awrite = r3 == 2;
           u.bsrc = L_RM;
-          u.bsz = 8;
+          u.bsz = m32 ? 4 : 8;
         } else if (r3 == 6) {
           u.op = O_PUSH;
           u.asrc = L_PUSH;
-          u.asz = u.bsz = p66 ? 2 : 8;
+          u.asz = u.bsz = sstk;
           u.aread = 0;
           u.awrite = 1;
           u.bsrc = L_RM;
         } else if (r3 == 3 || r3 == 5) {  // far call / jmp m16:osz (engine_sys.h)
           u.op = O_SYS2;
           u.asz = osz;
-          u.bsz = p66 ? 2 : 8;
+          u.bsz = sstk;
         } else if (r3 == 7) {
           u.op = O_UD;
         }
@@ -533,7 +559,7 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
       }
       if (u.op == O_SYS2) {  // group 15 beyond ldmxcsr / stmxcsr / the fences: engine_sys.h
         u.asz = osz;
-        u.bsz = p66 ? 2 : 8;
+        u.bsz = sstk;
       }
     }
     if (u.op == O_BT && grp != G_BA) u.sub = c == 0xa3 ? 4 : c == 0xab ? 5 : c == 0xb3 ? 6 : 7;
@@ -554,7 +580,7 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
           (c == 0xc7 && (u.is_mem || (u.reg & 7) < 6 || u.rep))) {
         u.op = O_SYS2;
         u.asz = osz;
-        u.bsz = p66 ? 2 : 8;
+        u.bsz = sstk;
       }
     }
   } else if (u.op == O_FLAGOP) {
@@ -564,7 +590,7 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
     if (!rexw) {
       u.op = O_SYS2;
       u.asz = osz;
-      u.bsz = p66 ? 2 : 8;
+      u.bsz = sstk;
     }
   } else if (u.op == O_STRING && c < 0x80) {
     u.sub |= 0x10;  // ins / outs (6c-6f)
@@ -588,6 +614,7 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
     case K_ENTER: n = 3; break;
     default: n = 0;
   }
+  if (m32 && !map2 && (c == 0x9a || c == 0xea)) n = osz + 2;  // ptr16:32 / ptr16:16
   if (pos + n > 15) return 2;
   if (pos + n > b.avail) return 1;
   const u64 raw = ib_get(b, pos, n);
@@ -598,6 +625,9 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u) {
   pos += n;
   u.len = pos;
   u.opbytes = pos >= 4 ? (u32)b.lo : ((u32)b.lo & ((1u << (8 * pos)) - 1));
+  // 16-bit addresses, and 16-bit instruction pointers (66 on a near branch), in 32-bit code
+  if (a16 || (m32 && p66 && (u.op == O_JCC || u.op == O_JMP || u.op == O_CALL || u.op == O_RET || u.op == O_LOOP)))
+    u.op = O_UNIMPL;
   u.supported = u.op != O_UNIMPL;
   return 0;
 }
@@ -968,7 +998,10 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
     if (u.p67) ea &= 0xffffffffull;
   }
   if (op == O_SYS2) return sys2_exec(P, L, u, nrip, next, ea + sb);
-  const u64 rsp = R(L, 4);
+  // 32-bit code (U29): esp addresses the stack, branch targets wrap at 4 GiB
+  const bool m32 = u.p67 & 2;
+  const u64 smask = m32 ? 0xffffffffull : ~0ull;
+  const u64 rsp = R(L, 4) & smask;
   // ---- register / immediate operands
   u64 a = (u.aread && !loc_is_mem(u, u.asrc)) ? loc_reg_read(L, u, u.asrc, u.asz) : 0;
   u64 b = loc_is_mem(u, u.bsrc) ? 0 : loc_reg_read(L, u, u.bsrc, u.bsz);
@@ -987,7 +1020,7 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
       case L_RM: addr = ea + sb; break;
       case L_POP: addr = rsp; break;
       case L_MOFFS: addr = u.imm + sb; break;
-      case L_RBPMEM: addr = R(L, 5); break;
+      case L_RBPMEM: addr = R(L, 5) & smask; break;
       default: {  // xlat
         u64 x = R(L, 3) + (R(L, 0) & 0xff);
         if (u.p67) x &= 0xffffffffull;
@@ -1159,11 +1192,11 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
     case O_CALL:
       res = nrip;
       next = u.bsrc == L_IMM ? nrip + b : b;
-      drsp = -8;
+      drsp = -(i64)asz;
       break;
     case O_RET:
       next = b;
-      drsp = 8 + (i64)u.imm;
+      drsp = (i64)u.bsz + (i64)u.imm;
       break;
     case O_PUSH:
       res = b;
@@ -1235,7 +1268,7 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
         fl = (fl & ~mask) | (f2 & mask) | 2;
         next = f0;
         RS(L, 4, f3);
-        S.cs = (u16)f1;
+        set_cs(L, S, (u32)f1 & 0xffff);
         S.ss = (u16)f4;
         if (ncpl != L.cpl) L.flush = 1;  // translations were permission-checked at the old cpl
         L.cpl = S.cpl = ncpl;
@@ -1298,7 +1331,7 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
           case 0x175: cur = F.sysenter_esp; canon = 1; break;
           case 0x176: cur = F.sysenter_eip; canon = 1; break;
           case 0x277: cur = F.pat; break;
-          case 0xc0000080u: cur = L.efer; break;
+          case 0xc0000080u: cur = L.efer & ~EFER_M32; break;
           case 0xc0000081u: cur = S.star; break;
           case 0xc0000082u: cur = S.lstar; canon = 1; break;
           case 0xc0000083u: cur = F.cstar; canon = 1; break;
@@ -1329,7 +1362,7 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
           case 0x176: F.sysenter_eip = v; break;
           case 0x277: F.pat = v; break;
           case 0xc0000080u:
-            L.efer = S.efer = (v & ~0x400ull) | (L.efer & 0x400ull);  // LMA is read-only
+            L.efer = S.efer = (v & ~0x400ull) | (L.efer & (0x400ull | EFER_M32));  // LMA is read-only
             L.flush = 1;
             break;
           case 0xc0000081u: S.star = v; break;
@@ -1362,29 +1395,25 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
         set_fault(L, WTFGPU_VEC_UD, 0, 0);
         return X_FAULT;
       }
-      if (u.sub == 0) {  // syscall
+      if (u.sub == 0) {  // syscall (from 32-bit code: to CSTAR, U29)
         RS(L, 1, nrip);
         RS(L, 11, fl & ~0x10000ull);
         fl = ((fl & ~S.sfmask) & ~0x10000ull) | 2;
-        next = S.lstar;
+        next = (u.p67 & 2) ? P.full[L.lane].cstar : S.lstar;
         L.cpl = S.cpl = 0;
-        S.cs = (u16)((S.star >> 32) & 0xfffc);
+        set_cs(L, S, (u32)((S.star >> 32) & 0xfffc));
         S.ss = (u16)(S.cs + 8);
       } else {  // sysretq
         if (L.cpl != 0) {
           set_fault(L, WTFGPU_VEC_GP, 0, 0);
           return X_FAULT;
         }
-        if (!(u.rex & 8)) {
-          // to compatibility mode at ecx: its first fetch faults (#PF through the
-          // IDT, as the host's would) unless ring 3 could fetch there: then
-          // 32-bit code would run, which is outside (U29)
+        if (!(u.rex & 8)) {  // to compatibility mode at ecx (U29)
           const u64 t32 = R(L, 1) & 0xffffffffull;
-          if (user_fetch_ok(P, L, t32)) return X_UNIMPL;
           fl = (R(L, 11) & 0x3c7fd7ull) | 2;
           next = t32;
           L.cpl = S.cpl = 3;
-          S.cs = (u16)(((S.star >> 48) & 0xffff) | 3);
+          set_cs(L, S, (u32)(((S.star >> 48) & 0xffff) | 3));
           S.ss = (u16)((((S.star >> 48) & 0xffff) + 8) | 3);
           L.flush = 1;
           break;
@@ -1397,7 +1426,7 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
         fl = (R(L, 11) & 0x3c7fd7ull) | 2;
         next = target;
         L.cpl = S.cpl = 3;
-        S.cs = (u16)((((S.star >> 48) & 0xffff) + 16) | 3);
+        set_cs(L, S, (u32)((((S.star >> 48) & 0xffff) + 16) | 3));
         S.ss = (u16)((((S.star >> 48) & 0xffff) + 8) | 3);
       }
       L.flush = 1;  // cached translations were permission-checked at the old cpl
@@ -1405,6 +1434,7 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
     }
     default: return X_UNIMPL;
   }
+  if (m32 && op != O_SYS) next &= 0xffffffffull;
   // ---- the memory write
   if (wa && amem) {
     u64 addr;
@@ -1412,7 +1442,7 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
       // pop r/m computes its address with rsp already incremented
       addr = (op == O_POP && u.base == 4 ? ea + u.bsz : ea) + sb;
     } else if (u.asrc == L_PUSH) {
-      addr = rsp - asz;
+      addr = (rsp - asz) & smask;
     } else {
       addr = u.imm + sb;
     }
@@ -1420,10 +1450,10 @@ __device__ __forceinline__ int exec(const Dev &P, Lane &L, const UOp &u, u64 nri
   }
   // ---- commit
   if (op == O_LEAVE) {
-    RS(L, 4, R(L, 5) + 8);
-    RS(L, 5, b);
+    RS(L, 4, (R(L, 5) + u.bsz) & smask);
+    RS(L, 5, m32 ? (b & 0xffffffffull) : b);
   }
-  if (drsp) RS(L, 4, rsp + (u64)drsp);
+  if (drsp) RS(L, 4, (rsp + (u64)drsp) & smask);
   if (u.bwrite && !bmem) setr(L, u.rex, loc_reg(u, u.bsrc), u.bsz, resb);  // xchg / xadd source
   if (wa && !amem) setr(L, u.rex, loc_reg(u, u.asrc), asz, res);  // xadd r,r: DEST := TEMP last (SDM)
   if (wrax) setr(L, u.rex, 0, raxsz, ra);

@@ -107,7 +107,7 @@ __device__ __noinline__ int soft_int(const Dev &P, Lane &L, u32 vec, bool dpl_ch
   for (u32 i = 0; i < 5; i++)
     if (!sup_write_pa(P, L, pa[i], frame[i])) return X_FAULT;
   if (ncpl < ocpl) S.ss = (u16)ncpl;
-  S.cs = (u16)sel;
+  set_cs(L, S, sel);
   if (ncpl != ocpl) L.flush = 1;
   L.cpl = S.cpl = ncpl;
   RS(L, 4, rsp - 40);
@@ -538,32 +538,36 @@ __device__ __noinline__ int exec_x87(const Dev &P, Lane &L, const UOp &u, u64 va
 
 // ---------------------------------------------------------------- U29 far transfers
 // far ret (iret = false, imm = the released bytes) / iret with osz-byte slots
-__device__ __noinline__ int far_pop(const Dev &P, Lane &L, u32 osz, u64 imm, bool iret, u64 &next) {
+// (from 32-bit code, m32: esp addresses the frame, and an iret at the same
+// privilege pops no SS:ESP, SDM IRET "IA-32e mode")
+__device__ __noinline__ int far_pop(const Dev &P, Lane &L, u32 osz, u64 imm, bool iret, bool m32, u64 &next) {
   LaneSys &S = P.sys[L.lane];
-  const u64 rsp = R(L, 4);
+  const u64 smask = m32 ? 0xffffffffull : ~0ull;
+  const u64 rsp = R(L, 4) & smask;
   const u32 ocpl = L.cpl;
   u64 f0, f1, f2 = 0, f3 = 0, f4 = 0;
-  if (!vread(L, rsp, osz, f0) || !vread(L, rsp + osz, osz, f1)) return X_FAULT;
-  if (iret && (!vread(L, rsp + 2 * osz, osz, f2) || !vread(L, rsp + 3 * osz, osz, f3) ||
-               !vread(L, rsp + 4 * osz, osz, f4)))
-    return X_FAULT;
+  if (!vread(L, rsp, osz, f0) || !vread(L, (rsp + osz) & smask, osz, f1)) return X_FAULT;
+  if (iret && !vread(L, (rsp + 2 * osz) & smask, osz, f2)) return X_FAULT;
   const u32 cs = (u32)f1 & 0xffff, ncpl = cs & 3;
+  const bool outer = iret ? (!m32 || ncpl > ocpl) : ncpl > ocpl;  // SS:RSP popped
+  if (iret && outer && (!vread(L, (rsp + 3 * osz) & smask, osz, f3) || !vread(L, (rsp + 4 * osz) & smask, osz, f4)))
+    return X_FAULT;
   if ((cs & 0xfffc) == 0 || ncpl < ocpl) return fault_x(L, WTFGPU_VEC_GP, cs & 0xfffc);
-  u64 nrsp = rsp + 2 * (u64)osz + imm, nss = S.ss;
+  u64 nrsp = (rsp + (iret ? 3 : 2) * (u64)osz + imm) & smask, nss = S.ss;
   if (!iret && ncpl > ocpl) {
-    if (!vread(L, rsp + 2 * (u64)osz + imm, osz, f3) || !vread(L, rsp + 3 * (u64)osz + imm, osz, f4)) return X_FAULT;
+    if (!vread(L, (rsp + 2 * (u64)osz + imm) & smask, osz, f3) || !vread(L, (rsp + 3 * (u64)osz + imm) & smask, osz, f4))
+      return X_FAULT;
   }
-  if (iret || ncpl > ocpl) {
+  if (outer) {
     nss = f4 & 0xffff;
     nrsp = f3 + (iret ? 0 : imm);
     if ((nss & 0xfffc) == 0 && ncpl == 3) return fault_x(L, WTFGPU_VEC_GP, 0);
   }
   if (!canonical(f0)) return fault_x(L, WTFGPU_VEC_GP, 0);
-  // back to SYSRET's compatibility-mode selector (U29): a rip past the 32-bit
-  // segment's limit is #GP(0); where ring 3 could fetch, 32-bit code runs
-  const bool compat = cs == ((((u32)(S.star >> 48)) & 0xffff) | 3);
+  // to SYSRET's compatibility-mode selector (U29): a rip past the 32-bit
+  // segment's limit is #GP(0)
+  const bool compat = compat_sel(S.star, cs);
   if (compat && (f0 >> 32)) return fault_x(L, WTFGPU_VEC_GP, 0);
-  if (compat && user_fetch_ok(P, L, f0)) return X_UNIMPL;
   if (iret) {
     u64 mask = 0x254dd5ull;
     if (ocpl == 0) mask |= 0x200ull | 0x3000ull | 0x80000ull | 0x100000ull;
@@ -571,7 +575,7 @@ __device__ __noinline__ int far_pop(const Dev &P, Lane &L, u32 osz, u64 imm, boo
     if (osz == 2) mask &= 0xffff;
     L.rflags = (L.rflags & ~mask) | (f2 & mask) | 2;
   }
-  S.cs = (u16)cs;
+  set_cs(L, S, cs);
   S.ss = (u16)nss;
   if (ncpl != ocpl) L.flush = 1;
   L.cpl = S.cpl = ncpl;
@@ -580,13 +584,118 @@ __device__ __noinline__ int far_pop(const Dev &P, Lane &L, u32 osz, u64 imm, boo
   return X_OK;
 }
 
+// ---------------------------------------------------------------- 32-bit code (U29)
+// The one-byte forms 64-bit mode leaves #UD: push / pop es cs ss ds, pusha /
+// popa, the BCD adjustments, far call / jmp ptr16:32, into. BCD flags the SDM
+// leaves undefined follow a logical result (SF ZF PF of AL, OF 0; U29).
+__device__ __noinline__ int sys32_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next) {
+  LaneSys &S = P.sys[L.lane];
+  wtfgpu_regs_t &F = P.full[L.lane];
+  const u32 c = u.sub & 0xff, osz = u.asz, sl = u.bsz;  // operand size, stack slot
+  const u64 esp = R(L, 4) & 0xffffffffull;
+  const u64 al = R(L, 0) & 0xff, ah = (R(L, 0) >> 8) & 0xff;
+  auto set_al_flags = [&](u64 nal, u64 nah, u64 cf, u64 af) {
+    RS(L, 0, (R(L, 0) & ~0xffffull) | (nah << 8) | (nal & 0xff));
+    L.rflags = (L.rflags & ~F_STATUS) | szp(nal & 0xff, 1) | (cf ? F_CF : 0) | (af ? F_AF : 0);
+  };
+  switch (c) {
+    case 0x06: case 0x0e: case 0x16: case 0x1e: {  // push es / cs / ss / ds
+      const u32 r = c >> 3;
+      const u64 v = r == WTFGPU_CS ? S.cs : r == WTFGPU_SS ? S.ss : F.seg[r].selector;
+      if (!vwrite(L, (esp - sl) & 0xffffffffull, sl, v)) return X_FAULT;
+      RS(L, 4, (esp - sl) & 0xffffffffull);
+      return X_OK;
+    }
+    case 0x07: case 0x17: case 0x1f: {  // pop es / ss / ds
+      u64 v;
+      if (!vread(L, esp, sl, v)) return X_FAULT;
+      if (!load_sreg(P, L, c >> 3, (u32)v & 0xffff, true)) return X_FAULT;
+      RS(L, 4, (esp + sl) & 0xffffffffull);
+      return X_OK;
+    }
+    case 0x60: {  // pusha: eax ecx edx ebx esp(before) ebp esi edi, eax highest
+      if (!span_w(L, (esp - 8 * osz) & 0xffffffffull, 8 * osz)) return X_FAULT;
+      for (u32 i = 0; i < 8; i++)
+        if (!vwrite(L, (esp - (i + 1) * osz) & 0xffffffffull, osz, i == 4 ? esp : R(L, i))) return X_FAULT;
+      RS(L, 4, (esp - 8 * osz) & 0xffffffffull);
+      return X_OK;
+    }
+    case 0x61: {  // popa: every slot read before a register changes; esp's slot skipped
+      u64 v[8];
+      for (u32 i = 0; i < 8; i++)
+        if (i != 3 && !vread(L, (esp + i * osz) & 0xffffffffull, osz, v[i])) return X_FAULT;
+      for (u32 i = 0; i < 8; i++)
+        if (i != 3) setr(L, 0, 7 - i, osz, v[i]);
+      RS(L, 4, (esp + 8 * osz) & 0xffffffffull);
+      return X_OK;
+    }
+    case 0x27: case 0x2f: {  // daa / das (bochs' order: CF of the low adjust, then the high)
+      const bool cf = L.rflags & F_CF, af = L.rflags & F_AF, sub = c == 0x2f;
+      u64 nal = al, ncf = 0, naf = 0;
+      if ((al & 0xf) > 9 || af) {
+        ncf = cf || (sub ? al < 6 : al > 0xf9);
+        nal = (sub ? nal - 6 : nal + 6) & 0xff;
+        naf = 1;
+      }
+      if (al > 0x99 || cf) {
+        nal = (sub ? nal - 0x60 : nal + 0x60) & 0xff;
+        ncf = 1;
+      }
+      set_al_flags(nal, ah, ncf, naf);
+      return X_OK;
+    }
+    case 0x37: case 0x3f: {  // aaa / aas
+      const bool adj = (al & 0xf) > 9 || (L.rflags & F_AF);
+      u64 ax = R(L, 0) & 0xffff;
+      if (adj && c == 0x37) ax = ax + 0x106;  // SDM: AX + 106H
+      if (adj && c == 0x3f) {                  // SDM: AX - 6, then AH - 1
+        ax = (ax - 6) & 0xffff;
+        ax = (ax & 0xff) | ((((ax >> 8) - 1) & 0xff) << 8);
+      }
+      set_al_flags(ax & 0x0f, (ax >> 8) & 0xff, adj, adj);
+      return X_OK;
+    }
+    case 0xd4: {  // aam imm8
+      const u64 b = u.imm & 0xff;
+      if (b == 0) return fault_x(L, WTFGPU_VEC_DE, 0);
+      set_al_flags(al % b, al / b, 0, 0);
+      return X_OK;
+    }
+    case 0xd5:  // aad imm8
+      set_al_flags((al + ah * (u.imm & 0xff)) & 0xff, 0, 0, 0);
+      return X_OK;
+    case 0xce:  // into
+      if (!(L.rflags & F_OF)) return X_OK;
+      return soft_int(P, L, 4, true, nrip, next);
+    case 0x9a: case 0xea: {  // far call / jmp ptr16:32 (ptr16:16 with 66)
+      const u64 off = u.imm & (osz == 2 ? 0xffffull : 0xffffffffull), sel = (u.imm >> (8 * osz)) & 0xffff;
+      if ((sel & 0xfffc) == 0) return fault_x(L, WTFGPU_VEC_GP, 0);
+      if (c == 0x9a) {
+        if (!span_w(L, (esp - 2 * osz) & 0xffffffffull, 2 * osz)) return X_FAULT;
+        if (!vwrite(L, (esp - osz) & 0xffffffffull, osz, S.cs) || !vwrite(L, (esp - 2 * osz) & 0xffffffffull, osz, nrip))
+          return X_FAULT;
+        RS(L, 4, (esp - 2 * osz) & 0xffffffffull);
+      }
+      set_cs(L, S, (u32)((sel & 0xfffc) | L.cpl));
+      next = off;
+      return X_OK;
+    }
+    default:
+      return X_UNIMPL;
+  }
+}
+
 // ---------------------------------------------------------------- dispatch
 __device__ __noinline__ int sys2_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next, u64 ea) {
   LaneSys &S = P.sys[L.lane];
   wtfgpu_regs_t &F = P.full[L.lane];
   const u32 c = u.sub & 0xff, map0f = u.sub >> 8, r3 = u.reg & 7, osz = u.asz;
   const bool p66 = u.bsz == 2, rexw = (u.rex >> 3) & 1;
+  const bool m32 = u.p67 & 2;  // 32-bit code (U29)
+  const u64 smask = m32 ? 0xffffffffull : ~0ull;
   const u32 cpl = L.cpl;
+  if (!map0f && m32 && (c < 0x40 || c == 0x60 || c == 0x61 || c == 0x9a || c == 0xce || c == 0xd4 || c == 0xd5 || c == 0xea))
+    return sys32_exec(P, L, u, nrip, next);
   const bool umip = (S.cr4 >> 11) & 1;
   u64 a = 0;
   if (!map0f) {
@@ -620,36 +729,37 @@ __device__ __noinline__ int sys2_exec(const Dev &P, Lane &L, const UOp &u, u64 n
         if ((L.cr0 & 0xa) == 0xa) return fault_x(L, VEC_NM, 0);
         if (x87_pending(F)) return fault_x(L, VEC_MF, 0);
         return X_OK;
-      case 0xc8: {  // enter (U29), 64-bit operand size
+      case 0xc8: {  // enter (U29), 64-bit operand size (32-bit in 32-bit code)
         if (p66) return X_UNIMPL;
         const u64 size = u.imm & 0xffff;
         const u32 level = (u32)(u.imm >> 16) & 31;
-        const u64 rsp0 = R(L, 4), rbp0 = R(L, 5);
-        // written: [rsp0 - 8 * (level + 1), rsp0); read: [rbp0 - 8 * (level - 1), rbp0)
-        const u32 nw = 8 * (level + 1);
-        if (!span_w(L, rsp0 - nw, nw)) return X_FAULT;
-        u64 rsp = rsp0 - 8, rbp = rbp0;
-        if (!vwrite(L, rsp, 8, rbp0)) return X_FAULT;
+        const u32 w = m32 ? 4 : 8;
+        const u64 rsp0 = R(L, 4) & smask, rbp0 = R(L, 5) & smask;
+        // written: [rsp0 - w * (level + 1), rsp0); read: [rbp0 - w * (level - 1), rbp0)
+        const u32 nw = w * (level + 1);
+        if (!span_w(L, (rsp0 - nw) & smask, nw)) return X_FAULT;
+        u64 rsp = (rsp0 - w) & smask, rbp = rbp0;
+        if (!vwrite(L, rsp, w, rbp0)) return X_FAULT;
         const u64 frame = rsp;
         if (level > 0) {
           for (u32 i = 1; i < level; i++) {
-            rbp -= 8;
+            rbp = (rbp - w) & smask;
             u64 t;
-            if (!vread(L, rbp, 8, t)) return X_FAULT;
-            rsp -= 8;
-            if (!vwrite(L, rsp, 8, t)) return X_FAULT;
+            if (!vread(L, rbp, w, t)) return X_FAULT;
+            rsp = (rsp - w) & smask;
+            if (!vwrite(L, rsp, w, t)) return X_FAULT;
           }
-          rsp -= 8;
-          if (!vwrite(L, rsp, 8, frame)) return X_FAULT;
+          rsp = (rsp - w) & smask;
+          if (!vwrite(L, rsp, w, frame)) return X_FAULT;
         }
         RS(L, 5, frame);
-        RS(L, 4, rsp - size);
+        RS(L, 4, (rsp - size) & smask);
         return X_OK;
       }
       case 0xca: case 0xcb:  // far ret (U29)
-        return far_pop(P, L, osz, c == 0xca ? (u.imm & 0xffff) : 0, false, next);
+        return far_pop(P, L, osz, c == 0xca ? (u.imm & 0xffff) : 0, false, m32, next);
       case 0xcf:  // iret / iretd (16- / 32-bit slots)
-        return far_pop(P, L, osz, 0, true, next);
+        return far_pop(P, L, osz, 0, true, m32, next);
       case 0xcd:  // int n (U24)
         if ((u.imm & 0xff) == 3) return X_INT3;
         return soft_int(P, L, (u32)u.imm & 0xff, true, nrip, next);
@@ -668,12 +778,13 @@ __device__ __noinline__ int sys2_exec(const Dev &P, Lane &L, const UOp &u, u64 n
         if (osz == 2) off &= 0xffff;
         if (!canonical(off)) return fault_x(L, WTFGPU_VEC_GP, 0);
         if (r3 == 3) {
-          const u64 rsp = R(L, 4);
-          if (!span_w(L, rsp - 2 * osz, 2 * osz)) return X_FAULT;
-          if (!vwrite(L, rsp - osz, osz, S.cs) || !vwrite(L, rsp - 2 * osz, osz, nrip)) return X_FAULT;
-          RS(L, 4, rsp - 2 * osz);
+          const u64 rsp = R(L, 4) & smask;
+          if (!span_w(L, (rsp - 2 * osz) & smask, 2 * osz)) return X_FAULT;
+          if (!vwrite(L, (rsp - osz) & smask, osz, S.cs) || !vwrite(L, (rsp - 2 * osz) & smask, osz, nrip))
+            return X_FAULT;
+          RS(L, 4, (rsp - 2 * osz) & smask);
         }
-        S.cs = (u16)((sel & 0xfffc) | cpl);
+        set_cs(L, S, (u32)((sel & 0xfffc) | cpl));
         next = off;
         return X_OK;
       }
@@ -837,7 +948,7 @@ __device__ __noinline__ int sys2_exec(const Dev &P, Lane &L, const UOp &u, u64 n
     case 0x34:  // sysenter
       if ((F.sysenter_cs & 0xfffc) == 0) return fault_x(L, WTFGPU_VEC_GP, 0);
       L.rflags &= ~(0x20000ull | 0x200ull | 0x10000ull);
-      S.cs = (u16)(F.sysenter_cs & 0xfffc);
+      set_cs(L, S, (u32)(F.sysenter_cs & 0xfffc));
       S.ss = (u16)((F.sysenter_cs & 0xfffc) + 8);
       if (cpl != 0) L.flush = 1;
       L.cpl = S.cpl = 0;
@@ -848,7 +959,7 @@ __device__ __noinline__ int sys2_exec(const Dev &P, Lane &L, const UOp &u, u64 n
       if (!rexw) return X_UNIMPL;
       if ((F.sysenter_cs & 0xfffc) == 0 || cpl) return fault_x(L, WTFGPU_VEC_GP, 0);
       if (!canonical(R(L, 2)) || !canonical(R(L, 1))) return fault_x(L, WTFGPU_VEC_GP, 0);
-      S.cs = (u16)(((F.sysenter_cs + 32) & 0xfffc) | 3);
+      set_cs(L, S, (u32)(((F.sysenter_cs + 32) & 0xfffc) | 3));
       S.ss = (u16)(((F.sysenter_cs + 40) & 0xfffc) | 3);
       L.flush = 1;
       L.cpl = S.cpl = 3;
@@ -857,17 +968,18 @@ __device__ __noinline__ int sys2_exec(const Dev &P, Lane &L, const UOp &u, u64 n
       return X_OK;
     case 0xa0:
     case 0xa8: {  // push fs / gs
-      const u32 sz = p66 ? 2 : 8;
-      if (!vwrite(L, R(L, 4) - sz, sz, F.seg[c == 0xa0 ? WTFGPU_FS : WTFGPU_GS].selector)) return X_FAULT;
-      RS(L, 4, R(L, 4) - sz);
+      const u32 sz = u.bsz;  // the stack slot
+      if (!vwrite(L, ((R(L, 4) & smask) - sz) & smask, sz, F.seg[c == 0xa0 ? WTFGPU_FS : WTFGPU_GS].selector))
+        return X_FAULT;
+      RS(L, 4, ((R(L, 4) & smask) - sz) & smask);
       return X_OK;
     }
     case 0xa1:
     case 0xa9: {  // pop fs / gs
-      const u32 sz = p66 ? 2 : 8;
-      if (!vread(L, R(L, 4), sz, a)) return X_FAULT;
+      const u32 sz = u.bsz;  // the stack slot
+      if (!vread(L, R(L, 4) & smask, sz, a)) return X_FAULT;
       if (!load_sreg(P, L, c == 0xa1 ? WTFGPU_FS : WTFGPU_GS, (u32)a & 0xffff, true)) return X_FAULT;
-      RS(L, 4, R(L, 4) + sz);
+      RS(L, 4, ((R(L, 4) & smask) + sz) & smask);
       return X_OK;
     }
     case 0xa2: {  // cpuid (U27)
