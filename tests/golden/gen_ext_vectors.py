@@ -3,7 +3,7 @@
 (convention U45; wtf_amd/csrc/engine_ext.h, oracle/x86_oracle_ext.inc):
 BMI1 / BMI2 (andn, bextr, blsi / blsmsk / blsr, bzhi, pdep, pext, mulx, rorx,
 sarx / shlx / shrx), ADX (adcx, adox), MOVBE, CRC32, SSE4.2 (pcmpgtq, the
-four string compares), AES and PCLMULQDQ, legacy and VEX, register and memory
+four string compares), AES, PCLMULQDQ and SHA, legacy and VEX, register and memory
 forms, 32- and 64-bit operand sizes (16 for movbe / crc32).
 
 Same machinery as gen_sse4_vectors.py (16 GPRs, RFLAGS, 16 YMM registers,
@@ -178,6 +178,21 @@ def gen_forms(rng):
         add(vrr(rng, 0x44, x(), x(), x(), 0, 1, mmmmm=3) + [k], "vpclmulqdq.rr")
     c, p, s = leg_mem(rng, 1, 0x44, x(), 16, map3=3)
     add(c + imm(), "pclmulqdq.m", ptrs=p, smalls=s)
+    # ---- SHA (no prefix, legacy only); own generator, so the forms above keep their encodings
+    srng = random.Random(0x5A4)
+    sx = lambda: srng.randrange(16)  # noqa: E731
+    for op, nm in ((0xC8, "sha1nexte"), (0xC9, "sha1msg1"), (0xCA, "sha1msg2"), (0xCB, "sha256rnds2"),
+                   (0xCC, "sha256msg1"), (0xCD, "sha256msg2")):
+        for _ in range(6):
+            add(leg_rr(0, op, sx(), sx(), map3=2), nm + ".rr")
+        for _ in range(2):
+            c, p, s = leg_mem(srng, 0, op, sx(), 16, map3=2)
+            add(c, nm + ".m", ptrs=p, smalls=s)
+    for k in range(4):
+        for _ in range(4):
+            add(leg_rr(0, 0xCC, sx(), sx(), map3=3) + [k | (srng.getrandbits(6) << 2)], "sha1rnds4.rr")
+    c, p, s = leg_mem(srng, 0, 0xCC, sx(), 16, map3=3)
+    add(c + [srng.randrange(256)], "sha1rnds4.m", ptrs=p, smalls=s)
     return forms
 
 

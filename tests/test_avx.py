@@ -163,7 +163,9 @@ AVX_FAULT_CASES = [
     ([0xF0, 0x66, 0x0F, 0x38, 0xF6, 0x06], EXIT_FAULT, 6),  # lock adcx: #UD (U34)
     ([0x66, 0x0F, 0x38, 0xDC, 0xC1], RUNNING, None),        # aesenc (AES)
     ([0x66, 0x0F, 0x38, 0x50, 0xC1], EXIT_FAULT, 6),        # 0f 38 50: undefined
-    ([0x0F, 0x38, 0xC9, 0xC1], EXIT_UNIMPLEMENTED, None),   # sha1msg1: SHA defined, not executed
+    ([0x0F, 0x38, 0xC9, 0xC1], RUNNING, None),              # sha1msg1 (SHA)
+    ([0x0F, 0x38, 0xC9, 0x06], EXIT_FAULT, 13),             # sha1msg1 xmm0, [rsi]: legacy needs alignment
+    ([0xC4, 0xE2, 0x78, 0xC9, 0xC1], EXIT_FAULT, 6),        # SHA has no VEX form
     ([0x66, 0x0F, 0x3A, 0x44, 0xC1, 0x00], RUNNING, None),  # pclmulqdq
     ([0x62, 0xF1, 0x7C, 0x48, 0x58, 0xC1], EXIT_UNIMPLEMENTED, None),  # EVEX vaddps zmm: AVX-512
     ([0x0F, 0x38, 0x00, 0xC1], EXIT_UNIMPLEMENTED, None),   # pshufb mm, mm (MMX form, defined)

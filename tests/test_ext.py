@@ -99,5 +99,6 @@ def test_ext_vector_file_is_substantial():
               "rorx", "adcx", "adox", "movbe16", "movbe32", "movbe64", "crc32b", "crc32w", "crc32d", "crc32q",
               "pcmpgtq", "vpcmpgtq", "pcmpestri", "pcmpestrm", "pcmpistri", "pcmpistrm", "vpcmpestri", "vpcmpistrm",
               "aesenc", "aesenclast", "aesdec", "aesdeclast", "aesimc", "aeskeygenassist", "vaesenc",
-              "pclmulqdq", "vpclmulqdq"):
+              "pclmulqdq", "vpclmulqdq", "sha1rnds4", "sha1nexte", "sha1msg1", "sha1msg2", "sha256rnds2",
+              "sha256msg1", "sha256msg2"):
         assert n in names, n

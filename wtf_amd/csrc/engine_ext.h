@@ -192,8 +192,10 @@ __device__ __noinline__ int gext_exec(const Dev &P, Lane &L, const UOp &u, u64 n
 }
 
 // ---------------------------------------------------------------- SIMD forms
-// 66 0f 38 37 db-df, 66 0f 3a 44 60-63 df; VEX the same (pp = 66)
-__host__ __device__ inline bool x42_form(u32 map, u32 c, u32 pp, bool) {
+// 66 0f 38 37 db-df, 66 0f 3a 44 60-63 df; VEX the same (pp = 66); SHA:
+// 0f 38 c8-cd, 0f 3a cc (no prefix, no VEX form)
+__host__ __device__ inline bool x42_form(u32 map, u32 c, u32 pp, bool vex) {
+  if (pp == 0 && !vex) return (map == 2 && c >= 0xc8 && c <= 0xcd) || (map == 3 && c == 0xcc);
   if (pp != 1) return false;
   if (map == 2) return c == 0x37 || (c >= 0xdb && c <= 0xdf);
   if (map == 3) return c == 0x44 || (c >= 0x60 && c <= 0x63) || c == 0xdf;
@@ -355,6 +357,67 @@ __device__ __forceinline__ u32 str_elen(u64 r, u32 wide, u32 n) {
   return m > n ? n : (u32)m;
 }
 
+// SHA-1 / SHA-256 message and round helpers (SDM vol. 2 SHA1RNDS4 ..
+// SHA256MSG2); dwords d[0] = bits 31:0 .. d[3] = bits 127:96
+__device__ __forceinline__ u32 rol32(u32 x, u32 k) { return (x << k) | (x >> (32 - k)); }
+__device__ __forceinline__ u32 ror32(u32 x, u32 k) { return (x >> k) | (x << (32 - k)); }
+__device__ __forceinline__ void x4(const X128 &v, u32 *d) {
+  d[0] = (u32)v.lo, d[1] = (u32)(v.lo >> 32), d[2] = (u32)v.hi, d[3] = (u32)(v.hi >> 32);
+}
+__device__ __forceinline__ X128 x4set(u32 d0, u32 d1, u32 d2, u32 d3) {
+  return X128{(u64)d0 | ((u64)d1 << 32), (u64)d2 | ((u64)d3 << 32)};
+}
+// c: 0f 38 c8 sha1nexte, c9 sha1msg1, ca sha1msg2, cb sha256rnds2 (wk = xmm0),
+// cc sha256msg1, cd sha256msg2; 0f 3a cc sha1rnds4 (imm: f / K)
+__device__ __noinline__ X128 sha_op(u32 map, u32 c, X128 a, X128 b, X128 wk, u32 imm) {
+  u32 s[4], t[4], w[4];
+  x4(a, s);
+  x4(b, t);
+  if (map == 3) {  // sha1rnds4: A B C D from src1, W0+E W1 W2 W3 from src2
+    const u32 K[4] = {0x5A827999u, 0x6ED9EBA1u, 0x8F1BBCDCu, 0xCA62C1D6u};
+    const u32 f = imm & 3;
+    u32 A = s[3], B = s[2], C = s[1], D = s[0], E = 0;
+    const u32 W[4] = {t[3], t[2], t[1], t[0]};
+    for (u32 i = 0; i < 4; i++) {
+      const u32 fv = f == 0 ? ((B & C) ^ (~B & D)) : f == 2 ? ((B & C) ^ (B & D) ^ (C & D)) : (B ^ C ^ D);
+      const u32 nA = fv + rol32(A, 5) + W[i] + E + K[f];
+      E = D, D = C, C = rol32(B, 30), B = A, A = nA;
+    }
+    return x4set(D, C, B, A);
+  }
+  switch (c) {
+    case 0xc8:  // sha1nexte
+      return x4set(t[0], t[1], t[2], t[3] + rol32(s[3], 30));
+    case 0xc9:  // sha1msg1
+      return x4set(t[2] ^ s[0], t[3] ^ s[1], s[0] ^ s[2], s[1] ^ s[3]);
+    case 0xca: {  // sha1msg2
+      const u32 w16 = rol32(s[3] ^ t[2], 1), w17 = rol32(s[2] ^ t[1], 1), w18 = rol32(s[1] ^ t[0], 1);
+      const u32 w19 = rol32(s[0] ^ w16, 1);
+      return x4set(w19, w18, w17, w16);
+    }
+    case 0xcb: {  // sha256rnds2: A B E F from src2, C D G H from src1, WK0 / WK1 from xmm0
+      x4(wk, w);
+      u32 A = t[3], B = t[2], C = s[3], D = s[2], E = t[1], F = t[0], G = s[1], H = s[0];
+      for (u32 i = 0; i < 2; i++) {
+        const u32 ch = (E & F) ^ (~E & G), maj = (A & B) ^ (A & C) ^ (B & C);
+        const u32 s0 = ror32(A, 2) ^ ror32(A, 13) ^ ror32(A, 22), s1 = ror32(E, 6) ^ ror32(E, 11) ^ ror32(E, 25);
+        const u32 t1 = ch + s1 + w[i] + H;
+        H = G, G = F, F = E, E = t1 + D, D = C, C = B, B = A, A = t1 + maj + s0;
+      }
+      return x4set(F, E, B, A);
+    }
+    case 0xcc: {  // sha256msg1
+      auto sg0 = [](u32 x) { return ror32(x, 7) ^ ror32(x, 18) ^ (x >> 3); };
+      return x4set(s[0] + sg0(s[1]), s[1] + sg0(s[2]), s[2] + sg0(s[3]), s[3] + sg0(t[0]));
+    }
+    default: {  // 0xcd sha256msg2
+      auto sg1 = [](u32 x) { return ror32(x, 17) ^ ror32(x, 19) ^ (x >> 10); };
+      const u32 w16 = s[0] + sg1(t[2]), w17 = s[1] + sg1(t[3]), w18 = s[2] + sg1(w16), w19 = s[3] + sg1(w17);
+      return x4set(w16, w17, w18, w19);
+    }
+  }
+}
+
 // One attempt at a SIMD extension form (legacy: the CR0 / CR4 checks ran in sse_exec).
 __device__ __noinline__ int x42_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next) {
   next = nrip;
@@ -363,7 +426,8 @@ __device__ __noinline__ int x42_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
   const u32 l256 = vex ? (x >> 1) & 1 : 0, W = vex ? (x >> 2) & 1 : (u.rex >> 3) & 1, vvvv = vex ? (x >> 4) & 15 : 0;
   const u32 imm = (u32)u.imm & 0xff;
   const bool str = map == 3 && c >= 0x60 && c <= 0x63;
-  const bool two = (map == 2 && c == 0xdb) || (map == 3 && c == 0xdf) || str;
+  const bool sha = (map == 2 && c >= 0xc8 && c <= 0xcd) || (map == 3 && c == 0xcc);
+  const bool two = (map == 2 && c == 0xdb) || (map == 3 && c == 0xdf) || str || sha;
   if (vex) {
     // VAES / VPCLMULQDQ (VEX.256): defined, not enumerated, not executed
     if (l256 && ((map == 2 && c >= 0xdc) || (map == 3 && c == 0x44))) return X_UNIMPL;
@@ -418,7 +482,9 @@ __device__ __noinline__ int x42_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
     return X_OK;
   }
   Y256 r{X128{0, 0}, X128{0, 0}};
-  if (map == 2 && c == 0x37) {  // pcmpgtq
+  if (sha) {
+    r.l = sha_op(map, c, a.l, b.l, c == 0xcb ? xmm_get(P, L, 0) : X128{0, 0}, imm);
+  } else if (map == 2 && c == 0x37) {  // pcmpgtq
     for (u32 i = 0; i < vl / 8; i++) yset(r, i, 8, (i64)yel(a, i, 8) > (i64)yel(b, i, 8) ? ~0ull : 0);
   } else if (map == 2) {  // aesimc (db), aesenc / enclast / dec / declast (dc-df): state a, round key b
     r.l = c == 0xdb ? aes_round(b.l, X128{0, 0}, 4) : aes_round(a.l, b.l, c - 0xdc);

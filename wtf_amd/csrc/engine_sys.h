@@ -134,7 +134,8 @@ __device__ __noinline__ void cpuid_leaf(u64 cr4, u64 xcr0, u32 leaf, u32 sub, u3
            (1u << 23) | (1u << 25) | (1u << 26) | (osxsave << 27) | (1u << 28) | (1u << 29) | (1u << 30);
     r[3] = 0x078bfbfd;
   } else if (leaf == 7) {
-    if (sub == 0) r[1] = (1u << 0) | (1u << 3) | (1u << 5) | (1u << 8) | (1u << 9) | (1u << 19);  // FSGSBASE BMI1 AVX2 BMI2 ERMS ADX
+    if (sub == 0)  // FSGSBASE BMI1 AVX2 BMI2 ERMS ADX SHA
+      r[1] = (1u << 0) | (1u << 3) | (1u << 5) | (1u << 8) | (1u << 9) | (1u << 19) | (1u << 29);
   } else if (leaf == 0xd) {
     if (sub == 0) {
       r[0] = 0x1f;
