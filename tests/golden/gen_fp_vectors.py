@@ -177,6 +177,21 @@ def gen_forms(rng):
             for op in (0x2C, 0x2D):
                 both(f"v{'t' if op == 0x2C else ''}cvts{SUF[pp][1]}2si.w{w}", 8 if pp == 3 else 4,
                      lambda: vrr(rng, op, g(), 0, x(), 0, pp, w=w), lambda: vmem(rng, op, g(), 0, 0, pp, 1, w=w))
+    # ---- dpps / dppd, legacy and VEX (own generator: the forms above keep their encodings)
+    drng = random.Random(0xD99)
+    dx = lambda: drng.randrange(16)  # noqa: E731
+    for op, nm, ew in ((0x40, "dpps", 4), (0x41, "dppd", 8)):
+        for _ in range(6):
+            forms.append(Form(leg_rr(1, op, dx(), dx(), map3=3) + [drng.randrange(256)], nm + ".rr", ew))
+        for _ in range(2):
+            c, p, s = leg_mem(drng, 1, op, dx(), 16, map3=3)
+            forms.append(Form(c + [drng.randrange(256)], nm + ".m", ew, p, s))
+        for l in ((0, 1) if op == 0x40 else (0,)):
+            for _ in range(4):
+                forms.append(Form(vrr(drng, op, dx(), dx(), dx(), l, 1, mmmmm=3) + [drng.randrange(256)],
+                                  f"v{nm}.L{l}.rr", ew))
+            c, p, s = vmem(drng, op, dx(), dx(), l, 1, 1, mmmmm=3)
+            forms.append(Form(c + [drng.randrange(256)], f"v{nm}.L{l}.m", ew, p, s))
     return forms
 
 

@@ -147,10 +147,12 @@ FP_FAULT_CASES = [
     ([0xC4, 0xE3, 0xF1, 0x4A, 0xC2, 0x30], EXIT_FAULT, 6),   # vblendvps with VEX.W = 1
     ([0xC4, 0xE3, 0x71, 0x4A, 0xC2, 0x30], RUNNING, None),   # vblendvps xmm0, xmm1, xmm2, xmm3
     ([0x66, 0xC5, 0xF8, 0x58, 0xC1], EXIT_FAULT, 6),         # 66 before VEX
-    # outside the executed set: MMX-operand conversions, dpps, rcpps / rsqrtps
+    ([0x66, 0x0F, 0x3A, 0x40, 0xC1, 0xFF], RUNNING, None),   # dpps
+    ([0x66, 0x0F, 0x3A, 0x41, 0x06, 0x33], EXIT_FAULT, 13),  # dppd xmm0, [rsi]: legacy needs alignment
+    ([0xC4, 0xE3, 0x7D, 0x40, 0x06, 0xFF], RUNNING, None),   # vdpps ymm0, ymm0, [rsi]
+    # outside the executed set: MMX-operand conversions, rcpps / rsqrtps
     ([0x0F, 0x2A, 0xC1], EXIT_UNIMPLEMENTED, None),          # cvtpi2ps xmm0, mm1
     ([0x0F, 0x2D, 0xC1], EXIT_UNIMPLEMENTED, None),          # cvtps2pi mm0, xmm1
-    ([0x66, 0x0F, 0x3A, 0x40, 0xC1, 0xFF], EXIT_UNIMPLEMENTED, None),  # dpps
     ([0x0F, 0x53, 0xC1], EXIT_UNIMPLEMENTED, None),          # rcpps
     ([0x0F, 0x52, 0xC1], EXIT_UNIMPLEMENTED, None),          # rsqrtps
 ]

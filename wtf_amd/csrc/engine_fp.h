@@ -44,7 +44,7 @@ __host__ __device__ inline bool fp_form(u32 map, u32 c, u32 pp, bool vex) {
   }
   if (pp != 1) return false;
   if (map == 2) return !vex && (c == 0x14 || c == 0x15);
-  if (map == 3) return (c >= 0x08 && c <= 0x0d) || (vex && (c == 0x4a || c == 0x4b));
+  if (map == 3) return (c >= 0x08 && c <= 0x0d) || c == 0x40 || c == 0x41 || (vex && (c == 0x4a || c == 0x4b));
   return false;
 }
 

@@ -41,7 +41,7 @@ __device__ __forceinline__ int xm_fault(Lane &L, u64 cr4) {
 }
 
 enum : u32 { FK_ARITH, FK_CMP, FK_COMI, FK_CVTF, FK_CVTI, FK_CVTPD, FK_SI2F, FK_F2SI, FK_HADD, FK_DUP, FK_LDDQU,
-             FK_ROUND, FK_BLEND, FK_BLENDV };
+             FK_ROUND, FK_BLEND, FK_BLENDV, FK_DP };
 
 __device__ __noinline__ int fp_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next) {
   next = nrip;
@@ -89,6 +89,9 @@ __device__ __noinline__ int fp_exec(const Dev &P, Lane &L, const UOp &u, u64 nri
   } else if (map == 2) {
     k = FK_BLENDV;
     w = c & 1;
+  } else if (c == 0x40 || c == 0x41) {  // dpps / dppd
+    k = FK_DP;
+    w = c & 1;
   } else if (c <= 0x0b) {
     k = FK_ROUND;
     w = c & 1;
@@ -107,6 +110,7 @@ __device__ __noinline__ int fp_exec(const Dev &P, Lane &L, const UOp &u, u64 nri
     if (!((cr4 >> 18) & 1) || (P.full[L.lane].xcr0 & 6) != 6) ud = true;
     if (two_op && vvvv != 0) ud = true;
     if (k == FK_BLENDV && W) ud = true;
+    if (k == FK_DP && w && l256) ud = true;  // vdppd has no 256-bit form
     if (k == FK_LDDQU && !mem) ud = true;
     if (ud) {
       set_fault(L, WTFGPU_VEC_UD, 0, 0);
@@ -262,6 +266,34 @@ __device__ __noinline__ int fp_exec(const Dev &P, Lane &L, const UOp &u, u64 nri
     case FK_BLEND:
       for (u32 i = 0; i < ne; i++) yset(r, i, ew, ((imm >> i) & 1) ? yel(b, i, ew) : yel(a, i, ew));
       break;
+    case FK_DP: {
+      // SDM DPPS / DPPD, as the hardware evaluates the sum: per 128-bit lane,
+      // products t_j (imm8[7:4] selects, else +0.0); dpps: for element i
+      // s_i = t_(i^1) + t_i, then s_i + s_(i^2); dppd: t_0 + t_1 for both;
+      // written where imm8[3:0] selects (+0.0 elsewhere). The operand order
+      // only shows in which NaN propagates (the fp vectors pin it). An
+      // unmasked exception ends the instruction at the step that raised it,
+      // the flags of the steps before it already in MXCSR (native vectors).
+      const u32 per = 16 / ew, nl = vl / 16;
+      u64 t[8], s1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      auto trapped = [&]() {
+        if (v.fl & ~v.masks & 63) return true;
+        F.mxcsr |= v.fl;  // the step completed: its flags stand
+        v.fl = 0;
+        return false;
+      };
+      for (u32 j = 0; j < per * nl; j++)
+        t[j] = ((imm >> (4 + j % per)) & 1) ? f_arith(v, FOP_MUL, yel(a, j, ew), yel(b, j, ew), w) : 0;
+      if (!trapped())
+        for (u32 j = 0; j < per * nl; j++)
+          s1[j] = per == 4 ? f_arith(v, FOP_ADD, t[j ^ 1], t[j], w) : f_arith(v, FOP_ADD, t[j & ~1u], t[j | 1], w);
+      if (!trapped() && per == 4)
+        for (u32 j = 0; j < per * nl; j++) t[j] = f_arith(v, FOP_ADD, s1[j], s1[j ^ 2], w);
+      else
+        for (u32 j = 0; j < per * nl; j++) t[j] = s1[j];
+      for (u32 j = 0; j < per * nl; j++) yset(r, j, ew, ((imm >> (j % per)) & 1) ? t[j] : 0);
+      break;
+    }
     default: {  // FK_BLENDV: the mask is xmm0 (legacy) or the register in imm8[7:4]
       const Y256 m = vex ? ymm_get(P, L, imm >> 4) : Y256{xmm_get(P, L, 0), X128{0, 0}};
       for (u32 i = 0; i < ne; i++) yset(r, i, ew, (yel(m, i, ew) >> (8 * ew - 1)) ? yel(b, i, ew) : yel(a, i, ew));
