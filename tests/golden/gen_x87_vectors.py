@@ -174,7 +174,55 @@ def make_cases(seed=0x87, per_reg=5, per_mem=48):
         for _ in range(per_mem):
             m = rand_mem(rng, kind) if not store else bytes(rng.getrandbits(8) for _ in range(10))
             cases.append(dict(code=code.hex(), mem=m.ljust(16, b"\0").hex(), **rand_state(rng, rng.random() < 0.03)))
+    # fbld / fbstp (own generator: the cases above keep their values)
+    brng = random.Random(seed ^ 0xBCD)
+    for code in (bytes([0xDF, 0x26]), bytes([0xDF, 0x36])):
+        for _ in range(per_mem * 4):
+            st = rand_state(brng, brng.random() < 0.03)
+            if code[1] == 0x26:
+                m = rand_bcd(brng)
+            else:
+                m = bytes(brng.getrandbits(8) for _ in range(10))
+                if brng.random() < 0.7:  # ST0 in (or near) the packed-BCD range, and valid
+                    st["st"][0] = bcd_range_f80(brng)
+                    top = (st["fsw"] >> 11) & 7
+                    st["ftw"] &= ~(3 << (2 * top))
+            cases.append(dict(code=code.hex(), mem=m.ljust(16, b"\0").hex(), **st))
     return cases
+
+
+def rand_bcd(rng):
+    """18 packed digits (a nibble above 9 now and then) and a sign byte."""
+    k = rng.random()
+    if k < 0.05:
+        return bytes(9) + bytes([rng.choice([0, 0x80])])
+    if k < 0.1:
+        return bytes([0x99] * 9) + bytes([rng.choice([0, 0x80])])
+    if k < 0.15:
+        return bytes([0, 0, 0, 0, 0, 0, 0, 0xC0, 0xFF, 0xFF])  # the BCD indefinite
+    n = rng.randint(1, 18)
+    digits = [rng.randrange(10) if i < n else 0 for i in range(18)]
+    if rng.random() < 0.15:
+        digits[rng.randrange(18)] = rng.randint(10, 15)
+    b = bytes(digits[2 * i] | (digits[2 * i + 1] << 4) for i in range(9))
+    return b + bytes([rng.choice([0, 0x80, 0x80, rng.getrandbits(8)])])
+
+
+def bcd_range_f80(rng):
+    """An extended value around the packed-BCD range: integers, fractions, halves, 10^18 +- 1."""
+    k = rng.random()
+    if k < 0.1:
+        v, frac = 10**18 + rng.choice([-1, 0, 1]), 0
+    else:
+        v = rng.randint(0, 10**rng.randint(0, 18))
+        frac = rng.choice([0, 0, 1, 2, 3])  # none, a quarter, a half, three quarters
+    s = rng.getrandbits(1)
+    num = v * 4 + frac
+    if num == 0:
+        return 0, s << 15
+    e = num.bit_length() - 1  # num = 1.f * 2^e, value = num / 4
+    m = (num << (63 - e)) & ((1 << 64) - 1) if e <= 63 else num >> (e - 63)
+    return m, (s << 15) | (0x3FFF + e - 2)
 
 
 def run_oracle(c, buf_va):

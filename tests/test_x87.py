@@ -108,7 +108,7 @@ X87_FAULT_CASES = [
     ([0xDB, 0x26], EXIT_FAULT, 6, {}),                        # db /4 m: reserved
     ([0xD9, 0xFE], EXIT_UNIMPLEMENTED, None, {}),             # fsin: outside
     ([0xD9, 0xFF], EXIT_UNIMPLEMENTED, None, {}),             # fcos: outside
-    ([0xDF, 0x26], EXIT_UNIMPLEMENTED, None, {}),             # fbld: outside
+    ([0xDF, 0x26], 0, None, {}),                              # fbld m80bcd (runs)
     ([0xD8, 0xC1], EXIT_FAULT, 16, dict(fcw=0x37E, fsw=0x8081)),  # pending unmasked IE: #MF
     ([0xD8, 0xC1], EXIT_FAULT, 16, dict(fcw=0x37E, fsw=0x0001)),  # pending even with ES clear
     ([0xD8, 0xC1], 0, None, dict(fcw=0x37F, fsw=0x0080)),     # ES alone, every flag masked: runs

@@ -15,8 +15,8 @@
 // destinations; a memory destination is not written). Any unmasked exception
 // sets ES and B; the next waiting x87 instruction then takes #MF first.
 // FOP / FIP / FDP are not maintained (U32). The transcendental forms (f2xm1,
-// fyl2x, fptan, fpatan, fyl2xp1, fsincos, fsin, fcos) and the BCD forms
-// (fbld, fbstp) stay UNIMPLEMENTED.
+// fyl2x, fptan, fpatan, fyl2xp1, fsincos, fsin, fcos) stay UNIMPLEMENTED.
+// fbld / fbstp: 18 packed BCD digits and a sign byte (x87 vectors pin them).
 #pragma once
 #include "engine_fp.h"
 
@@ -689,9 +689,30 @@ __device__ __noinline__ F80 x_fprem(XEnv &v, F80 a, F80 b, bool near, u32 &cc) {
 }
 
 // ---------------------------------------------------------------- memory operands
-enum : u32 { XM_NONE, XM_F32, XM_F64, XM_F80, XM_I16, XM_I32, XM_I64 };
+enum : u32 { XM_NONE, XM_F32, XM_F64, XM_F80, XM_I16, XM_I32, XM_I64, XM_BCD };
 __device__ __forceinline__ u32 xm_bytes(u32 k) {
-  return k == XM_F32 || k == XM_I32 ? 4 : k == XM_F64 || k == XM_I64 ? 8 : k == XM_F80 ? 10 : k == XM_I16 ? 2 : 0;
+  return k == XM_F32 || k == XM_I32 ? 4 : k == XM_F64 || k == XM_I64 ? 8 : (k == XM_F80 || k == XM_BCD) ? 10
+         : k == XM_I16 ? 2 : 0;
+}
+// packed BCD (fbld): digit i in nibble i of bytes 0-8, the sign in byte 9's bit
+// 7; a nibble above 9 counts with its binary value, as the hardware reads it
+__device__ __forceinline__ F80 x_from_bcd(u64 lo, u64 hi) {
+  u64 v = 0, p = 1;
+  for (u32 i = 0; i < 18; i++, p *= 10) v += (i < 16 ? (lo >> (4 * i)) & 15 : (hi >> (4 * (i - 16))) & 15) * p;
+  const u32 s = (u32)(hi >> 15) & 1;
+  if (!v) return F80{0, s << 15};
+  const F80 r = x_from_int((i64)v);
+  return F80{r.m, r.se | (s << 15)};
+}
+// fbstp: |q| <= 10^18 - 1 as 18 digits, sign s; the BCD indefinite otherwise
+__device__ __forceinline__ void x_to_bcd(u64 q, u32 s, u64 &lo, u64 &hi) {
+  lo = 0;
+  hi = (u64)s << 15;
+  for (u32 i = 0; i < 18; i++, q /= 10) {
+    const u64 d = q % 10;
+    if (i < 16) lo |= d << (4 * i);
+    else hi |= d << (4 * (i - 16));
+  }
 }
 // a memory source as an extended value (den: denormal m32 / m64)
 __device__ __forceinline__ F80 xm_value(u32 k, u64 lo, u64 hi, bool &den) {
@@ -702,16 +723,17 @@ __device__ __forceinline__ F80 xm_value(u32 k, u64 lo, u64 hi, bool &den) {
     case XM_F80: return F80{lo, (u32)hi & 0xffff};
     case XM_I16: return x_from_int((i64)(int16_t)lo);
     case XM_I32: return x_from_int((i64)(int32_t)lo);
+    case XM_BCD: return x_from_bcd(lo, hi);
     default: return x_from_int((i64)lo);
   }
 }
 __device__ __forceinline__ bool xm_read(Lane &L, u64 va, u32 k, u64 &lo, u64 &hi) {
   hi = 0;
-  if (k == XM_F80) return vread(L, va, 8, lo) && vread(L, va + 8, 2, hi);
+  if (k == XM_F80 || k == XM_BCD) return vread(L, va, 8, lo) && vread(L, va + 8, 2, hi);
   return vread(L, va, xm_bytes(k), lo);
 }
 __device__ __forceinline__ bool xm_write(Lane &L, u64 va, u32 k, u64 lo, u64 hi) {
-  if (k == XM_F80) return span_w(L, va, 10) && vwrite(L, va, 8, lo) && vwrite(L, va + 8, 2, hi);
+  if (k == XM_F80 || k == XM_BCD) return span_w(L, va, 10) && vwrite(L, va, 8, lo) && vwrite(L, va + 8, 2, hi);
   return vwrite(L, va, xm_bytes(k), lo);
 }
 
@@ -748,9 +770,8 @@ __device__ __noinline__ int x87_arith(const Dev &P, Lane &L, const UOp &u, u64 v
         store = r3 != 0;
         break;
       default:  // df
-        if (r3 == 4 || r3 == 6) return X_UNIMPL;  // fbld, fbstp
-        mk = r3 == 5 || r3 == 7 ? XM_I64 : XM_I16;
-        store = r3 != 0 && r3 != 5;
+        mk = r3 == 4 || r3 == 6 ? XM_BCD : r3 == 5 || r3 == 7 ? XM_I64 : XM_I16;
+        store = r3 != 0 && r3 != 4 && r3 != 5;
         break;
     }
   } else {
@@ -814,7 +835,7 @@ __device__ __noinline__ int x87_arith(const Dev &P, Lane &L, const UOp &u, u64 v
       switch (mk) {
         case XM_F32: lo = f_indef(0); break;
         case XM_F64: lo = f_indef(1); break;
-        case XM_F80: lo = 0xc000000000000000ull, hi = 0xffff; break;
+        case XM_F80: case XM_BCD: lo = 0xc000000000000000ull, hi = 0xffff; break;
         case XM_I16: lo = 0x8000; break;
         case XM_I32: lo = 0x80000000ull; break;
         default: lo = 0x8000000000000000ull; break;
@@ -826,6 +847,24 @@ __device__ __noinline__ int x87_arith(const Dev &P, Lane &L, const UOp &u, u64 v
       } else if (mk == XM_F32 || mk == XM_F64) {
         lo = x_to_f(v, a, mk == XM_F64);
         write = !(v.fl & ~masks & (SW_IE | SW_OE | SW_UE));
+      } else if (mk == XM_BCD) {  // fbstp: rounded by RC, at most 18 digits
+        u64 q = 0;
+        bool ok = x_to_int(v, a, 8, v.rc, q);
+        const u32 sgn = x_sign(a);
+        if (ok) {
+          const u64 mag = sgn ? (u64)0 - q : q;
+          if (mag > 999999999999999999ull) {
+            v.fl = (v.fl & ~(SW_PE)) | SW_IE;
+            v.c1 = 0;
+            ok = false;
+          } else {
+            x_to_bcd(mag, sgn, lo, hi);
+          }
+        }
+        if (!ok) {
+          lo = 0xc000000000000000ull, hi = 0xffff;
+          write = (masks & SW_IE) != 0;
+        }
       } else {
         const u32 isz = mk == XM_I16 ? 2 : mk == XM_I32 ? 4 : 8;
         const u32 rc = r3 == 1 ? 3u : v.rc;  // fisttp truncates
