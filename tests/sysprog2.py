@@ -39,12 +39,14 @@ UST = 0x00007FF000000000 - 0x4000  # user stack: 4 pages below this + 0x4000
 USP = UST + 0x3000
 DATA = 0x0000000150000000        # 4 pages user rw (images, far pointers, scratch); DATA + 0x4000 unmapped
 KDATA = 0xFFFFF80000800000       # 1 page supervisor rw
-GDT_LIMIT = 0x7F
+LDT_BASE = 0xFFFFF80000005000    # the LDT descriptor's base (no page: LLDT reads only the GDT)
+GDT_LIMIT = 0x9F
 
 # GDT: 0x10 kernel code, 0x18 kernel data, 0x23 user code32, 0x2b user data,
 # 0x33 user code64, 0x38 not present, 0x40 TSS (16 bytes), 0x53 data base
 # 0x12345000 (DPL 3), 0x5b not-present data, 0x60 conforming code, 0x68 data
-# DPL 0, 0x70 read-only data DPL 3, 0x78 data with G=1
+# DPL 0, 0x70 read-only data DPL 3, 0x78 data with G=1, 0x80 LDT (16 bytes),
+# 0x90 a second TSS (16 bytes, at TSS + 0x800: its own RSP0 / IST1)
 def _desc(base, limit, typ, s=1, dpl=0, p=1, l=0, db=1, g=0):
     return ((limit & 0xFFFF) | ((base & 0xFFFFFF) << 16) | (typ << 40) | (s << 44) | (dpl << 45) | (p << 47) |
             (((limit >> 16) & 0xF) << 48) | (l << 53) | (db << 54) | (g << 55) | (((base >> 24) & 0xFF) << 56))
@@ -63,6 +65,8 @@ def gdt_page() -> bytes:
     for off, v in ent.items():
         struct.pack_into("<Q", g, off, v)
     struct.pack_into("<QQ", g, 0x40, _desc(TSS & 0xFFFFFFFF, 0x67, 0x9, s=0, db=0), TSS >> 32)
+    struct.pack_into("<QQ", g, 0x80, _desc(LDT_BASE & 0xFFFFFFFF, 0xFFF, 0x2, s=0, db=0), LDT_BASE >> 32)
+    struct.pack_into("<QQ", g, 0x90, _desc((TSS + 0x800) & 0xFFFFFFFF, 0x67, 0x9, s=0, db=0), TSS >> 32)
     return bytes(g)
 
 
@@ -158,6 +162,11 @@ K = {  # ring 0 (each ends with hlt; a fault ends the lane)
     "rdrand16": "rdrand ax\n rdseed rbx\n hlt",
     "sysret32": "mov ecx, r8d\n mov r11d, 0x202\n .byte 0x0f, 0x07",  # to compatibility mode: the fetch faults
     "to_user": TO_USER,
+    "ltr": "ltr r8w\n str r9w\n hlt",
+    "ltr2": "ltr r8w\n ltr r8w\n hlt",           # the second finds the TSS busy: #GP(sel)
+    "ltrist": "ltr r8w\n int 0x2e\n hlt",          # IST1 from the new TSS
+    "lldt": "lldt r8w\n sldt r9w\n hlt",
+    "lldtm": "lldt [rsi]\n hlt",
 }
 U = {  # ring 3, entered through to_user (each ends with int3)
     "u_int29": "int 0x29\n int3",
@@ -265,6 +274,8 @@ def build_space(seed: int = 0x5157):
     tss = bytearray(0x1000)
     struct.pack_into("<Q", tss, 4, KSP + 0x800)       # RSP0
     struct.pack_into("<Q", tss, 0x24, ISTSTACK + 0xF80)  # IST1
+    struct.pack_into("<Q", tss, 0x800 + 4, KSP + 0x400)     # the second TSS: RSP0
+    struct.pack_into("<Q", tss, 0x800 + 0x24, ISTSTACK + 0x780)  # and IST1
     sp.map(TSS, bytes(tss), user=False, nx=True)
     for i in range(8):
         sp.map(KSTACK + i * 0x1000, b"", user=False, nx=True)
@@ -383,6 +394,9 @@ def lanes(n: int, seed: int, st: dict, lay: dict, data: bytes):
             g[8] = rng.choice([0x33, 0x3B, 0x35, 0x30, 0x3F])
         elif name in ("rdpmc", "u_rdpmc"):
             g[8] = rng.choice([0, 3, 4, 0x40000000])
+        elif name in ("ltr", "ltr2", "ltrist", "lldt", "lldtm"):
+            g[8] = rng.choice([0x40, 0x90, 0x80, 0, 3, 0x44, 0x38, 0x10, 0x2B, 0x1000, 0x93, 0x98])
+            g[6] = DATA + 0x3000 + 16 * rng.randrange(6)
         elif name in ("lar", "u_lar"):
             g[8] = rng.choice(SELS)
         elif name == "sysenter":

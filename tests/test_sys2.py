@@ -254,3 +254,25 @@ def test_gpu_matches_oracle(space):
         assert not bad, f"{len(bad)}/{n} lanes differ; first: {bad[:3]}"
     finally:
         eng.close()
+
+
+def test_ltr_lldt(space):
+    """LTR / LLDT read 16-byte GDT system descriptors; LTR marks the TSS busy in
+    the GDT and the IST / RSP0 stacks come from the new TSS (SDM LTR, LLDT)."""
+    r = _one(space, "ltr", r8=0x90)
+    assert r["exit"][0] == HLT and r["gpr"][9] == 0x90 and r["sel"][6] == 0x90
+    gdt = [p for a, p in r["pages"].items()]
+    assert any(struct.unpack_from("<Q", p, 0x90)[0] >> 40 & 0xF == 0xB for p in gdt)  # busy now
+    assert _one(space, "ltr2", r8=0x90)["exit"][:3] == (FAULT, 13, 0x90)   # busy: #GP(sel)
+    assert _one(space, "ltr", r8=0)["exit"][:3] == (FAULT, 13, 0)         # null: #GP(0)
+    assert _one(space, "ltr", r8=0x80)["exit"][:3] == (FAULT, 13, 0x80)   # an LDT, not a TSS
+    assert _one(space, "ltr", r8=0x44)["exit"][:3] == (FAULT, 13, 0x44)   # TI = 1
+    assert _one(space, "ltr", r8=0x98)["exit"][:3] == (FAULT, 13, 0x98)   # the descriptor's second half past the limit
+    r = _one(space, "ltrist", r8=0x90)  # IST1 of the second TSS
+    assert r["exit"][0] == HLT and r["gpr"][13] == ((S.ISTSTACK + 0x780) & ~0xF) - 40
+    r = _one(space, "lldt", r8=0x80)
+    assert r["exit"][0] == HLT and r["gpr"][9] == 0x80 and r["sel"][7] == 0x80
+    r = _one(space, "lldt", r8=3)  # a null selector leaves LDTR unusable, no fault
+    assert r["exit"][0] == HLT and r["gpr"][9] == 3
+    assert _one(space, "lldt", r8=0x90)["exit"][:3] == (FAULT, 13, 0x90)  # a TSS, not an LDT
+    assert _one(space, "u_lgdt")["exit"][0] != UNIMPL

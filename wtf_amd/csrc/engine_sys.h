@@ -804,7 +804,45 @@ __device__ __noinline__ int sys2_exec(const Dev &P, Lane &L, const UOp &u, u64 n
         setr(L, u.rex, u.rm, osz, a);
         return X_OK;
       }
-      if (r3 <= 3) return cpl ? fault_x(L, WTFGPU_VEC_GP, 0) : X_UNIMPL;  // lldt / ltr
+      if (r3 <= 3) {  // lldt / ltr: 16-byte system descriptors of the GDT (SDM LLDT / LTR, 64-bit mode)
+        if (cpl) return fault_x(L, WTFGPU_VEC_GP, 0);
+        if (u.is_mem) {
+          if (!vread(L, ea, 2, a)) return X_FAULT;
+        } else {
+          a = R(L, u.rm) & 0xffff;
+        }
+        const u32 sel = (u32)a & 0xffff, es = sel & 0xfffc, sr = r3 == 2 ? WTFGPU_LDTR : WTFGPU_TR;
+        if (es == 0) {  // ltr: #GP(0); lldt: LDTR unusable
+          if (r3 == 3) return fault_x(L, WTFGPU_VEC_GP, 0);
+          F.seg[sr].selector = (u16)sel;
+          F.seg[sr].present = 0;
+          return X_OK;
+        }
+        if ((sel & 4) || (u64)(sel | 7) + 8 > F.gdtr_limit) return fault_x(L, WTFGPU_VEC_GP, es);
+        const u64 da = F.gdtr_base + (sel & 0xfff8);
+        if (da & 7) return X_UNIMPL;  // a misaligned GDT (U35)
+        u64 d0, d1;
+        if (!sup_read_q(P, L, da, d0) || !sup_read_q(P, L, da + 8, d1)) return X_FAULT;
+        if (((d0 >> 40) & 0x1f) != (r3 == 2 ? 0x02u : 0x09u)) return fault_x(L, WTFGPU_VEC_GP, es);  // LDT / free TSS
+        if (!((d0 >> 47) & 1)) return fault_x(L, VEC_NP, es);
+        const u64 base = ((d0 >> 16) & 0xffffff) | (((d0 >> 56) & 0xff) << 24) | ((d1 & 0xffffffffull) << 32);
+        if (((d1 >> 40) & 0x1f) != 0 || !canonical(base)) return fault_x(L, WTFGPU_VEC_GP, es);
+        u64 lim = (d0 & 0xffff) | ((d0 >> 32) & 0xf0000);
+        if ((d0 >> 55) & 1) lim = (lim << 12) | 0xfff;
+        u64 nd0 = d0;
+        if (r3 == 3) {  // the TSS descriptor turns busy (the last access: nothing committed before it)
+          nd0 |= 2ull << 40;
+          u64 ga;
+          if (!sup_pa(P, L, da, 2, ga) || !sup_write_pa(P, L, ga, nd0)) return X_FAULT;
+          S.tss = base;
+        }
+        F.seg[sr].selector = (u16)sel;
+        F.seg[sr].base = base;
+        F.seg[sr].limit = (u32)lim;
+        F.seg[sr].attr = (u16)((nd0 >> 40) & 0xffff);
+        F.seg[sr].present = 1;
+        return X_OK;
+      }
       if (r3 <= 5) {  // verr / verw
         if (u.is_mem) {
           if (!vread(L, ea, 2, a)) return X_FAULT;
