@@ -103,3 +103,34 @@ def test_parallel_mutation_is_deterministic(target, tmp_path):
         out.append((sorted(os.listdir(os.path.join(d, "outputs"))), sorted(os.listdir(os.path.join(d, "crashes")))))
     assert out[0] == out[1]
     assert len(out[0][0]) > 10
+
+
+def test_dbgprintex_engine_error_path(target, tmp_path):
+    """The HEVD leg's engine errors (U43): an input 1-2 bytes longer than
+    TriggerBufferOverflowStack's frame (IOCTL 0x222003, no cookie) overwrites the
+    low bytes of the saved return address, the `ret` lands on nt!DbgPrintEx's
+    entry, and the module's handler reads a format pointer (r8) the guest never
+    set, which does not translate: the reference would __debugbreak there
+    (backend.cc:39-42); here the testcase ends as a handler fault.
+    tests/golden/hevd_dbgprint_error.bin was kept by a twin HEVD campaign
+    (all 21 errors of six 150 s campaigns were this IOCTL at 745-746 bytes)."""
+    import shutil
+    import struct
+
+    d = tmp_path / "in"
+    d.mkdir()
+    src = os.path.join(os.path.dirname(__file__), "golden", "hevd_dbgprint_error.bin")
+    shutil.copy(src, d / "err")
+    data = open(src, "rb").read()
+    assert struct.unpack_from("<I", data)[0] == 0x222003 and len(data) - 4 in (745, 746)
+    res = _run(target, str(d), str(tmp_path / "r.jsonl"))
+    r = res["err"]
+    assert r["error"] and r["handler_fault"], r
+    tr = tmp_path / "tr"
+    H.run(H.TWIN, target, str(d), str(tmp_path / "r2.jsonl"), lanes=1, name="hevd",
+          extra=("--trace-path", str(tr), "--trace-type", "rip"))
+    rips = [int(x, 16) for x in open(tr / "err.trace").read().split()]
+    import json
+    sym = json.load(open(os.path.join(target, "state", "symbol-store.json")))
+    assert rips[-1] == int(sym["nt!DbgPrintEx"], 16)                     # the last rip: the handler's
+    assert int(sym["nt!DbgPrintEx"], 16) < rips[-2] < int(sym["nt!DbgPrintEx"], 16) + 0x1000  # a ret in the driver
