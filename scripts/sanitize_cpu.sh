@@ -15,7 +15,7 @@ CC="gcc -std=gnu99 -fPIC $SAN"
 H=$ROOT/wtf_amd/host
 cd "$H"
 SRCS="wtf_api.cc kdmp.cc blake3_lite.cc host_pool.cc module_slots.cc module_instances.cc runner.cc mutator_lite.cc net_exchange.cc
-      wire.cc remote.cc modules/fuzzer_tlv_server.cc modules/crash_detection_umode.cc modules/fuzzer_hevd.cc"
+      wire.cc remote.cc merge_block.cc modules/fuzzer_tlv_server.cc modules/crash_detection_umode.cc modules/fuzzer_hevd.cc"
 objs=()
 pids=()
 for s in $SRCS; do
@@ -29,7 +29,7 @@ rm -f "$OUT/libwtfhost.a" && ar rcs "$OUT/libwtfhost.a" "${objs[@]}"
 cd "$ROOT/oracle"
 $CC -shared -o "$OUT/liboracle.so" x86_oracle.c
 $CC -c -o "$OUT/obj/x86_oracle.o" x86_oracle.c
-$CXX -o "$OUT/wtf_twin" twin_backend.cc "$OUT/obj/x86_oracle.o" -Wl,--whole-archive "$OUT/libwtfhost.a" -Wl,--no-whole-archive
+$CXX -rdynamic -o "$OUT/wtf_twin" twin_backend.cc "$OUT/obj/x86_oracle.o" -Wl,--whole-archive "$OUT/libwtfhost.a" -Wl,--no-whole-archive
 $CXX -DWTF_AMD_HOST -o "$OUT/hostcheck" hostcheck.cc -Wl,--whole-archive "$OUT/libwtfhost.a" -Wl,--no-whole-archive
 cd "$ROOT/tests/native"
 g++ -std=c++17 -DWTFGPU_HOST_SIM -fPIC -shared $SAN -o "$OUT/libsimlane.so" sim_lane.cc
