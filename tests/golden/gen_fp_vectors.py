@@ -192,6 +192,20 @@ def gen_forms(rng):
                                   f"v{nm}.L{l}.rr", ew))
             c, p, s = vmem(drng, op, dx(), dx(), l, 1, 1, mmmmm=3)
             forms.append(Form(c + [drng.randrange(256)], f"v{nm}.L{l}.m", ew, p, s))
+    # ---- rcpps / rcpss / rsqrtps / rsqrtss, legacy and VEX (own generator)
+    rrng = random.Random(0x4C9)
+    rx = lambda: rrng.randrange(16)  # noqa: E731
+    for op, nm in ((0x53, "rcp"), (0x52, "rsqrt")):
+        for pp, suf in ((0, "ps"), (2, "ss")):
+            for _ in range(5):
+                forms.append(Form(leg_rr(pp, op, rx(), rx()), f"{nm}{suf}.rr", 4))
+            c, p, s = leg_mem(rrng, pp, op, rx(), 16 if pp == 0 else 1)
+            forms.append(Form(c, f"{nm}{suf}.m", 4, p, s))
+            for l in ((0, 1) if pp == 0 else (0,)):
+                for _ in range(3):
+                    forms.append(Form(vrr(rrng, op, rx(), 0 if pp == 0 else rx(), rx(), l, pp), f"v{nm}{suf}.L{l}.rr", 4))
+                c, p, s = vmem(rrng, op, rx(), 0 if pp == 0 else rx(), l, pp, 1)
+                forms.append(Form(c, f"v{nm}{suf}.L{l}.m", 4, p, s))
     return forms
 
 

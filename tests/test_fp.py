@@ -150,11 +150,13 @@ FP_FAULT_CASES = [
     ([0x66, 0x0F, 0x3A, 0x40, 0xC1, 0xFF], RUNNING, None),   # dpps
     ([0x66, 0x0F, 0x3A, 0x41, 0x06, 0x33], EXIT_FAULT, 13),  # dppd xmm0, [rsi]: legacy needs alignment
     ([0xC4, 0xE3, 0x7D, 0x40, 0x06, 0xFF], RUNNING, None),   # vdpps ymm0, ymm0, [rsi]
-    # outside the executed set: MMX-operand conversions, rcpps / rsqrtps
+    ([0x0F, 0x53, 0xC1], RUNNING, None),                     # rcpps
+    ([0x0F, 0x52, 0x06], EXIT_FAULT, 13),                    # rsqrtps xmm0, [rsi]: legacy needs alignment
+    ([0xC5, 0xF0, 0x53, 0xC1], EXIT_FAULT, 6),               # vrcpps with vvvv != 1111
+    ([0xC5, 0xF2, 0x52, 0x06], RUNNING, None),               # vrsqrtss xmm0, xmm1, [rsi]
+    # outside the executed set: MMX-operand conversions
     ([0x0F, 0x2A, 0xC1], EXIT_UNIMPLEMENTED, None),          # cvtpi2ps xmm0, mm1
     ([0x0F, 0x2D, 0xC1], EXIT_UNIMPLEMENTED, None),          # cvtps2pi mm0, xmm1
-    ([0x0F, 0x53, 0xC1], EXIT_UNIMPLEMENTED, None),          # rcpps
-    ([0x0F, 0x52, 0xC1], EXIT_UNIMPLEMENTED, None),          # rsqrtps
 ]
 
 

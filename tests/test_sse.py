@@ -149,7 +149,7 @@ SSE_FAULT_CASES = [
     ([0x0F, 0xF7, 0xC1], EXIT_UNIMPLEMENTED, None),   # MMX maskmovq
     ([0x0F, 0x58, 0xC1], RUNNING, None),              # addps (floating point, U39)
     ([0xF2, 0x0F, 0xF0, 0x03], RUNNING, None),        # lddqu (SSE3, U39)
-    ([0x0F, 0x53, 0xC1], EXIT_UNIMPLEMENTED, None),   # rcpps (an approximation, outside)
+    ([0x0F, 0x53, 0xC1], RUNNING, None),              # rcpps (the host CPU's table, U40)
 ]
 
 

@@ -32,6 +32,7 @@ __host__ __device__ inline bool fp_form(u32 map, u32 c, u32 pp, bool vex) {
       case 0x51: case 0x58: case 0x59: case 0x5c: case 0x5d: case 0x5e: case 0x5f: case 0xc2: case 0x5a:
         return true;
       case 0x5b: return pp <= 2;
+      case 0x52: case 0x53: return pp == 0 || pp == 2;  // rsqrt / rcp ps, ss
       case 0x2e: case 0x2f: return pp <= 1;
       case 0x2a: case 0x2c: case 0x2d: return pp >= 2;
       case 0xe6: return pp >= 1;
@@ -283,6 +284,33 @@ __device__ __forceinline__ bool f_lt(u64 a, u64 b, u32 w) {
 }
 
 enum : u32 { FOP_ADD, FOP_SUB, FOP_MUL, FOP_DIV, FOP_MIN, FOP_MAX, FOP_SQRT };
+
+}  // namespace wtfgpu_dev
+#include "engine_rcp_tab.h"  // the host CPU's RCPPS / RSQRTPS tables (scripts/gen_rcp_tables.c)
+namespace wtfgpu_dev {
+// RCPPS / RSQRTPS of one binary32 (U40): a table of the result at the
+// reference exponent, rescaled; no flags, MXCSR ignored. rcp: +-0 and
+// denormals -> +-inf, +-inf -> +-0, a tiny result -> +-0. rsqrt: a negative
+// nonzero -> the default NaN, +-0 and denormals -> +-inf, +inf -> +0. NaNs
+// quietened. (Matches the host on every exponent and sign: tests/golden fp vectors.)
+__device__ __forceinline__ u32 f_rcp32(u32 x) {
+  const u32 s = x & 0x80000000u, e = (x >> 23) & 0xff, m = x & 0x7fffff;
+  if (e == 0xff) return m ? (x | 0x400000u) : s;
+  if (e == 0) return s | 0x7f800000u;
+  const u32 t = kRcpTab[m >> 12];
+  const i32 re = (i32)((t >> 23) & 0xff) + 127 - (i32)e;
+  if (re <= 0) return s;
+  return s | ((u32)re << 23) | (t & 0x7fffff);
+}
+__device__ __forceinline__ u32 f_rsq32(u32 x) {
+  const u32 s = x & 0x80000000u, e = (x >> 23) & 0xff, m = x & 0x7fffff;
+  if (e == 0xff) return m ? (x | 0x400000u) : (s ? 0xffc00000u : 0u);
+  if (e == 0) return s | 0x7f800000u;
+  if (s) return 0xffc00000u;
+  const u32 t = kRsqTab[(((e & 1) ^ 1) << 10) | (m >> 13)];
+  const i32 k = ((i32)e - 127 - ((e & 1) ? 0 : 1)) / 2;  // x = y * 4^k, y in [1, 4)
+  return ((u32)((i32)((t >> 23) & 0xff) - k) << 23) | (t & 0x7fffff);
+}
 
 // one element of an SSE arithmetic op: a = the first source (the
 // destination of a legacy form), b = the second; sqrt reads b only

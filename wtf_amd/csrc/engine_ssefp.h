@@ -41,7 +41,7 @@ __device__ __forceinline__ int xm_fault(Lane &L, u64 cr4) {
 }
 
 enum : u32 { FK_ARITH, FK_CMP, FK_COMI, FK_CVTF, FK_CVTI, FK_CVTPD, FK_SI2F, FK_F2SI, FK_HADD, FK_DUP, FK_LDDQU,
-             FK_ROUND, FK_BLEND, FK_BLENDV, FK_DP };
+             FK_ROUND, FK_BLEND, FK_BLENDV, FK_DP, FK_RCP };
 
 __device__ __noinline__ int fp_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next) {
   next = nrip;
@@ -65,6 +65,11 @@ __device__ __noinline__ int fp_exec(const Dev &P, Lane &L, const UOp &u, u64 nri
         if (pp == 0) n = l256 ? 16 : 8, align = false;
         break;
       case 0x5b: k = FK_CVTI; two_op = true; break;
+      case 0x52: case 0x53:  // rsqrt / rcp: ps, ss
+        k = FK_RCP;
+        scalar = pp == 2;
+        two_op = pp == 0;
+        break;
       case 0xe6:
         k = FK_CVTPD;
         two_op = true;
@@ -265,6 +270,14 @@ __device__ __noinline__ int fp_exec(const Dev &P, Lane &L, const UOp &u, u64 nri
     }
     case FK_BLEND:
       for (u32 i = 0; i < ne; i++) yset(r, i, ew, ((imm >> i) & 1) ? yel(b, i, ew) : yel(a, i, ew));
+      break;
+    case FK_RCP:
+      if (scalar) {
+        xset(r.l, 0, 4, c == 0x53 ? f_rcp32((u32)xel(b.l, 0, 4)) : f_rsq32((u32)xel(b.l, 0, 4)));
+        keep256 = 0;
+      } else {
+        for (u32 i = 0; i < ne; i++) yset(r, i, 4, c == 0x53 ? f_rcp32((u32)yel(b, i, 4)) : f_rsq32((u32)yel(b, i, 4)));
+      }
       break;
     case FK_DP: {
       // SDM DPPS / DPPD, as the hardware evaluates the sum: per 128-bit lane,
