@@ -91,6 +91,19 @@ def gen_forms(rng):
         forms.append(Form(enc_rr(F3, 0xD6, x(), m()), "movq2dq"))
         forms.append(Form(enc_rr(F2, 0xD6, m(), x()), "movdq2q"))
     forms.append(Form([0x0F, 0x77], "emms"))
+    # ---- the MMX-operand conversions (own generator: the forms above keep their cases)
+    crng = random.Random(0xC7)
+    cm = lambda: crng.randrange(16)  # noqa: E731
+    for pfx, sfx in ((NP, "ps"), ([0x66], "pd")):
+        for _ in range(4):
+            forms.append(Form(enc_rr(pfx, 0x2A, cm(), cm()), f"cvtpi2{sfx}.rr"))
+        code, p, s = enc_mem(crng, pfx, 0x2A, cm(), 1)
+        forms.append(Form(code, f"cvtpi2{sfx}.m", p, s))
+        for op, nm in ((0x2C, "cvtt"), (0x2D, "cvt")):
+            for _ in range(4):
+                forms.append(Form(enc_rr(pfx, op, cm(), cm()), f"{nm}{sfx}2pi.rr"))
+            code, p, s = enc_mem(crng, pfx, op, cm(), 16 if sfx == "pd" else 1)
+            forms.append(Form(code, f"{nm}{sfx}2pi.m", p, s))
     return forms
 
 

@@ -154,9 +154,9 @@ FP_FAULT_CASES = [
     ([0x0F, 0x52, 0x06], EXIT_FAULT, 13),                    # rsqrtps xmm0, [rsi]: legacy needs alignment
     ([0xC5, 0xF0, 0x53, 0xC1], EXIT_FAULT, 6),               # vrcpps with vvvv != 1111
     ([0xC5, 0xF2, 0x52, 0x06], RUNNING, None),               # vrsqrtss xmm0, xmm1, [rsi]
-    # outside the executed set: MMX-operand conversions
-    ([0x0F, 0x2A, 0xC1], EXIT_UNIMPLEMENTED, None),          # cvtpi2ps xmm0, mm1
-    ([0x0F, 0x2D, 0xC1], EXIT_UNIMPLEMENTED, None),          # cvtps2pi mm0, xmm1
+    ([0x0F, 0x2A, 0xC1], RUNNING, None),                     # cvtpi2ps xmm0, mm1 (tests/test_mmx.py)
+    ([0x0F, 0x2D, 0xC1], RUNNING, None),                     # cvtps2pi mm0, xmm1
+    ([0xC5, 0xF8, 0x2A, 0xC1], EXIT_FAULT, 6),               # no VEX form
 ]
 
 

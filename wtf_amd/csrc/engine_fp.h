@@ -34,7 +34,7 @@ __host__ __device__ inline bool fp_form(u32 map, u32 c, u32 pp, bool vex) {
       case 0x5b: return pp <= 2;
       case 0x52: case 0x53: return pp == 0 || pp == 2;  // rsqrt / rcp ps, ss
       case 0x2e: case 0x2f: return pp <= 1;
-      case 0x2a: case 0x2c: case 0x2d: return pp >= 2;
+      case 0x2a: case 0x2c: case 0x2d: return pp >= 2 || !vex;  // pp 0 / 1: the MMX-operand conversions
       case 0xe6: return pp >= 1;
       case 0x7c: case 0x7d: case 0xd0: return pp == 1 || pp == 3;
       case 0x12: return pp >= 2;

@@ -430,12 +430,6 @@ __device__ __forceinline__ u64 sse_ea(const Dev &P, const Lane &L, const UOp &u,
 
 __device__ __noinline__ int vex_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next);
 
-}  // namespace wtfgpu_dev
-#include "engine_ssefp.h"  // SSE / AVX floating point: fp_exec
-#include "engine_sse4.h"  // SSSE3 / SSE4.1 integer, AVX2 lane-crossing: s4_exec
-#include "engine_avx2x.h"  // FMA3, F16C, AVX2 gathers: ax_exec
-namespace wtfgpu_dev {
-
 // ---------------------------------------------------------------- MMX (U37)
 // The oracle's exec_mmx: mm i is physical x87 register R(i) = fpst[(i - TOS)
 // & 7] (fpst holds ST order); a completed MMX instruction rotates fpst to R
@@ -464,6 +458,12 @@ __device__ __forceinline__ void mmx_put(wtfgpu_regs_t &F, u32 i, u64 v) {
   F.fpst[i] = v;
   F.fpse[i] = 0xffff;
 }
+
+}  // namespace wtfgpu_dev
+#include "engine_ssefp.h"  // SSE / AVX floating point: fp_exec
+#include "engine_sse4.h"  // SSSE3 / SSE4.1 integer, AVX2 lane-crossing: s4_exec
+#include "engine_avx2x.h"  // FMA3, F16C, AVX2 gathers: ax_exec
+namespace wtfgpu_dev {
 
 __device__ __noinline__ int mmx_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next) {
   next = nrip;

@@ -41,7 +41,7 @@ __device__ __forceinline__ int xm_fault(Lane &L, u64 cr4) {
 }
 
 enum : u32 { FK_ARITH, FK_CMP, FK_COMI, FK_CVTF, FK_CVTI, FK_CVTPD, FK_SI2F, FK_F2SI, FK_HADD, FK_DUP, FK_LDDQU,
-             FK_ROUND, FK_BLEND, FK_BLENDV, FK_DP, FK_RCP };
+             FK_ROUND, FK_BLEND, FK_BLENDV, FK_DP, FK_RCP, FK_MMXCVT };
 
 __device__ __noinline__ int fp_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next) {
   next = nrip;
@@ -75,8 +75,25 @@ __device__ __noinline__ int fp_exec(const Dev &P, Lane &L, const UOp &u, u64 nri
         two_op = true;
         if (pp == 2) n = l256 ? 16 : 8, align = false;
         break;
-      case 0x2a: k = FK_SI2F; w = pp & 1; scalar = true; n = W ? 8 : 4; break;
-      case 0x2c: case 0x2d: k = FK_F2SI; w = pp & 1; scalar = true; two_op = true; break;
+      case 0x2a: case 0x2c: case 0x2d:
+        if (pp <= 1) {  // cvtpi2ps / cvtpi2pd (mm / m64 source), cvt(t)ps2pi / cvt(t)pd2pi (mm destination)
+          k = FK_MMXCVT;
+          w = pp & 1;
+          n = (c != 0x2a && pp == 1) ? 16 : 8;
+          break;
+        }
+        if (c == 0x2a) {
+          k = FK_SI2F;
+          w = pp & 1;
+          scalar = true;
+          n = W ? 8 : 4;
+        } else {
+          k = FK_F2SI;
+          w = pp & 1;
+          scalar = true;
+          two_op = true;
+        }
+        break;
       case 0x7c: case 0x7d: case 0xd0: k = FK_HADD; w = pp == 1; break;
       case 0x12: case 0x16:
         k = FK_DUP;
@@ -127,6 +144,11 @@ __device__ __noinline__ int fp_exec(const Dev &P, Lane &L, const UOp &u, u64 nri
     }
   } else if (k == FK_LDDQU && !mem) {
     set_fault(L, WTFGPU_VEC_UD, 0, 0);
+    return X_FAULT;
+  }
+  // an MMX register operand: a pending unmasked x87 exception first (#MF), as mmx_exec
+  if (k == FK_MMXCVT && (c != 0x2a || !mem) && (P.full[L.lane].fpsw & ~P.full[L.lane].fpcw & 0x3f)) {
+    set_fault(L, 16, 0, 0);
     return X_FAULT;
   }
   const u64 ea = mem ? sse_ea(P, L, u, nrip) : 0;
@@ -271,6 +293,24 @@ __device__ __noinline__ int fp_exec(const Dev &P, Lane &L, const UOp &u, u64 nri
     case FK_BLEND:
       for (u32 i = 0; i < ne; i++) yset(r, i, ew, ((imm >> i) & 1) ? yel(b, i, ew) : yel(a, i, ew));
       break;
+    case FK_MMXCVT:
+      if (c == 0x2a) {  // two int32 -> the low two floats (the rest of xmm stays) / two doubles
+        const u64 src = mem ? b.l.lo : mmx_get(F, u.rm & 7);
+        r.l = a.l;
+        if (pp) {
+          r.l.lo = f_from_int(v, (i64)(i32)(u32)src, 1);
+          r.l.hi = f_from_int(v, (i64)(i32)(u32)(src >> 32), 1);
+        } else {
+          xset(r.l, 0, 4, f_from_int(v, (i64)(i32)(u32)src, 0));
+          xset(r.l, 1, 4, f_from_int(v, (i64)(i32)(u32)(src >> 32), 0));
+        }
+      } else {  // two floats / doubles -> two int32 in mm (2c: truncated)
+        const u32 rc = c == 0x2c ? 3u : v.rc, e2 = pp ? 8 : 4;
+        const u64 lo = f_to_int(v, xel(b.l, 0, e2), pp, 4, rc), hi = f_to_int(v, xel(b.l, 1, e2), pp, 4, rc);
+        gval = (lo & 0xffffffffull) | (hi << 32);
+        gpr_out = 2;
+      }
+      break;
     case FK_RCP:
       if (scalar) {
         xset(r.l, 0, 4, c == 0x53 ? f_rcp32((u32)xel(b.l, 0, 4)) : f_rsq32((u32)xel(b.l, 0, 4)));
@@ -324,6 +364,11 @@ __device__ __noinline__ int fp_exec(const Dev &P, Lane &L, const UOp &u, u64 nri
     return xm_fault(L, cr4);
   }
   F.mxcsr |= v.fl;
+  if (k == FK_MMXCVT && (c != 0x2a || !mem)) mmx_commit(F);  // the x87 -> MMX transition
+  if (gpr_out == 2) {
+    mmx_put(F, u.reg & 7, gval);
+    return X_OK;
+  }
   if (gpr_out) {
     RS(L, u.reg, gval);
     return X_OK;
