@@ -127,7 +127,8 @@ AVX_FAULT_CASES = [
     ([0x66, 0x0F, 0x38, 0x00, 0x06], EXIT_FAULT, 13),      # pshufb xmm0, [rsi]: legacy needs alignment
     ([0x66, 0x0F, 0x38, 0x1C, 0xC1], RUNNING, None),        # pabsb (U41)
     ([0x66, 0x0F, 0x3A, 0x42, 0xC1, 0x00], RUNNING, None),  # mpsadbw (U41)
-    ([0x66, 0x0F, 0x3A, 0x40, 0xC1, 0x00], EXIT_UNIMPLEMENTED, None),  # dpps (outside)
+    ([0x66, 0x0F, 0x3A, 0x40, 0xC1, 0x00], RUNNING, None),   # dpps
+    ([0xC4, 0xE3, 0x7D, 0x41, 0xC1, 0x31], EXIT_FAULT, 6),   # vdppd ymm: no 256-bit form
     # U36 / U45: encodings no CPU defines are #UD; defined ones outside the engine are UNIMPLEMENTED
     ([0xC4, 0x30, 0x02, 0x00], EXIT_FAULT, 6),              # VEX map 0x10 (runaway HEVD bytes)
     ([0xC4, 0xE0, 0x79, 0x58, 0xC1], EXIT_FAULT, 6),        # VEX map 0
