@@ -325,14 +325,23 @@ static_assert(sizeof(UCEntry) == 64, "LDS entry size");
 constexpr u32 UC_QUEUES = 2;
 constexpr u64 UC_IMAGE_BYTES = (u64)UC_N * sizeof(UCEntry);
 
-// WTFGPU_UC_WAYS = 2: two-way sets (entries 2s, 2s + 1), a fill replaces the
-// way a per-wave counter picks; tlv's 228-instruction loop missed a fifth of
+// WTFGPU_UC_WAYS = 2: two-way sets (entries 2s, 2s + 1), a fill replaces
+// way 1 (WTFGPU_UC_MRU) or the way a per-wave counter picks; tlv's 228-instruction loop missed a fifth of
 // its wave-steps direct-mapped (scripts: a trace replay gives 23 % direct,
 // 14 % two-way at 256 entries).
 #ifndef WTFGPU_UC_WAYS
 #define WTFGPU_UC_WAYS 2
 #endif
 constexpr u32 UC_WAYS = WTFGPU_UC_WAYS;
+// WTFGPU_UC_MRU = 1: a fill takes way 0 and moves the old way 0 to way 1, so
+// the fast loop's first LDS read finds the newer entry (SYN 4 % shorter
+// launches than a counter-picked way; fill passes unchanged)
+#ifndef WTFGPU_UC_MRU
+#define WTFGPU_UC_MRU 1
+#endif
+__device__ __forceinline__ bool cacheable_key(u64 lptr, u64 pool_lo, u64 pool_span) {
+  return !m_ge64(lptr - pool_lo, pool_span);
+}
 __device__ __forceinline__ u32 uc_slot(u64 key) {
   if (UC_WAYS == 1) return (u32)((key ^ (key >> 12) * 0x9E3779B1u) & (UC_N - 1));
   // multiplicative hash: the offset bits mix into the set index too
@@ -1229,7 +1238,9 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
   asm volatile("" : "+v"(pool_lo), "+v"(pool_span), "+v"(limit_v), "+v"(max32));
   const FastMem fm = fast_mem(P);
   u32 steps = 0;
+#if !WTFGPU_UC_MRU
   u32 fill_way = 0;  // two-way uop cache: the way the next fill replaces (wave-uniform)
+#endif
 #ifdef WTFGPU_STAMPS
   u64 stamp_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u64 tprev_ = __builtin_amdgcn_s_memtime();
@@ -1458,7 +1469,16 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     UCEntry *e = &uc[uc_slot(key)];
     if (UC_WAYS == 2 && rfl64(e->key) != key) {
       if (rfl64(e[1].key) == key) e += 1;
+#if WTFGPU_UC_MRU
+      else if (cacheable_key(lptr, pool_lo, pool_span)) {
+        // the newest fill takes way 0 (the fast loop's first read), the old
+        // way 0 moves to way 1 (whose entry is the one dropped)
+        if (lid < 16) ((u32 *)&e[1])[lid] = ((const u32 *)e)[lid];
+        __builtin_amdgcn_wave_barrier();
+      }
+#else
       else e += (fill_way++ & 1);  // the way a fill replaces
+#endif
     }
     const bool cacheable = !m_ge64(lptr - pool_lo, pool_span);
     if (cacheable && rfl64(e->key) != key) {
