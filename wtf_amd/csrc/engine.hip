@@ -266,9 +266,12 @@ __device__ __forceinline__ void fetch_bytes(u64 pageptr, u32 off, u32 n, u64 &lo
 // already in the aggregate coverage map, and the lanes this wave has already
 // logged for it in this launch.
 #ifndef WTFGPU_UC_N
-#define WTFGPU_UC_N 256  // head-only entries (the UOp lives in the uop slots below)
+#define WTFGPU_UC_N 312  // head-only entries (the UOp lives in the uop slots below)
 #endif
-constexpr u32 UC_N = WTFGPU_UC_N;  // entries per wave (power of two)
+// entries per wave: 4 waves x 312 x 64 bytes + the uop slots = 81,792 bytes a
+// block, two blocks per CU in 160 KiB (256 entries: tlv's fill passes 16 % of
+// wave-steps, 312: 12 %; profiles/r05_stamps_ucindex_ab.txt)
+constexpr u32 UC_N = WTFGPU_UC_N;
 #ifndef WTFGPU_FILL_INLINE
 #define WTFGPU_FILL_INLINE 1  // k_run's fills take the shared-cache hit path inline (uc_fill_shared)
 #endif
@@ -333,6 +336,7 @@ constexpr u64 UC_IMAGE_BYTES = (u64)UC_N * sizeof(UCEntry);
 #define WTFGPU_UC_WAYS 2
 #endif
 constexpr u32 UC_WAYS = WTFGPU_UC_WAYS;
+static_assert(UC_N % UC_WAYS == 0, "whole sets");
 // WTFGPU_UC_MRU = 1: a fill takes way 0 and moves the old way 0 to way 1, so
 // the fast loop's first LDS read finds the newer entry (SYN 4 % shorter
 // launches than a counter-picked way; fill passes unchanged)
@@ -343,9 +347,12 @@ __device__ __forceinline__ bool cacheable_key(u64 lptr, u64 pool_lo, u64 pool_sp
   return !m_ge64(lptr - pool_lo, pool_span);
 }
 __device__ __forceinline__ u32 uc_slot(u64 key) {
-  if (UC_WAYS == 1) return (u32)((key ^ (key >> 12) * 0x9E3779B1u) & (UC_N - 1));
+  if (UC_WAYS == 1) return (u32)((key ^ (key >> 12) * 0x9E3779B1u) % UC_N);
   // multiplicative hash: the offset bits mix into the set index too
-  return (u32)((key * 0x9E3779B97F4A7C15ull) >> (64 - __builtin_ctz(UC_N / UC_WAYS))) * UC_WAYS;
+  // the product's high word scaled to the set count (any count: one
+  // s_mul_hi where a power of two took a shift)
+  const u32 h = (u32)((key * 0x9E3779B97F4A7C15ull) >> 32);
+  return __umulhi(h, UC_N / UC_WAYS) * UC_WAYS;
 }
 __device__ __forceinline__ u32 uu_slot(u64 key) { return (u32)((key ^ (key >> 12) * 0x9E3779B1u) & (UC_U - 1)); }
 
