@@ -56,8 +56,8 @@ def test_k_run_fits_two_blocks_per_cu(tmp_path):
     lds = int(k["group_segment_fixed_size"])
     # 4 waves x UC_N x 64-byte entries + 4 x UC_U uop slots: 312 entries today
     assert 256 * 64 * 4 <= lds <= LDS_PER_CU // 2, lds
-    # scratch: the slow step's out-of-line callees' frames (decode buffers, the
-    # UOp), 1,344 bytes a lane today; the fast loop itself keeps none
+    # scratch (stack frames and arrays the compiler could not keep in
+    # registers): 1,344 bytes a lane today; a jump means something new spilled
     assert int(k["private_segment_fixed_size"]) <= 2048, k["private_segment_fixed_size"]
 
 
