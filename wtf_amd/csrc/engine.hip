@@ -349,9 +349,10 @@ __device__ __forceinline__ bool cacheable_key(u64 lptr, u64 pool_lo, u64 pool_sp
 __device__ __forceinline__ u32 uc_slot(u64 key) {
   if (UC_WAYS == 1) return (u32)((key ^ (key >> 12) * 0x9E3779B1u) % UC_N);
   // multiplicative hash: the offset bits mix into the set index too
-  // the product's high word scaled to the set count (any count: one
-  // s_mul_hi where a power of two took a shift)
-  const u32 h = (u32)((key * 0x9E3779B97F4A7C15ull) >> 32);
+  // a 32-bit multiplicative hash (the page bits above 4 GiB folded in), its
+  // high bits scaled to the set count by one s_mul_hi (any count); cheaper
+  // than the 64-bit product and fewer tlv fill passes (13.0 -> 11.1 %)
+  const u32 h = ((u32)key ^ (u32)(key >> 17)) * 0x9E3779B1u;
   return __umulhi(h, UC_N / UC_WAYS) * UC_WAYS;
 }
 __device__ __forceinline__ u32 uu_slot(u64 key) { return (u32)((key ^ (key >> 12) * 0x9E3779B1u) & (UC_U - 1)); }
