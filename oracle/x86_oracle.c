@@ -2073,7 +2073,7 @@ static int exec_vex(orc_machine *m, insn *d) {
     switch (op) {
     case 0x10: case 0x11: n = pp <= 1 ? vl : pp == 2 ? 4 : 8; break;
     case 0x12: case 0x13: case 0x16: case 0x17: case 0xd6: n = 8; break;
-    case 0x6e: case 0x7e: n = (pp == 2 || d->vw) ? 8 : 4; break;
+    case 0x6e: case 0x7e: n = (pp == 2 || d->rexw) ? 8 : 4; break;
     case 0xc4: n = 2; break;
     case 0x28: case 0x29: case 0x2b: case 0xe7: align = 1; break;
     case 0x6f: case 0x7f: align = pp == 1; break;
@@ -3272,7 +3272,7 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
     d->rexb = (b == 0xc4 && !d->m32) ? !((b1 >> 5) & 1) : 0;
     d->opmap = b == 0xc4 ? (b1 & 31u) : 1;
     d->vw = b == 0xc4 ? (b2 >> 7) & 1u : 0;
-    d->rexw = d->vw;
+    d->rexw = d->m32 ? 0 : d->vw; /* a 64-bit GPR operand in 64-bit mode only (32-bit code ignores VEX.W1) */
     d->rex = 0x40 | (d->rexw << 3) | (d->rexr << 2) | (d->rexx << 1) | d->rexb;
     d->vvvv = (~b2 >> 3) & (d->m32 ? 7u : 15u);
     d->vl = (b2 >> 2) & 1u;

@@ -78,6 +78,8 @@ U32 = {
     "arpl": "arpl ax, bx\n int3",
     "jmp16": ".byte 0x66, 0xe9, 0x00, 0x00\n int3",
     "ud2": "ud2",
+    # andn eax, esi, edi with VEX.W1: 32-bit code runs it at 32 bits (W1 ignored)
+    "bmiw1": ".byte 0xc4, 0xe2, 0xc8, 0xf2, 0xc7\n int3",
 }
 
 

@@ -99,6 +99,19 @@ def test_outside_forms_and_ud(space):
     assert _one(space, "ud2")["exit"][:2] == (FAULT, 6)
 
 
+def test_vex_w1_gpr_form_is_32_bit(space):
+    """BMI's VEX.W1 selects a 64-bit operand in 64-bit mode only ("the operand
+    size is always 32 bits if not in 64-bit mode", SDM ANDN / RORX / ...):
+    ~esi & edi with edi's upper half set is 0 at 32 bits (ZF, not SF), where a
+    64-bit andn would give 0xffffffff00000000 with SF."""
+    ZF, SF = 0x40, 0x80
+    r = _one(space, "bmiw1", rax=0x1234, rsi=0, rdi=0xFFFFFFFF_00000000)
+    assert r["exit"][0] == INT3
+    assert r["gpr"][0] == 0 and r["rflags"] & ZF and not r["rflags"] & SF
+    r = _one(space, "bmiw1", rsi=0x0F0F0F0F, rdi=0xFFFFFFFF_FFFFFFFF)
+    assert r["gpr"][0] == 0xF0F0F0F0 and r["rflags"] & SF and not r["rflags"] & ZF
+
+
 def test_engine_code_matches_oracle(space):
     sp, st, lay, data = space
     ln = T.lanes(37 * 24, 21)

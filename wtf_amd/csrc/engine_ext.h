@@ -81,7 +81,8 @@ __device__ __noinline__ int gext_exec(const Dev &P, Lane &L, const UOp &u, u64 n
   const u32 f = gx_form(map, c, pp, vex);
   const u32 vvvv = (x >> 4) & 15;
   // adcx's 66 is its mandatory prefix, not an operand-size override
-  const u32 sz = vex ? (((x >> 2) & 1) ? 8 : 4) : f == GX_ADCX ? (((u.rex >> 3) & 1) ? 8 : 4) : u.asz;
+  // (VEX.W1 is a 64-bit operand in 64-bit mode only: 32-bit code runs it at 32 bits)
+  const u32 sz = vex ? (((x >> 2) & 1) && !(L.efer & EFER_M32) ? 8 : 4) : f == GX_ADCX ? (((u.rex >> 3) & 1) ? 8 : 4) : u.asz;
   // #UD: a legacy prefix before VEX, VEX.L = 1 (no CR4.OSXSAVE / XCR0 gate on
   // the VEX-encoded general-purpose forms); the register form of movbe;
   // group 17 beyond /1 /2 /3
@@ -423,7 +424,8 @@ __device__ __noinline__ int x42_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
   next = nrip;
   const u32 x = u.opreg, c = u.sub, map = vex_map(x);
   const bool vex = x & 1, mem = u.is_mem;
-  const u32 l256 = vex ? (x >> 1) & 1 : 0, W = vex ? (x >> 2) & 1 : (u.rex >> 3) & 1, vvvv = vex ? (x >> 4) & 15 : 0;
+  // W: the explicit-length forms' rax / rdx (64-bit mode only, as u.rex)
+  const u32 l256 = vex ? (x >> 1) & 1 : 0, W = (u.rex >> 3) & 1, vvvv = vex ? (x >> 4) & 15 : 0;
   const u32 imm = (u32)u.imm & 0xff;
   const bool str = map == 3 && c >= 0x60 && c <= 0x63;
   const bool sha = (map == 2 && c >= 0xc8 && c <= 0xcd) || (map == 3 && c == 0xcc);

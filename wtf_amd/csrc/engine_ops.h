@@ -322,7 +322,10 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u, bool m32 = false)
     const u32 vmap = c == 0xc4 ? (b1 & 31) : 1, vw = c == 0xc4 ? (b2 >> 7) & 1 : 0;
     vpp = b2 & 3;
     vex = 1 | (((b2 >> 2) & 1) << 1) | (vw << 2) | ((((~b2) >> 3) & (m32 ? 7 : 15)) << 4) | (vmap << 8) | (bad << 16);
-    rex = 0x40 | (vw << 3) | (vr << 2) | (vx << 1) | vb;
+    // VEX.W selects a 64-bit GPR operand in 64-bit mode only ("the operand size
+    // is always 32 bits if not in 64-bit mode"; VEX.W1 ignored): it stays in
+    // `vex` (bit 2) for the forms whose element size it picks in every mode
+    rex = 0x40 | ((m32 ? 0 : vw) << 3) | (vr << 2) | (vx << 1) | vb;
     c = ib_at(b, pos++);  // the opcode
     const bool def = !bad && vmap >= 1 && vmap <= 3 && vex_defined(vmap, c, vpp);
     if (!def || (vmap == 3 && !fp_form(3, c, vpp, true) && !s4_form(3, c, vpp, true) && !x42_form(3, c, vpp, true) &&

@@ -192,7 +192,11 @@ __device__ __noinline__ int s4_exec(const Dev &P, Lane &L, const UOp &u, u64 nri
   next = nrip;
   const u32 x = u.opreg, c = u.sub, pp = u.bsz, map = vex_map(x);
   const bool vex = x & 1, mem = u.is_mem;
-  const u32 l256 = vex ? (x >> 1) & 1 : 0, W = vex ? (x >> 2) & 1 : (u.rex >> 3) & 1, vvvv = vex ? (x >> 4) & 15 : 0;
+  // W: the element size where it picks one (every mode); for (v)pextrq /
+  // (v)pinsrq the GPR size, whose VEX.W1 32-bit code ignores (the W0 forms)
+  const u32 l256 = vex ? (x >> 1) & 1 : 0, vvvv = vex ? (x >> 4) & 15 : 0;
+  const u32 W = (vex ? (x >> 2) & 1 : (u.rex >> 3) & 1) &
+                ~(u32)(map == 3 && (c == 0x16 || c == 0x22) && (L.efer & EFER_M32) ? 1 : 0);
   const u32 imm = (u32)u.imm & 0xff;
   const u32 vl = l256 ? 32 : 16;
   const S4Form f = s4_desc(map, c, pp, vex, W);

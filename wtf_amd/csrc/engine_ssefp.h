@@ -47,7 +47,10 @@ __device__ __noinline__ int fp_exec(const Dev &P, Lane &L, const UOp &u, u64 nri
   next = nrip;
   const u32 x = u.opreg, c = u.sub, pp = u.bsz, map = vex_map(x);
   const bool vex = x & 1, mem = u.is_mem;
-  const u32 l256 = vex ? (x >> 1) & 1 : 0, W = vex ? (x >> 2) & 1 : (u.rex >> 3) & 1, vvvv = vex ? (x >> 4) & 15 : 0;
+  // W: the integer operand's size (cvtsi2s* / cvt(t)s*2si: 64-bit mode only,
+  // as u.rex); VW: VEX.W as encoded (vblendv W1 is #UD in every mode)
+  const u32 l256 = vex ? (x >> 1) & 1 : 0, W = (u.rex >> 3) & 1, VW = vex ? (x >> 2) & 1 : 0;
+  const u32 vvvv = vex ? (x >> 4) & 15 : 0;
   const u32 imm = (u32)u.imm & 0xff;
   const u64 cr4 = P.sys[L.lane].cr4;
   const u32 vl = l256 ? 32 : 16;
@@ -131,7 +134,7 @@ __device__ __noinline__ int fp_exec(const Dev &P, Lane &L, const UOp &u, u64 nri
     bool ud = (x >> 16) & 1;
     if (!((cr4 >> 18) & 1) || (P.full[L.lane].xcr0 & 6) != 6) ud = true;
     if (two_op && vvvv != 0) ud = true;
-    if (k == FK_BLENDV && W) ud = true;
+    if (k == FK_BLENDV && VW) ud = true;
     if (k == FK_DP && w && l256) ud = true;  // vdppd has no 256-bit form
     if (k == FK_LDDQU && !mem) ud = true;
     if (ud) {

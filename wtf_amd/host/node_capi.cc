@@ -3,6 +3,7 @@
 // One node per process (wtf's g_Backend / g_Dbg / target registry are process
 // globals, as in the reference).
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 
@@ -53,9 +54,16 @@ int wtfnode_open(const wtfnode_opts_t *o, wtfnode **out) {
   g_Backend = N->B;
   if (!N->B->Initialize(N->Opts, N->State)) return -3;
   if (O.regroup != ~0ull) wtfgpu_set_regroup(N->B->Engine(), O.regroup);
-  if (O.world > 1) {
-    N->X = std::make_unique<RcclExchange_t>(O.rank, O.world);
-    if (!N->X->Init(o->rccl_id, wtfgpu_stream(N->B->Engine()))) return -4;
+  if (const char *e = getenv("WTF_RCCL_FORCE")) O.rccl_force = atoi(e) != 0;
+  if (O.world > 1 || O.rccl_force) {
+    uint8_t Own[kRcclIdBytes];
+    const uint8_t *Id = o->rccl_id;
+    if (!Id) {  // forced at world 1 without an id: this process is the only rank
+      if (!RcclUniqueId(Own)) return -4;
+      Id = Own;
+    }
+    N->X = std::make_unique<RcclExchange_t>(O.rank, O.world, O.rccl_force);
+    if (!N->X->Init(Id, wtfgpu_stream(N->B->Engine()))) return -4;
   }
   Target_t *T = Targets_t::Instance().Get(O.name);
   if (!T) return -5;
@@ -100,7 +108,7 @@ int wtfnode_summary_json(wtfnode *n, char *buf, uint64_t cap) {
 
 int wtfnode_close(wtfnode *n) {
   if (!n) return 0;
-  if (n->F && n->X && n->X->World() > 1) n->F->FinishMerge();  // the merge the last step started (collective)
+  if (n->F && n->X && n->X->Exchanging()) n->F->FinishMerge();  // the merge the last step started (collective)
   n->F.reset();
   n->X.reset();
   delete n;  // the backend stays (process lifetime, as g_Backend in the reference)

@@ -1,12 +1,20 @@
 // rccl_exchange.cc — CoverageExchange_t for GPU shards: one RCCL
-// communicator over the node's GPUs (xGMI), an in-place
-// ncclAllReduce(uint8, ncclMax) of the device coverage map and
-// an all-gather of the values outside it. The collectives run on a stream of
-// their own: the engine's commits are synchronous, so the map is final when a
-// merge starts, and the host waits only for the collective, never for a k_run
-// slice another queue has in flight. The unique id travels out of band: through a file
-// (`wtfgpu fuzz --world n --rank r --nccl-id-file f`, rank 0 writes it) or
-// from the caller (libwtfnode, bench.py broadcasts it).
+// communicator over the node's GPUs (xGMI). Each node step's merge
+// (MergeBegin / MergeEnd) copies the device coverage map into a frozen
+// buffer, then runs one fused group on the exchange's own stream: an
+// out-of-place ncclAllReduce(uint8, ncclMax) of the frozen copy into `merged`
+//  and an ncclAllGather of every rank's MergeBlocks block (the
+// values outside the map plus the done flag). The next step's kernels run
+// meanwhile; the result is absorbed one step later. The host waits for the
+// D2D frozen copy before MergeBegin returns (a map-sized copy, tens of
+// microseconds: it orders the copy before the next step's commits on every
+// engine queue without an event per queue) and never for a k_run slice.
+// A world-1 node skips all of this unless it is forced (--rccl-force /
+// WTF_RCCL_FORCE=1), which runs every call against a one-rank communicator:
+// the GPU test of the RCCL path on a one-GPU box. The unique id travels out
+// of band: through a file (`wtfgpu fuzz --world n --rank r --nccl-id-file f`,
+// rank 0 writes it) or from the caller (libwtfnode, bench.py broadcasts it).
+// A failed hip / nccl call fails the merge, and the session with it.
 #include "rccl_exchange.h"
 
 #include "merge_block.h"
@@ -69,7 +77,8 @@ bool RcclIdViaFile(const std::string &Path, int Rank, uint8_t Id[kRcclIdBytes], 
   return false;
 }
 
-RcclExchange_t::RcclExchange_t(int Rank, int World) : rank_(Rank), world_(World), impl_(new Impl) {}
+RcclExchange_t::RcclExchange_t(int Rank, int World, bool Force)
+    : rank_(Rank), world_(World), force_(Force), impl_(new Impl) {}
 
 RcclExchange_t::~RcclExchange_t() {
   if (impl_->stream) (void)hipStreamSynchronize(impl_->stream);  // a merge still in flight completes (every rank issued it)
@@ -89,7 +98,7 @@ RcclExchange_t::~RcclExchange_t() {
 
 bool RcclExchange_t::Init(const uint8_t Id[kRcclIdBytes], void *Stream) {
   (void)Stream;  // the engine's stream: the collectives use their own (see above)
-  if (world_ <= 1) return true;
+  if (!Exchanging()) return true;
   if (hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking) != hipSuccess) return false;
   ncclUniqueId id;
   memcpy(&id, Id, sizeof(id));
@@ -102,14 +111,14 @@ bool RcclExchange_t::Init(const uint8_t Id[kRcclIdBytes], void *Stream) {
 }
 
 bool RcclExchange_t::AllReduceMax(uint8_t *Map, uint64_t Bytes, bool Device) {
-  if (world_ <= 1) return true;
+  if (!Exchanging()) return true;
   if (!Device || !impl_->comm) return false;
   if (ncclAllReduce(Map, Map, Bytes, ncclUint8, ncclMax, impl_->comm, impl_->stream) != ncclSuccess) return false;
   return hipStreamSynchronize(impl_->stream) == hipSuccess;
 }
 
 bool RcclExchange_t::AllDone(bool Mine, bool *All) {
-  if (world_ <= 1) {
+  if (!Exchanging()) {
     *All = Mine;
     return true;
   }
@@ -127,7 +136,7 @@ bool RcclExchange_t::AllDone(bool Mine, bool *All) {
 // counts first (one u64 per rank), then every list padded to the longest
 bool RcclExchange_t::AllGatherV(const std::vector<uint64_t> &Mine, std::vector<uint64_t> &All) {
   All = Mine;
-  if (world_ <= 1) return true;
+  if (!Exchanging()) return true;
   if (!impl_->comm) return false;
   auto grow = [&](uint64_t slots) {
     if (slots <= impl_->gcap) return true;
@@ -167,7 +176,7 @@ bool RcclExchange_t::AllGatherV(const std::vector<uint64_t> &Mine, std::vector<u
 bool RcclExchange_t::MergeBegin(const uint8_t *Map, uint64_t Bytes, bool Device, const std::vector<uint64_t> &Extras,
                                 bool Done) {
   Impl &I = *impl_;
-  if (world_ <= 1) {  // nothing to exchange: the result is this shard's own
+  if (!Exchanging()) {  // nothing to exchange: the result is this shard's own
     merged_extra_ = Extras;
     merged_done_ = Done;
     I.merged_bytes = 0;
@@ -218,7 +227,7 @@ bool RcclExchange_t::MergeEnd(const uint8_t **Merged, uint64_t *Bytes, std::vect
   Impl &I = *impl_;
   if (!I.inflight) return false;
   I.inflight = false;
-  if (world_ <= 1) {
+  if (!Exchanging()) {
     AllExtras.swap(merged_extra_);
     merged_extra_.clear();
     *AllDone = merged_done_;

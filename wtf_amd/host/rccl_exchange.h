@@ -18,12 +18,14 @@ bool RcclIdViaFile(const std::string &Path, int Rank, uint8_t Id[kRcclIdBytes], 
 
 class RcclExchange_t final : public CoverageExchange_t {
  public:
-  RcclExchange_t(int Rank, int World);
+  // Force: take the collective path at world 1 too (a one-rank communicator)
+  RcclExchange_t(int Rank, int World, bool Force = false);
   ~RcclExchange_t() override;
   // Stream: the engine's HIP stream (wtfgpu_stream); collective on every rank
   bool Init(const uint8_t Id[kRcclIdBytes], void *Stream);
   int Rank() const override { return rank_; }
   int World() const override { return world_; }
+  bool Exchanging() const override { return world_ > 1 || force_; }
   bool AllReduceMax(uint8_t *Map, uint64_t Bytes, bool Device) override;
   bool AllDone(bool Mine, bool *All) override;
   bool AllGatherV(const std::vector<uint64_t> &Mine, std::vector<uint64_t> &All) override;
@@ -39,6 +41,7 @@ class RcclExchange_t final : public CoverageExchange_t {
  private:
   struct Impl;
   int rank_, world_;
+  bool force_;
   Impl *impl_;
 };
 

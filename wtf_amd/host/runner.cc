@@ -258,6 +258,7 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
     else if (a == "--world") O.world = atoi(next("--world"));
     else if (a == "--exchange") O.exchange = next("--exchange");
     else if (a == "--nccl-id-file") O.nccl_id_file = next("--nccl-id-file");
+    else if (a == "--rccl-force") O.rccl_force = true;
     else if (a == "--address") O.address = next("--address");
     else if (a == "--nodes") O.nodes = atoi(next("--nodes"));
     else if (a == "--batched") O.batched = true;
@@ -268,6 +269,7 @@ bool ParseRunnerArgs(int argc, char **argv, RunnerOptions &O) {
       return false;
     }
   }
+  if (const char *e = getenv("WTF_RCCL_FORCE")) O.rccl_force = O.rccl_force || atoi(e) != 0;
   if (O.world < 1 || O.rank < 0 || O.rank >= O.world) {
     fprintf(stderr, "--rank must be in [0, --world)\n");
     return false;
@@ -563,7 +565,7 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
   if (!O.address.empty()) return NodeMain(O, Exec, *Target, Slots);
 
   // ---- fuzz: in-process master + batched node
-  if (X && X->World() > 1 && O.full_coverage) {
+  if (X && X->Exchanging() && O.full_coverage) {
     // parity mode resets the map every batch: a merge in flight reads a copy
     // taken when it started, but the shards' maps would mean nothing
     printf("--full-coverage is a single-node parity mode (not with --world > 1)\n");
@@ -574,7 +576,7 @@ int RunnerMain(const RunnerOptions &O, Executor_t &Exec, const Options_t &Opts, 
     printf("Nothing to run: empty corpus and no inputs\n");
     return 1;
   }
-  const bool Shards = X && X->World() > 1;
+  const bool Shards = X && X->Exchanging();
   for (;;) {
     // shards stop together, on the consensus of the last merge absorbed
     // (every shard absorbs the same one at the same step)
@@ -814,7 +816,7 @@ bool FuzzSession::Step() {
   // shards' merges, and one that is not always reaches its own merge below
   // (two reads could disagree under --seconds and skip a collective)
   const bool done = Done();
-  if (X_ && X_->World() > 1 && done) return MergeCoverage(true);
+  if (X_ && X_->Exchanging() && done) return MergeCoverage(true);
   if (stream_) {
     const auto tc = Clock::now();
     const bool ok = StreamStep(done);
@@ -840,7 +842,7 @@ bool FuzzSession::Step() {
   TcBatch NextBatch;
   if (Next_.valid()) NextBatch = Next_.get();  // before the corpus / mutator change below
   for (size_t i = 0; i < BatchRefs_.size(); i++) Account(BatchRefs_[i].data(), BatchRefs_[i].size(), R[i]);
-  if (X_ && X_->World() > 1 && !MergeCoverage(false)) return false;
+  if (X_ && X_->Exchanging() && !MergeCoverage(false)) return false;
   if (!NextBatch.empty() || !More(S_.execs))
     Batch_ = std::move(NextBatch);
   else
@@ -916,7 +918,7 @@ bool FuzzSession::StreamStep(bool Done) {
     if (F.tag >= Slot_.size()) return false;
   AccountStep(Out);
   S_.account_ms += secs_since(ta) * 1e3;
-  if (X_ && X_->World() > 1 && !MergeCoverage(false)) return false;
+  if (X_ && X_->Exchanging() && !MergeCoverage(false)) return false;
   S_.step_ms += secs_since(t_step) * 1e3;
   return true;
 }
@@ -1107,6 +1109,8 @@ bool FuzzSession::AbsorbMerge() {
   if (!Exec_.CoverageMap(&Map, &MapBytes, &Device)) return false;
   if (Bytes && Bytes == MapBytes) S_.merged_rips += Exec_.MergeCoverageMap(Merged, Bytes, Device);
   S_.merged_rips += Exec_.AbsorbExtra(All);
+  S_.merges++;
+  S_.merged_map_bytes += Bytes;
   AllDone_ = Every;
   return true;
 }
@@ -1158,6 +1162,7 @@ std::string FuzzSession::SummaryJson() const {
            "\"execs\":%llu,\"retired\":%llu,\"wall_s\":%.6f,\"run_s\":%.6f,\"execs_per_s\":%.3f,"
            "\"instr_per_s\":%.3f,\"coverage\":%zu,\"corpus\":%zu,\"crashes\":%llu,\"unique_crashes\":%zu,"
            "\"timeouts\":%llu,\"cr3\":%llu,\"errors\":%llu,\"error_retired\":%llu,\"merged_rips\":%llu,"
+           "\"merges\":%llu,\"merged_map_bytes\":%llu,"
            "\"merge_ms\":%.3f,\"produce_wait_ms\":%.3f,\"account_ms\":%.3f,\"make_ms\":%.3f,\"step_ms\":%.3f,\"fill_ms\":%.3f,"
            "\"newcov_ms\":%.3f,\"crashsave_ms\":%.3f,\"call_ms\":%.3f,\"cpu_s\":%.3f,\"mutate_cpu_ms\":%.3f,"
            "\"backend\":",
@@ -1166,7 +1171,8 @@ std::string FuzzSession::SummaryJson() const {
            S_.run_s, S_.run_s > 0 ? S_.execs / S_.run_s : 0.0, S_.run_s > 0 ? S_.retired / S_.run_s : 0.0,
            Exec_.CoverageSize(), Corpus_.Size(), (unsigned long long)S_.crashes, CrashNames_.size(),
            (unsigned long long)S_.timeouts, (unsigned long long)S_.cr3, (unsigned long long)S_.errors,
-           (unsigned long long)S_.error_retired, (unsigned long long)S_.merged_rips, S_.merge_ms, S_.produce_wait_ms,
+           (unsigned long long)S_.error_retired, (unsigned long long)S_.merged_rips,
+           (unsigned long long)S_.merges, (unsigned long long)S_.merged_map_bytes, S_.merge_ms, S_.produce_wait_ms,
            S_.account_ms, S_.make_ms, S_.step_ms, S_.fill_ms, S_.newcov_ms, S_.crashsave_ms, S_.call_ms, ProcessCpuSeconds(),
            MutateCpuNs_.load() * 1e-6);
   return std::string(b) + Exec_.StatsJson() + "}";

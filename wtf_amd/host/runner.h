@@ -145,6 +145,10 @@ class CoverageExchange_t {
   virtual ~CoverageExchange_t() = default;
   virtual int Rank() const = 0;
   virtual int World() const = 0;
+  // whether the session runs the per-step merge at all: across shards, or on
+  // one shard when the exchange is told to take its collective path anyway
+  // (RcclExchange_t's --rccl-force, a test of the RCCL calls at world 1)
+  virtual bool Exchanging() const { return World() > 1; }
   virtual bool AllReduceMax(uint8_t *Map, uint64_t Bytes, bool Device) = 0;
   // *All = every shard's Mine is true
   virtual bool AllDone(bool Mine, bool *All) = 0;
@@ -218,6 +222,10 @@ struct RunnerOptions {
   int rank = 0, world = 1;         // fuzz: shard rank of world (one node per GPU)
   std::string exchange = "127.0.0.1:31337";  // TCP coverage exchange (CPU shards): rank 0 listens here
   std::string nccl_id_file;        // GPU shards: RCCL unique id file (rank 0 writes it)
+  // GPU, test switch (also WTF_RCCL_FORCE=1): a world-1 node still builds the
+  // RCCL communicator and runs every step's merge through it (frozen copy,
+  // fused all-reduce + all-gather, unpack, absorb) instead of skipping it
+  bool rccl_force = false;
   // the wire protocol (remote.h, wire.h): `master` listens, `fuzz` dials
   std::string address;             // tcp://ip:port or unix://path
   int nodes = 1;                   // master: nodes to wait for
@@ -232,6 +240,7 @@ struct RunnerOptions {
 
 struct FuzzStats {
   uint64_t execs = 0, retired = 0, crashes = 0, timeouts = 0, cr3 = 0, errors = 0, batches = 0, merged_rips = 0;
+  uint64_t merges = 0, merged_map_bytes = 0;  // merges absorbed; merged-map bytes they carried
   uint64_t error_retired = 0;  // instructions retired by testcases the engine could not finish
   double run_s = 0, merge_ms = 0;
   double produce_wait_ms = 0, account_ms = 0;  // streaming: waiting on the mutator, master bookkeeping
