@@ -28,9 +28,14 @@ Also on the line (N=1, rank 0):
                 `wtf_twin fuzz` process per host core, same module, mutator
                 and seed scheme, over a bounded wall window.
   hevd          BASELINE.json configs[4] on one GPU: the synthetic ring-0 HEVD
-                snapshot, the hevd module, libFuzzer's mutator (bit-exact
-                restatement), --limit 10000000, --max_len 1028, >= 10 s of
-                node wall time, with its own roofline and twin baseline.
+                snapshot with the I/O manager's IRP path and benign-majority
+                seeds (wtf_amd/tools/hevd_io.py), the hevd module, libFuzzer's
+                mutator (bit-exact restatement), --limit 10000000, --max_len
+                1028, >= 10 s of node wall time, with its own roofline, crash
+                share and twin baseline.
+  hevd_bare     the same on the bare look-alike (wtf_amd/tools/hevd.py: the
+                handlers called from the system-call entry, ~300 instructions
+                per exec, mostly crashing traffic), the round-5 HEVD leg.
   syn           BASELINE.json configs[1]: the ring-3 ALU/branch/load-store
                 interpreter microbench, 65,536 lanes, with its roofline and the
                 C oracle's rate on the host cores.
@@ -61,9 +66,15 @@ TARGETS = {
     # name: (snapshot builder module, workload text, --max_len)
     "tlv_server": ("wtf_amd.tools.tlv", "fuzzer_tlv_server on the synthetic tlv_server snapshot "
                                         "(BASELINE.json configs[2]/[3]), tlv CustomMutator_t, seed 1337", 0x1000),
-    "hevd": ("wtf_amd.tools.hevd", "fuzzer_hevd on the synthetic ring-0 HEVD snapshot (BASELINE.json configs[4] "
-                                   "on one GPU), libFuzzer MutationDispatcher, seed 1337", 1028),
+    "hevd": ("wtf_amd.tools.hevd_io", "fuzzer_hevd on the synthetic ring-0 HEVD snapshot with the I/O manager's "
+                                      "IRP path (BASELINE.json configs[4] on one GPU), libFuzzer "
+                                      "MutationDispatcher, seed 1337", 1028),
+    "hevd_bare": ("wtf_amd.tools.hevd", "fuzzer_hevd on the bare HEVD look-alike (IOCTL handlers called from the "
+                                        "system-call entry, no I/O manager), libFuzzer MutationDispatcher, seed 1337",
+                  1028),
 }
+# the module a workload's snapshot runs (both HEVD snapshots run fuzzer_hevd)
+MODULE = {"tlv_server": "tlv_server", "hevd": "hevd", "hevd_bare": "hevd"}
 
 
 def parse():
@@ -194,13 +205,14 @@ def twin_baseline(name: str, base: str, seconds: float, cores: int, limit: int) 
     """One `wtf_twin fuzz` client per host core (the reference's one node per
     core), seeds 1337 + i, for `seconds` of wall time."""
     max_len = TARGETS[name][2]
+    module = MODULE[name]
     tmp = tempfile.mkdtemp(prefix=f"twin_{name}_")
     try:
         procs = []
         for i in range(cores):
             d = os.path.join(tmp, f"c{i}")
             shutil.copytree(base, d, ignore=shutil.ignore_patterns("outputs", "crashes", "work"))
-            procs.append(subprocess.Popen([TWIN, "fuzz", "--name", name, "--target", d, "--lanes", "1024",
+            procs.append(subprocess.Popen([TWIN, "fuzz", "--name", module, "--target", d, "--lanes", "1024",
                                            "--seconds", str(seconds), "--seed", str(1337 + i), "--limit", str(limit),
                                            "--max_len", str(max_len)], stdout=subprocess.PIPE, text=True,
                                           env={**os.environ, "OMP_NUM_THREADS": "1"}))
@@ -296,26 +308,32 @@ def sched_flags(a) -> list[str]:
     return f
 
 
-def hevd_leg(base: str, lanes: int, limit: int, seconds: float, flags=()) -> dict:
-    """`wtfgpu fuzz` (the product node binary) on HEVD for `seconds` of wall time."""
+def hevd_leg(base: str, lanes: int, limit: int, seconds: float, flags=(), name: str = "hevd") -> dict:
+    """`wtfgpu fuzz` (the product node binary) on an HEVD snapshot for
+    `seconds` of wall time: `hevd` (the I/O manager's IRP path) or
+    `hevd_bare` (the handlers called straight from the system-call entry)."""
     out = subprocess.run([WTFGPU, "fuzz", "--name", "hevd", "--target", base, "--lanes", str(lanes),
                           "--seconds", str(seconds), "--seed", "1337", "--limit", str(limit), "--max_len", "1028",
                           *flags],
                          check=True, capture_output=True, text=True, timeout=seconds * 6 + 300).stdout
     g = json.loads([x for x in out.splitlines() if x.startswith("{")][-1])
     b = g["backend"]
-    pmc = load_pmc("hevd", lanes, limit)
-    return {"workload": TARGETS["hevd"][1], "lanes": lanes, "limit": limit, "execs": g["execs"],
+    pmc = load_pmc(name, lanes, limit)
+    return {"workload": TARGETS[name][1], "lanes": lanes, "limit": limit, "execs": g["execs"],
             "wall_s": g["wall_s"], "value": g["execs"] / g["wall_s"], "unit": "execs/s",
             "instr_per_s": g["retired"] / g["wall_s"], "instr_per_exec": g["retired"] / max(1, g["execs"]),
+            "crash_share": g["crashes"] / max(1, g["execs"]),
             "unique_crashes": g["unique_crashes"], "coverage": g["coverage"], "errors": g["errors"],
             "gpu_retired_fraction": (g["retired"] - g["error_retired"]) / max(1, g["retired"]),
             "lanes_per_wave_step": g["retired"] / max(1, b["group_steps"]),
             "roofline": roofline(b["alg_bytes"], b["kernel_launches"], b["kernel_ms"], pmc, b["group_steps"],
                                  g["retired"]), "backend": b,
             "kernel_busy_frac": b["kernel_ms"] / (g["wall_s"] * 1e3),
-            "note": "the HEVD look-alike's IOCTL path is ~300 instructions per exec: no IO manager (SURVEY F3), so "
-                    "this leg says little about a real HEVD snapshot's throughput",
+            "note": ("the I/O manager's METHOD_NEITHER path (trap frame, handle table, IRP lookaside, a filter "
+                     "device, IofCompleteRequest) and benign-majority traffic; a real Windows + HEVD dump cannot be "
+                     "fetched (SURVEY F3)" if name == "hevd" else
+                     "the bare look-alike's IOCTL path is ~300 instructions per exec: no I/O manager, mostly "
+                     "crashing traffic"),
             "node": {k: g.get(k) for k in ("step_ms", "account_ms", "newcov_ms", "crashsave_ms", "produce_wait_ms",
                                            "make_ms", "fill_ms", "run_s", "batches", "crashes")}}
 
@@ -390,6 +408,7 @@ def run(a, rank, world, local, tmp):
     tlv_dir = build_target("tlv_server", os.path.join(tmp, "tlv"))
     legs = rank == 0 and world == 1 and not a.no_legs
     hevd_dir = build_target("hevd", os.path.join(tmp, "hevd")) if legs else None
+    bare_dir = build_target("hevd_bare", os.path.join(tmp, "hevd_bare")) if legs else None
     cores, core_info = cpu_cores()
     if a.cpu_threads:
         cores = a.cpu_threads
@@ -398,6 +417,7 @@ def run(a, rank, world, local, tmp):
         cpu["tlv_server"] = twin_baseline("tlv_server", tlv_dir, a.cpu_seconds, cores, a.limit)
         if legs:
             cpu["hevd"] = twin_baseline("hevd", hevd_dir, a.cpu_seconds, cores, a.hevd_limit)
+            cpu["hevd_bare"] = twin_baseline("hevd_bare", bare_dir, a.cpu_seconds, cores, a.hevd_limit)
             cpu["syn"] = syn_cpu_baseline(a.cpu_seconds, cores, a.limit)
 
     import torch
@@ -488,14 +508,15 @@ def run(a, rank, world, local, tmp):
             if out["cpu_node"]:
                 out["vs_cpu_node"] = out["cpu_node"]["vs_cpu_node"]
         if legs:
-            h = hevd_leg(hevd_dir, a.hevd_lanes, a.hevd_limit, a.leg_seconds, sched_flags(a))
-            if "hevd" in cpu:
-                h["cpu_baseline"] = cpu["hevd"]
-                h["vs_cpu"] = h["value"] / cpu["hevd"]["value"]
-                h["cpu_node"] = node_extrapolation(h["value"], cpu["hevd"], core_info)
-                if h["cpu_node"]:
-                    h["vs_cpu_node"] = h["cpu_node"]["vs_cpu_node"]
-            out["hevd"] = h
+            for leg, d in (("hevd", hevd_dir), ("hevd_bare", bare_dir)):
+                h = hevd_leg(d, a.hevd_lanes, a.hevd_limit, a.leg_seconds, sched_flags(a), leg)
+                if leg in cpu:
+                    h["cpu_baseline"] = cpu[leg]
+                    h["vs_cpu"] = h["value"] / cpu[leg]["value"]
+                    h["cpu_node"] = node_extrapolation(h["value"], cpu[leg], core_info)
+                    if h["cpu_node"]:
+                        h["vs_cpu_node"] = h["cpu_node"]["vs_cpu_node"]
+                out[leg] = h
             s = syn_leg(a.syn_lanes, a.limit, 10, local)
             if "syn" in cpu:
                 s["cpu_baseline"] = cpu["syn"]

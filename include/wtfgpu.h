@@ -326,6 +326,35 @@ int wtfgpu_run(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, uint64_t max_ste
 int wtfgpu_run_async(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, uint64_t max_steps);
 int wtfgpu_run_wait(wtfgpu_ctx *ctx, wtfgpu_run_stats_t *stats);
 
+/* Asynchronous plumbing. The calls that only change lane state
+ * (wtfgpu_restore_lanes, wtfgpu_stop, wtfgpu_resume, wtfgpu_set_feed_lanes,
+ * wtfgpu_clear_coverage_lanes) are queued on the current queue and return at
+ * once: they are ordered before the queue's later work, and
+ * wtfgpu_select_queue orders the next queue's work after them. (A
+ * synchronous call would wait until the other queue's k_run left a compute
+ * unit free, which is at its next launch boundary.)
+ *
+ * A slice's read-back, queued right after wtfgpu_run_async and complete when
+ * wtfgpu_run_wait returns (replaces wtfgpu_read_exits / _read_bytes /
+ * _read_dirty_counts / _read_stop_args for the range; every host pointer
+ * pinned, wtfgpu_host_alloc): exits[count] as wtfgpu_read_exits; optional
+ * bytes[count], dirty[count], stop_args[6 * count] (every lane's six kept
+ * arguments, meaningful for WTFGPU_EXIT_STOP_ARGS). Replaces the
+ * bochscpu_cpu_run return path's per-testcase state reads
+ * (bochscpu_backend.cc:388-410). */
+int wtfgpu_prefetch_results(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, wtfgpu_exit_t *exits,
+                            uint64_t *bytes, uint32_t *dirty, uint64_t *stop_args);
+/* The new-coverage sets of the range's stopped lanes (status neither RUNNING
+ * nor IDLE), gathered after the slice: hdr[0] = entries, hdr[1] & 1 = a set
+ * overflowed (pinned hdr[2], valid after wtfgpu_run_wait);
+ * wtfgpu_prefetched_coverage then copies the first n <= 2^22 (lane, rip)
+ * entries (more entries than that: read the sets with
+ * wtfgpu_collect_coverage_lanes). WTFGPU_ERR_STATE when coverage is off.
+ * The sets are not emptied (wtfgpu_clear_coverage_lanes, or the restore). */
+int wtfgpu_prefetch_coverage(wtfgpu_ctx *ctx, uint32_t first, uint32_t count, uint64_t *hdr);
+int wtfgpu_prefetched_coverage(wtfgpu_ctx *ctx, uint32_t *out_lanes, uint64_t *out_rips, uint64_t n);
+int wtfgpu_clear_coverage_lanes(wtfgpu_ctx *ctx, const uint32_t *lanes, uint32_t n);
+
 /* Per-lane memory. gva translation uses the lane's cr3 and its overlays. */
 int wtfgpu_lane_translate(wtfgpu_ctx *ctx, uint32_t lane, uint64_t gva, uint64_t *gpa);
 int wtfgpu_lane_read_phys(wtfgpu_ctx *ctx, uint32_t lane, uint64_t gpa, void *buf, uint64_t len);

@@ -10,7 +10,7 @@ from tests.cpu_bins import TWIN  # noqa: E402
 
 
 @pytest.mark.skipif(not os.path.exists(TWIN), reason="oracle/wtf_twin not built")
-@pytest.mark.parametrize("name", ["tlv_server", "hevd"])
+@pytest.mark.parametrize("name", ["tlv_server", "hevd", "hevd_bare"])
 def test_twin_baseline_fields(name, tmp_path):
     d = bench.build_target(name, str(tmp_path / name))
     cb = bench.twin_baseline(name, d, seconds=1.0, cores=2, limit=100000)
@@ -33,3 +33,22 @@ def test_roofline_and_node_fields():
 def test_cpu_cores_reports_share():
     used, info = bench.cpu_cores()
     assert used >= 1 and info["used"] == used and info["os_cpu_count"] >= 1
+
+
+@pytest.mark.skipif(not os.path.exists(TWIN), reason="oracle/wtf_twin not built")
+def test_hevd_io_seeds_return_a_status(tmp_path):
+    """The hevd leg's snapshot (wtf_amd/tools/hevd_io.py): every seed takes the
+    I/O manager's IRP path to a status (Ok, no bugcheck), the benign requests
+    run thousands of instructions, and the bare path is far shorter."""
+    from tests import tlv_harness as H
+
+    d = bench.build_target("hevd", str(tmp_path / "io"))
+    res = {r["input"]: r for r in H.run(H.TWIN, d, os.path.join(d, "inputs"), str(tmp_path / "r.jsonl"), lanes=64,
+                                         limit=10_000_000, name="hevd")}
+    assert all(r["result"] == "ok" and not r["error"] for r in res.values()), res
+    assert res["crc_1024"]["icount"] > 10000 and res["records_types"]["icount"] > 1500
+    assert 400 < res["invalid"]["icount"] < 1000  # the IRP path alone, around an unknown IOCTL
+    b = bench.build_target("hevd_bare", str(tmp_path / "bare"))
+    bare = {r["input"]: r for r in H.run(H.TWIN, b, os.path.join(b, "inputs"), str(tmp_path / "b.jsonl"), lanes=64,
+                                          limit=10_000_000, name="hevd")}
+    assert bare["invalid"]["icount"] < res["invalid"]["icount"] // 2

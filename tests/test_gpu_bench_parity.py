@@ -12,7 +12,8 @@ set. The samples are then run again on the GPU node at the same lane count
 through the streaming path (`wtfgpu run --stream-run --full-coverage`, two
 copies of each: two pipelined halves, regrouping), and each testcase's FULL
 coverage set must equal the twin's. tlv_server at --limit 100000 and HEVD at
---limit 10000000.
+--limit 10000000; the bench's HEVD leg runs the snapshot with
+the I/O manager's IRP path (wtf_amd/tools/hevd_io.py), checked the same way.
 
 Engine errors: the only ones allowed are handler faults (U43: a handler's
 guest access that does not translate, e.g. HEVD's nt!DbgPrintEx handler
@@ -119,6 +120,18 @@ def test_hevd_bench_config_parity(tmp_path):
                              max_len=1028, lanes=HEVD_LANES)
     assert len(got) >= 4096
     assert {g["result"] for g in got} >= {"ok", "crash"}
+
+
+def test_hevd_io_bench_config_parity(tmp_path):
+    """The hevd leg as benchmarked (the I/O manager's IRP path, benign-majority
+    seeds): mostly statuses, thousands of instructions per testcase."""
+    target = H.build_hevd_io_target(str(tmp_path / "hevd_io"))
+    got = _sample_and_replay(str(tmp_path), target, "hevd", runs=655360, every=128, limit=10_000_000,
+                             max_len=1028, lanes=HEVD_LANES)
+    assert len(got) >= 4096
+    ok = sum(g["result"] == "ok" for g in got)
+    assert ok > 0.8 * len(got) and {g["result"] for g in got} >= {"ok", "crash"}
+    assert sum(g["icount"] for g in got) / len(got) > 1500
 
 
 _SAME = ("execs", "retired", "coverage", "corpus", "crashes", "unique_crashes", "timeouts", "cr3", "errors")

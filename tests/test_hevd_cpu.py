@@ -133,4 +133,10 @@ def test_dbgprintex_engine_error_path(target, tmp_path):
     import json
     sym = json.load(open(os.path.join(target, "state", "symbol-store.json")))
     assert rips[-1] == int(sym["nt!DbgPrintEx"], 16)                     # the last rip: the handler's
-    assert int(sym["nt!DbgPrintEx"], 16) < rips[-2] < int(sym["nt!DbgPrintEx"], 16) + 0x1000  # a ret in the driver
+    # the rip before it is the driver's: TriggerBufferOverflowStack's own ret
+    # (the look-alike links the driver into nt's image, right after nt!DbgPrintEx)
+    from wtf_amd.tools import hevd
+    ks = {k[7:]: v for k, v in hevd.build_space(str(tmp_path / "img"))[3].items() if k.startswith("kernel:")}
+    f = ks["TriggerBufferOverflowStack"]
+    end = min(v for v in ks.values() if v > f)
+    assert f <= rips[-2] < end, (hex(rips[-2]), hex(f), hex(end))

@@ -18,6 +18,14 @@ def build_hevd_target(d: str) -> str:
     return d
 
 
+def build_hevd_io_target(d: str) -> str:
+    """The hevd leg's snapshot: the I/O manager's IRP path (wtf_amd/tools/hevd_io.py)."""
+    from wtf_amd.tools.hevd_io import build, seed_inputs
+    build(os.path.join(d, "state"), os.path.join(d, "work"))
+    seed_inputs(os.path.join(d, "inputs"))
+    return d
+
+
 def build_target(d: str) -> str:
     from wtf_amd.tools.tlv import build, seed_inputs
     build(os.path.join(d, "state"), os.path.join(d, "work"))

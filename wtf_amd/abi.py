@@ -121,6 +121,11 @@ def load_hip_library(path: str = LIB_PATH) -> C.CDLL:
         "wtfgpu_lane_seeds": ([P, C.POINTER(U32), U32, C.POINTER(U64), C.c_int], C.c_int),
         "wtfgpu_run_async": ([P, U32, U32, U64], C.c_int),
         "wtfgpu_run_wait": ([P, C.POINTER(RunStats)], C.c_int),
+        "wtfgpu_prefetch_results": ([P, U32, U32, C.POINTER(Exit), C.POINTER(U64), C.POINTER(U32), C.POINTER(U64)],
+                                    C.c_int),
+        "wtfgpu_prefetch_coverage": ([P, U32, U32, C.POINTER(U64)], C.c_int),
+        "wtfgpu_prefetched_coverage": ([P, C.POINTER(U32), C.POINTER(U64), U64], C.c_int),
+        "wtfgpu_clear_coverage_lanes": ([P, C.POINTER(U32), U32], C.c_int),
         "wtfgpu_set_breakpoints": ([P, C.POINTER(U64), U32], C.c_int),
         "wtfgpu_set_breakpoint_actions": ([P, C.POINTER(BpAction), U32], C.c_int),
         "wtfgpu_set_feed": ([P, U32, U32, C.POINTER(U64), C.c_char_p, C.c_char_p, U64], C.c_int),

@@ -2027,6 +2027,32 @@ __global__ void k_cov_collect(Dev P, const u32 *lanes, u32 first, u32 n, u32 *ou
   if (threadIdx.x == 0 && P.cov_overflow[lane]) atomicOr(ovf, 1u);
 }
 
+// The coverage sets of the stopped lanes of [first, first + count) (status
+// neither RUNNING nor IDLE: the lanes a slice finished or left at a host
+// breakpoint), compacted as k_cov_collect does (wtfgpu_prefetch_coverage).
+// One wave per lane; an empty set (cov_cnt 0, the common case once the
+// coverage has settled) costs one load.
+__global__ void k_cov_collect_stopped(Dev P, u32 first, u32 count, u32 *out_lane, u64 *out_rip, u64 cap,
+                                      unsigned long long *n_out, u32 *ovf) {
+  const u32 i = blockIdx.x * 4 + (threadIdx.x >> 6), lid = threadIdx.x & 63;
+  if (i >= count) return;
+  const u32 lane = first + i;
+  const u32 st = P.status[lane];
+  if (st == WTFGPU_RUNNING || st == WTFGPU_EXIT_IDLE) return;
+  if (P.cov_overflow[lane] && lid == 0) atomicOr(ovf, 1u);
+  if (P.cov_cnt[lane] == 0) return;
+  const u32 g = P.lane_gen[lane];
+  const u64 base = (u64)lane * P.H;
+  for (u32 k = lid; k < P.H; k += 64) {
+    if (P.cov_gen[base + k] != g) continue;
+    const unsigned long long pos = atomicAdd(n_out, 1ull);
+    if (pos < cap) {
+      out_lane[pos] = lane;
+      out_rip[pos] = P.cov_rip[base + k];
+    }
+  }
+}
+
 // Rdrand seeds of a lane list: gathered into / scattered from buf.
 __global__ void k_lane_seeds(Dev P, const u32 *lanes, u32 n, u64 *buf, int write) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2199,6 +2225,16 @@ struct QueueRes {
   void *d_rtemp = nullptr;
   size_t rtemp_bytes = 0;
   u32 async_launches = 0;  // wtfgpu_run_async in flight (0 = none)
+  // asynchronous plumbing (see ring_put / wtfgpu_prefetch_*): the pinned
+  // upload ring, the prefetched exits / coverage entries, the event after the
+  // queue's plumbing of its last run (another queue's work is ordered after it)
+  u8 *h_ring = nullptr;
+  u64 ring_cap = 0, ring_off = 0;
+  wtfgpu_exit_t *d_exq = nullptr;
+  u64 exq_cap = 0;
+  u8 *d_pcov = nullptr;
+  hipEvent_t ev_pre = nullptr;
+  bool pre_valid = false;
 };
 
 struct wtfgpu_ctx {
@@ -2290,6 +2326,13 @@ struct wtfgpu_ctx {
   double nspi_sched[2] = {0, 0};  // run-to-completion runs: kernel ns per retired instruction, EMA
   u64 rg_sync_runs = 0;
   u32 async_launches = 0;
+  u8 *h_ring = nullptr;
+  u64 ring_cap = 0, ring_off = 0;
+  wtfgpu_exit_t *d_exq = nullptr;
+  u64 exq_cap = 0;
+  u8 *d_pcov = nullptr;
+  hipEvent_t ev_pre = nullptr;
+  bool pre_valid = false;
   // the current queue's resources live in the members above; the others here
   QueueRes queues[2];
   u32 cur_queue = 0;
@@ -2344,6 +2387,35 @@ int ensure_stage(wtfgpu_ctx *c, u64 bytes) {
   return WTFGPU_OK;
 }
 
+// Pinned staging for an asynchronous upload on the current queue: the bytes
+// are copied into the queue's pinned ring and the caller queues the DMA from
+// there, so the call returns without waiting for the queue's stream (whose
+// earlier kernels may wait behind the other queue's k_run for free compute
+// units: every VGPR of a SIMD is taken by two k_run waves). The ring restarts
+// after each synchronisation of the stream (wtfgpu_run_wait, or here when
+// full): no DMA still reads it then.
+u8 *ring_put(wtfgpu_ctx *c, const void *src, u64 bytes) {
+  const u64 need = (bytes + 255) & ~255ull;
+  if (c->ring_off + need > c->ring_cap) {
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return nullptr;
+    c->ring_off = 0;
+    if (need > c->ring_cap) {
+      if (c->h_ring) (void)hipHostFree(c->h_ring);
+      c->h_ring = nullptr;
+      c->ring_cap = 0;
+      const u64 want = std::max<u64>(need * 2, 4ull << 20);
+      if (hipHostMalloc((void **)&c->h_ring, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+      c->ring_cap = want;
+    }
+  }
+  u8 *p = c->h_ring + c->ring_off;
+  if (src && bytes) memcpy(p, src, bytes);
+  c->ring_off += need;
+  return p;
+}
+// the current queue's stream is idle: the ring may be reused from its start
+void ring_reset(wtfgpu_ctx *c) { c->ring_off = 0; }
+
 void queue_save(wtfgpu_ctx *c, QueueRes &q) {
   q.stream = c->stream;
   q.d_scratch = c->d_scratch;
@@ -2360,6 +2432,14 @@ void queue_save(wtfgpu_ctx *c, QueueRes &q) {
   q.d_rtemp = c->d_rtemp;
   q.rtemp_bytes = c->rtemp_bytes;
   q.async_launches = c->async_launches;
+  q.h_ring = c->h_ring;
+  q.ring_cap = c->ring_cap;
+  q.ring_off = c->ring_off;
+  q.d_exq = c->d_exq;
+  q.exq_cap = c->exq_cap;
+  q.d_pcov = c->d_pcov;
+  q.ev_pre = c->ev_pre;
+  q.pre_valid = c->pre_valid;
 }
 void queue_load(wtfgpu_ctx *c, const QueueRes &q) {
   c->stream = q.stream;
@@ -2377,11 +2457,20 @@ void queue_load(wtfgpu_ctx *c, const QueueRes &q) {
   c->d_rtemp = q.d_rtemp;
   c->rtemp_bytes = q.rtemp_bytes;
   c->async_launches = q.async_launches;
+  c->h_ring = q.h_ring;
+  c->ring_cap = q.ring_cap;
+  c->ring_off = q.ring_off;
+  c->d_exq = q.d_exq;
+  c->exq_cap = q.exq_cap;
+  c->d_pcov = q.d_pcov;
+  c->ev_pre = q.ev_pre;
+  c->pre_valid = q.pre_valid;
 }
 int queue_create(QueueRes &q) {
   HIPCHK(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
   HIPCHK(hipEventCreate(&q.ev0));
   HIPCHK(hipEventCreate(&q.ev1));
+  HIPCHK(hipEventCreateWithFlags(&q.ev_pre, hipEventDisableTiming));
   if (dalloc(&q.d_stat, STAT_N) || dalloc(&q.d_dev, 1)) return WTFGPU_ERR_OOM;
   return WTFGPU_OK;
 }
@@ -2399,8 +2488,13 @@ void queue_destroy(QueueRes &q) {
   dfree(q.d_stat);
   dfree(q.d_dev);
   dfree(q.d_scratch);
+  dfree(q.d_exq);
+  dfree(q.d_pcov);
   if (q.h_stage) (void)hipHostFree(q.h_stage);
   q.h_stage = nullptr;
+  if (q.h_ring) (void)hipHostFree(q.h_ring);
+  q.h_ring = nullptr;
+  if (q.ev_pre) (void)hipEventDestroy(q.ev_pre);
   if (q.ev0) (void)hipEventDestroy(q.ev0);
   if (q.ev1) (void)hipEventDestroy(q.ev1);
   if (q.stream) (void)hipStreamDestroy(q.stream);
@@ -3012,12 +3106,13 @@ int wtfgpu_restore_lanes(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n) {
   for (u32 i = 0; i < n; i++)
     if (lanes[i] >= c->P.nlanes) return WTFGPU_ERR_INVALID;
   HIPCHK(hipSetDevice(c->device));
-  if (ensure_scratch(c, (u64)n * 4)) return WTFGPU_ERR_OOM;
-  HIPCHK(hipMemcpyAsync(c->d_scratch, lanes, (u64)n * 4, hipMemcpyHostToDevice, c->stream));
+  // queued without a wait (ordered before the queue's later work, see ring_put)
+  const u8 *st = ring_put(c, lanes, (u64)n * 4);
+  if (!st || ensure_scratch(c, (u64)n * 4)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemcpyAsync(c->d_scratch, st, (u64)n * 4, hipMemcpyHostToDevice, c->stream));
   k_restore_list<<<(n + 255) / 256, 256, 0, c->stream>>>(c->P, c->d_init, c->d_init_full, c->d_full,
                                                          (const u32 *)c->d_scratch, n);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(c->stream));
   return WTFGPU_OK;
 }
 
@@ -3032,8 +3127,8 @@ int wtfgpu_set_feed_lanes(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, cons
   }
   if (n == 0) return WTFGPU_OK;
   HIPCHK(hipSetDevice(c->device));
-  HIPCHK(hipStreamSynchronize(c->stream));
   const u64 N = c->P.nlanes;
+  if (!c->d_feedpos || c->feed_stride == 0) HIPCHK(hipDeviceSynchronize());  // first use: buffers change under every queue
   if (!c->d_feedpos) {
     if (dalloc(&c->d_feedpos, N) || dalloc(&c->d_feedend, N)) return WTFGPU_ERR_OOM;
     std::vector<u64> none(N, ~0ull);
@@ -3054,8 +3149,8 @@ int wtfgpu_set_feed_lanes(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, cons
   const u64 o_off = ((u64)n * 4 + 255) & ~255ull, o_has = (o_off + (u64)(n + 1) * 8 + 255) & ~255ull,
             o_data = (o_has + n + 255) & ~255ull;
   if (ensure_scratch(c, o_data + nbytes)) return WTFGPU_ERR_OOM;
-  if (ensure_stage(c, o_data)) return WTFGPU_ERR_OOM;
-  u8 *stage = c->h_stage;
+  u8 *stage = ring_put(c, nullptr, o_data);  // (see ring_put: no wait for the queue)
+  if (!stage) return WTFGPU_ERR_OOM;
   memcpy(stage, lanes, (u64)n * 4);
   memcpy(stage + o_off, offsets, (u64)(n + 1) * 8);
   if (has_feed) memcpy(stage + o_has, has_feed, n);
@@ -3194,14 +3289,16 @@ static int set_status_list(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n, uin
     if (lanes[i] >= c->P.nlanes) return WTFGPU_ERR_INVALID;
   HIPCHK(hipSetDevice(c->device));
   // lane list (+ skip flags) -> scratch, one scatter kernel: no whole-array round trips
+  // queued without a wait (ordered before the queue's later work, see ring_put)
   const u64 o_skip = ((u64)n * 4 + 255) & ~255ull;
-  if (ensure_scratch(c, o_skip + n)) return WTFGPU_ERR_OOM;
-  HIPCHK(hipMemcpyAsync(c->d_scratch, lanes, (u64)n * 4, hipMemcpyHostToDevice, c->stream));
-  if (skip) HIPCHK(hipMemcpyAsync(c->d_scratch + o_skip, skip, n, hipMemcpyHostToDevice, c->stream));
+  u8 *st = ring_put(c, nullptr, o_skip + n);
+  if (!st || ensure_scratch(c, o_skip + n)) return WTFGPU_ERR_OOM;
+  memcpy(st, lanes, (u64)n * 4);
+  if (skip) memcpy(st + o_skip, skip, n);
+  HIPCHK(hipMemcpyAsync(c->d_scratch, st, skip ? o_skip + n : (u64)n * 4, hipMemcpyHostToDevice, c->stream));
   k_set_status<<<(n + 255) / 256, 256, 0, c->stream>>>(c->P, (const u32 *)c->d_scratch, n, status,
                                                       skip ? c->d_scratch + o_skip : nullptr);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(c->stream));
   return WTFGPU_OK;
 }
 
@@ -3429,6 +3526,8 @@ int wtfgpu_run_async(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t max
 #if WTFGPU_P_BYREF
   HIPCHK(hipMemcpyAsync(c->d_dev, &Q, sizeof(Dev), hipMemcpyHostToDevice, c->stream));
 #endif
+  HIPCHK(hipEventRecord(c->ev_pre, c->stream));  // the plumbing before this run (wtfgpu_select_queue)
+  c->pre_valid = true;
   HIPCHK(hipMemsetAsync(c->d_stat, 0, STAT_N * 8, c->stream));
   HIPCHK(hipEventRecord(c->ev0, c->stream));
   u32 k = 0;
@@ -3448,6 +3547,7 @@ int wtfgpu_run_wait(wtfgpu_ctx *c, wtfgpu_run_stats_t *stats) {
     u64 s[STAT_N];
     HIPCHK(hipMemcpyAsync(s, c->d_stat, sizeof(s), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    ring_reset(c);
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     st.kernel_launches = c->async_launches;
@@ -3459,6 +3559,77 @@ int wtfgpu_run_wait(wtfgpu_ctx *c, wtfgpu_run_stats_t *stats) {
     print_stamps(s);
   }
   if (stats) *stats = st;
+  return WTFGPU_OK;
+}
+
+int wtfgpu_prefetch_results(wtfgpu_ctx *c, uint32_t first, uint32_t count, wtfgpu_exit_t *exits, uint64_t *bytes,
+                            uint32_t *dirty, uint64_t *stop_args) {
+  if (!lanes_ok(c, first, count) || !exits) return WTFGPU_ERR_INVALID;
+  if (count == 0) return WTFGPU_OK;
+  HIPCHK(hipSetDevice(c->device));
+  if (c->exq_cap < count) {  // stream-ordered, as ensure_scratch
+    if (c->d_exq) HIPCHK(hipFreeAsync(c->d_exq, c->stream));
+    c->d_exq = nullptr;
+    c->exq_cap = 0;
+    if (hipMallocAsync((void **)&c->d_exq, (u64)count * sizeof(wtfgpu_exit_t), c->stream) != hipSuccess)
+      return WTFGPU_ERR_OOM;
+    c->exq_cap = count;
+  }
+  k_pack_exits<<<(count + 255) / 256, 256, 0, c->stream>>>(c->P, first, count, c->d_exq);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(exits, c->d_exq, (u64)count * sizeof(wtfgpu_exit_t), hipMemcpyDeviceToHost, c->stream));
+  if (bytes) HIPCHK(hipMemcpyAsync(bytes, c->d_nbytes + first, (u64)count * 8, hipMemcpyDeviceToHost, c->stream));
+  if (dirty) HIPCHK(hipMemcpyAsync(dirty, c->d_ovcount + first, (u64)count * 4, hipMemcpyDeviceToHost, c->stream));
+  if (stop_args && c->d_stopargs)
+    HIPCHK(hipMemcpyAsync(stop_args, c->d_stopargs + (u64)first * 6, (u64)count * 48, hipMemcpyDeviceToHost,
+                          c->stream));
+  return WTFGPU_OK;
+}
+
+constexpr u64 kPcovCap = 1ull << 22;  // prefetched coverage entries per queue
+constexpr u64 kPcovLanes = 256, kPcovRips = kPcovLanes + kPcovCap * 4;
+
+int wtfgpu_prefetch_coverage(wtfgpu_ctx *c, uint32_t first, uint32_t count, uint64_t *hdr) {
+  if (!lanes_ok(c, first, count) || !hdr) return WTFGPU_ERR_INVALID;
+  if (!c->d_covrip || count == 0) {
+    hdr[0] = hdr[1] = 0;
+    return WTFGPU_ERR_STATE;  // nothing to prefetch: the caller reads the sets itself
+  }
+  HIPCHK(hipSetDevice(c->device));
+  if (!c->d_pcov && hipMallocAsync((void **)&c->d_pcov, kPcovRips + kPcovCap * 8, c->stream) != hipSuccess) {
+    c->d_pcov = nullptr;
+    return WTFGPU_ERR_OOM;
+  }
+  HIPCHK(hipMemsetAsync(c->d_pcov, 0, 16, c->stream));
+  k_cov_collect_stopped<<<(count + 3) / 4, 256, 0, c->stream>>>(
+      c->P, first, count, (u32 *)(c->d_pcov + kPcovLanes), (u64 *)(c->d_pcov + kPcovRips), kPcovCap,
+      (unsigned long long *)c->d_pcov, (u32 *)(c->d_pcov + 8));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(hdr, c->d_pcov, 16, hipMemcpyDeviceToHost, c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_prefetched_coverage(wtfgpu_ctx *c, uint32_t *out_lanes, uint64_t *out_rips, uint64_t n) {
+  if (!c || (n && (!out_lanes || !out_rips)) || n > kPcovCap || (n && !c->d_pcov)) return WTFGPU_ERR_INVALID;
+  if (n == 0) return WTFGPU_OK;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemcpyAsync(out_lanes, c->d_pcov + kPcovLanes, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(out_rips, c->d_pcov + kPcovRips, n * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WTFGPU_OK;
+}
+
+int wtfgpu_clear_coverage_lanes(wtfgpu_ctx *c, const uint32_t *lanes, uint32_t n) {
+  if (!c || (n && !lanes)) return WTFGPU_ERR_INVALID;
+  if (!c->d_covrip || n == 0) return WTFGPU_OK;
+  for (u32 i = 0; i < n; i++)
+    if (lanes[i] >= c->P.nlanes) return WTFGPU_ERR_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  const u8 *st = ring_put(c, lanes, (u64)n * 4);
+  if (!st || ensure_scratch(c, (u64)n * 4)) return WTFGPU_ERR_OOM;
+  HIPCHK(hipMemcpyAsync(c->d_scratch, st, (u64)n * 4, hipMemcpyHostToDevice, c->stream));
+  k_cov_clear<<<(n + 255) / 256, 256, 0, c->stream>>>(c->P, (const u32 *)c->d_scratch, n);
+  HIPCHK(hipGetLastError());
   return WTFGPU_OK;
 }
 
@@ -3504,6 +3675,17 @@ int wtfgpu_select_queue(wtfgpu_ctx *c, uint32_t queue) {
   QueueRes &next = c->queues[queue];
   if (!next.stream)
     if (int rc = queue_create(next)) return rc;
+  // The plumbing queued on the old queue without a wait (restores, status
+  // and feed uploads, wtfgpu_restore_lanes ...) may touch lanes the new
+  // queue runs: the new queue's later work is ordered after it. Only after
+  // the plumbing: with a run in flight, after the event wtfgpu_run_async
+  // recorded before its launches (the two queues' slices still overlap);
+  // without one, after everything the old queue holds.
+  if (!c->async_launches) {
+    HIPCHK(hipEventRecord(c->ev_pre, c->stream));
+    c->pre_valid = true;
+  }
+  if (c->pre_valid) HIPCHK(hipStreamWaitEvent(next.stream, c->ev_pre, 0));
   queue_save(c, c->queues[c->cur_queue]);
   queue_load(c, next);
   c->cur_queue = queue;
@@ -3763,12 +3945,14 @@ int wtfgpu_host_free(wtfgpu_ctx *c, void *p) {
 int wtfgpu_read_dirty(wtfgpu_ctx *c, uint32_t lane, uint64_t *gpas, uint32_t cap, uint32_t *n) {
   if (!c || lane >= c->P.nlanes || !n) return WTFGPU_ERR_INVALID;
   HIPCHK(hipSetDevice(c->device));
-  u32 cnt = 0;
-  HIPCHK(hipMemcpy(&cnt, c->d_ovcount + lane, 4, hipMemcpyDeviceToHost));
+  u32 cnt = 0;  // (on the queue's stream: after its queued restores)
+  HIPCHK(hipMemcpyAsync(&cnt, c->d_ovcount + lane, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
   *n = cnt;
   for (u32 k = 0; k < cnt && k < cap; k++) {
     u32 g = 0;
-    HIPCHK(hipMemcpy(&g, c->d_ovgpfn + (u64)k * c->P.nlanes + lane, 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpyAsync(&g, c->d_ovgpfn + (u64)k * c->P.nlanes + lane, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     gpas[k] = (u64)g << 12;
   }
   return WTFGPU_OK;
@@ -3993,7 +4177,8 @@ int wtfgpu_coverage_rips(wtfgpu_ctx *c, uint64_t *rips, uint64_t cap, uint64_t *
   if (!c->d_covmap) return WTFGPU_OK;
   HIPCHK(hipSetDevice(c->device));
   std::vector<u8> m(c->ncovslots * WTFGPU_PAGE_SIZE);
-  HIPCHK(hipMemcpy(m.data(), c->d_covmap, m.size(), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpyAsync(m.data(), c->d_covmap, m.size(), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
   u64 k = 0;
   for (u64 s = 0; s < c->ncovslots; s++)
     for (u64 o = 0; o < WTFGPU_PAGE_SIZE; o++)

@@ -54,10 +54,9 @@ int gpr_index(Registers_t r) {
 
 GpuBackend_t::GpuBackend_t() = default;
 GpuBackend_t::~GpuBackend_t() {
-  for (Part &P : parts_) {
-    if (P.pin) wtfgpu_host_free(ctx_, P.pin);
-    if (P.ex) wtfgpu_host_free(ctx_, P.ex);
-  }
+  for (Part &P : parts_)
+    for (void *p : {(void *)P.pin, (void *)P.ex, (void *)P.nb, (void *)P.dc, (void *)P.sargs, (void *)P.cov_hdr})
+      if (p) wtfgpu_host_free(ctx_, p);
   if (wpin_) wtfgpu_host_free(ctx_, wpin_);
   if (ctx_) wtfgpu_destroy(ctx_);
 }
@@ -733,7 +732,8 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
 // module handler's failed VirtWriteDirty (fuzzer_tlv_server.cc:130-158): a
 // handler fault, the testcase an engine error (U43).
 bool GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first, const wtfgpu_exit_t *ex,
-                            std::vector<uint8_t> &done, std::vector<LaneResult> *out, std::vector<uint32_t> &hits) {
+                            std::vector<uint8_t> &done, std::vector<LaneResult> *out, std::vector<uint32_t> &hits,
+                            const uint64_t *stop_args) {
   std::vector<uint8_t> hit(pending.size(), 0);
   HostPool::Get().For(pending.size(), 1024, [&](size_t pi) {
     const uint32_t l = pending[pi];
@@ -781,7 +781,14 @@ bool GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first
   if (named.empty()) return true;
   // device StopWithArgs actions: the handler's Stop(Result(GetArg(0..5)))
   std::vector<uint64_t> args(named.size() * 6);
-  const bool ok = wtfgpu_read_stop_args(ctx_, named.data(), (uint32_t)named.size(), args.data()) == WTFGPU_OK;
+  bool ok = true;
+  if (stop_args) {
+    HostPool::Get().For(named.size(), 2048, [&](size_t k) {
+      memcpy(&args[k * 6], stop_args + (uint64_t)(named[k] - first) * 6, 48);
+    }, named.size() >= 8192);
+  } else {
+    ok = wtfgpu_read_stop_args(ctx_, named.data(), (uint32_t)named.size(), args.data()) == WTFGPU_OK;
+  }
   std::atomic<uint64_t> bad{0};
   HostPool::Get().For(named.size(), 512, [&](size_t k) {
     const uint32_t l = named[k];
@@ -1328,23 +1335,54 @@ void GpuBackend_t::target_restore(const Target_t &Target, const std::vector<uint
 // in the given order against the aggregate (bochscpu_backend.cc:501-504);
 // timed-out lanes' are revoked (client.cc:122-125); the fresh ones join the
 // device map. Their log bits are dropped (the lanes get new testcases next).
-void GpuBackend_t::collect_coverage(const std::vector<uint32_t> &lanes, std::vector<LaneResult> &res) {
+void GpuBackend_t::collect_coverage(const std::vector<uint32_t> &lanes, std::vector<LaneResult> &res,
+                                    const uint64_t *pf_hdr) {
   const auto t0 = Clock::now();
   uint64_t total = 0;
   uint32_t ovf = 0;
-  // one call into buffers that persist (the sets empty when it all fits);
-  // a larger result is read again at its size
-  if (cov_lanes_.size() < (1u << 16)) {
-    cov_lanes_.resize(1u << 16);
-    cov_rips_.resize(1u << 16);
+  constexpr uint64_t kPrefetchCap = 1ull << 22;  // wtfgpu_prefetched_coverage's limit
+  bool pf = pf_hdr && pf_hdr[0] <= kPrefetchCap;
+  if (pf) {
+    // the part's stopped lanes' sets, gathered behind the slice: only the
+    // entries of `lanes` count; their sets are emptied as a read here would
+    total = pf_hdr[0];
+    ovf = (uint32_t)pf_hdr[1] & 1;
+    if (cov_lanes_.size() < total) {
+      cov_lanes_.resize(total);
+      cov_rips_.resize(total);
+    }
+    pf = wtfgpu_prefetched_coverage(ctx_, cov_lanes_.data(), cov_rips_.data(), total) == WTFGPU_OK &&
+         wtfgpu_clear_coverage_lanes(ctx_, lanes.data(), (uint32_t)lanes.size()) == WTFGPU_OK;
+    if (pf && total) {
+      if (cov_want_.size() < nlanes_) cov_want_.assign(nlanes_, 0);
+      for (uint32_t l : lanes) cov_want_[l] = 1;
+      uint64_t k = 0;
+      for (uint64_t i = 0; i < total; i++)
+        if (cov_want_[cov_lanes_[i]]) {
+          cov_lanes_[k] = cov_lanes_[i];
+          cov_rips_[k++] = cov_rips_[i];
+        }
+      for (uint32_t l : lanes) cov_want_[l] = 0;
+      total = k;
+    }
   }
-  wtfgpu_collect_coverage_lanes(ctx_, lanes.data(), (uint32_t)lanes.size(), cov_lanes_.data(), cov_rips_.data(),
-                                cov_lanes_.size(), &total, &ovf);
-  if (total > cov_lanes_.size()) {
-    cov_lanes_.resize(total);
-    cov_rips_.resize(total);
+  if (!pf) {
+    total = 0;
+    ovf = 0;
+    // one call into buffers that persist (the sets empty when it all fits);
+    // a larger result is read again at its size
+    if (cov_lanes_.size() < (1u << 16)) {
+      cov_lanes_.resize(1u << 16);
+      cov_rips_.resize(1u << 16);
+    }
     wtfgpu_collect_coverage_lanes(ctx_, lanes.data(), (uint32_t)lanes.size(), cov_lanes_.data(), cov_rips_.data(),
                                   cov_lanes_.size(), &total, &ovf);
+    if (total > cov_lanes_.size()) {
+      cov_lanes_.resize(total);
+      cov_rips_.resize(total);
+      wtfgpu_collect_coverage_lanes(ctx_, lanes.data(), (uint32_t)lanes.size(), cov_lanes_.data(), cov_rips_.data(),
+                                    cov_lanes_.size(), &total, &ovf);
+    }
   }
   const std::vector<uint32_t> &cl = cov_lanes_;
   const std::vector<uint64_t> &cr = cov_rips_;
@@ -1410,9 +1448,7 @@ uint32_t GpuBackend_t::FreeLanes() const {
   if (busy_.empty()) return parts_n() > 1 ? nlanes_ / 2 : nlanes_;
   const Part &P = parts_[next_part_];
   if (P.launched) return P.hi - P.lo;  // its running lanes may all finish: an upper bound
-  uint32_t n = 0;
-  for (uint32_t l = P.lo; l < P.hi; l++) n += !busy_[l];
-  return n;
+  return (uint32_t)P.free.size();
 }
 
 // Streaming parts: one (every lane, synchronous) or two halves on their own
@@ -1442,8 +1478,11 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
     const uint32_t n = parts_n();
     parts_.assign(n, Part{});
     for (uint32_t p = 0; p < n; p++) {
-      parts_[p].lo = (uint32_t)((uint64_t)nlanes_ * p / n);
-      parts_[p].hi = (uint32_t)((uint64_t)nlanes_ * (p + 1) / n);
+      Part &Q = parts_[p];
+      Q.lo = (uint32_t)((uint64_t)nlanes_ * p / n);
+      Q.hi = (uint32_t)((uint64_t)nlanes_ * (p + 1) / n);
+      Q.free.resize(Q.hi - Q.lo);
+      for (uint32_t l = Q.lo; l < Q.hi; l++) Q.free[l - Q.lo] = l;
     }
     // every lane idle until it gets a testcase
     std::vector<uint32_t> all(nlanes_);
@@ -1463,11 +1502,13 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
   std::vector<std::pair<const uint8_t *, size_t>> tcs;
   fresh.reserve(std::min<size_t>(In.size(), P.hi - P.lo));
   tcs.reserve(fresh.capacity());
-  for (uint32_t l = P.lo; l < P.hi && fresh.size() < In.size(); l++)
-    if (!busy_[l]) {
-      fresh.push_back(l);
-      tcs.push_back({In[fresh.size() - 1].data, In[fresh.size() - 1].size});
-    }
+  {  // the lowest free lanes, in order
+    const size_t take = std::min(In.size(), P.free.size());
+    fresh.assign(P.free.begin(), P.free.begin() + (std::ptrdiff_t)take);
+    P.free.erase(P.free.begin(), P.free.begin() + (std::ptrdiff_t)take);
+    tcs.resize(take);
+    for (size_t i = 0; i < take; i++) tcs[i] = {In[i].data, In[i].size};
+  }
   if (Taken) *Taken = fresh.size();
   stats_.fresh_ms += ms_since(ti);
   if (!fresh.empty()) {
@@ -1566,18 +1607,51 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
   stats_.insert_ms += ms_since(ti);
   // ---- one slice over the part's occupied lanes
   const auto to = Clock::now();
-  P.occ.clear();
-  for (uint32_t l = P.lo; l < P.hi; l++)
-    if (busy_[l]) P.occ.push_back(l);
+  if (!fresh.empty()) {  // occupied: the lanes still running plus the refilled ones
+    std::vector<uint32_t> occ(P.occ.size() + fresh.size());
+    std::merge(P.occ.begin(), P.occ.end(), fresh.begin(), fresh.end(), occ.begin());
+    P.occ.swap(occ);
+  }
   stats_.occ_ms += ms_since(to);
   if (!P.occ.empty()) {
     const auto tk = Clock::now();
     if (wtfgpu_run_async(ctx_, P.lo, P.hi - P.lo, Slice ? Slice : 4096)) return false;
+    P.pf = pipelined && prefetch_part(P);
     stats_.run_ms += ms_since(tk);
     P.launched = true;
     if (!pipelined && !harvest_part(P, Target, Out, Slots)) return false;
   }
   stats_.total_ms += ms_since(t0);
+  return true;
+}
+
+// The slice's read-back queued behind it on the part's queue (exits, byte and
+// dirty counts, StopWithArgs arguments, the stopped lanes' coverage), into
+// pinned buffers the harvest reads after wtfgpu_run_wait without a device
+// call of its own. false: nothing queued (the harvest reads them itself).
+bool GpuBackend_t::prefetch_part(Part &P) {
+  const uint32_t count = P.hi - P.lo;
+  auto grow = [&](auto *&p, uint64_t bytes) {
+    if (p) return true;
+    void *q = nullptr;
+    if (wtfgpu_host_alloc(ctx_, bytes, &q)) return false;
+    p = (std::remove_reference_t<decltype(p)>)q;
+    return true;
+  };
+  if (P.ex_cap < count) {
+    if (P.ex) wtfgpu_host_free(ctx_, P.ex);
+    P.ex = nullptr;
+    P.ex_cap = 0;
+    if (!grow(P.ex, (uint64_t)count * sizeof(wtfgpu_exit_t))) return false;
+    P.ex_cap = count;
+  }
+  const bool args = !args_results_.empty();
+  if (!grow(P.nb, (uint64_t)count * 8) || !grow(P.dc, (uint64_t)count * 4) || !grow(P.cov_hdr, 16) ||
+      (args && !grow(P.sargs, (uint64_t)count * 48)))
+    return false;
+  if (wtfgpu_prefetch_results(ctx_, P.lo, count, P.ex, P.nb, P.dc, args ? P.sargs : nullptr) != WTFGPU_OK)
+    return false;
+  P.pf_cov = !full_coverage_ && wtfgpu_prefetch_coverage(ctx_, P.lo, count, P.cov_hdr) == WTFGPU_OK;
   return true;
 }
 
@@ -1609,26 +1683,34 @@ bool GpuBackend_t::harvest_part(Part &P, const Target_t &Target, std::vector<Str
     r.rip = 0;
     r.new_coverage.clear();
   }, P.occ.size() >= 8192);
-  if (P.ex_cap < count) {
-    if (P.ex) wtfgpu_host_free(ctx_, P.ex);
-    P.ex = nullptr;
-    P.ex_cap = 0;
-    void *p = nullptr;
-    if (wtfgpu_host_alloc(ctx_, (uint64_t)count * sizeof(wtfgpu_exit_t), &p)) return false;
-    P.ex = (wtfgpu_exit_t *)p;
-    P.ex_cap = count;
+  const bool pf = P.pf;  // the exits (and counts, arguments, coverage count) are in P's pinned buffers
+  P.pf = false;
+  if (!pf) {
+    if (P.ex_cap < count) {
+      if (P.ex) wtfgpu_host_free(ctx_, P.ex);
+      P.ex = nullptr;
+      P.ex_cap = 0;
+      void *p = nullptr;
+      if (wtfgpu_host_alloc(ctx_, (uint64_t)count * sizeof(wtfgpu_exit_t), &p)) return false;
+      P.ex = (wtfgpu_exit_t *)p;
+      P.ex_cap = count;
+    }
+    if (wtfgpu_read_exits(ctx_, first, count, P.ex)) return false;
   }
-  if (wtfgpu_read_exits(ctx_, first, count, P.ex)) return false;
   std::vector<uint8_t> done(count, 0);
   std::vector<uint32_t> hits;
-  if (!classify(P.occ, first, P.ex, done, &lres_, hits)) return false;
+  if (!classify(P.occ, first, P.ex, done, &lres_, hits, pf ? P.sargs : nullptr)) return false;
   stats_.exits_ms += ms_since(te);
   if (!hits.empty() && !service_hits(hits, first, done, Slots, Slots != nullptr)) return false;
   std::vector<uint32_t> finished;
   if (!fill_results(P.occ, first, P.ex, done, &lres_, &finished)) return false;
   if (finished.empty()) return true;
   const auto tc = Clock::now();
-  {  // B_exec = instruction + data bytes, testcase bytes, 2 x 4096 per dirty page
+  if (pf) {  // B_exec = instruction + data bytes, testcase bytes, 2 x 4096 per dirty page
+    uint64_t b = 0;
+    for (uint32_t l : finished) b += P.nb[l - first] + 2ull * 4096 * P.dc[l - first] + tc_bytes_[l];
+    stats_.alg_bytes += b;
+  } else {
     uint32_t lo = finished.front() & ~63u, hi = finished.back() + 1;
     std::vector<uint64_t> nb(hi - lo);
     std::vector<uint32_t> dc(hi - lo);
@@ -1637,7 +1719,7 @@ bool GpuBackend_t::harvest_part(Part &P, const Target_t &Target, std::vector<Str
       for (uint32_t l : finished) stats_.alg_bytes += nb[l - lo] + 2ull * 4096 * dc[l - lo] + tc_bytes_[l];
   }
   stats_.bytes_ms += ms_since(tc);
-  collect_coverage(finished, lres_);
+  collect_coverage(finished, lres_, pf && P.pf_cov ? P.cov_hdr : nullptr);
   const auto tr = Clock::now();
   stats_.coverage_ms += std::chrono::duration<double, std::milli>(tr - tc).count();
   target_restore(Target, finished, Slots);
@@ -1649,6 +1731,14 @@ bool GpuBackend_t::harvest_part(Part &P, const Target_t &Target, std::vector<Str
     const uint32_t l = finished[i];
     Out[base + i] = StreamResult_t{tag_[l], &lres_[l]};
     busy_[l] = 0;  // not runnable until refilled (a finished lane keeps its exit status)
+  }
+  {  // the finished lanes leave the occupied list for the free one (all ascending)
+    std::vector<uint32_t> occ(P.occ.size()), fr(P.free.size() + finished.size());
+    occ.resize(std::set_difference(P.occ.begin(), P.occ.end(), finished.begin(), finished.end(), occ.begin()) -
+               occ.begin());
+    std::merge(P.free.begin(), P.free.end(), finished.begin(), finished.end(), fr.begin());
+    P.occ.swap(occ);
+    P.free.swap(fr);
   }
   stats_.out_ms += ms_since(tout);
   stats_.batches++;

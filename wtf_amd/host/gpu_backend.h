@@ -215,8 +215,11 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   // until every lane has a result
   bool run_lanes(const std::vector<uint32_t> &lanes, std::vector<LaneResult> *out, ModuleSlots *slots,
                  bool per_lane_state);
+  // stop_args: the range's prefetched StopWithArgs arguments (6 per lane from
+  // `first`), else they are read for the lanes that need them
   bool classify(const std::vector<uint32_t> &pending, uint32_t first, const wtfgpu_exit_t *ex,
-                std::vector<uint8_t> &done, std::vector<LaneResult> *out, std::vector<uint32_t> &hits);
+                std::vector<uint8_t> &done, std::vector<LaneResult> *out, std::vector<uint32_t> &hits,
+                const uint64_t *stop_args = nullptr);
   bool fill_results(const std::vector<uint32_t> &lanes, uint32_t first, const wtfgpu_exit_t *ex,
                     const std::vector<uint8_t> &done, std::vector<LaneResult> *out, std::vector<uint32_t> *finished);
   bool stop_prestopped(const std::vector<uint32_t> &lanes);
@@ -230,7 +233,10 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
                     std::vector<uint8_t> &ok);
   void target_restore(const Target_t &Target, const std::vector<uint32_t> &lanes, ModuleSlots *Slots);
   // coverage of finished lanes, attributed in the order given (LastNewCoverage)
-  void collect_coverage(const std::vector<uint32_t> &lanes, std::vector<LaneResult> &res);
+  // (pf_hdr: a part's prefetched entry count; the entries of other lanes
+  // than `lanes` are skipped)
+  void collect_coverage(const std::vector<uint32_t> &lanes, std::vector<LaneResult> &res,
+                        const uint64_t *pf_hdr = nullptr);
   // streaming state: slot occupancy, the caller's tag per lane, results
   std::vector<uint8_t> busy_;
   std::vector<uint64_t> tag_;
@@ -239,6 +245,7 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   std::vector<uint8_t> lres_stale_;  // lres_[l] still holds a handed-out result: reset at the lane's next harvest
   std::vector<uint32_t> cov_lanes_;  // coverage collection buffers (streaming)
   std::vector<uint64_t> cov_rips_;
+  std::vector<uint8_t> cov_want_;  // lanes whose prefetched entries count (collect_coverage)
   std::vector<std::pair<uint32_t, uint64_t>> cov_sorted_;  // the same, sorted by (lane, rip)
   bool cov_ovf_warned_ = false;
   bool want_gprs_ = true;
@@ -250,12 +257,21 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   struct Part {
     uint32_t lo = 0, hi = 0;
     bool launched = false;
-    std::vector<uint32_t> occ;
+    // the part's occupied and free lanes, ascending, kept as lanes finish and
+    // are refilled (the refill takes the lowest free lanes first)
+    std::vector<uint32_t> occ, free;
     wtfgpu_exit_t *ex = nullptr;  // the slice's exit records: pinned (one DMA of 40 B per lane)
     uint64_t ex_cap = 0;
     uint8_t *pin = nullptr;
     uint64_t pin_cap = 0;
+    // the slice's read-back queued behind it (wtfgpu_prefetch_results /
+    // _coverage), pinned: byte and dirty-page counts, StopWithArgs
+    // arguments, the coverage entry count
+    bool pf = false, pf_cov = false;
+    uint64_t *nb = nullptr, *sargs = nullptr, *cov_hdr = nullptr;
+    uint32_t *dc = nullptr;
   };
+  bool prefetch_part(Part &P);
   std::vector<Part> parts_;
   uint8_t *wpin_ = nullptr;  // pinned staging of host-handler writes (flush_lanes; applied synchronously)
   uint64_t wpin_cap_ = 0;

@@ -68,12 +68,14 @@ def idt_page(ksyms: dict) -> bytes:
     return bytes(idt)
 
 
-def compile_images(work_dir: str) -> tuple[str, str]:
+def compile_images(work_dir: str, io: bool = False) -> tuple[str, str]:
+    """io: the HEVD_IO kernel (the I/O manager's IRP path, hevd_kernel.c)."""
     os.makedirs(work_dir, exist_ok=True)
     user = os.path.join(work_dir, "hevd_user.elf")
-    kernel = os.path.join(work_dir, "hevd_kernel.elf")
+    kernel = os.path.join(work_dir, "hevd_kernel_io.elf" if io else "hevd_kernel.elf")
     subprocess.check_call(["gcc", *CFLAGS, "-Wl,-T," + USER_LD, "-Wl,-e,UserMain", "-o", user, USER_SRC])
-    subprocess.check_call(["gcc", *CFLAGS, "-Wl,-T," + KERNEL_LD, "-o", kernel, KERNEL_SRC])
+    subprocess.check_call(["gcc", *CFLAGS, *(["-DHEVD_IO"] if io else []), "-Wl,-T," + KERNEL_LD, "-o", kernel,
+                           KERNEL_SRC])
     return user, kernel
 
 
@@ -84,17 +86,18 @@ def _map_image(sp: AddressSpace, segs, user: bool) -> None:
                      nx=not (flags & 1))
 
 
-def build(state_dir: str, work_dir: str | None = None) -> dict:
+def build(state_dir: str, work_dir: str | None = None, io: bool = False) -> dict:
     """Compiles both images and writes mem.dmp / regs.json / symbol-store.json
-    into state_dir. Returns {name: address} of the guest symbols."""
-    sp, st, symbols, syms = build_space(work_dir or state_dir)
+    into state_dir. Returns {name: address} of the guest symbols. io: the
+    HEVD_IO kernel (wtf_amd/tools/hevd_io.py)."""
+    sp, st, symbols, syms = build_space(work_dir or state_dir, io)
     write_snapshot(state_dir, sp, st, symbols)
     return syms
 
 
-def build_space(work_dir: str):
+def build_space(work_dir: str, io: bool = False):
     """(address space, CPU state, symbol store, guest symbols) of the snapshot."""
-    user_elf, kernel_elf = compile_images(work_dir)
+    user_elf, kernel_elf = compile_images(work_dir, io)
     usegs, usyms = _elf(user_elf)
     ksegs, ksyms = _elf(kernel_elf)
     sp = AddressSpace()
@@ -131,7 +134,7 @@ def build_space(work_dir: str):
         "nt!KiPageFault": ksyms["KiPageFault"],
         "nt!KiGeneralProtectionFault": ksyms["KiGeneralProtectionFault"],
         "nt!KiSystemCall64": ksyms["KiSystemCall64"],
-        "HEVD!IrpDeviceIoCtlHandler": ksyms["NtDeviceIoControlFile"],
+        "HEVD!IrpDeviceIoCtlHandler": ksyms["HevdIrpDeviceIoCtlHandler" if io else "NtDeviceIoControlFile"],
         "kernelbase!DeviceIoControl": usyms["DeviceIoControl"],
     }
     syms = {**{f"user:{k}": v for k, v in usyms.items()}, **{f"kernel:{k}": v for k, v in ksyms.items()}}
