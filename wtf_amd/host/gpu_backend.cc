@@ -83,7 +83,7 @@ bool GpuBackend_t::Initialize(const Options_t &Opts, const CpuState_t &CpuState)
   if (wtfgpu_load_pool(ctx_, gpfns.data(), blob.data(), gpfns.size())) return false;
   nlanes_ = std::max<uint32_t>(Opts.GpuLanes, 1);
   overlay_pages_ = std::max<uint32_t>(Opts.GpuOverlayPages, 1);
-  if (wtfgpu_alloc_lanes(ctx_, nlanes_, overlay_pages_, 1024)) return false;
+  if (wtfgpu_alloc_lanes(ctx_, nlanes_, overlay_pages_, Opts.GpuCoverageSet)) return false;
   views_.clear();
   views_.resize(nlanes_);
   arenas_.resize(HostPool::Get().Threads() + 1);

@@ -302,6 +302,7 @@ bool LoadTarget(const RunnerOptions &O, Options_t &Opts, CpuState_t &State) {
   Opts.GpuDevice = O.device;
   Opts.GpuLanes = O.lanes;
   Opts.GpuOverlayPages = O.overlay_pages;
+  if (O.full_coverage) Opts.GpuCoverageSet = 8192;
   Opts.Fuzz.Seed = (uint32_t)O.seed;
   if (!LoadCpuStateFromJSON(State, Opts.CpuStatePath)) {
     printf("Failed to load the CPU state from %s\n", Opts.CpuStatePath.string().c_str());

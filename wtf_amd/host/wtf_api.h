@@ -193,6 +193,10 @@ struct Options_t {
   int GpuDevice = 0;
   uint32_t GpuLanes = 1;
   uint32_t GpuOverlayPages = 32;
+  // per-lane new-coverage set entries (wtfgpu_alloc_lanes; 3/4 usable): a
+  // testcase's rips not yet in the aggregate; --full-coverage (parity mode,
+  // every rip of the testcase) takes the larger set
+  uint32_t GpuCoverageSet = 2048;
 };
 
 // ------------------------------------------------------------------ backend
