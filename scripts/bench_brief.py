@@ -22,11 +22,15 @@ def main(path):
                                               "target_restore_ms", "insert_ms", "restore_ms", "restore_dev_ms",
                                               "module_ms", "upload_ms", "up_prep_ms", "up_feed_ms", "fresh_ms",
                                               "occ_ms", "prepared"]))
-    h = d.get("hevd")
-    if h:
+    for leg in ("hevd", "hevd_bare"):
+        h = d.get(leg)
+        if not h:
+            continue
         hb = h["backend"]
         w = h["wall_s"] * 1e3
-        print(f"hevd value={h['value'] / 1e6:.3f}M busy={h['kernel_busy_frac']:.2f} errors={h['errors']} "
+        print(f"{leg} value={h['value'] / 1e6:.3f}M busy={h['kernel_busy_frac']:.2f} errors={h['errors']} "
+              f"instr/exec={h['instr_per_exec']:.0f} crash={h.get('crash_share', 0):.3f} "
+              f"lpws={h['lanes_per_wave_step']:.1f} "
               f"frac={h['roofline']['frac']:.4f} launch={h['roofline']['avg_launch_ms']:.3f}ms "
               f"insert={hb['insert_ms'] / w:.2f} harvest={hb['harvest_ms'] / w:.2f} "
               f"account={h['node']['account_ms'] / w:.2f} (fractions of wall)")

@@ -392,7 +392,7 @@ __attribute__((noipa)) static u32 TriggerParseRecords(const u8 *User, u64 Size) 
  * control interface) */
 static u64 CmdTable[64];
 typedef u32 (*CmdFn)(u32 A, u32 B, u32 C);
-#define CMD(n, body) static u32 Cmd##n(u32 A, u32 B, u32 C) { (void)A, (void)B, (void)C; body }
+#define CMD(n, ...) static u32 Cmd##n(u32 A, u32 B, u32 C) { (void)A, (void)B, (void)C; __VA_ARGS__ }
 CMD(0, { CmdTable[A & 63] = B | C << 8; return 0; })
 CMD(1, { return (u32)CmdTable[A & 63]; })
 CMD(2, { CmdTable[A & 63] += CmdTable[B & 63]; return 0; })
@@ -409,8 +409,25 @@ CMD(12, { if (A >= 64 || B > 64 - A) return 1; for (u32 i = 0; i < B; i++) CmdTa
 CMD(13, { u32 N = 0; for (u32 i = 0; i < 64; i++) N += CmdTable[i] == (u64)(B | C << 8); CmdTable[A & 63] = N; return 0; })
 CMD(14, { CmdTable[A & 63] = ~CmdTable[B & 63]; return 0; })
 CMD(15, { CmdTable[A & 63] &= CmdTable[B & 63] | C; return 0; })
-static const CmdFn CmdFns[16] = {Cmd0, Cmd1, Cmd2, Cmd3, Cmd4, Cmd5, Cmd6, Cmd7,
-                                 Cmd8, Cmd9, Cmd10, Cmd11, Cmd12, Cmd13, Cmd14, Cmd15};
+CMD(16, { if (A >= 64) return 1; u64 V = CmdTable[A], R = 0; while (V) { R += V & 1; V >>= 1; } CmdTable[B & 63] = R; return 0; })
+CMD(17, { if (A >= 64 || B >= 64) return 1; CmdTable[A] = CmdTable[A] > CmdTable[B] ? CmdTable[A] - CmdTable[B] : CmdTable[B] - CmdTable[A]; return 0; })
+CMD(18, { u64 H = 0xCBF29CE484222325ull; for (u32 i = 0; i < (A & 63); i++) H = (H ^ CmdTable[i]) * 0x100000001B3ull; CmdTable[B & 63] = H; return 0; })
+CMD(19, { if (C > 63) return 1; CmdTable[A & 63] = (CmdTable[A & 63] >> C) & ((1ull << (B & 63)) - 1); return 0; })
+CMD(20, { if (A >= 64 || B >= 64 || A > B) return 1; for (u32 i = A, j = B; i < j; i++, j--) { u64 T = CmdTable[i]; CmdTable[i] = CmdTable[j]; CmdTable[j] = T; } return 0; })
+CMD(21, { u32 Best = 0; for (u32 i = 1; i < 64; i++) if (CmdTable[i] > CmdTable[Best]) Best = i; return Best == (A & 63) ? 2 : 0; })
+CMD(22, { if (!C) return 1; CmdTable[A & 63] = CmdTable[B & 63] * C / (C + 1); return 0; })
+CMD(23, { u64 V = CmdTable[A & 63]; u32 D = 0; do { D++; V /= 10; } while (V); CmdTable[B & 63] = D; return 0; })
+CMD(24, { if (A >= 64 || B > 64 - A || C >= 64) return 1; u64 S = 0; for (u32 i = 0; i < B; i++) S ^= CmdTable[A + i] << (i & 7); CmdTable[C] = S; return 0; })
+CMD(25, { if (A >= 64) return 1; CmdTable[A] = CmdTable[A] ? 63 - __builtin_clzll(CmdTable[A]) : 64; return 0; })
+CMD(26, { if (B >= 8) return 1; CmdTable[A & 63] |= (u64)C << (8 * B); return 0; })
+CMD(27, { if (A >= 64 || B >= 64) return 1; return CmdTable[A] == CmdTable[B] ? 2 : CmdTable[A] & CmdTable[B] ? 3 : 0; })
+CMD(28, { u32 N = 0; for (u32 i = 0; i < 64; i++) if ((CmdTable[i] & 0xff) == A) N++; CmdTable[B & 63] = N; return N > C ? 2 : 0; })
+CMD(29, { if (A >= 64) return 1; CmdTable[A] = (CmdTable[A] * 6364136223846793005ull + 1442695040888963407ull) >> (C & 31); return 0; })
+CMD(30, { for (u32 i = 0; i < 64; i++) CmdTable[i] = (CmdTable[i] + A) ^ B; return 0; })
+CMD(31, { if (A >= 64 || B >= 64 || C >= 64) return 1; CmdTable[C] = CmdTable[A] < CmdTable[B] ? CmdTable[A] : CmdTable[B]; return 0; })
+static const CmdFn CmdFns[32] = {Cmd0, Cmd1, Cmd2, Cmd3, Cmd4, Cmd5, Cmd6, Cmd7, Cmd8, Cmd9, Cmd10,
+                                 Cmd11, Cmd12, Cmd13, Cmd14, Cmd15, Cmd16, Cmd17, Cmd18, Cmd19, Cmd20, Cmd21,
+                                 Cmd22, Cmd23, Cmd24, Cmd25, Cmd26, Cmd27, Cmd28, Cmd29, Cmd30, Cmd31};
 __attribute__((noipa)) static u32 TriggerCommands(const u8 *User, u64 Size) {
   u8 Kernel[256];
   if (Size > sizeof(Kernel) || (Size & 3)) return STATUS_INVALID_PARAMETER;
@@ -427,7 +444,7 @@ __attribute__((noipa)) static u32 TriggerCommands(const u8 *User, u64 Size) {
   u64 Acc = 0;
   for (u64 i = 0; i < Size; i += 4) {
     const u8 Op = Kernel[i];
-    if (Op >= 16) return STATUS_INVALID_PARAMETER;
+    if (Op >= 32) return STATUS_INVALID_PARAMETER;
     const u32 R = CmdFns[Op](Kernel[i + 1], Kernel[i + 2], Kernel[i + 3]);
     if (R == 1) return STATUS_INVALID_PARAMETER;
     Acc = Acc * 3 + R;
@@ -670,8 +687,46 @@ static void KeSetEvent(struct KEvent *E) {
   if (E->WaitListHead.Flink != &E->WaitListHead) ((void (*)(void))SwapContext)(); /* a waiter runs */
 }
 
-/* completion routines from the current location up, the status block to the
- * caller, the event, the IRP freed */
+/* the thread's kernel APC queue: IofCompleteRequest's second stage runs as a
+ * special kernel APC in the requesting thread (KeInsertQueueApc, delivered by
+ * KiDeliverApc when the IRQL drops) */
+struct KApc {
+  struct ListEntry Entry;
+  void (*Routine)(struct KApc *);
+  void *Arg;
+  u32 Inserted;
+};
+static struct ListEntry ApcListHead = {&ApcListHead, &ApcListHead};
+static u32 ApcPending;
+static void KeInsertQueueApc(struct KApc *A) {
+  if (A->Inserted) return;
+  A->Inserted = 1;
+  InsertTailList(&ApcListHead, &A->Entry);
+  ApcPending = 1;
+}
+__attribute__((noipa)) static void KiDeliverApc(void) {
+  while (ApcListHead.Flink != &ApcListHead) {
+    struct ListEntry *E = ApcListHead.Flink;
+    RemoveEntryList(E);
+    struct KApc *A = (struct KApc *)E;
+    A->Inserted = 0;
+    A->Routine(A);
+  }
+  ApcPending = 0;
+}
+/* the second stage (IopCompleteRequest): the status block to the caller, the
+ * event, the IRP off the thread's list and freed, the file object dereferenced */
+static void IopCompleteRequest(struct KApc *A) {
+  struct Irp *Irp = A->Arg;
+  *Irp->UserIosb = Irp->IoStatus;
+  KeSetEvent(&FileEvent);
+  RemoveEntryList(&Irp->ThreadListEntry);
+  CurrentThread.KernelApcDisable--;
+  ObDereferenceObject(Irp->Stack[Irp->StackCount - 1].FileObject);
+  IoFreeIrp(Irp);
+}
+static struct KApc CompletionApc;
+/* completion routines from the current location up, then the APC */
 __attribute__((noipa)) static void IofCompleteRequest(struct Irp *Irp) {
   while (Irp->CurrentLocation <= Irp->StackCount) {
     struct IoStackLocation *Sp = Irp->CurrentStackLocation;
@@ -682,12 +737,9 @@ __attribute__((noipa)) static void IofCompleteRequest(struct Irp *Irp) {
       Sp->CompletionRoutine(Irp->CurrentLocation <= Irp->StackCount ? Irp->CurrentStackLocation->DeviceObject : 0,
                             Irp, Sp->Context);
   }
-  *Irp->UserIosb = Irp->IoStatus;
-  KeSetEvent(&FileEvent);
-  RemoveEntryList(&Irp->ThreadListEntry);
-  CurrentThread.KernelApcDisable--;
-  ObDereferenceObject(Irp->Stack[Irp->StackCount - 1].FileObject);
-  IoFreeIrp(Irp);
+  CompletionApc.Routine = IopCompleteRequest;
+  CompletionApc.Arg = Irp;
+  KeInsertQueueApc(&CompletionApc);
 }
 
 static u32 IopDefaultDispatch(struct DeviceObject *Dev, struct Irp *Irp) {
@@ -719,11 +771,48 @@ static u32 FilterDispatch(struct DeviceObject *Dev, struct Irp *Irp) {
   return IofCallDriver(Dev->LowerDevice, Irp);
 }
 
+/* WPP-style request tracing: the IOCTL and a hex dump of the buffer's head go
+ * into the driver's circular trace buffer (what a driver's WPP / ETW provider
+ * does for every request, without DbgPrintEx) */
+static struct {
+  u64 Sequence;
+  u32 Head;
+  char Data[8192];
+} TraceBuffer;
+static void TracePut(char C) {
+  TraceBuffer.Data[TraceBuffer.Head] = C;
+  TraceBuffer.Head = (TraceBuffer.Head + 1) & 8191;
+}
+__attribute__((noipa)) static void WppTraceRequest(u32 Code, const u8 *User, u64 Size) {
+  static const char Hex[] = "0123456789abcdef";
+  TraceBuffer.Sequence++;
+  for (int i = 28; i >= 0; i -= 4) TracePut(Hex[(Code >> i) & 15]);
+  TracePut(' ');
+  const u64 N = Size < 192 ? Size : 192;
+  KTRY T;
+  TRY(T) {
+    ProbeForRead(User, N, 1);
+    for (u64 i = 0; i < N; i++) {
+      const u8 B = User[i];
+      TracePut(Hex[B >> 4]);
+      TracePut(Hex[B & 15]);
+      if ((i & 15) == 15) TracePut('\n');
+    }
+    END_TRY();
+  }
+  EXCEPT {
+    END_TRY();
+    TracePut('!');
+  }
+  TracePut('\n');
+}
+
 /* HEVD's IRP_MJ_DEVICE_CONTROL handler: the request from its stack location */
 static u32 HevdIrpDeviceIoCtlHandler(struct DeviceObject *Dev, struct Irp *Irp) {
   (void)Dev;
   struct IoStackLocation *Sp = Irp->CurrentStackLocation;
   LastInformation = 0;
+  WppTraceRequest(Sp->Parameters_IoControlCode, Sp->Type3InputBuffer, Sp->InputBufferLength);
   const u32 Status = HevdDispatchIoctl(Sp->Parameters_IoControlCode, Sp->Type3InputBuffer, Sp->InputBufferLength);
   Irp->IoStatus.Status = Status;
   Irp->IoStatus.Information = LastInformation;
@@ -759,6 +848,7 @@ __attribute__((noipa, used)) u64 NtDeviceIoControlFile(u64 Handle, u32 Code, con
   Sp->Type3InputBuffer = User;
   Irp->Stack[Top->StackSize - 1].FileObject = File;
   IofCallDriver(Top, Irp);
+  if (ApcPending) KiDeliverApc(); /* KeLowerIrql / KiCheckForKernelApcDelivery */
   return Iosb.Status;
 }
 #endif
@@ -779,9 +869,15 @@ __asm__(".globl KiSystemCall64\n"
         "  push %gs:0x10\n"
         "  push %rax\n  push %rdx\n  push %r8\n  push %r9\n  push %r10\n  push %rbp\n"
         "  mov %rsp, %rbp\n"
-        "  sub $0x28, %rsp\n"        /* home space; rsp = 8 mod 16 at the callee's entry */
+        /* the volatile XMM registers, as KiSystemCall64 saves them in KTRAP_FRAME */
+        "  sub $0x68, %rsp\n"
+        "  movdqu %xmm0, 0x00(%rsp)\n  movdqu %xmm1, 0x10(%rsp)\n  movdqu %xmm2, 0x20(%rsp)\n"
+        "  movdqu %xmm3, 0x30(%rsp)\n  movdqu %xmm4, 0x40(%rsp)\n  movdqu %xmm5, 0x50(%rsp)\n"
+        "  sub $0x20, %rsp\n"        /* home space; rsp = 8 mod 16 at the callee's entry */
         "  mov %r10, %rcx\n"
         "  call NtDeviceIoControlFile\n"
+        "  movdqu 0x20(%rsp), %xmm0\n  movdqu 0x30(%rsp), %xmm1\n  movdqu 0x40(%rsp), %xmm2\n"
+        "  movdqu 0x50(%rsp), %xmm3\n  movdqu 0x60(%rsp), %xmm4\n  movdqu 0x70(%rsp), %xmm5\n"
         "  mov %rbp, %rsp\n"
         "  pop %rbp\n  pop %r10\n  pop %r9\n  pop %r8\n  pop %rdx\n"
         "  add $16, %rsp\n"          /* rax (the status is the return value) and the saved rsp slot */
