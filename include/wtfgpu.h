@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define WTFGPU_ABI_VERSION 3
+#define WTFGPU_ABI_VERSION 4
 #define WTFGPU_PAGE_SIZE 4096u
 
 /* Status codes. */
@@ -127,6 +127,13 @@ typedef struct wtfgpu_regs {
   uint16_t fpse[8];     /* sign / exponent words of ST(0..7) (ABI 3): CpuState_t::Fpst
                            carries the 64-bit significands only (globals.h:1067), so a
                            snapshot loads these as 0 */
+  /* AVX-512 state (ABI 4; CpuState_t::Zmm[32], globals.h:1061-1062, bochscpu.hpp
+   * State::zmm): bits 511:256 of zmm0..15, zmm16..31 whole, and the opmask
+   * registers k0..k7 (bochs keeps these in its CPU; CpuState_t has none, so a
+   * restore zeroes them). */
+  uint64_t zmmh[16][4];   /* bits 511:256 of zmm0..15 (CpuState_t::Zmm[i].Q[4..7]) */
+  uint64_t zmm_hi[16][8]; /* zmm16..31 (CpuState_t::Zmm[16..31]) */
+  uint64_t k[8];          /* k0..k7 */
 } wtfgpu_regs_t;
 
 /* Why a lane stopped. */

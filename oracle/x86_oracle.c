@@ -1809,10 +1809,13 @@ static y256 yreg(orc_machine *m, u32 r) {
   memcpy(v.h.b, m->r.ymmh[r & 15], 16);
   return v;
 }
+/* a VEX destination: bits 255:128 zeroed by VEX.128, bits 511:256 by every
+ * VEX write (MAXVL 512, U47) */
 static void yput(orc_machine *m, u32 r, y256 v, int l256) {
   memcpy(m->r.xmm[r & 15], v.l.b, 16);
   if (l256) memcpy(m->r.ymmh[r & 15], v.h.b, 16);
   else memset(m->r.ymmh[r & 15], 0, 16);
+  memset(m->r.zmmh[r & 15], 0, 32);
 }
 
 #include "x86_oracle_fp.inc" /* SSE / AVX floating point (U39 / U40) */
@@ -2061,8 +2064,9 @@ static int exec_vex(orc_machine *m, insn *d) {
     return X_FAULT;
   }
   if (map == 1 && op == 0x77) { /* vzeroupper / vzeroall */
-    for (int i = 0; i < 16; i++) {
+    for (int i = 0; i < 16; i++) { /* zmm0..15 bits 511:128; zmm16..31 kept */
       memset(m->r.ymmh[i], 0, 16);
+      memset(m->r.zmmh[i], 0, 32);
       if (l256) memset(m->r.xmm[i], 0, 16);
     }
     return X_OK;

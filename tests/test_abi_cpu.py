@@ -18,7 +18,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_loader():
     lib = load_hip_library()
-    assert lib.wtfgpu_abi_version() == 3
+    assert lib.wtfgpu_abi_version() == 4
 
 
 def test_struct_layouts_match_header(tmp_path):

@@ -87,9 +87,13 @@ def test_cpuid_table(space):
     r = _one(space, "cpuid", r8=0, r9=0)
     assert r["gpr"][0] == 0xD and struct.pack("<III", r["gpr"][3], r["gpr"][2], r["gpr"][1]) == b"GenuineIntel"
     r = _one(space, "cpuid", r8=0xD, r9=0)
-    assert r["gpr"][0] == 0x1F and r["gpr"][3] == 1088      # xcr0 = 0x1f
+    assert r["gpr"][0] == 0xFF and r["gpr"][1] == 2688      # components 0..7 (U47): all of them
+    assert r["gpr"][3] == 1088                               # xcr0 = 0x1f: up to the MPX pair
+    r = _one(space, "cpuid", r8=0xD, r9=6)
+    assert (r["gpr"][0], r["gpr"][3]) == (512, 1152)         # ZMM_Hi256: size, offset
     r = _one(space, "cpuid", r8=7, r9=0)
     assert r["gpr"][3] & (1 << 5)                            # AVX2
+    assert r["gpr"][3] >> 30 == 3 and r["gpr"][3] & (1 << 16)  # AVX512F / BW / VL
 
 
 def test_cmpxchg16b(space):

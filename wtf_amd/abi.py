@@ -37,6 +37,7 @@ class Regs(C.Structure):
         ("fpcw", C.c_uint16), ("fpsw", C.c_uint16), ("fptw", C.c_uint16), ("fpop", C.c_uint16),
         ("pad0", C.c_uint32), ("fpst", C.c_uint64 * 8), ("xmm", (C.c_uint64 * 2) * 16),
         ("ymmh", (C.c_uint64 * 2) * 16), ("fpse", C.c_uint16 * 8),
+        ("zmmh", (C.c_uint64 * 4) * 16), ("zmm_hi", (C.c_uint64 * 8) * 16), ("k", C.c_uint64 * 8),
     ]
 
 

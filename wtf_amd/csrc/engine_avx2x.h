@@ -194,6 +194,7 @@ __device__ __noinline__ int ax_gather(const Dev &P, Lane &L, const UOp &u, u32 c
     yset(m2, j, ew, 0);
     F.xmm[dst][0] = d.l.lo, F.xmm[dst][1] = d.l.hi, F.ymmh[dst][0] = d.h.lo, F.ymmh[dst][1] = d.h.hi;
     F.xmm[msk][0] = m2.l.lo, F.xmm[msk][1] = m2.l.hi, F.ymmh[msk][0] = m2.h.lo, F.ymmh[msk][1] = m2.h.hi;
+    for (u32 q = 0; q < 4; q++) F.zmmh[dst][q] = F.zmmh[msk][q] = 0;  // VEX: bits 511:256 (U47)
   }
   // completion: bits above the n elements of the destination zeroed, the mask all zero
   Y256 d = ymm_get(P, L, dst);

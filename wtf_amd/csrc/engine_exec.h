@@ -20,17 +20,20 @@ struct Lane {
   u32 miss, miss_acc, flush, pend;  // pend: bytes accessed by the attempt in flight
   u32 nodeliver;                    // this fault could not be delivered through the guest IDT
   u32 cgen, ccnt;                   // coverage set: generation, live entries
-  u32 simd;                         // bit 0: SSE usable, bit 1: AVX usable (simd_bits)
+  u32 simd;                         // bit 0: SSE usable, bit 1: AVX usable, bit 2: AVX-512 state on (simd_bits)
 };
 
 // Which vector state the lane's cr0 / cr4 / xcr0 enable without a fault: bit 0
 // legacy SSE (CR0.EM = 0, CR0.TS = 0, CR4.OSFXSR), bit 1 VEX (CR4.OSXSAVE,
 // XCR0[2:1] = 11, CR0.TS = 0). The fast path runs vector moves only then.
+// Bit 2: EVEX usable (CR4.OSXSAVE, XCR0[7:5] = 111 with [2:1] = 11, CR0.TS = 0;
+// U47): a VEX write then also zeroes the register's bits 511:256.
 __device__ __forceinline__ u32 simd_bits(u64 cr0, u64 cr4, u64 xcr0) {
   const bool ts = (cr0 >> 3) & 1;
   const u32 sse = !((cr0 >> 2) & 1) && !ts && ((cr4 >> 9) & 1);
   const u32 avx = !ts && ((cr4 >> 18) & 1) && (xcr0 & 6) == 6;
-  return sse | avx << 1;
+  const u32 z = avx && (xcr0 & 0xe0) == 0xe0;
+  return sse | avx << 1 | z << 2;
 }
 
 // GPR r of the lane. r is wave-uniform and the halves live in two u32 arrays

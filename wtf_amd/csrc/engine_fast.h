@@ -361,6 +361,8 @@ __device__ __forceinline__ int fast_vec(wtfgpu_regs_t *full, Lane &L, const FOp 
   wtfgpu_regs_t &F = full[L.lane];
   if (op == FO_VZU) {
     for (u32 i = 0; i < 16; i++) F.ymmh[i][0] = F.ymmh[i][1] = 0;
+    if (L.simd & 4)
+      for (u32 i = 0; i < 16; i++) F.zmmh[i][0] = F.zmmh[i][1] = F.zmmh[i][2] = F.zmmh[i][3] = 0;
     return X_OK;
   }
   const u32 ra = fo_ra(f) & 15;
@@ -393,6 +395,7 @@ __device__ __forceinline__ int fast_vec(wtfgpu_regs_t *full, Lane &L, const FOp 
     F.ymmh[ra][0] = v[2];
     F.ymmh[ra][1] = v[3];
   }
+  if ((sub & 2) && (L.simd & 4)) F.zmmh[ra][0] = F.zmmh[ra][1] = F.zmmh[ra][2] = F.zmmh[ra][3] = 0;  // MAXVL 512
   return X_OK;
 }
 

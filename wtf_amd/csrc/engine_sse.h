@@ -273,13 +273,15 @@ __device__ __forceinline__ Y256 ymm_get(const Dev &P, const Lane &L, u32 r) {
   const wtfgpu_regs_t &F = P.full[L.lane];
   return Y256{X128{F.xmm[r & 15][0], F.xmm[r & 15][1]}, X128{F.ymmh[r & 15][0], F.ymmh[r & 15][1]}};
 }
-// a VEX destination: VEX.128 zeroes bits 255:128 (VLMAX)
+// a VEX destination: VEX.128 zeroes bits 255:128, and every VEX write bits
+// 511:256 (MAXVL = 512 on an AVX-512 machine, U47)
 __device__ __forceinline__ void ymm_put(const Dev &P, const Lane &L, u32 r, Y256 v, u32 l256) {
   wtfgpu_regs_t &F = P.full[L.lane];
   F.xmm[r & 15][0] = v.l.lo;
   F.xmm[r & 15][1] = v.l.hi;
   F.ymmh[r & 15][0] = l256 ? v.h.lo : 0;
   F.ymmh[r & 15][1] = l256 ? v.h.hi : 0;
+  for (u32 q = 0; q < 4; q++) F.zmmh[r & 15][q] = 0;
 }
 __device__ __forceinline__ bool yload(Lane &L, u64 ea, u32 n, Y256 &v) {
   v.h = X128{0, 0};
@@ -789,8 +791,9 @@ __device__ __noinline__ int vex_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
   }
   if (map == 1 && c == 0x77) {  // vzeroupper / vzeroall
     wtfgpu_regs_t &F = P.full[L.lane];
-    for (u32 i = 0; i < 16; i++) {
+    for (u32 i = 0; i < 16; i++) {  // zmm0..15 bits 511:128 (all of them: vzeroall); zmm16..31 kept
       F.ymmh[i][0] = F.ymmh[i][1] = 0;
+      for (u32 q = 0; q < 4; q++) F.zmmh[i][q] = 0;
       if (l256) F.xmm[i][0] = F.xmm[i][1] = 0;
     }
     return X_OK;

@@ -18,7 +18,15 @@
 namespace wtfgpu_dev {
 
 constexpr u32 VEC_DB = 1, VEC_NM = 7, VEC_NP = 11, VEC_MF = 16;
-constexpr u64 XS_SUPPORTED = 0x1f;  // x87, SSE, AVX, BNDREGS, BNDCSR
+constexpr u64 XS_SUPPORTED = 0xff;  // x87, SSE, AVX, BNDREGS, BNDCSR, opmask, ZMM_Hi256, Hi16_ZMM (U33, U47)
+// components 2..7: size and standard-format offset (CPUID.(0xd, i)); the
+// compacted format packs the requested ones in order (none is 64-byte aligned)
+__host__ __device__ constexpr u32 xs_size(u32 c) {
+  return c == 2 ? 256 : c == 3 || c == 4 || c == 5 ? 64 : c == 6 ? 512 : c == 7 ? 1024 : 0;
+}
+__host__ __device__ constexpr u32 xs_offset(u32 c) {
+  return c == 2 ? 576 : c == 3 ? 960 : c == 4 ? 1024 : c == 5 ? 1088 : c == 6 ? 1152 : c == 7 ? 1664 : 0;
+}
 
 __device__ __forceinline__ u32 lane_iopl(const Lane &L) { return (u32)(L.rflags >> 12) & 3; }
 
@@ -134,22 +142,24 @@ __device__ __noinline__ void cpuid_leaf(u64 cr4, u64 xcr0, u32 leaf, u32 sub, u3
            (1u << 23) | (1u << 25) | (1u << 26) | (osxsave << 27) | (1u << 28) | (1u << 29) | (1u << 30);
     r[3] = 0x078bfbfd;
   } else if (leaf == 7) {
-    if (sub == 0)  // FSGSBASE BMI1 AVX2 BMI2 ERMS ADX SHA
-      r[1] = (1u << 0) | (1u << 3) | (1u << 5) | (1u << 8) | (1u << 9) | (1u << 19) | (1u << 29);
+    if (sub == 0)  // FSGSBASE BMI1 AVX2 BMI2 ERMS AVX512F ADX SHA AVX512BW AVX512VL (U47)
+      r[1] = (1u << 0) | (1u << 3) | (1u << 5) | (1u << 8) | (1u << 9) | (1u << 16) | (1u << 19) | (1u << 29) |
+             (1u << 30) | (1u << 31);
   } else if (leaf == 0xd) {
     if (sub == 0) {
-      r[0] = 0x1f;
-      r[1] = (xcr0 & 16) ? 1088 : (xcr0 & 8) ? 1024 : (xcr0 & 4) ? 832 : 576;
-      r[2] = 1088;
+      r[0] = 0xff;
+      r[1] = 576;
+      for (u32 c = 2; c <= 7; c++)
+        if ((xcr0 >> c) & 1) r[1] = xs_offset(c) + xs_size(c);
+      r[2] = 2688;
     } else if (sub == 1) {
       r[0] = 1u | 2u | 8u;
-      r[1] = 576 + ((xcr0 & 4) ? 256 : 0) + ((xcr0 & 8) ? 64 : 0) + ((xcr0 & 16) ? 64 : 0);
-    } else if (sub == 2) {
-      r[0] = 256;
       r[1] = 576;
-    } else if (sub == 3 || sub == 4) {
-      r[0] = 64;
-      r[1] = sub == 3 ? 960 : 1024;
+      for (u32 c = 2; c <= 7; c++)
+        if ((xcr0 >> c) & 1) r[1] += xs_size(c);
+    } else if (sub >= 2 && sub <= 7) {
+      r[0] = xs_size(sub);
+      r[1] = xs_offset(sub);
     }
   } else if (leaf == 0x80000000u) {
     r[0] = 0x80000008u;
@@ -307,8 +317,15 @@ __device__ __noinline__ bool x87_load(const Dev &P, Lane &L, u64 va, bool commit
 
 enum : u32 { XS_SAVE, XS_SAVEOPT, XS_SAVEC, XS_SAVES, XS_RSTOR, XS_RSTORS };
 __device__ __forceinline__ u32 xs_extent(u64 rfbm, bool compact) {
-  if (compact) return 576 + ((rfbm & 4) ? 256 : 0) + ((rfbm & 8) ? 64 : 0) + ((rfbm & 16) ? 64 : 0);
-  return (rfbm & 16) ? 1088 : (rfbm & 8) ? 1024 : (rfbm & 4) ? 832 : 576;
+  u32 n = 576;
+  for (u32 c = 2; c <= 7; c++)
+    if ((rfbm >> c) & 1) n = compact ? n + xs_size(c) : xs_offset(c) + xs_size(c);
+  return n;
+}
+// the AVX-512 components' 8-byte words: 5 = k0..k7, 6 = zmm0..15 bits
+// 511:256, 7 = zmm16..31
+__device__ __forceinline__ u64 &xs_word(wtfgpu_regs_t &F, u32 c, u32 i) {
+  return c == 5 ? F.k[i] : c == 6 ? F.zmmh[i >> 2][i & 3] : F.zmm_hi[i >> 3][i & 7];
 }
 
 __device__ __noinline__ int xsave_op(const Dev &P, Lane &L, u32 kind, u64 va) {
@@ -324,7 +341,7 @@ __device__ __noinline__ int xsave_op(const Dev &P, Lane &L, u32 kind, u64 va) {
     if (!span_w(L, va, xs_extent(rfbm, compact))) return X_FAULT;
     u64 bv = 0;
     if (!compact && !vread(L, va + 512, 8, bv)) return X_FAULT;
-    const u64 inuse = rfbm & 7;
+    const u64 inuse = rfbm & 0xe7;
     if ((rfbm & 1) && (!legacy_store(P, L, va, 0, 24) || !legacy_store(P, L, va, 32, 128))) return X_FAULT;
     if ((rfbm & 6) && !legacy_store(P, L, va, 24, 8)) return X_FAULT;
     if ((rfbm & 2) && !legacy_store(P, L, va, 160, 256)) return X_FAULT;
@@ -339,12 +356,12 @@ __device__ __noinline__ int xsave_op(const Dev &P, Lane &L, u32 kind, u64 va) {
         if (!vwrite(L, va + off + 8 * i, 8, F.ymmh[i >> 1][i & 1])) return X_FAULT;
       off += 256;
     }
-    for (u32 c = 3; c <= 4; c++)
+    for (u32 c = 3; c <= 7; c++)
       if ((rfbm >> c) & 1) {
-        const u64 at = compact ? off : (c == 3 ? 960 : 1024);
-        for (u32 i = 0; i < 8; i++)
-          if (!vwrite(L, va + at + 8 * i, 8, 0)) return X_FAULT;
-        off += 64;
+        const u64 at = compact ? off : xs_offset(c);
+        for (u32 i = 0; i < xs_size(c) / 8; i++)
+          if (!vwrite(L, va + at + 8 * i, 8, c >= 5 ? xs_word(F, c, i) : 0)) return X_FAULT;
+        off += xs_size(c);
       }
     return X_OK;
   }
@@ -370,10 +387,17 @@ __device__ __noinline__ int xsave_op(const Dev &P, Lane &L, u32 kind, u64 va) {
   }
   const bool load_mx = compact ? ((rfbm & 2) && (xbv & 2)) : ((rfbm & 6) != 0);
   if (load_mx && (mx & ~(u64)mxcsr_mask_of(F))) return fault_x(L, WTFGPU_VEC_GP, 0);
-  if ((rfbm & 4) && (xbv & 4)) {
-    for (u32 o = 0; o < 256; o += 8) {
-      u64 q;
-      if (!vread(L, va + 576 + o, 8, q)) return X_FAULT;
+  {  // the extended components read before any commit (compacted: packed in order)
+    u32 off = 576;
+    for (u32 c = 2; c <= 7; c++) {
+      if (compact && !((xcomp >> c) & 1)) continue;
+      const u32 at = compact ? off : xs_offset(c);
+      off += xs_size(c);
+      if (c == 3 || c == 4 || !((rfbm >> c) & 1) || !((xbv >> c) & 1)) continue;
+      for (u32 o = 0; o < xs_size(c); o += 8) {
+        u64 q;
+        if (!vread(L, va + at + o, 8, q)) return X_FAULT;
+      }
     }
   }
   // commit: every byte above was read without a miss, so the reads below hit
@@ -396,11 +420,19 @@ __device__ __noinline__ int xsave_op(const Dev &P, Lane &L, u32 kind, u64 va) {
   }
   if (load_mx) F.mxcsr = (u32)mx;
   else if (compact && (rfbm & 2) && !(xbv & 2)) F.mxcsr = 0x1f80;
-  if (rfbm & 4) {
-    for (u32 i = 0; i < 32; i++) {
-      u64 q = 0;
-      if (xbv & 4) vread(L, va + 576 + 8 * i, 8, q);
-      F.ymmh[i >> 1][i & 1] = q;
+  {
+    u32 off = 576;
+    for (u32 c = 2; c <= 7; c++) {
+      if (compact && !((xcomp >> c) & 1)) continue;
+      const u32 at = compact ? off : xs_offset(c);
+      off += xs_size(c);
+      if (c == 3 || c == 4 || !((rfbm >> c) & 1)) continue;
+      for (u32 i = 0; i < xs_size(c) / 8; i++) {
+        u64 q = 0;  // a component not in XSTATE_BV: its initial state (zeros)
+        if ((xbv >> c) & 1) vread(L, va + at + 8 * i, 8, q);
+        if (c == 2) F.ymmh[i >> 1][i & 1] = q;
+        else xs_word(F, c, i) = q;
+      }
     }
   }
   L.pend = pend0;
@@ -919,7 +951,9 @@ __device__ __noinline__ int sys2_exec(const Dev &P, Lane &L, const UOp &u, u64 n
             return X_OK;
           }
           const u64 v = (R(L, 0) & 0xffffffffull) | (R(L, 2) << 32);
-          if (cpl || (v & ~XS_SUPPORTED) || !(v & 1) || ((v & 4) && !(v & 2)) || (((v >> 3) & 1) != ((v >> 4) & 1)))
+          // (bits 7:5, the AVX-512 state, all or none and only with 2:1 = 11)
+          if (cpl || (v & ~XS_SUPPORTED) || !(v & 1) || ((v & 4) && !(v & 2)) || (((v >> 3) & 1) != ((v >> 4) & 1)) ||
+              ((v & 0xe0) && ((v & 0xe0) != 0xe0 || (v & 6) != 6)))
             return fault_x(L, WTFGPU_VEC_GP, 0);
           F.xcr0 = v;
           L.simd = simd_bits(L.cr0, S.cr4, v);

@@ -154,6 +154,8 @@ wtfgpu_regs_t RegsFromCpuState(const CpuState_t &S) {
   for (int i = 0; i < 16; i++) {
     r.xmm[i][0] = S.Zmm[i].Q[0], r.xmm[i][1] = S.Zmm[i].Q[1];
     r.ymmh[i][0] = S.Zmm[i].Q[2], r.ymmh[i][1] = S.Zmm[i].Q[3];
+    for (int q = 0; q < 4; q++) r.zmmh[i][q] = S.Zmm[i].Q[4 + q];
+    for (int q = 0; q < 8; q++) r.zmm_hi[i][q] = S.Zmm[16 + i].Q[q];
   }
   return r;
 }

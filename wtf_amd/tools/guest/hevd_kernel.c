@@ -169,6 +169,34 @@ __attribute__((noipa)) void ExFreePoolWithTag(void *P, u32 Tag) {
 /* ---- the IOCTL handlers */
 #define TAG 0x6B636148 /* 'Hack' */
 
+struct GsFrame {
+  u8 Kernel[512];
+  u64 Cookie;
+};
+#ifdef HEVD_IO
+/* (HEVD_IO: built with /GS like the rest of the driver, so an overrun is
+ * caught by the cookie check before the return address is used: a bugcheck
+ * instead of a return into arbitrary kernel code) */
+__attribute__((noipa)) static u32 TriggerBufferOverflowStack(const u8 *User, u64 Size) {
+  struct GsFrame F;
+  KTRY T;
+  F.Cookie = __security_cookie ^ (u64)&F;
+  memset(F.Kernel, 0, sizeof(F.Kernel));
+  DbgPrintEx(77, 3, "[+] UserBuffer: 0x%p Size: 0x%zX\n", User, Size);
+  u32 Status = F.Kernel[0] == 0x41 ? STATUS_SUCCESS : STATUS_UNSUCCESSFUL;
+  TRY(T) {
+    memcpy(F.Kernel, User, Size); /* the bug: Size is the user's, not sizeof(Kernel) */
+    END_TRY();
+    Status = F.Kernel[0] == 0x41 ? STATUS_SUCCESS : STATUS_UNSUCCESSFUL;
+  }
+  EXCEPT {
+    END_TRY();
+    Status = STATUS_ACCESS_VIOLATION;
+  }
+  CheckCookie(F.Cookie, (u64)&F);
+  return Status;
+}
+#else
 __attribute__((noipa)) static u32 TriggerBufferOverflowStack(const u8 *User, u64 Size) {
   u8 Kernel[512];
   KTRY T;
@@ -184,11 +212,8 @@ __attribute__((noipa)) static u32 TriggerBufferOverflowStack(const u8 *User, u64
   }
   return Kernel[0] == 0x41 ? STATUS_SUCCESS : STATUS_UNSUCCESSFUL;
 }
+#endif
 
-struct GsFrame {
-  u8 Kernel[512];
-  u64 Cookie;
-};
 __attribute__((noipa)) static u32 TriggerBufferOverflowStackGS(const u8 *User, u64 Size) {
   struct GsFrame F;
   F.Cookie = __security_cookie ^ (u64)&F;
