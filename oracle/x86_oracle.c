@@ -564,6 +564,7 @@ typedef struct {
   u32 m32, a16; /* 32-bit code (U29); a 67 prefix there (16-bit addresses: outside) */
   u32 undef; /* U36: an encoding the emulated CPU does not define (#UD) */
   u32 vex, vl, vw, vvvv, vpp, vbad; /* VEX prefix: present, L, W, vvvv (decoded), pp; a legacy prefix before it */
+  u32 evex, ell, ez, eb, eaaa, er2; /* EVEX (U47): L'L, z, b, aaa, R' (vvvv has V' as bit 4) */
   u32 op;
   u32 has_modrm, mod, reg, rm; /* reg, rm include REX extension */
   u32 is_mem;
@@ -1822,6 +1823,7 @@ static void yput(orc_machine *m, u32 r, y256 v, int l256) {
 #include "x86_oracle_sse4.inc" /* SSSE3 / SSE4.1 integer, AVX2 lane crossing (U41) */
 #include "x86_oracle_ext.inc"  /* BMI1 / BMI2 / ADX / MOVBE / CRC32, SSE4.2, AES, PCLMULQDQ (U45) */
 #include "x86_oracle_avx2x.inc" /* FMA3, F16C, AVX2 gathers (U46) */
+#include "x86_oracle_avx512.inc" /* the AVX-512 subset and the opmask instructions (U47) */
 
 /* two-source ops of one 128-bit lane (the legacy semantics); 0 = not one */
 static int vlane(u32 op, int pc, const x128 *a, const x128 *b, u8 imm, u64 cnt, x128 *r) {
@@ -1967,6 +1969,10 @@ static int vex_defined(u32 map, u32 op, int pp) {
     case 0x77: return pp == 0;
     case 0x7c: case 0x7d: case 0xd0: return pp == 1 || pp == 3;
     case 0xf0: return pp == 3;
+    case 0x41: case 0x42: case 0x44: case 0x45: case 0x46: case 0x47: case 0x4a: case 0x4b: case 0x90: case 0x91:
+    case 0x98: case 0x99: /* the opmask instructions */
+      return pp <= 1;
+    case 0x92: case 0x93: return pp != 2;
     default:
       return pp == 1 && ((op >= 0x60 && op <= 0x6e) || (op >= 0x71 && op <= 0x76) || op == 0xc4 || op == 0xc5 ||
                          (op >= 0xd1 && op <= 0xfe));
@@ -1993,8 +1999,8 @@ static int vex_defined(u32 map, u32 op, int pp) {
     if (pp != 1) return 0;
     return op == 0x00 || op == 0x01 || op == 0x02 || op == 0x04 || op == 0x05 || op == 0x06 ||
            (op >= 0x08 && op <= 0x0f) || (op >= 0x14 && op <= 0x19) || op == 0x1d || (op >= 0x20 && op <= 0x22) ||
-           op == 0x38 || op == 0x39 || (op >= 0x40 && op <= 0x42) || op == 0x44 || op == 0x46 ||
-           (op >= 0x4a && op <= 0x4c) || (op >= 0x60 && op <= 0x63) || op == 0xce || op == 0xcf || op == 0xdf;
+           (op >= 0x30 && op <= 0x33) || op == 0x38 || op == 0x39 || (op >= 0x40 && op <= 0x42) || op == 0x44 ||
+           op == 0x46 || (op >= 0x4a && op <= 0x4c) || (op >= 0x60 && op <= 0x63) || op == 0xce || op == 0xcf || op == 0xdf;
   }
   return 0;
 }
@@ -2031,6 +2037,8 @@ static int exec_vex(orc_machine *m, insn *d) {
   const u32 op = d->op, r3 = d->reg & 7, map = d->opmap, vv = d->vvvv;
   const int pp = (int)d->vpp, l256 = (int)d->vl, mem = d->is_mem;
   const u8 imm = d->bytes[d->len - 1];
+  if (d->evex) return exec_evex(m, d);                 /* U47 */
+  if (kop_any(map, op, pp)) return exec_kop(m, d);
   if (fp_form_o(map, op, pp, 1)) return exec_fp(m, d); /* U39 / U40 */
   if (s4_form_o(map, op, pp, 1)) return exec_s4(m, d); /* U41 */
   if (gx_form_o(map, op, pp, 1)) return exec_gext(m, d); /* U45 */
@@ -3265,7 +3273,35 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
     les = (nb & 0xc0) != 0xc0;
     d->pos = (u32)save;
   }
-  if ((b == 0xc4 || b == 0xc5) && !les) { /* VEX (always VEX in 64-bit mode) */
+  zform ezf = {ZK_NONE, 0, 0, 0, 0};
+  if (b == 0x62 && !d->m32) { /* EVEX (U47; 32-bit code's bound stays outside) */
+    const u8 p0 = fetch8(m, d), p1 = fetch8(m, d), p2 = fetch8(m, d);
+    b = fetch8(m, d);
+    if (d->fetch_fail) return -1;
+    d->vex = d->evex = 1;
+    d->vbad = d->pfx66 || d->rep || d->rex || (p0 & 8) || !(p1 & 4);
+    d->rexr = !((p0 >> 7) & 1);
+    d->rexx = !((p0 >> 6) & 1);
+    d->rexb = !((p0 >> 5) & 1);
+    d->er2 = !((p0 >> 4) & 1);
+    d->opmap = p0 & 7u;
+    d->vw = d->rexw = (p1 >> 7) & 1u;
+    d->rex = 0x40 | (d->rexw << 3) | (d->rexr << 2) | (d->rexx << 1) | d->rexb;
+    d->vvvv = ((~p1 >> 3) & 15u) | ((((u32)~p2 >> 3) & 1u) << 4);
+    d->vpp = p1 & 3u;
+    d->ez = (p2 >> 7) & 1u;
+    d->ell = (p2 >> 5) & 3u;
+    d->eb = (p2 >> 4) & 1u;
+    d->eaaa = p2 & 7u;
+    d->op = b;
+    ezf = zform_of(d->opmap, b, (int)d->vpp, d->vw);
+    /* maps 1-3 and 5-6 (AVX512-FP16) are defined: outside the subset is UNIMPLEMENTED */
+    d->undef = d->vbad || d->opmap == 0 || d->opmap == 4 || d->opmap == 7;
+    if (d->undef || d->opmap > 3 || ezf.kind == ZK_NONE) {
+      d->len = d->pos;
+      return 1;
+    }
+  } else if ((b == 0xc4 || b == 0xc5) && !les) { /* VEX (always VEX in 64-bit mode) */
     d->vex = 1;
     d->vbad = d->pfx66 || d->rep || d->rex;
     const u8 b1 = fetch8(m, d);
@@ -3287,7 +3323,7 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
     if (d->opmap != 1 && d->opmap != 2 &&
         !(d->opmap == 3 && !d->undef && (fp_form_o(3, b, (int)d->vpp, 1) || s4_form_o(3, b, (int)d->vpp, 1) ||
                                          x42_form_o(3, b, (int)d->vpp, 1) || gx_form_o(3, b, (int)d->vpp, 1) ||
-                                         ax_form_o(3, b, (int)d->vpp, 1)))) {
+                                         ax_form_o(3, b, (int)d->vpp, 1) || kop_any(3, b, (int)d->vpp)))) {
       d->op = b;
       d->len = d->pos;
       return 1;
@@ -3415,9 +3451,18 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
       if ((b >= 0x70 && b <= 0x73) || b == 0xc2 || (b >= 0xc4 && b <= 0xc6)) imm = 1;
     }
   }
+  if (d->evex) {
+    has_modrm = 1;
+    imm = d->opmap == 3;
+  }
   if (has_modrm) {
     decode_modrm(m, d, mr);
     if (d->fetch_fail) return -1;
+    if (d->evex) { /* 5-bit registers; disp8 * N */
+      d->reg |= d->er2 << 4;
+      if (d->mod == 3) d->rm |= d->rexx << 4;
+      if (d->mod == 1) mr->disp *= zdisp_n(ezf, 16u << d->ell, d->eb);
+    }
   }
   if (d->opmap == 0 && (b == 0xf6 || b == 0xf7) && ((d->reg & 7) <= 1)) imm = b == 0xf6 ? 1 : izsz;
   for (int i = 0; i < imm; i++) {

@@ -150,7 +150,7 @@ K = {  # ring 0 (each ends with hlt; a fault ends the lane)
     "lockbad": "lock add [rdi], eax\n .byte 0xf0, 0x03, 0x07\n hlt",      # lock add eax, [rdi]: #UD
     "locknop": ".byte 0xf0, 0x90\n hlt",
     "lockreg": ".byte 0xf0, 0x48, 0xff, 0xc0\n hlt",                     # lock inc rax
-    "ud_evex": ".byte 0x62, 0xf1, 0x7c, 0x48, 0x10, 0xc1\n hlt",
+    "ud_evex": ".byte 0x62, 0xf1, 0x7c, 0x48, 0x58, 0xc1\n hlt",  # vaddps zmm0, zmm0, zmm1 (outside U47)
     "ud_0f": ".byte 0x0f, 0xff, 0xc0\n hlt",
     "ud_b9": ".byte 0x0f, 0xb9, 0xc0\n hlt",
     "ud_0e": ".byte 0x0f, 0x0e\n hlt",

@@ -493,3 +493,74 @@ def test_gpu_matches_native_avx2x_vectors():
     """FMA3, F16C and the AVX2 gathers (tests/golden/avx2x_vectors.json.gz, U46)."""
     from tests.test_avx2x import DOC, inputs
     _run_vector_doc(DOC, inputs, mem=True)
+
+
+def test_gpu_matches_native_avx512_vectors():
+    """The AVX-512 subset and the opmask instructions (tests/golden/avx512_vectors.json.gz, U47):
+    every case one lane with GPRs, RFLAGS, zmm0-31, k0-7 and the 512-byte window
+    across a page boundary; the guard cases (one of the two pages absent) in
+    their own address spaces, with the #PF error code and CR2 of the faults
+    (memory fault suppression)."""
+    from tests.test_avx512 import BOUND, DOC, WIN, XCR0, address_space, case_regs, check, get_zmm, inputs
+    from tests.test_avx512 import CODE_VA as CVA
+    from wtf_amd.abi import EXIT_FAULT
+    from wtf_amd.engine import Engine
+
+    buf_va = int(DOC["buf_va"], 16)
+    fails = []
+    total = 0
+    for guard in (0, 1, 2):
+        cases = [c for c in DOC["cases"] if c["guard"] == guard]
+        total += len(cases)
+        codes = sorted({c["code"] for c in cases})
+        slot = {c: i for i, c in enumerate(codes)}
+        blob = bytearray(32 * len(codes))
+        for c, i in slot.items():
+            b = bytes.fromhex(c) + b"\xcc"
+            blob[32 * i: 32 * i + len(b)] = b
+        sp = address_space(bytes(blob), buf_va, bytes(WIN), guard)
+        n = (len(cases) + 63) // 64 * 64
+        eng = Engine(0)
+        pfns, pblob = sp.phys()
+        eng.load_pool(pfns, pblob)
+        eng.alloc_lanes(n, overlay_pages=4, cov_entries=64)
+        init = regs_from_state(user_state(CVA, 0, sp.cr3))
+        init.xcr0 = XCR0
+        eng.set_initial_state(init)
+        eng.set_limit(0)
+        eng.restore()
+        regs = eng.read_regs(0, n)
+        writes, ins, wins = [], [], []
+        for i, c in enumerate(cases):
+            zin, win = inputs(c)
+            ins.append(zin)
+            wins.append(win)
+            r = case_regs(c, regs[i], zin)
+            r.rip = CVA + 32 * slot[c["code"]]
+            if guard != 2:
+                writes.append((i, buf_va, win[:BOUND]))
+            if guard != 1:
+                writes.append((i, buf_va + BOUND, win[BOUND:]))
+        for i in range(len(cases), n):
+            regs[i].rip = CVA + 32 * slot[cases[0]["code"]] + len(bytes.fromhex(cases[0]["code"]))
+        eng.write_regs(regs)
+        eng.apply_writes(writes)
+        eng.run()
+        ex = eng.exits()
+        out = eng.read_regs(0, n)
+        for i, c in enumerate(cases):
+            r, e = out[i], ex[i]
+            if "fault" not in c and (e.status != EXIT_INT3 or e.icount != 1):
+                fails.append((c["name"], c["code"], "exit", e.status, e.vector))
+                continue
+            if "fault" in c and e.status != EXIT_FAULT:
+                fails.append((c["name"], c["code"], "no fault", e.status))
+                continue
+            lo = bytes(BOUND) if guard == 2 else eng.read_virt(i, buf_va, BOUND)
+            hi = bytes(WIN - BOUND) if guard == 1 else eng.read_virt(i, buf_va + BOUND, WIN - BOUND)
+            bad = check(c, e.status, e.vector, e.error, e.addr, list(r.gpr), r.rflags, get_zmm(r), list(r.k),
+                        lo + hi, ins[i], wins[i])
+            if bad:
+                fails.append((c["name"], c["code"]) + bad)
+    assert total == len(DOC["cases"])
+    assert not fails, f"{len(fails)}/{total} mismatches, first: {fails[:6]}"

@@ -104,7 +104,7 @@ __device__ __forceinline__ u32 loc_regno(const UOp &u, u32 loc) {
 __device__ __forceinline__ void digest_sse(const UOp &u, u32 &op, u32 &sub, u32 &ra, u32 &rb, u32 &sz) {
   const u32 x = u.opreg, c = u.sub, pp = u.bsz;
   const bool vex = x & 1;
-  if (vex_map(x) != 1 || (x & 0x10000)) return;
+  if (vex_map(x) != 1 || (x & 0x30000)) return;  // a bad prefix, EVEX (engine_avx512.h)
   const u32 vvvv = vex ? (x >> 4) & 15 : 0;
   sz = vex && ((x >> 1) & 1) ? 4 : 2;
   sub = vex ? 2 : 0;

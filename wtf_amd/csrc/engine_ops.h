@@ -329,7 +329,8 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u, bool m32 = false)
     c = ib_at(b, pos++);  // the opcode
     const bool def = !bad && vmap >= 1 && vmap <= 3 && vex_defined(vmap, c, vpp);
     if (!def || (vmap == 3 && !fp_form(3, c, vpp, true) && !s4_form(3, c, vpp, true) && !x42_form(3, c, vpp, true) &&
-                 !gx_form(3, c, vpp, true) && !ax_form(3, c, vpp, true))) {  // U36: #UD from the opcode byte
+                 !gx_form(3, c, vpp, true) && !ax_form(3, c, vpp, true) &&
+                 !(kop_bits(3, c, vpp, 0) | kop_bits(3, c, vpp, 1)))) {  // U36: #UD from the opcode byte
       u.len = pos;
       u.op = (lock || !def) ? O_UD : O_UNIMPL;
       u.supported = lock || !def;
@@ -337,13 +338,48 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u, bool m32 = false)
       return 0;
     }
   }
+  // EVEX (62; 64-bit code only, 32-bit code's bound stays outside, U29):
+  // P0 = R X B R' 0 m m m, P1 = W v v v v 1 p p, P2 = z L' L b V' a a a
+  // (engine_avx512.h). Its fields become the REX bits and `vex` with EVX set.
+  EForm ef{EZ_NONE, 0, 0, false, false, false, false};
+  if (c == 0x62 && !m32 && !vex) {  // (after VEX, c is its opcode byte: 62 is vpunpckldq)
+    if (pos + 4 > 15) return 2;
+    if (pos + 4 > b.avail) return 1;
+    const u32 p0 = ib_at(b, pos), p1 = ib_at(b, pos + 1), p2 = ib_at(b, pos + 2);
+    pos += 3;
+    c = ib_at(b, pos++);
+    const u32 emap = p0 & 7, ew = (p1 >> 7) & 1;
+    vpp = p1 & 3;
+    ef = evex_form(emap, c, vpp, ew);
+    // a legacy 66 / f2 / f3 / REX before EVEX or a reserved bit: #UD; maps
+    // 1-3 and 5-6 (AVX512-FP16) are defined, the forms outside the subset
+    // UNIMPLEMENTED (U36)
+    const bool bad = p66 || u.rep || rex || (p0 & 8) || !(p1 & 4) || lock;
+    if (bad || !(emap == 1 || emap == 2 || emap == 3 || emap == 5 || emap == 6) || ef.kind == EZ_NONE) {
+      const bool ud = bad || emap == 0 || emap == 4 || emap == 7;
+      u.len = pos;
+      u.op = ud ? O_UD : O_UNIMPL;
+      u.supported = ud;
+      u.opbytes = (u32)b.lo;
+      return 0;
+    }
+    rex = 0x40 | (ew << 3) | ((((~p0) >> 7) & 1) << 2) | ((((~p0) >> 6) & 1) << 1) | (((~p0) >> 5) & 1);
+    vex = 1 | (ew << 2) | ((((~p1) >> 3) & 15) << 4) | (emap << 8) | EVX | (((p2 >> 5) & 3) << 18) |
+          (((p2 >> 7) & 1) << 21) | (((p2 >> 4) & 1) << 22) | ((p2 & 7) << 23) | ((((~p2) >> 3) & 1) << 26) |
+          ((((~p0) >> 4) & 1) << 27);  // bit 27: R' (moved into UOp::reg below)
+  }
   u.rex = rex;
   const u32 rexw = (rex >> 3) & 1, rexr = (rex >> 2) & 1, rexx = (rex >> 1) & 1, rexb = rex & 1;
   u32 e, map2 = 0, smap = 1;
-  if (vex) {
+  if (vex & EVX) {
+    smap = vex_map(vex);
+    map2 = 1;
+    e = smap == 3 ? kSseModrmImm : kSseModrm;
+  } else if (vex) {
     smap = vex_map(vex);
     map2 = 1;
     e = smap == 1 ? kMap2[c] : smap == 2 ? kSseModrm : kSseModrmImm;
+    if (smap == 1 && kop_bits(1, c, vpp, 0) | kop_bits(1, c, vpp, 1)) e = kSseModrm;  // the opmask instructions
     if (smap == 1 && (e & 63) != O_SSE) e = kUnimpl;
   } else if (c == 0x0f) {
     if (pos >= 15) return 2;
@@ -455,6 +491,7 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u, bool m32 = false)
         if (pos + 1 > 15) return 2;
         if (pos + 1 > b.avail) return 1;
         u.disp = sext(ib_get(b, pos, 1), 1);
+        if (vex & EVX) u.disp *= (i64)evex_disp8_n(ef, 16u << evex_ll(vex), (vex >> 22) & 1);  // disp8 * N
         pos += 1;
       } else if (mod == 2) {
         if (pos + 4 > 15) return 2;
@@ -462,6 +499,11 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u, bool m32 = false)
         u.disp = sext(ib_get(b, pos, 4), 4);
         pos += 4;
       }
+    }
+    if (vex & EVX) {  // 5-bit vector registers: R' above reg, X above a register r/m
+      u.reg |= ((vex >> 27) & 1) << 4;
+      if (mod == 3) u.rm |= rexx << 4;
+      vex &= ~(1u << 27);
     }
     // modrm.reg selected forms
     const u32 r3 = u.reg & 7;
@@ -537,7 +579,7 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u, bool m32 = false)
   }
   if (map2) {
     const u32 gpc = vex ? vpp : (u.rep == 0xf3 ? 2 : u.rep == 0xf2 ? 3 : p66 ? 1 : 0);
-    if (u.op == O_SSE && smap >= 2 && gx_form(smap, c, gpc, vex != 0)) {  // engine_ext.h (U45)
+    if (u.op == O_SSE && smap >= 2 && !(vex & EVX) && gx_form(smap, c, gpc, vex != 0)) {  // engine_ext.h (U45)
       u.op = O_GEXT;
       u.sub = c;
       u.bsz = gpc;
@@ -548,7 +590,9 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u, bool m32 = false)
       if (vex) {
         u.bsz = vpp;
         u.opreg = vex;
-        if (smap == 1 && c == 0xae && !(vpp == 0 && u.is_mem && ((u.reg & 7) == 2 || (u.reg & 7) == 3)))
+        if (vex & EVX) {
+          // the subset (evex_form) was checked before the ModRM
+        } else if (smap == 1 && c == 0xae && !(vpp == 0 && u.is_mem && ((u.reg & 7) == 2 || (u.reg & 7) == 3)))
           u.op = O_UD;  // U36: vldmxcsr / vstmxcsr are the only VEX group-15 forms
         else if (!vex_valid(smap, c, vpp, u.is_mem, u.reg & 7))
           u.op = O_UNIMPL;

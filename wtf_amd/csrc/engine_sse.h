@@ -30,6 +30,7 @@ namespace wtfgpu_dev {
 __host__ __device__ inline bool s4_form(u32 map, u32 c, u32 pp, bool vex);  // engine_sse4.h
 __host__ __device__ inline bool x42_form(u32 map, u32 c, u32 pp, bool vex);  // engine_ext.h
 __host__ __device__ inline u32 ax_form(u32 map, u32 c, u32 pp, bool vex);    // engine_avx2x.h
+__host__ __device__ inline u32 kop_bits(u32 map, u32 c, u32 pp, u32 w);       // engine_avx512.h
 struct UOp;
 __device__ __noinline__ int x42_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next);
 
@@ -116,6 +117,10 @@ __host__ __device__ inline bool vex_defined(u32 map, u32 op, u32 pp) {
       case 0x77: return pp == 0;
       case 0x7c: case 0x7d: case 0xd0: return pp == 1 || pp == 3;
       case 0xf0: return pp == 3;
+      case 0x41: case 0x42: case 0x44: case 0x45: case 0x46: case 0x47: case 0x4a: case 0x4b:
+      case 0x90: case 0x91: case 0x98: case 0x99:  // the opmask instructions (AVX-512)
+        return pp <= 1;
+      case 0x92: case 0x93: return pp != 2;
       default:
         return pp == 1 && ((op >= 0x60 && op <= 0x6e) || (op >= 0x71 && op <= 0x76) || op == 0xc4 || op == 0xc5 ||
                            (op >= 0xd1 && op <= 0xfe));
@@ -138,7 +143,8 @@ __host__ __device__ inline bool vex_defined(u32 map, u32 op, u32 pp) {
     if (pp == 3) return op == 0xf0;  // rorx
     if (pp != 1) return false;
     return op <= 0x02 || (op >= 0x04 && op <= 0x06) || (op >= 0x08 && op <= 0x0f) || (op >= 0x14 && op <= 0x19) ||
-           op == 0x1d || (op >= 0x20 && op <= 0x22) || op == 0x38 || op == 0x39 || (op >= 0x40 && op <= 0x42) ||
+           op == 0x1d || (op >= 0x20 && op <= 0x22) || (op >= 0x30 && op <= 0x33) || op == 0x38 || op == 0x39 ||
+           (op >= 0x40 && op <= 0x42) ||
            op == 0x44 || op == 0x46 || (op >= 0x4a && op <= 0x4c) || (op >= 0x60 && op <= 0x63) || op == 0xce ||
            op == 0xcf || op == 0xdf;
   }
@@ -167,6 +173,7 @@ __host__ __device__ inline bool legacy_3byte_defined(u32 map, u32 op, u32 pfx) {
 __device__ __forceinline__ bool vex_valid(u32 map, u32 c, u32 pp, u32 is_mem, u32 r3) {
   if (fp_form(map, c, pp, true) || s4_form(map, c, pp, true) || x42_form(map, c, pp, true) || ax_form(map, c, pp, true))
     return true;  // engine_ssefp.h, engine_sse4.h, engine_ext.h, engine_avx2x.h
+  if (kop_bits(map, c, pp, 0) || kop_bits(map, c, pp, 1)) return true;  // engine_avx512.h (W checked there)
   if (map == 2) return pp == 1 && (c == 0x00 || c == 0x17 || c == 0x58 || c == 0x59 || c == 0x78 || c == 0x79);
   if (map != 1) return false;
   if (c == 0x77) return pp == 0;
@@ -465,6 +472,7 @@ __device__ __forceinline__ void mmx_put(wtfgpu_regs_t &F, u32 i, u64 v) {
 #include "engine_ssefp.h"  // SSE / AVX floating point: fp_exec
 #include "engine_sse4.h"  // SSSE3 / SSE4.1 integer, AVX2 lane-crossing: s4_exec
 #include "engine_avx2x.h"  // FMA3, F16C, AVX2 gathers: ax_exec
+#include "engine_avx512.h"  // the EVEX subset and the opmask instructions: evex_exec, kop_exec
 namespace wtfgpu_dev {
 
 __device__ __noinline__ int mmx_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next) {
@@ -756,6 +764,8 @@ __device__ __noinline__ int sse_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
 __device__ __noinline__ int vex_exec(const Dev &P, Lane &L, const UOp &u, u64 nrip, u64 &next) {
   next = nrip;
   const u32 x = u.opreg, c = u.sub, pp = u.bsz, r3 = u.reg & 7, map = vex_map(x);
+  if (x & EVX) return evex_exec(P, L, u, nrip, next);                          // engine_avx512.h
+  if (kop_bits(map, c, pp, 0) || kop_bits(map, c, pp, 1)) return kop_exec(P, L, u, nrip, next);  // W checked there
   if (fp_form(map, c, pp, true)) return fp_exec(P, L, u, nrip, next);  // its own VEX checks
   if (s4_form(map, c, pp, true)) return s4_exec(P, L, u, nrip, next);
   if (x42_form(map, c, pp, true)) return x42_exec(P, L, u, nrip, next);  // its own VEX checks

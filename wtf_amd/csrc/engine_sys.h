@@ -343,7 +343,8 @@ __device__ __noinline__ int xsave_op(const Dev &P, Lane &L, u32 kind, u64 va) {
     if (!compact && !vread(L, va + 512, 8, bv)) return X_FAULT;
     const u64 inuse = rfbm & 0xe7;
     if ((rfbm & 1) && (!legacy_store(P, L, va, 0, 24) || !legacy_store(P, L, va, 32, 128))) return X_FAULT;
-    if ((rfbm & 6) && !legacy_store(P, L, va, 24, 8)) return X_FAULT;
+    // MXCSR / MXCSR_MASK: with SSE or AVX requested, but compacted only with SSE (native images)
+    if ((rfbm & (compact ? 2 : 6)) && !legacy_store(P, L, va, 24, 8)) return X_FAULT;
     if ((rfbm & 2) && !legacy_store(P, L, va, 160, 256)) return X_FAULT;
     if (compact) {
       if (!vwrite(L, va + 512, 8, inuse) || !vwrite(L, va + 520, 8, 0x8000000000000000ull | rfbm)) return X_FAULT;
