@@ -1166,6 +1166,9 @@ constexpr u32 STAT_N = 16;
 #ifndef WTFGPU_INLINE_ACTIONS
 #define WTFGPU_INLINE_ACTIONS 3  // SetGprs (1) / StopOk (2) actions applied without the lane copy
 #endif
+#ifndef WTFGPU_ACT_NESTED
+#define WTFGPU_ACT_NESTED 0  // the two inline actions in one nested block (the miscompiled form, A/B only)
+#endif
 #ifndef WTFGPU_FAST_FAULTS
 #define WTFGPU_FAST_FAULTS 1  // a fast attempt whose fill would fault raises the fault itself
 #endif
@@ -1546,7 +1549,23 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     }
     // (one block per kind: with the two kinds nested in one per-lane if/else
     // the build ran wrong on MI355X, tlv's lanes stopping Ok at their SetGprs
-    // breakpoint, although either kind alone ran right)
+    // breakpoint, although either kind alone ran right; WTFGPU_ACT_NESTED=1
+    // builds that form for the A/B in DESIGN.md §3)
+#if WTFGPU_ACT_NESTED
+    if (WTFGPU_INLINE_ACTIONS == 3 && (act_kind == WTFGPU_BPACT_SET_GPRS || act_kind == WTFGPU_BPACT_STOP_OK) && ing &&
+        !skip) {
+      if (act_kind == WTFGPU_BPACT_SET_GPRS) {
+#pragma unroll
+        for (u32 i = 0; i < 16; i++) RS(L, i, act->gprs[i]);
+        L.rip = act->gprs[16];
+        skip = L.rip == grip;
+      } else {
+        L.status = WTFGPU_EXIT_STOP_OK;
+        skip = true;
+      }
+      ing = false;
+    }
+#else
     if ((WTFGPU_INLINE_ACTIONS & 1) && act_kind == WTFGPU_BPACT_SET_GPRS && ing && !skip) {
 #pragma unroll
       for (u32 i = 0; i < 16; i++) RS(L, i, act->gprs[i]);
@@ -1559,6 +1578,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       skip = true;
       ing = false;
     }
+#endif
     if (ing) {
       if ((flags & UC_BP) && !skip) {
         // breakpoint hit: device action (the lane keeps running) or host exit
