@@ -1252,24 +1252,95 @@ static x128 x64(u64 v) {
   return r;
 }
 
+/* The SSSE3 instructions on mm registers (no prefix; 0f 38 00-0b / 1c-1e, 0f 3a 0f), after the SDM's
+ * operation sections: d = the destination's quadword, s = the source's. */
+static int ssse3_mm(u32 map, u32 op) { return map == 2 ? (op <= 0x0b || (op >= 0x1c && op <= 0x1e)) : (map == 3 && op == 0x0f); }
+static u64 ssse3_mm_op(u32 map, u32 op, u64 d, u64 s, u32 imm) {
+  u64 r = 0;
+  if (map == 3) { /* palignr: ((d << 64) | s) >> (imm * 8), low 64 bits */
+    for (u32 i = 0; i < 8; i++) {
+      const u32 k = i + imm; /* byte k of the 16-byte concatenation (0-7: s, 8-15: d) */
+      const u64 byte = k < 8 ? (s >> (8 * k)) & 0xff : k < 16 ? (d >> (8 * (k - 8))) & 0xff : 0;
+      r |= byte << (8 * i);
+    }
+    return r;
+  }
+  switch (op) {
+  case 0x00: /* pshufb */
+    for (u32 i = 0; i < 8; i++) {
+      const u32 k = (u32)(s >> (8 * i)) & 0xff;
+      if (!(k & 0x80)) r |= ((d >> (8 * (k & 7))) & 0xff) << (8 * i);
+    }
+    return r;
+  case 0x01: case 0x02: case 0x03: case 0x05: case 0x06: case 0x07: { /* phadd / phsub w, d, sw */
+    const u32 w = op == 0x02 || op == 0x06 ? 4 : 2, n = 8 / w;
+    for (u32 i = 0; i < n; i++) { /* result i: pair i of d (i < n / 2), else pair i - n / 2 of s */
+      const u64 src = i < n / 2 ? d : s;
+      const u32 j = 2 * (i % (n / 2));
+      const i64 x = (i64)sxn((src >> (8 * w * j)) & szmask((int)w), (int)w);
+      const i64 y = (i64)sxn((src >> (8 * w * (j + 1))) & szmask((int)w), (int)w);
+      i64 v = op >= 0x05 ? x - y : x + y;
+      if (op == 0x03 || op == 0x07) v = v > 32767 ? 32767 : v < -32768 ? -32768 : v;
+      r |= ((u64)v & szmask((int)w)) << (8 * w * i);
+    }
+    return r;
+  }
+  case 0x04: /* pmaddubsw: unsigned bytes of d times signed bytes of s, pairs, saturated */
+    for (u32 i = 0; i < 4; i++) {
+      const i64 v = (i64)((d >> (16 * i)) & 0xff) * (int8_t)(s >> (16 * i)) +
+                    (i64)((d >> (16 * i + 8)) & 0xff) * (int8_t)(s >> (16 * i + 8));
+      r |= (u64)(u16)(v > 32767 ? 32767 : v < -32768 ? -32768 : v) << (16 * i);
+    }
+    return r;
+  case 0x08: case 0x09: case 0x0a: { /* psignb / w / d */
+    const u32 w = 1u << (op - 8);
+    for (u32 i = 0; i < 8 / w; i++) {
+      const i64 sv = (i64)sxn((s >> (8 * w * i)) & szmask((int)w), (int)w);
+      const u64 dv = (d >> (8 * w * i)) & szmask((int)w);
+      const u64 v = sv < 0 ? (0 - dv) : sv == 0 ? 0 : dv;
+      r |= (v & szmask((int)w)) << (8 * w * i);
+    }
+    return r;
+  }
+  case 0x0b: /* pmulhrsw */
+    for (u32 i = 0; i < 4; i++) {
+      const int32_t t = (int32_t)(int16_t)(d >> (16 * i)) * (int32_t)(int16_t)(s >> (16 * i));
+      r |= (u64)(u16)(((t >> 14) + 1) >> 1) << (16 * i);
+    }
+    return r;
+  default: { /* 1c-1e pabsb / w / d of s */
+    const u32 w = 1u << (op - 0x1c);
+    for (u32 i = 0; i < 8 / w; i++) {
+      const i64 sv = (i64)sxn((s >> (8 * w * i)) & szmask((int)w), (int)w);
+      r |= ((u64)(sv < 0 ? -sv : sv) & szmask((int)w)) << (8 * w * i);
+    }
+    return r;
+  }
+  }
+}
+
 static int exec_mmx(orc_machine *m, insn *d, int pc) {
   const u32 op = d->op, r3 = d->reg & 7, mr = d->reg & 7, mm_rm = d->rm & 7;
   const int mem = d->is_mem;
   const u8 imm = d->bytes[d->len - 1];
-  if (pc == 0 && (op == 0xd0 || op == 0xd6 || op == 0xe6 || op == 0xf0 || op == 0x6c || op == 0x6d)) {
+  if (d->opmap == 1 && pc == 0 && (op == 0xd0 || op == 0xd6 || op == 0xe6 || op == 0xf0 || op == 0x6c || op == 0x6d)) {
     fault(m, WTFGPU_VEC_UD, 0);
     return X_FAULT;
   }
-  if (op == 0xf7) return X_UNIMPL; /* maskmovq */
-  if ((op >= 0x71 && op <= 0x73) && (mem || !((op == 0x73) ? (r3 == 2 || r3 == 6) : (r3 == 2 || r3 == 4 || r3 == 6)))) {
+  if (d->opmap == 1 && op == 0xf7 && mem) { /* maskmovq: register operands only */
+    fault(m, WTFGPU_VEC_UD, 0);
+    return X_FAULT;
+  }
+  if (d->opmap == 1 && (op >= 0x71 && op <= 0x73) &&
+      (mem || !((op == 0x73) ? (r3 == 2 || r3 == 6) : (r3 == 2 || r3 == 4 || r3 == 6)))) {
     fault(m, WTFGPU_VEC_UD, 0); /* register forms /2 /4 /6 (73: /2 /6) only */
     return X_FAULT;
   }
-  if ((op == 0xc5 || op == 0xd7 || (op == 0xd6 && pc)) && mem) {
+  if (d->opmap == 1 && (op == 0xc5 || op == 0xd7 || (op == 0xd6 && pc)) && mem) {
     fault(m, WTFGPU_VEC_UD, 0);
     return X_FAULT;
   }
-  if (op == 0xe7 && !mem) {
+  if (d->opmap == 1 && op == 0xe7 && !mem) {
     fault(m, WTFGPU_VEC_UD, 0);
     return X_FAULT;
   }
@@ -1285,8 +1356,43 @@ static int exec_mmx(orc_machine *m, insn *d, int pc) {
     fault(m, 16, 0);
     return X_FAULT;
   }
-  if (op == 0x77) { /* emms */
+  if (d->opmap == 1 && op == 0x77) { /* emms */
     m->r.fptw = 0xffff;
+    return X_OK;
+  }
+  if (d->opmap >= 2) { /* SSSE3 on mm registers (U41) */
+    const u64 dv = mmx_read(m, mr);
+    u64 sv = 0;
+    if (mem) {
+      if (vread(m, d->ea, 8, &sv)) return X_FAULT;
+    } else {
+      sv = mmx_read(m, mm_rm);
+    }
+    const u64 res = ssse3_mm_op(d->opmap, op, dv, sv, imm);
+    mmx_commit(m);
+    mmx_put(m, mr, res);
+    return X_OK;
+  }
+  if (op == 0xf7) { /* maskmovq mm1, mm2: mm1's bytes whose mm2 byte has bit 7 set, to [rdi] (seg override applies) */
+    const u64 dv = mmx_read(m, mr), sel = mmx_read(m, mm_rm);
+    u64 di = m->r.gpr[7];
+    if (d->pfx67) di &= 0xffffffffULL;
+    di += seg_base(m, d->seg);
+    u64 pa[2];
+    u32 nn[2];
+    for (u32 i = 0; i < 8; i++) /* every written byte's page first */
+      if (((sel >> (8 * i + 7)) & 1) && vprobe(m, di + i, 1, ACC_W, pa, nn)) return X_FAULT;
+    int rc = 0;
+    m->tn_mute++;
+    for (u32 i = 0; !rc && i < 8; i++)
+      if ((sel >> (8 * i + 7)) & 1) {
+        const u8 b = (u8)(dv >> (8 * i));
+        rc = vwrite(m, di + i, 1, &b);
+      }
+    m->tn_mute--;
+    if (rc) return X_FAULT;
+    tn_access(m, di, 8, TN_W);
+    mmx_commit(m);
     return X_OK;
   }
   if (op == 0xd6) { /* f3: movq2dq xmm, mm; f2: movdq2q mm, xmm */
@@ -1472,6 +1578,7 @@ static int exec_sse(orc_machine *m, insn *d) {
   x128 a, b, r;
   u64 v;
   if (d->opmap == 1 && ((pc == 0 && mmx_opcode(op)) || (op == 0xd6 && pc >= 2))) return exec_mmx(m, d, pc);
+  if (pc == 0 && ssse3_mm(d->opmap, op)) return exec_mmx(m, d, pc); /* U41: SSSE3 on mm registers */
   if (fp_form_o(d->opmap, op, pc, 0)) return exec_fp(m, d); /* U39 / U40 */
   if (s4_form_o(d->opmap, op, pc, 0)) return exec_s4(m, d); /* U41 */
   if (gx_form_o(d->opmap, op, pc, 0)) return exec_gext(m, d); /* U45 */
@@ -3345,7 +3452,7 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
       /* 0f 38 00 pshufb, 0f 38 17 ptest, the floating-point forms; the rest: outside */
       if ((d->opmap == 3 || (d->op != 0x00 && d->op != 0x17)) && !fp_form_o(d->opmap, d->op, pfx, 0) &&
           !s4_form_o(d->opmap, d->op, pfx, 0) && !x42_form_o(d->opmap, d->op, pfx, 0) &&
-          !gx_form_o(d->opmap, d->op, pfx, 0)) {
+          !gx_form_o(d->opmap, d->op, pfx, 0) && !(pfx == 0 && ssse3_mm(d->opmap, d->op))) {
         d->undef = !legacy_3byte_defined(d->opmap, d->op, pfx);
         d->len = d->pos;
         return 1;

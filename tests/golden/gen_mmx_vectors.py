@@ -104,6 +104,25 @@ def gen_forms(rng):
                 forms.append(Form(enc_rr(pfx, op, cm(), cm()), f"{nm}{sfx}2pi.rr"))
             code, p, s = enc_mem(crng, pfx, op, cm(), 16 if sfx == "pd" else 1)
             forms.append(Form(code, f"{nm}{sfx}2pi.m", p, s))
+    # ---- SSSE3 on mm registers (0f 38 00-0b / 1c-1e, 0f 3a 0f) and maskmovq (own generator)
+    srng = random.Random(0x55E3)
+    sm_ = lambda: srng.randrange(16)  # noqa: E731
+
+    def three(code, op):  # 0f <esc> modrm ... -> 0f <esc> op modrm ...
+        i = code.index(0x0F)
+        return code[:i + 2] + [op] + code[i + 2:]
+    for esc, ops in ((0x38, list(range(0x00, 0x0C)) + [0x1C, 0x1D, 0x1E]), (0x3A, [0x0F])):
+        for op in ops:
+            nm = "palignr" if esc == 0x3A else "ssse3.%02x" % op
+            for _ in range(4):
+                code = three(enc_rr(NP, esc, sm_(), sm_()), op)
+                forms.append(Form(code + ([srng.choice([0, 1, 3, 7, 8, 9, 15, 16, 17, 200])] if esc == 0x3A else []),
+                                  nm + ".rr"))
+            for _ in range(2):
+                code, p, s = enc_mem(srng, NP, esc, sm_(), 1)
+                forms.append(Form(three(code, op) + ([srng.randrange(24)] if esc == 0x3A else []), nm + ".m", p, s))
+    for _ in range(6):
+        forms.append(Form(enc_rr(NP, 0xF7, sm_(), sm_()), "maskmovq", {7: srng.randrange(16, WIN - 24)}))
     return forms
 
 

@@ -169,8 +169,8 @@ AVX_FAULT_CASES = [
     ([0xC4, 0xE2, 0x78, 0xC9, 0xC1], EXIT_FAULT, 6),        # SHA has no VEX form
     ([0x66, 0x0F, 0x3A, 0x44, 0xC1, 0x00], RUNNING, None),  # pclmulqdq
     ([0x62, 0xF1, 0x7C, 0x48, 0x58, 0xC1], EXIT_UNIMPLEMENTED, None),  # EVEX vaddps zmm: AVX-512
-    ([0x0F, 0x38, 0x00, 0xC1], EXIT_UNIMPLEMENTED, None),   # pshufb mm, mm (MMX form, defined)
-    ([0x0F, 0x3A, 0x0F, 0xC1, 0x01], EXIT_UNIMPLEMENTED, None),  # palignr mm, mm, 1
+    ([0x0F, 0x38, 0x00, 0xC1], RUNNING, None),              # pshufb mm, mm (SSSE3 on mm registers, U41)
+    ([0x0F, 0x3A, 0x0F, 0xC1, 0x01], RUNNING, None),        # palignr mm, mm, 1 (U41)
 ]
 
 

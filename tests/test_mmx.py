@@ -154,13 +154,16 @@ FAULT_CASES = [
     ([0x0F, 0xD7, 0x06], {}, EXIT_FAULT, 6),                          # pmovmskb of memory
     ([0x0F, 0xE7, 0xC1], {}, EXIT_FAULT, 6),                          # movntq to a register
     ([0x0F, 0xD6, 0xC1], {}, EXIT_FAULT, 6),                          # 0f d6 without a prefix
-    ([0x0F, 0xF7, 0xC1], {}, EXIT_UNIMPLEMENTED, None),               # maskmovq
+    ([0x0F, 0xF7, 0xC1], {}, RUNNING, None),                          # maskmovq, no byte selected (U37)
+    ([0x0F, 0xF7, 0x06], {}, EXIT_FAULT, 6),                          # maskmovq with a memory operand
     ([0x0F, 0x2A, 0xC1], {}, RUNNING, None),                          # cvtpi2ps xmm0, mm1
     ([0x0F, 0x2A, 0xC1], dict(fsw=0x8081, fcw=0x37E), EXIT_FAULT, 16),  # an mm source: #MF first
     ([0x0F, 0x2A, 0x06], dict(fsw=0x8081, fcw=0x37E), RUNNING, None),   # an m64 source: no x87 state touched
     ([0x0F, 0x2D, 0xC1], dict(fsw=0x8081, fcw=0x37E), EXIT_FAULT, 16),  # cvtps2pi: an mm destination
     ([0x66, 0x0F, 0x2D, 0x06], {}, EXIT_FAULT, 13),                   # cvtpd2pi mm0, [rsi]: m128 needs alignment
-    ([0x0F, 0x38, 0x01, 0xC1], {}, EXIT_UNIMPLEMENTED, None),         # phaddw mm (SSSE3)
+    ([0x0F, 0x38, 0x01, 0xC1], {}, RUNNING, None),                    # phaddw mm (SSSE3 on mm registers, U41)
+    ([0x0F, 0x38, 0x01, 0xC1], dict(fsw=0x8081, fcw=0x37E), EXIT_FAULT, 16),  # ... #MF first
+    ([0x0F, 0x38, 0x0C, 0xC1], {}, EXIT_FAULT, 6),                    # 0f 38 0c without 66: no instruction (U36)
 ]
 
 

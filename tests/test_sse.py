@@ -146,7 +146,7 @@ SSE_FAULT_CASES = [
     ([0x0F, 0x2B, 0xC1], EXIT_FAULT, 6),              # movntps reg form: #UD
     ([0x0F, 0xC3, 0xC1], EXIT_FAULT, 6),              # movnti reg form: #UD
     ([0x0F, 0xEF, 0xC1], RUNNING, None),              # MMX pxor mm0, mm1 (U37)
-    ([0x0F, 0xF7, 0xC1], EXIT_UNIMPLEMENTED, None),   # MMX maskmovq
+    ([0x0F, 0xF7, 0xC1], RUNNING, None),              # MMX maskmovq (no byte selected: nothing written)
     ([0x0F, 0x58, 0xC1], RUNNING, None),              # addps (floating point, U39)
     ([0xF2, 0x0F, 0xF0, 0x03], RUNNING, None),        # lddqu (SSE3, U39)
     ([0x0F, 0x53, 0xC1], RUNNING, None),              # rcpps (the host CPU's table, U40)

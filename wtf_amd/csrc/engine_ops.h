@@ -392,7 +392,7 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u, bool m32 = false)
       const u32 pfx3 = u.rep == 0xf3 ? 2 : u.rep == 0xf2 ? 3 : p66 ? 1 : 0;
       const u32 m3 = c == 0x38 ? 2 : 3;
       if ((c == 0x38 && (c3 == 0x00 || c3 == 0x17)) || fp_form(m3, c3, pfx3, false) || s4_form(m3, c3, pfx3, false) ||
-          x42_form(m3, c3, pfx3, false) || gx_form(m3, c3, pfx3, false)) {
+          x42_form(m3, c3, pfx3, false) || gx_form(m3, c3, pfx3, false) || (pfx3 == 0 && ssse3_mm(m3, c3))) {
         smap = c == 0x38 ? 2 : 3;
         e = smap == 3 ? kSseModrmImm : kSseModrm;
         c = c3;
@@ -599,7 +599,8 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u, bool m32 = false)
       } else {
         u.bsz = u.rep == 0xf3 ? 2 : u.rep == 0xf2 ? 3 : p66 ? 1 : 0;
         u.opreg = smap << 8;
-        if (smap == 1 && ((u.bsz == 0 && mmx_opcode(c)) || (c == 0xd6 && u.bsz >= 2)))
+        if ((smap == 1 && ((u.bsz == 0 && mmx_opcode(c)) || (c == 0xd6 && u.bsz >= 2))) ||
+            (u.bsz == 0 && ssse3_mm(smap, c)))
           u.opreg |= kMmxForm;  // U37: engine_sse.h mmx_exec
         else if (!sse_valid(smap, c, u.bsz, u.is_mem, u.reg & 7))
           u.op = (c == 0xae && smap == 1) ? O_SYS2 : O_UNIMPL;

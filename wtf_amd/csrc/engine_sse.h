@@ -450,6 +450,10 @@ constexpr u32 kMmxForm = 1u << 20;
 __host__ __device__ inline bool mmx_opcode(u32 c) {
   return (c >= 0x60 && c <= 0x7f && !(c >= 0x78 && c <= 0x7d)) || c == 0xc4 || c == 0xc5 || (c >= 0xd0 && c <= 0xfe);
 }
+// the SSSE3 forms on mm registers (no prefix): 0f 38 00-0b / 1c-1e, 0f 3a 0f palignr
+__host__ __device__ inline bool ssse3_mm(u32 map, u32 c) {
+  return map == 2 ? (c <= 0x0b || (c >= 0x1c && c <= 0x1e)) : (map == 3 && c == 0x0f);
+}
 __device__ __forceinline__ u64 mmx_get(const wtfgpu_regs_t &F, u32 i) { return F.fpst[(i - ((F.fpsw >> 11) & 7)) & 7]; }
 __device__ __forceinline__ void mmx_commit(wtfgpu_regs_t &F) {
   const u32 tos = (F.fpsw >> 11) & 7;
@@ -482,9 +486,10 @@ __device__ __noinline__ int mmx_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
   const u32 imm = (u32)u.imm & 0xff;
   const u64 ea = mem ? sse_ea(P, L, u, nrip) : 0;
   wtfgpu_regs_t &F = P.full[L.lane];
-  bool ud = pc == 0 && (c == 0xd0 || c == 0xd6 || c == 0xe6 || c == 0xf0 || c == 0x6c || c == 0x6d);
-  if (!ud && c == 0xf7) return X_UNIMPL;  // maskmovq
-  if (c >= 0x71 && c <= 0x73)
+  const u32 map = vex_map(u.opreg);  // 1, or 2 / 3 for the SSSE3 forms (ssse3_mm)
+  bool ud = map == 1 && pc == 0 && (c == 0xd0 || c == 0xd6 || c == 0xe6 || c == 0xf0 || c == 0x6c || c == 0x6d);
+  if (map == 1 && c == 0xf7) ud = ud || mem;  // maskmovq: register operands only
+  if (map == 1 && c >= 0x71 && c <= 0x73)
     ud = ud || mem || !(c == 0x73 ? (r3 == 2 || r3 == 6) : (r3 == 2 || r3 == 4 || r3 == 6));
   ud = ud || ((c == 0xc5 || c == 0xd7 || (c == 0xd6 && pc)) && mem) || (c == 0xe7 && !mem) || (L.cr0 & 4);
   if (ud) {
@@ -499,8 +504,49 @@ __device__ __noinline__ int mmx_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
     set_fault(L, 16, 0, 0);  // #MF: a pending unmasked x87 exception
     return X_FAULT;
   }
-  if (c == 0x77) {  // emms
+  if (map == 1 && c == 0x77) {  // emms
     F.fptw = 0xffff;
+    return X_OK;
+  }
+  if (map >= 2) {  // SSSE3 on mm registers: the 128-bit lane ops on the low quadwords (U41)
+    const u64 av = mmx_get(F, mr);
+    u64 bv;
+    if (mem) {
+      if (!vread(L, ea, 8, bv)) return X_FAULT;
+    } else {
+      bv = mmx_get(F, mrm);
+    }
+    u64 res = 0;
+    if (map == 3) {  // palignr: (a:b) >> 8 * imm, the low quadword
+      res = imm >= 16 ? 0 : imm >= 8 ? (imm == 8 ? av : av >> (8 * (imm - 8))) : imm == 0 ? bv
+                                                   : (bv >> (8 * imm)) | (av << (64 - 8 * imm));
+    } else if (c == 0x00) {  // pshufb: index bits 2:0, bit 7 zeroes
+      for (u32 i = 0; i < 8; i++) {
+        const u32 k = (u32)(bv >> (8 * i)) & 0xff;
+        if (!(k & 0x80)) res |= ((av >> (8 * (k & 7))) & 0xff) << (8 * i);
+      }
+    } else if ((c >= 0x01 && c <= 0x03) || (c >= 0x05 && c <= 0x07)) {  // horizontal: pairs of a, then of b
+      res = s4_lane2(c, X128{av, bv}, X128{0, 0}).lo;
+    } else {
+      res = s4_lane2(c, X128{av, 0}, X128{bv, 0}).lo;
+    }
+    mmx_commit(F);
+    mmx_put(F, mr, res);
+    return X_OK;
+  }
+  if (c == 0xf7) {  // maskmovq mm1, mm2: the bytes of mm1 whose mm2 byte has bit 7 set, to [rdi]
+    const u64 av = mmx_get(F, mr), sel = mmx_get(F, mrm);
+    u64 di = R(L, 7);
+    if (u.p67) di &= 0xffffffffull;
+    if (u.seg) di += u.seg == 4 ? P.fs_base[L.lane] : P.gs_base[L.lane];
+    for (u32 i = 0; i < 8; i++)  // every written byte's page checked first
+      if (((sel >> (8 * i + 7)) & 1) && !span_ok(L, di + i, 1, ACC_WPROBE)) return X_FAULT;
+    tn_mute(L.lane);
+    bool ok = true;
+    for (u32 i = 0; ok && i < 8; i++)
+      if ((sel >> (8 * i + 7)) & 1) ok = vwrite(L, di + i, 1, (av >> (8 * i)) & 0xff);
+    if (!tn_unmute(L.lane, di, 8, TN_W, ok)) return X_FAULT;
+    mmx_commit(F);
     return X_OK;
   }
   if (c == 0xd6) {  // f3: movq2dq xmm, mm; f2: movdq2q mm, xmm
