@@ -2643,8 +2643,23 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
     }
     case 0xc6:
     case 0xc7: {
-      if ((d->reg & 7) != 0) { /* the reserved forms; xabort / xbegin: RTM, defined, not executed (U45) */
-        if ((d->reg & 7) == 7 && !d->is_mem && (d->rm & 7) == 0) return X_UNIMPL;
+      if ((d->reg & 7) != 0) { /* the reserved forms; xabort / xbegin: RTM (U48) */
+        if ((d->reg & 7) == 7 && !d->is_mem && (d->rm & 7) == 0) {
+          if (op == 0xc6) return X_OK; /* xabort imm8: no transaction is ever active, a no-op */
+          if (osz == 2) return X_UNIMPL; /* xbegin rel16 */
+          /* xbegin rel32: the transaction aborts at once (RTM_ALWAYS_ABORT): EAX = 0 (no
+           * abort cause), execution continues at the fallback address */
+          u64 rel = 0;
+          memcpy(&rel, d->bytes + d->len - 4, 4);
+          const u64 target = (nrip + sxn(rel, 4)) & sm;
+          if (!d->m32 && !is_canonical(target)) {
+            fault(m, WTFGPU_VEC_GP, 0);
+            return X_FAULT;
+          }
+          m->r.gpr[0] = 0;
+          *next_rip = target;
+          return X_OK;
+        }
         fault(m, WTFGPU_VEC_UD, 0);
         return X_FAULT;
       }

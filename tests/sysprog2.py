@@ -154,7 +154,11 @@ K = {  # ring 0 (each ends with hlt; a fault ends the lane)
     "ud_0f": ".byte 0x0f, 0xff, 0xc0\n hlt",
     "ud_b9": ".byte 0x0f, 0xb9, 0xc0\n hlt",
     "ud_0e": ".byte 0x0f, 0x0e\n hlt",
-    "ud_xbegin": ".byte 0xc7, 0xf8, 0, 0, 0, 0\n hlt",
+    # RTM with every transaction aborted at xbegin (U48): rax = 0 at the fallback, which skips a hlt;
+    # xabort outside a transaction is a no-op, xtest sets ZF
+    "rtm": "mov eax, 0x1234\n .byte 0xc7, 0xf8, 1, 0, 0, 0\n hlt\n mov ebx, eax\n .byte 0xc6, 0xf8, 0x11\n"
+           " .byte 0x0f, 0x01, 0xd6\n hlt",
+    "xend_gp": ".byte 0x0f, 0x01, 0xd5\n hlt",  # xend outside a transaction: #GP(0)
     "ud_8f": ".byte 0x8f, 0xc8\n hlt",
     "ud_fe": ".byte 0xfe, 0xd0\n hlt",
     "ud_jmpe": ".byte 0x0f, 0xb8, 0xc0\n hlt",

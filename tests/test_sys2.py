@@ -94,6 +94,7 @@ def test_cpuid_table(space):
     r = _one(space, "cpuid", r8=7, r9=0)
     assert r["gpr"][3] & (1 << 5)                            # AVX2
     assert r["gpr"][3] >> 30 == 3 and r["gpr"][3] & (1 << 16)  # AVX512F / BW / VL
+    assert r["gpr"][3] & (1 << 11) and r["gpr"][2] & (1 << 11)  # RTM, RTM_ALWAYS_ABORT (U48)
 
 
 def test_cmpxchg16b(space):
@@ -157,8 +158,17 @@ def test_ud_opcodes(space):
     for n in ("ud_0f", "ud_b9", "ud_0e", "ud_8f", "ud_fe", "ud_jmpe", "ud_getsec", "movcs"):
         assert _one(space, n)["exit"][:2] == (FAULT, 6), n
     # defined on some CPU, not executed: an engine error, never a #UD crash (U45)
-    for n in ("ud_evex", "ud_xbegin"):
+    for n in ("ud_evex",):
         assert _one(space, n)["exit"][0] == UNIMPL, n
+
+
+def test_rtm_always_aborts(space):
+    """U48: xbegin aborts at once (EAX = 0, the fallback address), xabort is a
+    no-op and xtest reports no transaction (ZF = 1); xend is #GP(0); CPUID
+    enumerates RTM and RTM_ALWAYS_ABORT."""
+    r = _one(space, "rtm", rbx=0x5555)
+    assert r["exit"][0] == HLT and r["gpr"][0] == 0 and r["gpr"][3] == 0 and r["rflags"] & 0x40
+    assert _one(space, "xend_gp")["exit"][:2] == (FAULT, 13)
 
 
 # ---------------------------------------------------------------- engine code on the host vs the oracle
@@ -217,7 +227,7 @@ def test_engine_code_matches_oracle(space):
     assert {(HLT, 0), (INT3, 0), (FAULT, 6), (FAULT, 13), (FAULT, 14), (FAULT, 11), (FAULT, 7)} <= kinds, kinds
     # nothing leaves the engine but the defined-not-executed forms (U45)
     unimpl = {names.get(ln[i][0]) or names.get(ln[i][1][3]) for i, w in enumerate(want) if w["exit"][0] == UNIMPL}
-    assert unimpl <= {"ud_evex", "ud_xbegin"}, unimpl
+    assert unimpl <= {"ud_evex"}, unimpl
 
 
 # ---------------------------------------------------------------- GPU vs the oracle

@@ -561,7 +561,11 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u, bool m32 = false)
       case G_8F:
       case G_C6:
         if (r3 != 0) u.op = O_UD;  // xop and the reserved forms: #UD
-        if (grp == G_C6 && r3 == 7 && !u.is_mem && (u.rm & 7) == 0) u.op = O_UNIMPL;  // xabort / xbegin: RTM (U45)
+        if (grp == G_C6 && r3 == 7 && !u.is_mem && (u.rm & 7) == 0) {  // xabort / xbegin: RTM (U48)
+          u.op = O_SYS2;
+          u.asz = osz;
+          u.bsz = sstk;
+        }
         break;
       case G_BA:
         if (r3 < 4) u.op = O_UD;

@@ -142,9 +142,11 @@ __device__ __noinline__ void cpuid_leaf(u64 cr4, u64 xcr0, u32 leaf, u32 sub, u3
            (1u << 23) | (1u << 25) | (1u << 26) | (osxsave << 27) | (1u << 28) | (1u << 29) | (1u << 30);
     r[3] = 0x078bfbfd;
   } else if (leaf == 7) {
-    if (sub == 0)  // FSGSBASE BMI1 AVX2 BMI2 ERMS AVX512F ADX SHA AVX512BW AVX512VL (U47)
-      r[1] = (1u << 0) | (1u << 3) | (1u << 5) | (1u << 8) | (1u << 9) | (1u << 16) | (1u << 19) | (1u << 29) |
-             (1u << 30) | (1u << 31);
+    if (sub == 0) {  // FSGSBASE BMI1 AVX2 BMI2 ERMS RTM AVX512F ADX SHA AVX512BW AVX512VL (U47, U48)
+      r[1] = (1u << 0) | (1u << 3) | (1u << 5) | (1u << 8) | (1u << 9) | (1u << 11) | (1u << 16) | (1u << 19) |
+             (1u << 29) | (1u << 30) | (1u << 31);
+      r[3] = 1u << 11;  // RTM_ALWAYS_ABORT: xbegin always aborts (U48)
+    }
   } else if (leaf == 0xd) {
     if (sub == 0) {
       r[0] = 0xff;
@@ -740,6 +742,16 @@ __device__ __noinline__ int sys2_exec(const Dev &P, Lane &L, const UOp &u, u64 n
         if (cpl > lane_iopl(L)) return fault_x(L, WTFGPU_VEC_GP, 0);
         setr(L, u.rex, 0, (c & 1) ? (osz == 2 ? 2 : 4) : 1, ~0ull);
         return X_OK;
+      case 0xc6:  // xabort imm8: no transaction is ever active, a no-op (U48)
+        return X_OK;
+      case 0xc7: {  // xbegin rel32: the transaction aborts at once, EAX = 0, rip = the fallback (U48)
+        if (osz == 2) return X_UNIMPL;
+        const u64 target = (nrip + sext(u.imm & 0xffffffffull, 4)) & smask;
+        if (!m32 && !canonical(target)) return fault_x(L, WTFGPU_VEC_GP, 0);
+        RS(L, 0, 0);
+        next = target;
+        return X_OK;
+      }
       case 0xe6: case 0xe7: case 0xee: case 0xef:  // out
         if (cpl > lane_iopl(L)) return fault_x(L, WTFGPU_VEC_GP, 0);
         return X_OK;
@@ -958,6 +970,11 @@ __device__ __noinline__ int sys2_exec(const Dev &P, Lane &L, const UOp &u, u64 n
             return fault_x(L, WTFGPU_VEC_GP, 0);
           F.xcr0 = v;
           L.simd = simd_bits(L.cr0, S.cr4, v);
+          return X_OK;
+        }
+        if (modrm == 0xd5) return fault_x(L, WTFGPU_VEC_GP, 0);  // xend outside a transaction (U48)
+        if (modrm == 0xd6) {                                     // xtest: never in a transaction
+          L.rflags = (L.rflags & ~F_STATUS) | F_ZF;
           return X_OK;
         }
         if (r3 != 6) return fault_x(L, WTFGPU_VEC_UD, 0);
