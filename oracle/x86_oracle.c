@@ -2376,8 +2376,45 @@ static int exec_insn(orc_machine *m, insn *d, memref *mr, u64 *next_rip) {
     case 0x06: case 0x07: case 0x0e: case 0x16: case 0x17: case 0x1e: case 0x1f: case 0x27: case 0x2f:
     case 0x37: case 0x3f: case 0x60: case 0x61: case 0x9a: case 0xce: case 0xd4: case 0xd5: case 0xea:
       return exec_sys32(m, d, next_rip);
-    case 0x62: case 0x63: case 0xc4: case 0xc5: case 0xd6: /* bound, arpl, les / lds, salc */
-      return X_UNIMPL;
+    case 0x62: { /* bound r, m16&16 / m32&32: #BR (vector 5) unless lower <= index <= upper, signed */
+      if (!d->is_mem) {
+        fault(m, WTFGPU_VEC_UD, 0);
+        return X_FAULT;
+      }
+      u64 lo = 0, hi = 0;
+      CHK(vread(m, d->ea, (u32)osz, &lo));
+      CHK(vread(m, d->ea + (u64)osz, (u32)osz, &hi));
+      const i64 ix = (i64)sxn(getreg(m, d, d->reg, osz), osz);
+      if (ix < (i64)sxn(lo, osz) || ix > (i64)sxn(hi, osz)) {
+        fault(m, 5, 0);
+        return X_FAULT;
+      }
+      return X_OK;
+    }
+    case 0x63: { /* arpl r/m16, r16: SDM ARPL */
+      u64 dv = 0;
+      CHK(d->is_mem ? rd_rm_rmw(m, d, 2, &dv) : rd_rm(m, d, 2, &dv));
+      const u64 rpl = m->r.gpr[d->reg & 15] & 3;
+      const int adj = (dv & 3) < rpl;
+      if (adj) CHK(wr_rm(m, d, 2, (dv & ~3ULL) | rpl));
+      m->r.rflags = (m->r.rflags & ~RF_ZF) | (adj ? RF_ZF : 0);
+      return X_OK;
+    }
+    case 0xc4: case 0xc5: { /* les / lds r, m16:osz (U30) */
+      if (!d->is_mem) {
+        fault(m, WTFGPU_VEC_UD, 0);
+        return X_FAULT;
+      }
+      u64 off = 0, sel = 0;
+      CHK(vread(m, d->ea, (u32)osz, &off));
+      CHK(vread(m, d->ea + (u64)osz, 2, &sel));
+      if (load_sreg(m, op == 0xc4 ? WTFGPU_ES : WTFGPU_DS, (u16)sel)) return X_FAULT;
+      setreg(m, d, d->reg, osz, off);
+      return X_OK;
+    }
+    case 0xd6: /* salc */
+      m->r.gpr[0] = (m->r.gpr[0] & ~0xffULL) | ((m->r.rflags & RF_CF) ? 0xffULL : 0);
+      return X_OK;
     default:
       break;
     }
@@ -3536,6 +3573,9 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
       break;
     case 0x82: /* 32-bit code: 80's alias */
       if (d->m32) has_modrm = imm = 1;
+      break;
+    case 0x62: case 0xc4: case 0xc5: /* 32-bit code: bound, les / lds (c4 / c5 with mod != 11) */
+      if (d->m32) has_modrm = 1;
       break;
     case 0x9a: case 0xea: /* 32-bit code: far call / jmp ptr16:32 */
       if (d->m32) imm = osz + 2;

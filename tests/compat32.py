@@ -76,6 +76,8 @@ U32 = {
     "a16": "addr16 mov eax, [bx]\n int3",
     "bound": "bound eax, [esi]\n int3",
     "arpl": "arpl ax, bx\n int3",
+    "lds": "lds ecx, [esi]\n int3",
+    "salc": "stc\n .byte 0xd6\n mov ebx, eax\n clc\n .byte 0xd6\n int3",
     "jmp16": ".byte 0x66, 0xe9, 0x00, 0x00\n int3",
     "ud2": "ud2",
     # andn eax, esi, edi with VEX.W1: 32-bit code runs it at 32 bits (W1 ignored)
@@ -129,6 +131,7 @@ def build_space():
     rng = random.Random(0x3232)
     d32 = bytearray(rng.getrandbits(8) for _ in range(0x1000))
     d32[0x200:0x204] = (SLOT32["jmpind"] + 0x7F).to_bytes(4, "little")  # an indirect call target (the slot's int3 pad)
+    d32[0x60:0x68] = (-5 & 0xFFFFFFFF).to_bytes(4, "little") + (100).to_bytes(4, "little")  # bound: [-5, 100]
     sp.map(DATA32, bytes(d32), user=True, write=True, nx=True)
     for i in range(2):
         sp.map(STACK32 + 0x1000 * i, b"", user=True, write=True, nx=True)

@@ -94,9 +94,42 @@ def test_mode_switches(space):
 
 
 def test_outside_forms_and_ud(space):
-    for n in ("les", "a16", "bound", "arpl", "jmp16"):
+    for n in ("a16", "jmp16"):
         assert _one(space, n, rsi=T.DATA32)["exit"][0] == UNIMPL, n
     assert _one(space, "ud2")["exit"][:2] == (FAULT, 6)
+
+
+def _sx32(v):
+    return v - (1 << 32) if v & 0x80000000 else v
+
+
+def test_bound_arpl_les_lds_salc(space):
+    """The one-byte forms only 32-bit code has (SDM BOUND, ARPL, LDS / LES,
+    SALC; U29 / U30): bound faults #BR (vector 5) outside [lower, upper]
+    (signed) and is a no-op inside; arpl raises the destination's RPL to the
+    source's with ZF; les / lds load the offset and the selector (es / ds keep
+    only the selector, U30); salc sets AL from CF."""
+    sp, st, lay, data = space
+    for off in (0x40, 0x60):  # random bounds (here lower > upper: always #BR), and [-5, 100]
+        esi = T.DATA32 + off
+        lo = _sx32(int.from_bytes(data[off:off + 4], "little"))
+        hi = _sx32(int.from_bytes(data[off + 4:off + 8], "little"))
+        for ix in (lo, hi, lo - 1, hi + 1, (lo + hi) // 2, -1, 0):
+            if not -(1 << 31) <= ix < (1 << 31):
+                continue
+            want = (INT3, 0) if lo <= ix <= hi else (FAULT, 5)
+            assert _one(space, "bound", rsi=esi, rax=ix & M32)["exit"][:2] == want, (ix, lo, hi)
+    r = _one(space, "arpl", rax=0x10, rbx=0x3)
+    assert r["exit"][0] == INT3 and r["gpr"][0] & 0xFFFF == 0x13 and r["rflags"] & 0x40
+    r = _one(space, "arpl", rax=0x13, rbx=0x1)
+    assert r["gpr"][0] & 0xFFFF == 0x13 and not r["rflags"] & 0x40
+    for n, reg, sreg in (("les", 0, 0), ("lds", 1, 3)):
+        r = _one(space, n, rsi=T.DATA32 + 0x10)
+        assert r["exit"][0] == INT3, n
+        assert r["gpr"][reg] == int.from_bytes(data[0x10:0x14], "little"), n
+        assert r["sel"][sreg] == int.from_bytes(data[0x14:0x16], "little"), n
+    r = _one(space, "salc", rax=0x12345600)
+    assert r["exit"][0] == INT3 and r["gpr"][3] & 0xFF == 0xFF and r["gpr"][0] == 0x12345600
 
 
 def test_vex_w1_gpr_form_is_32_bit(space):

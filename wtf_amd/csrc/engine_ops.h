@@ -215,7 +215,7 @@ constexpr u32 kUnimpl = UN;
 // leaves #UD that engine_sys.h runs (push / pop es cs ss ds, pusha / popa,
 // daa das aaa aas, far call / jmp ptr16:32, into, aam / aad)
 constexpr u32 kIncDec32 = E(O_INCDEC, L_OPREG, 0, Z_V, Z_V, 1, 1, 0, 0, K_NONE, 0);
-constexpr u32 kSys32 = S2, kSys32B = S2B;
+constexpr u32 kSys32 = S2, kSys32B = S2B, kSys32M = S2M;
 #undef E
 #undef UN
 #undef UDE
@@ -421,8 +421,10 @@ __device__ __forceinline__ int decode(const IBytes &b, UOp &u, bool m32 = false)
                c == 0x27 || c == 0x2f || c == 0x37 || c == 0x3f || c == 0x60 || c == 0x61 || c == 0x9a ||
                c == 0xce || c == 0xea)
         e = kSys32;
-      else if (c == 0x62 || c == 0x63 || c == 0xc4 || c == 0xc5 || c == 0xd6)
-        e = kUnimpl;  // bound, arpl, les / lds, salc (U29)
+      else if (c == 0x62 || c == 0x63 || c == 0xc4 || c == 0xc5)
+        e = kSys32M;  // bound, arpl, les / lds (U29): engine_sys.h
+      else if (c == 0xd6)
+        e = kSys32;  // salc
     }
   }
   const u32 osz = rexw ? 8 : (p66 ? 2 : 4);

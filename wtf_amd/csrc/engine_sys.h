@@ -742,6 +742,47 @@ __device__ __noinline__ int sys2_exec(const Dev &P, Lane &L, const UOp &u, u64 n
         if (cpl > lane_iopl(L)) return fault_x(L, WTFGPU_VEC_GP, 0);
         setr(L, u.rex, 0, (c & 1) ? (osz == 2 ? 2 : 4) : 1, ~0ull);
         return X_OK;
+      // 32-bit code only (decode routes them here in compatibility mode, U29)
+      case 0x62: {  // bound r, m16&16 / m32&32: #BR unless lower <= index <= upper (signed)
+        if (!u.is_mem) return fault_x(L, WTFGPU_VEC_UD, 0);
+        u64 lo, hi;
+        if (!vread(L, ea, osz, lo) || !vread(L, ea + osz, osz, hi)) return X_FAULT;
+        const i64 ix = (i64)sext(R(L, u.reg) & szmask(osz), osz);
+        if (ix < (i64)sext(lo, osz) || ix > (i64)sext(hi, osz)) return fault_x(L, 5, 0);
+        return X_OK;
+      }
+      case 0x63: {  // arpl r/m16, r16: the destination selector's RPL raised to the source's (ZF = 1), else ZF = 0
+        u64 d;
+        if (u.is_mem) {
+          if (!vread(L, ea, 2, d, ACC_W)) return X_FAULT;
+        } else {
+          d = R(L, u.rm) & 0xffff;
+        }
+        const u64 rpl = R(L, u.reg) & 3;
+        const bool adj = (d & 3) < rpl;
+        if (adj) {
+          d = (d & ~3ull) | rpl;
+          if (u.is_mem) {
+            if (!vwrite(L, ea, 2, d)) return X_FAULT;
+          } else {
+            setr(L, 0, u.rm, 2, d);
+          }
+        }
+        L.rflags = (L.rflags & ~F_ZF) | (adj ? F_ZF : 0);
+        return X_OK;
+      }
+      case 0xc4:
+      case 0xc5: {  // les / lds r, m16:osz (c4 / c5 with a memory ModRM in 32-bit code; U30 for es / ds)
+        if (!u.is_mem) return fault_x(L, WTFGPU_VEC_UD, 0);
+        u64 off, sel;
+        if (!vread(L, ea, osz, off) || !vread(L, ea + osz, 2, sel)) return X_FAULT;
+        if (!load_sreg(P, L, c == 0xc4 ? WTFGPU_ES : WTFGPU_DS, (u32)sel, true)) return X_FAULT;
+        setr(L, 0, u.reg, osz, off);
+        return X_OK;
+      }
+      case 0xd6:  // salc: AL = CF ? ff : 00, flags kept
+        RS(L, 0, (R(L, 0) & ~0xffull) | ((L.rflags & F_CF) ? 0xffull : 0));
+        return X_OK;
       case 0xc6:  // xabort imm8: no transaction is ever active, a no-op (U48)
         return X_OK;
       case 0xc7: {  // xbegin rel32: the transaction aborts at once, EAX = 0, rip = the fallback (U48)
