@@ -3432,7 +3432,7 @@ static int decode(orc_machine *m, insn *d, memref *mr) {
     les = (nb & 0xc0) != 0xc0;
     d->pos = (u32)save;
   }
-  zform ezf = {ZK_NONE, 0, 0, 0, 0};
+  zform ezf = {ZK_NONE, 0, 0, 0, 0, 0};
   if (b == 0x62 && !d->m32) { /* EVEX (U47; 32-bit code's bound stays outside) */
     const u8 p0 = fetch8(m, d), p1 = fetch8(m, d), p2 = fetch8(m, d);
     b = fetch8(m, d);

@@ -14,12 +14,12 @@ elements never touch the page) and the #PF a selected element takes. Faults are 
 Forms (EVEX, 128 / 256 / 512 bits, merging and zeroing masks, register,
 memory, disp8*N and disp32, embedded broadcasts):
   vmovups / upd / aps / apd, vmovdqa32 / 64, vmovdqu8 / 16 / 32 / 64 (loads,
-  stores, register moves), vpand / andn / or / xor d q, vpadd / vpsub b w d q,
+  stores, register moves), vmovntps / pd / dq and vmovntdqa, vpand / andn / or / xor d q, vpadd / vpsub b w d q,
   vpminub / uw, vpmaxub / uw, vpcmpeq / gt b w d q, vpcmp(u) b w d q (every
   predicate), vptestm / vptestnm b w d q, vpternlog d q, vpbroadcast b w d q
   from xmm / memory / GPR; plus the VEX opmask instructions kmov b w d q
   (k / m / r forms), kand / andn / or / xnor / xor, knot, kortest, ktest,
-  kshiftl / r, and the #UD encodings (z with a k or memory destination, b in a
+  kshiftl / r, kadd, kunpck, and the #UD encodings (z with a k or memory destination, b in a
   register form or a non-broadcast form, L'L = 11, vvvv in two-operand forms,
   a prefix before 62, the reserved P0 / P1 bits).
 
@@ -145,6 +145,9 @@ def evex_forms():
                                ("vpcmpw", 0x3F, 1, 2, 0), ("vpcmpud", 0x1E, 0, 4, 1), ("vpcmpuq", 0x1E, 1, 8, 1),
                                ("vpcmpd", 0x1F, 0, 4, 1), ("vpcmpq", 0x1F, 1, 8, 1)):
         F.append((nm, 3, 1, w, opc, "kd", es, {"bc": bc, "imm": 1}))
+    # the non-temporal moves (memory only, no masking: a register form or aaa != 0 is #UD)
+    F += [("vmovntps", 1, 0, 0, 0x2B, "st", 4, {"al": 1}), ("vmovntpd", 1, 1, 1, 0x2B, "st", 8, {"al": 1}),
+          ("vmovntdq", 1, 1, 0, 0xE7, "st", 4, {"al": 1}), ("vmovntdqa", 2, 1, 0, 0x2A, "ld", 4, {"al": 1})]
     return F
 
 
@@ -182,6 +185,9 @@ def gen_evex_cases(rng):
             if kind == "bcr":
                 mem = False
             aaa = 0 if rng.random() < 0.25 else rng.randrange(1, 8)
+            if nm.startswith("vmovnt"):  # mostly the valid form: memory, no mask
+                mem = rng.random() < 0.85
+                aaa = 0 if rng.random() < 0.8 else aaa
             zok = kind not in ("kd",) and not (kind == "st" and mem)
             z = 1 if zok and rng.random() < 0.4 else 0
             b = 1 if mem and ex.get("bc") and rng.random() < 0.4 else 0
@@ -307,6 +313,12 @@ def gen_kop_cases(rng):
                                                                   rm=r.randrange(16)), {})] * 6
         K += [("kmov" + sfx + ".tor", lambda r, pp=pp, w=w: vex3(1, pp, w, 0, r.randrange(16), 0, 0x93,
                                                                 rm=r.randrange(8)), {})] * 6
+    for pp, w, sfx in ((0, 0, "w"), (0, 1, "q"), (1, 0, "b"), (1, 1, "d")):
+        K += [("kadd" + sfx, lambda r, pp=pp, w=w: vex3(1, pp, w, 1, r.randrange(8), r.randrange(8), 0x4A,
+                                                         rm=r.randrange(8)), {})] * 6
+    for pp, w, sfx in ((1, 0, "bw"), (0, 0, "wd"), (0, 1, "dq")):
+        K += [("kunpck" + sfx, lambda r, pp=pp, w=w: vex3(1, pp, w, 1, r.randrange(8), r.randrange(8), 0x4B,
+                                                           rm=r.randrange(8)), {})] * 6
     for opc, nm in ((0x30, "kshiftr"), (0x31, "kshiftr"), (0x32, "kshiftl"), (0x33, "kshiftl")):
         for w in (0, 1):
             bits = (64 if w else 32) if opc & 1 else (16 if w else 8)

@@ -2,7 +2,7 @@
 // logic, add / sub, unsigned min / max, compares and tests into opmask
 // registers, vpternlog and broadcasts at 128 / 256 / 512 bits with merging or
 // zeroing masks, and the VEX-encoded opmask instructions (kmov, kortest,
-// ktest, the k logic and shifts) — what vectorised memcpy / memset / strlen /
+// ktest, kadd, kunpck, the k logic and shifts) — what vectorised memcpy / memset / strlen /
 // memchr / strcmp paths built for AVX-512 run. Every other EVEX encoding is
 // UNIMPLEMENTED (U36). The state (zmm0-31, k0-7) lives in the lane's cold
 // state (wtfgpu_regs_t: xmm / ymmh / zmmh for zmm0-15, zmm_hi for 16-31, k).
@@ -33,6 +33,7 @@ enum : u32 {
 struct EForm {
   u32 kind, es, sub;  // sub: logic op (0 and 1 andn 2 or 3 xor), cmp signedness (1 signed), testm negation
   bool store, aligned, bcastok, kdest;
+  bool nt = false;    // the non-temporal moves: memory operand only, no masking (aaa != 0: #UD)
 };
 
 // The subset, by (map, opcode, pp, W). pp: 0 none, 1 66, 2 f3, 3 f2.
@@ -41,6 +42,8 @@ __host__ __device__ inline EForm evex_form(u32 map, u32 c, u32 pp, u32 w) {
   if (map == 1) {
     if ((c == 0x10 || c == 0x11 || c == 0x28 || c == 0x29) && pp <= 1 && w == pp)  // vmovups/upd, vmovaps/apd
       return EForm{EZ_MOV, pp ? 8u : 4u, 0, (c & 1) != 0, c >= 0x28, false, false};
+    if ((c == 0x2b && pp <= 1 && w == pp) || (c == 0xe7 && pp == 1 && !w))  // vmovntps / pd, vmovntdq
+      return EForm{EZ_MOV, c == 0x2b && pp ? 8u : 4u, 0, true, true, false, false, true};
     if (c == 0x6f || c == 0x7f) {
       if (pp == 1) return EForm{EZ_MOV, w ? 8u : 4u, 0, c == 0x7f, true, false, false};   // vmovdqa32 / 64
       if (pp == 2) return EForm{EZ_MOV, w ? 8u : 4u, 0, c == 0x7f, false, false, false};  // vmovdqu32 / 64
@@ -78,6 +81,7 @@ __host__ __device__ inline EForm evex_form(u32 map, u32 c, u32 pp, u32 w) {
                    true};
     if (pp != 1) return f;
     switch (c) {
+      case 0x2a: return w ? f : EForm{EZ_MOV, 4, 0, false, true, false, false, true};  // vmovntdqa
       case 0x29: return w ? EForm{EZ_CMPEQ, 8, 0, false, false, true, true} : f;
       case 0x37: return w ? EForm{EZ_CMPGT, 8, 0, false, false, true, true} : f;
       case 0x3a: return EForm{EZ_MINU, 2, 0, false, false, false, false};
@@ -113,8 +117,10 @@ __host__ __device__ inline u32 evex_disp8_n(const EForm &f, u32 vl, u32 b) {
 __host__ __device__ inline u32 kop_bits(u32 map, u32 c, u32 pp, u32 w) {
   if (map == 3) return (c >= 0x30 && c <= 0x33 && pp == 1) ? ((c & 1) ? (w ? 64u : 32u) : (w ? 16u : 8u)) : 0u;
   if (map != 1) return 0;
-  const bool grp = (c >= 0x41 && c <= 0x47 && c != 0x43) || c == 0x90 || c == 0x91 || c == 0x98 || c == 0x99;
+  const bool grp = (c >= 0x41 && c <= 0x47 && c != 0x43) || c == 0x4a || c == 0x90 || c == 0x91 || c == 0x98 ||
+                   c == 0x99;
   if (grp) return pp == 0 ? (w ? 64u : 16u) : pp == 1 ? (w ? 32u : 8u) : 0u;
+  if (c == 0x4b) return pp == 1 ? (w ? 0u : 16u) : pp == 0 ? (w ? 64u : 32u) : 0u;  // kunpckbw / wd / dq: result bits
   if (c == 0x92 || c == 0x93) return pp == 0 ? (w ? 0u : 16u) : pp == 1 ? (w ? 0u : 8u) : pp == 3 ? (w ? 64u : 32u) : 0u;
   return 0;
 }
@@ -220,6 +226,7 @@ __device__ __noinline__ int evex_exec(const Dev &P, Lane &L, const UOp &u, u64 n
   if (two && vvvv != 0) ud = true;
   if (b && (!mem || !f.bcastok)) ud = true;          // no rounding control in these forms
   if (z && (f.kdest || (f.store && mem) || aaa == 0)) ud = true;  // a k or memory destination merges only; z needs a mask
+  if (f.nt && (!mem || aaa != 0)) ud = true;                        // non-temporal moves: memory, no mask
   if (f.kind == EZ_BCASTR && mem) ud = true;
   if (ud) return z_ud(L);
   if (L.cr0 & 8) {
@@ -320,8 +327,8 @@ __device__ __noinline__ int kop_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
   const u32 vvvv = (x >> 4) & 15, bits = kop_bits(map, c, pp, w);
   wtfgpu_regs_t &F = P.full[L.lane];
   const bool mem = u.is_mem;
-  // VEX.L: 1 for the two-source logic ops, else 0; vvvv: only the two-source ops name a register
-  const bool two_src = map == 1 && c >= 0x41 && c <= 0x47 && c != 0x44;
+  // VEX.L: 1 for the two-source ops (logic, kadd, kunpck), else 0; vvvv: only they name a register
+  const bool two_src = map == 1 && ((c >= 0x41 && c <= 0x47 && c != 0x44) || c == 0x4a || c == 0x4b);
   bool ud = ((x >> 16) & 1) || !bits || l != (two_src ? 1u : 0u) || (!two_src && vvvv != 0);
   if (!((P.sys[L.lane].cr4 >> 18) & 1) || (F.xcr0 & 0xe6) != 0xe6) ud = true;
   if (mem && !(map == 1 && (c == 0x90 || c == 0x91))) ud = true;  // only kmov has memory forms
@@ -357,9 +364,16 @@ __device__ __noinline__ int kop_exec(const Dev &P, Lane &L, const UOp &u, u64 nr
       return X_OK;
     }
     case 0x44: F.k[kr] = ~F.k[km] & mk; return X_OK;
+    case 0x4b: {  // kunpck: the first source's low half above the second source's low half
+      const u32 h = bits / 2;
+      const u64 hm = kmask_bits(h);
+      F.k[kr] = ((F.k[vvvv & 7] & hm) << h) | (F.k[km] & hm);
+      return X_OK;
+    }
     default: {
       const u64 p = F.k[vvvv & 7] & mk, q = F.k[km] & mk;
-      const u64 v = c == 0x41 ? (p & q) : c == 0x42 ? (~p & q) : c == 0x45 ? (p | q) : c == 0x46 ? ~(p ^ q) : (p ^ q);
+      const u64 v = c == 0x41 ? (p & q) : c == 0x42 ? (~p & q) : c == 0x45 ? (p | q) : c == 0x46 ? ~(p ^ q)
+                  : c == 0x4a ? p + q : (p ^ q);  // 4a: kadd
       F.k[kr] = v & mk;
       return X_OK;
     }
