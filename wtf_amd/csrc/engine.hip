@@ -563,7 +563,7 @@ __device__ __forceinline__ bool uc_fill_shared(const Dev &P, UCEntry *e, UCUop *
                                                u32 lid) {
   if (!P.guc) return false;
   const u32 pj = guc_payload_index(lid);
-  u32 *head = e ? (u32 *)&e->flags : nullptr, *uop = (u32 *)&us->u;
+  u32 *head = e ? (u32 *)&e->flags : nullptr, *uop = us ? (u32 *)&us->u : nullptr;  // us null: the head only
   u32 *gw = P.guc + (u64)guc_slot(P, key) * GUC_WORDS;
   const u32 w = lid < GUC_WORDS ? gw[lid] : 0;
   const bool tag = lid < GUC_WORDS && (lid & 15) >= 14;
@@ -572,7 +572,7 @@ __device__ __forceinline__ bool uc_fill_shared(const Dev &P, UCEntry *e, UCUop *
   if (pj < GP_HEAD) {
     if (head) head[pj] = w;
   } else if (pj < GUC_PAYLOAD) {
-    uop[pj - GP_HEAD] = w;
+    if (uop) uop[pj - GP_HEAD] = w;
   }
   // UC_COVERED is cached in the shared entry once seen (coverage only grows
   // until wtfgpu_reset_coverage, which clears the shared cache): most fills
@@ -585,7 +585,7 @@ __device__ __forceinline__ bool uc_fill_shared(const Dev &P, UCEntry *e, UCUop *
   }
   __builtin_amdgcn_wave_barrier();
   if (lid == 0) {
-    us->key = key;
+    if (us) us->key = key;
     if (e) {
       e->logged = 0;
       e->flags = flags;
@@ -1166,6 +1166,9 @@ constexpr u32 STAT_N = 16;
 #ifndef WTFGPU_INLINE_ACTIONS
 #define WTFGPU_INLINE_ACTIONS 3  // SetGprs (1) / StopOk (2) actions applied without the lane copy
 #endif
+#ifndef WTFGPU_FILL_PREFETCH
+#define WTFGPU_FILL_PREFETCH 4  // entries a fill pass also brings in after the missed one (profiles/r06_ab_fill_prefetch.txt)
+#endif
 #ifndef WTFGPU_ACT_NESTED
 #define WTFGPU_ACT_NESTED 0  // the two inline actions in one nested block (the miscompiled form, A/B only)
 #endif
@@ -1498,6 +1501,26 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
         uc_fill(P, e, &uu[uu_slot(key)], key, lptr, off, grip, lid, true);
 #else
       uc_fill(P, e, &uu[uu_slot(key)], key, lptr, off, grip, lid);
+#endif
+#if WTFGPU_FILL_PREFETCH
+      // sequential prefetch: the instructions after this one in the page, from
+      // the shared cache into their sets' second (older) way, while the wave
+      // is in the slow step anyway; stops at the first that is cached, absent
+      // from the shared cache, or crosses the page
+      if (UC_WAYS == 2) {
+        u32 poff = off, pf = rfl32(e->flags), plen = (rfl32(e->f.w0) >> 20) & 0x3f;
+        for (u32 k = 0; k < WTFGPU_FILL_PREFETCH; k++) {
+          if ((pf & (UC_CROSS | UC_BADLEN)) || !plen) break;
+          poff += plen;
+          if (poff > 4096 - 16) break;
+          const u64 pkey = lptr | poff;
+          UCEntry *pe = &uc[uc_slot(pkey)];
+          if (rfl64(pe->key) == pkey || rfl64(pe[1].key) == pkey) break;
+          if (!uc_fill_shared(P, pe + 1, nullptr, pkey, poff, grip + (poff - off), lid)) break;
+          pf = rfl32(pe[1].flags);
+          plen = (rfl32(pe[1].f.w0) >> 20) & 0x3f;
+        }
+      }
 #endif
       // an entry the fast loop can run (a common op, nothing to log, no
       // breakpoint): back to it, this pass was only the fill
