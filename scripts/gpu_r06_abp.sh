@@ -1,4 +1,5 @@
-# Round 6 A/B: sequential prefetch on uop-cache fills (abp/pf0 = off, pf2, pf4),
+# Round 6 A/B: sequential prefetch on uop-cache fills and the fast loop after
+# coverage logging (abp/<variant>),
 # bench.py --no-cpu (tlv headline, HEVD I/O and bare, SYN), two passes in
 # opposite orders.
 set -o pipefail

@@ -1167,7 +1167,13 @@ constexpr u32 STAT_N = 16;
 #define WTFGPU_INLINE_ACTIONS 3  // SetGprs (1) / StopOk (2) actions applied without the lane copy
 #endif
 #ifndef WTFGPU_FILL_PREFETCH
-#define WTFGPU_FILL_PREFETCH 4  // entries a fill pass also brings in after the missed one (profiles/r06_ab_fill_prefetch.txt)
+#define WTFGPU_FILL_PREFETCH 8  // entries a fill pass also brings in after the missed one (profiles/r06_ab_fill_prefetch.txt)
+#endif
+#ifndef WTFGPU_COVER_FAST
+#define WTFGPU_COVER_FAST 1
+#endif
+#ifndef WTFGPU_FILL_PREFETCH_JUMPS
+#define WTFGPU_FILL_PREFETCH_JUMPS 0  // the prefetch chain follows direct jmp / call targets in the page
 #endif
 #ifndef WTFGPU_ACT_NESTED
 #define WTFGPU_ACT_NESTED 0  // the two inline actions in one nested block (the miscompiled form, A/B only)
@@ -1508,17 +1514,25 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       // is in the slow step anyway; stops at the first that is cached, absent
       // from the shared cache, or crosses the page
       if (UC_WAYS == 2) {
-        u32 poff = off, pf = rfl32(e->flags), plen = (rfl32(e->f.w0) >> 20) & 0x3f;
+        const UCEntry *pe = e;
+        u64 prip = grip;
         for (u32 k = 0; k < WTFGPU_FILL_PREFETCH; k++) {
+          const u32 pf = rfl32(pe->flags), pw0 = rfl32(pe->f.w0), plen = (pw0 >> 20) & 0x3f;
           if ((pf & (UC_CROSS | UC_BADLEN)) || !plen) break;
-          poff += plen;
-          if (poff > 4096 - 16) break;
+          u64 nxt = prip + plen;  // the fall-through; a direct jmp / call: its target (same page only)
+#if WTFGPU_FILL_PREFETCH_JUMPS
+          const u32 pop = pw0 & 0xff;
+          if ((pop == FO_JMP || pop == FO_CALL) && !(rfl32(pe->f.fl) & FF_BREG)) nxt += rfl64(pe->f.imm);
+          if (pop == FO_RET || ((pop == FO_JMP || pop == FO_CALL) && (rfl32(pe->f.fl) & FF_BREG))) break;
+#endif
+          if ((nxt >> 12) != (grip >> 12) || (nxt & 0xfff) > 4096 - 16) break;
+          const u32 poff = (u32)(nxt & 0xfff);
           const u64 pkey = lptr | poff;
-          UCEntry *pe = &uc[uc_slot(pkey)];
-          if (rfl64(pe->key) == pkey || rfl64(pe[1].key) == pkey) break;
-          if (!uc_fill_shared(P, pe + 1, nullptr, pkey, poff, grip + (poff - off), lid)) break;
-          pf = rfl32(pe[1].flags);
-          plen = (rfl32(pe[1].f.w0) >> 20) & 0x3f;
+          UCEntry *ps = &uc[uc_slot(pkey)];
+          if (rfl64(ps->key) == pkey || rfl64(ps[1].key) == pkey) break;
+          if (!uc_fill_shared(P, ps + 1, nullptr, pkey, poff, nxt, lid)) break;
+          pe = ps + 1;
+          prip = nxt;
         }
       }
 #endif
@@ -1551,14 +1565,26 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
 
     // ---- coverage, then breakpoint (bochscpu_backend.cc:501-547)
     if (P.trace && ing && !skip) trace_rip(P, L.lane, grip);  // a resumed breakpoint was logged at its hit
+    bool logged_now = false;  // wave-uniform
     if (cov_on && !(flags & UC_COVERED)) {
       const u64 logged = rfl64(e->logged);
       if (gmask & ~logged) {
         L.ccnt = cover(P, grip, ing && !((logged >> lid) & 1), L.lane, L.cgen, L.ccnt);
         if (lid == 0) e->logged = logged | gmask;
+        logged_now = true;
       }
     }
     STAMP(3);
+#if WTFGPU_COVER_FAST
+    // the group has just logged the rip (its lanes are all in the entry's mask
+    // now): an op the fast loop runs goes back to it, not to the generic exec.
+    // Only right after logging, so a group the fast loop hands back (a miss
+    // to serve) finds nothing to log and takes the generic path: no ping-pong
+    if (logged_now && !(flags & (UC_BP | UC_UNSUP)) && (rfl32(e->f.w0) & 0xff) != FO_GENERIC) {
+      steps--;
+      continue;
+    }
+#endif
     // a register-only device action (SetGprs, StopOk: the same for every lane)
     // is applied here, without the lane copy and call the others take
     u32 act_kind = ~0u;
