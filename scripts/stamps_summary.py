@@ -5,13 +5,16 @@ import sys
 
 PAT = re.compile(r"wtfgpu stamps \(cycles per wave-step, (\d+) steps\): fast loop (\S+), slow: xlate\+fill (\S+), "
                  r"coverage (\S+), exec (\S+), cross-page ([^;\s]+)(?:; slow steps: miss (\d+), codepage (\d+), "
-                 r"ucmiss (\d+), other (\d+))?(?:; fast lookup (\S+), fast exec (\S+))?")
+                 r"ucmiss (\d+), other (\d+))?(?:; fast lookup ([^,\s]+), fast exec ([^,\s]+))?(?:, bp (\S+))?")
 OPS = ("ALU TEST MOV MOVZX MOVSX XCHG XADD CMPXCHG INCDEC NOT NEG SHIFT SHXD MULDIV IMUL BT BSF BSR TZCNT LZCNT "
        "POPCNT CMOV SETCC BSWAP CBW CWD LAHF SAHF FLAGOP NOP JCC JMP CALL RET PUSH POP PUSHF POPF LEAVE STRING INT3 "
        "HLT UD LEA SYS SSE UNIMPL SYS2 LOOP GEXT").split()
+# 56 + breakpoint action kind (include/wtfgpu.h WTFGPU_BPACT_*): breakpoint hits
+OPS = OPS + [str(i) for i in range(len(OPS), 56)] + \
+    "BP:host BP:return BP:setgprs BP:feed BP:rdrand BP:stopok BP:stopargs BP:none".split()
 for path in sys.argv[1:]:
     steps = 0
-    tot = [0.0] * 7
+    tot = [0.0] * 8
     why = [0] * 4
     ops = {}
     for line in open(path):
@@ -35,10 +38,12 @@ for path in sys.argv[1:]:
         if m.group(11):
             tot[5] += float(m.group(11)) * n
             tot[6] += float(m.group(12)) * n
+        if m.group(13):
+            tot[7] += float(m.group(13)) * n
         if m.group(7):
             for i in range(4):
                 why[i] += int(m.group(7 + i))
-    names = ("fast", "xlate+fill", "coverage", "exec", "cross-page", "fast: lookup part", "fast: exec part")
+    names = ("fast", "xlate+fill", "coverage", "exec", "cross-page", "fast: lookup part", "fast: exec part", "bp")
     print(path, "wave-steps", steps, {k: round(v / max(1, steps)) for k, v in zip(names, tot)},
           "slow steps", dict(zip(("miss", "codepage", "ucmiss", "other"), why)))
     if ops:

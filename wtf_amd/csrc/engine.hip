@@ -725,47 +725,61 @@ __device__ __forceinline__ void retire(const Dev &P, Lane &L, int x, u32 len, u6
 // FEED action: the next chunk of the lane's feed goes to gpr[b] + window -
 // size, as fuzzer_tlv_server.cc:83-166 writes the next packet. Writes go
 // through the copy-on-write path (the pages are dirtied as VirtWriteDirty
-// does); 8-byte stores, then single bytes. Like Backend_t::VirtWrite
-// (backend.cc:91-121, translation with ValidateRead) only a missing
-// translation stops it: the stores run as supervisor with CR0.WP clear, so
-// U/S and R/W are not checked. A missing page ends the lane with
-// WTFGPU_EXIT_FEED_FAULT, where the module's handler aborts.
-// A host-side VirtWriteDirty of n bytes at va (backend.cc:91-121): the stores
-// run as supervisor with CR0.WP clear (translation with ValidateRead: only a
-// missing translation stops it), through copy-on-write, 8 bytes at a time and
-// then single bytes. false = a page did not translate: the lane ends with
+// does). A missing page ends the lane with WTFGPU_EXIT_FEED_FAULT, where the
+// module's handler aborts.
+// A host-side VirtWriteDirty of n bytes at va (backend.cc:91-121): page by page,
+// the stores run as supervisor with CR0.WP clear (translation with
+// ValidateRead: only a missing translation stops it, U/S and R/W are not
+// checked), through copy-on-write. false = a page did not translate (the
+// pages before it are written, as VirtWrite leaves them): the lane ends with
 // WTFGPU_EXIT_FEED_FAULT (the host handler's failed write, U43).
-__device__ __noinline__ bool host_write(const Dev &P, Lane &L, u64 va, const u8 *src, u64 n) {
+__device__ __noinline__ bool host_write(const Dev &P, Lane &L, u64 va, const u8 *__restrict__ src, u64 n) {
   const u32 cpl0 = L.cpl;
   const u64 cr00 = L.cr0;
   L.cpl = 0;
   L.cr0 &= ~(1ull << 16);
+  bool ok = true;
+  // page by page, as VirtWrite does: translate (copy-on-write on the first
+  // write), then copy the page's part, 32 source bytes loaded per round
   for (u64 o = 0; o < n;) {
-    const u32 sz = n - o >= 8 ? 8 : 1;
-    u64 v = 0;
-    for (u32 i = 0; i < sz; i++) v |= (u64)src[o + i] << (8 * i);
+    const u64 a = va + o, room = 4096 - (a & 0xfff);
+    const u32 m = (u32)(n - o < room ? n - o : room);
+    u8 *d = nullptr;
+    u64 td = 0;
     for (int attempt = 0;; attempt++) {
       L.miss = 0;
-      if (vwrite(L, va + o, sz, v)) break;
+      if ((d = xlate(L, a, ACC_W, &td))) break;
       if (L.status != WTFGPU_RUNNING || !L.miss || !miss_service(P, L, attempt)) {
-        if (L.status == WTFGPU_RUNNING || L.status == WTFGPU_EXIT_FAULT) L.status = WTFGPU_EXIT_FEED_FAULT;
-        L.miss = 0;
-        L.pend = 0;
-        L.cpl = cpl0;
-        L.cr0 = cr00;
-        return false;
+        ok = false;
+        break;
       }
     }
-    o += sz;
+    if (!ok) break;
+    if (td & T_PT) L.flush = 1;  // a page-table page: cached translations go
+    const u8 *__restrict__ sp = src + o;
+    u32 k = 0;
+    for (; k + 32 <= m; k += 32) {
+      u8 t[32];
+#pragma unroll
+      for (u32 j = 0; j < 32; j++) t[j] = sp[k + j];
+#pragma unroll
+      for (u32 j = 0; j < 32; j++) d[k + j] = t[j];
+    }
+    for (; k < m; k++) d[k] = sp[k];
+    o += m;
+  }
+  if (!ok) {
+    if (L.status == WTFGPU_RUNNING || L.status == WTFGPU_EXIT_FAULT) L.status = WTFGPU_EXIT_FEED_FAULT;
+    L.miss = 0;
   }
   L.cpl = cpl0;
   L.cr0 = cr00;
   L.pend = 0;
-  if (L.flush) {
+  if (ok && L.flush) {
     tlb_flush(L);
     L.flush = 0;
   }
-  return true;
+  return ok;
 }
 
 __device__ __noinline__ bool feed_apply(const Dev &P, Lane &L, const wtfgpu_bp_action_t &a) {
@@ -864,10 +878,10 @@ __device__ __noinline__ void blake3_le64(u64 in, u64 &lo, u64 &hi) {
   hi = (u64)(v[2] ^ v[10]) | ((u64)(v[3] ^ v[11]) << 32);
 }
 
-__device__ __forceinline__ bool bp_apply_action(const Dev &P, Lane &L, u64 grip) {
+__device__ __forceinline__ bool bp_apply_action(const Dev &P, Lane &L, u64 grip, const wtfgpu_bp_action_t *found) {
   u32 s;
-  if (!P.act_keys || !hash_find(P.act_keys, P.act_mask, grip, s)) return false;
-  const wtfgpu_bp_action_t &a = P.act[s];
+  if (!found && (!P.act_keys || !hash_find(P.act_keys, P.act_mask, grip, s))) return false;
+  const wtfgpu_bp_action_t &a = found ? *found : P.act[s];
   if (a.kind == WTFGPU_BPACT_SET_GPRS) {
     for (u32 i = 0; i < 16; i++) RS(L, i, a.gprs[i]);
     L.rip = a.gprs[16];
@@ -913,20 +927,31 @@ __device__ __forceinline__ bool bp_apply_action(const Dev &P, Lane &L, u64 grip)
     // bytes (VirtReadString, backend.h:333-430): a byte that does not
     // translate before the terminator leaves the hit to the host handler,
     // whose read then decides (U43)
+    // (read as aligned 32-byte blocks, the four words of a block loaded at
+    // once: a block never crosses a page, so it translates exactly when the
+    // first byte of it the scan needs does)
     const u64 s = R(L, (u32)(a.gprs[0] - 1) & 15);
-    for (u64 i = 0; i < a.gprs[1]; i++) {
-      u64 c = 0;
+    const u64 lim = a.gprs[1];
+    for (u64 i = 0; i < lim;) {
+      const u64 va = s + i, al = va & ~31ull;
+      const u8 *p = nullptr;
       for (int attempt = 0;; attempt++) {
         L.miss = 0;
-        if (vread(L, s + i, 1, c)) break;
+        if ((p = xlate(L, al, ACC_R))) break;
         if (L.status != WTFGPU_RUNNING || !L.miss || !miss_service(P, L, attempt)) {
           L.status = WTFGPU_RUNNING;  // undo a fault: the host handler decides
           L.miss = 0;
-          L.pend = 0;
           return false;
         }
       }
-      if ((c & 0xff) == 0) break;
+      const u64 *w = (const u64 *)p;
+      const u64 c0 = w[0], c1 = w[1], c2 = w[2], c3 = w[3];
+      bool term = false;
+      for (u32 b = (u32)(va - al); b < 32 && i < lim && !term; b++, i++) {
+        const u64 c = b < 8 ? c0 : b < 16 ? c1 : b < 24 ? c2 : c3;
+        term = ((c >> (8 * (b & 7))) & 0xff) == 0;
+      }
+      if (term) break;
     }
   }
   const u64 rsp = R(L, WTFGPU_RSP);
@@ -951,9 +976,10 @@ __device__ __forceinline__ bool bp_apply_action(const Dev &P, Lane &L, u64 grip)
 // The action stands in for a host handler, whose guest-memory reads and writes
 // (VirtRead / VirtWrite) are no CPU accesses: Tenet does not log them
 // (bochscpu_backend.cc:1215-1323 logs the lin_access hook only).
-__device__ __noinline__ bool bp_apply(const Dev &P, Lane &L, u64 grip) {
+// found: the action k_run already looked up (nullptr: look it up)
+__device__ __noinline__ bool bp_apply(const Dev &P, Lane &L, u64 grip, const wtfgpu_bp_action_t *found = nullptr) {
   tn_mute(L.lane);
-  const bool r = bp_apply_action(P, L, grip);
+  const bool r = bp_apply_action(P, L, grip, found);
   tn_unmute(L.lane, 0, 0, 0, false);
   return r;
 }
@@ -1596,6 +1622,10 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
         act_kind = rfl32(act->kind);
       }
     }
+#ifdef WTFGPU_STAMPS
+    // breakpoint hits by action kind (56 + kind; 63: none found)
+    if (__ballot(ing && (flags & UC_BP) && !skip)) OPHIST(56 + (act_kind < 7 ? act_kind : 7));
+#endif
     // (one block per kind: with the two kinds nested in one per-lane if/else
     // the build ran wrong on MI355X, tlv's lanes stopping Ok at their SetGprs
     // breakpoint, although either kind alone ran right; WTFGPU_ACT_NESTED=1
@@ -1632,7 +1662,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       if ((flags & UC_BP) && !skip) {
         // breakpoint hit: device action (the lane keeps running) or host exit
         bool applied = false;
-        if (P.act_keys) WITH_LANE_COPY(applied = bp_apply(P, T, grip));
+        if (P.act_keys) WITH_LANE_COPY(applied = bp_apply(P, T, grip, act));
         if (!applied) L.status = WTFGPU_EXIT_BREAKPOINT;
         skip = applied && L.rip == grip;
         if (applied && !skip && g_tn.buf) WITH_LANE_COPY(tn_regs(P, T));  // Tenet: the action moved rip
@@ -1641,6 +1671,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
         skip = false;
       }
     }
+    STAMP(4);
     // the UOp for the generic path (wave-uniform: the slot fill is a wave operation)
     const UOp *u = nullptr;
     if (__ballot(ing)) u = uc_uop(P, uu, key, lptr, off, grip, lid);
@@ -3511,10 +3542,10 @@ static void print_stamps(const u64 *s) {
     fprintf(stderr,
             "wtfgpu stamps (cycles per wave-step, %llu steps): fast loop %.0f, slow: xlate+fill %.0f, coverage %.0f, "
             "exec %.0f, cross-page %.0f; slow steps: miss %llu, codepage %llu, ucmiss %llu, other %llu; "
-            "fast lookup %.0f, fast exec %.0f\n",
+            "fast lookup %.0f, fast exec %.0f, bp %.0f\n",
             (unsigned long long)s[0], (double)s[4] / s[0], (double)s[6] / s[0], (double)s[7] / s[0],
             (double)s[5] / s[0], (double)s[9] / s[0], (unsigned long long)s[12], (unsigned long long)s[13],
-            (unsigned long long)s[14], (unsigned long long)s[15], (double)s[10] / s[0], (double)s[11] / s[0]);
+            (unsigned long long)s[14], (unsigned long long)s[15], (double)s[10] / s[0], (double)s[11] / s[0], (double)s[8] / s[0]);
   fprintf(stderr, "wtfgpu stamps generic ops:");
   for (int k = 0; k < 512; k++)
     if (s[16 + k]) fprintf(stderr, " %d:%llu", k, (unsigned long long)s[16 + k]);
