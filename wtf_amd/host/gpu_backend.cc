@@ -86,6 +86,8 @@ bool GpuBackend_t::Initialize(const Options_t &Opts, const CpuState_t &CpuState)
   if (wtfgpu_alloc_lanes(ctx_, nlanes_, overlay_pages_, Opts.GpuCoverageSet)) return false;
   views_.clear();
   views_.resize(nlanes_);
+  touched_.assign(nlanes_, 0);
+  pf_.assign(nlanes_, PrepFeed{});
   arenas_.resize(HostPool::Get().Threads() + 1);
   if (Opts.Limit) SetLimit(Opts.Limit);
   if (Opts.Edges && wtfgpu_set_edges(ctx_, 1) != WTFGPU_OK) return false;  // bochscpu_backend.cc:308-312
@@ -120,15 +122,13 @@ void GpuBackend_t::reset_view(uint32_t lane) {
   v.seed = initial_.Seed;  // Rdrand seed (bochscpu_backend.cc:1030)
   v.has_feed = false;
   v.feed.clear();
-  v.ext = nullptr;
-  v.ext_len = 0;
-  v.ext_insert = false;
   v.dirty_known = true;    // a restored lane has an empty overlay
   v.dirty.clear();
   v.wlog.clear();
   v.wdata.clear();
   v.win_len = 0;
   drop_staged(v);
+  touched_[lane] = 0;
 }
 
 void GpuBackend_t::Stop(const TestcaseResult_t &Res) { cur().result = Res; }
@@ -283,13 +283,13 @@ int GpuBackend_t::upload_feed(uint32_t n) {
   std::vector<uint64_t> off(n + 1);
   std::vector<uint8_t> has(n);
   uint64_t total = 0;
-  for (uint32_t l = 0; l < n; l++) total += views_[l].feed.size();
+  for (uint32_t l = 0; l < n; l++) total += view(l).feed.size();
   std::vector<uint8_t> bytes;
   bytes.reserve(total);
   for (uint32_t l = 0; l < n; l++) {
     off[l] = bytes.size();
-    has[l] = views_[l].has_feed;
-    bytes.insert(bytes.end(), views_[l].feed.begin(), views_[l].feed.end());
+    has[l] = view(l).has_feed;
+    bytes.insert(bytes.end(), view(l).feed.begin(), view(l).feed.end());
   }
   off[n] = bytes.size();
   return wtfgpu_set_feed(ctx_, 0, n, off.data(), has.data(), bytes.data(), bytes.size());
@@ -351,7 +351,7 @@ bool GpuBackend_t::parallel_service(const ModuleSlots *slots) const {
 uint8_t *GpuBackend_t::stage(uint32_t lane, uint64_t gpfn, const uint8_t *orig, uint8_t *data) const {
   // orig / data: slots alloc_slots counted as live, or (orig only) a dump or
   // zero page with a fresh slot for data
-  LaneView &v = views_[lane];
+  LaneView &v = view(lane);
   v.pages.push_back(Staged{gpfn, data, orig});
   for (LaneView::Logged &w : v.wlog)  // logged writes to this page move into it
     if (w.len && (w.gpa >> 12) == gpfn) {
@@ -371,7 +371,7 @@ bool GpuBackend_t::PhysWriteDirect(const Gpa_t Gpa, const uint8_t *Buffer, const
     memcpy(p->data + (Gpa.U64() & 0xfff), Buffer, Size);
     return true;
   }
-  LaneView &v = views_[lane];
+  LaneView &v = view(lane);
   if (v.win_len && Gpa.U64() < v.win_gpa + v.win_len && Gpa.U64() + Size > v.win_gpa) {  // keep the window current
     const uint64_t lo = std::max(Gpa.U64(), v.win_gpa), hi = std::min(Gpa.U64() + Size, v.win_gpa + v.win_len);
     memcpy(v.win + (lo - v.win_gpa), Buffer + (lo - Gpa.U64()), hi - lo);
@@ -400,7 +400,7 @@ bool GpuBackend_t::PhysReadDirect(const Gpa_t Gpa, uint8_t *Buffer, const uint64
     memcpy(Buffer, p->data + (Gpa.U64() & 0xfff), Size);
     return true;
   }
-  const LaneView &v = views_[lane];
+  const LaneView &v = view(lane);
   if (v.win_len && Gpa.U64() >= v.win_gpa && Gpa.U64() + Size <= v.win_gpa + v.win_len) {
     memcpy(Buffer, v.win + (Gpa.U64() - v.win_gpa), Size);
     return true;
@@ -441,7 +441,7 @@ void GpuBackend_t::recycle_arenas() const {
 }
 
 GpuBackend_t::Staged *GpuBackend_t::find_staged(uint32_t lane, uint64_t gpfn) const {
-  for (Staged &p : views_[lane].pages)
+  for (Staged &p : view(lane).pages)
     if (p.gpfn == gpfn) return &p;
   return nullptr;
 }
@@ -454,7 +454,7 @@ bool GpuBackend_t::in_overlay(const LaneView &v, uint64_t gpfn) const {
 // the lane's overlay page, else the dump page (or zeros).
 uint8_t *GpuBackend_t::lane_page(uint32_t lane, uint64_t gpfn) const {
   if (Staged *p = find_staged(lane, gpfn)) return p->data;
-  LaneView &v = views_[lane];
+  LaneView &v = view(lane);
   if (!v.dirty_known) {
     std::vector<uint32_t> buf(overlay_pages_ + 1);
     std::lock_guard<std::mutex> g(engine_mu_);
@@ -495,7 +495,7 @@ void GpuBackend_t::learn(uint64_t gpfn) const {
 
 const uint8_t *GpuBackend_t::lane_page_ro(uint32_t lane, uint64_t gpfn) const {
   if (Staged *p = find_staged(lane, gpfn)) return p->data;
-  const LaneView &v = views_[lane];
+  const LaneView &v = view(lane);
   if (!v.dirty_known || in_overlay(v, gpfn)) return lane_page(lane, gpfn);
   const uint8_t *p = dump_.GetPhysicalPage(gpfn << 12);
   return p ? p : kZeroPage;
@@ -517,7 +517,7 @@ thread_local WalkMemo t_walk_memo[64];
 
 bool GpuBackend_t::VirtTranslate(const Gva_t Gva, Gpa_t &Gpa, const MemoryValidate_t) const {
   const uint64_t va = Gva.U64(), vpn = va >> 12;
-  const LaneView &v = views_[cur_];
+  const LaneView &v = view(cur_);
   WalkMemo &m = t_walk_memo[vpn & 63];
   if (m.vpn == vpn && v.dirty_known && (!(v.cr_known & 2) || v.cr[1] == initial_.Cr3)) {
     bool clean = true;
@@ -604,7 +604,7 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
   std::vector<uint64_t> rcnt(nl + 1, 0), pcnt(nl + 1, 0), roff(nl + 1, 0), boff(nl + 1, 0);
   std::atomic<bool> any_cr{false};
   HostPool::Get().For(nl, 256, [&](size_t i) {
-    const LaneView &v = views_[lanes[i]];
+    const LaneView &v = view(lanes[i]);
     rcnt[i + 1] = v.regs_dirty ? 1 : 0;
     pcnt[i + 1] = v.pages.size();
     uint64_t r = 0, b = 0;
@@ -625,7 +625,7 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
   }
   if (any_cr)
     for (uint32_t l : lanes) {
-      LaneView &v = views_[l];
+      LaneView &v = view(l);
       for (int k = 0; k < 2; k++)
         if (v.cr_dirty & (1 << k)) {
           std::lock_guard<std::mutex> g(engine_mu_);
@@ -644,7 +644,7 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
   std::vector<Cand> cand(pcnt[nl]);
   HostPool::Get().For(nl, 256, [&](size_t i) {
     const uint32_t l = lanes[i];
-    LaneView &v = views_[l];
+    LaneView &v = view(l);
     if (v.regs_dirty) {
       rl[rcnt[i]] = l;
       memcpy(&regs[rcnt[i] * 18], v.gpr, 18 * 8);
@@ -684,7 +684,7 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
   }
   HostPool::Get().For(nl, 256, [&](size_t i) {
     const uint32_t l = lanes[i];
-    LaneView &v = views_[l];
+    LaneView &v = view(l);
     uint64_t r = roff[i], b = boff[i];
     for (const LaneView::Logged &w : v.wlog) {
       if (!w.len) continue;
@@ -708,12 +708,12 @@ int GpuBackend_t::flush_lanes(const std::vector<uint32_t> &lanes) {
       memcpy(wpin_ + b, c.p->data + c.lo, w.len);
       b += w.len;
       writes[r++] = w;
-      views_[c.lane].dirty_known = false;  // the device overlay changed
+      view(c.lane).dirty_known = false;  // the device overlay changed
     }
   }
   stats_.staged_pages += cand.size();
   if (!cand.empty())
-    for (uint32_t l : lanes) drop_staged(views_[l]);
+    for (uint32_t l : lanes) drop_staged(view(l));
   int rc = WTFGPU_OK;
   const auto tr = Clock::now();
   stats_.up_prep_ms += std::chrono::duration<double, std::milli>(tr - tp).count();
@@ -739,26 +739,34 @@ bool GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first
     const uint32_t l = pending[pi];
     if (done[l - first]) return;
     const wtfgpu_exit_t &e = ex[l - first];
+    // a view the host has not touched since its reset holds no result: the
+    // common exits (Stop(Ok), still running, a breakpoint) leave it so
     LaneView &v = views_[l];
+    const auto mark = [&]() -> LaneView & {
+      touched_[l] = 1;
+      return v;
+    };
     switch (e.status) {
       case WTFGPU_EXIT_BREAKPOINT: hit[pi] = 1; return;
       case WTFGPU_RUNNING: return;  // sliced: still running when the slice ended
-      case WTFGPU_EXIT_TIMEOUT: v.result = Timedout_t(); break;    // bochscpu_backend.cc:458-469
-      case WTFGPU_EXIT_INT3:                                         // :595-619
-      case WTFGPU_EXIT_HLT: v.result = Crash_t(); break;             // :690-697
-      case WTFGPU_EXIT_CR3: v.result = Cr3Change_t(); break;         // :628-657
-      case WTFGPU_EXIT_FAULT: v.result = FaultToResult(e.vector, e.error, e.rip, e.addr, e.opcode); break;
+      case WTFGPU_EXIT_TIMEOUT: mark().result = Timedout_t(); break;  // bochscpu_backend.cc:458-469
+      case WTFGPU_EXIT_INT3:                                           // :595-619
+      case WTFGPU_EXIT_HLT: mark().result = Crash_t(); break;          // :690-697
+      case WTFGPU_EXIT_CR3: mark().result = Cr3Change_t(); break;      // :628-657
+      case WTFGPU_EXIT_FAULT: mark().result = FaultToResult(e.vector, e.error, e.rip, e.addr, e.opcode); break;
       case WTFGPU_EXIT_STOPPED: break;
-      case WTFGPU_EXIT_STOP_OK: v.result = Ok_t(); break;           // device Feed action: Stop(Ok_t())
-      case WTFGPU_EXIT_STOP_ARGS: hit[pi] = 2; return;            // named below from the kept arguments
-      case WTFGPU_EXIT_FEED_FAULT: v.handler_fault = true; break;  // U43: fill_results makes it an engine error
+      case WTFGPU_EXIT_STOP_OK:  // device Feed action: Stop(Ok_t()) (an untouched view reads as Ok already)
+        if (touched_[l]) v.result = Ok_t();
+        break;
+      case WTFGPU_EXIT_STOP_ARGS: hit[pi] = 2; return;                  // named below from the kept arguments
+      case WTFGPU_EXIT_FEED_FAULT: mark().handler_fault = true; break;  // U43: fill_results makes it an engine error
       default:
         // unimplemented opcode / overlay full / a device Feed write that
         // failed: the engine cannot finish the testcase. Not a target bug:
         // flagged as an engine error, with an unnamed Crash_t (which no
         // master saves, server.h:861-877) as its result
         if (out) (*out)[l].error = true;
-        if (!v.result) v.result = Crash_t();
+        if (!v.result) mark().result = Crash_t();
         if (e.status == WTFGPU_EXIT_UNIMPLEMENTED) {
           stats_.err_unimpl++;
           stats_.unimpl_ops.add(e.opcode);
@@ -792,7 +800,7 @@ bool GpuBackend_t::classify(const std::vector<uint32_t> &pending, uint32_t first
   std::atomic<uint64_t> bad{0};
   HostPool::Get().For(named.size(), 512, [&](size_t k) {
     const uint32_t l = named[k];
-    LaneView &v = views_[l];
+    LaneView &v = view(l);
     const auto it = args_results_.find(ex[l - first].rip);
     if (ok && it != args_results_.end()) {
       v.result = it->second(&args[k * 6]);
@@ -839,9 +847,10 @@ bool GpuBackend_t::fill_results(const std::vector<uint32_t> &lanes, uint32_t fir
   }
   HostPool::Get().For(fin.size(), 1024, [&](size_t i) {
     LaneResult &r = (*out)[fin[i]];
-    const LaneView &v = views_[fin[i]];
-    r.result = v.result ? std::move(*v.result) : TestcaseResult_t(Ok_t());  // the view is reset at refill
-    if (v.handler_fault) {  // U43: an engine error, never a named crash
+    const LaneView &v = views_[fin[i]];  // untouched since its reset: no result, no fault
+    const bool t = touched_[fin[i]] != 0;
+    r.result = t && v.result ? std::move(*v.result) : TestcaseResult_t(Ok_t());  // the view is reset at refill
+    if (t && v.handler_fault) {  // U43: an engine error, never a named crash
       r.result = Crash_t();
       r.error = true;
       r.handler_fault = true;
@@ -869,7 +878,7 @@ bool GpuBackend_t::fill_results(const std::vector<uint32_t> &lanes, uint32_t fir
 // the next classification gives them their result.
 bool GpuBackend_t::stop_prestopped(const std::vector<uint32_t> &lanes) {
   std::vector<uint8_t> has(lanes.size());
-  HostPool::Get().For(lanes.size(), 1024, [&](size_t i) { has[i] = views_[lanes[i]].result.has_value(); },
+  HostPool::Get().For(lanes.size(), 1024, [&](size_t i) { has[i] = touched_[lanes[i]] && views_[lanes[i]].result.has_value(); },
                       lanes.size() >= 4096);
   std::vector<uint32_t> pre;
   for (size_t i = 0; i < lanes.size(); i++)
@@ -941,7 +950,7 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
     std::vector<uint64_t> sp_gpfn(hits.size(), ~0ull), sp_gpa(hits.size(), ~0ull);
     // lane views of the hits (independent per lane: all host threads)
     HostPool::Get().For(hits.size(), 256, [&](size_t i) {
-      LaneView &v = views_[hits[i]];
+      LaneView &v = view(hits[i]);
       memcpy(v.gpr, &regs[i * 18], 18 * 8);
       v.seed = seeds[i];
       v.regs_dirty = false;
@@ -971,7 +980,7 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
     std::vector<uint8_t> action(hits.size());  // 0 stop, 1 resume, 2 resume + skip the breakpoint
     auto service = [&](size_t h) {
       const uint32_t l = hits[h];
-      LaneView &v = views_[l];
+      LaneView &v = view(l);
       cur_ = l;
       const uint64_t rip0 = v.gpr[16];
       servicing_sp_ = sp_gpfn[h];
@@ -1002,7 +1011,7 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
     // the other lanes' handlers will touch
     std::vector<uint8_t> scouted(hits.size(), 0);
     for (size_t i = 0; i < hits.size(); i++) {
-      if (!bp_seen_.insert(views_[hits[i]].gpr[16]).second) continue;
+      if (!bp_seen_.insert(view(hits[i]).gpr[16]).second) continue;
       scouting_ = true;
       service(i);
       scouting_ = false;
@@ -1020,13 +1029,13 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
     std::vector<uint8_t> use_win(hits.size(), 0);
     HostPool::Get().For(hits.size(), 256, [&](size_t i) {
       if (scouted[i] || sp_gpfn[i] == ~0ull) return;
-      const LaneView &v = views_[hits[i]];
+      const LaneView &v = view(hits[i]);
       if (bp_stack_.count(v.gpr[16]) && in_overlay(v, sp_gpfn[i]))
         use_win[i] = (sp_gpa[i] & 0xfff) + LaneView::kWin <= Page::Size ? 1 : 2;  // 2: whole page
     });
     for (size_t i = 0; i < hits.size(); i++) {
       if (scouted[i]) continue;
-      const LaneView &v = views_[hits[i]];
+      const LaneView &v = view(hits[i]);
       auto want = [&](uint64_t gpfn) {
         if (!in_overlay(v, gpfn)) return;
         for (size_t k = pf_gpas.size(); k-- > 0 && pf_lanes[k] == hits[i];)
@@ -1052,7 +1061,7 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
       if (wtfgpu_gather_bytes(ctx_, win_lanes.data(), win_gpas.data(), (uint32_t)nw, LaneView::kWin, buf.data()))
         return false;
       HostPool::Get().For(nw, 256, [&](size_t i) {
-        LaneView &v = views_[win_lanes[i]];
+        LaneView &v = view(win_lanes[i]);
         v.win_gpa = win_gpas[i];
         v.win_len = LaneView::kWin;
         memcpy(v.win, buf.data() + i * LaneView::kWin, LaneView::kWin);
@@ -1088,16 +1097,16 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
     const auto t3 = Clock::now();
     stats_.handler_ms += std::chrono::duration<double, std::milli>(t3 - t2).count();
     if (flush_lanes(hits)) return false;
-    for (size_t i = 0; i < hits.size(); i++) seeds[i] = views_[hits[i]].seed;
+    for (size_t i = 0; i < hits.size(); i++) seeds[i] = view(hits[i]).seed;
     if (wtfgpu_lane_seeds(ctx_, hits.data(), (uint32_t)hits.size(), seeds.data(), 1)) return false;
     {  // PageFaultsMemoryIfNeeded requests: #PF through the guest IDT, resume at the handler
       std::vector<uint32_t> il;
       std::vector<uint64_t> ia;
       std::vector<size_t> ih;
       for (size_t h = 0; h < hits.size(); h++)
-        if (action[h] != 0 && views_[hits[h]].inject != ~0ull) {
+        if (action[h] != 0 && view(hits[h]).inject != ~0ull) {
           il.push_back(hits[h]);
-          ia.push_back(views_[hits[h]].inject);
+          ia.push_back(view(hits[h]).inject);
           ih.push_back(h);
         }
       if (!il.empty()) {
@@ -1109,7 +1118,7 @@ bool GpuBackend_t::service_hits(const std::vector<uint32_t> &hits, uint32_t firs
           if (ok[k]) {
             action[ih[k]] = 1;  // resume at the handler, no breakpoint skip
           } else {
-            views_[il[k]].result = Crash_t();  // no IDT to take it: the triple fault bochs stops on
+            view(il[k]).result = Crash_t();  // no IDT to take it: the triple fault bochs stops on
             action[ih[k]] = 0;
           }
         }
@@ -1185,7 +1194,7 @@ std::optional<TestcaseResult_t> GpuBackend_t::Run(const uint8_t *, const uint64_
   if (!run_lanes({0}, &out, nullptr, false)) return std::nullopt;
   // the lane's final registers back into its view: GetReg after Run reads
   // them (the client's own code and Target.Restore may do so)
-  LaneView &v = views_[0];
+  LaneView &v = view(0);
   if (wtfgpu_read_gprs_list(ctx_, &cur_, 1, v.gpr)) return std::nullopt;
   v.regs_dirty = false;
   v.cr_known = 0;
@@ -1245,7 +1254,7 @@ bool GpuBackend_t::RunBatch(const Target_t &Target, const std::vector<std::pair<
   std::vector<uint8_t> insert_ok;
   insert_lanes(Target, lanes, Testcases, Slots, insert_ok);
   for (uint32_t l = 0; l < n; l++)
-    if (!insert_ok[l]) views_[l].result = Crash_t("insert-testcase-failed");
+    if (!insert_ok[l]) view(l).result = Crash_t("insert-testcase-failed");
   const auto tu = Clock::now();
   stats_.module_ms += std::chrono::duration<double, std::milli>(tu - tm).count();
   if (flush_lanes(lanes) || upload_feed(n)) return false;
@@ -1292,7 +1301,7 @@ void GpuBackend_t::insert_lanes(const Target_t &Target, const std::vector<uint32
     try {
       ok[i] = T.InsertTestcase(tcs[i].first, tcs[i].second);
     } catch (const HandlerFault_t &) {  // see service_hits
-      views_[l].handler_fault = true;
+      view(l).handler_fault = true;
       ok[i] = 0;
     }
     if (Slots) Slots->SwapOut(l);
@@ -1520,24 +1529,26 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
     std::vector<uint8_t> prepared(fresh.size(), 0);
     HostPool::Get().For(fresh.size(), 256, [&](size_t i) {
       const uint32_t l = fresh[i];
-      reset_view(l);
+      // a view the host touched goes back to the initial state; an untouched
+      // one still is in it (the common case: no host handler ran on the lane)
+      if (touched_[l]) reset_view(l);
+      pf_[l] = PrepFeed{};
       busy_[l] = 1;
       tag_[l] = In[i].tag;
       tc_bytes_[l] = In[i].size;
       lres_stale_[l] = 1;  // its last result may not be consumed yet (this call's Out)
       const StreamTestcase_t &T = In[i];
-      LaneView &v = views_[l];
       switch (T.prep) {
         case PreparedInsert_t::Call: return;
-        case PreparedInsert_t::Failed: v.result = Crash_t("insert-testcase-failed"); break;
+        case PreparedInsert_t::Failed: view(l).result = Crash_t("insert-testcase-failed"); break;
         case PreparedInsert_t::Nothing: break;
         case PreparedInsert_t::Feed:  // SetFeed would refuse it: InsertTestcase keeps its host path
           if (!feed_action_ || T.prep_size > kFeedRegion) return;
-          v.has_feed = true, v.ext = T.prep_data, v.ext_len = (uint32_t)T.prep_size;
+          pf_[l] = PrepFeed{T.prep_data, (uint32_t)T.prep_size, 1, 0};
           break;
         case PreparedInsert_t::Insert:  // as SetInsert
           if (!insert_action_ || T.size + 4 > kFeedRegion) return;
-          v.has_feed = true, v.ext = T.data, v.ext_len = (uint32_t)T.size, v.ext_insert = true;
+          pf_[l] = PrepFeed{T.data, (uint32_t)T.size, 1, 1};
           break;
       }
       if (Slots) Slots->ResetLane(l);
@@ -1558,7 +1569,7 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
       std::vector<uint8_t> ok;
       insert_lanes(Target, call, call_tcs, Slots, ok);
       for (size_t i = 0; i < call.size(); i++)
-        if (!ok[i]) views_[call[i]].result = Crash_t("insert-testcase-failed");
+        if (!ok[i]) view(call[i]).result = Crash_t("insert-testcase-failed");
     }
     const auto tu = Clock::now();
     stats_.module_ms += std::chrono::duration<double, std::milli>(tu - tm).count();
@@ -1568,10 +1579,12 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
       const size_t n = fresh.size();
       std::vector<uint64_t> off(n + 1, 0);
       std::vector<uint8_t> has(n);
-      HostPool::Get().For(n, 1024, [&](size_t i) {  // the views are scattered: read them on all threads
-        const LaneView &v = views_[fresh[i]];
-        off[i + 1] = v.feed_size();
-        has[i] = v.has_feed;
+      HostPool::Get().For(n, 1024, [&](size_t i) {  // prepared feeds, else a view's SetFeed / SetInsert bytes
+        const uint32_t l = fresh[i];
+        const PrepFeed &f = pf_[l];
+        const bool t = !f.has && touched_[l];
+        off[i + 1] = f.has ? f.len + (f.ins ? 4 : 0) : t ? views_[l].feed.size() : 0;
+        has[i] = f.has || (t && views_[l].has_feed);
       });
       for (size_t i = 0; i < n; i++) off[i + 1] += off[i];
       // packed into the part's pinned buffer on all host threads: one DMA
@@ -1584,16 +1597,17 @@ bool GpuBackend_t::StreamStep(const Target_t &Target, const std::vector<StreamTe
         P.pin = (uint8_t *)p;
       }
       HostPool::Get().For(n, 256, [&](size_t i) {
-        const LaneView &v = views_[fresh[i]];
+        const uint32_t l = fresh[i];
+        const PrepFeed &f = pf_[l];
         uint8_t *o = P.pin + off[i];
-        if (v.ext) {
-          if (v.ext_insert) {
-            memcpy(o, &v.ext_len, 4);
+        if (f.has) {
+          if (f.ins) {
+            memcpy(o, &f.len, 4);
             o += 4;
           }
-          if (v.ext_len) memcpy(o, v.ext, v.ext_len);
-        } else if (!v.feed.empty()) {
-          memcpy(o, v.feed.data(), v.feed.size());
+          if (f.len) memcpy(o, f.p, f.len);
+        } else if (touched_[l] && !views_[l].feed.empty()) {
+          memcpy(o, views_[l].feed.data(), views_[l].feed.size());
         }
       });
       if (wtfgpu_set_feed_lanes(ctx_, fresh.data(), (uint32_t)n, off.data(), has.data(), P.pin, off[n]))

@@ -170,13 +170,6 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
     uint64_t inject = ~0ull;  // PageFaultsMemoryIfNeeded: page to #PF after the handler
     bool has_feed = false;    // SetFeed / SetInsert: chunks for the device Feed action / insert
     std::vector<uint8_t> feed;
-    // a prepared insert's bytes instead of `feed` (StreamTestcase_t::prep,
-    // valid during the StreamStep call): the feed itself, or with ext_insert
-    // the testcase the feed's one chunk (u32 size, bytes) holds
-    const uint8_t *ext = nullptr;
-    uint32_t ext_len = 0;
-    bool ext_insert = false;
-    uint64_t feed_size() const { return ext ? ext_len + (ext_insert ? 4 : 0) : feed.size(); }
     bool dirty_known = false;
     std::vector<uint32_t> dirty;  // gpfns the lane's overlay holds
     std::vector<Staged> pages;    // staged pages (few per lane: linear search)
@@ -196,7 +189,15 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
     uint8_t win[kWin];
   };
 
-  LaneView &cur() const { return views_[cur_]; }
+  // a lane's view for the host to read or change: marks it touched, so the
+  // lane's next refill resets it (reset_view); the per-lane loops of the
+  // harvest and refill read views_ directly and treat an untouched view as
+  // reset (no result, no feed) without pulling its cache lines in
+  LaneView &view(uint32_t lane) const {
+    touched_[lane] = 1;
+    return views_[lane];
+  }
+  LaneView &cur() const { return view(cur_); }
   void reset_view(uint32_t lane);
   uint8_t *lane_page(uint32_t lane, uint64_t gpfn) const;
   // read-only view for page walks: the dump page when the lane's overlay does
@@ -288,6 +289,16 @@ class GpuBackend_t final : public Backend_t, public Executor_t {
   uint32_t nlanes_ = 0, overlay_pages_ = 0;
   uint64_t limit_ = 0;
   mutable std::vector<LaneView> views_;
+  mutable std::vector<uint8_t> touched_;  // view(lane) was taken since the lane's last reset_view
+  // a prepared insert's bytes for the lane's feed upload (StreamTestcase_t::prep,
+  // valid during the StreamStep call): the feed itself, or with ins the testcase
+  // the feed's one chunk (u32 size, bytes) holds
+  struct PrepFeed {
+    const uint8_t *p = nullptr;
+    uint32_t len = 0;
+    uint8_t has = 0, ins = 0;
+  };
+  std::vector<PrepFeed> pf_;
   // the lane the calling thread services (handlers of different lanes run on
   // several threads when the module state is thread_local, module_slots.h)
   static thread_local uint32_t cur_;
