@@ -220,6 +220,38 @@ static int cmd_mutate(int argc, char **argv, bool grow = false) {
 }
 
 #ifdef WTF_AMD_HOST
+// tlv-prep <seed> <count>: the tlv mutator over a corpus that grows every 64th
+// output; each output's PrepareInsert feed (the mutator's own, handed over
+// without a parse) against TestcaseFeedBytes (the JSON parsed back), and a
+// truncated copy (parsed). Prints "P <testcases> <mismatches>".
+static int cmd_tlv_prep(int argc, char **argv) {
+  if (argc != 4) return 2;
+  std::mt19937_64 Rng(strtoull(argv[2], nullptr, 0));
+  const size_t count = strtoull(argv[3], nullptr, 0);
+  Corpus_t Corpus("", Rng);
+  const std::string seed = "{\"Packets\":[{\"Body\":[65,66,67],\"BodySize\":3,\"Command\":0,\"Id\":0}]}";
+  Corpus.SaveTestcase(Ok_t(), Testcase_t((const uint8_t *)seed.data(), seed.size()));
+  Target_t *T = Targets_t::Instance().Get("tlv_server");
+  if (!T || !T->PrepareInsert) return 3;
+  auto M = T->CreateMutator(Rng, 4096);
+  size_t bad = 0;
+  std::vector<uint8_t> A, B;
+  for (size_t i = 1; i <= count; i++) {
+    const std::string s = M->GetNewTestcase(Corpus);
+    const auto *d = (const uint8_t *)s.data();
+    const bool pa = T->PrepareInsert(d, s.size(), A) == PreparedInsert_t::Feed;
+    const bool pb = TlvServer::TestcaseFeedBytes(d, s.size(), B);
+    if (pa != pb || (pa && A != B)) bad++;
+    const size_t cut = s.size() / 2;  // not the mutator's bytes: parsed (and refused)
+    const bool qa = T->PrepareInsert(d, cut, A) == PreparedInsert_t::Feed;
+    const bool qb = TlvServer::TestcaseFeedBytes(d, cut, B);
+    if (qa != qb || (qa && A != B)) bad++;
+    if (i % 64 == 0) Corpus.SaveTestcase(Ok_t(), Testcase_t(d, s.size()));
+  }
+  printf("P %zu %zu\n", count, bad);
+  return bad ? 1 : 0;
+}
+
 static int cmd_merge_blocks(int argc, char **argv) {
   if (argc < 4) return 2;
   const uint64_t cap = strtoull(argv[2], nullptr, 0), world = strtoull(argv[3], nullptr, 0);
@@ -340,6 +372,9 @@ int main(int argc, char **argv) {
   const std::string cmd = argv[1];
   if (cmd.rfind("wire-", 0) == 0 && argc >= 3) return cmd_wire(argc, argv);
   if (cmd == "tlv-feed" && argc == 3) return cmd_tlv_feed(argv[2]);
+#ifdef WTF_AMD_HOST
+  if (cmd == "tlv-prep") return cmd_tlv_prep(argc, argv);
+#endif
 #ifdef WTF_AMD_HOST
   if (cmd == "xof" && argc == 4) {
     const auto b = unhex(argv[2]);

@@ -41,3 +41,14 @@ def test_feeds_match_reference_live_on_large_packets():
     tcs = [canonical([packet(rng, 1200) for _ in range(rng.randint(1, 10))]) for _ in range(400)]
     tcs += [t[:rng.randint(0, len(t))] for t in tcs[:100]]
     assert feeds(OURS, tcs) == feeds(REF, tcs)
+
+
+def test_mutator_handoff_feed_equals_parsed_feed():
+    """PrepareInsert takes the feed the tlv mutator built with the testcase
+    (no JSON parse) when the bytes are the mutator's last output: over a
+    growing corpus, that feed and a truncated copy's (parsed) equal
+    TestcaseFeed's parse of the same bytes."""
+    import subprocess
+    out = subprocess.run([OURS, "tlv-prep", "7", "20000"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert out.stdout.split() == ["P", "20000", "0"]

@@ -377,11 +377,46 @@ bool InsertTestcase(const uint8_t *Buffer, const size_t BufferSize) {
 // InsertTestcase ahead of time (PrepareInsert_t): on a backend that takes the
 // feed, InsertTestcase is SetFeed(TestcaseFeed(testcase)) and nothing else (the
 // queue it clears is empty after a lane reset)
+// The mutator's last testcase on this thread and its feed, written while it
+// built the JSON from packets it already held (CustomMutator_t below): a
+// PrepareInsert of the same bytes takes that feed instead of parsing the JSON
+// back (the parse was half of the node's per-testcase mutation time). Any
+// other testcase (a truncated one, a corpus input) is parsed.
+namespace {
+thread_local struct {
+  std::string Json;
+  std::vector<uint8_t> Feed;
+} LastMutation;
+}  // namespace
+
 PreparedInsert_t PrepareInsert(const uint8_t *Buffer, const size_t BufferSize, std::vector<uint8_t> &Out) {
+  const auto &M = LastMutation;
+  if (BufferSize == M.Json.size() && BufferSize && !memcmp(Buffer, M.Json.data(), BufferSize)) {
+    Out.assign(M.Feed.begin(), M.Feed.end());
+    return PreparedInsert_t::Feed;
+  }
   std::vector<Packet_t> Packets;
   if (!TestcaseFeed(Buffer, BufferSize, Out, Packets)) return PreparedInsert_t::Failed;
   return PreparedInsert_t::Feed;
 }
+
+namespace {
+// one packet's feed chunk (TestcaseFeed's layout): u32 Size, u32 Command, u16 Id,
+// u16 BodySize, Body; Body == nullptr: Len zero bytes
+inline void PutChunk(std::vector<uint8_t> &F, uint32_t Command, uint16_t Id, uint16_t BodySize, const uint8_t *Body,
+                     uint32_t Len) {
+  const size_t At = F.size();
+  F.resize(At + 12 + Len);
+  uint8_t *Q = F.data() + At;
+  const uint32_t Size = 8 + Len;
+  memcpy(Q, &Size, 4);
+  memcpy(Q + 4, &Command, 4);
+  memcpy(Q + 8, &Id, 2);
+  memcpy(Q + 10, &BodySize, 2);
+  if (Body) memcpy(Q + 12, Body, Len);
+  else memset(Q + 12, 0, Len);
+}
+}  // namespace
 
 void OnProcessPacket(Backend_t *Backend) {
   if (GlobalState.Packets.empty()) return g_Backend->Stop(Ok_t());
@@ -453,6 +488,8 @@ struct ParsedTestcase {
   std::vector<Head> Heads;
   std::vector<uint32_t> BodyOff{0};  // body text of packet i: Text[BodyOff[i], BodyOff[i + 1])
   std::string Text;
+  std::vector<uint32_t> BinOff{0};  // body bytes of packet i: Bin[BinOff[i], BinOff[i + 1])
+  std::string Bin;
 };
 
 ParsedTestcase ParseTestcase(const uint8_t *Data, const size_t DataLen) {
@@ -469,6 +506,8 @@ ParsedTestcase ParseTestcase(const uint8_t *Data, const size_t DataLen) {
     }
     P.Text += ']';
     P.BodyOff.push_back((uint32_t)P.Text.size());
+    P.Bin.append((const char *)Pk.Body.data(), Pk.Body.size());
+    P.BinOff.push_back((uint32_t)P.Bin.size());
   }
   return P;
 }
@@ -529,6 +568,10 @@ class CustomMutator_t : public Mutator_t {
     }
     o = PutLit(o, "]}", 2);
     S.resize((size_t)(o - S.data()));
+    std::vector<uint8_t> &F = LastMutation.Feed;
+    F.clear();
+    for (uint32_t Idx = 0; Idx < N; Idx++) PutChunk(F, Gs[Idx].Command, (uint16_t)Idx, Gs[Idx].BodySize, nullptr, Gs[Idx].Len);
+    LastMutation.Json = S;
     return S;
   }
 
@@ -589,6 +632,12 @@ class CustomMutator_t : public Mutator_t {
     }
     o = PutLit(o, "]}", 2);
     S.resize((size_t)(o - S.data()));
+    std::vector<uint8_t> &F = LastMutation.Feed;
+    F.clear();
+    for (const Ref &r : R)
+      PutChunk(F, r.Command, r.Id, r.BodySize, (const uint8_t *)P.Bin.data() + P.BinOff[r.Body],
+               P.BinOff[r.Body + 1] - P.BinOff[r.Body]);
+    LastMutation.Json = S;
     return S;
   }
 
