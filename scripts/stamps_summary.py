@@ -17,7 +17,13 @@ for path in sys.argv[1:]:
     tot = [0.0] * 8
     why = [0] * 4
     ops = {}
+    bpc = {}
     for line in open(path):
+        if line.startswith("wtfgpu stamps bp_apply cycles by kind:"):
+            for kv in line.split(":", 1)[1].split():
+                k, v = kv.split(":")
+                bpc[int(k)] = bpc.get(int(k), 0) + int(v)
+            continue
         if line.startswith("wtfgpu stamps generic ops:"):
             for kv in line.split(":", 1)[1].split():
                 k, v = kv.split(":")
@@ -48,3 +54,6 @@ for path in sys.argv[1:]:
           "slow steps", dict(zip(("miss", "codepage", "ucmiss", "other"), why)))
     if ops:
         print("  generic ops", dict(sorted(ops.items(), key=lambda kv: -kv[1])))
+    if bpc:  # cycles inside bp_apply per wave-step, by action kind
+        names = "host return setgprs feed rdrand stopok stopargs none".split()
+        print("  bp_apply cycles per wave-step", {names[k]: round(v / max(1, steps)) for k, v in bpc.items() if v})

@@ -1152,7 +1152,7 @@ struct LaneCopy {
 // and which generic ops the slow step executed (O_* / O_SYS2 etc.), one count per
 // group, in stat[16..528): index op | why << 6 | covered << 8
 #define OPHIST(op) ophist_[((op) & 63) | (why_ & 3) << 6 | ((op) & 64 ? 256 : 0)]++
-constexpr u32 STAT_N = 528;
+constexpr u32 STAT_N = 536;  // + stat[528..535]: cycles in bp_apply by action kind
 #else
 constexpr u32 STAT_N = 16;
 #define OPHIST(op) \
@@ -1194,6 +1194,9 @@ constexpr u32 STAT_N = 16;
 #endif
 #ifndef WTFGPU_FILL_PREFETCH
 #define WTFGPU_FILL_PREFETCH 8  // entries a fill pass also brings in after the missed one (profiles/r06_ab_fill_prefetch.txt)
+#endif
+#ifndef WTFGPU_FEED_PREFAULT
+#define WTFGPU_FEED_PREFAULT 1
 #endif
 #ifndef WTFGPU_COVER_FAST
 #define WTFGPU_COVER_FAST 1
@@ -1293,6 +1296,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
   u64 whyc_[4] = {0, 0, 0, 0};
   u32 why_ = 3;
   u32 ophist_[512] = {};
+  u64 bpcyc_[8] = {};
 #endif
 
   for (;;) {
@@ -1658,11 +1662,70 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
       ing = false;
     }
 #endif
+#if WTFGPU_FEED_PREFAULT
+    // a Feed action about to write a packet (feed_apply's checks) whose first
+    // page is not yet the lane's own: that page's copy-on-write is made here
+    // by the whole wave, 64 bytes a position (as the fast loop's first writes),
+    // instead of by each lane's 16-round copy inside host_write. Same walk
+    // (supervisor, CR0.WP clear, as host_write), same overlay slot, same page:
+    // host_write then finds it private. Anything else is left to host_write.
+    if (act_kind == WTFGPU_BPACT_FEED && P.feed_pos) {
+      bool want = false;
+      if (ing && !skip) {
+        const u64 pos = P.feed_pos[L.lane];
+        const u64 end = P.feed_end[L.lane];
+        if (pos != ~0ull && pos + 4 <= end) {
+          const u8 *src = P.feed_data + pos;
+          const u32 n = (u32)src[0] | ((u32)src[1] << 8) | ((u32)src[2] << 16) | ((u32)src[3] << 24);
+          const u64 win = act->value;
+          if (n && n < win && pos + 4 + n <= end) {
+            const u64 va = R(L, (u32)act->gprs[0] & 15) + win - n;
+            u64 td;
+            if (!(tlb_get(L, va >> 12, td) && (td & T_PRIV))) {
+              L.miss_va = va;
+              L.miss_acc = ACC_W;
+              want = true;
+            }
+          }
+        }
+      }
+      u64 csrc = 0, cdst = 0, cgpfn = 0, ctd = 0;
+      if (want) {
+        const u32 cpl0 = L.cpl;
+        const u64 cr00 = L.cr0;
+        L.cpl = 0;
+        L.cr0 &= ~(1ull << 16);
+        want = fast_fill_prep(P, L, csrc, cdst, cgpfn, ctd);
+        L.cpl = cpl0;
+        L.cr0 = cr00;
+      }
+      RECONVERGE();
+      for (u64 cm = __ballot(want && cdst); cm; cm &= cm - 1) {
+        const int l = __ffsll((long long)cm) - 1;
+        const uint4 *s4 = (const uint4 *)(uintptr_t)readlane64(csrc, l) + lid * 4;
+        uint4 *d4 = (uint4 *)(uintptr_t)readlane64(cdst, l) + lid * 4;
+        const uint4 a = s4[0], b = s4[1], c = s4[2], d = s4[3];
+        d4[0] = a;
+        d4[1] = b;
+        d4[2] = c;
+        d4[3] = d;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      if (want && cdst) fast_fill_finish(P, L, cdst, cgpfn, ctd);
+      RECONVERGE();
+    }
+#endif
     if (ing) {
       if ((flags & UC_BP) && !skip) {
         // breakpoint hit: device action (the lane keeps running) or host exit
         bool applied = false;
+#ifdef WTFGPU_STAMPS
+        const u64 tb_ = __builtin_amdgcn_s_memtime();
+#endif
         if (P.act_keys) WITH_LANE_COPY(applied = bp_apply(P, T, grip, act));
+#ifdef WTFGPU_STAMPS
+        bpcyc_[act_kind < 7 ? act_kind : 7] += __builtin_amdgcn_s_memtime() - tb_;
+#endif
         if (!applied) L.status = WTFGPU_EXIT_BREAKPOINT;
         skip = applied && L.rip == grip;
         if (applied && !skip && g_tn.buf) WITH_LANE_COPY(tn_regs(P, T));  // Tenet: the action moved rip
@@ -1738,6 +1801,7 @@ __global__ __launch_bounds__(256, WTFGPU_KRUN_WAVES) void k_run(Dev P, u32 first
     for (int k = 0; k < 4; k++) atomicAdd((unsigned long long *)&P.stat[12 + k], (unsigned long long)whyc_[k]);
     for (int k = 0; k < 512; k++)
       if (ophist_[k]) atomicAdd((unsigned long long *)&P.stat[16 + k], (unsigned long long)ophist_[k]);
+    for (int k = 0; k < 8; k++) atomicAdd((unsigned long long *)&P.stat[528 + k], (unsigned long long)bpcyc_[k]);
 #endif
   }
 }
@@ -3549,6 +3613,9 @@ static void print_stamps(const u64 *s) {
   fprintf(stderr, "wtfgpu stamps generic ops:");
   for (int k = 0; k < 512; k++)
     if (s[16 + k]) fprintf(stderr, " %d:%llu", k, (unsigned long long)s[16 + k]);
+  fprintf(stderr, "\n");
+  fprintf(stderr, "wtfgpu stamps bp_apply cycles by kind:");
+  for (int k = 0; k < 8; k++) fprintf(stderr, " %d:%llu", k, (unsigned long long)s[528 + k]);
   fprintf(stderr, "\n");
 #else
   (void)s;
