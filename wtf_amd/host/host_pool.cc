@@ -16,7 +16,11 @@ unsigned host_threads() {
 }
 
 namespace {
-constexpr int kSpin = 4000;  // pause iterations before a worker sleeps (~10-40 us)
+// pause iterations before a worker sleeps (~10-40 us; WTFGPU_POOL_SPIN for A/Bs)
+const int kSpin = [] {
+  const char *e = getenv("WTFGPU_POOL_SPIN");
+  return e ? atoi(e) : 4000;
+}();
 thread_local unsigned t_index = 0;
 thread_local bool t_in_loop = false;
 }  // namespace

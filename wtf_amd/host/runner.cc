@@ -776,7 +776,13 @@ TcBatch FuzzSession::MakeBatch(uint64_t n) {
       CpuNs += ThreadCpuNs() - c0;
     };
     std::vector<std::thread> Pool;
-    for (unsigned t = 1; t < host_threads(); t++) Pool.emplace_back(Work);
+    // (WTF_MUTATE_THREADS: the threads mutating, for A/Bs; the chunks make the
+    // batch the same whatever the count)
+    static const unsigned MutThreads = [] {
+      const char *e = getenv("WTF_MUTATE_THREADS");
+      return e && atoi(e) > 0 ? (unsigned)atoi(e) : host_threads();
+    }();
+    for (unsigned t = 1; t < MutThreads; t++) Pool.emplace_back(Work);
     Work();
     for (std::thread &Th : Pool) Th.join();
     MutateCpuNs_ += CpuNs.load();
