@@ -1,4 +1,4 @@
-# Round 6: host-side A/B of the tlv headline (bench.py --no-cpu --no-legs,
+# Round 6: environment A/B of bench.py (BENCH_ARGS, default --no-cpu --no-legs,
 # 120 timed steps): HOSTVARS is a list of name=ENV1=v1,ENV2=v2 entries ('-' = none),
 # each run twice in opposite orders; results under gpurun_out/hab.
 set -o pipefail
@@ -9,8 +9,8 @@ for v in $order; do
   name=${v%%=*}; envs=${v#*=}
   i=$(ls gpurun_out/hab | grep -c "^$name\.")
   ( [ "$envs" != "-" ] && for kv in $(echo $envs | tr ',' ' '); do export "$kv"; done
-    timeout -k 10 240 python -u bench.py --no-cpu --no-legs --steps 120 > gpurun_out/hab/$name.$i.log 2>&1 ) \
+    timeout -k 10 300 python -u bench.py ${BENCH_ARGS:---no-cpu --no-legs --steps 120} > gpurun_out/hab/$name.$i.log 2>&1 ) \
     || { echo "FAIL $name"; tail -20 gpurun_out/hab/$name.$i.log; exit 1; }
   tail -1 gpurun_out/hab/$name.$i.log > gpurun_out/hab/$name.$i.json
-  echo "== $name ($envs)"; python3 scripts/bench_brief.py gpurun_out/hab/$name.$i.json | head -3
+  echo "== $name ($envs)"; python3 scripts/bench_brief.py gpurun_out/hab/$name.$i.json | grep -v "node/step\|backend/step"
 done

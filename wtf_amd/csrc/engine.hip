@@ -2766,9 +2766,10 @@ int wtfgpu_create(int device, wtfgpu_ctx **out) {
   if (const char *e = getenv("WTFGPU_REGROUP_STEPS")) c->regroup_steps = strtoull(e, nullptr, 0);
   if (const char *e = getenv("WTFGPU_REGROUP_AUTO")) c->regroup_auto = e[0] != '0';
   {
-    // shared decoded-uop cache: 32K entries of 192 bytes (WTFGPU_GUC=0: off)
+    // shared decoded-uop cache: 256K entries of 192 bytes, 48 MB (WTFGPU_GUC=0:
+    // off; 32K entries had HEVD I/O launches 2-3 % longer, profiles/r06_ab_guc_size.txt)
     const char *e = getenv("WTFGPU_GUC");
-    const u32 n = e ? (u32)strtoul(e, nullptr, 0) : 32768u;
+    const u32 n = e ? (u32)strtoul(e, nullptr, 0) : 262144u;
     if (n && !(n & (n - 1))) {
       if (dalloc(&c->d_guc, (u64)n * GUC_WORDS)) {
         delete c;
